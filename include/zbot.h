@@ -1,0 +1,169 @@
+/*
+ * zbot.h — C ABI of the MI355X-native batched ZBOT-6 walking simulator (zbot-6b-walking-v2).
+ *
+ * One handle owns N environments' persistent state in HBM (SoA, [field][env], fp32) and steps
+ * them with one fused HIP kernel per policy step (4 physics substeps + contact sensor + MDP +
+ * in-kernel auto-reset). The CPU oracle (oracle/zbot_oracle.c) exports the same entry points with
+ * the prefix `zbo_` and host pointers; it is test infrastructure only.
+ *
+ * Reference interfaces replaced (paths relative to the reference repo root):
+ *   zb_create   <- gym.make("zbot-6b-walking-v2") -> ZbotDirectEnvV2.__init__
+ *                  (source/zbot/zbot/tasks/zbot6b_direct/__init__.py:41-49;
+ *                   .../zbot_direct_6dof_bipedal_env_v2.py:211-257, _setup_scene 259-274)
+ *   zb_reset    <- DirectRLEnv.reset() -> ZbotDirectEnvV2._reset_idx (v2.py:413-459)
+ *   zb_step     <- DirectRLEnv.step(a): _pre_physics_step (v2.py:276-287), 4 x {_apply_action
+ *                  (v2.py:309-310), PhysX sim.step, scene.update}, _get_dones (v2.py:384-411),
+ *                  _get_rewards (v2.py:371-382), _reset_idx (v2.py:413-459),
+ *                  _get_observations (v2.py:312-369)
+ *   zb_observe  <- ZbotDirectEnvV2._get_observations (v2.py:312-369), used by reset()
+ *   zb_read_log <- extras["log"] written in _reset_idx (v2.py:441-459)
+ *   zb_get_state / zb_set_state / zb_physics_substeps: parity + debugging (no reference analogue;
+ *                  they stand in for Articulation.data reads / write_*_to_sim)
+ *
+ * Conventions: quaternions (w, x, y, z); world Z-up; gravity (0, 0, -9.81); every env in its
+ * own env-local frame (origin 0; the plane is infinite and envs are collision-filtered in the
+ * reference, v2.py:271, so physics is translation invariant).
+ * All device entry points are stream-ordered and never synchronise the host. Return 0 on
+ * success, a negative code on error (message via zb_last_error()). Not thread-safe per handle.
+ */
+#ifndef ZBOT_H_
+#define ZBOT_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ZB_NUM_LINKS 12       /* foot_0 b1 a2 b2 a3 b3 base b4 a5 b5 a6 foot_1 */
+#define ZB_NUM_BODIES 7       /* rigid composites after merging the 5 fixed joints */
+#define ZB_NUM_DOF 6          /* revolute joint1..joint6 */
+#define ZB_ACT_DIM 6
+#define ZB_OBS_DIM 23
+#define ZB_NUM_REWARD_TERMS 13
+#define ZB_HIST 5             /* contact sensor history_length (v2.py:32) */
+#define ZB_MAX_SELF_PAIRS 64
+
+/* Persistent per-env state, SoA [ZB_STATE_DIM][num_envs] float32. */
+enum zb_state_field {
+  ZB_S_ROOT_POS = 0,        /* 3  root link (foot_0) origin, env-local */
+  ZB_S_ROOT_QUAT = 3,       /* 4  wxyz */
+  ZB_S_ROOT_LINVEL = 7,     /* 3  world velocity of the root link origin */
+  ZB_S_ROOT_ANGVEL = 10,    /* 3  world */
+  ZB_S_JOINT_POS = 13,      /* 6 */
+  ZB_S_JOINT_VEL = 19,      /* 6 */
+  ZB_S_P_DELTA = 25,        /* 6  v2.py:245,280-286 */
+  ZB_S_ACTIONS = 31,        /* 6  tanh(actions) of the last step (= _previous_actions next step) */
+  ZB_S_FEET_DOWN_POS = 37,  /* 6  [foot][xyz] v2.py:235 */
+  ZB_S_FEET_STEP_LEN = 43,  /* 2  v2.py:236 */
+  ZB_S_FEET_F_LAST = 45,    /* 2  v2.py:231 */
+  ZB_S_HEADING_SUM = 47,    /* 1  v2.py:239 */
+  ZB_S_Y_ERR_SUM = 48,      /* 1  v2.py:240 */
+  ZB_S_FEET_FZ_HIST = 49,   /* 10 [slot][foot], slot 0 newest: net_forces_w_history[..., feet, 2] */
+  ZB_S_UNDES_FMAX_HIST = 59,/* 5  [slot]: max over the 10 undesired bodies of |net force| */
+  ZB_S_FEET_AIR_CUR = 64,   /* 2  ContactSensor current_air_time[feet] */
+  ZB_S_FEET_AIR_LAST = 66,  /* 2  last_air_time[feet] */
+  ZB_S_FEET_CONTACT_CUR = 68,/*2  current_contact_time[feet] */
+  ZB_S_EP_LEN = 70,         /* 1  episode_length_buf (integer-valued float) */
+  ZB_S_EP_SUMS = 71,        /* 13 _episode_sums in reward-term order */
+  ZB_STATE_DIM = 84
+};
+
+/* Reward term order = dict order of ZbotDirectEnvCfgV2.reward_cfg (v2.py:190-206). */
+enum zb_reward_term {
+  ZB_R_BASE_VEL_FORWARD = 0, ZB_R_FEET_DOWNWARD, ZB_R_FEET_FORWARD, ZB_R_BASE_HEADING_X,
+  ZB_R_BASE_HEADING_X_SUM, ZB_R_STEP_LENGTH, ZB_R_AIRTIME_BALANCE, ZB_R_ACTION_RATE,
+  ZB_R_TORQUES, ZB_R_FEET_SLIDE, ZB_R_BASE_POS_Y_ERR, ZB_R_BASE_POS_Y_ERR_SUM, ZB_R_AIRTIME_SUM
+};
+
+/* Robot model: ZBOT_6S_CFG (zbot_cfg.py:621-669) + zbot_6s_new.usd, fixed joints merged.
+ * Filled by zbot_lab_amd/model.py from zbot_lab_amd/assets/zbot6s_model.json. */
+typedef struct zb_model {
+  /* composite rigid bodies; body b>0 hangs off body b-1 through revolute joint b-1 */
+  float body_mass[ZB_NUM_BODIES];
+  float body_com[ZB_NUM_BODIES][3];       /* body frame */
+  float body_inertia[ZB_NUM_BODIES][6];   /* about COM, body frame: xx yy zz xy xz yz */
+  /* revolute joint k: X_{k+1} = X_k * T(jp_pos, jp_rot) * Rz(q_k) * T(jc_pos, jc_rot) */
+  float joint_parent_pos[ZB_NUM_DOF][3];
+  float joint_parent_rot[ZB_NUM_DOF][4];
+  float joint_child_pos[ZB_NUM_DOF][3];
+  float joint_child_rot[ZB_NUM_DOF][4];
+  /* links (Isaac Lab body order) */
+  int32_t link_body[ZB_NUM_LINKS];
+  float link_pos[ZB_NUM_LINKS][3];        /* link frame in body frame */
+  float link_rot[ZB_NUM_LINKS][4];
+  float link_com[ZB_NUM_LINKS][3];        /* authored link COM, body frame */
+  /* collision shape = convex hull of two circles: centre C, semi-axes E1, E2 (body frame) */
+  float link_circle[ZB_NUM_LINKS][2][9];
+  float link_sphere[ZB_NUM_LINKS][2][4];  /* self-collision spheres: centre (body frame), radius */
+  float link_bound[ZB_NUM_LINKS][4];      /* bounding sphere of the shape: centre (body), radius */
+  int32_t num_self_pairs;
+  int32_t self_pairs[ZB_MAX_SELF_PAIRS][2];
+  /* defaults */
+  float default_root_pos[3];
+  float default_root_quat[4];
+  float default_joint_pos[ZB_NUM_DOF];
+  /* ImplicitActuatorCfg (zbot_cfg.py:658-668) + rigid props (zbot_cfg.py:626-634) */
+  float kp, kd, effort_limit, velocity_limit, max_depenetration_velocity;
+  /* indices used by the MDP */
+  int32_t base_link, foot_links[2], undesired_links[10];
+} zb_model;
+
+/* Task / simulation constants: ZbotDirectEnvCfgV2 (v2.py:26-206) + solver parameters. */
+typedef struct zb_task_cfg {
+  float sim_dt;                /* 1/200 (v2.py:48) */
+  int32_t decimation;          /* 4 (v2.py:40) */
+  int32_t max_episode_length;  /* ceil(20 s / 0.02 s) = 1000 (v2.py:39) */
+  float termination_height;    /* 0.22 (v2.py:44) */
+  float reward_scales[ZB_NUM_REWARD_TERMS]; /* weights x step_dt (v2.py:250-252) */
+  float terminal_penalty;      /* 20 (v2.py:380) */
+  float joint_speed_limit;     /* 1.0 (v2.py:243) */
+  float gravity;               /* 9.81 */
+  float friction;              /* 1.0 static = dynamic, multiply combine (v2.py:49-56,62-68) */
+  float contact_force_threshold; /* 1.0 N ContactSensorCfg.force_threshold default */
+  float contact_margin;        /* speculative contact distance (m) */
+  float baumgarte;             /* penetration correction per step (fraction) */
+  int32_t solver_iterations;   /* PGS sweeps per substep */
+  int32_t enable_self_collision;
+} zb_task_cfg;
+
+typedef struct zb_sim* zb_handle;
+
+/* Create N envs on HIP device `hip_device`; state starts at the default pose, ep_len 0.
+ * `seed` drives the full-reset episode_length_buf randomisation (v2.py:418-422). */
+int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_device, uint64_t seed,
+              zb_handle* out);
+void zb_destroy(zb_handle h);
+const char* zb_last_error(void);
+int zb_num_envs(zb_handle h);
+
+/* Reset env_ids (device int32[n]); env_ids == NULL => all envs, which also draws
+ * episode_length_buf ~ U{0..max_episode_length-1} (v2.py:418-422). */
+int zb_reset(zb_handle h, const int32_t* env_ids, int n, void* stream);
+
+/* One policy step for all envs. actions: device float[N][6] (raw policy output);
+ * obs: device float[N][23]; reward: float[N]; terminated/truncated: uint8[N] (torch.bool). */
+int zb_step(zb_handle h, const float* actions, float* obs, float* reward, uint8_t* terminated,
+            uint8_t* truncated, void* stream);
+
+/* Observation of the current state (v2.py:351-365), as reset() returns. obs: float[N][23]. */
+int zb_observe(zb_handle h, float* obs, void* stream);
+
+/* Episode log of the most recent step with resets: term_means[13] = mean episodic sum / 20 s,
+ * counts[2] = {body_contact, time_out} (v2.py:441-459). Device pointers. */
+int zb_read_log(zb_handle h, float* term_means, int32_t* counts, void* stream);
+
+/* Persistent state, device float[ZB_STATE_DIM][N]. */
+int zb_get_state(zb_handle h, float* dst, void* stream);
+int zb_set_state(zb_handle h, const float* src, void* stream);
+
+/* Parity/debug: run `nsub` physics substeps with joint targets float[N][6] (no MDP);
+ * if net_force != NULL it receives the last substep's net contact force, float[N][12][3],
+ * and applied_torque (if != NULL) Isaac Lab's clipped PD estimate float[N][6]. */
+int zb_physics_substeps(zb_handle h, const float* targets, int nsub, float* net_force,
+                        float* applied_torque, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ZBOT_H_ */

@@ -1,0 +1,1361 @@
+/*
+ * zbot_oracle.c — CPU ORACLE for the zbot-6b-walking-v2 hot path. TEST INFRASTRUCTURE ONLY.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this library,
+ * and only as the checker / CPU baseline. The product path (zbot_lab_amd, libzbot.so) never
+ * links or calls it and fails loudly when its HIP extension is missing.
+ *
+ * What it restates (reference paths relative to the reference repo root):
+ *   MDP  : ZbotDirectEnvV2 (source/zbot/zbot/tasks/zbot6b_direct/zbot_direct_6dof_bipedal_env_v2.py)
+ *          _pre_physics_step 276-287, _get_observations 312-369, _get_rewards 371-382 and the
+ *          13 reward terms 461-561, _get_dones 384-411, _reset_idx 413-459; DirectRLEnv.step
+ *          order; Isaac Lab ContactSensor lazy update semantics
+ *          (DESIGN.md §4). PINNED against golden vectors generated from the reference's own v2
+ *          code (tests/golden/, tools/gen_mdp_goldens.py) by zbo_mdp_eval / zbo_pre_physics.
+ *   Model: ZBOT_6S_CFG (source/zbot/zbot/assets/zbot_cfg.py:621-669) + zbot_6s_new.usd;
+ *          forward kinematics PINNED to the reference's printed known answers (v2.py:403-404,
+ *          v4.py:816) in tests/test_model.py.
+ *   Physics (PhysX 5 articulation + contact; closed source, absent here): PARITY UNPINNED against
+ *          PhysX. This is the simulator's own algorithm, checked only by physical
+ *          invariants (free fall, momentum without contact, PD response, resting contact) and
+ *          used as the reference the HIP kernel must match.
+ *
+ * Physics substep (same algorithm as the HIP kernel):
+ *   FK of 7 composites -> world spatial inertias about P = root origin -> RNEA bias forces
+ *   (gravity as base acceleration) -> CRBA mass matrix -> implicit PD drives (armature
+ *   dt*kd + dt^2*kp on the joint diagonal; a joint whose implicit torque exceeds the effort
+ *   limit is re-solved with an explicit +-limit torque and no armature) -> Cholesky M = L L^T ->
+ *   contacts (circle-pair support points vs plane, sphere pairs for self collision) -> projected
+ *   Gauss-Seidel on the whitened velocity w = L^T u with rows Y = L^-1 J^T (Coulomb disk
+ *   friction) -> u = L^-T w -> joint speed clamp -> semi-implicit Euler, joint wrap.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/zbot.h"
+
+#ifndef ZBO_REAL
+#define ZBO_REAL float
+#endif
+typedef ZBO_REAL real;
+
+#define NB ZB_NUM_BODIES
+#define ND ZB_NUM_DOF
+#define NL ZB_NUM_LINKS
+#define NV (6 + ND)  /* generalized velocity: [omega(3), v_P(3), qdot(6)] */
+#define NC_MAX 16    /* contact slots per env per substep (= ZB kernel) */
+#define NCAND_PER_LINK 4
+#define TWO_PI 6.283185307179586
+#define PI_R 3.14159265358979323846
+
+/* ------------------------------------------------------------------------- small math */
+static inline void v3_cross(const real a[3], const real b[3], real o[3]) {
+  real x = a[1] * b[2] - a[2] * b[1], y = a[2] * b[0] - a[0] * b[2], z = a[0] * b[1] - a[1] * b[0];
+  o[0] = x; o[1] = y; o[2] = z;
+}
+static inline real v3_dot(const real a[3], const real b[3]) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+static inline void q_mul(const real a[4], const real b[4], real o[4]) {
+  real w = a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3];
+  real x = a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2];
+  real y = a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1];
+  real z = a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0];
+  o[0] = w; o[1] = x; o[2] = y; o[3] = z;
+}
+static inline void q_to_mat(const real q[4], real R[9]) {
+  real w = q[0], x = q[1], y = q[2], z = q[3];
+  R[0] = 1 - 2 * (y * y + z * z); R[1] = 2 * (x * y - w * z);     R[2] = 2 * (x * z + w * y);
+  R[3] = 2 * (x * y + w * z);     R[4] = 1 - 2 * (x * x + z * z); R[5] = 2 * (y * z - w * x);
+  R[6] = 2 * (x * z - w * y);     R[7] = 2 * (y * z + w * x);     R[8] = 1 - 2 * (x * x + y * y);
+}
+static inline void m3_v(const real R[9], const real v[3], real o[3]) {
+  real x = R[0] * v[0] + R[1] * v[1] + R[2] * v[2];
+  real y = R[3] * v[0] + R[4] * v[1] + R[5] * v[2];
+  real z = R[6] * v[0] + R[7] * v[1] + R[8] * v[2];
+  o[0] = x; o[1] = y; o[2] = z;
+}
+static inline void q_normalize(real q[4]) {
+  real n = (real)sqrt((double)(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]));
+  for (int i = 0; i < 4; ++i) q[i] /= n;
+}
+static inline real clampr(real x, real lo, real hi) { return x < lo ? lo : (x > hi ? hi : x); }
+static inline real sqrtr(real x) { return (real)sqrt((double)x); }
+
+/* splitmix64 finaliser: counter-based hash shared with the kernel for episode-length draws */
+static inline uint64_t zb_hash64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+/* ------------------------------------------------------------------------- model (real) */
+typedef struct {
+  real body_mass[NB], body_com[NB][3], body_I[NB][6];
+  real jp_pos[ND][3], jp_rot[ND][4], jc_pos[ND][3], jc_rot[ND][4];
+  int link_body[NL];
+  real link_pos[NL][3], link_rot[NL][4], link_com[NL][3];
+  real circle[NL][2][9], sphere[NL][2][4], bound[NL][4];
+  int npairs, pairs[ZB_MAX_SELF_PAIRS][2];
+  real root_pos0[3], root_quat0[4], jq0[ND];
+  real kp, kd, effort, vlim, max_depen;
+  int base_link, foot_links[2], undesired[10];
+} mdl_t;
+
+static void load_mdl(const zb_model* m, mdl_t* o) {
+  for (int b = 0; b < NB; ++b) {
+    o->body_mass[b] = m->body_mass[b];
+    for (int a = 0; a < 3; ++a) o->body_com[b][a] = m->body_com[b][a];
+    for (int a = 0; a < 6; ++a) o->body_I[b][a] = m->body_inertia[b][a];
+  }
+  for (int j = 0; j < ND; ++j) {
+    for (int a = 0; a < 3; ++a) { o->jp_pos[j][a] = m->joint_parent_pos[j][a]; o->jc_pos[j][a] = m->joint_child_pos[j][a]; }
+    for (int a = 0; a < 4; ++a) { o->jp_rot[j][a] = m->joint_parent_rot[j][a]; o->jc_rot[j][a] = m->joint_child_rot[j][a]; }
+    o->jq0[j] = m->default_joint_pos[j];
+  }
+  for (int l = 0; l < NL; ++l) {
+    o->link_body[l] = m->link_body[l];
+    for (int a = 0; a < 3; ++a) { o->link_pos[l][a] = m->link_pos[l][a]; o->link_com[l][a] = m->link_com[l][a]; }
+    for (int a = 0; a < 4; ++a) { o->link_rot[l][a] = m->link_rot[l][a]; o->bound[l][a] = m->link_bound[l][a]; }
+    for (int c = 0; c < 2; ++c) {
+      for (int a = 0; a < 9; ++a) o->circle[l][c][a] = m->link_circle[l][c][a];
+      for (int a = 0; a < 4; ++a) o->sphere[l][c][a] = m->link_sphere[l][c][a];
+    }
+  }
+  o->npairs = m->num_self_pairs;
+  for (int p = 0; p < o->npairs; ++p) { o->pairs[p][0] = m->self_pairs[p][0]; o->pairs[p][1] = m->self_pairs[p][1]; }
+  for (int a = 0; a < 3; ++a) o->root_pos0[a] = m->default_root_pos[a];
+  for (int a = 0; a < 4; ++a) o->root_quat0[a] = m->default_root_quat[a];
+  o->kp = m->kp; o->kd = m->kd; o->effort = m->effort_limit; o->vlim = m->velocity_limit;
+  o->max_depen = m->max_depenetration_velocity;
+  o->base_link = m->base_link;
+  o->foot_links[0] = m->foot_links[0]; o->foot_links[1] = m->foot_links[1];
+  for (int k = 0; k < 10; ++k) o->undesired[k] = m->undesired_links[k];
+}
+
+/* ------------------------------------------------------------------------- per-env state */
+typedef struct {
+  real root_pos[3], root_quat[4], root_linvel[3], root_angvel[3];
+  real jq[ND], jqd[ND];
+} phys_t;
+
+typedef struct {
+  real p_delta[ND], actions[ND];
+  real feet_down_pos[2][3], feet_step_len[2], feet_f_last[2];
+  real heading_sum, yerr_sum;
+  real feet_fz_hist[ZB_HIST][2], undes_fmax_hist[ZB_HIST];
+  real feet_air_cur[2], feet_air_last[2], feet_contact_cur[2];
+  int32_t ep_len;
+  real ep_sums[ZB_NUM_REWARD_TERMS];
+} mdp_t;
+
+typedef struct { phys_t ph; mdp_t md; } env_t;
+
+struct zbo_sim {
+  mdl_t m;
+  zb_task_cfg c;
+  int n;
+  uint64_t seed, reset_counter;
+  env_t* env;
+  float log_means[ZB_NUM_REWARD_TERMS];
+  int32_t log_counts[2];
+};
+typedef struct zbo_sim zbo_sim;
+
+/* ------------------------------------------------------------------------- kinematics */
+typedef struct {
+  real q[NB][4], R[NB][9], p[NB][3];  /* body frames; p relative to P = root origin */
+  real axis[ND][3], org[ND][3];       /* joint axis (world) and point (rel P) */
+} kin_t;
+
+/* X_{b+1} = X_b * T(jp_pos, jp_rot) * Rz(q_b) * T(jc_pos, jc_rot)  (PhysX composition order) */
+static void fk(const mdl_t* m, const phys_t* s, kin_t* k) {
+  for (int a = 0; a < 4; ++a) k->q[0][a] = s->root_quat[a];
+  q_normalize(k->q[0]);
+  q_to_mat(k->q[0], k->R[0]);
+  k->p[0][0] = k->p[0][1] = k->p[0][2] = 0;
+  for (int j = 0; j < ND; ++j) {
+    real qj[4], Rj[9], t[3];
+    q_mul(k->q[j], m->jp_rot[j], qj);
+    q_to_mat(qj, Rj);
+    m3_v(k->R[j], m->jp_pos[j], t);
+    for (int a = 0; a < 3; ++a) { k->org[j][a] = k->p[j][a] + t[a]; k->axis[j][a] = Rj[3 * a + 2]; }
+    real h = (real)0.5 * s->jq[j];
+    real qz[4] = {(real)cos((double)h), 0, 0, (real)sin((double)h)};
+    real qa[4];
+    q_mul(qj, qz, qa);
+    real Ra[9];
+    q_to_mat(qa, Ra);
+    m3_v(Ra, m->jc_pos[j], t);
+    for (int a = 0; a < 3; ++a) k->p[j + 1][a] = k->org[j][a] + t[a];
+    q_mul(qa, m->jc_rot[j], k->q[j + 1]);
+    q_normalize(k->q[j + 1]);
+    q_to_mat(k->q[j + 1], k->R[j + 1]);
+  }
+}
+
+/* link l world pose: position relative to P, quaternion */
+static void link_pose(const mdl_t* m, const kin_t* k, int l, real pos[3], real quat[4]) {
+  int b = m->link_body[l];
+  real t[3];
+  m3_v(k->R[b], m->link_pos[l], t);
+  for (int a = 0; a < 3; ++a) pos[a] = k->p[b][a] + t[a];
+  q_mul(k->q[b], m->link_rot[l], quat);
+}
+
+/* spatial velocity of every body at P: V = [omega; v_P] */
+static void body_vel(const kin_t* k, const phys_t* s, real V[NB][6]) {
+  for (int a = 0; a < 3; ++a) { V[0][a] = s->root_angvel[a]; V[0][3 + a] = s->root_linvel[a]; }
+  for (int j = 0; j < ND; ++j) {
+    real S[6], oxa[3];
+    v3_cross(k->org[j], k->axis[j], oxa);
+    for (int a = 0; a < 3; ++a) { S[a] = k->axis[j][a]; S[3 + a] = oxa[a]; }
+    for (int a = 0; a < 6; ++a) V[j + 1][a] = V[j][a] + S[a] * s->jqd[j];
+  }
+}
+
+/* world linear velocity of a point x (rel P) moving with body b */
+static void point_vel(const real V[6], const real x[3], real o[3]) {
+  real c[3];
+  v3_cross(V, x, c);
+  for (int a = 0; a < 3; ++a) o[a] = V[3 + a] + c[a];
+}
+
+/* ------------------------------------------------------------------------- spatial algebra */
+typedef struct { real m, h[3], I[6]; } sinertia; /* about P: I = [xx yy zz xy xz yz] */
+
+static inline void sym_mv(const real I[6], const real w[3], real o[3]) {
+  real x = I[0] * w[0] + I[3] * w[1] + I[4] * w[2];
+  real y = I[3] * w[0] + I[1] * w[1] + I[5] * w[2];
+  real z = I[4] * w[0] + I[5] * w[1] + I[2] * w[2];
+  o[0] = x; o[1] = y; o[2] = z;
+}
+/* f = I V : n = I w + h x v ; f = m v - h x w */
+static void si_mul(const sinertia* I, const real V[6], real f[6]) {
+  real Iw[3], hv[3], hw[3];
+  sym_mv(I->I, V, Iw);
+  v3_cross(I->h, V + 3, hv);
+  v3_cross(I->h, V, hw);
+  for (int a = 0; a < 3; ++a) { f[a] = Iw[a] + hv[a]; f[3 + a] = I->m * V[3 + a] - hw[a]; }
+}
+static void si_add(sinertia* a, const sinertia* b) {
+  a->m += b->m;
+  for (int i = 0; i < 3; ++i) a->h[i] += b->h[i];
+  for (int i = 0; i < 6; ++i) a->I[i] += b->I[i];
+}
+/* motion cross: V x_m S = [w x a ; w x b + v x a] */
+static void crossm(const real V[6], const real S[6], real o[6]) {
+  real t1[3], t2[3], t3[3];
+  v3_cross(V, S, t1);
+  v3_cross(V, S + 3, t2);
+  v3_cross(V + 3, S, t3);
+  for (int a = 0; a < 3; ++a) { o[a] = t1[a]; o[3 + a] = t2[a] + t3[a]; }
+}
+/* force cross: V x_f F = [w x n + v x f ; w x f] */
+static void crossf(const real V[6], const real F[6], real o[6]) {
+  real t1[3], t2[3], t3[3];
+  v3_cross(V, F, t1);
+  v3_cross(V + 3, F + 3, t2);
+  v3_cross(V, F + 3, t3);
+  for (int a = 0; a < 3; ++a) { o[a] = t1[a] + t2[a]; o[3 + a] = t3[a]; }
+}
+
+/* world spatial inertia of body b about P */
+static void body_sinertia(const mdl_t* m, const kin_t* k, int b, sinertia* o) {
+  const real* R = k->R[b];
+  real c[3];
+  m3_v(R, m->body_com[b], c);
+  for (int a = 0; a < 3; ++a) c[a] += k->p[b][a];
+  /* Ic_world = R Ilocal R^T */
+  const real* L = m->body_I[b];
+  real Il[9] = {L[0], L[3], L[4], L[3], L[1], L[5], L[4], L[5], L[2]};
+  real T[9], W[9];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) T[3 * i + j] = R[3 * i] * Il[j] + R[3 * i + 1] * Il[3 + j] + R[3 * i + 2] * Il[6 + j];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) W[3 * i + j] = T[3 * i] * R[3 * j] + T[3 * i + 1] * R[3 * j + 1] + T[3 * i + 2] * R[3 * j + 2];
+  real mm = m->body_mass[b];
+  real cc = v3_dot(c, c);
+  o->m = mm;
+  for (int a = 0; a < 3; ++a) o->h[a] = mm * c[a];
+  o->I[0] = W[0] + mm * (cc - c[0] * c[0]);
+  o->I[1] = W[4] + mm * (cc - c[1] * c[1]);
+  o->I[2] = W[8] + mm * (cc - c[2] * c[2]);
+  o->I[3] = W[1] - mm * c[0] * c[1];
+  o->I[4] = W[2] - mm * c[0] * c[2];
+  o->I[5] = W[5] - mm * c[1] * c[2];
+}
+
+/* ------------------------------------------------------------------------- contacts */
+typedef struct {
+  int la, lb;          /* links (lb = -1 for ground) */
+  real x[3];           /* contact point, rel P */
+  real n[3];           /* normal: impulse on la along +n */
+  real sep;            /* separation (negative = penetration) */
+} contact_t;
+
+typedef struct { contact_t c[NC_MAX]; int n; } clist_t;
+
+static void clist_add(clist_t* L, const contact_t* c) {
+  if (L->n < NC_MAX) { L->c[L->n++] = *c; return; }
+  int worst = 0;
+  for (int i = 1; i < NC_MAX; ++i)
+    if (L->c[i].sep > L->c[worst].sep) worst = i;
+  if (c->sep < L->c[worst].sep) L->c[worst] = *c;
+}
+
+/* Ground: each link's shape is the convex hull of two circles (C, E1, E2 in body frame). The
+ * lowest rim point of each circle plus its three 90-degree rotations along the rim are the
+ * candidates (4 per circle: a flat disk resting on the plane yields a 4-point manifold);
+ * per link the NCAND_PER_LINK deepest below the speculative margin are kept. */
+static void detect(const mdl_t* m, const zb_task_cfg* cfg, const kin_t* k, real Pz, clist_t* L) {
+  L->n = 0;
+  const real margin = cfg->contact_margin;
+  for (int l = 0; l < NL; ++l) {
+    int b = m->link_body[l];
+    const real* R = k->R[b];
+    /* cull: bounding sphere entirely above the margin */
+    real bc[3];
+    m3_v(R, m->bound[l], bc);
+    if (Pz + k->p[b][2] + bc[2] - m->bound[l][3] > margin) continue;
+    contact_t cand[8];
+    int nc = 0;
+    for (int ci = 0; ci < 2; ++ci) {
+      const real* cd = m->circle[l][ci];
+      real C[3], E1[3], E2[3];
+      m3_v(R, cd, C);
+      m3_v(R, cd + 3, E1);
+      m3_v(R, cd + 6, E2);
+      for (int a = 0; a < 3; ++a) C[a] += k->p[b][a];
+      real al = -E1[2], be = -E2[2];
+      real nrm = sqrtr(al * al + be * be);
+      real cs = 1, sn = 0;
+      if (nrm > (real)1e-9) { cs = al / nrm; sn = be / nrm; }
+      for (int r = 0; r < 4; ++r) {
+        real cr, sr;
+        if (r == 0) { cr = cs; sr = sn; }
+        else if (r == 1) { cr = -sn; sr = cs; }
+        else if (r == 2) { cr = -cs; sr = -sn; }
+        else { cr = sn; sr = -cs; }
+        contact_t c;
+        for (int a = 0; a < 3; ++a) c.x[a] = C[a] + cr * E1[a] + sr * E2[a];
+        c.sep = Pz + c.x[2];
+        if (c.sep < margin) {
+          c.la = l; c.lb = -1;
+          c.n[0] = 0; c.n[1] = 0; c.n[2] = 1;
+          cand[nc++] = c;
+        }
+      }
+    }
+    /* keep the NCAND_PER_LINK deepest (stable: earlier candidate wins ties) */
+    for (int s = 0; s < nc && s < NCAND_PER_LINK; ++s) {
+      int best = s;
+      for (int t = s + 1; t < nc; ++t)
+        if (cand[t].sep < cand[best].sep) best = t;
+      contact_t tmp = cand[s]; cand[s] = cand[best]; cand[best] = tmp;
+      clist_add(L, &cand[s]);
+    }
+  }
+  if (!cfg->enable_self_collision) return;
+  for (int p = 0; p < m->npairs; ++p) {
+    int la = m->pairs[p][0], lb = m->pairs[p][1];
+    int ba = m->link_body[la], bb = m->link_body[lb];
+    real ca[3], cb[3];
+    m3_v(k->R[ba], m->bound[la], ca);
+    m3_v(k->R[bb], m->bound[lb], cb);
+    real d2 = 0;
+    for (int a = 0; a < 3; ++a) { real d = (k->p[ba][a] + ca[a]) - (k->p[bb][a] + cb[a]); d2 += d * d; }
+    real rr = m->bound[la][3] + m->bound[lb][3] + margin;
+    if (d2 > rr * rr) continue;
+    for (int sa = 0; sa < 2; ++sa) {
+      real xa[3];
+      m3_v(k->R[ba], m->sphere[la][sa], xa);
+      for (int a = 0; a < 3; ++a) xa[a] += k->p[ba][a];
+      real ra = m->sphere[la][sa][3];
+      for (int sb = 0; sb < 2; ++sb) {
+        real xb[3];
+        m3_v(k->R[bb], m->sphere[lb][sb], xb);
+        for (int a = 0; a < 3; ++a) xb[a] += k->p[bb][a];
+        real rb = m->sphere[lb][sb][3];
+        real dv[3] = {xa[0] - xb[0], xa[1] - xb[1], xa[2] - xb[2]};
+        real dist = sqrtr(v3_dot(dv, dv));
+        real sep = dist - (ra + rb);
+        if (sep < margin && dist > (real)1e-9) {
+          contact_t c;
+          c.la = la; c.lb = lb; c.sep = sep;
+          for (int a = 0; a < 3; ++a) {
+            c.n[a] = dv[a] / dist;
+            c.x[a] = (real)0.5 * ((xa[a] - c.n[a] * ra) + (xb[a] + c.n[a] * rb));
+          }
+          clist_add(L, &c);
+        }
+      }
+    }
+  }
+}
+
+/* tangent basis for normal n (deterministic, shared with the kernel) */
+static void tangents(const real n[3], real t1[3], real t2[3]) {
+  if (fabs((double)n[2]) < (real)0.9) { /* t1 = normalize(z x n) */
+    real v[3] = {-n[1], n[0], 0};
+    real s = sqrtr(v[0] * v[0] + v[1] * v[1]);
+    t1[0] = v[0] / s; t1[1] = v[1] / s; t1[2] = 0;
+  } else { /* t1 = normalize(n x x) ... = (0, n2, -n1)/|.| */
+    real v[3] = {0, n[2], -n[1]};
+    real s = sqrtr(v[1] * v[1] + v[2] * v[2]);
+    t1[0] = 0; t1[1] = v[1] / s; t1[2] = v[2] / s;
+  }
+  v3_cross(n, t1, t2);
+}
+
+/* J row (length NV) of direction d at point x on body b: [x x d ; d ; S_k . f for k < b] */
+static void jac_row(const kin_t* k, int b, const real x[3], const real d[3], real J[NV]) {
+  real f[6];
+  v3_cross(x, d, f);
+  for (int a = 0; a < 3; ++a) f[3 + a] = d[a];
+  for (int a = 0; a < 6; ++a) J[a] = f[a];
+  for (int j = 0; j < ND; ++j) {
+    if (j < b) {
+      real xo[3] = {x[0] - k->org[j][0], x[1] - k->org[j][1], x[2] - k->org[j][2]};
+      real c[3];
+      v3_cross(xo, d, c);
+      J[6 + j] = v3_dot(k->axis[j], c);
+    } else {
+      J[6 + j] = 0;
+    }
+  }
+}
+
+/* ------------------------------------------------------------------------- dense solve */
+/* L L^T = A (A symmetric NVxNV, lower triangle used) */
+static void cholesky(real A[NV][NV], real L[NV][NV]) {
+  for (int j = 0; j < NV; ++j) {
+    real s = A[j][j];
+    for (int k = 0; k < j; ++k) s -= L[j][k] * L[j][k];
+    real d = sqrtr(s > (real)1e-12 ? s : (real)1e-12);
+    L[j][j] = d;
+    real inv = (real)1 / d;
+    for (int i = j + 1; i < NV; ++i) {
+      real t = A[i][j];
+      for (int k = 0; k < j; ++k) t -= L[i][k] * L[j][k];
+      L[i][j] = t * inv;
+    }
+    for (int i = 0; i < j; ++i) L[i][j] = 0;
+  }
+}
+static void fwd_sub(real L[NV][NV], const real b[NV], real y[NV]) { /* L y = b */
+  for (int i = 0; i < NV; ++i) {
+    real t = b[i];
+    for (int k = 0; k < i; ++k) t -= L[i][k] * y[k];
+    y[i] = t / L[i][i];
+  }
+}
+static void bwd_sub(real L[NV][NV], const real y[NV], real x[NV]) { /* L^T x = y */
+  for (int i = NV - 1; i >= 0; --i) {
+    real t = y[i];
+    for (int k = i + 1; k < NV; ++k) t -= L[k][i] * x[k];
+    x[i] = t / L[i][i];
+  }
+}
+static void lt_mul(real L[NV][NV], const real u[NV], real w[NV]) { /* w = L^T u */
+  for (int i = 0; i < NV; ++i) {
+    real t = 0;
+    for (int k = i; k < NV; ++k) t += L[k][i] * u[k];
+    w[i] = t;
+  }
+}
+
+/* ------------------------------------------------------------------------- one substep */
+typedef struct {
+  real net_force[NL][3];   /* net contact force per link (N) of this substep */
+  real applied_torque[ND]; /* Isaac Lab ImplicitActuator estimate at substep start */
+} substep_out_t;
+
+static void substep(const mdl_t* m, const zb_task_cfg* cfg, phys_t* s, const real target[ND],
+                    substep_out_t* out) {
+  const real dt = cfg->sim_dt;
+  kin_t k;
+  fk(m, s, &k);
+
+  /* Isaac Lab's reported applied torque: clip(kp (q* - q) - kd qdot, +-effort) */
+  for (int j = 0; j < ND; ++j)
+    out->applied_torque[j] = clampr(m->kp * (target[j] - s->jq[j]) - m->kd * s->jqd[j], -m->effort, m->effort);
+
+  sinertia I[NB], Ic[NB];
+  for (int b = 0; b < NB; ++b) body_sinertia(m, &k, b, &I[b]);
+  Ic[NB - 1] = I[NB - 1];
+  for (int b = NB - 2; b >= 0; --b) { Ic[b] = I[b]; si_add(&Ic[b], &Ic[b + 1]); }
+
+  real S[ND][6];
+  for (int j = 0; j < ND; ++j) {
+    real oxa[3];
+    v3_cross(k.org[j], k.axis[j], oxa);
+    for (int a = 0; a < 3; ++a) { S[j][a] = k.axis[j][a]; S[j][3 + a] = oxa[a]; }
+  }
+
+  /* RNEA bias forces (qddot = 0, gravity as base acceleration) */
+  real V[NB][6], A[NB][6], f[NB][6];
+  body_vel(&k, s, V);
+  for (int a = 0; a < 6; ++a) A[0][a] = 0;
+  A[0][5] = cfg->gravity;
+  for (int j = 0; j < ND; ++j) {
+    real cm[6];
+    crossm(V[j + 1], S[j], cm);
+    for (int a = 0; a < 6; ++a) A[j + 1][a] = A[j][a] + cm[a] * s->jqd[j];
+  }
+  for (int b = 0; b < NB; ++b) {
+    real IA[6], IV[6], cf[6];
+    si_mul(&I[b], A[b], IA);
+    si_mul(&I[b], V[b], IV);
+    crossf(V[b], IV, cf);
+    for (int a = 0; a < 6; ++a) f[b][a] = IA[a] + cf[a];
+  }
+  for (int b = NB - 2; b >= 0; --b)
+    for (int a = 0; a < 6; ++a) f[b][a] += f[b + 1][a];
+  real Cb[NV];
+  for (int a = 0; a < 6; ++a) Cb[a] = f[0][a];
+  for (int j = 0; j < ND; ++j) {
+    real t = 0;
+    for (int a = 0; a < 6; ++a) t += S[j][a] * f[j + 1][a];
+    Cb[6 + j] = t;
+  }
+
+  /* CRBA */
+  real M[NV][NV];
+  memset(M, 0, sizeof(M));
+  {
+    const sinertia* T = &Ic[0];
+    M[0][0] = T->I[0]; M[1][1] = T->I[1]; M[2][2] = T->I[2];
+    M[1][0] = M[0][1] = T->I[3]; M[2][0] = M[0][2] = T->I[4]; M[2][1] = M[1][2] = T->I[5];
+    /* top-right [h]x, bottom-left its transpose */
+    real hx = T->h[0], hy = T->h[1], hz = T->h[2];
+    real H[3][3] = {{0, -hz, hy}, {hz, 0, -hx}, {-hy, hx, 0}};
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) { M[i][3 + j] = H[i][j]; M[3 + j][i] = H[i][j]; }
+    M[3][3] = M[4][4] = M[5][5] = T->m;
+  }
+  for (int kk = 0; kk < ND; ++kk) {
+    real F[6];
+    si_mul(&Ic[kk + 1], S[kk], F);
+    for (int a = 0; a < 6; ++a) { M[a][6 + kk] = F[a]; M[6 + kk][a] = F[a]; }
+    for (int jj = 0; jj <= kk; ++jj) {
+      real t = 0;
+      for (int a = 0; a < 6; ++a) t += S[jj][a] * F[a];
+      M[6 + jj][6 + kk] = t;
+      M[6 + kk][6 + jj] = t;
+    }
+  }
+
+  /* implicit PD drive, pass 1 (all implicit) / pass 2 (saturated joints explicit) */
+  const real arm = dt * (m->kd + dt * m->kp);
+  real u[NV];
+  for (int a = 0; a < 3; ++a) { u[a] = s->root_angvel[a]; u[3 + a] = s->root_linvel[a]; }
+  for (int j = 0; j < ND; ++j) u[6 + j] = s->jqd[j];
+  real rhs_impl[ND];
+  for (int j = 0; j < ND; ++j)
+    rhs_impl[j] = m->kp * (target[j] - s->jq[j]) - (m->kd + dt * m->kp) * s->jqd[j];
+
+  real L[NV][NV], w[NV], Mw[NV][NV];
+  int sat[ND] = {0, 0, 0, 0, 0, 0};
+  real sat_tau[ND] = {0, 0, 0, 0, 0, 0};
+  for (int pass = 0; pass < 2; ++pass) {
+    memcpy(Mw, M, sizeof(M));
+    real b[NV];
+    for (int a = 0; a < 6; ++a) b[a] = -dt * Cb[a];
+    for (int j = 0; j < ND; ++j) {
+      if (sat[j]) {
+        b[6 + j] = dt * (sat_tau[j] - Cb[6 + j]);
+      } else {
+        Mw[6 + j][6 + j] += arm;
+        b[6 + j] = dt * (rhs_impl[j] - Cb[6 + j]);
+      }
+    }
+    cholesky(Mw, L);
+    real z[NV];
+    lt_mul(L, u, w);
+    fwd_sub(L, b, z);
+    for (int a = 0; a < NV; ++a) w[a] += z[a];
+    if (pass == 1) break;
+    real uf[NV];
+    bwd_sub(L, w, uf);
+    int any = 0;
+    for (int j = 0; j < ND; ++j) {
+      real tau = rhs_impl[j] - (arm / dt) * (uf[6 + j] - s->jqd[j]);
+      if (tau > m->effort || tau < -m->effort) { sat[j] = 1; sat_tau[j] = tau > 0 ? m->effort : -m->effort; any = 1; }
+    }
+    if (!any) break;
+  }
+
+  /* contacts */
+  clist_t CL;
+  detect(m, cfg, &k, s->root_pos[2], &CL);
+  int nc = CL.n;
+  real Y[NC_MAX][3][NV];
+  real invm[NC_MAX][3], vmin[NC_MAX], lam[NC_MAX][3];
+  real dirs[NC_MAX][3][3];
+  for (int c = 0; c < nc; ++c) {
+    const contact_t* ct = &CL.c[c];
+    for (int a = 0; a < 3; ++a) dirs[c][0][a] = ct->n[a];
+    tangents(ct->n, dirs[c][1], dirs[c][2]);
+    for (int r = 0; r < 3; ++r) {
+      real J[NV], Jb[NV];
+      jac_row(&k, m->link_body[ct->la], ct->x, dirs[c][r], J);
+      if (ct->lb >= 0) {
+        jac_row(&k, m->link_body[ct->lb], ct->x, dirs[c][r], Jb);
+        for (int a = 0; a < NV; ++a) J[a] -= Jb[a];
+      }
+      fwd_sub(L, J, Y[c][r]);
+      real yy = 0;
+      for (int a = 0; a < NV; ++a) yy += Y[c][r][a] * Y[c][r][a];
+      invm[c][r] = (real)1 / (yy + (real)1e-9);
+      lam[c][r] = 0;
+    }
+    real sep = ct->sep;
+    if (sep >= 0) vmin[c] = -sep / dt;
+    else {
+      real push = cfg->baumgarte * (-sep) / dt;
+      vmin[c] = push < m->max_depen ? push : m->max_depen;
+    }
+  }
+  const real mu = cfg->friction;
+  for (int it = 0; it < cfg->solver_iterations; ++it) {
+    for (int c = 0; c < nc; ++c) {
+      real vn = 0;
+      for (int a = 0; a < NV; ++a) vn += Y[c][0][a] * w[a];
+      real ln = lam[c][0] + (vmin[c] - vn) * invm[c][0];
+      if (ln < 0) ln = 0;
+      real dl = ln - lam[c][0];
+      lam[c][0] = ln;
+      for (int a = 0; a < NV; ++a) w[a] += Y[c][0][a] * dl;
+      real vt1 = 0, vt2 = 0;
+      for (int a = 0; a < NV; ++a) { vt1 += Y[c][1][a] * w[a]; vt2 += Y[c][2][a] * w[a]; }
+      real l1 = lam[c][1] - vt1 * invm[c][1];
+      real l2 = lam[c][2] - vt2 * invm[c][2];
+      real lim = mu * lam[c][0];
+      real mag2 = l1 * l1 + l2 * l2;
+      if (mag2 > lim * lim) {
+        real sc = lim / sqrtr(mag2);
+        l1 *= sc; l2 *= sc;
+      }
+      real d1 = l1 - lam[c][1], d2 = l2 - lam[c][2];
+      lam[c][1] = l1; lam[c][2] = l2;
+      for (int a = 0; a < NV; ++a) w[a] += Y[c][1][a] * d1 + Y[c][2][a] * d2;
+    }
+  }
+  real un[NV];
+  bwd_sub(L, w, un);
+
+  /* net contact force per link */
+  for (int l = 0; l < NL; ++l) out->net_force[l][0] = out->net_force[l][1] = out->net_force[l][2] = 0;
+  for (int c = 0; c < nc; ++c) {
+    const contact_t* ct = &CL.c[c];
+    for (int a = 0; a < 3; ++a) {
+      real F = (lam[c][0] * dirs[c][0][a] + lam[c][1] * dirs[c][1][a] + lam[c][2] * dirs[c][2][a]) / dt;
+      out->net_force[ct->la][a] += F;
+      if (ct->lb >= 0) out->net_force[ct->lb][a] -= F;
+    }
+  }
+
+  /* joint speed limit (PhysX max joint velocity = actuator velocity_limit) */
+  for (int j = 0; j < ND; ++j) un[6 + j] = clampr(un[6 + j], -m->vlim, m->vlim);
+
+  /* semi-implicit Euler. u holds the root twist at the fixed point P; the root origin's
+   * classical acceleration adds omega x v_P (spatial -> classical). */
+  real wv[3];
+  v3_cross(s->root_angvel, s->root_linvel, wv);
+  for (int a = 0; a < 3; ++a) {
+    s->root_angvel[a] = un[a];
+    s->root_linvel[a] = un[3 + a] + dt * wv[a];
+    s->root_pos[a] += dt * s->root_linvel[a];
+  }
+  {
+    real* om = s->root_angvel;
+    real th = sqrtr(om[0] * om[0] + om[1] * om[1] + om[2] * om[2]) * dt;
+    real dq[4];
+    if (th > (real)1e-12) {
+      real sc = (real)sin((double)(0.5 * th)) / th * dt;
+      dq[0] = (real)cos((double)(0.5 * th));
+      dq[1] = om[0] * sc; dq[2] = om[1] * sc; dq[3] = om[2] * sc;
+    } else {
+      dq[0] = 1; dq[1] = (real)0.5 * dt * om[0]; dq[2] = (real)0.5 * dt * om[1]; dq[3] = (real)0.5 * dt * om[2];
+    }
+    real qn[4];
+    q_mul(dq, s->root_quat, qn);
+    q_normalize(qn);
+    for (int a = 0; a < 4; ++a) s->root_quat[a] = qn[a];
+  }
+  for (int j = 0; j < ND; ++j) {
+    s->jqd[j] = un[6 + j];
+    real q = s->jq[j] + dt * s->jqd[j];
+    /* PhysX reports unlimited revolute joints wrapped to [-2pi, 2pi] (test_articulation.py:19-20) */
+    if (q > (real)TWO_PI) q -= (real)(2 * TWO_PI);
+    else if (q < -(real)TWO_PI) q += (real)(2 * TWO_PI);
+    s->jq[j] = q;
+  }
+}
+
+/* ------------------------------------------------------------------------- MDP pieces */
+/* cached kinematics of v2 _get_observations (v2.py:315-345), from a physics state */
+typedef struct {
+  real base_pos[3], base_quat[4], fwd[3], heading_err, vfwd;
+  real feet_pos[2][3], feet_z[2][3], feet_x[2][3];
+} obs_cache_t;
+
+static void quat_apply(const real q[4], const real v[3], real o[3]) {
+  real R[9];
+  q_to_mat(q, R);
+  m3_v(R, v, o);
+}
+
+/* fills the cache from base/feet link poses and the base COM velocity (all world) */
+static void make_cache(const real base_pos[3], const real base_quat[4], const real feet_pos[2][3],
+                       const real feet_quat[2][4], const real base_com_vel[3], obs_cache_t* o) {
+  static const real zax[3] = {0, 0, 1}, xax[3] = {1, 0, 0}, mzax[3] = {0, 0, -1};
+  static const real g[3] = {0, 0, -1}; /* GRAVITY_VEC_W: normalised gravity direction */
+  real sh[3];
+  for (int a = 0; a < 3; ++a) o->base_pos[a] = base_pos[a];
+  for (int a = 0; a < 4; ++a) o->base_quat[a] = base_quat[a];
+  quat_apply(base_quat, zax, sh);            /* v2.py:322 */
+  v3_cross(g, sh, o->fwd);                   /* v2.py:323 */
+  o->heading_err = -o->fwd[1];               /* v2.py:324 */
+  o->vfwd = v3_dot(base_com_vel, o->fwd);    /* v2.py:326-327 */
+  for (int f = 0; f < 2; ++f) {
+    for (int a = 0; a < 3; ++a) o->feet_pos[f][a] = feet_pos[f][a];
+    quat_apply(feet_quat[f], f == 0 ? zax : mzax, o->feet_z[f]); /* v2.py:341-344 */
+    quat_apply(feet_quat[f], xax, o->feet_x[f]);                 /* v2.py:338-345 */
+  }
+}
+
+static void cache_from_phys(const mdl_t* m, const phys_t* s, obs_cache_t* o) {
+  kin_t k;
+  fk(m, s, &k);
+  real V[NB][6];
+  body_vel(&k, s, V);
+  real bp[3], bq[4], fp[2][3], fq[2][4], bv[3], c[3];
+  link_pose(m, &k, m->base_link, bp, bq);
+  for (int f = 0; f < 2; ++f) link_pose(m, &k, m->foot_links[f], fp[f], fq[f]);
+  int bb = m->link_body[m->base_link];
+  m3_v(k.R[bb], m->link_com[m->base_link], c);
+  for (int a = 0; a < 3; ++a) c[a] += k.p[bb][a];
+  point_vel(V[bb], c, bv);
+  for (int a = 0; a < 3; ++a) {
+    bp[a] += s->root_pos[a];
+    fp[0][a] += s->root_pos[a];
+    fp[1][a] += s->root_pos[a];
+  }
+  make_cache(bp, bq, fp, fq, bv, o);
+}
+
+/* post-step quantities the reward/done terms read directly from the sim (no lag) */
+typedef struct {
+  real jq[ND], jqd[ND], applied_torque[ND];
+  real feet_vel[2][3];              /* body_com_lin_vel_w of the feet */
+  real feet_fz_hist[ZB_HIST][2];    /* sensor history, slot 0 newest */
+  real undes_fmax_hist[ZB_HIST];
+  real feet_air_last[2];
+  int32_t ep_len;                   /* after the += 1 */
+  real origin_y;
+} post_t;
+
+/* _get_dones (v2.py:384-411) + _get_rewards (v2.py:371-382, terms 461-561). Updates the MDP
+ * integrators in `md`; returns reward; terms[] receives the scaled per-term rewards. */
+static real mdp_eval(const zb_task_cfg* cfg, const real jq0[ND], const obs_cache_t* pre,
+                     const post_t* ps, mdp_t* md, const real act[ND], const real prev_act[ND],
+                     real terms[ZB_NUM_REWARD_TERMS], int* died_out, int* timeout_out) {
+  /* ---- dones */
+  int time_out = ps->ep_len >= cfg->max_episode_length - 1;
+  real feetF[2];
+  for (int f = 0; f < 2; ++f) {
+    real s = 0;
+    for (int h = 0; h < ZB_HIST; ++h) s += ps->feet_fz_hist[h][f];
+    feetF[f] = s / (real)ZB_HIST;                          /* v2.py:387-390 */
+  }
+  int died = 0;
+  for (int h = 0; h < ZB_HIST; ++h) died |= ps->undes_fmax_hist[h] > (real)1.0; /* v2.py:396-402 */
+  died |= pre->base_pos[2] < cfg->termination_height;      /* v2.py:405 */
+  real base_y_err = pre->base_pos[1] - ps->origin_y;       /* v2.py:406 */
+  died |= fabs((double)base_y_err) > 0.5;                  /* v2.py:407 */
+
+  /* ---- rewards in dict order */
+  const float* sc = cfg->reward_scales;
+  real r[ZB_NUM_REWARD_TERMS];
+  r[ZB_R_BASE_VEL_FORWARD] = (real)tanh((double)(10 * pre->vfwd / cfg->joint_speed_limit));
+  {
+    real s = 0;
+    for (int f = 0; f < 2; ++f) {
+      real d[3] = {pre->feet_z[f][0], pre->feet_z[f][1], pre->feet_z[f][2] - 1};
+      s += sqrtr(v3_dot(d, d));
+    }
+    r[ZB_R_FEET_DOWNWARD] = s;
+  }
+  {
+    real s = 0;
+    for (int f = 0; f < 2; ++f) {
+      real d[3] = {pre->feet_x[f][0] - pre->fwd[0], pre->feet_x[f][1] - pre->fwd[1], pre->feet_x[f][2] - pre->fwd[2]};
+      s += sqrtr(v3_dot(d, d));
+    }
+    r[ZB_R_FEET_FORWARD] = s;
+  }
+  r[ZB_R_BASE_HEADING_X] = (real)fabs((double)pre->heading_err);
+  md->heading_sum = clampr(md->heading_sum + (real)0.01 * pre->heading_err, -1, 1);
+  r[ZB_R_BASE_HEADING_X_SUM] = (real)fabs((double)md->heading_sum);
+  {
+    /* step_length v2.py:509-533 */
+    real minlen = 0;
+    for (int f = 0; f < 2; ++f) {
+      int down = feetF[f] > (real)10.0 && md->feet_f_last[f] < (real)10.0;
+      if (down) {
+        real d[3] = {pre->feet_pos[f][0] - md->feet_down_pos[f][0], pre->feet_pos[f][1] - md->feet_down_pos[f][1],
+                     pre->feet_pos[f][2] - md->feet_down_pos[f][2]};
+        md->feet_step_len[f] = v3_dot(d, pre->fwd);
+        for (int a = 0; a < 3; ++a) md->feet_down_pos[f][a] = pre->feet_pos[f][a];
+      }
+    }
+    minlen = md->feet_step_len[0] < md->feet_step_len[1] ? md->feet_step_len[0] : md->feet_step_len[1];
+    md->feet_f_last[0] = feetF[0];
+    md->feet_f_last[1] = feetF[1];
+    r[ZB_R_STEP_LENGTH] = (real)tanh((double)(15 * minlen));
+  }
+  r[ZB_R_AIRTIME_BALANCE] = (real)fabs((double)(ps->feet_air_last[0] - ps->feet_air_last[1]));
+  {
+    real s = 0;
+    for (int j = 0; j < ND; ++j) { real d = act[j] - prev_act[j]; s += d * d; }
+    r[ZB_R_ACTION_RATE] = s;
+  }
+  {
+    real s = 0;
+    for (int j = 0; j < ND; ++j) s += ps->applied_torque[j] * ps->applied_torque[j];
+    r[ZB_R_TORQUES] = s;
+  }
+  {
+    real s = 0;
+    for (int f = 0; f < 2; ++f) {
+      real v = sqrtr(ps->feet_vel[f][0] * ps->feet_vel[f][0] + ps->feet_vel[f][1] * ps->feet_vel[f][1]);
+      s += v * (feetF[f] > (real)1.0 ? (real)1 : (real)0);
+    }
+    r[ZB_R_FEET_SLIDE] = s;
+  }
+  r[ZB_R_BASE_POS_Y_ERR] = (real)fabs((double)(pre->feet_pos[0][1] + pre->feet_pos[1][1] - 2 * ps->origin_y)) +
+                           (real)fabs((double)(pre->base_pos[1] - ps->origin_y));
+  md->yerr_sum = clampr(md->yerr_sum + (real)0.01 * base_y_err, -1, 1);
+  r[ZB_R_BASE_POS_Y_ERR_SUM] = (real)fabs((double)md->yerr_sum);
+  r[ZB_R_AIRTIME_SUM] = (real)tanh((double)(ps->feet_air_last[0] + ps->feet_air_last[1]));
+
+  real rew = 0;
+  for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) {
+    real v = r[t] * sc[t];
+    terms[t] = v;
+    rew += v;
+    md->ep_sums[t] += v;
+  }
+  if (died) rew -= cfg->terminal_penalty;  /* v2.py:379-380 */
+  (void)jq0;
+  *died_out = died;
+  *timeout_out = time_out;
+  return rew;
+}
+
+/* ContactSensor lazy update once per policy step: history roll, air/contact
+ * timers with elapsed = step_dt, is_contact = |F| > threshold. */
+static void sensor_update(const mdl_t* m, const zb_task_cfg* cfg, mdp_t* md, const real F[NL][3]) {
+  for (int h = ZB_HIST - 1; h > 0; --h) {
+    md->feet_fz_hist[h][0] = md->feet_fz_hist[h - 1][0];
+    md->feet_fz_hist[h][1] = md->feet_fz_hist[h - 1][1];
+    md->undes_fmax_hist[h] = md->undes_fmax_hist[h - 1];
+  }
+  real fmax = 0;
+  for (int k = 0; k < 10; ++k) {
+    const real* f = F[m->undesired[k]];
+    real nrm = sqrtr(v3_dot(f, f));
+    if (nrm > fmax) fmax = nrm;
+  }
+  md->undes_fmax_hist[0] = fmax;
+  const real el = cfg->sim_dt * (real)cfg->decimation;
+  for (int f = 0; f < 2; ++f) {
+    const real* Ff = F[m->foot_links[f]];
+    md->feet_fz_hist[0][f] = Ff[2];
+    int contact = sqrtr(v3_dot(Ff, Ff)) > cfg->contact_force_threshold;
+    int first_contact = md->feet_air_cur[f] > 0 && contact;
+    if (first_contact) md->feet_air_last[f] = md->feet_air_cur[f] + el;
+    md->feet_air_cur[f] = contact ? 0 : md->feet_air_cur[f] + el;
+    md->feet_contact_cur[f] = contact ? md->feet_contact_cur[f] + el : 0;
+  }
+}
+
+/* default physical state (reset pose) */
+static void phys_default(const mdl_t* m, phys_t* s) {
+  for (int a = 0; a < 3; ++a) { s->root_pos[a] = m->root_pos0[a]; s->root_linvel[a] = 0; s->root_angvel[a] = 0; }
+  for (int a = 0; a < 4; ++a) s->root_quat[a] = m->root_quat0[a];
+  for (int j = 0; j < ND; ++j) { s->jq[j] = m->jq0[j]; s->jqd[j] = 0; }
+}
+
+/* _reset_idx for one env (v2.py:413-459); the episode-log accumulation is done by the caller */
+static void reset_env(const mdl_t* m, env_t* e) {
+  phys_default(m, &e->ph);
+  mdp_t* md = &e->md;
+  for (int j = 0; j < ND; ++j) { md->p_delta[j] = 0; md->actions[j] = 0; }
+  /* feet_down_pos_last <- post-reset feet positions (Isaac Lab refreshes link
+   * kinematics on read after write_*_to_sim) */
+  {
+    kin_t k;
+    fk(m, &e->ph, &k);
+    for (int f = 0; f < 2; ++f) {
+      real p[3], q[4];
+      link_pose(m, &k, m->foot_links[f], p, q);
+      for (int a = 0; a < 3; ++a) md->feet_down_pos[f][a] = p[a] + e->ph.root_pos[a];
+    }
+  }
+  md->heading_sum = 0;
+  md->yerr_sum = 0;
+  /* ContactSensor.reset: history and timers zeroed */
+  for (int h = 0; h < ZB_HIST; ++h) { md->feet_fz_hist[h][0] = md->feet_fz_hist[h][1] = 0; md->undes_fmax_hist[h] = 0; }
+  for (int f = 0; f < 2; ++f) { md->feet_air_cur[f] = md->feet_air_last[f] = md->feet_contact_cur[f] = 0; }
+  md->ep_len = 0;
+  for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) md->ep_sums[t] = 0;
+  /* NOT reset (reference quirk): feet_step_len, feet_f_last */
+}
+
+static void write_obs(const mdl_t* m, const env_t* e, float* obs) {
+  obs_cache_t oc;
+  cache_from_phys(m, &e->ph, &oc);
+  for (int a = 0; a < 4; ++a) obs[a] = (float)oc.base_quat[a];
+  for (int j = 0; j < ND; ++j) {
+    obs[4 + j] = (float)(e->ph.jq[j] - m->jq0[j]);
+    obs[10 + j] = (float)e->ph.jqd[j];
+    obs[16 + j] = (float)e->md.actions[j];
+  }
+  obs[22] = 1.0f; /* joint_speed_limit (v2.py:243) */
+}
+
+/* ========================================================================= public API */
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+zbo_sim* zbo_create(const zb_model* model, const zb_task_cfg* cfg, int num_envs, uint64_t seed) {
+  zbo_sim* s = (zbo_sim*)calloc(1, sizeof(zbo_sim));
+  load_mdl(model, &s->m);
+  s->c = *cfg;
+  s->n = num_envs;
+  s->seed = seed;
+  s->env = (env_t*)calloc((size_t)num_envs, sizeof(env_t));
+  for (int i = 0; i < num_envs; ++i) {
+    memset(&s->env[i], 0, sizeof(env_t));
+    reset_env(&s->m, &s->env[i]);
+  }
+  return s;
+}
+
+void zbo_destroy(zbo_sim* s) {
+  if (!s) return;
+  free(s->env);
+  free(s);
+}
+
+int zbo_set_threads(int n) {
+#ifdef _OPENMP
+  if (n > 0) omp_set_num_threads(n);
+  return omp_get_max_threads();
+#else
+  (void)n;
+  return 1;
+#endif
+}
+
+int zbo_reset(zbo_sim* s, const int32_t* env_ids, int n) {
+  int all = env_ids == NULL || n == s->n;
+  int cnt = env_ids ? n : s->n;
+  for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) s->log_means[t] = 0;
+  for (int i = 0; i < cnt; ++i) {
+    int e = env_ids ? env_ids[i] : i;
+    for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) s->log_means[t] += (float)s->env[e].md.ep_sums[t];
+    reset_env(&s->m, &s->env[e]);
+  }
+  const float ep_s = s->c.sim_dt * s->c.decimation * s->c.max_episode_length;
+  for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) s->log_means[t] = cnt ? s->log_means[t] / cnt / ep_s : 0;
+  s->log_counts[0] = s->log_counts[1] = 0;
+  if (all) {
+    /* v2.py:418-422 episode_length_buf ~ U{0..max_episode_length-1} */
+    uint64_t ctr = s->reset_counter++;
+    for (int e = 0; e < s->n; ++e) {
+      uint64_t h = zb_hash64(s->seed ^ zb_hash64(ctr * 0x100000001B3ull + (uint64_t)e));
+      s->env[e].md.ep_len = (int32_t)(h % (uint64_t)s->c.max_episode_length);
+    }
+  }
+  return 0;
+}
+
+int zbo_observe(zbo_sim* s, float* obs) {
+  for (int e = 0; e < s->n; ++e) write_obs(&s->m, &s->env[e], obs + (size_t)e * ZB_OBS_DIM);
+  return 0;
+}
+
+/* full policy step for env e; returns reward, sets flags; accumulates log into acc[15] */
+static real step_env(const mdl_t* m, const zb_task_cfg* cfg, env_t* e, const float* action, float* obs,
+                     int* died, int* tout, real acc[ZB_NUM_REWARD_TERMS]) {
+  mdp_t* md = &e->md;
+  /* _pre_physics_step (v2.py:276-287) */
+  real act[ND], prev[ND], target[ND];
+  for (int j = 0; j < ND; ++j) {
+    prev[j] = md->actions[j];
+    act[j] = (real)tanh((double)action[j]);
+    real pd = md->p_delta[j] + (real)PI_R * act[j] * cfg->joint_speed_limit * (cfg->sim_dt * cfg->decimation);
+    pd = clampr(pd, -(real)PI_R, (real)PI_R);
+    md->p_delta[j] = pd;
+    target[j] = pd + m->jq0[j];
+  }
+  /* the previous step's _get_observations cache (one-step lag) */
+  obs_cache_t pre;
+  cache_from_phys(m, &e->ph, &pre);
+  /* physics */
+  substep_out_t so;
+  for (int k = 0; k < cfg->decimation; ++k) substep(m, cfg, &e->ph, target, &so);
+  sensor_update(m, cfg, md, so.net_force);
+  md->ep_len += 1;
+  /* post-step reads */
+  post_t ps;
+  {
+    kin_t k;
+    fk(m, &e->ph, &k);
+    real V[NB][6];
+    body_vel(&k, &e->ph, V);
+    for (int f = 0; f < 2; ++f) {
+      int l = m->foot_links[f], b = m->link_body[l];
+      real c[3];
+      m3_v(k.R[b], m->link_com[l], c);
+      for (int a = 0; a < 3; ++a) c[a] += k.p[b][a];
+      point_vel(V[b], c, ps.feet_vel[f]);
+    }
+  }
+  for (int j = 0; j < ND; ++j) { ps.jq[j] = e->ph.jq[j]; ps.jqd[j] = e->ph.jqd[j]; ps.applied_torque[j] = so.applied_torque[j]; }
+  for (int h = 0; h < ZB_HIST; ++h) {
+    ps.feet_fz_hist[h][0] = md->feet_fz_hist[h][0];
+    ps.feet_fz_hist[h][1] = md->feet_fz_hist[h][1];
+    ps.undes_fmax_hist[h] = md->undes_fmax_hist[h];
+  }
+  ps.feet_air_last[0] = md->feet_air_last[0];
+  ps.feet_air_last[1] = md->feet_air_last[1];
+  ps.ep_len = md->ep_len;
+  ps.origin_y = 0;
+  real terms[ZB_NUM_REWARD_TERMS];
+  for (int j = 0; j < ND; ++j) md->actions[j] = act[j];
+  real rew = mdp_eval(cfg, m->jq0, &pre, &ps, md, act, prev, terms, died, tout);
+  if (*died || *tout) {
+    for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) acc[t] += md->ep_sums[t];
+    reset_env(m, e);
+  }
+  write_obs(m, e, obs);
+  return rew;
+}
+
+int zbo_step(zbo_sim* s, const float* actions, float* obs, float* reward, uint8_t* terminated, uint8_t* truncated) {
+  real acc[ZB_NUM_REWARD_TERMS];
+  for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) acc[t] = 0;
+  int nreset = 0, nterm = 0, ntout = 0;
+#pragma omp parallel
+  {
+    real acc_l[ZB_NUM_REWARD_TERMS];
+    int nr = 0, nt = 0, no = 0;
+    for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) acc_l[t] = 0;
+#pragma omp for schedule(static)
+    for (int e = 0; e < s->n; ++e) {
+      int died = 0, tout = 0;
+      reward[e] = (float)step_env(&s->m, &s->c, &s->env[e], actions + (size_t)e * ZB_ACT_DIM,
+                                  obs + (size_t)e * ZB_OBS_DIM, &died, &tout, acc_l);
+      terminated[e] = (uint8_t)died;
+      truncated[e] = (uint8_t)tout;
+      nr += died || tout; nt += died; no += tout;
+    }
+#pragma omp critical
+    {
+      for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) acc[t] += acc_l[t];
+      nreset += nr; nterm += nt; ntout += no;
+    }
+  }
+  if (nreset > 0) {
+    const float ep_s = s->c.sim_dt * s->c.decimation * s->c.max_episode_length;
+    for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) s->log_means[t] = (float)(acc[t] / nreset / ep_s);
+    s->log_counts[0] = nterm;
+    s->log_counts[1] = ntout;
+  }
+  if (nreset == s->n) {
+    /* every env reset in this step: _reset_idx saw len(env_ids) == num_envs (v2.py:418-422) */
+    uint64_t ctr = s->reset_counter++;
+    for (int e = 0; e < s->n; ++e) {
+      uint64_t h = zb_hash64(s->seed ^ zb_hash64(ctr * 0x100000001B3ull + (uint64_t)e));
+      s->env[e].md.ep_len = (int32_t)(h % (uint64_t)s->c.max_episode_length);
+    }
+  }
+  return 0;
+}
+
+int zbo_read_log(zbo_sim* s, float* term_means, int32_t* counts) {
+  for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) term_means[t] = s->log_means[t];
+  counts[0] = s->log_counts[0];
+  counts[1] = s->log_counts[1];
+  return 0;
+}
+
+/* state <-> SoA [ZB_STATE_DIM][N] */
+static void pack_env(const env_t* e, float* st, int n, int i) {
+#define PUT(off, val) st[(size_t)(off) * n + i] = (float)(val)
+  for (int a = 0; a < 3; ++a) { PUT(ZB_S_ROOT_POS + a, e->ph.root_pos[a]); PUT(ZB_S_ROOT_LINVEL + a, e->ph.root_linvel[a]); PUT(ZB_S_ROOT_ANGVEL + a, e->ph.root_angvel[a]); }
+  for (int a = 0; a < 4; ++a) PUT(ZB_S_ROOT_QUAT + a, e->ph.root_quat[a]);
+  for (int j = 0; j < ND; ++j) {
+    PUT(ZB_S_JOINT_POS + j, e->ph.jq[j]); PUT(ZB_S_JOINT_VEL + j, e->ph.jqd[j]);
+    PUT(ZB_S_P_DELTA + j, e->md.p_delta[j]); PUT(ZB_S_ACTIONS + j, e->md.actions[j]);
+  }
+  for (int f = 0; f < 2; ++f) {
+    for (int a = 0; a < 3; ++a) PUT(ZB_S_FEET_DOWN_POS + 3 * f + a, e->md.feet_down_pos[f][a]);
+    PUT(ZB_S_FEET_STEP_LEN + f, e->md.feet_step_len[f]);
+    PUT(ZB_S_FEET_F_LAST + f, e->md.feet_f_last[f]);
+    PUT(ZB_S_FEET_AIR_CUR + f, e->md.feet_air_cur[f]);
+    PUT(ZB_S_FEET_AIR_LAST + f, e->md.feet_air_last[f]);
+    PUT(ZB_S_FEET_CONTACT_CUR + f, e->md.feet_contact_cur[f]);
+  }
+  PUT(ZB_S_HEADING_SUM, e->md.heading_sum);
+  PUT(ZB_S_Y_ERR_SUM, e->md.yerr_sum);
+  for (int h = 0; h < ZB_HIST; ++h) {
+    PUT(ZB_S_FEET_FZ_HIST + 2 * h, e->md.feet_fz_hist[h][0]);
+    PUT(ZB_S_FEET_FZ_HIST + 2 * h + 1, e->md.feet_fz_hist[h][1]);
+    PUT(ZB_S_UNDES_FMAX_HIST + h, e->md.undes_fmax_hist[h]);
+  }
+  PUT(ZB_S_EP_LEN, e->md.ep_len);
+  for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) PUT(ZB_S_EP_SUMS + t, e->md.ep_sums[t]);
+#undef PUT
+}
+static void unpack_env(env_t* e, const float* st, int n, int i) {
+#define GET(off) ((real)st[(size_t)(off) * n + i])
+  for (int a = 0; a < 3; ++a) { e->ph.root_pos[a] = GET(ZB_S_ROOT_POS + a); e->ph.root_linvel[a] = GET(ZB_S_ROOT_LINVEL + a); e->ph.root_angvel[a] = GET(ZB_S_ROOT_ANGVEL + a); }
+  for (int a = 0; a < 4; ++a) e->ph.root_quat[a] = GET(ZB_S_ROOT_QUAT + a);
+  for (int j = 0; j < ND; ++j) {
+    e->ph.jq[j] = GET(ZB_S_JOINT_POS + j); e->ph.jqd[j] = GET(ZB_S_JOINT_VEL + j);
+    e->md.p_delta[j] = GET(ZB_S_P_DELTA + j); e->md.actions[j] = GET(ZB_S_ACTIONS + j);
+  }
+  for (int f = 0; f < 2; ++f) {
+    for (int a = 0; a < 3; ++a) e->md.feet_down_pos[f][a] = GET(ZB_S_FEET_DOWN_POS + 3 * f + a);
+    e->md.feet_step_len[f] = GET(ZB_S_FEET_STEP_LEN + f);
+    e->md.feet_f_last[f] = GET(ZB_S_FEET_F_LAST + f);
+    e->md.feet_air_cur[f] = GET(ZB_S_FEET_AIR_CUR + f);
+    e->md.feet_air_last[f] = GET(ZB_S_FEET_AIR_LAST + f);
+    e->md.feet_contact_cur[f] = GET(ZB_S_FEET_CONTACT_CUR + f);
+  }
+  e->md.heading_sum = GET(ZB_S_HEADING_SUM);
+  e->md.yerr_sum = GET(ZB_S_Y_ERR_SUM);
+  for (int h = 0; h < ZB_HIST; ++h) {
+    e->md.feet_fz_hist[h][0] = GET(ZB_S_FEET_FZ_HIST + 2 * h);
+    e->md.feet_fz_hist[h][1] = GET(ZB_S_FEET_FZ_HIST + 2 * h + 1);
+    e->md.undes_fmax_hist[h] = GET(ZB_S_UNDES_FMAX_HIST + h);
+  }
+  e->md.ep_len = (int32_t)lrint((double)st[(size_t)ZB_S_EP_LEN * n + i]);
+  for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) e->md.ep_sums[t] = GET(ZB_S_EP_SUMS + t);
+#undef GET
+}
+
+int zbo_get_state(zbo_sim* s, float* dst) {
+  for (int e = 0; e < s->n; ++e) pack_env(&s->env[e], dst, s->n, e);
+  return 0;
+}
+int zbo_set_state(zbo_sim* s, const float* src) {
+  for (int e = 0; e < s->n; ++e) unpack_env(&s->env[e], src, s->n, e);
+  return 0;
+}
+
+int zbo_physics_substeps(zbo_sim* s, const float* targets, int nsub, float* net_force, float* applied_torque) {
+#pragma omp parallel for schedule(static)
+  for (int e = 0; e < s->n; ++e) {
+    real tg[ND];
+    for (int j = 0; j < ND; ++j) tg[j] = targets[(size_t)e * ND + j];
+    substep_out_t so;
+    memset(&so, 0, sizeof(so));
+    for (int k = 0; k < nsub; ++k) substep(&s->m, &s->c, &s->env[e].ph, tg, &so);
+    if (net_force)
+      for (int l = 0; l < NL; ++l)
+        for (int a = 0; a < 3; ++a) net_force[((size_t)e * NL + l) * 3 + a] = (float)so.net_force[l][a];
+    if (applied_torque)
+      for (int j = 0; j < ND; ++j) applied_torque[(size_t)e * ND + j] = (float)so.applied_torque[j];
+  }
+  return 0;
+}
+
+/* ------------------------------------------------------------------ golden-vector entry points
+ * These expose the MDP restatement on raw Isaac-Lab-shaped inputs so it can be checked against
+ * vectors produced by the reference's own ZbotDirectEnvV2 code (tests/test_oracle_mdp.py). */
+
+/* _pre_physics_step: actions [n][6] -> tanh actions, p_delta (in/out), targets */
+int zbo_pre_physics(int n, const zb_task_cfg* cfg, const float* jq0, const float* actions, float* p_delta,
+                    float* act_out, float* targets) {
+  for (int e = 0; e < n; ++e)
+    for (int j = 0; j < ND; ++j) {
+      size_t i = (size_t)e * ND + j;
+      real a = (real)tanh((double)actions[i]);
+      real pd = (real)p_delta[i] + (real)PI_R * a * cfg->joint_speed_limit * (cfg->sim_dt * cfg->decimation);
+      pd = clampr(pd, -(real)PI_R, (real)PI_R);
+      p_delta[i] = (float)pd;
+      act_out[i] = (float)a;
+      targets[i] = (float)(pd + jq0[j]);
+    }
+  return 0;
+}
+
+/* cached kinematics of _get_observations from Isaac-Lab-shaped body data:
+ * base/feet link pose + base COM velocity -> cache[n][24]:
+ * base_pos 3, base_quat 4, fwd 3, heading_err 1, vfwd 1, feet_pos 6, feet_z 6 (-> 24) ; feet_x 6 separately */
+int zbo_obs_cache(int n, const float* base_pos, const float* base_quat, const float* feet_pos, const float* feet_quat,
+                  const float* base_com_vel, float* cache /*[n][30]*/) {
+  for (int e = 0; e < n; ++e) {
+    real bp[3], bq[4], fp[2][3], fq[2][4], bv[3];
+    for (int a = 0; a < 3; ++a) { bp[a] = base_pos[e * 3 + a]; bv[a] = base_com_vel[e * 3 + a]; }
+    for (int a = 0; a < 4; ++a) bq[a] = base_quat[e * 4 + a];
+    for (int f = 0; f < 2; ++f) {
+      for (int a = 0; a < 3; ++a) fp[f][a] = feet_pos[(e * 2 + f) * 3 + a];
+      for (int a = 0; a < 4; ++a) fq[f][a] = feet_quat[(e * 2 + f) * 4 + a];
+    }
+    obs_cache_t o;
+    make_cache(bp, bq, fp, fq, bv, &o);
+    float* c = cache + (size_t)e * 30;
+    for (int a = 0; a < 3; ++a) c[a] = (float)o.base_pos[a];
+    for (int a = 0; a < 4; ++a) c[3 + a] = (float)o.base_quat[a];
+    for (int a = 0; a < 3; ++a) c[7 + a] = (float)o.fwd[a];
+    c[10] = (float)o.heading_err;
+    c[11] = (float)o.vfwd;
+    for (int f = 0; f < 2; ++f)
+      for (int a = 0; a < 3; ++a) {
+        c[12 + 3 * f + a] = (float)o.feet_pos[f][a];
+        c[18 + 3 * f + a] = (float)o.feet_z[f][a];
+        c[24 + 3 * f + a] = (float)o.feet_x[f][a];
+      }
+  }
+  return 0;
+}
+
+/* _get_dones + _get_rewards on raw inputs. cache: [n][30] from zbo_obs_cache of the PREVIOUS
+ * _get_observations; mdp_state: [n][13] = feet_down_pos 6, feet_step_len 2, feet_f_last 2,
+ * heading_sum, yerr_sum, (pad); ep_sums [n][13] in/out. */
+int zbo_mdp_eval(int n, const zb_task_cfg* cfg, const float* cache, const float* applied_torque,
+                 const float* feet_vel /*[n][2][3]*/, const float* feet_fz_hist /*[n][5][2]*/,
+                 const float* undes_fmax_hist /*[n][5]*/, const float* feet_air_last /*[n][2]*/,
+                 const int32_t* ep_len, const float* origin_y, const float* act, const float* prev_act,
+                 float* mdp_state, float* ep_sums, float* reward, float* terms, uint8_t* died, uint8_t* time_out) {
+  real jq0[ND] = {0, 0, 0, 0, 0, 0};
+  for (int e = 0; e < n; ++e) {
+    const float* c = cache + (size_t)e * 30;
+    obs_cache_t pre;
+    for (int a = 0; a < 3; ++a) { pre.base_pos[a] = c[a]; pre.fwd[a] = c[7 + a]; }
+    for (int a = 0; a < 4; ++a) pre.base_quat[a] = c[3 + a];
+    pre.heading_err = c[10];
+    pre.vfwd = c[11];
+    for (int f = 0; f < 2; ++f)
+      for (int a = 0; a < 3; ++a) {
+        pre.feet_pos[f][a] = c[12 + 3 * f + a];
+        pre.feet_z[f][a] = c[18 + 3 * f + a];
+        pre.feet_x[f][a] = c[24 + 3 * f + a];
+      }
+    post_t ps;
+    memset(&ps, 0, sizeof(ps));
+    for (int j = 0; j < ND; ++j) ps.applied_torque[j] = applied_torque[(size_t)e * ND + j];
+    for (int f = 0; f < 2; ++f) {
+      for (int a = 0; a < 3; ++a) ps.feet_vel[f][a] = feet_vel[((size_t)e * 2 + f) * 3 + a];
+      ps.feet_air_last[f] = feet_air_last[(size_t)e * 2 + f];
+    }
+    for (int h = 0; h < ZB_HIST; ++h) {
+      ps.feet_fz_hist[h][0] = feet_fz_hist[((size_t)e * ZB_HIST + h) * 2];
+      ps.feet_fz_hist[h][1] = feet_fz_hist[((size_t)e * ZB_HIST + h) * 2 + 1];
+      ps.undes_fmax_hist[h] = undes_fmax_hist[(size_t)e * ZB_HIST + h];
+    }
+    ps.ep_len = ep_len[e];
+    ps.origin_y = origin_y[e];
+    mdp_t md;
+    memset(&md, 0, sizeof(md));
+    float* st = mdp_state + (size_t)e * 13;
+    for (int f = 0; f < 2; ++f) {
+      for (int a = 0; a < 3; ++a) md.feet_down_pos[f][a] = st[3 * f + a];
+      md.feet_step_len[f] = st[6 + f];
+      md.feet_f_last[f] = st[8 + f];
+    }
+    md.heading_sum = st[10];
+    md.yerr_sum = st[11];
+    for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) md.ep_sums[t] = ep_sums[(size_t)e * ZB_NUM_REWARD_TERMS + t];
+    real a_[ND], p_[ND], tr[ZB_NUM_REWARD_TERMS];
+    for (int j = 0; j < ND; ++j) { a_[j] = act[(size_t)e * ND + j]; p_[j] = prev_act[(size_t)e * ND + j]; }
+    int d = 0, to = 0;
+    reward[e] = (float)mdp_eval(cfg, jq0, &pre, &ps, &md, a_, p_, tr, &d, &to);
+    for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) {
+      terms[(size_t)e * ZB_NUM_REWARD_TERMS + t] = (float)tr[t];
+      ep_sums[(size_t)e * ZB_NUM_REWARD_TERMS + t] = (float)md.ep_sums[t];
+    }
+    for (int f = 0; f < 2; ++f) {
+      for (int a = 0; a < 3; ++a) st[3 * f + a] = (float)md.feet_down_pos[f][a];
+      st[6 + f] = (float)md.feet_step_len[f];
+      st[8 + f] = (float)md.feet_f_last[f];
+    }
+    st[10] = (float)md.heading_sum;
+    st[11] = (float)md.yerr_sum;
+    died[e] = (uint8_t)d;
+    time_out[e] = (uint8_t)to;
+  }
+  return 0;
+}
+
+/* world link poses for FK known-answer tests: pos [n][12][3] (env-local), quat [n][12][4] */
+int zbo_link_poses(zbo_sim* s, float* pos, float* quat) {
+  for (int e = 0; e < s->n; ++e) {
+    kin_t k;
+    fk(&s->m, &s->env[e].ph, &k);
+    for (int l = 0; l < NL; ++l) {
+      real p[3], q[4];
+      link_pose(&s->m, &k, l, p, q);
+      for (int a = 0; a < 3; ++a) pos[((size_t)e * NL + l) * 3 + a] = (float)(p[a] + s->env[e].ph.root_pos[a]);
+      for (int a = 0; a < 4; ++a) quat[((size_t)e * NL + l) * 4 + a] = (float)q[a];
+    }
+  }
+  return 0;
+}
+
+/* link COM linear velocities [n][12][3] (body_com_lin_vel_w) */
+int zbo_link_com_vel(zbo_sim* s, float* vel) {
+  for (int e = 0; e < s->n; ++e) {
+    kin_t k;
+    fk(&s->m, &s->env[e].ph, &k);
+    real V[NB][6];
+    body_vel(&k, &s->env[e].ph, V);
+    for (int l = 0; l < NL; ++l) {
+      int b = s->m.link_body[l];
+      real c[3], v[3];
+      m3_v(k.R[b], s->m.link_com[l], c);
+      for (int a = 0; a < 3; ++a) c[a] += k.p[b][a];
+      point_vel(V[b], c, v);
+      for (int a = 0; a < 3; ++a) vel[((size_t)e * NL + l) * 3 + a] = (float)v[a];
+    }
+  }
+  return 0;
+}
+
+/* total mechanical energy and momentum (invariant tests): out[n][7] = E, p(3), L_about_origin(3) */
+int zbo_energy_momentum(zbo_sim* s, float* out) {
+  for (int e = 0; e < s->n; ++e) {
+    const phys_t* ph = &s->env[e].ph;
+    kin_t k;
+    fk(&s->m, ph, &k);
+    real V[NB][6];
+    body_vel(&k, ph, V);
+    real E = 0, P[3] = {0, 0, 0}, Lm[3] = {0, 0, 0};
+    for (int b = 0; b < NB; ++b) {
+      sinertia I;
+      body_sinertia(&s->m, &k, b, &I);
+      real f[6];
+      si_mul(&I, V[b], f);
+      E += (real)0.5 * (f[0] * V[b][0] + f[1] * V[b][1] + f[2] * V[b][2] + f[3] * V[b][3] + f[4] * V[b][4] + f[5] * V[b][5]);
+      real cz = I.h[2] / I.m + ph->root_pos[2];
+      E += I.m * s->c.gravity * cz;
+      for (int a = 0; a < 3; ++a) { P[a] += f[3 + a]; Lm[a] += f[a]; }
+    }
+    /* angular momentum about the world origin: L_O = L_P + P_root x p */
+    real rp[3];
+    v3_cross(ph->root_pos, P, rp);
+    out[(size_t)e * 7] = (float)E;
+    for (int a = 0; a < 3; ++a) { out[(size_t)e * 7 + 1 + a] = (float)P[a]; out[(size_t)e * 7 + 4 + a] = (float)(Lm[a] + rp[a]); }
+  }
+  return 0;
+}
