@@ -43,6 +43,7 @@ extern "C" {
 #define ZB_NUM_REWARD_TERMS 13
 #define ZB_HIST 5             /* contact sensor history_length (v2.py:32) */
 #define ZB_MAX_SELF_PAIRS 64
+#define ZB_MAX_CONTACTS 12    /* contact slots per env per substep (deepest kept) */
 
 /* Persistent per-env state, SoA [ZB_STATE_DIM][num_envs] float32. */
 enum zb_state_field {
@@ -162,6 +163,12 @@ int zb_set_state(zb_handle h, const float* src, void* stream);
  * and applied_torque (if != NULL) Isaac Lab's clipped PD estimate float[N][6]. */
 int zb_physics_substeps(zb_handle h, const float* targets, int nsub, float* net_force,
                         float* applied_torque, void* stream);
+
+/* Measurement: time the next `max_launches` zb_step_kernel launches with hipEvents recorded on
+ * the launch stream right around the kernel (bench.py's roofline figure). zb_profile_end waits
+ * for the last event and returns the summed kernel time. */
+int zb_profile_begin(zb_handle h, int max_launches);
+int zb_profile_end(zb_handle h, float* total_ms, int* count);
 
 #ifdef __cplusplus
 }

@@ -45,7 +45,7 @@ typedef ZBO_REAL real;
 #define ND ZB_NUM_DOF
 #define NL ZB_NUM_LINKS
 #define NV (6 + ND)  /* generalized velocity: [omega(3), v_P(3), qdot(6)] */
-#define NC_MAX 16    /* contact slots per env per substep (= ZB kernel) */
+#define NC_MAX ZB_MAX_CONTACTS /* contact slots per env per substep (= the HIP kernel) */
 #define NCAND_PER_LINK 4
 #define TWO_PI 6.283185307179586
 #define PI_R 3.14159265358979323846
@@ -156,7 +156,7 @@ struct zbo_sim {
   mdl_t m;
   zb_task_cfg c;
   int n;
-  uint64_t seed, reset_counter;
+  uint64_t seed, call_counter; /* zb_step / zb_reset calls so far (RNG stream position) */
   env_t* env;
   float log_means[ZB_NUM_REWARD_TERMS];
   int32_t log_counts[2];
@@ -975,9 +975,9 @@ int zbo_reset(zbo_sim* s, const int32_t* env_ids, int n) {
   const float ep_s = s->c.sim_dt * s->c.decimation * s->c.max_episode_length;
   for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) s->log_means[t] = cnt ? s->log_means[t] / cnt / ep_s : 0;
   s->log_counts[0] = s->log_counts[1] = 0;
+  uint64_t ctr = s->call_counter++;
   if (all) {
     /* v2.py:418-422 episode_length_buf ~ U{0..max_episode_length-1} */
-    uint64_t ctr = s->reset_counter++;
     for (int e = 0; e < s->n; ++e) {
       uint64_t h = zb_hash64(s->seed ^ zb_hash64(ctr * 0x100000001B3ull + (uint64_t)e));
       s->env[e].md.ep_len = (int32_t)(h % (uint64_t)s->c.max_episode_length);
@@ -1079,9 +1079,9 @@ int zbo_step(zbo_sim* s, const float* actions, float* obs, float* reward, uint8_
     s->log_counts[0] = nterm;
     s->log_counts[1] = ntout;
   }
+  uint64_t ctr = s->call_counter++;
   if (nreset == s->n) {
     /* every env reset in this step: _reset_idx saw len(env_ids) == num_envs (v2.py:418-422) */
-    uint64_t ctr = s->reset_counter++;
     for (int e = 0; e < s->n; ++e) {
       uint64_t h = zb_hash64(s->seed ^ zb_hash64(ctr * 0x100000001B3ull + (uint64_t)e));
       s->env[e].md.ep_len = (int32_t)(h % (uint64_t)s->c.max_episode_length);

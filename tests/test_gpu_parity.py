@@ -1,0 +1,194 @@
+"""HIP kernel (libzbot.so, through the C ABI) vs the CPU oracle on identical seeded states.
+
+Bar: fp32 on both sides, different operation order / FMA contraction / libm, so
+  * one substep from identical states: joint/root velocities within 2e-3 abs + 1e-3 rel,
+    positions within 1e-5 (they move by dt * velocity);
+  * one policy step (4 substeps + MDP): observations / rewards within the tolerances below for
+    >= 99 % of envs, done flags identical for >= 99 % (contact activation at the speculative
+    margin is a discontinuity: a 1-ulp difference can flip one contact); integer / counter state
+    (episode length, reset draws) bit-exact;
+  * 300 random-action steps: trajectories diverge (chaotic contact), so episode statistics are
+    compared: mean reward and termination rate within statistical tolerance.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from helpers import S, perturbed_states
+from zbot_lab_amd import model as zm
+
+pytestmark = pytest.mark.gpu
+
+
+def _pair(n, cfg=None, seed=0):
+    import torch
+    from oracle.pyoracle import OracleSim
+    from zbot_lab_amd.sim import ZbotSim
+    cfg = cfg or zm.TaskCfg()
+    g = ZbotSim(n, cfg, device="cuda:0", seed=seed)
+    o = OracleSim(n, cfg, seed=seed)
+    return g, o, torch
+
+
+def _set_both(g, o, st):
+    import torch
+    g.set_state(torch.from_numpy(st).cuda())
+    o.set_state(st)
+
+
+def test_library_loads_native(gpu):
+    from zbot_lab_amd import _native as nat
+    L = nat.lib()
+    for name in nat.EXPORTED:
+        assert hasattr(L, name)
+
+
+def test_default_pose_observation(gpu):
+    g, o, torch = _pair(64)
+    og = g.observe().cpu().numpy()
+    oo = o.observe()
+    np.testing.assert_allclose(og, oo, atol=2e-6)
+    # FK known answer of the reference (v2.py:404): base quat at the default pose
+    np.testing.assert_allclose(og[0, :4], [0.6003, -0.6003, -0.3735, -0.3739], atol=1e-4)
+
+
+def test_state_roundtrip(gpu):
+    g, o, torch = _pair(128)
+    st = perturbed_states(128, seed=3)
+    g.set_state(torch.from_numpy(st).cuda())
+    back = g.get_state().cpu().numpy()
+    np.testing.assert_array_equal(back, st)
+
+
+@pytest.mark.parametrize("airborne", [0.0, 0.5])
+def test_one_substep_parity(gpu, airborne):
+    n = 512
+    g, o, torch = _pair(n)
+    st = perturbed_states(n, seed=11, airborne=airborne)
+    _set_both(g, o, st)
+    rng = np.random.default_rng(5)
+    tg = (st[S["JOINT_POS"]:S["JOINT_POS"] + 6].T + rng.normal(0, 0.2, (n, 6))).astype(np.float32)
+    nf_g, tau_g = g.physics_substeps(torch.from_numpy(tg).cuda(), 1)
+    nf_o, tau_o = o.physics_substeps(tg, 1)
+    sg = g.get_state().cpu().numpy()
+    so = o.get_state()
+    np.testing.assert_allclose(tau_g.cpu().numpy(), tau_o, rtol=1e-5, atol=1e-4)
+    vel = slice(S["ROOT_LINVEL"], S["JOINT_VEL"] + 6)
+    dv = np.abs(sg[vel] - so[vel]) - (2e-3 + 1e-3 * np.abs(so[vel]))
+    ok = (dv <= 0).all(axis=0)
+    assert ok.mean() >= 0.99, f"velocity parity in {ok.mean():.4f} of envs; worst {dv.max():.3e}"
+    pos = slice(S["ROOT_POS"], S["JOINT_POS"] + 6)
+    dp = np.abs(sg[pos] - so[pos])
+    okp = (dp <= 1e-5 + 1e-5 * np.abs(so[pos])).all(axis=0)
+    assert okp.mean() >= 0.99, f"position parity in {okp.mean():.4f} of envs; worst {dp.max():.3e}"
+    # contact forces: same support (which links touch), magnitudes close
+    fg = nf_g.cpu().numpy()
+    okf = (np.abs(fg - nf_o) <= 0.05 + 0.02 * np.abs(nf_o)).all(axis=(1, 2))
+    assert okf.mean() >= 0.98, f"contact-force parity in {okf.mean():.4f} of envs"
+
+
+def test_four_substeps_parity(gpu):
+    n = 512
+    g, o, torch = _pair(n)
+    st = perturbed_states(n, seed=21)
+    _set_both(g, o, st)
+    tg = st[S["JOINT_POS"]:S["JOINT_POS"] + 6].T.copy()
+    g.physics_substeps(torch.from_numpy(tg).cuda(), 4)
+    o.physics_substeps(tg, 4)
+    sg = g.get_state().cpu().numpy()
+    so = o.get_state()
+    sl = slice(S["ROOT_POS"], S["JOINT_VEL"] + 6)
+    d = np.abs(sg[sl] - so[sl]) <= 5e-3 + 5e-3 * np.abs(so[sl])
+    assert d.all(axis=0).mean() >= 0.98
+
+
+def test_one_step_parity(gpu):
+    n = 1024
+    g, o, torch = _pair(n)
+    st = perturbed_states(n, seed=31, jq_sigma=0.15, jqd_sigma=0.5)
+    _set_both(g, o, st)
+    rng = np.random.default_rng(7)
+    a = rng.normal(size=(n, 6)).astype(np.float32)
+    obs_g, rew_g, te_g, tr_g = g.step(torch.from_numpy(a).cuda())
+    obs_o, rew_o, te_o, tr_o = o.step(a)
+    obs_g = obs_g.cpu().numpy()
+    rew_g = rew_g.cpu().numpy()
+    te_g = te_g.cpu().numpy()
+    tr_g = tr_g.cpu().numpy()
+    assert (tr_g == tr_o).all()                         # time-outs are pure integer logic
+    assert (te_g == te_o).mean() >= 0.99
+    same = te_g == te_o
+    ok_obs = (np.abs(obs_g - obs_o) <= 5e-3 + 5e-3 * np.abs(obs_o)).all(axis=1)
+    assert ok_obs[same].mean() >= 0.99
+    ok_rew = np.abs(rew_g - rew_o) <= 2e-3 + 2e-3 * np.abs(rew_o)
+    assert ok_rew[same].mean() >= 0.99
+    sg = g.get_state().cpu().numpy()
+    so = o.get_state()
+    np.testing.assert_array_equal(sg[S["EP_LEN"]][same], so[S["EP_LEN"]][same])
+
+
+def test_reset_parity_bit_exact(gpu):
+    n = 2048
+    g, o, torch = _pair(n, seed=1234)
+    st = perturbed_states(n, seed=41)
+    _set_both(g, o, st)
+    ids = np.arange(0, n, 3, dtype=np.int32)
+    g.reset(torch.from_numpy(ids).cuda())
+    o.reset(ids)
+    np.testing.assert_allclose(g.get_state().cpu().numpy(), o.get_state(), atol=1e-6)
+    # full reset: episode_length_buf ~ U{0..999} from the shared counter-based hash
+    g.reset(None)
+    o.reset(None)
+    eg = g.get_state().cpu().numpy()[S["EP_LEN"]]
+    eo = o.get_state()[S["EP_LEN"]]
+    np.testing.assert_array_equal(eg, eo)
+    assert eg.min() >= 0 and eg.max() <= 999 and len(np.unique(eg)) > 800
+    lg, cg = g.read_log()
+    lo, co = o.read_log()
+    np.testing.assert_allclose(lg.cpu().numpy(), lo, rtol=1e-4, atol=1e-6)
+
+
+def test_timeout_and_log(gpu):
+    n = 256
+    g, o, torch = _pair(n)
+    st = zm.default_state(n)
+    st[S["EP_LEN"]] = 997.0  # -> 998 after this step (no timeout), 999 after the next (timeout)
+    _set_both(g, o, st)
+    a = np.zeros((n, 6), np.float32)
+    for k in range(2):
+        _, _, te_g, tr_g = g.step(torch.from_numpy(a).cuda())
+        _, _, te_o, tr_o = o.step(a)
+        assert (tr_g.cpu().numpy() == tr_o).all()
+    assert tr_o.all()
+    eg = g.get_state().cpu().numpy()[S["EP_LEN"]]
+    eo = o.get_state()[S["EP_LEN"]]
+    np.testing.assert_array_equal(eg, eo)  # all envs reset together -> full-reset draw
+    lg, cg = g.read_log()
+    lo, co = o.read_log()
+    np.testing.assert_array_equal(cg.cpu().numpy(), co)
+    np.testing.assert_allclose(lg.cpu().numpy(), lo, rtol=2e-3, atol=1e-5)
+
+
+def test_rollout_statistics(gpu):
+    """Chaotic contact makes per-env trajectories diverge; compare episode statistics."""
+    n, steps = 1024, 300
+    g, o, torch = _pair(n, seed=7)
+    g.reset(None)
+    o.reset(None)
+    rng = np.random.default_rng(42)
+    rg, ro, dg, do = [], [], [], []
+    for _ in range(steps):
+        a = rng.normal(size=(n, 6)).astype(np.float32)
+        _, r1, t1, _ = g.step(torch.from_numpy(a).cuda())
+        _, r2, t2, _ = o.step(a)
+        rg.append(r1.mean().item())
+        ro.append(r2.mean())
+        dg.append(t1.float().mean().item())
+        do.append(t2.mean())
+    rg, ro, dg, do = map(np.asarray, (rg, ro, dg, do))
+    # first steps start from identical states: tight
+    np.testing.assert_allclose(rg[:3], ro[:3], rtol=0.02, atol=0.002)
+    # whole rollout: statistics
+    assert abs(rg.mean() - ro.mean()) <= 0.1 * abs(ro.mean()) + 0.01, (rg.mean(), ro.mean())
+    assert abs(dg.mean() - do.mean()) <= 0.25 * do.mean() + 0.002, (dg.mean(), do.mean())

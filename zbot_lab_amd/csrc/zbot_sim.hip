@@ -1,0 +1,1511 @@
+// zbot_sim.hip — MI355X (gfx950) batched ZBOT-6 simulator: one fused kernel per policy step.
+//
+// Replaces, for zbot-6b-walking-v2, the reference's DirectRLEnv.step:
+//   _pre_physics_step (v2.py:276-287) -> 4 x [ImplicitActuator + PhysX articulation/contact
+//   substep] -> ContactSensor update -> _get_dones (v2.py:384-411) -> _get_rewards
+//   (v2.py:371-382, terms 461-561) -> _reset_idx (v2.py:413-459) -> _get_observations
+//   (v2.py:312-369)      [v2.py = source/zbot/zbot/tasks/zbot6b_direct/zbot_direct_6dof_bipedal_env_v2.py]
+//
+// Mapping: one env per lane, 64-lane workgroups (one wave). Persistent state is
+// SoA [field][env] in HBM, so every field load/store is one coalesced 256-B wave access; it is
+// read once and written once per step. Model constants are wave-uniform (scalar loads). The
+// 12-DoF dynamics (FK, RNEA, CRBA, 12x12 Cholesky, triangular solves) live in VGPRs, fully
+// unrolled over the fixed ZBOT-6 topology. The variable-length contact system (up to
+// ZB_MAX_CONTACTS rows x 3 directions x 12 whitened coordinates) is staged in LDS, lane-strided
+// ([slot][field][lane]) so every ds_read/ds_write is bank-conflict free. No MFMA: the largest
+// dense contraction is 12x12 per env.
+//
+// The algorithm is the one restated on the CPU in oracle/zbot_oracle.c (the parity oracle);
+// the two are written independently and compared by tests/test_gpu_parity.py.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "zbot.h"
+
+namespace {
+
+constexpr int NB = ZB_NUM_BODIES;
+constexpr int ND = ZB_NUM_DOF;
+constexpr int NL = ZB_NUM_LINKS;
+constexpr int NV = 6 + ND;
+constexpr int NCM = ZB_MAX_CONTACTS;
+constexpr int WAVE = 64;
+constexpr float PI_F = 3.14159265358979323846f;
+constexpr float TWO_PI_F = 6.28318530717958647692f;
+
+// LDS contact slot layout (floats), [slot][field][lane]
+constexpr int SLOT = 48;
+constexpr int SL_Y = 0;      // 3 rows x 12 whitened coords
+constexpr int SL_INVM = 36;  // 3
+constexpr int SL_VMIN = 39;  // 1 (holds sep during detection)
+constexpr int SL_LAM = 40;   // 3
+constexpr int SL_N = 43;     // 3 normal
+constexpr int SL_LA = 46;    // link a (float)
+constexpr int SL_LB = 47;    // link b (float, -1 ground)
+constexpr int LDS_FLOATS = NCM * SLOT * WAVE;
+
+// The ZBOT-6 chain topology is compiled in (zb_create checks the model against it):
+// link l belongs to composite body (l+1)/2; joint j connects body j -> j+1.
+__host__ __device__ constexpr int link_body(int l) { return (l + 1) >> 1; }
+
+// Model pointer in the constant address space (4): wave-uniform loads through it are scalar
+// (s_load) and land in SGPRs, never in per-lane VGPRs.
+using MP = const __attribute__((address_space(4))) zb_model*;
+using CF = const __attribute__((address_space(4))) float;
+template <int N>
+__device__ __forceinline__ void ldc(float (&d)[N], CF* s) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) d[i] = s[i];
+}
+__device__ __forceinline__ MP to_mp(const zb_model* m) { return (MP)(uintptr_t)m; }
+
+struct Lane {
+  float* p;  // lds + lane
+  __device__ __forceinline__ float& at(int slot, int f) const { return p[(slot * SLOT + f) * WAVE]; }
+};
+
+// ------------------------------------------------------------------------- math
+__device__ __forceinline__ void cross3(const float a[3], const float b[3], float o[3]) {
+  float x = a[1] * b[2] - a[2] * b[1], y = a[2] * b[0] - a[0] * b[2], z = a[0] * b[1] - a[1] * b[0];
+  o[0] = x; o[1] = y; o[2] = z;
+}
+__device__ __forceinline__ float dot3(const float a[3], const float b[3]) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+__device__ __forceinline__ void qmul(const float a[4], const float b[4], float o[4]) {
+  float w = a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3];
+  float x = a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2];
+  float y = a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1];
+  float z = a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0];
+  o[0] = w; o[1] = x; o[2] = y; o[3] = z;
+}
+__device__ __forceinline__ void qmat(const float q[4], float R[9]) {
+  float w = q[0], x = q[1], y = q[2], z = q[3];
+  R[0] = 1.f - 2.f * (y * y + z * z); R[1] = 2.f * (x * y - w * z); R[2] = 2.f * (x * z + w * y);
+  R[3] = 2.f * (x * y + w * z); R[4] = 1.f - 2.f * (x * x + z * z); R[5] = 2.f * (y * z - w * x);
+  R[6] = 2.f * (x * z - w * y); R[7] = 2.f * (y * z + w * x); R[8] = 1.f - 2.f * (x * x + y * y);
+}
+__device__ __forceinline__ void mv3(const float R[9], const float v[3], float o[3]) {
+  float x = R[0] * v[0] + R[1] * v[1] + R[2] * v[2];
+  float y = R[3] * v[0] + R[4] * v[1] + R[5] * v[2];
+  float z = R[6] * v[0] + R[7] * v[1] + R[8] * v[2];
+  o[0] = x; o[1] = y; o[2] = z;
+}
+__device__ __forceinline__ void qnormalize(float q[4]) {
+  float r = 1.f / sqrtf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  q[0] *= r; q[1] *= r; q[2] *= r; q[3] *= r;
+}
+__device__ __forceinline__ float clampf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
+
+__host__ __device__ __forceinline__ uint64_t hash64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+// ------------------------------------------------------------------------- state in registers
+struct Phys {
+  float pos[3], quat[4], lv[3], av[3], jq[ND], jqd[ND];
+};
+
+struct Kin {
+  float q[NB][4], R[NB][9], p[NB][3];  // p relative to P = root origin
+  float ax[ND][3], org[ND][3];
+};
+
+__device__ __forceinline__ void fk(MP m, const Phys& s, Kin& k) {
+  k.q[0][0] = s.quat[0]; k.q[0][1] = s.quat[1]; k.q[0][2] = s.quat[2]; k.q[0][3] = s.quat[3];
+  qnormalize(k.q[0]);
+  qmat(k.q[0], k.R[0]);
+  k.p[0][0] = k.p[0][1] = k.p[0][2] = 0.f;
+#pragma unroll
+  for (int j = 0; j < ND; ++j) {
+    float qj[4], Rj[9], t[3];
+    float jpr[4], jpp[3], jcp[3], jcr[4];
+    ldc(jpr, m->joint_parent_rot[j]);
+    ldc(jpp, m->joint_parent_pos[j]);
+    ldc(jcp, m->joint_child_pos[j]);
+    ldc(jcr, m->joint_child_rot[j]);
+    qmul(k.q[j], jpr, qj);
+    qmat(qj, Rj);
+    mv3(k.R[j], jpp, t);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) { k.org[j][a] = k.p[j][a] + t[a]; k.ax[j][a] = Rj[3 * a + 2]; }
+    float sn, cs;
+    sincosf(0.5f * s.jq[j], &sn, &cs);
+    const float qz[4] = {cs, 0.f, 0.f, sn};
+    float qa[4], Ra[9];
+    qmul(qj, qz, qa);
+    qmat(qa, Ra);
+    mv3(Ra, jcp, t);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) k.p[j + 1][a] = k.org[j][a] + t[a];
+    qmul(qa, jcr, k.q[j + 1]);
+    qnormalize(k.q[j + 1]);
+    qmat(k.q[j + 1], k.R[j + 1]);
+  }
+}
+
+// spatial velocities V = [omega; v_P] of all bodies
+__device__ __forceinline__ void body_vel(const Kin& k, const Phys& s, float V[NB][6]) {
+#pragma unroll
+  for (int a = 0; a < 3; ++a) { V[0][a] = s.av[a]; V[0][3 + a] = s.lv[a]; }
+#pragma unroll
+  for (int j = 0; j < ND; ++j) {
+    float oxa[3];
+    cross3(k.org[j], k.ax[j], oxa);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      V[j + 1][a] = V[j][a] + k.ax[j][a] * s.jqd[j];
+      V[j + 1][3 + a] = V[j][3 + a] + oxa[a] * s.jqd[j];
+    }
+  }
+}
+
+// ------------------------------------------------------------------------- spatial inertia
+struct SI { float m, h[3], I[6]; };  // about P, I = xx yy zz xy xz yz
+
+__device__ __forceinline__ void si_mul(const SI& I, const float V[6], float f[6]) {
+  const float* w = V;
+  const float* v = V + 3;
+  float Iw0 = I.I[0] * w[0] + I.I[3] * w[1] + I.I[4] * w[2];
+  float Iw1 = I.I[3] * w[0] + I.I[1] * w[1] + I.I[5] * w[2];
+  float Iw2 = I.I[4] * w[0] + I.I[5] * w[1] + I.I[2] * w[2];
+  float hv[3], hw[3];
+  cross3(I.h, v, hv);
+  cross3(I.h, w, hw);
+  f[0] = Iw0 + hv[0]; f[1] = Iw1 + hv[1]; f[2] = Iw2 + hv[2];
+  f[3] = I.m * v[0] - hw[0]; f[4] = I.m * v[1] - hw[1]; f[5] = I.m * v[2] - hw[2];
+}
+
+__device__ __forceinline__ void body_si(MP m, const Kin& k, int b, SI& o) {
+  const float* R = k.R[b];
+  float c[3];
+  float bcom[3], L[6];
+  ldc(bcom, m->body_com[b]);
+  ldc(L, m->body_inertia[b]);
+  mv3(R, bcom, c);
+  c[0] += k.p[b][0]; c[1] += k.p[b][1]; c[2] += k.p[b][2];
+  const float Il[9] = {L[0], L[3], L[4], L[3], L[1], L[5], L[4], L[5], L[2]};
+  float T[9], W[9];
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int q = 0; q < 3; ++q) T[3 * r + q] = R[3 * r] * Il[q] + R[3 * r + 1] * Il[3 + q] + R[3 * r + 2] * Il[6 + q];
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int q = 0; q < 3; ++q) W[3 * r + q] = T[3 * r] * R[3 * q] + T[3 * r + 1] * R[3 * q + 1] + T[3 * r + 2] * R[3 * q + 2];
+  const float mm = m->body_mass[b];
+  const float cc = dot3(c, c);
+  o.m = mm;
+  o.h[0] = mm * c[0]; o.h[1] = mm * c[1]; o.h[2] = mm * c[2];
+  o.I[0] = W[0] + mm * (cc - c[0] * c[0]);
+  o.I[1] = W[4] + mm * (cc - c[1] * c[1]);
+  o.I[2] = W[8] + mm * (cc - c[2] * c[2]);
+  o.I[3] = W[1] - mm * c[0] * c[1];
+  o.I[4] = W[2] - mm * c[0] * c[2];
+  o.I[5] = W[5] - mm * c[1] * c[2];
+}
+
+// ------------------------------------------------------------------------- packed lower-triangular 12x12
+constexpr int tri(int r, int c) { return r * (r + 1) / 2 + c; }  // r >= c
+constexpr int NT = NV * (NV + 1) / 2;
+
+// in place: A (lower triangle) -> L with L L^T = A
+__device__ __forceinline__ void cholesky_inplace(float A[NT]) {
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    float s = A[tri(j, j)];
+#pragma unroll
+    for (int k = 0; k < j; ++k) s -= A[tri(j, k)] * A[tri(j, k)];
+    const float d = sqrtf(fmaxf(s, 1e-12f));
+    A[tri(j, j)] = d;
+    const float inv = 1.f / d;
+#pragma unroll
+    for (int i = j + 1; i < NV; ++i) {
+      float t = A[tri(i, j)];
+#pragma unroll
+      for (int k = 0; k < j; ++k) t -= A[tri(i, k)] * A[tri(j, k)];
+      A[tri(i, j)] = t * inv;
+    }
+  }
+}
+// rank-1 downdate L L^T - a e_J e_J^T (removes the drive armature of a saturated joint);
+// mathematically identical to re-factoring, as the oracle does.
+template <int J>
+__device__ __forceinline__ void chol_downdate(float L[NT], float a) {
+  float x[NV];
+#pragma unroll
+  for (int i = J; i < NV; ++i) x[i] = 0.f;
+  x[J] = sqrtf(a);
+#pragma unroll
+  for (int k = J; k < NV; ++k) {
+    const float lkk = L[tri(k, k)];
+    const float r = sqrtf(fmaxf(lkk * lkk - x[k] * x[k], 1e-12f));
+    const float c = r / lkk, sn = x[k] / lkk;
+    L[tri(k, k)] = r;
+    const float ic = 1.f / c;
+#pragma unroll
+    for (int i = k + 1; i < NV; ++i) {
+      const float lik = (L[tri(i, k)] - sn * x[i]) * ic;
+      x[i] = c * x[i] - sn * lik;
+      L[tri(i, k)] = lik;
+    }
+  }
+}
+__device__ __forceinline__ void fwd_sub(const float L[NT], const float b[NV], float y[NV]) {
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    float t = b[i];
+#pragma unroll
+    for (int k = 0; k < i; ++k) t -= L[tri(i, k)] * y[k];
+    y[i] = t / L[tri(i, i)];
+  }
+}
+__device__ __forceinline__ void bwd_sub(const float L[NT], const float y[NV], float x[NV]) {
+#pragma unroll
+  for (int i = NV - 1; i >= 0; --i) {
+    float t = y[i];
+#pragma unroll
+    for (int k = i + 1; k < NV; ++k) t -= L[tri(k, i)] * x[k];
+    x[i] = t / L[tri(i, i)];
+  }
+}
+__device__ __forceinline__ void lt_mul(const float L[NT], const float u[NV], float w[NV]) {
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = i; k < NV; ++k) t += L[tri(k, i)] * u[k];
+    w[i] = t;
+  }
+}
+
+// Model constants are wave-uniform and re-loaded (scalar loads) where used; routing the pointer
+// through an empty asm keeps the compiler from hoisting hundreds of them out of the substep loop
+// into long-lived registers.
+__device__ __forceinline__ MP opaque(MP m) {
+  uint64_t v = (uint64_t)m;
+  asm volatile("" : "+s"(v));
+  return (MP)v;
+}
+
+// ------------------------------------------------------------------------- contacts
+__device__ __forceinline__ void contact_add(const Lane& ld, int& nc, const float x[3], const float n[3], float sep,
+                                            int la, int lb) {
+  int slot;
+  if (nc < NCM) {
+    slot = nc++;
+  } else {
+    int worst = 0;
+    float wsep = ld.at(0, SL_VMIN);
+    for (int c = 1; c < NCM; ++c) {
+      const float s = ld.at(c, SL_VMIN);
+      if (s > wsep) { wsep = s; worst = c; }
+    }
+    if (!(sep < wsep)) return;
+    slot = worst;
+  }
+  ld.at(slot, SL_Y + 0) = x[0];
+  ld.at(slot, SL_Y + 1) = x[1];
+  ld.at(slot, SL_Y + 2) = x[2];
+  ld.at(slot, SL_N + 0) = n[0];
+  ld.at(slot, SL_N + 1) = n[1];
+  ld.at(slot, SL_N + 2) = n[2];
+  ld.at(slot, SL_VMIN) = sep;
+  ld.at(slot, SL_LA) = (float)la;
+  ld.at(slot, SL_LB) = (float)lb;
+}
+
+// Staging area for world sphere/bound centres during detection: fields 3..35 of the contact
+// slots' Y block, which detection never writes (contact x lives in fields 0..2).
+constexpr int STAGE_PER_SLOT = 33;
+__device__ __forceinline__ float& stage(const Lane& ld, int idx) {
+  return ld.at(idx / STAGE_PER_SLOT, 3 + idx % STAGE_PER_SLOT);
+}
+constexpr int STG_SPH = 0;    // [link][sphere][xyz] 72
+constexpr int STG_BND = 72;   // [link][xyz] 36
+
+// Ground: the 4 rim points of each of the link's two circles (lowest + 90-degree rotations),
+// the 4 deepest below the margin per link; then sphere pairs for self collision.
+__device__ __forceinline__ int detect(MP m, const zb_task_cfg& cfg, const Kin& k, float Pz,
+                                      const Lane& ld) {
+  int nc = 0;
+  const float margin = cfg.contact_margin;
+  const float up[3] = {0.f, 0.f, 1.f};
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
+    const int b = link_body(l);
+    const float* R = k.R[b];
+    float bc[3], lb4[4];
+    ldc(lb4, m->link_bound[l]);
+    mv3(R, lb4, bc);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) stage(ld, STG_BND + 3 * l + a) = bc[a] + k.p[b][a];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      float sc[3], sp[3];
+      ldc(sp, m->link_sphere[l][s2]);
+      mv3(R, sp, sc);
+#pragma unroll
+      for (int a = 0; a < 3; ++a) stage(ld, STG_SPH + 6 * l + 3 * s2 + a) = sc[a] + k.p[b][a];
+    }
+    if (Pz + k.p[b][2] + bc[2] - lb4[3] > margin) continue;
+    float cx[8][3], cs[8];
+#pragma unroll
+    for (int ci = 0; ci < 2; ++ci) {
+      float cd[9];
+      ldc(cd, m->link_circle[l][ci]);
+      float C[3], E1[3], E2[3];
+      mv3(R, cd, C);
+      mv3(R, cd + 3, E1);
+      mv3(R, cd + 6, E2);
+      C[0] += k.p[b][0]; C[1] += k.p[b][1]; C[2] += k.p[b][2];
+      const float al = -E1[2], be = -E2[2];
+      const float nrm = sqrtf(al * al + be * be);
+      float c0 = 1.f, s0 = 0.f;
+      if (nrm > 1e-9f) { c0 = al / nrm; s0 = be / nrm; }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float cr = r == 0 ? c0 : (r == 1 ? -s0 : (r == 2 ? -c0 : s0));
+        const float sr = r == 0 ? s0 : (r == 1 ? c0 : (r == 2 ? -s0 : -c0));
+        const int idx = ci * 4 + r;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) cx[idx][a] = C[a] + cr * E1[a] + sr * E2[a];
+        cs[idx] = Pz + cx[idx][2];
+      }
+    }
+    // stable selection of the 4 deepest valid candidates (ties: lowest index)
+    unsigned used = 0;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      int best = -1;
+      float bs = 0.f;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const bool ok = cs[t] < margin && !((used >> t) & 1u);
+        if (ok && (best < 0 || cs[t] < bs)) { best = t; bs = cs[t]; }
+      }
+      if (best < 0) break;
+      used |= 1u << best;
+      float x[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < 8; ++t)
+        if (t == best) { x[0] = cx[t][0]; x[1] = cx[t][1]; x[2] = cx[t][2]; }
+      contact_add(ld, nc, x, up, bs, l, -1);
+    }
+  }
+  if (!cfg.enable_self_collision) return nc;
+  for (int la = 0; la < NL; ++la) {
+    for (int lb = la + 2; lb < NL; ++lb) {  // consecutive links are joint-connected (filtered)
+      const float d0 = stage(ld, STG_BND + 3 * la) - stage(ld, STG_BND + 3 * lb);
+      const float d1 = stage(ld, STG_BND + 3 * la + 1) - stage(ld, STG_BND + 3 * lb + 1);
+      const float d2 = stage(ld, STG_BND + 3 * la + 2) - stage(ld, STG_BND + 3 * lb + 2);
+      const float rr = m->link_bound[la][3] + m->link_bound[lb][3] + margin;
+      if (d0 * d0 + d1 * d1 + d2 * d2 > rr * rr) continue;
+#pragma unroll
+      for (int sa = 0; sa < 2; ++sa) {
+        const float ra = m->link_sphere[la][sa][3];
+        const float xa[3] = {stage(ld, STG_SPH + 6 * la + 3 * sa), stage(ld, STG_SPH + 6 * la + 3 * sa + 1),
+                             stage(ld, STG_SPH + 6 * la + 3 * sa + 2)};
+#pragma unroll
+        for (int sb = 0; sb < 2; ++sb) {
+          const float rb = m->link_sphere[lb][sb][3];
+          const float xb[3] = {stage(ld, STG_SPH + 6 * lb + 3 * sb), stage(ld, STG_SPH + 6 * lb + 3 * sb + 1),
+                               stage(ld, STG_SPH + 6 * lb + 3 * sb + 2)};
+          const float dv[3] = {xa[0] - xb[0], xa[1] - xb[1], xa[2] - xb[2]};
+          const float dist = sqrtf(dot3(dv, dv));
+          const float sep = dist - (ra + rb);
+          if (sep < margin && dist > 1e-9f) {
+            float n[3], x[3];
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+              n[a] = dv[a] / dist;
+              x[a] = 0.5f * ((xa[a] - n[a] * ra) + (xb[a] + n[a] * rb));
+            }
+            contact_add(ld, nc, x, n, sep, la, lb);
+          }
+        }
+      }
+    }
+  }
+  return nc;
+}
+
+__device__ __forceinline__ void tangents(const float n[3], float t1[3], float t2[3]) {
+  if (fabsf(n[2]) < 0.9f) {
+    const float s = sqrtf(n[1] * n[1] + n[0] * n[0]);
+    t1[0] = -n[1] / s; t1[1] = n[0] / s; t1[2] = 0.f;
+  } else {
+    const float s = sqrtf(n[2] * n[2] + n[1] * n[1]);
+    t1[0] = 0.f; t1[1] = n[2] / s; t1[2] = -n[1] / s;
+  }
+  cross3(n, t1, t2);
+}
+
+// J row of direction d at point x on body b (predicated over the fixed chain, no dynamic indexing)
+__device__ __forceinline__ void jac_row(const float S[ND][6], const float org[ND][3], int b, const float x[3],
+                                        const float d[3], float J[NV]) {
+  float xd[3];
+  cross3(x, d, xd);
+  J[0] = xd[0]; J[1] = xd[1]; J[2] = xd[2];
+  J[3] = d[0]; J[4] = d[1]; J[5] = d[2];
+#pragma unroll
+  for (int j = 0; j < ND; ++j) {
+    const float xo[3] = {x[0] - org[j][0], x[1] - org[j][1], x[2] - org[j][2]};
+    float c[3];
+    cross3(xo, d, c);
+    J[6 + j] = (j < b) ? (S[j][0] * c[0] + S[j][1] * c[1] + S[j][2] * c[2]) : 0.f;
+  }
+}
+
+// What the MDP needs from the last substep (instead of 12 per-link force vectors).
+struct SensorOut {
+  float feet_f[2][3];   // net contact force on foot_0 / foot_1
+  float undes_fmax;     // max over the 10 undesired links of |net force|
+  float tau2;           // sum of squared Isaac Lab applied torques (torques reward)
+};
+
+// ------------------------------------------------------------------------- one substep
+template <bool kDebugForces>
+__device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
+                                        const float target[ND], const Lane& ld, bool last, SensorOut& so,
+                                        float (*dbgF)[3], float* dbgTau) {
+  const float dt = cfg.sim_dt;
+  MP m = opaque(m0);
+
+  if (last) {
+    float t2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+      const float t = clampf(m->kp * (target[j] - s.jq[j]) - m->kd * s.jqd[j], -m->effort_limit, m->effort_limit);
+      t2 += t * t;
+      if (kDebugForces) dbgTau[j] = t;
+    }
+    so.tau2 = t2;
+  }
+
+  float S[ND][6], org[ND][3];
+  SI I[NB];
+  int nc;
+  {
+    Kin k;
+    fk(m, s, k);
+    nc = detect(opaque(m0), cfg, k, s.pos[2], ld);
+    m = opaque(m0);
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+      float oxa[3];
+      cross3(k.org[j], k.ax[j], oxa);
+#pragma unroll
+      for (int a = 0; a < 3; ++a) { S[j][a] = k.ax[j][a]; S[j][3 + a] = oxa[a]; org[j][a] = k.org[j][a]; }
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b) body_si(m, k, b, I[b]);
+  }
+
+  // RNEA bias forces (qddot = 0, gravity as base acceleration); f_b formed in the forward pass
+  float Cb[NV];
+  {
+    float f[NB][6];
+    float V[6], A[6];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) { V[a] = s.av[a]; V[3 + a] = s.lv[a]; A[a] = 0.f; A[3 + a] = 0.f; }
+    A[5] = cfg.gravity;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      if (b > 0) {
+        const int j = b - 1;
+#pragma unroll
+        for (int a = 0; a < 6; ++a) V[a] += S[j][a] * s.jqd[j];
+        float t1[3], t2[3], t3[3];
+        cross3(V, S[j], t1);
+        cross3(V, S[j] + 3, t2);
+        cross3(V + 3, S[j], t3);
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+          A[a] += t1[a] * s.jqd[j];
+          A[3 + a] += (t2[a] + t3[a]) * s.jqd[j];
+        }
+      }
+      float IA[6], IV[6], t1[3], t2[3], t3[3];
+      si_mul(I[b], A, IA);
+      si_mul(I[b], V, IV);
+      cross3(V, IV, t1);
+      cross3(V + 3, IV + 3, t2);
+      cross3(V, IV + 3, t3);
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        f[b][a] = IA[a] + t1[a] + t2[a];
+        f[b][3 + a] = IA[3 + a] + t3[a];
+      }
+    }
+#pragma unroll
+    for (int b = NB - 2; b >= 0; --b)
+#pragma unroll
+      for (int a = 0; a < 6; ++a) f[b][a] += f[b + 1][a];
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+      float t = 0.f;
+#pragma unroll
+      for (int a = 0; a < 6; ++a) t += S[j][a] * f[j + 1][a];
+      Cb[6 + j] = t;
+    }
+#pragma unroll
+    for (int a = 0; a < 6; ++a) Cb[a] = f[0][a];
+  }
+
+  // CRBA (composite inertias accumulated in place) straight into the factor storage
+  const float arm = dt * (m->kd + dt * m->kp);
+  float L[NT];
+#pragma unroll
+  for (int b = NB - 2; b >= 0; --b) {
+    I[b].m += I[b + 1].m;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) I[b].h[a] += I[b + 1].h[a];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) I[b].I[a] += I[b + 1].I[a];
+  }
+  {
+    const SI& T = I[0];
+    L[tri(0, 0)] = T.I[0]; L[tri(1, 1)] = T.I[1]; L[tri(2, 2)] = T.I[2];
+    L[tri(1, 0)] = T.I[3]; L[tri(2, 0)] = T.I[4]; L[tri(2, 1)] = T.I[5];
+    const float hx = T.h[0], hy = T.h[1], hz = T.h[2];
+    L[tri(3, 0)] = 0.f; L[tri(3, 1)] = hz;  L[tri(3, 2)] = -hy;
+    L[tri(4, 0)] = -hz; L[tri(4, 1)] = 0.f; L[tri(4, 2)] = hx;
+    L[tri(5, 0)] = hy;  L[tri(5, 1)] = -hx; L[tri(5, 2)] = 0.f;
+    L[tri(3, 3)] = T.m; L[tri(4, 4)] = T.m; L[tri(5, 5)] = T.m;
+    L[tri(4, 3)] = 0.f; L[tri(5, 3)] = 0.f; L[tri(5, 4)] = 0.f;
+  }
+#pragma unroll
+  for (int kk = 0; kk < ND; ++kk) {
+    float Fk[6];
+    si_mul(I[kk + 1], S[kk], Fk);
+#pragma unroll
+    for (int a = 0; a < 6; ++a) L[tri(6 + kk, a)] = Fk[a];
+#pragma unroll
+    for (int jj = 0; jj <= kk; ++jj) {
+      float t = 0.f;
+#pragma unroll
+      for (int a = 0; a < 6; ++a) t += S[jj][a] * Fk[a];
+      L[tri(6 + kk, 6 + jj)] = t + (jj == kk ? arm : 0.f);
+    }
+  }
+
+  // implicit PD drives. Pass 1: all implicit (armature on the diagonal). A joint whose implicit
+  // torque exceeds the effort limit gets an explicit +-limit torque and loses its armature
+  // (rank-1 downdate of the factor), then the free velocity is re-solved.
+  cholesky_inplace(L);
+  float u[NV], b[NV], w[NV];
+  u[0] = s.av[0]; u[1] = s.av[1]; u[2] = s.av[2];
+  u[3] = s.lv[0]; u[4] = s.lv[1]; u[5] = s.lv[2];
+#pragma unroll
+  for (int a = 0; a < 6; ++a) b[a] = -dt * Cb[a];
+  float rhs[ND];
+#pragma unroll
+  for (int j = 0; j < ND; ++j) {
+    u[6 + j] = s.jqd[j];
+    rhs[j] = m->kp * (target[j] - s.jq[j]) - (m->kd + dt * m->kp) * s.jqd[j];
+    b[6 + j] = dt * (rhs[j] - Cb[6 + j]);
+  }
+  {
+    float z[NV];
+    lt_mul(L, u, w);
+    fwd_sub(L, b, z);
+#pragma unroll
+    for (int a = 0; a < NV; ++a) w[a] += z[a];
+  }
+  {
+    float uf[NV];
+    bwd_sub(L, w, uf);
+    unsigned sat = 0;
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+      const float tau = rhs[j] - (arm / dt) * (uf[6 + j] - s.jqd[j]);
+      if (tau > m->effort_limit || tau < -m->effort_limit) {
+        sat |= 1u << j;
+        b[6 + j] = dt * ((tau > 0.f ? m->effort_limit : -m->effort_limit) - Cb[6 + j]);
+      }
+    }
+    if (sat) {
+      if (sat & 1u) chol_downdate<6>(L, arm);
+      if (sat & 2u) chol_downdate<7>(L, arm);
+      if (sat & 4u) chol_downdate<8>(L, arm);
+      if (sat & 8u) chol_downdate<9>(L, arm);
+      if (sat & 16u) chol_downdate<10>(L, arm);
+      if (sat & 32u) chol_downdate<11>(L, arm);
+      float z[NV];
+      lt_mul(L, u, w);
+      fwd_sub(L, b, z);
+#pragma unroll
+      for (int a = 0; a < NV; ++a) w[a] += z[a];
+    }
+  }
+
+  // contact rows: Y = L^-1 J^T (whitened), effective masses and bias velocities
+  for (int c = 0; c < nc; ++c) {
+    const float x[3] = {ld.at(c, SL_Y + 0), ld.at(c, SL_Y + 1), ld.at(c, SL_Y + 2)};
+    const float n[3] = {ld.at(c, SL_N + 0), ld.at(c, SL_N + 1), ld.at(c, SL_N + 2)};
+    const float sep = ld.at(c, SL_VMIN);
+    const int la = (int)ld.at(c, SL_LA), lb = (int)ld.at(c, SL_LB);
+    const int ba = link_body(la);
+    const int bb = lb >= 0 ? link_body(lb) : -1;
+    float t1[3], t2[3];
+    tangents(n, t1, t2);
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      float d[3];
+#pragma unroll
+      for (int a = 0; a < 3; ++a) d[a] = r == 0 ? n[a] : (r == 1 ? t1[a] : t2[a]);
+      float J[NV], Y[NV];
+      jac_row(S, org, ba, x, d, J);
+      if (bb >= 0) {
+        float Jb[NV];
+        jac_row(S, org, bb, x, d, Jb);
+#pragma unroll
+        for (int a = 0; a < NV; ++a) J[a] -= Jb[a];
+      }
+      fwd_sub(L, J, Y);
+      float yy = 0.f;
+#pragma unroll
+      for (int a = 0; a < NV; ++a) { ld.at(c, SL_Y + 12 * r + a) = Y[a]; yy += Y[a] * Y[a]; }
+      ld.at(c, SL_INVM + r) = 1.f / (yy + 1e-9f);
+      ld.at(c, SL_LAM + r) = 0.f;
+    }
+    float vmin;
+    if (sep >= 0.f) vmin = -sep / dt;
+    else vmin = fminf(cfg.baumgarte * (-sep) / dt, m->max_depenetration_velocity);
+    ld.at(c, SL_VMIN) = vmin;
+  }
+
+  // projected Gauss-Seidel on the whitened velocity (Coulomb disk friction)
+  const float mu = cfg.friction;
+  for (int it = 0; it < cfg.solver_iterations; ++it) {
+    for (int c = 0; c < nc; ++c) {
+      float vn = 0.f;
+#pragma unroll
+      for (int a = 0; a < NV; ++a) vn += ld.at(c, SL_Y + a) * w[a];
+      const float ln0 = ld.at(c, SL_LAM + 0);
+      const float ln = fmaxf(ln0 + (ld.at(c, SL_VMIN) - vn) * ld.at(c, SL_INVM + 0), 0.f);
+      const float dl = ln - ln0;
+      ld.at(c, SL_LAM + 0) = ln;
+#pragma unroll
+      for (int a = 0; a < NV; ++a) w[a] += ld.at(c, SL_Y + a) * dl;
+      float vt1 = 0.f, vt2 = 0.f;
+#pragma unroll
+      for (int a = 0; a < NV; ++a) { vt1 += ld.at(c, SL_Y + 12 + a) * w[a]; vt2 += ld.at(c, SL_Y + 24 + a) * w[a]; }
+      const float l1o = ld.at(c, SL_LAM + 1), l2o = ld.at(c, SL_LAM + 2);
+      float l1 = l1o - vt1 * ld.at(c, SL_INVM + 1);
+      float l2 = l2o - vt2 * ld.at(c, SL_INVM + 2);
+      const float lim = mu * ln;
+      const float mag2 = l1 * l1 + l2 * l2;
+      if (mag2 > lim * lim) {
+        const float sc = lim / sqrtf(mag2);
+        l1 *= sc; l2 *= sc;
+      }
+      const float d1 = l1 - l1o, d2 = l2 - l2o;
+      ld.at(c, SL_LAM + 1) = l1;
+      ld.at(c, SL_LAM + 2) = l2;
+#pragma unroll
+      for (int a = 0; a < NV; ++a) w[a] += ld.at(c, SL_Y + 12 + a) * d1 + ld.at(c, SL_Y + 24 + a) * d2;
+    }
+  }
+  float un[NV];
+  bwd_sub(L, w, un);
+
+  if (last) {
+    // ContactSensor inputs: net force on the feet, max |net force| over undesired links
+    float Fl[NL][3];
+#pragma unroll
+    for (int l = 0; l < NL; ++l) Fl[l][0] = Fl[l][1] = Fl[l][2] = 0.f;
+    for (int c = 0; c < nc; ++c) {
+      const float n[3] = {ld.at(c, SL_N + 0), ld.at(c, SL_N + 1), ld.at(c, SL_N + 2)};
+      float t1[3], t2[3];
+      tangents(n, t1, t2);
+      const float l0 = ld.at(c, SL_LAM + 0), l1 = ld.at(c, SL_LAM + 1), l2 = ld.at(c, SL_LAM + 2);
+      float f[3];
+#pragma unroll
+      for (int a = 0; a < 3; ++a) f[a] = (l0 * n[a] + l1 * t1[a] + l2 * t2[a]) / dt;
+      const int la = (int)ld.at(c, SL_LA), lb = (int)ld.at(c, SL_LB);
+#pragma unroll
+      for (int l = 0; l < NL; ++l) {
+        const float sa = (l == la ? 1.f : 0.f) - (l == lb ? 1.f : 0.f);
+        Fl[l][0] += sa * f[0]; Fl[l][1] += sa * f[1]; Fl[l][2] += sa * f[2];
+      }
+    }
+    float fmax = 0.f;
+#pragma unroll
+    for (int l = 1; l <= 10; ++l) fmax = fmaxf(fmax, sqrtf(dot3(Fl[l], Fl[l])));
+    so.undes_fmax = fmax;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) { so.feet_f[0][a] = Fl[0][a]; so.feet_f[1][a] = Fl[11][a]; }
+    if (kDebugForces)
+#pragma unroll
+      for (int l = 0; l < NL; ++l) { dbgF[l][0] = Fl[l][0]; dbgF[l][1] = Fl[l][1]; dbgF[l][2] = Fl[l][2]; }
+  }
+
+#pragma unroll
+  for (int j = 0; j < ND; ++j) un[6 + j] = clampf(un[6 + j], -m->velocity_limit, m->velocity_limit);
+
+  // semi-implicit Euler (root twist at P -> classical root-origin velocity adds omega x v dt)
+  float wv[3];
+  cross3(s.av, s.lv, wv);
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    s.av[a] = un[a];
+    s.lv[a] = un[3 + a] + dt * wv[a];
+    s.pos[a] += dt * s.lv[a];
+  }
+  {
+    const float th = sqrtf(s.av[0] * s.av[0] + s.av[1] * s.av[1] + s.av[2] * s.av[2]) * dt;
+    float dq[4];
+    if (th > 1e-12f) {
+      float sn, cs;
+      sincosf(0.5f * th, &sn, &cs);
+      const float sc = sn / th * dt;
+      dq[0] = cs; dq[1] = s.av[0] * sc; dq[2] = s.av[1] * sc; dq[3] = s.av[2] * sc;
+    } else {
+      dq[0] = 1.f; dq[1] = 0.5f * dt * s.av[0]; dq[2] = 0.5f * dt * s.av[1]; dq[3] = 0.5f * dt * s.av[2];
+    }
+    float qn[4];
+    qmul(dq, s.quat, qn);
+    qnormalize(qn);
+    s.quat[0] = qn[0]; s.quat[1] = qn[1]; s.quat[2] = qn[2]; s.quat[3] = qn[3];
+  }
+#pragma unroll
+  for (int j = 0; j < ND; ++j) {
+    s.jqd[j] = un[6 + j];
+    float q = s.jq[j] + dt * s.jqd[j];
+    if (q > TWO_PI_F) q -= 2.f * TWO_PI_F;
+    else if (q < -TWO_PI_F) q += 2.f * TWO_PI_F;
+    s.jq[j] = q;
+  }
+}
+
+// ------------------------------------------------------------------------- MDP helpers
+struct Cache {
+  float base_pos[3], base_quat[4], fwd[3], heading_err, vfwd;
+  float feet_pos[2][3], feet_z[2][3], feet_x[2][3];
+};
+
+__device__ __forceinline__ void link_pose(MP m, const Kin& k, int l, float pos[3],
+                                          float quat[4]) {
+  const int b = link_body(l);
+  float t[3];
+  float lp[3], lr[4];
+  ldc(lp, m->link_pos[l]);
+  ldc(lr, m->link_rot[l]);
+  mv3(k.R[b], lp, t);
+  pos[0] = k.p[b][0] + t[0]; pos[1] = k.p[b][1] + t[1]; pos[2] = k.p[b][2] + t[2];
+  qmul(k.q[b], lr, quat);
+}
+
+__device__ __forceinline__ void link_com_vel(MP m, const Kin& k, const float V[NB][6], int l,
+                                             float v[3]) {
+  const int b = link_body(l);
+  float c[3];
+  float lc[3];
+  ldc(lc, m->link_com[l]);
+  mv3(k.R[b], lc, c);
+  c[0] += k.p[b][0]; c[1] += k.p[b][1]; c[2] += k.p[b][2];
+  float wc[3];
+  cross3(V[b], c, wc);
+  v[0] = V[b][3] + wc[0]; v[1] = V[b][4] + wc[1]; v[2] = V[b][5] + wc[2];
+}
+
+// the _get_observations cache (v2.py:315-345) of a physics state
+__device__ __forceinline__ void make_cache(MP m, const Phys& s, Cache& o) {
+  Kin k;
+  fk(m, s, k);
+  float V[NB][6];
+  body_vel(k, s, V);
+  constexpr int BASE = 6, F0 = 0, F1 = 11;
+  float bq[4], fq[2][4], bv[3];
+  link_pose(m, k, BASE, o.base_pos, bq);
+  link_pose(m, k, F0, o.feet_pos[0], fq[0]);
+  link_pose(m, k, F1, o.feet_pos[1], fq[1]);
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    o.base_pos[a] += s.pos[a];
+    o.feet_pos[0][a] += s.pos[a];
+    o.feet_pos[1][a] += s.pos[a];
+  }
+#pragma unroll
+  for (int a = 0; a < 4; ++a) o.base_quat[a] = bq[a];
+  link_com_vel(m, k, V, BASE, bv);
+  float R[9];
+  qmat(bq, R);
+  const float sh[3] = {R[2], R[5], R[8]};              // quat_apply(base_quat, z)  v2.py:322
+  o.fwd[0] = sh[1];                                     // (0,0,-1) x sh              v2.py:323
+  o.fwd[1] = -sh[0];
+  o.fwd[2] = 0.f * sh[0];
+  o.heading_err = -o.fwd[1];                            // v2.py:324
+  o.vfwd = dot3(bv, o.fwd);                             // v2.py:326-327
+#pragma unroll
+  for (int f = 0; f < 2; ++f) {
+    qmat(fq[f], R);
+    const float sg = f == 0 ? 1.f : -1.f;               // axis_z_feet = (0,0,1),(0,0,-1) v2.py:341-343
+    o.feet_z[f][0] = sg * R[2]; o.feet_z[f][1] = sg * R[5]; o.feet_z[f][2] = sg * R[8];
+    o.feet_x[f][0] = R[0]; o.feet_x[f][1] = R[3]; o.feet_x[f][2] = R[6];  // axis_x_feet v2.py:338-340
+  }
+}
+
+struct Mdp {
+  float p_delta[ND], actions[ND];
+  float down_pos[2][3], step_len[2], f_last[2];
+  float heading_sum, yerr_sum;
+  float fz_hist[ZB_HIST][2], fmax_hist[ZB_HIST];
+  float air_cur[2], air_last[2], contact_cur[2];
+  float ep_len;
+  float sums[ZB_NUM_REWARD_TERMS];
+};
+
+__device__ __forceinline__ void load_state(const float* __restrict__ st, int N, int i, Phys& p, Mdp& d) {
+#define LD(f) st[(size_t)(f) * N + i]
+#pragma unroll
+  for (int a = 0; a < 3; ++a) { p.pos[a] = LD(ZB_S_ROOT_POS + a); p.lv[a] = LD(ZB_S_ROOT_LINVEL + a); p.av[a] = LD(ZB_S_ROOT_ANGVEL + a); }
+#pragma unroll
+  for (int a = 0; a < 4; ++a) p.quat[a] = LD(ZB_S_ROOT_QUAT + a);
+#pragma unroll
+  for (int j = 0; j < ND; ++j) {
+    p.jq[j] = LD(ZB_S_JOINT_POS + j); p.jqd[j] = LD(ZB_S_JOINT_VEL + j);
+    d.p_delta[j] = LD(ZB_S_P_DELTA + j); d.actions[j] = LD(ZB_S_ACTIONS + j);
+  }
+#pragma unroll
+  for (int f = 0; f < 2; ++f) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) d.down_pos[f][a] = LD(ZB_S_FEET_DOWN_POS + 3 * f + a);
+    d.step_len[f] = LD(ZB_S_FEET_STEP_LEN + f);
+    d.f_last[f] = LD(ZB_S_FEET_F_LAST + f);
+    d.air_cur[f] = LD(ZB_S_FEET_AIR_CUR + f);
+    d.air_last[f] = LD(ZB_S_FEET_AIR_LAST + f);
+    d.contact_cur[f] = LD(ZB_S_FEET_CONTACT_CUR + f);
+  }
+  d.heading_sum = LD(ZB_S_HEADING_SUM);
+  d.yerr_sum = LD(ZB_S_Y_ERR_SUM);
+#pragma unroll
+  for (int h = 0; h < ZB_HIST; ++h) {
+    d.fz_hist[h][0] = LD(ZB_S_FEET_FZ_HIST + 2 * h);
+    d.fz_hist[h][1] = LD(ZB_S_FEET_FZ_HIST + 2 * h + 1);
+    d.fmax_hist[h] = LD(ZB_S_UNDES_FMAX_HIST + h);
+  }
+  d.ep_len = LD(ZB_S_EP_LEN);
+#pragma unroll
+  for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) d.sums[t] = LD(ZB_S_EP_SUMS + t);
+#undef LD
+}
+
+__device__ __forceinline__ void store_state(float* __restrict__ st, int N, int i, const Phys& p, const Mdp& d) {
+#define SV(f, v) st[(size_t)(f) * N + i] = (v)
+#pragma unroll
+  for (int a = 0; a < 3; ++a) { SV(ZB_S_ROOT_POS + a, p.pos[a]); SV(ZB_S_ROOT_LINVEL + a, p.lv[a]); SV(ZB_S_ROOT_ANGVEL + a, p.av[a]); }
+#pragma unroll
+  for (int a = 0; a < 4; ++a) SV(ZB_S_ROOT_QUAT + a, p.quat[a]);
+#pragma unroll
+  for (int j = 0; j < ND; ++j) {
+    SV(ZB_S_JOINT_POS + j, p.jq[j]); SV(ZB_S_JOINT_VEL + j, p.jqd[j]);
+    SV(ZB_S_P_DELTA + j, d.p_delta[j]); SV(ZB_S_ACTIONS + j, d.actions[j]);
+  }
+#pragma unroll
+  for (int f = 0; f < 2; ++f) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) SV(ZB_S_FEET_DOWN_POS + 3 * f + a, d.down_pos[f][a]);
+    SV(ZB_S_FEET_STEP_LEN + f, d.step_len[f]);
+    SV(ZB_S_FEET_F_LAST + f, d.f_last[f]);
+    SV(ZB_S_FEET_AIR_CUR + f, d.air_cur[f]);
+    SV(ZB_S_FEET_AIR_LAST + f, d.air_last[f]);
+    SV(ZB_S_FEET_CONTACT_CUR + f, d.contact_cur[f]);
+  }
+  SV(ZB_S_HEADING_SUM, d.heading_sum);
+  SV(ZB_S_Y_ERR_SUM, d.yerr_sum);
+#pragma unroll
+  for (int h = 0; h < ZB_HIST; ++h) {
+    SV(ZB_S_FEET_FZ_HIST + 2 * h, d.fz_hist[h][0]);
+    SV(ZB_S_FEET_FZ_HIST + 2 * h + 1, d.fz_hist[h][1]);
+    SV(ZB_S_UNDES_FMAX_HIST + h, d.fmax_hist[h]);
+  }
+  SV(ZB_S_EP_LEN, d.ep_len);
+#pragma unroll
+  for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) SV(ZB_S_EP_SUMS + t, d.sums[t]);
+#undef SV
+}
+
+// _reset_idx for one env (v2.py:413-459); feet_step_len and f_last are NOT reset (reference)
+__device__ __forceinline__ void reset_env(MP m, Phys& p, Mdp& d) {
+#pragma unroll
+  for (int a = 0; a < 3; ++a) { p.pos[a] = m->default_root_pos[a]; p.lv[a] = 0.f; p.av[a] = 0.f; }
+#pragma unroll
+  for (int a = 0; a < 4; ++a) p.quat[a] = m->default_root_quat[a];
+#pragma unroll
+  for (int j = 0; j < ND; ++j) { p.jq[j] = m->default_joint_pos[j]; p.jqd[j] = 0.f; d.p_delta[j] = 0.f; d.actions[j] = 0.f; }
+  {
+    Kin k;
+    fk(m, p, k);
+    float q[4];
+    link_pose(m, k, 0, d.down_pos[0], q);
+    link_pose(m, k, 11, d.down_pos[1], q);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) { d.down_pos[0][a] += p.pos[a]; d.down_pos[1][a] += p.pos[a]; }
+  }
+  d.heading_sum = 0.f;
+  d.yerr_sum = 0.f;
+#pragma unroll
+  for (int h = 0; h < ZB_HIST; ++h) { d.fz_hist[h][0] = d.fz_hist[h][1] = 0.f; d.fmax_hist[h] = 0.f; }
+#pragma unroll
+  for (int f = 0; f < 2; ++f) { d.air_cur[f] = d.air_last[f] = d.contact_cur[f] = 0.f; }
+  d.ep_len = 0.f;
+#pragma unroll
+  for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) d.sums[t] = 0.f;
+}
+
+__device__ __forceinline__ void write_obs(MP m, const Phys& p, const Mdp& d,
+                                          float* __restrict__ obs, int i) {
+  Cache c;
+  make_cache(m, p, c);
+  float* o = obs + (size_t)i * ZB_OBS_DIM;
+  o[0] = c.base_quat[0]; o[1] = c.base_quat[1]; o[2] = c.base_quat[2]; o[3] = c.base_quat[3];
+#pragma unroll
+  for (int j = 0; j < ND; ++j) {
+    o[4 + j] = p.jq[j] - m->default_joint_pos[j];
+    o[10 + j] = p.jqd[j];
+    o[16 + j] = d.actions[j];
+  }
+  o[22] = 1.0f;
+}
+
+// accumulator layout: [0..12] episode-sum totals of reset envs, [13] n_reset, [14] n_died, [15] n_timeout
+constexpr int ACC = 16;
+
+// ------------------------------------------------------------------------- kernels
+__device__ __forceinline__ void load_phys(const float* __restrict__ st, int N, int i, Phys& p) {
+#define LD(f) st[(size_t)(f) * N + i]
+#pragma unroll
+  for (int a = 0; a < 3; ++a) { p.pos[a] = LD(ZB_S_ROOT_POS + a); p.lv[a] = LD(ZB_S_ROOT_LINVEL + a); p.av[a] = LD(ZB_S_ROOT_ANGVEL + a); }
+#pragma unroll
+  for (int a = 0; a < 4; ++a) p.quat[a] = LD(ZB_S_ROOT_QUAT + a);
+#pragma unroll
+  for (int j = 0; j < ND; ++j) { p.jq[j] = LD(ZB_S_JOINT_POS + j); p.jqd[j] = LD(ZB_S_JOINT_VEL + j); }
+#undef LD
+}
+
+// One policy step per lane. Live state across the 4 substeps is kept to the physics state, the
+// joint targets and the ~15 floats of the lagged observation cache the rewards need; the MDP
+// state is loaded from HBM only after the physics.
+__global__ __launch_bounds__(WAVE, 1) void zb_step_kernel(const zb_model* __restrict__ mg, zb_task_cfg cfg, int N,
+                                                          float* __restrict__ st, const float* __restrict__ act,
+                                                          float* __restrict__ obs, float* __restrict__ rew,
+                                                          uint8_t* __restrict__ term, uint8_t* __restrict__ trunc,
+                                                          float* __restrict__ acc) {
+  MP m = to_mp(mg);
+  __shared__ float lds[LDS_FLOATS];
+  const int i = blockIdx.x * WAVE + threadIdx.x;
+  if (i >= N) return;
+  const Lane ld{lds + threadIdx.x};
+#define ST(f) st[(size_t)(f) * N + i]
+  Phys p;
+  load_phys(st, N, i, p);
+
+  // _pre_physics_step (v2.py:276-287); _actions / p_delta are final here and stored at once
+  const float step_dt = cfg.sim_dt * (float)cfg.decimation;
+  float target[ND];
+  float r_action_rate = 0.f;
+#pragma unroll
+  for (int j = 0; j < ND; ++j) {
+    const float a_prev = ST(ZB_S_ACTIONS + j);
+    const float a_now = tanhf(act[(size_t)i * ZB_ACT_DIM + j]);
+    const float pd = clampf(ST(ZB_S_P_DELTA + j) + PI_F * a_now * cfg.joint_speed_limit * step_dt, -PI_F, PI_F);
+    ST(ZB_S_P_DELTA + j) = pd;
+    ST(ZB_S_ACTIONS + j) = a_now;
+    target[j] = pd + m->default_joint_pos[j];
+    r_action_rate += (a_now - a_prev) * (a_now - a_prev);   // v2.py:502-507
+  }
+
+  // the previous _get_observations cache (one-step lag, v2.py:315-345): the pre-step terms are
+  // evaluated now, only what step_length / dones need is carried across the physics
+  float r_pre[5];
+  float pre_base_y, pre_base_z, pre_heading, pre_fwd[3], pre_feet[2][3];
+  {
+    Cache c;
+    make_cache(opaque(m), p, c);
+    r_pre[0] = tanhf(10.f * c.vfwd / cfg.joint_speed_limit);                     // base_vel_forward
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+      const float dz[3] = {c.feet_z[f][0], c.feet_z[f][1], c.feet_z[f][2] - 1.f};
+      s1 += sqrtf(dot3(dz, dz));                                                 // feet_downward
+      const float dx[3] = {c.feet_x[f][0] - c.fwd[0], c.feet_x[f][1] - c.fwd[1], c.feet_x[f][2] - c.fwd[2]};
+      s2 += sqrtf(dot3(dx, dx));                                                 // feet_forward
+    }
+    r_pre[1] = s1;
+    r_pre[2] = s2;
+    r_pre[3] = fabsf(c.heading_err);                                             // base_heading_x
+    r_pre[4] = fabsf(c.feet_pos[0][1] + c.feet_pos[1][1]) + fabsf(c.base_pos[1]); // base_pos_y_err (origin 0)
+    pre_base_y = c.base_pos[1];
+    pre_base_z = c.base_pos[2];
+    pre_heading = c.heading_err;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) { pre_fwd[a] = c.fwd[a]; pre_feet[0][a] = c.feet_pos[0][a]; pre_feet[1][a] = c.feet_pos[1][a]; }
+  }
+
+  // 4 physics substeps (the last one reports the contact-sensor inputs and applied torques)
+  SensorOut so;
+  for (int k = 0; k < cfg.decimation; ++k)
+    substep<false>(m, cfg, p, target, ld, k == cfg.decimation - 1, so, nullptr, nullptr);
+  m = opaque(m);
+
+  // ContactSensor lazy update, once per policy step (history roll, air/contact timers)
+  float fz_hist[ZB_HIST][2], fmax_hist[ZB_HIST];
+#pragma unroll
+  for (int h = ZB_HIST - 1; h > 0; --h) {
+    fz_hist[h][0] = ST(ZB_S_FEET_FZ_HIST + 2 * (h - 1));
+    fz_hist[h][1] = ST(ZB_S_FEET_FZ_HIST + 2 * (h - 1) + 1);
+    fmax_hist[h] = ST(ZB_S_UNDES_FMAX_HIST + h - 1);
+  }
+  fmax_hist[0] = so.undes_fmax;
+  float air_last[2];
+#pragma unroll
+  for (int f = 0; f < 2; ++f) {
+    fz_hist[0][f] = so.feet_f[f][2];
+    const bool contact = sqrtf(dot3(so.feet_f[f], so.feet_f[f])) > cfg.contact_force_threshold;
+    const float air_cur = ST(ZB_S_FEET_AIR_CUR + f);
+    air_last[f] = ST(ZB_S_FEET_AIR_LAST + f);
+    if (air_cur > 0.f && contact) air_last[f] = air_cur + step_dt;
+    ST(ZB_S_FEET_AIR_CUR + f) = contact ? 0.f : air_cur + step_dt;
+    ST(ZB_S_FEET_CONTACT_CUR + f) = contact ? ST(ZB_S_FEET_CONTACT_CUR + f) + step_dt : 0.f;
+    ST(ZB_S_FEET_AIR_LAST + f) = air_last[f];
+  }
+#pragma unroll
+  for (int h = 0; h < ZB_HIST; ++h) {
+    ST(ZB_S_FEET_FZ_HIST + 2 * h) = fz_hist[h][0];
+    ST(ZB_S_FEET_FZ_HIST + 2 * h + 1) = fz_hist[h][1];
+    ST(ZB_S_UNDES_FMAX_HIST + h) = fmax_hist[h];
+  }
+  const float ep_len = ST(ZB_S_EP_LEN) + 1.f;
+
+  // post-step feet COM velocities (feet_slide)
+  float feet_vel[2][3];
+  {
+    Kin k;
+    fk(m, p, k);
+    float V[NB][6];
+    body_vel(k, p, V);
+    link_com_vel(m, k, V, 0, feet_vel[0]);
+    link_com_vel(m, k, V, 11, feet_vel[1]);
+  }
+
+  // _get_dones (v2.py:384-411)
+  const bool time_out = ep_len >= (float)(cfg.max_episode_length - 1);
+  float feetF[2];
+#pragma unroll
+  for (int f = 0; f < 2; ++f) {
+    float sacc = 0.f;
+#pragma unroll
+    for (int h = 0; h < ZB_HIST; ++h) sacc += fz_hist[h][f];
+    feetF[f] = sacc / (float)ZB_HIST;
+  }
+  bool died = false;
+#pragma unroll
+  for (int h = 0; h < ZB_HIST; ++h) died |= fmax_hist[h] > 1.0f;
+  died |= pre_base_z < cfg.termination_height;
+  died |= fabsf(pre_base_y) > 0.5f;  // base_pos_y_err vs env origin (local frame: 0)
+
+  // _get_rewards (v2.py:371-382) in dict order
+  float r[ZB_NUM_REWARD_TERMS];
+  r[ZB_R_BASE_VEL_FORWARD] = r_pre[0];
+  r[ZB_R_FEET_DOWNWARD] = r_pre[1];
+  r[ZB_R_FEET_FORWARD] = r_pre[2];
+  r[ZB_R_BASE_HEADING_X] = r_pre[3];
+  {
+    const float hs = clampf(ST(ZB_S_HEADING_SUM) + 0.01f * pre_heading, -1.f, 1.f);
+    ST(ZB_S_HEADING_SUM) = hs;
+    r[ZB_R_BASE_HEADING_X_SUM] = fabsf(hs);
+  }
+  {
+    float step_len[2];
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+      step_len[f] = ST(ZB_S_FEET_STEP_LEN + f);
+      if (feetF[f] > 10.f && ST(ZB_S_FEET_F_LAST + f) < 10.f) {   // touchdown, v2.py:514-517
+        float dv[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+          dv[a] = pre_feet[f][a] - ST(ZB_S_FEET_DOWN_POS + 3 * f + a);
+          ST(ZB_S_FEET_DOWN_POS + 3 * f + a) = pre_feet[f][a];
+        }
+        step_len[f] = dot3(dv, pre_fwd);
+        ST(ZB_S_FEET_STEP_LEN + f) = step_len[f];
+      }
+      ST(ZB_S_FEET_F_LAST + f) = feetF[f];
+    }
+    r[ZB_R_STEP_LENGTH] = tanhf(15.f * fminf(step_len[0], step_len[1]));
+  }
+  r[ZB_R_AIRTIME_BALANCE] = fabsf(air_last[0] - air_last[1]);
+  r[ZB_R_ACTION_RATE] = r_action_rate;
+  r[ZB_R_TORQUES] = so.tau2;
+  {
+    float sacc = 0.f;
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+      sacc += sqrtf(feet_vel[f][0] * feet_vel[f][0] + feet_vel[f][1] * feet_vel[f][1]) * (feetF[f] > 1.f ? 1.f : 0.f);
+    r[ZB_R_FEET_SLIDE] = sacc;
+  }
+  r[ZB_R_BASE_POS_Y_ERR] = r_pre[4];
+  {
+    const float ys = clampf(ST(ZB_S_Y_ERR_SUM) + 0.01f * pre_base_y, -1.f, 1.f);
+    ST(ZB_S_Y_ERR_SUM) = ys;
+    r[ZB_R_BASE_POS_Y_ERR_SUM] = fabsf(ys);
+  }
+  r[ZB_R_AIRTIME_SUM] = tanhf(air_last[0] + air_last[1]);
+
+  float reward = 0.f;
+  const bool reset = died || time_out;
+#pragma unroll
+  for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) {
+    const float v = r[t] * cfg.reward_scales[t];
+    reward += v;
+    const float sum = ST(ZB_S_EP_SUMS + t) + v;
+    ST(ZB_S_EP_SUMS + t) = reset ? 0.f : sum;
+    if (reset) atomicAdd(&acc[t], sum);   // episode log (v2.py:441-448)
+  }
+  if (died) reward -= cfg.terminal_penalty;  // v2.py:379-380
+  ST(ZB_S_EP_LEN) = reset ? 0.f : ep_len;
+
+  // in-kernel auto-reset (v2.py:413-459); the state written above is overwritten for reset envs
+  if (reset) {
+    atomicAdd(&acc[13], 1.f);
+    if (died) atomicAdd(&acc[14], 1.f);
+    if (time_out) atomicAdd(&acc[15], 1.f);
+    Mdp d;
+    load_state(st, N, i, p, d);
+    reset_env(m, p, d);
+    store_state(st, N, i, p, d);
+  } else {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) { ST(ZB_S_ROOT_POS + a) = p.pos[a]; ST(ZB_S_ROOT_LINVEL + a) = p.lv[a]; ST(ZB_S_ROOT_ANGVEL + a) = p.av[a]; }
+#pragma unroll
+    for (int a = 0; a < 4; ++a) ST(ZB_S_ROOT_QUAT + a) = p.quat[a];
+#pragma unroll
+    for (int j = 0; j < ND; ++j) { ST(ZB_S_JOINT_POS + j) = p.jq[j]; ST(ZB_S_JOINT_VEL + j) = p.jqd[j]; }
+  }
+  // _get_observations (v2.py:351-365) of the post-step / post-reset state
+  {
+    Cache c;
+    make_cache(m, p, c);
+    float* o = obs + (size_t)i * ZB_OBS_DIM;
+    o[0] = c.base_quat[0]; o[1] = c.base_quat[1]; o[2] = c.base_quat[2]; o[3] = c.base_quat[3];
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+      o[4 + j] = p.jq[j] - m->default_joint_pos[j];
+      o[10 + j] = p.jqd[j];
+      o[16 + j] = reset ? 0.f : ST(ZB_S_ACTIONS + j);
+    }
+    o[22] = cfg.joint_speed_limit;
+  }
+  rew[i] = reward;
+  term[i] = died ? 1 : 0;
+  trunc[i] = time_out ? 1 : 0;
+#undef ST
+}
+
+// reset env_ids (or all when ids == nullptr); logs the reset envs' episode sums into acc
+__global__ void zb_reset_kernel(const zb_model* __restrict__ mg, int N, float* __restrict__ st,
+                                const int32_t* __restrict__ ids, int n, float* __restrict__ acc) {
+  MP m = to_mp(mg);
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const int i = ids ? ids[t] : t;
+  if (i < 0 || i >= N) return;
+  Phys p;
+  Mdp d;
+  load_state(st, N, i, p, d);
+#pragma unroll
+  for (int k = 0; k < ZB_NUM_REWARD_TERMS; ++k) atomicAdd(&acc[k], d.sums[k]);
+  atomicAdd(&acc[13], 1.f);
+  reset_env(m, p, d);
+  store_state(st, N, i, p, d);
+}
+
+// episode log finalisation + full-reset episode_length_buf draw (v2.py:418-422)
+__global__ void zb_finalize_kernel(int N, float* __restrict__ st, const float* __restrict__ acc,
+                                   float* __restrict__ log_means, int32_t* __restrict__ log_counts, float episode_s,
+                                   int max_ep_len, uint64_t seed, uint64_t ctr, int force_full, int reset_counts) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const float nres = acc[13];
+  if (i == 0 && nres > 0.f) {
+#pragma unroll
+    for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) log_means[t] = acc[t] / nres / episode_s;
+    log_counts[0] = reset_counts ? 0 : (int32_t)acc[14];
+    log_counts[1] = reset_counts ? 0 : (int32_t)acc[15];
+  }
+  if (i < N && (force_full || nres == (float)N)) {
+    const uint64_t h = hash64(seed ^ hash64(ctr * 0x100000001B3ull + (uint64_t)i));
+    st[(size_t)ZB_S_EP_LEN * N + i] = (float)(int)(h % (uint64_t)max_ep_len);
+  }
+}
+
+__global__ void zb_observe_kernel(const zb_model* __restrict__ mg, int N, const float* __restrict__ st,
+                                  float* __restrict__ obs) {
+  MP m = to_mp(mg);
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  Phys p;
+  Mdp d;
+  load_state(st, N, i, p, d);
+  write_obs(m, p, d, obs, i);
+}
+
+__global__ __launch_bounds__(WAVE, 1) void zb_substeps_kernel(const zb_model* __restrict__ mg, zb_task_cfg cfg, int N,
+                                                              float* __restrict__ st, const float* __restrict__ targets,
+                                                              int nsub, float* __restrict__ net_force,
+                                                              float* __restrict__ tau_out) {
+  MP m = to_mp(mg);
+  __shared__ float lds[LDS_FLOATS];
+  const int i = blockIdx.x * WAVE + threadIdx.x;
+  if (i >= N) return;
+  const Lane ld{lds + threadIdx.x};
+  Phys p;
+  load_phys(st, N, i, p);
+  float tg[ND], tau[ND], F[NL][3];
+#pragma unroll
+  for (int j = 0; j < ND; ++j) { tg[j] = targets[(size_t)i * ND + j]; tau[j] = 0.f; }
+  SensorOut so;
+  for (int k = 0; k < nsub; ++k) substep<true>(m, cfg, p, tg, ld, k == nsub - 1, so, F, tau);
+  if (net_force)
+#pragma unroll
+    for (int l = 0; l < NL; ++l)
+#pragma unroll
+      for (int a = 0; a < 3; ++a) net_force[((size_t)i * NL + l) * 3 + a] = F[l][a];
+  if (tau_out)
+#pragma unroll
+    for (int j = 0; j < ND; ++j) tau_out[(size_t)i * ND + j] = tau[j];
+#define SV(f, v) st[(size_t)(f) * N + i] = (v)
+#pragma unroll
+  for (int a = 0; a < 3; ++a) { SV(ZB_S_ROOT_POS + a, p.pos[a]); SV(ZB_S_ROOT_LINVEL + a, p.lv[a]); SV(ZB_S_ROOT_ANGVEL + a, p.av[a]); }
+#pragma unroll
+  for (int a = 0; a < 4; ++a) SV(ZB_S_ROOT_QUAT + a, p.quat[a]);
+#pragma unroll
+  for (int j = 0; j < ND; ++j) { SV(ZB_S_JOINT_POS + j, p.jq[j]); SV(ZB_S_JOINT_VEL + j, p.jqd[j]); }
+#undef SV
+}
+
+}  // namespace
+
+// =========================================================================== C ABI
+struct zb_sim {
+  int device;
+  int n;
+  uint64_t seed;
+  uint64_t calls;
+  zb_task_cfg cfg;
+  zb_model* d_model;
+  float* d_state;
+  float* d_acc;
+  float* d_log_means;
+  int32_t* d_log_counts;
+  // optional per-launch timing of zb_step_kernel (hipEvents on the launch stream)
+  int prof_max = 0, prof_n = 0;
+  hipEvent_t* prof_ev = nullptr;
+};
+
+static thread_local char g_err[512] = "";
+
+static int set_err(int code, const char* what, hipError_t e) {
+  snprintf(g_err, sizeof(g_err), "%s: %s", what, e == hipSuccess ? "invalid argument" : hipGetErrorString(e));
+  return code;
+}
+
+#define HIPCHK(x, what)                                   \
+  do {                                                    \
+    hipError_t e_ = (x);                                  \
+    if (e_ != hipSuccess) return set_err(-2, what, e_);   \
+  } while (0)
+
+static int launch_check(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_err(-3, what, e);
+  return 0;
+}
+
+extern "C" {
+
+const char* zb_last_error(void) { return g_err; }
+
+int zb_num_envs(zb_handle h) { return h ? h->n : -1; }
+
+int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_device, uint64_t seed, zb_handle* out) {
+  if (!m || !c || !out || num_envs <= 0) return set_err(-1, "zb_create", hipSuccess);
+  for (int l = 0; l < NL; ++l)
+    if (m->link_body[l] != link_body(l)) return set_err(-1, "zb_create: model topology != compiled ZBOT-6 chain", hipSuccess);
+  if (m->base_link != 6 || m->foot_links[0] != 0 || m->foot_links[1] != 11)
+    return set_err(-1, "zb_create: unexpected base/feet link indices", hipSuccess);
+  for (int k = 0; k < 10; ++k)
+    if (m->undesired_links[k] != k + 1) return set_err(-1, "zb_create: unexpected undesired link set", hipSuccess);
+  {
+    int np = 0;
+    for (int a = 0; a < NL; ++a)
+      for (int b = a + 2; b < NL; ++b) {
+        if (np >= m->num_self_pairs || m->self_pairs[np][0] != a || m->self_pairs[np][1] != b)
+          return set_err(-1, "zb_create: self-collision pair list != compiled list", hipSuccess);
+        ++np;
+      }
+    if (np != m->num_self_pairs) return set_err(-1, "zb_create: self-collision pair count", hipSuccess);
+  }
+  if (c->decimation < 1 || c->solver_iterations < 0) return set_err(-1, "zb_create: cfg", hipSuccess);
+  HIPCHK(hipSetDevice(hip_device), "hipSetDevice");
+  zb_sim* h = new zb_sim();
+  h->device = hip_device;
+  h->n = num_envs;
+  h->seed = seed;
+  h->calls = 0;
+  h->cfg = *c;
+  HIPCHK(hipMalloc(&h->d_model, sizeof(zb_model)), "hipMalloc model");
+  HIPCHK(hipMalloc(&h->d_state, sizeof(float) * (size_t)ZB_STATE_DIM * num_envs), "hipMalloc state");
+  HIPCHK(hipMalloc(&h->d_acc, sizeof(float) * ACC), "hipMalloc acc");
+  HIPCHK(hipMalloc(&h->d_log_means, sizeof(float) * ZB_NUM_REWARD_TERMS), "hipMalloc log");
+  HIPCHK(hipMalloc(&h->d_log_counts, sizeof(int32_t) * 2), "hipMalloc log");
+  HIPCHK(hipMemcpy(h->d_model, m, sizeof(zb_model), hipMemcpyHostToDevice), "hipMemcpy model");
+  HIPCHK(hipMemset(h->d_state, 0, sizeof(float) * (size_t)ZB_STATE_DIM * num_envs), "hipMemset state");
+  HIPCHK(hipMemset(h->d_log_means, 0, sizeof(float) * ZB_NUM_REWARD_TERMS), "hipMemset log");
+  HIPCHK(hipMemset(h->d_log_counts, 0, sizeof(int32_t) * 2), "hipMemset log");
+  HIPCHK(hipMemset(h->d_acc, 0, sizeof(float) * ACC), "hipMemset acc");
+  // start at the default pose (ep_len 0, as after construction; reset() randomises it)
+  zb_reset_kernel<<<(num_envs + 255) / 256, 256>>>(h->d_model, num_envs, h->d_state, nullptr, num_envs, h->d_acc);
+  int rc = launch_check("zb_reset_kernel");
+  if (rc) return rc;
+  HIPCHK(hipMemset(h->d_acc, 0, sizeof(float) * ACC), "hipMemset acc");
+  HIPCHK(hipDeviceSynchronize(), "zb_create sync");
+  *out = h;
+  return 0;
+}
+
+static void prof_free(zb_handle h) {
+  for (int k = 0; k < 2 * h->prof_max; ++k) (void)hipEventDestroy(h->prof_ev[k]);
+  delete[] h->prof_ev;
+  h->prof_ev = nullptr;
+  h->prof_max = h->prof_n = 0;
+}
+
+int zb_profile_begin(zb_handle h, int max_launches) {
+  if (!h || max_launches < 0) return set_err(-1, "zb_profile_begin", hipSuccess);
+  prof_free(h);
+  h->prof_ev = new hipEvent_t[2 * (size_t)max_launches];
+  for (int k = 0; k < 2 * max_launches; ++k) HIPCHK(hipEventCreate(&h->prof_ev[k]), "hipEventCreate");
+  h->prof_max = max_launches;
+  h->prof_n = 0;
+  return 0;
+}
+
+int zb_profile_end(zb_handle h, float* total_ms, int* count) {
+  if (!h || !total_ms || !count) return set_err(-1, "zb_profile_end", hipSuccess);
+  float tot = 0.f;
+  for (int k = 0; k < h->prof_n; ++k) {
+    HIPCHK(hipEventSynchronize(h->prof_ev[2 * k + 1]), "hipEventSynchronize");
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, h->prof_ev[2 * k], h->prof_ev[2 * k + 1]), "hipEventElapsedTime");
+    tot += ms;
+  }
+  *total_ms = tot;
+  *count = h->prof_n;
+  prof_free(h);
+  return 0;
+}
+
+void zb_destroy(zb_handle h) {
+  if (!h) return;
+  prof_free(h);
+  (void)hipSetDevice(h->device);
+  (void)hipFree(h->d_model);
+  (void)hipFree(h->d_state);
+  (void)hipFree(h->d_acc);
+  (void)hipFree(h->d_log_means);
+  (void)hipFree(h->d_log_counts);
+  delete h;
+}
+
+int zb_reset(zb_handle h, const int32_t* env_ids, int n, void* stream) {
+  if (!h) return set_err(-1, "zb_reset", hipSuccess);
+  hipStream_t s = (hipStream_t)stream;
+  const int cnt = env_ids ? n : h->n;
+  if (cnt <= 0) return 0;
+  HIPCHK(hipMemsetAsync(h->d_acc, 0, sizeof(float) * ACC, s), "hipMemsetAsync acc");
+  zb_reset_kernel<<<(cnt + 255) / 256, 256, 0, s>>>(h->d_model, h->n, h->d_state, env_ids, cnt, h->d_acc);
+  int rc = launch_check("zb_reset_kernel");
+  if (rc) return rc;
+  const uint64_t ctr = h->calls++;
+  const float ep_s = h->cfg.sim_dt * h->cfg.decimation * h->cfg.max_episode_length;
+  const int full = env_ids == nullptr || n == h->n;
+  zb_finalize_kernel<<<(h->n + 255) / 256, 256, 0, s>>>(h->n, h->d_state, h->d_acc, h->d_log_means, h->d_log_counts,
+                                                        ep_s, h->cfg.max_episode_length, h->seed, ctr, full, 1);
+  return launch_check("zb_finalize_kernel");
+}
+
+int zb_step(zb_handle h, const float* actions, float* obs, float* reward, uint8_t* terminated, uint8_t* truncated,
+            void* stream) {
+  if (!h || !actions || !obs || !reward || !terminated || !truncated) return set_err(-1, "zb_step", hipSuccess);
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK(hipMemsetAsync(h->d_acc, 0, sizeof(float) * ACC, s), "hipMemsetAsync acc");
+  const int blocks = (h->n + WAVE - 1) / WAVE;
+  const bool prof = h->prof_n < h->prof_max;
+  if (prof) HIPCHK(hipEventRecord(h->prof_ev[2 * h->prof_n], s), "hipEventRecord");
+  zb_step_kernel<<<blocks, WAVE, 0, s>>>(h->d_model, h->cfg, h->n, h->d_state, actions, obs, reward, terminated,
+                                         truncated, h->d_acc);
+  int rc = launch_check("zb_step_kernel");
+  if (prof) {
+    HIPCHK(hipEventRecord(h->prof_ev[2 * h->prof_n + 1], s), "hipEventRecord");
+    ++h->prof_n;
+  }
+  if (rc) return rc;
+  const uint64_t ctr = h->calls++;
+  const float ep_s = h->cfg.sim_dt * h->cfg.decimation * h->cfg.max_episode_length;
+  zb_finalize_kernel<<<(h->n + 255) / 256, 256, 0, s>>>(h->n, h->d_state, h->d_acc, h->d_log_means, h->d_log_counts,
+                                                        ep_s, h->cfg.max_episode_length, h->seed, ctr, 0, 0);
+  return launch_check("zb_finalize_kernel");
+}
+
+int zb_observe(zb_handle h, float* obs, void* stream) {
+  if (!h || !obs) return set_err(-1, "zb_observe", hipSuccess);
+  zb_observe_kernel<<<(h->n + 255) / 256, 256, 0, (hipStream_t)stream>>>(h->d_model, h->n, h->d_state, obs);
+  return launch_check("zb_observe_kernel");
+}
+
+int zb_read_log(zb_handle h, float* term_means, int32_t* counts, void* stream) {
+  if (!h) return set_err(-1, "zb_read_log", hipSuccess);
+  hipStream_t s = (hipStream_t)stream;
+  if (term_means)
+    HIPCHK(hipMemcpyAsync(term_means, h->d_log_means, sizeof(float) * ZB_NUM_REWARD_TERMS, hipMemcpyDeviceToDevice, s),
+           "hipMemcpyAsync log");
+  if (counts)
+    HIPCHK(hipMemcpyAsync(counts, h->d_log_counts, sizeof(int32_t) * 2, hipMemcpyDeviceToDevice, s), "hipMemcpyAsync log");
+  return 0;
+}
+
+int zb_get_state(zb_handle h, float* dst, void* stream) {
+  if (!h || !dst) return set_err(-1, "zb_get_state", hipSuccess);
+  HIPCHK(hipMemcpyAsync(dst, h->d_state, sizeof(float) * (size_t)ZB_STATE_DIM * h->n, hipMemcpyDeviceToDevice,
+                        (hipStream_t)stream),
+         "hipMemcpyAsync state");
+  return 0;
+}
+
+int zb_set_state(zb_handle h, const float* src, void* stream) {
+  if (!h || !src) return set_err(-1, "zb_set_state", hipSuccess);
+  HIPCHK(hipMemcpyAsync(h->d_state, src, sizeof(float) * (size_t)ZB_STATE_DIM * h->n, hipMemcpyDeviceToDevice,
+                        (hipStream_t)stream),
+         "hipMemcpyAsync state");
+  return 0;
+}
+
+int zb_physics_substeps(zb_handle h, const float* targets, int nsub, float* net_force, float* applied_torque,
+                        void* stream) {
+  if (!h || !targets || nsub < 1) return set_err(-1, "zb_physics_substeps", hipSuccess);
+  const int blocks = (h->n + WAVE - 1) / WAVE;
+  zb_substeps_kernel<<<blocks, WAVE, 0, (hipStream_t)stream>>>(h->d_model, h->cfg, h->n, h->d_state, targets, nsub,
+                                                               net_force, applied_torque);
+  return launch_check("zb_substeps_kernel");
+}
+
+}  // extern "C"

@@ -1,0 +1,192 @@
+"""``zbot-6b-walking-v2`` with the reference's DirectRLEnv interface, stepped by the HIP simulator.
+
+Reference: ``source/zbot/zbot/tasks/zbot6b_direct/zbot_direct_6dof_bipedal_env_v2.py`` (``v2.py``):
+``ZbotDirectEnvCfgV2`` (v2.py:26-206) and ``ZbotDirectEnvV2`` (v2.py:208-605), driven by Isaac Lab's
+``DirectRLEnv.step`` / ``reset``. Callers see the same 5-tuple ``step`` contract
+(``obs {"policy": [N,23]}, reward [N], terminated [N] bool, truncated [N] bool, extras``), the
+same ``reset() -> (obs, extras)`` and the attributes rsl_rl and the reference scripts use
+(``num_envs``, ``device``, ``step_dt``, ``max_episode_length``, settable ``episode_length_buf``,
+``cfg``, ``single_action_space``, ``single_observation_space``, ``unwrapped``, ...).
+
+Everything per step runs in one fused HIP kernel (``libzbot.so``); this class only moves
+pointers. Differences from the reference are listed in DESIGN.md §4 (no rendering, env-local
+coordinates internally, `episode_length_buf` returned as a copy).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from .. import model as zm
+from .. import spaces
+from ..sim import ZbotSim
+
+
+@dataclass
+class SimulationCfg:
+    dt: float = 1.0 / 200.0          # v2.py:48
+    render_interval: int = 4          # v2.py:49
+    device: str = "cuda:0"
+    gravity: tuple = (0.0, 0.0, -9.81)
+    static_friction: float = 1.0      # v2.py:49-56 (multiply combine with the ground's 1.0)
+    dynamic_friction: float = 1.0
+    restitution: float = 0.0
+
+
+@dataclass
+class InteractiveSceneCfg:
+    num_envs: int = 4096              # v2.py:73-75
+    env_spacing: float = 4.0
+    replicate_physics: bool = True
+
+
+@dataclass
+class SolverCfg:
+    """Parameters of this simulator's contact/drive solver (no reference counterpart)."""
+    iterations: int = 8
+    contact_margin: float = 0.004
+    baumgarte: float = 0.2
+    self_collision: bool = True       # enabled_self_collisions=True (zbot_cfg.py:636)
+
+
+@dataclass
+class ZbotDirectEnvCfgV2:
+    """Mirror of ``ZbotDirectEnvCfgV2`` (v2.py:26-206)."""
+    episode_length_s: float = 20.0
+    decimation: int = 4
+    action_space: int = 6
+    observation_space: int = 23
+    state_space: int = 0
+    termination_height: float = 0.22
+    sim: SimulationCfg = field(default_factory=SimulationCfg)
+    scene: InteractiveSceneCfg = field(default_factory=InteractiveSceneCfg)
+    solver: SolverCfg = field(default_factory=SolverCfg)
+    seed: int | None = None
+    reward_cfg: dict = field(default_factory=lambda: {"reward_scales": dict(zm.REWARD_WEIGHTS)})
+
+    def task_cfg(self) -> zm.TaskCfg:
+        return zm.TaskCfg(
+            sim_dt=self.sim.dt, decimation=self.decimation, episode_length_s=self.episode_length_s,
+            termination_height=self.termination_height,
+            reward_weights=dict(self.reward_cfg["reward_scales"]), gravity=-self.sim.gravity[2],
+            friction=self.sim.static_friction, contact_margin=self.solver.contact_margin,
+            baumgarte=self.solver.baumgarte, solver_iterations=self.solver.iterations,
+            enable_self_collision=self.solver.self_collision,
+        )
+
+
+def grid_env_origins(num_envs: int, spacing: float) -> torch.Tensor:
+    """Isaac Lab's TerrainImporter grid of env origins (plane terrain, ``env_spacing``)."""
+    num_rows = int(np.ceil(num_envs / np.sqrt(num_envs)))
+    num_cols = int(np.ceil(num_envs / num_rows))
+    ii, jj = torch.meshgrid(torch.arange(num_rows), torch.arange(num_cols), indexing="ij")
+    origins = torch.zeros(num_envs, 3)
+    origins[:, 0] = -(ii.flatten()[:num_envs] - (num_rows - 1) / 2) * spacing
+    origins[:, 1] = (jj.flatten()[:num_envs] - (num_cols - 1) / 2) * spacing
+    return origins
+
+
+class ZbotDirectEnvV2:
+    """DirectRLEnv-compatible ``zbot-6b-walking-v2`` (v2.py:208-605) on the MI355X simulator."""
+
+    is_vector_env = True
+    metadata = {"render_modes": [None], "isaac_sim_version": None}
+
+    def __init__(self, cfg: ZbotDirectEnvCfgV2 | None = None, render_mode: str | None = None, **kwargs):
+        self.cfg = cfg or ZbotDirectEnvCfgV2()
+        if render_mode not in (None, "rgb_array"):
+            raise ValueError("rendering is out of scope for this simulator")
+        self.render_mode = render_mode
+        self.device = torch.device(kwargs.get("device", self.cfg.sim.device))
+        self.num_envs = int(kwargs.get("num_envs", self.cfg.scene.num_envs))
+        self.physics_dt = self.cfg.sim.dt
+        self.step_dt = self.cfg.sim.dt * self.cfg.decimation
+        self.max_episode_length_s = self.cfg.episode_length_s
+        self.max_episode_length = math.ceil(self.max_episode_length_s / self.step_dt)
+        seed = self.cfg.seed if self.cfg.seed is not None else 0
+        self._task = self.cfg.task_cfg()
+        self.sim = ZbotSim(self.num_envs, self._task, device=self.device, seed=seed)
+        self.device = self.sim.device
+        self.env_origins = grid_env_origins(self.num_envs, self.cfg.scene.env_spacing).to(self.device)
+        # v2.py:250-252 — weights scaled by step_dt (kept as a new dict; the reference mutates cfg)
+        self.reward_scales = {k: v * self.step_dt for k, v in self.cfg.reward_cfg["reward_scales"].items()}
+        self.single_observation_space = spaces.Dict(policy=spaces.Box(-np.inf, np.inf, (self.cfg.observation_space,)))
+        self.single_action_space = spaces.Box(-np.inf, np.inf, (self.cfg.action_space,))
+        self.observation_space = spaces.Dict(
+            policy=spaces.Box(-np.inf, np.inf, (self.num_envs, self.cfg.observation_space)))
+        self.action_space = spaces.Box(-np.inf, np.inf, (self.num_envs, self.cfg.action_space))
+        self.common_step_counter = 0
+        self.extras: dict = {}
+        self._log_keys = [f"Episode_Reward/{k}" for k in zm.REWARD_TERMS] + [
+            "Episode_Termination/body_contact", "Episode_Termination/time_out"]
+        self.obs_buf = None
+
+    # ------------------------------------------------------------------ gym API
+    @property
+    def unwrapped(self):
+        return self
+
+    @property
+    def reset_terminated(self) -> torch.Tensor:
+        return self.sim.terminated
+
+    @property
+    def reset_time_outs(self) -> torch.Tensor:
+        return self.sim.truncated
+
+    @property
+    def reset_buf(self) -> torch.Tensor:
+        return self.sim.terminated | self.sim.truncated
+
+    @property
+    def episode_length_buf(self) -> torch.Tensor:
+        """Copy of the in-HBM episode counters (int64, like Isaac Lab's buffer)."""
+        return self.sim.get_state()[zm.S["EP_LEN"]].round().to(torch.long)
+
+    @episode_length_buf.setter
+    def episode_length_buf(self, value: torch.Tensor) -> None:
+        st = self.sim.get_state()
+        st[zm.S["EP_LEN"]] = value.to(device=self.device, dtype=torch.float32)
+        self.sim.set_state(st)
+
+    def seed(self, seed: int = -1) -> int:
+        return seed
+
+    def reset(self, seed: int | None = None, options: dict | None = None):
+        """DirectRLEnv.reset: reset all envs (v2.py:413-459, full-reset episode-length draw)."""
+        self.sim.reset(None)
+        self.obs_buf = {"policy": self.sim.observe()}
+        self._update_log()
+        return self.obs_buf, self.extras
+
+    def step(self, action: torch.Tensor):
+        """DirectRLEnv.step: one fused kernel (physics x decimation, sensor, dones, rewards, resets, obs)."""
+        obs, rew, term, trunc = self.sim.step(action)
+        self.common_step_counter += 1
+        self.obs_buf = {"policy": obs}
+        self.reward_buf = rew
+        self._update_log()
+        return self.obs_buf, rew, term, trunc, self.extras
+
+    def _update_log(self) -> None:
+        means, counts = self.sim.read_log()
+        log = {k: means[i] for i, k in enumerate(self._log_keys[:zm.NUM_TERMS])}
+        log["Episode_Termination/body_contact"] = counts[0]
+        log["Episode_Termination/time_out"] = counts[1]
+        self.extras["log"] = log
+
+    def get_observations(self):
+        if self.obs_buf is None:
+            self.obs_buf = {"policy": self.sim.observe()}
+        return self.obs_buf
+
+    def render(self, recompute: bool = False):
+        return None
+
+    def close(self) -> None:
+        if getattr(self, "sim", None) is not None:
+            self.sim.close()
+            self.sim = None

@@ -1,0 +1,50 @@
+"""``PPORunnerCfgV2`` (reference ``source/zbot/zbot/tasks/zbot6b_direct/agents/rsl_rl_ppo_cfg.py:65-91``).
+
+Hyper-parameters only; the PPO runner itself is the next §8(f) row."""
+from __future__ import annotations
+
+from dataclasses import asdict, dataclass, field
+
+
+@dataclass
+class RslRlPpoActorCriticCfg:
+    class_name: str = "ActorCritic"
+    init_noise_std: float = 1.0
+    actor_hidden_dims: list = field(default_factory=lambda: [128, 128, 128])
+    critic_hidden_dims: list = field(default_factory=lambda: [128, 128, 128])
+    activation: str = "elu"
+
+
+@dataclass
+class RslRlPpoAlgorithmCfg:
+    class_name: str = "PPO"
+    value_loss_coef: float = 1.0
+    use_clipped_value_loss: bool = True
+    clip_param: float = 0.2
+    entropy_coef: float = 0.005
+    num_learning_epochs: int = 5
+    num_mini_batches: int = 4
+    learning_rate: float = 1.0e-3
+    schedule: str = "adaptive"
+    gamma: float = 0.99
+    lam: float = 0.95
+    desired_kl: float = 0.01
+    max_grad_norm: float = 1.0
+
+
+@dataclass
+class PPORunnerCfgV2:
+    class_name: str = "OnPolicyRunner"
+    seed: int = 42
+    device: str = "cuda:0"
+    num_steps_per_env: int = 24
+    max_iterations: int = 1000
+    save_interval: int = 100
+    experiment_name: str = "zbot_6b_flat_direct_v2"
+    empirical_normalization: bool = False
+    clip_actions: float | None = None
+    policy: RslRlPpoActorCriticCfg = field(default_factory=RslRlPpoActorCriticCfg)
+    algorithm: RslRlPpoAlgorithmCfg = field(default_factory=RslRlPpoAlgorithmCfg)
+
+    def to_dict(self) -> dict:
+        return asdict(self)

@@ -1,0 +1,124 @@
+"""Torch-facing handle on the HIP simulator (``libzbot.so``): one handle = N envs on one GPU.
+
+All calls are stream-ordered on the current torch CUDA stream and never synchronise the host.
+Persistent state lives in HBM, owned by the library (SoA ``[ZB_STATE_DIM][N]`` fp32).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from . import _native as nat
+from . import model as zm
+
+
+def _stream(device: torch.device) -> C.c_void_p:
+    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+class ZbotSim:
+    def __init__(self, num_envs: int, cfg: zm.TaskCfg | None = None, device: str | torch.device = "cuda:0",
+                 seed: int = 0, robot: zm.RobotModel | None = None):
+        if num_envs < 1:
+            raise ValueError("num_envs must be >= 1")
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise nat.ZbotError("ZbotSim runs on a ROCm GPU only (device must be cuda:<i>); there is no CPU path")
+        if not torch.cuda.is_available():
+            raise nat.ZbotError("no ROCm GPU visible: the HIP simulator cannot run here")
+        self.lib = nat.lib()
+        self.num_envs = int(num_envs)
+        self.cfg = cfg or zm.TaskCfg()
+        self.robot = robot or zm.load_model()
+        self._m = zm.pack_model(self.robot)
+        self._c = self.cfg.pack()
+        idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        self.device = torch.device("cuda", idx)
+        h = C.c_void_p()
+        with torch.cuda.device(self.device):
+            nat.check(self.lib.zb_create(C.byref(self._m), C.byref(self._c), self.num_envs, idx, int(seed) & (2**64 - 1),
+                                         C.byref(h)), "zb_create")
+        self._h = h
+        # persistent outputs (reference: terminated/truncated buffers are mutated in place)
+        self.terminated = torch.zeros(self.num_envs, dtype=torch.bool, device=self.device)
+        self.truncated = torch.zeros(self.num_envs, dtype=torch.bool, device=self.device)
+        self._log_means = torch.zeros(zm.NUM_TERMS, dtype=torch.float32, device=self.device)
+        self._log_counts = torch.zeros(2, dtype=torch.int32, device=self.device)
+
+    # ------------------------------------------------------------------ lifecycle
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self.lib.zb_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ ops
+    def reset(self, env_ids: torch.Tensor | None = None) -> None:
+        if env_ids is None:
+            nat.check(self.lib.zb_reset(self._h, None, self.num_envs, _stream(self.device)), "zb_reset")
+            return
+        ids = env_ids.to(device=self.device, dtype=torch.int32).contiguous()
+        if ids.numel() == 0:
+            return
+        nat.check(self.lib.zb_reset(self._h, nat.ptr(ids), ids.numel(), _stream(self.device)), "zb_reset")
+
+    def step(self, actions: torch.Tensor):
+        a = actions.to(device=self.device, dtype=torch.float32).contiguous()
+        if a.shape != (self.num_envs, zm.ACT_DIM):
+            raise ValueError(f"actions must be [{self.num_envs}, {zm.ACT_DIM}], got {tuple(a.shape)}")
+        obs = torch.empty(self.num_envs, zm.OBS_DIM, dtype=torch.float32, device=self.device)
+        rew = torch.empty(self.num_envs, dtype=torch.float32, device=self.device)
+        nat.check(self.lib.zb_step(self._h, nat.ptr(a), nat.ptr(obs), nat.ptr(rew), nat.ptr(self.terminated),
+                                   nat.ptr(self.truncated), _stream(self.device)), "zb_step")
+        return obs, rew, self.terminated, self.truncated
+
+    def step_into(self, actions: torch.Tensor, obs: torch.Tensor, rew: torch.Tensor) -> None:
+        """Allocation-free variant for benchmarking / graph capture (caller-owned outputs)."""
+        nat.check(self.lib.zb_step(self._h, nat.ptr(actions), nat.ptr(obs), nat.ptr(rew), nat.ptr(self.terminated),
+                                   nat.ptr(self.truncated), _stream(self.device)), "zb_step")
+
+    def observe(self) -> torch.Tensor:
+        obs = torch.empty(self.num_envs, zm.OBS_DIM, dtype=torch.float32, device=self.device)
+        nat.check(self.lib.zb_observe(self._h, nat.ptr(obs), _stream(self.device)), "zb_observe")
+        return obs
+
+    def read_log(self):
+        """(term_means[13], counts[2]) device tensors of the most recent step that had resets."""
+        nat.check(self.lib.zb_read_log(self._h, nat.ptr(self._log_means), nat.ptr(self._log_counts),
+                                       _stream(self.device)), "zb_read_log")
+        return self._log_means, self._log_counts
+
+    def get_state(self) -> torch.Tensor:
+        st = torch.empty(zm.STATE_DIM, self.num_envs, dtype=torch.float32, device=self.device)
+        nat.check(self.lib.zb_get_state(self._h, nat.ptr(st), _stream(self.device)), "zb_get_state")
+        return st
+
+    def set_state(self, st: torch.Tensor) -> None:
+        s = st.to(device=self.device, dtype=torch.float32).contiguous()
+        if s.shape != (zm.STATE_DIM, self.num_envs):
+            raise ValueError(f"state must be [{zm.STATE_DIM}, {self.num_envs}]")
+        nat.check(self.lib.zb_set_state(self._h, nat.ptr(s), _stream(self.device)), "zb_set_state")
+        torch.cuda.current_stream(self.device).synchronize()  # `s` may be a temporary
+
+    def profile_begin(self, max_launches: int) -> None:
+        nat.check(self.lib.zb_profile_begin(self._h, int(max_launches)), "zb_profile_begin")
+
+    def profile_end(self):
+        """(summed zb_step_kernel milliseconds, launches timed)."""
+        ms, n = C.c_float(), C.c_int()
+        nat.check(self.lib.zb_profile_end(self._h, C.byref(ms), C.byref(n)), "zb_profile_end")
+        return float(ms.value), int(n.value)
+
+    def physics_substeps(self, targets: torch.Tensor, nsub: int):
+        t = targets.to(device=self.device, dtype=torch.float32).contiguous()
+        nf = torch.zeros(self.num_envs, zm.NUM_LINKS, 3, dtype=torch.float32, device=self.device)
+        tau = torch.zeros(self.num_envs, zm.NUM_DOF, dtype=torch.float32, device=self.device)
+        nat.check(self.lib.zb_physics_substeps(self._h, nat.ptr(t), int(nsub), nat.ptr(nf), nat.ptr(tau),
+                                               _stream(self.device)), "zb_physics_substeps")
+        return nf, tau

@@ -1,0 +1,60 @@
+"""Task registry: ``make("zbot-6b-walking-v2")`` like ``gym.make`` on the reference's registration
+(``source/zbot/zbot/tasks/zbot6b_direct/__init__.py:41-49``)."""
+from __future__ import annotations
+
+import importlib
+from dataclasses import dataclass, field
+
+
+@dataclass
+class EnvSpec:
+    id: str
+    entry_point: str
+    kwargs: dict = field(default_factory=dict)
+
+
+_REGISTRY: dict[str, EnvSpec] = {}
+
+
+def register(id: str, entry_point: str, kwargs: dict | None = None, disable_env_checker: bool = True) -> None:
+    _REGISTRY[id] = EnvSpec(id, entry_point, dict(kwargs or {}))
+
+
+def _load(ref):
+    if not isinstance(ref, str):
+        return ref
+    mod, name = ref.split(":")
+    return getattr(importlib.import_module(mod), name)
+
+
+def spec(id: str) -> EnvSpec:
+    if id not in _REGISTRY:
+        raise KeyError(f"unknown task {id!r}; registered: {sorted(_REGISTRY)}")
+    return _REGISTRY[id]
+
+
+def load_cfg(id: str, key: str = "env_cfg_entry_point"):
+    ref = spec(id).kwargs[key]
+    obj = _load(ref)
+    return obj() if isinstance(obj, type) else obj
+
+
+def make(id: str, cfg=None, render_mode=None, **kwargs):
+    s = spec(id)
+    env_cls = _load(s.entry_point)
+    cfg = cfg if cfg is not None else load_cfg(id)
+    return env_cls(cfg, render_mode=render_mode, **kwargs)
+
+
+def registered() -> list[str]:
+    return sorted(_REGISTRY)
+
+
+register(
+    id="zbot-6b-walking-v2",
+    entry_point="zbot_lab_amd.envs.walking_v2:ZbotDirectEnvV2",
+    kwargs={
+        "env_cfg_entry_point": "zbot_lab_amd.envs.walking_v2:ZbotDirectEnvCfgV2",
+        "rsl_rl_cfg_entry_point": "zbot_lab_amd.rl.cfg:PPORunnerCfgV2",
+    },
+)
