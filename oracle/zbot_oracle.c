@@ -47,6 +47,7 @@ typedef ZBO_REAL real;
 #define NV (6 + ND)  /* generalized velocity: [omega(3), v_P(3), qdot(6)] */
 #define NC_MAX ZB_MAX_CONTACTS /* contact slots per env per substep (= the HIP kernel) */
 #define NCAND_PER_LINK 4
+#define RIM_EPS 1e-3 /* m; = 2% of the 5 cm module radius */
 #define TWO_PI 6.283185307179586
 #define PI_R 3.14159265358979323846
 
@@ -328,10 +329,12 @@ static void detect(const mdl_t* m, const zb_task_cfg* cfg, const kin_t* k, real 
       m3_v(R, cd + 3, E1);
       m3_v(R, cd + 6, E2);
       for (int a = 0; a < 3; ++a) C[a] += k->p[b][a];
-      real al = -E1[2], be = -E2[2];
+      /* rim angle of the lowest point, biased by RIM_EPS toward E1 so that a (nearly) flat disk
+       * gets a fixed, body-attached 4-point manifold instead of a rounding-noise direction */
+      real al = -E1[2] + (real)RIM_EPS, be = -E2[2];
       real nrm = sqrtr(al * al + be * be);
       real cs = 1, sn = 0;
-      if (nrm > (real)1e-9) { cs = al / nrm; sn = be / nrm; }
+      if (nrm > (real)1e-12) { cs = al / nrm; sn = be / nrm; }
       for (int r = 0; r < 4; ++r) {
         real cr, sr;
         if (r == 0) { cr = cs; sr = sn; }
@@ -348,14 +351,10 @@ static void detect(const mdl_t* m, const zb_task_cfg* cfg, const kin_t* k, real 
         }
       }
     }
-    /* keep the NCAND_PER_LINK deepest (stable: earlier candidate wins ties) */
-    for (int s = 0; s < nc && s < NCAND_PER_LINK; ++s) {
-      int best = s;
-      for (int t = s + 1; t < nc; ++t)
-        if (cand[t].sep < cand[best].sep) best = t;
-      contact_t tmp = cand[s]; cand[s] = cand[best]; cand[best] = tmp;
-      clist_add(L, &cand[s]);
-    }
+    /* the first NCAND_PER_LINK valid candidates in the fixed order (circle 0: lowest, +90, +180,
+     * +270 degrees; then circle 1). A fixed order (not a depth sort) keeps the Gauss-Seidel row order
+     * independent of rounding when several rim points sit at the same depth (flat foot). */
+    for (int s = 0; s < nc && s < NCAND_PER_LINK; ++s) clist_add(L, &cand[s]);
   }
   if (!cfg->enable_self_collision) return;
   for (int p = 0; p < m->npairs; ++p) {

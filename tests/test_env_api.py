@@ -1,0 +1,117 @@
+"""Host-side API mirrors of the reference interfaces: registry, DirectRLEnv 5-tuple, rsl_rl VecEnv.
+
+CPU part: the wrapper / registry logic on a fake env. GPU part (marked): the real env."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+import zbot_lab_amd
+from zbot_lab_amd import model as zm
+from zbot_lab_amd.rl import PPORunnerCfgV2, RslRlVecEnvWrapper
+from zbot_lab_amd.tasks import load_cfg, spec
+
+
+class FakeEnv:
+    def __init__(self, n=4):
+        self.num_envs = n
+        self.device = torch.device("cpu")
+        self.max_episode_length = 1000
+        self.cfg = object()
+        from zbot_lab_amd import spaces
+        self.single_action_space = spaces.Box(-np.inf, np.inf, (6,))
+        self._ep = torch.zeros(n, dtype=torch.long)
+        self.last_action = None
+
+    @property
+    def unwrapped(self):
+        return self
+
+    @property
+    def episode_length_buf(self):
+        return self._ep
+
+    @episode_length_buf.setter
+    def episode_length_buf(self, v):
+        self._ep = v
+
+    def reset(self):
+        return {"policy": torch.zeros(self.num_envs, 23)}, {}
+
+    def get_observations(self):
+        return {"policy": torch.zeros(self.num_envs, 23)}
+
+    def step(self, a):
+        self.last_action = a
+        term = torch.tensor([True, False, False, False])
+        trunc = torch.tensor([False, True, False, False])
+        return {"policy": torch.ones(self.num_envs, 23)}, torch.ones(self.num_envs), term, trunc, {"log": {}}
+
+    def seed(self, s):
+        return s
+
+    def close(self):
+        pass
+
+
+def test_registry_matches_reference_registration():
+    assert "zbot-6b-walking-v2" in zbot_lab_amd.registered()
+    s = spec("zbot-6b-walking-v2")
+    assert s.entry_point.endswith("ZbotDirectEnvV2")
+    cfg = load_cfg("zbot-6b-walking-v2")
+    assert cfg.decimation == 4 and cfg.action_space == 6 and cfg.observation_space == 23
+    assert cfg.scene.num_envs == 4096 and cfg.scene.env_spacing == 4.0
+    assert abs(cfg.sim.dt - 1 / 200) < 1e-12 and cfg.termination_height == 0.22
+    assert list(cfg.reward_cfg["reward_scales"]) == zm.REWARD_TERMS
+    agent = load_cfg("zbot-6b-walking-v2", "rsl_rl_cfg_entry_point")
+    assert isinstance(agent, PPORunnerCfgV2)
+    d = agent.to_dict()
+    assert d["num_steps_per_env"] == 24 and d["policy"]["actor_hidden_dims"] == [128, 128, 128]
+    assert d["algorithm"]["desired_kl"] == 0.01 and d["algorithm"]["num_mini_batches"] == 4
+
+
+def test_vecenv_wrapper_contract():
+    env = FakeEnv()
+    w = RslRlVecEnvWrapper(env, clip_actions=1.0)
+    assert w.num_envs == 4 and w.num_actions == 6 and w.max_episode_length == 1000
+    obs, rew, dones, extras = w.step(torch.full((4, 6), 3.0))
+    assert torch.equal(dones, torch.tensor([1, 1, 0, 0]))
+    assert torch.equal(extras["time_outs"], torch.tensor([False, True, False, False]))
+    assert env.last_action.max() == 1.0           # clip_actions applied
+    w.episode_length_buf = torch.full((4,), 7)
+    assert (w.episode_length_buf == 7).all()
+    assert w.get_observations()["policy"].shape == (4, 23)
+
+
+def test_grid_env_origins():
+    from zbot_lab_amd.envs import grid_env_origins
+    o = grid_env_origins(16, 4.0)
+    assert o.shape == (16, 3)
+    d = torch.cdist(o, o) + torch.eye(16) * 100
+    assert abs(d.min().item() - 4.0) < 1e-6
+
+
+@pytest.mark.gpu
+def test_env_step_contract_gpu(gpu):
+    env = zbot_lab_amd.make("zbot-6b-walking-v2", num_envs=256)
+    obs, extras = env.reset()
+    assert obs["policy"].shape == (256, 23) and obs["policy"].device.type == "cuda"
+    ep = env.episode_length_buf
+    assert ep.dtype == torch.long and 0 <= ep.min() and ep.max() <= 999 and len(ep.unique()) > 100
+    term_buf = env.reset_terminated
+    for _ in range(50):
+        a = torch.randn(256, 6, device="cuda")
+        obs, rew, term, trunc, extras = env.step(a)
+    assert term is term_buf                              # persistent, mutated in place
+    assert rew.shape == (256,) and rew.dtype == torch.float32 and torch.isfinite(rew).all()
+    assert term.dtype == torch.bool and trunc.dtype == torch.bool
+    assert set(extras["log"]) >= {"Episode_Reward/step_length", "Episode_Termination/body_contact"}
+    assert torch.allclose(obs["policy"][:, 22], torch.ones(256, device="cuda"))
+    env.episode_length_buf = torch.full((256,), 998, device="cuda")
+    _, _, _, trunc, _ = env.step(torch.zeros(256, 6, device="cuda"))
+    assert trunc.all()                                   # 998 + 1 >= max_episode_length - 1
+    w = RslRlVecEnvWrapper(env)
+    o, r, d, ex = w.step(torch.zeros(256, 6, device="cuda"))
+    assert d.dtype == torch.long and "time_outs" in ex
+    env.close()

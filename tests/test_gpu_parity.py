@@ -78,9 +78,9 @@ def test_one_substep_parity(gpu, airborne):
     dv = np.abs(sg[vel] - so[vel]) - (2e-3 + 1e-3 * np.abs(so[vel]))
     ok = (dv <= 0).all(axis=0)
     assert ok.mean() >= 0.99, f"velocity parity in {ok.mean():.4f} of envs; worst {dv.max():.3e}"
-    pos = slice(S["ROOT_POS"], S["JOINT_POS"] + 6)
+    pos = np.r_[S["ROOT_POS"]:S["ROOT_POS"] + 7, S["JOINT_POS"]:S["JOINT_POS"] + 6]
     dp = np.abs(sg[pos] - so[pos])
-    okp = (dp <= 1e-5 + 1e-5 * np.abs(so[pos])).all(axis=0)
+    okp = (dp <= 2e-5 + 1e-5 * np.abs(so[pos])).all(axis=0)
     assert okp.mean() >= 0.99, f"position parity in {okp.mean():.4f} of envs; worst {dp.max():.3e}"
     # contact forces: same support (which links touch), magnitudes close
     fg = nf_g.cpu().numpy()

@@ -1,0 +1,159 @@
+"""Physical invariants of the oracle integrator (its algorithm is the HIP kernel's; PhysX itself is
+not available, so these pin the physics)."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from helpers import S, perturbed_states
+from zbot_lab_amd import model as zm
+
+
+def _sim(n, cfg=None, model_edit=None, double=False):
+    from oracle.pyoracle import OracleSim
+    s = OracleSim(n, cfg or zm.TaskCfg(), double=double)
+    if model_edit:
+        model_edit(s._m)
+        s.lib.zbo_destroy(s.h)
+        s.h = s.lib.zbo_create(C.byref(s._m), C.byref(s._c), n, 0)
+    return s
+
+
+def _airborne(n, seed=0, **kw):
+    st = perturbed_states(n, seed=seed, **kw)
+    st[S["ROOT_POS"] + 2] += 2.0
+    return st
+
+
+def test_free_fall():
+    n = 8
+    s = _sim(n)
+    st = _airborne(n, jqd_sigma=0.0, vel=0.0, tilt=0.0)
+    s.set_state(st)
+    tg = st[S["JOINT_POS"]:S["JOINT_POS"] + 6].T.copy()
+    k = 20
+    s.physics_substeps(tg, k)
+    out = s.get_state()
+    dt, g = 0.005, 9.81
+    np.testing.assert_allclose(out[S["ROOT_LINVEL"] + 2], -g * dt * k, rtol=1e-4)
+    np.testing.assert_allclose(out[S["ROOT_POS"] + 2] - st[S["ROOT_POS"] + 2], -g * dt * dt * k * (k + 1) / 2, rtol=1e-4)
+    np.testing.assert_allclose(out[S["JOINT_VEL"]:S["JOINT_VEL"] + 6], 0, atol=1e-4)
+
+
+def test_momentum_first_order_without_gravity_and_contact():
+    """Free-floating chain, drives active (internal forces only): spatial momentum is conserved up
+    to the first-order error of semi-implicit Euler in generalised coordinates (M(q) changes
+    within the step) - the drift must halve when dt halves and stay < 5 % of |p| over 0.1 s (strong drive transients)."""
+    drift = []
+    for dt in (0.005, 0.0025):
+        n = 8
+        s = _sim(n, zm.TaskCfg(gravity=0.0, sim_dt=dt), double=True)
+        st = _airborne(n, seed=3, jqd_sigma=2.0, vel=0.5)
+        s.set_state(st)
+        em0 = s.energy_momentum()
+        tg = st[S["JOINT_POS"]:S["JOINT_POS"] + 6].T.copy()
+        s.physics_substeps(tg, int(round(0.1 / dt)))
+        em1 = s.energy_momentum()
+        drift.append((np.abs(em1[:, 1:4] - em0[:, 1:4]).max(), np.abs(em1[:, 4:7] - em0[:, 4:7]).max(),
+                      np.abs(em0[:, 1:4]).max()))
+    (p1, l1, pn), (p2, l2, _) = drift
+    assert p1 < 0.05 * pn
+    assert 1.6 < p1 / p2 < 2.4 and 1.6 < l1 / l2 < 2.4, drift
+
+
+def test_energy_without_drives_gravity_contact():
+    """No drives, gravity or contact (self collision off: it is inelastic, e = 0): kinetic energy
+    drifts only at first order in dt (< 3 % over 0.5 s at dt = 5 ms, halving with dt)."""
+    def no_drive(m):
+        m.kp = 0.0
+        m.kd = 0.0
+    errs = []
+    for dt in (0.005, 0.0025):
+        n = 16
+        s = _sim(n, zm.TaskCfg(gravity=0.0, sim_dt=dt, enable_self_collision=False), model_edit=no_drive,
+                 double=True)
+        st = _airborne(n, seed=5, jqd_sigma=1.0, vel=0.2)
+        s.set_state(st)
+        e0 = s.energy_momentum()[:, 0]
+        s.physics_substeps(st[S["JOINT_POS"]:S["JOINT_POS"] + 6].T.copy(), int(round(0.5 / dt)))
+        errs.append(np.abs(s.energy_momentum()[:, 0] / e0 - 1).max())
+    assert errs[0] < 0.03 and 1.6 < errs[0] / errs[1] < 2.4, errs
+
+
+def test_pd_step_response():
+    n = 4
+    s = _sim(n, zm.TaskCfg(gravity=0.0))
+    st = _airborne(n, seed=7, jq_sigma=0.0, jqd_sigma=0.0, vel=0.0, tilt=0.0)
+    s.set_state(st)
+    tg = st[S["JOINT_POS"]:S["JOINT_POS"] + 6].T.copy()
+    tg[:, 2] += 0.2
+    s.physics_substeps(tg, 200)   # 1 s
+    out = s.get_state()
+    q = out[S["JOINT_POS"] + 2]
+    np.testing.assert_allclose(q, tg[:, 2], atol=0.01)
+    assert np.abs(out[S["JOINT_VEL"]:S["JOINT_VEL"] + 6]).max() < 0.05
+
+
+def test_standing_at_default_pose_is_stable():
+    n = 8
+    s = _sim(n)
+    s.reset()
+    st = s.get_state()
+    st[S["EP_LEN"]] = 0
+    s.set_state(st)
+    for _ in range(250):  # 5 s of zero actions
+        _, r, term, trunc = s.step(np.zeros((n, 6), np.float32))
+        assert not term.any()
+    p, _ = s.link_poses()
+    np.testing.assert_allclose(p[:, 6, 2], 0.2545, atol=2e-3)
+    out = s.get_state()
+    assert np.abs(out[S["JOINT_VEL"]:S["JOINT_VEL"] + 6]).max() < 0.1
+    # both feet carry the weight: contact-sensor F_z history sums to ~m g
+    fz = out[S["FEET_FZ_HIST"]:S["FEET_FZ_HIST"] + 2]
+    np.testing.assert_allclose(fz.sum(axis=0), 3.005 * 9.81, rtol=0.05)
+
+
+def test_joint_wrap():
+    def no_drive(m):
+        m.kp = 0.0
+        m.kd = 0.0
+    n = 2
+    s = _sim(n, zm.TaskCfg(gravity=0.0), model_edit=no_drive)
+    st = _airborne(n, jq_sigma=0.0, jqd_sigma=0.0, vel=0.0)
+    st[S["JOINT_POS"] + 3] = 6.27
+    st[S["JOINT_VEL"] + 3] = 15.0
+    s.set_state(st)
+    tg = st[S["JOINT_POS"]:S["JOINT_POS"] + 6].T.copy()
+    tg[:, 3] = 6.27
+    s.physics_substeps(tg, 1)
+    q = s.get_state()[S["JOINT_POS"] + 3]
+    assert (q < 0).all() and (q > -2 * np.pi).all()    # crossed +2pi -> wrapped by 4pi
+
+
+def test_velocity_limit():
+    n = 2
+    s = _sim(n, zm.TaskCfg(gravity=0.0))
+    st = _airborne(n, jq_sigma=0.0, jqd_sigma=0.0, vel=0.0)
+    s.set_state(st)
+    tg = st[S["JOINT_POS"]:S["JOINT_POS"] + 6].T.copy()
+    tg[:, 5] += 3.0   # saturating step on the distal joint
+    s.physics_substeps(tg, 3)
+    assert np.abs(s.get_state()[S["JOINT_VEL"]:S["JOINT_VEL"] + 6]).max() <= 20.0 + 1e-4
+
+
+def test_random_rollout_sane():
+    from oracle.pyoracle import OracleSim
+    n = 64
+    s = OracleSim(n, seed=3)
+    s.reset()
+    rng = np.random.default_rng(0)
+    died = 0
+    for _ in range(200):
+        obs, r, te, tr = s.step(rng.normal(size=(n, 6)).astype(np.float32))
+        assert np.isfinite(obs).all() and np.isfinite(r).all()
+        died += te.sum()
+    st = s.get_state()
+    assert np.isfinite(st).all()
+    assert 0 < died < n * 200 * 0.2

@@ -36,6 +36,7 @@ constexpr int NCM = ZB_MAX_CONTACTS;
 constexpr int WAVE = 64;
 constexpr float PI_F = 3.14159265358979323846f;
 constexpr float TWO_PI_F = 6.28318530717958647692f;
+constexpr float RIM_EPS = 1e-3f;  // m; 2% of the module radius (see detect)
 
 // LDS contact slot layout (floats), [slot][field][lane]
 constexpr int SLOT = 48;
@@ -365,10 +366,11 @@ __device__ __forceinline__ int detect(MP m, const zb_task_cfg& cfg, const Kin& k
       mv3(R, cd + 3, E1);
       mv3(R, cd + 6, E2);
       C[0] += k.p[b][0]; C[1] += k.p[b][1]; C[2] += k.p[b][2];
-      const float al = -E1[2], be = -E2[2];
+      // lowest rim point, biased toward E1 so a flat disk gets a fixed body-attached manifold
+      const float al = -E1[2] + RIM_EPS, be = -E2[2];
       const float nrm = sqrtf(al * al + be * be);
       float c0 = 1.f, s0 = 0.f;
-      if (nrm > 1e-9f) { c0 = al / nrm; s0 = be / nrm; }
+      if (nrm > 1e-12f) { c0 = al / nrm; s0 = be / nrm; }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float cr = r == 0 ? c0 : (r == 1 ? -s0 : (r == 2 ? -c0 : s0));
@@ -379,24 +381,14 @@ __device__ __forceinline__ int detect(MP m, const zb_task_cfg& cfg, const Kin& k
         cs[idx] = Pz + cx[idx][2];
       }
     }
-    // stable selection of the 4 deepest valid candidates (ties: lowest index)
-    unsigned used = 0;
+    // the first 4 valid candidates in fixed order (rounding-independent Gauss-Seidel row order)
+    int taken = 0;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      int best = -1;
-      float bs = 0.f;
-#pragma unroll
-      for (int t = 0; t < 8; ++t) {
-        const bool ok = cs[t] < margin && !((used >> t) & 1u);
-        if (ok && (best < 0 || cs[t] < bs)) { best = t; bs = cs[t]; }
+    for (int t = 0; t < 8; ++t) {
+      if (cs[t] < margin && taken < 4) {
+        contact_add(ld, nc, cx[t], up, cs[t], l, -1);
+        ++taken;
       }
-      if (best < 0) break;
-      used |= 1u << best;
-      float x[3] = {0.f, 0.f, 0.f};
-#pragma unroll
-      for (int t = 0; t < 8; ++t)
-        if (t == best) { x[0] = cx[t][0]; x[1] = cx[t][1]; x[2] = cx[t][2]; }
-      contact_add(ld, nc, x, up, bs, l, -1);
     }
   }
   if (!cfg.enable_self_collision) return nc;
