@@ -12,6 +12,8 @@ Bar: fp32 on both sides, different operation order / FMA contrac
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import pytest
 
@@ -178,10 +180,19 @@ def test_rollout_statistics(gpu):
     o.reset(None)
     rng = np.random.default_rng(42)
     rg, ro, dg, do = [], [], [], []
-    for _ in range(steps):
+    for k in range(steps):
         a = rng.normal(size=(n, 6)).astype(np.float32)
+        prev = g.get_state()
         _, r1, t1, _ = g.step(torch.from_numpy(a).cuda())
         _, r2, t2, _ = o.step(a)
+        if not torch.isfinite(r1).all():
+            bad = torch.nonzero(~torch.isfinite(r1)).flatten().cpu().numpy()
+            st = prev.cpu().numpy()
+            dump = os.environ.get("ZB_NAN_DUMP")
+            if dump:
+                np.savez(dump, state=st, actions=a, envs=bad, step=k)
+            raise AssertionError(f"non-finite GPU reward at step {k}, envs {bad[:8]}, "
+                                 f"pre-step state of env {bad[0]}: {np.array2string(st[:, bad[0]], precision=4)}")
         rg.append(r1.mean().item())
         ro.append(r2.mean())
         dg.append(t1.float().mean().item())
