@@ -37,7 +37,30 @@ def parse():
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--action-pool", type=int, default=64, help="distinct pre-drawn randn action batches cycled")
+    # ablation knobs (the reported line uses the defaults)
+    p.add_argument("--solver-iterations", type=int, default=None)
+    p.add_argument("--no-self-collision", action="store_true")
     return p.parse_args()
+
+
+def pmc_traffic(num_envs: int):
+    """HBM bytes per zb_step_kernel launch from the committed rocprofv3 PMC passes (separate
+    FETCH_SIZE / WRITE_SIZE runs, profiles/<round>/pmc_*_zb_step_kernel.csv) for the same grid.
+    FETCH_SIZE/WRITE_SIZE are KiB; our accesses are 4-B-per-lane (uncalibrated width per the
+    microarch guide, so no 2x read correction is applied). Returns (bytes, source) or (None, None)."""
+    import csv
+    import glob
+    here = os.path.dirname(os.path.abspath(__file__))
+    for d in sorted(glob.glob(os.path.join(here, "profiles", "r*")), reverse=True):
+        vals = {}
+        for name in ("FETCH_SIZE", "WRITE_SIZE"):
+            for f in glob.glob(os.path.join(d, "pmc_*_zb_step_kernel.csv")):
+                for row in csv.DictReader(open(f)):
+                    if row["counter"] == name and int(row["grid"]) == num_envs:
+                        vals[name] = float(row["mean_per_dispatch"]) * 1024.0
+        if len(vals) == 2:
+            return vals["FETCH_SIZE"] + vals["WRITE_SIZE"], os.path.relpath(d, here)
+    return None, None
 
 
 def cpu_baseline(num_envs: int, seconds: float) -> dict:
@@ -79,6 +102,10 @@ def main():
     cfg.scene.num_envs = args.envs_per_gpu
     cfg.sim.device = str(dev)
     cfg.seed = 42 + rank
+    if args.solver_iterations is not None:
+        cfg.solver.iterations = args.solver_iterations
+    if args.no_self_collision:
+        cfg.solver.self_collision = False
     env = ZbotDirectEnvV2(cfg)
     n = env.num_envs
     env.reset()
@@ -113,6 +140,7 @@ def main():
 
     if rank == 0:
         kern_s = kern_ms / 1e3 / max(kern_n, 1)
+        traffic, traffic_src = pmc_traffic(n)
         achieved = n * BYTES_PER_ENV_STEP / kern_s / 1e9
         out = {
             "metric": "env-steps/sec at 4096/65536 envs, 1->8 GPUs; % HBM roofline",
@@ -131,7 +159,7 @@ def main():
                        "envs_per_gpu": n, "total_envs": n * world, "decimation": 4, "sim_dt": 0.005,
                        "parallelism": f"env-sharded x{world} (replicas, no collective)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "zb_step_kernel", "kernel_ms": kern_s * 1e3,
                          "bytes_per_env_step": BYTES_PER_ENV_STEP},
             "cpu_baseline": None,
