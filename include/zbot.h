@@ -170,6 +170,11 @@ int zb_physics_substeps(zb_handle h, const float* targets, int nsub, float* net_
 int zb_profile_begin(zb_handle h, int max_launches);
 int zb_profile_end(zb_handle h, float* total_ms, int* count);
 
+/* Diagnostic builds only (compiled with -DZB_STAMPS): per-phase s_memtime cycle sums of
+ * zb_step_kernel over all waves since the previous call (phases: DESIGN.md §7). Returns <0 in
+ * the product build. */
+int zb_read_stamps(uint64_t* out16);
+
 #ifdef __cplusplus
 }
 #endif

@@ -13,7 +13,7 @@ import os
 from . import model as zm
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libzbot.so")
+LIB_PATH = os.path.join(HERE, os.environ.get("ZBOT_LIB", "libzbot.so"))
 
 
 class ZbotError(RuntimeError):
@@ -46,6 +46,8 @@ def lib():
     L.zb_physics_substeps.argtypes = [P, P, C.c_int, P, P, P]
     L.zb_profile_begin.argtypes = [P, C.c_int]
     L.zb_profile_end.argtypes = [P, C.POINTER(C.c_float), C.POINTER(C.c_int)]
+    L.zb_read_stamps.argtypes = [P]
+    L.zb_read_stamps.restype = C.c_int
     for name in ("zb_create", "zb_num_envs", "zb_reset", "zb_step", "zb_observe", "zb_read_log", "zb_get_state",
                  "zb_set_state", "zb_physics_substeps", "zb_profile_begin", "zb_profile_end"):
         getattr(L, name).restype = C.c_int
@@ -55,7 +57,7 @@ def lib():
 
 EXPORTED = ["zb_create", "zb_destroy", "zb_last_error", "zb_num_envs", "zb_reset", "zb_step", "zb_observe",
             "zb_read_log", "zb_get_state", "zb_set_state", "zb_physics_substeps", "zb_profile_begin",
-            "zb_profile_end"]
+            "zb_profile_end", "zb_read_stamps"]
 
 
 def check(rc: int, what: str) -> None:

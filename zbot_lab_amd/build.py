@@ -20,18 +20,24 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found")
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
+STAMPS_OUT = os.path.join(HERE, "libzbot_stamps.so")
+
+
+def build(force: bool = False, verbose: bool = False, stamps: bool = False) -> str:
+    out = STAMPS_OUT if stamps else OUT
     deps = [SRC, os.path.join(ROOT, "include", "zbot.h")]
-    if not force and os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in deps):
-        return OUT
+    if not force and os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(d) for d in deps):
+        return out
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-I", os.path.join(ROOT, "include"), "-o", OUT + ".tmp", SRC]
+           "-I", os.path.join(ROOT, "include"), "-o", out + ".tmp", SRC]
+    if stamps:
+        cmd.insert(1, "-DZB_STAMPS")
     if verbose:
         cmd.insert(1, "-Rpass-analysis=kernel-resource-usage")
     subprocess.run(cmd, check=True)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose="-v" in sys.argv))
+    print(build(force="--force" in sys.argv, verbose="-v" in sys.argv, stamps="--stamps" in sys.argv))

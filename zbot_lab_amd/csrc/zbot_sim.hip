@@ -38,16 +38,14 @@ constexpr float PI_F = 3.14159265358979323846f;
 constexpr float TWO_PI_F = 6.28318530717958647692f;
 constexpr float RIM_EPS = 1e-3f;  // m; 2% of the module radius (see detect)
 
-// LDS contact slot layout (floats), [slot][field][lane]
-constexpr int SLOT = 48;
-constexpr int SL_Y = 0;      // 3 rows x 12 whitened coords
-constexpr int SL_INVM = 36;  // 3
-constexpr int SL_VMIN = 39;  // 1 (holds sep during detection)
-constexpr int SL_LAM = 40;   // 3
-constexpr int SL_N = 43;     // 3 normal
-constexpr int SL_LA = 46;    // link a (float)
-constexpr int SL_LB = 47;    // link b (float, -1 ground)
-constexpr int LDS_FLOATS = NCM * SLOT * WAVE;
+// LDS contact slot layout: 12 float4 granules per slot, [slot][granule][lane] (16 B per lane), so
+// every access is one conflict-free ds_read_b128 / ds_write_b128 per wave (1 KiB contiguous).
+//   g0..g2  Y row 0 (normal)   g3..g5 Y row 1 (tangent 1)   g6..g8 Y row 2 (tangent 2)
+//   g9  {invm0, invm1, invm2, vmin}   g10 {lam0, lam1, lam2, la}   g11 {n.x, n.y, n.z, lb}
+// During detection g0 holds {x.x, x.y, x.z, sep}.
+constexpr int SLOT4 = 12;
+constexpr int G_INVM = 9, G_LAM = 10, G_N = 11;
+constexpr int LDS_FLOATS = NCM * SLOT4 * 4 * WAVE;
 
 // The ZBOT-6 chain topology is compiled in (zb_create checks the model against it):
 // link l belongs to composite body (l+1)/2; joint j connects body j -> j+1.
@@ -65,9 +63,39 @@ __device__ __forceinline__ void ldc(float (&d)[N], CF* s) {
 __device__ __forceinline__ MP to_mp(const zb_model* m) { return (MP)(uintptr_t)m; }
 
 struct Lane {
-  float* p;  // lds + lane
-  __device__ __forceinline__ float& at(int slot, int f) const { return p[(slot * SLOT + f) * WAVE]; }
+  float4* p;  // (float4*)lds + lane
+  __device__ __forceinline__ float4& g(int slot, int q) const { return p[(slot * SLOT4 + q) * WAVE]; }
 };
+
+// ------------------------------------------------------------------------- diagnostic stamps
+// Built only with -DZB_STAMPS (python -m zbot_lab_amd.build --stamps): s_memtime deltas per phase,
+// summed per wave (lane 0) into g_stamps. Never part of the measured product build.
+constexpr int NSTAMP = 10;
+#ifdef ZB_STAMPS
+__device__ unsigned long long g_stamps[NSTAMP];
+struct Stamps {
+  unsigned long long t, acc[NSTAMP];
+  __device__ void begin() {
+    t = __builtin_amdgcn_s_memtime();
+    for (int k = 0; k < NSTAMP; ++k) acc[k] = 0;
+  }
+  __device__ void mark(int k) {
+    const unsigned long long n = __builtin_amdgcn_s_memtime();
+    acc[k] += n - t;
+    t = n;
+  }
+  __device__ void flush() {
+    if ((threadIdx.x & 63) == 0)
+      for (int k = 0; k < NSTAMP; ++k) atomicAdd(&g_stamps[k], acc[k]);
+  }
+};
+#else
+struct Stamps {
+  __device__ void begin() {}
+  __device__ void mark(int) {}
+  __device__ void flush() {}
+};
+#endif
 
 // ------------------------------------------------------------------------- math
 __device__ __forceinline__ void cross3(const float a[3], const float b[3], float o[3]) {
@@ -216,8 +244,8 @@ __device__ __forceinline__ void body_si(MP m, const Kin& k, int b, SI& o) {
 constexpr int tri(int r, int c) { return r * (r + 1) / 2 + c; }  // r >= c
 constexpr int NT = NV * (NV + 1) / 2;
 
-// in place: A (lower triangle) -> L with L L^T = A
-__device__ __forceinline__ void cholesky_inplace(float A[NT]) {
+// in place: A (lower triangle) -> L with L L^T = A; inv[j] = 1 / L_jj
+__device__ __forceinline__ void cholesky_inplace(float A[NT], float inv[NV]) {
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
     float s = A[tri(j, j)];
@@ -225,20 +253,21 @@ __device__ __forceinline__ void cholesky_inplace(float A[NT]) {
     for (int k = 0; k < j; ++k) s -= A[tri(j, k)] * A[tri(j, k)];
     const float d = sqrtf(fmaxf(s, 1e-12f));
     A[tri(j, j)] = d;
-    const float inv = 1.f / d;
+    const float iv = 1.f / d;
+    inv[j] = iv;
 #pragma unroll
     for (int i = j + 1; i < NV; ++i) {
       float t = A[tri(i, j)];
 #pragma unroll
       for (int k = 0; k < j; ++k) t -= A[tri(i, k)] * A[tri(j, k)];
-      A[tri(i, j)] = t * inv;
+      A[tri(i, j)] = t * iv;
     }
   }
 }
 // rank-1 downdate L L^T - a e_J e_J^T (removes the drive armature of a saturated joint);
 // mathematically identical to re-factoring, as the oracle does.
 template <int J>
-__device__ __forceinline__ void chol_downdate(float L[NT], float a) {
+__device__ __forceinline__ void chol_downdate(float L[NT], float inv[NV], float a) {
   float x[NV];
 #pragma unroll
   for (int i = J; i < NV; ++i) x[i] = 0.f;
@@ -247,8 +276,9 @@ __device__ __forceinline__ void chol_downdate(float L[NT], float a) {
   for (int k = J; k < NV; ++k) {
     const float lkk = L[tri(k, k)];
     const float r = sqrtf(fmaxf(lkk * lkk - x[k] * x[k], 1e-12f));
-    const float c = r / lkk, sn = x[k] / lkk;
+    const float c = r * inv[k], sn = x[k] * inv[k];
     L[tri(k, k)] = r;
+    inv[k] = 1.f / r;
     const float ic = 1.f / c;
 #pragma unroll
     for (int i = k + 1; i < NV; ++i) {
@@ -258,22 +288,22 @@ __device__ __forceinline__ void chol_downdate(float L[NT], float a) {
     }
   }
 }
-__device__ __forceinline__ void fwd_sub(const float L[NT], const float b[NV], float y[NV]) {
+__device__ __forceinline__ void fwd_sub(const float L[NT], const float inv[NV], const float b[NV], float y[NV]) {
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     float t = b[i];
 #pragma unroll
     for (int k = 0; k < i; ++k) t -= L[tri(i, k)] * y[k];
-    y[i] = t / L[tri(i, i)];
+    y[i] = t * inv[i];
   }
 }
-__device__ __forceinline__ void bwd_sub(const float L[NT], const float y[NV], float x[NV]) {
+__device__ __forceinline__ void bwd_sub(const float L[NT], const float inv[NV], const float y[NV], float x[NV]) {
 #pragma unroll
   for (int i = NV - 1; i >= 0; --i) {
     float t = y[i];
 #pragma unroll
     for (int k = i + 1; k < NV; ++k) t -= L[tri(k, i)] * x[k];
-    x[i] = t / L[tri(i, i)];
+    x[i] = t * inv[i];
   }
 }
 __device__ __forceinline__ void lt_mul(const float L[NT], const float u[NV], float w[NV]) {
@@ -284,6 +314,13 @@ __device__ __forceinline__ void lt_mul(const float L[NT], const float u[NV], flo
     for (int k = i; k < NV; ++k) t += L[tri(k, i)] * u[k];
     w[i] = t;
   }
+}
+// 12-term dot with a 4-way split accumulation (shorter dependency chain than a serial sum)
+__device__ __forceinline__ float dot12(const float a[NV], const float b[NV]) {
+  float s0 = a[0] * b[0], s1 = a[1] * b[1], s2 = a[2] * b[2], s3 = a[3] * b[3];
+  s0 += a[4] * b[4]; s1 += a[5] * b[5]; s2 += a[6] * b[6]; s3 += a[7] * b[7];
+  s0 += a[8] * b[8]; s1 += a[9] * b[9]; s2 += a[10] * b[10]; s3 += a[11] * b[11];
+  return (s0 + s1) + (s2 + s3);
 }
 
 // Model constants are wave-uniform and re-loaded (scalar loads) where used; routing the pointer
@@ -296,46 +333,57 @@ __device__ __forceinline__ MP opaque(MP m) {
 }
 
 // ------------------------------------------------------------------------- contacts
-__device__ __forceinline__ void contact_add(const Lane& ld, int& nc, const float x[3], const float n[3], float sep,
-                                            int la, int lb) {
-  int slot;
-  if (nc < NCM) {
-    slot = nc++;
-  } else {
-    int worst = 0;
-    float wsep = ld.at(0, SL_VMIN);
-    for (int c = 1; c < NCM; ++c) {
-      const float s = ld.at(c, SL_VMIN);
-      if (s > wsep) { wsep = s; worst = c; }
-    }
-    if (!(sep < wsep)) return;
-    slot = worst;
+// Detection writes a RAW candidate list (ground: <= 4 per link in fixed order, then self pairs),
+// capped at NRAW, into granules 1..8 of the slots (2 granules per entry: {x, sep}, {n, code}
+// with code = 16*la + (lb+1)). One compact pass then inserts them in order into the NCM solver
+// slots, replacing the shallowest when full (= oracle clist_add over the same list). Keeping the
+// insertion out of the unrolled detection code keeps the kernel small enough for the I-cache.
+constexpr int NRAW = 48;
+__device__ __forceinline__ float4& raw(const Lane& ld, int e, int h) {  // e < NRAW, h in {0, 1}
+  const int gi = 2 * e + h;                                             // 96 granules = 12 slots x 8
+  return ld.g(gi >> 3, 1 + (gi & 7));
+}
+__device__ __forceinline__ void raw_push(const Lane& ld, int& nraw, const float x[3], float sep, const float n[3],
+                                         int la, int lb) {
+  if (nraw < NRAW) {
+    raw(ld, nraw, 0) = make_float4(x[0], x[1], x[2], sep);
+    raw(ld, nraw, 1) = make_float4(n[0], n[1], n[2], (float)(16 * la + lb + 1));
+    ++nraw;
   }
-  ld.at(slot, SL_Y + 0) = x[0];
-  ld.at(slot, SL_Y + 1) = x[1];
-  ld.at(slot, SL_Y + 2) = x[2];
-  ld.at(slot, SL_N + 0) = n[0];
-  ld.at(slot, SL_N + 1) = n[1];
-  ld.at(slot, SL_N + 2) = n[2];
-  ld.at(slot, SL_VMIN) = sep;
-  ld.at(slot, SL_LA) = (float)la;
-  ld.at(slot, SL_LB) = (float)lb;
 }
-
-// Staging area for world sphere/bound centres during detection: fields 3..35 of the contact
-// slots' Y block, which detection never writes (contact x lives in fields 0..2).
-constexpr int STAGE_PER_SLOT = 33;
-__device__ __forceinline__ float& stage(const Lane& ld, int idx) {
-  return ld.at(idx / STAGE_PER_SLOT, 3 + idx % STAGE_PER_SLOT);
-}
-constexpr int STG_SPH = 0;    // [link][sphere][xyz] 72
-constexpr int STG_BND = 72;   // [link][xyz] 36
-
-// Ground: the 4 rim points of each of the link's two circles (lowest + 90-degree rotations),
-// the 4 deepest below the margin per link; then sphere pairs for self collision.
-__device__ __forceinline__ int detect(MP m, const zb_task_cfg& cfg, const Kin& k, float Pz,
-                                      const Lane& ld) {
+// sequential insertion of the raw list into the solver slots (g0 {x, sep}, g10.w la, g11 {n, lb})
+__device__ __forceinline__ int insert_raw(const Lane& ld, int nraw) {
   int nc = 0;
+  for (int e = 0; e < nraw; ++e) {
+    const float4 r0 = raw(ld, e, 0), r1 = raw(ld, e, 1);
+    int slot = nc;
+    if (nc < NCM) {
+      ++nc;
+    } else {
+      int worst = 0;
+      float wsep = ld.g(0, 0).w;
+      for (int c = 1; c < NCM; ++c) {
+        const float s = ld.g(c, 0).w;
+        if (s > wsep) { wsep = s; worst = c; }
+      }
+      if (!(r0.w < wsep)) continue;
+      slot = worst;
+    }
+    const int code = (int)r1.w;
+    ld.g(slot, 0) = r0;
+    ld.g(slot, G_LAM) = make_float4(0.f, 0.f, 0.f, (float)(code >> 4));
+    ld.g(slot, G_N) = make_float4(r1.x, r1.y, r1.z, (float)((code & 15) - 1));
+  }
+  return nc;
+}
+
+// Ground: the 4 rim points of each of the link's two circles (lowest + 90-degree rotations), the
+// first 4 within the margin per link. Self: inscribed sphere pairs of non-adjacent links behind a
+// sphere-union broadphase (centre = midpoint of a link's two spheres, radius r + half their
+// distance: conservative, so it changes which pairs are tested, never which contacts are found).
+__device__ __forceinline__ int detect(MP m, const zb_task_cfg& cfg, const Kin& k, float Pz,
+                                      const Lane& ld, Stamps& sp) {
+  int nraw = 0;
   const float margin = cfg.contact_margin;
   const float up[3] = {0.f, 0.f, 1.f};
 #pragma unroll
@@ -345,16 +393,6 @@ __device__ __forceinline__ int detect(MP m, const zb_task_cfg& cfg, const Kin& k
     float bc[3], lb4[4];
     ldc(lb4, m->link_bound[l]);
     mv3(R, lb4, bc);
-#pragma unroll
-    for (int a = 0; a < 3; ++a) stage(ld, STG_BND + 3 * l + a) = bc[a] + k.p[b][a];
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      float sc[3], sp[3];
-      ldc(sp, m->link_sphere[l][s2]);
-      mv3(R, sp, sc);
-#pragma unroll
-      for (int a = 0; a < 3; ++a) stage(ld, STG_SPH + 6 * l + 3 * s2 + a) = sc[a] + k.p[b][a];
-    }
     if (Pz + k.p[b][2] + bc[2] - lb4[3] > margin) continue;
     float cx[8][3], cs[8];
 #pragma unroll
@@ -381,51 +419,93 @@ __device__ __forceinline__ int detect(MP m, const zb_task_cfg& cfg, const Kin& k
         cs[idx] = Pz + cx[idx][2];
       }
     }
-    // the first 4 valid candidates in fixed order (rounding-independent Gauss-Seidel row order)
     int taken = 0;
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
       if (cs[t] < margin && taken < 4) {
-        contact_add(ld, nc, cx[t], up, cs[t], l, -1);
+        raw_push(ld, nraw, cx[t], cs[t], up, l, -1);
         ++taken;
       }
     }
   }
-  if (!cfg.enable_self_collision) return nc;
-  for (int la = 0; la < NL; ++la) {
-    for (int lb = la + 2; lb < NL; ++lb) {  // consecutive links are joint-connected (filtered)
-      const float d0 = stage(ld, STG_BND + 3 * la) - stage(ld, STG_BND + 3 * lb);
-      const float d1 = stage(ld, STG_BND + 3 * la + 1) - stage(ld, STG_BND + 3 * lb + 1);
-      const float d2 = stage(ld, STG_BND + 3 * la + 2) - stage(ld, STG_BND + 3 * lb + 2);
-      const float rr = m->link_bound[la][3] + m->link_bound[lb][3] + margin;
-      if (d0 * d0 + d1 * d1 + d2 * d2 > rr * rr) continue;
+  sp.mark(1);
+  if (cfg.enable_self_collision) {
+    m = opaque(m);
+    float ub[NL][3], ur[NL];
+    unsigned long long mask = 0ull;
 #pragma unroll
+    for (int l = 0; l < NL; ++l) {
+      float s0[4], s1[4];
+      ldc(s0, m->link_sphere[l][0]);
+      ldc(s1, m->link_sphere[l][1]);
+      const float mid[3] = {0.5f * (s0[0] + s1[0]), 0.5f * (s0[1] + s1[1]), 0.5f * (s0[2] + s1[2])};
+      const float hd = 0.5f * sqrtf((s0[0] - s1[0]) * (s0[0] - s1[0]) + (s0[1] - s1[1]) * (s0[1] - s1[1]) +
+                                    (s0[2] - s1[2]) * (s0[2] - s1[2]));
+      ur[l] = fmaxf(s0[3], s1[3]) + hd;
+      const int b = link_body(l);
+      mv3(k.R[b], mid, ub[l]);
+      ub[l][0] += k.p[b][0]; ub[l][1] += k.p[b][1]; ub[l][2] += k.p[b][2];
+    }
+    {
+      int pidx = 0;
+#pragma unroll
+      for (int la = 0; la < NL; ++la)
+#pragma unroll
+        for (int lb = la + 2; lb < NL; ++lb, ++pidx) {
+          const float d0 = ub[la][0] - ub[lb][0], d1 = ub[la][1] - ub[lb][1], d2 = ub[la][2] - ub[lb][2];
+          const float rr = ur[la] + ur[lb] + margin;
+          if (d0 * d0 + d1 * d1 + d2 * d2 <= rr * rr) mask |= 1ull << pidx;
+        }
+    }
+    // narrow phase over the (rare) candidate pairs, one code copy
+    while (mask) {
+      const int pidx = __builtin_ctzll(mask);
+      mask &= mask - 1ull;
+      int la = 0, rem = pidx;
+      while (rem >= NL - 2 - la) { rem -= NL - 2 - la; ++la; }
+      const int lb = la + 2 + rem;
+      float Ra[9], pa[3], Rb[9], pb[3];
+      // body frames of the two links, selected without dynamic register indexing
+#pragma unroll
+      for (int bb = 0; bb < NB; ++bb) {
+        if (bb == link_body(la)) {
+#pragma unroll
+          for (int q = 0; q < 9; ++q) Ra[q] = k.R[bb][q];
+          pa[0] = k.p[bb][0]; pa[1] = k.p[bb][1]; pa[2] = k.p[bb][2];
+        }
+        if (bb == link_body(lb)) {
+#pragma unroll
+          for (int q = 0; q < 9; ++q) Rb[q] = k.R[bb][q];
+          pb[0] = k.p[bb][0]; pb[1] = k.p[bb][1]; pb[2] = k.p[bb][2];
+        }
+      }
       for (int sa = 0; sa < 2; ++sa) {
-        const float ra = m->link_sphere[la][sa][3];
-        const float xa[3] = {stage(ld, STG_SPH + 6 * la + 3 * sa), stage(ld, STG_SPH + 6 * la + 3 * sa + 1),
-                             stage(ld, STG_SPH + 6 * la + 3 * sa + 2)};
-#pragma unroll
+        float spa[4], xa[3];
+        ldc(spa, m->link_sphere[la][sa]);
+        mv3(Ra, spa, xa);
+        xa[0] += pa[0]; xa[1] += pa[1]; xa[2] += pa[2];
         for (int sb = 0; sb < 2; ++sb) {
-          const float rb = m->link_sphere[lb][sb][3];
-          const float xb[3] = {stage(ld, STG_SPH + 6 * lb + 3 * sb), stage(ld, STG_SPH + 6 * lb + 3 * sb + 1),
-                               stage(ld, STG_SPH + 6 * lb + 3 * sb + 2)};
+          float spb[4], xb[3];
+          ldc(spb, m->link_sphere[lb][sb]);
+          mv3(Rb, spb, xb);
+          xb[0] += pb[0]; xb[1] += pb[1]; xb[2] += pb[2];
           const float dv[3] = {xa[0] - xb[0], xa[1] - xb[1], xa[2] - xb[2]};
           const float dist = sqrtf(dot3(dv, dv));
-          const float sep = dist - (ra + rb);
+          const float sep = dist - (spa[3] + spb[3]);
           if (sep < margin && dist > 1e-9f) {
             float n[3], x[3];
 #pragma unroll
             for (int a = 0; a < 3; ++a) {
               n[a] = dv[a] / dist;
-              x[a] = 0.5f * ((xa[a] - n[a] * ra) + (xb[a] + n[a] * rb));
+              x[a] = 0.5f * ((xa[a] - n[a] * spa[3]) + (xb[a] + n[a] * spb[3]));
             }
-            contact_add(ld, nc, x, n, sep, la, lb);
+            raw_push(ld, nraw, x, sep, n, la, lb);
           }
         }
       }
     }
   }
-  return nc;
+  return insert_raw(ld, nraw);
 }
 
 __device__ __forceinline__ void tangents(const float n[3], float t1[3], float t2[3]) {
@@ -439,22 +519,6 @@ __device__ __forceinline__ void tangents(const float n[3], float t1[3], float t2
   cross3(n, t1, t2);
 }
 
-// J row of direction d at point x on body b (predicated over the fixed chain, no dynamic indexing)
-__device__ __forceinline__ void jac_row(const float S[ND][6], const float org[ND][3], int b, const float x[3],
-                                        const float d[3], float J[NV]) {
-  float xd[3];
-  cross3(x, d, xd);
-  J[0] = xd[0]; J[1] = xd[1]; J[2] = xd[2];
-  J[3] = d[0]; J[4] = d[1]; J[5] = d[2];
-#pragma unroll
-  for (int j = 0; j < ND; ++j) {
-    const float xo[3] = {x[0] - org[j][0], x[1] - org[j][1], x[2] - org[j][2]};
-    float c[3];
-    cross3(xo, d, c);
-    J[6 + j] = (j < b) ? (S[j][0] * c[0] + S[j][1] * c[1] + S[j][2] * c[2]) : 0.f;
-  }
-}
-
 // What the MDP needs from the last substep (instead of 12 per-link force vectors).
 struct SensorOut {
   float feet_f[2][3];   // net contact force on foot_0 / foot_1
@@ -466,7 +530,7 @@ struct SensorOut {
 template <bool kDebugForces>
 __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
                                         const float target[ND], const Lane& ld, bool last, SensorOut& so,
-                                        float (*dbgF)[3], float* dbgTau) {
+                                        float (*dbgF)[3], float* dbgTau, Stamps& sp) {
   const float dt = cfg.sim_dt;
   MP m = opaque(m0);
 
@@ -487,7 +551,8 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
   {
     Kin k;
     fk(m, s, k);
-    nc = detect(opaque(m0), cfg, k, s.pos[2], ld);
+    nc = detect(opaque(m0), cfg, k, s.pos[2], ld, sp);
+    sp.mark(2);
     m = opaque(m0);
 #pragma unroll
     for (int j = 0; j < ND; ++j) {
@@ -591,7 +656,9 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
   // implicit PD drives. Pass 1: all implicit (armature on the diagonal). A joint whose implicit
   // torque exceeds the effort limit gets an explicit +-limit torque and loses its armature
   // (rank-1 downdate of the factor), then the free velocity is re-solved.
-  cholesky_inplace(L);
+  sp.mark(3);
+  float Li[NV];
+  cholesky_inplace(L, Li);
   float u[NV], b[NV], w[NV];
   u[0] = s.av[0]; u[1] = s.av[1]; u[2] = s.av[2];
   u[3] = s.lv[0]; u[4] = s.lv[1]; u[5] = s.lv[2];
@@ -607,13 +674,13 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
   {
     float z[NV];
     lt_mul(L, u, w);
-    fwd_sub(L, b, z);
+    fwd_sub(L, Li, b, z);
 #pragma unroll
     for (int a = 0; a < NV; ++a) w[a] += z[a];
   }
   {
     float uf[NV];
-    bwd_sub(L, w, uf);
+    bwd_sub(L, Li, w, uf);
     unsigned sat = 0;
 #pragma unroll
     for (int j = 0; j < ND; ++j) {
@@ -624,90 +691,109 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
       }
     }
     if (sat) {
-      if (sat & 1u) chol_downdate<6>(L, arm);
-      if (sat & 2u) chol_downdate<7>(L, arm);
-      if (sat & 4u) chol_downdate<8>(L, arm);
-      if (sat & 8u) chol_downdate<9>(L, arm);
-      if (sat & 16u) chol_downdate<10>(L, arm);
-      if (sat & 32u) chol_downdate<11>(L, arm);
+      if (sat & 1u) chol_downdate<6>(L, Li, arm);
+      if (sat & 2u) chol_downdate<7>(L, Li, arm);
+      if (sat & 4u) chol_downdate<8>(L, Li, arm);
+      if (sat & 8u) chol_downdate<9>(L, Li, arm);
+      if (sat & 16u) chol_downdate<10>(L, Li, arm);
+      if (sat & 32u) chol_downdate<11>(L, Li, arm);
       float z[NV];
       lt_mul(L, u, w);
-      fwd_sub(L, b, z);
+      fwd_sub(L, Li, b, z);
 #pragma unroll
       for (int a = 0; a < NV; ++a) w[a] += z[a];
     }
   }
 
-  // contact rows: Y = L^-1 J^T (whitened), effective masses and bias velocities
+  sp.mark(4);
+  // contact rows: Y = L^-1 J^T (whitened), effective masses and bias velocities.
+  // J of direction d at point x on body b: [x x d ; d ; d.(a_j x (x - o_j)) for joints j < b]
   for (int c = 0; c < nc; ++c) {
-    const float x[3] = {ld.at(c, SL_Y + 0), ld.at(c, SL_Y + 1), ld.at(c, SL_Y + 2)};
-    const float n[3] = {ld.at(c, SL_N + 0), ld.at(c, SL_N + 1), ld.at(c, SL_N + 2)};
-    const float sep = ld.at(c, SL_VMIN);
-    const int la = (int)ld.at(c, SL_LA), lb = (int)ld.at(c, SL_LB);
-    const int ba = link_body(la);
+    const float4 g0 = ld.g(c, 0), gn = ld.g(c, G_N);
+    const float la_f = ld.g(c, G_LAM).w;
+    const float x[3] = {g0.x, g0.y, g0.z};
+    const float n[3] = {gn.x, gn.y, gn.z};
+    const float sep = g0.w;
+    const int ba = link_body((int)la_f);
+    const int lb = (int)gn.w;
     const int bb = lb >= 0 ? link_body(lb) : -1;
+    // per-joint lever vectors a_j x (x - o_j), signed by which side of the contact the joint is on
+    float cj[ND][3];
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+      const float xo[3] = {x[0] - org[j][0], x[1] - org[j][1], x[2] - org[j][2]};
+      float c3[3];
+      cross3(S[j], xo, c3);
+      const float sg = (j < ba ? 1.f : 0.f) - (j < bb ? 1.f : 0.f);
+      cj[j][0] = sg * c3[0]; cj[j][1] = sg * c3[1]; cj[j][2] = sg * c3[2];
+    }
+    const float root = bb >= 0 ? 0.f : 1.f;  // self contacts: the root terms cancel
     float t1[3], t2[3];
     tangents(n, t1, t2);
+    float invm[3];
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
       float d[3];
 #pragma unroll
       for (int a = 0; a < 3; ++a) d[a] = r == 0 ? n[a] : (r == 1 ? t1[a] : t2[a]);
       float J[NV], Y[NV];
-      jac_row(S, org, ba, x, d, J);
-      if (bb >= 0) {
-        float Jb[NV];
-        jac_row(S, org, bb, x, d, Jb);
+      float xd[3];
+      cross3(x, d, xd);
+      J[0] = root * xd[0]; J[1] = root * xd[1]; J[2] = root * xd[2];
+      J[3] = root * d[0]; J[4] = root * d[1]; J[5] = root * d[2];
 #pragma unroll
-        for (int a = 0; a < NV; ++a) J[a] -= Jb[a];
-      }
-      fwd_sub(L, J, Y);
-      float yy = 0.f;
+      for (int j = 0; j < ND; ++j) J[6 + j] = dot3(cj[j], d);
+      fwd_sub(L, Li, J, Y);
+      invm[r] = 1.f / (dot12(Y, Y) + 1e-9f);
 #pragma unroll
-      for (int a = 0; a < NV; ++a) { ld.at(c, SL_Y + 12 * r + a) = Y[a]; yy += Y[a] * Y[a]; }
-      ld.at(c, SL_INVM + r) = 1.f / (yy + 1e-9f);
-      ld.at(c, SL_LAM + r) = 0.f;
+      for (int q = 0; q < 3; ++q) ld.g(c, 3 * r + q) = make_float4(Y[4 * q], Y[4 * q + 1], Y[4 * q + 2], Y[4 * q + 3]);
     }
     float vmin;
     if (sep >= 0.f) vmin = -sep / dt;
     else vmin = fminf(cfg.baumgarte * (-sep) / dt, m->max_depenetration_velocity);
-    ld.at(c, SL_VMIN) = vmin;
+    ld.g(c, G_INVM) = make_float4(invm[0], invm[1], invm[2], vmin);
   }
 
-  // projected Gauss-Seidel on the whitened velocity (Coulomb disk friction)
+  sp.mark(5);
+  // projected Gauss-Seidel on the whitened velocity (Coulomb disk friction); each contact's three
+  // rows are read once (9 ds_read_b128) and kept in registers for its update
   const float mu = cfg.friction;
   for (int it = 0; it < cfg.solver_iterations; ++it) {
     for (int c = 0; c < nc; ++c) {
-      float vn = 0.f;
+      float y0[NV], y1[NV], y2[NV];
 #pragma unroll
-      for (int a = 0; a < NV; ++a) vn += ld.at(c, SL_Y + a) * w[a];
-      const float ln0 = ld.at(c, SL_LAM + 0);
-      const float ln = fmaxf(ln0 + (ld.at(c, SL_VMIN) - vn) * ld.at(c, SL_INVM + 0), 0.f);
-      const float dl = ln - ln0;
-      ld.at(c, SL_LAM + 0) = ln;
+      for (int q = 0; q < 3; ++q) {
+        const float4 a0 = ld.g(c, q), a1 = ld.g(c, 3 + q), a2 = ld.g(c, 6 + q);
+        y0[4 * q] = a0.x; y0[4 * q + 1] = a0.y; y0[4 * q + 2] = a0.z; y0[4 * q + 3] = a0.w;
+        y1[4 * q] = a1.x; y1[4 * q + 1] = a1.y; y1[4 * q + 2] = a1.z; y1[4 * q + 3] = a1.w;
+        y2[4 * q] = a2.x; y2[4 * q + 1] = a2.y; y2[4 * q + 2] = a2.z; y2[4 * q + 3] = a2.w;
+      }
+      const float4 im = ld.g(c, G_INVM);
+      float4 lam = ld.g(c, G_LAM);
+      const float vn = dot12(y0, w);
+      const float ln = fmaxf(lam.x + (im.w - vn) * im.x, 0.f);
+      const float dl = ln - lam.x;
 #pragma unroll
-      for (int a = 0; a < NV; ++a) w[a] += ld.at(c, SL_Y + a) * dl;
-      float vt1 = 0.f, vt2 = 0.f;
-#pragma unroll
-      for (int a = 0; a < NV; ++a) { vt1 += ld.at(c, SL_Y + 12 + a) * w[a]; vt2 += ld.at(c, SL_Y + 24 + a) * w[a]; }
-      const float l1o = ld.at(c, SL_LAM + 1), l2o = ld.at(c, SL_LAM + 2);
-      float l1 = l1o - vt1 * ld.at(c, SL_INVM + 1);
-      float l2 = l2o - vt2 * ld.at(c, SL_INVM + 2);
+      for (int a = 0; a < NV; ++a) w[a] += y0[a] * dl;
+      const float vt1 = dot12(y1, w), vt2 = dot12(y2, w);
+      float l1 = lam.y - vt1 * im.y;
+      float l2 = lam.z - vt2 * im.z;
       const float lim = mu * ln;
       const float mag2 = l1 * l1 + l2 * l2;
       if (mag2 > lim * lim) {
         const float sc = lim / sqrtf(mag2);
         l1 *= sc; l2 *= sc;
       }
-      const float d1 = l1 - l1o, d2 = l2 - l2o;
-      ld.at(c, SL_LAM + 1) = l1;
-      ld.at(c, SL_LAM + 2) = l2;
+      const float d1 = l1 - lam.y, d2 = l2 - lam.z;
 #pragma unroll
-      for (int a = 0; a < NV; ++a) w[a] += ld.at(c, SL_Y + 12 + a) * d1 + ld.at(c, SL_Y + 24 + a) * d2;
+      for (int a = 0; a < NV; ++a) w[a] += y1[a] * d1 + y2[a] * d2;
+      lam.x = ln; lam.y = l1; lam.z = l2;
+      ld.g(c, G_LAM) = lam;
     }
   }
+  sp.mark(6);
   float un[NV];
-  bwd_sub(L, w, un);
+  bwd_sub(L, Li, w, un);
 
   if (last) {
     // ContactSensor inputs: net force on the feet, max |net force| over undesired links
@@ -715,14 +801,14 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
 #pragma unroll
     for (int l = 0; l < NL; ++l) Fl[l][0] = Fl[l][1] = Fl[l][2] = 0.f;
     for (int c = 0; c < nc; ++c) {
-      const float n[3] = {ld.at(c, SL_N + 0), ld.at(c, SL_N + 1), ld.at(c, SL_N + 2)};
+      const float4 gn = ld.g(c, G_N), lam = ld.g(c, G_LAM);
+      const float n[3] = {gn.x, gn.y, gn.z};
       float t1[3], t2[3];
       tangents(n, t1, t2);
-      const float l0 = ld.at(c, SL_LAM + 0), l1 = ld.at(c, SL_LAM + 1), l2 = ld.at(c, SL_LAM + 2);
       float f[3];
 #pragma unroll
-      for (int a = 0; a < 3; ++a) f[a] = (l0 * n[a] + l1 * t1[a] + l2 * t2[a]) / dt;
-      const int la = (int)ld.at(c, SL_LA), lb = (int)ld.at(c, SL_LB);
+      for (int a = 0; a < 3; ++a) f[a] = (lam.x * n[a] + lam.y * t1[a] + lam.z * t2[a]) / dt;
+      const int la = (int)lam.w, lb = (int)gn.w;
 #pragma unroll
       for (int l = 0; l < NL; ++l) {
         const float sa = (l == la ? 1.f : 0.f) - (l == lb ? 1.f : 0.f);
@@ -993,11 +1079,13 @@ __global__ __launch_bounds__(WAVE, 1) void zb_step_kernel(const zb_model* __rest
                                                           uint8_t* __restrict__ term, uint8_t* __restrict__ trunc,
                                                           float* __restrict__ acc) {
   MP m = to_mp(mg);
-  __shared__ float lds[LDS_FLOATS];
+  __shared__ __attribute__((aligned(16))) float lds[LDS_FLOATS];
   const int i = blockIdx.x * WAVE + threadIdx.x;
   if (i >= N) return;
-  const Lane ld{lds + threadIdx.x};
+  const Lane ld{reinterpret_cast<float4*>(lds) + threadIdx.x};
 #define ST(f) st[(size_t)(f) * N + i]
+  Stamps sp;
+  sp.begin();
   Phys p;
   load_phys(st, N, i, p);
 
@@ -1045,8 +1133,11 @@ __global__ __launch_bounds__(WAVE, 1) void zb_step_kernel(const zb_model* __rest
 
   // 4 physics substeps (the last one reports the contact-sensor inputs and applied torques)
   SensorOut so;
-  for (int k = 0; k < cfg.decimation; ++k)
-    substep<false>(m, cfg, p, target, ld, k == cfg.decimation - 1, so, nullptr, nullptr);
+  sp.mark(0);
+  for (int k = 0; k < cfg.decimation; ++k) {
+    substep<false>(m, cfg, p, target, ld, k == cfg.decimation - 1, so, nullptr, nullptr, sp);
+    sp.mark(7);
+  }
   m = opaque(m);
 
   // ContactSensor lazy update, once per policy step (history roll, air/contact timers)
@@ -1200,6 +1291,8 @@ __global__ __launch_bounds__(WAVE, 1) void zb_step_kernel(const zb_model* __rest
   rew[i] = reward;
   term[i] = died ? 1 : 0;
   trunc[i] = time_out ? 1 : 0;
+  sp.mark(8);
+  sp.flush();
 #undef ST
 }
 
@@ -1255,17 +1348,18 @@ __global__ __launch_bounds__(WAVE, 1) void zb_substeps_kernel(const zb_model* __
                                                               int nsub, float* __restrict__ net_force,
                                                               float* __restrict__ tau_out) {
   MP m = to_mp(mg);
-  __shared__ float lds[LDS_FLOATS];
+  __shared__ __attribute__((aligned(16))) float lds[LDS_FLOATS];
   const int i = blockIdx.x * WAVE + threadIdx.x;
   if (i >= N) return;
-  const Lane ld{lds + threadIdx.x};
+  const Lane ld{reinterpret_cast<float4*>(lds) + threadIdx.x};
   Phys p;
   load_phys(st, N, i, p);
   float tg[ND], tau[ND], F[NL][3];
 #pragma unroll
   for (int j = 0; j < ND; ++j) { tg[j] = targets[(size_t)i * ND + j]; tau[j] = 0.f; }
   SensorOut so;
-  for (int k = 0; k < nsub; ++k) substep<true>(m, cfg, p, tg, ld, k == nsub - 1, so, F, tau);
+  Stamps sp;
+  for (int k = 0; k < nsub; ++k) substep<true>(m, cfg, p, tg, ld, k == nsub - 1, so, F, tau, sp);
   if (net_force)
 #pragma unroll
     for (int l = 0; l < NL; ++l)
@@ -1404,6 +1498,21 @@ int zb_profile_end(zb_handle h, float* total_ms, int* count) {
   *count = h->prof_n;
   prof_free(h);
   return 0;
+}
+
+// Diagnostic build only (-DZB_STAMPS): per-phase cycle sums over all waves since the last call.
+int zb_read_stamps(uint64_t* out16) {
+#ifdef ZB_STAMPS
+  unsigned long long tmp[NSTAMP];
+  HIPCHK(hipMemcpyFromSymbol(tmp, HIP_SYMBOL(g_stamps), sizeof(tmp)), "hipMemcpyFromSymbol");
+  for (int k = 0; k < 16; ++k) out16[k] = k < NSTAMP ? tmp[k] : 0;
+  unsigned long long z[NSTAMP] = {0};
+  HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z)), "hipMemcpyToSymbol");
+  return 0;
+#else
+  (void)out16;
+  return set_err(-1, "zb_read_stamps: library built without -DZB_STAMPS", hipSuccess);
+#endif
 }
 
 void zb_destroy(zb_handle h) {
