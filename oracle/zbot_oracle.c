@@ -296,20 +296,35 @@ typedef struct {
   real sep;            /* separation (negative = penetration) */
 } contact_t;
 
-typedef struct { contact_t c[NC_MAX]; int n; } clist_t;
+/* Candidate list (canonical order): ground candidates link by link (<= NCAND_PER_LINK each),
+ * then self-collision candidates in (pair, sphere a, sphere b) order, at most NSELF_MAX of them.
+ * When more than NC_MAX candidates exist the NC_MAX smallest by (sep, canonical index) are kept;
+ * the kept contacts are solved in canonical order. Same rule as the kernel's quad selection. */
+#define NSELF_MAX 18
+#define NCAND_MAX (NL * NCAND_PER_LINK + NSELF_MAX)
+typedef struct { contact_t c[NCAND_MAX]; int n; } clist_t;
 
-static void clist_add(clist_t* L, const contact_t* c) {
-  if (L->n < NC_MAX) { L->c[L->n++] = *c; return; }
-  int worst = 0;
-  for (int i = 1; i < NC_MAX; ++i)
-    if (L->c[i].sep > L->c[worst].sep) worst = i;
-  if (c->sep < L->c[worst].sep) L->c[worst] = *c;
+static void select_contacts(clist_t* L) {
+  if (L->n <= NC_MAX) return;
+  int keep[NCAND_MAX];
+  for (int i = 0; i < L->n; ++i) {
+    int rank = 0;
+    for (int j = 0; j < L->n; ++j)
+      if (L->c[j].sep < L->c[i].sep || (L->c[j].sep == L->c[i].sep && j < i)) ++rank;
+    keep[i] = rank < NC_MAX;
+  }
+  int k = 0;
+  for (int i = 0; i < L->n; ++i)
+    if (keep[i]) L->c[k++] = L->c[i];
+  L->n = k;
 }
 
 /* Ground: each link's shape is the convex hull of two circles (C, E1, E2 in body frame). The
  * lowest rim point of each circle plus its three 90-degree rotations along the rim are the
  * candidates (4 per circle: a flat disk resting on the plane yields a 4-point manifold);
- * per link the NCAND_PER_LINK deepest below the speculative margin are kept. */
+ * per link the first NCAND_PER_LINK below the speculative margin are kept. Self: every sphere
+ * pair of every non-adjacent link pair (the kernel's broadphase is conservative, so testing all
+ * pairs here finds the same candidates). */
 static void detect(const mdl_t* m, const zb_task_cfg* cfg, const kin_t* k, real Pz, clist_t* L) {
   L->n = 0;
   const real margin = cfg->contact_margin;
@@ -320,8 +335,7 @@ static void detect(const mdl_t* m, const zb_task_cfg* cfg, const kin_t* k, real 
     real bc[3];
     m3_v(R, m->bound[l], bc);
     if (Pz + k->p[b][2] + bc[2] - m->bound[l][3] > margin) continue;
-    contact_t cand[8];
-    int nc = 0;
+    int taken = 0;
     for (int ci = 0; ci < 2; ++ci) {
       const real* cd = m->circle[l][ci];
       real C[3], E1[3], E2[3];
@@ -344,54 +358,51 @@ static void detect(const mdl_t* m, const zb_task_cfg* cfg, const kin_t* k, real 
         contact_t c;
         for (int a = 0; a < 3; ++a) c.x[a] = C[a] + cr * E1[a] + sr * E2[a];
         c.sep = Pz + c.x[2];
-        if (c.sep < margin) {
+        /* the first NCAND_PER_LINK valid candidates in the fixed order (circle 0: lowest, +90,
+         * +180, +270 degrees; then circle 1): a fixed order (not a depth sort) keeps the
+         * Gauss-Seidel row order independent of rounding when rim points sit at one depth */
+        if (c.sep < margin && taken < NCAND_PER_LINK) {
           c.la = l; c.lb = -1;
           c.n[0] = 0; c.n[1] = 0; c.n[2] = 1;
-          cand[nc++] = c;
+          L->c[L->n++] = c;
+          ++taken;
         }
       }
     }
-    /* the first NCAND_PER_LINK valid candidates in the fixed order (circle 0: lowest, +90, +180,
-     * +270 degrees; then circle 1). A fixed order (not a depth sort) keeps the Gauss-Seidel row order
-     * independent of rounding when several rim points sit at the same depth (flat foot). */
-    for (int s = 0; s < nc && s < NCAND_PER_LINK; ++s) clist_add(L, &cand[s]);
   }
-  if (!cfg->enable_self_collision) return;
-  for (int p = 0; p < m->npairs; ++p) {
-    int la = m->pairs[p][0], lb = m->pairs[p][1];
-    int ba = m->link_body[la], bb = m->link_body[lb];
-    real ca[3], cb[3];
-    m3_v(k->R[ba], m->bound[la], ca);
-    m3_v(k->R[bb], m->bound[lb], cb);
-    real d2 = 0;
-    for (int a = 0; a < 3; ++a) { real d = (k->p[ba][a] + ca[a]) - (k->p[bb][a] + cb[a]); d2 += d * d; }
-    real rr = m->bound[la][3] + m->bound[lb][3] + margin;
-    if (d2 > rr * rr) continue;
-    for (int sa = 0; sa < 2; ++sa) {
-      real xa[3];
-      m3_v(k->R[ba], m->sphere[la][sa], xa);
-      for (int a = 0; a < 3; ++a) xa[a] += k->p[ba][a];
-      real ra = m->sphere[la][sa][3];
-      for (int sb = 0; sb < 2; ++sb) {
-        real xb[3];
-        m3_v(k->R[bb], m->sphere[lb][sb], xb);
-        for (int a = 0; a < 3; ++a) xb[a] += k->p[bb][a];
-        real rb = m->sphere[lb][sb][3];
-        real dv[3] = {xa[0] - xb[0], xa[1] - xb[1], xa[2] - xb[2]};
-        real dist = sqrtr(v3_dot(dv, dv));
-        real sep = dist - (ra + rb);
-        if (sep < margin && dist > (real)1e-9) {
-          contact_t c;
-          c.la = la; c.lb = lb; c.sep = sep;
-          for (int a = 0; a < 3; ++a) {
-            c.n[a] = dv[a] / dist;
-            c.x[a] = (real)0.5 * ((xa[a] - c.n[a] * ra) + (xb[a] + c.n[a] * rb));
+  if (cfg->enable_self_collision) {
+    int nself = 0;
+    for (int p = 0; p < m->npairs && nself < NSELF_MAX; ++p) {
+      int la = m->pairs[p][0], lb = m->pairs[p][1];
+      int ba = m->link_body[la], bb = m->link_body[lb];
+      for (int sa = 0; sa < 2; ++sa) {
+        real xa[3];
+        m3_v(k->R[ba], m->sphere[la][sa], xa);
+        for (int a = 0; a < 3; ++a) xa[a] += k->p[ba][a];
+        real ra = m->sphere[la][sa][3];
+        for (int sb = 0; sb < 2; ++sb) {
+          real xb[3];
+          m3_v(k->R[bb], m->sphere[lb][sb], xb);
+          for (int a = 0; a < 3; ++a) xb[a] += k->p[bb][a];
+          real rb = m->sphere[lb][sb][3];
+          real dv[3] = {xa[0] - xb[0], xa[1] - xb[1], xa[2] - xb[2]};
+          real dist = sqrtr(v3_dot(dv, dv));
+          real sep = dist - (ra + rb);
+          if (sep < margin && dist > (real)1e-9 && nself < NSELF_MAX) {
+            contact_t c;
+            c.la = la; c.lb = lb; c.sep = sep;
+            for (int a = 0; a < 3; ++a) {
+              c.n[a] = dv[a] / dist;
+              c.x[a] = (real)0.5 * ((xa[a] - c.n[a] * ra) + (xb[a] + c.n[a] * rb));
+            }
+            L->c[L->n++] = c;
+            ++nself;
           }
-          clist_add(L, &c);
         }
       }
     }
   }
+  select_contacts(L);
 }
 
 /* tangent basis for normal n (deterministic, shared with the kernel) */
@@ -591,7 +602,7 @@ static void substep(const mdl_t* m, const zb_task_cfg* cfg, phys_t* s, const rea
   detect(m, cfg, &k, s->root_pos[2], &CL);
   int nc = CL.n;
   real Y[NC_MAX][3][NV];
-  real invm[NC_MAX][3], vmin[NC_MAX], lam[NC_MAX][3];
+  real invm[NC_MAX][3], vmin[NC_MAX], lam[NC_MAX][3], c01[NC_MAX], c02[NC_MAX];
   real dirs[NC_MAX][3][3];
   for (int c = 0; c < nc; ++c) {
     const contact_t* ct = &CL.c[c];
@@ -610,6 +621,8 @@ static void substep(const mdl_t* m, const zb_task_cfg* cfg, phys_t* s, const rea
       invm[c][r] = (real)1 / (yy + (real)1e-9);
       lam[c][r] = 0;
     }
+    c01[c] = 0; c02[c] = 0;
+    for (int a = 0; a < NV; ++a) { c01[c] += Y[c][1][a] * Y[c][0][a]; c02[c] += Y[c][2][a] * Y[c][0][a]; }
     real sep = ct->sep;
     if (sep >= 0) vmin[c] = -sep / dt;
     else {
@@ -617,29 +630,29 @@ static void substep(const mdl_t* m, const zb_task_cfg* cfg, phys_t* s, const rea
       vmin[c] = push < m->max_depen ? push : m->max_depen;
     }
   }
+  /* Gauss-Seidel over contacts; the three row dots of a contact use the same w, the normal
+   * update enters the tangent velocities through the cross terms c01 = Y1.Y0, c02 = Y2.Y0
+   * (algebraically the sequential normal-then-friction update). */
   const real mu = cfg->friction;
   for (int it = 0; it < cfg->solver_iterations; ++it) {
     for (int c = 0; c < nc; ++c) {
-      real vn = 0;
-      for (int a = 0; a < NV; ++a) vn += Y[c][0][a] * w[a];
+      real vn = 0, v1 = 0, v2 = 0;
+      for (int a = 0; a < NV; ++a) { vn += Y[c][0][a] * w[a]; v1 += Y[c][1][a] * w[a]; v2 += Y[c][2][a] * w[a]; }
       real ln = lam[c][0] + (vmin[c] - vn) * invm[c][0];
       if (ln < 0) ln = 0;
       real dl = ln - lam[c][0];
-      lam[c][0] = ln;
-      for (int a = 0; a < NV; ++a) w[a] += Y[c][0][a] * dl;
-      real vt1 = 0, vt2 = 0;
-      for (int a = 0; a < NV; ++a) { vt1 += Y[c][1][a] * w[a]; vt2 += Y[c][2][a] * w[a]; }
+      real vt1 = v1 + c01[c] * dl, vt2 = v2 + c02[c] * dl;
       real l1 = lam[c][1] - vt1 * invm[c][1];
       real l2 = lam[c][2] - vt2 * invm[c][2];
-      real lim = mu * lam[c][0];
+      real lim = mu * ln;
       real mag2 = l1 * l1 + l2 * l2;
       if (mag2 > lim * lim) {
         real sc = lim / sqrtr(mag2);
         l1 *= sc; l2 *= sc;
       }
       real d1 = l1 - lam[c][1], d2 = l2 - lam[c][2];
-      lam[c][1] = l1; lam[c][2] = l2;
-      for (int a = 0; a < NV; ++a) w[a] += Y[c][1][a] * d1 + Y[c][2][a] * d2;
+      lam[c][0] = ln; lam[c][1] = l1; lam[c][2] = l2;
+      for (int a = 0; a < NV; ++a) w[a] += Y[c][0][a] * dl + Y[c][1][a] * d1 + Y[c][2][a] * d2;
     }
   }
   real un[NV];

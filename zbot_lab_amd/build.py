@@ -25,10 +25,12 @@ STAMPS_OUT = os.path.join(HERE, "libzbot_stamps.so")
 
 def build(force: bool = False, verbose: bool = False, stamps: bool = False) -> str:
     out = STAMPS_OUT if stamps else OUT
-    deps = [SRC, os.path.join(ROOT, "include", "zbot.h")]
+    deps = [SRC, os.path.join(ROOT, "include", "zbot.h"), os.path.abspath(__file__)]
     if not force and os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(d) for d in deps):
         return out
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+    # -fno-slp-vectorize: packing scalar f32 math into v_pk_* pairs forces aligned register pairs
+    # and shuffles; on this register-bound kernel it costs ~1.1 KB/lane of scratch spills.
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fno-slp-vectorize", "-fPIC", "-shared",
            "-I", os.path.join(ROOT, "include"), "-o", out + ".tmp", SRC]
     if stamps:
         cmd.insert(1, "-DZB_STAMPS")

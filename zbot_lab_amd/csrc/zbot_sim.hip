@@ -38,15 +38,6 @@ constexpr float PI_F = 3.14159265358979323846f;
 constexpr float TWO_PI_F = 6.28318530717958647692f;
 constexpr float RIM_EPS = 1e-3f;  // m; 2% of the module radius (see detect)
 
-// LDS contact slot layout: 12 float4 granules per slot, [slot][granule][lane] (16 B per lane), so
-// every access is one conflict-free ds_read_b128 / ds_write_b128 per wave (1 KiB contiguous).
-//   g0..g2  Y row 0 (normal)   g3..g5 Y row 1 (tangent 1)   g6..g8 Y row 2 (tangent 2)
-//   g9  {invm0, invm1, invm2, vmin}   g10 {lam0, lam1, lam2, la}   g11 {n.x, n.y, n.z, lb}
-// During detection g0 holds {x.x, x.y, x.z, sep}.
-constexpr int SLOT4 = 12;
-constexpr int G_INVM = 9, G_LAM = 10, G_N = 11;
-constexpr int LDS_FLOATS = NCM * SLOT4 * 4 * WAVE;
-
 // The ZBOT-6 chain topology is compiled in (zb_create checks the model against it):
 // link l belongs to composite body (l+1)/2; joint j connects body j -> j+1.
 __host__ __device__ constexpr int link_body(int l) { return (l + 1) >> 1; }
@@ -61,11 +52,6 @@ __device__ __forceinline__ void ldc(float (&d)[N], CF* s) {
   for (int i = 0; i < N; ++i) d[i] = s[i];
 }
 __device__ __forceinline__ MP to_mp(const zb_model* m) { return (MP)(uintptr_t)m; }
-
-struct Lane {
-  float4* p;  // (float4*)lds + lane
-  __device__ __forceinline__ float4& g(int slot, int q) const { return p[(slot * SLOT4 + q) * WAVE]; }
-};
 
 // ------------------------------------------------------------------------- diagnostic stamps
 // Built only with -DZB_STAMPS (python -m zbot_lab_amd.build --stamps): s_memtime deltas per phase,
@@ -332,121 +318,170 @@ __device__ __forceinline__ MP opaque(MP m) {
   return (MP)v;
 }
 
-// ------------------------------------------------------------------------- contacts
-// Detection writes a RAW candidate list (ground: <= 4 per link in fixed order, then self pairs),
-// capped at NRAW, into granules 1..8 of the slots (2 granules per entry: {x, sep}, {n, code}
-// with code = 16*la + (lb+1)). One compact pass then inserts them in order into the NCM solver
-// slots, replacing the shallowest when full (= oracle clist_add over the same list). Keeping the
-// insertion out of the unrolled detection code keeps the kernel small enough for the I-cache.
-constexpr int NRAW = 48;
-__device__ __forceinline__ float4& raw(const Lane& ld, int e, int h) {  // e < NRAW, h in {0, 1}
-  const int gi = 2 * e + h;                                             // 96 granules = 12 slots x 8
-  return ld.g(gi >> 3, 1 + (gi & 7));
+// ------------------------------------------------------------------------- quads
+// Four lanes per env (a "quad", lane = 4*e + s). The articulated-body dynamics (FK, RNEA, CRBA,
+// Cholesky) are evaluated redundantly by the four lanes; the contact work is split: each lane
+// tests 3 links against the ground and a quarter of the self-collision candidate pairs, builds
+// the rows of every 4th contact slot, and in the Gauss-Seidel sweep owns 3 of the 12 whitened
+// coordinates (row dots are reduced across the quad with DPP quad_perm adds, which give all four
+// lanes bit-identical sums, so the redundant scalar work stays identical across the quad).
+template <int CTRL>
+__device__ __forceinline__ float dppf(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
 }
-__device__ __forceinline__ void raw_push(const Lane& ld, int& nraw, const float x[3], float sep, const float n[3],
-                                         int la, int lb) {
-  if (nraw < NRAW) {
-    raw(ld, nraw, 0) = make_float4(x[0], x[1], x[2], sep);
-    raw(ld, nraw, 1) = make_float4(n[0], n[1], n[2], (float)(16 * la + lb + 1));
-    ++nraw;
-  }
+template <int CTRL>
+__device__ __forceinline__ int dppi(int x) {
+  return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xF, 0xF, false);
 }
-// sequential insertion of the raw list into the solver slots (g0 {x, sep}, g10.w la, g11 {n, lb})
-__device__ __forceinline__ int insert_raw(const Lane& ld, int nraw) {
-  int nc = 0;
-  for (int e = 0; e < nraw; ++e) {
-    const float4 r0 = raw(ld, e, 0), r1 = raw(ld, e, 1);
-    int slot = nc;
-    if (nc < NCM) {
-      ++nc;
-    } else {
-      int worst = 0;
-      float wsep = ld.g(0, 0).w;
-      for (int c = 1; c < NCM; ++c) {
-        const float s = ld.g(c, 0).w;
-        if (s > wsep) { wsep = s; worst = c; }
-      }
-      if (!(r0.w < wsep)) continue;
-      slot = worst;
-    }
-    const int code = (int)r1.w;
-    ld.g(slot, 0) = r0;
-    ld.g(slot, G_LAM) = make_float4(0.f, 0.f, 0.f, (float)(code >> 4));
-    ld.g(slot, G_N) = make_float4(r1.x, r1.y, r1.z, (float)((code & 15) - 1));
-  }
-  return nc;
+constexpr int QP_XOR1 = 0xB1;  // quad_perm [1,0,3,2]
+constexpr int QP_XOR2 = 0x4E;  // quad_perm [2,3,0,1]
+__device__ __forceinline__ float qsum(float x) {
+  x += dppf<QP_XOR1>(x);
+  return x + dppf<QP_XOR2>(x);
+}
+__device__ __forceinline__ float qmax(float x) {
+  x = fmaxf(x, dppf<QP_XOR1>(x));
+  return fmaxf(x, dppf<QP_XOR2>(x));
+}
+template <int K>
+__device__ __forceinline__ float qb(float x) { return dppf<K * 0x55>(x); }  // broadcast quad lane K
+template <int K>
+__device__ __forceinline__ int qbi(int x) { return dppi<K * 0x55>(x); }
+
+// Device-side per-link collision table (built by zb_create), float4-aligned for per-lane loads:
+// [0] bounding sphere, [1+3ci..3+3ci] circle ci: C, E1, E2 (body frame), [7], [8] inscribed spheres.
+constexpr int LINK4 = 9;
+
+// Candidate list in canonical order: ground (link by link, <= 4 each), then self candidates in
+// (pair, sphere a, sphere b) order, at most NSELF. More than NCM candidates: the NCM smallest by
+// (sep, canonical index) are kept; kept contacts are solved in canonical order (= oracle detect).
+constexpr int NSELF = 18;
+constexpr int NCAND = NL * 4 + NSELF;
+
+// LDS layout of one workgroup (16 envs), float4 units:
+//   YG   [NCM][4][WAVE]  lane-owned row granules: r < 3 {Y_r[3s..3s+2], X_r}, X = {invm0, c01, c02};
+//                        r = 3 {invm1, invm2, vmin, 0}. During detection: the lane's candidate
+//                        staging (granule k = ground 4t+j {x, sep}; self 12+2i {x, sep}, 13+2i {n, code})
+//   LAM  [NCM][WAVE]     lane copy of the contact impulses {ln, l1, l2, 0}; during detection the
+//                        env's body frames [7][3][EPW] and the overflow keys / keep flags
+//   INFO [NCM][2][EPW]   selected contacts {x, sep}, {n, code = 16 la + lb + 1}; at the last
+//                        substep [c][0] = {force, -}
+constexpr int EPW = WAVE / 4;
+constexpr int YG_OFF = 0;
+constexpr int LAM_OFF = YG_OFF + NCM * 4 * WAVE;
+constexpr int INFO_OFF = LAM_OFF + NCM * WAVE;
+constexpr int LDS4 = INFO_OFF + NCM * 2 * EPW;
+static_assert(NB * 3 * EPW <= NCM * WAVE, "frames alias LAM");
+static_assert(2 * EPW * NCAND <= 4 * NCM * WAVE, "keys alias LAM");
+static_assert(12 + 2 * NSELF <= 4 * NCM, "staging fits YG");
+
+struct Q {
+  float4* b;
+  int lane, e, s;
+  __device__ __forceinline__ float4& yg(int c, int r) const { return b[YG_OFF + (c * 4 + r) * WAVE + lane]; }
+  __device__ __forceinline__ float4& yg_at(int c, int r, int ln) const { return b[YG_OFF + (c * 4 + r) * WAVE + ln]; }
+  __device__ __forceinline__ float4& stg(int k) const { return b[YG_OFF + k * WAVE + lane]; }
+  __device__ __forceinline__ float4& lam(int c) const { return b[LAM_OFF + c * WAVE + lane]; }
+  __device__ __forceinline__ float4& lam_at(int c, int ln) const { return b[LAM_OFF + c * WAVE + ln]; }
+  __device__ __forceinline__ float4& info(int c, int h) const { return b[INFO_OFF + (c * 2 + h) * EPW + e]; }
+  __device__ __forceinline__ float4& frame(int body, int r) const { return b[LAM_OFF + (body * 3 + r) * EPW + e]; }
+  __device__ __forceinline__ float* keys() const { return reinterpret_cast<float*>(b + LAM_OFF) + e * NCAND; }
+  __device__ __forceinline__ float* keep() const { return reinterpret_cast<float*>(b + LAM_OFF) + (EPW + e) * NCAND; }
+};
+
+__device__ __forceinline__ void read_frame(const Q& q, int body, float R[9], float p[3]) {
+  const float4 a = q.frame(body, 0), b = q.frame(body, 1), c = q.frame(body, 2);
+  R[0] = a.x; R[1] = a.y; R[2] = a.z; p[0] = a.w;
+  R[3] = b.x; R[4] = b.y; R[5] = b.z; p[1] = b.w;
+  R[6] = c.x; R[7] = c.y; R[8] = c.z; p[2] = c.w;
+}
+__device__ __forceinline__ void mv3f(const float R[9], const float4 v, float o[3]) {
+  const float a[3] = {v.x, v.y, v.z};
+  mv3(R, a, o);
 }
 
-// Ground: the 4 rim points of each of the link's two circles (lowest + 90-degree rotations), the
-// first 4 within the margin per link. Self: inscribed sphere pairs of non-adjacent links behind a
-// sphere-union broadphase (centre = midpoint of a link's two spheres, radius r + half their
-// distance: conservative, so it changes which pairs are tested, never which contacts are found).
-__device__ __forceinline__ int detect(MP m, const zb_task_cfg& cfg, const Kin& k, float Pz,
-                                      const Lane& ld, Stamps& sp) {
-  int nraw = 0;
+// ------------------------------------------------------------------------- contacts
+// Detection + selection for the quad's env; returns the number of contacts (quad-uniform) and
+// leaves them in INFO[0..nc). Ground: lane s tests links 3s..3s+2 (the lowest rim point of each
+// circle + 90-degree rotations, the first 4 within the margin per link). Self: a sphere-union
+// broadphase over the 55 non-adjacent link pairs (centre = midpoint of a link's two spheres,
+// radius r + half their distance: conservative, so it changes which pairs are tested, never which
+// contacts are found), evaluated redundantly; the candidate pairs are split in rank order into 4
+// contiguous chunks, one per lane, so the quad's candidates stay in canonical order lane by lane.
+__device__ __forceinline__ int detect(MP m, const float4* __restrict__ links, const zb_task_cfg& cfg,
+                                      const Kin& k, float Pz, const Q& q, Stamps& sp) {
   const float margin = cfg.contact_margin;
-  const float up[3] = {0.f, 0.f, 1.f};
 #pragma unroll
-  for (int l = 0; l < NL; ++l) {
-    const int b = link_body(l);
-    const float* R = k.R[b];
-    float bc[3], lb4[4];
-    ldc(lb4, m->link_bound[l]);
-    mv3(R, lb4, bc);
-    if (Pz + k.p[b][2] + bc[2] - lb4[3] > margin) continue;
-    float cx[8][3], cs[8];
+  for (int b = 0; b < NB; ++b) {
+    q.frame(b, 0) = make_float4(k.R[b][0], k.R[b][1], k.R[b][2], k.p[b][0]);
+    q.frame(b, 1) = make_float4(k.R[b][3], k.R[b][4], k.R[b][5], k.p[b][1]);
+    q.frame(b, 2) = make_float4(k.R[b][6], k.R[b][7], k.R[b][8], k.p[b][2]);
+  }
+  __syncthreads();
+
+  int taken[3], cnt_g = 0;
 #pragma unroll
-    for (int ci = 0; ci < 2; ++ci) {
-      float cd[9];
-      ldc(cd, m->link_circle[l][ci]);
-      float C[3], E1[3], E2[3];
-      mv3(R, cd, C);
-      mv3(R, cd + 3, E1);
-      mv3(R, cd + 6, E2);
-      C[0] += k.p[b][0]; C[1] += k.p[b][1]; C[2] += k.p[b][2];
-      // lowest rim point, biased toward E1 so a flat disk gets a fixed body-attached manifold
-      const float al = -E1[2] + RIM_EPS, be = -E2[2];
-      const float nrm = sqrtf(al * al + be * be);
-      float c0 = 1.f, s0 = 0.f;
-      if (nrm > 1e-12f) { c0 = al / nrm; s0 = be / nrm; }
+  for (int t = 0; t < 3; ++t) {
+    const int l = 3 * q.s + t;
+    float R[9], p[3];
+    read_frame(q, (l + 1) >> 1, R, p);
+    const float4* L = links + l * LINK4;
+    const float4 bd = L[0];
+    float bc[3];
+    mv3f(R, bd, bc);
+    int tk = 0;
+    if (!(Pz + p[2] + bc[2] - bd.w > margin)) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float cr = r == 0 ? c0 : (r == 1 ? -s0 : (r == 2 ? -c0 : s0));
-        const float sr = r == 0 ? s0 : (r == 1 ? c0 : (r == 2 ? -s0 : -c0));
-        const int idx = ci * 4 + r;
+      for (int ci = 0; ci < 2; ++ci) {
+        float C[3], E1[3], E2[3];
+        mv3f(R, L[1 + 3 * ci], C);
+        mv3f(R, L[2 + 3 * ci], E1);
+        mv3f(R, L[3 + 3 * ci], E2);
+        C[0] += p[0]; C[1] += p[1]; C[2] += p[2];
+        // lowest rim point, biased toward E1 so a flat disk gets a fixed body-attached manifold
+        const float al = -E1[2] + RIM_EPS, be = -E2[2];
+        const float nrm = sqrtf(al * al + be * be);
+        float c0 = 1.f, s0 = 0.f;
+        if (nrm > 1e-12f) { c0 = al / nrm; s0 = be / nrm; }
 #pragma unroll
-        for (int a = 0; a < 3; ++a) cx[idx][a] = C[a] + cr * E1[a] + sr * E2[a];
-        cs[idx] = Pz + cx[idx][2];
+        for (int r = 0; r < 4; ++r) {
+          const float cr = r == 0 ? c0 : (r == 1 ? -s0 : (r == 2 ? -c0 : s0));
+          const float sr = r == 0 ? s0 : (r == 1 ? c0 : (r == 2 ? -s0 : -c0));
+          float x[3];
+#pragma unroll
+          for (int a = 0; a < 3; ++a) x[a] = C[a] + cr * E1[a] + sr * E2[a];
+          const float sep = Pz + x[2];
+          if (sep < margin && tk < 4) {
+            q.stg(4 * t + tk) = make_float4(x[0], x[1], x[2], sep);
+            ++tk;
+          }
+        }
       }
     }
-    int taken = 0;
-#pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      if (cs[t] < margin && taken < 4) {
-        raw_push(ld, nraw, cx[t], cs[t], up, l, -1);
-        ++taken;
-      }
-    }
+    taken[t] = tk;
+    cnt_g += tk;
   }
   sp.mark(1);
+
+  int cnt_s = 0;
   if (cfg.enable_self_collision) {
     m = opaque(m);
-    float ub[NL][3], ur[NL];
     unsigned long long mask = 0ull;
-#pragma unroll
-    for (int l = 0; l < NL; ++l) {
-      float s0[4], s1[4];
-      ldc(s0, m->link_sphere[l][0]);
-      ldc(s1, m->link_sphere[l][1]);
-      const float mid[3] = {0.5f * (s0[0] + s1[0]), 0.5f * (s0[1] + s1[1]), 0.5f * (s0[2] + s1[2])};
-      const float hd = 0.5f * sqrtf((s0[0] - s1[0]) * (s0[0] - s1[0]) + (s0[1] - s1[1]) * (s0[1] - s1[1]) +
-                                    (s0[2] - s1[2]) * (s0[2] - s1[2]));
-      ur[l] = fmaxf(s0[3], s1[3]) + hd;
-      const int b = link_body(l);
-      mv3(k.R[b], mid, ub[l]);
-      ub[l][0] += k.p[b][0]; ub[l][1] += k.p[b][1]; ub[l][2] += k.p[b][2];
-    }
     {
+      float ub[NL][3], ur[NL];
+#pragma unroll
+      for (int l = 0; l < NL; ++l) {
+        float s0[4], s1[4];
+        ldc(s0, m->link_sphere[l][0]);
+        ldc(s1, m->link_sphere[l][1]);
+        const float mid[3] = {0.5f * (s0[0] + s1[0]), 0.5f * (s0[1] + s1[1]), 0.5f * (s0[2] + s1[2])};
+        const float hd = 0.5f * sqrtf((s0[0] - s1[0]) * (s0[0] - s1[0]) + (s0[1] - s1[1]) * (s0[1] - s1[1]) +
+                                      (s0[2] - s1[2]) * (s0[2] - s1[2]));
+        ur[l] = fmaxf(s0[3], s1[3]) + hd;
+        const int b = link_body(l);
+        mv3(k.R[b], mid, ub[l]);
+        ub[l][0] += k.p[b][0]; ub[l][1] += k.p[b][1]; ub[l][2] += k.p[b][2];
+      }
       int pidx = 0;
 #pragma unroll
       for (int la = 0; la < NL; ++la)
@@ -457,55 +492,125 @@ __device__ __forceinline__ int detect(MP m, const zb_task_cfg& cfg, const Kin& k
           if (d0 * d0 + d1 * d1 + d2 * d2 <= rr * rr) mask |= 1ull << pidx;
         }
     }
-    // narrow phase over the (rare) candidate pairs, one code copy
-    while (mask) {
+    const int K = __popcll(mask);
+    const int chunk = (K + 3) >> 2;
+    for (int i = q.s * chunk; i > 0 && mask; --i) mask &= mask - 1ull;
+    for (int j = 0; j < chunk && mask; ++j) {
       const int pidx = __builtin_ctzll(mask);
       mask &= mask - 1ull;
       int la = 0, rem = pidx;
       while (rem >= NL - 2 - la) { rem -= NL - 2 - la; ++la; }
       const int lb = la + 2 + rem;
       float Ra[9], pa[3], Rb[9], pb[3];
-      // body frames of the two links, selected without dynamic register indexing
+      read_frame(q, link_body(la), Ra, pa);
+      read_frame(q, link_body(lb), Rb, pb);
+      const float4* LA = links + la * LINK4;
+      const float4* LB = links + lb * LINK4;
 #pragma unroll
-      for (int bb = 0; bb < NB; ++bb) {
-        if (bb == link_body(la)) {
-#pragma unroll
-          for (int q = 0; q < 9; ++q) Ra[q] = k.R[bb][q];
-          pa[0] = k.p[bb][0]; pa[1] = k.p[bb][1]; pa[2] = k.p[bb][2];
-        }
-        if (bb == link_body(lb)) {
-#pragma unroll
-          for (int q = 0; q < 9; ++q) Rb[q] = k.R[bb][q];
-          pb[0] = k.p[bb][0]; pb[1] = k.p[bb][1]; pb[2] = k.p[bb][2];
-        }
-      }
       for (int sa = 0; sa < 2; ++sa) {
-        float spa[4], xa[3];
-        ldc(spa, m->link_sphere[la][sa]);
-        mv3(Ra, spa, xa);
+        const float4 spa = LA[7 + sa];
+        float xa[3];
+        mv3f(Ra, spa, xa);
         xa[0] += pa[0]; xa[1] += pa[1]; xa[2] += pa[2];
+#pragma unroll
         for (int sb = 0; sb < 2; ++sb) {
-          float spb[4], xb[3];
-          ldc(spb, m->link_sphere[lb][sb]);
-          mv3(Rb, spb, xb);
+          const float4 spb = LB[7 + sb];
+          float xb[3];
+          mv3f(Rb, spb, xb);
           xb[0] += pb[0]; xb[1] += pb[1]; xb[2] += pb[2];
           const float dv[3] = {xa[0] - xb[0], xa[1] - xb[1], xa[2] - xb[2]};
           const float dist = sqrtf(dot3(dv, dv));
-          const float sep = dist - (spa[3] + spb[3]);
-          if (sep < margin && dist > 1e-9f) {
+          const float sep = dist - (spa.w + spb.w);
+          if (sep < margin && dist > 1e-9f && cnt_s < NSELF) {
             float n[3], x[3];
 #pragma unroll
             for (int a = 0; a < 3; ++a) {
               n[a] = dv[a] / dist;
-              x[a] = 0.5f * ((xa[a] - n[a] * spa[3]) + (xb[a] + n[a] * spb[3]));
+              x[a] = 0.5f * ((xa[a] - n[a] * spa.w) + (xb[a] + n[a] * spb.w));
             }
-            raw_push(ld, nraw, x, sep, n, la, lb);
+            q.stg(12 + 2 * cnt_s) = make_float4(x[0], x[1], x[2], sep);
+            q.stg(13 + 2 * cnt_s) = make_float4(n[0], n[1], n[2], (float)(16 * la + lb + 1));
+            ++cnt_s;
           }
         }
       }
     }
   }
-  return insert_raw(ld, nraw);
+
+  // canonical positions: ground lane by lane, then self lane by lane (first NSELF kept)
+  const int packed = cnt_g | (cnt_s << 8);
+  const int pk0 = qbi<0>(packed), pk1 = qbi<1>(packed), pk2 = qbi<2>(packed), pk3 = qbi<3>(packed);
+  const int g_tot = (pk0 & 255) + (pk1 & 255) + (pk2 & 255) + (pk3 & 255);
+  const int s_tot = (pk0 >> 8) + (pk1 >> 8) + (pk2 >> 8) + (pk3 >> 8);
+  const int g_before = (q.s > 0 ? pk0 & 255 : 0) + (q.s > 1 ? pk1 & 255 : 0) + (q.s > 2 ? pk2 & 255 : 0);
+  const int s_before = (q.s > 0 ? pk0 >> 8 : 0) + (q.s > 1 ? pk1 >> 8 : 0) + (q.s > 2 ? pk2 >> 8 : 0);
+  const int my_s = min(cnt_s, max(0, NSELF - s_before));
+  const int n = g_tot + min(s_tot, NSELF);
+  const bool over = n > NCM;
+
+  // overflow (rare): rank every candidate by (sep, canonical index) against the env's list
+  if (__ballot(over) != 0ull) {
+    __syncthreads();  // body frames are dead; KEYS/KEEP alias them
+    if (over) {
+      float* keys = q.keys();
+      int pos = g_before;
+#pragma unroll
+      for (int t = 0; t < 3; ++t)
+        for (int j = 0; j < taken[t]; ++j) keys[pos++] = q.stg(4 * t + j).w;
+      for (int i = 0; i < my_s; ++i) keys[g_tot + s_before + i] = q.stg(12 + 2 * i).w;
+    }
+    __syncthreads();
+    if (over) {
+      const float* keys = q.keys();
+      float* keep = q.keep();
+      auto rank_of = [&](int pos, float sep) {
+        int r = 0;
+        for (int j = 0; j < n; ++j) r += (keys[j] < sep || (keys[j] == sep && j < pos)) ? 1 : 0;
+        return r;
+      };
+      int pos = g_before;
+#pragma unroll
+      for (int t = 0; t < 3; ++t)
+        for (int j = 0; j < taken[t]; ++j, ++pos) keep[pos] = rank_of(pos, keys[pos]) < NCM ? 1.f : 0.f;
+      for (int i = 0; i < my_s; ++i) {
+        const int ps = g_tot + s_before + i;
+        keep[ps] = rank_of(ps, keys[ps]) < NCM ? 1.f : 0.f;
+      }
+    }
+    __syncthreads();
+  }
+  // move the kept candidates into their solver slots
+  {
+    const float* keep = q.keep();
+    auto slot_of = [&](int pos) {
+      if (!over) return pos;
+      if (keep[pos] == 0.f) return -1;
+      int c = 0;
+      for (int j = 0; j < pos; ++j) c += keep[j] != 0.f ? 1 : 0;
+      return c;
+    };
+    int pos = g_before;
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      const float code = (float)(16 * (3 * q.s + t));
+      for (int j = 0; j < taken[t]; ++j, ++pos) {
+        const int c = slot_of(pos);
+        if (c >= 0) {
+          q.info(c, 0) = q.stg(4 * t + j);
+          q.info(c, 1) = make_float4(0.f, 0.f, 1.f, code);
+        }
+      }
+    }
+    for (int i = 0; i < my_s; ++i) {
+      const int c = slot_of(g_tot + s_before + i);
+      if (c >= 0) {
+        q.info(c, 0) = q.stg(12 + 2 * i);
+        q.info(c, 1) = q.stg(13 + 2 * i);
+      }
+    }
+  }
+  __syncthreads();
+  return over ? NCM : n;
 }
 
 __device__ __forceinline__ void tangents(const float n[3], float t1[3], float t2[3]) {
@@ -526,10 +631,44 @@ struct SensorOut {
   float tau2;           // sum of squared Isaac Lab applied torques (torques reward)
 };
 
+// One Gauss-Seidel contact update (normal + Coulomb disk). a0..a2: the lane's row granules
+// {Y_r[3s..3s+2], X_r} (X = invm0, c01, c02), a3 = {invm1, invm2, vmin, -}; lam = {ln, l1, l2}.
+// The three row dots are reduced across the quad; the tangent velocities see the normal update
+// through the cross terms. Returns the new impulses; w0..w2 (the lane's coordinates) updated.
+__device__ __forceinline__ float4 pgs_update(const float4 a0, const float4 a1, const float4 a2, const float4 a3,
+                                             const float4 lam, float mu, float& w0, float& w1, float& w2) {
+  const float p0 = qsum(a0.x * w0 + a0.y * w1 + a0.z * w2);
+  const float p1 = qsum(a1.x * w0 + a1.y * w1 + a1.z * w2);
+  const float p2 = qsum(a2.x * w0 + a2.y * w1 + a2.z * w2);
+  const float ln = fmaxf(lam.x + (a3.z - p0) * a0.w, 0.f);
+  const float dl = ln - lam.x;
+  const float vt1 = p1 + a1.w * dl, vt2 = p2 + a2.w * dl;
+  float l1 = lam.y - vt1 * a3.x;
+  float l2 = lam.z - vt2 * a3.y;
+  const float lim = mu * ln;
+  const float mag2 = l1 * l1 + l2 * l2;
+  if (mag2 > lim * lim) {
+    const float sc = lim * __builtin_amdgcn_rsqf(mag2);  // mag2 > 0 here
+    l1 *= sc; l2 *= sc;
+  }
+  const float d1 = l1 - lam.y, d2 = l2 - lam.z;
+  w0 += a0.x * dl + a1.x * d1 + a2.x * d2;
+  w1 += a0.y * dl + a1.y * d1 + a2.y * d2;
+  w2 += a0.z * dl + a1.z * d1 + a2.z * d2;
+  return make_float4(ln, l1, l2, 0.f);
+}
+
+// write the 3 granules of a 12-vector split over the quad's lanes: lane s' gets v[3s'..3s'+2]
+__device__ __forceinline__ void put_split(const Q& q, int c, int r, const float v[NV], float x) {
+  const int base = 4 * q.e;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) q.yg_at(c, r, base + k) = make_float4(v[3 * k], v[3 * k + 1], v[3 * k + 2], x);
+}
+
 // ------------------------------------------------------------------------- one substep
 template <bool kDebugForces>
-__device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
-                                        const float target[ND], const Lane& ld, bool last, SensorOut& so,
+__device__ __forceinline__ void substep(MP m0, const float4* __restrict__ links, const zb_task_cfg& cfg, Phys& s,
+                                        const float target[ND], const Q& q, bool last, SensorOut& so,
                                         float (*dbgF)[3], float* dbgTau, Stamps& sp) {
   const float dt = cfg.sim_dt;
   MP m = opaque(m0);
@@ -548,10 +687,11 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
   float S[ND][6], org[ND][3];
   SI I[NB];
   int nc;
+  __syncthreads();  // the previous substep's LDS readers are done (frames alias LAM)
   {
     Kin k;
     fk(m, s, k);
-    nc = detect(opaque(m0), cfg, k, s.pos[2], ld, sp);
+    nc = detect(opaque(m0), links, cfg, k, s.pos[2], q, sp);
     sp.mark(2);
     m = opaque(m0);
 #pragma unroll
@@ -706,124 +846,158 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
   }
 
   sp.mark(4);
-  // contact rows: Y = L^-1 J^T (whitened), effective masses and bias velocities.
-  // J of direction d at point x on body b: [x x d ; d ; d.(a_j x (x - o_j)) for joints j < b]
-  for (int c = 0; c < nc; ++c) {
-    const float4 g0 = ld.g(c, 0), gn = ld.g(c, G_N);
-    const float la_f = ld.g(c, G_LAM).w;
-    const float x[3] = {g0.x, g0.y, g0.z};
-    const float n[3] = {gn.x, gn.y, gn.z};
-    const float sep = g0.w;
-    const int ba = link_body((int)la_f);
-    const int lb = (int)gn.w;
-    const int bb = lb >= 0 ? link_body(lb) : -1;
-    // per-joint lever vectors a_j x (x - o_j), signed by which side of the contact the joint is on
-    float cj[ND][3];
+  // contact rows (lane s builds slots s, s+4, s+8): Y = L^-1 J^T (whitened), effective masses,
+  // the normal/tangent cross terms and the bias velocity. J of direction d at point x on body b:
+  // [x x d ; d ; d.(a_j x (x - o_j)) for joints j < b]
 #pragma unroll
-    for (int j = 0; j < ND; ++j) {
-      const float xo[3] = {x[0] - org[j][0], x[1] - org[j][1], x[2] - org[j][2]};
-      float c3[3];
-      cross3(S[j], xo, c3);
-      const float sg = (j < ba ? 1.f : 0.f) - (j < bb ? 1.f : 0.f);
-      cj[j][0] = sg * c3[0]; cj[j][1] = sg * c3[1]; cj[j][2] = sg * c3[2];
+  for (int t = 0; t < 3; ++t) {
+    const int c = q.s + 4 * t;
+    if (c < nc) {
+      const float4 g0 = q.info(c, 0), gn = q.info(c, 1);
+      const float x[3] = {g0.x, g0.y, g0.z};
+      const float n[3] = {gn.x, gn.y, gn.z};
+      const float sep = g0.w;
+      const int code = (int)gn.w;
+      const int ba = link_body(code >> 4);
+      const int lb = (code & 15) - 1;
+      const int bb = lb >= 0 ? link_body(lb) : -1;
+      // per-joint lever vectors a_j x (x - o_j), signed by which side of the contact the joint is on
+      float cj[ND][3];
+#pragma unroll
+      for (int j = 0; j < ND; ++j) {
+        const float xo[3] = {x[0] - org[j][0], x[1] - org[j][1], x[2] - org[j][2]};
+        float c3[3];
+        cross3(S[j], xo, c3);
+        const float sg = (j < ba ? 1.f : 0.f) - (j < bb ? 1.f : 0.f);
+        cj[j][0] = sg * c3[0]; cj[j][1] = sg * c3[1]; cj[j][2] = sg * c3[2];
+      }
+      const float root = bb >= 0 ? 0.f : 1.f;  // self contacts: the root terms cancel
+      float t1[3], t2[3];
+      tangents(n, t1, t2);
+      float invm[3], Y0[NV];
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        float d[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) d[a] = r == 0 ? n[a] : (r == 1 ? t1[a] : t2[a]);
+        float J[NV], Y[NV];
+        float xd[3];
+        cross3(x, d, xd);
+        J[0] = root * xd[0]; J[1] = root * xd[1]; J[2] = root * xd[2];
+        J[3] = root * d[0]; J[4] = root * d[1]; J[5] = root * d[2];
+#pragma unroll
+        for (int j = 0; j < ND; ++j) J[6 + j] = dot3(cj[j], d);
+        fwd_sub(L, Li, J, Y);
+        invm[r] = 1.f / (dot12(Y, Y) + 1e-9f);
+        if (r == 0) {
+#pragma unroll
+          for (int a = 0; a < NV; ++a) Y0[a] = Y[a];
+          put_split(q, c, 0, Y, invm[0]);
+        } else {
+          put_split(q, c, r, Y, dot12(Y, Y0));  // c01 / c02
+        }
+      }
+      float vmin;
+      if (sep >= 0.f) vmin = -sep / dt;
+      else vmin = fminf(cfg.baumgarte * (-sep) / dt, m->max_depenetration_velocity);
+      const int base = 4 * q.e;
+#pragma unroll
+      for (int kq = 0; kq < 4; ++kq) {
+        q.yg_at(c, 3, base + kq) = make_float4(invm[1], invm[2], vmin, 0.f);
+        q.lam_at(c, base + kq) = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
     }
-    const float root = bb >= 0 ? 0.f : 1.f;  // self contacts: the root terms cancel
-    float t1[3], t2[3];
-    tangents(n, t1, t2);
-    float invm[3];
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-      float d[3];
-#pragma unroll
-      for (int a = 0; a < 3; ++a) d[a] = r == 0 ? n[a] : (r == 1 ? t1[a] : t2[a]);
-      float J[NV], Y[NV];
-      float xd[3];
-      cross3(x, d, xd);
-      J[0] = root * xd[0]; J[1] = root * xd[1]; J[2] = root * xd[2];
-      J[3] = root * d[0]; J[4] = root * d[1]; J[5] = root * d[2];
-#pragma unroll
-      for (int j = 0; j < ND; ++j) J[6 + j] = dot3(cj[j], d);
-      fwd_sub(L, Li, J, Y);
-      invm[r] = 1.f / (dot12(Y, Y) + 1e-9f);
-#pragma unroll
-      for (int q = 0; q < 3; ++q) ld.g(c, 3 * r + q) = make_float4(Y[4 * q], Y[4 * q + 1], Y[4 * q + 2], Y[4 * q + 3]);
-    }
-    float vmin;
-    if (sep >= 0.f) vmin = -sep / dt;
-    else vmin = fminf(cfg.baumgarte * (-sep) / dt, m->max_depenetration_velocity);
-    ld.g(c, G_INVM) = make_float4(invm[0], invm[1], invm[2], vmin);
   }
+  __syncthreads();
 
   sp.mark(5);
-  // projected Gauss-Seidel on the whitened velocity (Coulomb disk friction); each contact's three
-  // rows are read once (9 ds_read_b128) and kept in registers for its update
-  const float mu = cfg.friction;
-  for (int it = 0; it < cfg.solver_iterations; ++it) {
-    for (int c = 0; c < nc; ++c) {
-      float y0[NV], y1[NV], y2[NV];
-#pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        const float4 a0 = ld.g(c, q), a1 = ld.g(c, 3 + q), a2 = ld.g(c, 6 + q);
-        y0[4 * q] = a0.x; y0[4 * q + 1] = a0.y; y0[4 * q + 2] = a0.z; y0[4 * q + 3] = a0.w;
-        y1[4 * q] = a1.x; y1[4 * q + 1] = a1.y; y1[4 * q + 2] = a1.z; y1[4 * q + 3] = a1.w;
-        y2[4 * q] = a2.x; y2[4 * q + 1] = a2.y; y2[4 * q + 2] = a2.z; y2[4 * q + 3] = a2.w;
-      }
-      const float4 im = ld.g(c, G_INVM);
-      float4 lam = ld.g(c, G_LAM);
-      const float vn = dot12(y0, w);
-      const float ln = fmaxf(lam.x + (im.w - vn) * im.x, 0.f);
-      const float dl = ln - lam.x;
-#pragma unroll
-      for (int a = 0; a < NV; ++a) w[a] += y0[a] * dl;
-      const float vt1 = dot12(y1, w), vt2 = dot12(y2, w);
-      float l1 = lam.y - vt1 * im.y;
-      float l2 = lam.z - vt2 * im.z;
-      const float lim = mu * ln;
-      const float mag2 = l1 * l1 + l2 * l2;
-      if (mag2 > lim * lim) {
-        const float sc = lim / sqrtf(mag2);
-        l1 *= sc; l2 *= sc;
-      }
-      const float d1 = l1 - lam.y, d2 = l2 - lam.z;
-#pragma unroll
-      for (int a = 0; a < NV; ++a) w[a] += y1[a] * d1 + y2[a] * d2;
-      lam.x = ln; lam.y = l1; lam.z = l2;
-      ld.g(c, G_LAM) = lam;
+  // projected Gauss-Seidel on the whitened velocity (Coulomb disk friction). Lane s owns
+  // w[3s..3s+2]; per contact: 4 granule reads + the impulse, three quad-reduced row dots.
+  {
+    const float mu = cfg.friction;
+    float w0, w1, w2;
+    {
+      const int s3 = q.s;
+      w0 = s3 == 0 ? w[0] : (s3 == 1 ? w[3] : (s3 == 2 ? w[6] : w[9]));
+      w1 = s3 == 0 ? w[1] : (s3 == 1 ? w[4] : (s3 == 2 ? w[7] : w[10]));
+      w2 = s3 == 0 ? w[2] : (s3 == 1 ? w[5] : (s3 == 2 ? w[8] : w[11]));
     }
+    // The sweep is flattened to K = iterations x nc contact updates and unrolled by two with
+    // ping-pong register sets: the granules and impulse of update k+1 are read while update k
+    // computes. With one contact the prefetched impulse is the one being updated (forwarded).
+    const int K = cfg.solver_iterations * nc;
+    int cA = 0;
+    float4 A0 = q.yg(0, 0), A1 = q.yg(0, 1), A2 = q.yg(0, 2), A3 = q.yg(0, 3), LA = q.lam(0);
+    for (int k = 0; k < K; k += 2) {
+      const int cB = cA + 1 == nc ? 0 : cA + 1;
+      const float4 B0 = q.yg(cB, 0), B1 = q.yg(cB, 1), B2 = q.yg(cB, 2), B3 = q.yg(cB, 3);
+      float4 LB = q.lam(cB);
+      const float4 nA = pgs_update(A0, A1, A2, A3, LA, mu, w0, w1, w2);
+      q.lam(cA) = nA;
+      if (cB == cA) LB = nA;
+      if (k + 1 < K) {
+        const int cA2 = cB + 1 == nc ? 0 : cB + 1;
+        A0 = q.yg(cA2, 0); A1 = q.yg(cA2, 1); A2 = q.yg(cA2, 2); A3 = q.yg(cA2, 3);
+        LA = q.lam(cA2);
+        const float4 nB = pgs_update(B0, B1, B2, B3, LB, mu, w0, w1, w2);
+        q.lam(cB) = nB;
+        if (cA2 == cB) LA = nB;
+        cA = cA2;
+      }
+    }
+    w[0] = qb<0>(w0); w[1] = qb<0>(w1); w[2] = qb<0>(w2);
+    w[3] = qb<1>(w0); w[4] = qb<1>(w1); w[5] = qb<1>(w2);
+    w[6] = qb<2>(w0); w[7] = qb<2>(w1); w[8] = qb<2>(w2);
+    w[9] = qb<3>(w0); w[10] = qb<3>(w1); w[11] = qb<3>(w2);
   }
   sp.mark(6);
   float un[NV];
   bwd_sub(L, Li, w, un);
 
   if (last) {
-    // ContactSensor inputs: net force on the feet, max |net force| over undesired links
-    float Fl[NL][3];
+    // ContactSensor inputs: net force on the feet, max |net force| over undesired links.
+    // Lane s forms the forces of its slots, then sums the env's contacts onto links 3s..3s+2.
 #pragma unroll
-    for (int l = 0; l < NL; ++l) Fl[l][0] = Fl[l][1] = Fl[l][2] = 0.f;
+    for (int t = 0; t < 3; ++t) {
+      const int c = q.s + 4 * t;
+      if (c < nc) {
+        const float4 gn = q.info(c, 1), lam = q.lam(c);
+        const float n[3] = {gn.x, gn.y, gn.z};
+        float t1[3], t2[3];
+        tangents(n, t1, t2);
+        float f[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) f[a] = (lam.x * n[a] + lam.y * t1[a] + lam.z * t2[a]) / dt;
+        q.info(c, 0) = make_float4(f[0], f[1], f[2], gn.w);
+      }
+    }
+    __syncthreads();
+    float Fl[3][3];
+#pragma unroll
+    for (int t = 0; t < 3; ++t) Fl[t][0] = Fl[t][1] = Fl[t][2] = 0.f;
     for (int c = 0; c < nc; ++c) {
-      const float4 gn = ld.g(c, G_N), lam = ld.g(c, G_LAM);
-      const float n[3] = {gn.x, gn.y, gn.z};
-      float t1[3], t2[3];
-      tangents(n, t1, t2);
-      float f[3];
+      const float4 f = q.info(c, 0);
+      const int code = (int)f.w;
+      const int la = code >> 4, lb = (code & 15) - 1;
 #pragma unroll
-      for (int a = 0; a < 3; ++a) f[a] = (lam.x * n[a] + lam.y * t1[a] + lam.z * t2[a]) / dt;
-      const int la = (int)lam.w, lb = (int)gn.w;
-#pragma unroll
-      for (int l = 0; l < NL; ++l) {
+      for (int t = 0; t < 3; ++t) {
+        const int l = 3 * q.s + t;
         const float sa = (l == la ? 1.f : 0.f) - (l == lb ? 1.f : 0.f);
-        Fl[l][0] += sa * f[0]; Fl[l][1] += sa * f[1]; Fl[l][2] += sa * f[2];
+        Fl[t][0] += sa * f.x; Fl[t][1] += sa * f.y; Fl[t][2] += sa * f.z;
       }
     }
     float fmax = 0.f;
 #pragma unroll
-    for (int l = 1; l <= 10; ++l) fmax = fmaxf(fmax, sqrtf(dot3(Fl[l], Fl[l])));
-    so.undes_fmax = fmax;
+    for (int t = 0; t < 3; ++t) {
+      const int l = 3 * q.s + t;
+      if (l >= 1 && l <= 10) fmax = fmaxf(fmax, sqrtf(dot3(Fl[t], Fl[t])));
+    }
+    so.undes_fmax = qmax(fmax);
 #pragma unroll
-    for (int a = 0; a < 3; ++a) { so.feet_f[0][a] = Fl[0][a]; so.feet_f[1][a] = Fl[11][a]; }
+    for (int a = 0; a < 3; ++a) { so.feet_f[0][a] = qb<0>(Fl[0][a]); so.feet_f[1][a] = qb<3>(Fl[2][a]); }
     if (kDebugForces)
 #pragma unroll
-      for (int l = 0; l < NL; ++l) { dbgF[l][0] = Fl[l][0]; dbgF[l][1] = Fl[l][1]; dbgF[l][2] = Fl[l][2]; }
+      for (int t = 0; t < 3; ++t) { dbgF[t][0] = Fl[t][0]; dbgF[t][1] = Fl[t][1]; dbgF[t][2] = Fl[t][2]; }
   }
 
 #pragma unroll
@@ -857,10 +1031,10 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
 #pragma unroll
   for (int j = 0; j < ND; ++j) {
     s.jqd[j] = un[6 + j];
-    float q = s.jq[j] + dt * s.jqd[j];
-    if (q > TWO_PI_F) q -= 2.f * TWO_PI_F;
-    else if (q < -TWO_PI_F) q += 2.f * TWO_PI_F;
-    s.jq[j] = q;
+    float qv = s.jq[j] + dt * s.jqd[j];
+    if (qv > TWO_PI_F) qv -= 2.f * TWO_PI_F;
+    else if (qv < -TWO_PI_F) qv += 2.f * TWO_PI_F;
+    s.jq[j] = qv;
   }
 }
 
@@ -1073,16 +1247,20 @@ __device__ __forceinline__ void load_phys(const float* __restrict__ st, int N, i
 // One policy step per lane. Live state across the 4 substeps is kept to the physics state, the
 // joint targets and the ~15 floats of the lagged observation cache the rewards need; the MDP
 // state is loaded from HBM only after the physics.
-__global__ __launch_bounds__(WAVE, 1) void zb_step_kernel(const zb_model* __restrict__ mg, zb_task_cfg cfg, int N,
+__global__ __launch_bounds__(WAVE, 1) void zb_step_kernel(const zb_model* __restrict__ mg,
+                                                          const float4* __restrict__ links, zb_task_cfg cfg, int N,
                                                           float* __restrict__ st, const float* __restrict__ act,
                                                           float* __restrict__ obs, float* __restrict__ rew,
                                                           uint8_t* __restrict__ term, uint8_t* __restrict__ trunc,
                                                           float* __restrict__ acc) {
   MP m = to_mp(mg);
-  __shared__ __attribute__((aligned(16))) float lds[LDS_FLOATS];
-  const int i = blockIdx.x * WAVE + threadIdx.x;
-  if (i >= N) return;
-  const Lane ld{reinterpret_cast<float4*>(lds) + threadIdx.x};
+  __shared__ float4 lds[LDS4];
+  const int lane = threadIdx.x;
+  const int env = blockIdx.x * EPW + (lane >> 2);
+  // a quad past N recomputes env N-1 (identical values, identical stores); it never logs
+  const int i = env < N ? env : N - 1;
+  const bool lead = env < N && (lane & 3) == 0;
+  const Q q{lds, lane, lane >> 2, lane & 3};
 #define ST(f) st[(size_t)(f) * N + i]
   Stamps sp;
   sp.begin();
@@ -1135,7 +1313,7 @@ __global__ __launch_bounds__(WAVE, 1) void zb_step_kernel(const zb_model* __rest
   SensorOut so;
   sp.mark(0);
   for (int k = 0; k < cfg.decimation; ++k) {
-    substep<false>(m, cfg, p, target, ld, k == cfg.decimation - 1, so, nullptr, nullptr, sp);
+    substep<false>(m, links, cfg, p, target, q, k == cfg.decimation - 1, so, nullptr, nullptr, sp);
     sp.mark(7);
   }
   m = opaque(m);
@@ -1252,16 +1430,18 @@ __global__ __launch_bounds__(WAVE, 1) void zb_step_kernel(const zb_model* __rest
     reward += v;
     const float sum = ST(ZB_S_EP_SUMS + t) + v;
     ST(ZB_S_EP_SUMS + t) = reset ? 0.f : sum;
-    if (reset) atomicAdd(&acc[t], sum);   // episode log (v2.py:441-448)
+    if (reset && lead) atomicAdd(&acc[t], sum);   // episode log (v2.py:441-448)
   }
   if (died) reward -= cfg.terminal_penalty;  // v2.py:379-380
   ST(ZB_S_EP_LEN) = reset ? 0.f : ep_len;
 
   // in-kernel auto-reset (v2.py:413-459); the state written above is overwritten for reset envs
   if (reset) {
-    atomicAdd(&acc[13], 1.f);
-    if (died) atomicAdd(&acc[14], 1.f);
-    if (time_out) atomicAdd(&acc[15], 1.f);
+    if (lead) {
+      atomicAdd(&acc[13], 1.f);
+      if (died) atomicAdd(&acc[14], 1.f);
+      if (time_out) atomicAdd(&acc[15], 1.f);
+    }
     Mdp d;
     load_state(st, N, i, p, d);
     reset_env(m, p, d);
@@ -1343,28 +1523,30 @@ __global__ void zb_observe_kernel(const zb_model* __restrict__ mg, int N, const 
   write_obs(m, p, d, obs, i);
 }
 
-__global__ __launch_bounds__(WAVE, 1) void zb_substeps_kernel(const zb_model* __restrict__ mg, zb_task_cfg cfg, int N,
+__global__ __launch_bounds__(WAVE, 1) void zb_substeps_kernel(const zb_model* __restrict__ mg,
+                                                              const float4* __restrict__ links, zb_task_cfg cfg, int N,
                                                               float* __restrict__ st, const float* __restrict__ targets,
                                                               int nsub, float* __restrict__ net_force,
                                                               float* __restrict__ tau_out) {
   MP m = to_mp(mg);
-  __shared__ __attribute__((aligned(16))) float lds[LDS_FLOATS];
-  const int i = blockIdx.x * WAVE + threadIdx.x;
-  if (i >= N) return;
-  const Lane ld{reinterpret_cast<float4*>(lds) + threadIdx.x};
+  __shared__ float4 lds[LDS4];
+  const int lane = threadIdx.x;
+  const int env = blockIdx.x * EPW + (lane >> 2);
+  const int i = env < N ? env : N - 1;
+  const Q q{lds, lane, lane >> 2, lane & 3};
   Phys p;
   load_phys(st, N, i, p);
-  float tg[ND], tau[ND], F[NL][3];
+  float tg[ND], tau[ND], F[3][3];
 #pragma unroll
   for (int j = 0; j < ND; ++j) { tg[j] = targets[(size_t)i * ND + j]; tau[j] = 0.f; }
   SensorOut so;
   Stamps sp;
-  for (int k = 0; k < nsub; ++k) substep<true>(m, cfg, p, tg, ld, k == nsub - 1, so, F, tau, sp);
+  for (int k = 0; k < nsub; ++k) substep<true>(m, links, cfg, p, tg, q, k == nsub - 1, so, F, tau, sp);
   if (net_force)
 #pragma unroll
-    for (int l = 0; l < NL; ++l)
+    for (int t = 0; t < 3; ++t)
 #pragma unroll
-      for (int a = 0; a < 3; ++a) net_force[((size_t)i * NL + l) * 3 + a] = F[l][a];
+      for (int a = 0; a < 3; ++a) net_force[((size_t)i * NL + 3 * q.s + t) * 3 + a] = F[t][a];
   if (tau_out)
 #pragma unroll
     for (int j = 0; j < ND; ++j) tau_out[(size_t)i * ND + j] = tau[j];
@@ -1388,6 +1570,7 @@ struct zb_sim {
   uint64_t calls;
   zb_task_cfg cfg;
   zb_model* d_model;
+  float4* d_links;  // per-link collision table [NL][LINK4] (detect)
   float* d_state;
   float* d_acc;
   float* d_log_means;
@@ -1454,6 +1637,24 @@ int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_dev
   HIPCHK(hipMalloc(&h->d_log_means, sizeof(float) * ZB_NUM_REWARD_TERMS), "hipMalloc log");
   HIPCHK(hipMalloc(&h->d_log_counts, sizeof(int32_t) * 2), "hipMalloc log");
   HIPCHK(hipMemcpy(h->d_model, m, sizeof(zb_model), hipMemcpyHostToDevice), "hipMemcpy model");
+  {
+    float4 tab[NL * LINK4];
+    for (int l = 0; l < NL; ++l) {
+      float4* t = tab + l * LINK4;
+      t[0] = make_float4(m->link_bound[l][0], m->link_bound[l][1], m->link_bound[l][2], m->link_bound[l][3]);
+      for (int ci = 0; ci < 2; ++ci)
+        for (int v = 0; v < 3; ++v) {
+          const float* c = m->link_circle[l][ci] + 3 * v;
+          t[1 + 3 * ci + v] = make_float4(c[0], c[1], c[2], 0.f);
+        }
+      for (int sp = 0; sp < 2; ++sp) {
+        const float* c = m->link_sphere[l][sp];
+        t[7 + sp] = make_float4(c[0], c[1], c[2], c[3]);
+      }
+    }
+    HIPCHK(hipMalloc(&h->d_links, sizeof(tab)), "hipMalloc links");
+    HIPCHK(hipMemcpy(h->d_links, tab, sizeof(tab), hipMemcpyHostToDevice), "hipMemcpy links");
+  }
   HIPCHK(hipMemset(h->d_state, 0, sizeof(float) * (size_t)ZB_STATE_DIM * num_envs), "hipMemset state");
   HIPCHK(hipMemset(h->d_log_means, 0, sizeof(float) * ZB_NUM_REWARD_TERMS), "hipMemset log");
   HIPCHK(hipMemset(h->d_log_counts, 0, sizeof(int32_t) * 2), "hipMemset log");
@@ -1520,6 +1721,7 @@ void zb_destroy(zb_handle h) {
   prof_free(h);
   (void)hipSetDevice(h->device);
   (void)hipFree(h->d_model);
+  (void)hipFree(h->d_links);
   (void)hipFree(h->d_state);
   (void)hipFree(h->d_acc);
   (void)hipFree(h->d_log_means);
@@ -1549,10 +1751,10 @@ int zb_step(zb_handle h, const float* actions, float* obs, float* reward, uint8_
   if (!h || !actions || !obs || !reward || !terminated || !truncated) return set_err(-1, "zb_step", hipSuccess);
   hipStream_t s = (hipStream_t)stream;
   HIPCHK(hipMemsetAsync(h->d_acc, 0, sizeof(float) * ACC, s), "hipMemsetAsync acc");
-  const int blocks = (h->n + WAVE - 1) / WAVE;
+  const int blocks = (h->n + EPW - 1) / EPW;
   const bool prof = h->prof_n < h->prof_max;
   if (prof) HIPCHK(hipEventRecord(h->prof_ev[2 * h->prof_n], s), "hipEventRecord");
-  zb_step_kernel<<<blocks, WAVE, 0, s>>>(h->d_model, h->cfg, h->n, h->d_state, actions, obs, reward, terminated,
+  zb_step_kernel<<<blocks, WAVE, 0, s>>>(h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward, terminated,
                                          truncated, h->d_acc);
   int rc = launch_check("zb_step_kernel");
   if (prof) {
@@ -1603,8 +1805,8 @@ int zb_set_state(zb_handle h, const float* src, void* stream) {
 int zb_physics_substeps(zb_handle h, const float* targets, int nsub, float* net_force, float* applied_torque,
                         void* stream) {
   if (!h || !targets || nsub < 1) return set_err(-1, "zb_physics_substeps", hipSuccess);
-  const int blocks = (h->n + WAVE - 1) / WAVE;
-  zb_substeps_kernel<<<blocks, WAVE, 0, (hipStream_t)stream>>>(h->d_model, h->cfg, h->n, h->d_state, targets, nsub,
+  const int blocks = (h->n + EPW - 1) / EPW;
+  zb_substeps_kernel<<<blocks, WAVE, 0, (hipStream_t)stream>>>(h->d_model, h->d_links, h->cfg, h->n, h->d_state, targets, nsub,
                                                                net_force, applied_torque);
   return launch_check("zb_substeps_kernel");
 }
