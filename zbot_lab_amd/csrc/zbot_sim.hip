@@ -114,6 +114,35 @@ __device__ __forceinline__ void qnormalize(float q[4]) {
 }
 __device__ __forceinline__ float clampf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
 
+// sin/cos with Cody-Waite reduction by pi/2 and Cephes minimax polynomials on [-pi/4, pi/4]
+// (<= 2 ulp for the half joint angles and rotation angles seen here, |x| < 1e3; no Payne-Hanek
+// slow path, which would otherwise be inlined at each of the ~40 call sites of the kernel).
+__device__ __forceinline__ void sincos_r(float x, float* sn, float* cs) {
+  const float kf = rintf(x * 0.636619772367581343f);
+  const int k = (int)kf;
+  float r = fmaf(-kf, 1.57079637050628662f, x);
+  r = fmaf(kf, 4.37113900018624283e-8f, r);
+  const float z = r * r;
+  const float sp = fmaf(fmaf(fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f), z, -1.6666654611e-1f), z * r, r);
+  const float cp = fmaf(fmaf(fmaf(fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f), z, 4.166664568298827e-2f), z,
+                             -0.5f), z, 1.f);
+  const float s0 = (k & 1) ? cp : sp;
+  const float c0 = (k & 1) ? sp : cp;
+  *sn = (k & 2) ? -s0 : s0;
+  *cs = ((k + 1) & 2) ? -c0 : c0;
+}
+// tanh: Cephes odd polynomial below 0.625, 1 - 2 / (exp(2|x|) + 1) above (~1e-7 abs)
+__device__ __forceinline__ float tanh_r(float x) {
+  const float ax = fabsf(x);
+  if (ax < 0.625f) {
+    const float z = x * x;
+    return fmaf(fmaf(fmaf(fmaf(fmaf(-5.70498872745e-3f, z, 2.06390887954e-2f), z, -5.37397155531e-2f), z,
+                          1.33314422036e-1f), z, -3.33332819422e-1f), z * x, x);
+  }
+  const float e = __expf(2.f * fminf(ax, 20.f));
+  return copysignf(1.f - 2.f * __builtin_amdgcn_rcpf(e + 1.f), x);
+}
+
 __host__ __device__ __forceinline__ uint64_t hash64(uint64_t x) {
   x += 0x9E3779B97F4A7C15ull;
   x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -150,7 +179,7 @@ __device__ __forceinline__ void fk(MP m, const Phys& s, Kin& k) {
 #pragma unroll
     for (int a = 0; a < 3; ++a) { k.org[j][a] = k.p[j][a] + t[a]; k.ax[j][a] = Rj[3 * a + 2]; }
     float sn, cs;
-    sincosf(0.5f * s.jq[j], &sn, &cs);
+    sincos_r(0.5f * s.jq[j], &sn, &cs);
     const float qz[4] = {cs, 0.f, 0.f, sn};
     float qa[4], Ra[9];
     qmul(qj, qz, qa);
@@ -349,8 +378,14 @@ template <int K>
 __device__ __forceinline__ int qbi(int x) { return dppi<K * 0x55>(x); }
 
 // Device-side per-link collision table (built by zb_create), float4-aligned for per-lane loads:
-// [0] bounding sphere, [1+3ci..3+3ci] circle ci: C, E1, E2 (body frame), [7], [8] inscribed spheres.
-constexpr int LINK4 = 9;
+// [0] bounding sphere, [1+3ci..3+3ci] circle ci: C, E1, E2 (body frame), [7], [8] inscribed spheres,
+// [9] union sphere of the two (midpoint, max r + half their distance + 1 um) for the broadphase.
+// After the NL links: the self-pair list as ints (16 la + lb), NPAIR of them.
+constexpr int LINK4 = 10;
+constexpr int NPAIR = (NL - 1) * (NL - 2) / 2;  // non-adjacent link pairs (55), checked by zb_create
+constexpr int PAIR_CHUNK = (NPAIR + 3) / 4;  // broadphase pairs per lane
+constexpr int DFLT_OFF = NL * LINK4 + (NPAIR + 3) / 4;  // default-pose feet positions, base quat
+constexpr int LNK4 = DFLT_OFF + 3;
 
 // Candidate list in canonical order: ground (link by link, <= 4 each), then self candidates in
 // (pair, sphere a, sphere b) order, at most NSELF. More than NCM candidates: the NCM smallest by
@@ -363,14 +398,19 @@ constexpr int NCAND = NL * 4 + NSELF;
 //                        r = 3 {invm1, invm2, vmin, 0}. During detection: the lane's candidate
 //                        staging (granule k = ground 4t+j {x, sep}; self 12+2i {x, sep}, 13+2i {n, code})
 //   LAM  [NCM][WAVE]     lane copy of the contact impulses {ln, l1, l2, 0}; during detection the
-//                        env's body frames [7][3][EPW] and the overflow keys / keep flags
+//                        env's body frames [7][3][EPW], union spheres [NL][EPW], then the
+//                        overflow keys / keep flags
 //   INFO [NCM][2][EPW]   selected contacts {x, sep}, {n, code = 16 la + lb + 1}; at the last
 //                        substep [c][0] = {force, -}
+//   LNK  [NL][LINK4]     the link collision table, copied once per workgroup (per-lane reads)
 constexpr int EPW = WAVE / 4;
 constexpr int YG_OFF = 0;
 constexpr int LAM_OFF = YG_OFF + NCM * 4 * WAVE;
 constexpr int INFO_OFF = LAM_OFF + NCM * WAVE;
-constexpr int LDS4 = INFO_OFF + NCM * 2 * EPW;
+constexpr int LNK_OFF = INFO_OFF + NCM * 2 * EPW;  // copy of the link table (LNK4 granules)
+constexpr int LDS4 = LNK_OFF + LNK4;
+constexpr int UB_OFF = LAM_OFF + NB * 3 * EPW;     // [NL][EPW] world union spheres (aliases LAM)
+static_assert(NB * 3 * EPW + NL * EPW <= NCM * WAVE, "frames + union spheres alias LAM");
 static_assert(NB * 3 * EPW <= NCM * WAVE, "frames alias LAM");
 static_assert(2 * EPW * NCAND <= 4 * NCM * WAVE, "keys alias LAM");
 static_assert(12 + 2 * NSELF <= 4 * NCM, "staging fits YG");
@@ -385,6 +425,10 @@ struct Q {
   __device__ __forceinline__ float4& lam_at(int c, int ln) const { return b[LAM_OFF + c * WAVE + ln]; }
   __device__ __forceinline__ float4& info(int c, int h) const { return b[INFO_OFF + (c * 2 + h) * EPW + e]; }
   __device__ __forceinline__ float4& frame(int body, int r) const { return b[LAM_OFF + (body * 3 + r) * EPW + e]; }
+  __device__ __forceinline__ const float4* link(int l) const { return b + LNK_OFF + l * LINK4; }
+  __device__ __forceinline__ int pair_code(int p) const { return reinterpret_cast<const int*>(b + LNK_OFF + NL * LINK4)[p]; }
+  __device__ __forceinline__ const float4* dflt() const { return b + LNK_OFF + DFLT_OFF; }
+  __device__ __forceinline__ float4& ub(int l) const { return b[UB_OFF + l * EPW + e]; }
   __device__ __forceinline__ float* keys() const { return reinterpret_cast<float*>(b + LAM_OFF) + e * NCAND; }
   __device__ __forceinline__ float* keep() const { return reinterpret_cast<float*>(b + LAM_OFF) + (EPW + e) * NCAND; }
 };
@@ -408,7 +452,7 @@ __device__ __forceinline__ void mv3f(const float R[9], const float4 v, float o[3
 // radius r + half their distance: conservative, so it changes which pairs are tested, never which
 // contacts are found), evaluated redundantly; the candidate pairs are split in rank order into 4
 // contiguous chunks, one per lane, so the quad's candidates stay in canonical order lane by lane.
-__device__ __forceinline__ int detect(MP m, const float4* __restrict__ links, const zb_task_cfg& cfg,
+__device__ __forceinline__ int detect(MP m, const zb_task_cfg& cfg,
                                       const Kin& k, float Pz, const Q& q, Stamps& sp) {
   const float margin = cfg.contact_margin;
 #pragma unroll
@@ -425,7 +469,13 @@ __device__ __forceinline__ int detect(MP m, const float4* __restrict__ links, co
     const int l = 3 * q.s + t;
     float R[9], p[3];
     read_frame(q, (l + 1) >> 1, R, p);
-    const float4* L = links + l * LINK4;
+    const float4* L = q.link(l);
+    {
+      const float4 us = L[9];
+      float c[3];
+      mv3f(R, us, c);
+      q.ub(l) = make_float4(c[0] + p[0], c[1] + p[1], c[2] + p[2], us.w);
+    }
     const float4 bd = L[0];
     float bc[3];
     mv3f(R, bd, bc);
@@ -465,32 +515,25 @@ __device__ __forceinline__ int detect(MP m, const float4* __restrict__ links, co
 
   int cnt_s = 0;
   if (cfg.enable_self_collision) {
-    m = opaque(m);
+    __syncthreads();  // union spheres of all 12 links
+    // broadphase: lane s tests pairs [PAIR_CHUNK s, PAIR_CHUNK (s+1)); the quad ORs the bits
     unsigned long long mask = 0ull;
-    {
-      float ub[NL][3], ur[NL];
 #pragma unroll
-      for (int l = 0; l < NL; ++l) {
-        float s0[4], s1[4];
-        ldc(s0, m->link_sphere[l][0]);
-        ldc(s1, m->link_sphere[l][1]);
-        const float mid[3] = {0.5f * (s0[0] + s1[0]), 0.5f * (s0[1] + s1[1]), 0.5f * (s0[2] + s1[2])};
-        const float hd = 0.5f * sqrtf((s0[0] - s1[0]) * (s0[0] - s1[0]) + (s0[1] - s1[1]) * (s0[1] - s1[1]) +
-                                      (s0[2] - s1[2]) * (s0[2] - s1[2]));
-        ur[l] = fmaxf(s0[3], s1[3]) + hd;
-        const int b = link_body(l);
-        mv3(k.R[b], mid, ub[l]);
-        ub[l][0] += k.p[b][0]; ub[l][1] += k.p[b][1]; ub[l][2] += k.p[b][2];
+    for (int j = 0; j < PAIR_CHUNK; ++j) {
+      const int pidx = PAIR_CHUNK * q.s + j;
+      if (pidx < NPAIR) {
+        const int code = q.pair_code(pidx);
+        const float4 A = q.ub(code >> 4), B = q.ub(code & 15);
+        const float d0 = A.x - B.x, d1 = A.y - B.y, d2 = A.z - B.z;
+        const float rr = A.w + B.w + margin;
+        if (d0 * d0 + d1 * d1 + d2 * d2 <= rr * rr) mask |= 1ull << pidx;
       }
-      int pidx = 0;
-#pragma unroll
-      for (int la = 0; la < NL; ++la)
-#pragma unroll
-        for (int lb = la + 2; lb < NL; ++lb, ++pidx) {
-          const float d0 = ub[la][0] - ub[lb][0], d1 = ub[la][1] - ub[lb][1], d2 = ub[la][2] - ub[lb][2];
-          const float rr = ur[la] + ur[lb] + margin;
-          if (d0 * d0 + d1 * d1 + d2 * d2 <= rr * rr) mask |= 1ull << pidx;
-        }
+    }
+    {
+      int lo = (int)(unsigned)mask, hi = (int)(unsigned)(mask >> 32);
+      lo |= dppi<QP_XOR1>(lo); hi |= dppi<QP_XOR1>(hi);
+      lo |= dppi<QP_XOR2>(lo); hi |= dppi<QP_XOR2>(hi);
+      mask = (unsigned long long)(unsigned)lo | ((unsigned long long)(unsigned)hi << 32);
     }
     const int K = __popcll(mask);
     const int chunk = (K + 3) >> 2;
@@ -498,14 +541,13 @@ __device__ __forceinline__ int detect(MP m, const float4* __restrict__ links, co
     for (int j = 0; j < chunk && mask; ++j) {
       const int pidx = __builtin_ctzll(mask);
       mask &= mask - 1ull;
-      int la = 0, rem = pidx;
-      while (rem >= NL - 2 - la) { rem -= NL - 2 - la; ++la; }
-      const int lb = la + 2 + rem;
+      const int pcode = q.pair_code(pidx);
+      const int la = pcode >> 4, lb = pcode & 15;
       float Ra[9], pa[3], Rb[9], pb[3];
       read_frame(q, link_body(la), Ra, pa);
       read_frame(q, link_body(lb), Rb, pb);
-      const float4* LA = links + la * LINK4;
-      const float4* LB = links + lb * LINK4;
+      const float4* LA = q.link(la);
+      const float4* LB = q.link(lb);
 #pragma unroll
       for (int sa = 0; sa < 2; ++sa) {
         const float4 spa = LA[7 + sa];
@@ -667,7 +709,7 @@ __device__ __forceinline__ void put_split(const Q& q, int c, int r, const float 
 
 // ------------------------------------------------------------------------- one substep
 template <bool kDebugForces>
-__device__ __forceinline__ void substep(MP m0, const float4* __restrict__ links, const zb_task_cfg& cfg, Phys& s,
+__device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
                                         const float target[ND], const Q& q, bool last, SensorOut& so,
                                         float (*dbgF)[3], float* dbgTau, Stamps& sp) {
   const float dt = cfg.sim_dt;
@@ -691,7 +733,8 @@ __device__ __forceinline__ void substep(MP m0, const float4* __restrict__ links,
   {
     Kin k;
     fk(m, s, k);
-    nc = detect(opaque(m0), links, cfg, k, s.pos[2], q, sp);
+    sp.mark(9);
+    nc = detect(opaque(m0), cfg, k, s.pos[2], q, sp);
     sp.mark(2);
     m = opaque(m0);
 #pragma unroll
@@ -1017,7 +1060,7 @@ __device__ __forceinline__ void substep(MP m0, const float4* __restrict__ links,
     float dq[4];
     if (th > 1e-12f) {
       float sn, cs;
-      sincosf(0.5f * th, &sn, &cs);
+      sincos_r(0.5f * th, &sn, &cs);
       const float sc = sn / th * dt;
       dq[0] = cs; dq[1] = s.av[0] * sc; dq[2] = s.av[1] * sc; dq[3] = s.av[2] * sc;
     } else {
@@ -1186,23 +1229,18 @@ __device__ __forceinline__ void store_state(float* __restrict__ st, int N, int i
 #undef SV
 }
 
-// _reset_idx for one env (v2.py:413-459); feet_step_len and f_last are NOT reset (reference)
-__device__ __forceinline__ void reset_env(MP m, Phys& p, Mdp& d) {
+// _reset_idx for one env (v2.py:413-459); feet_step_len and f_last are NOT reset (reference).
+// feet_down_pos_last = the feet positions of the default pose (dflt[0], dflt[1], zb_derive_kernel).
+__device__ __forceinline__ void reset_env(MP m, const float4* dflt, Phys& p, Mdp& d) {
 #pragma unroll
   for (int a = 0; a < 3; ++a) { p.pos[a] = m->default_root_pos[a]; p.lv[a] = 0.f; p.av[a] = 0.f; }
 #pragma unroll
   for (int a = 0; a < 4; ++a) p.quat[a] = m->default_root_quat[a];
 #pragma unroll
   for (int j = 0; j < ND; ++j) { p.jq[j] = m->default_joint_pos[j]; p.jqd[j] = 0.f; d.p_delta[j] = 0.f; d.actions[j] = 0.f; }
-  {
-    Kin k;
-    fk(m, p, k);
-    float q[4];
-    link_pose(m, k, 0, d.down_pos[0], q);
-    link_pose(m, k, 11, d.down_pos[1], q);
-#pragma unroll
-    for (int a = 0; a < 3; ++a) { d.down_pos[0][a] += p.pos[a]; d.down_pos[1][a] += p.pos[a]; }
-  }
+  const float4 f0 = dflt[0], f1 = dflt[1];
+  d.down_pos[0][0] = f0.x; d.down_pos[0][1] = f0.y; d.down_pos[0][2] = f0.z;
+  d.down_pos[1][0] = f1.x; d.down_pos[1][1] = f1.y; d.down_pos[1][2] = f1.z;
   d.heading_sum = 0.f;
   d.yerr_sum = 0.f;
 #pragma unroll
@@ -1261,6 +1299,7 @@ __global__ __launch_bounds__(WAVE, 1) void zb_step_kernel(const zb_model* __rest
   const int i = env < N ? env : N - 1;
   const bool lead = env < N && (lane & 3) == 0;
   const Q q{lds, lane, lane >> 2, lane & 3};
+  for (int t = lane; t < LNK4; t += WAVE) lds[LNK_OFF + t] = links[t];
 #define ST(f) st[(size_t)(f) * N + i]
   Stamps sp;
   sp.begin();
@@ -1274,7 +1313,7 @@ __global__ __launch_bounds__(WAVE, 1) void zb_step_kernel(const zb_model* __rest
 #pragma unroll
   for (int j = 0; j < ND; ++j) {
     const float a_prev = ST(ZB_S_ACTIONS + j);
-    const float a_now = tanhf(act[(size_t)i * ZB_ACT_DIM + j]);
+    const float a_now = tanh_r(act[(size_t)i * ZB_ACT_DIM + j]);
     const float pd = clampf(ST(ZB_S_P_DELTA + j) + PI_F * a_now * cfg.joint_speed_limit * step_dt, -PI_F, PI_F);
     ST(ZB_S_P_DELTA + j) = pd;
     ST(ZB_S_ACTIONS + j) = a_now;
@@ -1289,7 +1328,7 @@ __global__ __launch_bounds__(WAVE, 1) void zb_step_kernel(const zb_model* __rest
   {
     Cache c;
     make_cache(opaque(m), p, c);
-    r_pre[0] = tanhf(10.f * c.vfwd / cfg.joint_speed_limit);                     // base_vel_forward
+    r_pre[0] = tanh_r(10.f * c.vfwd / cfg.joint_speed_limit);                     // base_vel_forward
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int f = 0; f < 2; ++f) {
@@ -1313,7 +1352,7 @@ __global__ __launch_bounds__(WAVE, 1) void zb_step_kernel(const zb_model* __rest
   SensorOut so;
   sp.mark(0);
   for (int k = 0; k < cfg.decimation; ++k) {
-    substep<false>(m, links, cfg, p, target, q, k == cfg.decimation - 1, so, nullptr, nullptr, sp);
+    substep<false>(m, cfg, p, target, q, k == cfg.decimation - 1, so, nullptr, nullptr, sp);
     sp.mark(7);
   }
   m = opaque(m);
@@ -1348,7 +1387,7 @@ __global__ __launch_bounds__(WAVE, 1) void zb_step_kernel(const zb_model* __rest
   const float ep_len = ST(ZB_S_EP_LEN) + 1.f;
 
   // post-step feet COM velocities (feet_slide)
-  float feet_vel[2][3];
+  float feet_vel[2][3], obs_q[4];
   {
     Kin k;
     fk(m, p, k);
@@ -1356,6 +1395,8 @@ __global__ __launch_bounds__(WAVE, 1) void zb_step_kernel(const zb_model* __rest
     body_vel(k, p, V);
     link_com_vel(m, k, V, 0, feet_vel[0]);
     link_com_vel(m, k, V, 11, feet_vel[1]);
+    float bp[3];
+    link_pose(m, k, 6, bp, obs_q);  // base quat of the post-step state (observation)
   }
 
   // _get_dones (v2.py:384-411)
@@ -1402,7 +1443,7 @@ __global__ __launch_bounds__(WAVE, 1) void zb_step_kernel(const zb_model* __rest
       }
       ST(ZB_S_FEET_F_LAST + f) = feetF[f];
     }
-    r[ZB_R_STEP_LENGTH] = tanhf(15.f * fminf(step_len[0], step_len[1]));
+    r[ZB_R_STEP_LENGTH] = tanh_r(15.f * fminf(step_len[0], step_len[1]));
   }
   r[ZB_R_AIRTIME_BALANCE] = fabsf(air_last[0] - air_last[1]);
   r[ZB_R_ACTION_RATE] = r_action_rate;
@@ -1420,7 +1461,7 @@ __global__ __launch_bounds__(WAVE, 1) void zb_step_kernel(const zb_model* __rest
     ST(ZB_S_Y_ERR_SUM) = ys;
     r[ZB_R_BASE_POS_Y_ERR_SUM] = fabsf(ys);
   }
-  r[ZB_R_AIRTIME_SUM] = tanhf(air_last[0] + air_last[1]);
+  r[ZB_R_AIRTIME_SUM] = tanh_r(air_last[0] + air_last[1]);
 
   float reward = 0.f;
   const bool reset = died || time_out;
@@ -1444,8 +1485,10 @@ __global__ __launch_bounds__(WAVE, 1) void zb_step_kernel(const zb_model* __rest
     }
     Mdp d;
     load_state(st, N, i, p, d);
-    reset_env(m, p, d);
+    reset_env(m, q.dflt(), p, d);
     store_state(st, N, i, p, d);
+    const float4 dq = q.dflt()[2];
+    obs_q[0] = dq.x; obs_q[1] = dq.y; obs_q[2] = dq.z; obs_q[3] = dq.w;
   } else {
 #pragma unroll
     for (int a = 0; a < 3; ++a) { ST(ZB_S_ROOT_POS + a) = p.pos[a]; ST(ZB_S_ROOT_LINVEL + a) = p.lv[a]; ST(ZB_S_ROOT_ANGVEL + a) = p.av[a]; }
@@ -1456,10 +1499,8 @@ __global__ __launch_bounds__(WAVE, 1) void zb_step_kernel(const zb_model* __rest
   }
   // _get_observations (v2.py:351-365) of the post-step / post-reset state
   {
-    Cache c;
-    make_cache(m, p, c);
     float* o = obs + (size_t)i * ZB_OBS_DIM;
-    o[0] = c.base_quat[0]; o[1] = c.base_quat[1]; o[2] = c.base_quat[2]; o[3] = c.base_quat[3];
+    o[0] = obs_q[0]; o[1] = obs_q[1]; o[2] = obs_q[2]; o[3] = obs_q[3];
 #pragma unroll
     for (int j = 0; j < ND; ++j) {
       o[4 + j] = p.jq[j] - m->default_joint_pos[j];
@@ -1477,8 +1518,9 @@ __global__ __launch_bounds__(WAVE, 1) void zb_step_kernel(const zb_model* __rest
 }
 
 // reset env_ids (or all when ids == nullptr); logs the reset envs' episode sums into acc
-__global__ void zb_reset_kernel(const zb_model* __restrict__ mg, int N, float* __restrict__ st,
-                                const int32_t* __restrict__ ids, int n, float* __restrict__ acc) {
+__global__ void zb_reset_kernel(const zb_model* __restrict__ mg, const float4* __restrict__ links, int N,
+                                float* __restrict__ st, const int32_t* __restrict__ ids, int n,
+                                float* __restrict__ acc) {
   MP m = to_mp(mg);
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n) return;
@@ -1490,8 +1532,30 @@ __global__ void zb_reset_kernel(const zb_model* __restrict__ mg, int N, float* _
 #pragma unroll
   for (int k = 0; k < ZB_NUM_REWARD_TERMS; ++k) atomicAdd(&acc[k], d.sums[k]);
   atomicAdd(&acc[13], 1.f);
-  reset_env(m, p, d);
+  reset_env(m, links + DFLT_OFF, p, d);
   store_state(st, N, i, p, d);
+}
+
+// default-pose constants for resets (once, at zb_create): feet link positions and the base
+// link quaternion of the default root pose / joint positions
+__global__ void zb_derive_kernel(const zb_model* __restrict__ mg, float4* __restrict__ links) {
+  MP m = to_mp(mg);
+  Phys p;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) { p.pos[a] = m->default_root_pos[a]; p.lv[a] = 0.f; p.av[a] = 0.f; }
+#pragma unroll
+  for (int a = 0; a < 4; ++a) p.quat[a] = m->default_root_quat[a];
+#pragma unroll
+  for (int j = 0; j < ND; ++j) { p.jq[j] = m->default_joint_pos[j]; p.jqd[j] = 0.f; }
+  Kin k;
+  fk(m, p, k);
+  float f0[3], f1[3], bp[3], q0[4];
+  link_pose(m, k, 0, f0, q0);
+  link_pose(m, k, 11, f1, q0);
+  link_pose(m, k, 6, bp, q0);
+  links[DFLT_OFF + 0] = make_float4(f0[0] + p.pos[0], f0[1] + p.pos[1], f0[2] + p.pos[2], 0.f);
+  links[DFLT_OFF + 1] = make_float4(f1[0] + p.pos[0], f1[1] + p.pos[1], f1[2] + p.pos[2], 0.f);
+  links[DFLT_OFF + 2] = make_float4(q0[0], q0[1], q0[2], q0[3]);
 }
 
 // episode log finalisation + full-reset episode_length_buf draw (v2.py:418-422)
@@ -1534,6 +1598,7 @@ __global__ __launch_bounds__(WAVE, 1) void zb_substeps_kernel(const zb_model* __
   const int env = blockIdx.x * EPW + (lane >> 2);
   const int i = env < N ? env : N - 1;
   const Q q{lds, lane, lane >> 2, lane & 3};
+  for (int t = lane; t < LNK4; t += WAVE) lds[LNK_OFF + t] = links[t];
   Phys p;
   load_phys(st, N, i, p);
   float tg[ND], tau[ND], F[3][3];
@@ -1541,7 +1606,7 @@ __global__ __launch_bounds__(WAVE, 1) void zb_substeps_kernel(const zb_model* __
   for (int j = 0; j < ND; ++j) { tg[j] = targets[(size_t)i * ND + j]; tau[j] = 0.f; }
   SensorOut so;
   Stamps sp;
-  for (int k = 0; k < nsub; ++k) substep<true>(m, links, cfg, p, tg, q, k == nsub - 1, so, F, tau, sp);
+  for (int k = 0; k < nsub; ++k) substep<true>(m, cfg, p, tg, q, k == nsub - 1, so, F, tau, sp);
   if (net_force)
 #pragma unroll
     for (int t = 0; t < 3; ++t)
@@ -1638,7 +1703,8 @@ int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_dev
   HIPCHK(hipMalloc(&h->d_log_counts, sizeof(int32_t) * 2), "hipMalloc log");
   HIPCHK(hipMemcpy(h->d_model, m, sizeof(zb_model), hipMemcpyHostToDevice), "hipMemcpy model");
   {
-    float4 tab[NL * LINK4];
+    float4 tab[LNK4];
+    memset(tab, 0, sizeof(tab));
     for (int l = 0; l < NL; ++l) {
       float4* t = tab + l * LINK4;
       t[0] = make_float4(m->link_bound[l][0], m->link_bound[l][1], m->link_bound[l][2], m->link_bound[l][3]);
@@ -1647,11 +1713,17 @@ int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_dev
           const float* c = m->link_circle[l][ci] + 3 * v;
           t[1 + 3 * ci + v] = make_float4(c[0], c[1], c[2], 0.f);
         }
-      for (int sp = 0; sp < 2; ++sp) {
-        const float* c = m->link_sphere[l][sp];
-        t[7 + sp] = make_float4(c[0], c[1], c[2], c[3]);
-      }
+      const float* s0 = m->link_sphere[l][0];
+      const float* s1 = m->link_sphere[l][1];
+      t[7] = make_float4(s0[0], s0[1], s0[2], s0[3]);
+      t[8] = make_float4(s1[0], s1[1], s1[2], s1[3]);
+      const double hd = 0.5 * sqrt((double)(s0[0] - s1[0]) * (s0[0] - s1[0]) + (double)(s0[1] - s1[1]) * (s0[1] - s1[1]) +
+                                   (double)(s0[2] - s1[2]) * (s0[2] - s1[2]));
+      t[9] = make_float4(0.5f * (s0[0] + s1[0]), 0.5f * (s0[1] + s1[1]), 0.5f * (s0[2] + s1[2]),
+                         (float)(fmax((double)s0[3], (double)s1[3]) + hd + 1e-6));
     }
+    int* pc = reinterpret_cast<int*>(tab + NL * LINK4);
+    for (int p = 0; p < m->num_self_pairs; ++p) pc[p] = 16 * m->self_pairs[p][0] + m->self_pairs[p][1];
     HIPCHK(hipMalloc(&h->d_links, sizeof(tab)), "hipMalloc links");
     HIPCHK(hipMemcpy(h->d_links, tab, sizeof(tab), hipMemcpyHostToDevice), "hipMemcpy links");
   }
@@ -1660,8 +1732,12 @@ int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_dev
   HIPCHK(hipMemset(h->d_log_counts, 0, sizeof(int32_t) * 2), "hipMemset log");
   HIPCHK(hipMemset(h->d_acc, 0, sizeof(float) * ACC), "hipMemset acc");
   // start at the default pose (ep_len 0, as after construction; reset() randomises it)
-  zb_reset_kernel<<<(num_envs + 255) / 256, 256>>>(h->d_model, num_envs, h->d_state, nullptr, num_envs, h->d_acc);
-  int rc = launch_check("zb_reset_kernel");
+  zb_derive_kernel<<<1, 1>>>(h->d_model, h->d_links);
+  int rc = launch_check("zb_derive_kernel");
+  if (rc) return rc;
+  zb_reset_kernel<<<(num_envs + 255) / 256, 256>>>(h->d_model, h->d_links, num_envs, h->d_state, nullptr, num_envs,
+                                                    h->d_acc);
+  rc = launch_check("zb_reset_kernel");
   if (rc) return rc;
   HIPCHK(hipMemset(h->d_acc, 0, sizeof(float) * ACC), "hipMemset acc");
   HIPCHK(hipDeviceSynchronize(), "zb_create sync");
@@ -1735,7 +1811,7 @@ int zb_reset(zb_handle h, const int32_t* env_ids, int n, void* stream) {
   const int cnt = env_ids ? n : h->n;
   if (cnt <= 0) return 0;
   HIPCHK(hipMemsetAsync(h->d_acc, 0, sizeof(float) * ACC, s), "hipMemsetAsync acc");
-  zb_reset_kernel<<<(cnt + 255) / 256, 256, 0, s>>>(h->d_model, h->n, h->d_state, env_ids, cnt, h->d_acc);
+  zb_reset_kernel<<<(cnt + 255) / 256, 256, 0, s>>>(h->d_model, h->d_links, h->n, h->d_state, env_ids, cnt, h->d_acc);
   int rc = launch_check("zb_reset_kernel");
   if (rc) return rc;
   const uint64_t ctr = h->calls++;

@@ -45,8 +45,8 @@ class InteractiveSceneCfg:
 
 @dataclass
 class SolverCfg:
-    """Parameters of this simulator's contact/drive solver (no reference counterpart)."""
-    iterations: int = 8
+    """Parameters of this simulator's contact/drive solver."""
+    iterations: int = 4               # PGS sweeps/substep = solver_position_iteration_count=4 (zbot_cfg.py:637)
     contact_margin: float = 0.004
     baumgarte: float = 0.2
     self_collision: bool = True       # enabled_self_collisions=True (zbot_cfg.py:636)

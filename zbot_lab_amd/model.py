@@ -338,7 +338,7 @@ class TaskCfg:
     contact_force_threshold: float = 1.0
     contact_margin: float = 0.004
     baumgarte: float = 0.2
-    solver_iterations: int = 8
+    solver_iterations: int = 4   # = solver_position_iteration_count (zbot_cfg.py:637)
     enable_self_collision: bool = True
 
     @property
