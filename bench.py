@@ -43,9 +43,13 @@ def parse():
     return p.parse_args()
 
 
+ENVS_PER_WORKGROUP = 16        # zb_step_kernel: one 64-lane workgroup = 16 envs x 4 lanes
+
+
 def pmc_traffic(num_envs: int):
     """HBM bytes per zb_step_kernel launch from the committed rocprofv3 PMC passes (separate
-    FETCH_SIZE / WRITE_SIZE runs, profiles/<round>/pmc_*_zb_step_kernel.csv) for the same grid.
+    FETCH_SIZE / WRITE_SIZE runs, profiles/<round>/pmc_*_zb_step_kernel.csv) for the same grid
+    (work-items = 64 per workgroup of 16 envs).
     FETCH_SIZE/WRITE_SIZE are KiB; our accesses are 4-B-per-lane (uncalibrated width per the
     microarch guide, so no 2x read correction is applied). Returns (bytes, source) or (None, None)."""
     import csv
@@ -56,7 +60,8 @@ def pmc_traffic(num_envs: int):
         for name in ("FETCH_SIZE", "WRITE_SIZE"):
             for f in glob.glob(os.path.join(d, "pmc_*_zb_step_kernel.csv")):
                 for row in csv.DictReader(open(f)):
-                    if row["counter"] == name and int(row["grid"]) == num_envs:
+                    grid = -(-num_envs // ENVS_PER_WORKGROUP) * 64
+                    if row["counter"] == name and int(row["grid"]) == grid:
                         vals[name] = float(row["mean_per_dispatch"]) * 1024.0
         if len(vals) == 2:
             return vals["FETCH_SIZE"] + vals["WRITE_SIZE"], os.path.relpath(d, here)

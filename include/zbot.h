@@ -16,7 +16,7 @@
  *                  _get_rewards (v2.py:371-382), _reset_idx (v2.py:413-459),
  *                  _get_observations (v2.py:312-369)
  *   zb_observe  <- ZbotDirectEnvV2._get_observations (v2.py:312-369), used by reset()
- *   zb_read_log <- extras["log"] written in _reset_idx (v2.py:441-459)
+ *   zb_read_log / zb_set_log_buffers <- extras["log"] written in _reset_idx (v2.py:441-459)
  *   zb_get_state / zb_set_state / zb_physics_substeps: parity + debugging (no reference analogue;
  *                  they stand in for Articulation.data reads / write_*_to_sim)
  *
@@ -153,6 +153,10 @@ int zb_observe(zb_handle h, float* obs, void* stream);
 /* Episode log of the most recent step with resets: term_means[13] = mean episodic sum / 20 s,
  * counts[2] = {body_contact, time_out} (v2.py:441-459). Device pointers. */
 int zb_read_log(zb_handle h, float* term_means, int32_t* counts, void* stream);
+/* Register caller-owned device buffers (float[13], int32[2]) that every later step/reset with
+ * resets fills in stream order, exactly as zb_read_log would (no per-step copies). NULL, NULL
+ * unregisters. */
+int zb_set_log_buffers(zb_handle h, float* term_means, int32_t* counts);
 
 /* Persistent state, device float[ZB_STATE_DIM][N]. */
 int zb_get_state(zb_handle h, float* dst, void* stream);

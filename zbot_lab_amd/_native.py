@@ -41,6 +41,7 @@ def lib():
     L.zb_step.argtypes = [P, P, P, P, P, P, P]
     L.zb_observe.argtypes = [P, P, P]
     L.zb_read_log.argtypes = [P, P, P, P]
+    L.zb_set_log_buffers.argtypes = [P, P, P]
     L.zb_get_state.argtypes = [P, P, P]
     L.zb_set_state.argtypes = [P, P, P]
     L.zb_physics_substeps.argtypes = [P, P, C.c_int, P, P, P]
@@ -48,7 +49,8 @@ def lib():
     L.zb_profile_end.argtypes = [P, C.POINTER(C.c_float), C.POINTER(C.c_int)]
     L.zb_read_stamps.argtypes = [P]
     L.zb_read_stamps.restype = C.c_int
-    for name in ("zb_create", "zb_num_envs", "zb_reset", "zb_step", "zb_observe", "zb_read_log", "zb_get_state",
+    for name in ("zb_create", "zb_num_envs", "zb_reset", "zb_step", "zb_observe", "zb_read_log", "zb_set_log_buffers",
+                 "zb_get_state",
                  "zb_set_state", "zb_physics_substeps", "zb_profile_begin", "zb_profile_end"):
         getattr(L, name).restype = C.c_int
     _lib = L
@@ -56,7 +58,7 @@ def lib():
 
 
 EXPORTED = ["zb_create", "zb_destroy", "zb_last_error", "zb_num_envs", "zb_reset", "zb_step", "zb_observe",
-            "zb_read_log", "zb_get_state", "zb_set_state", "zb_physics_substeps", "zb_profile_begin",
+            "zb_read_log", "zb_set_log_buffers", "zb_get_state", "zb_set_state", "zb_physics_substeps", "zb_profile_begin",
             "zb_profile_end", "zb_read_stamps"]
 
 

@@ -30,7 +30,10 @@ def build(force: bool = False, verbose: bool = False, stamps: bool = False) -> s
         return out
     # -fno-slp-vectorize: packing scalar f32 math into v_pk_* pairs forces aligned register pairs
     # and shuffles; on this register-bound kernel it costs ~1.1 KB/lane of scratch spills.
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fno-slp-vectorize", "-fPIC", "-shared",
+    # -fno-hip-fp32-correctly-rounded-divide-sqrt: f32 '/' and sqrtf as v_rcp/v_sqrt sequences
+    # (<= 2.5 ulp, OpenCL precision) instead of the ~10-instruction correctly rounded expansions.
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fno-slp-vectorize",
+           "-fno-hip-fp32-correctly-rounded-divide-sqrt", "-fPIC", "-shared",
            "-I", os.path.join(ROOT, "include"), "-o", out + ".tmp", SRC]
     if stamps:
         cmd.insert(1, "-DZB_STAMPS")

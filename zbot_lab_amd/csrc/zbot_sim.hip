@@ -1559,21 +1559,34 @@ __global__ void zb_derive_kernel(const zb_model* __restrict__ mg, float4* __rest
 }
 
 // episode log finalisation + full-reset episode_length_buf draw (v2.py:418-422)
-__global__ void zb_finalize_kernel(int N, float* __restrict__ st, const float* __restrict__ acc,
-                                   float* __restrict__ log_means, int32_t* __restrict__ log_counts, float episode_s,
+// episode log finalisation + full-reset episode_length_buf draw (v2.py:418-422); leaves the
+// accumulator zeroed for the next launch. Single workgroup (grid-strided over envs).
+__global__ void zb_finalize_kernel(int N, float* __restrict__ st, float* __restrict__ acc,
+                                   float* __restrict__ log_means, int32_t* __restrict__ log_counts,
+                                   float* __restrict__ user_means, int32_t* __restrict__ user_counts, float episode_s,
                                    int max_ep_len, uint64_t seed, uint64_t ctr, int force_full, int reset_counts) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
   const float nres = acc[13];
-  if (i == 0 && nres > 0.f) {
+  const bool full = force_full || nres == (float)N;
+  __syncthreads();
+  if (threadIdx.x == 0 && nres > 0.f) {
 #pragma unroll
-    for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) log_means[t] = acc[t] / nres / episode_s;
-    log_counts[0] = reset_counts ? 0 : (int32_t)acc[14];
-    log_counts[1] = reset_counts ? 0 : (int32_t)acc[15];
+    for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) {
+      const float v = acc[t] / nres / episode_s;
+      log_means[t] = v;
+      if (user_means) user_means[t] = v;
+    }
+    const int32_t c0 = reset_counts ? 0 : (int32_t)acc[14], c1 = reset_counts ? 0 : (int32_t)acc[15];
+    log_counts[0] = c0;
+    log_counts[1] = c1;
+    if (user_counts) { user_counts[0] = c0; user_counts[1] = c1; }
   }
-  if (i < N && (force_full || nres == (float)N)) {
-    const uint64_t h = hash64(seed ^ hash64(ctr * 0x100000001B3ull + (uint64_t)i));
-    st[(size_t)ZB_S_EP_LEN * N + i] = (float)(int)(h % (uint64_t)max_ep_len);
-  }
+  __syncthreads();
+  if (threadIdx.x < ACC) acc[threadIdx.x] = 0.f;
+  if (full)
+    for (int i = threadIdx.x; i < N; i += blockDim.x) {
+      const uint64_t h = hash64(seed ^ hash64(ctr * 0x100000001B3ull + (uint64_t)i));
+      st[(size_t)ZB_S_EP_LEN * N + i] = (float)(int)(h % (uint64_t)max_ep_len);
+    }
 }
 
 __global__ void zb_observe_kernel(const zb_model* __restrict__ mg, int N, const float* __restrict__ st,
@@ -1640,6 +1653,8 @@ struct zb_sim {
   float* d_acc;
   float* d_log_means;
   int32_t* d_log_counts;
+  float* u_log_means = nullptr;     // optional caller buffers (zb_set_log_buffers)
+  int32_t* u_log_counts = nullptr;
   // optional per-launch timing of zb_step_kernel (hipEvents on the launch stream)
   int prof_max = 0, prof_n = 0;
   hipEvent_t* prof_ev = nullptr;
@@ -1810,15 +1825,14 @@ int zb_reset(zb_handle h, const int32_t* env_ids, int n, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const int cnt = env_ids ? n : h->n;
   if (cnt <= 0) return 0;
-  HIPCHK(hipMemsetAsync(h->d_acc, 0, sizeof(float) * ACC, s), "hipMemsetAsync acc");
   zb_reset_kernel<<<(cnt + 255) / 256, 256, 0, s>>>(h->d_model, h->d_links, h->n, h->d_state, env_ids, cnt, h->d_acc);
   int rc = launch_check("zb_reset_kernel");
   if (rc) return rc;
   const uint64_t ctr = h->calls++;
   const float ep_s = h->cfg.sim_dt * h->cfg.decimation * h->cfg.max_episode_length;
   const int full = env_ids == nullptr || n == h->n;
-  zb_finalize_kernel<<<(h->n + 255) / 256, 256, 0, s>>>(h->n, h->d_state, h->d_acc, h->d_log_means, h->d_log_counts,
-                                                        ep_s, h->cfg.max_episode_length, h->seed, ctr, full, 1);
+  zb_finalize_kernel<<<1, 1024, 0, s>>>(h->n, h->d_state, h->d_acc, h->d_log_means, h->d_log_counts, h->u_log_means,
+                                        h->u_log_counts, ep_s, h->cfg.max_episode_length, h->seed, ctr, full, 1);
   return launch_check("zb_finalize_kernel");
 }
 
@@ -1826,7 +1840,6 @@ int zb_step(zb_handle h, const float* actions, float* obs, float* reward, uint8_
             void* stream) {
   if (!h || !actions || !obs || !reward || !terminated || !truncated) return set_err(-1, "zb_step", hipSuccess);
   hipStream_t s = (hipStream_t)stream;
-  HIPCHK(hipMemsetAsync(h->d_acc, 0, sizeof(float) * ACC, s), "hipMemsetAsync acc");
   const int blocks = (h->n + EPW - 1) / EPW;
   const bool prof = h->prof_n < h->prof_max;
   if (prof) HIPCHK(hipEventRecord(h->prof_ev[2 * h->prof_n], s), "hipEventRecord");
@@ -1840,8 +1853,8 @@ int zb_step(zb_handle h, const float* actions, float* obs, float* reward, uint8_
   if (rc) return rc;
   const uint64_t ctr = h->calls++;
   const float ep_s = h->cfg.sim_dt * h->cfg.decimation * h->cfg.max_episode_length;
-  zb_finalize_kernel<<<(h->n + 255) / 256, 256, 0, s>>>(h->n, h->d_state, h->d_acc, h->d_log_means, h->d_log_counts,
-                                                        ep_s, h->cfg.max_episode_length, h->seed, ctr, 0, 0);
+  zb_finalize_kernel<<<1, 1024, 0, s>>>(h->n, h->d_state, h->d_acc, h->d_log_means, h->d_log_counts, h->u_log_means,
+                                        h->u_log_counts, ep_s, h->cfg.max_episode_length, h->seed, ctr, 0, 0);
   return launch_check("zb_finalize_kernel");
 }
 
@@ -1859,6 +1872,13 @@ int zb_read_log(zb_handle h, float* term_means, int32_t* counts, void* stream) {
            "hipMemcpyAsync log");
   if (counts)
     HIPCHK(hipMemcpyAsync(counts, h->d_log_counts, sizeof(int32_t) * 2, hipMemcpyDeviceToDevice, s), "hipMemcpyAsync log");
+  return 0;
+}
+
+int zb_set_log_buffers(zb_handle h, float* term_means, int32_t* counts) {
+  if (!h || (!term_means) != (!counts)) return set_err(-1, "zb_set_log_buffers", hipSuccess);
+  h->u_log_means = term_means;
+  h->u_log_counts = counts;
   return 0;
 }
 

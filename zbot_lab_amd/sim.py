@@ -45,6 +45,9 @@ class ZbotSim:
         self.truncated = torch.zeros(self.num_envs, dtype=torch.bool, device=self.device)
         self._log_means = torch.zeros(zm.NUM_TERMS, dtype=torch.float32, device=self.device)
         self._log_counts = torch.zeros(2, dtype=torch.int32, device=self.device)
+        # the library fills these in stream order at every step/reset with resets (no copies)
+        nat.check(self.lib.zb_set_log_buffers(self._h, nat.ptr(self._log_means), nat.ptr(self._log_counts)),
+                  "zb_set_log_buffers")
 
     # ------------------------------------------------------------------ lifecycle
     def close(self) -> None:
@@ -89,9 +92,8 @@ class ZbotSim:
         return obs
 
     def read_log(self):
-        """(term_means[13], counts[2]) device tensors of the most recent step that had resets."""
-        nat.check(self.lib.zb_read_log(self._h, nat.ptr(self._log_means), nat.ptr(self._log_counts),
-                                       _stream(self.device)), "zb_read_log")
+        """(term_means[13], counts[2]) device tensors of the most recent step that had resets
+        (registered with zb_set_log_buffers, so no per-step copy)."""
         return self._log_means, self._log_counts
 
     def get_state(self) -> torch.Tensor:
