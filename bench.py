@@ -43,13 +43,13 @@ def parse():
     return p.parse_args()
 
 
-ENVS_PER_WORKGROUP = 16        # zb_step_kernel: one 64-lane workgroup = 16 envs x 4 lanes
+ENVS_PER_WORKGROUP = 4         # zb_step_kernel: one 64-lane workgroup = 4 envs x 16 lanes
 
 
 def pmc_traffic(num_envs: int):
     """HBM bytes per zb_step_kernel launch from the committed rocprofv3 PMC passes (separate
     FETCH_SIZE / WRITE_SIZE runs, profiles/<round>/pmc_*_zb_step_kernel.csv) for the same grid
-    (work-items = 64 per workgroup of 16 envs).
+    (work-items = 64 per workgroup of 4 envs).
     FETCH_SIZE/WRITE_SIZE are KiB; our accesses are 4-B-per-lane (uncalibrated width per the
     microarch guide, so no 2x read correction is applied). Returns (bytes, source) or (None, None)."""
     import csv

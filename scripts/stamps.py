@@ -6,7 +6,7 @@ import torch
 from zbot_lab_amd.envs import ZbotDirectEnvCfgV2, ZbotDirectEnvV2
 from zbot_lab_amd import _native as nat
 names = ["prologue(pre+cache)", "ground", "self-collision", "inertia+rnea+crba", "chol+drives",
-         "contact rows", "pgs", "post(solve,forces,integrate)", "mdp epilogue", "fk(substep)"]
+         "contact rows", "pgs", "post(solve,forces,integrate)", "mdp stores", "fk(substep)", "mdp loads", "mdp fk", "mdp rewards+reset"]
 cfg = ZbotDirectEnvCfgV2(); cfg.scene.num_envs = int(os.environ.get("N", "4096"))
 env = ZbotDirectEnvV2(cfg); env.reset()
 g = torch.Generator(device="cuda"); g.manual_seed(42)
@@ -17,8 +17,8 @@ steps = 100
 for k in range(steps): env.step(torch.randn(env.num_envs, 6, device="cuda", generator=g))
 torch.cuda.synchronize()
 nat.lib().zb_read_stamps(buf)
-waves = (env.num_envs + 15) // 16  # one wave per 16 envs (quad per env)
-tot = sum(buf[k] for k in range(10))
+waves = (env.num_envs + 3) // 4  # one wave per 4 envs (16 lanes per env)
+tot = sum(buf[k] for k in range(len(names)))
 print(f"cycles per wave per step: {tot / waves / steps:.0f}")
-for k in range(10):
+for k in range(len(names)):
     print(f"  {names[k]:32s} {buf[k] / waves / steps:10.0f}  {100 * buf[k] / tot:5.1f} %")

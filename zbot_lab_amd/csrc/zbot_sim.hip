@@ -56,7 +56,7 @@ __device__ __forceinline__ MP to_mp(const zb_model* m) { return (MP)(uintptr_t)m
 // ------------------------------------------------------------------------- diagnostic stamps
 // Built only with -DZB_STAMPS (python -m zbot_lab_amd.build --stamps): s_memtime deltas per phase,
 // summed per wave (lane 0) into g_stamps. Never part of the measured product build.
-constexpr int NSTAMP = 10;
+constexpr int NSTAMP = 16;
 #ifdef ZB_STAMPS
 __device__ unsigned long long g_stamps[NSTAMP];
 struct Stamps {
@@ -347,13 +347,17 @@ __device__ __forceinline__ MP opaque(MP m) {
   return (MP)v;
 }
 
-// ------------------------------------------------------------------------- quads
-// Four lanes per env (a "quad", lane = 4*e + s). The articulated-body dynamics (FK, RNEA, CRBA,
-// Cholesky) are evaluated redundantly by the four lanes; the contact work is split: each lane
-// tests 3 links against the ground and a quarter of the self-collision candidate pairs, builds
-// the rows of every 4th contact slot, and in the Gauss-Seidel sweep owns 3 of the 12 whitened
-// coordinates (row dots are reduced across the quad with DPP quad_perm adds, which give all four
-// lanes bit-identical sums, so the redundant scalar work stays identical across the quad).
+// ------------------------------------------------------------------------- teams
+// Sixteen lanes per env: a team is one 16-lane DPP row (lane = 16 e + s, 4 envs per wave). The
+// articulated-body dynamics (FK, RNEA, CRBA, Cholesky) are evaluated redundantly by the team;
+// the contact work is split: lane s tests link s against the ground, a sixteenth of the
+// self-collision pairs, builds the rows of contact slot s, and in the Gauss-Seidel sweep owns
+// whitened coordinate s (s < 12). Row dots are reduced across the team with DPP adds
+// (quad_perm, row_half_mirror, row_mirror), which leave all 16 lanes bit-identical sums, so the
+// redundant scalar work stays identical across the team.
+constexpr int TL = 16;           // lanes per env
+constexpr int EPW = WAVE / TL;   // envs per wave / workgroup
+
 template <int CTRL>
 __device__ __forceinline__ float dppf(float x) {
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
@@ -362,28 +366,49 @@ template <int CTRL>
 __device__ __forceinline__ int dppi(int x) {
   return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xF, 0xF, false);
 }
-constexpr int QP_XOR1 = 0xB1;  // quad_perm [1,0,3,2]
-constexpr int QP_XOR2 = 0x4E;  // quad_perm [2,3,0,1]
-__device__ __forceinline__ float qsum(float x) {
-  x += dppf<QP_XOR1>(x);
-  return x + dppf<QP_XOR2>(x);
+template <int CTRL>
+__device__ __forceinline__ int dppz(int x) {  // out-of-row source lanes read 0 (row shifts)
+  return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xF, 0xF, true);
 }
-__device__ __forceinline__ float qmax(float x) {
-  x = fmaxf(x, dppf<QP_XOR1>(x));
-  return fmaxf(x, dppf<QP_XOR2>(x));
+constexpr int DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_HALF_MIRROR = 0x141, DPP_MIRROR = 0x140;
+constexpr int DPP_BCAST = 0x150, DPP_SHR = 0x110;  // row_newbcast:k, row_shr:k
+
+__device__ __forceinline__ float tsum(float x) {
+  x += dppf<DPP_XOR1>(x);
+  x += dppf<DPP_XOR2>(x);
+  x += dppf<DPP_HALF_MIRROR>(x);
+  return x + dppf<DPP_MIRROR>(x);
+}
+__device__ __forceinline__ float tmax(float x) {
+  x = fmaxf(x, dppf<DPP_XOR1>(x));
+  x = fmaxf(x, dppf<DPP_XOR2>(x));
+  x = fmaxf(x, dppf<DPP_HALF_MIRROR>(x));
+  return fmaxf(x, dppf<DPP_MIRROR>(x));
+}
+__device__ __forceinline__ int tor(int x) {
+  x |= dppi<DPP_XOR1>(x);
+  x |= dppi<DPP_XOR2>(x);
+  x |= dppi<DPP_HALF_MIRROR>(x);
+  return x | dppi<DPP_MIRROR>(x);
+}
+__device__ __forceinline__ int tscan(int x) {  // inclusive prefix sum over the team
+  x += dppz<DPP_SHR + 1>(x);
+  x += dppz<DPP_SHR + 2>(x);
+  x += dppz<DPP_SHR + 4>(x);
+  return x + dppz<DPP_SHR + 8>(x);
 }
 template <int K>
-__device__ __forceinline__ float qb(float x) { return dppf<K * 0x55>(x); }  // broadcast quad lane K
+__device__ __forceinline__ float tb(float x) { return dppf<DPP_BCAST + K>(x); }  // lane K of the team
 template <int K>
-__device__ __forceinline__ int qbi(int x) { return dppi<K * 0x55>(x); }
+__device__ __forceinline__ int tbi(int x) { return dppi<DPP_BCAST + K>(x); }
 
 // Device-side per-link collision table (built by zb_create), float4-aligned for per-lane loads:
 // [0] bounding sphere, [1+3ci..3+3ci] circle ci: C, E1, E2 (body frame), [7], [8] inscribed spheres,
 // [9] union sphere of the two (midpoint, max r + half their distance + 1 um) for the broadphase.
-// After the NL links: the self-pair list as ints (16 la + lb), NPAIR of them.
+// After the NL links: the self-pair list as ints (16 la + lb), then the default-pose constants.
 constexpr int LINK4 = 10;
 constexpr int NPAIR = (NL - 1) * (NL - 2) / 2;  // non-adjacent link pairs (55), checked by zb_create
-constexpr int PAIR_CHUNK = (NPAIR + 3) / 4;  // broadphase pairs per lane
+constexpr int PAIRS_PER_LANE = (NPAIR + TL - 1) / TL;
 constexpr int DFLT_OFF = NL * LINK4 + (NPAIR + 3) / 4;  // default-pose feet positions, base quat
 constexpr int LNK4 = DFLT_OFF + 3;
 
@@ -393,44 +418,45 @@ constexpr int LNK4 = DFLT_OFF + 3;
 constexpr int NSELF = 18;
 constexpr int NCAND = NL * 4 + NSELF;
 
-// LDS layout of one workgroup (16 envs), float4 units:
-//   YG   [NCM][4][WAVE]  lane-owned row granules: r < 3 {Y_r[3s..3s+2], X_r}, X = {invm0, c01, c02};
-//                        r = 3 {invm1, invm2, vmin, 0}. During detection: the lane's candidate
-//                        staging (granule k = ground 4t+j {x, sep}; self 12+2i {x, sep}, 13+2i {n, code})
-//   LAM  [NCM][WAVE]     lane copy of the contact impulses {ln, l1, l2, 0}; during detection the
-//                        env's body frames [7][3][EPW], union spheres [NL][EPW], then the
-//                        overflow keys / keep flags
-//   INFO [NCM][2][EPW]   selected contacts {x, sep}, {n, code = 16 la + lb + 1}; at the last
-//                        substep [c][0] = {force, -}
-//   LNK  [NL][LINK4]     the link collision table, copied once per workgroup (per-lane reads)
-constexpr int EPW = WAVE / 4;
+// LDS layout of one workgroup (EPW envs), float4 units:
+//   YG    [NCM][WAVE]       lane (e, d) of slot c: {Y0[d], Y1[d], Y2[d], 0} (zero for d >= 12)
+//   AUX   [NCM][2][EPW]     {invm0, invm1, invm2, vmin}, {c01, c02, 0, 0}
+//   LAM   [NCM][EPW]        contact impulses {ln, l1, l2, 0}
+//   FRC   [NCM][EPW]        last substep: contact force {f, code}
+//   CAND  [EPW][NCAND][2]   candidates {x, sep}, {n, code = 16 la + lb + 1}
+//   MAP   [EPW][NCM] int    overflow only: solver slot -> candidate position
+//   KEEP  [EPW][NCAND] f32  overflow only: kept flags
+//   FRAME [NB][3][EPW]      body frames {R row, p}
+//   UB    [NL][EPW]         world union spheres
+//   LNK   [LNK4]            link table copy
 constexpr int YG_OFF = 0;
-constexpr int LAM_OFF = YG_OFF + NCM * 4 * WAVE;
-constexpr int INFO_OFF = LAM_OFF + NCM * WAVE;
-constexpr int LNK_OFF = INFO_OFF + NCM * 2 * EPW;  // copy of the link table (LNK4 granules)
+constexpr int AUX_OFF = YG_OFF + NCM * WAVE;
+constexpr int LAM_OFF = AUX_OFF + NCM * 2 * EPW;
+constexpr int FRC_OFF = LAM_OFF + NCM * EPW;
+constexpr int CAND_OFF = FRC_OFF + NCM * EPW;
+constexpr int MAP_OFF = CAND_OFF + EPW * NCAND * 2;
+constexpr int KEEP_OFF = MAP_OFF + (EPW * NCM + 3) / 4;
+constexpr int FRAME_OFF = KEEP_OFF + (EPW * NCAND + 3) / 4;
+constexpr int UB_OFF = FRAME_OFF + NB * 3 * EPW;
+constexpr int LNK_OFF = UB_OFF + NL * EPW;
 constexpr int LDS4 = LNK_OFF + LNK4;
-constexpr int UB_OFF = LAM_OFF + NB * 3 * EPW;     // [NL][EPW] world union spheres (aliases LAM)
-static_assert(NB * 3 * EPW + NL * EPW <= NCM * WAVE, "frames + union spheres alias LAM");
-static_assert(NB * 3 * EPW <= NCM * WAVE, "frames alias LAM");
-static_assert(2 * EPW * NCAND <= 4 * NCM * WAVE, "keys alias LAM");
-static_assert(12 + 2 * NSELF <= 4 * NCM, "staging fits YG");
 
 struct Q {
   float4* b;
   int lane, e, s;
-  __device__ __forceinline__ float4& yg(int c, int r) const { return b[YG_OFF + (c * 4 + r) * WAVE + lane]; }
-  __device__ __forceinline__ float4& yg_at(int c, int r, int ln) const { return b[YG_OFF + (c * 4 + r) * WAVE + ln]; }
-  __device__ __forceinline__ float4& stg(int k) const { return b[YG_OFF + k * WAVE + lane]; }
-  __device__ __forceinline__ float4& lam(int c) const { return b[LAM_OFF + c * WAVE + lane]; }
-  __device__ __forceinline__ float4& lam_at(int c, int ln) const { return b[LAM_OFF + c * WAVE + ln]; }
-  __device__ __forceinline__ float4& info(int c, int h) const { return b[INFO_OFF + (c * 2 + h) * EPW + e]; }
-  __device__ __forceinline__ float4& frame(int body, int r) const { return b[LAM_OFF + (body * 3 + r) * EPW + e]; }
+  __device__ __forceinline__ float4& yg(int c) const { return b[YG_OFF + c * WAVE + lane]; }
+  __device__ __forceinline__ float4& yg_at(int c, int d) const { return b[YG_OFF + c * WAVE + TL * e + d]; }
+  __device__ __forceinline__ float4& aux(int c, int h) const { return b[AUX_OFF + (c * 2 + h) * EPW + e]; }
+  __device__ __forceinline__ float4& lam(int c) const { return b[LAM_OFF + c * EPW + e]; }
+  __device__ __forceinline__ float4& frc(int c) const { return b[FRC_OFF + c * EPW + e]; }
+  __device__ __forceinline__ float4& cand(int p, int h) const { return b[CAND_OFF + (e * NCAND + p) * 2 + h]; }
+  __device__ __forceinline__ int& map(int c) const { return reinterpret_cast<int*>(b + MAP_OFF)[e * NCM + c]; }
+  __device__ __forceinline__ float& keep(int p) const { return reinterpret_cast<float*>(b + KEEP_OFF)[e * NCAND + p]; }
+  __device__ __forceinline__ float4& frame(int body, int r) const { return b[FRAME_OFF + (body * 3 + r) * EPW + e]; }
+  __device__ __forceinline__ float4& ub(int l) const { return b[UB_OFF + l * EPW + e]; }
   __device__ __forceinline__ const float4* link(int l) const { return b + LNK_OFF + l * LINK4; }
   __device__ __forceinline__ int pair_code(int p) const { return reinterpret_cast<const int*>(b + LNK_OFF + NL * LINK4)[p]; }
   __device__ __forceinline__ const float4* dflt() const { return b + LNK_OFF + DFLT_OFF; }
-  __device__ __forceinline__ float4& ub(int l) const { return b[UB_OFF + l * EPW + e]; }
-  __device__ __forceinline__ float* keys() const { return reinterpret_cast<float*>(b + LAM_OFF) + e * NCAND; }
-  __device__ __forceinline__ float* keep() const { return reinterpret_cast<float*>(b + LAM_OFF) + (EPW + e) * NCAND; }
 };
 
 __device__ __forceinline__ void read_frame(const Q& q, int body, float R[9], float p[3]) {
@@ -445,82 +471,122 @@ __device__ __forceinline__ void mv3f(const float R[9], const float4 v, float o[3
 }
 
 // ------------------------------------------------------------------------- contacts
-// Detection + selection for the quad's env; returns the number of contacts (quad-uniform) and
-// leaves them in INFO[0..nc). Ground: lane s tests links 3s..3s+2 (the lowest rim point of each
-// circle + 90-degree rotations, the first 4 within the margin per link). Self: a sphere-union
-// broadphase over the 55 non-adjacent link pairs (centre = midpoint of a link's two spheres,
-// radius r + half their distance: conservative, so it changes which pairs are tested, never which
-// contacts are found), evaluated redundantly; the candidate pairs are split in rank order into 4
-// contiguous chunks, one per lane, so the quad's candidates stay in canonical order lane by lane.
-__device__ __forceinline__ int detect(MP m, const zb_task_cfg& cfg,
-                                      const Kin& k, float Pz, const Q& q, Stamps& sp) {
-  const float margin = cfg.contact_margin;
+// One self-collision candidate pair: up to 4 sphere-pair contacts, in (sa, sb) order. Emits
+// through `out(x, sep, n, code)`; returns the number found.
+template <class F>
+__device__ __forceinline__ int narrow_pair(const Q& q, int pidx, float margin, F&& out) {
+  const int pcode = q.pair_code(pidx);
+  const int la = pcode >> 4, lb = pcode & 15;
+  float Ra[9], pa[3], Rb[9], pb[3];
+  read_frame(q, link_body(la), Ra, pa);
+  read_frame(q, link_body(lb), Rb, pb);
+  const float4* LA = q.link(la);
+  const float4* LB = q.link(lb);
+  int cnt = 0;
 #pragma unroll
-  for (int b = 0; b < NB; ++b) {
-    q.frame(b, 0) = make_float4(k.R[b][0], k.R[b][1], k.R[b][2], k.p[b][0]);
-    q.frame(b, 1) = make_float4(k.R[b][3], k.R[b][4], k.R[b][5], k.p[b][1]);
-    q.frame(b, 2) = make_float4(k.R[b][6], k.R[b][7], k.R[b][8], k.p[b][2]);
+  for (int sa = 0; sa < 2; ++sa) {
+    const float4 spa = LA[7 + sa];
+    float xa[3];
+    mv3f(Ra, spa, xa);
+    xa[0] += pa[0]; xa[1] += pa[1]; xa[2] += pa[2];
+#pragma unroll
+    for (int sb = 0; sb < 2; ++sb) {
+      const float4 spb = LB[7 + sb];
+      float xb[3];
+      mv3f(Rb, spb, xb);
+      xb[0] += pb[0]; xb[1] += pb[1]; xb[2] += pb[2];
+      const float dv[3] = {xa[0] - xb[0], xa[1] - xb[1], xa[2] - xb[2]};
+      const float dist = sqrtf(dot3(dv, dv));
+      const float sep = dist - (spa.w + spb.w);
+      if (sep < margin && dist > 1e-9f) {
+        float n[3], x[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+          n[a] = dv[a] / dist;
+          x[a] = 0.5f * ((xa[a] - n[a] * spa.w) + (xb[a] + n[a] * spb.w));
+        }
+        out(x, sep, n, (float)(16 * la + lb + 1));
+        ++cnt;
+      }
+    }
+  }
+  return cnt;
+}
+
+// Detection + selection for the team's env; returns the number of contacts (team-uniform) and
+// `over` (more than NCM candidates: slots go through MAP). Ground: lane s tests link s (the lowest
+// rim point of each circle + 90-degree rotations, the first 4 within the margin). Self: a
+// sphere-union broadphase (centre = midpoint of a link's two spheres, radius r + half their
+// distance: conservative, so it changes which pairs are tested, never which contacts are found),
+// pairs split over the team; candidate pairs are split in rank order into contiguous chunks, one
+// per lane, so candidates stay in canonical order lane by lane. Counting pass, team scan, then
+// each lane writes its candidates at their canonical positions.
+__device__ __forceinline__ int detect(const zb_task_cfg& cfg, const Kin& k, float Pz, const Q& q, bool& over,
+                                      Stamps& sp) {
+  const float margin = cfg.contact_margin;
+  if (q.s == 0) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      q.frame(b, 0) = make_float4(k.R[b][0], k.R[b][1], k.R[b][2], k.p[b][0]);
+      q.frame(b, 1) = make_float4(k.R[b][3], k.R[b][4], k.R[b][5], k.p[b][1]);
+      q.frame(b, 2) = make_float4(k.R[b][6], k.R[b][7], k.R[b][8], k.p[b][2]);
+    }
   }
   __syncthreads();
 
-  int taken[3], cnt_g = 0;
-#pragma unroll
-  for (int t = 0; t < 3; ++t) {
-    const int l = 3 * q.s + t;
+  // ground, counting pass: lane s = link s; keep the world circle frames for the write pass
+  const int l = q.s < NL ? q.s : NL - 1;
+  float C[2][3], E1[2][3], E2[2][3], cr0[2], sr0[2];
+  unsigned vmask = 0;  // valid rim candidates (bit 4 ci + r), first 4 only
+  {
     float R[9], p[3];
-    read_frame(q, (l + 1) >> 1, R, p);
+    read_frame(q, link_body(l), R, p);
     const float4* L = q.link(l);
     {
       const float4 us = L[9];
       float c[3];
       mv3f(R, us, c);
-      q.ub(l) = make_float4(c[0] + p[0], c[1] + p[1], c[2] + p[2], us.w);
+      if (q.s < NL) q.ub(l) = make_float4(c[0] + p[0], c[1] + p[1], c[2] + p[2], us.w);
     }
     const float4 bd = L[0];
     float bc[3];
     mv3f(R, bd, bc);
+    const bool near = q.s < NL && !(Pz + p[2] + bc[2] - bd.w > margin);
     int tk = 0;
-    if (!(Pz + p[2] + bc[2] - bd.w > margin)) {
 #pragma unroll
-      for (int ci = 0; ci < 2; ++ci) {
-        float C[3], E1[3], E2[3];
-        mv3f(R, L[1 + 3 * ci], C);
-        mv3f(R, L[2 + 3 * ci], E1);
-        mv3f(R, L[3 + 3 * ci], E2);
-        C[0] += p[0]; C[1] += p[1]; C[2] += p[2];
-        // lowest rim point, biased toward E1 so a flat disk gets a fixed body-attached manifold
-        const float al = -E1[2] + RIM_EPS, be = -E2[2];
-        const float nrm = sqrtf(al * al + be * be);
-        float c0 = 1.f, s0 = 0.f;
-        if (nrm > 1e-12f) { c0 = al / nrm; s0 = be / nrm; }
+    for (int ci = 0; ci < 2; ++ci) {
+      mv3f(R, L[1 + 3 * ci], C[ci]);
+      mv3f(R, L[2 + 3 * ci], E1[ci]);
+      mv3f(R, L[3 + 3 * ci], E2[ci]);
+      C[ci][0] += p[0]; C[ci][1] += p[1]; C[ci][2] += p[2];
+      // lowest rim point, biased toward E1 so a flat disk gets a fixed body-attached manifold
+      const float al = -E1[ci][2] + RIM_EPS, be = -E2[ci][2];
+      const float nrm = sqrtf(al * al + be * be);
+      cr0[ci] = 1.f; sr0[ci] = 0.f;
+      if (nrm > 1e-12f) { cr0[ci] = al / nrm; sr0[ci] = be / nrm; }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float cr = r == 0 ? c0 : (r == 1 ? -s0 : (r == 2 ? -c0 : s0));
-          const float sr = r == 0 ? s0 : (r == 1 ? c0 : (r == 2 ? -s0 : -c0));
-          float x[3];
-#pragma unroll
-          for (int a = 0; a < 3; ++a) x[a] = C[a] + cr * E1[a] + sr * E2[a];
-          const float sep = Pz + x[2];
-          if (sep < margin && tk < 4) {
-            q.stg(4 * t + tk) = make_float4(x[0], x[1], x[2], sep);
-            ++tk;
-          }
-        }
+      for (int r = 0; r < 4; ++r) {
+        const float c0 = cr0[ci], s0 = sr0[ci];
+        const float cr = r == 0 ? c0 : (r == 1 ? -s0 : (r == 2 ? -c0 : s0));
+        const float sr = r == 0 ? s0 : (r == 1 ? c0 : (r == 2 ? -s0 : -c0));
+        const float z = C[ci][2] + cr * E1[ci][2] + sr * E2[ci][2];
+        if (near && Pz + z < margin && tk < 4) { vmask |= 1u << (4 * ci + r); ++tk; }
       }
     }
-    taken[t] = tk;
-    cnt_g += tk;
   }
+  const int cnt_g = __popc(vmask);
   sp.mark(1);
 
-  int cnt_s = 0;
+  // self: broadphase (lane s: pairs [PAIRS_PER_LANE s, +PAIRS_PER_LANE)), team OR of the bits,
+  // then the candidate pairs' narrow phase (counting pass)
+  unsigned long long cmask = 0ull;
+  int cnt_s = 0, chunk = 0, first = 0;
   if (cfg.enable_self_collision) {
-    __syncthreads();  // union spheres of all 12 links
-    // broadphase: lane s tests pairs [PAIR_CHUNK s, PAIR_CHUNK (s+1)); the quad ORs the bits
+    __syncthreads();  // union spheres
     unsigned long long mask = 0ull;
 #pragma unroll
-    for (int j = 0; j < PAIR_CHUNK; ++j) {
-      const int pidx = PAIR_CHUNK * q.s + j;
+    for (int j = 0; j < PAIRS_PER_LANE; ++j) {
+      const int pidx = PAIRS_PER_LANE * q.s + j;
       if (pidx < NPAIR) {
         const int code = q.pair_code(pidx);
         const float4 A = q.ub(code >> 4), B = q.ub(code & 15);
@@ -530,125 +596,91 @@ __device__ __forceinline__ int detect(MP m, const zb_task_cfg& cfg,
       }
     }
     {
-      int lo = (int)(unsigned)mask, hi = (int)(unsigned)(mask >> 32);
-      lo |= dppi<QP_XOR1>(lo); hi |= dppi<QP_XOR1>(hi);
-      lo |= dppi<QP_XOR2>(lo); hi |= dppi<QP_XOR2>(hi);
+      const int lo = tor((int)(unsigned)mask), hi = tor((int)(unsigned)(mask >> 32));
       mask = (unsigned long long)(unsigned)lo | ((unsigned long long)(unsigned)hi << 32);
     }
     const int K = __popcll(mask);
-    const int chunk = (K + 3) >> 2;
-    for (int i = q.s * chunk; i > 0 && mask; --i) mask &= mask - 1ull;
+    chunk = (K + TL - 1) / TL;
+    first = q.s * chunk;
+    for (int i = first; i > 0 && mask; --i) mask &= mask - 1ull;
+    cmask = mask;  // this lane's chunk starts at the lowest remaining bit
     for (int j = 0; j < chunk && mask; ++j) {
       const int pidx = __builtin_ctzll(mask);
       mask &= mask - 1ull;
-      const int pcode = q.pair_code(pidx);
-      const int la = pcode >> 4, lb = pcode & 15;
-      float Ra[9], pa[3], Rb[9], pb[3];
-      read_frame(q, link_body(la), Ra, pa);
-      read_frame(q, link_body(lb), Rb, pb);
-      const float4* LA = q.link(la);
-      const float4* LB = q.link(lb);
-#pragma unroll
-      for (int sa = 0; sa < 2; ++sa) {
-        const float4 spa = LA[7 + sa];
-        float xa[3];
-        mv3f(Ra, spa, xa);
-        xa[0] += pa[0]; xa[1] += pa[1]; xa[2] += pa[2];
-#pragma unroll
-        for (int sb = 0; sb < 2; ++sb) {
-          const float4 spb = LB[7 + sb];
-          float xb[3];
-          mv3f(Rb, spb, xb);
-          xb[0] += pb[0]; xb[1] += pb[1]; xb[2] += pb[2];
-          const float dv[3] = {xa[0] - xb[0], xa[1] - xb[1], xa[2] - xb[2]};
-          const float dist = sqrtf(dot3(dv, dv));
-          const float sep = dist - (spa.w + spb.w);
-          if (sep < margin && dist > 1e-9f && cnt_s < NSELF) {
-            float n[3], x[3];
-#pragma unroll
-            for (int a = 0; a < 3; ++a) {
-              n[a] = dv[a] / dist;
-              x[a] = 0.5f * ((xa[a] - n[a] * spa.w) + (xb[a] + n[a] * spb.w));
-            }
-            q.stg(12 + 2 * cnt_s) = make_float4(x[0], x[1], x[2], sep);
-            q.stg(13 + 2 * cnt_s) = make_float4(n[0], n[1], n[2], (float)(16 * la + lb + 1));
-            ++cnt_s;
-          }
-        }
-      }
+      cnt_s += narrow_pair(q, pidx, margin, [](const float*, float, const float*, float) {});
     }
   }
+  sp.mark(2);
 
-  // canonical positions: ground lane by lane, then self lane by lane (first NSELF kept)
+  // canonical positions (team scans of the packed counts)
   const int packed = cnt_g | (cnt_s << 8);
-  const int pk0 = qbi<0>(packed), pk1 = qbi<1>(packed), pk2 = qbi<2>(packed), pk3 = qbi<3>(packed);
-  const int g_tot = (pk0 & 255) + (pk1 & 255) + (pk2 & 255) + (pk3 & 255);
-  const int s_tot = (pk0 >> 8) + (pk1 >> 8) + (pk2 >> 8) + (pk3 >> 8);
-  const int g_before = (q.s > 0 ? pk0 & 255 : 0) + (q.s > 1 ? pk1 & 255 : 0) + (q.s > 2 ? pk2 & 255 : 0);
-  const int s_before = (q.s > 0 ? pk0 >> 8 : 0) + (q.s > 1 ? pk1 >> 8 : 0) + (q.s > 2 ? pk2 >> 8 : 0);
-  const int my_s = min(cnt_s, max(0, NSELF - s_before));
+  const int incl = tscan(packed);
+  const int tot = tbi<TL - 1>(incl);
+  const int excl = incl - packed;
+  const int g_tot = tot & 255, s_tot = tot >> 8;
+  const int g_before = excl & 255, s_before = excl >> 8;
   const int n = g_tot + min(s_tot, NSELF);
-  const bool over = n > NCM;
+  over = n > NCM;
 
-  // overflow (rare): rank every candidate by (sep, canonical index) against the env's list
-  if (__ballot(over) != 0ull) {
-    __syncthreads();  // body frames are dead; KEYS/KEEP alias them
-    if (over) {
-      float* keys = q.keys();
-      int pos = g_before;
-#pragma unroll
-      for (int t = 0; t < 3; ++t)
-        for (int j = 0; j < taken[t]; ++j) keys[pos++] = q.stg(4 * t + j).w;
-      for (int i = 0; i < my_s; ++i) keys[g_tot + s_before + i] = q.stg(12 + 2 * i).w;
-    }
-    __syncthreads();
-    if (over) {
-      const float* keys = q.keys();
-      float* keep = q.keep();
-      auto rank_of = [&](int pos, float sep) {
-        int r = 0;
-        for (int j = 0; j < n; ++j) r += (keys[j] < sep || (keys[j] == sep && j < pos)) ? 1 : 0;
-        return r;
-      };
-      int pos = g_before;
-#pragma unroll
-      for (int t = 0; t < 3; ++t)
-        for (int j = 0; j < taken[t]; ++j, ++pos) keep[pos] = rank_of(pos, keys[pos]) < NCM ? 1.f : 0.f;
-      for (int i = 0; i < my_s; ++i) {
-        const int ps = g_tot + s_before + i;
-        keep[ps] = rank_of(ps, keys[ps]) < NCM ? 1.f : 0.f;
-      }
-    }
-    __syncthreads();
-  }
-  // move the kept candidates into their solver slots
-  {
-    const float* keep = q.keep();
-    auto slot_of = [&](int pos) {
-      if (!over) return pos;
-      if (keep[pos] == 0.f) return -1;
-      int c = 0;
-      for (int j = 0; j < pos; ++j) c += keep[j] != 0.f ? 1 : 0;
-      return c;
-    };
+  // write pass: ground candidates of link s, then this lane's self candidates (first NSELF)
+  if (cnt_g) {
     int pos = g_before;
+    const float code = (float)(16 * l);
 #pragma unroll
-    for (int t = 0; t < 3; ++t) {
-      const float code = (float)(16 * (3 * q.s + t));
-      for (int j = 0; j < taken[t]; ++j, ++pos) {
-        const int c = slot_of(pos);
-        if (c >= 0) {
-          q.info(c, 0) = q.stg(4 * t + j);
-          q.info(c, 1) = make_float4(0.f, 0.f, 1.f, code);
+    for (int ci = 0; ci < 2; ++ci)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (vmask & (1u << (4 * ci + r))) {
+          const float c0 = cr0[ci], s0 = sr0[ci];
+          const float cr = r == 0 ? c0 : (r == 1 ? -s0 : (r == 2 ? -c0 : s0));
+          const float sr = r == 0 ? s0 : (r == 1 ? c0 : (r == 2 ? -s0 : -c0));
+          float x[3];
+#pragma unroll
+          for (int a = 0; a < 3; ++a) x[a] = C[ci][a] + cr * E1[ci][a] + sr * E2[ci][a];
+          q.cand(pos, 0) = make_float4(x[0], x[1], x[2], Pz + x[2]);
+          q.cand(pos, 1) = make_float4(0.f, 0.f, 1.f, code);
+          ++pos;
         }
-      }
+  }
+  if (cnt_s && s_before < NSELF) {
+    int pos = g_tot + s_before;
+    const int end = g_tot + NSELF;
+    unsigned long long mask = cmask;
+    for (int j = 0; j < chunk && mask; ++j) {
+      const int pidx = __builtin_ctzll(mask);
+      mask &= mask - 1ull;
+      narrow_pair(q, pidx, margin, [&](const float* x, float sep, const float* nn, float code) {
+        if (pos < end) {
+          q.cand(pos, 0) = make_float4(x[0], x[1], x[2], sep);
+          q.cand(pos, 1) = make_float4(nn[0], nn[1], nn[2], code);
+        }
+        ++pos;
+      });
     }
-    for (int i = 0; i < my_s; ++i) {
-      const int c = slot_of(g_tot + s_before + i);
-      if (c >= 0) {
-        q.info(c, 0) = q.stg(12 + 2 * i);
-        q.info(c, 1) = q.stg(13 + 2 * i);
+  }
+
+  // overflow (rare): rank every candidate by (sep, canonical index); MAP = kept positions in order
+  if (__ballot(over) != 0ull) {
+    __syncthreads();
+    if (over)
+      for (int p = q.s; p < n; p += TL) {
+        const float sp_ = q.cand(p, 0).w;
+        int r = 0;
+        for (int j = 0; j < n; ++j) {
+          const float sj = q.cand(j, 0).w;
+          r += (sj < sp_ || (sj == sp_ && j < p)) ? 1 : 0;
+        }
+        q.keep(p) = r < NCM ? 1.f : 0.f;
       }
+    __syncthreads();
+    if (over && q.s < NCM) {
+      int c = 0, pos = -1;
+      for (int p = 0; p < n; ++p)
+        if (q.keep(p) != 0.f) {
+          if (c == q.s) pos = p;
+          ++c;
+        }
+      q.map(q.s) = pos;
     }
   }
   __syncthreads();
@@ -673,20 +705,20 @@ struct SensorOut {
   float tau2;           // sum of squared Isaac Lab applied torques (torques reward)
 };
 
-// One Gauss-Seidel contact update (normal + Coulomb disk). a0..a2: the lane's row granules
-// {Y_r[3s..3s+2], X_r} (X = invm0, c01, c02), a3 = {invm1, invm2, vmin, -}; lam = {ln, l1, l2}.
-// The three row dots are reduced across the quad; the tangent velocities see the normal update
-// through the cross terms. Returns the new impulses; w0..w2 (the lane's coordinates) updated.
-__device__ __forceinline__ float4 pgs_update(const float4 a0, const float4 a1, const float4 a2, const float4 a3,
-                                             const float4 lam, float mu, float& w0, float& w1, float& w2) {
-  const float p0 = qsum(a0.x * w0 + a0.y * w1 + a0.z * w2);
-  const float p1 = qsum(a1.x * w0 + a1.y * w1 + a1.z * w2);
-  const float p2 = qsum(a2.x * w0 + a2.y * w1 + a2.z * w2);
-  const float ln = fmaxf(lam.x + (a3.z - p0) * a0.w, 0.f);
+// One Gauss-Seidel contact update (normal + Coulomb disk). g = {Y0[d], Y1[d], Y2[d], -} of this
+// lane's coordinate d, a0 = {invm0, invm1, invm2, vmin}, a1 = {c01, c02, -, -}, lam = {ln, l1, l2}.
+// The three row dots are reduced across the team; the tangent velocities see the normal update
+// through the cross terms. Returns the new impulses; wd (the lane's coordinate) updated.
+__device__ __forceinline__ float4 pgs_update(const float4 g, const float4 a0, const float4 a1, const float4 lam,
+                                             float mu, float& wd) {
+  const float p0 = tsum(g.x * wd);
+  const float p1 = tsum(g.y * wd);
+  const float p2 = tsum(g.z * wd);
+  const float ln = fmaxf(lam.x + (a0.w - p0) * a0.x, 0.f);
   const float dl = ln - lam.x;
-  const float vt1 = p1 + a1.w * dl, vt2 = p2 + a2.w * dl;
-  float l1 = lam.y - vt1 * a3.x;
-  float l2 = lam.z - vt2 * a3.y;
+  const float vt1 = p1 + a1.x * dl, vt2 = p2 + a1.y * dl;
+  float l1 = lam.y - vt1 * a0.y;
+  float l2 = lam.z - vt2 * a0.z;
   const float lim = mu * ln;
   const float mag2 = l1 * l1 + l2 * l2;
   if (mag2 > lim * lim) {
@@ -694,17 +726,8 @@ __device__ __forceinline__ float4 pgs_update(const float4 a0, const float4 a1, c
     l1 *= sc; l2 *= sc;
   }
   const float d1 = l1 - lam.y, d2 = l2 - lam.z;
-  w0 += a0.x * dl + a1.x * d1 + a2.x * d2;
-  w1 += a0.y * dl + a1.y * d1 + a2.y * d2;
-  w2 += a0.z * dl + a1.z * d1 + a2.z * d2;
+  wd += g.x * dl + g.y * d1 + g.z * d2;
   return make_float4(ln, l1, l2, 0.f);
-}
-
-// write the 3 granules of a 12-vector split over the quad's lanes: lane s' gets v[3s'..3s'+2]
-__device__ __forceinline__ void put_split(const Q& q, int c, int r, const float v[NV], float x) {
-  const int base = 4 * q.e;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) q.yg_at(c, r, base + k) = make_float4(v[3 * k], v[3 * k + 1], v[3 * k + 2], x);
 }
 
 // ------------------------------------------------------------------------- one substep
@@ -729,13 +752,13 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
   float S[ND][6], org[ND][3];
   SI I[NB];
   int nc;
-  __syncthreads();  // the previous substep's LDS readers are done (frames alias LAM)
+  bool over;
+  __syncthreads();  // the previous substep's LDS readers are done
   {
     Kin k;
     fk(m, s, k);
     sp.mark(9);
-    nc = detect(opaque(m0), cfg, k, s.pos[2], q, sp);
-    sp.mark(2);
+    nc = detect(cfg, k, s.pos[2], q, over, sp);
     m = opaque(m0);
 #pragma unroll
     for (int j = 0; j < ND; ++j) {
@@ -889,158 +912,130 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
   }
 
   sp.mark(4);
-  // contact rows (lane s builds slots s, s+4, s+8): Y = L^-1 J^T (whitened), effective masses,
-  // the normal/tangent cross terms and the bias velocity. J of direction d at point x on body b:
+  // contact rows (lane s builds slot s): Y = L^-1 J^T (whitened), effective masses, the
+  // normal/tangent cross terms and the bias velocity. J of direction d at point x on body b:
   // [x x d ; d ; d.(a_j x (x - o_j)) for joints j < b]
+  if (q.s < nc) {
+    const int c = q.s;
+    const int pos = over ? q.map(c) : c;
+    const float4 g0 = q.cand(pos, 0), gn = q.cand(pos, 1);
+    const float x[3] = {g0.x, g0.y, g0.z};
+    const float n[3] = {gn.x, gn.y, gn.z};
+    const float sep = g0.w;
+    const int code = (int)gn.w;
+    const int ba = link_body(code >> 4);
+    const int lb = (code & 15) - 1;
+    const int bb = lb >= 0 ? link_body(lb) : -1;
+    // per-joint lever vectors a_j x (x - o_j), signed by which side of the contact the joint is on
+    float cj[ND][3];
 #pragma unroll
-  for (int t = 0; t < 3; ++t) {
-    const int c = q.s + 4 * t;
-    if (c < nc) {
-      const float4 g0 = q.info(c, 0), gn = q.info(c, 1);
-      const float x[3] = {g0.x, g0.y, g0.z};
-      const float n[3] = {gn.x, gn.y, gn.z};
-      const float sep = g0.w;
-      const int code = (int)gn.w;
-      const int ba = link_body(code >> 4);
-      const int lb = (code & 15) - 1;
-      const int bb = lb >= 0 ? link_body(lb) : -1;
-      // per-joint lever vectors a_j x (x - o_j), signed by which side of the contact the joint is on
-      float cj[ND][3];
-#pragma unroll
-      for (int j = 0; j < ND; ++j) {
-        const float xo[3] = {x[0] - org[j][0], x[1] - org[j][1], x[2] - org[j][2]};
-        float c3[3];
-        cross3(S[j], xo, c3);
-        const float sg = (j < ba ? 1.f : 0.f) - (j < bb ? 1.f : 0.f);
-        cj[j][0] = sg * c3[0]; cj[j][1] = sg * c3[1]; cj[j][2] = sg * c3[2];
-      }
-      const float root = bb >= 0 ? 0.f : 1.f;  // self contacts: the root terms cancel
-      float t1[3], t2[3];
-      tangents(n, t1, t2);
-      float invm[3], Y0[NV];
-#pragma unroll
-      for (int r = 0; r < 3; ++r) {
-        float d[3];
-#pragma unroll
-        for (int a = 0; a < 3; ++a) d[a] = r == 0 ? n[a] : (r == 1 ? t1[a] : t2[a]);
-        float J[NV], Y[NV];
-        float xd[3];
-        cross3(x, d, xd);
-        J[0] = root * xd[0]; J[1] = root * xd[1]; J[2] = root * xd[2];
-        J[3] = root * d[0]; J[4] = root * d[1]; J[5] = root * d[2];
-#pragma unroll
-        for (int j = 0; j < ND; ++j) J[6 + j] = dot3(cj[j], d);
-        fwd_sub(L, Li, J, Y);
-        invm[r] = 1.f / (dot12(Y, Y) + 1e-9f);
-        if (r == 0) {
-#pragma unroll
-          for (int a = 0; a < NV; ++a) Y0[a] = Y[a];
-          put_split(q, c, 0, Y, invm[0]);
-        } else {
-          put_split(q, c, r, Y, dot12(Y, Y0));  // c01 / c02
-        }
-      }
-      float vmin;
-      if (sep >= 0.f) vmin = -sep / dt;
-      else vmin = fminf(cfg.baumgarte * (-sep) / dt, m->max_depenetration_velocity);
-      const int base = 4 * q.e;
-#pragma unroll
-      for (int kq = 0; kq < 4; ++kq) {
-        q.yg_at(c, 3, base + kq) = make_float4(invm[1], invm[2], vmin, 0.f);
-        q.lam_at(c, base + kq) = make_float4(0.f, 0.f, 0.f, 0.f);
-      }
+    for (int j = 0; j < ND; ++j) {
+      const float xo[3] = {x[0] - org[j][0], x[1] - org[j][1], x[2] - org[j][2]};
+      float c3[3];
+      cross3(S[j], xo, c3);
+      const float sg = (j < ba ? 1.f : 0.f) - (j < bb ? 1.f : 0.f);
+      cj[j][0] = sg * c3[0]; cj[j][1] = sg * c3[1]; cj[j][2] = sg * c3[2];
     }
+    const float root = bb >= 0 ? 0.f : 1.f;  // self contacts: the root terms cancel
+    float t1[3], t2[3];
+    tangents(n, t1, t2);
+    float invm[3], Y[3][NV];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      float d[3];
+#pragma unroll
+      for (int a = 0; a < 3; ++a) d[a] = r == 0 ? n[a] : (r == 1 ? t1[a] : t2[a]);
+      float J[NV];
+      float xd[3];
+      cross3(x, d, xd);
+      J[0] = root * xd[0]; J[1] = root * xd[1]; J[2] = root * xd[2];
+      J[3] = root * d[0]; J[4] = root * d[1]; J[5] = root * d[2];
+#pragma unroll
+      for (int j = 0; j < ND; ++j) J[6 + j] = dot3(cj[j], d);
+      fwd_sub(L, Li, J, Y[r]);
+      invm[r] = 1.f / (dot12(Y[r], Y[r]) + 1e-9f);
+    }
+#pragma unroll
+    for (int d = 0; d < NV; ++d) q.yg_at(c, d) = make_float4(Y[0][d], Y[1][d], Y[2][d], 0.f);
+#pragma unroll
+    for (int d = NV; d < TL; ++d) q.yg_at(c, d) = make_float4(0.f, 0.f, 0.f, 0.f);
+    float vmin;
+    if (sep >= 0.f) vmin = -sep / dt;
+    else vmin = fminf(cfg.baumgarte * (-sep) / dt, m->max_depenetration_velocity);
+    q.aux(c, 0) = make_float4(invm[0], invm[1], invm[2], vmin);
+    q.aux(c, 1) = make_float4(dot12(Y[1], Y[0]), dot12(Y[2], Y[0]), 0.f, 0.f);  // c01, c02
+    q.lam(c) = make_float4(0.f, 0.f, 0.f, 0.f);
   }
   __syncthreads();
 
   sp.mark(5);
-  // projected Gauss-Seidel on the whitened velocity (Coulomb disk friction). Lane s owns
-  // w[3s..3s+2]; per contact: 4 granule reads + the impulse, three quad-reduced row dots.
+  // projected Gauss-Seidel on the whitened velocity (Coulomb disk friction); lane s owns w[s].
+  // The sweep is flattened to K = iterations x nc contact updates and unrolled by two with
+  // ping-pong register sets: the granules and impulse of update k+1 are read while update k
+  // computes. With one contact the prefetched impulse is the one being updated (forwarded).
   {
     const float mu = cfg.friction;
-    float w0, w1, w2;
-    {
-      const int s3 = q.s;
-      w0 = s3 == 0 ? w[0] : (s3 == 1 ? w[3] : (s3 == 2 ? w[6] : w[9]));
-      w1 = s3 == 0 ? w[1] : (s3 == 1 ? w[4] : (s3 == 2 ? w[7] : w[10]));
-      w2 = s3 == 0 ? w[2] : (s3 == 1 ? w[5] : (s3 == 2 ? w[8] : w[11]));
-    }
-    // The sweep is flattened to K = iterations x nc contact updates and unrolled by two with
-    // ping-pong register sets: the granules and impulse of update k+1 are read while update k
-    // computes. With one contact the prefetched impulse is the one being updated (forwarded).
+    float wd = 0.f;
+#pragma unroll
+    for (int d = 0; d < NV; ++d) wd = q.s == d ? w[d] : wd;
+    const bool lead = q.s == 0;
     const int K = cfg.solver_iterations * nc;
     int cA = 0;
-    float4 A0 = q.yg(0, 0), A1 = q.yg(0, 1), A2 = q.yg(0, 2), A3 = q.yg(0, 3), LA = q.lam(0);
+    float4 GA = q.yg(0), XA = q.aux(0, 0), ZA = q.aux(0, 1), LA = q.lam(0);
     for (int k = 0; k < K; k += 2) {
       const int cB = cA + 1 == nc ? 0 : cA + 1;
-      const float4 B0 = q.yg(cB, 0), B1 = q.yg(cB, 1), B2 = q.yg(cB, 2), B3 = q.yg(cB, 3);
+      const float4 GB = q.yg(cB), XB = q.aux(cB, 0), ZB = q.aux(cB, 1);
       float4 LB = q.lam(cB);
-      const float4 nA = pgs_update(A0, A1, A2, A3, LA, mu, w0, w1, w2);
-      q.lam(cA) = nA;
+      const float4 nA = pgs_update(GA, XA, ZA, LA, mu, wd);
+      if (lead) q.lam(cA) = nA;
       if (cB == cA) LB = nA;
       if (k + 1 < K) {
         const int cA2 = cB + 1 == nc ? 0 : cB + 1;
-        A0 = q.yg(cA2, 0); A1 = q.yg(cA2, 1); A2 = q.yg(cA2, 2); A3 = q.yg(cA2, 3);
+        GA = q.yg(cA2); XA = q.aux(cA2, 0); ZA = q.aux(cA2, 1);
         LA = q.lam(cA2);
-        const float4 nB = pgs_update(B0, B1, B2, B3, LB, mu, w0, w1, w2);
-        q.lam(cB) = nB;
+        const float4 nB = pgs_update(GB, XB, ZB, LB, mu, wd);
+        if (lead) q.lam(cB) = nB;
         if (cA2 == cB) LA = nB;
         cA = cA2;
       }
     }
-    w[0] = qb<0>(w0); w[1] = qb<0>(w1); w[2] = qb<0>(w2);
-    w[3] = qb<1>(w0); w[4] = qb<1>(w1); w[5] = qb<1>(w2);
-    w[6] = qb<2>(w0); w[7] = qb<2>(w1); w[8] = qb<2>(w2);
-    w[9] = qb<3>(w0); w[10] = qb<3>(w1); w[11] = qb<3>(w2);
+    w[0] = tb<0>(wd); w[1] = tb<1>(wd); w[2] = tb<2>(wd); w[3] = tb<3>(wd);
+    w[4] = tb<4>(wd); w[5] = tb<5>(wd); w[6] = tb<6>(wd); w[7] = tb<7>(wd);
+    w[8] = tb<8>(wd); w[9] = tb<9>(wd); w[10] = tb<10>(wd); w[11] = tb<11>(wd);
   }
+  __syncthreads();  // last impulses visible to every lane
   sp.mark(6);
   float un[NV];
   bwd_sub(L, Li, w, un);
 
   if (last) {
     // ContactSensor inputs: net force on the feet, max |net force| over undesired links.
-    // Lane s forms the forces of its slots, then sums the env's contacts onto links 3s..3s+2.
+    // Lane s forms the force of slot s, then sums the env's contacts onto link s.
+    if (q.s < nc) {
+      const int pos = over ? q.map(q.s) : q.s;
+      const float4 gn = q.cand(pos, 1), lam = q.lam(q.s);
+      const float n[3] = {gn.x, gn.y, gn.z};
+      float t1[3], t2[3];
+      tangents(n, t1, t2);
+      float f[3];
 #pragma unroll
-    for (int t = 0; t < 3; ++t) {
-      const int c = q.s + 4 * t;
-      if (c < nc) {
-        const float4 gn = q.info(c, 1), lam = q.lam(c);
-        const float n[3] = {gn.x, gn.y, gn.z};
-        float t1[3], t2[3];
-        tangents(n, t1, t2);
-        float f[3];
-#pragma unroll
-        for (int a = 0; a < 3; ++a) f[a] = (lam.x * n[a] + lam.y * t1[a] + lam.z * t2[a]) / dt;
-        q.info(c, 0) = make_float4(f[0], f[1], f[2], gn.w);
-      }
+      for (int a = 0; a < 3; ++a) f[a] = (lam.x * n[a] + lam.y * t1[a] + lam.z * t2[a]) / dt;
+      q.frc(q.s) = make_float4(f[0], f[1], f[2], gn.w);
     }
     __syncthreads();
-    float Fl[3][3];
-#pragma unroll
-    for (int t = 0; t < 3; ++t) Fl[t][0] = Fl[t][1] = Fl[t][2] = 0.f;
+    float Fl[3] = {0.f, 0.f, 0.f};
     for (int c = 0; c < nc; ++c) {
-      const float4 f = q.info(c, 0);
+      const float4 f = q.frc(c);
       const int code = (int)f.w;
       const int la = code >> 4, lb = (code & 15) - 1;
-#pragma unroll
-      for (int t = 0; t < 3; ++t) {
-        const int l = 3 * q.s + t;
-        const float sa = (l == la ? 1.f : 0.f) - (l == lb ? 1.f : 0.f);
-        Fl[t][0] += sa * f.x; Fl[t][1] += sa * f.y; Fl[t][2] += sa * f.z;
-      }
+      const float sa = (q.s == la ? 1.f : 0.f) - (q.s == lb ? 1.f : 0.f);
+      Fl[0] += sa * f.x; Fl[1] += sa * f.y; Fl[2] += sa * f.z;
     }
-    float fmax = 0.f;
+    const float fm = (q.s >= 1 && q.s <= 10) ? sqrtf(dot3(Fl, Fl)) : 0.f;
+    so.undes_fmax = tmax(fm);
 #pragma unroll
-    for (int t = 0; t < 3; ++t) {
-      const int l = 3 * q.s + t;
-      if (l >= 1 && l <= 10) fmax = fmaxf(fmax, sqrtf(dot3(Fl[t], Fl[t])));
-    }
-    so.undes_fmax = qmax(fmax);
-#pragma unroll
-    for (int a = 0; a < 3; ++a) { so.feet_f[0][a] = qb<0>(Fl[0][a]); so.feet_f[1][a] = qb<3>(Fl[2][a]); }
-    if (kDebugForces)
-#pragma unroll
-      for (int t = 0; t < 3; ++t) { dbgF[t][0] = Fl[t][0]; dbgF[t][1] = Fl[t][1]; dbgF[t][2] = Fl[t][2]; }
+    for (int a = 0; a < 3; ++a) { so.feet_f[0][a] = tb<0>(Fl[a]); so.feet_f[1][a] = tb<11>(Fl[a]); }
+    if (kDebugForces) { dbgF[0][0] = Fl[0]; dbgF[0][1] = Fl[1]; dbgF[0][2] = Fl[2]; }
   }
 
 #pragma unroll
@@ -1294,31 +1289,37 @@ __global__ __launch_bounds__(WAVE, 1) void zb_step_kernel(const zb_model* __rest
   MP m = to_mp(mg);
   __shared__ float4 lds[LDS4];
   const int lane = threadIdx.x;
-  const int env = blockIdx.x * EPW + (lane >> 2);
-  // a quad past N recomputes env N-1 (identical values, identical stores); it never logs
+  const int env = blockIdx.x * EPW + lane / TL;
+  // a team past N recomputes env N-1 (identical values, identical stores); it never logs
   const int i = env < N ? env : N - 1;
-  const bool lead = env < N && (lane & 3) == 0;
-  const Q q{lds, lane, lane >> 2, lane & 3};
+  const bool lead = env < N && lane % TL == 0;
+  const Q q{lds, lane, lane / TL, lane % TL};
   for (int t = lane; t < LNK4; t += WAVE) lds[LNK_OFF + t] = links[t];
-#define ST(f) st[(size_t)(f) * N + i]
+  // the env's state row: lane s loads fields s, s+16, ... (one coalesced load per field group)
   Stamps sp;
   sp.begin();
+#define ST(f) st[(size_t)(f) * N + i]
   Phys p;
-  load_phys(st, N, i, p);
+#pragma unroll
+  for (int a = 0; a < 3; ++a) { p.pos[a] = ST(ZB_S_ROOT_POS + a); p.lv[a] = ST(ZB_S_ROOT_LINVEL + a); p.av[a] = ST(ZB_S_ROOT_ANGVEL + a); }
+#pragma unroll
+  for (int a = 0; a < 4; ++a) p.quat[a] = ST(ZB_S_ROOT_QUAT + a);
+#pragma unroll
+  for (int j = 0; j < ND; ++j) { p.jq[j] = ST(ZB_S_JOINT_POS + j); p.jqd[j] = ST(ZB_S_JOINT_VEL + j); }
 
-  // _pre_physics_step (v2.py:276-287); _actions / p_delta are final here and stored at once
+  // _pre_physics_step (v2.py:276-287); _actions / p_delta are stored with the rest at the end
+  // (one writer lane per env; the team holds identical values)
+  const bool writer = q.s == 0;
   const float step_dt = cfg.sim_dt * (float)cfg.decimation;
-  float target[ND];
+  float target[ND], a_now[ND], pdel[ND];
   float r_action_rate = 0.f;
 #pragma unroll
   for (int j = 0; j < ND; ++j) {
     const float a_prev = ST(ZB_S_ACTIONS + j);
-    const float a_now = tanh_r(act[(size_t)i * ZB_ACT_DIM + j]);
-    const float pd = clampf(ST(ZB_S_P_DELTA + j) + PI_F * a_now * cfg.joint_speed_limit * step_dt, -PI_F, PI_F);
-    ST(ZB_S_P_DELTA + j) = pd;
-    ST(ZB_S_ACTIONS + j) = a_now;
-    target[j] = pd + m->default_joint_pos[j];
-    r_action_rate += (a_now - a_prev) * (a_now - a_prev);   // v2.py:502-507
+    a_now[j] = tanh_r(act[(size_t)i * ZB_ACT_DIM + j]);
+    pdel[j] = clampf(ST(ZB_S_P_DELTA + j) + PI_F * a_now[j] * cfg.joint_speed_limit * step_dt, -PI_F, PI_F);
+    target[j] = pdel[j] + m->default_joint_pos[j];
+    r_action_rate += (a_now[j] - a_prev) * (a_now[j] - a_prev);   // v2.py:502-507
   }
 
   // the previous _get_observations cache (one-step lag, v2.py:315-345): the pre-step terms are
@@ -1357,34 +1358,40 @@ __global__ __launch_bounds__(WAVE, 1) void zb_step_kernel(const zb_model* __rest
   }
   m = opaque(m);
 
-  // ContactSensor lazy update, once per policy step (history roll, air/contact timers)
-  float fz_hist[ZB_HIST][2], fmax_hist[ZB_HIST];
+  // MDP state of this env (every lane loads; one writer lane stores at the end)
+  float fz_prev[ZB_HIST - 1][2], fmax_prev[ZB_HIST - 1], air_cur0[2], air_last0[2], contact0[2];
+  float step_len[2], f_last0[2], down[2][3], sums0[ZB_NUM_REWARD_TERMS];
 #pragma unroll
-  for (int h = ZB_HIST - 1; h > 0; --h) {
-    fz_hist[h][0] = ST(ZB_S_FEET_FZ_HIST + 2 * (h - 1));
-    fz_hist[h][1] = ST(ZB_S_FEET_FZ_HIST + 2 * (h - 1) + 1);
-    fmax_hist[h] = ST(ZB_S_UNDES_FMAX_HIST + h - 1);
+  for (int h = 0; h < ZB_HIST - 1; ++h) {
+    fz_prev[h][0] = ST(ZB_S_FEET_FZ_HIST + 2 * h);
+    fz_prev[h][1] = ST(ZB_S_FEET_FZ_HIST + 2 * h + 1);
+    fmax_prev[h] = ST(ZB_S_UNDES_FMAX_HIST + h);
   }
-  fmax_hist[0] = so.undes_fmax;
-  float air_last[2];
 #pragma unroll
   for (int f = 0; f < 2; ++f) {
-    fz_hist[0][f] = so.feet_f[f][2];
-    const bool contact = sqrtf(dot3(so.feet_f[f], so.feet_f[f])) > cfg.contact_force_threshold;
-    const float air_cur = ST(ZB_S_FEET_AIR_CUR + f);
-    air_last[f] = ST(ZB_S_FEET_AIR_LAST + f);
-    if (air_cur > 0.f && contact) air_last[f] = air_cur + step_dt;
-    ST(ZB_S_FEET_AIR_CUR + f) = contact ? 0.f : air_cur + step_dt;
-    ST(ZB_S_FEET_CONTACT_CUR + f) = contact ? ST(ZB_S_FEET_CONTACT_CUR + f) + step_dt : 0.f;
-    ST(ZB_S_FEET_AIR_LAST + f) = air_last[f];
-  }
+    air_cur0[f] = ST(ZB_S_FEET_AIR_CUR + f);
+    air_last0[f] = ST(ZB_S_FEET_AIR_LAST + f);
+    contact0[f] = ST(ZB_S_FEET_CONTACT_CUR + f);
+    step_len[f] = ST(ZB_S_FEET_STEP_LEN + f);
+    f_last0[f] = ST(ZB_S_FEET_F_LAST + f);
 #pragma unroll
-  for (int h = 0; h < ZB_HIST; ++h) {
-    ST(ZB_S_FEET_FZ_HIST + 2 * h) = fz_hist[h][0];
-    ST(ZB_S_FEET_FZ_HIST + 2 * h + 1) = fz_hist[h][1];
-    ST(ZB_S_UNDES_FMAX_HIST + h) = fmax_hist[h];
+    for (int a = 0; a < 3; ++a) down[f][a] = ST(ZB_S_FEET_DOWN_POS + 3 * f + a);
   }
   const float ep_len = ST(ZB_S_EP_LEN) + 1.f;
+  const float hs0 = ST(ZB_S_HEADING_SUM), ys0 = ST(ZB_S_Y_ERR_SUM);
+#pragma unroll
+  for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) sums0[t] = ST(ZB_S_EP_SUMS + t);
+  sp.mark(10);
+
+  // ContactSensor lazy update, once per policy step (history roll, air/contact timers)
+  float air_cur[2], air_last[2], contact_t[2];
+#pragma unroll
+  for (int f = 0; f < 2; ++f) {
+    const bool contact = sqrtf(dot3(so.feet_f[f], so.feet_f[f])) > cfg.contact_force_threshold;
+    air_last[f] = (air_cur0[f] > 0.f && contact) ? air_cur0[f] + step_dt : air_last0[f];
+    air_cur[f] = contact ? 0.f : air_cur0[f] + step_dt;
+    contact_t[f] = contact ? contact0[f] + step_dt : 0.f;
+  }
 
   // post-step feet COM velocities (feet_slide)
   float feet_vel[2][3], obs_q[4];
@@ -1398,20 +1405,21 @@ __global__ __launch_bounds__(WAVE, 1) void zb_step_kernel(const zb_model* __rest
     float bp[3];
     link_pose(m, k, 6, bp, obs_q);  // base quat of the post-step state (observation)
   }
+  sp.mark(11);
 
   // _get_dones (v2.py:384-411)
   const bool time_out = ep_len >= (float)(cfg.max_episode_length - 1);
   float feetF[2];
 #pragma unroll
   for (int f = 0; f < 2; ++f) {
-    float sacc = 0.f;
+    float sacc = so.feet_f[f][2];
 #pragma unroll
-    for (int h = 0; h < ZB_HIST; ++h) sacc += fz_hist[h][f];
+    for (int h = 0; h < ZB_HIST - 1; ++h) sacc += fz_prev[h][f];
     feetF[f] = sacc / (float)ZB_HIST;
   }
-  bool died = false;
+  bool died = so.undes_fmax > 1.0f;
 #pragma unroll
-  for (int h = 0; h < ZB_HIST; ++h) died |= fmax_hist[h] > 1.0f;
+  for (int h = 0; h < ZB_HIST - 1; ++h) died |= fmax_prev[h] > 1.0f;
   died |= pre_base_z < cfg.termination_height;
   died |= fabsf(pre_base_y) > 0.5f;  // base_pos_y_err vs env origin (local frame: 0)
 
@@ -1421,30 +1429,21 @@ __global__ __launch_bounds__(WAVE, 1) void zb_step_kernel(const zb_model* __rest
   r[ZB_R_FEET_DOWNWARD] = r_pre[1];
   r[ZB_R_FEET_FORWARD] = r_pre[2];
   r[ZB_R_BASE_HEADING_X] = r_pre[3];
-  {
-    const float hs = clampf(ST(ZB_S_HEADING_SUM) + 0.01f * pre_heading, -1.f, 1.f);
-    ST(ZB_S_HEADING_SUM) = hs;
-    r[ZB_R_BASE_HEADING_X_SUM] = fabsf(hs);
-  }
-  {
-    float step_len[2];
+  const float hs = clampf(hs0 + 0.01f * pre_heading, -1.f, 1.f);
+  r[ZB_R_BASE_HEADING_X_SUM] = fabsf(hs);
 #pragma unroll
-    for (int f = 0; f < 2; ++f) {
-      step_len[f] = ST(ZB_S_FEET_STEP_LEN + f);
-      if (feetF[f] > 10.f && ST(ZB_S_FEET_F_LAST + f) < 10.f) {   // touchdown, v2.py:514-517
-        float dv[3];
+  for (int f = 0; f < 2; ++f) {
+    if (feetF[f] > 10.f && f_last0[f] < 10.f) {   // touchdown, v2.py:514-517
+      float dv[3];
 #pragma unroll
-        for (int a = 0; a < 3; ++a) {
-          dv[a] = pre_feet[f][a] - ST(ZB_S_FEET_DOWN_POS + 3 * f + a);
-          ST(ZB_S_FEET_DOWN_POS + 3 * f + a) = pre_feet[f][a];
-        }
-        step_len[f] = dot3(dv, pre_fwd);
-        ST(ZB_S_FEET_STEP_LEN + f) = step_len[f];
+      for (int a = 0; a < 3; ++a) {
+        dv[a] = pre_feet[f][a] - down[f][a];
+        down[f][a] = pre_feet[f][a];
       }
-      ST(ZB_S_FEET_F_LAST + f) = feetF[f];
+      step_len[f] = dot3(dv, pre_fwd);
     }
-    r[ZB_R_STEP_LENGTH] = tanh_r(15.f * fminf(step_len[0], step_len[1]));
   }
+  r[ZB_R_STEP_LENGTH] = tanh_r(15.f * fminf(step_len[0], step_len[1]));
   r[ZB_R_AIRTIME_BALANCE] = fabsf(air_last[0] - air_last[1]);
   r[ZB_R_ACTION_RATE] = r_action_rate;
   r[ZB_R_TORQUES] = so.tau2;
@@ -1456,62 +1455,90 @@ __global__ __launch_bounds__(WAVE, 1) void zb_step_kernel(const zb_model* __rest
     r[ZB_R_FEET_SLIDE] = sacc;
   }
   r[ZB_R_BASE_POS_Y_ERR] = r_pre[4];
-  {
-    const float ys = clampf(ST(ZB_S_Y_ERR_SUM) + 0.01f * pre_base_y, -1.f, 1.f);
-    ST(ZB_S_Y_ERR_SUM) = ys;
-    r[ZB_R_BASE_POS_Y_ERR_SUM] = fabsf(ys);
-  }
+  const float ys = clampf(ys0 + 0.01f * pre_base_y, -1.f, 1.f);
+  r[ZB_R_BASE_POS_Y_ERR_SUM] = fabsf(ys);
   r[ZB_R_AIRTIME_SUM] = tanh_r(air_last[0] + air_last[1]);
 
-  float reward = 0.f;
+  float reward = 0.f, sums[ZB_NUM_REWARD_TERMS];
   const bool reset = died || time_out;
 #pragma unroll
   for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) {
     const float v = r[t] * cfg.reward_scales[t];
     reward += v;
-    const float sum = ST(ZB_S_EP_SUMS + t) + v;
-    ST(ZB_S_EP_SUMS + t) = reset ? 0.f : sum;
-    if (reset && lead) atomicAdd(&acc[t], sum);   // episode log (v2.py:441-448)
+    sums[t] = sums0[t] + v;
   }
   if (died) reward -= cfg.terminal_penalty;  // v2.py:379-380
-  ST(ZB_S_EP_LEN) = reset ? 0.f : ep_len;
 
-  // in-kernel auto-reset (v2.py:413-459); the state written above is overwritten for reset envs
+  // in-kernel auto-reset (v2.py:413-459): the episode log, then the default state; step_len and
+  // f_last are not reset (reference), feet_down_pos_last = the default feet positions
   if (reset) {
     if (lead) {
+#pragma unroll
+      for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) atomicAdd(&acc[t], sums[t]);   // v2.py:441-448
       atomicAdd(&acc[13], 1.f);
       if (died) atomicAdd(&acc[14], 1.f);
       if (time_out) atomicAdd(&acc[15], 1.f);
     }
-    Mdp d;
-    load_state(st, N, i, p, d);
-    reset_env(m, q.dflt(), p, d);
-    store_state(st, N, i, p, d);
-    const float4 dq = q.dflt()[2];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) { p.pos[a] = m->default_root_pos[a]; p.lv[a] = 0.f; p.av[a] = 0.f; }
+#pragma unroll
+    for (int a = 0; a < 4; ++a) p.quat[a] = m->default_root_quat[a];
+#pragma unroll
+    for (int j = 0; j < ND; ++j) { p.jq[j] = m->default_joint_pos[j]; p.jqd[j] = 0.f; }
+    const float4 d0 = q.dflt()[0], d1 = q.dflt()[1], dq = q.dflt()[2];
+    down[0][0] = d0.x; down[0][1] = d0.y; down[0][2] = d0.z;
+    down[1][0] = d1.x; down[1][1] = d1.y; down[1][2] = d1.z;
     obs_q[0] = dq.x; obs_q[1] = dq.y; obs_q[2] = dq.z; obs_q[3] = dq.w;
-  } else {
+  }
+  sp.mark(12);
+  if (writer) {
+    auto live = [reset](float v) { return reset ? 0.f : v; };  // fields zeroed by _reset_idx
 #pragma unroll
     for (int a = 0; a < 3; ++a) { ST(ZB_S_ROOT_POS + a) = p.pos[a]; ST(ZB_S_ROOT_LINVEL + a) = p.lv[a]; ST(ZB_S_ROOT_ANGVEL + a) = p.av[a]; }
 #pragma unroll
     for (int a = 0; a < 4; ++a) ST(ZB_S_ROOT_QUAT + a) = p.quat[a];
 #pragma unroll
     for (int j = 0; j < ND; ++j) { ST(ZB_S_JOINT_POS + j) = p.jq[j]; ST(ZB_S_JOINT_VEL + j) = p.jqd[j]; }
-  }
-  // _get_observations (v2.py:351-365) of the post-step / post-reset state
-  {
+#pragma unroll
+    for (int j = 0; j < ND; ++j) { ST(ZB_S_P_DELTA + j) = live(pdel[j]); ST(ZB_S_ACTIONS + j) = live(a_now[j]); }
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+#pragma unroll
+      for (int a = 0; a < 3; ++a) ST(ZB_S_FEET_DOWN_POS + 3 * f + a) = down[f][a];
+      ST(ZB_S_FEET_STEP_LEN + f) = step_len[f];
+      ST(ZB_S_FEET_F_LAST + f) = feetF[f];
+      ST(ZB_S_FEET_AIR_CUR + f) = live(air_cur[f]);
+      ST(ZB_S_FEET_AIR_LAST + f) = live(air_last[f]);
+      ST(ZB_S_FEET_CONTACT_CUR + f) = live(contact_t[f]);
+      ST(ZB_S_FEET_FZ_HIST + f) = live(so.feet_f[f][2]);
+#pragma unroll
+      for (int h = 1; h < ZB_HIST; ++h) ST(ZB_S_FEET_FZ_HIST + 2 * h + f) = live(fz_prev[h - 1][f]);
+    }
+    ST(ZB_S_UNDES_FMAX_HIST) = live(so.undes_fmax);
+#pragma unroll
+    for (int h = 1; h < ZB_HIST; ++h) ST(ZB_S_UNDES_FMAX_HIST + h) = live(fmax_prev[h - 1]);
+    ST(ZB_S_HEADING_SUM) = live(hs);
+    ST(ZB_S_Y_ERR_SUM) = live(ys);
+    ST(ZB_S_EP_LEN) = live(ep_len);
+#pragma unroll
+    for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) ST(ZB_S_EP_SUMS + t) = live(sums[t]);
+
+    // _get_observations (v2.py:351-365) of the post-step / post-reset state
     float* o = obs + (size_t)i * ZB_OBS_DIM;
     o[0] = obs_q[0]; o[1] = obs_q[1]; o[2] = obs_q[2]; o[3] = obs_q[3];
 #pragma unroll
     for (int j = 0; j < ND; ++j) {
       o[4 + j] = p.jq[j] - m->default_joint_pos[j];
       o[10 + j] = p.jqd[j];
-      o[16 + j] = reset ? 0.f : ST(ZB_S_ACTIONS + j);
+      o[16 + j] = live(a_now[j]);
     }
     o[22] = cfg.joint_speed_limit;
+    rew[i] = reward;
+    term[i] = died ? 1 : 0;
+    trunc[i] = time_out ? 1 : 0;
   }
-  rew[i] = reward;
-  term[i] = died ? 1 : 0;
-  trunc[i] = time_out ? 1 : 0;
+  __syncthreads();
+  // coalesced stores of the state rows and observations (lane s: fields s, s+16, ...)
   sp.mark(8);
   sp.flush();
 #undef ST
@@ -1608,23 +1635,21 @@ __global__ __launch_bounds__(WAVE, 1) void zb_substeps_kernel(const zb_model* __
   MP m = to_mp(mg);
   __shared__ float4 lds[LDS4];
   const int lane = threadIdx.x;
-  const int env = blockIdx.x * EPW + (lane >> 2);
+  const int env = blockIdx.x * EPW + lane / TL;
   const int i = env < N ? env : N - 1;
-  const Q q{lds, lane, lane >> 2, lane & 3};
+  const Q q{lds, lane, lane / TL, lane % TL};
   for (int t = lane; t < LNK4; t += WAVE) lds[LNK_OFF + t] = links[t];
   Phys p;
   load_phys(st, N, i, p);
-  float tg[ND], tau[ND], F[3][3];
+  float tg[ND], tau[ND], F[1][3];
 #pragma unroll
   for (int j = 0; j < ND; ++j) { tg[j] = targets[(size_t)i * ND + j]; tau[j] = 0.f; }
   SensorOut so;
   Stamps sp;
   for (int k = 0; k < nsub; ++k) substep<true>(m, cfg, p, tg, q, k == nsub - 1, so, F, tau, sp);
-  if (net_force)
+  if (net_force && q.s < NL)
 #pragma unroll
-    for (int t = 0; t < 3; ++t)
-#pragma unroll
-      for (int a = 0; a < 3; ++a) net_force[((size_t)i * NL + 3 * q.s + t) * 3 + a] = F[t][a];
+    for (int a = 0; a < 3; ++a) net_force[((size_t)i * NL + q.s) * 3 + a] = F[0][a];
   if (tau_out)
 #pragma unroll
     for (int j = 0; j < ND; ++j) tau_out[(size_t)i * ND + j] = tau[j];
