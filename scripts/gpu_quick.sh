@@ -4,7 +4,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out
 export ZB_NAN_DUMP=$PWD/gpurun_out/nan_case.npz
 timeout -k 10 600 python -m pytest tests -m gpu -q > gpurun_out/pytest_gpu.log 2>&1; rc=$?
 echo "pytest rc=$rc"; grep -E "passed|failed|Error|assert" gpurun_out/pytest_gpu.log | head -12
-if [ $rc -gt 1 ]; then exit $rc; fi
+if [ $rc -ne 0 ]; then exit $rc; fi
 timeout -k 10 300 python scripts/stamps.py > gpurun_out/stamps.log 2>&1 || exit $?
 grep -v amdgpu.ids gpurun_out/stamps.log
 timeout -k 10 300 python bench.py --steps 300 --warmup 30 --no-cpu-baseline > gpurun_out/bench.log 2>&1 || exit $?

@@ -371,8 +371,22 @@ __device__ __forceinline__ int dppz(int x) {  // out-of-row source lanes read 0 
   return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xF, 0xF, true);
 }
 constexpr int DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_HALF_MIRROR = 0x141, DPP_MIRROR = 0x140;
-constexpr int DPP_BCAST = 0x150, DPP_SHR = 0x110;  // row_newbcast:k, row_shr:k
+constexpr int DPP_BCAST = 0x150, DPP_SHR = 0x110, DPP_SHL = 0x100;  // row_newbcast:k, row_shr:k, row_shl:k
 
+template <int CTRL>
+__device__ __forceinline__ float dppzf(float x) {  // out-of-row source lanes read 0 (row shifts)
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, true));
+}
+// suffix sums over the team: x_b <- sum_{b' >= b} x_b' (lanes past the row contribute 0)
+template <int NF>
+__device__ __forceinline__ void suffix_sum(float (&x)[NF]) {
+#pragma unroll
+  for (int a = 0; a < NF; ++a) x[a] += dppzf<DPP_SHL + 1>(x[a]);
+#pragma unroll
+  for (int a = 0; a < NF; ++a) x[a] += dppzf<DPP_SHL + 2>(x[a]);
+#pragma unroll
+  for (int a = 0; a < NF; ++a) x[a] += dppzf<DPP_SHL + 4>(x[a]);
+}
 __device__ __forceinline__ float tsum(float x) {
   x += dppf<DPP_XOR1>(x);
   x += dppf<DPP_XOR2>(x);
@@ -402,6 +416,24 @@ __device__ __forceinline__ float tb(float x) { return dppf<DPP_BCAST + K>(x); } 
 template <int K>
 __device__ __forceinline__ int tbi(int x) { return dppi<DPP_BCAST + K>(x); }
 
+// Workgroups of the step / substep kernels are exactly one wave: LDS operations of a wave execute
+// in order, so cross-lane LDS hand-offs need only a compiler-level fence (no s_barrier, and no
+// wait on outstanding global loads/stores, which __syncthreads would add).
+__device__ __forceinline__ void wave_sync() {
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  __builtin_amdgcn_wave_barrier();
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
+// Workgroup b runs on XCD b % 8 (round-robin dispatch). Give the workgroups of one XCD a
+// contiguous range of envs so that the 64-B segments of a state field that neighbouring
+// workgroups touch share that XCD's L2 (otherwise each line is fetched once per XCD).
+constexpr int NXCD = 8;
+__device__ __forceinline__ int xcd_block(int b, int nb) {
+  if (nb % NXCD) return b;
+  return (b % NXCD) * (nb / NXCD) + b / NXCD;
+}
+
 // Device-side per-link collision table (built by zb_create), float4-aligned for per-lane loads:
 // [0] bounding sphere, [1+3ci..3+3ci] circle ci: C, E1, E2 (body frame), [7], [8] inscribed spheres,
 // [9] union sphere of the two (midpoint, max r + half their distance + 1 um) for the broadphase.
@@ -410,7 +442,9 @@ constexpr int LINK4 = 10;
 constexpr int NPAIR = (NL - 1) * (NL - 2) / 2;  // non-adjacent link pairs (55), checked by zb_create
 constexpr int PAIRS_PER_LANE = (NPAIR + TL - 1) / TL;
 constexpr int DFLT_OFF = NL * LINK4 + (NPAIR + 3) / 4;  // default-pose feet positions, base quat
-constexpr int LNK4 = DFLT_OFF + 3;
+constexpr int JT_OFF = DFLT_OFF + 3;  // joints: {jpr}, {jpp}, {jcp}, {jcr}, {a_local = R(jpr) z}
+constexpr int BT_OFF = JT_OFF + ND * 5;  // bodies: {com, mass}, {Ixx, Iyy, Izz, Ixy}, {Ixz, Iyz, 0, 0}
+constexpr int LNK4 = BT_OFF + NB * 3;
 
 // Candidate list in canonical order: ground (link by link, <= 4 each), then self candidates in
 // (pair, sphere a, sphere b) order, at most NSELF. More than NCM candidates: the NCM smallest by
@@ -426,7 +460,8 @@ constexpr int NCAND = NL * 4 + NSELF;
 //   CAND  [EPW][NCAND][2]   candidates {x, sep}, {n, code = 16 la + lb + 1}
 //   MAP   [EPW][NCM] int    overflow only: solver slot -> candidate position
 //   KEEP  [EPW][NCAND] f32  overflow only: kept flags
-//   FRAME [NB][3][EPW]      body frames {R row, p}
+//   BODY  [NB][4][EPW]      body poses {R row 0, p.x}, {R row 1, p.y}, {R row 2, p.z}, {quat}
+//   JNT   [ND][3][EPW]      joints {a, o.x}, {o x a, o.y}, {o.z, -}
 //   UB    [NL][EPW]         world union spheres
 //   LNK   [LNK4]            link table copy
 constexpr int YG_OFF = 0;
@@ -436,8 +471,9 @@ constexpr int FRC_OFF = LAM_OFF + NCM * EPW;
 constexpr int CAND_OFF = FRC_OFF + NCM * EPW;
 constexpr int MAP_OFF = CAND_OFF + EPW * NCAND * 2;
 constexpr int KEEP_OFF = MAP_OFF + (EPW * NCM + 3) / 4;
-constexpr int FRAME_OFF = KEEP_OFF + (EPW * NCAND + 3) / 4;
-constexpr int UB_OFF = FRAME_OFF + NB * 3 * EPW;
+constexpr int BODY_OFF = KEEP_OFF + (EPW * NCAND + 3) / 4;
+constexpr int JNT_OFF = BODY_OFF + NB * 4 * EPW;
+constexpr int UB_OFF = JNT_OFF + ND * 3 * EPW;
 constexpr int LNK_OFF = UB_OFF + NL * EPW;
 constexpr int LDS4 = LNK_OFF + LNK4;
 
@@ -452,7 +488,11 @@ struct Q {
   __device__ __forceinline__ float4& cand(int p, int h) const { return b[CAND_OFF + (e * NCAND + p) * 2 + h]; }
   __device__ __forceinline__ int& map(int c) const { return reinterpret_cast<int*>(b + MAP_OFF)[e * NCM + c]; }
   __device__ __forceinline__ float& keep(int p) const { return reinterpret_cast<float*>(b + KEEP_OFF)[e * NCAND + p]; }
-  __device__ __forceinline__ float4& frame(int body, int r) const { return b[FRAME_OFF + (body * 3 + r) * EPW + e]; }
+  __device__ __forceinline__ float4& body(int bb, int r) const { return b[BODY_OFF + (bb * 4 + r) * EPW + e]; }
+  __device__ __forceinline__ float4& frame(int bb, int r) const { return body(bb, r); }
+  __device__ __forceinline__ float4& jnt(int j, int r) const { return b[JNT_OFF + (j * 3 + r) * EPW + e]; }
+  __device__ __forceinline__ const float4* jtab(int j) const { return b + LNK_OFF + JT_OFF + j * 5; }
+  __device__ __forceinline__ const float4* btab(int bb) const { return b + LNK_OFF + BT_OFF + bb * 3; }
   __device__ __forceinline__ float4& ub(int l) const { return b[UB_OFF + l * EPW + e]; }
   __device__ __forceinline__ const float4* link(int l) const { return b + LNK_OFF + l * LINK4; }
   __device__ __forceinline__ int pair_code(int p) const { return reinterpret_cast<const int*>(b + LNK_OFF + NL * LINK4)[p]; }
@@ -468,6 +508,148 @@ __device__ __forceinline__ void read_frame(const Q& q, int body, float R[9], flo
 __device__ __forceinline__ void mv3f(const float R[9], const float4 v, float o[3]) {
   const float a[3] = {v.x, v.y, v.z};
   mv3(R, a, o);
+}
+
+// ------------------------------------------------------------------------- team kinematics
+// FK as a parallel prefix over the team: lane 0 holds the root (q0, 0), lane b >= 1 the local
+// transform of joint b-1, M = (jpr * qz(q) * jcr, jpp + rot(jpr * qz(q), jcp)); three DPP row
+// shifts (Hillis-Steele, composition (q1, t1) o (q2, t2) = (q1 q2, t1 + rot(q1, t2))) leave body
+// b's pose in lane b. Lane b then publishes body b (frame + quaternion) and joint b's axis /
+// origin / motion subspace to LDS and, for the dynamics, keeps body b's spatial inertia about P
+// and joint b's motion subspace in registers.
+__device__ __forceinline__ void qrot(const float q[4], const float v[3], float o[3]) {
+  // v + 2 w (u x v) + 2 u x (u x v), u = q.xyz
+  const float u[3] = {q[1], q[2], q[3]};
+  float t[3];
+  cross3(u, v, t);
+  t[0] *= 2.f; t[1] *= 2.f; t[2] *= 2.f;
+  float ut[3];
+  cross3(u, t, ut);
+  o[0] = v[0] + q[0] * t[0] + ut[0];
+  o[1] = v[1] + q[0] * t[1] + ut[1];
+  o[2] = v[2] + q[0] * t[2] + ut[2];
+}
+template <int D>
+__device__ __forceinline__ void fk_scan_step(float qv[4], float tv[3], int lane_b) {
+  float qs[4], ts[3];
+#pragma unroll
+  for (int a = 0; a < 4; ++a) qs[a] = dppf<DPP_SHR + D>(qv[a]);
+#pragma unroll
+  for (int a = 0; a < 3; ++a) ts[a] = dppf<DPP_SHR + D>(tv[a]);
+  if (lane_b >= D) {
+    float qn[4], rt[3];
+    qmul(qs, qv, qn);
+    qrot(qs, tv, rt);
+#pragma unroll
+    for (int a = 0; a < 4; ++a) qv[a] = qn[a];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) tv[a] = ts[a] + rt[a];
+  }
+}
+
+template <bool kInertia>
+__device__ __forceinline__ void fk_team(const Phys& s, const Q& q, SI& Ib, float (&Sown)[6]) {
+  const int b = q.s;
+  if (kInertia) {
+    Ib.m = 0.f;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) Ib.h[a] = 0.f;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) { Ib.I[a] = 0.f; Sown[a] = 0.f; }
+  }
+  float qv[4], tv[3] = {0.f, 0.f, 0.f};
+  if (b == 0) {
+    qv[0] = s.quat[0]; qv[1] = s.quat[1]; qv[2] = s.quat[2]; qv[3] = s.quat[3];
+    qnormalize(qv);
+  } else {
+    const int j = b <= ND ? b - 1 : ND - 1;
+    float qj = s.jq[0];
+#pragma unroll
+    for (int k = 1; k < ND; ++k) qj = j == k ? s.jq[k] : qj;
+    const float4* J = q.jtab(j);
+    const float4 jpr = J[0], jpp = J[1], jcp = J[2], jcr = J[3];
+    float sn, cs;
+    sincos_r(0.5f * qj, &sn, &cs);
+    const float pr[4] = {jpr.x, jpr.y, jpr.z, jpr.w}, qz[4] = {cs, 0.f, 0.f, sn}, cr[4] = {jcr.x, jcr.y, jcr.z, jcr.w};
+    float qa[4], t[3];
+    qmul(pr, qz, qa);
+    const float cp[3] = {jcp.x, jcp.y, jcp.z};
+    qrot(qa, cp, t);
+    tv[0] = jpp.x + t[0]; tv[1] = jpp.y + t[1]; tv[2] = jpp.z + t[2];
+    qmul(qa, cr, qv);
+  }
+  fk_scan_step<1>(qv, tv, b);
+  fk_scan_step<2>(qv, tv, b);
+  fk_scan_step<4>(qv, tv, b);
+  if (b < NB) {
+    qnormalize(qv);
+    float R[9];
+    qmat(qv, R);
+    q.body(b, 0) = make_float4(R[0], R[1], R[2], tv[0]);
+    q.body(b, 1) = make_float4(R[3], R[4], R[5], tv[1]);
+    q.body(b, 2) = make_float4(R[6], R[7], R[8], tv[2]);
+    q.body(b, 3) = make_float4(qv[0], qv[1], qv[2], qv[3]);
+    if (b < ND) {  // joint b: parent body b
+      const float4* J = q.jtab(b);
+      const float4 jpp = J[1], al = J[4];
+      float o[3], ax[3], oxa[3];
+      mv3f(R, jpp, o);
+      o[0] += tv[0]; o[1] += tv[1]; o[2] += tv[2];
+      mv3f(R, al, ax);
+      cross3(o, ax, oxa);
+      q.jnt(b, 0) = make_float4(ax[0], ax[1], ax[2], o[0]);
+      q.jnt(b, 1) = make_float4(oxa[0], oxa[1], oxa[2], o[1]);
+      q.jnt(b, 2) = make_float4(o[2], 0.f, 0.f, 0.f);
+      if (kInertia) {
+        Sown[0] = ax[0]; Sown[1] = ax[1]; Sown[2] = ax[2];
+        Sown[3] = oxa[0]; Sown[4] = oxa[1]; Sown[5] = oxa[2];
+      }
+    }
+    if (kInertia) {  // spatial inertia of body b about P (world axes)
+      const float4* B = q.btab(b);
+      const float4 cm = B[0], i0 = B[1], i1 = B[2];
+      float c[3];
+      mv3f(R, cm, c);
+      c[0] += tv[0]; c[1] += tv[1]; c[2] += tv[2];
+      const float Il[9] = {i0.x, i0.w, i1.x, i0.w, i0.y, i1.y, i1.x, i1.y, i0.z};
+      float T[9], W[9];
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) T[3 * r + k] = R[3 * r] * Il[k] + R[3 * r + 1] * Il[3 + k] + R[3 * r + 2] * Il[6 + k];
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) W[3 * r + k] = T[3 * r] * R[3 * k] + T[3 * r + 1] * R[3 * k + 1] + T[3 * r + 2] * R[3 * k + 2];
+      const float mm = cm.w;
+      const float cc = dot3(c, c);
+      Ib.m = mm;
+      Ib.h[0] = mm * c[0]; Ib.h[1] = mm * c[1]; Ib.h[2] = mm * c[2];
+      Ib.I[0] = W[0] + mm * (cc - c[0] * c[0]);
+      Ib.I[1] = W[4] + mm * (cc - c[1] * c[1]);
+      Ib.I[2] = W[8] + mm * (cc - c[2] * c[2]);
+      Ib.I[3] = W[1] - mm * c[0] * c[1];
+      Ib.I[4] = W[2] - mm * c[0] * c[2];
+      Ib.I[5] = W[5] - mm * c[1] * c[2];
+    }
+  }
+}
+
+__device__ __forceinline__ void fk_team_pose(const Phys& s, const Q& q) {
+  SI dummy;
+  float ds[6];
+  fk_team<false>(s, q, dummy, ds);
+}
+
+// joint motion subspaces S_j = [a_j; o_j x a_j] and origins o_j (relative to P) from LDS
+__device__ __forceinline__ void read_joints(const Q& q, float S[ND][6], float org[ND][3]) {
+#pragma unroll
+  for (int j = 0; j < ND; ++j) {
+    const float4 g0 = q.jnt(j, 0), g1 = q.jnt(j, 1), g2 = q.jnt(j, 2);
+    S[j][0] = g0.x; S[j][1] = g0.y; S[j][2] = g0.z;
+    S[j][3] = g1.x; S[j][4] = g1.y; S[j][5] = g1.z;
+    org[j][0] = g0.w; org[j][1] = g1.w; org[j][2] = g2.x;
+  }
 }
 
 // ------------------------------------------------------------------------- contacts
@@ -521,18 +703,8 @@ __device__ __forceinline__ int narrow_pair(const Q& q, int pidx, float margin, F
 // pairs split over the team; candidate pairs are split in rank order into contiguous chunks, one
 // per lane, so candidates stay in canonical order lane by lane. Counting pass, team scan, then
 // each lane writes its candidates at their canonical positions.
-__device__ __forceinline__ int detect(const zb_task_cfg& cfg, const Kin& k, float Pz, const Q& q, bool& over,
-                                      Stamps& sp) {
+__device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q& q, bool& over, Stamps& sp) {
   const float margin = cfg.contact_margin;
-  if (q.s == 0) {
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      q.frame(b, 0) = make_float4(k.R[b][0], k.R[b][1], k.R[b][2], k.p[b][0]);
-      q.frame(b, 1) = make_float4(k.R[b][3], k.R[b][4], k.R[b][5], k.p[b][1]);
-      q.frame(b, 2) = make_float4(k.R[b][6], k.R[b][7], k.R[b][8], k.p[b][2]);
-    }
-  }
-  __syncthreads();
 
   // ground, counting pass: lane s = link s; keep the world circle frames for the write pass
   const int l = q.s < NL ? q.s : NL - 1;
@@ -582,7 +754,7 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, const Kin& k, floa
   unsigned long long cmask = 0ull;
   int cnt_s = 0, chunk = 0, first = 0;
   if (cfg.enable_self_collision) {
-    __syncthreads();  // union spheres
+    wave_sync();  // union spheres
     unsigned long long mask = 0ull;
 #pragma unroll
     for (int j = 0; j < PAIRS_PER_LANE; ++j) {
@@ -661,7 +833,7 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, const Kin& k, floa
 
   // overflow (rare): rank every candidate by (sep, canonical index); MAP = kept positions in order
   if (__ballot(over) != 0ull) {
-    __syncthreads();
+    wave_sync();
     if (over)
       for (int p = q.s; p < n; p += TL) {
         const float sp_ = q.cand(p, 0).w;
@@ -672,7 +844,7 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, const Kin& k, floa
         }
         q.keep(p) = r < NCM ? 1.f : 0.f;
       }
-    __syncthreads();
+    wave_sync();
     if (over && q.s < NCM) {
       int c = 0, pos = -1;
       for (int p = 0; p < n; ++p)
@@ -683,7 +855,7 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, const Kin& k, floa
       q.map(q.s) = pos;
     }
   }
-  __syncthreads();
+  wave_sync();
   return over ? NCM : n;
 }
 
@@ -730,6 +902,15 @@ __device__ __forceinline__ float4 pgs_update(const float4 g, const float4 a0, co
   return make_float4(ln, l1, l2, 0.f);
 }
 
+// mass-matrix column of joint K (computed in lane K) into every lane's packed lower triangle
+template <int K>
+__device__ __forceinline__ void crba_column(float L[NT], const float Fk[6], const float Mk[ND], float arm) {
+#pragma unroll
+  for (int a = 0; a < 6; ++a) L[tri(6 + K, a)] = tb<K>(Fk[a]);
+#pragma unroll
+  for (int jj = 0; jj <= K; ++jj) L[tri(6 + K, 6 + jj)] = tb<K>(Mk[jj]) + (jj == K ? arm : 0.f);
+}
+
 // ------------------------------------------------------------------------- one substep
 template <bool kDebugForces>
 __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
@@ -750,113 +931,105 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
   }
 
   float S[ND][6], org[ND][3];
-  SI I[NB];
+  SI Ib;                   // this lane's body (b = s < NB; zero elsewhere)
+  float Sown[6];           // this lane's joint motion subspace (j = s < ND; zero elsewhere)
   int nc;
   bool over;
-  __syncthreads();  // the previous substep's LDS readers are done
-  {
-    Kin k;
-    fk(m, s, k);
-    sp.mark(9);
-    nc = detect(cfg, k, s.pos[2], q, over, sp);
-    m = opaque(m0);
-#pragma unroll
-    for (int j = 0; j < ND; ++j) {
-      float oxa[3];
-      cross3(k.org[j], k.ax[j], oxa);
-#pragma unroll
-      for (int a = 0; a < 3; ++a) { S[j][a] = k.ax[j][a]; S[j][3 + a] = oxa[a]; org[j][a] = k.org[j][a]; }
-    }
-#pragma unroll
-    for (int b = 0; b < NB; ++b) body_si(m, k, b, I[b]);
-  }
+  wave_sync();  // the previous substep's LDS readers are done
+  fk_team<true>(s, q, Ib, Sown);
+  wave_sync();
+  sp.mark(9);
+  nc = detect(cfg, s.pos[2], q, over, sp);
+  read_joints(q, S, org);
+  m = opaque(m0);
 
-  // RNEA bias forces (qddot = 0, gravity as base acceleration); f_b formed in the forward pass
+  // RNEA bias forces (qddot = 0, gravity as base acceleration), one body per lane: lane b runs
+  // the velocity / acceleration chain up to its body (joints j >= b contribute zero), forms f_b,
+  // and the team suffix sum F_b = sum_{b' >= b} f_b' (DPP row shifts) gives the joint forces.
   float Cb[NV];
   {
-    float f[NB][6];
-    float V[6], A[6];
+    const int b = q.s;
+    float V[6] = {s.av[0], s.av[1], s.av[2], s.lv[0], s.lv[1], s.lv[2]};
+    float A[6] = {0.f, 0.f, 0.f, 0.f, 0.f, cfg.gravity};
 #pragma unroll
-    for (int a = 0; a < 3; ++a) { V[a] = s.av[a]; V[3 + a] = s.lv[a]; A[a] = 0.f; A[3 + a] = 0.f; }
-    A[5] = cfg.gravity;
+    for (int j = 0; j < ND; ++j) {
+      const float qd = j < b ? s.jqd[j] : 0.f;
 #pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      if (b > 0) {
-        const int j = b - 1;
+      for (int a = 0; a < 6; ++a) V[a] += S[j][a] * qd;
+      float t1[3], t2[3], t3[3];
+      cross3(V, S[j], t1);
+      cross3(V, S[j] + 3, t2);
+      cross3(V + 3, S[j], t3);
 #pragma unroll
-        for (int a = 0; a < 6; ++a) V[a] += S[j][a] * s.jqd[j];
-        float t1[3], t2[3], t3[3];
-        cross3(V, S[j], t1);
-        cross3(V, S[j] + 3, t2);
-        cross3(V + 3, S[j], t3);
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-          A[a] += t1[a] * s.jqd[j];
-          A[3 + a] += (t2[a] + t3[a]) * s.jqd[j];
-        }
+      for (int a = 0; a < 3; ++a) {
+        A[a] += t1[a] * qd;
+        A[3 + a] += (t2[a] + t3[a]) * qd;
       }
+    }
+    float f[6];
+    {
       float IA[6], IV[6], t1[3], t2[3], t3[3];
-      si_mul(I[b], A, IA);
-      si_mul(I[b], V, IV);
+      si_mul(Ib, A, IA);
+      si_mul(Ib, V, IV);
       cross3(V, IV, t1);
       cross3(V + 3, IV + 3, t2);
       cross3(V, IV + 3, t3);
 #pragma unroll
       for (int a = 0; a < 3; ++a) {
-        f[b][a] = IA[a] + t1[a] + t2[a];
-        f[b][3 + a] = IA[3 + a] + t3[a];
+        f[a] = IA[a] + t1[a] + t2[a];
+        f[3 + a] = IA[3 + a] + t3[a];
       }
     }
+    suffix_sum<6>(f);
+    float Fn[6];
 #pragma unroll
-    for (int b = NB - 2; b >= 0; --b)
+    for (int a = 0; a < 6; ++a) Fn[a] = dppzf<DPP_SHL + 1>(f[a]);  // F_{j+1} in lane j
+    float cj = 0.f;
 #pragma unroll
-      for (int a = 0; a < 6; ++a) f[b][a] += f[b + 1][a];
+    for (int a = 0; a < 6; ++a) cj += Sown[a] * Fn[a];
 #pragma unroll
-    for (int j = 0; j < ND; ++j) {
-      float t = 0.f;
-#pragma unroll
-      for (int a = 0; a < 6; ++a) t += S[j][a] * f[j + 1][a];
-      Cb[6 + j] = t;
-    }
-#pragma unroll
-    for (int a = 0; a < 6; ++a) Cb[a] = f[0][a];
+    for (int a = 0; a < 6; ++a) Cb[a] = tb<0>(f[a]);
+    Cb[6] = tb<0>(cj); Cb[7] = tb<1>(cj); Cb[8] = tb<2>(cj);
+    Cb[9] = tb<3>(cj); Cb[10] = tb<4>(cj); Cb[11] = tb<5>(cj);
   }
 
-  // CRBA (composite inertias accumulated in place) straight into the factor storage
+  // CRBA: composite inertias by a team suffix sum; lane k forms F_k = Ic_{k+1} S_k and its
+  // mass-matrix column S_jj . F_k, then the team assembles the lower triangle in every lane
   const float arm = dt * (m->kd + dt * m->kp);
   float L[NT];
-#pragma unroll
-  for (int b = NB - 2; b >= 0; --b) {
-    I[b].m += I[b + 1].m;
-#pragma unroll
-    for (int a = 0; a < 3; ++a) I[b].h[a] += I[b + 1].h[a];
-#pragma unroll
-    for (int a = 0; a < 6; ++a) I[b].I[a] += I[b + 1].I[a];
-  }
   {
-    const SI& T = I[0];
-    L[tri(0, 0)] = T.I[0]; L[tri(1, 1)] = T.I[1]; L[tri(2, 2)] = T.I[2];
-    L[tri(1, 0)] = T.I[3]; L[tri(2, 0)] = T.I[4]; L[tri(2, 1)] = T.I[5];
-    const float hx = T.h[0], hy = T.h[1], hz = T.h[2];
-    L[tri(3, 0)] = 0.f; L[tri(3, 1)] = hz;  L[tri(3, 2)] = -hy;
-    L[tri(4, 0)] = -hz; L[tri(4, 1)] = 0.f; L[tri(4, 2)] = hx;
-    L[tri(5, 0)] = hy;  L[tri(5, 1)] = -hx; L[tri(5, 2)] = 0.f;
-    L[tri(3, 3)] = T.m; L[tri(4, 4)] = T.m; L[tri(5, 5)] = T.m;
-    L[tri(4, 3)] = 0.f; L[tri(5, 3)] = 0.f; L[tri(5, 4)] = 0.f;
-  }
+    float ic[10] = {Ib.m, Ib.h[0], Ib.h[1], Ib.h[2], Ib.I[0], Ib.I[1], Ib.I[2], Ib.I[3], Ib.I[4], Ib.I[5]};
+    suffix_sum<10>(ic);
+    SI In;  // Ic_{k+1}
+    In.m = dppzf<DPP_SHL + 1>(ic[0]);
 #pragma unroll
-  for (int kk = 0; kk < ND; ++kk) {
-    float Fk[6];
-    si_mul(I[kk + 1], S[kk], Fk);
+    for (int a = 0; a < 3; ++a) In.h[a] = dppzf<DPP_SHL + 1>(ic[1 + a]);
 #pragma unroll
-    for (int a = 0; a < 6; ++a) L[tri(6 + kk, a)] = Fk[a];
+    for (int a = 0; a < 6; ++a) In.I[a] = dppzf<DPP_SHL + 1>(ic[4 + a]);
+    float Fk[6], Mk[ND];
+    si_mul(In, Sown, Fk);
 #pragma unroll
-    for (int jj = 0; jj <= kk; ++jj) {
+    for (int jj = 0; jj < ND; ++jj) {
       float t = 0.f;
 #pragma unroll
       for (int a = 0; a < 6; ++a) t += S[jj][a] * Fk[a];
-      L[tri(6 + kk, 6 + jj)] = t + (jj == kk ? arm : 0.f);
+      Mk[jj] = t;
     }
+    // root block from Ic_0 (lane 0)
+    const float m0t = tb<0>(ic[0]), hx = tb<0>(ic[1]), hy = tb<0>(ic[2]), hz = tb<0>(ic[3]);
+    L[tri(0, 0)] = tb<0>(ic[4]); L[tri(1, 1)] = tb<0>(ic[5]); L[tri(2, 2)] = tb<0>(ic[6]);
+    L[tri(1, 0)] = tb<0>(ic[7]); L[tri(2, 0)] = tb<0>(ic[8]); L[tri(2, 1)] = tb<0>(ic[9]);
+    L[tri(3, 0)] = 0.f; L[tri(3, 1)] = hz;  L[tri(3, 2)] = -hy;
+    L[tri(4, 0)] = -hz; L[tri(4, 1)] = 0.f; L[tri(4, 2)] = hx;
+    L[tri(5, 0)] = hy;  L[tri(5, 1)] = -hx; L[tri(5, 2)] = 0.f;
+    L[tri(3, 3)] = m0t; L[tri(4, 4)] = m0t; L[tri(5, 5)] = m0t;
+    L[tri(4, 3)] = 0.f; L[tri(5, 3)] = 0.f; L[tri(5, 4)] = 0.f;
+    crba_column<0>(L, Fk, Mk, arm);
+    crba_column<1>(L, Fk, Mk, arm);
+    crba_column<2>(L, Fk, Mk, arm);
+    crba_column<3>(L, Fk, Mk, arm);
+    crba_column<4>(L, Fk, Mk, arm);
+    crba_column<5>(L, Fk, Mk, arm);
   }
 
   // implicit PD drives. Pass 1: all implicit (armature on the diagonal). A joint whose implicit
@@ -966,7 +1139,7 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
     q.aux(c, 1) = make_float4(dot12(Y[1], Y[0]), dot12(Y[2], Y[0]), 0.f, 0.f);  // c01, c02
     q.lam(c) = make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  __syncthreads();
+  wave_sync();
 
   sp.mark(5);
   // projected Gauss-Seidel on the whitened velocity (Coulomb disk friction); lane s owns w[s].
@@ -1003,7 +1176,7 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
     w[4] = tb<4>(wd); w[5] = tb<5>(wd); w[6] = tb<6>(wd); w[7] = tb<7>(wd);
     w[8] = tb<8>(wd); w[9] = tb<9>(wd); w[10] = tb<10>(wd); w[11] = tb<11>(wd);
   }
-  __syncthreads();  // last impulses visible to every lane
+  wave_sync();  // last impulses visible to every lane
   sp.mark(6);
   float un[NV];
   bwd_sub(L, Li, w, un);
@@ -1022,7 +1195,7 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
       for (int a = 0; a < 3; ++a) f[a] = (lam.x * n[a] + lam.y * t1[a] + lam.z * t2[a]) / dt;
       q.frc(q.s) = make_float4(f[0], f[1], f[2], gn.w);
     }
-    __syncthreads();
+    wave_sync();
     float Fl[3] = {0.f, 0.f, 0.f};
     for (int c = 0; c < nc; ++c) {
       const float4 f = q.frc(c);
@@ -1127,6 +1300,77 @@ __device__ __forceinline__ void make_cache(MP m, const Phys& s, Cache& o) {
 #pragma unroll
   for (int a = 0; a < 4; ++a) o.base_quat[a] = bq[a];
   link_com_vel(m, k, V, BASE, bv);
+  float R[9];
+  qmat(bq, R);
+  const float sh[3] = {R[2], R[5], R[8]};              // quat_apply(base_quat, z)  v2.py:322
+  o.fwd[0] = sh[1];                                     // (0,0,-1) x sh              v2.py:323
+  o.fwd[1] = -sh[0];
+  o.fwd[2] = 0.f * sh[0];
+  o.heading_err = -o.fwd[1];                            // v2.py:324
+  o.vfwd = dot3(bv, o.fwd);                             // v2.py:326-327
+#pragma unroll
+  for (int f = 0; f < 2; ++f) {
+    qmat(fq[f], R);
+    const float sg = f == 0 ? 1.f : -1.f;               // axis_z_feet = (0,0,1),(0,0,-1) v2.py:341-343
+    o.feet_z[f][0] = sg * R[2]; o.feet_z[f][1] = sg * R[5]; o.feet_z[f][2] = sg * R[8];
+    o.feet_x[f][0] = R[0]; o.feet_x[f][1] = R[3]; o.feet_x[f][2] = R[6];  // axis_x_feet v2.py:338-340
+  }
+}
+
+// link l's world pose (position relative to P, quaternion) from the published body pose
+__device__ __forceinline__ void link_pose_q(MP m, const Q& q, int l, float pos[3], float quat[4]) {
+  const int b = link_body(l);
+  float R[9], p[3];
+  read_frame(q, b, R, p);
+  const float4 bq = q.body(b, 3);
+  const float qb[4] = {bq.x, bq.y, bq.z, bq.w};
+  float t[3], lp[3], lr[4];
+  ldc(lp, m->link_pos[l]);
+  ldc(lr, m->link_rot[l]);
+  mv3(R, lp, t);
+  pos[0] = p[0] + t[0]; pos[1] = p[1] + t[1]; pos[2] = p[2] + t[2];
+  qmul(qb, lr, quat);
+}
+
+// world linear velocity of link l's COM: body b's twist at P from the joint rates, then v + w x c
+__device__ __forceinline__ void link_com_vel_q(MP m, const Q& q, const Phys& s, const float S[ND][6], int l,
+                                               float v[3]) {
+  const int b = link_body(l);
+  float V[6] = {s.av[0], s.av[1], s.av[2], s.lv[0], s.lv[1], s.lv[2]};
+#pragma unroll
+  for (int j = 0; j < ND; ++j)
+    if (j < b)
+#pragma unroll
+      for (int a = 0; a < 6; ++a) V[a] += S[j][a] * s.jqd[j];
+  float R[9], p[3], lc[3], c[3];
+  read_frame(q, b, R, p);
+  ldc(lc, m->link_com[l]);
+  mv3(R, lc, c);
+  c[0] += p[0]; c[1] += p[1]; c[2] += p[2];
+  float wc[3];
+  cross3(V, c, wc);
+  v[0] = V[3] + wc[0]; v[1] = V[4] + wc[1]; v[2] = V[5] + wc[2];
+}
+
+// the _get_observations cache (v2.py:315-345) of a physics state, from the published poses
+// (call after fk_team + a barrier)
+__device__ __forceinline__ void make_cache_q(MP m, const Q& q, const Phys& s, Cache& o) {
+  constexpr int BASE = 6, F0 = 0, F1 = 11;
+  float S[ND][6], org[ND][3];
+  read_joints(q, S, org);
+  float bq[4], fq[2][4], bv[3];
+  link_pose_q(m, q, BASE, o.base_pos, bq);
+  link_pose_q(m, q, F0, o.feet_pos[0], fq[0]);
+  link_pose_q(m, q, F1, o.feet_pos[1], fq[1]);
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    o.base_pos[a] += s.pos[a];
+    o.feet_pos[0][a] += s.pos[a];
+    o.feet_pos[1][a] += s.pos[a];
+  }
+#pragma unroll
+  for (int a = 0; a < 4; ++a) o.base_quat[a] = bq[a];
+  link_com_vel_q(m, q, s, S, BASE, bv);
   float R[9];
   qmat(bq, R);
   const float sh[3] = {R[2], R[5], R[8]};              // quat_apply(base_quat, z)  v2.py:322
@@ -1289,7 +1533,7 @@ __global__ __launch_bounds__(WAVE, 1) void zb_step_kernel(const zb_model* __rest
   MP m = to_mp(mg);
   __shared__ float4 lds[LDS4];
   const int lane = threadIdx.x;
-  const int env = blockIdx.x * EPW + lane / TL;
+  const int env = xcd_block(blockIdx.x, gridDim.x) * EPW + lane / TL;
   // a team past N recomputes env N-1 (identical values, identical stores); it never logs
   const int i = env < N ? env : N - 1;
   const bool lead = env < N && lane % TL == 0;
@@ -1328,7 +1572,14 @@ __global__ __launch_bounds__(WAVE, 1) void zb_step_kernel(const zb_model* __rest
   float pre_base_y, pre_base_z, pre_heading, pre_fwd[3], pre_feet[2][3];
   {
     Cache c;
+#ifdef ZB_PRO_OLD
     make_cache(opaque(m), p, c);
+#else
+    wave_sync();  // link table copy
+    fk_team_pose(p, q);
+    wave_sync();
+    make_cache_q(opaque(m), q, p, c);
+#endif
     r_pre[0] = tanh_r(10.f * c.vfwd / cfg.joint_speed_limit);                     // base_vel_forward
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -1395,6 +1646,7 @@ __global__ __launch_bounds__(WAVE, 1) void zb_step_kernel(const zb_model* __rest
 
   // post-step feet COM velocities (feet_slide)
   float feet_vel[2][3], obs_q[4];
+#ifdef ZB_POST_OLD
   {
     Kin k;
     fk(m, p, k);
@@ -1403,8 +1655,21 @@ __global__ __launch_bounds__(WAVE, 1) void zb_step_kernel(const zb_model* __rest
     link_com_vel(m, k, V, 0, feet_vel[0]);
     link_com_vel(m, k, V, 11, feet_vel[1]);
     float bp[3];
-    link_pose(m, k, 6, bp, obs_q);  // base quat of the post-step state (observation)
+    link_pose(m, k, 6, bp, obs_q);
   }
+#else
+  {
+    wave_sync();  // the last substep's readers of the body poses are done
+    fk_team_pose(p, q);
+    wave_sync();
+    float S[ND][6], org[ND][3];
+    read_joints(q, S, org);
+    link_com_vel_q(m, q, p, S, 0, feet_vel[0]);
+    link_com_vel_q(m, q, p, S, 11, feet_vel[1]);
+    float bp[3];
+    link_pose_q(m, q, 6, bp, obs_q);  // base quat of the post-step state (observation)
+  }
+#endif
   sp.mark(11);
 
   // _get_dones (v2.py:384-411)
@@ -1537,8 +1802,6 @@ __global__ __launch_bounds__(WAVE, 1) void zb_step_kernel(const zb_model* __rest
     term[i] = died ? 1 : 0;
     trunc[i] = time_out ? 1 : 0;
   }
-  __syncthreads();
-  // coalesced stores of the state rows and observations (lane s: fields s, s+16, ...)
   sp.mark(8);
   sp.flush();
 #undef ST
@@ -1635,7 +1898,7 @@ __global__ __launch_bounds__(WAVE, 1) void zb_substeps_kernel(const zb_model* __
   MP m = to_mp(mg);
   __shared__ float4 lds[LDS4];
   const int lane = threadIdx.x;
-  const int env = blockIdx.x * EPW + lane / TL;
+  const int env = xcd_block(blockIdx.x, gridDim.x) * EPW + lane / TL;
   const int i = env < N ? env : N - 1;
   const Q q{lds, lane, lane / TL, lane % TL};
   for (int t = lane; t < LNK4; t += WAVE) lds[LNK_OFF + t] = links[t];
@@ -1761,6 +2024,24 @@ int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_dev
                                    (double)(s0[2] - s1[2]) * (s0[2] - s1[2]));
       t[9] = make_float4(0.5f * (s0[0] + s1[0]), 0.5f * (s0[1] + s1[1]), 0.5f * (s0[2] + s1[2]),
                          (float)(fmax((double)s0[3], (double)s1[3]) + hd + 1e-6));
+    }
+    for (int j = 0; j < ND; ++j) {
+      float4* t = tab + JT_OFF + j * 5;
+      const float* r = m->joint_parent_rot[j];
+      t[0] = make_float4(r[0], r[1], r[2], r[3]);
+      t[1] = make_float4(m->joint_parent_pos[j][0], m->joint_parent_pos[j][1], m->joint_parent_pos[j][2], 0.f);
+      t[2] = make_float4(m->joint_child_pos[j][0], m->joint_child_pos[j][1], m->joint_child_pos[j][2], 0.f);
+      const float* c = m->joint_child_rot[j];
+      t[3] = make_float4(c[0], c[1], c[2], c[3]);
+      const float w = r[0], x = r[1], y = r[2], z = r[3];  // third column of R(jpr)
+      t[4] = make_float4(2.f * (x * z + w * y), 2.f * (y * z - w * x), 1.f - 2.f * (x * x + y * y), 0.f);
+    }
+    for (int b = 0; b < NB; ++b) {
+      float4* t = tab + BT_OFF + b * 3;
+      const float* I = m->body_inertia[b];
+      t[0] = make_float4(m->body_com[b][0], m->body_com[b][1], m->body_com[b][2], m->body_mass[b]);
+      t[1] = make_float4(I[0], I[1], I[2], I[3]);
+      t[2] = make_float4(I[4], I[5], 0.f, 0.f);
     }
     int* pc = reinterpret_cast<int*>(tab + NL * LINK4);
     for (int p = 0; p < m->num_self_pairs; ++p) pc[p] = 16 * m->self_pairs[p][0] + m->self_pairs[p][1];
