@@ -475,7 +475,17 @@ constexpr int BODY_OFF = KEEP_OFF + (EPW * NCAND + 3) / 4;
 constexpr int JNT_OFF = BODY_OFF + NB * 4 * EPW;
 constexpr int UB_OFF = JNT_OFF + ND * 3 * EPW;
 constexpr int LNK_OFF = UB_OFF + NL * EPW;
-constexpr int LDS4 = LNK_OFF + LNK4;
+constexpr int PRE_OFF = LNK_OFF + LNK4;  // [EPW] Pre records (prologue -> MDP)
+constexpr int PRE4 = 8;                   // float4 per Pre record (30 floats)
+constexpr int LDS4 = PRE_OFF + EPW * PRE4;
+
+// prologue results the MDP reads after the physics (parked in LDS across the substeps)
+struct Pre {
+  float a_now[ND], pdel[ND], r_pre[5];
+  float base_y, base_z, heading, fwd[3], feet[2][3], action_rate;
+};
+
+static_assert(sizeof(Pre) <= 16 * 8, "Pre fits PRE4 granules");
 
 struct Q {
   float4* b;
@@ -497,6 +507,7 @@ struct Q {
   __device__ __forceinline__ const float4* link(int l) const { return b + LNK_OFF + l * LINK4; }
   __device__ __forceinline__ int pair_code(int p) const { return reinterpret_cast<const int*>(b + LNK_OFF + NL * LINK4)[p]; }
   __device__ __forceinline__ const float4* dflt() const { return b + LNK_OFF + DFLT_OFF; }
+  __device__ __forceinline__ Pre& pre() const { return *reinterpret_cast<Pre*>(b + PRE_OFF + e * PRE4); }
 };
 
 __device__ __forceinline__ void read_frame(const Q& q, int body, float R[9], float p[3]) {
@@ -563,9 +574,17 @@ __device__ __forceinline__ void fk_team(const Phys& s, const Q& q, SI& Ib, float
     qnormalize(qv);
   } else {
     const int j = b <= ND ? b - 1 : ND - 1;
-    float qj = s.jq[0];
+    // select this lane's joint angle with v_cndmask (values pinned in registers first, so the
+    // select chain is not folded into a dynamically indexed load from a stack copy of the state)
+    float jqv[ND];
 #pragma unroll
-    for (int k = 1; k < ND; ++k) qj = j == k ? s.jq[k] : qj;
+    for (int k = 0; k < ND; ++k) {
+      jqv[k] = s.jq[k];
+      asm volatile("" : "+v"(jqv[k]));
+    }
+    float qj = jqv[0];
+#pragma unroll
+    for (int k = 1; k < ND; ++k) qj = j == k ? jqv[k] : qj;
     const float4* J = q.jtab(j);
     const float4 jpr = J[0], jpp = J[1], jcp = J[2], jcr = J[3];
     float sn, cs;
@@ -1555,32 +1574,28 @@ __global__ __launch_bounds__(WAVE, 1) void zb_step_kernel(const zb_model* __rest
   // (one writer lane per env; the team holds identical values)
   const bool writer = q.s == 0;
   const float step_dt = cfg.sim_dt * (float)cfg.decimation;
-  float target[ND], a_now[ND], pdel[ND];
-  float r_action_rate = 0.f;
-#pragma unroll
-  for (int j = 0; j < ND; ++j) {
-    const float a_prev = ST(ZB_S_ACTIONS + j);
-    a_now[j] = tanh_r(act[(size_t)i * ZB_ACT_DIM + j]);
-    pdel[j] = clampf(ST(ZB_S_P_DELTA + j) + PI_F * a_now[j] * cfg.joint_speed_limit * step_dt, -PI_F, PI_F);
-    target[j] = pdel[j] + m->default_joint_pos[j];
-    r_action_rate += (a_now[j] - a_prev) * (a_now[j] - a_prev);   // v2.py:502-507
-  }
-
-  // the previous _get_observations cache (one-step lag, v2.py:315-345): the pre-step terms are
-  // evaluated now, only what step_length / dones need is carried across the physics
-  float r_pre[5];
-  float pre_base_y, pre_base_z, pre_heading, pre_fwd[3], pre_feet[2][3];
+  float target[ND];
   {
+    // what the MDP needs after the physics is parked in LDS (Pre), not held in registers
+    Pre pr;
+    pr.action_rate = 0.f;
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+      const float a_prev = ST(ZB_S_ACTIONS + j);
+      pr.a_now[j] = tanh_r(act[(size_t)i * ZB_ACT_DIM + j]);
+      pr.pdel[j] = clampf(ST(ZB_S_P_DELTA + j) + PI_F * pr.a_now[j] * cfg.joint_speed_limit * step_dt, -PI_F, PI_F);
+      target[j] = pr.pdel[j] + m->default_joint_pos[j];
+      pr.action_rate += (pr.a_now[j] - a_prev) * (pr.a_now[j] - a_prev);   // v2.py:502-507
+    }
+
+    // the previous _get_observations cache (one-step lag, v2.py:315-345): the pre-step terms are
+    // evaluated now, only what step_length / dones need is carried across the physics
     Cache c;
-#ifdef ZB_PRO_OLD
-    make_cache(opaque(m), p, c);
-#else
     wave_sync();  // link table copy
     fk_team_pose(p, q);
     wave_sync();
     make_cache_q(opaque(m), q, p, c);
-#endif
-    r_pre[0] = tanh_r(10.f * c.vfwd / cfg.joint_speed_limit);                     // base_vel_forward
+    pr.r_pre[0] = tanh_r(10.f * c.vfwd / cfg.joint_speed_limit);                     // base_vel_forward
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int f = 0; f < 2; ++f) {
@@ -1589,15 +1604,16 @@ __global__ __launch_bounds__(WAVE, 1) void zb_step_kernel(const zb_model* __rest
       const float dx[3] = {c.feet_x[f][0] - c.fwd[0], c.feet_x[f][1] - c.fwd[1], c.feet_x[f][2] - c.fwd[2]};
       s2 += sqrtf(dot3(dx, dx));                                                 // feet_forward
     }
-    r_pre[1] = s1;
-    r_pre[2] = s2;
-    r_pre[3] = fabsf(c.heading_err);                                             // base_heading_x
-    r_pre[4] = fabsf(c.feet_pos[0][1] + c.feet_pos[1][1]) + fabsf(c.base_pos[1]); // base_pos_y_err (origin 0)
-    pre_base_y = c.base_pos[1];
-    pre_base_z = c.base_pos[2];
-    pre_heading = c.heading_err;
+    pr.r_pre[1] = s1;
+    pr.r_pre[2] = s2;
+    pr.r_pre[3] = fabsf(c.heading_err);                                             // base_heading_x
+    pr.r_pre[4] = fabsf(c.feet_pos[0][1] + c.feet_pos[1][1]) + fabsf(c.base_pos[1]); // base_pos_y_err (origin 0)
+    pr.base_y = c.base_pos[1];
+    pr.base_z = c.base_pos[2];
+    pr.heading = c.heading_err;
 #pragma unroll
-    for (int a = 0; a < 3; ++a) { pre_fwd[a] = c.fwd[a]; pre_feet[0][a] = c.feet_pos[0][a]; pre_feet[1][a] = c.feet_pos[1][a]; }
+    for (int a = 0; a < 3; ++a) { pr.fwd[a] = c.fwd[a]; pr.feet[0][a] = c.feet_pos[0][a]; pr.feet[1][a] = c.feet_pos[1][a]; }
+    if (writer) q.pre() = pr;
   }
 
   // 4 physics substeps (the last one reports the contact-sensor inputs and applied torques)
@@ -1608,6 +1624,15 @@ __global__ __launch_bounds__(WAVE, 1) void zb_step_kernel(const zb_model* __rest
     sp.mark(7);
   }
   m = opaque(m);
+  wave_sync();
+  const Pre pr = q.pre();
+  const float(&a_now)[ND] = pr.a_now;
+  const float(&pdel)[ND] = pr.pdel;
+  const float(&r_pre)[5] = pr.r_pre;
+  const float pre_base_y = pr.base_y, pre_base_z = pr.base_z, pre_heading = pr.heading;
+  const float(&pre_fwd)[3] = pr.fwd;
+  const float(&pre_feet)[2][3] = pr.feet;
+  const float r_action_rate = pr.action_rate;
 
   // MDP state of this env (every lane loads; one writer lane stores at the end)
   float fz_prev[ZB_HIST - 1][2], fmax_prev[ZB_HIST - 1], air_cur0[2], air_last0[2], contact0[2];
@@ -1646,18 +1671,6 @@ __global__ __launch_bounds__(WAVE, 1) void zb_step_kernel(const zb_model* __rest
 
   // post-step feet COM velocities (feet_slide)
   float feet_vel[2][3], obs_q[4];
-#ifdef ZB_POST_OLD
-  {
-    Kin k;
-    fk(m, p, k);
-    float V[NB][6];
-    body_vel(k, p, V);
-    link_com_vel(m, k, V, 0, feet_vel[0]);
-    link_com_vel(m, k, V, 11, feet_vel[1]);
-    float bp[3];
-    link_pose(m, k, 6, bp, obs_q);
-  }
-#else
   {
     wave_sync();  // the last substep's readers of the body poses are done
     fk_team_pose(p, q);
@@ -1669,7 +1682,6 @@ __global__ __launch_bounds__(WAVE, 1) void zb_step_kernel(const zb_model* __rest
     float bp[3];
     link_pose_q(m, q, 6, bp, obs_q);  // base quat of the post-step state (observation)
   }
-#endif
   sp.mark(11);
 
   // _get_dones (v2.py:384-411)
