@@ -454,7 +454,7 @@ constexpr int NCAND = NL * 4 + NSELF;
 
 // LDS layout of one workgroup (EPW envs), float4 units:
 //   YG    [NCM][WAVE]       lane (e, d) of slot c: {Y0[d], Y1[d], Y2[d], 0} (zero for d >= 12)
-//   AUX   [NCM][2][EPW]     {invm0, invm1, invm2, vmin}, {c01, c02, 0, 0}
+//   AUX   [NCM][2][EPW]     {invm0, invm1, invm2, vmin invm0}, {c01 invm1, c02 invm2, 0, 0}
 //   LAM   [NCM][EPW]        contact impulses {ln, l1, l2, 0}
 //   FRC   [NCM][EPW]        last substep: contact force {f, code}
 //   CAND  [EPW][NCAND][2]   candidates {x, sep}, {n, code = 16 la + lb + 1}
@@ -897,27 +897,30 @@ struct SensorOut {
 };
 
 // One Gauss-Seidel contact update (normal + Coulomb disk). g = {Y0[d], Y1[d], Y2[d], -} of this
-// lane's coordinate d, a0 = {invm0, invm1, invm2, vmin}, a1 = {c01, c02, -, -}, lam = {ln, l1, l2}.
-// The three row dots are reduced across the team; the tangent velocities see the normal update
-// through the cross terms. Returns the new impulses; wd (the lane's coordinate) updated.
+// lane's coordinate d, a0 = {invm0, invm1, invm2, vmin invm0}, a1 = {c01 invm1, c02 invm2, -, -}
+// (c0r = Y_r . Y_0), lam = {ln, l1, l2}. The three row dots are reduced across the team; the
+// tangent velocities see the normal update through the cross terms. Arranged for a short
+// dependency chain: the impulse-independent parts are formed while the normal row resolves, and
+// the disk projection is min(1, lim / |l|) (rsq; NaN-free for |l| = 0 via minNum). Returns the
+// new impulses; wd (the lane's coordinate) updated.
 __device__ __forceinline__ float4 pgs_update(const float4 g, const float4 a0, const float4 a1, const float4 lam,
                                              float mu, float& wd) {
   const float p0 = tsum(g.x * wd);
   const float p1 = tsum(g.y * wd);
   const float p2 = tsum(g.z * wd);
-  const float ln = fmaxf(lam.x + (a0.w - p0) * a0.x, 0.f);
+  const float ln = fmaxf(fmaf(-p0, a0.x, lam.x + a0.w), 0.f);
   const float dl = ln - lam.x;
-  const float vt1 = p1 + a1.x * dl, vt2 = p2 + a1.y * dl;
-  float l1 = lam.y - vt1 * a0.y;
-  float l2 = lam.z - vt2 * a0.z;
+  const float u1 = fmaf(-p1, a0.y, lam.y), u2 = fmaf(-p2, a0.z, lam.z);
+  float l1 = fmaf(-a1.x, dl, u1);
+  float l2 = fmaf(-a1.y, dl, u2);
   const float lim = mu * ln;
-  const float mag2 = l1 * l1 + l2 * l2;
-  if (mag2 > lim * lim) {
-    const float sc = lim * __builtin_amdgcn_rsqf(mag2);  // mag2 > 0 here
-    l1 *= sc; l2 *= sc;
-  }
+  const float sc = fminf(1.f, lim * __builtin_amdgcn_rsqf(fmaf(l1, l1, l2 * l2)));
+  l1 *= sc;
+  l2 *= sc;
   const float d1 = l1 - lam.y, d2 = l2 - lam.z;
-  wd += g.x * dl + g.y * d1 + g.z * d2;
+  wd = fmaf(g.x, dl, wd);
+  wd = fmaf(g.y, d1, wd);
+  wd = fmaf(g.z, d2, wd);
   return make_float4(ln, l1, l2, 0.f);
 }
 
@@ -1154,8 +1157,8 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
     float vmin;
     if (sep >= 0.f) vmin = -sep / dt;
     else vmin = fminf(cfg.baumgarte * (-sep) / dt, m->max_depenetration_velocity);
-    q.aux(c, 0) = make_float4(invm[0], invm[1], invm[2], vmin);
-    q.aux(c, 1) = make_float4(dot12(Y[1], Y[0]), dot12(Y[2], Y[0]), 0.f, 0.f);  // c01, c02
+    q.aux(c, 0) = make_float4(invm[0], invm[1], invm[2], vmin * invm[0]);
+    q.aux(c, 1) = make_float4(dot12(Y[1], Y[0]) * invm[1], dot12(Y[2], Y[0]) * invm[2], 0.f, 0.f);
     q.lam(c) = make_float4(0.f, 0.f, 0.f, 0.f);
   }
   wave_sync();
