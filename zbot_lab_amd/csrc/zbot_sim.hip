@@ -356,7 +356,15 @@ __device__ __forceinline__ MP opaque(MP m) {
 // (quad_perm, row_half_mirror, row_mirror), which leave all 16 lanes bit-identical sums, so the
 // redundant scalar work stays identical across the team.
 constexpr int TL = 16;           // lanes per env
-constexpr int EPW = WAVE / TL;   // envs per wave / workgroup
+#ifndef ZB_EPW
+#define ZB_EPW 4
+#endif
+#ifndef ZB_WAVES_PER_SIMD
+#define ZB_WAVES_PER_SIMD 1
+#endif
+constexpr int EPW = ZB_EPW;      // envs per workgroup (one wave; EPW < 4 leaves lanes idle)
+constexpr int WGT = TL * EPW;    // threads per workgroup
+static_assert(WGT <= WAVE, "one wave per workgroup");
 
 template <int CTRL>
 __device__ __forceinline__ float dppf(float x) {
@@ -453,7 +461,7 @@ constexpr int NSELF = 18;
 constexpr int NCAND = NL * 4 + NSELF;
 
 // LDS layout of one workgroup (EPW envs), float4 units:
-//   YG    [NCM][WAVE]       lane (e, d) of slot c: {Y0[d], Y1[d], Y2[d], 0} (zero for d >= 12)
+//   YG    [NCM][WGT]        lane (e, d) of slot c: {Y0[d], Y1[d], Y2[d], 0} (zero for d >= 12)
 //   AUX   [NCM][2][EPW]     {invm0, invm1, invm2, vmin invm0}, {c01 invm1, c02 invm2, 0, 0}
 //   LAM   [NCM][EPW]        contact impulses {ln, l1, l2, 0}
 //   FRC   [NCM][EPW]        last substep: contact force {f, code}
@@ -465,7 +473,7 @@ constexpr int NCAND = NL * 4 + NSELF;
 //   UB    [NL][EPW]         world union spheres
 //   LNK   [LNK4]            link table copy
 constexpr int YG_OFF = 0;
-constexpr int AUX_OFF = YG_OFF + NCM * WAVE;
+constexpr int AUX_OFF = YG_OFF + NCM * WGT;
 constexpr int LAM_OFF = AUX_OFF + NCM * 2 * EPW;
 constexpr int FRC_OFF = LAM_OFF + NCM * EPW;
 constexpr int CAND_OFF = FRC_OFF + NCM * EPW;
@@ -490,8 +498,8 @@ static_assert(sizeof(Pre) <= 16 * 8, "Pre fits PRE4 granules");
 struct Q {
   float4* b;
   int lane, e, s;
-  __device__ __forceinline__ float4& yg(int c) const { return b[YG_OFF + c * WAVE + lane]; }
-  __device__ __forceinline__ float4& yg_at(int c, int d) const { return b[YG_OFF + c * WAVE + TL * e + d]; }
+  __device__ __forceinline__ float4& yg(int c) const { return b[YG_OFF + c * WGT + lane]; }
+  __device__ __forceinline__ float4& yg_at(int c, int d) const { return b[YG_OFF + c * WGT + TL * e + d]; }
   __device__ __forceinline__ float4& aux(int c, int h) const { return b[AUX_OFF + (c * 2 + h) * EPW + e]; }
   __device__ __forceinline__ float4& lam(int c) const { return b[LAM_OFF + c * EPW + e]; }
   __device__ __forceinline__ float4& frc(int c) const { return b[FRC_OFF + c * EPW + e]; }
@@ -660,6 +668,15 @@ __device__ __forceinline__ void fk_team_pose(const Phys& s, const Q& q) {
   fk_team<false>(s, q, dummy, ds);
 }
 
+__device__ __forceinline__ void read_S(const Q& q, float S[ND][6]) {
+#pragma unroll
+  for (int j = 0; j < ND; ++j) {
+    const float4 g0 = q.jnt(j, 0), g1 = q.jnt(j, 1);
+    S[j][0] = g0.x; S[j][1] = g0.y; S[j][2] = g0.z;
+    S[j][3] = g1.x; S[j][4] = g1.y; S[j][5] = g1.z;
+  }
+}
+
 // joint motion subspaces S_j = [a_j; o_j x a_j] and origins o_j (relative to P) from LDS
 __device__ __forceinline__ void read_joints(const Q& q, float S[ND][6], float org[ND][3]) {
 #pragma unroll
@@ -669,6 +686,12 @@ __device__ __forceinline__ void read_joints(const Q& q, float S[ND][6], float or
     S[j][3] = g1.x; S[j][4] = g1.y; S[j][5] = g1.z;
     org[j][0] = g0.w; org[j][1] = g1.w; org[j][2] = g2.x;
   }
+}
+
+template <class T>
+__device__ __forceinline__ T* opaque_ptr(T* p) {
+  asm volatile("" : "+v"(p));
+  return p;
 }
 
 // ------------------------------------------------------------------------- contacts
@@ -952,7 +975,6 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
     so.tau2 = t2;
   }
 
-  float S[ND][6], org[ND][3];
   SI Ib;                   // this lane's body (b = s < NB; zero elsewhere)
   float Sown[6];           // this lane's joint motion subspace (j = s < ND; zero elsewhere)
   int nc;
@@ -962,13 +984,17 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
   wave_sync();
   sp.mark(9);
   nc = detect(cfg, s.pos[2], q, over, sp);
-  read_joints(q, S, org);
   m = opaque(m0);
 
   // RNEA bias forces (qddot = 0, gravity as base acceleration), one body per lane: lane b runs
   // the velocity / acceleration chain up to its body (joints j >= b contribute zero), forms f_b,
   // and the team suffix sum F_b = sum_{b' >= b} f_b' (DPP row shifts) gives the joint forces.
   float Cb[NV];
+  const float arm = dt * (m->kd + dt * m->kp);
+  float L[NT];
+  {
+  float S[ND][6];  // joint motion subspaces (LDS), live through RNEA + CRBA only
+  read_S(q, S);
   {
     const int b = q.s;
     float V[6] = {s.av[0], s.av[1], s.av[2], s.lv[0], s.lv[1], s.lv[2]};
@@ -1017,8 +1043,6 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
 
   // CRBA: composite inertias by a team suffix sum; lane k forms F_k = Ic_{k+1} S_k and its
   // mass-matrix column S_jj . F_k, then the team assembles the lower triangle in every lane
-  const float arm = dt * (m->kd + dt * m->kp);
-  float L[NT];
   {
     float ic[10] = {Ib.m, Ib.h[0], Ib.h[1], Ib.h[2], Ib.I[0], Ib.I[1], Ib.I[2], Ib.I[3], Ib.I[4], Ib.I[5]};
     suffix_sum<10>(ic);
@@ -1053,6 +1077,7 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
     crba_column<4>(L, Fk, Mk, arm);
     crba_column<5>(L, Fk, Mk, arm);
   }
+  }  // S
 
   // implicit PD drives. Pass 1: all implicit (armature on the diagonal). A joint whose implicit
   // torque exceeds the effort limit gets an explicit +-limit torque and loses its armature
@@ -1113,6 +1138,8 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
   if (q.s < nc) {
     const int c = q.s;
     const int pos = over ? q.map(c) : c;
+    float S[ND][6], org[ND][3];
+    read_joints(q, S, org);
     const float4 g0 = q.cand(pos, 0), gn = q.cand(pos, 1);
     const float x[3] = {g0.x, g0.y, g0.z};
     const float n[3] = {gn.x, gn.y, gn.z};
@@ -1546,7 +1573,7 @@ __device__ __forceinline__ void load_phys(const float* __restrict__ st, int N, i
 // One policy step per lane. Live state across the 4 substeps is kept to the physics state, the
 // joint targets and the ~15 floats of the lagged observation cache the rewards need; the MDP
 // state is loaded from HBM only after the physics.
-__global__ __launch_bounds__(WAVE, 1) void zb_step_kernel(const zb_model* __restrict__ mg,
+__global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_step_kernel(const zb_model* __restrict__ mg,
                                                           const float4* __restrict__ links, zb_task_cfg cfg, int N,
                                                           float* __restrict__ st, const float* __restrict__ act,
                                                           float* __restrict__ obs, float* __restrict__ rew,
@@ -1560,7 +1587,7 @@ __global__ __launch_bounds__(WAVE, 1) void zb_step_kernel(const zb_model* __rest
   const int i = env < N ? env : N - 1;
   const bool lead = env < N && lane % TL == 0;
   const Q q{lds, lane, lane / TL, lane % TL};
-  for (int t = lane; t < LNK4; t += WAVE) lds[LNK_OFF + t] = links[t];
+  for (int t = lane; t < LNK4; t += WGT) lds[LNK_OFF + t] = links[t];
   // the env's state row: lane s loads fields s, s+16, ... (one coalesced load per field group)
   Stamps sp;
   sp.begin();
@@ -1637,7 +1664,10 @@ __global__ __launch_bounds__(WAVE, 1) void zb_step_kernel(const zb_model* __rest
   const float(&pre_feet)[2][3] = pr.feet;
   const float r_action_rate = pr.action_rate;
 
-  // MDP state of this env (every lane loads; one writer lane stores at the end)
+  // MDP state of this env (every lane loads; one writer lane stores at the end). The state
+  // pointer goes through an empty asm so these loads are not hoisted above the physics (they
+  // would be held in registers across all substeps).
+  st = opaque_ptr(st);
   float fz_prev[ZB_HIST - 1][2], fmax_prev[ZB_HIST - 1], air_cur0[2], air_last0[2], contact0[2];
   float step_len[2], f_last0[2], down[2][3], sums0[ZB_NUM_REWARD_TERMS];
 #pragma unroll
@@ -1905,7 +1935,7 @@ __global__ void zb_observe_kernel(const zb_model* __restrict__ mg, int N, const 
   write_obs(m, p, d, obs, i);
 }
 
-__global__ __launch_bounds__(WAVE, 1) void zb_substeps_kernel(const zb_model* __restrict__ mg,
+__global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_substeps_kernel(const zb_model* __restrict__ mg,
                                                               const float4* __restrict__ links, zb_task_cfg cfg, int N,
                                                               float* __restrict__ st, const float* __restrict__ targets,
                                                               int nsub, float* __restrict__ net_force,
@@ -1916,7 +1946,7 @@ __global__ __launch_bounds__(WAVE, 1) void zb_substeps_kernel(const zb_model* __
   const int env = xcd_block(blockIdx.x, gridDim.x) * EPW + lane / TL;
   const int i = env < N ? env : N - 1;
   const Q q{lds, lane, lane / TL, lane % TL};
-  for (int t = lane; t < LNK4; t += WAVE) lds[LNK_OFF + t] = links[t];
+  for (int t = lane; t < LNK4; t += WGT) lds[LNK_OFF + t] = links[t];
   Phys p;
   load_phys(st, N, i, p);
   float tg[ND], tau[ND], F[1][3];
@@ -2164,7 +2194,7 @@ int zb_step(zb_handle h, const float* actions, float* obs, float* reward, uint8_
   const int blocks = (h->n + EPW - 1) / EPW;
   const bool prof = h->prof_n < h->prof_max;
   if (prof) HIPCHK(hipEventRecord(h->prof_ev[2 * h->prof_n], s), "hipEventRecord");
-  zb_step_kernel<<<blocks, WAVE, 0, s>>>(h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward, terminated,
+  zb_step_kernel<<<blocks, WGT, 0, s>>>(h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward, terminated,
                                          truncated, h->d_acc);
   int rc = launch_check("zb_step_kernel");
   if (prof) {
@@ -2223,7 +2253,7 @@ int zb_physics_substeps(zb_handle h, const float* targets, int nsub, float* net_
                         void* stream) {
   if (!h || !targets || nsub < 1) return set_err(-1, "zb_physics_substeps", hipSuccess);
   const int blocks = (h->n + EPW - 1) / EPW;
-  zb_substeps_kernel<<<blocks, WAVE, 0, (hipStream_t)stream>>>(h->d_model, h->d_links, h->cfg, h->n, h->d_state, targets, nsub,
+  zb_substeps_kernel<<<blocks, WGT, 0, (hipStream_t)stream>>>(h->d_model, h->d_links, h->cfg, h->n, h->d_state, targets, nsub,
                                                                net_force, applied_torque);
   return launch_check("zb_substeps_kernel");
 }
