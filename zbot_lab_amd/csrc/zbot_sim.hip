@@ -1899,7 +1899,11 @@ __global__ void zb_derive_kernel(const zb_model* __restrict__ mg, float4* __rest
 __global__ void zb_finalize_kernel(int N, float* __restrict__ st, float* __restrict__ acc,
                                    float* __restrict__ log_means, int32_t* __restrict__ log_counts,
                                    float* __restrict__ user_means, int32_t* __restrict__ user_counts, float episode_s,
-                                   int max_ep_len, uint64_t seed, uint64_t ctr, int force_full, int reset_counts) {
+                                   int max_ep_len, uint64_t seed, uint64_t* __restrict__ calls, int force_full,
+                                   int reset_counts) {
+  // the call counter (the episode-length RNG stream position) lives on the device so that a
+  // captured graph of zb_step advances it on every replay
+  const uint64_t ctr = *calls;
   const float nres = acc[13];
   const bool full = force_full || nres == (float)N;
   __syncthreads();
@@ -1917,6 +1921,7 @@ __global__ void zb_finalize_kernel(int N, float* __restrict__ st, float* __restr
   }
   __syncthreads();
   if (threadIdx.x < ACC) acc[threadIdx.x] = 0.f;
+  if (threadIdx.x == 0) *calls = ctr + 1;
   if (full)
     for (int i = threadIdx.x; i < N; i += blockDim.x) {
       const uint64_t h = hash64(seed ^ hash64(ctr * 0x100000001B3ull + (uint64_t)i));
@@ -1978,7 +1983,7 @@ struct zb_sim {
   int device;
   int n;
   uint64_t seed;
-  uint64_t calls;
+  uint64_t* d_calls;  // zb_step / zb_reset calls so far (device counter, graph-replay safe)
   zb_task_cfg cfg;
   zb_model* d_model;
   float4* d_links;  // per-link collision table [NL][LINK4] (detect)
@@ -2042,11 +2047,13 @@ int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_dev
   h->device = hip_device;
   h->n = num_envs;
   h->seed = seed;
-  h->calls = 0;
+  h->d_calls = nullptr;
   h->cfg = *c;
   HIPCHK(hipMalloc(&h->d_model, sizeof(zb_model)), "hipMalloc model");
   HIPCHK(hipMalloc(&h->d_state, sizeof(float) * (size_t)ZB_STATE_DIM * num_envs), "hipMalloc state");
   HIPCHK(hipMalloc(&h->d_acc, sizeof(float) * ACC), "hipMalloc acc");
+  HIPCHK(hipMalloc(&h->d_calls, sizeof(uint64_t)), "hipMalloc calls");
+  HIPCHK(hipMemset(h->d_calls, 0, sizeof(uint64_t)), "hipMemset calls");
   HIPCHK(hipMalloc(&h->d_log_means, sizeof(float) * ZB_NUM_REWARD_TERMS), "hipMalloc log");
   HIPCHK(hipMalloc(&h->d_log_counts, sizeof(int32_t) * 2), "hipMalloc log");
   HIPCHK(hipMemcpy(h->d_model, m, sizeof(zb_model), hipMemcpyHostToDevice), "hipMemcpy model");
@@ -2166,6 +2173,7 @@ void zb_destroy(zb_handle h) {
   (void)hipFree(h->d_links);
   (void)hipFree(h->d_state);
   (void)hipFree(h->d_acc);
+  (void)hipFree(h->d_calls);
   (void)hipFree(h->d_log_means);
   (void)hipFree(h->d_log_counts);
   delete h;
@@ -2179,11 +2187,10 @@ int zb_reset(zb_handle h, const int32_t* env_ids, int n, void* stream) {
   zb_reset_kernel<<<(cnt + 255) / 256, 256, 0, s>>>(h->d_model, h->d_links, h->n, h->d_state, env_ids, cnt, h->d_acc);
   int rc = launch_check("zb_reset_kernel");
   if (rc) return rc;
-  const uint64_t ctr = h->calls++;
   const float ep_s = h->cfg.sim_dt * h->cfg.decimation * h->cfg.max_episode_length;
   const int full = env_ids == nullptr || n == h->n;
   zb_finalize_kernel<<<1, 1024, 0, s>>>(h->n, h->d_state, h->d_acc, h->d_log_means, h->d_log_counts, h->u_log_means,
-                                        h->u_log_counts, ep_s, h->cfg.max_episode_length, h->seed, ctr, full, 1);
+                                        h->u_log_counts, ep_s, h->cfg.max_episode_length, h->seed, h->d_calls, full, 1);
   return launch_check("zb_finalize_kernel");
 }
 
@@ -2202,10 +2209,9 @@ int zb_step(zb_handle h, const float* actions, float* obs, float* reward, uint8_
     ++h->prof_n;
   }
   if (rc) return rc;
-  const uint64_t ctr = h->calls++;
   const float ep_s = h->cfg.sim_dt * h->cfg.decimation * h->cfg.max_episode_length;
   zb_finalize_kernel<<<1, 1024, 0, s>>>(h->n, h->d_state, h->d_acc, h->d_log_means, h->d_log_counts, h->u_log_means,
-                                        h->u_log_counts, ep_s, h->cfg.max_episode_length, h->seed, ctr, 0, 0);
+                                        h->u_log_counts, ep_s, h->cfg.max_episode_length, h->seed, h->d_calls, 0, 0);
   return launch_check("zb_finalize_kernel");
 }
 

@@ -1,6 +1,6 @@
 """``PPORunnerCfgV2`` (reference ``source/zbot/zbot/tasks/zbot6b_direct/agents/rsl_rl_ppo_cfg.py:65-91``).
 
-Hyper-parameters only; the PPO runner itself is the next §8(f) row."""
+Consumed by ``zbot_lab_amd.rl.OnPolicyRunner`` (``agent_cfg.to_dict()``, as ``train.py:192``)."""
 from __future__ import annotations
 
 from dataclasses import asdict, dataclass, field

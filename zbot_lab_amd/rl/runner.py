@@ -1,0 +1,201 @@
+"""``OnPolicyRunner`` with rsl-rl-lib's interface, as the reference's training script drives it
+(``scripts/rsl_rl/train.py:158-205``: ``OnPolicyRunner(env, agent_cfg.to_dict(), log_dir=...,
+device=...)``, ``runner.learn(num_learning_iterations=max_iterations, init_at_random_ep_len=True)``;
+``play.py:150-175``: ``runner.load(path)``, ``runner.get_inference_policy(device=...)``).
+
+Checkpoints keep rsl_rl's keys (``model_state_dict``, ``optimizer_state_dict``, ``iter``,
+``infos``) as ``model_{it}.pt``. Multi-GPU follows rsl_rl: when ``WORLD_SIZE > 1`` the process
+group must already be initialised (torchrun, one process per GPU; ``nccl`` = RCCL on ROCm), rank 0
+logs and saves, parameters are broadcast from rank 0 at start and PPO averages gradients per
+minibatch (``PPO.reduce_parameters``).
+
+Speed: the rollout keeps obs/actions on the GPU, the env step is one fused kernel, and episode
+statistics are accumulated on the device (one host sync per iteration for the log line). On a GPU
+the whole 24-step rollout (policy sampling, the env kernels through the C ABI, storage writes,
+statistics) is captured once as a HIP graph and replayed every iteration; the first iteration runs
+eagerly and serves as the capture warm-up.
+"""
+from __future__ import annotations
+
+import os
+import statistics
+import time
+from collections import deque
+
+import torch
+import torch.distributed as dist
+
+from .ppo import PPO, ActorCritic
+
+
+def _policy_obs(obs):
+    return obs["policy"] if isinstance(obs, dict) or hasattr(obs, "keys") else obs
+
+
+class OnPolicyRunner:
+    def __init__(self, env, train_cfg: dict, log_dir: str | None = None, device: str = "cpu",
+                 use_graph: bool | None = None):
+        self.cfg = train_cfg
+        self.alg_cfg = dict(train_cfg["algorithm"])
+        self.policy_cfg = dict(train_cfg["policy"])
+        self.device = device
+        self.env = env
+        self._configure_multi_gpu()
+        obs = _policy_obs(self.env.get_observations())
+        num_obs = obs.shape[1]
+        self.alg_cfg.pop("class_name", None)
+        self.policy_cfg.pop("class_name", None)
+        policy = ActorCritic(num_obs, num_obs, self.env.num_actions, **self.policy_cfg).to(self.device)
+        self.alg = PPO(policy, device=self.device, multi_gpu_cfg=self.multi_gpu_cfg, **self.alg_cfg)
+        self.num_steps_per_env = int(train_cfg["num_steps_per_env"])
+        self.save_interval = int(train_cfg["save_interval"])
+        self.alg.init_storage(self.env.num_envs, self.num_steps_per_env, num_obs, num_obs, self.env.num_actions)
+        self.log_dir = log_dir
+        self.current_learning_iteration = 0
+        self.tot_timesteps = 0
+        self.tot_time = 0.0
+        self.log: list[dict] = []
+        # episode statistics persist across learn() calls (device accumulators, rsl_rl's deques)
+        self.rewbuffer, self.lenbuffer = deque(maxlen=100), deque(maxlen=100)
+        self.cur_rew = torch.zeros(self.env.num_envs, device=self.device)
+        self.cur_len = torch.zeros(self.env.num_envs, device=self.device)
+        self.ep_stats = torch.zeros(3, device=self.device)  # reward sum, length sum, count
+        self.use_graph = (torch.device(device).type == "cuda") if use_graph is None else use_graph
+        self._graph = None
+        self._g_obs = None
+        self._update_graph = None
+        # capturing the update (autograd + fused Adam) segfaults in torch 2.10 / ROCm 7 here
+        # (AccumulateGrad stream mismatch); kept opt-in until that is resolved
+        self.graph_update = False
+
+    def _configure_multi_gpu(self) -> None:
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.is_distributed = world > 1
+        if not self.is_distributed:
+            self.gpu_global_rank, self.gpu_world_size, self.multi_gpu_cfg = 0, 1, None
+            return
+        if not dist.is_initialized():
+            raise RuntimeError("WORLD_SIZE > 1 but torch.distributed is not initialised (launch with torchrun)")
+        self.gpu_global_rank = dist.get_rank()
+        self.gpu_world_size = dist.get_world_size()
+        self.multi_gpu_cfg = {"global_rank": self.gpu_global_rank, "world_size": self.gpu_world_size}
+
+    # ------------------------------------------------------------------ training
+    def learn(self, num_learning_iterations: int, init_at_random_ep_len: bool = False) -> list[dict]:
+        env = self.env
+        if init_at_random_ep_len:
+            env.episode_length_buf = torch.randint_like(env.episode_length_buf, high=int(env.max_episode_length))
+        obs = _policy_obs(env.get_observations()).to(self.device)
+        self.alg.policy.train()
+        if self.is_distributed:
+            self.alg.broadcast_parameters()
+        rewbuffer, lenbuffer = self.rewbuffer, self.lenbuffer
+        start_iter = self.current_learning_iteration
+        for it in range(start_iter, start_iter + num_learning_iterations):
+            t0 = time.perf_counter()
+            with torch.no_grad():  # not inference_mode: graph capture updates the RNG state tensors
+                if self.use_graph and self._graph is not None:
+                    self._graph.replay()
+                    obs = self._g_obs
+                else:
+                    obs = self._rollout(obs)
+                    if self.use_graph:
+                        self._capture(obs)
+                        obs = self._g_obs
+                collect_time = time.perf_counter() - t0
+                t1 = time.perf_counter()
+                self.alg.compute_returns(obs)
+            if self._update_graph is not None:
+                self._update_graph.replay()
+            else:
+                self.alg.update_steps()
+                if self.graph_update and self._graph is not None:
+                    self._capture_update()
+            losses = self.alg.update_stats()
+            learn_time = time.perf_counter() - t1
+            stats = self.ep_stats.tolist()
+            if stats[2] > 0:
+                rewbuffer.append(stats[0] / stats[2])
+                lenbuffer.append(stats[1] / stats[2])
+            self.current_learning_iteration = it
+            self.tot_timesteps += self.num_steps_per_env * env.num_envs * self.gpu_world_size
+            self.tot_time += collect_time + learn_time
+            rec = {"iteration": it, "collection_time": collect_time, "learn_time": learn_time,
+                   "fps": self.num_steps_per_env * env.num_envs * self.gpu_world_size / (collect_time + learn_time),
+                   "mean_reward": statistics.mean(rewbuffer) if rewbuffer else float("nan"),
+                   "mean_episode_length": statistics.mean(lenbuffer) if lenbuffer else float("nan"),
+                   "learning_rate": self.alg.learning_rate, "mean_noise_std": self.alg.policy.std.mean().item(),
+                   **{f"loss/{k}": v for k, v in losses.items()}}
+            log = self._extras.get("log", {}) if isinstance(self._extras, dict) else {}
+            for k, v in log.items():
+                rec[k] = float(v) if not torch.is_tensor(v) else float(v.float().mean())
+            self.log.append(rec)
+            if self.gpu_global_rank == 0 and self.log_dir and (it % self.save_interval == 0):
+                self.save(os.path.join(self.log_dir, f"model_{it}.pt"))
+        self.current_learning_iteration = start_iter + num_learning_iterations
+        if self.gpu_global_rank == 0 and self.log_dir:
+            self.save(os.path.join(self.log_dir, f"model_{self.current_learning_iteration}.pt"))
+        return self.log
+
+    def _rollout(self, obs: torch.Tensor) -> torch.Tensor:
+        """num_steps_per_env env steps into the storage; episode statistics into ep_stats."""
+        env = self.env
+        self.ep_stats.zero_()
+        for _ in range(self.num_steps_per_env):
+            actions = self.alg.act(obs, obs)
+            obs_d, rewards, dones, extras = env.step(actions.to(env.device))
+            obs = _policy_obs(obs_d).to(self.device)
+            rewards, dones = rewards.to(self.device), dones.to(self.device)
+            self.alg.process_env_step(rewards, dones, extras)
+            self.cur_rew += rewards
+            self.cur_len += 1
+            d = dones > 0
+            self.ep_stats += torch.stack([torch.where(d, self.cur_rew, 0.0).sum(),
+                                          torch.where(d, self.cur_len, 0.0).sum(), d.sum().float()])
+            self.cur_rew.masked_fill_(d, 0.0)
+            self.cur_len.masked_fill_(d, 0.0)
+        self._extras = extras
+        return obs
+
+    def _capture(self, obs: torch.Tensor) -> None:
+        """Record one rollout (reading obs from a static buffer) as a graph; nothing executes."""
+        self._g_obs = obs.clone()
+        storage_step = self.alg.storage.step
+        self.alg.storage.step = 0
+        torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            last = self._rollout(self._g_obs)
+            self._g_obs.copy_(last)
+        self.alg.storage.step = storage_step
+        self._graph = g
+
+    def _capture_update(self) -> None:
+        """Record the 20 minibatch updates (forward, backward, gradient all-reduce, clip, fused Adam
+        with a device learning rate) as a graph; the eager first update was the warm-up."""
+        torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.alg.update_steps()
+        self._update_graph = g
+
+    # ------------------------------------------------------------------ checkpoints / inference
+    def save(self, path: str, infos: dict | None = None) -> None:
+        os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+        torch.save({"model_state_dict": self.alg.policy.state_dict(),
+                    "optimizer_state_dict": self.alg.optimizer.state_dict(),
+                    "iter": self.current_learning_iteration, "infos": infos}, path)
+
+    def load(self, path: str, load_optimizer: bool = True) -> dict | None:
+        d = torch.load(path, map_location=self.device, weights_only=True)
+        self.alg.policy.load_state_dict(d["model_state_dict"])
+        if load_optimizer:
+            self.alg.optimizer.load_state_dict(d["optimizer_state_dict"])
+        self.current_learning_iteration = d["iter"]
+        return d.get("infos")
+
+    def get_inference_policy(self, device=None):
+        self.alg.policy.eval()
+        if device is not None:
+            self.alg.policy.to(device)
+        return self.alg.policy.act_inference
