@@ -13,6 +13,10 @@ process with hipEvents on the launch stream (libzbot ``zb_profile_begin/end``). 
 per env-step = 794 B: 84 fp32 persistent state read + written, actions 24 B,
 obs 92 B, reward 4 B, two flag bytes. ``cpu_baseline``: the C oracle (same model + algorithm,
 OpenMP over envs) on this host's cores, on a bounded sample.
+
+``--task standup`` measures the stand-up task instead (zbot-6b-standup-v0,
+32768 envs, friction randomisation on; kernel ``zb_su_step_kernel``, 510 B per env-step: 43 fp32
+state rows read + written, 12 friction coefficients read, actions 24 B, obs 88 B, reward, flags).
 """
 from __future__ import annotations
 
@@ -26,6 +30,7 @@ import torch
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 BYTES_PER_ENV_STEP = 794
+SU_BYTES_PER_ENV_STEP = 2 * 43 * 4 + 12 * 4 + 24 + 88 + 4 + 2  # = 510, stand-up task
 
 
 def parse():
@@ -33,7 +38,8 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=500)
     p.add_argument("--warmup", type=int, default=50)
-    p.add_argument("--envs-per-gpu", type=int, default=4096)
+    p.add_argument("--task", choices=("walking", "standup"), default="walking")
+    p.add_argument("--envs-per-gpu", type=int, default=None, help="default 4096 (walking) / 32768 (standup, C5)")
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--action-pool", type=int, default=64, help="distinct pre-drawn randn action batches cycled")
@@ -46,7 +52,7 @@ def parse():
 ENVS_PER_WORKGROUP = 4         # zb_step_kernel: one 64-lane workgroup = 4 envs x 16 lanes
 
 
-def pmc_traffic(num_envs: int):
+def pmc_traffic(num_envs: int, kernel: str = "zb_step_kernel"):
     """HBM bytes per zb_step_kernel launch from the committed rocprofv3 PMC passes (separate
     FETCH_SIZE / WRITE_SIZE runs, profiles/<round>/pmc_*_zb_step_kernel.csv) for the same grid
     (work-items = 64 per workgroup of 4 envs).
@@ -58,7 +64,7 @@ def pmc_traffic(num_envs: int):
     for d in sorted(glob.glob(os.path.join(here, "profiles", "r*")), reverse=True):
         vals = {}
         for name in ("FETCH_SIZE", "WRITE_SIZE"):
-            for f in glob.glob(os.path.join(d, "pmc_*_zb_step_kernel.csv")):
+            for f in glob.glob(os.path.join(d, f"pmc_*_{kernel}.csv")):
                 for row in csv.DictReader(open(f)):
                     grid = -(-num_envs // ENVS_PER_WORKGROUP) * 64
                     if row["counter"] == name and int(row["grid"]) == grid:
@@ -68,12 +74,13 @@ def pmc_traffic(num_envs: int):
     return None, None
 
 
-def cpu_baseline(num_envs: int, seconds: float) -> dict:
+def cpu_baseline(num_envs: int, seconds: float, standup: bool = False) -> dict:
     """Time the C oracle (test infrastructure, used here only as the CPU baseline)."""
     import numpy as np
     from oracle.pyoracle import OracleSim
+    from zbot_lab_amd import model as zm
     threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
-    sim = OracleSim(num_envs, threads=threads, seed=0)
+    sim = OracleSim(num_envs, zm.TaskCfg.standup() if standup else None, threads=threads, seed=0)
     sim.reset()
     rng = np.random.default_rng(42)
     acts = [rng.standard_normal((num_envs, 6)).astype(np.float32) for _ in range(8)]
@@ -102,16 +109,17 @@ def main():
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
 
-    from zbot_lab_amd.envs import ZbotDirectEnvCfgV2, ZbotDirectEnvV2
-    cfg = ZbotDirectEnvCfgV2()
-    cfg.scene.num_envs = args.envs_per_gpu
+    from zbot_lab_amd.envs import Zbot6SUpEnv, Zbot6SUpEnvCfg, ZbotDirectEnvCfgV2, ZbotDirectEnvV2
+    standup = args.task == "standup"
+    cfg = Zbot6SUpEnvCfg() if standup else ZbotDirectEnvCfgV2()
+    cfg.scene.num_envs = args.envs_per_gpu or (32768 if standup else 4096)
     cfg.sim.device = str(dev)
     cfg.seed = 42 + rank
     if args.solver_iterations is not None:
         cfg.solver.iterations = args.solver_iterations
     if args.no_self_collision:
         cfg.solver.self_collision = False
-    env = ZbotDirectEnvV2(cfg)
+    env = Zbot6SUpEnv(cfg) if standup else ZbotDirectEnvV2(cfg)
     n = env.num_envs
     env.reset()
     gen = torch.Generator(device=dev)
@@ -145,8 +153,12 @@ def main():
 
     if rank == 0:
         kern_s = kern_ms / 1e3 / max(kern_n, 1)
-        traffic, traffic_src = pmc_traffic(n)
-        achieved = n * BYTES_PER_ENV_STEP / kern_s / 1e9
+        kname = "zb_su_step_kernel" if standup else "zb_step_kernel"
+        bpe = SU_BYTES_PER_ENV_STEP if standup else BYTES_PER_ENV_STEP
+        traffic, traffic_src = pmc_traffic(n, kname)
+        achieved = n * bpe / kern_s / 1e9
+        workload = (f"zbot-6b-standup-v0 (C5), {n} envs/GPU x {world} GPU, friction DR, random-action throughput"
+                    if standup else f"zbot-6b-walking-v2, {n} envs/GPU x {world} GPU, random-action throughput")
         out = {
             "metric": "env-steps/sec at 4096/65536 envs, 1->8 GPUs; % HBM roofline",
             "value": value,
@@ -160,17 +172,17 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic: default-pose starts, full reset, randn(N,6) actions seeded 42+rank",
-            "config": {"workload": f"zbot-6b-walking-v2, {n} envs/GPU x {world} GPU, random-action throughput",
+            "config": {"workload": workload,
                        "envs_per_gpu": n, "total_envs": n * world, "decimation": 4, "sim_dt": 0.005,
                        "parallelism": f"env-sharded x{world} (replicas, no collective)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": "zb_step_kernel", "kernel_ms": kern_s * 1e3,
-                         "bytes_per_env_step": BYTES_PER_ENV_STEP},
+                         "kernel": kname, "kernel_ms": kern_s * 1e3,
+                         "bytes_per_env_step": bpe},
             "cpu_baseline": None,
         }
         if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = cpu_baseline(n, args.cpu_baseline_seconds)
+            out["cpu_baseline"] = cpu_baseline(min(n, 4096), args.cpu_baseline_seconds, standup)
         print(json.dumps(out), flush=True)
     env.close()
     if dist is not None:

@@ -1,5 +1,6 @@
 /*
- * zbot.h — C ABI of the MI355X-native batched ZBOT-6 walking simulator (zbot-6b-walking-v2).
+ * zbot.h — C ABI of the MI355X-native batched ZBOT-6 simulator: zbot-6b-walking-v2 (the hot path)
+ * and zbot-6b-standup-v0 (the snake -> biped stand-up task on the same robot and physics).
  *
  * One handle owns N environments' persistent state in HBM (SoA, [field][env], fp32) and steps
  * them with one fused HIP kernel per policy step (4 physics substeps + contact sensor + MDP +
@@ -19,6 +20,17 @@
  *   zb_read_log / zb_set_log_buffers <- extras["log"] written in _reset_idx (v2.py:441-459)
  *   zb_get_state / zb_set_state / zb_physics_substeps: parity + debugging (no reference analogue;
  *                  they stand in for Articulation.data reads / write_*_to_sim)
+ *
+ * Stand-up task (task = ZB_TASK_STANDUP_V0; source/zbot/zbot/tasks/zbot6b_direct/
+ * zbot_direct_6_standup_env_v0.py = "standup.py", robot ZBOT_6S_CFG_2 zbot_cfg.py:721-763):
+ *   zb_create   <- gym.make("zbot-6b-standup-v0") -> Zbot6SUpEnv.__init__ (standup.py:453-535)
+ *   zb_step     <- _pre_physics_step (538-551), 4 x physics, _get_dones (634-643) with
+ *                  _compute_intermediate_values (571-591), _get_rewards (620-632, terms 705-856),
+ *                  _reset_idx (645-703) incl. the reset events reset_root_state_uniform (33-97)
+ *                  and my_curriculum (99-111), _get_observations (593-618)
+ *   zb_set_link_friction <- EventCfg.physics_material = randomize_rigid_body_material
+ *                  (startup event, standup.py:124-136): the sampled per-shape friction
+ *   zb_read_curriculum <- Zbot6SUpEnv.curriculum_stage / common_step_counter
  *
  * Conventions: quaternions (w, x, y, z); world Z-up; gravity (0, 0, -9.81); every env in its
  * own env-local frame (origin 0; the plane is infinite and envs are collision-filtered in the
@@ -45,6 +57,11 @@ extern "C" {
 #define ZB_MAX_SELF_PAIRS 64
 #define ZB_MAX_CONTACTS 12    /* contact slots per env per substep (deepest kept) */
 
+#define ZB_TASK_WALKING_V2 0  /* zbot-6b-walking-v2 (v2.py) */
+#define ZB_TASK_STANDUP_V0 1  /* zbot-6b-standup-v0 (standup.py) */
+#define ZB_SU_OBS_DIM 22      /* standup.py:199 */
+#define ZB_SU_NUM_REWARD_TERMS 4
+
 /* Persistent per-env state, SoA [ZB_STATE_DIM][num_envs] float32. */
 enum zb_state_field {
   ZB_S_ROOT_POS = 0,        /* 3  root link (foot_0) origin, env-local */
@@ -68,6 +85,23 @@ enum zb_state_field {
   ZB_S_EP_LEN = 70,         /* 1  episode_length_buf (integer-valued float) */
   ZB_S_EP_SUMS = 71,        /* 13 _episode_sums in reward-term order */
   ZB_STATE_DIM = 84
+};
+
+/* Stand-up task state, SoA [ZB_SU_STATE_DIM][num_envs] float32. Rows 0..24 (root, joints) are
+ * laid out as in zb_state_field. */
+enum zb_standup_state_field {
+  ZB_SU_P_DELTA = 25,       /* 6  standup.py:484,540-548 */
+  ZB_SU_ACTIONS = 31,       /* 6  tanh(actions) of the last step */
+  ZB_SU_CENTER_Z_LAST = 37, /* 1  standup.py:511,639-641 */
+  ZB_SU_EP_LEN = 38,        /* 1  episode_length_buf (integer-valued float) */
+  ZB_SU_EP_SUMS = 39,       /* 4  _episode_sums in reward-term order */
+  ZB_SU_LINK_MU = 43,       /* 12 per-link friction coefficient (read-only for zb_step) */
+  ZB_SU_STATE_DIM = 55
+};
+
+/* Stand-up reward term order = dict order of Zbot6SUpEnvCfg.reward_cfg (standup.py:418-427). */
+enum zb_standup_reward_term {
+  ZB_SU_R_UPWARD_2 = 0, ZB_SU_R_SHAPE_SYMMETRY, ZB_SU_R_FEET_DOWNWARD, ZB_SU_R_FEET_DOWNWARD_4
 };
 
 /* Reward term order = dict order of ZbotDirectEnvCfgV2.reward_cfg (v2.py:190-206). */
@@ -110,14 +144,17 @@ typedef struct zb_model {
   int32_t base_link, foot_links[2], undesired_links[10];
 } zb_model;
 
-/* Task / simulation constants: ZbotDirectEnvCfgV2 (v2.py:26-206) + solver parameters. */
+/* Task / simulation constants: ZbotDirectEnvCfgV2 (v2.py:26-206) or Zbot6SUpEnvCfg
+ * (standup.py:191-447) + solver parameters. Fields marked "standup" are ignored by the walking task. */
 typedef struct zb_task_cfg {
   float sim_dt;                /* 1/200 (v2.py:48) */
   int32_t decimation;          /* 4 (v2.py:40) */
   int32_t max_episode_length;  /* ceil(20 s / 0.02 s) = 1000 (v2.py:39) */
   float termination_height;    /* 0.22 (v2.py:44) */
-  float reward_scales[ZB_NUM_REWARD_TERMS]; /* weights x step_dt (v2.py:250-252) */
-  float terminal_penalty;      /* 20 (v2.py:380) */
+  float reward_scales[ZB_NUM_REWARD_TERMS]; /* walking: weights x step_dt (v2.py:250-252);
+                                              standup: weights, the kernel multiplies by step_dt
+                                              per term (standup.py:624) */
+  float terminal_penalty;      /* 20 (v2.py:380); standup 2 (standup.py:630) */
   float joint_speed_limit;     /* 1.0 (v2.py:243) */
   float gravity;               /* 9.81 */
   float friction;              /* 1.0 static = dynamic, multiply combine (v2.py:49-56,62-68) */
@@ -126,6 +163,16 @@ typedef struct zb_task_cfg {
   float baumgarte;             /* penetration correction per step (fraction) */
   int32_t solver_iterations;   /* PGS sweeps per substep */
   int32_t enable_self_collision;
+  int32_t task;                /* ZB_TASK_WALKING_V2 / ZB_TASK_STANDUP_V0 */
+  /* standup: reset_root_state_uniform pose ranges {lo, hi} of x, y, roll, yaw added to the
+   * default root pose (standup.py:159-175); pitch and z ranges are 0 there */
+  float reset_pose_range[4][2];
+  float center_z_init;         /* standup: center_z_last after a reset, 0.05 (standup.py:511,701) */
+  float center_z_drop;         /* standup: died when center_z_last - base z > this, 0.05 (638) */
+  int32_t center_z_period;     /* standup: center_z_last refresh when ep_len % period == period-1 (640) */
+  int32_t curriculum_steps;    /* standup: my_curriculum threshold on common_step_counter,
+                                  max_episode_length * 80 (standup.py:102); 0 = no curriculum */
+  float curriculum_scales[ZB_NUM_REWARD_TERMS]; /* standup: reward weights from curriculum stage 1 */
 } zb_task_cfg;
 
 typedef struct zb_sim* zb_handle;
@@ -143,7 +190,8 @@ int zb_num_envs(zb_handle h);
 int zb_reset(zb_handle h, const int32_t* env_ids, int n, void* stream);
 
 /* One policy step for all envs. actions: device float[N][6] (raw policy output);
- * obs: device float[N][23]; reward: float[N]; terminated/truncated: uint8[N] (torch.bool). */
+ * obs: device float[N][23] (standup: float[N][22]); reward: float[N]; terminated/truncated:
+ * uint8[N] (torch.bool). */
 int zb_step(zb_handle h, const float* actions, float* obs, float* reward, uint8_t* terminated,
             uint8_t* truncated, void* stream);
 
@@ -158,7 +206,8 @@ int zb_read_log(zb_handle h, float* term_means, int32_t* counts, void* stream);
  * unregisters. */
 int zb_set_log_buffers(zb_handle h, float* term_means, int32_t* counts);
 
-/* Persistent state, device float[ZB_STATE_DIM][N]. */
+/* Persistent state, device float[zb_state_dim(h)][N] (ZB_STATE_DIM / ZB_SU_STATE_DIM). */
+int zb_state_dim(zb_handle h);
 int zb_get_state(zb_handle h, float* dst, void* stream);
 int zb_set_state(zb_handle h, const float* src, void* stream);
 
@@ -167,6 +216,16 @@ int zb_set_state(zb_handle h, const float* src, void* stream);
  * and applied_torque (if != NULL) Isaac Lab's clipped PD estimate float[N][6]. */
 int zb_physics_substeps(zb_handle h, const float* targets, int nsub, float* net_force,
                         float* applied_torque, void* stream);
+
+/* Standup: per-link friction coefficients, device float[N][12] (link order of ZB_NUM_LINKS),
+ * e.g. the static friction sampled by randomize_rigid_body_material. Ground contacts use
+ * mu[link] * cfg.friction (the terrain's coefficient, multiply combine), self contacts
+ * mu[a] * mu[b]. A new handle starts at cfg.friction for every link. */
+int zb_set_link_friction(zb_handle h, const float* mu, void* stream);
+
+/* Standup: curriculum stage (0/1) and common_step_counter (zb_step calls). Host pointers;
+ * synchronises with the device. */
+int zb_read_curriculum(zb_handle h, int32_t* stage, int64_t* common_step_counter);
 
 /* Measurement: time the next `max_launches` zb_step_kernel launches with hipEvents recorded on
  * the launch stream right around the kernel (bench.py's roofline figure). zb_profile_end waits

@@ -50,6 +50,13 @@ def _load(double: bool = False):
     lib.zbo_obs_cache.argtypes = [C.c_int, _f, _f, _f, _f, _f, _f]
     lib.zbo_mdp_eval.argtypes = [C.c_int, C.POINTER(zm.ZbTaskCfg), _f, _f, _f, _f, _f, _f, _i, _f, _f, _f,
                                  _f, _f, _f, _f, _u8, _u8]
+    lib.zbo_state_dim.argtypes = [P]
+    lib.zbo_set_link_friction.argtypes = [P, _f]
+    lib.zbo_read_curriculum.argtypes = [P, C.POINTER(C.c_int32), C.POINTER(C.c_int64)]
+    lib.zbo_su_mdp_eval.argtypes = [C.c_int, C.POINTER(zm.ZbTaskCfg), C.c_int, _f, _f, _i, _f, _f, _f, _f, _u8, _u8]
+    lib.zbo_su_reset_pose.argtypes = [C.POINTER(zm.ZbModel), C.POINTER(zm.ZbTaskCfg), C.c_uint64, C.c_uint64, C.c_int,
+                                      _f, _f]
+    lib.zbo_su_pose_from_samples.argtypes = [C.POINTER(zm.ZbModel), C.c_int, _f, _f, _f]
     return lib
 
 
@@ -74,7 +81,10 @@ class OracleSim:
         self.lib = lib(double)
         self.cfg = cfg or zm.TaskCfg()
         self.n = num_envs
-        self._m = zm.pack_model()
+        self.obs_dim, self.state_dim = self.cfg.obs_dim, self.cfg.state_dim
+        self.num_terms = len(self.cfg.reward_terms)
+        standup = self.cfg.task == zm.TASK_STANDUP_V0
+        self._m = zm.pack_model(zm.standup_model() if standup else None)
         self._c = self.cfg.pack()
         if threads:
             self.lib.zbo_set_threads(threads)
@@ -94,7 +104,7 @@ class OracleSim:
             self.lib.zbo_reset(self.h, ids.ctypes.data_as(C.c_void_p), len(ids))
 
     def step(self, actions):
-        obs = np.zeros((self.n, zm.OBS_DIM), np.float32)
+        obs = np.zeros((self.n, self.obs_dim), np.float32)
         rew = np.zeros(self.n, np.float32)
         term = np.zeros(self.n, np.uint8)
         trunc = np.zeros(self.n, np.uint8)
@@ -102,7 +112,7 @@ class OracleSim:
         return obs, rew, term.astype(bool), trunc.astype(bool)
 
     def observe(self):
-        obs = np.zeros((self.n, zm.OBS_DIM), np.float32)
+        obs = np.zeros((self.n, self.obs_dim), np.float32)
         self.lib.zbo_observe(self.h, obs)
         return obs
 
@@ -110,10 +120,19 @@ class OracleSim:
         m = np.zeros(zm.NUM_TERMS, np.float32)
         c = np.zeros(2, np.int32)
         self.lib.zbo_read_log(self.h, m, c)
-        return m, c
+        return m[:self.num_terms], c
+
+    def set_link_friction(self, mu):
+        if self.lib.zbo_set_link_friction(self.h, f32(mu)) != 0:
+            raise ValueError("per-link friction is a standup-task state")
+
+    def read_curriculum(self):
+        st, n = C.c_int32(), C.c_int64()
+        self.lib.zbo_read_curriculum(self.h, C.byref(st), C.byref(n))
+        return int(st.value), int(n.value)
 
     def get_state(self):
-        st = np.zeros((zm.STATE_DIM, self.n), np.float32)
+        st = np.zeros((self.state_dim, self.n), np.float32)
         self.lib.zbo_get_state(self.h, st)
         return st
 
@@ -142,3 +161,40 @@ class OracleSim:
         o = np.zeros((self.n, 7), np.float32)
         self.lib.zbo_energy_momentum(self.h, o)
         return o
+
+
+def su_mdp_eval(cfg: zm.TaskCfg, stage: int, link_state, p_delta, ep_len, center_z_last, ep_sums):
+    """Stand-up _get_dones + _get_rewards on raw body_link_state_w inputs (zbo_su_mdp_eval)."""
+    n = len(ep_len)
+    c = cfg.pack()
+    czl = f32(center_z_last).copy()
+    sums = f32(ep_sums).copy()
+    rew = np.zeros(n, np.float32)
+    terms = np.zeros((n, zm.SU_NUM_TERMS), np.float32)
+    died = np.zeros(n, np.uint8)
+    tout = np.zeros(n, np.uint8)
+    lib().zbo_su_mdp_eval(n, C.byref(c), int(stage), f32(link_state), f32(p_delta),
+                          np.ascontiguousarray(ep_len, np.int32), czl, sums, rew, terms, died, tout)
+    return dict(reward=rew, terms=terms, died=died.astype(bool), time_out=tout.astype(bool), center_z_last=czl,
+                episode_sums=sums)
+
+
+def su_reset_pose(cfg: zm.TaskCfg, seed: int, ctr: int, n: int):
+    """Root (pos [n,3], quat [n,4]) of reset_root_state_uniform at RNG position ctr."""
+    m = zm.pack_model(zm.standup_model())
+    c = cfg.pack()
+    pos = np.zeros((n, 3), np.float32)
+    quat = np.zeros((n, 4), np.float32)
+    lib().zbo_su_reset_pose(C.byref(m), C.byref(c), seed, ctr, n, pos, quat)
+    return pos, quat
+
+
+def su_pose_from_samples(samples):
+    """Root (pos [n,3], quat [n,4]) from reset_root_state_uniform samples [n,4] = x, y, roll, yaw."""
+    m = zm.pack_model(zm.standup_model())
+    smp = f32(samples)
+    n = len(smp)
+    pos = np.zeros((n, 3), np.float32)
+    quat = np.zeros((n, 4), np.float32)
+    lib().zbo_su_pose_from_samples(C.byref(m), n, smp, pos, quat)
+    return pos, quat

@@ -143,6 +143,8 @@ typedef struct {
 
 typedef struct {
   real p_delta[ND], actions[ND];
+  real center_z_last;                 /* standup only (standup.py:511) */
+  real mu[NL];                        /* standup only: per-link friction (DR) */
   real feet_down_pos[2][3], feet_step_len[2], feet_f_last[2];
   real heading_sum, yerr_sum;
   real feet_fz_hist[ZB_HIST][2], undes_fmax_hist[ZB_HIST];
@@ -158,6 +160,8 @@ struct zbo_sim {
   zb_task_cfg c;
   int n;
   uint64_t seed, call_counter; /* zb_step / zb_reset calls so far (RNG stream position) */
+  uint64_t steps;               /* common_step_counter (zb_step calls) */
+  int stage;                    /* standup curriculum stage */
   env_t* env;
   float log_means[ZB_NUM_REWARD_TERMS];
   int32_t log_counts[2];
@@ -482,8 +486,10 @@ typedef struct {
   real applied_torque[ND]; /* Isaac Lab ImplicitActuator estimate at substep start */
 } substep_out_t;
 
+/* mu_link: per-link friction (standup DR; contact coefficient = product, the ground's being
+ * cfg->friction), or NULL for cfg->friction on every contact */
 static void substep(const mdl_t* m, const zb_task_cfg* cfg, phys_t* s, const real target[ND],
-                    substep_out_t* out) {
+                    const real* mu_link, substep_out_t* out) {
   const real dt = cfg->sim_dt;
   kin_t k;
   fk(m, s, &k);
@@ -602,12 +608,14 @@ static void substep(const mdl_t* m, const zb_task_cfg* cfg, phys_t* s, const rea
   detect(m, cfg, &k, s->root_pos[2], &CL);
   int nc = CL.n;
   real Y[NC_MAX][3][NV];
-  real invm[NC_MAX][3], vmin[NC_MAX], lam[NC_MAX][3], c01[NC_MAX], c02[NC_MAX];
+  real invm[NC_MAX][3], vmin[NC_MAX], lam[NC_MAX][3], c01[NC_MAX], c02[NC_MAX], muc[NC_MAX];
   real dirs[NC_MAX][3][3];
   for (int c = 0; c < nc; ++c) {
     const contact_t* ct = &CL.c[c];
     for (int a = 0; a < 3; ++a) dirs[c][0][a] = ct->n[a];
     tangents(ct->n, dirs[c][1], dirs[c][2]);
+    /* friction combine mode "multiply" (link x ground, link x link) */
+    muc[c] = mu_link ? mu_link[ct->la] * (ct->lb >= 0 ? mu_link[ct->lb] : (real)cfg->friction) : (real)cfg->friction;
     for (int r = 0; r < 3; ++r) {
       real J[NV], Jb[NV];
       jac_row(&k, m->link_body[ct->la], ct->x, dirs[c][r], J);
@@ -633,9 +641,9 @@ static void substep(const mdl_t* m, const zb_task_cfg* cfg, phys_t* s, const rea
   /* Gauss-Seidel over contacts; the three row dots of a contact use the same w, the normal
    * update enters the tangent velocities through the cross terms c01 = Y1.Y0, c02 = Y2.Y0
    * (algebraically the sequential normal-then-friction update). */
-  const real mu = cfg->friction;
   for (int it = 0; it < cfg->solver_iterations; ++it) {
     for (int c = 0; c < nc; ++c) {
+      const real mu = muc[c];
       real vn = 0, v1 = 0, v2 = 0;
       for (int a = 0; a < NV; ++a) { vn += Y[c][0][a] * w[a]; v1 += Y[c][1][a] * w[a]; v2 += Y[c][2][a] * w[a]; }
       real ln = lam[c][0] + (vmin[c] - vn) * invm[c][0];
@@ -940,6 +948,204 @@ static void write_obs(const mdl_t* m, const env_t* e, float* obs) {
   obs[22] = 1.0f; /* joint_speed_limit (v2.py:243) */
 }
 
+
+/* ========================================================================= stand-up task
+ * zbot-6b-standup-v0: reference source/zbot/zbot/tasks/zbot6b_direct/zbot_direct_6_standup_env_v0.py
+ * (standup.py). Same physics with per-link friction (startup material randomisation), rewards
+ * from post-step link states, died on a 5 cm height drop per 50 steps, in-step resets to a
+ * random root pose (reset_root_state_uniform), curriculum on common_step_counter. */
+
+static inline real su_u01(uint64_t h) { return (real)((float)(h >> 40) * (1.0f / 16777216.0f)); }
+
+static void su_pose_from_samples(const mdl_t* m, const real r[4], phys_t* p);
+
+/* reset_root_state_uniform (standup.py:33-97) at RNG position ctr (same draws as the kernel) */
+static void su_reset_pose(const mdl_t* m, const zb_task_cfg* cfg, uint64_t seed, uint64_t ctr, int i, phys_t* p) {
+  const uint64_t h = zb_hash64(seed ^ zb_hash64(ctr * 0x100000001B3ull + (uint64_t)i));
+  real r[4];
+  for (int k = 0; k < 4; ++k) {
+    const real u = su_u01(zb_hash64(h + 0x632BE59BD9B4E019ull * (uint64_t)(k + 1)));
+    r[k] = u * ((real)cfg->reset_pose_range[k][1] - (real)cfg->reset_pose_range[k][0]) + (real)cfg->reset_pose_range[k][0];
+  }
+  su_pose_from_samples(m, r, p);
+}
+
+/* root pose from the samples (x, y, roll, yaw) of reset_root_state_uniform */
+static void su_pose_from_samples(const mdl_t* m, const real r[4], phys_t* p) {
+  /* quat_from_euler_xyz(roll, pitch = 0, yaw) (Isaac Lab math: extrinsic X then Z) */
+  const real cr = (real)cos(0.5 * (double)r[2]), sr = (real)sin(0.5 * (double)r[2]);
+  const real cy = (real)cos(0.5 * (double)r[3]), sy = (real)sin(0.5 * (double)r[3]);
+  const real dq[4] = {cy * cr, cy * sr, sy * sr, sy * cr};
+  real qn[4];
+  q_mul(dq, m->root_quat0, qn); /* world-frame rotation: delta * default (standup.py:87-88) */
+  q_normalize(qn);
+  for (int a = 0; a < 4; ++a) p->root_quat[a] = qn[a];
+  p->root_pos[0] = m->root_pos0[0] + r[0];
+  p->root_pos[1] = m->root_pos0[1] + r[1];
+  p->root_pos[2] = m->root_pos0[2];
+  for (int a = 0; a < 3; ++a) { p->root_linvel[a] = 0; p->root_angvel[a] = 0; }
+  for (int j = 0; j < ND; ++j) { p->jq[j] = m->jq0[j]; p->jqd[j] = 0; }
+}
+
+/* _reset_idx (standup.py:645-703) minus the log: pose event, joints default, p_delta / actions
+ * zero, center_z_last 0.05, ep_len 0, episode sums zero; the friction (startup event) stays */
+static void su_reset_env(const mdl_t* m, const zb_task_cfg* cfg, uint64_t seed, uint64_t ctr, int i, env_t* e) {
+  su_reset_pose(m, cfg, seed, ctr, i, &e->ph);
+  mdp_t* md = &e->md;
+  for (int j = 0; j < ND; ++j) { md->p_delta[j] = 0; md->actions[j] = 0; }
+  md->center_z_last = cfg->center_z_init;
+  md->ep_len = 0;
+  for (int t = 0; t < ZB_SU_NUM_REWARD_TERMS; ++t) md->ep_sums[t] = 0;
+}
+
+/* the stand-up MDP's reads of body_link_state_w: link z heights (4 = a3, 6 = base, 8 = a5),
+ * link-origin z velocities (5 = b3, 6), feet link quaternions, base link quaternion */
+typedef struct { real z4, z6, z8, vz5, vz6, feet_quat[2][4], base_quat[4]; } su_links_t;
+
+static void su_links(const mdl_t* m, const phys_t* s, su_links_t* o) {
+  kin_t k;
+  fk(m, s, &k);
+  real V[NB][6], p[3], q[4];
+  body_vel(&k, s, V);
+  link_pose(m, &k, 4, p, q); o->z4 = p[2] + s->root_pos[2];
+  link_pose(m, &k, 8, p, q); o->z8 = p[2] + s->root_pos[2];
+  link_pose(m, &k, 6, p, o->base_quat); o->z6 = p[2] + s->root_pos[2];
+  link_pose(m, &k, m->foot_links[0], p, o->feet_quat[0]);
+  link_pose(m, &k, m->foot_links[1], p, o->feet_quat[1]);
+  const int ls[2] = {5, 6};
+  real* vz[2] = {&o->vz5, &o->vz6};
+  for (int t = 0; t < 2; ++t) {
+    const int l = ls[t], b = m->link_body[l];
+    real x[3], v[3];
+    m3_v(k.R[b], m->link_pos[l], x); /* link frame origin: body_link_lin_vel_w */
+    for (int a = 0; a < 3; ++a) x[a] += k.p[b][a];
+    point_vel(V[b], x, v);
+    *vz[t] = v[2];
+  }
+}
+
+/* _get_dones (634-643) + _get_rewards (620-632; terms upward_2 843-856, shape_symmetry 782-789,
+ * feet_downward 735-745, feet_downward_4 827-840). ep_len is after the += 1. Updates
+ * center_z_last and the episode sums; returns the reward. */
+static real su_mdp_eval(const zb_task_cfg* cfg, int stage, const su_links_t* L, const real pdel[ND], int32_t ep_len,
+                        real* center_z_last, real ep_sums[ZB_SU_NUM_REWARD_TERMS], real terms[ZB_SU_NUM_REWARD_TERMS],
+                        int* died_out, int* tout_out) {
+  static const real zax[3] = {0, 0, 1}, mzax[3] = {0, 0, -1};
+  const int time_out = ep_len >= cfg->max_episode_length - 1;
+  const int died = (*center_z_last - L->z6) > (real)cfg->center_z_drop;
+  if (ep_len % cfg->center_z_period == cfg->center_z_period - 1) *center_z_last = L->z6;
+  real fz[2][3];
+  quat_apply(L->feet_quat[0], zax, fz[0]);
+  quat_apply(L->feet_quat[1], mzax, fz[1]);
+  real r[ZB_SU_NUM_REWARD_TERMS];
+  {
+    const real rh = L->z6 + (real)0.5 * L->z4 + (real)0.5 * L->z8 - (real)0.1f;
+    real up = L->z6 < (real)0.22f ? rh + (real)0.5 * L->vz6 + (real)0.5 * L->vz5 : (real)1.35f;
+    if ((fz[0][2] < (real)0.5 || fz[1][2] < (real)0.5) && L->z6 > (real)0.1f) up = (real)-5.0 * up;
+    r[ZB_SU_R_UPWARD_2] = up;
+  }
+  r[ZB_SU_R_SHAPE_SYMMETRY] = (real)(fabs((double)(pdel[0] + pdel[5])) + fabs((double)(pdel[1] + pdel[4])) +
+                                     fabs((double)(pdel[2] + pdel[3])));
+  {
+    real sd = 0;
+    for (int f = 0; f < 2; ++f) {
+      const real d[3] = {fz[f][0], fz[f][1], fz[f][2] - 1};
+      sd += sqrtr(v3_dot(d, d));
+    }
+    r[ZB_SU_R_FEET_DOWNWARD] = sd;
+  }
+  r[ZB_SU_R_FEET_DOWNWARD_4] = L->z6 < (real)0.15f ? fz[0][2] + fz[1][2] : (real)1.6f;
+  const real step_dt = (real)(cfg->sim_dt * (float)cfg->decimation);
+  real rew = 0;
+  for (int t = 0; t < ZB_SU_NUM_REWARD_TERMS; ++t) {
+    const real w = stage ? (real)cfg->curriculum_scales[t] : (real)cfg->reward_scales[t];
+    const real v = (r[t] * w) * step_dt;
+    terms[t] = v;
+    rew += v;
+    ep_sums[t] += v;
+  }
+  if (died) rew -= cfg->terminal_penalty;
+  *died_out = died;
+  *tout_out = time_out;
+  return rew;
+}
+
+static void su_write_obs(const mdl_t* m, const env_t* e, float* obs) {
+  su_links_t L;
+  su_links(m, &e->ph, &L);
+  for (int a = 0; a < 4; ++a) obs[a] = (float)L.base_quat[a];
+  for (int j = 0; j < ND; ++j) {
+    obs[4 + j] = (float)(e->ph.jq[j] - m->jq0[j]);
+    obs[10 + j] = (float)e->ph.jqd[j];
+    obs[16 + j] = (float)e->md.actions[j];
+  }
+}
+
+static real su_step_env(const mdl_t* m, const zb_task_cfg* cfg, int stage, uint64_t seed, uint64_t ctr, int i,
+                        env_t* e, const float* action, float* obs, int* died, int* tout,
+                        real acc[ZB_SU_NUM_REWARD_TERMS]) {
+  mdp_t* md = &e->md;
+  real act[ND], target[ND];
+  const real step_dt = (real)(cfg->sim_dt * (float)cfg->decimation);
+  for (int j = 0; j < ND; ++j) { /* _pre_physics_step mode 1 (standup.py:538-551) */
+    act[j] = (real)tanh((double)action[j]);
+    real pd = md->p_delta[j] + (real)PI_R * act[j] * cfg->joint_speed_limit * step_dt;
+    md->p_delta[j] = clampr(pd, -(real)PI_R, (real)PI_R);
+    target[j] = md->p_delta[j] + m->jq0[j];
+  }
+  substep_out_t so;
+  for (int k = 0; k < cfg->decimation; ++k) substep(m, cfg, &e->ph, target, md->mu, &so);
+  md->ep_len += 1;
+  for (int j = 0; j < ND; ++j) md->actions[j] = act[j];
+  su_links_t L;
+  su_links(m, &e->ph, &L);
+  real terms[ZB_SU_NUM_REWARD_TERMS];
+  real rew = su_mdp_eval(cfg, stage, &L, md->p_delta, md->ep_len, &md->center_z_last, md->ep_sums, terms, died, tout);
+  if (*died || *tout) {
+    /* Episode_Reward/<term> = mean over reset envs of sum / max(ep_len * step_dt, step_dt) (653-659) */
+    real dur = (real)md->ep_len * step_dt;
+    if (dur < step_dt) dur = step_dt;
+    for (int t = 0; t < ZB_SU_NUM_REWARD_TERMS; ++t) acc[t] += md->ep_sums[t] / dur;
+    su_reset_env(m, cfg, seed, ctr, i, e);
+  }
+  su_write_obs(m, e, obs);
+  return rew;
+}
+
+static void su_pack_env(const env_t* e, float* st, int n, int i) {
+#define PUT(off, val) st[(size_t)(off) * n + i] = (float)(val)
+  for (int a = 0; a < 3; ++a) { PUT(ZB_S_ROOT_POS + a, e->ph.root_pos[a]); PUT(ZB_S_ROOT_LINVEL + a, e->ph.root_linvel[a]); PUT(ZB_S_ROOT_ANGVEL + a, e->ph.root_angvel[a]); }
+  for (int a = 0; a < 4; ++a) PUT(ZB_S_ROOT_QUAT + a, e->ph.root_quat[a]);
+  for (int j = 0; j < ND; ++j) {
+    PUT(ZB_S_JOINT_POS + j, e->ph.jq[j]); PUT(ZB_S_JOINT_VEL + j, e->ph.jqd[j]);
+    PUT(ZB_SU_P_DELTA + j, e->md.p_delta[j]); PUT(ZB_SU_ACTIONS + j, e->md.actions[j]);
+  }
+  PUT(ZB_SU_CENTER_Z_LAST, e->md.center_z_last);
+  PUT(ZB_SU_EP_LEN, e->md.ep_len);
+  for (int t = 0; t < ZB_SU_NUM_REWARD_TERMS; ++t) PUT(ZB_SU_EP_SUMS + t, e->md.ep_sums[t]);
+  for (int l = 0; l < NL; ++l) PUT(ZB_SU_LINK_MU + l, e->md.mu[l]);
+#undef PUT
+}
+static void su_unpack_env(env_t* e, const float* st, int n, int i) {
+#define GET(off) ((real)st[(size_t)(off) * n + i])
+  for (int a = 0; a < 3; ++a) { e->ph.root_pos[a] = GET(ZB_S_ROOT_POS + a); e->ph.root_linvel[a] = GET(ZB_S_ROOT_LINVEL + a); e->ph.root_angvel[a] = GET(ZB_S_ROOT_ANGVEL + a); }
+  for (int a = 0; a < 4; ++a) e->ph.root_quat[a] = GET(ZB_S_ROOT_QUAT + a);
+  for (int j = 0; j < ND; ++j) {
+    e->ph.jq[j] = GET(ZB_S_JOINT_POS + j); e->ph.jqd[j] = GET(ZB_S_JOINT_VEL + j);
+    e->md.p_delta[j] = GET(ZB_SU_P_DELTA + j); e->md.actions[j] = GET(ZB_SU_ACTIONS + j);
+  }
+  e->md.center_z_last = GET(ZB_SU_CENTER_Z_LAST);
+  e->md.ep_len = (int32_t)lrint((double)st[(size_t)ZB_SU_EP_LEN * n + i]);
+  for (int t = 0; t < ZB_SU_NUM_REWARD_TERMS; ++t) e->md.ep_sums[t] = GET(ZB_SU_EP_SUMS + t);
+  for (int l = 0; l < NL; ++l) e->md.mu[l] = GET(ZB_SU_LINK_MU + l);
+#undef GET
+}
+
+static void su_curriculum(zbo_sim* s, int nreset) { /* my_curriculum (standup.py:99-111) */
+  if (s->c.curriculum_steps > 0 && s->stage == 0 && nreset > 0 && s->steps >= (uint64_t)s->c.curriculum_steps)
+    s->stage = 1;
+}
+
 /* ========================================================================= public API */
 #ifdef _OPENMP
 #include <omp.h>
@@ -954,8 +1160,14 @@ zbo_sim* zbo_create(const zb_model* model, const zb_task_cfg* cfg, int num_envs,
   s->env = (env_t*)calloc((size_t)num_envs, sizeof(env_t));
   for (int i = 0; i < num_envs; ++i) {
     memset(&s->env[i], 0, sizeof(env_t));
-    reset_env(&s->m, &s->env[i]);
+    if (cfg->task == ZB_TASK_STANDUP_V0) {
+      for (int l = 0; l < NL; ++l) s->env[i].md.mu[l] = cfg->friction;
+      su_reset_env(&s->m, cfg, seed, 0, i, &s->env[i]); /* construction draws at RNG position 0 */
+    } else {
+      reset_env(&s->m, &s->env[i]);
+    }
   }
+  if (cfg->task == ZB_TASK_STANDUP_V0) s->call_counter = 1;
   return s;
 }
 
@@ -978,6 +1190,29 @@ int zbo_set_threads(int n) {
 int zbo_reset(zbo_sim* s, const int32_t* env_ids, int n) {
   int all = env_ids == NULL || n == s->n;
   int cnt = env_ids ? n : s->n;
+  if (s->c.task == ZB_TASK_STANDUP_V0) {
+    const real step_dt = (real)(s->c.sim_dt * (float)s->c.decimation);
+    double accl[ZB_SU_NUM_REWARD_TERMS] = {0, 0, 0, 0};
+    const uint64_t ctr = s->call_counter;
+    for (int i = 0; i < cnt; ++i) {
+      int e = env_ids ? env_ids[i] : i;
+      real dur = (real)s->env[e].md.ep_len * step_dt;
+      if (dur < step_dt) dur = step_dt;
+      for (int t = 0; t < ZB_SU_NUM_REWARD_TERMS; ++t) accl[t] += s->env[e].md.ep_sums[t] / dur;
+      su_reset_env(&s->m, &s->c, s->seed, ctr, e, &s->env[e]);
+    }
+    for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t)
+      s->log_means[t] = (t < ZB_SU_NUM_REWARD_TERMS && cnt) ? (float)(accl[t] / cnt) : 0.f;
+    s->log_counts[0] = s->log_counts[1] = 0;
+    s->call_counter++;
+    su_curriculum(s, cnt);
+    if (all)
+      for (int e = 0; e < s->n; ++e) {
+        uint64_t h = zb_hash64(s->seed ^ zb_hash64(ctr * 0x100000001B3ull + (uint64_t)e));
+        s->env[e].md.ep_len = (int32_t)(h % (uint64_t)s->c.max_episode_length);
+      }
+    return 0;
+  }
   for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) s->log_means[t] = 0;
   for (int i = 0; i < cnt; ++i) {
     int e = env_ids ? env_ids[i] : i;
@@ -999,7 +1234,53 @@ int zbo_reset(zbo_sim* s, const int32_t* env_ids, int n) {
 }
 
 int zbo_observe(zbo_sim* s, float* obs) {
+  if (s->c.task == ZB_TASK_STANDUP_V0) {
+    for (int e = 0; e < s->n; ++e) su_write_obs(&s->m, &s->env[e], obs + (size_t)e * ZB_SU_OBS_DIM);
+    return 0;
+  }
   for (int e = 0; e < s->n; ++e) write_obs(&s->m, &s->env[e], obs + (size_t)e * ZB_OBS_DIM);
+  return 0;
+}
+
+static int su_step(zbo_sim* s, const float* actions, float* obs, float* reward, uint8_t* terminated,
+                   uint8_t* truncated) {
+  double acc[ZB_SU_NUM_REWARD_TERMS] = {0, 0, 0, 0};
+  int nreset = 0, nterm = 0, ntout = 0;
+  const uint64_t ctr = s->call_counter;
+  const int stage = s->stage;
+  s->steps++; /* DirectRLEnv.step: common_step_counter += 1 before dones / rewards / resets */
+#pragma omp parallel
+  {
+    real acc_l[ZB_SU_NUM_REWARD_TERMS] = {0, 0, 0, 0};
+    int nr = 0, nt = 0, no = 0;
+#pragma omp for schedule(static)
+    for (int e = 0; e < s->n; ++e) {
+      int died = 0, tout = 0;
+      reward[e] = (float)su_step_env(&s->m, &s->c, stage, s->seed, ctr, e, &s->env[e], actions + (size_t)e * ZB_ACT_DIM,
+                                     obs + (size_t)e * ZB_SU_OBS_DIM, &died, &tout, acc_l);
+      terminated[e] = (uint8_t)died;
+      truncated[e] = (uint8_t)tout;
+      nr += died || tout; nt += died; no += tout;
+    }
+#pragma omp critical
+    {
+      for (int t = 0; t < ZB_SU_NUM_REWARD_TERMS; ++t) acc[t] += acc_l[t];
+      nreset += nr; nterm += nt; ntout += no;
+    }
+  }
+  if (nreset > 0) {
+    for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t)
+      s->log_means[t] = t < ZB_SU_NUM_REWARD_TERMS ? (float)(acc[t] / nreset) : 0.f;
+    s->log_counts[0] = nterm;
+    s->log_counts[1] = ntout;
+  }
+  s->call_counter++;
+  su_curriculum(s, nreset);
+  if (nreset == s->n)
+    for (int e = 0; e < s->n; ++e) {
+      uint64_t h = zb_hash64(s->seed ^ zb_hash64(ctr * 0x100000001B3ull + (uint64_t)e));
+      s->env[e].md.ep_len = (int32_t)(h % (uint64_t)s->c.max_episode_length);
+    }
   return 0;
 }
 
@@ -1022,7 +1303,7 @@ static real step_env(const mdl_t* m, const zb_task_cfg* cfg, env_t* e, const flo
   cache_from_phys(m, &e->ph, &pre);
   /* physics */
   substep_out_t so;
-  for (int k = 0; k < cfg->decimation; ++k) substep(m, cfg, &e->ph, target, &so);
+  for (int k = 0; k < cfg->decimation; ++k) substep(m, cfg, &e->ph, target, NULL, &so);
   sensor_update(m, cfg, md, so.net_force);
   md->ep_len += 1;
   /* post-step reads */
@@ -1062,6 +1343,8 @@ static real step_env(const mdl_t* m, const zb_task_cfg* cfg, env_t* e, const flo
 }
 
 int zbo_step(zbo_sim* s, const float* actions, float* obs, float* reward, uint8_t* terminated, uint8_t* truncated) {
+  if (s->c.task == ZB_TASK_STANDUP_V0) return su_step(s, actions, obs, reward, terminated, truncated);
+  s->steps++;
   real acc[ZB_NUM_REWARD_TERMS];
   for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) acc[t] = 0;
   int nreset = 0, nterm = 0, ntout = 0;
@@ -1166,11 +1449,30 @@ static void unpack_env(env_t* e, const float* st, int n, int i) {
 }
 
 int zbo_get_state(zbo_sim* s, float* dst) {
-  for (int e = 0; e < s->n; ++e) pack_env(&s->env[e], dst, s->n, e);
+  for (int e = 0; e < s->n; ++e)
+    if (s->c.task == ZB_TASK_STANDUP_V0) su_pack_env(&s->env[e], dst, s->n, e);
+    else pack_env(&s->env[e], dst, s->n, e);
   return 0;
 }
 int zbo_set_state(zbo_sim* s, const float* src) {
-  for (int e = 0; e < s->n; ++e) unpack_env(&s->env[e], src, s->n, e);
+  for (int e = 0; e < s->n; ++e)
+    if (s->c.task == ZB_TASK_STANDUP_V0) su_unpack_env(&s->env[e], src, s->n, e);
+    else unpack_env(&s->env[e], src, s->n, e);
+  return 0;
+}
+int zbo_state_dim(zbo_sim* s) { return s->c.task == ZB_TASK_STANDUP_V0 ? ZB_SU_STATE_DIM : ZB_STATE_DIM; }
+
+/* standup: per-link friction [n][12] */
+int zbo_set_link_friction(zbo_sim* s, const float* mu) {
+  if (s->c.task != ZB_TASK_STANDUP_V0) return -1;
+  for (int e = 0; e < s->n; ++e)
+    for (int l = 0; l < NL; ++l) s->env[e].md.mu[l] = mu[(size_t)e * NL + l];
+  return 0;
+}
+
+int zbo_read_curriculum(zbo_sim* s, int32_t* stage, int64_t* steps) {
+  if (stage) *stage = s->stage;
+  if (steps) *steps = (int64_t)s->steps;
   return 0;
 }
 
@@ -1181,7 +1483,8 @@ int zbo_physics_substeps(zbo_sim* s, const float* targets, int nsub, float* net_
     for (int j = 0; j < ND; ++j) tg[j] = targets[(size_t)e * ND + j];
     substep_out_t so;
     memset(&so, 0, sizeof(so));
-    for (int k = 0; k < nsub; ++k) substep(&s->m, &s->c, &s->env[e].ph, tg, &so);
+    const real* mu = s->c.task == ZB_TASK_STANDUP_V0 ? s->env[e].md.mu : NULL;
+    for (int k = 0; k < nsub; ++k) substep(&s->m, &s->c, &s->env[e].ph, tg, mu, &so);
     if (net_force)
       for (int l = 0; l < NL; ++l)
         for (int a = 0; a < 3; ++a) net_force[((size_t)e * NL + l) * 3 + a] = (float)so.net_force[l][a];
@@ -1368,6 +1671,69 @@ int zbo_energy_momentum(zbo_sim* s, float* out) {
     v3_cross(ph->root_pos, P, rp);
     out[(size_t)e * 7] = (float)E;
     for (int a = 0; a < 3; ++a) { out[(size_t)e * 7 + 1 + a] = (float)P[a]; out[(size_t)e * 7 + 4 + a] = (float)(Lm[a] + rp[a]); }
+  }
+  return 0;
+}
+
+/* Stand-up MDP on raw Isaac-Lab-shaped inputs (golden vectors from the reference's own
+ * Zbot6SUpEnv code, tests/test_oracle_standup.py): link_state [n][12][13] = body_link_state_w
+ * (pos 3, quat 4, lin vel 3, ang vel 3), p_delta [n][6] after _pre_physics_step, ep_len [n]
+ * after the += 1, center_z_last [n] in/out, ep_sums [n][4] in/out. */
+int zbo_su_mdp_eval(int n, const zb_task_cfg* cfg, int stage, const float* link_state, const float* p_delta,
+                    const int32_t* ep_len, float* center_z_last, float* ep_sums, float* reward, float* terms,
+                    uint8_t* died, uint8_t* time_out) {
+  for (int e = 0; e < n; ++e) {
+    const float* ls = link_state + (size_t)e * NL * 13;
+    su_links_t L;
+    L.z4 = ls[4 * 13 + 2]; L.z6 = ls[6 * 13 + 2]; L.z8 = ls[8 * 13 + 2];
+    L.vz5 = ls[5 * 13 + 9]; L.vz6 = ls[6 * 13 + 9];
+    for (int a = 0; a < 4; ++a) {
+      L.feet_quat[0][a] = ls[0 * 13 + 3 + a];
+      L.feet_quat[1][a] = ls[11 * 13 + 3 + a];
+      L.base_quat[a] = ls[6 * 13 + 3 + a];
+    }
+    real pd[ND], sums[ZB_SU_NUM_REWARD_TERMS], tr[ZB_SU_NUM_REWARD_TERMS];
+    for (int j = 0; j < ND; ++j) pd[j] = p_delta[(size_t)e * ND + j];
+    for (int t = 0; t < ZB_SU_NUM_REWARD_TERMS; ++t) sums[t] = ep_sums[(size_t)e * ZB_SU_NUM_REWARD_TERMS + t];
+    real czl = center_z_last[e];
+    int d = 0, to = 0;
+    reward[e] = (float)su_mdp_eval(cfg, stage, &L, pd, ep_len[e], &czl, sums, tr, &d, &to);
+    center_z_last[e] = (float)czl;
+    for (int t = 0; t < ZB_SU_NUM_REWARD_TERMS; ++t) {
+      terms[(size_t)e * ZB_SU_NUM_REWARD_TERMS + t] = (float)tr[t];
+      ep_sums[(size_t)e * ZB_SU_NUM_REWARD_TERMS + t] = (float)sums[t];
+    }
+    died[e] = (uint8_t)d;
+    time_out[e] = (uint8_t)to;
+  }
+  return 0;
+}
+
+/* reset_root_state_uniform draws (root pos [n][3], quat [n][4]) at RNG position ctr */
+int zbo_su_reset_pose(const zb_model* model, const zb_task_cfg* cfg, uint64_t seed, uint64_t ctr, int n, float* pos,
+                      float* quat) {
+  mdl_t m;
+  load_mdl(model, &m);
+  for (int e = 0; e < n; ++e) {
+    phys_t p;
+    su_reset_pose(&m, cfg, seed, ctr, e, &p);
+    for (int a = 0; a < 3; ++a) pos[(size_t)e * 3 + a] = (float)p.root_pos[a];
+    for (int a = 0; a < 4; ++a) quat[(size_t)e * 4 + a] = (float)p.root_quat[a];
+  }
+  return 0;
+}
+
+/* root pose from reset_root_state_uniform samples [n][4] = (x, y, roll, yaw) */
+int zbo_su_pose_from_samples(const zb_model* model, int n, const float* samples, float* pos, float* quat) {
+  mdl_t m;
+  load_mdl(model, &m);
+  for (int e = 0; e < n; ++e) {
+    phys_t p;
+    real r[4];
+    for (int k = 0; k < 4; ++k) r[k] = samples[(size_t)e * 4 + k];
+    su_pose_from_samples(&m, r, &p);
+    for (int a = 0; a < 3; ++a) pos[(size_t)e * 3 + a] = (float)p.root_pos[a];
+    for (int a = 0; a < 4; ++a) quat[(size_t)e * 4 + a] = (float)p.root_quat[a];
   }
   return 0;
 }

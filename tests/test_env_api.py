@@ -71,6 +71,32 @@ def test_registry_matches_reference_registration():
     assert d["algorithm"]["desired_kl"] == 0.01 and d["algorithm"]["num_mini_batches"] == 4
 
 
+def test_standup_registration_and_cfg():
+    """zbot-6b-standup-v0 (reference __init__.py:111-119, Zbot6SUpEnvCfg standup.py:191-447)."""
+    from zbot_lab_amd.rl import Zbot6SUpEnvPPOCfg
+    s = spec("zbot-6b-standup-v0")
+    assert s.entry_point.endswith("Zbot6SUpEnv")
+    cfg = load_cfg("zbot-6b-standup-v0")
+    assert cfg.episode_length_s == 6.0 and cfg.observation_space == 22 and cfg.action_space == 6
+    assert list(cfg.reward_cfg["reward_scales"]) == zm.SU_REWARD_TERMS
+    pm = cfg.events.physics_material.params
+    assert pm["static_friction_range"] == (0.6, 1.0) and pm["num_buckets"] == 64
+    t = cfg.task_cfg()
+    assert t.task == zm.TASK_STANDUP_V0 and t.max_episode_length == 300 and t.terminal_penalty == 2.0
+    c = t.pack()
+    assert c.curriculum_steps == 24000 and c.task == 1
+    assert list(c.reward_scales[:4]) == [10.0, -1.0, -1.0, 0.0]       # weights; x step_dt in the kernel
+    assert list(c.curriculum_scales[:4]) == [10.0, -2.0, -1.0, 2.0]
+    np.testing.assert_allclose(np.array(c.reset_pose_range), [[-0.5, 0.5], [-0.5, 0.5], [-0.7854, 0.7854],
+                                                              [-3.14, 3.14]], rtol=1e-6)
+    cfg.events.my_curric = None                                       # play-script variant: no curriculum
+    assert cfg.task_cfg().pack().curriculum_steps == 0
+    agent = load_cfg("zbot-6b-standup-v0", "rsl_rl_cfg_entry_point")
+    assert isinstance(agent, Zbot6SUpEnvPPOCfg)
+    assert agent.to_dict()["policy"]["actor_hidden_dims"] == [256, 256, 128]
+    assert agent.experiment_name == "zbot_6b_flat_direct_standup"
+
+
 def test_vecenv_wrapper_contract():
     env = FakeEnv()
     w = RslRlVecEnvWrapper(env, clip_actions=1.0)

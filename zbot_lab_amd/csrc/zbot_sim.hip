@@ -143,6 +143,14 @@ __device__ __forceinline__ float tanh_r(float x) {
   return copysignf(1.f - 2.f * __builtin_amdgcn_rcpf(e + 1.f), x);
 }
 
+// device-side counters of one handle
+struct Counters {
+  uint64_t calls;  // zb_step + zb_reset calls (RNG stream position of resets)
+  uint64_t steps;  // zb_step calls (common_step_counter)
+  int32_t stage;   // curriculum stage (standup my_curriculum)
+  int32_t pad;
+};
+
 __host__ __device__ __forceinline__ uint64_t hash64(uint64_t x) {
   x += 0x9E3779B97F4A7C15ull;
   x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -449,8 +457,9 @@ __device__ __forceinline__ int xcd_block(int b, int nb) {
 constexpr int LINK4 = 10;
 constexpr int NPAIR = (NL - 1) * (NL - 2) / 2;  // non-adjacent link pairs (55), checked by zb_create
 constexpr int PAIRS_PER_LANE = (NPAIR + TL - 1) / TL;
-constexpr int DFLT_OFF = NL * LINK4 + (NPAIR + 3) / 4;  // default-pose feet positions, base quat
-constexpr int JT_OFF = DFLT_OFF + 3;  // joints: {jpr}, {jpp}, {jcp}, {jcr}, {a_local = R(jpr) z}
+// default pose: feet positions, base quat, base quat relative to the root (zb_derive_kernel)
+constexpr int DFLT_OFF = NL * LINK4 + (NPAIR + 3) / 4;
+constexpr int JT_OFF = DFLT_OFF + 4;  // joints: {jpr}, {jpp}, {jcp}, {jcr}, {a_local = R(jpr) z}
 constexpr int BT_OFF = JT_OFF + ND * 5;  // bodies: {com, mass}, {Ixx, Iyy, Izz, Ixy}, {Ixz, Iyz, 0, 0}
 constexpr int LNK4 = BT_OFF + NB * 3;
 
@@ -462,7 +471,7 @@ constexpr int NCAND = NL * 4 + NSELF;
 
 // LDS layout of one workgroup (EPW envs), float4 units:
 //   YG    [NCM][WGT]        lane (e, d) of slot c: {Y0[d], Y1[d], Y2[d], 0} (zero for d >= 12)
-//   AUX   [NCM][2][EPW]     {invm0, invm1, invm2, vmin invm0}, {c01 invm1, c02 invm2, 0, 0}
+//   AUX   [NCM][2][EPW]     {invm0, invm1, invm2, vmin invm0}, {c01 invm1, c02 invm2, mu, 0}
 //   LAM   [NCM][EPW]        contact impulses {ln, l1, l2, 0}
 //   FRC   [NCM][EPW]        last substep: contact force {f, code}
 //   CAND  [EPW][NCAND][2]   candidates {x, sep}, {n, code = 16 la + lb + 1}
@@ -472,6 +481,8 @@ constexpr int NCAND = NL * 4 + NSELF;
 //   JNT   [ND][3][EPW]      joints {a, o.x}, {o x a, o.y}, {o.z, -}
 //   UB    [NL][EPW]         world union spheres
 //   LNK   [LNK4]            link table copy
+//   PRE   [EPW][PRE4]       prologue results parked across the physics
+//   FRIC  [EPW][NL] f32     per-link friction coefficients (standup)
 constexpr int YG_OFF = 0;
 constexpr int AUX_OFF = YG_OFF + NCM * WGT;
 constexpr int LAM_OFF = AUX_OFF + NCM * 2 * EPW;
@@ -485,7 +496,8 @@ constexpr int UB_OFF = JNT_OFF + ND * 3 * EPW;
 constexpr int LNK_OFF = UB_OFF + NL * EPW;
 constexpr int PRE_OFF = LNK_OFF + LNK4;  // [EPW] Pre records (prologue -> MDP)
 constexpr int PRE4 = 8;                   // float4 per Pre record (30 floats)
-constexpr int LDS4 = PRE_OFF + EPW * PRE4;
+constexpr int FRIC_OFF = PRE_OFF + EPW * PRE4;  // [EPW][NL] f32 per-link friction (standup)
+constexpr int LDS4 = FRIC_OFF + (EPW * NL + 3) / 4;
 
 // prologue results the MDP reads after the physics (parked in LDS across the substeps)
 struct Pre {
@@ -516,6 +528,7 @@ struct Q {
   __device__ __forceinline__ int pair_code(int p) const { return reinterpret_cast<const int*>(b + LNK_OFF + NL * LINK4)[p]; }
   __device__ __forceinline__ const float4* dflt() const { return b + LNK_OFF + DFLT_OFF; }
   __device__ __forceinline__ Pre& pre() const { return *reinterpret_cast<Pre*>(b + PRE_OFF + e * PRE4); }
+  __device__ __forceinline__ float& fric(int l) const { return reinterpret_cast<float*>(b + FRIC_OFF)[e * NL + l]; }
 };
 
 __device__ __forceinline__ void read_frame(const Q& q, int body, float R[9], float p[3]) {
@@ -957,7 +970,9 @@ __device__ __forceinline__ void crba_column(float L[NT], const float Fk[6], cons
 }
 
 // ------------------------------------------------------------------------- one substep
-template <bool kDebugForces>
+// kLinkFriction: per-contact Coulomb coefficient from the per-link table q.fric (standup DR);
+// otherwise cfg.friction everywhere.
+template <bool kDebugForces, bool kLinkFriction>
 __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
                                         const float target[ND], const Q& q, bool last, SensorOut& so,
                                         float (*dbgF)[3], float* dbgTau, Stamps& sp) {
@@ -1185,7 +1200,9 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
     if (sep >= 0.f) vmin = -sep / dt;
     else vmin = fminf(cfg.baumgarte * (-sep) / dt, m->max_depenetration_velocity);
     q.aux(c, 0) = make_float4(invm[0], invm[1], invm[2], vmin * invm[0]);
-    q.aux(c, 1) = make_float4(dot12(Y[1], Y[0]) * invm[1], dot12(Y[2], Y[0]) * invm[2], 0.f, 0.f);
+    // friction combine mode "multiply": ground (terrain coefficient) x link, link x link
+    const float mu_c = kLinkFriction ? q.fric(code >> 4) * (lb >= 0 ? q.fric(lb) : cfg.friction) : 0.f;
+    q.aux(c, 1) = make_float4(dot12(Y[1], Y[0]) * invm[1], dot12(Y[2], Y[0]) * invm[2], mu_c, 0.f);
     q.lam(c) = make_float4(0.f, 0.f, 0.f, 0.f);
   }
   wave_sync();
@@ -1208,14 +1225,14 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
       const int cB = cA + 1 == nc ? 0 : cA + 1;
       const float4 GB = q.yg(cB), XB = q.aux(cB, 0), ZB = q.aux(cB, 1);
       float4 LB = q.lam(cB);
-      const float4 nA = pgs_update(GA, XA, ZA, LA, mu, wd);
+      const float4 nA = pgs_update(GA, XA, ZA, LA, kLinkFriction ? ZA.z : mu, wd);
       if (lead) q.lam(cA) = nA;
       if (cB == cA) LB = nA;
       if (k + 1 < K) {
         const int cA2 = cB + 1 == nc ? 0 : cB + 1;
         GA = q.yg(cA2); XA = q.aux(cA2, 0); ZA = q.aux(cA2, 1);
         LA = q.lam(cA2);
-        const float4 nB = pgs_update(GB, XB, ZB, LB, mu, wd);
+        const float4 nB = pgs_update(GB, XB, ZB, LB, kLinkFriction ? ZB.z : mu, wd);
         if (lead) q.lam(cB) = nB;
         if (cA2 == cB) LA = nB;
         cA = cA2;
@@ -1379,6 +1396,33 @@ __device__ __forceinline__ void link_pose_q(MP m, const Q& q, int l, float pos[3
   mv3(R, lp, t);
   pos[0] = p[0] + t[0]; pos[1] = p[1] + t[1]; pos[2] = p[2] + t[2];
   qmul(qb, lr, quat);
+}
+
+// world linear velocity of the point lc (body frame of body b): body b's twist at P from the
+// joint rates, then v + w x c
+__device__ __forceinline__ void body_point_vel_q(const Q& q, const Phys& s, const float S[ND][6], int b,
+                                                 const float lc[3], float v[3]) {
+  float V[6] = {s.av[0], s.av[1], s.av[2], s.lv[0], s.lv[1], s.lv[2]};
+#pragma unroll
+  for (int j = 0; j < ND; ++j)
+    if (j < b)
+#pragma unroll
+      for (int a = 0; a < 6; ++a) V[a] += S[j][a] * s.jqd[j];
+  float R[9], p[3], c[3];
+  read_frame(q, b, R, p);
+  mv3(R, lc, c);
+  c[0] += p[0]; c[1] += p[1]; c[2] += p[2];
+  float wc[3];
+  cross3(V, c, wc);
+  v[0] = V[3] + wc[0]; v[1] = V[4] + wc[1]; v[2] = V[5] + wc[2];
+}
+
+// world linear velocity of link l's frame origin (body_link_lin_vel_w, standup.py:774-856)
+__device__ __forceinline__ void link_origin_vel_q(MP m, const Q& q, const Phys& s, const float S[ND][6], int l,
+                                                  float v[3]) {
+  float lp[3];
+  ldc(lp, m->link_pos[l]);
+  body_point_vel_q(q, s, S, link_body(l), lp, v);
 }
 
 // world linear velocity of link l's COM: body b's twist at P from the joint rates, then v + w x c
@@ -1650,7 +1694,7 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_step_kernel(const z
   SensorOut so;
   sp.mark(0);
   for (int k = 0; k < cfg.decimation; ++k) {
-    substep<false>(m, cfg, p, target, q, k == cfg.decimation - 1, so, nullptr, nullptr, sp);
+    substep<false, false>(m, cfg, p, target, q, k == cfg.decimation - 1, so, nullptr, nullptr, sp);
     sp.mark(7);
   }
   m = opaque(m);
@@ -1891,22 +1935,34 @@ __global__ void zb_derive_kernel(const zb_model* __restrict__ mg, float4* __rest
   links[DFLT_OFF + 0] = make_float4(f0[0] + p.pos[0], f0[1] + p.pos[1], f0[2] + p.pos[2], 0.f);
   links[DFLT_OFF + 1] = make_float4(f1[0] + p.pos[0], f1[1] + p.pos[1], f1[2] + p.pos[2], 0.f);
   links[DFLT_OFF + 2] = make_float4(q0[0], q0[1], q0[2], q0[3]);
+  // base link orientation relative to the root at the default joint positions
+#pragma unroll
+  for (int a = 0; a < 4; ++a) p.quat[a] = a == 0 ? 1.f : 0.f;
+  fk(m, p, k);
+  link_pose(m, k, 6, bp, q0);
+  links[DFLT_OFF + 3] = make_float4(q0[0], q0[1], q0[2], q0[3]);
 }
 
-// episode log finalisation + full-reset episode_length_buf draw (v2.py:418-422)
 // episode log finalisation + full-reset episode_length_buf draw (v2.py:418-422); leaves the
 // accumulator zeroed for the next launch. Single workgroup (grid-strided over envs).
+// The counters (RNG stream position, common_step_counter, curriculum stage) live on the device
+// so that a captured graph of zb_step advances them on every replay. my_curriculum
+// (standup.py:99-111) runs as a reset event: stage 0 -> 1 at the first call with resets once
+// common_step_counter >= curriculum_steps; the new weights apply from the next step's rewards.
 __global__ void zb_finalize_kernel(int N, float* __restrict__ st, float* __restrict__ acc,
                                    float* __restrict__ log_means, int32_t* __restrict__ log_counts,
                                    float* __restrict__ user_means, int32_t* __restrict__ user_counts, float episode_s,
-                                   int max_ep_len, uint64_t seed, uint64_t* __restrict__ calls, int force_full,
-                                   int reset_counts) {
-  // the call counter (the episode-length RNG stream position) lives on the device so that a
-  // captured graph of zb_step advances it on every replay
-  const uint64_t ctr = *calls;
+                                   int max_ep_len, uint64_t seed, Counters* __restrict__ cnt, int force_full,
+                                   int reset_counts, int is_step, int ep_len_row, int curriculum_steps) {
+  const uint64_t ctr = cnt->calls;
+  const uint64_t steps = cnt->steps + (is_step ? 1 : 0);
   const float nres = acc[13];
   const bool full = force_full || nres == (float)N;
   __syncthreads();
+  if (threadIdx.x == 0) {
+    cnt->steps = steps;
+    if (curriculum_steps > 0 && cnt->stage == 0 && nres > 0.f && steps >= (uint64_t)curriculum_steps) cnt->stage = 1;
+  }
   if (threadIdx.x == 0 && nres > 0.f) {
 #pragma unroll
     for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) {
@@ -1921,11 +1977,11 @@ __global__ void zb_finalize_kernel(int N, float* __restrict__ st, float* __restr
   }
   __syncthreads();
   if (threadIdx.x < ACC) acc[threadIdx.x] = 0.f;
-  if (threadIdx.x == 0) *calls = ctr + 1;
+  if (threadIdx.x == 0) cnt->calls = ctr + 1;
   if (full)
     for (int i = threadIdx.x; i < N; i += blockDim.x) {
       const uint64_t h = hash64(seed ^ hash64(ctr * 0x100000001B3ull + (uint64_t)i));
-      st[(size_t)ZB_S_EP_LEN * N + i] = (float)(int)(h % (uint64_t)max_ep_len);
+      st[(size_t)ep_len_row * N + i] = (float)(int)(h % (uint64_t)max_ep_len);
     }
 }
 
@@ -1940,6 +1996,7 @@ __global__ void zb_observe_kernel(const zb_model* __restrict__ mg, int N, const 
   write_obs(m, p, d, obs, i);
 }
 
+template <bool kLinkFriction>
 __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_substeps_kernel(const zb_model* __restrict__ mg,
                                                               const float4* __restrict__ links, zb_task_cfg cfg, int N,
                                                               float* __restrict__ st, const float* __restrict__ targets,
@@ -1952,6 +2009,7 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_substeps_kernel(con
   const int i = env < N ? env : N - 1;
   const Q q{lds, lane, lane / TL, lane % TL};
   for (int t = lane; t < LNK4; t += WGT) lds[LNK_OFF + t] = links[t];
+  if (kLinkFriction && q.s < NL) q.fric(q.s) = st[(size_t)(ZB_SU_LINK_MU + q.s) * N + i];
   Phys p;
   load_phys(st, N, i, p);
   float tg[ND], tau[ND], F[1][3];
@@ -1959,7 +2017,7 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_substeps_kernel(con
   for (int j = 0; j < ND; ++j) { tg[j] = targets[(size_t)i * ND + j]; tau[j] = 0.f; }
   SensorOut so;
   Stamps sp;
-  for (int k = 0; k < nsub; ++k) substep<true>(m, cfg, p, tg, q, k == nsub - 1, so, F, tau, sp);
+  for (int k = 0; k < nsub; ++k) substep<true, kLinkFriction>(m, cfg, p, tg, q, k == nsub - 1, so, F, tau, sp);
   if (net_force && q.s < NL)
 #pragma unroll
     for (int a = 0; a < 3; ++a) net_force[((size_t)i * NL + q.s) * 3 + a] = F[0][a];
@@ -1976,6 +2034,283 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_substeps_kernel(con
 #undef SV
 }
 
+
+// =========================================================================== stand-up task
+// zbot-6b-standup-v0 (reference zbot_direct_6_standup_env_v0.py = standup.py) on the same robot
+// and physics: ZBOT_6S_CFG_2 lying init (zbot_cfg.py:721-763), per-link friction from the
+// startup material randomisation, rewards from the post-step link states, died on a height drop,
+// reset pose randomised in-kernel (reset_root_state_uniform) and a device-side curriculum.
+
+__host__ __device__ __forceinline__ float u01(uint64_t h) { return (float)(h >> 40) * (1.0f / 16777216.0f); }
+
+// reset_root_state_uniform (standup.py:33-97) for env i at RNG position ctr: x, y, roll, yaw ~ U
+// (the cfg ranges; pitch / z / velocities 0), root = default + (x, y, 0),
+// quat = quat_from_euler_xyz(roll, 0, yaw) * default quat (world-frame rotation, left multiply),
+// normalised; joints default, every velocity zero.
+__device__ __forceinline__ void su_reset_pose(MP m, const zb_task_cfg& cfg, uint64_t seed, uint64_t ctr, int i,
+                                              Phys& p) {
+  const uint64_t h = hash64(seed ^ hash64(ctr * 0x100000001B3ull + (uint64_t)i));
+  float r[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float u = u01(hash64(h + 0x632BE59BD9B4E019ull * (uint64_t)(k + 1)));
+    r[k] = u * (cfg.reset_pose_range[k][1] - cfg.reset_pose_range[k][0]) + cfg.reset_pose_range[k][0];
+  }
+  float sr, cr, sy, cy;
+  sincos_r(0.5f * r[2], &sr, &cr);
+  sincos_r(0.5f * r[3], &sy, &cy);
+  const float dq[4] = {cy * cr, cy * sr, sy * sr, sy * cr};  // quat_from_euler_xyz(roll, 0, yaw)
+  const float q0[4] = {m->default_root_quat[0], m->default_root_quat[1], m->default_root_quat[2],
+                       m->default_root_quat[3]};
+  float qn[4];
+  qmul(dq, q0, qn);
+  qnormalize(qn);
+#pragma unroll
+  for (int a = 0; a < 4; ++a) p.quat[a] = qn[a];
+  p.pos[0] = m->default_root_pos[0] + r[0];
+  p.pos[1] = m->default_root_pos[1] + r[1];
+  p.pos[2] = m->default_root_pos[2];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) { p.lv[a] = 0.f; p.av[a] = 0.f; }
+#pragma unroll
+  for (int j = 0; j < ND; ++j) { p.jq[j] = m->default_joint_pos[j]; p.jqd[j] = 0.f; }
+}
+
+// One stand-up policy step per team (same mapping as zb_step_kernel; no contact sensor).
+__global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_su_step_kernel(
+    const zb_model* __restrict__ mg, const float4* __restrict__ links, zb_task_cfg cfg, int N, float* __restrict__ st,
+    const float* __restrict__ act, float* __restrict__ obs, float* __restrict__ rew, uint8_t* __restrict__ term,
+    uint8_t* __restrict__ trunc, float* __restrict__ acc, const Counters* __restrict__ cnt, uint64_t seed) {
+  MP m = to_mp(mg);
+  __shared__ float4 lds[LDS4];
+  const int lane = threadIdx.x;
+  const int env = xcd_block(blockIdx.x, gridDim.x) * EPW + lane / TL;
+  const int i = env < N ? env : N - 1;
+  const bool lead = env < N && lane % TL == 0;
+  const Q q{lds, lane, lane / TL, lane % TL};
+  for (int t = lane; t < LNK4; t += WGT) lds[LNK_OFF + t] = links[t];
+  Stamps sp;
+  sp.begin();
+#define ST(f) st[(size_t)(f) * N + i]
+  Phys p;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) { p.pos[a] = ST(ZB_S_ROOT_POS + a); p.lv[a] = ST(ZB_S_ROOT_LINVEL + a); p.av[a] = ST(ZB_S_ROOT_ANGVEL + a); }
+#pragma unroll
+  for (int a = 0; a < 4; ++a) p.quat[a] = ST(ZB_S_ROOT_QUAT + a);
+#pragma unroll
+  for (int j = 0; j < ND; ++j) { p.jq[j] = ST(ZB_S_JOINT_POS + j); p.jqd[j] = ST(ZB_S_JOINT_VEL + j); }
+  if (q.s < NL) q.fric(q.s) = ST(ZB_SU_LINK_MU + q.s);  // lane l: link l (visible after the first barrier)
+
+  // _pre_physics_step (standup.py:538-551, mode 1)
+  const bool writer = q.s == 0;
+  const float step_dt = cfg.sim_dt * (float)cfg.decimation;
+  float target[ND];
+  {
+    Pre pr;
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+      pr.a_now[j] = tanh_r(act[(size_t)i * ZB_ACT_DIM + j]);
+      pr.pdel[j] = clampf(ST(ZB_SU_P_DELTA + j) + PI_F * pr.a_now[j] * cfg.joint_speed_limit * step_dt, -PI_F, PI_F);
+      target[j] = pr.pdel[j] + m->default_joint_pos[j];
+    }
+    if (writer) q.pre() = pr;
+  }
+
+  SensorOut so;
+  sp.mark(0);
+  for (int k = 0; k < cfg.decimation; ++k) {
+    substep<false, true>(m, cfg, p, target, q, false, so, nullptr, nullptr, sp);
+    sp.mark(7);
+  }
+  m = opaque(m);
+  wave_sync();
+  const Pre pr = q.pre();
+  st = opaque_ptr(st);
+  const float czl0 = ST(ZB_SU_CENTER_Z_LAST);
+  const float ep_len = ST(ZB_SU_EP_LEN) + 1.f;
+  float sums0[ZB_SU_NUM_REWARD_TERMS];
+#pragma unroll
+  for (int t = 0; t < ZB_SU_NUM_REWARD_TERMS; ++t) sums0[t] = ST(ZB_SU_EP_SUMS + t);
+  const int stage = cnt->stage;
+
+  // post-step link states (_compute_intermediate_values 571-591, body_link_state_w)
+  float z4, z6, z8, vz5, vz6, fz[2][3], obs_q[4];
+  {
+    wave_sync();
+    fk_team_pose(p, q);
+    wave_sync();
+    float S[ND][6], org[ND][3];
+    read_joints(q, S, org);
+    float lp[3], lq[4], v[3], R[9];
+    link_pose_q(m, q, 4, lp, lq);
+    z4 = lp[2] + p.pos[2];
+    link_pose_q(m, q, 8, lp, lq);
+    z8 = lp[2] + p.pos[2];
+    link_pose_q(m, q, 6, lp, obs_q);
+    z6 = lp[2] + p.pos[2];
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+      link_pose_q(m, q, f == 0 ? 0 : 11, lp, lq);
+      qmat(lq, R);
+      const float sg = f == 0 ? 1.f : -1.f;  // axis_z_feet = (0,0,1), (0,0,-1) (standup.py:503-505)
+      fz[f][0] = sg * R[2]; fz[f][1] = sg * R[5]; fz[f][2] = sg * R[8];
+    }
+    link_origin_vel_q(m, q, p, S, 6, v);
+    vz6 = v[2];
+    link_origin_vel_q(m, q, p, S, 5, v);
+    vz5 = v[2];
+  }
+
+  // _get_dones (standup.py:634-643)
+  const bool time_out = ep_len >= (float)(cfg.max_episode_length - 1);
+  const bool died = (czl0 - z6) > cfg.center_z_drop;
+  const float czl = ((int)ep_len % cfg.center_z_period == cfg.center_z_period - 1) ? z6 : czl0;
+
+  // _get_rewards (standup.py:620-632): reward_func() * scale * step_dt per term, dict order
+  float r[ZB_SU_NUM_REWARD_TERMS];
+  {
+    const float rh = z6 + 0.5f * z4 + 0.5f * z8 - 0.1f;  // _reward_upward_2 (843-856)
+    float up = z6 < 0.22f ? rh + 0.5f * vz6 + 0.5f * vz5 : 1.35f;
+    if ((fz[0][2] < 0.5f || fz[1][2] < 0.5f) && z6 > 0.1f) up = -5.f * up;
+    r[ZB_SU_R_UPWARD_2] = up;
+  }
+  r[ZB_SU_R_SHAPE_SYMMETRY] = fabsf(pr.pdel[0] + pr.pdel[5]) + fabsf(pr.pdel[1] + pr.pdel[4]) +
+                              fabsf(pr.pdel[2] + pr.pdel[3]);  // 782-789
+  {
+    float sd = 0.f;
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+      const float d[3] = {fz[f][0], fz[f][1], fz[f][2] - 1.f};
+      sd += sqrtf(dot3(d, d));
+    }
+    r[ZB_SU_R_FEET_DOWNWARD] = sd;  // 735-745
+  }
+  r[ZB_SU_R_FEET_DOWNWARD_4] = z6 < 0.15f ? fz[0][2] + fz[1][2] : 1.6f;  // 827-840
+  float w[ZB_SU_NUM_REWARD_TERMS];
+#pragma unroll
+  for (int t = 0; t < ZB_SU_NUM_REWARD_TERMS; ++t) w[t] = stage ? cfg.curriculum_scales[t] : cfg.reward_scales[t];
+  float reward = 0.f, sums[ZB_SU_NUM_REWARD_TERMS];
+#pragma unroll
+  for (int t = 0; t < ZB_SU_NUM_REWARD_TERMS; ++t) {
+    const float v = (r[t] * w[t]) * step_dt;
+    reward += v;
+    sums[t] = sums0[t] + v;
+  }
+  if (died) reward -= cfg.terminal_penalty;  // 629-630
+  const bool reset = died || time_out;
+
+  // _reset_idx (645-703): episode log (sums per second of the env's own episode), new random
+  // root pose, default joints; the reset env's observation sees the new pose
+  if (reset) {
+    if (lead) {
+      const float dur = fmaxf(ep_len * step_dt, step_dt);
+#pragma unroll
+      for (int t = 0; t < ZB_SU_NUM_REWARD_TERMS; ++t) atomicAdd(&acc[t], sums[t] / dur);
+      atomicAdd(&acc[13], 1.f);
+      if (died) atomicAdd(&acc[14], 1.f);
+      if (time_out) atomicAdd(&acc[15], 1.f);
+    }
+    su_reset_pose(m, cfg, seed, cnt->calls, i, p);
+    const float4 qr = q.dflt()[3];
+    const float qrel[4] = {qr.x, qr.y, qr.z, qr.w};
+    qmul(p.quat, qrel, obs_q);
+  }
+  sp.mark(12);
+  if (writer) {
+    auto live = [reset](float v) { return reset ? 0.f : v; };
+#pragma unroll
+    for (int a = 0; a < 3; ++a) { ST(ZB_S_ROOT_POS + a) = p.pos[a]; ST(ZB_S_ROOT_LINVEL + a) = p.lv[a]; ST(ZB_S_ROOT_ANGVEL + a) = p.av[a]; }
+#pragma unroll
+    for (int a = 0; a < 4; ++a) ST(ZB_S_ROOT_QUAT + a) = p.quat[a];
+#pragma unroll
+    for (int j = 0; j < ND; ++j) { ST(ZB_S_JOINT_POS + j) = p.jq[j]; ST(ZB_S_JOINT_VEL + j) = p.jqd[j]; }
+#pragma unroll
+    for (int j = 0; j < ND; ++j) { ST(ZB_SU_P_DELTA + j) = live(pr.pdel[j]); ST(ZB_SU_ACTIONS + j) = live(pr.a_now[j]); }
+    ST(ZB_SU_CENTER_Z_LAST) = reset ? cfg.center_z_init : czl;
+    ST(ZB_SU_EP_LEN) = live(ep_len);
+#pragma unroll
+    for (int t = 0; t < ZB_SU_NUM_REWARD_TERMS; ++t) ST(ZB_SU_EP_SUMS + t) = live(sums[t]);
+
+    // _get_observations (593-618): base quat, joint_pos - default, joint_vel, actions
+    float* o = obs + (size_t)i * ZB_SU_OBS_DIM;
+    o[0] = obs_q[0]; o[1] = obs_q[1]; o[2] = obs_q[2]; o[3] = obs_q[3];
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+      o[4 + j] = p.jq[j] - m->default_joint_pos[j];
+      o[10 + j] = p.jqd[j];
+      o[16 + j] = live(pr.a_now[j]);
+    }
+    rew[i] = reward;
+    term[i] = died ? 1 : 0;
+    trunc[i] = time_out ? 1 : 0;
+  }
+  sp.mark(8);
+  sp.flush();
+#undef ST
+}
+
+// explicit resets (env_ids, or all when ids == nullptr): episode log into acc, then the reset
+// pose of su_reset_pose; one thread per env
+__global__ void zb_su_reset_kernel(const zb_model* __restrict__ mg, zb_task_cfg cfg, int N, float* __restrict__ st,
+                                   const int32_t* __restrict__ ids, int n, float* __restrict__ acc,
+                                   const Counters* __restrict__ cnt, uint64_t seed) {
+  MP m = to_mp(mg);
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const int i = ids ? ids[t] : t;
+  if (i < 0 || i >= N) return;
+#define ST(f) st[(size_t)(f) * N + i]
+  const float step_dt = cfg.sim_dt * (float)cfg.decimation;
+  const float dur = fmaxf(ST(ZB_SU_EP_LEN) * step_dt, step_dt);
+#pragma unroll
+  for (int k = 0; k < ZB_SU_NUM_REWARD_TERMS; ++k) atomicAdd(&acc[k], ST(ZB_SU_EP_SUMS + k) / dur);
+  atomicAdd(&acc[13], 1.f);
+  Phys p;
+  su_reset_pose(m, cfg, seed, cnt->calls, i, p);
+#pragma unroll
+  for (int a = 0; a < 3; ++a) { ST(ZB_S_ROOT_POS + a) = p.pos[a]; ST(ZB_S_ROOT_LINVEL + a) = p.lv[a]; ST(ZB_S_ROOT_ANGVEL + a) = p.av[a]; }
+#pragma unroll
+  for (int a = 0; a < 4; ++a) ST(ZB_S_ROOT_QUAT + a) = p.quat[a];
+#pragma unroll
+  for (int j = 0; j < ND; ++j) {
+    ST(ZB_S_JOINT_POS + j) = p.jq[j]; ST(ZB_S_JOINT_VEL + j) = p.jqd[j];
+    ST(ZB_SU_P_DELTA + j) = 0.f; ST(ZB_SU_ACTIONS + j) = 0.f;
+  }
+  ST(ZB_SU_CENTER_Z_LAST) = cfg.center_z_init;
+  ST(ZB_SU_EP_LEN) = 0.f;
+#pragma unroll
+  for (int k = 0; k < ZB_SU_NUM_REWARD_TERMS; ++k) ST(ZB_SU_EP_SUMS + k) = 0.f;
+#undef ST
+}
+
+__global__ void zb_su_observe_kernel(const zb_model* __restrict__ mg, int N, const float* __restrict__ st,
+                                     float* __restrict__ obs) {
+  MP m = to_mp(mg);
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  Phys p;
+  load_phys(st, N, i, p);
+  Kin k;
+  fk(m, p, k);
+  float bp[3], bq[4];
+  link_pose(m, k, 6, bp, bq);
+  float* o = obs + (size_t)i * ZB_SU_OBS_DIM;
+  o[0] = bq[0]; o[1] = bq[1]; o[2] = bq[2]; o[3] = bq[3];
+#pragma unroll
+  for (int j = 0; j < ND; ++j) {
+    o[4 + j] = p.jq[j] - m->default_joint_pos[j];
+    o[10 + j] = p.jqd[j];
+    o[16 + j] = st[(size_t)(ZB_SU_ACTIONS + j) * N + i];
+  }
+}
+
+// per-link friction [N][NL] -> state rows ZB_SU_LINK_MU (mu == nullptr: fill with `fill`)
+__global__ void zb_su_friction_kernel(int N, float* __restrict__ st, const float* __restrict__ mu, float fill) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= N * NL) return;
+  const int i = t / NL, l = t % NL;
+  st[(size_t)(ZB_SU_LINK_MU + l) * N + i] = mu ? mu[t] : fill;
+}
 }  // namespace
 
 // =========================================================================== C ABI
@@ -1983,7 +2318,9 @@ struct zb_sim {
   int device;
   int n;
   uint64_t seed;
-  uint64_t* d_calls;  // zb_step / zb_reset calls so far (device counter, graph-replay safe)
+  int task;           // ZB_TASK_*
+  int state_dim;      // ZB_STATE_DIM / ZB_SU_STATE_DIM
+  Counters* d_cnt;    // device counters (graph-replay safe)
   zb_task_cfg cfg;
   zb_model* d_model;
   float4* d_links;  // per-link collision table [NL][LINK4] (detect)
@@ -2042,18 +2379,22 @@ int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_dev
     if (np != m->num_self_pairs) return set_err(-1, "zb_create: self-collision pair count", hipSuccess);
   }
   if (c->decimation < 1 || c->solver_iterations < 0) return set_err(-1, "zb_create: cfg", hipSuccess);
+  if (c->task != ZB_TASK_WALKING_V2 && c->task != ZB_TASK_STANDUP_V0) return set_err(-1, "zb_create: unknown task", hipSuccess);
+  if (c->task == ZB_TASK_STANDUP_V0 && c->center_z_period < 1) return set_err(-1, "zb_create: center_z_period", hipSuccess);
   HIPCHK(hipSetDevice(hip_device), "hipSetDevice");
   zb_sim* h = new zb_sim();
   h->device = hip_device;
   h->n = num_envs;
   h->seed = seed;
-  h->d_calls = nullptr;
+  h->task = c->task;
+  h->state_dim = c->task == ZB_TASK_STANDUP_V0 ? ZB_SU_STATE_DIM : ZB_STATE_DIM;
+  h->d_cnt = nullptr;
   h->cfg = *c;
   HIPCHK(hipMalloc(&h->d_model, sizeof(zb_model)), "hipMalloc model");
-  HIPCHK(hipMalloc(&h->d_state, sizeof(float) * (size_t)ZB_STATE_DIM * num_envs), "hipMalloc state");
+  HIPCHK(hipMalloc(&h->d_state, sizeof(float) * (size_t)h->state_dim * num_envs), "hipMalloc state");
   HIPCHK(hipMalloc(&h->d_acc, sizeof(float) * ACC), "hipMalloc acc");
-  HIPCHK(hipMalloc(&h->d_calls, sizeof(uint64_t)), "hipMalloc calls");
-  HIPCHK(hipMemset(h->d_calls, 0, sizeof(uint64_t)), "hipMemset calls");
+  HIPCHK(hipMalloc(&h->d_cnt, sizeof(Counters)), "hipMalloc counters");
+  HIPCHK(hipMemset(h->d_cnt, 0, sizeof(Counters)), "hipMemset counters");
   HIPCHK(hipMalloc(&h->d_log_means, sizeof(float) * ZB_NUM_REWARD_TERMS), "hipMalloc log");
   HIPCHK(hipMalloc(&h->d_log_counts, sizeof(int32_t) * 2), "hipMalloc log");
   HIPCHK(hipMemcpy(h->d_model, m, sizeof(zb_model), hipMemcpyHostToDevice), "hipMemcpy model");
@@ -2100,7 +2441,7 @@ int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_dev
     HIPCHK(hipMalloc(&h->d_links, sizeof(tab)), "hipMalloc links");
     HIPCHK(hipMemcpy(h->d_links, tab, sizeof(tab), hipMemcpyHostToDevice), "hipMemcpy links");
   }
-  HIPCHK(hipMemset(h->d_state, 0, sizeof(float) * (size_t)ZB_STATE_DIM * num_envs), "hipMemset state");
+  HIPCHK(hipMemset(h->d_state, 0, sizeof(float) * (size_t)h->state_dim * num_envs), "hipMemset state");
   HIPCHK(hipMemset(h->d_log_means, 0, sizeof(float) * ZB_NUM_REWARD_TERMS), "hipMemset log");
   HIPCHK(hipMemset(h->d_log_counts, 0, sizeof(int32_t) * 2), "hipMemset log");
   HIPCHK(hipMemset(h->d_acc, 0, sizeof(float) * ACC), "hipMemset acc");
@@ -2108,9 +2449,22 @@ int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_dev
   zb_derive_kernel<<<1, 1>>>(h->d_model, h->d_links);
   int rc = launch_check("zb_derive_kernel");
   if (rc) return rc;
-  zb_reset_kernel<<<(num_envs + 255) / 256, 256>>>(h->d_model, h->d_links, num_envs, h->d_state, nullptr, num_envs,
-                                                    h->d_acc);
-  rc = launch_check("zb_reset_kernel");
+  if (h->task == ZB_TASK_STANDUP_V0) {
+    zb_su_friction_kernel<<<(num_envs * NL + 255) / 256, 256>>>(num_envs, h->d_state, nullptr, c->friction);
+    rc = launch_check("zb_su_friction_kernel");
+    if (rc) return rc;
+    // the construction-time reset draws its poses at RNG position 0; later calls start at 1
+    zb_su_reset_kernel<<<(num_envs + 255) / 256, 256>>>(h->d_model, h->cfg, num_envs, h->d_state, nullptr, num_envs,
+                                                       h->d_acc, h->d_cnt, h->seed);
+    rc = launch_check("zb_su_reset_kernel");
+    if (rc) return rc;
+    const Counters c1{1, 0, 0, 0};
+    HIPCHK(hipMemcpy(h->d_cnt, &c1, sizeof(Counters), hipMemcpyHostToDevice), "hipMemcpy counters");
+  } else {
+    zb_reset_kernel<<<(num_envs + 255) / 256, 256>>>(h->d_model, h->d_links, num_envs, h->d_state, nullptr, num_envs,
+                                                      h->d_acc);
+    rc = launch_check("zb_reset_kernel");
+  }
   if (rc) return rc;
   HIPCHK(hipMemset(h->d_acc, 0, sizeof(float) * ACC), "hipMemset acc");
   HIPCHK(hipDeviceSynchronize(), "zb_create sync");
@@ -2173,10 +2527,25 @@ void zb_destroy(zb_handle h) {
   (void)hipFree(h->d_links);
   (void)hipFree(h->d_state);
   (void)hipFree(h->d_acc);
-  (void)hipFree(h->d_calls);
+  (void)hipFree(h->d_cnt);
   (void)hipFree(h->d_log_means);
   (void)hipFree(h->d_log_counts);
   delete h;
+}
+
+// episode-log divisor: walking divides the summed episode sums by the 20 s episode (v2.py:446),
+// standup already divided each env's sums by its own duration (standup.py:653-659)
+static float log_episode_s(zb_handle h) {
+  return h->task == ZB_TASK_STANDUP_V0 ? 1.f : h->cfg.sim_dt * h->cfg.decimation * h->cfg.max_episode_length;
+}
+
+static int finalize(zb_handle h, hipStream_t s, int full, int reset_counts, int is_step) {
+  const int ep_row = h->task == ZB_TASK_STANDUP_V0 ? ZB_SU_EP_LEN : ZB_S_EP_LEN;
+  const int cur = h->task == ZB_TASK_STANDUP_V0 ? h->cfg.curriculum_steps : 0;
+  zb_finalize_kernel<<<1, 1024, 0, s>>>(h->n, h->d_state, h->d_acc, h->d_log_means, h->d_log_counts, h->u_log_means,
+                                        h->u_log_counts, log_episode_s(h), h->cfg.max_episode_length, h->seed,
+                                        h->d_cnt, full, reset_counts, is_step, ep_row, cur);
+  return launch_check("zb_finalize_kernel");
 }
 
 int zb_reset(zb_handle h, const int32_t* env_ids, int n, void* stream) {
@@ -2184,14 +2553,14 @@ int zb_reset(zb_handle h, const int32_t* env_ids, int n, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const int cnt = env_ids ? n : h->n;
   if (cnt <= 0) return 0;
-  zb_reset_kernel<<<(cnt + 255) / 256, 256, 0, s>>>(h->d_model, h->d_links, h->n, h->d_state, env_ids, cnt, h->d_acc);
+  if (h->task == ZB_TASK_STANDUP_V0)
+    zb_su_reset_kernel<<<(cnt + 255) / 256, 256, 0, s>>>(h->d_model, h->cfg, h->n, h->d_state, env_ids, cnt, h->d_acc,
+                                                         h->d_cnt, h->seed);
+  else
+    zb_reset_kernel<<<(cnt + 255) / 256, 256, 0, s>>>(h->d_model, h->d_links, h->n, h->d_state, env_ids, cnt, h->d_acc);
   int rc = launch_check("zb_reset_kernel");
   if (rc) return rc;
-  const float ep_s = h->cfg.sim_dt * h->cfg.decimation * h->cfg.max_episode_length;
-  const int full = env_ids == nullptr || n == h->n;
-  zb_finalize_kernel<<<1, 1024, 0, s>>>(h->n, h->d_state, h->d_acc, h->d_log_means, h->d_log_counts, h->u_log_means,
-                                        h->u_log_counts, ep_s, h->cfg.max_episode_length, h->seed, h->d_calls, full, 1);
-  return launch_check("zb_finalize_kernel");
+  return finalize(h, s, env_ids == nullptr || n == h->n, 1, 0);
 }
 
 int zb_step(zb_handle h, const float* actions, float* obs, float* reward, uint8_t* terminated, uint8_t* truncated,
@@ -2201,24 +2570,46 @@ int zb_step(zb_handle h, const float* actions, float* obs, float* reward, uint8_
   const int blocks = (h->n + EPW - 1) / EPW;
   const bool prof = h->prof_n < h->prof_max;
   if (prof) HIPCHK(hipEventRecord(h->prof_ev[2 * h->prof_n], s), "hipEventRecord");
-  zb_step_kernel<<<blocks, WGT, 0, s>>>(h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward, terminated,
-                                         truncated, h->d_acc);
+  if (h->task == ZB_TASK_STANDUP_V0)
+    zb_su_step_kernel<<<blocks, WGT, 0, s>>>(h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward,
+                                             terminated, truncated, h->d_acc, h->d_cnt, h->seed);
+  else
+    zb_step_kernel<<<blocks, WGT, 0, s>>>(h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward,
+                                          terminated, truncated, h->d_acc);
   int rc = launch_check("zb_step_kernel");
   if (prof) {
     HIPCHK(hipEventRecord(h->prof_ev[2 * h->prof_n + 1], s), "hipEventRecord");
     ++h->prof_n;
   }
   if (rc) return rc;
-  const float ep_s = h->cfg.sim_dt * h->cfg.decimation * h->cfg.max_episode_length;
-  zb_finalize_kernel<<<1, 1024, 0, s>>>(h->n, h->d_state, h->d_acc, h->d_log_means, h->d_log_counts, h->u_log_means,
-                                        h->u_log_counts, ep_s, h->cfg.max_episode_length, h->seed, h->d_calls, 0, 0);
-  return launch_check("zb_finalize_kernel");
+  return finalize(h, s, 0, 0, 1);
 }
 
 int zb_observe(zb_handle h, float* obs, void* stream) {
   if (!h || !obs) return set_err(-1, "zb_observe", hipSuccess);
-  zb_observe_kernel<<<(h->n + 255) / 256, 256, 0, (hipStream_t)stream>>>(h->d_model, h->n, h->d_state, obs);
+  if (h->task == ZB_TASK_STANDUP_V0)
+    zb_su_observe_kernel<<<(h->n + 255) / 256, 256, 0, (hipStream_t)stream>>>(h->d_model, h->n, h->d_state, obs);
+  else
+    zb_observe_kernel<<<(h->n + 255) / 256, 256, 0, (hipStream_t)stream>>>(h->d_model, h->n, h->d_state, obs);
   return launch_check("zb_observe_kernel");
+}
+
+int zb_state_dim(zb_handle h) { return h ? h->state_dim : -1; }
+
+int zb_set_link_friction(zb_handle h, const float* mu, void* stream) {
+  if (!h || !mu) return set_err(-1, "zb_set_link_friction", hipSuccess);
+  if (h->task != ZB_TASK_STANDUP_V0) return set_err(-1, "zb_set_link_friction: per-link friction is a standup-task state", hipSuccess);
+  zb_su_friction_kernel<<<(h->n * NL + 255) / 256, 256, 0, (hipStream_t)stream>>>(h->n, h->d_state, mu, 0.f);
+  return launch_check("zb_su_friction_kernel");
+}
+
+int zb_read_curriculum(zb_handle h, int32_t* stage, int64_t* common_step_counter) {
+  if (!h) return set_err(-1, "zb_read_curriculum", hipSuccess);
+  Counters c;
+  HIPCHK(hipMemcpy(&c, h->d_cnt, sizeof(Counters), hipMemcpyDeviceToHost), "hipMemcpy counters");
+  if (stage) *stage = c.stage;
+  if (common_step_counter) *common_step_counter = (int64_t)c.steps;
+  return 0;
 }
 
 int zb_read_log(zb_handle h, float* term_means, int32_t* counts, void* stream) {
@@ -2241,7 +2632,7 @@ int zb_set_log_buffers(zb_handle h, float* term_means, int32_t* counts) {
 
 int zb_get_state(zb_handle h, float* dst, void* stream) {
   if (!h || !dst) return set_err(-1, "zb_get_state", hipSuccess);
-  HIPCHK(hipMemcpyAsync(dst, h->d_state, sizeof(float) * (size_t)ZB_STATE_DIM * h->n, hipMemcpyDeviceToDevice,
+  HIPCHK(hipMemcpyAsync(dst, h->d_state, sizeof(float) * (size_t)h->state_dim * h->n, hipMemcpyDeviceToDevice,
                         (hipStream_t)stream),
          "hipMemcpyAsync state");
   return 0;
@@ -2249,7 +2640,7 @@ int zb_get_state(zb_handle h, float* dst, void* stream) {
 
 int zb_set_state(zb_handle h, const float* src, void* stream) {
   if (!h || !src) return set_err(-1, "zb_set_state", hipSuccess);
-  HIPCHK(hipMemcpyAsync(h->d_state, src, sizeof(float) * (size_t)ZB_STATE_DIM * h->n, hipMemcpyDeviceToDevice,
+  HIPCHK(hipMemcpyAsync(h->d_state, src, sizeof(float) * (size_t)h->state_dim * h->n, hipMemcpyDeviceToDevice,
                         (hipStream_t)stream),
          "hipMemcpyAsync state");
   return 0;
@@ -2259,8 +2650,12 @@ int zb_physics_substeps(zb_handle h, const float* targets, int nsub, float* net_
                         void* stream) {
   if (!h || !targets || nsub < 1) return set_err(-1, "zb_physics_substeps", hipSuccess);
   const int blocks = (h->n + EPW - 1) / EPW;
-  zb_substeps_kernel<<<blocks, WGT, 0, (hipStream_t)stream>>>(h->d_model, h->d_links, h->cfg, h->n, h->d_state, targets, nsub,
-                                                               net_force, applied_torque);
+  if (h->task == ZB_TASK_STANDUP_V0)
+    zb_substeps_kernel<true><<<blocks, WGT, 0, (hipStream_t)stream>>>(h->d_model, h->d_links, h->cfg, h->n, h->d_state,
+                                                                       targets, nsub, net_force, applied_torque);
+  else
+    zb_substeps_kernel<false><<<blocks, WGT, 0, (hipStream_t)stream>>>(h->d_model, h->d_links, h->cfg, h->n, h->d_state,
+                                                                        targets, nsub, net_force, applied_torque);
   return launch_check("zb_substeps_kernel");
 }
 

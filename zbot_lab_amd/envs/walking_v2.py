@@ -94,6 +94,8 @@ class ZbotDirectEnvV2:
 
     is_vector_env = True
     metadata = {"render_modes": [None], "isaac_sim_version": None}
+    _termination_keys = ("Episode_Termination/body_contact", "Episode_Termination/time_out")  # v2.py:449-457
+    _ep_len_row = zm.S["EP_LEN"]
 
     def __init__(self, cfg: ZbotDirectEnvCfgV2 | None = None, render_mode: str | None = None, **kwargs):
         self.cfg = cfg or ZbotDirectEnvCfgV2()
@@ -120,9 +122,12 @@ class ZbotDirectEnvV2:
         self.action_space = spaces.Box(-np.inf, np.inf, (self.num_envs, self.cfg.action_space))
         self.common_step_counter = 0
         self.extras: dict = {}
-        self._log_keys = [f"Episode_Reward/{k}" for k in zm.REWARD_TERMS] + [
-            "Episode_Termination/body_contact", "Episode_Termination/time_out"]
+        self._log_keys = [f"Episode_Reward/{k}" for k in self._task.reward_terms]
         self.obs_buf = None
+        self._startup()
+
+    def _startup(self) -> None:
+        """Startup events (none for v2)."""
 
     # ------------------------------------------------------------------ gym API
     @property
@@ -144,12 +149,12 @@ class ZbotDirectEnvV2:
     @property
     def episode_length_buf(self) -> torch.Tensor:
         """Copy of the in-HBM episode counters (int64, like Isaac Lab's buffer)."""
-        return self.sim.get_state()[zm.S["EP_LEN"]].round().to(torch.long)
+        return self.sim.get_state()[self._ep_len_row].round().to(torch.long)
 
     @episode_length_buf.setter
     def episode_length_buf(self, value: torch.Tensor) -> None:
         st = self.sim.get_state()
-        st[zm.S["EP_LEN"]] = value.to(device=self.device, dtype=torch.float32)
+        st[self._ep_len_row] = value.to(device=self.device, dtype=torch.float32)
         self.sim.set_state(st)
 
     def seed(self, seed: int = -1) -> int:
@@ -173,9 +178,9 @@ class ZbotDirectEnvV2:
 
     def _update_log(self) -> None:
         means, counts = self.sim.read_log()
-        log = {k: means[i] for i, k in enumerate(self._log_keys[:zm.NUM_TERMS])}
-        log["Episode_Termination/body_contact"] = counts[0]
-        log["Episode_Termination/time_out"] = counts[1]
+        log = {k: means[i] for i, k in enumerate(self._log_keys)}
+        log[self._termination_keys[0]] = counts[0]
+        log[self._termination_keys[1]] = counts[1]
         self.extras["log"] = log
 
     def get_observations(self):

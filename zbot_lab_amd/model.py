@@ -38,6 +38,18 @@ REWARD_WEIGHTS = {  # v2.py:190-206 ("train reward 2000 step4")
     "airtime_sum": 3.0,
 }
 
+# zbot-6b-standup-v0 (include/zbot.h enum zb_standup_state_field / zb_standup_reward_term)
+TASK_WALKING_V2, TASK_STANDUP_V0 = 0, 1
+SU_OBS_DIM, SU_NUM_TERMS, SU_STATE_DIM = 22, 4, 55
+SU_REWARD_TERMS = ["upward_2", "shape_symmetry", "feet_downward", "feet_downward_4"]  # standup.py:418-427
+SU_REWARD_WEIGHTS = {"upward_2": 10.0, "shape_symmetry": -1.0, "feet_downward": -1.0, "feet_downward_4": 0.0}
+SU_CURRICULUM_WEIGHTS = {"upward_2": 10.0, "shape_symmetry": -2.0, "feet_downward": -1.0,
+                         "feet_downward_4": 2.0}  # my_curriculum stage 1 (standup.py:103-107)
+SU = dict(P_DELTA=25, ACTIONS=31, CENTER_Z_LAST=37, EP_LEN=38, EP_SUMS=39, LINK_MU=43)
+# ZBOT_6S_CFG_2 init_state (zbot_cfg.py:744-753): lying on its side, joints straight
+SU_ROOT_POS = (0.0, 0.0, 0.05)
+SU_ROOT_ROT = (0.707, 0.0, -0.707, 0.0)
+
 # state field offsets (include/zbot.h enum zb_state_field)
 S = dict(ROOT_POS=0, ROOT_QUAT=3, ROOT_LINVEL=7, ROOT_ANGVEL=10, JOINT_POS=13, JOINT_VEL=19,
          P_DELTA=25, ACTIONS=31, FEET_DOWN_POS=37, FEET_STEP_LEN=43, FEET_F_LAST=45, HEADING_SUM=47,
@@ -81,6 +93,9 @@ class ZbTaskCfg(C.Structure):
         ("friction", C.c_float), ("contact_force_threshold", C.c_float),
         ("contact_margin", C.c_float), ("baumgarte", C.c_float),
         ("solver_iterations", C.c_int32), ("enable_self_collision", C.c_int32),
+        ("task", C.c_int32), ("reset_pose_range", (C.c_float * 2) * 4),
+        ("center_z_init", C.c_float), ("center_z_drop", C.c_float), ("center_z_period", C.c_int32),
+        ("curriculum_steps", C.c_int32), ("curriculum_scales", C.c_float * NUM_TERMS),
     ]
 
 
@@ -271,6 +286,16 @@ def load_model(path: str = ASSET) -> RobotModel:
                       default_root_quat=np.array(cfg["root_rot_wxyz"], float), cfg=cfg)
 
 
+def standup_model(rm: RobotModel | None = None) -> RobotModel:
+    """``ZBOT_6S_CFG_2`` (zbot_cfg.py:721-763): the same robot / actuators as ``ZBOT_6S_CFG`` with
+    the lying initial state (root (0, 0, 0.05), rot (0.707, 0, -0.707, 0), joints 0)."""
+    import dataclasses
+    rm = rm or load_model()
+    return dataclasses.replace(rm, default_joint_pos=np.zeros(NUM_DOF),
+                               default_root_pos=np.array(SU_ROOT_POS, float),
+                               default_root_quat=np.array(SU_ROOT_ROT, float))
+
+
 def pack_model(rm: RobotModel | None = None) -> ZbModel:
     rm = rm or load_model()
     m = ZbModel()
@@ -340,6 +365,34 @@ class TaskCfg:
     baumgarte: float = 0.2
     solver_iterations: int = 4   # = solver_position_iteration_count (zbot_cfg.py:637)
     enable_self_collision: bool = True
+    task: int = TASK_WALKING_V2
+    # stand-up task only (standup.py)
+    reset_pose_range: tuple = ((-0.5, 0.5), (-0.5, 0.5), (-0.7854, 0.7854), (-3.14, 3.14))  # x, y, roll, yaw
+    center_z_init: float = 0.05
+    center_z_drop: float = 0.05
+    center_z_period: int = 50
+    curriculum_steps: int | None = None  # my_curriculum threshold; None = max_episode_length * 80 (standup.py:102)
+    curriculum_weights: dict | None = None
+
+    @classmethod
+    def standup(cls, **kw) -> "TaskCfg":
+        """Zbot6SUpEnvCfg (standup.py:191-447): 6 s episodes, terminal penalty 2, 4 reward terms."""
+        d = dict(task=TASK_STANDUP_V0, episode_length_s=6.0, terminal_penalty=2.0, termination_height=0.20,
+                 reward_weights=dict(SU_REWARD_WEIGHTS), curriculum_weights=dict(SU_CURRICULUM_WEIGHTS))
+        d.update(kw)
+        return cls(**d)
+
+    @property
+    def obs_dim(self) -> int:
+        return SU_OBS_DIM if self.task == TASK_STANDUP_V0 else OBS_DIM
+
+    @property
+    def state_dim(self) -> int:
+        return SU_STATE_DIM if self.task == TASK_STANDUP_V0 else STATE_DIM
+
+    @property
+    def reward_terms(self) -> list:
+        return SU_REWARD_TERMS if self.task == TASK_STANDUP_V0 else REWARD_TERMS
 
     @property
     def step_dt(self) -> float:
@@ -355,9 +408,24 @@ class TaskCfg:
         c.decimation = self.decimation
         c.max_episode_length = self.max_episode_length
         c.termination_height = self.termination_height
-        for k, name in enumerate(REWARD_TERMS):
-            # v2.py:250-252 multiplies every weight by step_dt at env construction
-            c.reward_scales[k] = self.reward_weights.get(name, 0.0) * self.step_dt
+        if self.task == TASK_STANDUP_V0:
+            # standup.py:624 multiplies by step_dt per term in _get_rewards (the kernel does)
+            for k, name in enumerate(SU_REWARD_TERMS):
+                c.reward_scales[k] = self.reward_weights.get(name, 0.0)
+                cw = self.curriculum_weights if self.curriculum_weights is not None else self.reward_weights
+                c.curriculum_scales[k] = cw.get(name, 0.0)
+            thr = self.max_episode_length * 80 if self.curriculum_steps is None else self.curriculum_steps
+            c.curriculum_steps = thr if self.curriculum_weights else 0
+        else:
+            for k, name in enumerate(REWARD_TERMS):
+                # v2.py:250-252 multiplies every weight by step_dt at env construction
+                c.reward_scales[k] = self.reward_weights.get(name, 0.0) * self.step_dt
+        c.task = self.task
+        for k in range(4):
+            c.reset_pose_range[k][0], c.reset_pose_range[k][1] = self.reset_pose_range[k]
+        c.center_z_init = self.center_z_init
+        c.center_z_drop = self.center_z_drop
+        c.center_z_period = self.center_z_period
         c.terminal_penalty = self.terminal_penalty
         c.joint_speed_limit = self.joint_speed_limit
         c.gravity = self.gravity

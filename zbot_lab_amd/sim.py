@@ -30,7 +30,12 @@ class ZbotSim:
         self.lib = nat.lib()
         self.num_envs = int(num_envs)
         self.cfg = cfg or zm.TaskCfg()
-        self.robot = robot or zm.load_model()
+        self.task = self.cfg.task
+        self.obs_dim, self.state_dim = self.cfg.obs_dim, self.cfg.state_dim
+        self.num_terms = len(self.cfg.reward_terms)
+        if robot is None:
+            robot = zm.standup_model() if self.task == zm.TASK_STANDUP_V0 else zm.load_model()
+        self.robot = robot
         self._m = zm.pack_model(self.robot)
         self._c = self.cfg.pack()
         idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
@@ -40,10 +45,12 @@ class ZbotSim:
             nat.check(self.lib.zb_create(C.byref(self._m), C.byref(self._c), self.num_envs, idx, int(seed) & (2**64 - 1),
                                          C.byref(h)), "zb_create")
         self._h = h
+        if self.lib.zb_state_dim(h) != self.state_dim:
+            raise nat.ZbotError("libzbot state layout does not match zbot_lab_amd.model")
         # persistent outputs (reference: terminated/truncated buffers are mutated in place)
         self.terminated = torch.zeros(self.num_envs, dtype=torch.bool, device=self.device)
         self.truncated = torch.zeros(self.num_envs, dtype=torch.bool, device=self.device)
-        self._log_means = torch.zeros(zm.NUM_TERMS, dtype=torch.float32, device=self.device)
+        self._log_means = torch.zeros(zm.NUM_TERMS, dtype=torch.float32, device=self.device)  # first num_terms used
         self._log_counts = torch.zeros(2, dtype=torch.int32, device=self.device)
         # the library fills these in stream order at every step/reset with resets (no copies)
         nat.check(self.lib.zb_set_log_buffers(self._h, nat.ptr(self._log_means), nat.ptr(self._log_counts)),
@@ -75,7 +82,7 @@ class ZbotSim:
         a = actions.to(device=self.device, dtype=torch.float32).contiguous()
         if a.shape != (self.num_envs, zm.ACT_DIM):
             raise ValueError(f"actions must be [{self.num_envs}, {zm.ACT_DIM}], got {tuple(a.shape)}")
-        obs = torch.empty(self.num_envs, zm.OBS_DIM, dtype=torch.float32, device=self.device)
+        obs = torch.empty(self.num_envs, self.obs_dim, dtype=torch.float32, device=self.device)
         rew = torch.empty(self.num_envs, dtype=torch.float32, device=self.device)
         nat.check(self.lib.zb_step(self._h, nat.ptr(a), nat.ptr(obs), nat.ptr(rew), nat.ptr(self.terminated),
                                    nat.ptr(self.truncated), _stream(self.device)), "zb_step")
@@ -87,24 +94,38 @@ class ZbotSim:
                                    nat.ptr(self.truncated), _stream(self.device)), "zb_step")
 
     def observe(self) -> torch.Tensor:
-        obs = torch.empty(self.num_envs, zm.OBS_DIM, dtype=torch.float32, device=self.device)
+        obs = torch.empty(self.num_envs, self.obs_dim, dtype=torch.float32, device=self.device)
         nat.check(self.lib.zb_observe(self._h, nat.ptr(obs), _stream(self.device)), "zb_observe")
         return obs
 
     def read_log(self):
-        """(term_means[13], counts[2]) device tensors of the most recent step that had resets
+        """(term_means[num_terms], counts[2]) device tensors of the most recent step that had resets
         (registered with zb_set_log_buffers, so no per-step copy)."""
-        return self._log_means, self._log_counts
+        return self._log_means[:self.num_terms], self._log_counts
+
+    def set_link_friction(self, mu: torch.Tensor) -> None:
+        """Standup: per-link friction coefficients [N, 12] (randomize_rigid_body_material)."""
+        m = mu.to(device=self.device, dtype=torch.float32).contiguous()
+        if m.shape != (self.num_envs, zm.NUM_LINKS):
+            raise ValueError(f"friction must be [{self.num_envs}, {zm.NUM_LINKS}]")
+        nat.check(self.lib.zb_set_link_friction(self._h, nat.ptr(m), _stream(self.device)), "zb_set_link_friction")
+        torch.cuda.current_stream(self.device).synchronize()  # `m` may be a temporary
+
+    def read_curriculum(self):
+        """(curriculum stage, common_step_counter) from the device (synchronises)."""
+        st, n = C.c_int32(), C.c_int64()
+        nat.check(self.lib.zb_read_curriculum(self._h, C.byref(st), C.byref(n)), "zb_read_curriculum")
+        return int(st.value), int(n.value)
 
     def get_state(self) -> torch.Tensor:
-        st = torch.empty(zm.STATE_DIM, self.num_envs, dtype=torch.float32, device=self.device)
+        st = torch.empty(self.state_dim, self.num_envs, dtype=torch.float32, device=self.device)
         nat.check(self.lib.zb_get_state(self._h, nat.ptr(st), _stream(self.device)), "zb_get_state")
         return st
 
     def set_state(self, st: torch.Tensor) -> None:
         s = st.to(device=self.device, dtype=torch.float32).contiguous()
-        if s.shape != (zm.STATE_DIM, self.num_envs):
-            raise ValueError(f"state must be [{zm.STATE_DIM}, {self.num_envs}]")
+        if s.shape != (self.state_dim, self.num_envs):
+            raise ValueError(f"state must be [{self.state_dim}, {self.num_envs}]")
         nat.check(self.lib.zb_set_state(self._h, nat.ptr(s), _stream(self.device)), "zb_set_state")
         torch.cuda.current_stream(self.device).synchronize()  # `s` may be a temporary
 

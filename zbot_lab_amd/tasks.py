@@ -1,5 +1,5 @@
 """Task registry: ``make("zbot-6b-walking-v2")`` like ``gym.make`` on the reference's registration
-(``source/zbot/zbot/tasks/zbot6b_direct/__init__.py:41-49``)."""
+(``source/zbot/zbot/tasks/zbot6b_direct/__init__.py:41-49``; ``zbot-6b-standup-v0`` 111-119)."""
 from __future__ import annotations
 
 import importlib
@@ -56,5 +56,14 @@ register(
     kwargs={
         "env_cfg_entry_point": "zbot_lab_amd.envs.walking_v2:ZbotDirectEnvCfgV2",
         "rsl_rl_cfg_entry_point": "zbot_lab_amd.rl.cfg:PPORunnerCfgV2",
+    },
+)
+
+register(
+    id="zbot-6b-standup-v0",
+    entry_point="zbot_lab_amd.envs.standup_v0:Zbot6SUpEnv",
+    kwargs={
+        "env_cfg_entry_point": "zbot_lab_amd.envs.standup_v0:Zbot6SUpEnvCfg",
+        "rsl_rl_cfg_entry_point": "zbot_lab_amd.rl.cfg:Zbot6SUpEnvPPOCfg",
     },
 )
