@@ -14,7 +14,7 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "zb_step_kernel"
+KERNEL = os.environ.get("KERNEL", "zb_step_kernel")
 
 
 def main(tag: str) -> None:

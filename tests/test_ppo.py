@@ -41,6 +41,35 @@ class ToyVecEnv:
         return self._obs(), rew, tout.long(), {"time_outs": tout, "log": {}}
 
 
+class LogToyEnv(ToyVecEnv):
+    """extras["log"] holds one in-place tensor (like the simulator's registered log buffers) plus
+    a python int, changing every step."""
+
+    def __init__(self, **kw):
+        super().__init__(**kw)
+        self.k = 0
+        self.buf = torch.zeros(1)
+
+    def step(self, a):
+        o, r, d, ex = super().step(a)
+        self.k += 1
+        self.buf[0] = float(self.k)
+        ex["log"] = {"Episode_Reward/x": self.buf[0], "Episode_Termination/n": self.k % 2}
+        return o, r, d, ex
+
+
+def test_runner_log_is_mean_over_rollout_steps():
+    """rsl_rl appends every step's extras["log"] and logs the mean over the rollout."""
+    from zbot_lab_amd.rl import OnPolicyRunner, PPORunnerCfgV2
+    cfg = PPORunnerCfgV2()
+    cfg.num_steps_per_env = 4
+    runner = OnPolicyRunner(LogToyEnv(n=16), cfg.to_dict(), log_dir=None, device="cpu")
+    log = runner.learn(2)
+    assert log[0]["Episode_Reward/x"] == pytest.approx((1 + 2 + 3 + 4) / 4)
+    assert log[1]["Episode_Reward/x"] == pytest.approx((5 + 6 + 7 + 8) / 4)
+    assert log[1]["Episode_Termination/n"] == pytest.approx(0.5)
+
+
 def _gae_ref(rew, val, dones, last, gamma, lam):
     T = rew.shape[0]
     adv = np.zeros_like(last)

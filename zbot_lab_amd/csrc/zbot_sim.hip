@@ -2542,7 +2542,7 @@ static float log_episode_s(zb_handle h) {
 static int finalize(zb_handle h, hipStream_t s, int full, int reset_counts, int is_step) {
   const int ep_row = h->task == ZB_TASK_STANDUP_V0 ? ZB_SU_EP_LEN : ZB_S_EP_LEN;
   const int cur = h->task == ZB_TASK_STANDUP_V0 ? h->cfg.curriculum_steps : 0;
-  zb_finalize_kernel<<<1, 1024, 0, s>>>(h->n, h->d_state, h->d_acc, h->d_log_means, h->d_log_counts, h->u_log_means,
+  zb_finalize_kernel<<<1, 256, 0, s>>>(h->n, h->d_state, h->d_acc, h->d_log_means, h->d_log_counts, h->u_log_means,
                                         h->u_log_counts, log_episode_s(h), h->cfg.max_episode_length, h->seed,
                                         h->d_cnt, full, reset_counts, is_step, ep_row, cur);
   return launch_check("zb_finalize_kernel");

@@ -177,11 +177,14 @@ class ZbotDirectEnvV2:
         return self.obs_buf, rew, term, trunc, self.extras
 
     def _update_log(self) -> None:
-        means, counts = self.sim.read_log()
-        log = {k: means[i] for i, k in enumerate(self._log_keys)}
-        log[self._termination_keys[0]] = counts[0]
-        log[self._termination_keys[1]] = counts[1]
-        self.extras["log"] = log
+        # the library refreshes the registered log buffers in stream order; the dict of views into
+        # them is built once (no per-step tensor work)
+        if getattr(self, "_log", None) is None:
+            means, counts = self.sim.read_log()
+            self._log = {k: means[i] for i, k in enumerate(self._log_keys)}
+            self._log[self._termination_keys[0]] = counts[0]
+            self._log[self._termination_keys[1]] = counts[1]
+        self.extras["log"] = self._log
 
     def get_observations(self):
         if self.obs_buf is None:

@@ -60,6 +60,7 @@ class OnPolicyRunner:
         self.cur_rew = torch.zeros(self.env.num_envs, device=self.device)
         self.cur_len = torch.zeros(self.env.num_envs, device=self.device)
         self.ep_stats = torch.zeros(3, device=self.device)  # reward sum, length sum, count
+        self._log_keys, self._log_acc = None, None
         self.use_graph = (torch.device(device).type == "cuda") if use_graph is None else use_graph
         self._graph = None
         self._g_obs = None
@@ -126,9 +127,9 @@ class OnPolicyRunner:
                    "mean_episode_length": statistics.mean(lenbuffer) if lenbuffer else float("nan"),
                    "learning_rate": self.alg.learning_rate, "mean_noise_std": self.alg.policy.std.mean().item(),
                    **{f"loss/{k}": v for k, v in losses.items()}}
-            log = self._extras.get("log", {}) if isinstance(self._extras, dict) else {}
-            for k, v in log.items():
-                rec[k] = float(v) if not torch.is_tensor(v) else float(v.float().mean())
+            if self._log_keys:  # rsl_rl: mean over the rollout's per-step extras["log"] values
+                for k, v in zip(self._log_keys, (self._log_acc / self.num_steps_per_env).tolist()):
+                    rec[k] = v
             self.log.append(rec)
             if self.gpu_global_rank == 0 and self.log_dir and (it % self.save_interval == 0):
                 self.save(os.path.join(self.log_dir, f"model_{it}.pt"))
@@ -141,6 +142,8 @@ class OnPolicyRunner:
         """num_steps_per_env env steps into the storage; episode statistics into ep_stats."""
         env = self.env
         self.ep_stats.zero_()
+        if self._log_acc is not None:
+            self._log_acc.zero_()
         for _ in range(self.num_steps_per_env):
             actions = self.alg.act(obs, obs)
             obs_d, rewards, dones, extras = env.step(actions.to(env.device))
@@ -154,8 +157,21 @@ class OnPolicyRunner:
                                           torch.where(d, self.cur_len, 0.0).sum(), d.sum().float()])
             self.cur_rew.masked_fill_(d, 0.0)
             self.cur_len.masked_fill_(d, 0.0)
+            self._accumulate_log(extras)
         self._extras = extras
         return obs
+
+    def _accumulate_log(self, extras) -> None:
+        """Sum this step's extras["log"] values on the device (rsl_rl appends every step's log and
+        averages at log time; here the sum is captured in the rollout graph)."""
+        log = extras.get("log") if isinstance(extras, dict) else None
+        if not log:
+            return
+        if self._log_keys is None:
+            self._log_keys = list(log.keys())
+            self._log_acc = torch.zeros(len(self._log_keys), device=self.device)
+        vals = [log[k] if torch.is_tensor(log[k]) else torch.tensor(float(log[k])) for k in self._log_keys]
+        self._log_acc += torch.stack([v.to(self.device, torch.float32).reshape(()) for v in vals])
 
     def _capture(self, obs: torch.Tensor) -> None:
         """Record one rollout (reading obs from a static buffer) as a graph; nothing executes."""
