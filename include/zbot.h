@@ -59,8 +59,19 @@ extern "C" {
 
 #define ZB_TASK_WALKING_V2 0  /* zbot-6b-walking-v2 (v2.py) */
 #define ZB_TASK_STANDUP_V0 1  /* zbot-6b-standup-v0 (standup.py) */
+#define ZB_TASK_WALKING_V4 2  /* zbot-6b-walking-v4 (v4.py): v2 + commands, events, curricula */
 #define ZB_SU_OBS_DIM 22      /* standup.py:199 */
 #define ZB_SU_NUM_REWARD_TERMS 4
+#define ZB_V4_OBS_DIM 24      /* v4.py:453 */
+#define ZB_V4_NUM_REWARD_TERMS 15
+#define ZB_V4_HIST 3          /* v4 contact sensor history_length (v4.py:522) */
+#define ZB_MAX_REWARD_TERMS 16
+#define ZB_MAX_STAGES 4       /* curriculum stages */
+#define ZB_V4_RING 24         /* range_curriculum reward buffers: deque(maxlen=24) (v4.py:700-701) */
+/* Episode log buffer (zb_read_log): [0..15] Episode_Reward/<term> means in term order,
+ * [16] Curriculum/curriculum_stage, [17..18] Curriculum/vel_lower_bound, vel_upper_bound,
+ * [19] Curriculum/yaw_bound (v4 only; v4.py:952-957) */
+#define ZB_LOG_LEN 20
 
 /* Persistent per-env state, SoA [ZB_STATE_DIM][num_envs] float32. */
 enum zb_state_field {
@@ -97,6 +108,35 @@ enum zb_standup_state_field {
   ZB_SU_EP_SUMS = 39,       /* 4  _episode_sums in reward-term order */
   ZB_SU_LINK_MU = 43,       /* 12 per-link friction coefficient (read-only for zb_step) */
   ZB_SU_STATE_DIM = 55
+};
+
+/* v4 state, SoA [ZB_V4_STATE_DIM][num_envs] float32; rows 0..24 as in zb_state_field. */
+enum zb_v4_state_field {
+  ZB_V4_P_DELTA = 25,         /* 6 */
+  ZB_V4_ACTIONS = 31,         /* 6 */
+  ZB_V4_COMMANDS = 37,        /* 2  commands: target forward velocity, relative yaw (v4.py:697) */
+  ZB_V4_TARGET_YAW = 39,      /* 1  target_heading_yaw (world, v4.py:699) */
+  ZB_V4_INTERVAL_LEFT = 40,   /* 1  interval_command_resample time left (s) */
+  ZB_V4_FEET_DOWN_POS = 41,   /* 6 */
+  ZB_V4_FEET_STEP_LEN = 47,   /* 2 */
+  ZB_V4_FEET_F_LAST = 49,     /* 2 */
+  ZB_V4_FEET_FZ_HIST = 51,    /* 6  [slot][foot], slot 0 newest */
+  ZB_V4_UNDES_FMAX_HIST = 57, /* 3 */
+  ZB_V4_FEET_AIR_CUR = 60,    /* 2 */
+  ZB_V4_FEET_CONTACT_CUR = 62,/* 2 */
+  ZB_V4_FEET_AIR_LAST = 64,   /* 2 */
+  ZB_V4_FEET_CONTACT_LAST = 66,/*2 */
+  ZB_V4_EP_LEN = 68,          /* 1 */
+  ZB_V4_EP_SUMS = 69,         /* 15 */
+  ZB_V4_CURRENT_YAW = 84,     /* 1  current_yaw: post-step heading, or the reset event's yaw sample */
+  ZB_V4_STATE_DIM = 85
+};
+
+/* v4 reward term order = dict order of Zbot6SEnvV4Cfg.reward_cfg (v4.py:620-641). */
+enum zb_v4_reward_term {
+  ZB_V4_R_TRACK_LIN_VEL_X = 0, ZB_V4_R_TRACK_HEADING_YAW, ZB_V4_R_LIN_VEL_Y, ZB_V4_R_ACTION_RATE, ZB_V4_R_TORQUES,
+  ZB_V4_R_JOINT_VEL, ZB_V4_R_JOINT_ACC, ZB_V4_R_FEET_DOWNWARD, ZB_V4_R_FEET_FORWARD, ZB_V4_R_STEP_LENGTH,
+  ZB_V4_R_FEET_AIR_TIME_BIPED, ZB_V4_R_AIRTIME_VARIANCE, ZB_V4_R_FEET_SLIDE, ZB_V4_R_FEET_HARMONY, ZB_V4_R_FEET_CLOSE
 };
 
 /* Stand-up reward term order = dict order of Zbot6SUpEnvCfg.reward_cfg (standup.py:418-427). */
@@ -163,16 +203,35 @@ typedef struct zb_task_cfg {
   float baumgarte;             /* penetration correction per step (fraction) */
   int32_t solver_iterations;   /* PGS sweeps per substep */
   int32_t enable_self_collision;
-  int32_t task;                /* ZB_TASK_WALKING_V2 / ZB_TASK_STANDUP_V0 */
-  /* standup: reset_root_state_uniform pose ranges {lo, hi} of x, y, roll, yaw added to the
-   * default root pose (standup.py:159-175); pitch and z ranges are 0 there */
+  int32_t task;                /* ZB_TASK_* */
+  /* standup / v4: reset_root_state_uniform pose ranges {lo, hi} of x, y, roll, yaw added to the
+   * default root pose (standup.py:159-175, v4.py:274); pitch and z ranges are 0 there */
   float reset_pose_range[4][2];
+  int32_t reset_pose_body_frame; /* 1: root quat * delta (v4.py:88), 0: delta * root quat (standup.py:88) */
   float center_z_init;         /* standup: center_z_last after a reset, 0.05 (standup.py:511,701) */
   float center_z_drop;         /* standup: died when center_z_last - base z > this, 0.05 (638) */
   int32_t center_z_period;     /* standup: center_z_last refresh when ep_len % period == period-1 (640) */
-  int32_t curriculum_steps;    /* standup: my_curriculum threshold on common_step_counter,
-                                  max_episode_length * 80 (standup.py:102); 0 = no curriculum */
-  float curriculum_scales[ZB_NUM_REWARD_TERMS]; /* standup: reward weights from curriculum stage 1 */
+  /* standup / v4 my_curriculum (standup.py:99-111, v4.py:137-199): stage s >= 1 is entered at the
+   * first call with resets once common_step_counter >= stage_steps[s], one stage per call */
+  int32_t num_stages;          /* 1 = no curriculum */
+  int32_t stage_steps[ZB_MAX_STAGES];
+  float stage_scales[ZB_MAX_STAGES][ZB_MAX_REWARD_TERMS]; /* reward weights of each stage (x step_dt in-kernel) */
+  float stage_prob_pos[ZB_MAX_STAGES]; /* v4: resample_commands prob_pos of each stage */
+  /* v4 resample_commands (v4.py:107-135; reset and interval events 400-439) */
+  float cmd_vel_range[2];      /* initial velocity_range (0.3, 0.3) */
+  float cmd_yaw_range[2];      /* initial yaw_range (-0.1, 0.1) */
+  int32_t cmd_dual_sign;
+  float cmd_offset;
+  float cmd_interval_s[2];     /* interval_range_s (3, 6) */
+  /* v4 range_curriculum (v4.py:201-265, cfg 392-398 + 686) */
+  float range_limit_vel[2], range_limit_yaw[2];
+  int32_t range_start_steps;   /* max_episode_length * 48 */
+  int32_t range_period_steps;  /* max_episode_length * 12 */
+  int32_t range_min_buffer;    /* 20 */
+  float range_threshold;       /* 0.85 */
+  float range_delta;           /* 0.05 */
+  float undesired_force_threshold; /* died: max |F| of an undesired body over the history > this (v2 1.0, v4 0.5) */
+  float feet_f_last_init;      /* v4 feet_contact_forces_last after construction / reset: 15 (v4.py:731,979) */
 } zb_task_cfg;
 
 typedef struct zb_sim* zb_handle;
@@ -198,10 +257,11 @@ int zb_step(zb_handle h, const float* actions, float* obs, float* reward, uint8_
 /* Observation of the current state (v2.py:351-365), as reset() returns. obs: float[N][23]. */
 int zb_observe(zb_handle h, float* obs, void* stream);
 
-/* Episode log of the most recent step with resets: term_means[13] = mean episodic sum / 20 s,
- * counts[2] = {body_contact, time_out} (v2.py:441-459). Device pointers. */
+/* Episode log of the most recent step with resets: term_means[ZB_LOG_LEN] (layout at
+ * ZB_LOG_LEN; walking v2: mean episodic sum / 20 s, standup / v4: mean of sum / own duration),
+ * counts[2] = {body_contact | died, time_out} (v2.py:441-459). Device pointers. */
 int zb_read_log(zb_handle h, float* term_means, int32_t* counts, void* stream);
-/* Register caller-owned device buffers (float[13], int32[2]) that every later step/reset with
+/* Register caller-owned device buffers (float[ZB_LOG_LEN], int32[2]) that every later step/reset with
  * resets fills in stream order, exactly as zb_read_log would (no per-step copies). NULL, NULL
  * unregisters. */
 int zb_set_log_buffers(zb_handle h, float* term_means, int32_t* counts);
@@ -223,8 +283,7 @@ int zb_physics_substeps(zb_handle h, const float* targets, int nsub, float* net_
  * mu[a] * mu[b]. A new handle starts at cfg.friction for every link. */
 int zb_set_link_friction(zb_handle h, const float* mu, void* stream);
 
-/* Standup: curriculum stage (0/1) and common_step_counter (zb_step calls). Host pointers;
- * synchronises with the device. */
+/* Curriculum stage and common_step_counter (zb_step calls). Host pointers; synchronises. */
 int zb_read_curriculum(zb_handle h, int32_t* stage, int64_t* common_step_counter);
 
 /* Measurement: time the next `max_launches` zb_step_kernel launches with hipEvents recorded on

@@ -56,7 +56,12 @@ def _load(double: bool = False):
     lib.zbo_su_mdp_eval.argtypes = [C.c_int, C.POINTER(zm.ZbTaskCfg), C.c_int, _f, _f, _i, _f, _f, _f, _f, _u8, _u8]
     lib.zbo_su_reset_pose.argtypes = [C.POINTER(zm.ZbModel), C.POINTER(zm.ZbTaskCfg), C.c_uint64, C.c_uint64, C.c_int,
                                       _f, _f]
-    lib.zbo_su_pose_from_samples.argtypes = [C.POINTER(zm.ZbModel), C.c_int, _f, _f, _f]
+    lib.zbo_su_pose_from_samples.argtypes = [C.POINTER(zm.ZbModel), C.c_int, _f, C.c_int, _f, _f]
+    lib.zbo_v4_mdp_eval.argtypes = [C.c_int, C.POINTER(zm.ZbTaskCfg), C.c_int, C.POINTER(zm.ZbModel)] + [_f] * 12 + \
+        [_i, _f, _f, _f, _f, _f, _f, _f, _f, _f, _f, _u8, _u8, _f, _f]
+    lib.zbo_v4_commands_from_draws.argtypes = [C.c_int, _f, _f, _f, _f, _f, _f, _f]
+    lib.zbo_curriculum_probe.argtypes = [C.POINTER(zm.ZbTaskCfg), C.c_int64, C.c_int, C.c_int, C.c_int, C.c_float,
+                                         C.c_float, _f]
     return lib
 
 
@@ -116,11 +121,11 @@ class OracleSim:
         self.lib.zbo_observe(self.h, obs)
         return obs
 
-    def read_log(self):
-        m = np.zeros(zm.NUM_TERMS, np.float32)
+    def read_log(self, full: bool = False):
+        m = np.zeros(zm.LOG_LEN, np.float32)
         c = np.zeros(2, np.int32)
         self.lib.zbo_read_log(self.h, m, c)
-        return m[:self.num_terms], c
+        return (m if full else m[:self.num_terms]), c
 
     def set_link_friction(self, mu):
         if self.lib.zbo_set_link_friction(self.h, f32(mu)) != 0:
@@ -189,12 +194,56 @@ def su_reset_pose(cfg: zm.TaskCfg, seed: int, ctr: int, n: int):
     return pos, quat
 
 
-def su_pose_from_samples(samples):
-    """Root (pos [n,3], quat [n,4]) from reset_root_state_uniform samples [n,4] = x, y, roll, yaw."""
-    m = zm.pack_model(zm.standup_model())
+def su_pose_from_samples(samples, body_frame: bool = False, robot=None):
+    """Root (pos [n,3], quat [n,4]) from reset_root_state_uniform samples [n,4] = x, y, roll, yaw
+    (standup: world-frame delta on ZBOT_6S_CFG_2; v4: body-frame delta on ZBOT_6S_CFG)."""
+    m = zm.pack_model(robot if robot is not None else zm.standup_model())
     smp = f32(samples)
     n = len(smp)
     pos = np.zeros((n, 3), np.float32)
     quat = np.zeros((n, 4), np.float32)
-    lib().zbo_su_pose_from_samples(C.byref(m), n, smp, pos, quat)
+    lib().zbo_su_pose_from_samples(C.byref(m), n, smp, int(body_frame), pos, quat)
     return pos, quat
+
+
+def v4_mdp_eval(cfg: zm.TaskCfg, stage: int, frame: dict, ep_len, act, prev_act, state: dict):
+    """v4 _get_dones + _get_rewards on Isaac-Lab-shaped frame data (zbo_v4_mdp_eval). ``state`` holds
+    commands, target_yaw, feet_down_pos, feet_step_len, feet_f_last, ep_sums (updated copies returned)."""
+    n = len(ep_len)
+    c = cfg.pack()
+    m = zm.pack_model()
+    st = {k: f32(v).copy() for k, v in state.items()}
+    out = dict(reward=np.zeros(n, np.float32), terms=np.zeros((n, zm.V4_NUM_TERMS), np.float32),
+               died=np.zeros(n, np.uint8), time_out=np.zeros(n, np.uint8), cur_yaw=np.zeros(n, np.float32),
+               heading_err=np.zeros(n, np.float32))
+    lib().zbo_v4_mdp_eval(n, C.byref(c), int(stage), C.byref(m), f32(frame["body_link_pos_w"]),
+                          f32(frame["body_link_quat_w"]), f32(frame["body_link_lin_vel_w"]),
+                          f32(frame["body_com_lin_vel_w"]), f32(frame["joint_vel"]), f32(frame["joint_acc"]),
+                          f32(frame["applied_torque"]), f32(frame["net_forces_w_history"]),
+                          f32(frame["current_air_time"]), f32(frame["current_contact_time"]),
+                          f32(frame["last_air_time"]), f32(frame["last_contact_time"]),
+                          np.ascontiguousarray(ep_len, np.int32), f32(act), f32(prev_act), st["commands"],
+                          st["target_yaw"], st["feet_down_pos"], st["feet_step_len"], st["feet_f_last"], st["ep_sums"],
+                          out["reward"], out["terms"], out["died"], out["time_out"], out["cur_yaw"], out["heading_err"])
+    out["died"] = out["died"].astype(bool)
+    out["time_out"] = out["time_out"].astype(bool)
+    out.update(st)
+    return out
+
+
+def v4_commands_from_draws(params, u_sign, u_vel, u_yaw, cur_yaw):
+    n = len(u_sign)
+    cmd = np.zeros((n, 2), np.float32)
+    tgt = np.zeros(n, np.float32)
+    lib().zbo_v4_commands_from_draws(n, f32(params), f32(u_sign), f32(u_vel), f32(u_yaw), f32(cur_yaw), cmd, tgt)
+    return cmd, tgt
+
+
+def curriculum_probe(cfg: zm.TaskCfg, steps: int, io, run_my=True, run_range=True, ring_n=0, ring_vel=0.0,
+                     ring_yaw=0.0):
+    """The reset-event curricula on a counter state io = [stage, prob_pos, vel lo, vel hi, yaw lo, yaw hi]."""
+    c = cfg.pack()
+    v = f32(io).copy()
+    lib().zbo_curriculum_probe(C.byref(c), int(steps), int(run_my), int(run_range), int(ring_n), float(ring_vel),
+                               float(ring_yaw), v)
+    return v

@@ -145,12 +145,13 @@ typedef struct {
   real p_delta[ND], actions[ND];
   real center_z_last;                 /* standup only (standup.py:511) */
   real mu[NL];                        /* standup only: per-link friction (DR) */
+  real commands[2], target_yaw, interval_left, current_yaw; /* v4 only */
   real feet_down_pos[2][3], feet_step_len[2], feet_f_last[2];
   real heading_sum, yerr_sum;
   real feet_fz_hist[ZB_HIST][2], undes_fmax_hist[ZB_HIST];
-  real feet_air_cur[2], feet_air_last[2], feet_contact_cur[2];
+  real feet_air_cur[2], feet_air_last[2], feet_contact_cur[2], feet_contact_last[2];
   int32_t ep_len;
-  real ep_sums[ZB_NUM_REWARD_TERMS];
+  real ep_sums[ZB_MAX_REWARD_TERMS];
 } mdp_t;
 
 typedef struct { phys_t ph; mdp_t md; } env_t;
@@ -161,9 +162,12 @@ struct zbo_sim {
   int n;
   uint64_t seed, call_counter; /* zb_step / zb_reset calls so far (RNG stream position) */
   uint64_t steps;               /* common_step_counter (zb_step calls) */
-  int stage;                    /* standup curriculum stage */
+  int stage;                    /* curriculum stage */
+  float vel[2], yaw[2], prob_pos; /* v4 command sampling params (changed by the curricula) */
+  int ring_n, ring_head;
+  float ring_vel[ZB_V4_RING], ring_yaw[ZB_V4_RING];
   env_t* env;
-  float log_means[ZB_NUM_REWARD_TERMS];
+  float log_means[ZB_LOG_LEN];
   int32_t log_counts[2];
 };
 typedef struct zbo_sim zbo_sim;
@@ -957,27 +961,38 @@ static void write_obs(const mdl_t* m, const env_t* e, float* obs) {
 
 static inline real su_u01(uint64_t h) { return (real)((float)(h >> 40) * (1.0f / 16777216.0f)); }
 
-static void su_pose_from_samples(const mdl_t* m, const real r[4], phys_t* p);
+static void pose_from_samples(const mdl_t* m, const real r[4], int body_frame, phys_t* p);
 
-/* reset_root_state_uniform (standup.py:33-97) at RNG position ctr (same draws as the kernel) */
-static void su_reset_pose(const mdl_t* m, const zb_task_cfg* cfg, uint64_t seed, uint64_t ctr, int i, phys_t* p) {
-  const uint64_t h = zb_hash64(seed ^ zb_hash64(ctr * 0x100000001B3ull + (uint64_t)i));
+static inline uint64_t env_hash(uint64_t seed, uint64_t ctr, int i) {
+  return zb_hash64(seed ^ zb_hash64(ctr * 0x100000001B3ull + (uint64_t)i));
+}
+static inline real draw(uint64_t h, int k) { return su_u01(zb_hash64(h + 0x632BE59BD9B4E019ull * (uint64_t)k)); }
+
+/* reset_root_state_uniform (standup.py:33-97, v4.py:59-105) from stream h (draws 1..4, same
+ * as the kernel); returns the yaw sample (stored as env.current_yaw) */
+static real reset_pose(const mdl_t* m, const zb_task_cfg* cfg, uint64_t h, phys_t* p) {
   real r[4];
-  for (int k = 0; k < 4; ++k) {
-    const real u = su_u01(zb_hash64(h + 0x632BE59BD9B4E019ull * (uint64_t)(k + 1)));
-    r[k] = u * ((real)cfg->reset_pose_range[k][1] - (real)cfg->reset_pose_range[k][0]) + (real)cfg->reset_pose_range[k][0];
-  }
-  su_pose_from_samples(m, r, p);
+  for (int k = 0; k < 4; ++k)
+    r[k] = draw(h, k + 1) * ((real)cfg->reset_pose_range[k][1] - (real)cfg->reset_pose_range[k][0]) +
+           (real)cfg->reset_pose_range[k][0];
+  pose_from_samples(m, r, cfg->reset_pose_body_frame, p);
+  return r[3];
 }
 
-/* root pose from the samples (x, y, roll, yaw) of reset_root_state_uniform */
-static void su_pose_from_samples(const mdl_t* m, const real r[4], phys_t* p) {
+static void su_reset_pose(const mdl_t* m, const zb_task_cfg* cfg, uint64_t seed, uint64_t ctr, int i, phys_t* p) {
+  (void)reset_pose(m, cfg, env_hash(seed, ctr, i), p);
+}
+
+/* root pose from the samples (x, y, roll, yaw): quat_from_euler_xyz(roll, 0, yaw) applied in the
+ * world frame (delta * default, standup.py:87-88) or the body frame (default * delta, v4.py:88) */
+static void pose_from_samples(const mdl_t* m, const real r[4], int body_frame, phys_t* p) {
   /* quat_from_euler_xyz(roll, pitch = 0, yaw) (Isaac Lab math: extrinsic X then Z) */
   const real cr = (real)cos(0.5 * (double)r[2]), sr = (real)sin(0.5 * (double)r[2]);
   const real cy = (real)cos(0.5 * (double)r[3]), sy = (real)sin(0.5 * (double)r[3]);
   const real dq[4] = {cy * cr, cy * sr, sy * sr, sy * cr};
   real qn[4];
-  q_mul(dq, m->root_quat0, qn); /* world-frame rotation: delta * default (standup.py:87-88) */
+  if (body_frame) q_mul(m->root_quat0, dq, qn);
+  else q_mul(dq, m->root_quat0, qn);
   q_normalize(qn);
   for (int a = 0; a < 4; ++a) p->root_quat[a] = qn[a];
   p->root_pos[0] = m->root_pos0[0] + r[0];
@@ -1058,7 +1073,7 @@ static real su_mdp_eval(const zb_task_cfg* cfg, int stage, const su_links_t* L, 
   const real step_dt = (real)(cfg->sim_dt * (float)cfg->decimation);
   real rew = 0;
   for (int t = 0; t < ZB_SU_NUM_REWARD_TERMS; ++t) {
-    const real w = stage ? (real)cfg->curriculum_scales[t] : (real)cfg->reward_scales[t];
+    const real w = (real)cfg->stage_scales[stage][t];
     const real v = (r[t] * w) * step_dt;
     terms[t] = v;
     rew += v;
@@ -1083,7 +1098,7 @@ static void su_write_obs(const mdl_t* m, const env_t* e, float* obs) {
 
 static real su_step_env(const mdl_t* m, const zb_task_cfg* cfg, int stage, uint64_t seed, uint64_t ctr, int i,
                         env_t* e, const float* action, float* obs, int* died, int* tout,
-                        real acc[ZB_SU_NUM_REWARD_TERMS]) {
+                        real acc[ZB_MAX_REWARD_TERMS]) {
   mdp_t* md = &e->md;
   real act[ND], target[ND];
   const real step_dt = (real)(cfg->sim_dt * (float)cfg->decimation);
@@ -1141,9 +1156,428 @@ static void su_unpack_env(env_t* e, const float* st, int n, int i) {
 #undef GET
 }
 
-static void su_curriculum(zbo_sim* s, int nreset) { /* my_curriculum (standup.py:99-111) */
-  if (s->c.curriculum_steps > 0 && s->stage == 0 && nreset > 0 && s->steps >= (uint64_t)s->c.curriculum_steps)
-    s->stage = 1;
+/* ========================================================================= walking v4
+ * zbot-6b-walking-v4: reference source/zbot/zbot/tasks/zbot6b_direct/zbot_direct_6dof_bipedal_env_v4.py
+ * (v4.py). v2's robot and physics; commands (forward velocity, relative yaw) resampled by reset
+ * and interval events; a history-3 contact sensor with contact-time tracking; 15 reward terms on
+ * the post-step state; my_curriculum (stage weights, command sign probability) and
+ * range_curriculum (command ranges). */
+
+static real wrap_to_pi_r(real x) { /* isaaclab.utils.math.wrap_to_pi */
+  double a = fmod((double)x, TWO_PI);
+  if (a < 0) a += TWO_PI;
+  return (real)(a > PI_R ? a - TWO_PI : a);
+}
+
+/* resample_commands (v4.py:107-135) on uniform draws (u_sign < prob_pos: Bernoulli sign) */
+static void v4_commands(int dual_sign, real prob_pos, const float vr[2], const float yr[2], real offset, real u_sign,
+                        real u_vel, real u_yaw, real cur_yaw, real cmd[2], real* target) {
+  const real lo = vr[0], hi0 = vr[1];
+  if (dual_sign) {
+    const real sg = u_sign < prob_pos ? 1 : -1; /* bernoulli(prob_pos) * 2 - 1 */
+    const real hi = hi0 + offset * (sg - 1);
+    cmd[0] = (u_vel * (hi - lo) + lo) * sg;
+  } else {
+    cmd[0] = u_vel * (hi0 - lo) + lo;
+  }
+  cmd[1] = u_yaw * ((real)yr[1] - (real)yr[0]) + (real)yr[0];
+  *target = wrap_to_pi_r(cur_yaw + cmd[1]);
+}
+
+/* the same with draws k0 .. k0+2 of stream h and the sim's current params */
+static void v4_resample(const zbo_sim* s, uint64_t h, int k0, real cur_yaw, real cmd[2], real* target) {
+  v4_commands(s->c.cmd_dual_sign, (real)s->prob_pos, s->vel, s->yaw, (real)s->c.cmd_offset, draw(h, k0),
+              draw(h, k0 + 1), draw(h, k0 + 2), cur_yaw, cmd, target);
+}
+
+/* what the v4 MDP reads after the physics (Isaac Lab data names) */
+typedef struct {
+  real base_pos[3], base_quat[4], base_lin_vel[3];  /* body_link_*_w[base] */
+  real feet_pos[2][3], feet_quat[2][4], feet_com_vel[2][3];
+  real jqd[ND], joint_acc[ND], applied_torque[ND];
+  real fz_hist[ZB_V4_HIST][2];     /* net_forces_w_history[..., feet, 2], slot 0 newest */
+  real undes_fmax_hist[ZB_V4_HIST];/* max over undesired bodies of |net force| per slot */
+  real air_cur[2], con_cur[2], air_last[2], con_last[2]; /* sensor timers after the update */
+  int32_t ep_len;                  /* after the += 1 */
+} v4_post_t;
+
+typedef struct { real cur_yaw, heading_err; } v4_aux_t;
+
+/* _get_dones (896-918) + _get_rewards (883-894; terms 1003-1171 in dict order) with the
+ * intermediate values of 809-849. Updates the step-length state and the episode sums. */
+static real v4_mdp_eval(const zb_task_cfg* cfg, int stage, const v4_post_t* P, mdp_t* md, const real act[ND],
+                        const real prev[ND], real terms[ZB_V4_NUM_REWARD_TERMS], int* died_out, int* tout_out,
+                        v4_aux_t* aux) {
+  static const real zax[3] = {0, 0, 1}, mzax[3] = {0, 0, -1}, xax[3] = {1, 0, 0};
+  const int time_out = P->ep_len >= cfg->max_episode_length - 1;
+  real fm = 0;
+  for (int h = 0; h < ZB_V4_HIST; ++h) fm = P->undes_fmax_hist[h] > fm ? P->undes_fmax_hist[h] : fm;
+  const int died = fm > (real)cfg->undesired_force_threshold || P->base_pos[2] < (real)cfg->termination_height;
+  real sh[3], fwd[3];
+  quat_apply(P->base_quat, zax, sh);
+  fwd[0] = sh[1]; fwd[1] = -sh[0]; fwd[2] = 0; /* GRAVITY_VEC_W (0,0,-1) x shoulder */
+  const real cur_yaw = (real)atan2((double)fwd[1], (double)fwd[0]);
+  const real d = md->target_yaw - cur_yaw;
+  const real he = (real)atan2(sin((double)d), cos((double)d));
+  const real vfwd = v3_dot(P->base_lin_vel, fwd);
+  real feetF[2];
+  for (int f = 0; f < 2; ++f) {
+    real a = 0;
+    for (int h = 0; h < ZB_V4_HIST; ++h) a += P->fz_hist[h][f];
+    feetF[f] = a / (real)ZB_V4_HIST;
+  }
+  real fz[2][3], fx[2][3];
+  for (int f = 0; f < 2; ++f) {
+    quat_apply(P->feet_quat[f], f == 0 ? zax : mzax, fz[f]);
+    quat_apply(P->feet_quat[f], xax, fx[f]);
+  }
+  real r[ZB_V4_NUM_REWARD_TERMS];
+  {
+    const real e = md->commands[0] - vfwd;
+    r[ZB_V4_R_TRACK_LIN_VEL_X] = (real)exp(-(double)(e * e) / 0.25);
+    r[ZB_V4_R_TRACK_HEADING_YAW] = (real)exp(-(double)(he * he) / 0.25);
+    const real vy = v3_dot(P->base_lin_vel, sh);
+    r[ZB_V4_R_LIN_VEL_Y] = vy * vy;
+    real ar = 0, jv = 0, ja = 0, tq = 0;
+    for (int j = 0; j < ND; ++j) {
+      ar += (act[j] - prev[j]) * (act[j] - prev[j]);
+      jv += P->jqd[j] * P->jqd[j];
+      ja += P->joint_acc[j] * P->joint_acc[j];
+      tq += P->applied_torque[j] * P->applied_torque[j];
+    }
+    r[ZB_V4_R_ACTION_RATE] = ar;
+    r[ZB_V4_R_TORQUES] = tq;
+    r[ZB_V4_R_JOINT_VEL] = jv;
+    r[ZB_V4_R_JOINT_ACC] = ja;
+    real sd = 0, sf = 0;
+    for (int f = 0; f < 2; ++f) {
+      const real dz[3] = {fz[f][0], fz[f][1], fz[f][2] - 1};
+      sd += sqrtr(v3_dot(dz, dz));
+      const real dx[3] = {fx[f][0] - fwd[0], fx[f][1] - fwd[1], fx[f][2] - fwd[2]};
+      sf += sqrtr(v3_dot(dx, dx));
+    }
+    r[ZB_V4_R_FEET_DOWNWARD] = sd;
+    r[ZB_V4_R_FEET_FORWARD] = sf;
+    /* step_length (1058-1095) */
+    const real csg = md->commands[0] > 0 ? 1 : (md->commands[0] < 0 ? -1 : 0);
+    for (int f = 0; f < 2; ++f) {
+      if (feetF[f] > (real)10.0 && md->feet_f_last[f] < (real)10.0) {
+        const real dv[3] = {P->feet_pos[f][0] - md->feet_down_pos[f][0], P->feet_pos[f][1] - md->feet_down_pos[f][1],
+                            P->feet_pos[f][2] - md->feet_down_pos[f][2]};
+        md->feet_step_len[f] = v3_dot(dv, fwd) * csg;
+        for (int a = 0; a < 3; ++a) md->feet_down_pos[f][a] = P->feet_pos[f][a];
+      }
+    }
+    const real mn = md->feet_step_len[0] < md->feet_step_len[1] ? md->feet_step_len[0] : md->feet_step_len[1];
+    md->feet_step_len[0] *= (real)0.99f;
+    md->feet_step_len[1] *= (real)0.99f;
+    md->feet_f_last[0] = feetF[0];
+    md->feet_f_last[1] = feetF[1];
+    r[ZB_V4_R_STEP_LENGTH] = (real)tanh((double)(15 * mn));
+    /* feet_air_time_biped (1129-1143) */
+    const int in0 = P->con_cur[0] > 0, in1 = P->con_cur[1] > 0;
+    const int single = in0 + in1 == 1;
+    real m0 = single ? (in0 ? P->con_cur[0] : P->air_cur[0]) : 0;
+    real m1 = single ? (in1 ? P->con_cur[1] : P->air_cur[1]) : 0;
+    real bi = m0 < m1 ? m0 : m1;
+    r[ZB_V4_R_FEET_AIR_TIME_BIPED] = bi > 2 ? 2 : bi;
+    /* airtime_variance (1097-1103): torch.var (unbiased) of two values = (a - b)^2 / 2 */
+    const real a0 = P->air_last[0] < (real)0.5 ? P->air_last[0] : (real)0.5;
+    const real a1 = P->air_last[1] < (real)0.5 ? P->air_last[1] : (real)0.5;
+    const real c0 = P->con_last[0] < (real)0.5 ? P->con_last[0] : (real)0.5;
+    const real c1 = P->con_last[1] < (real)0.5 ? P->con_last[1] : (real)0.5;
+    r[ZB_V4_R_AIRTIME_VARIANCE] = (real)0.5 * (a0 - a1) * (a0 - a1) + (real)0.5 * (c0 - c1) * (c0 - c1);
+    real sl = 0;
+    for (int f = 0; f < 2; ++f) {
+      const real v = sqrtr(P->feet_com_vel[f][0] * P->feet_com_vel[f][0] + P->feet_com_vel[f][1] * P->feet_com_vel[f][1]);
+      sl += v * (feetF[f] > (real)1.0 ? (real)1 : (real)0);
+    }
+    r[ZB_V4_R_FEET_SLIDE] = sl;
+    r[ZB_V4_R_FEET_HARMONY] = (P->air_last[0] + P->air_last[1]) - 3 * (real)fabs((double)(P->air_last[0] - P->air_last[1]));
+    const real dx = P->feet_pos[0][0] - P->feet_pos[1][0], dy = P->feet_pos[0][1] - P->feet_pos[1][1];
+    const real cl = (real)0.115f - sqrtr(dx * dx + dy * dy);
+    r[ZB_V4_R_FEET_CLOSE] = cl > 0 ? cl : 0;
+  }
+  const real step_dt = (real)(cfg->sim_dt * (float)cfg->decimation);
+  real rew = 0;
+  for (int t = 0; t < ZB_V4_NUM_REWARD_TERMS; ++t) {
+    const real v = (r[t] * (real)cfg->stage_scales[stage][t]) * step_dt;
+    terms[t] = v;
+    rew += v;
+    md->ep_sums[t] += v;
+  }
+  if (died) rew -= cfg->terminal_penalty;
+  *died_out = died;
+  *tout_out = time_out;
+  aux->cur_yaw = cur_yaw;
+  aux->heading_err = he;
+  return rew;
+}
+
+/* ContactSensor update (history 3; last_contact_time tracked, v4.py:522-527) */
+static void v4_sensor_update(const mdl_t* m, const zb_task_cfg* cfg, mdp_t* md, const real F[NL][3]) {
+  for (int h = ZB_V4_HIST - 1; h > 0; --h) {
+    md->feet_fz_hist[h][0] = md->feet_fz_hist[h - 1][0];
+    md->feet_fz_hist[h][1] = md->feet_fz_hist[h - 1][1];
+    md->undes_fmax_hist[h] = md->undes_fmax_hist[h - 1];
+  }
+  real fmax = 0;
+  for (int k = 0; k < 10; ++k) {
+    const real* f = F[m->undesired[k]];
+    const real nrm = sqrtr(v3_dot(f, f));
+    if (nrm > fmax) fmax = nrm;
+  }
+  md->undes_fmax_hist[0] = fmax;
+  const real el = cfg->sim_dt * (real)cfg->decimation;
+  for (int f = 0; f < 2; ++f) {
+    const real* Ff = F[m->foot_links[f]];
+    md->feet_fz_hist[0][f] = Ff[2];
+    const int c = sqrtr(v3_dot(Ff, Ff)) > cfg->contact_force_threshold;
+    if (md->feet_air_cur[f] > 0 && c) md->feet_air_last[f] = md->feet_air_cur[f] + el;
+    md->feet_air_cur[f] = c ? 0 : md->feet_air_cur[f] + el;
+    if (md->feet_contact_cur[f] > 0 && !c) md->feet_contact_last[f] = md->feet_contact_cur[f] + el;
+    md->feet_contact_cur[f] = c ? md->feet_contact_cur[f] + el : 0;
+  }
+}
+
+/* _reset_idx (920-1001) minus the log: reset events (pose; commands), defaults. init: the
+ * construction-time interval timer draw. */
+static void v4_reset_env(const zbo_sim* s, uint64_t ctr, int i, env_t* e, int init) {
+  const mdl_t* m = &s->m;
+  const uint64_t h = env_hash(s->seed, ctr, i);
+  mdp_t* md = &e->md;
+  md->current_yaw = reset_pose(m, &s->c, h, &e->ph);
+  v4_resample(s, h, 5, md->current_yaw, md->commands, &md->target_yaw);
+  if (init) md->interval_left = draw(h, 8) * (s->c.cmd_interval_s[1] - s->c.cmd_interval_s[0]) + s->c.cmd_interval_s[0];
+  for (int j = 0; j < ND; ++j) { md->p_delta[j] = 0; md->actions[j] = 0; }
+  kin_t k;
+  fk(m, &e->ph, &k);
+  for (int f = 0; f < 2; ++f) {
+    real p[3], q[4];
+    link_pose(m, &k, m->foot_links[f], p, q);
+    for (int a = 0; a < 3; ++a) md->feet_down_pos[f][a] = p[a] + e->ph.root_pos[a];
+    md->feet_f_last[f] = s->c.feet_f_last_init;
+    md->feet_step_len[f] = 0;
+    md->feet_air_cur[f] = md->feet_air_last[f] = md->feet_contact_cur[f] = md->feet_contact_last[f] = 0;
+  }
+  for (int h2 = 0; h2 < ZB_HIST; ++h2) { md->feet_fz_hist[h2][0] = md->feet_fz_hist[h2][1] = 0; md->undes_fmax_hist[h2] = 0; }
+  md->ep_len = 0;
+  for (int t = 0; t < ZB_MAX_REWARD_TERMS; ++t) md->ep_sums[t] = 0;
+}
+
+static void v4_write_obs(const mdl_t* m, const env_t* e, float* obs) {
+  kin_t k;
+  fk(m, &e->ph, &k);
+  real p[3], q[4];
+  link_pose(m, &k, m->base_link, p, q);
+  for (int a = 0; a < 4; ++a) obs[a] = (float)q[a];
+  for (int j = 0; j < ND; ++j) {
+    obs[4 + j] = (float)(e->ph.jq[j] - m->jq0[j]);
+    obs[10 + j] = (float)e->ph.jqd[j];
+    obs[16 + j] = (float)e->md.actions[j];
+  }
+  obs[22] = (float)e->md.commands[0];
+  const double d = (double)(e->md.target_yaw - e->md.current_yaw);
+  obs[23] = (float)atan2(sin(d), cos(d));
+}
+
+static real v4_step_env(const zbo_sim* s, int stage, uint64_t ctr, int i, env_t* e, const float* action, float* obs,
+                        int* died, int* tout, real acc[ZB_MAX_REWARD_TERMS]) {
+  const mdl_t* m = &s->m;
+  const zb_task_cfg* cfg = &s->c;
+  mdp_t* md = &e->md;
+  real act[ND], prev[ND], target[ND];
+  const real step_dt = (real)(cfg->sim_dt * (float)cfg->decimation);
+  for (int j = 0; j < ND; ++j) {
+    prev[j] = md->actions[j];
+    act[j] = (real)tanh((double)action[j]);
+    md->p_delta[j] = clampr(md->p_delta[j] + (real)PI_R * act[j] * cfg->joint_speed_limit * step_dt, -(real)PI_R,
+                            (real)PI_R);
+    target[j] = md->p_delta[j] + m->jq0[j];
+  }
+  substep_out_t so;
+  real jqd_prev[ND];
+  for (int k = 0; k < cfg->decimation; ++k) {
+    if (k == cfg->decimation - 1)
+      for (int j = 0; j < ND; ++j) jqd_prev[j] = e->ph.jqd[j];
+    substep(m, cfg, &e->ph, target, NULL, &so);
+  }
+  v4_sensor_update(m, cfg, md, so.net_force);
+  md->ep_len += 1;
+  v4_post_t P;
+  {
+    kin_t k;
+    fk(m, &e->ph, &k);
+    real V[NB][6], q[4];
+    body_vel(&k, &e->ph, V);
+    link_pose(m, &k, m->base_link, P.base_pos, P.base_quat);
+    const int bb = m->link_body[m->base_link];
+    real x[3];
+    m3_v(k.R[bb], m->link_pos[m->base_link], x);
+    for (int a = 0; a < 3; ++a) x[a] += k.p[bb][a];
+    point_vel(V[bb], x, P.base_lin_vel); /* link-origin velocity */
+    for (int a = 0; a < 3; ++a) P.base_pos[a] += e->ph.root_pos[a];
+    for (int f = 0; f < 2; ++f) {
+      const int l = m->foot_links[f], b = m->link_body[l];
+      link_pose(m, &k, l, P.feet_pos[f], P.feet_quat[f]);
+      for (int a = 0; a < 3; ++a) P.feet_pos[f][a] += e->ph.root_pos[a];
+      real c[3];
+      m3_v(k.R[b], m->link_com[l], c);
+      for (int a = 0; a < 3; ++a) c[a] += k.p[b][a];
+      point_vel(V[b], c, P.feet_com_vel[f]);
+    }
+    (void)q;
+  }
+  for (int j = 0; j < ND; ++j) {
+    P.jqd[j] = e->ph.jqd[j];
+    P.joint_acc[j] = (e->ph.jqd[j] - jqd_prev[j]) / (real)cfg->sim_dt;
+    P.applied_torque[j] = so.applied_torque[j];
+  }
+  for (int h = 0; h < ZB_V4_HIST; ++h) {
+    P.fz_hist[h][0] = md->feet_fz_hist[h][0];
+    P.fz_hist[h][1] = md->feet_fz_hist[h][1];
+    P.undes_fmax_hist[h] = md->undes_fmax_hist[h];
+  }
+  for (int f = 0; f < 2; ++f) {
+    P.air_cur[f] = md->feet_air_cur[f]; P.con_cur[f] = md->feet_contact_cur[f];
+    P.air_last[f] = md->feet_air_last[f]; P.con_last[f] = md->feet_contact_last[f];
+  }
+  P.ep_len = md->ep_len;
+  for (int j = 0; j < ND; ++j) md->actions[j] = act[j];
+  real terms[ZB_V4_NUM_REWARD_TERMS];
+  v4_aux_t aux;
+  const real rew = v4_mdp_eval(cfg, stage, &P, md, act, prev, terms, died, tout, &aux);
+  md->current_yaw = aux.cur_yaw;
+  const uint64_t h = env_hash(s->seed, ctr, i);
+  if (*died || *tout) {
+    real dur = (real)md->ep_len * step_dt;
+    if (dur < step_dt) dur = step_dt;
+    for (int t = 0; t < ZB_V4_NUM_REWARD_TERMS; ++t) acc[t] += md->ep_sums[t] / dur;
+    v4_reset_env(s, ctr, i, e, 0);
+  }
+  /* interval_command_resample (after the resets; v4.py:426-439) */
+  md->interval_left -= step_dt;
+  if (md->interval_left < (real)1e-6) {
+    md->interval_left = draw(h, 8) * (cfg->cmd_interval_s[1] - cfg->cmd_interval_s[0]) + cfg->cmd_interval_s[0];
+    v4_resample(s, h, 9, md->current_yaw, md->commands, &md->target_yaw);
+  }
+  v4_write_obs(m, e, obs);
+  return rew;
+}
+
+static void v4_pack_env(const env_t* e, float* st, int n, int i) {
+#define PUT(off, val) st[(size_t)(off) * n + i] = (float)(val)
+  for (int a = 0; a < 3; ++a) { PUT(ZB_S_ROOT_POS + a, e->ph.root_pos[a]); PUT(ZB_S_ROOT_LINVEL + a, e->ph.root_linvel[a]); PUT(ZB_S_ROOT_ANGVEL + a, e->ph.root_angvel[a]); }
+  for (int a = 0; a < 4; ++a) PUT(ZB_S_ROOT_QUAT + a, e->ph.root_quat[a]);
+  for (int j = 0; j < ND; ++j) {
+    PUT(ZB_S_JOINT_POS + j, e->ph.jq[j]); PUT(ZB_S_JOINT_VEL + j, e->ph.jqd[j]);
+    PUT(ZB_V4_P_DELTA + j, e->md.p_delta[j]); PUT(ZB_V4_ACTIONS + j, e->md.actions[j]);
+  }
+  PUT(ZB_V4_COMMANDS, e->md.commands[0]); PUT(ZB_V4_COMMANDS + 1, e->md.commands[1]);
+  PUT(ZB_V4_TARGET_YAW, e->md.target_yaw); PUT(ZB_V4_INTERVAL_LEFT, e->md.interval_left);
+  PUT(ZB_V4_CURRENT_YAW, e->md.current_yaw);
+  for (int f = 0; f < 2; ++f) {
+    for (int a = 0; a < 3; ++a) PUT(ZB_V4_FEET_DOWN_POS + 3 * f + a, e->md.feet_down_pos[f][a]);
+    PUT(ZB_V4_FEET_STEP_LEN + f, e->md.feet_step_len[f]);
+    PUT(ZB_V4_FEET_F_LAST + f, e->md.feet_f_last[f]);
+    PUT(ZB_V4_FEET_AIR_CUR + f, e->md.feet_air_cur[f]);
+    PUT(ZB_V4_FEET_CONTACT_CUR + f, e->md.feet_contact_cur[f]);
+    PUT(ZB_V4_FEET_AIR_LAST + f, e->md.feet_air_last[f]);
+    PUT(ZB_V4_FEET_CONTACT_LAST + f, e->md.feet_contact_last[f]);
+    for (int h = 0; h < ZB_V4_HIST; ++h) PUT(ZB_V4_FEET_FZ_HIST + 2 * h + f, e->md.feet_fz_hist[h][f]);
+  }
+  for (int h = 0; h < ZB_V4_HIST; ++h) PUT(ZB_V4_UNDES_FMAX_HIST + h, e->md.undes_fmax_hist[h]);
+  PUT(ZB_V4_EP_LEN, e->md.ep_len);
+  for (int t = 0; t < ZB_V4_NUM_REWARD_TERMS; ++t) PUT(ZB_V4_EP_SUMS + t, e->md.ep_sums[t]);
+#undef PUT
+}
+static void v4_unpack_env(env_t* e, const float* st, int n, int i) {
+#define GET(off) ((real)st[(size_t)(off) * n + i])
+  for (int a = 0; a < 3; ++a) { e->ph.root_pos[a] = GET(ZB_S_ROOT_POS + a); e->ph.root_linvel[a] = GET(ZB_S_ROOT_LINVEL + a); e->ph.root_angvel[a] = GET(ZB_S_ROOT_ANGVEL + a); }
+  for (int a = 0; a < 4; ++a) e->ph.root_quat[a] = GET(ZB_S_ROOT_QUAT + a);
+  for (int j = 0; j < ND; ++j) {
+    e->ph.jq[j] = GET(ZB_S_JOINT_POS + j); e->ph.jqd[j] = GET(ZB_S_JOINT_VEL + j);
+    e->md.p_delta[j] = GET(ZB_V4_P_DELTA + j); e->md.actions[j] = GET(ZB_V4_ACTIONS + j);
+  }
+  e->md.commands[0] = GET(ZB_V4_COMMANDS); e->md.commands[1] = GET(ZB_V4_COMMANDS + 1);
+  e->md.target_yaw = GET(ZB_V4_TARGET_YAW); e->md.interval_left = GET(ZB_V4_INTERVAL_LEFT);
+  e->md.current_yaw = GET(ZB_V4_CURRENT_YAW);
+  for (int f = 0; f < 2; ++f) {
+    for (int a = 0; a < 3; ++a) e->md.feet_down_pos[f][a] = GET(ZB_V4_FEET_DOWN_POS + 3 * f + a);
+    e->md.feet_step_len[f] = GET(ZB_V4_FEET_STEP_LEN + f);
+    e->md.feet_f_last[f] = GET(ZB_V4_FEET_F_LAST + f);
+    e->md.feet_air_cur[f] = GET(ZB_V4_FEET_AIR_CUR + f);
+    e->md.feet_contact_cur[f] = GET(ZB_V4_FEET_CONTACT_CUR + f);
+    e->md.feet_air_last[f] = GET(ZB_V4_FEET_AIR_LAST + f);
+    e->md.feet_contact_last[f] = GET(ZB_V4_FEET_CONTACT_LAST + f);
+    for (int h = 0; h < ZB_V4_HIST; ++h) e->md.feet_fz_hist[h][f] = GET(ZB_V4_FEET_FZ_HIST + 2 * h + f);
+  }
+  for (int h = 0; h < ZB_V4_HIST; ++h) e->md.undes_fmax_hist[h] = GET(ZB_V4_UNDES_FMAX_HIST + h);
+  e->md.ep_len = (int32_t)lrint((double)st[(size_t)ZB_V4_EP_LEN * n + i]);
+  for (int t = 0; t < ZB_V4_NUM_REWARD_TERMS; ++t) e->md.ep_sums[t] = GET(ZB_V4_EP_SUMS + t);
+#undef GET
+}
+
+/* ========================================================================= call epilogue
+ * Mirror of the kernel's zb_finalize_kernel: episode log (means over reset envs; walking divides
+ * by the 20 s episode, the other tasks already divided per env), curriculum log entries (pre-event
+ * values), v4 range-curriculum buffers, my_curriculum, range_curriculum, full-reset ep_len draw. */
+static void curriculum_events(zbo_sim* s, int run_my, int run_range);
+
+static void finish_call(zbo_sim* s, int nres, const double* acc, double ep_s, int nterm, int ntout, int reset_counts,
+                        int full) {
+  const uint64_t ctr = s->call_counter;
+  const zb_task_cfg* c = &s->c;
+  if (nres > 0) {
+    float v[ZB_LOG_LEN];
+    for (int t = 0; t < ZB_MAX_REWARD_TERMS; ++t) v[t] = (float)(acc[t] / nres / ep_s);
+    v[16] = (float)s->stage;
+    v[17] = s->vel[0];
+    v[18] = s->vel[1];
+    v[19] = s->yaw[0];
+    for (int t = 0; t < ZB_LOG_LEN; ++t) s->log_means[t] = v[t];
+    s->log_counts[0] = reset_counts ? 0 : nterm;
+    s->log_counts[1] = reset_counts ? 0 : ntout;
+    if (c->task == ZB_TASK_WALKING_V4) {
+      s->ring_vel[s->ring_head] = v[ZB_V4_R_TRACK_LIN_VEL_X];
+      s->ring_yaw[s->ring_head] = v[ZB_V4_R_TRACK_HEADING_YAW];
+      s->ring_head = (s->ring_head + 1) % ZB_V4_RING;
+      if (s->ring_n < ZB_V4_RING) s->ring_n++;
+    }
+    curriculum_events(s, 1, 1);
+  }
+  s->call_counter++;
+  if (full)
+    for (int e = 0; e < s->n; ++e) /* episode_length_buf ~ U{0..max_episode_length-1} (v2.py:418-422) */
+      s->env[e].md.ep_len = (int32_t)(env_hash(s->seed, ctr, e) % (uint64_t)c->max_episode_length);
+}
+
+/* reset-mode curriculum events in EventCfg order: my_curriculum (one stage per call), then
+ * range_curriculum (v4) on the buffered per-call tracking rewards */
+static void curriculum_events(zbo_sim* s, int run_my, int run_range) {
+  const zb_task_cfg* c = &s->c;
+  {
+    if (run_my && s->stage + 1 < c->num_stages && s->steps >= (uint64_t)c->stage_steps[s->stage + 1]) {
+      s->stage++;
+      s->prob_pos = c->stage_prob_pos[s->stage];
+    }
+    /* range_curriculum (v4.py:201-265) */
+    if (run_range && c->task == ZB_TASK_WALKING_V4 && s->ring_n >= c->range_min_buffer && c->range_period_steps > 0 &&
+        s->steps >= (uint64_t)c->range_start_steps && s->steps % (uint64_t)c->range_period_steps == 0) {
+      float mv = 0, my = 0;
+      for (int k = 0; k < s->ring_n; ++k) { mv += s->ring_vel[k]; my += s->ring_yaw[k]; }
+      mv /= (float)s->ring_n;
+      my /= (float)s->ring_n;
+      if (mv > c->stage_scales[s->stage][ZB_V4_R_TRACK_LIN_VEL_X] * c->range_threshold) {
+        s->vel[0] = (float)clampr(s->vel[0] - c->range_delta, c->range_limit_vel[0], c->range_limit_vel[1]);
+        s->vel[1] = (float)clampr(s->vel[1] + c->range_delta, c->range_limit_vel[0], c->range_limit_vel[1]);
+      }
+      if (my > c->stage_scales[s->stage][ZB_V4_R_TRACK_HEADING_YAW] * c->range_threshold) {
+        s->yaw[0] = (float)clampr(s->yaw[0] - c->range_delta, c->range_limit_yaw[0], c->range_limit_yaw[1]);
+        s->yaw[1] = (float)clampr(s->yaw[1] + c->range_delta, c->range_limit_yaw[0], c->range_limit_yaw[1]);
+      }
+    }
+  }
 }
 
 /* ========================================================================= public API */
@@ -1157,17 +1591,22 @@ zbo_sim* zbo_create(const zb_model* model, const zb_task_cfg* cfg, int num_envs,
   s->c = *cfg;
   s->n = num_envs;
   s->seed = seed;
+  s->vel[0] = cfg->cmd_vel_range[0]; s->vel[1] = cfg->cmd_vel_range[1];
+  s->yaw[0] = cfg->cmd_yaw_range[0]; s->yaw[1] = cfg->cmd_yaw_range[1];
+  s->prob_pos = cfg->stage_prob_pos[0];
   s->env = (env_t*)calloc((size_t)num_envs, sizeof(env_t));
   for (int i = 0; i < num_envs; ++i) {
     memset(&s->env[i], 0, sizeof(env_t));
     if (cfg->task == ZB_TASK_STANDUP_V0) {
       for (int l = 0; l < NL; ++l) s->env[i].md.mu[l] = cfg->friction;
       su_reset_env(&s->m, cfg, seed, 0, i, &s->env[i]); /* construction draws at RNG position 0 */
+    } else if (cfg->task == ZB_TASK_WALKING_V4) {
+      v4_reset_env(s, 0, i, &s->env[i], 1);
     } else {
       reset_env(&s->m, &s->env[i]);
     }
   }
-  if (cfg->task == ZB_TASK_STANDUP_V0) s->call_counter = 1;
+  if (cfg->task != ZB_TASK_WALKING_V2) s->call_counter = 1;
   return s;
 }
 
@@ -1188,105 +1627,43 @@ int zbo_set_threads(int n) {
 }
 
 int zbo_reset(zbo_sim* s, const int32_t* env_ids, int n) {
-  int all = env_ids == NULL || n == s->n;
-  int cnt = env_ids ? n : s->n;
-  if (s->c.task == ZB_TASK_STANDUP_V0) {
-    const real step_dt = (real)(s->c.sim_dt * (float)s->c.decimation);
-    double accl[ZB_SU_NUM_REWARD_TERMS] = {0, 0, 0, 0};
-    const uint64_t ctr = s->call_counter;
-    for (int i = 0; i < cnt; ++i) {
-      int e = env_ids ? env_ids[i] : i;
-      real dur = (real)s->env[e].md.ep_len * step_dt;
-      if (dur < step_dt) dur = step_dt;
-      for (int t = 0; t < ZB_SU_NUM_REWARD_TERMS; ++t) accl[t] += s->env[e].md.ep_sums[t] / dur;
-      su_reset_env(&s->m, &s->c, s->seed, ctr, e, &s->env[e]);
-    }
-    for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t)
-      s->log_means[t] = (t < ZB_SU_NUM_REWARD_TERMS && cnt) ? (float)(accl[t] / cnt) : 0.f;
-    s->log_counts[0] = s->log_counts[1] = 0;
-    s->call_counter++;
-    su_curriculum(s, cnt);
-    if (all)
-      for (int e = 0; e < s->n; ++e) {
-        uint64_t h = zb_hash64(s->seed ^ zb_hash64(ctr * 0x100000001B3ull + (uint64_t)e));
-        s->env[e].md.ep_len = (int32_t)(h % (uint64_t)s->c.max_episode_length);
-      }
-    return 0;
-  }
-  for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) s->log_means[t] = 0;
+  const int all = env_ids == NULL || n == s->n;
+  const int cnt = env_ids ? n : s->n;
+  const uint64_t ctr = s->call_counter;
+  const real step_dt = (real)(s->c.sim_dt * (float)s->c.decimation);
+  double acc[ZB_MAX_REWARD_TERMS];
+  for (int t = 0; t < ZB_MAX_REWARD_TERMS; ++t) acc[t] = 0;
   for (int i = 0; i < cnt; ++i) {
-    int e = env_ids ? env_ids[i] : i;
-    for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) s->log_means[t] += (float)s->env[e].md.ep_sums[t];
-    reset_env(&s->m, &s->env[e]);
-  }
-  const float ep_s = s->c.sim_dt * s->c.decimation * s->c.max_episode_length;
-  for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) s->log_means[t] = cnt ? s->log_means[t] / cnt / ep_s : 0;
-  s->log_counts[0] = s->log_counts[1] = 0;
-  uint64_t ctr = s->call_counter++;
-  if (all) {
-    /* v2.py:418-422 episode_length_buf ~ U{0..max_episode_length-1} */
-    for (int e = 0; e < s->n; ++e) {
-      uint64_t h = zb_hash64(s->seed ^ zb_hash64(ctr * 0x100000001B3ull + (uint64_t)e));
-      s->env[e].md.ep_len = (int32_t)(h % (uint64_t)s->c.max_episode_length);
+    const int e = env_ids ? env_ids[i] : i;
+    env_t* en = &s->env[e];
+    if (s->c.task == ZB_TASK_WALKING_V2) {
+      for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) acc[t] += en->md.ep_sums[t];
+      reset_env(&s->m, en);
+    } else {
+      real dur = (real)en->md.ep_len * step_dt;
+      if (dur < step_dt) dur = step_dt;
+      for (int t = 0; t < ZB_MAX_REWARD_TERMS; ++t) acc[t] += en->md.ep_sums[t] / dur;
+      if (s->c.task == ZB_TASK_STANDUP_V0) su_reset_env(&s->m, &s->c, s->seed, ctr, e, en);
+      else v4_reset_env(s, ctr, e, en, 0);
     }
   }
+  const double ep_s = s->c.task == ZB_TASK_WALKING_V2 ? s->c.sim_dt * s->c.decimation * s->c.max_episode_length : 1.0;
+  finish_call(s, cnt, acc, ep_s, 0, 0, 1, all);
   return 0;
 }
 
 int zbo_observe(zbo_sim* s, float* obs) {
-  if (s->c.task == ZB_TASK_STANDUP_V0) {
-    for (int e = 0; e < s->n; ++e) su_write_obs(&s->m, &s->env[e], obs + (size_t)e * ZB_SU_OBS_DIM);
-    return 0;
+  for (int e = 0; e < s->n; ++e) {
+    if (s->c.task == ZB_TASK_STANDUP_V0) su_write_obs(&s->m, &s->env[e], obs + (size_t)e * ZB_SU_OBS_DIM);
+    else if (s->c.task == ZB_TASK_WALKING_V4) v4_write_obs(&s->m, &s->env[e], obs + (size_t)e * ZB_V4_OBS_DIM);
+    else write_obs(&s->m, &s->env[e], obs + (size_t)e * ZB_OBS_DIM);
   }
-  for (int e = 0; e < s->n; ++e) write_obs(&s->m, &s->env[e], obs + (size_t)e * ZB_OBS_DIM);
   return 0;
 }
 
-static int su_step(zbo_sim* s, const float* actions, float* obs, float* reward, uint8_t* terminated,
-                   uint8_t* truncated) {
-  double acc[ZB_SU_NUM_REWARD_TERMS] = {0, 0, 0, 0};
-  int nreset = 0, nterm = 0, ntout = 0;
-  const uint64_t ctr = s->call_counter;
-  const int stage = s->stage;
-  s->steps++; /* DirectRLEnv.step: common_step_counter += 1 before dones / rewards / resets */
-#pragma omp parallel
-  {
-    real acc_l[ZB_SU_NUM_REWARD_TERMS] = {0, 0, 0, 0};
-    int nr = 0, nt = 0, no = 0;
-#pragma omp for schedule(static)
-    for (int e = 0; e < s->n; ++e) {
-      int died = 0, tout = 0;
-      reward[e] = (float)su_step_env(&s->m, &s->c, stage, s->seed, ctr, e, &s->env[e], actions + (size_t)e * ZB_ACT_DIM,
-                                     obs + (size_t)e * ZB_SU_OBS_DIM, &died, &tout, acc_l);
-      terminated[e] = (uint8_t)died;
-      truncated[e] = (uint8_t)tout;
-      nr += died || tout; nt += died; no += tout;
-    }
-#pragma omp critical
-    {
-      for (int t = 0; t < ZB_SU_NUM_REWARD_TERMS; ++t) acc[t] += acc_l[t];
-      nreset += nr; nterm += nt; ntout += no;
-    }
-  }
-  if (nreset > 0) {
-    for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t)
-      s->log_means[t] = t < ZB_SU_NUM_REWARD_TERMS ? (float)(acc[t] / nreset) : 0.f;
-    s->log_counts[0] = nterm;
-    s->log_counts[1] = ntout;
-  }
-  s->call_counter++;
-  su_curriculum(s, nreset);
-  if (nreset == s->n)
-    for (int e = 0; e < s->n; ++e) {
-      uint64_t h = zb_hash64(s->seed ^ zb_hash64(ctr * 0x100000001B3ull + (uint64_t)e));
-      s->env[e].md.ep_len = (int32_t)(h % (uint64_t)s->c.max_episode_length);
-    }
-  return 0;
-}
-
-/* full policy step for env e; returns reward, sets flags; accumulates log into acc[15] */
+/* full walking-v2 policy step for env e; returns reward, sets flags; accumulates the log */
 static real step_env(const mdl_t* m, const zb_task_cfg* cfg, env_t* e, const float* action, float* obs,
-                     int* died, int* tout, real acc[ZB_NUM_REWARD_TERMS]) {
+                     int* died, int* tout, real acc[ZB_MAX_REWARD_TERMS]) {
   mdp_t* md = &e->md;
   /* _pre_physics_step (v2.py:276-287) */
   real act[ND], prev[ND], target[ND];
@@ -1343,50 +1720,46 @@ static real step_env(const mdl_t* m, const zb_task_cfg* cfg, env_t* e, const flo
 }
 
 int zbo_step(zbo_sim* s, const float* actions, float* obs, float* reward, uint8_t* terminated, uint8_t* truncated) {
-  if (s->c.task == ZB_TASK_STANDUP_V0) return su_step(s, actions, obs, reward, terminated, truncated);
-  s->steps++;
-  real acc[ZB_NUM_REWARD_TERMS];
-  for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) acc[t] = 0;
+  double acc[ZB_MAX_REWARD_TERMS];
+  for (int t = 0; t < ZB_MAX_REWARD_TERMS; ++t) acc[t] = 0;
   int nreset = 0, nterm = 0, ntout = 0;
+  const uint64_t ctr = s->call_counter;
+  const int stage = s->stage;
+  const int task = s->c.task;
+  const int od = task == ZB_TASK_STANDUP_V0 ? ZB_SU_OBS_DIM : task == ZB_TASK_WALKING_V4 ? ZB_V4_OBS_DIM : ZB_OBS_DIM;
+  s->steps++; /* DirectRLEnv.step: common_step_counter += 1 before dones / rewards / resets */
 #pragma omp parallel
   {
-    real acc_l[ZB_NUM_REWARD_TERMS];
+    real acc_l[ZB_MAX_REWARD_TERMS];
     int nr = 0, nt = 0, no = 0;
-    for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) acc_l[t] = 0;
+    for (int t = 0; t < ZB_MAX_REWARD_TERMS; ++t) acc_l[t] = 0;
 #pragma omp for schedule(static)
     for (int e = 0; e < s->n; ++e) {
       int died = 0, tout = 0;
-      reward[e] = (float)step_env(&s->m, &s->c, &s->env[e], actions + (size_t)e * ZB_ACT_DIM,
-                                  obs + (size_t)e * ZB_OBS_DIM, &died, &tout, acc_l);
+      const float* a = actions + (size_t)e * ZB_ACT_DIM;
+      float* o = obs + (size_t)e * od;
+      real r;
+      if (task == ZB_TASK_STANDUP_V0) r = su_step_env(&s->m, &s->c, stage, s->seed, ctr, e, &s->env[e], a, o, &died, &tout, acc_l);
+      else if (task == ZB_TASK_WALKING_V4) r = v4_step_env(s, stage, ctr, e, &s->env[e], a, o, &died, &tout, acc_l);
+      else r = step_env(&s->m, &s->c, &s->env[e], a, o, &died, &tout, acc_l);
+      reward[e] = (float)r;
       terminated[e] = (uint8_t)died;
       truncated[e] = (uint8_t)tout;
       nr += died || tout; nt += died; no += tout;
     }
 #pragma omp critical
     {
-      for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) acc[t] += acc_l[t];
+      for (int t = 0; t < ZB_MAX_REWARD_TERMS; ++t) acc[t] += acc_l[t];
       nreset += nr; nterm += nt; ntout += no;
     }
   }
-  if (nreset > 0) {
-    const float ep_s = s->c.sim_dt * s->c.decimation * s->c.max_episode_length;
-    for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) s->log_means[t] = (float)(acc[t] / nreset / ep_s);
-    s->log_counts[0] = nterm;
-    s->log_counts[1] = ntout;
-  }
-  uint64_t ctr = s->call_counter++;
-  if (nreset == s->n) {
-    /* every env reset in this step: _reset_idx saw len(env_ids) == num_envs (v2.py:418-422) */
-    for (int e = 0; e < s->n; ++e) {
-      uint64_t h = zb_hash64(s->seed ^ zb_hash64(ctr * 0x100000001B3ull + (uint64_t)e));
-      s->env[e].md.ep_len = (int32_t)(h % (uint64_t)s->c.max_episode_length);
-    }
-  }
+  const double ep_s = task == ZB_TASK_WALKING_V2 ? s->c.sim_dt * s->c.decimation * s->c.max_episode_length : 1.0;
+  finish_call(s, nreset, acc, ep_s, nterm, ntout, 0, nreset == s->n);
   return 0;
 }
 
 int zbo_read_log(zbo_sim* s, float* term_means, int32_t* counts) {
-  for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) term_means[t] = s->log_means[t];
+  for (int t = 0; t < ZB_LOG_LEN; ++t) term_means[t] = s->log_means[t];
   counts[0] = s->log_counts[0];
   counts[1] = s->log_counts[1];
   return 0;
@@ -1451,16 +1824,20 @@ static void unpack_env(env_t* e, const float* st, int n, int i) {
 int zbo_get_state(zbo_sim* s, float* dst) {
   for (int e = 0; e < s->n; ++e)
     if (s->c.task == ZB_TASK_STANDUP_V0) su_pack_env(&s->env[e], dst, s->n, e);
+    else if (s->c.task == ZB_TASK_WALKING_V4) v4_pack_env(&s->env[e], dst, s->n, e);
     else pack_env(&s->env[e], dst, s->n, e);
   return 0;
 }
 int zbo_set_state(zbo_sim* s, const float* src) {
   for (int e = 0; e < s->n; ++e)
     if (s->c.task == ZB_TASK_STANDUP_V0) su_unpack_env(&s->env[e], src, s->n, e);
+    else if (s->c.task == ZB_TASK_WALKING_V4) v4_unpack_env(&s->env[e], src, s->n, e);
     else unpack_env(&s->env[e], src, s->n, e);
   return 0;
 }
-int zbo_state_dim(zbo_sim* s) { return s->c.task == ZB_TASK_STANDUP_V0 ? ZB_SU_STATE_DIM : ZB_STATE_DIM; }
+int zbo_state_dim(zbo_sim* s) {
+  return s->c.task == ZB_TASK_STANDUP_V0 ? ZB_SU_STATE_DIM : s->c.task == ZB_TASK_WALKING_V4 ? ZB_V4_STATE_DIM : ZB_STATE_DIM;
+}
 
 /* standup: per-link friction [n][12] */
 int zbo_set_link_friction(zbo_sim* s, const float* mu) {
@@ -1724,16 +2101,136 @@ int zbo_su_reset_pose(const zb_model* model, const zb_task_cfg* cfg, uint64_t se
 }
 
 /* root pose from reset_root_state_uniform samples [n][4] = (x, y, roll, yaw) */
-int zbo_su_pose_from_samples(const zb_model* model, int n, const float* samples, float* pos, float* quat) {
+int zbo_su_pose_from_samples(const zb_model* model, int n, const float* samples, int body_frame, float* pos,
+                             float* quat) {
   mdl_t m;
   load_mdl(model, &m);
   for (int e = 0; e < n; ++e) {
     phys_t p;
     real r[4];
     for (int k = 0; k < 4; ++k) r[k] = samples[(size_t)e * 4 + k];
-    su_pose_from_samples(&m, r, &p);
+    pose_from_samples(&m, r, body_frame, &p);
     for (int a = 0; a < 3; ++a) pos[(size_t)e * 3 + a] = (float)p.root_pos[a];
     for (int a = 0; a < 4; ++a) quat[(size_t)e * 4 + a] = (float)p.root_quat[a];
   }
+  return 0;
+}
+
+/* ------------------------------------------------------------------ v4 golden-vector entry points */
+
+/* v4 _get_dones + _get_rewards on Isaac-Lab-shaped data (tests/test_oracle_v4.py):
+ * link_pos [n][12][3], link_quat [n][12][4], link_lin_vel [n][12][3] (body_link_lin_vel_w),
+ * com_lin_vel [n][12][3] (body_com_lin_vel_w), joint_vel / joint_acc / applied_torque [n][6],
+ * net_forces_hist [n][3][12][3], sensor times [n][12] x 4 (current air, current contact, last air,
+ * last contact), ep_len [n] (after += 1), actions / prev actions [n][6]; in/out commands [n][2],
+ * target_yaw [n], feet_down_pos [n][2][3], feet_step_len [n][2], feet_f_last [n][2], ep_sums [n][15]. */
+int zbo_v4_mdp_eval(int n, const zb_task_cfg* cfg, int stage, const zb_model* model, const float* link_pos,
+                    const float* link_quat, const float* link_lin_vel, const float* com_lin_vel, const float* joint_vel,
+                    const float* joint_acc, const float* applied_torque, const float* net_forces_hist,
+                    const float* air_cur, const float* con_cur, const float* air_last, const float* con_last,
+                    const int32_t* ep_len, const float* act, const float* prev_act, const float* commands,
+                    const float* target_yaw, float* feet_down_pos, float* feet_step_len, float* feet_f_last,
+                    float* ep_sums, float* reward, float* terms, uint8_t* died, uint8_t* time_out, float* cur_yaw,
+                    float* heading_err) {
+  mdl_t m;
+  load_mdl(model, &m);
+  for (int e = 0; e < n; ++e) {
+    v4_post_t P;
+    const int B = m.base_link;
+    for (int a = 0; a < 3; ++a) {
+      P.base_pos[a] = link_pos[((size_t)e * NL + B) * 3 + a];
+      P.base_lin_vel[a] = link_lin_vel[((size_t)e * NL + B) * 3 + a];
+    }
+    for (int a = 0; a < 4; ++a) P.base_quat[a] = link_quat[((size_t)e * NL + B) * 4 + a];
+    for (int f = 0; f < 2; ++f) {
+      const int l = m.foot_links[f];
+      for (int a = 0; a < 3; ++a) {
+        P.feet_pos[f][a] = link_pos[((size_t)e * NL + l) * 3 + a];
+        P.feet_com_vel[f][a] = com_lin_vel[((size_t)e * NL + l) * 3 + a];
+      }
+      for (int a = 0; a < 4; ++a) P.feet_quat[f][a] = link_quat[((size_t)e * NL + l) * 4 + a];
+      P.air_cur[f] = air_cur[(size_t)e * NL + l]; P.con_cur[f] = con_cur[(size_t)e * NL + l];
+      P.air_last[f] = air_last[(size_t)e * NL + l]; P.con_last[f] = con_last[(size_t)e * NL + l];
+    }
+    for (int j = 0; j < ND; ++j) {
+      P.jqd[j] = joint_vel[(size_t)e * ND + j];
+      P.joint_acc[j] = joint_acc[(size_t)e * ND + j];
+      P.applied_torque[j] = applied_torque[(size_t)e * ND + j];
+    }
+    for (int h = 0; h < ZB_V4_HIST; ++h) {
+      const float* F = net_forces_hist + ((size_t)e * ZB_V4_HIST + h) * NL * 3;
+      P.fz_hist[h][0] = F[m.foot_links[0] * 3 + 2];
+      P.fz_hist[h][1] = F[m.foot_links[1] * 3 + 2];
+      real fm = 0;
+      for (int k = 0; k < 10; ++k) {
+        const float* f3 = F + m.undesired[k] * 3;
+        const real nrm = sqrtr((real)f3[0] * f3[0] + (real)f3[1] * f3[1] + (real)f3[2] * f3[2]);
+        if (nrm > fm) fm = nrm;
+      }
+      P.undes_fmax_hist[h] = fm;
+    }
+    P.ep_len = ep_len[e];
+    mdp_t md;
+    memset(&md, 0, sizeof(md));
+    md.commands[0] = commands[(size_t)e * 2]; md.commands[1] = commands[(size_t)e * 2 + 1];
+    md.target_yaw = target_yaw[e];
+    for (int f = 0; f < 2; ++f) {
+      for (int a = 0; a < 3; ++a) md.feet_down_pos[f][a] = feet_down_pos[((size_t)e * 2 + f) * 3 + a];
+      md.feet_step_len[f] = feet_step_len[(size_t)e * 2 + f];
+      md.feet_f_last[f] = feet_f_last[(size_t)e * 2 + f];
+    }
+    for (int t = 0; t < ZB_V4_NUM_REWARD_TERMS; ++t) md.ep_sums[t] = ep_sums[(size_t)e * ZB_V4_NUM_REWARD_TERMS + t];
+    real a_[ND], p_[ND], tr[ZB_V4_NUM_REWARD_TERMS];
+    for (int j = 0; j < ND; ++j) { a_[j] = act[(size_t)e * ND + j]; p_[j] = prev_act[(size_t)e * ND + j]; }
+    int d = 0, to = 0;
+    v4_aux_t aux;
+    reward[e] = (float)v4_mdp_eval(cfg, stage, &P, &md, a_, p_, tr, &d, &to, &aux);
+    for (int t = 0; t < ZB_V4_NUM_REWARD_TERMS; ++t) {
+      terms[(size_t)e * ZB_V4_NUM_REWARD_TERMS + t] = (float)tr[t];
+      ep_sums[(size_t)e * ZB_V4_NUM_REWARD_TERMS + t] = (float)md.ep_sums[t];
+    }
+    for (int f = 0; f < 2; ++f) {
+      for (int a = 0; a < 3; ++a) feet_down_pos[((size_t)e * 2 + f) * 3 + a] = (float)md.feet_down_pos[f][a];
+      feet_step_len[(size_t)e * 2 + f] = (float)md.feet_step_len[f];
+      feet_f_last[(size_t)e * 2 + f] = (float)md.feet_f_last[f];
+    }
+    died[e] = (uint8_t)d;
+    time_out[e] = (uint8_t)to;
+    cur_yaw[e] = (float)aux.cur_yaw;
+    heading_err[e] = (float)aux.heading_err;
+  }
+  return 0;
+}
+
+/* resample_commands on given draws: params = {prob_pos, vel lo, vel hi, yaw lo, yaw hi, offset} */
+int zbo_v4_commands_from_draws(int n, const float* params, const float* u_sign, const float* u_vel, const float* u_yaw,
+                               const float* cur_yaw, float* cmd, float* target) {
+  const float vr[2] = {params[1], params[2]}, yr[2] = {params[3], params[4]};
+  for (int e = 0; e < n; ++e) {
+    real c[2], t;
+    v4_commands(1, params[0], vr, yr, params[5], u_sign[e], u_vel[e], u_yaw[e], cur_yaw[e], c, &t);
+    cmd[(size_t)e * 2] = (float)c[0];
+    cmd[(size_t)e * 2 + 1] = (float)c[1];
+    target[e] = (float)t;
+  }
+  return 0;
+}
+
+/* the reset-event curricula on a given counter state: io = {stage, prob_pos, vel lo, vel hi, yaw lo,
+ * yaw hi} in / out; the range buffers hold ring_n copies of (ring_vel, ring_yaw) */
+int zbo_curriculum_probe(const zb_task_cfg* cfg, int64_t steps, int run_my, int run_range, int ring_n, float ring_vel,
+                         float ring_yaw, float* io) {
+  zbo_sim s;
+  memset(&s, 0, sizeof(s));
+  s.c = *cfg;
+  s.steps = (uint64_t)steps;
+  s.stage = (int)io[0];
+  s.prob_pos = io[1];
+  s.vel[0] = io[2]; s.vel[1] = io[3]; s.yaw[0] = io[4]; s.yaw[1] = io[5];
+  s.ring_n = ring_n;
+  for (int k = 0; k < ring_n; ++k) { s.ring_vel[k] = ring_vel; s.ring_yaw[k] = ring_yaw; }
+  curriculum_events(&s, run_my, run_range);
+  io[0] = (float)s.stage; io[1] = s.prob_pos;
+  io[2] = s.vel[0]; io[3] = s.vel[1]; io[4] = s.yaw[0]; io[5] = s.yaw[1];
   return 0;
 }

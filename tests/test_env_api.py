@@ -84,17 +84,35 @@ def test_standup_registration_and_cfg():
     t = cfg.task_cfg()
     assert t.task == zm.TASK_STANDUP_V0 and t.max_episode_length == 300 and t.terminal_penalty == 2.0
     c = t.pack()
-    assert c.curriculum_steps == 24000 and c.task == 1
-    assert list(c.reward_scales[:4]) == [10.0, -1.0, -1.0, 0.0]       # weights; x step_dt in the kernel
-    assert list(c.curriculum_scales[:4]) == [10.0, -2.0, -1.0, 2.0]
+    assert c.num_stages == 2 and c.stage_steps[1] == 24000 and c.task == 1
+    assert list(c.stage_scales[0][:4]) == [10.0, -1.0, -1.0, 0.0]     # weights; x step_dt in the kernel
+    assert list(c.stage_scales[1][:4]) == [10.0, -2.0, -1.0, 2.0]
     np.testing.assert_allclose(np.array(c.reset_pose_range), [[-0.5, 0.5], [-0.5, 0.5], [-0.7854, 0.7854],
                                                               [-3.14, 3.14]], rtol=1e-6)
     cfg.events.my_curric = None                                       # play-script variant: no curriculum
-    assert cfg.task_cfg().pack().curriculum_steps == 0
+    assert cfg.task_cfg().pack().num_stages == 1
     agent = load_cfg("zbot-6b-standup-v0", "rsl_rl_cfg_entry_point")
     assert isinstance(agent, Zbot6SUpEnvPPOCfg)
     assert agent.to_dict()["policy"]["actor_hidden_dims"] == [256, 256, 128]
     assert agent.experiment_name == "zbot_6b_flat_direct_standup"
+
+
+def test_walking_v4_registration_and_cfg():
+    """zbot-6b-walking-v4 (reference __init__.py:91-99, Zbot6SEnvV4Cfg v4.py:443-686)."""
+    from zbot_lab_amd.rl import Zbot6SEnvV4PPOCfg
+    assert spec("zbot-6b-walking-v4").entry_point.endswith("Zbot6SEnvV4")
+    cfg = load_cfg("zbot-6b-walking-v4")
+    assert cfg.observation_space == 24 and cfg.contact_history_length == 3 and cfg.termination_height == 0.20
+    assert list(cfg.reward_cfg["reward_scales"]) == zm.V4_REWARD_TERMS
+    c = cfg.task_cfg().pack()
+    assert c.task == zm.TASK_WALKING_V4 and c.num_stages == 4 and list(c.stage_steps) == [0, 12000, 24000, 144000]
+    assert list(c.stage_prob_pos) == pytest.approx([1.0, 1.0, 0.8, 0.6])
+    assert (c.range_start_steps, c.range_period_steps, c.range_min_buffer) == (48000, 12000, 20)
+    assert list(c.range_limit_yaw) == [-0.5, 0.5] and c.undesired_force_threshold == 0.5
+    assert list(c.cmd_vel_range) == pytest.approx([0.3, 0.3]) and c.reset_pose_body_frame == 1
+    agent = load_cfg("zbot-6b-walking-v4", "rsl_rl_cfg_entry_point")
+    assert isinstance(agent, Zbot6SEnvV4PPOCfg) and agent.max_iterations == 2000
+    assert agent.to_dict()["policy"]["critic_hidden_dims"] == [256, 256, 128]
 
 
 def test_vecenv_wrapper_contract():

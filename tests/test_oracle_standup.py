@@ -30,7 +30,7 @@ def test_golden_metadata(gold):
     assert list(gold["term_names"]) == zm.SU_REWARD_TERMS
     cfg = zm.TaskCfg.standup()
     np.testing.assert_allclose(gold["weights_stage0"], [cfg.reward_weights[k] for k in zm.SU_REWARD_TERMS])
-    np.testing.assert_allclose(gold["weights_stage1"], [cfg.curriculum_weights[k] for k in zm.SU_REWARD_TERMS])
+    np.testing.assert_allclose(gold["weights_stage1"], [cfg.stage_weights()[1][k] for k in zm.SU_REWARD_TERMS])
     assert cfg.max_episode_length == int(gold["max_episode_length"]) == 300
     assert float(gold["episode_length_s"]) == cfg.episode_length_s
     assert int(gold["observation_space"]) == zm.SU_OBS_DIM
@@ -38,7 +38,7 @@ def test_golden_metadata(gold):
     # my_curriculum fires at common_step_counter >= max_episode_length * 80, not before
     thr = gold["curriculum_threshold"]
     assert [tuple(r) for r in thr] == [(23999, 0), (24000, 1), (24001, 1)]
-    assert cfg.pack().curriculum_steps == 24000
+    assert cfg.pack().num_stages == 2 and cfg.pack().stage_steps[1] == 24000
     # the golden run exercises every branch
     assert 0.1 < gold["died"].mean() < 0.9 and 0.05 < gold["time_out"].mean() < 0.5
     assert list(gold["stage"][:8]) == [0] * 8 and list(gold["stage"][8:]) == [1] * 8

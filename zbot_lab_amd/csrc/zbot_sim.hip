@@ -147,8 +147,12 @@ __device__ __forceinline__ float tanh_r(float x) {
 struct Counters {
   uint64_t calls;  // zb_step + zb_reset calls (RNG stream position of resets)
   uint64_t steps;  // zb_step calls (common_step_counter)
-  int32_t stage;   // curriculum stage (standup my_curriculum)
+  int32_t stage;   // curriculum stage (my_curriculum)
   int32_t pad;
+  // v4 command sampling state (resample_commands params, changed by the curricula)
+  float vel[2], yaw[2], prob_pos;
+  int32_t ring_n, ring_head;  // range_curriculum reward buffers (deque(maxlen=24))
+  float ring_vel[ZB_V4_RING], ring_yaw[ZB_V4_RING];
 };
 
 __host__ __device__ __forceinline__ uint64_t hash64(uint64_t x) {
@@ -457,9 +461,10 @@ __device__ __forceinline__ int xcd_block(int b, int nb) {
 constexpr int LINK4 = 10;
 constexpr int NPAIR = (NL - 1) * (NL - 2) / 2;  // non-adjacent link pairs (55), checked by zb_create
 constexpr int PAIRS_PER_LANE = (NPAIR + TL - 1) / TL;
-// default pose: feet positions, base quat, base quat relative to the root (zb_derive_kernel)
+// default pose (zb_derive_kernel): feet positions, base quat, base quat relative to the root, feet
+// positions in the root frame (at the default joint positions)
 constexpr int DFLT_OFF = NL * LINK4 + (NPAIR + 3) / 4;
-constexpr int JT_OFF = DFLT_OFF + 4;  // joints: {jpr}, {jpp}, {jcp}, {jcr}, {a_local = R(jpr) z}
+constexpr int JT_OFF = DFLT_OFF + 6;  // joints: {jpr}, {jpp}, {jcp}, {jcr}, {a_local = R(jpr) z}
 constexpr int BT_OFF = JT_OFF + ND * 5;  // bodies: {com, mass}, {Ixx, Iyy, Izz, Ixy}, {Ixz, Iyz, 0, 0}
 constexpr int LNK4 = BT_OFF + NB * 3;
 
@@ -1599,8 +1604,9 @@ __device__ __forceinline__ void write_obs(MP m, const Phys& p, const Mdp& d,
   o[22] = 1.0f;
 }
 
-// accumulator layout: [0..12] episode-sum totals of reset envs, [13] n_reset, [14] n_died, [15] n_timeout
-constexpr int ACC = 16;
+// accumulator layout: [0..15] episode-sum totals of reset envs, then n_reset, n_died, n_timeout
+constexpr int ACC_NRES = ZB_MAX_REWARD_TERMS, ACC_DIED = ACC_NRES + 1, ACC_TOUT = ACC_NRES + 2;
+constexpr int ACC = ACC_NRES + 4;
 
 // ------------------------------------------------------------------------- kernels
 __device__ __forceinline__ void load_phys(const float* __restrict__ st, int N, int i, Phys& p) {
@@ -1829,9 +1835,9 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_step_kernel(const z
     if (lead) {
 #pragma unroll
       for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) atomicAdd(&acc[t], sums[t]);   // v2.py:441-448
-      atomicAdd(&acc[13], 1.f);
-      if (died) atomicAdd(&acc[14], 1.f);
-      if (time_out) atomicAdd(&acc[15], 1.f);
+      atomicAdd(&acc[ACC_NRES], 1.f);
+      if (died) atomicAdd(&acc[ACC_DIED], 1.f);
+      if (time_out) atomicAdd(&acc[ACC_TOUT], 1.f);
     }
 #pragma unroll
     for (int a = 0; a < 3; ++a) { p.pos[a] = m->default_root_pos[a]; p.lv[a] = 0.f; p.av[a] = 0.f; }
@@ -1910,7 +1916,7 @@ __global__ void zb_reset_kernel(const zb_model* __restrict__ mg, const float4* _
   load_state(st, N, i, p, d);
 #pragma unroll
   for (int k = 0; k < ZB_NUM_REWARD_TERMS; ++k) atomicAdd(&acc[k], d.sums[k]);
-  atomicAdd(&acc[13], 1.f);
+  atomicAdd(&acc[ACC_NRES], 1.f);
   reset_env(m, links + DFLT_OFF, p, d);
   store_state(st, N, i, p, d);
 }
@@ -1938,42 +1944,86 @@ __global__ void zb_derive_kernel(const zb_model* __restrict__ mg, float4* __rest
   // base link orientation relative to the root at the default joint positions
 #pragma unroll
   for (int a = 0; a < 4; ++a) p.quat[a] = a == 0 ? 1.f : 0.f;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) p.pos[a] = 0.f;
   fk(m, p, k);
   link_pose(m, k, 6, bp, q0);
   links[DFLT_OFF + 3] = make_float4(q0[0], q0[1], q0[2], q0[3]);
+  link_pose(m, k, 0, f0, q0);
+  link_pose(m, k, 11, f1, q0);
+  links[DFLT_OFF + 4] = make_float4(f0[0], f0[1], f0[2], 0.f);
+  links[DFLT_OFF + 5] = make_float4(f1[0], f1[1], f1[2], 0.f);
 }
 
-// episode log finalisation + full-reset episode_length_buf draw (v2.py:418-422); leaves the
-// accumulator zeroed for the next launch. Single workgroup (grid-strided over envs).
-// The counters (RNG stream position, common_step_counter, curriculum stage) live on the device
-// so that a captured graph of zb_step advances them on every replay. my_curriculum
-// (standup.py:99-111) runs as a reset event: stage 0 -> 1 at the first call with resets once
-// common_step_counter >= curriculum_steps; the new weights apply from the next step's rewards.
+// Episode log finalisation, curricula and the full-reset episode_length_buf draw (v2.py:418-422);
+// leaves the accumulator zeroed for the next launch. Single workgroup (grid-strided over envs).
+// The counters (RNG stream position, common_step_counter, curriculum state) live on the device so
+// that a captured graph of zb_step advances them on every replay. Reset-mode events in the
+// reference's order (v4 EventCfg 268-439): the episode log and the range-curriculum buffers
+// (_reset_idx before the events), my_curriculum (one stage per call with resets once
+// common_step_counter >= stage_steps[next]), range_curriculum (v4: widen the command ranges when
+// the buffered tracking rewards exceed 85 % of their weight). New weights / ranges apply from the
+// next step (the reference applies the reset-event ones to the commands it resamples in the same
+// call).
 __global__ void zb_finalize_kernel(int N, float* __restrict__ st, float* __restrict__ acc,
                                    float* __restrict__ log_means, int32_t* __restrict__ log_counts,
                                    float* __restrict__ user_means, int32_t* __restrict__ user_counts, float episode_s,
-                                   int max_ep_len, uint64_t seed, Counters* __restrict__ cnt, int force_full,
-                                   int reset_counts, int is_step, int ep_len_row, int curriculum_steps) {
+                                   uint64_t seed, Counters* __restrict__ cnt, int force_full, int reset_counts,
+                                   int is_step, int ep_len_row, zb_task_cfg cfg) {
   const uint64_t ctr = cnt->calls;
   const uint64_t steps = cnt->steps + (is_step ? 1 : 0);
-  const float nres = acc[13];
+  const float nres = acc[ACC_NRES];
   const bool full = force_full || nres == (float)N;
   __syncthreads();
   if (threadIdx.x == 0) {
     cnt->steps = steps;
-    if (curriculum_steps > 0 && cnt->stage == 0 && nres > 0.f && steps >= (uint64_t)curriculum_steps) cnt->stage = 1;
-  }
-  if (threadIdx.x == 0 && nres > 0.f) {
+    if (nres > 0.f) {
+      float v[ZB_LOG_LEN];
 #pragma unroll
-    for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) {
-      const float v = acc[t] / nres / episode_s;
-      log_means[t] = v;
-      if (user_means) user_means[t] = v;
+      for (int t = 0; t < ZB_MAX_REWARD_TERMS; ++t) v[t] = acc[t] / nres / episode_s;
+      v[16] = (float)cnt->stage;  // logged before the events run (v4.py:952-957)
+      v[17] = cnt->vel[0];
+      v[18] = cnt->vel[1];
+      v[19] = cnt->yaw[0];
+#pragma unroll
+      for (int t = 0; t < ZB_LOG_LEN; ++t) {
+        log_means[t] = v[t];
+        if (user_means) user_means[t] = v[t];
+      }
+      const int32_t c0 = reset_counts ? 0 : (int32_t)acc[ACC_DIED], c1 = reset_counts ? 0 : (int32_t)acc[ACC_TOUT];
+      log_counts[0] = c0;
+      log_counts[1] = c1;
+      if (user_counts) { user_counts[0] = c0; user_counts[1] = c1; }
+      if (cfg.task == ZB_TASK_WALKING_V4) {  // curriculum_*_reward_buffer.append (v4.py:941-944)
+        cnt->ring_vel[cnt->ring_head] = v[ZB_V4_R_TRACK_LIN_VEL_X];
+        cnt->ring_yaw[cnt->ring_head] = v[ZB_V4_R_TRACK_HEADING_YAW];
+        cnt->ring_head = (cnt->ring_head + 1) % ZB_V4_RING;
+        cnt->ring_n = min(cnt->ring_n + 1, ZB_V4_RING);
+      }
+      // my_curriculum
+      const int s0 = cnt->stage;
+      if (s0 + 1 < cfg.num_stages && s0 + 1 < ZB_MAX_STAGES && steps >= (uint64_t)cfg.stage_steps[s0 + 1]) {
+        cnt->stage = s0 + 1;
+        cnt->prob_pos = cfg.stage_prob_pos[s0 + 1];
+      }
+      // range_curriculum (v4.py:201-265)
+      if (cfg.task == ZB_TASK_WALKING_V4 && cnt->ring_n >= cfg.range_min_buffer && cfg.range_period_steps > 0 &&
+          steps >= (uint64_t)cfg.range_start_steps && steps % (uint64_t)cfg.range_period_steps == 0) {
+        float mv = 0.f, my = 0.f;
+        for (int k = 0; k < cnt->ring_n; ++k) { mv += cnt->ring_vel[k]; my += cnt->ring_yaw[k]; }
+        mv /= (float)cnt->ring_n;
+        my /= (float)cnt->ring_n;
+        const int sg = cnt->stage;
+        if (mv > cfg.stage_scales[sg][ZB_V4_R_TRACK_LIN_VEL_X] * cfg.range_threshold) {
+          cnt->vel[0] = clampf(cnt->vel[0] - cfg.range_delta, cfg.range_limit_vel[0], cfg.range_limit_vel[1]);
+          cnt->vel[1] = clampf(cnt->vel[1] + cfg.range_delta, cfg.range_limit_vel[0], cfg.range_limit_vel[1]);
+        }
+        if (my > cfg.stage_scales[sg][ZB_V4_R_TRACK_HEADING_YAW] * cfg.range_threshold) {
+          cnt->yaw[0] = clampf(cnt->yaw[0] - cfg.range_delta, cfg.range_limit_yaw[0], cfg.range_limit_yaw[1]);
+          cnt->yaw[1] = clampf(cnt->yaw[1] + cfg.range_delta, cfg.range_limit_yaw[0], cfg.range_limit_yaw[1]);
+        }
+      }
     }
-    const int32_t c0 = reset_counts ? 0 : (int32_t)acc[14], c1 = reset_counts ? 0 : (int32_t)acc[15];
-    log_counts[0] = c0;
-    log_counts[1] = c1;
-    if (user_counts) { user_counts[0] = c0; user_counts[1] = c1; }
   }
   __syncthreads();
   if (threadIdx.x < ACC) acc[threadIdx.x] = 0.f;
@@ -1981,7 +2031,7 @@ __global__ void zb_finalize_kernel(int N, float* __restrict__ st, float* __restr
   if (full)
     for (int i = threadIdx.x; i < N; i += blockDim.x) {
       const uint64_t h = hash64(seed ^ hash64(ctr * 0x100000001B3ull + (uint64_t)i));
-      st[(size_t)ep_len_row * N + i] = (float)(int)(h % (uint64_t)max_ep_len);
+      st[(size_t)ep_len_row * N + i] = (float)(int)(h % (uint64_t)cfg.max_episode_length);
     }
 }
 
@@ -2043,19 +2093,30 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_substeps_kernel(con
 
 __host__ __device__ __forceinline__ float u01(uint64_t h) { return (float)(h >> 40) * (1.0f / 16777216.0f); }
 
-// reset_root_state_uniform (standup.py:33-97) for env i at RNG position ctr: x, y, roll, yaw ~ U
-// (the cfg ranges; pitch / z / velocities 0), root = default + (x, y, 0),
-// quat = quat_from_euler_xyz(roll, 0, yaw) * default quat (world-frame rotation, left multiply),
-// normalised; joints default, every velocity zero.
-__device__ __forceinline__ void su_reset_pose(MP m, const zb_task_cfg& cfg, uint64_t seed, uint64_t ctr, int i,
-                                              Phys& p) {
-  const uint64_t h = hash64(seed ^ hash64(ctr * 0x100000001B3ull + (uint64_t)i));
+// reward weight of term t in curriculum stage `stage` (compile-time indices into the kernarg table)
+__device__ __forceinline__ float stage_weight(const zb_task_cfg& cfg, int stage, int t) {
+  float w = cfg.stage_scales[0][t];
+#pragma unroll
+  for (int sg = 1; sg < ZB_MAX_STAGES; ++sg) w = stage == sg ? cfg.stage_scales[sg][t] : w;
+  return w;
+}
+
+// counter-based random stream of env i at call ctr; draw k of it (shared with the oracle)
+__device__ __forceinline__ uint64_t env_hash(uint64_t seed, uint64_t ctr, int i) {
+  return hash64(seed ^ hash64(ctr * 0x100000001B3ull + (uint64_t)i));
+}
+__device__ __forceinline__ float draw(uint64_t h, int k) { return u01(hash64(h + 0x632BE59BD9B4E019ull * (uint64_t)k)); }
+
+// reset_root_state_uniform (standup.py:33-97, v4.py:59-105) from stream h (draws 1..4): x, y,
+// roll, yaw ~ U (the cfg ranges; pitch / z / velocities 0), root = default + (x, y, 0), quat =
+// quat_from_euler_xyz(roll, 0, yaw) applied in the world frame (delta * default, standup) or the
+// body frame (default * delta, v4), normalised; joints default, every velocity zero. Returns the
+// yaw sample (the events store it as env.current_yaw).
+__device__ __forceinline__ float reset_pose(MP m, const zb_task_cfg& cfg, uint64_t h, Phys& p) {
   float r[4];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const float u = u01(hash64(h + 0x632BE59BD9B4E019ull * (uint64_t)(k + 1)));
-    r[k] = u * (cfg.reset_pose_range[k][1] - cfg.reset_pose_range[k][0]) + cfg.reset_pose_range[k][0];
-  }
+  for (int k = 0; k < 4; ++k)
+    r[k] = draw(h, k + 1) * (cfg.reset_pose_range[k][1] - cfg.reset_pose_range[k][0]) + cfg.reset_pose_range[k][0];
   float sr, cr, sy, cy;
   sincos_r(0.5f * r[2], &sr, &cr);
   sincos_r(0.5f * r[3], &sy, &cy);
@@ -2063,7 +2124,8 @@ __device__ __forceinline__ void su_reset_pose(MP m, const zb_task_cfg& cfg, uint
   const float q0[4] = {m->default_root_quat[0], m->default_root_quat[1], m->default_root_quat[2],
                        m->default_root_quat[3]};
   float qn[4];
-  qmul(dq, q0, qn);
+  if (cfg.reset_pose_body_frame) qmul(q0, dq, qn);
+  else qmul(dq, q0, qn);
   qnormalize(qn);
 #pragma unroll
   for (int a = 0; a < 4; ++a) p.quat[a] = qn[a];
@@ -2074,6 +2136,12 @@ __device__ __forceinline__ void su_reset_pose(MP m, const zb_task_cfg& cfg, uint
   for (int a = 0; a < 3; ++a) { p.lv[a] = 0.f; p.av[a] = 0.f; }
 #pragma unroll
   for (int j = 0; j < ND; ++j) { p.jq[j] = m->default_joint_pos[j]; p.jqd[j] = 0.f; }
+  return r[3];
+}
+
+__device__ __forceinline__ void su_reset_pose(MP m, const zb_task_cfg& cfg, uint64_t seed, uint64_t ctr, int i,
+                                              Phys& p) {
+  (void)reset_pose(m, cfg, env_hash(seed, ctr, i), p);
 }
 
 // One stand-up policy step per team (same mapping as zb_step_kernel; no contact sensor).
@@ -2188,7 +2256,7 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_su_step_kernel(
   r[ZB_SU_R_FEET_DOWNWARD_4] = z6 < 0.15f ? fz[0][2] + fz[1][2] : 1.6f;  // 827-840
   float w[ZB_SU_NUM_REWARD_TERMS];
 #pragma unroll
-  for (int t = 0; t < ZB_SU_NUM_REWARD_TERMS; ++t) w[t] = stage ? cfg.curriculum_scales[t] : cfg.reward_scales[t];
+  for (int t = 0; t < ZB_SU_NUM_REWARD_TERMS; ++t) w[t] = stage_weight(cfg, stage, t);
   float reward = 0.f, sums[ZB_SU_NUM_REWARD_TERMS];
 #pragma unroll
   for (int t = 0; t < ZB_SU_NUM_REWARD_TERMS; ++t) {
@@ -2206,9 +2274,9 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_su_step_kernel(
       const float dur = fmaxf(ep_len * step_dt, step_dt);
 #pragma unroll
       for (int t = 0; t < ZB_SU_NUM_REWARD_TERMS; ++t) atomicAdd(&acc[t], sums[t] / dur);
-      atomicAdd(&acc[13], 1.f);
-      if (died) atomicAdd(&acc[14], 1.f);
-      if (time_out) atomicAdd(&acc[15], 1.f);
+      atomicAdd(&acc[ACC_NRES], 1.f);
+      if (died) atomicAdd(&acc[ACC_DIED], 1.f);
+      if (time_out) atomicAdd(&acc[ACC_TOUT], 1.f);
     }
     su_reset_pose(m, cfg, seed, cnt->calls, i, p);
     const float4 qr = q.dflt()[3];
@@ -2264,7 +2332,7 @@ __global__ void zb_su_reset_kernel(const zb_model* __restrict__ mg, zb_task_cfg 
   const float dur = fmaxf(ST(ZB_SU_EP_LEN) * step_dt, step_dt);
 #pragma unroll
   for (int k = 0; k < ZB_SU_NUM_REWARD_TERMS; ++k) atomicAdd(&acc[k], ST(ZB_SU_EP_SUMS + k) / dur);
-  atomicAdd(&acc[13], 1.f);
+  atomicAdd(&acc[ACC_NRES], 1.f);
   Phys p;
   su_reset_pose(m, cfg, seed, cnt->calls, i, p);
 #pragma unroll
@@ -2310,6 +2378,450 @@ __global__ void zb_su_friction_kernel(int N, float* __restrict__ st, const float
   if (t >= N * NL) return;
   const int i = t / NL, l = t % NL;
   st[(size_t)(ZB_SU_LINK_MU + l) * N + i] = mu ? mu[t] : fill;
+}
+
+// =========================================================================== walking v4
+// zbot-6b-walking-v4 (reference zbot_direct_6dof_bipedal_env_v4.py = v4.py): v2's robot and
+// physics with forward-velocity / heading commands (reset and interval resample events), a
+// history-3 contact sensor that also tracks contact time, 15 reward terms evaluated on the
+// post-step state, and the two curricula (stage weights + command ranges in the device counters).
+
+__device__ __forceinline__ float wrap_to_pi(float x) {  // isaaclab.utils.math.wrap_to_pi
+  float a = fmodf(x, TWO_PI_F);
+  if (a < 0.f) a += TWO_PI_F;
+  return a > PI_F ? a - TWO_PI_F : a;
+}
+
+// resample_commands (v4.py:107-135) from stream h, draws k0 .. k0+2, with the device-side params
+__device__ __forceinline__ void v4_resample(const zb_task_cfg& cfg, const Counters* cnt, uint64_t h, int k0,
+                                            float cur_yaw, float cmd[2], float& target) {
+  const float lo = cnt->vel[0], hi0 = cnt->vel[1];
+  if (cfg.cmd_dual_sign) {
+    const float sg = draw(h, k0) < cnt->prob_pos ? 1.f : -1.f;  // bernoulli(prob_pos) * 2 - 1
+    const float hi = hi0 + cfg.cmd_offset * (sg - 1.f);
+    cmd[0] = (draw(h, k0 + 1) * (hi - lo) + lo) * sg;
+  } else {
+    cmd[0] = draw(h, k0 + 1) * (hi0 - lo) + lo;
+  }
+  cmd[1] = draw(h, k0 + 2) * (cnt->yaw[1] - cnt->yaw[0]) + cnt->yaw[0];
+  target = wrap_to_pi(cur_yaw + cmd[1]);
+}
+
+// prologue values parked in LDS across the physics (overlays the Pre record)
+struct PreV4 {
+  float a_now[ND], pdel[ND], jqd_prev[ND], action_rate;
+};
+static_assert(sizeof(PreV4) <= 16 * PRE4, "PreV4 fits PRE4 granules");
+
+__global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_v4_step_kernel(
+    const zb_model* __restrict__ mg, const float4* __restrict__ links, zb_task_cfg cfg, int N, float* __restrict__ st,
+    const float* __restrict__ act, float* __restrict__ obs, float* __restrict__ rew, uint8_t* __restrict__ term,
+    uint8_t* __restrict__ trunc, float* __restrict__ acc, const Counters* __restrict__ cnt, uint64_t seed) {
+  MP m = to_mp(mg);
+  __shared__ float4 lds[LDS4];
+  const int lane = threadIdx.x;
+  const int env = xcd_block(blockIdx.x, gridDim.x) * EPW + lane / TL;
+  const int i = env < N ? env : N - 1;
+  const bool lead = env < N && lane % TL == 0;
+  const Q q{lds, lane, lane / TL, lane % TL};
+  for (int t = lane; t < LNK4; t += WGT) lds[LNK_OFF + t] = links[t];
+  Stamps sp;
+  sp.begin();
+#define ST(f) st[(size_t)(f) * N + i]
+  Phys p;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) { p.pos[a] = ST(ZB_S_ROOT_POS + a); p.lv[a] = ST(ZB_S_ROOT_LINVEL + a); p.av[a] = ST(ZB_S_ROOT_ANGVEL + a); }
+#pragma unroll
+  for (int a = 0; a < 4; ++a) p.quat[a] = ST(ZB_S_ROOT_QUAT + a);
+#pragma unroll
+  for (int j = 0; j < ND; ++j) { p.jq[j] = ST(ZB_S_JOINT_POS + j); p.jqd[j] = ST(ZB_S_JOINT_VEL + j); }
+
+  // _pre_physics_step (v4.py:776-804, mode 1)
+  const bool writer = q.s == 0;
+  const float step_dt = cfg.sim_dt * (float)cfg.decimation;
+  PreV4& pv = *reinterpret_cast<PreV4*>(&q.pre());
+  float target[ND];
+  {
+    PreV4 pr;
+    pr.action_rate = 0.f;
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+      const float a_prev = ST(ZB_V4_ACTIONS + j);
+      pr.a_now[j] = tanh_r(act[(size_t)i * ZB_ACT_DIM + j]);
+      pr.pdel[j] = clampf(ST(ZB_V4_P_DELTA + j) + PI_F * pr.a_now[j] * cfg.joint_speed_limit * step_dt, -PI_F, PI_F);
+      target[j] = pr.pdel[j] + m->default_joint_pos[j];
+      pr.action_rate += (pr.a_now[j] - a_prev) * (pr.a_now[j] - a_prev);
+      pr.jqd_prev[j] = 0.f;
+    }
+    if (writer) pv = pr;
+  }
+
+  // 4 substeps; the last reports the sensor inputs / applied torques, the joint velocities before
+  // it give Isaac Lab's finite-difference joint_acc (ArticulationData.update every substep)
+  SensorOut so;
+  sp.mark(0);
+  for (int k = 0; k < cfg.decimation; ++k) {
+    const bool last = k == cfg.decimation - 1;
+    if (last && writer) {
+#pragma unroll
+      for (int j = 0; j < ND; ++j) pv.jqd_prev[j] = p.jqd[j];
+    }
+    substep<false, false>(m, cfg, p, target, q, last, so, nullptr, nullptr, sp);
+    sp.mark(7);
+  }
+  m = opaque(m);
+  wave_sync();
+  const PreV4 pr = pv;
+  st = opaque_ptr(st);
+
+  // ContactSensor lazy update (history 3, air / contact timers incl. last_contact_time)
+  float fz_prev[ZB_V4_HIST - 1][2], fmax_prev[ZB_V4_HIST - 1];
+#pragma unroll
+  for (int h = 0; h < ZB_V4_HIST - 1; ++h) {
+    fz_prev[h][0] = ST(ZB_V4_FEET_FZ_HIST + 2 * h);
+    fz_prev[h][1] = ST(ZB_V4_FEET_FZ_HIST + 2 * h + 1);
+    fmax_prev[h] = ST(ZB_V4_UNDES_FMAX_HIST + h);
+  }
+  float air_cur[2], con_cur[2], air_last[2], con_last[2], feetF[2];
+  bool in_contact[2];
+#pragma unroll
+  for (int f = 0; f < 2; ++f) {
+    const float ac0 = ST(ZB_V4_FEET_AIR_CUR + f), cc0 = ST(ZB_V4_FEET_CONTACT_CUR + f);
+    const bool c = sqrtf(dot3(so.feet_f[f], so.feet_f[f])) > cfg.contact_force_threshold;
+    air_last[f] = (ac0 > 0.f && c) ? ac0 + step_dt : ST(ZB_V4_FEET_AIR_LAST + f);
+    air_cur[f] = c ? 0.f : ac0 + step_dt;
+    con_last[f] = (cc0 > 0.f && !c) ? cc0 + step_dt : ST(ZB_V4_FEET_CONTACT_LAST + f);
+    con_cur[f] = c ? cc0 + step_dt : 0.f;
+    in_contact[f] = con_cur[f] > 0.f;
+    float sacc = so.feet_f[f][2];
+#pragma unroll
+    for (int h = 0; h < ZB_V4_HIST - 1; ++h) sacc += fz_prev[h][f];
+    feetF[f] = sacc / (float)ZB_V4_HIST;  // mean over the history (v4.py:846-849)
+  }
+  const float ep_len = ST(ZB_V4_EP_LEN) + 1.f;
+  float cmd[2] = {ST(ZB_V4_COMMANDS), ST(ZB_V4_COMMANDS + 1)};
+  float tgt = ST(ZB_V4_TARGET_YAW);
+  float ileft = ST(ZB_V4_INTERVAL_LEFT);
+  float f_last[2] = {ST(ZB_V4_FEET_F_LAST), ST(ZB_V4_FEET_F_LAST + 1)};
+  float step_len[2] = {ST(ZB_V4_FEET_STEP_LEN), ST(ZB_V4_FEET_STEP_LEN + 1)};
+  float down[2][3];
+#pragma unroll
+  for (int f = 0; f < 2; ++f)
+#pragma unroll
+    for (int a = 0; a < 3; ++a) down[f][a] = ST(ZB_V4_FEET_DOWN_POS + 3 * f + a);
+  float sums0[ZB_V4_NUM_REWARD_TERMS];
+#pragma unroll
+  for (int t = 0; t < ZB_V4_NUM_REWARD_TERMS; ++t) sums0[t] = ST(ZB_V4_EP_SUMS + t);
+  const int stage = cnt->stage;
+
+  // _compute_intermediate_values (v4.py:809-849) on the post-step state
+  float bq[4], sh[3], fwd[3], vb[3], feet[2][3], fzax[2][3], fxax[2][3], fvel[2][3];
+  bool died;
+  {
+    wave_sync();
+    fk_team_pose(p, q);
+    wave_sync();
+    float S[ND][6], org[ND][3];
+    read_joints(q, S, org);
+    float bp[3], R[9], fq[4];
+    link_pose_q(m, q, 6, bp, bq);
+    qmat(bq, R);
+    sh[0] = R[2]; sh[1] = R[5]; sh[2] = R[8];            // quat_apply(base_quat, z)
+    fwd[0] = sh[1]; fwd[1] = -sh[0]; fwd[2] = 0.f;       // GRAVITY_VEC_W x shoulder
+    link_origin_vel_q(m, q, p, S, 6, vb);                // body_link_lin_vel_w[base]
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+      const int l = f == 0 ? 0 : 11;
+      link_pose_q(m, q, l, feet[f], fq);
+#pragma unroll
+      for (int a = 0; a < 3; ++a) feet[f][a] += p.pos[a];
+      qmat(fq, R);
+      const float sg = f == 0 ? 1.f : -1.f;
+      fzax[f][0] = sg * R[2]; fzax[f][1] = sg * R[5]; fzax[f][2] = sg * R[8];
+      fxax[f][0] = R[0]; fxax[f][1] = R[3]; fxax[f][2] = R[6];
+      link_com_vel_q(m, q, p, S, l, fvel[f]);            // body_com_lin_vel_w[feet]
+    }
+    const float base_z = bp[2] + p.pos[2];
+    // _get_dones (v4.py:896-918)
+    float fm = so.undes_fmax;
+#pragma unroll
+    for (int h = 0; h < ZB_V4_HIST - 1; ++h) fm = fmaxf(fm, fmax_prev[h]);
+    died = fm > cfg.undesired_force_threshold || base_z < cfg.termination_height;
+  }
+  const bool time_out = ep_len >= (float)(cfg.max_episode_length - 1);
+  float cur_yaw = atan2f(fwd[1], fwd[0]);
+  float he;
+  {
+    float sn, cs;
+    sincos_r(tgt - cur_yaw, &sn, &cs);
+    he = atan2f(sn, cs);
+  }
+  const float vfwd = dot3(vb, fwd);
+
+  // _get_rewards (v4.py:883-894), terms 1003-1171 in dict order
+  float r[ZB_V4_NUM_REWARD_TERMS];
+  {
+    const float e = cmd[0] - vfwd;
+    r[ZB_V4_R_TRACK_LIN_VEL_X] = __expf(-e * e / 0.25f);
+    r[ZB_V4_R_TRACK_HEADING_YAW] = __expf(-he * he / 0.25f);
+    const float vy = dot3(vb, sh);
+    r[ZB_V4_R_LIN_VEL_Y] = vy * vy;
+    r[ZB_V4_R_ACTION_RATE] = pr.action_rate;
+    r[ZB_V4_R_TORQUES] = so.tau2;
+    float jv = 0.f, ja = 0.f;
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+      jv += p.jqd[j] * p.jqd[j];
+      const float aj = (p.jqd[j] - pr.jqd_prev[j]) / cfg.sim_dt;
+      ja += aj * aj;
+    }
+    r[ZB_V4_R_JOINT_VEL] = jv;
+    r[ZB_V4_R_JOINT_ACC] = ja;
+    float sd = 0.f, sfw = 0.f;
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+      const float dz[3] = {fzax[f][0], fzax[f][1], fzax[f][2] - 1.f};
+      sd += sqrtf(dot3(dz, dz));
+      const float dx[3] = {fxax[f][0] - fwd[0], fxax[f][1] - fwd[1], fxax[f][2] - fwd[2]};
+      sfw += sqrtf(dot3(dx, dx));
+    }
+    r[ZB_V4_R_FEET_DOWNWARD] = sd;
+    r[ZB_V4_R_FEET_FORWARD] = sfw;
+    // step_length (v4.py:1058-1095): touchdown foot records its step along the heading, signed by
+    // the commanded direction; the stored lengths decay by 0.99 per step
+    const float csg = cmd[0] > 0.f ? 1.f : (cmd[0] < 0.f ? -1.f : 0.f);
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+      if (feetF[f] > 10.f && f_last[f] < 10.f) {
+        const float dv[3] = {feet[f][0] - down[f][0], feet[f][1] - down[f][1], feet[f][2] - down[f][2]};
+        step_len[f] = dot3(dv, fwd) * csg;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) down[f][a] = feet[f][a];
+      }
+    }
+    const float mn = fminf(step_len[0], step_len[1]);
+    step_len[0] *= 0.99f;
+    step_len[1] *= 0.99f;
+    f_last[0] = feetF[0];
+    f_last[1] = feetF[1];
+    r[ZB_V4_R_STEP_LENGTH] = tanh_r(15.f * mn);
+    // feet_air_time_biped (1129-1143)
+    const bool single = (in_contact[0] ? 1 : 0) + (in_contact[1] ? 1 : 0) == 1;
+    float bi = 3.4e38f;
+#pragma unroll
+    for (int f = 0; f < 2; ++f) bi = fminf(bi, single ? (in_contact[f] ? con_cur[f] : air_cur[f]) : 0.f);
+    r[ZB_V4_R_FEET_AIR_TIME_BIPED] = fminf(bi, 2.f);
+    // airtime_variance (1097-1103): unbiased variance of two values = (a - b)^2 / 2
+    const float da = fminf(air_last[0], 0.5f) - fminf(air_last[1], 0.5f);
+    const float dc = fminf(con_last[0], 0.5f) - fminf(con_last[1], 0.5f);
+    r[ZB_V4_R_AIRTIME_VARIANCE] = 0.5f * da * da + 0.5f * dc * dc;
+    float sl = 0.f;
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+      sl += sqrtf(fvel[f][0] * fvel[f][0] + fvel[f][1] * fvel[f][1]) * (feetF[f] > 1.f ? 1.f : 0.f);
+    r[ZB_V4_R_FEET_SLIDE] = sl;
+    r[ZB_V4_R_FEET_HARMONY] = (air_last[0] + air_last[1]) - 3.f * fabsf(air_last[0] - air_last[1]);
+    const float dx = feet[0][0] - feet[1][0], dy = feet[0][1] - feet[1][1];
+    r[ZB_V4_R_FEET_CLOSE] = fmaxf(0.115f - sqrtf(dx * dx + dy * dy), 0.f);
+  }
+  float reward = 0.f, sums[ZB_V4_NUM_REWARD_TERMS];
+#pragma unroll
+  for (int t = 0; t < ZB_V4_NUM_REWARD_TERMS; ++t) {
+    const float v = (r[t] * stage_weight(cfg, stage, t)) * step_dt;
+    reward += v;
+    sums[t] = sums0[t] + v;
+  }
+  if (died) reward -= cfg.terminal_penalty;  // v4.py:892-893
+  const bool reset = died || time_out;
+  const uint64_t hs = env_hash(seed, cnt->calls, i);
+  float obs_q[4] = {bq[0], bq[1], bq[2], bq[3]};
+
+  // _reset_idx (v4.py:920-1001): log (sum / own duration), reset events (pose, commands), defaults
+  if (reset) {
+    if (lead) {
+      const float dur = fmaxf(ep_len * step_dt, step_dt);
+#pragma unroll
+      for (int t = 0; t < ZB_V4_NUM_REWARD_TERMS; ++t) atomicAdd(&acc[t], sums[t] / dur);
+      atomicAdd(&acc[ACC_NRES], 1.f);
+      if (died) atomicAdd(&acc[ACC_DIED], 1.f);
+      if (time_out) atomicAdd(&acc[ACC_TOUT], 1.f);
+    }
+    cur_yaw = reset_pose(m, cfg, hs, p);
+    v4_resample(cfg, cnt, hs, 5, cur_yaw, cmd, tgt);
+    const float4 qr = q.dflt()[3];
+    const float qrel[4] = {qr.x, qr.y, qr.z, qr.w};
+    qmul(p.quat, qrel, obs_q);
+    float R[9];
+    qmat(p.quat, R);
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {  // feet_down_pos_last = the reset pose's feet
+      const float4 fr = q.dflt()[4 + f];
+      const float v[3] = {fr.x, fr.y, fr.z};
+      float w3[3];
+      mv3(R, v, w3);
+#pragma unroll
+      for (int a = 0; a < 3; ++a) down[f][a] = p.pos[a] + w3[a];
+      f_last[f] = cfg.feet_f_last_init;
+      step_len[f] = 0.f;
+    }
+  }
+  // interval_command_resample (mode "interval", 3-6 s per env; after the resets, v4.py:426-439)
+  ileft -= step_dt;
+  if (ileft < 1e-6f) {
+    ileft = draw(hs, 8) * (cfg.cmd_interval_s[1] - cfg.cmd_interval_s[0]) + cfg.cmd_interval_s[0];
+    v4_resample(cfg, cnt, hs, 9, cur_yaw, cmd, tgt);
+  }
+  float he_obs;
+  {
+    float sn, cs;
+    sincos_r(tgt - cur_yaw, &sn, &cs);
+    he_obs = atan2f(sn, cs);
+  }
+  sp.mark(12);
+  if (writer) {
+    auto live = [reset](float v) { return reset ? 0.f : v; };
+#pragma unroll
+    for (int a = 0; a < 3; ++a) { ST(ZB_S_ROOT_POS + a) = p.pos[a]; ST(ZB_S_ROOT_LINVEL + a) = p.lv[a]; ST(ZB_S_ROOT_ANGVEL + a) = p.av[a]; }
+#pragma unroll
+    for (int a = 0; a < 4; ++a) ST(ZB_S_ROOT_QUAT + a) = p.quat[a];
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+      ST(ZB_S_JOINT_POS + j) = p.jq[j]; ST(ZB_S_JOINT_VEL + j) = p.jqd[j];
+      ST(ZB_V4_P_DELTA + j) = live(pr.pdel[j]); ST(ZB_V4_ACTIONS + j) = live(pr.a_now[j]);
+    }
+    ST(ZB_V4_COMMANDS) = cmd[0];
+    ST(ZB_V4_COMMANDS + 1) = cmd[1];
+    ST(ZB_V4_TARGET_YAW) = tgt;
+    ST(ZB_V4_INTERVAL_LEFT) = ileft;
+    ST(ZB_V4_CURRENT_YAW) = cur_yaw;
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+#pragma unroll
+      for (int a = 0; a < 3; ++a) ST(ZB_V4_FEET_DOWN_POS + 3 * f + a) = down[f][a];
+      ST(ZB_V4_FEET_STEP_LEN + f) = step_len[f];
+      ST(ZB_V4_FEET_F_LAST + f) = f_last[f];
+      ST(ZB_V4_FEET_AIR_CUR + f) = live(air_cur[f]);
+      ST(ZB_V4_FEET_CONTACT_CUR + f) = live(con_cur[f]);
+      ST(ZB_V4_FEET_AIR_LAST + f) = live(air_last[f]);
+      ST(ZB_V4_FEET_CONTACT_LAST + f) = live(con_last[f]);
+      ST(ZB_V4_FEET_FZ_HIST + f) = live(so.feet_f[f][2]);
+#pragma unroll
+      for (int h = 1; h < ZB_V4_HIST; ++h) ST(ZB_V4_FEET_FZ_HIST + 2 * h + f) = live(fz_prev[h - 1][f]);
+    }
+    ST(ZB_V4_UNDES_FMAX_HIST) = live(so.undes_fmax);
+#pragma unroll
+    for (int h = 1; h < ZB_V4_HIST; ++h) ST(ZB_V4_UNDES_FMAX_HIST + h) = live(fmax_prev[h - 1]);
+    ST(ZB_V4_EP_LEN) = live(ep_len);
+#pragma unroll
+    for (int t = 0; t < ZB_V4_NUM_REWARD_TERMS; ++t) ST(ZB_V4_EP_SUMS + t) = live(sums[t]);
+
+    // _get_observations (v4.py:851-881)
+    float* o = obs + (size_t)i * ZB_V4_OBS_DIM;
+    o[0] = obs_q[0]; o[1] = obs_q[1]; o[2] = obs_q[2]; o[3] = obs_q[3];
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+      o[4 + j] = p.jq[j] - m->default_joint_pos[j];
+      o[10 + j] = p.jqd[j];
+      o[16 + j] = live(pr.a_now[j]);
+    }
+    o[22] = cmd[0];
+    o[23] = he_obs;
+    rew[i] = reward;
+    term[i] = died ? 1 : 0;
+    trunc[i] = time_out ? 1 : 0;
+  }
+  sp.mark(8);
+  sp.flush();
+#undef ST
+}
+
+// explicit resets / construction (init = 1 also draws the interval-event timers, as Isaac Lab's
+// EventManager does when it is created): log, reset events, defaults; one thread per env
+__global__ void zb_v4_reset_kernel(const zb_model* __restrict__ mg, const float4* __restrict__ links, zb_task_cfg cfg,
+                                   int N, float* __restrict__ st, const int32_t* __restrict__ ids, int n,
+                                   float* __restrict__ acc, const Counters* __restrict__ cnt, uint64_t seed, int init) {
+  MP m = to_mp(mg);
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const int i = ids ? ids[t] : t;
+  if (i < 0 || i >= N) return;
+#define ST(f) st[(size_t)(f) * N + i]
+  const float step_dt = cfg.sim_dt * (float)cfg.decimation;
+  if (!init) {
+    const float dur = fmaxf(ST(ZB_V4_EP_LEN) * step_dt, step_dt);
+#pragma unroll
+    for (int k = 0; k < ZB_V4_NUM_REWARD_TERMS; ++k) atomicAdd(&acc[k], ST(ZB_V4_EP_SUMS + k) / dur);
+    atomicAdd(&acc[ACC_NRES], 1.f);
+  }
+  Phys p;
+  const uint64_t hs = env_hash(seed, cnt->calls, i);
+  const float cur_yaw = reset_pose(m, cfg, hs, p);
+  float cmd[2], tgt;
+  v4_resample(cfg, cnt, hs, 5, cur_yaw, cmd, tgt);
+#pragma unroll
+  for (int a = 0; a < 3; ++a) { ST(ZB_S_ROOT_POS + a) = p.pos[a]; ST(ZB_S_ROOT_LINVEL + a) = p.lv[a]; ST(ZB_S_ROOT_ANGVEL + a) = p.av[a]; }
+#pragma unroll
+  for (int a = 0; a < 4; ++a) ST(ZB_S_ROOT_QUAT + a) = p.quat[a];
+#pragma unroll
+  for (int j = 0; j < ND; ++j) {
+    ST(ZB_S_JOINT_POS + j) = p.jq[j]; ST(ZB_S_JOINT_VEL + j) = p.jqd[j];
+    ST(ZB_V4_P_DELTA + j) = 0.f; ST(ZB_V4_ACTIONS + j) = 0.f;
+  }
+  ST(ZB_V4_COMMANDS) = cmd[0];
+  ST(ZB_V4_COMMANDS + 1) = cmd[1];
+  ST(ZB_V4_TARGET_YAW) = tgt;
+  ST(ZB_V4_CURRENT_YAW) = cur_yaw;
+  if (init) ST(ZB_V4_INTERVAL_LEFT) = draw(hs, 8) * (cfg.cmd_interval_s[1] - cfg.cmd_interval_s[0]) + cfg.cmd_interval_s[0];
+  float R[9];
+  qmat(p.quat, R);
+#pragma unroll
+  for (int f = 0; f < 2; ++f) {
+    const float4 fr = links[DFLT_OFF + 4 + f];
+    const float v[3] = {fr.x, fr.y, fr.z};
+    float w3[3];
+    mv3(R, v, w3);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) ST(ZB_V4_FEET_DOWN_POS + 3 * f + a) = p.pos[a] + w3[a];
+    ST(ZB_V4_FEET_STEP_LEN + f) = 0.f;
+    ST(ZB_V4_FEET_F_LAST + f) = cfg.feet_f_last_init;
+    ST(ZB_V4_FEET_AIR_CUR + f) = 0.f;
+    ST(ZB_V4_FEET_CONTACT_CUR + f) = 0.f;
+    ST(ZB_V4_FEET_AIR_LAST + f) = 0.f;
+    ST(ZB_V4_FEET_CONTACT_LAST + f) = 0.f;
+#pragma unroll
+    for (int h = 0; h < ZB_V4_HIST; ++h) ST(ZB_V4_FEET_FZ_HIST + 2 * h + f) = 0.f;
+  }
+#pragma unroll
+  for (int h = 0; h < ZB_V4_HIST; ++h) ST(ZB_V4_UNDES_FMAX_HIST + h) = 0.f;
+  ST(ZB_V4_EP_LEN) = 0.f;
+#pragma unroll
+  for (int k = 0; k < ZB_V4_NUM_REWARD_TERMS; ++k) ST(ZB_V4_EP_SUMS + k) = 0.f;
+#undef ST
+}
+
+__global__ void zb_v4_observe_kernel(const zb_model* __restrict__ mg, int N, const float* __restrict__ st,
+                                     float* __restrict__ obs) {
+  MP m = to_mp(mg);
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  Phys p;
+  load_phys(st, N, i, p);
+  Kin k;
+  fk(m, p, k);
+  float bp[3], bq[4];
+  link_pose(m, k, 6, bp, bq);
+  float* o = obs + (size_t)i * ZB_V4_OBS_DIM;
+  o[0] = bq[0]; o[1] = bq[1]; o[2] = bq[2]; o[3] = bq[3];
+#pragma unroll
+  for (int j = 0; j < ND; ++j) {
+    o[4 + j] = p.jq[j] - m->default_joint_pos[j];
+    o[10 + j] = p.jqd[j];
+    o[16 + j] = st[(size_t)(ZB_V4_ACTIONS + j) * N + i];
+  }
+  o[22] = st[(size_t)ZB_V4_COMMANDS * N + i];
+  float sn, cs;
+  sincos_r(st[(size_t)ZB_V4_TARGET_YAW * N + i] - st[(size_t)ZB_V4_CURRENT_YAW * N + i], &sn, &cs);
+  o[23] = atan2f(sn, cs);
 }
 }  // namespace
 
@@ -2379,7 +2891,9 @@ int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_dev
     if (np != m->num_self_pairs) return set_err(-1, "zb_create: self-collision pair count", hipSuccess);
   }
   if (c->decimation < 1 || c->solver_iterations < 0) return set_err(-1, "zb_create: cfg", hipSuccess);
-  if (c->task != ZB_TASK_WALKING_V2 && c->task != ZB_TASK_STANDUP_V0) return set_err(-1, "zb_create: unknown task", hipSuccess);
+  if (c->task != ZB_TASK_WALKING_V2 && c->task != ZB_TASK_STANDUP_V0 && c->task != ZB_TASK_WALKING_V4)
+    return set_err(-1, "zb_create: unknown task", hipSuccess);
+  if (c->num_stages < 1 || c->num_stages > ZB_MAX_STAGES) return set_err(-1, "zb_create: num_stages", hipSuccess);
   if (c->task == ZB_TASK_STANDUP_V0 && c->center_z_period < 1) return set_err(-1, "zb_create: center_z_period", hipSuccess);
   HIPCHK(hipSetDevice(hip_device), "hipSetDevice");
   zb_sim* h = new zb_sim();
@@ -2387,15 +2901,23 @@ int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_dev
   h->n = num_envs;
   h->seed = seed;
   h->task = c->task;
-  h->state_dim = c->task == ZB_TASK_STANDUP_V0 ? ZB_SU_STATE_DIM : ZB_STATE_DIM;
+  h->state_dim = c->task == ZB_TASK_STANDUP_V0 ? ZB_SU_STATE_DIM
+                 : c->task == ZB_TASK_WALKING_V4 ? ZB_V4_STATE_DIM : ZB_STATE_DIM;
   h->d_cnt = nullptr;
   h->cfg = *c;
   HIPCHK(hipMalloc(&h->d_model, sizeof(zb_model)), "hipMalloc model");
   HIPCHK(hipMalloc(&h->d_state, sizeof(float) * (size_t)h->state_dim * num_envs), "hipMalloc state");
   HIPCHK(hipMalloc(&h->d_acc, sizeof(float) * ACC), "hipMalloc acc");
   HIPCHK(hipMalloc(&h->d_cnt, sizeof(Counters)), "hipMalloc counters");
-  HIPCHK(hipMemset(h->d_cnt, 0, sizeof(Counters)), "hipMemset counters");
-  HIPCHK(hipMalloc(&h->d_log_means, sizeof(float) * ZB_NUM_REWARD_TERMS), "hipMalloc log");
+  {
+    Counters c0;
+    memset(&c0, 0, sizeof(c0));
+    c0.vel[0] = c->cmd_vel_range[0]; c0.vel[1] = c->cmd_vel_range[1];
+    c0.yaw[0] = c->cmd_yaw_range[0]; c0.yaw[1] = c->cmd_yaw_range[1];
+    c0.prob_pos = c->stage_prob_pos[0];
+    HIPCHK(hipMemcpy(h->d_cnt, &c0, sizeof(Counters), hipMemcpyHostToDevice), "hipMemcpy counters");
+  }
+  HIPCHK(hipMalloc(&h->d_log_means, sizeof(float) * ZB_LOG_LEN), "hipMalloc log");
   HIPCHK(hipMalloc(&h->d_log_counts, sizeof(int32_t) * 2), "hipMalloc log");
   HIPCHK(hipMemcpy(h->d_model, m, sizeof(zb_model), hipMemcpyHostToDevice), "hipMemcpy model");
   {
@@ -2442,7 +2964,7 @@ int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_dev
     HIPCHK(hipMemcpy(h->d_links, tab, sizeof(tab), hipMemcpyHostToDevice), "hipMemcpy links");
   }
   HIPCHK(hipMemset(h->d_state, 0, sizeof(float) * (size_t)h->state_dim * num_envs), "hipMemset state");
-  HIPCHK(hipMemset(h->d_log_means, 0, sizeof(float) * ZB_NUM_REWARD_TERMS), "hipMemset log");
+  HIPCHK(hipMemset(h->d_log_means, 0, sizeof(float) * ZB_LOG_LEN), "hipMemset log");
   HIPCHK(hipMemset(h->d_log_counts, 0, sizeof(int32_t) * 2), "hipMemset log");
   HIPCHK(hipMemset(h->d_acc, 0, sizeof(float) * ACC), "hipMemset acc");
   // start at the default pose (ep_len 0, as after construction; reset() randomises it)
@@ -2458,8 +2980,16 @@ int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_dev
                                                        h->d_acc, h->d_cnt, h->seed);
     rc = launch_check("zb_su_reset_kernel");
     if (rc) return rc;
-    const Counters c1{1, 0, 0, 0};
-    HIPCHK(hipMemcpy(h->d_cnt, &c1, sizeof(Counters), hipMemcpyHostToDevice), "hipMemcpy counters");
+    const uint64_t one = 1;
+    HIPCHK(hipMemcpy(&h->d_cnt->calls, &one, sizeof(one), hipMemcpyHostToDevice), "hipMemcpy counters");
+  } else if (h->task == ZB_TASK_WALKING_V4) {
+    // construction: reset events at RNG position 0 (+ interval timers); later calls start at 1
+    zb_v4_reset_kernel<<<(num_envs + 255) / 256, 256>>>(h->d_model, h->d_links, h->cfg, num_envs, h->d_state, nullptr,
+                                                       num_envs, h->d_acc, h->d_cnt, h->seed, 1);
+    rc = launch_check("zb_v4_reset_kernel");
+    if (rc) return rc;
+    const uint64_t one = 1;
+    HIPCHK(hipMemcpy(&h->d_cnt->calls, &one, sizeof(one), hipMemcpyHostToDevice), "hipMemcpy counters");
   } else {
     zb_reset_kernel<<<(num_envs + 255) / 256, 256>>>(h->d_model, h->d_links, num_envs, h->d_state, nullptr, num_envs,
                                                       h->d_acc);
@@ -2536,15 +3066,14 @@ void zb_destroy(zb_handle h) {
 // episode-log divisor: walking divides the summed episode sums by the 20 s episode (v2.py:446),
 // standup already divided each env's sums by its own duration (standup.py:653-659)
 static float log_episode_s(zb_handle h) {
-  return h->task == ZB_TASK_STANDUP_V0 ? 1.f : h->cfg.sim_dt * h->cfg.decimation * h->cfg.max_episode_length;
+  return h->task == ZB_TASK_WALKING_V2 ? h->cfg.sim_dt * h->cfg.decimation * h->cfg.max_episode_length : 1.f;
 }
 
 static int finalize(zb_handle h, hipStream_t s, int full, int reset_counts, int is_step) {
-  const int ep_row = h->task == ZB_TASK_STANDUP_V0 ? ZB_SU_EP_LEN : ZB_S_EP_LEN;
-  const int cur = h->task == ZB_TASK_STANDUP_V0 ? h->cfg.curriculum_steps : 0;
+  const int ep_row = h->task == ZB_TASK_STANDUP_V0 ? ZB_SU_EP_LEN : h->task == ZB_TASK_WALKING_V4 ? ZB_V4_EP_LEN : ZB_S_EP_LEN;
   zb_finalize_kernel<<<1, 256, 0, s>>>(h->n, h->d_state, h->d_acc, h->d_log_means, h->d_log_counts, h->u_log_means,
-                                        h->u_log_counts, log_episode_s(h), h->cfg.max_episode_length, h->seed,
-                                        h->d_cnt, full, reset_counts, is_step, ep_row, cur);
+                                       h->u_log_counts, log_episode_s(h), h->seed, h->d_cnt, full, reset_counts, is_step,
+                                       ep_row, h->cfg);
   return launch_check("zb_finalize_kernel");
 }
 
@@ -2556,6 +3085,9 @@ int zb_reset(zb_handle h, const int32_t* env_ids, int n, void* stream) {
   if (h->task == ZB_TASK_STANDUP_V0)
     zb_su_reset_kernel<<<(cnt + 255) / 256, 256, 0, s>>>(h->d_model, h->cfg, h->n, h->d_state, env_ids, cnt, h->d_acc,
                                                          h->d_cnt, h->seed);
+  else if (h->task == ZB_TASK_WALKING_V4)
+    zb_v4_reset_kernel<<<(cnt + 255) / 256, 256, 0, s>>>(h->d_model, h->d_links, h->cfg, h->n, h->d_state, env_ids, cnt,
+                                                         h->d_acc, h->d_cnt, h->seed, 0);
   else
     zb_reset_kernel<<<(cnt + 255) / 256, 256, 0, s>>>(h->d_model, h->d_links, h->n, h->d_state, env_ids, cnt, h->d_acc);
   int rc = launch_check("zb_reset_kernel");
@@ -2573,6 +3105,9 @@ int zb_step(zb_handle h, const float* actions, float* obs, float* reward, uint8_
   if (h->task == ZB_TASK_STANDUP_V0)
     zb_su_step_kernel<<<blocks, WGT, 0, s>>>(h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward,
                                              terminated, truncated, h->d_acc, h->d_cnt, h->seed);
+  else if (h->task == ZB_TASK_WALKING_V4)
+    zb_v4_step_kernel<<<blocks, WGT, 0, s>>>(h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward,
+                                             terminated, truncated, h->d_acc, h->d_cnt, h->seed);
   else
     zb_step_kernel<<<blocks, WGT, 0, s>>>(h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward,
                                           terminated, truncated, h->d_acc);
@@ -2589,6 +3124,8 @@ int zb_observe(zb_handle h, float* obs, void* stream) {
   if (!h || !obs) return set_err(-1, "zb_observe", hipSuccess);
   if (h->task == ZB_TASK_STANDUP_V0)
     zb_su_observe_kernel<<<(h->n + 255) / 256, 256, 0, (hipStream_t)stream>>>(h->d_model, h->n, h->d_state, obs);
+  else if (h->task == ZB_TASK_WALKING_V4)
+    zb_v4_observe_kernel<<<(h->n + 255) / 256, 256, 0, (hipStream_t)stream>>>(h->d_model, h->n, h->d_state, obs);
   else
     zb_observe_kernel<<<(h->n + 255) / 256, 256, 0, (hipStream_t)stream>>>(h->d_model, h->n, h->d_state, obs);
   return launch_check("zb_observe_kernel");
@@ -2616,7 +3153,7 @@ int zb_read_log(zb_handle h, float* term_means, int32_t* counts, void* stream) {
   if (!h) return set_err(-1, "zb_read_log", hipSuccess);
   hipStream_t s = (hipStream_t)stream;
   if (term_means)
-    HIPCHK(hipMemcpyAsync(term_means, h->d_log_means, sizeof(float) * ZB_NUM_REWARD_TERMS, hipMemcpyDeviceToDevice, s),
+    HIPCHK(hipMemcpyAsync(term_means, h->d_log_means, sizeof(float) * ZB_LOG_LEN, hipMemcpyDeviceToDevice, s),
            "hipMemcpyAsync log");
   if (counts)
     HIPCHK(hipMemcpyAsync(counts, h->d_log_counts, sizeof(int32_t) * 2, hipMemcpyDeviceToDevice, s), "hipMemcpyAsync log");

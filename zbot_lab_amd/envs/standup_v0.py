@@ -72,7 +72,7 @@ class Zbot6SUpEnvCfg:
             contact_margin=self.solver.contact_margin, baumgarte=self.solver.baumgarte,
             solver_iterations=self.solver.iterations, enable_self_collision=self.solver.self_collision,
             reset_pose_range=tuple(tuple(pr.get(k, (0.0, 0.0))) for k in ("x", "y", "roll", "yaw")),
-            curriculum_weights=dict(self.curriculum_weights) if self.events.my_curric is not None else None,
+            curriculum=self.events.my_curric is not None, curriculum_weights=dict(self.curriculum_weights),
         )
 
 
@@ -104,9 +104,7 @@ class Zbot6SUpEnv(ZbotDirectEnvV2):
     @property
     def reward_scales(self) -> dict:
         """Reward weights of the current curriculum stage (the reference mutates this dict)."""
-        w = self._task.curriculum_weights if (self._task.curriculum_weights and self.curriculum_stage) \
-            else self._task.reward_weights
-        return dict(w)
+        return dict(self._task.stage_weights()[self.curriculum_stage])
 
     @reward_scales.setter
     def reward_scales(self, value) -> None:  # set by the base __init__; the weights live in _task

@@ -39,7 +39,8 @@ REWARD_WEIGHTS = {  # v2.py:190-206 ("train reward 2000 step4")
 }
 
 # zbot-6b-standup-v0 (include/zbot.h enum zb_standup_state_field / zb_standup_reward_term)
-TASK_WALKING_V2, TASK_STANDUP_V0 = 0, 1
+TASK_WALKING_V2, TASK_STANDUP_V0, TASK_WALKING_V4 = 0, 1, 2
+MAX_REWARD_TERMS, MAX_STAGES, LOG_LEN = 16, 4, 20
 SU_OBS_DIM, SU_NUM_TERMS, SU_STATE_DIM = 22, 4, 55
 SU_REWARD_TERMS = ["upward_2", "shape_symmetry", "feet_downward", "feet_downward_4"]  # standup.py:418-427
 SU_REWARD_WEIGHTS = {"upward_2": 10.0, "shape_symmetry": -1.0, "feet_downward": -1.0, "feet_downward_4": 0.0}
@@ -49,6 +50,29 @@ SU = dict(P_DELTA=25, ACTIONS=31, CENTER_Z_LAST=37, EP_LEN=38, EP_SUMS=39, LINK_
 # ZBOT_6S_CFG_2 init_state (zbot_cfg.py:744-753): lying on its side, joints straight
 SU_ROOT_POS = (0.0, 0.0, 0.05)
 SU_ROOT_ROT = (0.707, 0.0, -0.707, 0.0)
+
+# zbot-6b-walking-v4 (include/zbot.h enum zb_v4_state_field / zb_v4_reward_term)
+V4_OBS_DIM, V4_NUM_TERMS, V4_STATE_DIM, V4_HIST, V4_RING = 24, 15, 85, 3, 24
+V4_REWARD_TERMS = [  # dict order of Zbot6SEnvV4Cfg.reward_cfg (v4.py:620-641)
+    "track_lin_vel_x", "track_heading_yaw", "lin_vel_y", "action_rate", "torques", "joint_vel", "joint_acc",
+    "feet_downward", "feet_forward", "step_length", "feet_air_time_biped", "airtime_variance", "feet_slide",
+    "feet_harmony", "feet_close",
+]
+V4_REWARD_WEIGHTS = {
+    "track_lin_vel_x": 1.0, "track_heading_yaw": 1.0, "lin_vel_y": -1.0, "action_rate": -0.1, "torques": -2e-4,
+    "joint_vel": -0.001, "joint_acc": -2.5e-7, "feet_downward": -1.0, "feet_forward": -0.5, "step_length": 5.0,
+    "feet_air_time_biped": 1.0, "airtime_variance": -5.0, "feet_slide": -1.0, "feet_harmony": 0.0, "feet_close": -10.0,
+}
+# my_curriculum (v4.py:137-199): (common_step_counter threshold in episodes, weight updates, prob_pos)
+V4_STAGES = [
+    (12, {"airtime_variance": -10.0, "feet_forward": -1.0, "feet_slide": -2.0}, None),
+    (24, {"airtime_variance": -40.0, "feet_downward": -5.0}, 0.8),
+    (144, {"feet_harmony": 1.0, "feet_downward": -10.0, "step_length": 7.0, "track_heading_yaw": 2.0,
+           "feet_close": -120.0}, 0.6),
+]
+V4 = dict(P_DELTA=25, ACTIONS=31, COMMANDS=37, TARGET_YAW=39, INTERVAL_LEFT=40, FEET_DOWN_POS=41,
+          FEET_STEP_LEN=47, FEET_F_LAST=49, FEET_FZ_HIST=51, UNDES_FMAX_HIST=57, FEET_AIR_CUR=60,
+          FEET_CONTACT_CUR=62, FEET_AIR_LAST=64, FEET_CONTACT_LAST=66, EP_LEN=68, EP_SUMS=69, CURRENT_YAW=84)
 
 # state field offsets (include/zbot.h enum zb_state_field)
 S = dict(ROOT_POS=0, ROOT_QUAT=3, ROOT_LINVEL=7, ROOT_ANGVEL=10, JOINT_POS=13, JOINT_VEL=19,
@@ -93,9 +117,15 @@ class ZbTaskCfg(C.Structure):
         ("friction", C.c_float), ("contact_force_threshold", C.c_float),
         ("contact_margin", C.c_float), ("baumgarte", C.c_float),
         ("solver_iterations", C.c_int32), ("enable_self_collision", C.c_int32),
-        ("task", C.c_int32), ("reset_pose_range", (C.c_float * 2) * 4),
+        ("task", C.c_int32), ("reset_pose_range", (C.c_float * 2) * 4), ("reset_pose_body_frame", C.c_int32),
         ("center_z_init", C.c_float), ("center_z_drop", C.c_float), ("center_z_period", C.c_int32),
-        ("curriculum_steps", C.c_int32), ("curriculum_scales", C.c_float * NUM_TERMS),
+        ("num_stages", C.c_int32), ("stage_steps", C.c_int32 * MAX_STAGES),
+        ("stage_scales", (C.c_float * MAX_REWARD_TERMS) * MAX_STAGES), ("stage_prob_pos", C.c_float * MAX_STAGES),
+        ("cmd_vel_range", C.c_float * 2), ("cmd_yaw_range", C.c_float * 2), ("cmd_dual_sign", C.c_int32),
+        ("cmd_offset", C.c_float), ("cmd_interval_s", C.c_float * 2),
+        ("range_limit_vel", C.c_float * 2), ("range_limit_yaw", C.c_float * 2), ("range_start_steps", C.c_int32),
+        ("range_period_steps", C.c_int32), ("range_min_buffer", C.c_int32), ("range_threshold", C.c_float),
+        ("range_delta", C.c_float), ("undesired_force_threshold", C.c_float), ("feet_f_last_init", C.c_float),
     ]
 
 
@@ -366,33 +396,72 @@ class TaskCfg:
     solver_iterations: int = 4   # = solver_position_iteration_count (zbot_cfg.py:637)
     enable_self_collision: bool = True
     task: int = TASK_WALKING_V2
-    # stand-up task only (standup.py)
-    reset_pose_range: tuple = ((-0.5, 0.5), (-0.5, 0.5), (-0.7854, 0.7854), (-3.14, 3.14))  # x, y, roll, yaw
+    # stand-up / v4 reset pose (reset_root_state_uniform): x, y, roll, yaw ranges
+    reset_pose_range: tuple = ((-0.5, 0.5), (-0.5, 0.5), (-0.7854, 0.7854), (-3.14, 3.14))
+    reset_pose_body_frame: bool = False
     center_z_init: float = 0.05
     center_z_drop: float = 0.05
     center_z_period: int = 50
-    curriculum_steps: int | None = None  # my_curriculum threshold; None = max_episode_length * 80 (standup.py:102)
-    curriculum_weights: dict | None = None
+    # curriculum: [(common_step_counter threshold, {term: weight updates}, prob_pos or None)], cumulative
+    stages: list = field(default_factory=list)
+    # v4 commands / range curriculum
+    cmd_vel_range: tuple = (0.3, 0.3)
+    cmd_yaw_range: tuple = (-0.1, 0.1)
+    cmd_dual_sign: bool = True
+    cmd_offset: float = 0.0
+    cmd_prob_pos: float = 1.0
+    cmd_interval_s: tuple = (3.0, 6.0)
+    range_limit_vel: tuple = (0.0, 0.3)
+    range_limit_yaw: tuple = (-0.5, 0.5)
+    range_start_episodes: int = 48
+    range_period_episodes: int = 12
+    range_min_buffer: int = 20
+    range_threshold: float = 0.85
+    range_delta: float = 0.05
+    undesired_force_threshold: float = 1.0
+    feet_f_last_init: float = 0.0
 
     @classmethod
-    def standup(cls, **kw) -> "TaskCfg":
-        """Zbot6SUpEnvCfg (standup.py:191-447): 6 s episodes, terminal penalty 2, 4 reward terms."""
+    def standup(cls, curriculum_steps: int | None = None, curriculum: bool = True,
+                curriculum_weights: dict | None = None, **kw) -> "TaskCfg":
+        """Zbot6SUpEnvCfg (standup.py:191-447): 6 s episodes, terminal penalty 2, 4 reward terms,
+        my_curriculum at max_episode_length * 80 steps (or ``curriculum_steps``)."""
         d = dict(task=TASK_STANDUP_V0, episode_length_s=6.0, terminal_penalty=2.0, termination_height=0.20,
-                 reward_weights=dict(SU_REWARD_WEIGHTS), curriculum_weights=dict(SU_CURRICULUM_WEIGHTS))
+                 reward_weights=dict(SU_REWARD_WEIGHTS))
         d.update(kw)
-        return cls(**d)
+        c = cls(**d)
+        if curriculum:
+            thr = c.max_episode_length * 80 if curriculum_steps is None else curriculum_steps
+            c.stages = [(thr, dict(curriculum_weights or SU_CURRICULUM_WEIGHTS), None)]
+        return c
+
+    @classmethod
+    def walking_v4(cls, curriculum: bool = True, stage_scale: float | None = None, **kw) -> "TaskCfg":
+        """Zbot6SEnvV4Cfg (v4.py:443-686): 20 s episodes, history-3 contact sensor, died on an
+        undesired body force > 0.5 N or base below 0.20 m, 15 reward terms, commands, curricula.
+        ``stage_scale`` rescales the curriculum thresholds (tests)."""
+        d = dict(task=TASK_WALKING_V4, episode_length_s=20.0, terminal_penalty=20.0, termination_height=0.20,
+                 reward_weights=dict(V4_REWARD_WEIGHTS), reset_pose_range=((-0.5, 0.5), (-0.5, 0.5), (0.0, 0.0),
+                                                                           (-3.14, 3.14)),
+                 reset_pose_body_frame=True, undesired_force_threshold=0.5, feet_f_last_init=15.0)
+        d.update(kw)
+        c = cls(**d)
+        if curriculum:
+            L = c.max_episode_length if stage_scale is None else stage_scale
+            c.stages = [(int(ep * L), dict(w), p) for ep, w, p in V4_STAGES]
+        return c
 
     @property
     def obs_dim(self) -> int:
-        return SU_OBS_DIM if self.task == TASK_STANDUP_V0 else OBS_DIM
+        return {TASK_STANDUP_V0: SU_OBS_DIM, TASK_WALKING_V4: V4_OBS_DIM}.get(self.task, OBS_DIM)
 
     @property
     def state_dim(self) -> int:
-        return SU_STATE_DIM if self.task == TASK_STANDUP_V0 else STATE_DIM
+        return {TASK_STANDUP_V0: SU_STATE_DIM, TASK_WALKING_V4: V4_STATE_DIM}.get(self.task, STATE_DIM)
 
     @property
     def reward_terms(self) -> list:
-        return SU_REWARD_TERMS if self.task == TASK_STANDUP_V0 else REWARD_TERMS
+        return {TASK_STANDUP_V0: SU_REWARD_TERMS, TASK_WALKING_V4: V4_REWARD_TERMS}.get(self.task, REWARD_TERMS)
 
     @property
     def step_dt(self) -> float:
@@ -402,24 +471,54 @@ class TaskCfg:
     def max_episode_length(self) -> int:
         return math.ceil(self.episode_length_s / self.step_dt)
 
+    def stage_weights(self) -> list:
+        """Reward weights of every curriculum stage (stage 0 = reward_weights), cumulative updates."""
+        out = [dict(self.reward_weights)]
+        for _, upd, _ in self.stages:
+            w = dict(out[-1])
+            w.update(upd)
+            out.append(w)
+        return out
+
     def pack(self) -> ZbTaskCfg:
         c = ZbTaskCfg()
         c.sim_dt = self.sim_dt
         c.decimation = self.decimation
         c.max_episode_length = self.max_episode_length
         c.termination_height = self.termination_height
-        if self.task == TASK_STANDUP_V0:
-            # standup.py:624 multiplies by step_dt per term in _get_rewards (the kernel does)
-            for k, name in enumerate(SU_REWARD_TERMS):
-                c.reward_scales[k] = self.reward_weights.get(name, 0.0)
-                cw = self.curriculum_weights if self.curriculum_weights is not None else self.reward_weights
-                c.curriculum_scales[k] = cw.get(name, 0.0)
-            thr = self.max_episode_length * 80 if self.curriculum_steps is None else self.curriculum_steps
-            c.curriculum_steps = thr if self.curriculum_weights else 0
-        else:
+        if self.task == TASK_WALKING_V2:
             for k, name in enumerate(REWARD_TERMS):
                 # v2.py:250-252 multiplies every weight by step_dt at env construction
                 c.reward_scales[k] = self.reward_weights.get(name, 0.0) * self.step_dt
+        # standup.py:624 / v4.py:886 multiply by step_dt per term in _get_rewards (the kernel does)
+        ws = self.stage_weights()
+        if len(ws) > MAX_STAGES:
+            raise ValueError(f"at most {MAX_STAGES - 1} curriculum stages")
+        c.num_stages = len(ws)
+        prob = self.cmd_prob_pos
+        for sidx, w in enumerate(ws):
+            for k, name in enumerate(self.reward_terms if self.task != TASK_WALKING_V2 else []):
+                c.stage_scales[sidx][k] = w.get(name, 0.0)
+            if sidx > 0:
+                c.stage_steps[sidx] = int(self.stages[sidx - 1][0])
+                if self.stages[sidx - 1][2] is not None:
+                    prob = self.stages[sidx - 1][2]
+            c.stage_prob_pos[sidx] = prob
+        c.cmd_vel_range[0], c.cmd_vel_range[1] = self.cmd_vel_range
+        c.cmd_yaw_range[0], c.cmd_yaw_range[1] = self.cmd_yaw_range
+        c.cmd_dual_sign = int(self.cmd_dual_sign)
+        c.cmd_offset = self.cmd_offset
+        c.cmd_interval_s[0], c.cmd_interval_s[1] = self.cmd_interval_s
+        c.range_limit_vel[0], c.range_limit_vel[1] = self.range_limit_vel
+        c.range_limit_yaw[0], c.range_limit_yaw[1] = self.range_limit_yaw
+        c.range_start_steps = self.max_episode_length * self.range_start_episodes
+        c.range_period_steps = self.max_episode_length * self.range_period_episodes
+        c.range_min_buffer = self.range_min_buffer
+        c.range_threshold = self.range_threshold
+        c.range_delta = self.range_delta
+        c.undesired_force_threshold = self.undesired_force_threshold
+        c.feet_f_last_init = self.feet_f_last_init
+        c.reset_pose_body_frame = int(self.reset_pose_body_frame)
         c.task = self.task
         for k in range(4):
             c.reset_pose_range[k][0], c.reset_pose_range[k][1] = self.reset_pose_range[k]

@@ -1,4 +1,4 @@
 from .vecenv import RslRlVecEnvWrapper  # noqa: F401
-from .cfg import PPORunnerCfgV2, Zbot6SUpEnvPPOCfg  # noqa: F401
+from .cfg import PPORunnerCfgV2, Zbot6SEnvV4PPOCfg, Zbot6SUpEnvPPOCfg  # noqa: F401
 from .ppo import PPO, ActorCritic, RolloutStorage  # noqa: F401
 from .runner import OnPolicyRunner  # noqa: F401

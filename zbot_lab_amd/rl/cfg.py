@@ -1,5 +1,5 @@
 """``PPORunnerCfgV2`` (reference ``source/zbot/zbot/tasks/zbot6b_direct/agents/rsl_rl_ppo_cfg.py:65-91``) and
-``Zbot6SUpEnvPPOCfg`` (same file, 264-289).
+``Zbot6SUpEnvPPOCfg`` (same file, 264-289), ``Zbot6SEnvV4PPOCfg`` (206-233).
 
 Consumed by ``zbot_lab_amd.rl.OnPolicyRunner`` (``agent_cfg.to_dict()``, as ``train.py:192``)."""
 from __future__ import annotations
@@ -55,5 +55,15 @@ class PPORunnerCfgV2:
 class Zbot6SUpEnvPPOCfg(PPORunnerCfgV2):
     """rsl_rl_ppo_cfg.py:264-289: the stand-up task's [256, 256, 128] actor / critic."""
     experiment_name: str = "zbot_6b_flat_direct_standup"
+    policy: RslRlPpoActorCriticCfg = field(default_factory=lambda: RslRlPpoActorCriticCfg(
+        actor_hidden_dims=[256, 256, 128], critic_hidden_dims=[256, 256, 128]))
+
+
+@dataclass
+class Zbot6SEnvV4PPOCfg(PPORunnerCfgV2):
+    """rsl_rl_ppo_cfg.py:206-233: v4's [256, 256, 128] actor / critic, 2000 iterations."""
+    max_iterations: int = 2000
+    save_interval: int = 1000
+    experiment_name: str = "zbot_6b_flat_direct_v4"
     policy: RslRlPpoActorCriticCfg = field(default_factory=lambda: RslRlPpoActorCriticCfg(
         actor_hidden_dims=[256, 256, 128], critic_hidden_dims=[256, 256, 128]))

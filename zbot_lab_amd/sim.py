@@ -50,7 +50,7 @@ class ZbotSim:
         # persistent outputs (reference: terminated/truncated buffers are mutated in place)
         self.terminated = torch.zeros(self.num_envs, dtype=torch.bool, device=self.device)
         self.truncated = torch.zeros(self.num_envs, dtype=torch.bool, device=self.device)
-        self._log_means = torch.zeros(zm.NUM_TERMS, dtype=torch.float32, device=self.device)  # first num_terms used
+        self._log_means = torch.zeros(zm.LOG_LEN, dtype=torch.float32, device=self.device)  # include/zbot.h ZB_LOG_LEN
         self._log_counts = torch.zeros(2, dtype=torch.int32, device=self.device)
         # the library fills these in stream order at every step/reset with resets (no copies)
         nat.check(self.lib.zb_set_log_buffers(self._h, nat.ptr(self._log_means), nat.ptr(self._log_counts)),
@@ -102,6 +102,11 @@ class ZbotSim:
         """(term_means[num_terms], counts[2]) device tensors of the most recent step that had resets
         (registered with zb_set_log_buffers, so no per-step copy)."""
         return self._log_means[:self.num_terms], self._log_counts
+
+    @property
+    def log_buffer(self) -> torch.Tensor:
+        """The whole float[ZB_LOG_LEN] log buffer (term means, then the curriculum entries)."""
+        return self._log_means
 
     def set_link_friction(self, mu: torch.Tensor) -> None:
         """Standup: per-link friction coefficients [N, 12] (randomize_rigid_body_material)."""

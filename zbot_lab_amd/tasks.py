@@ -1,5 +1,6 @@
 """Task registry: ``make("zbot-6b-walking-v2")`` like ``gym.make`` on the reference's registration
-(``source/zbot/zbot/tasks/zbot6b_direct/__init__.py:41-49``; ``zbot-6b-standup-v0`` 111-119)."""
+(``source/zbot/zbot/tasks/zbot6b_direct/__init__.py:41-49``; ``zbot-6b-standup-v0`` 111-119;
+``zbot-6b-walking-v4`` 91-99)."""
 from __future__ import annotations
 
 import importlib
@@ -65,5 +66,14 @@ register(
     kwargs={
         "env_cfg_entry_point": "zbot_lab_amd.envs.standup_v0:Zbot6SUpEnvCfg",
         "rsl_rl_cfg_entry_point": "zbot_lab_amd.rl.cfg:Zbot6SUpEnvPPOCfg",
+    },
+)
+
+register(
+    id="zbot-6b-walking-v4",
+    entry_point="zbot_lab_amd.envs.walking_v4:Zbot6SEnvV4",
+    kwargs={
+        "env_cfg_entry_point": "zbot_lab_amd.envs.walking_v4:Zbot6SEnvV4Cfg",
+        "rsl_rl_cfg_entry_point": "zbot_lab_amd.rl.cfg:Zbot6SEnvV4PPOCfg",
     },
 )
