@@ -150,11 +150,34 @@ def fit_sphere_pair(circles, rng_seed=0):
     return best
 
 
-def main():
-    c = Crate(REF_USD)
+# ZBOT_6S_V2_CFG (zbot_cfg.py:959-1005) on zbot_6s_v09.usd, the manager-based env's robot: the same
+# 12 modules re-rooted at the base (two 3-joint branches); links listed here in chain order
+# foot0 -> foot1 so that the simulator's serial-chain model can be built from it (model.py).
+V09_USD = "/root/reference/source/zbot/zbot/assets/zbot_assets/zbot_6s_v09.usd"
+V09_OUT = os.path.join(os.path.dirname(__file__), "..", "zbot_lab_amd", "assets", "zbot6s_v09_model.json")
+V09_LINKS = ["foot0", "a3", "b2", "a2", "b1", "base", "a7", "b7", "a8", "b8", "a9", "foot1"]
+V09_CFG = {
+    # zbot_cfg.py:978-993 init_state (the articulation root is the base link)
+    "root_link": "base",
+    "root_pos": [0.0, 0.0, 0.2545],
+    "root_rot_wxyz": [1.0, 0.0, 0.0, 0.0],
+    "joint_pos": {"joint1": 2.02, "joint2": -0.837, "joint3": -0.312, "joint7": -2.02, "joint8": 0.837,
+                  "joint9": 0.312},
+    # zbot_cfg.py:995-1004 ImplicitActuatorCfg
+    "stiffness": 20.0, "damping": 0.5, "effort_limit": 20.0, "velocity_limit": 10.0,
+    # zbot_cfg.py:960-976 spawn props
+    "max_depenetration_velocity": 1.0, "linear_damping": 0.0, "angular_damping": 0.0,
+    "enabled_self_collisions": True, "solver_position_iteration_count": 4,
+    "solver_velocity_iteration_count": 0,
+}
+
+
+def main(usd: str = REF_USD, link_names: list = LINKS, out: str = OUT, cfg: dict | None = None,
+         source_cfg: str = "source/zbot/zbot/assets/zbot_cfg.py:621-669 (ZBOT_6S_CFG)"):
+    c = Crate(usd)
     links = []
     shape_cache = {}
-    for name in LINKS:
+    for name in link_names:
         p = f"/zbot/{name}"
         col = f"{p}/collisions"
         pts = np.array(c.get(col + ".points"), dtype=np.float64)
@@ -212,17 +235,17 @@ def main():
         if j["type"] == "revolute":
             j["axis"] = c.get(path + ".physics:axis")
         joints.append(j)
-    joints.sort(key=lambda j: LINKS.index(j["body0"]))
+    joints.sort(key=lambda j: min(link_names.index(j["body0"]), link_names.index(j["body1"])))
 
     model = {
         "source": {
-            "usd": "source/zbot/zbot/assets/zbot_assets/zbot_6s_new.usd (USDC crate 0.8.0)",
-            "cfg": "source/zbot/zbot/assets/zbot_cfg.py:621-669 (ZBOT_6S_CFG)",
+            "usd": os.path.relpath(usd, "/root/reference") + " (USDC crate 0.8.0)",
+            "cfg": source_cfg,
             "tool": "tools/extract_model.py",
         },
         "links": links,
         "joints": joints,
-        "cfg": {
+        "cfg": cfg if cfg is not None else {
             # zbot_cfg.py:641-656 init_state
             "root_pos": [0.0, -0.06, 0.0],
             "root_rot_wxyz": [1.0, 0.0, 0.0, 0.0],
@@ -236,11 +259,14 @@ def main():
             "solver_velocity_iteration_count": 0,
         },
     }
-    os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    with open(OUT, "w") as f:
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    with open(out, "w") as f:
         json.dump(model, f, indent=1)
-    print("wrote", os.path.normpath(OUT))
+    print("wrote", os.path.normpath(out))
 
 
 if __name__ == "__main__":
-    main()
+    if "--v09" in sys.argv:
+        main(V09_USD, V09_LINKS, V09_OUT, V09_CFG, "source/zbot/zbot/assets/zbot_cfg.py:959-1005 (ZBOT_6S_V2_CFG)")
+    else:
+        main()

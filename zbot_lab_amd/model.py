@@ -201,6 +201,15 @@ class RobotModel:
     default_root_pos: np.ndarray
     default_root_quat: np.ndarray
     cfg: dict
+    # Isaac Lab view of the articulation (differs from the internal chain when the USD's
+    # articulation root is not the first chain link, e.g. zbot_6s_v09.usd rooted at the base):
+    link_names: list = field(default_factory=lambda: list(LINK_NAMES))
+    joint_names: list = field(default_factory=lambda: list(JOINT_NAMES))  # USD name of internal joint k
+    joint_sign: np.ndarray = field(default_factory=lambda: np.ones(NUM_DOF))  # q_usd = sign * q_internal
+    api_joint_index: list = field(default_factory=lambda: list(range(NUM_DOF)))  # Isaac Lab index of joint k
+    api_root_link: int = 0            # chain index of the Isaac Lab root link
+    api_root_in_root: tuple = ((0.0, 0.0, 0.0), (1.0, 0.0, 0.0, 0.0))  # its pose in the chain root frame
+    base_link: int = 6
 
     def fk(self, root_pos, root_quat, q):
         """World transforms of the 7 bodies and 12 links (float64, composition order of PhysX)."""
@@ -220,47 +229,55 @@ def _perp_basis(n):
     return e1, np.cross(n, e1)
 
 
+_AXIS_TO_Z = {  # rotation taking the local z axis onto the joint axis
+    "Z": np.array([1.0, 0.0, 0.0, 0.0]),
+    "Y": np.array([math.cos(-math.pi / 4), math.sin(-math.pi / 4), 0.0, 0.0]),   # Rx(-90 deg): z -> y
+    "X": np.array([math.cos(math.pi / 4), 0.0, math.sin(math.pi / 4), 0.0]),     # Ry(+90 deg): z -> x
+}
+
+
 def load_model(path: str = ASSET) -> RobotModel:
+    """Build the serial-chain model from a decoded asset whose ``links`` are listed in chain order
+    (first link = the simulator's root). Joints may point either way along the chain (a USD whose
+    articulation root is mid-chain); a joint traversed against its body0 -> body1 direction is
+    inverted and its angle negated. Revolute axes other than Z get a constant frame rotation."""
     raw = json.load(open(path))
+    names = [l["name"] for l in raw["links"]]
+    assert len(names) == NUM_LINKS
     links = {l["name"]: l for l in raw["links"]}
-    assert [l["name"] for l in raw["links"]] == LINK_NAMES
-    by_parent = {j["body0"]: j for j in raw["joints"]}
-    root = [l["name"] for l in raw["links"] if l["articulation_root"]]
-    assert root == ["foot_0"], root
+    pair = {frozenset((j["body0"], j["body1"])): j for j in raw["joints"]}
 
     link_body = [0] * NUM_LINKS
     link_xf = [Xf() for _ in range(NUM_LINKS)]
     joints = []
+    joint_names, joint_sign = [], []
     body = 0
-    cur = "foot_0"
-    while cur in by_parent:
-        j = by_parent[cur]
-        lp0 = np.array(j["local_pos0"], float)
-        lr0 = qnorm(j["local_rot0_wxyz"])
-        lp1 = np.array(j["local_pos1"], float)
-        lr1 = qnorm(j["local_rot1_wxyz"])
-        child = j["body1"]
-        ci, pi = LINK_NAMES.index(child), LINK_NAMES.index(cur)
-        j0 = Xf(lp0, lr0)
-        j1inv = Xf(lp1, lr1).inv()
+    for k in range(1, NUM_LINKS):
+        prev, cur = names[k - 1], names[k]
+        j = pair[frozenset((prev, cur))]
+        fwd = j["body0"] == prev
+        T0 = Xf(np.array(j["local_pos0"], float), qnorm(j["local_rot0_wxyz"]))
+        T1 = Xf(np.array(j["local_pos1"], float), qnorm(j["local_rot1_wxyz"]))
+        Tp, Tc = (T0, T1) if fwd else (T1, T0)  # parent-side / child-side joint frames
         if j["type"] == "fixed":
-            link_body[ci] = body
-            link_xf[ci] = link_xf[pi] * j0 * j1inv
+            link_body[k] = body
+            link_xf[k] = link_xf[k - 1] * Tp * Tc.inv()
         else:
-            assert j["axis"] == "Z"
+            A = Xf(np.zeros(3), _AXIS_TO_Z[j["axis"]])
             body += 1
-            link_body[ci] = body
-            link_xf[ci] = Xf()
-            joints.append({"name": j["name"], "parent_xf": link_xf[pi] * j0, "child_xf": j1inv})
-        cur = child
-    assert body == NUM_BODIES - 1 and [j["name"] for j in joints] == JOINT_NAMES
+            link_body[k] = body
+            link_xf[k] = Xf()
+            joints.append({"name": j["name"], "parent_xf": link_xf[k - 1] * Tp * A, "child_xf": (Tc * A).inv()})
+            joint_names.append(j["name"])
+            joint_sign.append(1.0 if fwd else -1.0)
+    assert body == NUM_BODIES - 1 and len(joints) == NUM_DOF
 
     # composite mass properties (authored link values, used verbatim)
     body_mass = np.zeros(NUM_BODIES)
     body_mc = np.zeros((NUM_BODIES, 3))
     link_com = np.zeros((NUM_LINKS, 3))
     link_I = []
-    for i, name in enumerate(LINK_NAMES):
+    for i, name in enumerate(names):
         l = links[name]
         xf = link_xf[i]
         com_b = xf.apply(l["com"])
@@ -273,7 +290,7 @@ def load_model(path: str = ASSET) -> RobotModel:
         body_mc[link_body[i]] += l["mass"] * com_b
     body_com = body_mc / body_mass[:, None]
     body_inertia = np.zeros((NUM_BODIES, 3, 3))
-    for i, name in enumerate(LINK_NAMES):
+    for i, name in enumerate(names):
         b = link_body[i]
         d = link_com[i] - body_com[b]
         m = links[name]["mass"]
@@ -282,7 +299,7 @@ def load_model(path: str = ASSET) -> RobotModel:
     circles = np.zeros((NUM_LINKS, 2, 9))
     spheres = np.zeros((NUM_LINKS, 2, 4))
     bounds = np.zeros((NUM_LINKS, 4))
-    for i, name in enumerate(LINK_NAMES):
+    for i, name in enumerate(names):
         l = links[name]
         xf = link_xf[i]
         pts = []
@@ -301,19 +318,54 @@ def load_model(path: str = ASSET) -> RobotModel:
         bounds[i] = np.r_[ctr, np.linalg.norm(pts - ctr, axis=1).max() + 1e-4]
 
     # PhysX filters self-collision between joint-connected links (incl. fixed joints)
-    connected = {frozenset((LINK_NAMES.index(j["body0"]), LINK_NAMES.index(j["body1"])))
-                 for j in raw["joints"]}
+    connected = {frozenset((names.index(j["body0"]), names.index(j["body1"]))) for j in raw["joints"]}
     self_pairs = [(a, b) for a in range(NUM_LINKS) for b in range(a + 1, NUM_LINKS)
                   if frozenset((a, b)) not in connected]
 
     cfg = raw["cfg"]
-    q0 = np.array([cfg["joint_pos"][n] for n in JOINT_NAMES], float)
-    return RobotModel(raw=raw, link_body=link_body, link_xf=link_xf, joints=joints,
-                      body_mass=body_mass, body_com=body_com, body_inertia=body_inertia,
-                      link_com=link_com, circles=circles, spheres=spheres, bounds=bounds,
-                      self_pairs=self_pairs, default_joint_pos=q0,
-                      default_root_pos=np.array(cfg["root_pos"], float),
-                      default_root_quat=np.array(cfg["root_rot_wxyz"], float), cfg=cfg)
+    sign = np.array(joint_sign)
+    q0 = sign * np.array([cfg["joint_pos"][n] for n in joint_names], float)
+    # Isaac Lab orders joints breadth-first from the articulation root (PhysX tensor API)
+    root_name = cfg.get("root_link", names[0])
+    root_idx = names.index(root_name)
+    order, seen, queue = [], {root_name}, [root_name]
+    while queue:
+        cur = queue.pop(0)
+        nbr = sorted((j for j in raw["joints"] if cur in (j["body0"], j["body1"])),
+                     key=lambda j: min(names.index(j["body0"]), names.index(j["body1"])))
+        for j in nbr:
+            other = j["body1"] if j["body0"] == cur else j["body0"]
+            if other in seen:
+                continue
+            seen.add(other)
+            queue.append(other)
+            if j["type"] != "fixed":
+                order.append(j["name"])
+    api_index = [order.index(n) for n in joint_names]
+    rm = RobotModel(raw=raw, link_body=link_body, link_xf=link_xf, joints=joints,
+                    body_mass=body_mass, body_com=body_com, body_inertia=body_inertia,
+                    link_com=link_com, circles=circles, spheres=spheres, bounds=bounds,
+                    self_pairs=self_pairs, default_joint_pos=q0,
+                    default_root_pos=np.array(cfg["root_pos"], float),
+                    default_root_quat=np.array(cfg["root_rot_wxyz"], float), cfg=cfg,
+                    link_names=names, joint_names=joint_names, joint_sign=sign, api_joint_index=api_index,
+                    api_root_link=root_idx, base_link=names.index("base"))
+    if root_idx != 0:
+        # the cfg's root pose is the Isaac Lab root's; the chain root's follows from the default pose
+        _, lk = rm.fk(np.zeros(3), np.array([1.0, 0, 0, 0]), q0)
+        T = lk[root_idx]
+        rm.api_root_in_root = (tuple(T.p), tuple(T.q))
+        Xroot = Xf(rm.default_root_pos, qnorm(rm.default_root_quat)) * T.inv()
+        rm.default_root_pos, rm.default_root_quat = Xroot.p, Xroot.q
+    return rm
+
+
+V09_ASSET = os.path.join(os.path.dirname(__file__), "assets", "zbot6s_v09_model.json")
+
+
+def load_v09_model() -> RobotModel:
+    """ZBOT_6S_V2_CFG on zbot_6s_v09.usd (zbot_cfg.py:959-1005): the manager-based env's robot."""
+    return load_model(V09_ASSET)
 
 
 def standup_model(rm: RobotModel | None = None) -> RobotModel:
@@ -369,9 +421,10 @@ def pack_model(rm: RobotModel | None = None) -> ZbModel:
     m.kp, m.kd = c["stiffness"], c["damping"]
     m.effort_limit, m.velocity_limit = c["effort_limit"], c["velocity_limit"]
     m.max_depenetration_velocity = c["max_depenetration_velocity"]
-    m.base_link = LINK_NAMES.index("base")
-    m.foot_links[0], m.foot_links[1] = LINK_NAMES.index("foot_0"), LINK_NAMES.index("foot_1")
-    undesired = [i for i, n in enumerate(LINK_NAMES) if n == "base" or n[0] in "ab"]
+    m.base_link = rm.base_link
+    feet = [i for i, n in enumerate(rm.link_names) if n.startswith("foot")]  # "foot.*"
+    m.foot_links[0], m.foot_links[1] = feet
+    undesired = [i for i, n in enumerate(rm.link_names) if n == "base" or n[0] in "ab"]  # "base|a.*|b.*"
     assert len(undesired) == 10
     for k, i in enumerate(undesired):
         m.undesired_links[k] = i
