@@ -60,6 +60,9 @@ extern "C" {
 #define ZB_TASK_WALKING_V2 0  /* zbot-6b-walking-v2 (v2.py) */
 #define ZB_TASK_STANDUP_V0 1  /* zbot-6b-standup-v0 (standup.py) */
 #define ZB_TASK_WALKING_V4 2  /* zbot-6b-walking-v4 (v4.py): v2 + commands, events, curricula */
+#define ZB_TASK_MANAGER_V0 3  /* zbot-6b-walking-m-v0: the manager-based flat env (zbotlab_env_cfg.py) */
+#define ZB_M_OBS_DIM 25       /* base quat 4, velocity command 3, joint pos 6, joint vel 6, last action 6 */
+#define ZB_M_NUM_REWARD_TERMS 11
 #define ZB_SU_OBS_DIM 22      /* standup.py:199 */
 #define ZB_SU_NUM_REWARD_TERMS 4
 #define ZB_V4_OBS_DIM 24      /* v4.py:453 */
@@ -72,6 +75,10 @@ extern "C" {
  * [16] Curriculum/curriculum_stage, [17..18] Curriculum/vel_lower_bound, vel_upper_bound,
  * [19] Curriculum/yaw_bound (v4 only; v4.py:952-957) */
 #define ZB_LOG_LEN 20
+/* Termination counts (zb_read_log counts[ZB_LOG_COUNTS]): walking v2 {body_contact, time_out},
+ * standup / v4 {died, time_out}, manager {base_height, time_out, feet_close}; the manager's log
+ * floats [16..18] are Curriculum/lin_vel_cmd_levels, Metrics/base_velocity/error_vel_xy, error_vel_yaw */
+#define ZB_LOG_COUNTS 4
 
 /* Persistent per-env state, SoA [ZB_STATE_DIM][num_envs] float32. */
 enum zb_state_field {
@@ -132,6 +139,38 @@ enum zb_v4_state_field {
   ZB_V4_STATE_DIM = 85
 };
 
+/* Manager-based flat env state (zbot-6b-walking-m-v0), SoA [ZB_M_STATE_DIM][num_envs]; rows 0..24
+ * are the internal chain's physics state as in zb_state_field (the Isaac Lab root is the base link,
+ * see zb_model.api_root_*). */
+enum zb_manager_state_field {
+  ZB_M_ACTIONS = 25,          /* 6  raw actions of the last step, Isaac Lab joint order (last_action) */
+  ZB_M_COMMANDS = 31,         /* 3  base_velocity command (lin x, lin y, ang z) */
+  ZB_M_CMD_TIME_LEFT = 34,    /* 1  command resampling timer (s) */
+  ZB_M_CMD_STANDING = 35,     /* 1  is_standing_env (0 / 1) */
+  ZB_M_FEET_DOWN_POS = 36,    /* 6  env.feet_down_pos_last (rewards.py:29-35) */
+  ZB_M_FEET_STEP_LEN = 42,    /* 2 */
+  ZB_M_FEET_F_LAST = 44,      /* 2 */
+  ZB_M_FEET_FZ_HIST = 46,     /* 6  [slot][foot] net_forces_w_history[..., feet, 2], slot 0 newest; the
+                                 sensor (history 3) updates every physics step: substeps 4, 3, 2 */
+  ZB_M_FEET_FN_HIST = 52,     /* 6  [slot][foot] |net force| of the feet */
+  ZB_M_FEET_AIR_CUR = 58,     /* 2 */
+  ZB_M_FEET_AIR_LAST = 60,    /* 2 */
+  ZB_M_METRICS = 62,          /* 2  command metrics error_vel_xy, error_vel_yaw */
+  ZB_M_EP_LEN = 64,           /* 1 */
+  ZB_M_EP_SUMS = 65,          /* 11 reward manager episode sums */
+  ZB_M_LINK_MU = 76,          /* 12 per-link friction (physics_material startup event) */
+  ZB_M_STATE_DIM = 88
+};
+
+/* Manager reward term order = RewardsCfg field order of Zbot6BFlatEnvCfg (zbotlab_env_cfg.py,
+ * flat_env_cfg.py) with the terms the flat cfg sets to None removed
+ * (zbotlab_env_cfg.py:261-377, flat_env_cfg.py:169-182). */
+enum zb_manager_reward_term {
+  ZB_M_R_TRACK_LIN_VEL_XY = 0, ZB_M_R_TRACK_ANG_VEL_Z, ZB_M_R_TERMINATION, ZB_M_R_DOF_TORQUES, ZB_M_R_DOF_ACC,
+  ZB_M_R_ACTION_RATE, ZB_M_R_FOOT_STEP_LENGTH, ZB_M_R_FOOT_DOWNWARD, ZB_M_R_FOOT_FORWARD, ZB_M_R_FEET_SLIDE,
+  ZB_M_R_AIR_TIME_BALANCE
+};
+
 /* v4 reward term order = dict order of Zbot6SEnvV4Cfg.reward_cfg (v4.py:620-641). */
 enum zb_v4_reward_term {
   ZB_V4_R_TRACK_LIN_VEL_X = 0, ZB_V4_R_TRACK_HEADING_YAW, ZB_V4_R_LIN_VEL_Y, ZB_V4_R_ACTION_RATE, ZB_V4_R_TORQUES,
@@ -182,6 +221,13 @@ typedef struct zb_model {
   float kp, kd, effort_limit, velocity_limit, max_depenetration_velocity;
   /* indices used by the MDP */
   int32_t base_link, foot_links[2], undesired_links[10];
+  /* Isaac Lab's view when its articulation root is not chain link 0 (zbot_6s_v09.usd: the base):
+   * the root link, its pose in the chain root's frame at the default joints, and per internal joint
+   * k the Isaac Lab (breadth-first) joint index and sign (q_isaac = sign * q_internal) */
+  int32_t api_root_link;
+  float api_root_in_root[7];    /* pos 3, quat wxyz 4 */
+  int32_t api_joint_index[ZB_NUM_DOF];
+  float api_joint_sign[ZB_NUM_DOF];
 } zb_model;
 
 /* Task / simulation constants: ZbotDirectEnvCfgV2 (v2.py:26-206) or Zbot6SUpEnvCfg
@@ -232,6 +278,17 @@ typedef struct zb_task_cfg {
   float range_delta;           /* 0.05 */
   float undesired_force_threshold; /* died: max |F| of an undesired body over the history > this (v2 1.0, v4 0.5) */
   float feet_f_last_init;      /* v4 feet_contact_forces_last after construction / reset: 15 (v4.py:731,979) */
+  /* manager env (zbotlab_env_cfg.py): RelativeJointPositionAction, observation noise, command
+   * term, terminations; the command ranges reuse cmd_vel_range (lin_vel_x) and cmd_yaw_range
+   * (lin_vel_y), and lin_vel_cmd_levels reuses range_* (limit_ranges x / y, delta 0.1, threshold
+   * 0.8, period max_episode_length; curriculums.py:57-83) */
+  float action_scale;          /* 0.04 pi (zbotlab_env_cfg.py:125-131) */
+  float action_clip;           /* processed-action clip +-0.04 pi */
+  int32_t obs_corruption;      /* ObsGroup enable_corruption */
+  float obs_noise[3];          /* additive U(-n, n): base quat 0.01, joint pos 0.01, joint vel 1.5 */
+  float cmd_resample_s;        /* resampling_time_range (10, 10) */
+  float cmd_rel_standing;      /* rel_standing_envs 0.02 */
+  float feet_close_min;        /* feet_close termination: feet distance < 0.12 m */
 } zb_task_cfg;
 
 typedef struct zb_sim* zb_handle;
@@ -259,9 +316,9 @@ int zb_observe(zb_handle h, float* obs, void* stream);
 
 /* Episode log of the most recent step with resets: term_means[ZB_LOG_LEN] (layout at
  * ZB_LOG_LEN; walking v2: mean episodic sum / 20 s, standup / v4: mean of sum / own duration),
- * counts[2] = {body_contact | died, time_out} (v2.py:441-459). Device pointers. */
+ * counts[ZB_LOG_COUNTS] (layout at ZB_LOG_COUNTS; v2.py:441-459). Device pointers. */
 int zb_read_log(zb_handle h, float* term_means, int32_t* counts, void* stream);
-/* Register caller-owned device buffers (float[ZB_LOG_LEN], int32[2]) that every later step/reset with
+/* Register caller-owned device buffers (float[ZB_LOG_LEN], int32[ZB_LOG_COUNTS]) that every later step/reset with
  * resets fills in stream order, exactly as zb_read_log would (no per-step copies). NULL, NULL
  * unregisters. */
 int zb_set_log_buffers(zb_handle h, float* term_means, int32_t* counts);

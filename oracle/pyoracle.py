@@ -88,8 +88,9 @@ class OracleSim:
         self.n = num_envs
         self.obs_dim, self.state_dim = self.cfg.obs_dim, self.cfg.state_dim
         self.num_terms = len(self.cfg.reward_terms)
-        standup = self.cfg.task == zm.TASK_STANDUP_V0
-        self._m = zm.pack_model(zm.standup_model() if standup else None)
+        task = self.cfg.task
+        self._m = zm.pack_model(zm.standup_model() if task == zm.TASK_STANDUP_V0
+                                else zm.load_v09_model() if task == zm.TASK_MANAGER_V0 else None)
         self._c = self.cfg.pack()
         if threads:
             self.lib.zbo_set_threads(threads)
@@ -123,13 +124,13 @@ class OracleSim:
 
     def read_log(self, full: bool = False):
         m = np.zeros(zm.LOG_LEN, np.float32)
-        c = np.zeros(2, np.int32)
+        c = np.zeros(zm.LOG_COUNTS, np.int32)
         self.lib.zbo_read_log(self.h, m, c)
         return (m if full else m[:self.num_terms]), c
 
     def set_link_friction(self, mu):
         if self.lib.zbo_set_link_friction(self.h, f32(mu)) != 0:
-            raise ValueError("per-link friction is a standup-task state")
+            raise ValueError("per-link friction is a standup / manager task state")
 
     def read_curriculum(self):
         st, n = C.c_int32(), C.c_int64()

@@ -102,6 +102,9 @@ typedef struct {
   real root_pos0[3], root_quat0[4], jq0[ND];
   real kp, kd, effort, vlim, max_depen;
   int base_link, foot_links[2], undesired[10];
+  real api_t[3], api_q[4];            /* Isaac Lab root in the chain root's frame (v09: the base) */
+  int api_index[ND];                  /* chain joint j -> Isaac Lab joint order */
+  real api_sign[ND];
 } mdl_t;
 
 static void load_mdl(const zb_model* m, mdl_t* o) {
@@ -133,6 +136,9 @@ static void load_mdl(const zb_model* m, mdl_t* o) {
   o->base_link = m->base_link;
   o->foot_links[0] = m->foot_links[0]; o->foot_links[1] = m->foot_links[1];
   for (int k = 0; k < 10; ++k) o->undesired[k] = m->undesired_links[k];
+  for (int a = 0; a < 3; ++a) o->api_t[a] = m->api_root_in_root[a];
+  for (int a = 0; a < 4; ++a) o->api_q[a] = m->api_root_in_root[3 + a];
+  for (int j = 0; j < ND; ++j) { o->api_index[j] = m->api_joint_index[j]; o->api_sign[j] = m->api_joint_sign[j]; }
 }
 
 /* ------------------------------------------------------------------------- per-env state */
@@ -145,7 +151,10 @@ typedef struct {
   real p_delta[ND], actions[ND];
   real center_z_last;                 /* standup only (standup.py:511) */
   real mu[NL];                        /* standup only: per-link friction (DR) */
-  real commands[2], target_yaw, interval_left, current_yaw; /* v4 only */
+  real commands[3], target_yaw, interval_left, current_yaw; /* v4 (2 commands) / manager (3; interval_left =
+                                                             command time_left) */
+  real cmd_standing, metrics[2];      /* manager only */
+  real feet_fn_hist[3][2];            /* manager only: |net force| of the feet, per physics step */
   real feet_down_pos[2][3], feet_step_len[2], feet_f_last[2];
   real heading_sum, yerr_sum;
   real feet_fz_hist[ZB_HIST][2], undes_fmax_hist[ZB_HIST];
@@ -168,7 +177,10 @@ struct zbo_sim {
   float ring_vel[ZB_V4_RING], ring_yaw[ZB_V4_RING];
   env_t* env;
   float log_means[ZB_LOG_LEN];
-  int32_t log_counts[2];
+  int32_t log_counts[ZB_LOG_COUNTS];
+  int changed;                  /* manager: lin_vel_cmd_levels widened the ranges in this call */
+  double met_acc[2];            /* manager: summed command metrics of this call's reset envs */
+  int nclose;                   /* manager: feet_close terminations of this call */
 };
 typedef struct zbo_sim zbo_sim;
 
@@ -990,14 +1002,25 @@ static void pose_from_samples(const mdl_t* m, const real r[4], int body_frame, p
   const real cr = (real)cos(0.5 * (double)r[2]), sr = (real)sin(0.5 * (double)r[2]);
   const real cy = (real)cos(0.5 * (double)r[3]), sy = (real)sin(0.5 * (double)r[3]);
   const real dq[4] = {cy * cr, cy * sr, sy * sr, sy * cr};
-  real qn[4];
-  if (body_frame) q_mul(m->root_quat0, dq, qn);
-  else q_mul(dq, m->root_quat0, qn);
-  q_normalize(qn);
+  /* the sampled pose is the Isaac Lab root's: its default pose is chain-root default * T
+   * (T = api_root_in_root; identity unless the asset is rooted elsewhere, as v09 at the base) */
+  real qa0[4], ta[3], R0[9];
+  q_mul(m->root_quat0, m->api_q, qa0);
+  q_to_mat(m->root_quat0, R0);
+  m3_v(R0, m->api_t, ta);
+  real qa[4];
+  if (body_frame) q_mul(qa0, dq, qa);
+  else q_mul(dq, qa0, qa);
+  q_normalize(qa);
+  const real pa[3] = {m->root_pos0[0] + ta[0] + r[0], m->root_pos0[1] + ta[1] + r[1], m->root_pos0[2] + ta[2]};
+  /* back to the chain root: q = qa * conj(qT), p = pa - R(q) tT */
+  const real qTc[4] = {m->api_q[0], -m->api_q[1], -m->api_q[2], -m->api_q[3]};
+  real qn[4], Rn[9], tq[3];
+  q_mul(qa, qTc, qn);
+  q_to_mat(qn, Rn);
+  m3_v(Rn, m->api_t, tq);
   for (int a = 0; a < 4; ++a) p->root_quat[a] = qn[a];
-  p->root_pos[0] = m->root_pos0[0] + r[0];
-  p->root_pos[1] = m->root_pos0[1] + r[1];
-  p->root_pos[2] = m->root_pos0[2];
+  for (int a = 0; a < 3; ++a) p->root_pos[a] = pa[a] - tq[a];
   for (int a = 0; a < 3; ++a) { p->root_linvel[a] = 0; p->root_angvel[a] = 0; }
   for (int j = 0; j < ND; ++j) { p->jq[j] = m->jq0[j]; p->jqd[j] = 0; }
 }
@@ -1518,6 +1541,344 @@ static void v4_unpack_env(env_t* e, const float* st, int n, int i) {
 #undef GET
 }
 
+/* ========================================================================= manager-based env
+ * zbot-6b-walking-m-v0: ManagerBasedRLEnv over Zbot6BFlatEnvCfg (zbotlab_env_cfg.py = "mgr.py",
+ * config/zbot6b_manager/flat_env_cfg.py, mdp/rewards.py, terminations.py, curriculums.py) on
+ * ZBOT_6S_V2_CFG (Isaac Lab root = the base link). Step order (ManagerBasedRLEnv.step): action
+ * processing, 4 x (apply_action, physics, scene.update -> contact sensor with history 3 > 0 updated
+ * every physics step), ep_len + 1, terminations, rewards, _reset_idx (curriculum, reset events,
+ * managers), command compute, observations (additive noise). The counter-based draws are the
+ * kernel's: reset pose 1..4, reset command 5..7, interval command 9..11, observation noise 16..37. */
+#define M_DRAW_RESET_CMD 5
+#define M_DRAW_CMD 9
+#define M_DRAW_NOISE 16
+
+/* UniformVelocityCommand._resample_command: lin x ~ U(ranges.lin_vel_x), lin y ~ U(ranges.lin_vel_y)
+ * (s->yaw holds the lin_vel_y range for this task), ang z ~ U(0, 0), standing ~ U(0,1) <= rel */
+static void m_resample(const zbo_sim* s, uint64_t h, int k0, real cmd[3], real* standing) {
+  cmd[0] = draw(h, k0) * ((real)s->vel[1] - (real)s->vel[0]) + (real)s->vel[0];
+  cmd[1] = draw(h, k0 + 1) * ((real)s->yaw[1] - (real)s->yaw[0]) + (real)s->yaw[0];
+  cmd[2] = 0;
+  *standing = draw(h, k0 + 2) <= (real)s->c.cmd_rel_standing ? 1 : 0;
+}
+
+/* the post-step articulation / sensor data the flat manager terms read */
+typedef struct {
+  real base_pos[3], base_quat[4];   /* root_link_pos_w / root_link_quat_w (= root_pos_w / root_quat_w) */
+  real base_lin_vel[3];             /* root_link_lin_vel_w */
+  real base_ang_vel[3];             /* root_link_ang_vel_w */
+  real feet_pos[2][3], feet_quat[2][4], feet_vel[2][3]; /* body_link_pos/quat_w, body_lin_vel_w (COM) */
+  real fz_hist[3][2], fn_hist[3][2];  /* net_forces_w_history[:, :, feet, 2] and its |F| */
+  real air_last[2];                 /* last_air_time[feet] */
+  real applied_torque[ND], joint_acc[ND];
+  int32_t ep_len;
+} m_post_t;
+
+/* TerminationManager.compute + RewardManager.compute (weight x step_dt, cfg order). md: commands,
+ * feet_down_pos / feet_step_len / feet_f_last (foot_step_length's env state), ep_sums (updated). */
+static real m_mdp_eval(const zb_task_cfg* cfg, const m_post_t* P, mdp_t* md, const real act[ND], const real prev[ND],
+                       real terms[ZB_M_NUM_REWARD_TERMS], int* low, int* close, int* tout) {
+  const real step_dt = (real)(cfg->sim_dt * (float)cfg->decimation);
+  /* terminations.py / Isaac Lab: time_out (ep_len >= max), root_height_below_minimum (0.2),
+   * feet_close (terminations.py:186-191: |foot_0 - foot_1| < 0.12) */
+  *tout = P->ep_len >= cfg->max_episode_length;
+  *low = P->base_pos[2] < (real)cfg->termination_height;
+  real fd[3];
+  for (int a = 0; a < 3; ++a) fd[a] = P->feet_pos[0][a] - P->feet_pos[1][a];
+  *close = sqrtr(v3_dot(fd, fd)) < (real)cfg->feet_close_min;
+  const int terminated = *low || *close;
+  real R[9];
+  q_to_mat(P->base_quat, R);
+  const real fwd[3] = {R[4], -R[1], 0}; /* GRAVITY_VEC_W x quat_apply(root_quat_w, y) (rewards.py:64-65) */
+  { /* track_lin_vel_xy_yaw_frame_exp (rewards.py:289-301): yaw_quat + quat_apply_inverse */
+    const real* q = P->base_quat;
+    const double yaw = atan2(2.0 * ((double)q[0] * q[3] + (double)q[1] * q[2]),
+                             1.0 - 2.0 * ((double)q[2] * q[2] + (double)q[3] * q[3]));
+    const real c = (real)cos(yaw), sn = (real)sin(yaw);
+    const real vx = c * P->base_lin_vel[0] + sn * P->base_lin_vel[1];
+    const real vy = -sn * P->base_lin_vel[0] + c * P->base_lin_vel[1];
+    const real ex = md->commands[0] - vx, ey = md->commands[1] - vy;
+    terms[ZB_M_R_TRACK_LIN_VEL_XY] = (real)exp(-(double)(ex * ex + ey * ey) / 0.25);
+    const real ez = md->commands[2] - P->base_ang_vel[2]; /* track_ang_vel_z_world_exp (303-312) */
+    terms[ZB_M_R_TRACK_ANG_VEL_Z] = (real)exp(-(double)(ez * ez) / 0.25);
+  }
+  terms[ZB_M_R_TERMINATION] = (real)terminated;        /* is_terminated */
+  real t2 = 0, a2 = 0, r2 = 0;
+  for (int j = 0; j < ND; ++j) {
+    t2 += P->applied_torque[j] * P->applied_torque[j]; /* joint_torques_l2 */
+    a2 += P->joint_acc[j] * P->joint_acc[j];           /* joint_acc_l2 */
+    r2 += (act[j] - prev[j]) * (act[j] - prev[j]);     /* action_rate_l2 */
+  }
+  terms[ZB_M_R_DOF_TORQUES] = t2;
+  terms[ZB_M_R_DOF_ACC] = a2;
+  terms[ZB_M_R_ACTION_RATE] = r2;
+  { /* foot_step_length (rewards.py:44-104): touchdown = mean F_z over the history > 10 after < 10 */
+    const real nrm = sqrtr(v3_dot(fwd, fwd)) + (real)1e-6;
+    const real fh[3] = {fwd[0] / nrm, fwd[1] / nrm, fwd[2] / nrm};
+    for (int f = 0; f < 2; ++f) {
+      const real fz = (P->fz_hist[0][f] + P->fz_hist[1][f] + P->fz_hist[2][f]) / 3;
+      if (fz > 10 && md->feet_f_last[f] < 10) {
+        real dv[3];
+        for (int a = 0; a < 3; ++a) dv[a] = P->feet_pos[f][a] - md->feet_down_pos[f][a];
+        md->feet_step_len[f] = (real)fabs((double)v3_dot(dv, fh));
+        for (int a = 0; a < 3; ++a) md->feet_down_pos[f][a] = P->feet_pos[f][a];
+      }
+      md->feet_f_last[f] = fz;
+    }
+    const real mn = md->feet_step_len[0] < md->feet_step_len[1] ? md->feet_step_len[0] : md->feet_step_len[1];
+    terms[ZB_M_R_FOOT_STEP_LENGTH] = (real)tanh(15.0 * (double)mn);
+  }
+  real sd = 0, sf = 0, sl = 0;
+  for (int f = 0; f < 2; ++f) {
+    real Rf[9];
+    q_to_mat(P->feet_quat[f], Rf);
+    const real sg = f == 0 ? 1 : -1; /* foot_downward (106-121): feet axes (0, +-1, 0) vs world z */
+    const real dz[3] = {sg * Rf[1], sg * Rf[4], sg * Rf[7] - 1};
+    sd += sqrtr(v3_dot(dz, dz));
+    const real dx[3] = {Rf[0] - fwd[0], Rf[3] - fwd[1], Rf[6] - fwd[2]}; /* foot_forward (123-142) */
+    sf += sqrtr(v3_dot(dx, dx));
+    real fm = P->fn_hist[0][f]; /* feet_slide (250-264): max |F| over the history > 1 */
+    if (P->fn_hist[1][f] > fm) fm = P->fn_hist[1][f];
+    if (P->fn_hist[2][f] > fm) fm = P->fn_hist[2][f];
+    const real v2 = P->feet_vel[f][0] * P->feet_vel[f][0] + P->feet_vel[f][1] * P->feet_vel[f][1];
+    sl += sqrtr(v2) * (fm > 1 ? 1 : 0);
+  }
+  terms[ZB_M_R_FOOT_DOWNWARD] = sd;
+  terms[ZB_M_R_FOOT_FORWARD] = sf;
+  terms[ZB_M_R_FEET_SLIDE] = sl;
+  terms[ZB_M_R_AIR_TIME_BALANCE] = (real)fabs((double)(P->air_last[0] - P->air_last[1])); /* 241-248 */
+  real rew = 0;
+  for (int t = 0; t < ZB_M_NUM_REWARD_TERMS; ++t) {
+    const real v = terms[t] * (real)cfg->stage_scales[0][t] * step_dt;
+    rew += v;
+    md->ep_sums[t] += v;
+  }
+  return rew;
+}
+
+/* reset events (reset_base = reset_root_state_uniform, reset_robot_joints = defaults,
+ * reset_my_data = feet data at the post-reset feet) and the managers' resets (actions,
+ * episode sums, command resample + metrics, contact sensor). init: the construction-time reset. */
+static void m_reset_env(const zbo_sim* s, uint64_t ctr, int i, env_t* e) {
+  const mdl_t* m = &s->m;
+  const uint64_t h = env_hash(s->seed, ctr, i);
+  mdp_t* md = &e->md;
+  (void)reset_pose(m, &s->c, h, &e->ph);
+  m_resample(s, h, M_DRAW_RESET_CMD, md->commands, &md->cmd_standing);
+  md->interval_left = s->c.cmd_resample_s;
+  md->metrics[0] = md->metrics[1] = 0;
+  for (int j = 0; j < ND; ++j) md->actions[j] = 0;
+  kin_t k;
+  fk(m, &e->ph, &k);
+  for (int f = 0; f < 2; ++f) {
+    real p[3], q[4];
+    link_pose(m, &k, m->foot_links[f], p, q);
+    for (int a = 0; a < 3; ++a) md->feet_down_pos[f][a] = p[a] + e->ph.root_pos[a];
+    md->feet_f_last[f] = 0;
+    md->feet_step_len[f] = 0;
+    md->feet_air_cur[f] = md->feet_air_last[f] = 0;
+    for (int h2 = 0; h2 < 3; ++h2) md->feet_fz_hist[h2][f] = md->feet_fn_hist[h2][f] = 0;
+  }
+  md->ep_len = 0;
+  for (int t = 0; t < ZB_MAX_REWARD_TERMS; ++t) md->ep_sums[t] = 0;
+}
+
+/* policy group (mgr.py:139-161): root_quat_w, generated_commands, joint_pos_rel, joint_vel_rel
+ * (Isaac Lab joint order), last_action; additive U(-n, n) on quat / joint pos / joint vel */
+static void m_write_obs(const zbo_sim* s, const env_t* e, uint64_t h, float* obs) {
+  const mdl_t* m = &s->m;
+  const zb_task_cfg* c = &s->c;
+  kin_t k;
+  fk(m, &e->ph, &k);
+  real p[3], q[4];
+  link_pose(m, &k, m->base_link, p, q);
+  const real cor = c->obs_corruption ? 1 : 0;
+#define NOISE(kk, nn) (cor * (draw(h, M_DRAW_NOISE + (kk)) * (2 * (real)(nn)) - (real)(nn)))
+  for (int a = 0; a < 4; ++a) obs[a] = (float)(q[a] + NOISE(a, c->obs_noise[0]));
+  for (int a = 0; a < 3; ++a) obs[4 + a] = (float)e->md.commands[a];
+  for (int j = 0; j < ND; ++j) {
+    const int ai = m->api_index[j];
+    obs[7 + ai] = (float)(m->api_sign[j] * (e->ph.jq[j] - m->jq0[j]) + NOISE(4 + ai, c->obs_noise[1]));
+    obs[13 + ai] = (float)(m->api_sign[j] * e->ph.jqd[j] + NOISE(10 + ai, c->obs_noise[2]));
+  }
+#undef NOISE
+  for (int a = 0; a < ND; ++a) obs[19 + a] = (float)e->md.actions[a];
+}
+
+/* UniformVelocityCommand._update_metrics with root_lin_vel_b / root_ang_vel_b (the base link's
+ * COM velocity and angular velocity in its frame), then the timer / resample / standing zeroing */
+static void m_command_compute(const zbo_sim* s, uint64_t h, env_t* e, const real vb[3], const real wb[3]) {
+  mdp_t* md = &e->md;
+  const zb_task_cfg* c = &s->c;
+  const real step_dt = (real)(c->sim_dt * (float)c->decimation);
+  const real max_steps = (real)c->cmd_resample_s / step_dt;
+  const real ex = md->commands[0] - vb[0], ey = md->commands[1] - vb[1];
+  md->metrics[0] += sqrtr(ex * ex + ey * ey) / max_steps;
+  md->metrics[1] += (real)fabs((double)(md->commands[2] - wb[2])) / max_steps;
+  md->interval_left -= step_dt;
+  if (md->interval_left <= 0) {
+    m_resample(s, h, M_DRAW_CMD, md->commands, &md->cmd_standing);
+    md->interval_left = c->cmd_resample_s;
+  }
+  if (md->cmd_standing > (real)0.5) md->commands[0] = md->commands[1] = md->commands[2] = 0;
+}
+
+static real m_step_env(const zbo_sim* s, uint64_t ctr, int i, env_t* e, const float* action, float* obs, int* low,
+                       int* close, int* tout, real acc[ZB_MAX_REWARD_TERMS], double met[2]) {
+  const mdl_t* m = &s->m;
+  const zb_task_cfg* cfg = &s->c;
+  mdp_t* md = &e->md;
+  /* RelativeJointPositionAction.process_actions: raw * scale (zero offset), clipped; Isaac Lab
+   * joint order -> chain joints */
+  real act[ND], prev[ND], delta[ND];
+  for (int a = 0; a < ND; ++a) { act[a] = (real)action[a]; prev[a] = md->actions[a]; }
+  for (int j = 0; j < ND; ++j)
+    delta[j] = m->api_sign[j] * clampr(act[m->api_index[j]] * (real)cfg->action_scale, -(real)cfg->action_clip,
+                                       (real)cfg->action_clip);
+  substep_out_t so;
+  real jqd_prev[ND];
+  for (int k = 0; k < cfg->decimation; ++k) {
+    real target[ND];
+    for (int j = 0; j < ND; ++j) target[j] = e->ph.jq[j] + delta[j]; /* apply_actions: q + delta */
+    if (k == cfg->decimation - 1)
+      for (int j = 0; j < ND; ++j) jqd_prev[j] = e->ph.jqd[j];
+    substep(m, cfg, &e->ph, target, md->mu, &so);
+    /* ContactSensor.update (every physics step): history shift, air time with elapsed sim_dt */
+    for (int f = 0; f < 2; ++f) {
+      const real* F = so.net_force[m->foot_links[f]];
+      const real fn = sqrtr(v3_dot(F, F));
+      md->feet_fz_hist[2][f] = md->feet_fz_hist[1][f];
+      md->feet_fz_hist[1][f] = md->feet_fz_hist[0][f];
+      md->feet_fz_hist[0][f] = F[2];
+      md->feet_fn_hist[2][f] = md->feet_fn_hist[1][f];
+      md->feet_fn_hist[1][f] = md->feet_fn_hist[0][f];
+      md->feet_fn_hist[0][f] = fn;
+      const int c = fn > (real)cfg->contact_force_threshold;
+      if (md->feet_air_cur[f] > 0 && c) md->feet_air_last[f] = md->feet_air_cur[f] + (real)cfg->sim_dt;
+      md->feet_air_cur[f] = c ? 0 : md->feet_air_cur[f] + (real)cfg->sim_dt;
+    }
+  }
+  md->ep_len += 1;
+  m_post_t P;
+  real vcom[3];
+  {
+    kin_t k;
+    fk(m, &e->ph, &k);
+    real V[NB][6];
+    body_vel(&k, &e->ph, V);
+    const int B = m->base_link, bb = m->link_body[B];
+    link_pose(m, &k, B, P.base_pos, P.base_quat);
+    real x[3];
+    m3_v(k.R[bb], m->link_pos[B], x);
+    for (int a = 0; a < 3; ++a) x[a] += k.p[bb][a];
+    point_vel(V[bb], x, P.base_lin_vel);
+    m3_v(k.R[bb], m->link_com[B], x);
+    for (int a = 0; a < 3; ++a) x[a] += k.p[bb][a];
+    point_vel(V[bb], x, vcom);
+    for (int a = 0; a < 3; ++a) { P.base_ang_vel[a] = V[bb][a]; P.base_pos[a] += e->ph.root_pos[a]; }
+    for (int f = 0; f < 2; ++f) {
+      const int l = m->foot_links[f], b = m->link_body[l];
+      link_pose(m, &k, l, P.feet_pos[f], P.feet_quat[f]);
+      for (int a = 0; a < 3; ++a) P.feet_pos[f][a] += e->ph.root_pos[a];
+      real c[3];
+      m3_v(k.R[b], m->link_com[l], c);
+      for (int a = 0; a < 3; ++a) c[a] += k.p[b][a];
+      point_vel(V[b], c, P.feet_vel[f]);
+    }
+  }
+  for (int j = 0; j < ND; ++j) {
+    P.applied_torque[j] = so.applied_torque[j];
+    P.joint_acc[j] = (e->ph.jqd[j] - jqd_prev[j]) / (real)cfg->sim_dt;
+  }
+  for (int h = 0; h < 3; ++h)
+    for (int f = 0; f < 2; ++f) { P.fz_hist[h][f] = md->feet_fz_hist[h][f]; P.fn_hist[h][f] = md->feet_fn_hist[h][f]; }
+  P.air_last[0] = md->feet_air_last[0];
+  P.air_last[1] = md->feet_air_last[1];
+  P.ep_len = md->ep_len;
+  for (int a = 0; a < ND; ++a) md->actions[a] = act[a];
+  real terms[ZB_M_NUM_REWARD_TERMS];
+  const real rew = m_mdp_eval(cfg, &P, md, act, prev, terms, low, close, tout);
+  const uint64_t h = env_hash(s->seed, ctr, i);
+  real vb[3] = {0, 0, 0}, wb[3] = {0, 0, 0};
+  if (*low || *close || *tout) {
+    for (int t = 0; t < ZB_M_NUM_REWARD_TERMS; ++t) acc[t] += md->ep_sums[t];
+    met[0] += md->metrics[0];
+    met[1] += md->metrics[1];
+    m_reset_env(s, ctr, i, e);
+  } else {
+    real Rb[9];
+    q_to_mat(P.base_quat, Rb);
+    for (int a = 0; a < 3; ++a) {
+      vb[a] = Rb[a] * vcom[0] + Rb[3 + a] * vcom[1] + Rb[6 + a] * vcom[2];
+      wb[a] = Rb[a] * P.base_ang_vel[0] + Rb[3 + a] * P.base_ang_vel[1] + Rb[6 + a] * P.base_ang_vel[2];
+    }
+  }
+  m_command_compute(s, h, e, vb, wb);
+  m_write_obs(s, e, h, obs);
+  return rew;
+}
+
+/* a reset env's command redrawn after lin_vel_cmd_levels widened the ranges in the same call
+ * (the reference's curriculum runs before the command manager's reset); velocity 0 after reset */
+static void m_fixup_env(const zbo_sim* s, uint64_t ctr, int i, env_t* e, float* obs) {
+  mdp_t* md = &e->md;
+  const uint64_t h = env_hash(s->seed, ctr, i);
+  m_resample(s, h, M_DRAW_RESET_CMD, md->commands, &md->cmd_standing);
+  md->metrics[0] = md->metrics[1] = 0;
+  md->interval_left = s->c.cmd_resample_s;
+  const real zero[3] = {0, 0, 0};
+  m_command_compute(s, h, e, zero, zero);
+  for (int a = 0; a < 3; ++a) obs[4 + a] = (float)md->commands[a];
+}
+
+static void m_pack_env(const env_t* e, float* st, int n, int i) {
+#define PUT(off, val) st[(size_t)(off) * n + i] = (float)(val)
+  for (int a = 0; a < 3; ++a) { PUT(ZB_S_ROOT_POS + a, e->ph.root_pos[a]); PUT(ZB_S_ROOT_LINVEL + a, e->ph.root_linvel[a]); PUT(ZB_S_ROOT_ANGVEL + a, e->ph.root_angvel[a]); }
+  for (int a = 0; a < 4; ++a) PUT(ZB_S_ROOT_QUAT + a, e->ph.root_quat[a]);
+  for (int j = 0; j < ND; ++j) { PUT(ZB_S_JOINT_POS + j, e->ph.jq[j]); PUT(ZB_S_JOINT_VEL + j, e->ph.jqd[j]); PUT(ZB_M_ACTIONS + j, e->md.actions[j]); }
+  for (int a = 0; a < 3; ++a) PUT(ZB_M_COMMANDS + a, e->md.commands[a]);
+  PUT(ZB_M_CMD_TIME_LEFT, e->md.interval_left);
+  PUT(ZB_M_CMD_STANDING, e->md.cmd_standing);
+  PUT(ZB_M_METRICS, e->md.metrics[0]);
+  PUT(ZB_M_METRICS + 1, e->md.metrics[1]);
+  for (int f = 0; f < 2; ++f) {
+    for (int a = 0; a < 3; ++a) PUT(ZB_M_FEET_DOWN_POS + 3 * f + a, e->md.feet_down_pos[f][a]);
+    PUT(ZB_M_FEET_STEP_LEN + f, e->md.feet_step_len[f]);
+    PUT(ZB_M_FEET_F_LAST + f, e->md.feet_f_last[f]);
+    PUT(ZB_M_FEET_AIR_CUR + f, e->md.feet_air_cur[f]);
+    PUT(ZB_M_FEET_AIR_LAST + f, e->md.feet_air_last[f]);
+    for (int h = 0; h < 3; ++h) { PUT(ZB_M_FEET_FZ_HIST + 2 * h + f, e->md.feet_fz_hist[h][f]); PUT(ZB_M_FEET_FN_HIST + 2 * h + f, e->md.feet_fn_hist[h][f]); }
+  }
+  PUT(ZB_M_EP_LEN, e->md.ep_len);
+  for (int t = 0; t < ZB_M_NUM_REWARD_TERMS; ++t) PUT(ZB_M_EP_SUMS + t, e->md.ep_sums[t]);
+  for (int l = 0; l < NL; ++l) PUT(ZB_M_LINK_MU + l, e->md.mu[l]);
+#undef PUT
+}
+
+static void m_unpack_env(env_t* e, const float* st, int n, int i) {
+#define GET(off) ((real)st[(size_t)(off) * n + i])
+  for (int a = 0; a < 3; ++a) { e->ph.root_pos[a] = GET(ZB_S_ROOT_POS + a); e->ph.root_linvel[a] = GET(ZB_S_ROOT_LINVEL + a); e->ph.root_angvel[a] = GET(ZB_S_ROOT_ANGVEL + a); }
+  for (int a = 0; a < 4; ++a) e->ph.root_quat[a] = GET(ZB_S_ROOT_QUAT + a);
+  for (int j = 0; j < ND; ++j) { e->ph.jq[j] = GET(ZB_S_JOINT_POS + j); e->ph.jqd[j] = GET(ZB_S_JOINT_VEL + j); e->md.actions[j] = GET(ZB_M_ACTIONS + j); }
+  for (int a = 0; a < 3; ++a) e->md.commands[a] = GET(ZB_M_COMMANDS + a);
+  e->md.interval_left = GET(ZB_M_CMD_TIME_LEFT);
+  e->md.cmd_standing = GET(ZB_M_CMD_STANDING);
+  e->md.metrics[0] = GET(ZB_M_METRICS);
+  e->md.metrics[1] = GET(ZB_M_METRICS + 1);
+  for (int f = 0; f < 2; ++f) {
+    for (int a = 0; a < 3; ++a) e->md.feet_down_pos[f][a] = GET(ZB_M_FEET_DOWN_POS + 3 * f + a);
+    e->md.feet_step_len[f] = GET(ZB_M_FEET_STEP_LEN + f);
+    e->md.feet_f_last[f] = GET(ZB_M_FEET_F_LAST + f);
+    e->md.feet_air_cur[f] = GET(ZB_M_FEET_AIR_CUR + f);
+    e->md.feet_air_last[f] = GET(ZB_M_FEET_AIR_LAST + f);
+    for (int h = 0; h < 3; ++h) { e->md.feet_fz_hist[h][f] = GET(ZB_M_FEET_FZ_HIST + 2 * h + f); e->md.feet_fn_hist[h][f] = GET(ZB_M_FEET_FN_HIST + 2 * h + f); }
+  }
+  e->md.ep_len = (int32_t)lrint((double)st[(size_t)ZB_M_EP_LEN * n + i]);
+  for (int t = 0; t < ZB_M_NUM_REWARD_TERMS; ++t) e->md.ep_sums[t] = GET(ZB_M_EP_SUMS + t);
+  for (int l = 0; l < NL; ++l) e->md.mu[l] = GET(ZB_M_LINK_MU + l);
+#undef GET
+}
+
 /* ========================================================================= call epilogue
  * Mirror of the kernel's zb_finalize_kernel: episode log (means over reset envs; walking divides
  * by the 20 s episode, the other tasks already divided per env), curriculum log entries (pre-event
@@ -1535,9 +1896,28 @@ static void finish_call(zbo_sim* s, int nres, const double* acc, double ep_s, in
     v[17] = s->vel[0];
     v[18] = s->vel[1];
     v[19] = s->yaw[0];
+    if (c->task == ZB_TASK_MANAGER_V0) {
+      /* lin_vel_cmd_levels (curriculums.py:57-83), first in _reset_idx: on calls where
+       * common_step_counter % max_episode_length == 0, widen the x / y ranges by +-0.1 (clamped to
+       * limit_ranges) when mean(episode sums of track_lin_vel_xy_exp) / 20 s > 0.8 x weight */
+      if (c->range_period_steps > 0 && s->steps % (uint64_t)c->range_period_steps == 0 &&
+          v[ZB_M_R_TRACK_LIN_VEL_XY] > c->stage_scales[0][ZB_M_R_TRACK_LIN_VEL_XY] * c->range_threshold) {
+        s->vel[0] = (float)clampr(s->vel[0] - c->range_delta, c->range_limit_vel[0], c->range_limit_vel[1]);
+        s->vel[1] = (float)clampr(s->vel[1] + c->range_delta, c->range_limit_vel[0], c->range_limit_vel[1]);
+        s->yaw[0] = (float)clampr(s->yaw[0] - c->range_delta, c->range_limit_yaw[0], c->range_limit_yaw[1]);
+        s->yaw[1] = (float)clampr(s->yaw[1] + c->range_delta, c->range_limit_yaw[0], c->range_limit_yaw[1]);
+        s->changed = 1;
+      }
+      v[16] = s->vel[1];                       /* Curriculum/lin_vel_cmd_levels */
+      v[17] = (float)(s->met_acc[0] / nres);   /* Metrics/base_velocity/error_vel_xy */
+      v[18] = (float)(s->met_acc[1] / nres);   /* Metrics/base_velocity/error_vel_yaw */
+      v[19] = 0;
+    }
     for (int t = 0; t < ZB_LOG_LEN; ++t) s->log_means[t] = v[t];
     s->log_counts[0] = reset_counts ? 0 : nterm;
     s->log_counts[1] = reset_counts ? 0 : ntout;
+    s->log_counts[2] = reset_counts ? 0 : s->nclose;
+    s->log_counts[3] = 0;
     if (c->task == ZB_TASK_WALKING_V4) {
       s->ring_vel[s->ring_head] = v[ZB_V4_R_TRACK_LIN_VEL_X];
       s->ring_yaw[s->ring_head] = v[ZB_V4_R_TRACK_HEADING_YAW];
@@ -1547,7 +1927,7 @@ static void finish_call(zbo_sim* s, int nres, const double* acc, double ep_s, in
     curriculum_events(s, 1, 1);
   }
   s->call_counter++;
-  if (full)
+  if (full && c->task != ZB_TASK_MANAGER_V0) /* ManagerBasedRLEnv has no full-reset draw */
     for (int e = 0; e < s->n; ++e) /* episode_length_buf ~ U{0..max_episode_length-1} (v2.py:418-422) */
       s->env[e].md.ep_len = (int32_t)(env_hash(s->seed, ctr, e) % (uint64_t)c->max_episode_length);
 }
@@ -1602,6 +1982,9 @@ zbo_sim* zbo_create(const zb_model* model, const zb_task_cfg* cfg, int num_envs,
       su_reset_env(&s->m, cfg, seed, 0, i, &s->env[i]); /* construction draws at RNG position 0 */
     } else if (cfg->task == ZB_TASK_WALKING_V4) {
       v4_reset_env(s, 0, i, &s->env[i], 1);
+    } else if (cfg->task == ZB_TASK_MANAGER_V0) {
+      for (int l = 0; l < NL; ++l) s->env[i].md.mu[l] = cfg->friction;
+      m_reset_env(s, 0, i, &s->env[i]);
     } else {
       reset_env(&s->m, &s->env[i]);
     }
@@ -1633,10 +2016,18 @@ int zbo_reset(zbo_sim* s, const int32_t* env_ids, int n) {
   const real step_dt = (real)(s->c.sim_dt * (float)s->c.decimation);
   double acc[ZB_MAX_REWARD_TERMS];
   for (int t = 0; t < ZB_MAX_REWARD_TERMS; ++t) acc[t] = 0;
+  s->met_acc[0] = s->met_acc[1] = 0;
+  s->nclose = 0;
+  s->changed = 0;
   for (int i = 0; i < cnt; ++i) {
     const int e = env_ids ? env_ids[i] : i;
     env_t* en = &s->env[e];
-    if (s->c.task == ZB_TASK_WALKING_V2) {
+    if (s->c.task == ZB_TASK_MANAGER_V0) {
+      for (int t = 0; t < ZB_M_NUM_REWARD_TERMS; ++t) acc[t] += en->md.ep_sums[t];
+      s->met_acc[0] += en->md.metrics[0];
+      s->met_acc[1] += en->md.metrics[1];
+      m_reset_env(s, ctr, e, en);
+    } else if (s->c.task == ZB_TASK_WALKING_V2) {
       for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) acc[t] += en->md.ep_sums[t];
       reset_env(&s->m, en);
     } else {
@@ -1647,7 +2038,8 @@ int zbo_reset(zbo_sim* s, const int32_t* env_ids, int n) {
       else v4_reset_env(s, ctr, e, en, 0);
     }
   }
-  const double ep_s = s->c.task == ZB_TASK_WALKING_V2 ? s->c.sim_dt * s->c.decimation * s->c.max_episode_length : 1.0;
+  const int per_episode = s->c.task == ZB_TASK_WALKING_V2 || s->c.task == ZB_TASK_MANAGER_V0;
+  const double ep_s = per_episode ? (double)(s->c.sim_dt * (float)s->c.decimation * (float)s->c.max_episode_length) : 1.0;
   finish_call(s, cnt, acc, ep_s, 0, 0, 1, all);
   return 0;
 }
@@ -1656,6 +2048,8 @@ int zbo_observe(zbo_sim* s, float* obs) {
   for (int e = 0; e < s->n; ++e) {
     if (s->c.task == ZB_TASK_STANDUP_V0) su_write_obs(&s->m, &s->env[e], obs + (size_t)e * ZB_SU_OBS_DIM);
     else if (s->c.task == ZB_TASK_WALKING_V4) v4_write_obs(&s->m, &s->env[e], obs + (size_t)e * ZB_V4_OBS_DIM);
+    else if (s->c.task == ZB_TASK_MANAGER_V0)
+      m_write_obs(s, &s->env[e], env_hash(s->seed, s->call_counter, e), obs + (size_t)e * ZB_M_OBS_DIM);
     else write_obs(&s->m, &s->env[e], obs + (size_t)e * ZB_OBS_DIM);
   }
   return 0;
@@ -1726,42 +2120,58 @@ int zbo_step(zbo_sim* s, const float* actions, float* obs, float* reward, uint8_
   const uint64_t ctr = s->call_counter;
   const int stage = s->stage;
   const int task = s->c.task;
-  const int od = task == ZB_TASK_STANDUP_V0 ? ZB_SU_OBS_DIM : task == ZB_TASK_WALKING_V4 ? ZB_V4_OBS_DIM : ZB_OBS_DIM;
-  s->steps++; /* DirectRLEnv.step: common_step_counter += 1 before dones / rewards / resets */
+  const int od = task == ZB_TASK_STANDUP_V0 ? ZB_SU_OBS_DIM : task == ZB_TASK_WALKING_V4 ? ZB_V4_OBS_DIM
+               : task == ZB_TASK_MANAGER_V0 ? ZB_M_OBS_DIM : ZB_OBS_DIM;
+  s->steps++; /* DirectRLEnv / ManagerBasedRLEnv.step: common_step_counter += 1 before dones / rewards / resets */
+  s->met_acc[0] = s->met_acc[1] = 0;
+  s->nclose = 0;
+  s->changed = 0;
+  int nclose = 0;
+  double met0 = 0, met1 = 0;
 #pragma omp parallel
   {
     real acc_l[ZB_MAX_REWARD_TERMS];
-    int nr = 0, nt = 0, no = 0;
+    double met_l[2] = {0, 0};
+    int nr = 0, nt = 0, no = 0, nc = 0;
     for (int t = 0; t < ZB_MAX_REWARD_TERMS; ++t) acc_l[t] = 0;
 #pragma omp for schedule(static)
     for (int e = 0; e < s->n; ++e) {
-      int died = 0, tout = 0;
+      int died = 0, tout = 0, close = 0;
       const float* a = actions + (size_t)e * ZB_ACT_DIM;
       float* o = obs + (size_t)e * od;
       real r;
       if (task == ZB_TASK_STANDUP_V0) r = su_step_env(&s->m, &s->c, stage, s->seed, ctr, e, &s->env[e], a, o, &died, &tout, acc_l);
       else if (task == ZB_TASK_WALKING_V4) r = v4_step_env(s, stage, ctr, e, &s->env[e], a, o, &died, &tout, acc_l);
+      else if (task == ZB_TASK_MANAGER_V0) r = m_step_env(s, ctr, e, &s->env[e], a, o, &died, &close, &tout, acc_l, met_l);
       else r = step_env(&s->m, &s->c, &s->env[e], a, o, &died, &tout, acc_l);
       reward[e] = (float)r;
-      terminated[e] = (uint8_t)died;
+      /* manager: terminated = base_height | feet_close; the log counts each term */
+      terminated[e] = (uint8_t)(died || close);
       truncated[e] = (uint8_t)tout;
-      nr += died || tout; nt += died; no += tout;
+      nr += died || close || tout; nt += died; no += tout; nc += close;
     }
 #pragma omp critical
     {
       for (int t = 0; t < ZB_MAX_REWARD_TERMS; ++t) acc[t] += acc_l[t];
-      nreset += nr; nterm += nt; ntout += no;
+      nreset += nr; nterm += nt; ntout += no; nclose += nc;
+      met0 += met_l[0]; met1 += met_l[1];
     }
   }
-  const double ep_s = task == ZB_TASK_WALKING_V2 ? s->c.sim_dt * s->c.decimation * s->c.max_episode_length : 1.0;
+  s->met_acc[0] = met0;
+  s->met_acc[1] = met1;
+  s->nclose = nclose;
+  const int per_episode = task == ZB_TASK_WALKING_V2 || task == ZB_TASK_MANAGER_V0;
+  const double ep_s = per_episode ? (double)(s->c.sim_dt * (float)s->c.decimation * (float)s->c.max_episode_length) : 1.0;
   finish_call(s, nreset, acc, ep_s, nterm, ntout, 0, nreset == s->n);
+  if (task == ZB_TASK_MANAGER_V0 && s->changed)
+    for (int e = 0; e < s->n; ++e)
+      if (terminated[e] || truncated[e]) m_fixup_env(s, ctr, e, &s->env[e], obs + (size_t)e * od);
   return 0;
 }
 
 int zbo_read_log(zbo_sim* s, float* term_means, int32_t* counts) {
   for (int t = 0; t < ZB_LOG_LEN; ++t) term_means[t] = s->log_means[t];
-  counts[0] = s->log_counts[0];
-  counts[1] = s->log_counts[1];
+  for (int k = 0; k < ZB_LOG_COUNTS; ++k) counts[k] = s->log_counts[k];
   return 0;
 }
 
@@ -1825,6 +2235,7 @@ int zbo_get_state(zbo_sim* s, float* dst) {
   for (int e = 0; e < s->n; ++e)
     if (s->c.task == ZB_TASK_STANDUP_V0) su_pack_env(&s->env[e], dst, s->n, e);
     else if (s->c.task == ZB_TASK_WALKING_V4) v4_pack_env(&s->env[e], dst, s->n, e);
+    else if (s->c.task == ZB_TASK_MANAGER_V0) m_pack_env(&s->env[e], dst, s->n, e);
     else pack_env(&s->env[e], dst, s->n, e);
   return 0;
 }
@@ -1832,16 +2243,18 @@ int zbo_set_state(zbo_sim* s, const float* src) {
   for (int e = 0; e < s->n; ++e)
     if (s->c.task == ZB_TASK_STANDUP_V0) su_unpack_env(&s->env[e], src, s->n, e);
     else if (s->c.task == ZB_TASK_WALKING_V4) v4_unpack_env(&s->env[e], src, s->n, e);
+    else if (s->c.task == ZB_TASK_MANAGER_V0) m_unpack_env(&s->env[e], src, s->n, e);
     else unpack_env(&s->env[e], src, s->n, e);
   return 0;
 }
 int zbo_state_dim(zbo_sim* s) {
-  return s->c.task == ZB_TASK_STANDUP_V0 ? ZB_SU_STATE_DIM : s->c.task == ZB_TASK_WALKING_V4 ? ZB_V4_STATE_DIM : ZB_STATE_DIM;
+  return s->c.task == ZB_TASK_STANDUP_V0 ? ZB_SU_STATE_DIM : s->c.task == ZB_TASK_WALKING_V4 ? ZB_V4_STATE_DIM
+         : s->c.task == ZB_TASK_MANAGER_V0 ? ZB_M_STATE_DIM : ZB_STATE_DIM;
 }
 
-/* standup: per-link friction [n][12] */
+/* standup / manager: per-link friction [n][12] */
 int zbo_set_link_friction(zbo_sim* s, const float* mu) {
-  if (s->c.task != ZB_TASK_STANDUP_V0) return -1;
+  if (s->c.task != ZB_TASK_STANDUP_V0 && s->c.task != ZB_TASK_MANAGER_V0) return -1;
   for (int e = 0; e < s->n; ++e)
     for (int l = 0; l < NL; ++l) s->env[e].md.mu[l] = mu[(size_t)e * NL + l];
   return 0;
@@ -1860,7 +2273,7 @@ int zbo_physics_substeps(zbo_sim* s, const float* targets, int nsub, float* net_
     for (int j = 0; j < ND; ++j) tg[j] = targets[(size_t)e * ND + j];
     substep_out_t so;
     memset(&so, 0, sizeof(so));
-    const real* mu = s->c.task == ZB_TASK_STANDUP_V0 ? s->env[e].md.mu : NULL;
+    const real* mu = s->c.task == ZB_TASK_STANDUP_V0 || s->c.task == ZB_TASK_MANAGER_V0 ? s->env[e].md.mu : NULL;
     for (int k = 0; k < nsub; ++k) substep(&s->m, &s->c, &s->env[e].ph, tg, mu, &so);
     if (net_force)
       for (int l = 0; l < NL; ++l)

@@ -148,7 +148,7 @@ struct Counters {
   uint64_t calls;  // zb_step + zb_reset calls (RNG stream position of resets)
   uint64_t steps;  // zb_step calls (common_step_counter)
   int32_t stage;   // curriculum stage (my_curriculum)
-  int32_t pad;
+  int32_t changed;  // the last finalize widened the command ranges (manager fixup)
   // v4 command sampling state (resample_commands params, changed by the curricula)
   float vel[2], yaw[2], prob_pos;
   int32_t ring_n, ring_head;  // range_curriculum reward buffers (deque(maxlen=24))
@@ -1605,8 +1605,10 @@ __device__ __forceinline__ void write_obs(MP m, const Phys& p, const Mdp& d,
 }
 
 // accumulator layout: [0..15] episode-sum totals of reset envs, then n_reset, n_died, n_timeout
+// (the manager env also counts a second termination term and averages its two command metrics)
 constexpr int ACC_NRES = ZB_MAX_REWARD_TERMS, ACC_DIED = ACC_NRES + 1, ACC_TOUT = ACC_NRES + 2;
-constexpr int ACC = ACC_NRES + 4;
+constexpr int ACC_TERM2 = ACC_NRES + 3, ACC_MET0 = ACC_NRES + 4, ACC_MET1 = ACC_NRES + 5;
+constexpr int ACC = ACC_NRES + 8;
 
 // ------------------------------------------------------------------------- kernels
 __device__ __forceinline__ void load_phys(const float* __restrict__ st, int N, int i, Phys& p) {
@@ -1955,86 +1957,6 @@ __global__ void zb_derive_kernel(const zb_model* __restrict__ mg, float4* __rest
   links[DFLT_OFF + 5] = make_float4(f1[0], f1[1], f1[2], 0.f);
 }
 
-// Episode log finalisation, curricula and the full-reset episode_length_buf draw (v2.py:418-422);
-// leaves the accumulator zeroed for the next launch. Single workgroup (grid-strided over envs).
-// The counters (RNG stream position, common_step_counter, curriculum state) live on the device so
-// that a captured graph of zb_step advances them on every replay. Reset-mode events in the
-// reference's order (v4 EventCfg 268-439): the episode log and the range-curriculum buffers
-// (_reset_idx before the events), my_curriculum (one stage per call with resets once
-// common_step_counter >= stage_steps[next]), range_curriculum (v4: widen the command ranges when
-// the buffered tracking rewards exceed 85 % of their weight). New weights / ranges apply from the
-// next step (the reference applies the reset-event ones to the commands it resamples in the same
-// call).
-__global__ void zb_finalize_kernel(int N, float* __restrict__ st, float* __restrict__ acc,
-                                   float* __restrict__ log_means, int32_t* __restrict__ log_counts,
-                                   float* __restrict__ user_means, int32_t* __restrict__ user_counts, float episode_s,
-                                   uint64_t seed, Counters* __restrict__ cnt, int force_full, int reset_counts,
-                                   int is_step, int ep_len_row, zb_task_cfg cfg) {
-  const uint64_t ctr = cnt->calls;
-  const uint64_t steps = cnt->steps + (is_step ? 1 : 0);
-  const float nres = acc[ACC_NRES];
-  const bool full = force_full || nres == (float)N;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    cnt->steps = steps;
-    if (nres > 0.f) {
-      float v[ZB_LOG_LEN];
-#pragma unroll
-      for (int t = 0; t < ZB_MAX_REWARD_TERMS; ++t) v[t] = acc[t] / nres / episode_s;
-      v[16] = (float)cnt->stage;  // logged before the events run (v4.py:952-957)
-      v[17] = cnt->vel[0];
-      v[18] = cnt->vel[1];
-      v[19] = cnt->yaw[0];
-#pragma unroll
-      for (int t = 0; t < ZB_LOG_LEN; ++t) {
-        log_means[t] = v[t];
-        if (user_means) user_means[t] = v[t];
-      }
-      const int32_t c0 = reset_counts ? 0 : (int32_t)acc[ACC_DIED], c1 = reset_counts ? 0 : (int32_t)acc[ACC_TOUT];
-      log_counts[0] = c0;
-      log_counts[1] = c1;
-      if (user_counts) { user_counts[0] = c0; user_counts[1] = c1; }
-      if (cfg.task == ZB_TASK_WALKING_V4) {  // curriculum_*_reward_buffer.append (v4.py:941-944)
-        cnt->ring_vel[cnt->ring_head] = v[ZB_V4_R_TRACK_LIN_VEL_X];
-        cnt->ring_yaw[cnt->ring_head] = v[ZB_V4_R_TRACK_HEADING_YAW];
-        cnt->ring_head = (cnt->ring_head + 1) % ZB_V4_RING;
-        cnt->ring_n = min(cnt->ring_n + 1, ZB_V4_RING);
-      }
-      // my_curriculum
-      const int s0 = cnt->stage;
-      if (s0 + 1 < cfg.num_stages && s0 + 1 < ZB_MAX_STAGES && steps >= (uint64_t)cfg.stage_steps[s0 + 1]) {
-        cnt->stage = s0 + 1;
-        cnt->prob_pos = cfg.stage_prob_pos[s0 + 1];
-      }
-      // range_curriculum (v4.py:201-265)
-      if (cfg.task == ZB_TASK_WALKING_V4 && cnt->ring_n >= cfg.range_min_buffer && cfg.range_period_steps > 0 &&
-          steps >= (uint64_t)cfg.range_start_steps && steps % (uint64_t)cfg.range_period_steps == 0) {
-        float mv = 0.f, my = 0.f;
-        for (int k = 0; k < cnt->ring_n; ++k) { mv += cnt->ring_vel[k]; my += cnt->ring_yaw[k]; }
-        mv /= (float)cnt->ring_n;
-        my /= (float)cnt->ring_n;
-        const int sg = cnt->stage;
-        if (mv > cfg.stage_scales[sg][ZB_V4_R_TRACK_LIN_VEL_X] * cfg.range_threshold) {
-          cnt->vel[0] = clampf(cnt->vel[0] - cfg.range_delta, cfg.range_limit_vel[0], cfg.range_limit_vel[1]);
-          cnt->vel[1] = clampf(cnt->vel[1] + cfg.range_delta, cfg.range_limit_vel[0], cfg.range_limit_vel[1]);
-        }
-        if (my > cfg.stage_scales[sg][ZB_V4_R_TRACK_HEADING_YAW] * cfg.range_threshold) {
-          cnt->yaw[0] = clampf(cnt->yaw[0] - cfg.range_delta, cfg.range_limit_yaw[0], cfg.range_limit_yaw[1]);
-          cnt->yaw[1] = clampf(cnt->yaw[1] + cfg.range_delta, cfg.range_limit_yaw[0], cfg.range_limit_yaw[1]);
-        }
-      }
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x < ACC) acc[threadIdx.x] = 0.f;
-  if (threadIdx.x == 0) cnt->calls = ctr + 1;
-  if (full)
-    for (int i = threadIdx.x; i < N; i += blockDim.x) {
-      const uint64_t h = hash64(seed ^ hash64(ctr * 0x100000001B3ull + (uint64_t)i));
-      st[(size_t)ep_len_row * N + i] = (float)(int)(h % (uint64_t)cfg.max_episode_length);
-    }
-}
-
 __global__ void zb_observe_kernel(const zb_model* __restrict__ mg, int N, const float* __restrict__ st,
                                   float* __restrict__ obs) {
   MP m = to_mp(mg);
@@ -2059,7 +1981,8 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_substeps_kernel(con
   const int i = env < N ? env : N - 1;
   const Q q{lds, lane, lane / TL, lane % TL};
   for (int t = lane; t < LNK4; t += WGT) lds[LNK_OFF + t] = links[t];
-  if (kLinkFriction && q.s < NL) q.fric(q.s) = st[(size_t)(ZB_SU_LINK_MU + q.s) * N + i];
+  const int mu_row = cfg.task == ZB_TASK_MANAGER_V0 ? ZB_M_LINK_MU : ZB_SU_LINK_MU;
+  if (kLinkFriction && q.s < NL) q.fric(q.s) = st[(size_t)(mu_row + q.s) * N + i];
   Phys p;
   load_phys(st, N, i, p);
   float tg[ND], tau[ND], F[1][3];
@@ -2121,17 +2044,31 @@ __device__ __forceinline__ float reset_pose(MP m, const zb_task_cfg& cfg, uint64
   sincos_r(0.5f * r[2], &sr, &cr);
   sincos_r(0.5f * r[3], &sy, &cy);
   const float dq[4] = {cy * cr, cy * sr, sy * sr, sy * cr};  // quat_from_euler_xyz(roll, 0, yaw)
+  // the sampled pose is the Isaac Lab root's (the chain root unless the asset is rooted elsewhere):
+  // its default pose is chain-root default * T (T = api_root_in_root, identity for the others)
   const float q0[4] = {m->default_root_quat[0], m->default_root_quat[1], m->default_root_quat[2],
                        m->default_root_quat[3]};
-  float qn[4];
-  if (cfg.reset_pose_body_frame) qmul(q0, dq, qn);
-  else qmul(dq, q0, qn);
-  qnormalize(qn);
+  const float tT[3] = {m->api_root_in_root[0], m->api_root_in_root[1], m->api_root_in_root[2]};
+  const float qT[4] = {m->api_root_in_root[3], m->api_root_in_root[4], m->api_root_in_root[5], m->api_root_in_root[6]};
+  float qa0[4], ta[3];
+  qmul(q0, qT, qa0);
+  qrot(q0, tT, ta);
+  float qa[4];
+  if (cfg.reset_pose_body_frame) qmul(qa0, dq, qa);
+  else qmul(dq, qa0, qa);
+  qnormalize(qa);
+  const float pa[3] = {m->default_root_pos[0] + ta[0] + r[0], m->default_root_pos[1] + ta[1] + r[1],
+                       m->default_root_pos[2] + ta[2]};
+  // back to the chain root: q = qa * conj(qT), p = pa - R(q) tT
+  const float qTc[4] = {qT[0], -qT[1], -qT[2], -qT[3]};
+  float qn[4], tq[3];
+  qmul(qa, qTc, qn);
+  qrot(qn, tT, tq);
 #pragma unroll
   for (int a = 0; a < 4; ++a) p.quat[a] = qn[a];
-  p.pos[0] = m->default_root_pos[0] + r[0];
-  p.pos[1] = m->default_root_pos[1] + r[1];
-  p.pos[2] = m->default_root_pos[2];
+  p.pos[0] = pa[0] - tq[0];
+  p.pos[1] = pa[1] - tq[1];
+  p.pos[2] = pa[2] - tq[2];
 #pragma unroll
   for (int a = 0; a < 3; ++a) { p.lv[a] = 0.f; p.av[a] = 0.f; }
 #pragma unroll
@@ -2373,11 +2310,11 @@ __global__ void zb_su_observe_kernel(const zb_model* __restrict__ mg, int N, con
 }
 
 // per-link friction [N][NL] -> state rows ZB_SU_LINK_MU (mu == nullptr: fill with `fill`)
-__global__ void zb_su_friction_kernel(int N, float* __restrict__ st, const float* __restrict__ mu, float fill) {
+__global__ void zb_su_friction_kernel(int N, float* __restrict__ st, const float* __restrict__ mu, float fill, int row) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= N * NL) return;
   const int i = t / NL, l = t % NL;
-  st[(size_t)(ZB_SU_LINK_MU + l) * N + i] = mu ? mu[t] : fill;
+  st[(size_t)(row + l) * N + i] = mu ? mu[t] : fill;
 }
 
 // =========================================================================== walking v4
@@ -2823,6 +2760,586 @@ __global__ void zb_v4_observe_kernel(const zb_model* __restrict__ mg, int N, con
   sincos_r(st[(size_t)ZB_V4_TARGET_YAW * N + i] - st[(size_t)ZB_V4_CURRENT_YAW * N + i], &sn, &cs);
   o[23] = atan2f(sn, cs);
 }
+
+// =========================================================================== manager-based env
+// zbot-6b-walking-m-v0 (reference tasks/zbotlab_manager: zbotlab_env_cfg.py = "mgr.py",
+// config/zbot6b_manager/flat_env_cfg.py, mdp/rewards.py, terminations.py, curriculums.py) on
+// ZBOT_6S_V2_CFG (zbot_6s_v09.usd, rooted at the base link). ManagerBasedRLEnv.step order: action
+// (RelativeJointPositionAction re-targets q + delta every substep), 4 x (substep, scene.update:
+// the contact sensor with history_length 3 > 0 updates every physics step), terminations,
+// rewards, resets (curriculum, events, managers), command update, observations with noise.
+
+// world angular velocity of body b (root twist + the joint rates before it)
+__device__ __forceinline__ void body_ang_vel_q(const Phys& s, const float S[ND][6], int b, float w[3]) {
+  w[0] = s.av[0]; w[1] = s.av[1]; w[2] = s.av[2];
+#pragma unroll
+  for (int j = 0; j < ND; ++j)
+    if (j < b)
+#pragma unroll
+      for (int a = 0; a < 3; ++a) w[a] += S[j][a] * s.jqd[j];
+}
+
+// UniformVelocityCommand._resample_command: lin x ~ U(ranges.lin_vel_x) (cnt->vel), lin y ~
+// U(ranges.lin_vel_y) (cnt->yaw holds the lin_vel_y range for this task), ang z ~ U(0, 0),
+// standing ~ U(0, 1) <= rel_standing_envs; draws k0 .. k0 + 2
+__device__ __forceinline__ void m_resample(const zb_task_cfg& cfg, const Counters* cnt, uint64_t h, int k0, float cmd[3],
+                                           float& standing) {
+  cmd[0] = draw(h, k0) * (cnt->vel[1] - cnt->vel[0]) + cnt->vel[0];
+  cmd[1] = draw(h, k0 + 1) * (cnt->yaw[1] - cnt->yaw[0]) + cnt->yaw[0];
+  cmd[2] = 0.f;
+  standing = draw(h, k0 + 2) <= cfg.cmd_rel_standing ? 1.f : 0.f;
+}
+constexpr int M_DRAW_RESET_CMD = 5, M_DRAW_CMD = 9, M_DRAW_NOISE = 16;  // reset_pose uses draws 1..4
+
+// the policy observation group (mgr.py:136-161, corruption on): root quat, command, joint pos rel,
+// joint vel rel (Isaac Lab joint order), last action; additive U(-n, n) noise from draws 16..37
+__device__ __forceinline__ void m_write_obs(MP m, const zb_task_cfg& cfg, uint64_t h, const float bq[4],
+                                            const float cmd[3], const Phys& p, const float a_obs[ND], float* o) {
+  const float cor = cfg.obs_corruption ? 1.f : 0.f;
+  auto noise = [&](int k, float n) { return cor * (draw(h, M_DRAW_NOISE + k) * (2.f * n) - n); };
+#pragma unroll
+  for (int a = 0; a < 4; ++a) o[a] = bq[a] + noise(a, cfg.obs_noise[0]);
+#pragma unroll
+  for (int a = 0; a < 3; ++a) o[4 + a] = cmd[a];
+#pragma unroll
+  for (int j = 0; j < ND; ++j) {
+    const int ai = m->api_joint_index[j];
+    const float sg = m->api_joint_sign[j];
+    o[7 + ai] = sg * (p.jq[j] - m->default_joint_pos[j]) + noise(4 + ai, cfg.obs_noise[1]);
+    o[13 + ai] = sg * p.jqd[j] + noise(10 + ai, cfg.obs_noise[2]);
+  }
+#pragma unroll
+  for (int a = 0; a < ND; ++a) o[19 + a] = a_obs[a];
+}
+
+struct PreM {
+  float delta[ND], jqd_prev[ND], a_raw[ND], action_rate;
+};
+static_assert(sizeof(PreM) <= 16 * PRE4, "PreM fits PRE4 granules");
+
+__global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_m_step_kernel(
+    const zb_model* __restrict__ mg, const float4* __restrict__ links, zb_task_cfg cfg, int N, float* __restrict__ st,
+    const float* __restrict__ act, float* __restrict__ obs, float* __restrict__ rew, uint8_t* __restrict__ term,
+    uint8_t* __restrict__ trunc, float* __restrict__ acc, const Counters* __restrict__ cnt, uint64_t seed) {
+  MP m = to_mp(mg);
+  __shared__ float4 lds[LDS4];
+  const int lane = threadIdx.x;
+  const int env = xcd_block(blockIdx.x, gridDim.x) * EPW + lane / TL;
+  const int i = env < N ? env : N - 1;
+  const bool lead = env < N && lane % TL == 0;
+  const Q q{lds, lane, lane / TL, lane % TL};
+  for (int t = lane; t < LNK4; t += WGT) lds[LNK_OFF + t] = links[t];
+  Stamps sp;
+  sp.begin();
+#define ST(f) st[(size_t)(f) * N + i]
+  Phys p;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) { p.pos[a] = ST(ZB_S_ROOT_POS + a); p.lv[a] = ST(ZB_S_ROOT_LINVEL + a); p.av[a] = ST(ZB_S_ROOT_ANGVEL + a); }
+#pragma unroll
+  for (int a = 0; a < 4; ++a) p.quat[a] = ST(ZB_S_ROOT_QUAT + a);
+#pragma unroll
+  for (int j = 0; j < ND; ++j) { p.jq[j] = ST(ZB_S_JOINT_POS + j); p.jqd[j] = ST(ZB_S_JOINT_VEL + j); }
+  if (q.s < NL) q.fric(q.s) = ST(ZB_M_LINK_MU + q.s);
+
+  // ActionManager.process_action: RelativeJointPositionAction (scale 0.04 pi, zero offset, clip
+  // +-0.04 pi) in the Isaac Lab joint order, mapped onto the chain's joints
+  const bool writer = q.s == 0;
+  const float step_dt = cfg.sim_dt * (float)cfg.decimation;
+  PreM& pv = *reinterpret_cast<PreM*>(&q.pre());
+  float delta[ND];
+  {
+    PreM pr;
+    pr.action_rate = 0.f;
+#pragma unroll
+    for (int a = 0; a < ND; ++a) {
+      pr.a_raw[a] = act[(size_t)i * ZB_ACT_DIM + a];
+      const float d = pr.a_raw[a] - ST(ZB_M_ACTIONS + a);
+      pr.action_rate += d * d;
+    }
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+      float a = pr.a_raw[0];
+#pragma unroll
+      for (int b = 1; b < ND; ++b) a = m->api_joint_index[j] == b ? pr.a_raw[b] : a;
+      delta[j] = m->api_joint_sign[j] * clampf(a * cfg.action_scale, -cfg.action_clip, cfg.action_clip);
+      pr.jqd_prev[j] = 0.f;
+    }
+    if (writer) pv = pr;
+  }
+
+  // 4 x (apply_action: target = q + delta from the current joint positions; physics step;
+  // ContactSensor.update: feet net force into the 3-slot history, air-time timers + sim_dt).
+  // With 4 substeps the 3 history slots are this step's substeps 2..4.
+  SensorOut so;
+  float fz_h[3][2], fn_h[3][2];
+  float air_cur[2] = {ST(ZB_M_FEET_AIR_CUR), ST(ZB_M_FEET_AIR_CUR + 1)};
+  float air_last[2] = {ST(ZB_M_FEET_AIR_LAST), ST(ZB_M_FEET_AIR_LAST + 1)};
+#pragma unroll
+  for (int h = 0; h < 3; ++h)
+#pragma unroll
+    for (int f = 0; f < 2; ++f) { fz_h[h][f] = ST(ZB_M_FEET_FZ_HIST + 2 * h + f); fn_h[h][f] = ST(ZB_M_FEET_FN_HIST + 2 * h + f); }
+  sp.mark(0);
+  for (int k = 0; k < cfg.decimation; ++k) {
+    float target[ND];
+#pragma unroll
+    for (int j = 0; j < ND; ++j) target[j] = p.jq[j] + delta[j];
+    if (k == cfg.decimation - 1 && writer) {
+#pragma unroll
+      for (int j = 0; j < ND; ++j) pv.jqd_prev[j] = p.jqd[j];
+    }
+    substep<false, true>(m, cfg, p, target, q, true, so, nullptr, nullptr, sp);
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+      const float fn = sqrtf(dot3(so.feet_f[f], so.feet_f[f]));
+      fz_h[2][f] = fz_h[1][f]; fz_h[1][f] = fz_h[0][f]; fz_h[0][f] = so.feet_f[f][2];
+      fn_h[2][f] = fn_h[1][f]; fn_h[1][f] = fn_h[0][f]; fn_h[0][f] = fn;
+      const bool c = fn > cfg.contact_force_threshold;
+      air_last[f] = (air_cur[f] > 0.f && c) ? air_cur[f] + cfg.sim_dt : air_last[f];
+      air_cur[f] = c ? 0.f : air_cur[f] + cfg.sim_dt;
+    }
+    sp.mark(7);
+  }
+  m = opaque(m);
+  wave_sync();
+  const PreM pr = pv;
+  st = opaque_ptr(st);
+
+  const float ep_len = ST(ZB_M_EP_LEN) + 1.f;
+  float cmd[3] = {ST(ZB_M_COMMANDS), ST(ZB_M_COMMANDS + 1), ST(ZB_M_COMMANDS + 2)};
+  float tleft = ST(ZB_M_CMD_TIME_LEFT), standing = ST(ZB_M_CMD_STANDING);
+  float met[2] = {ST(ZB_M_METRICS), ST(ZB_M_METRICS + 1)};
+  float f_last[2] = {ST(ZB_M_FEET_F_LAST), ST(ZB_M_FEET_F_LAST + 1)};
+  float step_len[2] = {ST(ZB_M_FEET_STEP_LEN), ST(ZB_M_FEET_STEP_LEN + 1)};
+  float down[2][3];
+#pragma unroll
+  for (int f = 0; f < 2; ++f)
+#pragma unroll
+    for (int a = 0; a < 3; ++a) down[f][a] = ST(ZB_M_FEET_DOWN_POS + 3 * f + a);
+
+  // post-step articulation data: root (= base link) pose, link-origin / COM velocity, angular
+  // velocity; feet link poses and COM velocities
+  float bq[4], bp[3], vb[3], vcom[3], wb[3], feet[2][3], fq[2][4], fvel[2][3];
+  {
+    wave_sync();
+    fk_team_pose(p, q);
+    wave_sync();
+    float S[ND][6], org[ND][3];
+    read_joints(q, S, org);
+    const int B = m->base_link;
+    link_pose_q(m, q, B, bp, bq);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) bp[a] += p.pos[a];
+    link_origin_vel_q(m, q, p, S, B, vb);
+    link_com_vel_q(m, q, p, S, B, vcom);
+    body_ang_vel_q(p, S, link_body(B), wb);
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+      const int l = f == 0 ? 0 : 11;
+      link_pose_q(m, q, l, feet[f], fq[f]);
+#pragma unroll
+      for (int a = 0; a < 3; ++a) feet[f][a] += p.pos[a];
+      link_com_vel_q(m, q, p, S, l, fvel[f]);
+    }
+  }
+  // TerminationManager (flat: time_out, base_height < 0.2, feet_close < 0.12)
+  const bool time_out = ep_len >= (float)cfg.max_episode_length;
+  const bool low = bp[2] < cfg.termination_height;
+  const float fd[3] = {feet[0][0] - feet[1][0], feet[0][1] - feet[1][1], feet[0][2] - feet[1][2]};
+  const bool close = sqrtf(dot3(fd, fd)) < cfg.feet_close_min;
+  const bool terminated = low || close;
+
+  // RewardManager.compute: term * weight * step_dt in cfg order (mgr.py:262-357, flat overrides)
+  float r[ZB_M_NUM_REWARD_TERMS];
+  {
+    float Rb[9];
+    qmat(bq, Rb);
+    const float fwd[3] = {Rb[4], -Rb[1], 0.f};  // GRAVITY_VEC_W x quat_apply(root_quat, y)
+    float vx, vy;
+    {  // yaw_quat + quat_apply_inverse on root_link_lin_vel_w
+      const float yaw = atan2f(2.f * (bq[0] * bq[3] + bq[1] * bq[2]), 1.f - 2.f * (bq[2] * bq[2] + bq[3] * bq[3]));
+      float sy, cy;
+      sincos_r(yaw, &sy, &cy);
+      vx = cy * vb[0] + sy * vb[1];
+      vy = -sy * vb[0] + cy * vb[1];
+    }
+    const float ex = cmd[0] - vx, ey = cmd[1] - vy;
+    r[ZB_M_R_TRACK_LIN_VEL_XY] = __expf(-(ex * ex + ey * ey) / 0.25f);
+    const float ez = cmd[2] - wb[2];
+    r[ZB_M_R_TRACK_ANG_VEL_Z] = __expf(-(ez * ez) / 0.25f);
+    r[ZB_M_R_TERMINATION] = terminated ? 1.f : 0.f;
+    r[ZB_M_R_DOF_TORQUES] = so.tau2;
+    float ja = 0.f;
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+      const float aj = (p.jqd[j] - pr.jqd_prev[j]) / cfg.sim_dt;
+      ja += aj * aj;
+    }
+    r[ZB_M_R_DOF_ACC] = ja;
+    r[ZB_M_R_ACTION_RATE] = pr.action_rate;
+    // foot_step_length (rewards.py:44-104)
+    const float nrm = sqrtf(dot3(fwd, fwd)) + 1e-6f;
+    const float fh[3] = {fwd[0] / nrm, fwd[1] / nrm, fwd[2] / nrm};
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+      const float fz = (fz_h[0][f] + fz_h[1][f] + fz_h[2][f]) / 3.f;
+      if (fz > 10.f && f_last[f] < 10.f) {
+        const float dv[3] = {feet[f][0] - down[f][0], feet[f][1] - down[f][1], feet[f][2] - down[f][2]};
+        step_len[f] = fabsf(dot3(dv, fh));
+#pragma unroll
+        for (int a = 0; a < 3; ++a) down[f][a] = feet[f][a];
+      }
+      f_last[f] = fz;
+    }
+    r[ZB_M_R_FOOT_STEP_LENGTH] = tanh_r(15.f * fminf(step_len[0], step_len[1]));
+    float sd = 0.f, sfw = 0.f, sl = 0.f;
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+      float R[9];
+      qmat(fq[f], R);
+      const float sg = f == 0 ? 1.f : -1.f;  // foot_downward: feet axes (0, 1, 0), (0, -1, 0) vs z
+      const float dz[3] = {sg * R[1], sg * R[4], sg * R[7] - 1.f};
+      sd += sqrtf(dot3(dz, dz));
+      const float dx[3] = {R[0] - fwd[0], R[3] - fwd[1], R[6] - fwd[2]};  // foot_forward
+      sfw += sqrtf(dot3(dx, dx));
+      const bool c = fmaxf(fn_h[0][f], fmaxf(fn_h[1][f], fn_h[2][f])) > 1.0f;  // feet_slide
+      sl += sqrtf(fvel[f][0] * fvel[f][0] + fvel[f][1] * fvel[f][1]) * (c ? 1.f : 0.f);
+    }
+    r[ZB_M_R_FOOT_DOWNWARD] = sd;
+    r[ZB_M_R_FOOT_FORWARD] = sfw;
+    r[ZB_M_R_FEET_SLIDE] = sl;
+    r[ZB_M_R_AIR_TIME_BALANCE] = fabsf(air_last[0] - air_last[1]);
+  }
+  float reward = 0.f, sums[ZB_M_NUM_REWARD_TERMS];
+#pragma unroll
+  for (int t = 0; t < ZB_M_NUM_REWARD_TERMS; ++t) {
+    const float v = r[t] * cfg.stage_scales[0][t] * step_dt;
+    reward += v;
+    sums[t] = ST(ZB_M_EP_SUMS + t) + v;
+  }
+  const bool reset = terminated || time_out;
+  const uint64_t hs = env_hash(seed, cnt->calls, i);
+  float a_obs[ND];
+#pragma unroll
+  for (int a = 0; a < ND; ++a) a_obs[a] = pr.a_raw[a];
+  float vcb[3], wcb[3];  // root_lin_vel_b (COM), root_ang_vel_b after the resets
+
+  // _reset_idx: curriculum (finalize), events reset_base / reset_robot_joints / reset_my_data,
+  // managers (actions 0, reward sums and metrics logged, command resampled, sensor cleared)
+  if (reset) {
+    if (lead) {
+#pragma unroll
+      for (int t = 0; t < ZB_M_NUM_REWARD_TERMS; ++t) atomicAdd(&acc[t], sums[t]);
+      atomicAdd(&acc[ACC_NRES], 1.f);
+      if (low) atomicAdd(&acc[ACC_DIED], 1.f);
+      if (time_out) atomicAdd(&acc[ACC_TOUT], 1.f);
+      if (close) atomicAdd(&acc[ACC_TERM2], 1.f);
+      atomicAdd(&acc[ACC_MET0], met[0]);
+      atomicAdd(&acc[ACC_MET1], met[1]);
+    }
+    (void)reset_pose(m, cfg, hs, p);
+    const float4 qr = q.dflt()[3];
+    const float qrel[4] = {qr.x, qr.y, qr.z, qr.w};
+    qmul(p.quat, qrel, bq);
+    float R[9];
+    qmat(p.quat, R);
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+      const float4 fr = q.dflt()[4 + f];
+      const float v[3] = {fr.x, fr.y, fr.z};
+      float w3[3];
+      mv3(R, v, w3);
+#pragma unroll
+      for (int a = 0; a < 3; ++a) down[f][a] = p.pos[a] + w3[a];
+      f_last[f] = 0.f;
+      step_len[f] = 0.f;
+    }
+    m_resample(cfg, cnt, hs, M_DRAW_RESET_CMD, cmd, standing);
+    tleft = cfg.cmd_resample_s;
+    met[0] = met[1] = 0.f;
+#pragma unroll
+    for (int a = 0; a < ND; ++a) a_obs[a] = 0.f;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) { vcb[a] = 0.f; wcb[a] = 0.f; }
+  } else {
+    float R[9];
+    qmat(bq, R);
+    vcb[0] = R[0] * vcom[0] + R[3] * vcom[1] + R[6] * vcom[2];
+    vcb[1] = R[1] * vcom[0] + R[4] * vcom[1] + R[7] * vcom[2];
+    vcb[2] = R[2] * vcom[0] + R[5] * vcom[1] + R[8] * vcom[2];
+    wcb[0] = R[0] * wb[0] + R[3] * wb[1] + R[6] * wb[2];
+    wcb[1] = R[1] * wb[0] + R[4] * wb[1] + R[7] * wb[2];
+    wcb[2] = R[2] * wb[0] + R[5] * wb[1] + R[8] * wb[2];
+  }
+  // CommandManager.compute: metrics (UniformVelocityCommand._update_metrics), timer, resample,
+  // standing envs zeroed
+  {
+    const float max_steps = cfg.cmd_resample_s / step_dt;
+    const float ex = cmd[0] - vcb[0], ey = cmd[1] - vcb[1];
+    met[0] += sqrtf(ex * ex + ey * ey) / max_steps;
+    met[1] += fabsf(cmd[2] - wcb[2]) / max_steps;
+    tleft -= step_dt;
+    if (tleft <= 0.f) {
+      m_resample(cfg, cnt, hs, M_DRAW_CMD, cmd, standing);
+      tleft = cfg.cmd_resample_s;
+    }
+    if (standing > 0.5f) cmd[0] = cmd[1] = cmd[2] = 0.f;
+  }
+  sp.mark(12);
+  if (writer) {
+    auto live = [reset](float v) { return reset ? 0.f : v; };
+#pragma unroll
+    for (int a = 0; a < 3; ++a) { ST(ZB_S_ROOT_POS + a) = p.pos[a]; ST(ZB_S_ROOT_LINVEL + a) = p.lv[a]; ST(ZB_S_ROOT_ANGVEL + a) = p.av[a]; }
+#pragma unroll
+    for (int a = 0; a < 4; ++a) ST(ZB_S_ROOT_QUAT + a) = p.quat[a];
+#pragma unroll
+    for (int j = 0; j < ND; ++j) { ST(ZB_S_JOINT_POS + j) = p.jq[j]; ST(ZB_S_JOINT_VEL + j) = p.jqd[j]; }
+#pragma unroll
+    for (int a = 0; a < ND; ++a) ST(ZB_M_ACTIONS + a) = a_obs[a];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) ST(ZB_M_COMMANDS + a) = cmd[a];
+    ST(ZB_M_CMD_TIME_LEFT) = tleft;
+    ST(ZB_M_CMD_STANDING) = standing;
+    ST(ZB_M_METRICS) = met[0];
+    ST(ZB_M_METRICS + 1) = met[1];
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+#pragma unroll
+      for (int a = 0; a < 3; ++a) ST(ZB_M_FEET_DOWN_POS + 3 * f + a) = down[f][a];
+      ST(ZB_M_FEET_STEP_LEN + f) = step_len[f];
+      ST(ZB_M_FEET_F_LAST + f) = f_last[f];
+      ST(ZB_M_FEET_AIR_CUR + f) = live(air_cur[f]);
+      ST(ZB_M_FEET_AIR_LAST + f) = live(air_last[f]);
+#pragma unroll
+      for (int h = 0; h < 3; ++h) { ST(ZB_M_FEET_FZ_HIST + 2 * h + f) = live(fz_h[h][f]); ST(ZB_M_FEET_FN_HIST + 2 * h + f) = live(fn_h[h][f]); }
+    }
+    ST(ZB_M_EP_LEN) = live(ep_len);
+#pragma unroll
+    for (int t = 0; t < ZB_M_NUM_REWARD_TERMS; ++t) ST(ZB_M_EP_SUMS + t) = live(sums[t]);
+    m_write_obs(m, cfg, hs, bq, cmd, p, a_obs, obs + (size_t)i * ZB_M_OBS_DIM);
+    rew[i] = reward;
+    term[i] = terminated ? 1 : 0;
+    trunc[i] = time_out ? 1 : 0;
+  }
+  sp.mark(8);
+  sp.flush();
+#undef ST
+}
+
+// command of a reset env redrawn after lin_vel_cmd_levels widened the ranges (zb_finalize_kernel):
+// the post-reset state has zero velocity, so the first metric update reads |command| only
+__device__ __forceinline__ void m_fixup_env(const zb_task_cfg& cfg, int N, float* __restrict__ st, float* __restrict__ obs,
+                                            const Counters* cnt, uint64_t hs, int i) {
+  float cmd[3], standing;
+  m_resample(cfg, cnt, hs, M_DRAW_RESET_CMD, cmd, standing);
+  const float step_dt = cfg.sim_dt * (float)cfg.decimation;
+  const float max_steps = cfg.cmd_resample_s / step_dt;
+  const float ex = cmd[0] - 0.f, ey = cmd[1] - 0.f;
+  st[(size_t)ZB_M_METRICS * N + i] = 0.f + sqrtf(ex * ex + ey * ey) / max_steps;
+  st[(size_t)(ZB_M_METRICS + 1) * N + i] = 0.f + fabsf(cmd[2] - 0.f) / max_steps;
+  st[(size_t)ZB_M_CMD_STANDING * N + i] = standing;
+  if (standing > 0.5f) cmd[0] = cmd[1] = cmd[2] = 0.f;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    st[(size_t)(ZB_M_COMMANDS + a) * N + i] = cmd[a];
+    obs[(size_t)i * ZB_M_OBS_DIM + 4 + a] = cmd[a];
+  }
+}
+
+// explicit resets / construction (init: also the friction default): one thread per env. The
+// command is resampled but not yet zeroed for standing envs (that happens in the next
+// CommandManager.compute, i.e. the next step).
+__global__ void zb_m_reset_kernel(const zb_model* __restrict__ mg, const float4* __restrict__ links, zb_task_cfg cfg,
+                                  int N, float* __restrict__ st, const int32_t* __restrict__ ids, int n,
+                                  float* __restrict__ acc, const Counters* __restrict__ cnt, uint64_t seed, int init) {
+  MP m = to_mp(mg);
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const int i = ids ? ids[t] : t;
+  if (i < 0 || i >= N) return;
+#define ST(f) st[(size_t)(f) * N + i]
+  if (!init) {
+#pragma unroll
+    for (int k = 0; k < ZB_M_NUM_REWARD_TERMS; ++k) atomicAdd(&acc[k], ST(ZB_M_EP_SUMS + k));
+    atomicAdd(&acc[ACC_NRES], 1.f);
+    atomicAdd(&acc[ACC_MET0], ST(ZB_M_METRICS));
+    atomicAdd(&acc[ACC_MET1], ST(ZB_M_METRICS + 1));
+  }
+  Phys p;
+  const uint64_t hs = env_hash(seed, cnt->calls, i);
+  (void)reset_pose(m, cfg, hs, p);
+  float cmd[3], standing;
+  m_resample(cfg, cnt, hs, M_DRAW_RESET_CMD, cmd, standing);
+#pragma unroll
+  for (int a = 0; a < 3; ++a) { ST(ZB_S_ROOT_POS + a) = p.pos[a]; ST(ZB_S_ROOT_LINVEL + a) = p.lv[a]; ST(ZB_S_ROOT_ANGVEL + a) = p.av[a]; }
+#pragma unroll
+  for (int a = 0; a < 4; ++a) ST(ZB_S_ROOT_QUAT + a) = p.quat[a];
+#pragma unroll
+  for (int j = 0; j < ND; ++j) { ST(ZB_S_JOINT_POS + j) = p.jq[j]; ST(ZB_S_JOINT_VEL + j) = p.jqd[j]; ST(ZB_M_ACTIONS + j) = 0.f; }
+#pragma unroll
+  for (int a = 0; a < 3; ++a) ST(ZB_M_COMMANDS + a) = cmd[a];
+  ST(ZB_M_CMD_TIME_LEFT) = cfg.cmd_resample_s;
+  ST(ZB_M_CMD_STANDING) = standing;
+  ST(ZB_M_METRICS) = 0.f;
+  ST(ZB_M_METRICS + 1) = 0.f;
+  float R[9];
+  qmat(p.quat, R);
+#pragma unroll
+  for (int f = 0; f < 2; ++f) {
+    const float4 fr = links[DFLT_OFF + 4 + f];
+    const float v[3] = {fr.x, fr.y, fr.z};
+    float w3[3];
+    mv3(R, v, w3);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) ST(ZB_M_FEET_DOWN_POS + 3 * f + a) = p.pos[a] + w3[a];
+    ST(ZB_M_FEET_STEP_LEN + f) = 0.f;
+    ST(ZB_M_FEET_F_LAST + f) = 0.f;
+    ST(ZB_M_FEET_AIR_CUR + f) = 0.f;
+    ST(ZB_M_FEET_AIR_LAST + f) = 0.f;
+#pragma unroll
+    for (int h = 0; h < 3; ++h) { ST(ZB_M_FEET_FZ_HIST + 2 * h + f) = 0.f; ST(ZB_M_FEET_FN_HIST + 2 * h + f) = 0.f; }
+  }
+  ST(ZB_M_EP_LEN) = 0.f;
+#pragma unroll
+  for (int k = 0; k < ZB_M_NUM_REWARD_TERMS; ++k) ST(ZB_M_EP_SUMS + k) = 0.f;
+  if (init) {
+#pragma unroll
+    for (int l = 0; l < NL; ++l) ST(ZB_M_LINK_MU + l) = cfg.friction;
+  }
+#undef ST
+}
+
+// the observation of the current state (reset(): ObservationManager.compute after _reset_idx);
+// noise from this call's stream
+__global__ void zb_m_observe_kernel(const zb_model* __restrict__ mg, zb_task_cfg cfg, int N, const float* __restrict__ st,
+                                    float* __restrict__ obs, const Counters* __restrict__ cnt, uint64_t seed) {
+  MP m = to_mp(mg);
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  Phys p;
+  load_phys(st, N, i, p);
+  Kin k;
+  fk(m, p, k);
+  float bp[3], bq[4];
+  link_pose(m, k, m->base_link, bp, bq);
+  const float cmd[3] = {st[(size_t)ZB_M_COMMANDS * N + i], st[(size_t)(ZB_M_COMMANDS + 1) * N + i],
+                        st[(size_t)(ZB_M_COMMANDS + 2) * N + i]};
+  float a_obs[ND];
+#pragma unroll
+  for (int a = 0; a < ND; ++a) a_obs[a] = st[(size_t)(ZB_M_ACTIONS + a) * N + i];
+  m_write_obs(m, cfg, env_hash(seed, cnt->calls, i), bq, cmd, p, a_obs, obs + (size_t)i * ZB_M_OBS_DIM);
+}
+
+// Episode log finalisation, curricula and the full-reset episode_length_buf draw (v2.py:418-422);
+// leaves the accumulator zeroed for the next launch. Single workgroup (grid-strided over envs).
+// The counters (RNG stream position, common_step_counter, curriculum state) live on the device so
+// that a captured graph of zb_step advances them on every replay. Reset-mode events in the
+// reference's order (v4 EventCfg 268-439): the episode log and the range-curriculum buffers
+// (_reset_idx before the events), my_curriculum (one stage per call with resets once
+// common_step_counter >= stage_steps[next]), range_curriculum (v4: widen the command ranges when
+// the buffered tracking rewards exceed 85 % of their weight). New weights / ranges apply from the
+// next step (the reference applies the reset-event ones to the commands it resamples in the same
+// call). The manager's lin_vel_cmd_levels is exact: the reset envs' commands are
+// redrawn here when it fires.
+__global__ void zb_finalize_kernel(int N, float* __restrict__ st, float* __restrict__ acc,
+                                   float* __restrict__ log_means, int32_t* __restrict__ log_counts,
+                                   float* __restrict__ user_means, int32_t* __restrict__ user_counts, float episode_s,
+                                   uint64_t seed, Counters* __restrict__ cnt, int force_full, int reset_counts,
+                                   int is_step, int ep_len_row, zb_task_cfg cfg, float* __restrict__ obs,
+                                   const uint8_t* __restrict__ term, const uint8_t* __restrict__ trunc) {
+  const uint64_t ctr = cnt->calls;
+  const uint64_t steps = cnt->steps + (is_step ? 1 : 0);
+  const float nres = acc[ACC_NRES];
+  const bool full = force_full || nres == (float)N;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    cnt->steps = steps;
+    cnt->changed = 0;
+    if (nres > 0.f) {
+      float v[ZB_LOG_LEN];
+#pragma unroll
+      for (int t = 0; t < ZB_MAX_REWARD_TERMS; ++t) v[t] = acc[t] / nres / episode_s;
+      v[16] = (float)cnt->stage;  // logged before the events run (v4.py:952-957)
+      v[17] = cnt->vel[0];
+      v[18] = cnt->vel[1];
+      v[19] = cnt->yaw[0];
+      if (cfg.task == ZB_TASK_MANAGER_V0) {
+        // lin_vel_cmd_levels (curriculums.py:47-74) runs first in _reset_idx; it widens the
+        // velocity ranges by +-delta when the mean episodic tracking reward / 20 s of the reset envs
+        // exceeds 0.8 x its weight, on calls where common_step_counter % max_episode_length == 0
+        if (cfg.range_period_steps > 0 && steps % (uint64_t)cfg.range_period_steps == 0 &&
+            v[ZB_M_R_TRACK_LIN_VEL_XY] > cfg.stage_scales[0][ZB_M_R_TRACK_LIN_VEL_XY] * cfg.range_threshold) {
+          cnt->vel[0] = clampf(cnt->vel[0] - cfg.range_delta, cfg.range_limit_vel[0], cfg.range_limit_vel[1]);
+          cnt->vel[1] = clampf(cnt->vel[1] + cfg.range_delta, cfg.range_limit_vel[0], cfg.range_limit_vel[1]);
+          cnt->yaw[0] = clampf(cnt->yaw[0] - cfg.range_delta, cfg.range_limit_yaw[0], cfg.range_limit_yaw[1]);
+          cnt->yaw[1] = clampf(cnt->yaw[1] + cfg.range_delta, cfg.range_limit_yaw[0], cfg.range_limit_yaw[1]);
+          cnt->changed = 1;
+        }
+        v[16] = cnt->vel[1];             // Curriculum/lin_vel_cmd_levels (the state after compute)
+        v[17] = acc[ACC_MET0] / nres;    // Metrics/base_velocity/error_vel_xy
+        v[18] = acc[ACC_MET1] / nres;    // Metrics/base_velocity/error_vel_yaw
+        v[19] = 0.f;
+      }
+#pragma unroll
+      for (int t = 0; t < ZB_LOG_LEN; ++t) {
+        log_means[t] = v[t];
+        if (user_means) user_means[t] = v[t];
+      }
+      const int32_t c[ZB_LOG_COUNTS] = {reset_counts ? 0 : (int32_t)acc[ACC_DIED],
+                                        reset_counts ? 0 : (int32_t)acc[ACC_TOUT],
+                                        reset_counts ? 0 : (int32_t)acc[ACC_TERM2], 0};
+#pragma unroll
+      for (int k = 0; k < ZB_LOG_COUNTS; ++k) {
+        log_counts[k] = c[k];
+        if (user_counts) user_counts[k] = c[k];
+      }
+      if (cfg.task == ZB_TASK_WALKING_V4) {  // curriculum_*_reward_buffer.append (v4.py:941-944)
+        cnt->ring_vel[cnt->ring_head] = v[ZB_V4_R_TRACK_LIN_VEL_X];
+        cnt->ring_yaw[cnt->ring_head] = v[ZB_V4_R_TRACK_HEADING_YAW];
+        cnt->ring_head = (cnt->ring_head + 1) % ZB_V4_RING;
+        cnt->ring_n = min(cnt->ring_n + 1, ZB_V4_RING);
+      }
+      // my_curriculum
+      const int s0 = cnt->stage;
+      if (s0 + 1 < cfg.num_stages && s0 + 1 < ZB_MAX_STAGES && steps >= (uint64_t)cfg.stage_steps[s0 + 1]) {
+        cnt->stage = s0 + 1;
+        cnt->prob_pos = cfg.stage_prob_pos[s0 + 1];
+      }
+      // range_curriculum (v4.py:201-265)
+      if (cfg.task == ZB_TASK_WALKING_V4 && cnt->ring_n >= cfg.range_min_buffer && cfg.range_period_steps > 0 &&
+          steps >= (uint64_t)cfg.range_start_steps && steps % (uint64_t)cfg.range_period_steps == 0) {
+        float mv = 0.f, my = 0.f;
+        for (int k = 0; k < cnt->ring_n; ++k) { mv += cnt->ring_vel[k]; my += cnt->ring_yaw[k]; }
+        mv /= (float)cnt->ring_n;
+        my /= (float)cnt->ring_n;
+        const int sg = cnt->stage;
+        if (mv > cfg.stage_scales[sg][ZB_V4_R_TRACK_LIN_VEL_X] * cfg.range_threshold) {
+          cnt->vel[0] = clampf(cnt->vel[0] - cfg.range_delta, cfg.range_limit_vel[0], cfg.range_limit_vel[1]);
+          cnt->vel[1] = clampf(cnt->vel[1] + cfg.range_delta, cfg.range_limit_vel[0], cfg.range_limit_vel[1]);
+        }
+        if (my > cfg.stage_scales[sg][ZB_V4_R_TRACK_HEADING_YAW] * cfg.range_threshold) {
+          cnt->yaw[0] = clampf(cnt->yaw[0] - cfg.range_delta, cfg.range_limit_yaw[0], cfg.range_limit_yaw[1]);
+          cnt->yaw[1] = clampf(cnt->yaw[1] + cfg.range_delta, cfg.range_limit_yaw[0], cfg.range_limit_yaw[1]);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < ACC) acc[threadIdx.x] = 0.f;
+  if (threadIdx.x == 0) cnt->calls = ctr + 1;
+  // lin_vel_cmd_levels widened the ranges in this step: the reference's curriculum runs before the
+  // command manager resamples the reset envs, so their commands (and the metrics / observations
+  // that read them) are redrawn from the same draws with the new ranges (rare: at most once per
+  // max_episode_length steps, so one workgroup does it)
+  if (obs && cnt->changed)
+    for (int i = threadIdx.x; i < N; i += blockDim.x)
+      if (term[i] || trunc[i]) m_fixup_env(cfg, N, st, obs, cnt, env_hash(seed, ctr, i), i);
+  if (full && cfg.task != ZB_TASK_MANAGER_V0)  // ManagerBasedRLEnv has no full-reset draw
+    for (int i = threadIdx.x; i < N; i += blockDim.x) {
+      const uint64_t h = hash64(seed ^ hash64(ctr * 0x100000001B3ull + (uint64_t)i));
+      st[(size_t)ep_len_row * N + i] = (float)(int)(h % (uint64_t)cfg.max_episode_length);
+    }
+}
+
 }  // namespace
 
 // =========================================================================== C ABI
@@ -2876,7 +3393,8 @@ int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_dev
   if (!m || !c || !out || num_envs <= 0) return set_err(-1, "zb_create", hipSuccess);
   for (int l = 0; l < NL; ++l)
     if (m->link_body[l] != link_body(l)) return set_err(-1, "zb_create: model topology != compiled ZBOT-6 chain", hipSuccess);
-  if (m->base_link != 6 || m->foot_links[0] != 0 || m->foot_links[1] != 11)
+  if ((m->base_link != 6 && !(c->task == ZB_TASK_MANAGER_V0 && m->base_link == 5)) || m->foot_links[0] != 0 ||
+      m->foot_links[1] != 11)
     return set_err(-1, "zb_create: unexpected base/feet link indices", hipSuccess);
   for (int k = 0; k < 10; ++k)
     if (m->undesired_links[k] != k + 1) return set_err(-1, "zb_create: unexpected undesired link set", hipSuccess);
@@ -2891,7 +3409,8 @@ int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_dev
     if (np != m->num_self_pairs) return set_err(-1, "zb_create: self-collision pair count", hipSuccess);
   }
   if (c->decimation < 1 || c->solver_iterations < 0) return set_err(-1, "zb_create: cfg", hipSuccess);
-  if (c->task != ZB_TASK_WALKING_V2 && c->task != ZB_TASK_STANDUP_V0 && c->task != ZB_TASK_WALKING_V4)
+  if (c->task != ZB_TASK_WALKING_V2 && c->task != ZB_TASK_STANDUP_V0 && c->task != ZB_TASK_WALKING_V4 &&
+      c->task != ZB_TASK_MANAGER_V0)
     return set_err(-1, "zb_create: unknown task", hipSuccess);
   if (c->num_stages < 1 || c->num_stages > ZB_MAX_STAGES) return set_err(-1, "zb_create: num_stages", hipSuccess);
   if (c->task == ZB_TASK_STANDUP_V0 && c->center_z_period < 1) return set_err(-1, "zb_create: center_z_period", hipSuccess);
@@ -2902,7 +3421,8 @@ int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_dev
   h->seed = seed;
   h->task = c->task;
   h->state_dim = c->task == ZB_TASK_STANDUP_V0 ? ZB_SU_STATE_DIM
-                 : c->task == ZB_TASK_WALKING_V4 ? ZB_V4_STATE_DIM : ZB_STATE_DIM;
+                 : c->task == ZB_TASK_WALKING_V4 ? ZB_V4_STATE_DIM
+                 : c->task == ZB_TASK_MANAGER_V0 ? ZB_M_STATE_DIM : ZB_STATE_DIM;
   h->d_cnt = nullptr;
   h->cfg = *c;
   HIPCHK(hipMalloc(&h->d_model, sizeof(zb_model)), "hipMalloc model");
@@ -2918,7 +3438,7 @@ int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_dev
     HIPCHK(hipMemcpy(h->d_cnt, &c0, sizeof(Counters), hipMemcpyHostToDevice), "hipMemcpy counters");
   }
   HIPCHK(hipMalloc(&h->d_log_means, sizeof(float) * ZB_LOG_LEN), "hipMalloc log");
-  HIPCHK(hipMalloc(&h->d_log_counts, sizeof(int32_t) * 2), "hipMalloc log");
+  HIPCHK(hipMalloc(&h->d_log_counts, sizeof(int32_t) * ZB_LOG_COUNTS), "hipMalloc log");
   HIPCHK(hipMemcpy(h->d_model, m, sizeof(zb_model), hipMemcpyHostToDevice), "hipMemcpy model");
   {
     float4 tab[LNK4];
@@ -2965,14 +3485,14 @@ int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_dev
   }
   HIPCHK(hipMemset(h->d_state, 0, sizeof(float) * (size_t)h->state_dim * num_envs), "hipMemset state");
   HIPCHK(hipMemset(h->d_log_means, 0, sizeof(float) * ZB_LOG_LEN), "hipMemset log");
-  HIPCHK(hipMemset(h->d_log_counts, 0, sizeof(int32_t) * 2), "hipMemset log");
+  HIPCHK(hipMemset(h->d_log_counts, 0, sizeof(int32_t) * ZB_LOG_COUNTS), "hipMemset log");
   HIPCHK(hipMemset(h->d_acc, 0, sizeof(float) * ACC), "hipMemset acc");
   // start at the default pose (ep_len 0, as after construction; reset() randomises it)
   zb_derive_kernel<<<1, 1>>>(h->d_model, h->d_links);
   int rc = launch_check("zb_derive_kernel");
   if (rc) return rc;
   if (h->task == ZB_TASK_STANDUP_V0) {
-    zb_su_friction_kernel<<<(num_envs * NL + 255) / 256, 256>>>(num_envs, h->d_state, nullptr, c->friction);
+    zb_su_friction_kernel<<<(num_envs * NL + 255) / 256, 256>>>(num_envs, h->d_state, nullptr, c->friction, ZB_SU_LINK_MU);
     rc = launch_check("zb_su_friction_kernel");
     if (rc) return rc;
     // the construction-time reset draws its poses at RNG position 0; later calls start at 1
@@ -2987,6 +3507,15 @@ int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_dev
     zb_v4_reset_kernel<<<(num_envs + 255) / 256, 256>>>(h->d_model, h->d_links, h->cfg, num_envs, h->d_state, nullptr,
                                                        num_envs, h->d_acc, h->d_cnt, h->seed, 1);
     rc = launch_check("zb_v4_reset_kernel");
+    if (rc) return rc;
+    const uint64_t one = 1;
+    HIPCHK(hipMemcpy(&h->d_cnt->calls, &one, sizeof(one), hipMemcpyHostToDevice), "hipMemcpy counters");
+  } else if (h->task == ZB_TASK_MANAGER_V0) {
+    // construction: ManagerBasedRLEnv.__init__ -> load_managers + reset events at RNG position 0
+    // (friction default fill; the startup material event overwrites it); later calls start at 1
+    zb_m_reset_kernel<<<(num_envs + 255) / 256, 256>>>(h->d_model, h->d_links, h->cfg, num_envs, h->d_state, nullptr,
+                                                      num_envs, h->d_acc, h->d_cnt, h->seed, 1);
+    rc = launch_check("zb_m_reset_kernel");
     if (rc) return rc;
     const uint64_t one = 1;
     HIPCHK(hipMemcpy(&h->d_cnt->calls, &one, sizeof(one), hipMemcpyHostToDevice), "hipMemcpy counters");
@@ -3066,14 +3595,21 @@ void zb_destroy(zb_handle h) {
 // episode-log divisor: walking divides the summed episode sums by the 20 s episode (v2.py:446),
 // standup already divided each env's sums by its own duration (standup.py:653-659)
 static float log_episode_s(zb_handle h) {
-  return h->task == ZB_TASK_WALKING_V2 ? h->cfg.sim_dt * h->cfg.decimation * h->cfg.max_episode_length : 1.f;
+  // (the manager's RewardManager.reset divides by max_episode_length_s too)
+  return h->task == ZB_TASK_WALKING_V2 || h->task == ZB_TASK_MANAGER_V0
+             ? h->cfg.sim_dt * h->cfg.decimation * h->cfg.max_episode_length
+             : 1.f;
 }
 
-static int finalize(zb_handle h, hipStream_t s, int full, int reset_counts, int is_step) {
-  const int ep_row = h->task == ZB_TASK_STANDUP_V0 ? ZB_SU_EP_LEN : h->task == ZB_TASK_WALKING_V4 ? ZB_V4_EP_LEN : ZB_S_EP_LEN;
+static int finalize(zb_handle h, hipStream_t s, int full, int reset_counts, int is_step, float* obs = nullptr,
+                    const uint8_t* term = nullptr, const uint8_t* trunc = nullptr) {
+  const int ep_row = h->task == ZB_TASK_STANDUP_V0   ? ZB_SU_EP_LEN
+                     : h->task == ZB_TASK_WALKING_V4 ? ZB_V4_EP_LEN
+                     : h->task == ZB_TASK_MANAGER_V0 ? ZB_M_EP_LEN
+                                                     : ZB_S_EP_LEN;
   zb_finalize_kernel<<<1, 256, 0, s>>>(h->n, h->d_state, h->d_acc, h->d_log_means, h->d_log_counts, h->u_log_means,
                                        h->u_log_counts, log_episode_s(h), h->seed, h->d_cnt, full, reset_counts, is_step,
-                                       ep_row, h->cfg);
+                                       ep_row, h->cfg, obs, term, trunc);
   return launch_check("zb_finalize_kernel");
 }
 
@@ -3088,6 +3624,9 @@ int zb_reset(zb_handle h, const int32_t* env_ids, int n, void* stream) {
   else if (h->task == ZB_TASK_WALKING_V4)
     zb_v4_reset_kernel<<<(cnt + 255) / 256, 256, 0, s>>>(h->d_model, h->d_links, h->cfg, h->n, h->d_state, env_ids, cnt,
                                                          h->d_acc, h->d_cnt, h->seed, 0);
+  else if (h->task == ZB_TASK_MANAGER_V0)
+    zb_m_reset_kernel<<<(cnt + 255) / 256, 256, 0, s>>>(h->d_model, h->d_links, h->cfg, h->n, h->d_state, env_ids, cnt,
+                                                        h->d_acc, h->d_cnt, h->seed, 0);
   else
     zb_reset_kernel<<<(cnt + 255) / 256, 256, 0, s>>>(h->d_model, h->d_links, h->n, h->d_state, env_ids, cnt, h->d_acc);
   int rc = launch_check("zb_reset_kernel");
@@ -3108,6 +3647,9 @@ int zb_step(zb_handle h, const float* actions, float* obs, float* reward, uint8_
   else if (h->task == ZB_TASK_WALKING_V4)
     zb_v4_step_kernel<<<blocks, WGT, 0, s>>>(h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward,
                                              terminated, truncated, h->d_acc, h->d_cnt, h->seed);
+  else if (h->task == ZB_TASK_MANAGER_V0)
+    zb_m_step_kernel<<<blocks, WGT, 0, s>>>(h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward,
+                                            terminated, truncated, h->d_acc, h->d_cnt, h->seed);
   else
     zb_step_kernel<<<blocks, WGT, 0, s>>>(h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward,
                                           terminated, truncated, h->d_acc);
@@ -3117,7 +3659,7 @@ int zb_step(zb_handle h, const float* actions, float* obs, float* reward, uint8_
     ++h->prof_n;
   }
   if (rc) return rc;
-  return finalize(h, s, 0, 0, 1);
+  return finalize(h, s, 0, 0, 1, obs, terminated, truncated);
 }
 
 int zb_observe(zb_handle h, float* obs, void* stream) {
@@ -3126,6 +3668,9 @@ int zb_observe(zb_handle h, float* obs, void* stream) {
     zb_su_observe_kernel<<<(h->n + 255) / 256, 256, 0, (hipStream_t)stream>>>(h->d_model, h->n, h->d_state, obs);
   else if (h->task == ZB_TASK_WALKING_V4)
     zb_v4_observe_kernel<<<(h->n + 255) / 256, 256, 0, (hipStream_t)stream>>>(h->d_model, h->n, h->d_state, obs);
+  else if (h->task == ZB_TASK_MANAGER_V0)
+    zb_m_observe_kernel<<<(h->n + 255) / 256, 256, 0, (hipStream_t)stream>>>(h->d_model, h->cfg, h->n, h->d_state, obs,
+                                                                             h->d_cnt, h->seed);
   else
     zb_observe_kernel<<<(h->n + 255) / 256, 256, 0, (hipStream_t)stream>>>(h->d_model, h->n, h->d_state, obs);
   return launch_check("zb_observe_kernel");
@@ -3135,8 +3680,10 @@ int zb_state_dim(zb_handle h) { return h ? h->state_dim : -1; }
 
 int zb_set_link_friction(zb_handle h, const float* mu, void* stream) {
   if (!h || !mu) return set_err(-1, "zb_set_link_friction", hipSuccess);
-  if (h->task != ZB_TASK_STANDUP_V0) return set_err(-1, "zb_set_link_friction: per-link friction is a standup-task state", hipSuccess);
-  zb_su_friction_kernel<<<(h->n * NL + 255) / 256, 256, 0, (hipStream_t)stream>>>(h->n, h->d_state, mu, 0.f);
+  if (h->task != ZB_TASK_STANDUP_V0 && h->task != ZB_TASK_MANAGER_V0)
+    return set_err(-1, "zb_set_link_friction: per-link friction is a standup / manager task state", hipSuccess);
+  zb_su_friction_kernel<<<(h->n * NL + 255) / 256, 256, 0, (hipStream_t)stream>>>(
+      h->n, h->d_state, mu, 0.f, h->task == ZB_TASK_MANAGER_V0 ? ZB_M_LINK_MU : ZB_SU_LINK_MU);
   return launch_check("zb_su_friction_kernel");
 }
 
@@ -3156,7 +3703,8 @@ int zb_read_log(zb_handle h, float* term_means, int32_t* counts, void* stream) {
     HIPCHK(hipMemcpyAsync(term_means, h->d_log_means, sizeof(float) * ZB_LOG_LEN, hipMemcpyDeviceToDevice, s),
            "hipMemcpyAsync log");
   if (counts)
-    HIPCHK(hipMemcpyAsync(counts, h->d_log_counts, sizeof(int32_t) * 2, hipMemcpyDeviceToDevice, s), "hipMemcpyAsync log");
+    HIPCHK(hipMemcpyAsync(counts, h->d_log_counts, sizeof(int32_t) * ZB_LOG_COUNTS, hipMemcpyDeviceToDevice, s),
+           "hipMemcpyAsync log");
   return 0;
 }
 
@@ -3187,7 +3735,7 @@ int zb_physics_substeps(zb_handle h, const float* targets, int nsub, float* net_
                         void* stream) {
   if (!h || !targets || nsub < 1) return set_err(-1, "zb_physics_substeps", hipSuccess);
   const int blocks = (h->n + EPW - 1) / EPW;
-  if (h->task == ZB_TASK_STANDUP_V0)
+  if (h->task == ZB_TASK_STANDUP_V0 || h->task == ZB_TASK_MANAGER_V0)
     zb_substeps_kernel<true><<<blocks, WGT, 0, (hipStream_t)stream>>>(h->d_model, h->d_links, h->cfg, h->n, h->d_state,
                                                                        targets, nsub, net_force, applied_torque);
   else

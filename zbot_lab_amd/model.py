@@ -39,8 +39,8 @@ REWARD_WEIGHTS = {  # v2.py:190-206 ("train reward 2000 step4")
 }
 
 # zbot-6b-standup-v0 (include/zbot.h enum zb_standup_state_field / zb_standup_reward_term)
-TASK_WALKING_V2, TASK_STANDUP_V0, TASK_WALKING_V4 = 0, 1, 2
-MAX_REWARD_TERMS, MAX_STAGES, LOG_LEN = 16, 4, 20
+TASK_WALKING_V2, TASK_STANDUP_V0, TASK_WALKING_V4, TASK_MANAGER_V0 = 0, 1, 2, 3
+MAX_REWARD_TERMS, MAX_STAGES, LOG_LEN, LOG_COUNTS = 16, 4, 20, 4
 SU_OBS_DIM, SU_NUM_TERMS, SU_STATE_DIM = 22, 4, 55
 SU_REWARD_TERMS = ["upward_2", "shape_symmetry", "feet_downward", "feet_downward_4"]  # standup.py:418-427
 SU_REWARD_WEIGHTS = {"upward_2": 10.0, "shape_symmetry": -1.0, "feet_downward": -1.0, "feet_downward_4": 0.0}
@@ -74,6 +74,23 @@ V4 = dict(P_DELTA=25, ACTIONS=31, COMMANDS=37, TARGET_YAW=39, INTERVAL_LEFT=40, 
           FEET_STEP_LEN=47, FEET_F_LAST=49, FEET_FZ_HIST=51, UNDES_FMAX_HIST=57, FEET_AIR_CUR=60,
           FEET_CONTACT_CUR=62, FEET_AIR_LAST=64, FEET_CONTACT_LAST=66, EP_LEN=68, EP_SUMS=69, CURRENT_YAW=84)
 
+# zbot-6b-walking-m-v0, the manager-based flat env (include/zbot.h enum zb_manager_state_field /
+# zb_manager_reward_term); RewardsCfg order after flat_env_cfg.py's overrides (mgr.py:262-357)
+M_OBS_DIM, M_NUM_TERMS, M_STATE_DIM = 25, 11, 88
+M_REWARD_TERMS = [
+    "track_lin_vel_xy_exp", "track_ang_vel_z_exp", "termination_penalty", "dof_torques_l2", "dof_acc_l2",
+    "action_rate_l2", "foot_step_length", "foot_downward", "foot_forward", "feet_slide", "air_time_variance",
+]
+M_REWARD_WEIGHTS = {
+    "track_lin_vel_xy_exp": 1.0, "track_ang_vel_z_exp": 0.5, "termination_penalty": -200.0,
+    "dof_torques_l2": -1.0e-5, "dof_acc_l2": -2.5e-7, "action_rate_l2": -0.01, "foot_step_length": 5.0,
+    "foot_downward": -1.0, "foot_forward": -0.5, "feet_slide": -6.5, "air_time_variance": -15.0,
+}
+M_TERMINATION_TERMS = ["time_out", "base_height", "feet_close"]  # mgr.py:379-398 minus base_contact (flat)
+M = dict(ACTIONS=25, COMMANDS=31, CMD_TIME_LEFT=34, CMD_STANDING=35, FEET_DOWN_POS=36, FEET_STEP_LEN=42,
+         FEET_F_LAST=44, FEET_FZ_HIST=46, FEET_FN_HIST=52, FEET_AIR_CUR=58, FEET_AIR_LAST=60, METRICS=62,
+         EP_LEN=64, EP_SUMS=65, LINK_MU=76)
+
 # state field offsets (include/zbot.h enum zb_state_field)
 S = dict(ROOT_POS=0, ROOT_QUAT=3, ROOT_LINVEL=7, ROOT_ANGVEL=10, JOINT_POS=13, JOINT_VEL=19,
          P_DELTA=25, ACTIONS=31, FEET_DOWN_POS=37, FEET_STEP_LEN=43, FEET_F_LAST=45, HEADING_SUM=47,
@@ -106,6 +123,8 @@ class ZbModel(C.Structure):
         ("kp", C.c_float), ("kd", C.c_float), ("effort_limit", C.c_float),
         ("velocity_limit", C.c_float), ("max_depenetration_velocity", C.c_float),
         ("base_link", C.c_int32), ("foot_links", C.c_int32 * 2), ("undesired_links", C.c_int32 * 10),
+        ("api_root_link", C.c_int32), ("api_root_in_root", C.c_float * 7),
+        ("api_joint_index", C.c_int32 * NUM_DOF), ("api_joint_sign", C.c_float * NUM_DOF),
     ]
 
 
@@ -126,6 +145,9 @@ class ZbTaskCfg(C.Structure):
         ("range_limit_vel", C.c_float * 2), ("range_limit_yaw", C.c_float * 2), ("range_start_steps", C.c_int32),
         ("range_period_steps", C.c_int32), ("range_min_buffer", C.c_int32), ("range_threshold", C.c_float),
         ("range_delta", C.c_float), ("undesired_force_threshold", C.c_float), ("feet_f_last_init", C.c_float),
+        ("action_scale", C.c_float), ("action_clip", C.c_float), ("obs_corruption", C.c_int32),
+        ("obs_noise", C.c_float * 3), ("cmd_resample_s", C.c_float), ("cmd_rel_standing", C.c_float),
+        ("feet_close_min", C.c_float),
     ]
 
 
@@ -428,6 +450,13 @@ def pack_model(rm: RobotModel | None = None) -> ZbModel:
     assert len(undesired) == 10
     for k, i in enumerate(undesired):
         m.undesired_links[k] = i
+    m.api_root_link = rm.api_root_link
+    (px, py, pz), q = rm.api_root_in_root
+    for a, v in enumerate((px, py, pz, *q)):
+        m.api_root_in_root[a] = v
+    for k in range(NUM_DOF):
+        m.api_joint_index[k] = rm.api_joint_index[k]
+        m.api_joint_sign[k] = rm.joint_sign[k]
     return m
 
 
@@ -473,6 +502,15 @@ class TaskCfg:
     range_delta: float = 0.05
     undesired_force_threshold: float = 1.0
     feet_f_last_init: float = 0.0
+    # manager env: RelativeJointPositionAction, observation noise, UniformLevelVelocityCommand
+    action_scale: float = 0.04 * math.pi
+    action_clip: float = 0.04 * math.pi
+    obs_corruption: bool = True
+    obs_noise: tuple = (0.01, 0.01, 1.5)
+    cmd_resample_s: float = 10.0
+    cmd_rel_standing: float = 0.02
+    feet_close_min: float = 0.12
+    range_period_steps: int | None = None   # manager: lin_vel_cmd_levels fires on counter % this == 0
 
     @classmethod
     def standup(cls, curriculum_steps: int | None = None, curriculum: bool = True,
@@ -504,17 +542,34 @@ class TaskCfg:
             c.stages = [(int(ep * L), dict(w), p) for ep, w, p in V4_STAGES]
         return c
 
+    @classmethod
+    def manager_flat(cls, **kw) -> "TaskCfg":
+        """Zbot6BFlatEnvCfg (flat_env_cfg.py:10-111 over rough_env_cfg.py / mgr.py): ZBOT_6S_V2_CFG,
+        20 s episodes, relative joint-position actions, 11 reward terms, terminations time_out /
+        base_height < 0.2 / feet_close < 0.12, x-velocity command ~ U(-0.1, 0.1) widened by
+        lin_vel_cmd_levels up to (-0.3, 0.3), observation noise on."""
+        d = dict(task=TASK_MANAGER_V0, episode_length_s=20.0, termination_height=0.2, terminal_penalty=0.0,
+                 reward_weights=dict(M_REWARD_WEIGHTS),
+                 reset_pose_range=((-0.5, 0.5), (-0.5, 0.5), (0.0, 0.0), (-3.14, 3.14)), reset_pose_body_frame=True,
+                 cmd_vel_range=(-0.1, 0.1), cmd_yaw_range=(0.0, 0.0), range_limit_vel=(-0.3, 0.3),
+                 range_limit_yaw=(0.0, 0.0), range_threshold=0.8, range_delta=0.1)
+        d.update(kw)
+        return cls(**d)
+
     @property
     def obs_dim(self) -> int:
-        return {TASK_STANDUP_V0: SU_OBS_DIM, TASK_WALKING_V4: V4_OBS_DIM}.get(self.task, OBS_DIM)
+        return {TASK_STANDUP_V0: SU_OBS_DIM, TASK_WALKING_V4: V4_OBS_DIM,
+                TASK_MANAGER_V0: M_OBS_DIM}.get(self.task, OBS_DIM)
 
     @property
     def state_dim(self) -> int:
-        return {TASK_STANDUP_V0: SU_STATE_DIM, TASK_WALKING_V4: V4_STATE_DIM}.get(self.task, STATE_DIM)
+        return {TASK_STANDUP_V0: SU_STATE_DIM, TASK_WALKING_V4: V4_STATE_DIM,
+                TASK_MANAGER_V0: M_STATE_DIM}.get(self.task, STATE_DIM)
 
     @property
     def reward_terms(self) -> list:
-        return {TASK_STANDUP_V0: SU_REWARD_TERMS, TASK_WALKING_V4: V4_REWARD_TERMS}.get(self.task, REWARD_TERMS)
+        return {TASK_STANDUP_V0: SU_REWARD_TERMS, TASK_WALKING_V4: V4_REWARD_TERMS,
+                TASK_MANAGER_V0: M_REWARD_TERMS}.get(self.task, REWARD_TERMS)
 
     @property
     def step_dt(self) -> float:
@@ -566,11 +621,21 @@ class TaskCfg:
         c.range_limit_yaw[0], c.range_limit_yaw[1] = self.range_limit_yaw
         c.range_start_steps = self.max_episode_length * self.range_start_episodes
         c.range_period_steps = self.max_episode_length * self.range_period_episodes
+        if self.task == TASK_MANAGER_V0:  # lin_vel_cmd_levels: common_step_counter % max_episode_length
+            c.range_period_steps = self.range_period_steps or self.max_episode_length
         c.range_min_buffer = self.range_min_buffer
         c.range_threshold = self.range_threshold
         c.range_delta = self.range_delta
         c.undesired_force_threshold = self.undesired_force_threshold
         c.feet_f_last_init = self.feet_f_last_init
+        c.action_scale = self.action_scale
+        c.action_clip = self.action_clip
+        c.obs_corruption = int(self.obs_corruption)
+        for k in range(3):
+            c.obs_noise[k] = self.obs_noise[k]
+        c.cmd_resample_s = self.cmd_resample_s
+        c.cmd_rel_standing = self.cmd_rel_standing
+        c.feet_close_min = self.feet_close_min
         c.reset_pose_body_frame = int(self.reset_pose_body_frame)
         c.task = self.task
         for k in range(4):

@@ -34,7 +34,8 @@ class ZbotSim:
         self.obs_dim, self.state_dim = self.cfg.obs_dim, self.cfg.state_dim
         self.num_terms = len(self.cfg.reward_terms)
         if robot is None:
-            robot = zm.standup_model() if self.task == zm.TASK_STANDUP_V0 else zm.load_model()
+            robot = (zm.standup_model() if self.task == zm.TASK_STANDUP_V0
+                     else zm.load_v09_model() if self.task == zm.TASK_MANAGER_V0 else zm.load_model())
         self.robot = robot
         self._m = zm.pack_model(self.robot)
         self._c = self.cfg.pack()
@@ -51,7 +52,7 @@ class ZbotSim:
         self.terminated = torch.zeros(self.num_envs, dtype=torch.bool, device=self.device)
         self.truncated = torch.zeros(self.num_envs, dtype=torch.bool, device=self.device)
         self._log_means = torch.zeros(zm.LOG_LEN, dtype=torch.float32, device=self.device)  # include/zbot.h ZB_LOG_LEN
-        self._log_counts = torch.zeros(2, dtype=torch.int32, device=self.device)
+        self._log_counts = torch.zeros(zm.LOG_COUNTS, dtype=torch.int32, device=self.device)  # ZB_LOG_COUNTS
         # the library fills these in stream order at every step/reset with resets (no copies)
         nat.check(self.lib.zb_set_log_buffers(self._h, nat.ptr(self._log_means), nat.ptr(self._log_counts)),
                   "zb_set_log_buffers")
@@ -99,7 +100,7 @@ class ZbotSim:
         return obs
 
     def read_log(self):
-        """(term_means[num_terms], counts[2]) device tensors of the most recent step that had resets
+        """(term_means[num_terms], counts[ZB_LOG_COUNTS]) device tensors of the most recent step that had resets
         (registered with zb_set_log_buffers, so no per-step copy)."""
         return self._log_means[:self.num_terms], self._log_counts
 
@@ -109,7 +110,7 @@ class ZbotSim:
         return self._log_means
 
     def set_link_friction(self, mu: torch.Tensor) -> None:
-        """Standup: per-link friction coefficients [N, 12] (randomize_rigid_body_material)."""
+        """Standup / manager: per-link friction coefficients [N, 12] (randomize_rigid_body_material)."""
         m = mu.to(device=self.device, dtype=torch.float32).contiguous()
         if m.shape != (self.num_envs, zm.NUM_LINKS):
             raise ValueError(f"friction must be [{self.num_envs}, {zm.NUM_LINKS}]")
