@@ -16,6 +16,9 @@ OpenMP over envs) on this host's cores, on a bounded sample.
 
 ``--task v4`` measures zbot-6b-walking-v4 (commands / events / curricula; ``zb_v4_step_kernel``, 790 B
 per env-step: 81 state rows read, 85 written, actions, obs 96 B, reward, flags) at 4096 envs.
+``--task manager`` measures zbot-6b-walking-m-v0 (the manager-based flat env on ZBOT_6S_V2_CFG;
+``zb_m_step_kernel``, 738 B per env-step: 76 state rows read + written, actions 24 B, obs 100 B,
+reward, flags) at 4096 envs with the startup friction randomisation.
 ``--task standup`` measures the stand-up task instead (zbot-6b-standup-v0,
 32768 envs, friction randomisation on; kernel ``zb_su_step_kernel``, 510 B per env-step: 43 fp32
 state rows read + written, 12 friction coefficients read, actions 24 B, obs 88 B, reward, flags).
@@ -34,6 +37,7 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 BYTES_PER_ENV_STEP = 794
 SU_BYTES_PER_ENV_STEP = 2 * 43 * 4 + 12 * 4 + 24 + 88 + 4 + 2  # = 510, stand-up task
 V4_BYTES_PER_ENV_STEP = 81 * 4 + 85 * 4 + 24 + 96 + 4 + 2       # = 790, walking v4
+M_BYTES_PER_ENV_STEP = 76 * 4 + 76 * 4 + 24 + 100 + 4 + 2       # = 738, manager flat env
 
 
 def parse():
@@ -41,7 +45,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=500)
     p.add_argument("--warmup", type=int, default=50)
-    p.add_argument("--task", choices=("walking", "standup", "v4"), default="walking")
+    p.add_argument("--task", choices=("walking", "standup", "v4", "manager"), default="walking")
     p.add_argument("--envs-per-gpu", type=int, default=None, help="default 4096 (walking) / 32768 (standup, C5)")
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -83,7 +87,8 @@ def cpu_baseline(num_envs: int, seconds: float, task: str = "walking") -> dict:
     from oracle.pyoracle import OracleSim
     from zbot_lab_amd import model as zm
     threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
-    cfg = {"standup": zm.TaskCfg.standup, "v4": zm.TaskCfg.walking_v4}.get(task, zm.TaskCfg)()
+    cfg = {"standup": zm.TaskCfg.standup, "v4": zm.TaskCfg.walking_v4,
+           "manager": zm.TaskCfg.manager_flat}.get(task, zm.TaskCfg)()
     sim = OracleSim(num_envs, cfg, threads=threads, seed=0)
     sim.reset()
     rng = np.random.default_rng(42)
@@ -113,11 +118,13 @@ def main():
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
 
-    from zbot_lab_amd.envs import (Zbot6SEnvV4, Zbot6SEnvV4Cfg, Zbot6SUpEnv, Zbot6SUpEnvCfg, ZbotDirectEnvCfgV2,
-                                   ZbotDirectEnvV2)
+    from zbot_lab_amd.envs import (Zbot6BFlatEnvCfg, Zbot6SEnvV4, Zbot6SEnvV4Cfg, Zbot6SUpEnv, Zbot6SUpEnvCfg,
+                                   ZbotDirectEnvCfgV2, ZbotDirectEnvV2, ZbotManagerBasedRLEnv)
     standup = args.task == "standup"
     v4 = args.task == "v4"
-    cfg = Zbot6SUpEnvCfg() if standup else Zbot6SEnvV4Cfg() if v4 else ZbotDirectEnvCfgV2()
+    mgr = args.task == "manager"
+    cfg = (Zbot6SUpEnvCfg() if standup else Zbot6SEnvV4Cfg() if v4 else Zbot6BFlatEnvCfg() if mgr
+           else ZbotDirectEnvCfgV2())
     cfg.scene.num_envs = args.envs_per_gpu or (32768 if standup else 4096)
     cfg.sim.device = str(dev)
     cfg.seed = 42 + rank
@@ -125,7 +132,8 @@ def main():
         cfg.solver.iterations = args.solver_iterations
     if args.no_self_collision:
         cfg.solver.self_collision = False
-    env = Zbot6SUpEnv(cfg) if standup else Zbot6SEnvV4(cfg) if v4 else ZbotDirectEnvV2(cfg)
+    env = (Zbot6SUpEnv(cfg) if standup else Zbot6SEnvV4(cfg) if v4 else ZbotManagerBasedRLEnv(cfg) if mgr
+           else ZbotDirectEnvV2(cfg))
     n = env.num_envs
     env.reset()
     gen = torch.Generator(device=dev)
@@ -159,13 +167,17 @@ def main():
 
     if rank == 0:
         kern_s = kern_ms / 1e3 / max(kern_n, 1)
-        kname = "zb_su_step_kernel" if standup else "zb_v4_step_kernel" if v4 else "zb_step_kernel"
-        bpe = SU_BYTES_PER_ENV_STEP if standup else V4_BYTES_PER_ENV_STEP if v4 else BYTES_PER_ENV_STEP
+        kname = ("zb_su_step_kernel" if standup else "zb_v4_step_kernel" if v4 else "zb_m_step_kernel" if mgr
+                 else "zb_step_kernel")
+        bpe = (SU_BYTES_PER_ENV_STEP if standup else V4_BYTES_PER_ENV_STEP if v4 else M_BYTES_PER_ENV_STEP if mgr
+               else BYTES_PER_ENV_STEP)
         traffic, traffic_src = pmc_traffic(n, kname)
         achieved = n * bpe / kern_s / 1e9
         workload = (f"zbot-6b-standup-v0 (C5), {n} envs/GPU x {world} GPU, friction DR, random-action throughput"
                     if standup else f"zbot-6b-walking-v4, {n} envs/GPU x {world} GPU, commands + curricula, "
                     "random-action throughput" if v4 else
+                    f"zbot-6b-walking-m-v0 (ManagerBasedRLEnv flat), {n} envs/GPU x {world} GPU, friction DR, "
+                    "random-action throughput" if mgr else
                     f"zbot-6b-walking-v2, {n} envs/GPU x {world} GPU, random-action throughput")
         out = {
             "metric": "env-steps/sec at 4096/65536 envs, 1->8 GPUs; % HBM roofline",

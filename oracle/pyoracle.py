@@ -62,6 +62,10 @@ def _load(double: bool = False):
     lib.zbo_v4_commands_from_draws.argtypes = [C.c_int, _f, _f, _f, _f, _f, _f, _f]
     lib.zbo_curriculum_probe.argtypes = [C.POINTER(zm.ZbTaskCfg), C.c_int64, C.c_int, C.c_int, C.c_int, C.c_float,
                                          C.c_float, _f]
+    lib.zbo_m_mdp_eval.argtypes = [C.c_int, C.POINTER(zm.ZbTaskCfg)] + [_f] * 11 + [_i, _f, _f, _f, _f, _f, _f, _f,
+                                                                                _f, _f, _u8, _u8, _u8]
+    lib.zbo_m_curriculum_probe.argtypes = [C.POINTER(zm.ZbTaskCfg), C.c_int64, C.c_float, _f]
+    lib.zbo_m_process_actions.argtypes = [C.c_int, C.POINTER(zm.ZbTaskCfg), C.POINTER(zm.ZbModel), _f, _f, _f, _f]
     return lib
 
 
@@ -248,3 +252,48 @@ def curriculum_probe(cfg: zm.TaskCfg, steps: int, io, run_my=True, run_range=Tru
     lib().zbo_curriculum_probe(C.byref(c), int(steps), int(run_my), int(run_range), int(ring_n), float(ring_vel),
                                float(ring_yaw), v)
     return v
+
+
+FEET = [0, 11]  # feet rows of the golden frames' 12-body layout (tools/gen_manager_goldens.py)
+
+
+def m_mdp_eval(cfg: zm.TaskCfg, frame: dict, ep_len, act, prev_act, commands, state: dict):
+    """Manager flat terminations + rewards on Isaac-Lab-shaped frame data (zbo_m_mdp_eval). ``state``
+    holds feet_down_pos [n,2,3], feet_step_len [n,2], feet_f_last [n,2], ep_sums [n,11] (updated
+    copies returned)."""
+    n = len(ep_len)
+    c = cfg.pack()
+    st = {k: f32(v).copy() for k, v in state.items()}
+    out = dict(reward=np.zeros(n, np.float32), terms=np.zeros((n, zm.M_NUM_TERMS), np.float32),
+               low=np.zeros(n, np.uint8), close=np.zeros(n, np.uint8), time_out=np.zeros(n, np.uint8))
+    lib().zbo_m_mdp_eval(n, C.byref(c), f32(frame["root_pos_w"]), f32(frame["root_quat_w"]),
+                         f32(frame["root_link_lin_vel_w"]), f32(frame["root_link_ang_vel_w"]),
+                         f32(frame["body_link_pos_w"][:, FEET]), f32(frame["body_link_quat_w"][:, FEET]),
+                         f32(frame["body_lin_vel_w"][:, FEET]), f32(frame["net_forces_w_history"][:, :, FEET]),
+                         f32(frame["last_air_time"][:, FEET]), f32(frame["applied_torque"]), f32(frame["joint_acc"]),
+                         np.ascontiguousarray(ep_len, np.int32), f32(act), f32(prev_act), f32(commands),
+                         st["feet_down_pos"], st["feet_step_len"], st["feet_f_last"], st["ep_sums"],
+                         out["reward"], out["terms"], out["low"], out["close"], out["time_out"])
+    for k in ("low", "close", "time_out"):
+        out[k] = out[k].astype(bool)
+    out.update(st)
+    return out
+
+
+def m_curriculum_probe(cfg: zm.TaskCfg, steps: int, reward: float, ranges):
+    """lin_vel_cmd_levels on ranges [x lo, x hi, y lo, y hi]; returns (fired, new ranges)."""
+    c = cfg.pack()
+    io = f32(ranges).copy()
+    fired = lib().zbo_m_curriculum_probe(C.byref(c), int(steps), float(reward), io)
+    return bool(fired), io
+
+
+def m_process_actions(cfg: zm.TaskCfg, actions, jq):
+    """RelativeJointPositionAction: (processed actions [n,6] Isaac Lab order, chain targets q + delta)."""
+    c = cfg.pack()
+    m = zm.pack_model(zm.load_v09_model())
+    a = f32(actions)
+    proc = np.zeros_like(a)
+    tg = np.zeros_like(a)
+    lib().zbo_m_process_actions(len(a), C.byref(c), C.byref(m), a, f32(jq), proc, tg)
+    return proc, tg

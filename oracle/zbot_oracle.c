@@ -1879,6 +1879,18 @@ static void m_unpack_env(env_t* e, const float* st, int n, int i) {
 #undef GET
 }
 
+/* lin_vel_cmd_levels (curriculums.py:57-83) on the mean episodic tracking reward / 20 s of the reset
+ * envs; vel = ranges.lin_vel_x, yaw = ranges.lin_vel_y. Returns 1 when it widened the ranges. */
+static int m_lin_vel_cmd_levels(const zb_task_cfg* c, uint64_t steps, float reward, float vel[2], float yaw[2]) {
+  if (c->range_period_steps <= 0 || steps % (uint64_t)c->range_period_steps != 0) return 0;
+  if (!(reward > c->stage_scales[0][ZB_M_R_TRACK_LIN_VEL_XY] * c->range_threshold)) return 0;
+  vel[0] = (float)clampr(vel[0] - c->range_delta, c->range_limit_vel[0], c->range_limit_vel[1]);
+  vel[1] = (float)clampr(vel[1] + c->range_delta, c->range_limit_vel[0], c->range_limit_vel[1]);
+  yaw[0] = (float)clampr(yaw[0] - c->range_delta, c->range_limit_yaw[0], c->range_limit_yaw[1]);
+  yaw[1] = (float)clampr(yaw[1] + c->range_delta, c->range_limit_yaw[0], c->range_limit_yaw[1]);
+  return 1;
+}
+
 /* ========================================================================= call epilogue
  * Mirror of the kernel's zb_finalize_kernel: episode log (means over reset envs; walking divides
  * by the 20 s episode, the other tasks already divided per env), curriculum log entries (pre-event
@@ -1900,14 +1912,7 @@ static void finish_call(zbo_sim* s, int nres, const double* acc, double ep_s, in
       /* lin_vel_cmd_levels (curriculums.py:57-83), first in _reset_idx: on calls where
        * common_step_counter % max_episode_length == 0, widen the x / y ranges by +-0.1 (clamped to
        * limit_ranges) when mean(episode sums of track_lin_vel_xy_exp) / 20 s > 0.8 x weight */
-      if (c->range_period_steps > 0 && s->steps % (uint64_t)c->range_period_steps == 0 &&
-          v[ZB_M_R_TRACK_LIN_VEL_XY] > c->stage_scales[0][ZB_M_R_TRACK_LIN_VEL_XY] * c->range_threshold) {
-        s->vel[0] = (float)clampr(s->vel[0] - c->range_delta, c->range_limit_vel[0], c->range_limit_vel[1]);
-        s->vel[1] = (float)clampr(s->vel[1] + c->range_delta, c->range_limit_vel[0], c->range_limit_vel[1]);
-        s->yaw[0] = (float)clampr(s->yaw[0] - c->range_delta, c->range_limit_yaw[0], c->range_limit_yaw[1]);
-        s->yaw[1] = (float)clampr(s->yaw[1] + c->range_delta, c->range_limit_yaw[0], c->range_limit_yaw[1]);
-        s->changed = 1;
-      }
+      s->changed = m_lin_vel_cmd_levels(c, s->steps, v[ZB_M_R_TRACK_LIN_VEL_XY], s->vel, s->yaw);
       v[16] = s->vel[1];                       /* Curriculum/lin_vel_cmd_levels */
       v[17] = (float)(s->met_acc[0] / nres);   /* Metrics/base_velocity/error_vel_xy */
       v[18] = (float)(s->met_acc[1] / nres);   /* Metrics/base_velocity/error_vel_yaw */
@@ -2645,5 +2650,96 @@ int zbo_curriculum_probe(const zb_task_cfg* cfg, int64_t steps, int run_my, int 
   curriculum_events(&s, run_my, run_range);
   io[0] = (float)s.stage; io[1] = s.prob_pos;
   io[2] = s.vel[0]; io[3] = s.vel[1]; io[4] = s.yaw[0]; io[5] = s.yaw[1];
+  return 0;
+}
+
+/* manager flat MDP (terminations + rewards) on Isaac-Lab-shaped inputs, per env:
+ * base_pos[3], base_quat[4], base_lin_vel[3] (root_link_lin_vel_w), base_ang_vel[3]
+ * (root_link_ang_vel_w), feet_pos[2][3], feet_quat[2][4], feet_vel[2][3] (body_lin_vel_w),
+ * net_forces_w_history of the feet [3][2][3], last_air_time[2], applied_torque[6], joint_acc[6],
+ * ep_len, actions / prev actions [6]; state in/out: commands[3], feet_down_pos[2][3],
+ * feet_step_len[2], feet_f_last[2], ep_sums[11]; out: reward, terms[11], low, close, time_out */
+int zbo_m_mdp_eval(int n, const zb_task_cfg* cfg, const float* base_pos, const float* base_quat, const float* base_lin_vel,
+                   const float* base_ang_vel, const float* feet_pos, const float* feet_quat, const float* feet_vel,
+                   const float* hist, const float* air_last, const float* applied_torque, const float* joint_acc,
+                   const int32_t* ep_len, const float* act, const float* prev, const float* commands,
+                   float* feet_down_pos, float* feet_step_len, float* feet_f_last, float* ep_sums, float* reward,
+                   float* terms, uint8_t* low, uint8_t* close, uint8_t* tout) {
+  for (int e = 0; e < n; ++e) {
+    m_post_t P;
+    mdp_t md;
+    memset(&md, 0, sizeof(md));
+    for (int a = 0; a < 3; ++a) {
+      P.base_pos[a] = base_pos[3 * e + a];
+      P.base_lin_vel[a] = base_lin_vel[3 * e + a];
+      P.base_ang_vel[a] = base_ang_vel[3 * e + a];
+      md.commands[a] = commands[3 * e + a];
+    }
+    for (int a = 0; a < 4; ++a) P.base_quat[a] = base_quat[4 * e + a];
+    for (int f = 0; f < 2; ++f) {
+      for (int a = 0; a < 3; ++a) {
+        P.feet_pos[f][a] = feet_pos[6 * e + 3 * f + a];
+        P.feet_vel[f][a] = feet_vel[6 * e + 3 * f + a];
+        md.feet_down_pos[f][a] = feet_down_pos[6 * e + 3 * f + a];
+      }
+      for (int a = 0; a < 4; ++a) P.feet_quat[f][a] = feet_quat[8 * e + 4 * f + a];
+      for (int h = 0; h < 3; ++h) {
+        const float* F = hist + (size_t)e * 18 + h * 6 + f * 3;
+        P.fz_hist[h][f] = F[2];
+        P.fn_hist[h][f] = sqrtr((real)F[0] * F[0] + (real)F[1] * F[1] + (real)F[2] * F[2]);
+      }
+      P.air_last[f] = air_last[2 * e + f];
+      md.feet_step_len[f] = feet_step_len[2 * e + f];
+      md.feet_f_last[f] = feet_f_last[2 * e + f];
+    }
+    real a6[ND], p6[ND];
+    for (int j = 0; j < ND; ++j) {
+      P.applied_torque[j] = applied_torque[6 * e + j];
+      P.joint_acc[j] = joint_acc[6 * e + j];
+      a6[j] = act[6 * e + j];
+      p6[j] = prev[6 * e + j];
+    }
+    P.ep_len = ep_len[e];
+    for (int t = 0; t < ZB_M_NUM_REWARD_TERMS; ++t) md.ep_sums[t] = ep_sums[ZB_M_NUM_REWARD_TERMS * e + t];
+    real tm[ZB_M_NUM_REWARD_TERMS];
+    int lo = 0, cl = 0, to = 0;
+    reward[e] = (float)m_mdp_eval(cfg, &P, &md, a6, p6, tm, &lo, &cl, &to);
+    for (int t = 0; t < ZB_M_NUM_REWARD_TERMS; ++t) {
+      terms[ZB_M_NUM_REWARD_TERMS * e + t] = (float)tm[t];
+      ep_sums[ZB_M_NUM_REWARD_TERMS * e + t] = (float)md.ep_sums[t];
+    }
+    for (int f = 0; f < 2; ++f) {
+      for (int a = 0; a < 3; ++a) feet_down_pos[6 * e + 3 * f + a] = (float)md.feet_down_pos[f][a];
+      feet_step_len[2 * e + f] = (float)md.feet_step_len[f];
+      feet_f_last[2 * e + f] = (float)md.feet_f_last[f];
+    }
+    low[e] = (uint8_t)lo;
+    close[e] = (uint8_t)cl;
+    tout[e] = (uint8_t)to;
+  }
+  return 0;
+}
+
+/* lin_vel_cmd_levels on io = [x lo, x hi, y lo, y hi] (in/out); returns 1 if it fired */
+int zbo_m_curriculum_probe(const zb_task_cfg* cfg, int64_t steps, float reward, float* io) {
+  float vel[2] = {io[0], io[1]}, yaw[2] = {io[2], io[3]};
+  const int r = m_lin_vel_cmd_levels(cfg, (uint64_t)steps, reward, vel, yaw);
+  io[0] = vel[0]; io[1] = vel[1]; io[2] = yaw[0]; io[3] = yaw[1];
+  return r;
+}
+
+/* RelativeJointPositionAction: raw actions [n][6] (Isaac Lab joint order) -> processed actions
+ * (scale, clip) in the Isaac Lab order and the per-substep targets q + delta of the chain joints */
+int zbo_m_process_actions(int n, const zb_task_cfg* cfg, const zb_model* model, const float* actions, const float* jq,
+                          float* processed, float* targets) {
+  mdl_t m;
+  load_mdl(model, &m);
+  for (int e = 0; e < n; ++e) {
+    for (int a = 0; a < ND; ++a)
+      processed[6 * e + a] = (float)clampr((real)actions[6 * e + a] * (real)cfg->action_scale, -(real)cfg->action_clip,
+                                           (real)cfg->action_clip);
+    for (int j = 0; j < ND; ++j)
+      targets[6 * e + j] = (float)((real)jq[6 * e + j] + m.api_sign[j] * (real)processed[6 * e + m.api_index[j]]);
+  }
   return 0;
 }

@@ -115,6 +115,40 @@ def test_walking_v4_registration_and_cfg():
     assert agent.to_dict()["policy"]["critic_hidden_dims"] == [256, 256, 128]
 
 
+def test_manager_registration_and_cfg():
+    """zbot-6b-walking-m-v0 / -m-play-v0 (zbotlab_manager/config/zbot6b_manager/__init__.py:18-36):
+    the manager cfg compiles to TaskCfg.manager_flat(); unsupported terms raise instead of being
+    dropped; Zbot6BFlatPPORunnerCfg (agents/rsl_rl_ppo_cfg.py:40-49)."""
+    import dataclasses
+    from zbot_lab_amd import model as zm
+    from zbot_lab_amd.envs.manager_flat import DoneTerm, EventTerm, RewTerm
+    assert {"zbot-6b-walking-m-v0", "zbot-6b-walking-m-play-v0"} <= set(zbot_lab_amd.tasks.registered())
+    cfg = zbot_lab_amd.tasks.load_cfg("zbot-6b-walking-m-v0")
+    assert dataclasses.asdict(cfg.task_cfg()) == dataclasses.asdict(zm.TaskCfg.manager_flat())
+    cfg.rewards.feet_slide.weight = -3.0
+    cfg.commands.base_velocity.ranges.lin_vel_x = (-0.2, 0.2)
+    t = cfg.task_cfg()
+    assert t.reward_weights["feet_slide"] == -3.0 and t.cmd_vel_range == (-0.2, 0.2)
+    play = zbot_lab_amd.tasks.load_cfg("zbot-6b-walking-m-play-v0")
+    assert play.scene.num_envs == 64 and not play.task_cfg().obs_corruption
+    assert play.task_cfg().cmd_vel_range == (-0.3, 0.3)
+    for edit in (lambda c: setattr(c.rewards, "gait", RewTerm("feet_gait", 0.5)),
+                 lambda c: setattr(c.terminations, "base_contact", DoneTerm("illegal_contact")),
+                 lambda c: setattr(c.events, "push_robot", EventTerm("push_by_setting_velocity", "interval")),
+                 lambda c: setattr(c.rewards.track_lin_vel_xy_exp, "params", {"std": 0.4}),
+                 lambda c: setattr(c.commands.base_velocity, "heading_command", True)):
+        c = zbot_lab_amd.tasks.load_cfg("zbot-6b-walking-m-v0")
+        edit(c)
+        with pytest.raises(NotImplementedError):
+            c.task_cfg()
+    c = zbot_lab_amd.tasks.load_cfg("zbot-6b-walking-m-v0")
+    c.curriculum.lin_vel_cmd_levels = None
+    assert c.task_cfg().pack().range_period_steps <= 0
+    ppo = zbot_lab_amd.tasks.load_cfg("zbot-6b-walking-m-v0", "rsl_rl_cfg_entry_point").to_dict()
+    assert ppo["max_iterations"] == 1000 and ppo["experiment_name"] == "zbot_6b_flat_mana_v1"
+    assert ppo["policy"]["actor_hidden_dims"] == [128, 128, 128] and ppo["algorithm"]["entropy_coef"] == 0.01
+
+
 def test_vecenv_wrapper_contract():
     env = FakeEnv()
     w = RslRlVecEnvWrapper(env, clip_actions=1.0)

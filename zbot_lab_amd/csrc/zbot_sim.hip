@@ -2874,10 +2874,14 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_m_step_kernel(
   float fz_h[3][2], fn_h[3][2];
   float air_cur[2] = {ST(ZB_M_FEET_AIR_CUR), ST(ZB_M_FEET_AIR_CUR + 1)};
   float air_last[2] = {ST(ZB_M_FEET_AIR_LAST), ST(ZB_M_FEET_AIR_LAST + 1)};
+  const bool hist_in = cfg.decimation < 3;  // >= 3 substeps overwrite every slot: no read
 #pragma unroll
   for (int h = 0; h < 3; ++h)
 #pragma unroll
-    for (int f = 0; f < 2; ++f) { fz_h[h][f] = ST(ZB_M_FEET_FZ_HIST + 2 * h + f); fn_h[h][f] = ST(ZB_M_FEET_FN_HIST + 2 * h + f); }
+    for (int f = 0; f < 2; ++f) {
+      fz_h[h][f] = hist_in ? ST(ZB_M_FEET_FZ_HIST + 2 * h + f) : 0.f;
+      fn_h[h][f] = hist_in ? ST(ZB_M_FEET_FN_HIST + 2 * h + f) : 0.f;
+    }
   sp.mark(0);
   for (int k = 0; k < cfg.decimation; ++k) {
     float target[ND];

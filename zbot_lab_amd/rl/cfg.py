@@ -1,5 +1,6 @@
 """``PPORunnerCfgV2`` (reference ``source/zbot/zbot/tasks/zbot6b_direct/agents/rsl_rl_ppo_cfg.py:65-91``) and
-``Zbot6SUpEnvPPOCfg`` (same file, 264-289), ``Zbot6SEnvV4PPOCfg`` (206-233).
+``Zbot6SUpEnvPPOCfg`` (same file, 264-289), ``Zbot6SEnvV4PPOCfg`` (206-233) and the manager env's
+``Zbot6BFlatPPORunnerCfg`` (``zbotlab_manager/config/zbot6b_manager/agents/rsl_rl_ppo_cfg.py:11-49``).
 
 Consumed by ``zbot_lab_amd.rl.OnPolicyRunner`` (``agent_cfg.to_dict()``, as ``train.py:192``)."""
 from __future__ import annotations
@@ -14,6 +15,8 @@ class RslRlPpoActorCriticCfg:
     actor_hidden_dims: list = field(default_factory=lambda: [128, 128, 128])
     critic_hidden_dims: list = field(default_factory=lambda: [128, 128, 128])
     activation: str = "elu"
+    actor_obs_normalization: bool = False
+    critic_obs_normalization: bool = False
 
 
 @dataclass
@@ -67,3 +70,13 @@ class Zbot6SEnvV4PPOCfg(PPORunnerCfgV2):
     experiment_name: str = "zbot_6b_flat_direct_v4"
     policy: RslRlPpoActorCriticCfg = field(default_factory=lambda: RslRlPpoActorCriticCfg(
         actor_hidden_dims=[256, 256, 128], critic_hidden_dims=[256, 256, 128]))
+
+
+@dataclass
+class Zbot6BFlatPPORunnerCfg(PPORunnerCfgV2):
+    """zbotlab_manager agents/rsl_rl_ppo_cfg.py:11-49: Zbot6BRoughPPORunnerCfg (entropy 0.01, 24 steps)
+    with the flat overrides (1000 iterations, [128, 128, 128] actor / critic)."""
+    max_iterations: int = 1000
+    save_interval: int = 100
+    experiment_name: str = "zbot_6b_flat_mana_v1"
+    algorithm: RslRlPpoAlgorithmCfg = field(default_factory=lambda: RslRlPpoAlgorithmCfg(entropy_coef=0.01))

@@ -45,6 +45,9 @@ class OnPolicyRunner:
         num_obs = obs.shape[1]
         self.alg_cfg.pop("class_name", None)
         self.policy_cfg.pop("class_name", None)
+        for k in ("actor_obs_normalization", "critic_obs_normalization"):
+            if self.policy_cfg.pop(k, False):
+                raise NotImplementedError(f"{k}=True (rsl_rl EmpiricalNormalization) is not implemented")
         policy = ActorCritic(num_obs, num_obs, self.env.num_actions, **self.policy_cfg).to(self.device)
         self.alg = PPO(policy, device=self.device, multi_gpu_cfg=self.multi_gpu_cfg, **self.alg_cfg)
         self.num_steps_per_env = int(train_cfg["num_steps_per_env"])

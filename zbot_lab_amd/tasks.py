@@ -1,6 +1,8 @@
 """Task registry: ``make("zbot-6b-walking-v2")`` like ``gym.make`` on the reference's registration
 (``source/zbot/zbot/tasks/zbot6b_direct/__init__.py:41-49``; ``zbot-6b-standup-v0`` 111-119;
-``zbot-6b-walking-v4`` 91-99)."""
+``zbot-6b-walking-v4`` 91-99; ``zbot-6b-walking-m-v0`` / ``-m-play-v0``:
+``zbotlab_manager/config/zbot6b_manager/__init__.py:18-36``; the rough variants need the terrain
+generator and are out of scope)."""
 from __future__ import annotations
 
 import importlib
@@ -75,5 +77,23 @@ register(
     kwargs={
         "env_cfg_entry_point": "zbot_lab_amd.envs.walking_v4:Zbot6SEnvV4Cfg",
         "rsl_rl_cfg_entry_point": "zbot_lab_amd.rl.cfg:Zbot6SEnvV4PPOCfg",
+    },
+)
+
+register(
+    id="zbot-6b-walking-m-v0",
+    entry_point="zbot_lab_amd.envs.manager_flat:ZbotManagerBasedRLEnv",
+    kwargs={
+        "env_cfg_entry_point": "zbot_lab_amd.envs.manager_flat:Zbot6BFlatEnvCfg",
+        "rsl_rl_cfg_entry_point": "zbot_lab_amd.rl.cfg:Zbot6BFlatPPORunnerCfg",
+    },
+)
+
+register(
+    id="zbot-6b-walking-m-play-v0",
+    entry_point="zbot_lab_amd.envs.manager_flat:ZbotManagerBasedRLEnv",
+    kwargs={
+        "env_cfg_entry_point": "zbot_lab_amd.envs.manager_flat:Zbot6BFlatEnvCfg_PLAY",
+        "rsl_rl_cfg_entry_point": "zbot_lab_amd.rl.cfg:Zbot6BFlatPPORunnerCfg",
     },
 )
