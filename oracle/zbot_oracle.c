@@ -892,8 +892,9 @@ static real mdp_eval(const zb_task_cfg* cfg, const real jq0[ND], const obs_cache
   return rew;
 }
 
-/* ContactSensor lazy update once per policy step: history roll, air/contact
- * timers with elapsed = step_dt, is_contact = |F| > threshold. */
+/* ContactSensor.update after every physics step (history_length > 0 makes Isaac Lab's
+ * SensorBase.update refresh the buffers each scene.update(physics_dt)): history roll, air/contact
+ * timers with elapsed = sim_dt, is_contact = |F| > threshold. */
 static void sensor_update(const mdl_t* m, const zb_task_cfg* cfg, mdp_t* md, const real F[NL][3]) {
   for (int h = ZB_HIST - 1; h > 0; --h) {
     md->feet_fz_hist[h][0] = md->feet_fz_hist[h - 1][0];
@@ -907,7 +908,7 @@ static void sensor_update(const mdl_t* m, const zb_task_cfg* cfg, mdp_t* md, con
     if (nrm > fmax) fmax = nrm;
   }
   md->undes_fmax_hist[0] = fmax;
-  const real el = cfg->sim_dt * (real)cfg->decimation;
+  const real el = cfg->sim_dt;
   for (int f = 0; f < 2; ++f) {
     const real* Ff = F[m->foot_links[f]];
     md->feet_fz_hist[0][f] = Ff[2];
@@ -1351,7 +1352,7 @@ static void v4_sensor_update(const mdl_t* m, const zb_task_cfg* cfg, mdp_t* md, 
     if (nrm > fmax) fmax = nrm;
   }
   md->undes_fmax_hist[0] = fmax;
-  const real el = cfg->sim_dt * (real)cfg->decimation;
+  const real el = cfg->sim_dt; /* updated every physics step, like sensor_update */
   for (int f = 0; f < 2; ++f) {
     const real* Ff = F[m->foot_links[f]];
     md->feet_fz_hist[0][f] = Ff[2];
@@ -1424,8 +1425,8 @@ static real v4_step_env(const zbo_sim* s, int stage, uint64_t ctr, int i, env_t*
     if (k == cfg->decimation - 1)
       for (int j = 0; j < ND; ++j) jqd_prev[j] = e->ph.jqd[j];
     substep(m, cfg, &e->ph, target, NULL, &so);
+    v4_sensor_update(m, cfg, md, so.net_force);
   }
-  v4_sensor_update(m, cfg, md, so.net_force);
   md->ep_len += 1;
   v4_post_t P;
   {
@@ -2079,8 +2080,10 @@ static real step_env(const mdl_t* m, const zb_task_cfg* cfg, env_t* e, const flo
   cache_from_phys(m, &e->ph, &pre);
   /* physics */
   substep_out_t so;
-  for (int k = 0; k < cfg->decimation; ++k) substep(m, cfg, &e->ph, target, NULL, &so);
-  sensor_update(m, cfg, md, so.net_force);
+  for (int k = 0; k < cfg->decimation; ++k) {
+    substep(m, cfg, &e->ph, target, NULL, &so);
+    sensor_update(m, cfg, md, so.net_force);
+  }
   md->ep_len += 1;
   /* post-step reads */
   post_t ps;

@@ -488,6 +488,7 @@ constexpr int NCAND = NL * 4 + NSELF;
 //   LNK   [LNK4]            link table copy
 //   PRE   [EPW][PRE4]       prologue results parked across the physics
 //   FRIC  [EPW][NL] f32     per-link friction coefficients (standup)
+//   SENS  [EPW][MAXSUB][2]  per-substep contact-sensor record {fz0, fz1, |F0|, |F1|}, {undesired max |F|}
 constexpr int YG_OFF = 0;
 constexpr int AUX_OFF = YG_OFF + NCM * WGT;
 constexpr int LAM_OFF = AUX_OFF + NCM * 2 * EPW;
@@ -502,7 +503,9 @@ constexpr int LNK_OFF = UB_OFF + NL * EPW;
 constexpr int PRE_OFF = LNK_OFF + LNK4;  // [EPW] Pre records (prologue -> MDP)
 constexpr int PRE4 = 8;                   // float4 per Pre record (30 floats)
 constexpr int FRIC_OFF = PRE_OFF + EPW * PRE4;  // [EPW][NL] f32 per-link friction (standup)
-constexpr int LDS4 = FRIC_OFF + (EPW * NL + 3) / 4;
+constexpr int MAXSUB = 8;                 // decimation limit (zb_create checks)
+constexpr int SENS_OFF = FRIC_OFF + (EPW * NL + 3) / 4;
+constexpr int LDS4 = SENS_OFF + EPW * MAXSUB * 2;
 
 // prologue results the MDP reads after the physics (parked in LDS across the substeps)
 struct Pre {
@@ -534,6 +537,7 @@ struct Q {
   __device__ __forceinline__ const float4* dflt() const { return b + LNK_OFF + DFLT_OFF; }
   __device__ __forceinline__ Pre& pre() const { return *reinterpret_cast<Pre*>(b + PRE_OFF + e * PRE4); }
   __device__ __forceinline__ float& fric(int l) const { return reinterpret_cast<float*>(b + FRIC_OFF)[e * NL + l]; }
+  __device__ __forceinline__ float4& sens(int k, int h) const { return b[SENS_OFF + (e * MAXSUB + k) * 2 + h]; }
 };
 
 __device__ __forceinline__ void read_frame(const Q& q, int body, float R[9], float p[3]) {
@@ -704,6 +708,12 @@ __device__ __forceinline__ void read_joints(const Q& q, float S[ND][6], float or
     S[j][3] = g1.x; S[j][4] = g1.y; S[j][5] = g1.z;
     org[j][0] = g0.w; org[j][1] = g1.w; org[j][2] = g2.x;
   }
+}
+
+__device__ __forceinline__ bool opaque_true() {  // true, unknown to the optimiser
+  int one = 1;
+  asm volatile("" : "+s"(one));
+  return one != 0;
 }
 
 template <class T>
@@ -930,12 +940,90 @@ __device__ __forceinline__ void tangents(const float n[3], float t1[3], float t2
   cross3(n, t1, t2);
 }
 
-// What the MDP needs from the last substep (instead of 12 per-link force vectors).
+// What the MDP needs from a substep (instead of 12 per-link force vectors).
 struct SensorOut {
   float feet_f[2][3];   // net contact force on foot_0 / foot_1
   float undes_fmax;     // max over the 10 undesired links of |net force|
   float tau2;           // sum of squared Isaac Lab applied torques (torques reward)
 };
+
+// Isaac Lab's ContactSensor with history_length > 0 updates after every physics step
+// (SensorBase.update -> _update_outdated_buffers on each scene.update(physics_dt)): each substep
+// parks its sensor record in LDS (one lane per env), the MDP epilogue replays them.
+__device__ __forceinline__ void sens_record(const Q& q, int k, const SensorOut& so) {
+  if (q.s == 0) {
+    q.sens(k, 0) = make_float4(so.feet_f[0][2], so.feet_f[1][2], sqrtf(dot3(so.feet_f[0], so.feet_f[0])),
+                               sqrtf(dot3(so.feet_f[1], so.feet_f[1])));
+    q.sens(k, 1) = make_float4(so.undes_fmax, 0.f, 0.f, 0.f);
+  }
+}
+
+// After this step's `dec` physics steps: the sum of the feet F_z and the max undesired |F| over the
+// HIST-slot histories (slot 0 newest; the slots older than this step come from the state rows
+// fz_row / fm_row), and the air / contact timers advanced by dt per physics step
+// (ContactSensor._update_buffers_impl: first contact -> last_air_time, first detach ->
+// last_contact_time). Only reductions are kept in registers; sens_store writes the histories.
+template <int HIST>
+__device__ __forceinline__ void sens_replay(const Q& q, const float* __restrict__ st, int N, int i, int fz_row,
+                                            int fm_row, int dec, float dt, float thr, float fz_sum[2], float& fm_max,
+                                            float air_cur[2], float air_last[2], float con_cur[2], float con_last[2]) {
+  fz_sum[0] = fz_sum[1] = 0.f;
+  fm_max = 0.f;
+#pragma unroll
+  for (int h = 0; h < HIST; ++h) {
+    float a0, a1, m;
+    if (h < dec) {
+      const float4 a = q.sens(dec - 1 - h, 0);
+      a0 = a.x;
+      a1 = a.y;
+      m = q.sens(dec - 1 - h, 1).x;
+    } else {
+      const int j = h - dec;
+      a0 = st[(size_t)(fz_row + 2 * j) * N + i];
+      a1 = st[(size_t)(fz_row + 2 * j + 1) * N + i];
+      m = st[(size_t)(fm_row + j) * N + i];
+    }
+    fz_sum[0] += a0;
+    fz_sum[1] += a1;
+    fm_max = h == 0 ? m : fmaxf(fm_max, m);
+  }
+  for (int k = 0; k < dec; ++k) {
+    const float4 a = q.sens(k, 0);
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+      const bool c = (f == 0 ? a.z : a.w) > thr;
+      air_last[f] = (air_cur[f] > 0.f && c) ? air_cur[f] + dt : air_last[f];
+      air_cur[f] = c ? 0.f : air_cur[f] + dt;
+      con_last[f] = (con_cur[f] > 0.f && !c) ? con_cur[f] + dt : con_last[f];
+      con_cur[f] = c ? con_cur[f] + dt : 0.f;
+    }
+  }
+}
+
+// the new histories into the state rows (oldest slot first, so the carried slots are read before
+// they are overwritten); zero = the env was reset (ContactSensor.reset)
+template <int HIST>
+__device__ __forceinline__ void sens_store(const Q& q, float* __restrict__ st, int N, int i, int fz_row, int fm_row,
+                                           int dec, bool zero) {
+#pragma unroll
+  for (int h = HIST - 1; h >= 0; --h) {
+    float a0, a1, m;
+    if (h < dec) {
+      const float4 a = q.sens(dec - 1 - h, 0);
+      a0 = a.x;
+      a1 = a.y;
+      m = q.sens(dec - 1 - h, 1).x;
+    } else {
+      const int j = h - dec;
+      a0 = st[(size_t)(fz_row + 2 * j) * N + i];
+      a1 = st[(size_t)(fz_row + 2 * j + 1) * N + i];
+      m = st[(size_t)(fm_row + j) * N + i];
+    }
+    st[(size_t)(fz_row + 2 * h) * N + i] = zero ? 0.f : a0;
+    st[(size_t)(fz_row + 2 * h + 1) * N + i] = zero ? 0.f : a1;
+    st[(size_t)(fm_row + h) * N + i] = zero ? 0.f : m;
+  }
+}
 
 // One Gauss-Seidel contact update (normal + Coulomb disk). g = {Y0[d], Y1[d], Y2[d], -} of this
 // lane's coordinate d, a0 = {invm0, invm1, invm2, vmin invm0}, a1 = {c01 invm1, c02 invm2, -, -}
@@ -1698,11 +1786,14 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_step_kernel(const z
     if (writer) q.pre() = pr;
   }
 
-  // 4 physics substeps (the last one reports the contact-sensor inputs and applied torques)
+  // 4 physics substeps, each followed by the contact sensor's update (record parked in LDS); the
+  // last one's applied torques feed the torques term
   SensorOut so;
   sp.mark(0);
   for (int k = 0; k < cfg.decimation; ++k) {
-    substep<false, false>(m, cfg, p, target, q, k == cfg.decimation - 1, so, nullptr, nullptr, sp);
+    // (a compile-time `true` here lets the scheduler reshape the loop into a 36 B/lane spill)
+    substep<false, false>(m, cfg, p, target, q, opaque_true(), so, nullptr, nullptr, sp);
+    sens_record(q, k, so);
     sp.mark(7);
   }
   m = opaque(m);
@@ -1720,19 +1811,13 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_step_kernel(const z
   // pointer goes through an empty asm so these loads are not hoisted above the physics (they
   // would be held in registers across all substeps).
   st = opaque_ptr(st);
-  float fz_prev[ZB_HIST - 1][2], fmax_prev[ZB_HIST - 1], air_cur0[2], air_last0[2], contact0[2];
+  float air_cur[2], air_last[2], contact_t[2], con_last_unused[2] = {0.f, 0.f};
   float step_len[2], f_last0[2], down[2][3], sums0[ZB_NUM_REWARD_TERMS];
 #pragma unroll
-  for (int h = 0; h < ZB_HIST - 1; ++h) {
-    fz_prev[h][0] = ST(ZB_S_FEET_FZ_HIST + 2 * h);
-    fz_prev[h][1] = ST(ZB_S_FEET_FZ_HIST + 2 * h + 1);
-    fmax_prev[h] = ST(ZB_S_UNDES_FMAX_HIST + h);
-  }
-#pragma unroll
   for (int f = 0; f < 2; ++f) {
-    air_cur0[f] = ST(ZB_S_FEET_AIR_CUR + f);
-    air_last0[f] = ST(ZB_S_FEET_AIR_LAST + f);
-    contact0[f] = ST(ZB_S_FEET_CONTACT_CUR + f);
+    air_cur[f] = ST(ZB_S_FEET_AIR_CUR + f);
+    air_last[f] = ST(ZB_S_FEET_AIR_LAST + f);
+    contact_t[f] = ST(ZB_S_FEET_CONTACT_CUR + f);
     step_len[f] = ST(ZB_S_FEET_STEP_LEN + f);
     f_last0[f] = ST(ZB_S_FEET_F_LAST + f);
 #pragma unroll
@@ -1744,15 +1829,10 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_step_kernel(const z
   for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) sums0[t] = ST(ZB_S_EP_SUMS + t);
   sp.mark(10);
 
-  // ContactSensor lazy update, once per policy step (history roll, air/contact timers)
-  float air_cur[2], air_last[2], contact_t[2];
-#pragma unroll
-  for (int f = 0; f < 2; ++f) {
-    const bool contact = sqrtf(dot3(so.feet_f[f], so.feet_f[f])) > cfg.contact_force_threshold;
-    air_last[f] = (air_cur0[f] > 0.f && contact) ? air_cur0[f] + step_dt : air_last0[f];
-    air_cur[f] = contact ? 0.f : air_cur0[f] + step_dt;
-    contact_t[f] = contact ? contact0[f] + step_dt : 0.f;
-  }
+  // ContactSensor (history 5, updated every physics step): histories and timers after the substeps
+  float fz_sum[2], fm_max;
+  sens_replay<ZB_HIST>(q, st, N, i, ZB_S_FEET_FZ_HIST, ZB_S_UNDES_FMAX_HIST, cfg.decimation, cfg.sim_dt,
+                       cfg.contact_force_threshold, fz_sum, fm_max, air_cur, air_last, contact_t, con_last_unused);
 
   // post-step feet COM velocities (feet_slide)
   float feet_vel[2][3], obs_q[4];
@@ -1773,15 +1853,8 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_step_kernel(const z
   const bool time_out = ep_len >= (float)(cfg.max_episode_length - 1);
   float feetF[2];
 #pragma unroll
-  for (int f = 0; f < 2; ++f) {
-    float sacc = so.feet_f[f][2];
-#pragma unroll
-    for (int h = 0; h < ZB_HIST - 1; ++h) sacc += fz_prev[h][f];
-    feetF[f] = sacc / (float)ZB_HIST;
-  }
-  bool died = so.undes_fmax > 1.0f;
-#pragma unroll
-  for (int h = 0; h < ZB_HIST - 1; ++h) died |= fmax_prev[h] > 1.0f;
+  for (int f = 0; f < 2; ++f) feetF[f] = fz_sum[f] / (float)ZB_HIST;
+  bool died = fm_max > 1.0f;
   died |= pre_base_z < cfg.termination_height;
   died |= fabsf(pre_base_y) > 0.5f;  // base_pos_y_err vs env origin (local frame: 0)
 
@@ -1872,13 +1945,9 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_step_kernel(const z
       ST(ZB_S_FEET_AIR_CUR + f) = live(air_cur[f]);
       ST(ZB_S_FEET_AIR_LAST + f) = live(air_last[f]);
       ST(ZB_S_FEET_CONTACT_CUR + f) = live(contact_t[f]);
-      ST(ZB_S_FEET_FZ_HIST + f) = live(so.feet_f[f][2]);
-#pragma unroll
-      for (int h = 1; h < ZB_HIST; ++h) ST(ZB_S_FEET_FZ_HIST + 2 * h + f) = live(fz_prev[h - 1][f]);
+
     }
-    ST(ZB_S_UNDES_FMAX_HIST) = live(so.undes_fmax);
-#pragma unroll
-    for (int h = 1; h < ZB_HIST; ++h) ST(ZB_S_UNDES_FMAX_HIST + h) = live(fmax_prev[h - 1]);
+    sens_store<ZB_HIST>(q, st, N, i, ZB_S_FEET_FZ_HIST, ZB_S_UNDES_FMAX_HIST, cfg.decimation, reset);
     ST(ZB_S_HEADING_SUM) = live(hs);
     ST(ZB_S_Y_ERR_SUM) = live(ys);
     ST(ZB_S_EP_LEN) = live(ep_len);
@@ -2393,8 +2462,9 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_v4_step_kernel(
     if (writer) pv = pr;
   }
 
-  // 4 substeps; the last reports the sensor inputs / applied torques, the joint velocities before
-  // it give Isaac Lab's finite-difference joint_acc (ArticulationData.update every substep)
+  // 4 substeps, each followed by the contact sensor's update (record parked in LDS); the last one's
+  // applied torques feed the torques term, the joint velocities before it give Isaac Lab's
+  // finite-difference joint_acc (ArticulationData.update every substep)
   SensorOut so;
   sp.mark(0);
   for (int k = 0; k < cfg.decimation; ++k) {
@@ -2403,7 +2473,8 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_v4_step_kernel(
 #pragma unroll
       for (int j = 0; j < ND; ++j) pv.jqd_prev[j] = p.jqd[j];
     }
-    substep<false, false>(m, cfg, p, target, q, last, so, nullptr, nullptr, sp);
+    substep<false, false>(m, cfg, p, target, q, true, so, nullptr, nullptr, sp);
+    sens_record(q, k, so);
     sp.mark(7);
   }
   m = opaque(m);
@@ -2411,29 +2482,24 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_v4_step_kernel(
   const PreV4 pr = pv;
   st = opaque_ptr(st);
 
-  // ContactSensor lazy update (history 3, air / contact timers incl. last_contact_time)
-  float fz_prev[ZB_V4_HIST - 1][2], fmax_prev[ZB_V4_HIST - 1];
-#pragma unroll
-  for (int h = 0; h < ZB_V4_HIST - 1; ++h) {
-    fz_prev[h][0] = ST(ZB_V4_FEET_FZ_HIST + 2 * h);
-    fz_prev[h][1] = ST(ZB_V4_FEET_FZ_HIST + 2 * h + 1);
-    fmax_prev[h] = ST(ZB_V4_UNDES_FMAX_HIST + h);
-  }
+  // ContactSensor (history 3, updated every physics step; air / contact timers incl.
+  // last_contact_time)
+  float fz_sum[2], fm_max;
   float air_cur[2], con_cur[2], air_last[2], con_last[2], feetF[2];
   bool in_contact[2];
 #pragma unroll
   for (int f = 0; f < 2; ++f) {
-    const float ac0 = ST(ZB_V4_FEET_AIR_CUR + f), cc0 = ST(ZB_V4_FEET_CONTACT_CUR + f);
-    const bool c = sqrtf(dot3(so.feet_f[f], so.feet_f[f])) > cfg.contact_force_threshold;
-    air_last[f] = (ac0 > 0.f && c) ? ac0 + step_dt : ST(ZB_V4_FEET_AIR_LAST + f);
-    air_cur[f] = c ? 0.f : ac0 + step_dt;
-    con_last[f] = (cc0 > 0.f && !c) ? cc0 + step_dt : ST(ZB_V4_FEET_CONTACT_LAST + f);
-    con_cur[f] = c ? cc0 + step_dt : 0.f;
-    in_contact[f] = con_cur[f] > 0.f;
-    float sacc = so.feet_f[f][2];
+    air_cur[f] = ST(ZB_V4_FEET_AIR_CUR + f);
+    con_cur[f] = ST(ZB_V4_FEET_CONTACT_CUR + f);
+    air_last[f] = ST(ZB_V4_FEET_AIR_LAST + f);
+    con_last[f] = ST(ZB_V4_FEET_CONTACT_LAST + f);
+  }
+  sens_replay<ZB_V4_HIST>(q, st, N, i, ZB_V4_FEET_FZ_HIST, ZB_V4_UNDES_FMAX_HIST, cfg.decimation, cfg.sim_dt,
+                          cfg.contact_force_threshold, fz_sum, fm_max, air_cur, air_last, con_cur, con_last);
 #pragma unroll
-    for (int h = 0; h < ZB_V4_HIST - 1; ++h) sacc += fz_prev[h][f];
-    feetF[f] = sacc / (float)ZB_V4_HIST;  // mean over the history (v4.py:846-849)
+  for (int f = 0; f < 2; ++f) {
+    in_contact[f] = con_cur[f] > 0.f;
+    feetF[f] = fz_sum[f] / (float)ZB_V4_HIST;  // mean over the history (v4.py:846-849)
   }
   const float ep_len = ST(ZB_V4_EP_LEN) + 1.f;
   float cmd[2] = {ST(ZB_V4_COMMANDS), ST(ZB_V4_COMMANDS + 1)};
@@ -2480,9 +2546,7 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_v4_step_kernel(
     }
     const float base_z = bp[2] + p.pos[2];
     // _get_dones (v4.py:896-918)
-    float fm = so.undes_fmax;
-#pragma unroll
-    for (int h = 0; h < ZB_V4_HIST - 1; ++h) fm = fmaxf(fm, fmax_prev[h]);
+    const float fm = fm_max;
     died = fm > cfg.undesired_force_threshold || base_z < cfg.termination_height;
   }
   const bool time_out = ep_len >= (float)(cfg.max_episode_length - 1);
@@ -2641,13 +2705,9 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_v4_step_kernel(
       ST(ZB_V4_FEET_CONTACT_CUR + f) = live(con_cur[f]);
       ST(ZB_V4_FEET_AIR_LAST + f) = live(air_last[f]);
       ST(ZB_V4_FEET_CONTACT_LAST + f) = live(con_last[f]);
-      ST(ZB_V4_FEET_FZ_HIST + f) = live(so.feet_f[f][2]);
-#pragma unroll
-      for (int h = 1; h < ZB_V4_HIST; ++h) ST(ZB_V4_FEET_FZ_HIST + 2 * h + f) = live(fz_prev[h - 1][f]);
+
     }
-    ST(ZB_V4_UNDES_FMAX_HIST) = live(so.undes_fmax);
-#pragma unroll
-    for (int h = 1; h < ZB_V4_HIST; ++h) ST(ZB_V4_UNDES_FMAX_HIST + h) = live(fmax_prev[h - 1]);
+    sens_store<ZB_V4_HIST>(q, st, N, i, ZB_V4_FEET_FZ_HIST, ZB_V4_UNDES_FMAX_HIST, cfg.decimation, reset);
     ST(ZB_V4_EP_LEN) = live(ep_len);
 #pragma unroll
     for (int t = 0; t < ZB_V4_NUM_REWARD_TERMS; ++t) ST(ZB_V4_EP_SUMS + t) = live(sums[t]);
@@ -3412,7 +3472,8 @@ int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_dev
       }
     if (np != m->num_self_pairs) return set_err(-1, "zb_create: self-collision pair count", hipSuccess);
   }
-  if (c->decimation < 1 || c->solver_iterations < 0) return set_err(-1, "zb_create: cfg", hipSuccess);
+  if (c->decimation < 1 || c->decimation > MAXSUB || c->solver_iterations < 0)
+    return set_err(-1, "zb_create: cfg (decimation 1..8, solver_iterations >= 0)", hipSuccess);
   if (c->task != ZB_TASK_WALKING_V2 && c->task != ZB_TASK_STANDUP_V0 && c->task != ZB_TASK_WALKING_V4 &&
       c->task != ZB_TASK_MANAGER_V0)
     return set_err(-1, "zb_create: unknown task", hipSuccess);
