@@ -81,6 +81,28 @@ def pmc_traffic(num_envs: int, kernel: str = "zb_step_kernel"):
     return None, None
 
 
+def pmc_issue(num_envs: int, kernel: str = "zb_step_kernel"):
+    """VALU issue fraction of the dominant kernel from the committed PMC passes (same grid): the
+    quad-cycles a wave spends issuing VALU instructions (SQ_ACTIVE_INST_VALU) over its resident
+    quad-cycles (SQ_WAVE_CYCLES), plus VALU instructions per wave. With one wave per SIMD (4096
+    envs) this is the SIMD's VALU utilisation — the kernel's real bound."""
+    import csv
+    import glob
+    here = os.path.dirname(os.path.abspath(__file__))
+    grid = -(-num_envs // ENVS_PER_WORKGROUP) * 64
+    for d in sorted(glob.glob(os.path.join(here, "profiles", "r*")), reverse=True):
+        vals = {}
+        for f in glob.glob(os.path.join(d, f"pmc_sq*_{kernel}.csv")):
+            for row in csv.DictReader(open(f)):
+                if int(row["grid"]) == grid:
+                    vals[row["counter"]] = float(row["mean_per_dispatch"])
+        if all(k in vals for k in ("SQ_ACTIVE_INST_VALU", "SQ_WAVE_CYCLES", "SQ_INSTS_VALU", "SQ_WAVES")):
+            return {"bound": "valu-issue", "frac": vals["SQ_ACTIVE_INST_VALU"] / vals["SQ_WAVE_CYCLES"],
+                    "valu_insts_per_wave": vals["SQ_INSTS_VALU"] / vals["SQ_WAVES"],
+                    "waves": vals["SQ_WAVES"], "source": os.path.relpath(d, here)}
+    return None
+
+
 def cpu_baseline(num_envs: int, seconds: float, task: str = "walking") -> dict:
     """Time the C oracle (test infrastructure, used here only as the CPU baseline)."""
     import numpy as np
@@ -198,7 +220,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": kname, "kernel_ms": kern_s * 1e3,
-                         "bytes_per_env_step": bpe},
+                         "bytes_per_env_step": bpe, "issue": pmc_issue(n, kname)},
             "cpu_baseline": None,
         }
         if not args.no_cpu_baseline and world == 1:
