@@ -23,8 +23,11 @@ def hipcc() -> str:
 STAMPS_OUT = os.path.join(HERE, "libzbot_stamps.so")
 
 
-def build(force: bool = False, verbose: bool = False, stamps: bool = False) -> str:
-    out = STAMPS_OUT if stamps else OUT
+def build(force: bool = False, verbose: bool = False, stamps: bool = False, defines: tuple = (),
+          out: str | None = None) -> str:
+    """defines / out: an experiment variant (e.g. ``-DZB_STAGED_STORES=0`` into ``libzbot_x.so``),
+    selected at run time with ZBOT_LIB=<file name>."""
+    out = os.path.join(HERE, out) if out else (STAMPS_OUT if stamps else OUT)
     deps = [SRC, os.path.join(ROOT, "include", "zbot.h"), os.path.abspath(__file__)]
     if not force and os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(d) for d in deps):
         return out
@@ -37,6 +40,8 @@ def build(force: bool = False, verbose: bool = False, stamps: bool = False) -> s
            "-I", os.path.join(ROOT, "include"), "-o", out + ".tmp", SRC]
     if stamps:
         cmd.insert(1, "-DZB_STAMPS")
+    for d in defines:
+        cmd.insert(1, f"-D{d}")
     if verbose:
         cmd.insert(1, "-Rpass-analysis=kernel-resource-usage")
     subprocess.run(cmd, check=True)
@@ -45,4 +50,7 @@ def build(force: bool = False, verbose: bool = False, stamps: bool = False) -> s
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose="-v" in sys.argv, stamps="--stamps" in sys.argv))
+    defs = tuple(a[2:] for a in sys.argv[1:] if a.startswith("-D"))
+    outs = [a[6:] for a in sys.argv[1:] if a.startswith("--out=")]
+    print(build(force="--force" in sys.argv, verbose="-v" in sys.argv, stamps="--stamps" in sys.argv,
+                defines=defs, out=outs[0] if outs else None))

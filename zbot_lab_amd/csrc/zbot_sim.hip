@@ -538,6 +538,7 @@ struct Q {
   __device__ __forceinline__ Pre& pre() const { return *reinterpret_cast<Pre*>(b + PRE_OFF + e * PRE4); }
   __device__ __forceinline__ float& fric(int l) const { return reinterpret_cast<float*>(b + FRIC_OFF)[e * NL + l]; }
   __device__ __forceinline__ float4& sens(int k, int h) const { return b[SENS_OFF + (e * MAXSUB + k) * 2 + h]; }
+  __device__ __forceinline__ float& stg(int k) const;  // epilogue staging row of this env (staged_store)
 };
 
 __device__ __forceinline__ void read_frame(const Q& q, int body, float R[9], float p[3]) {
@@ -1002,9 +1003,9 @@ __device__ __forceinline__ void sens_replay(const Q& q, const float* __restrict_
 
 // the new histories into the state rows (oldest slot first, so the carried slots are read before
 // they are overwritten); zero = the env was reset (ContactSensor.reset)
-template <int HIST>
-__device__ __forceinline__ void sens_store(const Q& q, float* __restrict__ st, int N, int i, int fz_row, int fm_row,
-                                           int dec, bool zero) {
+template <int HIST, class Put>
+__device__ __forceinline__ void sens_store(const Q& q, const float* __restrict__ st, int N, int i, int fz_row,
+                                           int fm_row, int dec, bool zero, Put&& put) {
 #pragma unroll
   for (int h = HIST - 1; h >= 0; --h) {
     float a0, a1, m;
@@ -1019,10 +1020,49 @@ __device__ __forceinline__ void sens_store(const Q& q, float* __restrict__ st, i
       a1 = st[(size_t)(fz_row + 2 * j + 1) * N + i];
       m = st[(size_t)(fm_row + j) * N + i];
     }
-    st[(size_t)(fz_row + 2 * h) * N + i] = zero ? 0.f : a0;
-    st[(size_t)(fz_row + 2 * h + 1) * N + i] = zero ? 0.f : a1;
-    st[(size_t)(fm_row + h) * N + i] = zero ? 0.f : m;
+    put(fz_row + 2 * h, zero ? 0.f : a0);
+    put(fz_row + 2 * h + 1, zero ? 0.f : a1);
+    put(fm_row + h, zero ? 0.f : m);
   }
+}
+template <int HIST>
+__device__ __forceinline__ void sens_store(const Q& q, float* __restrict__ st, int N, int i, int fz_row, int fm_row,
+                                           int dec, bool zero) {
+  sens_store<HIST>(q, st, N, i, fz_row, fm_row, dec, zero,
+                   [&](int row, float v) { st[(size_t)row * N + i] = v; });
+}
+
+// Staged epilogue: the writer lane of each env puts its outputs (state rows, then the observation,
+// reward, terminated, truncated) into LDS (aliasing the contact rows, dead after the physics), and
+// the whole wave stores them: one store instruction covers 16 state rows x the EPW consecutive
+// envs of the workgroup, the EPW observation rows go out as one contiguous run. This replaces ~110
+// single-lane-per-env store instructions per wave with ~9 full-wave ones.
+#ifndef ZB_STAGED_STORES
+#define ZB_STAGED_STORES 1
+#endif
+constexpr int STG_LEN = 88 + 25 + 3;  // >= max state dim + max obs dim + {reward, term, trunc}
+static_assert(EPW * STG_LEN <= NCM * WGT * 4, "staging fits the contact-row area");
+__device__ __forceinline__ float& Q::stg(int k) const { return reinterpret_cast<float*>(b + YG_OFF)[e * STG_LEN + k]; }
+template <int SD, int OD>
+__device__ __forceinline__ void staged_store(const Q& q, int env0, int N, float* __restrict__ st,
+                                             float* __restrict__ obs, float* __restrict__ rew,
+                                             uint8_t* __restrict__ term, uint8_t* __restrict__ trunc) {
+  static_assert(SD + OD + 3 <= STG_LEN, "staging row");
+  wave_sync();
+  const float* S = reinterpret_cast<const float*>(q.b + YG_OFF);
+  const int e = q.lane % EPW, f0 = q.lane / EPW;
+  const int env = env0 + e;
+  if (env < N) {
+#pragma unroll
+    for (int f = f0; f < SD; f += WGT / EPW) st[(size_t)f * N + env] = S[e * STG_LEN + f];
+    if (f0 == 0) rew[env] = S[e * STG_LEN + SD + OD];
+    if (f0 == 1) term[env] = S[e * STG_LEN + SD + OD + 1] != 0.f ? 1 : 0;
+    if (f0 == 2) trunc[env] = S[e * STG_LEN + SD + OD + 2] != 0.f ? 1 : 0;
+  }
+  const int nv = min(EPW, N - env0);
+#pragma unroll
+  for (int t = q.lane; t < EPW * OD; t += WGT)
+    if (t < nv * OD) obs[(size_t)env0 * OD + t] = S[(t / OD) * STG_LEN + SD + t % OD];
 }
 
 // One Gauss-Seidel contact update (normal + Coulomb disk). g = {Y0[d], Y1[d], Y2[d], -} of this
@@ -1926,36 +1966,46 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_step_kernel(const z
     obs_q[0] = dq.x; obs_q[1] = dq.y; obs_q[2] = dq.z; obs_q[3] = dq.w;
   }
   sp.mark(12);
+#if ZB_STAGED_STORES
+#define OUT(f) q.stg(f)
+#else
+#define OUT(f) ST(f)
+#endif
   if (writer) {
     auto live = [reset](float v) { return reset ? 0.f : v; };  // fields zeroed by _reset_idx
 #pragma unroll
-    for (int a = 0; a < 3; ++a) { ST(ZB_S_ROOT_POS + a) = p.pos[a]; ST(ZB_S_ROOT_LINVEL + a) = p.lv[a]; ST(ZB_S_ROOT_ANGVEL + a) = p.av[a]; }
+    for (int a = 0; a < 3; ++a) { OUT(ZB_S_ROOT_POS + a) = p.pos[a]; OUT(ZB_S_ROOT_LINVEL + a) = p.lv[a]; OUT(ZB_S_ROOT_ANGVEL + a) = p.av[a]; }
 #pragma unroll
-    for (int a = 0; a < 4; ++a) ST(ZB_S_ROOT_QUAT + a) = p.quat[a];
+    for (int a = 0; a < 4; ++a) OUT(ZB_S_ROOT_QUAT + a) = p.quat[a];
 #pragma unroll
-    for (int j = 0; j < ND; ++j) { ST(ZB_S_JOINT_POS + j) = p.jq[j]; ST(ZB_S_JOINT_VEL + j) = p.jqd[j]; }
+    for (int j = 0; j < ND; ++j) { OUT(ZB_S_JOINT_POS + j) = p.jq[j]; OUT(ZB_S_JOINT_VEL + j) = p.jqd[j]; }
 #pragma unroll
-    for (int j = 0; j < ND; ++j) { ST(ZB_S_P_DELTA + j) = live(pdel[j]); ST(ZB_S_ACTIONS + j) = live(a_now[j]); }
+    for (int j = 0; j < ND; ++j) { OUT(ZB_S_P_DELTA + j) = live(pdel[j]); OUT(ZB_S_ACTIONS + j) = live(a_now[j]); }
 #pragma unroll
     for (int f = 0; f < 2; ++f) {
 #pragma unroll
-      for (int a = 0; a < 3; ++a) ST(ZB_S_FEET_DOWN_POS + 3 * f + a) = down[f][a];
-      ST(ZB_S_FEET_STEP_LEN + f) = step_len[f];
-      ST(ZB_S_FEET_F_LAST + f) = feetF[f];
-      ST(ZB_S_FEET_AIR_CUR + f) = live(air_cur[f]);
-      ST(ZB_S_FEET_AIR_LAST + f) = live(air_last[f]);
-      ST(ZB_S_FEET_CONTACT_CUR + f) = live(contact_t[f]);
+      for (int a = 0; a < 3; ++a) OUT(ZB_S_FEET_DOWN_POS + 3 * f + a) = down[f][a];
+      OUT(ZB_S_FEET_STEP_LEN + f) = step_len[f];
+      OUT(ZB_S_FEET_F_LAST + f) = feetF[f];
+      OUT(ZB_S_FEET_AIR_CUR + f) = live(air_cur[f]);
+      OUT(ZB_S_FEET_AIR_LAST + f) = live(air_last[f]);
+      OUT(ZB_S_FEET_CONTACT_CUR + f) = live(contact_t[f]);
 
     }
-    sens_store<ZB_HIST>(q, st, N, i, ZB_S_FEET_FZ_HIST, ZB_S_UNDES_FMAX_HIST, cfg.decimation, reset);
-    ST(ZB_S_HEADING_SUM) = live(hs);
-    ST(ZB_S_Y_ERR_SUM) = live(ys);
-    ST(ZB_S_EP_LEN) = live(ep_len);
+    sens_store<ZB_HIST>(q, st, N, i, ZB_S_FEET_FZ_HIST, ZB_S_UNDES_FMAX_HIST, cfg.decimation, reset,
+                        [&](int row, float v) { OUT(row) = v; });
+    OUT(ZB_S_HEADING_SUM) = live(hs);
+    OUT(ZB_S_Y_ERR_SUM) = live(ys);
+    OUT(ZB_S_EP_LEN) = live(ep_len);
 #pragma unroll
-    for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) ST(ZB_S_EP_SUMS + t) = live(sums[t]);
+    for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) OUT(ZB_S_EP_SUMS + t) = live(sums[t]);
 
     // _get_observations (v2.py:351-365) of the post-step / post-reset state
+#if ZB_STAGED_STORES
+    float* o = &q.stg(ZB_STATE_DIM);
+#else
     float* o = obs + (size_t)i * ZB_OBS_DIM;
+#endif
     o[0] = obs_q[0]; o[1] = obs_q[1]; o[2] = obs_q[2]; o[3] = obs_q[3];
 #pragma unroll
     for (int j = 0; j < ND; ++j) {
@@ -1964,10 +2014,20 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_step_kernel(const z
       o[16 + j] = live(a_now[j]);
     }
     o[22] = cfg.joint_speed_limit;
+#if ZB_STAGED_STORES
+    o[ZB_OBS_DIM] = reward;
+    o[ZB_OBS_DIM + 1] = died ? 1.f : 0.f;
+    o[ZB_OBS_DIM + 2] = time_out ? 1.f : 0.f;
+#else
     rew[i] = reward;
     term[i] = died ? 1 : 0;
     trunc[i] = time_out ? 1 : 0;
+#endif
   }
+#if ZB_STAGED_STORES
+  staged_store<ZB_STATE_DIM, ZB_OBS_DIM>(q, xcd_block(blockIdx.x, gridDim.x) * EPW, N, st, obs, rew, term, trunc);
+#endif
+#undef OUT
   sp.mark(8);
   sp.flush();
 #undef ST
