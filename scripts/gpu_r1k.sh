@@ -8,8 +8,10 @@ tail -15 gpurun_out/test_gpu_all.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 for r in 1 2; do
   for lib in libzbot.so libzbot_nostage.so; do
-    ZBOT_LIB=$lib timeout -k 10 120 python bench.py --steps 1000 --warmup 100 --no-cpu-baseline > gpurun_out/ab_$lib.$r.log 2>&1 || exit $?
-    echo "$lib $r $(tail -1 gpurun_out/ab_$lib.$r.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(round(d["value"]/1e6,2), "M/s kernel_ms", round(d["roofline"]["kernel_ms"],4))')"
+    for task in walking manager; do
+      ZBOT_LIB=$lib timeout -k 10 120 python bench.py --task $task --steps 1000 --warmup 100 --no-cpu-baseline > gpurun_out/ab_$task.$lib.$r.log 2>&1 || exit $?
+      echo "$task $lib $r $(tail -1 gpurun_out/ab_$task.$lib.$r.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(round(d["value"]/1e6,2), "M/s kernel_ms", round(d["roofline"]["kernel_ms"],4))')"
+    done
   done
 done
 timeout -k 10 300 python bench.py --steps 1000 --warmup 100 > gpurun_out/bench_v2.log 2>&1 || exit $?

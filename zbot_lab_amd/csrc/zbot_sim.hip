@@ -2350,23 +2350,32 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_su_step_kernel(
     qmul(p.quat, qrel, obs_q);
   }
   sp.mark(12);
+#if ZB_STAGED_STORES
+#define OUT(f) q.stg(f)
+#else
+#define OUT(f) ST(f)
+#endif
   if (writer) {
     auto live = [reset](float v) { return reset ? 0.f : v; };
 #pragma unroll
-    for (int a = 0; a < 3; ++a) { ST(ZB_S_ROOT_POS + a) = p.pos[a]; ST(ZB_S_ROOT_LINVEL + a) = p.lv[a]; ST(ZB_S_ROOT_ANGVEL + a) = p.av[a]; }
+    for (int a = 0; a < 3; ++a) { OUT(ZB_S_ROOT_POS + a) = p.pos[a]; OUT(ZB_S_ROOT_LINVEL + a) = p.lv[a]; OUT(ZB_S_ROOT_ANGVEL + a) = p.av[a]; }
 #pragma unroll
-    for (int a = 0; a < 4; ++a) ST(ZB_S_ROOT_QUAT + a) = p.quat[a];
+    for (int a = 0; a < 4; ++a) OUT(ZB_S_ROOT_QUAT + a) = p.quat[a];
 #pragma unroll
-    for (int j = 0; j < ND; ++j) { ST(ZB_S_JOINT_POS + j) = p.jq[j]; ST(ZB_S_JOINT_VEL + j) = p.jqd[j]; }
+    for (int j = 0; j < ND; ++j) { OUT(ZB_S_JOINT_POS + j) = p.jq[j]; OUT(ZB_S_JOINT_VEL + j) = p.jqd[j]; }
 #pragma unroll
-    for (int j = 0; j < ND; ++j) { ST(ZB_SU_P_DELTA + j) = live(pr.pdel[j]); ST(ZB_SU_ACTIONS + j) = live(pr.a_now[j]); }
-    ST(ZB_SU_CENTER_Z_LAST) = reset ? cfg.center_z_init : czl;
-    ST(ZB_SU_EP_LEN) = live(ep_len);
+    for (int j = 0; j < ND; ++j) { OUT(ZB_SU_P_DELTA + j) = live(pr.pdel[j]); OUT(ZB_SU_ACTIONS + j) = live(pr.a_now[j]); }
+    OUT(ZB_SU_CENTER_Z_LAST) = reset ? cfg.center_z_init : czl;
+    OUT(ZB_SU_EP_LEN) = live(ep_len);
 #pragma unroll
-    for (int t = 0; t < ZB_SU_NUM_REWARD_TERMS; ++t) ST(ZB_SU_EP_SUMS + t) = live(sums[t]);
+    for (int t = 0; t < ZB_SU_NUM_REWARD_TERMS; ++t) OUT(ZB_SU_EP_SUMS + t) = live(sums[t]);
 
     // _get_observations (593-618): base quat, joint_pos - default, joint_vel, actions
+#if ZB_STAGED_STORES
+    float* o = &q.stg(ZB_SU_LINK_MU);
+#else
     float* o = obs + (size_t)i * ZB_SU_OBS_DIM;
+#endif
     o[0] = obs_q[0]; o[1] = obs_q[1]; o[2] = obs_q[2]; o[3] = obs_q[3];
 #pragma unroll
     for (int j = 0; j < ND; ++j) {
@@ -2374,10 +2383,20 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_su_step_kernel(
       o[10 + j] = p.jqd[j];
       o[16 + j] = live(pr.a_now[j]);
     }
+#if ZB_STAGED_STORES
+    q.stg(ZB_SU_LINK_MU + ZB_SU_OBS_DIM) = reward;
+    q.stg(ZB_SU_LINK_MU + ZB_SU_OBS_DIM + 1) = died ? 1.f : 0.f;
+    q.stg(ZB_SU_LINK_MU + ZB_SU_OBS_DIM + 2) = time_out ? 1.f : 0.f;
+#else
     rew[i] = reward;
     term[i] = died ? 1 : 0;
     trunc[i] = time_out ? 1 : 0;
+#endif
   }
+#if ZB_STAGED_STORES
+  staged_store<ZB_SU_LINK_MU, ZB_SU_OBS_DIM>(q, xcd_block(blockIdx.x, gridDim.x) * EPW, N, st, obs, rew, term, trunc);
+#endif
+#undef OUT
   sp.mark(8);
   sp.flush();
 #undef ST
@@ -2739,41 +2758,51 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_v4_step_kernel(
     he_obs = atan2f(sn, cs);
   }
   sp.mark(12);
+#if ZB_STAGED_STORES
+#define OUT(f) q.stg(f)
+#else
+#define OUT(f) ST(f)
+#endif
   if (writer) {
     auto live = [reset](float v) { return reset ? 0.f : v; };
 #pragma unroll
-    for (int a = 0; a < 3; ++a) { ST(ZB_S_ROOT_POS + a) = p.pos[a]; ST(ZB_S_ROOT_LINVEL + a) = p.lv[a]; ST(ZB_S_ROOT_ANGVEL + a) = p.av[a]; }
+    for (int a = 0; a < 3; ++a) { OUT(ZB_S_ROOT_POS + a) = p.pos[a]; OUT(ZB_S_ROOT_LINVEL + a) = p.lv[a]; OUT(ZB_S_ROOT_ANGVEL + a) = p.av[a]; }
 #pragma unroll
-    for (int a = 0; a < 4; ++a) ST(ZB_S_ROOT_QUAT + a) = p.quat[a];
+    for (int a = 0; a < 4; ++a) OUT(ZB_S_ROOT_QUAT + a) = p.quat[a];
 #pragma unroll
     for (int j = 0; j < ND; ++j) {
-      ST(ZB_S_JOINT_POS + j) = p.jq[j]; ST(ZB_S_JOINT_VEL + j) = p.jqd[j];
-      ST(ZB_V4_P_DELTA + j) = live(pr.pdel[j]); ST(ZB_V4_ACTIONS + j) = live(pr.a_now[j]);
+      OUT(ZB_S_JOINT_POS + j) = p.jq[j]; OUT(ZB_S_JOINT_VEL + j) = p.jqd[j];
+      OUT(ZB_V4_P_DELTA + j) = live(pr.pdel[j]); OUT(ZB_V4_ACTIONS + j) = live(pr.a_now[j]);
     }
-    ST(ZB_V4_COMMANDS) = cmd[0];
-    ST(ZB_V4_COMMANDS + 1) = cmd[1];
-    ST(ZB_V4_TARGET_YAW) = tgt;
-    ST(ZB_V4_INTERVAL_LEFT) = ileft;
-    ST(ZB_V4_CURRENT_YAW) = cur_yaw;
+    OUT(ZB_V4_COMMANDS) = cmd[0];
+    OUT(ZB_V4_COMMANDS + 1) = cmd[1];
+    OUT(ZB_V4_TARGET_YAW) = tgt;
+    OUT(ZB_V4_INTERVAL_LEFT) = ileft;
+    OUT(ZB_V4_CURRENT_YAW) = cur_yaw;
 #pragma unroll
     for (int f = 0; f < 2; ++f) {
 #pragma unroll
-      for (int a = 0; a < 3; ++a) ST(ZB_V4_FEET_DOWN_POS + 3 * f + a) = down[f][a];
-      ST(ZB_V4_FEET_STEP_LEN + f) = step_len[f];
-      ST(ZB_V4_FEET_F_LAST + f) = f_last[f];
-      ST(ZB_V4_FEET_AIR_CUR + f) = live(air_cur[f]);
-      ST(ZB_V4_FEET_CONTACT_CUR + f) = live(con_cur[f]);
-      ST(ZB_V4_FEET_AIR_LAST + f) = live(air_last[f]);
-      ST(ZB_V4_FEET_CONTACT_LAST + f) = live(con_last[f]);
+      for (int a = 0; a < 3; ++a) OUT(ZB_V4_FEET_DOWN_POS + 3 * f + a) = down[f][a];
+      OUT(ZB_V4_FEET_STEP_LEN + f) = step_len[f];
+      OUT(ZB_V4_FEET_F_LAST + f) = f_last[f];
+      OUT(ZB_V4_FEET_AIR_CUR + f) = live(air_cur[f]);
+      OUT(ZB_V4_FEET_CONTACT_CUR + f) = live(con_cur[f]);
+      OUT(ZB_V4_FEET_AIR_LAST + f) = live(air_last[f]);
+      OUT(ZB_V4_FEET_CONTACT_LAST + f) = live(con_last[f]);
 
     }
-    sens_store<ZB_V4_HIST>(q, st, N, i, ZB_V4_FEET_FZ_HIST, ZB_V4_UNDES_FMAX_HIST, cfg.decimation, reset);
-    ST(ZB_V4_EP_LEN) = live(ep_len);
+    sens_store<ZB_V4_HIST>(q, st, N, i, ZB_V4_FEET_FZ_HIST, ZB_V4_UNDES_FMAX_HIST, cfg.decimation, reset,
+                           [&](int row, float v) { OUT(row) = v; });
+    OUT(ZB_V4_EP_LEN) = live(ep_len);
 #pragma unroll
-    for (int t = 0; t < ZB_V4_NUM_REWARD_TERMS; ++t) ST(ZB_V4_EP_SUMS + t) = live(sums[t]);
+    for (int t = 0; t < ZB_V4_NUM_REWARD_TERMS; ++t) OUT(ZB_V4_EP_SUMS + t) = live(sums[t]);
 
     // _get_observations (v4.py:851-881)
+#if ZB_STAGED_STORES
+    float* o = &q.stg(ZB_V4_STATE_DIM);
+#else
     float* o = obs + (size_t)i * ZB_V4_OBS_DIM;
+#endif
     o[0] = obs_q[0]; o[1] = obs_q[1]; o[2] = obs_q[2]; o[3] = obs_q[3];
 #pragma unroll
     for (int j = 0; j < ND; ++j) {
@@ -2783,10 +2812,20 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_v4_step_kernel(
     }
     o[22] = cmd[0];
     o[23] = he_obs;
+#if ZB_STAGED_STORES
+    q.stg(ZB_V4_STATE_DIM + ZB_V4_OBS_DIM) = reward;
+    q.stg(ZB_V4_STATE_DIM + ZB_V4_OBS_DIM + 1) = died ? 1.f : 0.f;
+    q.stg(ZB_V4_STATE_DIM + ZB_V4_OBS_DIM + 2) = time_out ? 1.f : 0.f;
+#else
     rew[i] = reward;
     term[i] = died ? 1 : 0;
     trunc[i] = time_out ? 1 : 0;
+#endif
   }
+#if ZB_STAGED_STORES
+  staged_store<ZB_V4_STATE_DIM, ZB_V4_OBS_DIM>(q, xcd_block(blockIdx.x, gridDim.x) * EPW, N, st, obs, rew, term, trunc);
+#endif
+#undef OUT
   sp.mark(8);
   sp.flush();
 #undef ST
@@ -3209,41 +3248,60 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_m_step_kernel(
     if (standing > 0.5f) cmd[0] = cmd[1] = cmd[2] = 0.f;
   }
   sp.mark(12);
+#if ZB_STAGED_STORES
+#define OUT(f) q.stg(f)
+#else
+#define OUT(f) ST(f)
+#endif
   if (writer) {
     auto live = [reset](float v) { return reset ? 0.f : v; };
 #pragma unroll
-    for (int a = 0; a < 3; ++a) { ST(ZB_S_ROOT_POS + a) = p.pos[a]; ST(ZB_S_ROOT_LINVEL + a) = p.lv[a]; ST(ZB_S_ROOT_ANGVEL + a) = p.av[a]; }
+    for (int a = 0; a < 3; ++a) { OUT(ZB_S_ROOT_POS + a) = p.pos[a]; OUT(ZB_S_ROOT_LINVEL + a) = p.lv[a]; OUT(ZB_S_ROOT_ANGVEL + a) = p.av[a]; }
 #pragma unroll
-    for (int a = 0; a < 4; ++a) ST(ZB_S_ROOT_QUAT + a) = p.quat[a];
+    for (int a = 0; a < 4; ++a) OUT(ZB_S_ROOT_QUAT + a) = p.quat[a];
 #pragma unroll
-    for (int j = 0; j < ND; ++j) { ST(ZB_S_JOINT_POS + j) = p.jq[j]; ST(ZB_S_JOINT_VEL + j) = p.jqd[j]; }
+    for (int j = 0; j < ND; ++j) { OUT(ZB_S_JOINT_POS + j) = p.jq[j]; OUT(ZB_S_JOINT_VEL + j) = p.jqd[j]; }
 #pragma unroll
-    for (int a = 0; a < ND; ++a) ST(ZB_M_ACTIONS + a) = a_obs[a];
+    for (int a = 0; a < ND; ++a) OUT(ZB_M_ACTIONS + a) = a_obs[a];
 #pragma unroll
-    for (int a = 0; a < 3; ++a) ST(ZB_M_COMMANDS + a) = cmd[a];
-    ST(ZB_M_CMD_TIME_LEFT) = tleft;
-    ST(ZB_M_CMD_STANDING) = standing;
-    ST(ZB_M_METRICS) = met[0];
-    ST(ZB_M_METRICS + 1) = met[1];
+    for (int a = 0; a < 3; ++a) OUT(ZB_M_COMMANDS + a) = cmd[a];
+    OUT(ZB_M_CMD_TIME_LEFT) = tleft;
+    OUT(ZB_M_CMD_STANDING) = standing;
+    OUT(ZB_M_METRICS) = met[0];
+    OUT(ZB_M_METRICS + 1) = met[1];
 #pragma unroll
     for (int f = 0; f < 2; ++f) {
 #pragma unroll
-      for (int a = 0; a < 3; ++a) ST(ZB_M_FEET_DOWN_POS + 3 * f + a) = down[f][a];
-      ST(ZB_M_FEET_STEP_LEN + f) = step_len[f];
-      ST(ZB_M_FEET_F_LAST + f) = f_last[f];
-      ST(ZB_M_FEET_AIR_CUR + f) = live(air_cur[f]);
-      ST(ZB_M_FEET_AIR_LAST + f) = live(air_last[f]);
+      for (int a = 0; a < 3; ++a) OUT(ZB_M_FEET_DOWN_POS + 3 * f + a) = down[f][a];
+      OUT(ZB_M_FEET_STEP_LEN + f) = step_len[f];
+      OUT(ZB_M_FEET_F_LAST + f) = f_last[f];
+      OUT(ZB_M_FEET_AIR_CUR + f) = live(air_cur[f]);
+      OUT(ZB_M_FEET_AIR_LAST + f) = live(air_last[f]);
 #pragma unroll
-      for (int h = 0; h < 3; ++h) { ST(ZB_M_FEET_FZ_HIST + 2 * h + f) = live(fz_h[h][f]); ST(ZB_M_FEET_FN_HIST + 2 * h + f) = live(fn_h[h][f]); }
+      for (int h = 0; h < 3; ++h) { OUT(ZB_M_FEET_FZ_HIST + 2 * h + f) = live(fz_h[h][f]); OUT(ZB_M_FEET_FN_HIST + 2 * h + f) = live(fn_h[h][f]); }
     }
-    ST(ZB_M_EP_LEN) = live(ep_len);
+    OUT(ZB_M_EP_LEN) = live(ep_len);
 #pragma unroll
-    for (int t = 0; t < ZB_M_NUM_REWARD_TERMS; ++t) ST(ZB_M_EP_SUMS + t) = live(sums[t]);
+    for (int t = 0; t < ZB_M_NUM_REWARD_TERMS; ++t) OUT(ZB_M_EP_SUMS + t) = live(sums[t]);
+#if ZB_STAGED_STORES
+    m_write_obs(m, cfg, hs, bq, cmd, p, a_obs, &q.stg(ZB_M_LINK_MU));
+#else
     m_write_obs(m, cfg, hs, bq, cmd, p, a_obs, obs + (size_t)i * ZB_M_OBS_DIM);
+#endif
+#if ZB_STAGED_STORES
+    q.stg(ZB_M_LINK_MU + ZB_M_OBS_DIM) = reward;
+    q.stg(ZB_M_LINK_MU + ZB_M_OBS_DIM + 1) = terminated ? 1.f : 0.f;
+    q.stg(ZB_M_LINK_MU + ZB_M_OBS_DIM + 2) = time_out ? 1.f : 0.f;
+#else
     rew[i] = reward;
     term[i] = terminated ? 1 : 0;
     trunc[i] = time_out ? 1 : 0;
+#endif
   }
+#if ZB_STAGED_STORES
+  staged_store<ZB_M_LINK_MU, ZB_M_OBS_DIM>(q, xcd_block(blockIdx.x, gridDim.x) * EPW, N, st, obs, rew, term, trunc);
+#endif
+#undef OUT
   sp.mark(8);
   sp.flush();
 #undef ST
