@@ -2066,9 +2066,9 @@ __global__ void zb_derive_kernel(const zb_model* __restrict__ mg, float4* __rest
   Kin k;
   fk(m, p, k);
   float f0[3], f1[3], bp[3], q0[4];
-  link_pose(m, k, 0, f0, q0);
-  link_pose(m, k, 11, f1, q0);
-  link_pose(m, k, 6, bp, q0);
+  link_pose(m, k, m->foot_links[0], f0, q0);
+  link_pose(m, k, m->foot_links[1], f1, q0);
+  link_pose(m, k, m->base_link, bp, q0);
   links[DFLT_OFF + 0] = make_float4(f0[0] + p.pos[0], f0[1] + p.pos[1], f0[2] + p.pos[2], 0.f);
   links[DFLT_OFF + 1] = make_float4(f1[0] + p.pos[0], f1[1] + p.pos[1], f1[2] + p.pos[2], 0.f);
   links[DFLT_OFF + 2] = make_float4(q0[0], q0[1], q0[2], q0[3]);
@@ -2078,10 +2078,10 @@ __global__ void zb_derive_kernel(const zb_model* __restrict__ mg, float4* __rest
 #pragma unroll
   for (int a = 0; a < 3; ++a) p.pos[a] = 0.f;
   fk(m, p, k);
-  link_pose(m, k, 6, bp, q0);
+  link_pose(m, k, m->base_link, bp, q0);
   links[DFLT_OFF + 3] = make_float4(q0[0], q0[1], q0[2], q0[3]);
-  link_pose(m, k, 0, f0, q0);
-  link_pose(m, k, 11, f1, q0);
+  link_pose(m, k, m->foot_links[0], f0, q0);
+  link_pose(m, k, m->foot_links[1], f1, q0);
   links[DFLT_OFF + 4] = make_float4(f0[0], f0[1], f0[2], 0.f);
   links[DFLT_OFF + 5] = make_float4(f1[0], f1[1], f1[2], 0.f);
 }
