@@ -3,12 +3,14 @@ import os, sys, ctypes as C
 os.environ["ZBOT_LIB"] = "libzbot_stamps.so"
 R = os.path.dirname(os.path.dirname(os.path.abspath(__file__))); sys.path.insert(0, R)
 import torch
-from zbot_lab_amd.envs import ZbotDirectEnvCfgV2, ZbotDirectEnvV2
 from zbot_lab_amd import _native as nat
+from zbot_lab_amd.tasks import load_cfg, make
 names = ["prologue(pre+cache)", "ground", "self-collision", "inertia+rnea+crba", "chol+drives",
          "contact rows", "pgs", "post(solve,forces,integrate)", "mdp stores", "fk(substep)", "mdp loads", "mdp fk", "mdp rewards+reset"]
-cfg = ZbotDirectEnvCfgV2(); cfg.scene.num_envs = int(os.environ.get("N", "4096"))
-env = ZbotDirectEnvV2(cfg); env.reset()
+task = os.environ.get("TASK", "zbot-6b-walking-v2")
+cfg = load_cfg(task); cfg.scene.num_envs = int(os.environ.get("N", "4096"))
+env = make(task, cfg); env.reset()
+print(task, env.num_envs, "envs")
 g = torch.Generator(device="cuda"); g.manual_seed(42)
 for k in range(30): env.step(torch.randn(env.num_envs, 6, device="cuda", generator=g))
 torch.cuda.synchronize()

@@ -489,6 +489,7 @@ constexpr int NCAND = NL * 4 + NSELF;
 //   PRE   [EPW][PRE4]       prologue results parked across the physics
 //   FRIC  [EPW][NL] f32     per-link friction coefficients (standup)
 //   SENS  [EPW][MAXSUB][2]  per-substep contact-sensor record {fz0, fz1, |F0|, |F1|}, {undesired max |F|}
+//   LOGR  [EPW][ACC] f32    episode-log row of a resetting env (log_flush)
 constexpr int YG_OFF = 0;
 constexpr int AUX_OFF = YG_OFF + NCM * WGT;
 constexpr int LAM_OFF = AUX_OFF + NCM * 2 * EPW;
@@ -505,7 +506,9 @@ constexpr int PRE4 = 8;                   // float4 per Pre record (30 floats)
 constexpr int FRIC_OFF = PRE_OFF + EPW * PRE4;  // [EPW][NL] f32 per-link friction (standup)
 constexpr int MAXSUB = 8;                 // decimation limit (zb_create checks)
 constexpr int SENS_OFF = FRIC_OFF + (EPW * NL + 3) / 4;
-constexpr int LDS4 = SENS_OFF + EPW * MAXSUB * 2;
+constexpr int LOGR_OFF = SENS_OFF + EPW * MAXSUB * 2;
+constexpr int LOGR_W = ZB_MAX_REWARD_TERMS + 8;  // = ACC (episode-log entries, defined with the step kernels)
+constexpr int LDS4 = LOGR_OFF + EPW * LOGR_W / 4;
 
 // prologue results the MDP reads after the physics (parked in LDS across the substeps)
 struct Pre {
@@ -539,6 +542,7 @@ struct Q {
   __device__ __forceinline__ float& fric(int l) const { return reinterpret_cast<float*>(b + FRIC_OFF)[e * NL + l]; }
   __device__ __forceinline__ float4& sens(int k, int h) const { return b[SENS_OFF + (e * MAXSUB + k) * 2 + h]; }
   __device__ __forceinline__ float& stg(int k) const;  // epilogue staging row of this env (staged_store)
+  __device__ __forceinline__ float* logr(int ee) const { return reinterpret_cast<float*>(b + LOGR_OFF) + ee * LOGR_W; }
 };
 
 __device__ __forceinline__ void read_frame(const Q& q, int body, float R[9], float p[3]) {
@@ -1737,6 +1741,36 @@ __device__ __forceinline__ void write_obs(MP m, const Phys& p, const Mdp& d,
 constexpr int ACC_NRES = ZB_MAX_REWARD_TERMS, ACC_DIED = ACC_NRES + 1, ACC_TOUT = ACC_NRES + 2;
 constexpr int ACC_TERM2 = ACC_NRES + 3, ACC_MET0 = ACC_NRES + 4, ACC_MET1 = ACC_NRES + 5;
 constexpr int ACC = ACC_NRES + 8;
+static_assert(ACC == LOGR_W && ACC % 4 == 0, "log row width");
+// The episode-log accumulator is ACC_SLOTS copies of the ACC floats, one 128-B line each: a step
+// kernel adds into the slot of its workgroup, so the adds of one step spread over many L2 lines
+// instead of serialising on one (at a 30 % reset rate one shared line took ~100 us per step);
+// zb_finalize_kernel folds the slots and clears them.
+constexpr int ACC_STRIDE = 32, ACC_SLOTS = 64;
+static_assert(ACC <= ACC_STRIDE, "slot width");
+__device__ __forceinline__ float* acc_slot(float* acc, unsigned k) { return acc + (k % ACC_SLOTS) * ACC_STRIDE; }
+
+// Log row of a resetting env: the team lead clears its LDS row and fills the entries it logs.
+__device__ __forceinline__ float* log_row(const Q& q) {
+  float4* r = reinterpret_cast<float4*>(q.logr(q.e));
+#pragma unroll
+  for (int k = 0; k < ACC / 4; ++k) r[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+  return q.logr(q.e);
+}
+// Wave-level log reduction (uniform control flow): lane t < ACC adds entry t of the rows of the
+// resetting envs of this wave (mask = ballot of their team leads) and issues one atomic into the
+// workgroup's slot: at most ACC atomics per wave instead of ACC per resetting env.
+__device__ __forceinline__ void log_flush(const Q& q, uint64_t mask, float* acc) {
+  if (!mask) return;
+  wave_sync();
+  if (q.lane < ACC) {
+    float v = 0.f;
+#pragma unroll
+    for (int e = 0; e < EPW; ++e)
+      if ((mask >> (e * TL)) & 1ull) v += q.logr(e)[q.lane];
+    if (v != 0.f) atomicAdd(acc_slot(acc, blockIdx.x) + q.lane, v);
+  }
+}
 
 // ------------------------------------------------------------------------- kernels
 __device__ __forceinline__ void load_phys(const float* __restrict__ st, int N, int i, Phys& p) {
@@ -1946,13 +1980,15 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_step_kernel(const z
 
   // in-kernel auto-reset (v2.py:413-459): the episode log, then the default state; step_len and
   // f_last are not reset (reference), feet_down_pos_last = the default feet positions
+  const uint64_t lmask = __ballot(reset && lead);
   if (reset) {
     if (lead) {
+      float* lr = log_row(q);
 #pragma unroll
-      for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) atomicAdd(&acc[t], sums[t]);   // v2.py:441-448
-      atomicAdd(&acc[ACC_NRES], 1.f);
-      if (died) atomicAdd(&acc[ACC_DIED], 1.f);
-      if (time_out) atomicAdd(&acc[ACC_TOUT], 1.f);
+      for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) lr[t] = sums[t];   // v2.py:441-448
+      lr[ACC_NRES] = 1.f;
+      lr[ACC_DIED] = died ? 1.f : 0.f;
+      lr[ACC_TOUT] = time_out ? 1.f : 0.f;
     }
 #pragma unroll
     for (int a = 0; a < 3; ++a) { p.pos[a] = m->default_root_pos[a]; p.lv[a] = 0.f; p.av[a] = 0.f; }
@@ -1965,6 +2001,7 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_step_kernel(const z
     down[1][0] = d1.x; down[1][1] = d1.y; down[1][2] = d1.z;
     obs_q[0] = dq.x; obs_q[1] = dq.y; obs_q[2] = dq.z; obs_q[3] = dq.w;
   }
+  log_flush(q, lmask, acc);
   sp.mark(12);
 #if ZB_STAGED_STORES
 #define OUT(f) q.stg(f)
@@ -2046,8 +2083,8 @@ __global__ void zb_reset_kernel(const zb_model* __restrict__ mg, const float4* _
   Mdp d;
   load_state(st, N, i, p, d);
 #pragma unroll
-  for (int k = 0; k < ZB_NUM_REWARD_TERMS; ++k) atomicAdd(&acc[k], d.sums[k]);
-  atomicAdd(&acc[ACC_NRES], 1.f);
+  for (int k = 0; k < ZB_NUM_REWARD_TERMS; ++k) atomicAdd(&acc_slot(acc, t)[k], d.sums[k]);
+  atomicAdd(&acc_slot(acc, t)[ACC_NRES], 1.f);
   reset_env(m, links + DFLT_OFF, p, d);
   store_state(st, N, i, p, d);
 }
@@ -2335,20 +2372,23 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_su_step_kernel(
 
   // _reset_idx (645-703): episode log (sums per second of the env's own episode), new random
   // root pose, default joints; the reset env's observation sees the new pose
+  const uint64_t lmask = __ballot(reset && lead);
   if (reset) {
     if (lead) {
       const float dur = fmaxf(ep_len * step_dt, step_dt);
+      float* lr = log_row(q);
 #pragma unroll
-      for (int t = 0; t < ZB_SU_NUM_REWARD_TERMS; ++t) atomicAdd(&acc[t], sums[t] / dur);
-      atomicAdd(&acc[ACC_NRES], 1.f);
-      if (died) atomicAdd(&acc[ACC_DIED], 1.f);
-      if (time_out) atomicAdd(&acc[ACC_TOUT], 1.f);
+      for (int t = 0; t < ZB_SU_NUM_REWARD_TERMS; ++t) lr[t] = sums[t] / dur;
+      lr[ACC_NRES] = 1.f;
+      lr[ACC_DIED] = died ? 1.f : 0.f;
+      lr[ACC_TOUT] = time_out ? 1.f : 0.f;
     }
     su_reset_pose(m, cfg, seed, cnt->calls, i, p);
     const float4 qr = q.dflt()[3];
     const float qrel[4] = {qr.x, qr.y, qr.z, qr.w};
     qmul(p.quat, qrel, obs_q);
   }
+  log_flush(q, lmask, acc);
   sp.mark(12);
 #if ZB_STAGED_STORES
 #define OUT(f) q.stg(f)
@@ -2416,8 +2456,8 @@ __global__ void zb_su_reset_kernel(const zb_model* __restrict__ mg, zb_task_cfg 
   const float step_dt = cfg.sim_dt * (float)cfg.decimation;
   const float dur = fmaxf(ST(ZB_SU_EP_LEN) * step_dt, step_dt);
 #pragma unroll
-  for (int k = 0; k < ZB_SU_NUM_REWARD_TERMS; ++k) atomicAdd(&acc[k], ST(ZB_SU_EP_SUMS + k) / dur);
-  atomicAdd(&acc[ACC_NRES], 1.f);
+  for (int k = 0; k < ZB_SU_NUM_REWARD_TERMS; ++k) atomicAdd(&acc_slot(acc, t)[k], ST(ZB_SU_EP_SUMS + k) / dur);
+  atomicAdd(&acc_slot(acc, t)[ACC_NRES], 1.f);
   Phys p;
   su_reset_pose(m, cfg, seed, cnt->calls, i, p);
 #pragma unroll
@@ -2717,14 +2757,16 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_v4_step_kernel(
   float obs_q[4] = {bq[0], bq[1], bq[2], bq[3]};
 
   // _reset_idx (v4.py:920-1001): log (sum / own duration), reset events (pose, commands), defaults
+  const uint64_t lmask = __ballot(reset && lead);
   if (reset) {
     if (lead) {
       const float dur = fmaxf(ep_len * step_dt, step_dt);
+      float* lr = log_row(q);
 #pragma unroll
-      for (int t = 0; t < ZB_V4_NUM_REWARD_TERMS; ++t) atomicAdd(&acc[t], sums[t] / dur);
-      atomicAdd(&acc[ACC_NRES], 1.f);
-      if (died) atomicAdd(&acc[ACC_DIED], 1.f);
-      if (time_out) atomicAdd(&acc[ACC_TOUT], 1.f);
+      for (int t = 0; t < ZB_V4_NUM_REWARD_TERMS; ++t) lr[t] = sums[t] / dur;
+      lr[ACC_NRES] = 1.f;
+      lr[ACC_DIED] = died ? 1.f : 0.f;
+      lr[ACC_TOUT] = time_out ? 1.f : 0.f;
     }
     cur_yaw = reset_pose(m, cfg, hs, p);
     v4_resample(cfg, cnt, hs, 5, cur_yaw, cmd, tgt);
@@ -2757,6 +2799,7 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_v4_step_kernel(
     sincos_r(tgt - cur_yaw, &sn, &cs);
     he_obs = atan2f(sn, cs);
   }
+  log_flush(q, lmask, acc);
   sp.mark(12);
 #if ZB_STAGED_STORES
 #define OUT(f) q.stg(f)
@@ -2846,8 +2889,8 @@ __global__ void zb_v4_reset_kernel(const zb_model* __restrict__ mg, const float4
   if (!init) {
     const float dur = fmaxf(ST(ZB_V4_EP_LEN) * step_dt, step_dt);
 #pragma unroll
-    for (int k = 0; k < ZB_V4_NUM_REWARD_TERMS; ++k) atomicAdd(&acc[k], ST(ZB_V4_EP_SUMS + k) / dur);
-    atomicAdd(&acc[ACC_NRES], 1.f);
+    for (int k = 0; k < ZB_V4_NUM_REWARD_TERMS; ++k) atomicAdd(&acc_slot(acc, t)[k], ST(ZB_V4_EP_SUMS + k) / dur);
+    atomicAdd(&acc_slot(acc, t)[ACC_NRES], 1.f);
   }
   Phys p;
   const uint64_t hs = env_hash(seed, cnt->calls, i);
@@ -3188,16 +3231,18 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_m_step_kernel(
 
   // _reset_idx: curriculum (finalize), events reset_base / reset_robot_joints / reset_my_data,
   // managers (actions 0, reward sums and metrics logged, command resampled, sensor cleared)
+  const uint64_t lmask = __ballot(reset && lead);
   if (reset) {
     if (lead) {
+      float* lr = log_row(q);
 #pragma unroll
-      for (int t = 0; t < ZB_M_NUM_REWARD_TERMS; ++t) atomicAdd(&acc[t], sums[t]);
-      atomicAdd(&acc[ACC_NRES], 1.f);
-      if (low) atomicAdd(&acc[ACC_DIED], 1.f);
-      if (time_out) atomicAdd(&acc[ACC_TOUT], 1.f);
-      if (close) atomicAdd(&acc[ACC_TERM2], 1.f);
-      atomicAdd(&acc[ACC_MET0], met[0]);
-      atomicAdd(&acc[ACC_MET1], met[1]);
+      for (int t = 0; t < ZB_M_NUM_REWARD_TERMS; ++t) lr[t] = sums[t];
+      lr[ACC_NRES] = 1.f;
+      lr[ACC_DIED] = low ? 1.f : 0.f;
+      lr[ACC_TOUT] = time_out ? 1.f : 0.f;
+      lr[ACC_TERM2] = close ? 1.f : 0.f;
+      lr[ACC_MET0] = met[0];
+      lr[ACC_MET1] = met[1];
     }
     (void)reset_pose(m, cfg, hs, p);
     const float4 qr = q.dflt()[3];
@@ -3247,6 +3292,7 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_m_step_kernel(
     }
     if (standing > 0.5f) cmd[0] = cmd[1] = cmd[2] = 0.f;
   }
+  log_flush(q, lmask, acc);
   sp.mark(12);
 #if ZB_STAGED_STORES
 #define OUT(f) q.stg(f)
@@ -3341,10 +3387,10 @@ __global__ void zb_m_reset_kernel(const zb_model* __restrict__ mg, const float4*
 #define ST(f) st[(size_t)(f) * N + i]
   if (!init) {
 #pragma unroll
-    for (int k = 0; k < ZB_M_NUM_REWARD_TERMS; ++k) atomicAdd(&acc[k], ST(ZB_M_EP_SUMS + k));
-    atomicAdd(&acc[ACC_NRES], 1.f);
-    atomicAdd(&acc[ACC_MET0], ST(ZB_M_METRICS));
-    atomicAdd(&acc[ACC_MET1], ST(ZB_M_METRICS + 1));
+    for (int k = 0; k < ZB_M_NUM_REWARD_TERMS; ++k) atomicAdd(&acc_slot(acc, t)[k], ST(ZB_M_EP_SUMS + k));
+    atomicAdd(&acc_slot(acc, t)[ACC_NRES], 1.f);
+    atomicAdd(&acc_slot(acc, t)[ACC_MET0], ST(ZB_M_METRICS));
+    atomicAdd(&acc_slot(acc, t)[ACC_MET1], ST(ZB_M_METRICS + 1));
   }
   Phys p;
   const uint64_t hs = env_hash(seed, cnt->calls, i);
@@ -3430,7 +3476,14 @@ __global__ void zb_finalize_kernel(int N, float* __restrict__ st, float* __restr
                                    const uint8_t* __restrict__ term, const uint8_t* __restrict__ trunc) {
   const uint64_t ctr = cnt->calls;
   const uint64_t steps = cnt->steps + (is_step ? 1 : 0);
-  const float nres = acc[ACC_NRES];
+  __shared__ float acc_sum[ACC];  // the accumulator slots folded (acc_slot)
+  if (threadIdx.x < ACC) {
+    float v = 0.f;
+    for (int k = 0; k < ACC_SLOTS; ++k) v += acc[k * ACC_STRIDE + threadIdx.x];
+    acc_sum[threadIdx.x] = v;
+  }
+  __syncthreads();
+  const float nres = acc_sum[ACC_NRES];
   const bool full = force_full || nres == (float)N;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -3439,7 +3492,7 @@ __global__ void zb_finalize_kernel(int N, float* __restrict__ st, float* __restr
     if (nres > 0.f) {
       float v[ZB_LOG_LEN];
 #pragma unroll
-      for (int t = 0; t < ZB_MAX_REWARD_TERMS; ++t) v[t] = acc[t] / nres / episode_s;
+      for (int t = 0; t < ZB_MAX_REWARD_TERMS; ++t) v[t] = acc_sum[t] / nres / episode_s;
       v[16] = (float)cnt->stage;  // logged before the events run (v4.py:952-957)
       v[17] = cnt->vel[0];
       v[18] = cnt->vel[1];
@@ -3457,8 +3510,8 @@ __global__ void zb_finalize_kernel(int N, float* __restrict__ st, float* __restr
           cnt->changed = 1;
         }
         v[16] = cnt->vel[1];             // Curriculum/lin_vel_cmd_levels (the state after compute)
-        v[17] = acc[ACC_MET0] / nres;    // Metrics/base_velocity/error_vel_xy
-        v[18] = acc[ACC_MET1] / nres;    // Metrics/base_velocity/error_vel_yaw
+        v[17] = acc_sum[ACC_MET0] / nres;    // Metrics/base_velocity/error_vel_xy
+        v[18] = acc_sum[ACC_MET1] / nres;    // Metrics/base_velocity/error_vel_yaw
         v[19] = 0.f;
       }
 #pragma unroll
@@ -3466,9 +3519,9 @@ __global__ void zb_finalize_kernel(int N, float* __restrict__ st, float* __restr
         log_means[t] = v[t];
         if (user_means) user_means[t] = v[t];
       }
-      const int32_t c[ZB_LOG_COUNTS] = {reset_counts ? 0 : (int32_t)acc[ACC_DIED],
-                                        reset_counts ? 0 : (int32_t)acc[ACC_TOUT],
-                                        reset_counts ? 0 : (int32_t)acc[ACC_TERM2], 0};
+      const int32_t c[ZB_LOG_COUNTS] = {reset_counts ? 0 : (int32_t)acc_sum[ACC_DIED],
+                                        reset_counts ? 0 : (int32_t)acc_sum[ACC_TOUT],
+                                        reset_counts ? 0 : (int32_t)acc_sum[ACC_TERM2], 0};
 #pragma unroll
       for (int k = 0; k < ZB_LOG_COUNTS; ++k) {
         log_counts[k] = c[k];
@@ -3506,7 +3559,7 @@ __global__ void zb_finalize_kernel(int N, float* __restrict__ st, float* __restr
     }
   }
   __syncthreads();
-  if (threadIdx.x < ACC) acc[threadIdx.x] = 0.f;
+  for (int k = threadIdx.x; k < ACC_SLOTS * ACC_STRIDE; k += blockDim.x) acc[k] = 0.f;
   if (threadIdx.x == 0) cnt->calls = ctr + 1;
   // lin_vel_cmd_levels widened the ranges in this step: the reference's curriculum runs before the
   // command manager resamples the reset envs, so their commands (and the metrics / observations
@@ -3610,7 +3663,7 @@ int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_dev
   h->cfg = *c;
   HIPCHK(hipMalloc(&h->d_model, sizeof(zb_model)), "hipMalloc model");
   HIPCHK(hipMalloc(&h->d_state, sizeof(float) * (size_t)h->state_dim * num_envs), "hipMalloc state");
-  HIPCHK(hipMalloc(&h->d_acc, sizeof(float) * ACC), "hipMalloc acc");
+  HIPCHK(hipMalloc(&h->d_acc, sizeof(float) * ACC_SLOTS * ACC_STRIDE), "hipMalloc acc");
   HIPCHK(hipMalloc(&h->d_cnt, sizeof(Counters)), "hipMalloc counters");
   {
     Counters c0;
@@ -3669,7 +3722,7 @@ int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_dev
   HIPCHK(hipMemset(h->d_state, 0, sizeof(float) * (size_t)h->state_dim * num_envs), "hipMemset state");
   HIPCHK(hipMemset(h->d_log_means, 0, sizeof(float) * ZB_LOG_LEN), "hipMemset log");
   HIPCHK(hipMemset(h->d_log_counts, 0, sizeof(int32_t) * ZB_LOG_COUNTS), "hipMemset log");
-  HIPCHK(hipMemset(h->d_acc, 0, sizeof(float) * ACC), "hipMemset acc");
+  HIPCHK(hipMemset(h->d_acc, 0, sizeof(float) * ACC_SLOTS * ACC_STRIDE), "hipMemset acc");
   // start at the default pose (ep_len 0, as after construction; reset() randomises it)
   zb_derive_kernel<<<1, 1>>>(h->d_model, h->d_links);
   int rc = launch_check("zb_derive_kernel");
@@ -3708,7 +3761,7 @@ int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_dev
     rc = launch_check("zb_reset_kernel");
   }
   if (rc) return rc;
-  HIPCHK(hipMemset(h->d_acc, 0, sizeof(float) * ACC), "hipMemset acc");
+  HIPCHK(hipMemset(h->d_acc, 0, sizeof(float) * ACC_SLOTS * ACC_STRIDE), "hipMemset acc");
   HIPCHK(hipDeviceSynchronize(), "zb_create sync");
   *out = h;
   return 0;
