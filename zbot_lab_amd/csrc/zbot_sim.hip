@@ -490,6 +490,7 @@ constexpr int NCAND = NL * 4 + NSELF;
 //   FRIC  [EPW][NL] f32     per-link friction coefficients (standup)
 //   SENS  [EPW][MAXSUB][2]  per-substep contact-sensor record {fz0, fz1, |F0|, |F1|}, {undesired max |F|}
 //   LOGR  [EPW][ACC] f32    episode-log row of a resetting env (log_flush)
+//   CARRY [EPW][CARRY_W] f32  the env's MDP state rows, prefetched in the prologue (carry_prefetch)
 constexpr int YG_OFF = 0;
 constexpr int AUX_OFF = YG_OFF + NCM * WGT;
 constexpr int LAM_OFF = AUX_OFF + NCM * 2 * EPW;
@@ -508,7 +509,9 @@ constexpr int MAXSUB = 8;                 // decimation limit (zb_create checks)
 constexpr int SENS_OFF = FRIC_OFF + (EPW * NL + 3) / 4;
 constexpr int LOGR_OFF = SENS_OFF + EPW * MAXSUB * 2;
 constexpr int LOGR_W = ZB_MAX_REWARD_TERMS + 8;  // = ACC (episode-log entries, defined with the step kernels)
-constexpr int LDS4 = LOGR_OFF + EPW * LOGR_W / 4;
+constexpr int CARRY0 = ZB_S_P_DELTA, CARRY_W = 64;  // state rows [CARRY0, CARRY0 + CARRY_W)
+constexpr int CARRY_OFF = LOGR_OFF + EPW * LOGR_W / 4;
+constexpr int LDS4 = CARRY_OFF + EPW * CARRY_W / 4;
 
 // prologue results the MDP reads after the physics (parked in LDS across the substeps)
 struct Pre {
@@ -543,6 +546,7 @@ struct Q {
   __device__ __forceinline__ float4& sens(int k, int h) const { return b[SENS_OFF + (e * MAXSUB + k) * 2 + h]; }
   __device__ __forceinline__ float& stg(int k) const;  // epilogue staging row of this env (staged_store)
   __device__ __forceinline__ float* logr(int ee) const { return reinterpret_cast<float*>(b + LOGR_OFF) + ee * LOGR_W; }
+  __device__ __forceinline__ float* carry() const { return reinterpret_cast<float*>(b + CARRY_OFF) + e * CARRY_W; }
 };
 
 __device__ __forceinline__ void read_frame(const Q& q, int body, float R[9], float p[3]) {
@@ -1044,6 +1048,9 @@ __device__ __forceinline__ void sens_store(const Q& q, float* __restrict__ st, i
 #ifndef ZB_STAGED_STORES
 #define ZB_STAGED_STORES 1
 #endif
+#ifndef ZB_CARRY
+#define ZB_CARRY 1
+#endif
 constexpr int STG_LEN = 88 + 25 + 3;  // >= max state dim + max obs dim + {reward, term, trunc}
 static_assert(EPW * STG_LEN <= NCM * WGT * 4, "staging fits the contact-row area");
 __device__ __forceinline__ float& Q::stg(int k) const { return reinterpret_cast<float*>(b + YG_OFF)[e * STG_LEN + k]; }
@@ -1067,6 +1074,27 @@ __device__ __forceinline__ void staged_store(const Q& q, int env0, int N, float*
 #pragma unroll
   for (int t = q.lane; t < EPW * OD; t += WGT)
     if (t < nv * OD) obs[(size_t)env0 * OD + t] = S[(t / OD) * STG_LEN + SD + t % OD];
+}
+
+// MDP carry prefetch: the env's MDP state rows (everything after the 25 physics rows) are loaded
+// in the prologue, in the same batch as the physics rows, and parked in LDS across the substeps:
+// lane s of team e loads rows CARRY0 + s + 16 k of env e, so one load instruction covers 16 rows x
+// the EPW envs of the wave. The epilogue then reads LDS instead of waiting on ~40 HBM loads issued
+// after the physics. Returns the env's carry row indexed by state row (valid for rows >= CARRY0).
+template <int SD>
+__device__ __forceinline__ const float* carry_prefetch(const Q& q, const float* __restrict__ st, int N, int i) {
+  static_assert(SD - CARRY0 <= CARRY_W, "carry width");
+  constexpr int K = (SD - CARRY0 + TL - 1) / TL;
+  float v[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int r = CARRY0 + q.s + TL * k;
+    v[k] = r < SD ? st[(size_t)r * N + i] : 0.f;
+  }
+  float* c = q.carry();
+#pragma unroll
+  for (int k = 0; k < K; ++k) c[q.s + TL * k] = v[k];
+  return c - CARRY0;
 }
 
 // One Gauss-Seidel contact update (normal + Coulomb disk). g = {Y0[d], Y1[d], Y2[d], -} of this
@@ -1813,6 +1841,13 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_step_kernel(const z
   for (int a = 0; a < 4; ++a) p.quat[a] = ST(ZB_S_ROOT_QUAT + a);
 #pragma unroll
   for (int j = 0; j < ND; ++j) { p.jq[j] = ST(ZB_S_JOINT_POS + j); p.jqd[j] = ST(ZB_S_JOINT_VEL + j); }
+#if ZB_CARRY
+  const float* cst = carry_prefetch<ZB_STATE_DIM>(q, st, N, i);
+#define CST(f) cst[f]
+#else
+  const float* cst = st;
+#define CST(f) ST(f)
+#endif
 
   // _pre_physics_step (v2.py:276-287); _actions / p_delta are stored with the rest at the end
   // (one writer lane per env; the team holds identical values)
@@ -1881,31 +1916,31 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_step_kernel(const z
   const float(&pre_feet)[2][3] = pr.feet;
   const float r_action_rate = pr.action_rate;
 
-  // MDP state of this env (every lane loads; one writer lane stores at the end). The state
-  // pointer goes through an empty asm so these loads are not hoisted above the physics (they
-  // would be held in registers across all substeps).
+  // MDP state of this env (the LDS carry, or every lane loads; one writer lane stores at the
+  // end). The state pointer goes through an empty asm so direct loads are not hoisted above the
+  // physics (they would be held in registers across all substeps).
   st = opaque_ptr(st);
   float air_cur[2], air_last[2], contact_t[2], con_last_unused[2] = {0.f, 0.f};
   float step_len[2], f_last0[2], down[2][3], sums0[ZB_NUM_REWARD_TERMS];
 #pragma unroll
   for (int f = 0; f < 2; ++f) {
-    air_cur[f] = ST(ZB_S_FEET_AIR_CUR + f);
-    air_last[f] = ST(ZB_S_FEET_AIR_LAST + f);
-    contact_t[f] = ST(ZB_S_FEET_CONTACT_CUR + f);
-    step_len[f] = ST(ZB_S_FEET_STEP_LEN + f);
-    f_last0[f] = ST(ZB_S_FEET_F_LAST + f);
+    air_cur[f] = CST(ZB_S_FEET_AIR_CUR + f);
+    air_last[f] = CST(ZB_S_FEET_AIR_LAST + f);
+    contact_t[f] = CST(ZB_S_FEET_CONTACT_CUR + f);
+    step_len[f] = CST(ZB_S_FEET_STEP_LEN + f);
+    f_last0[f] = CST(ZB_S_FEET_F_LAST + f);
 #pragma unroll
-    for (int a = 0; a < 3; ++a) down[f][a] = ST(ZB_S_FEET_DOWN_POS + 3 * f + a);
+    for (int a = 0; a < 3; ++a) down[f][a] = CST(ZB_S_FEET_DOWN_POS + 3 * f + a);
   }
-  const float ep_len = ST(ZB_S_EP_LEN) + 1.f;
-  const float hs0 = ST(ZB_S_HEADING_SUM), ys0 = ST(ZB_S_Y_ERR_SUM);
+  const float ep_len = CST(ZB_S_EP_LEN) + 1.f;
+  const float hs0 = CST(ZB_S_HEADING_SUM), ys0 = CST(ZB_S_Y_ERR_SUM);
 #pragma unroll
-  for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) sums0[t] = ST(ZB_S_EP_SUMS + t);
+  for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) sums0[t] = CST(ZB_S_EP_SUMS + t);
   sp.mark(10);
 
   // ContactSensor (history 5, updated every physics step): histories and timers after the substeps
   float fz_sum[2], fm_max;
-  sens_replay<ZB_HIST>(q, st, N, i, ZB_S_FEET_FZ_HIST, ZB_S_UNDES_FMAX_HIST, cfg.decimation, cfg.sim_dt,
+  sens_replay<ZB_HIST>(q, ZB_CARRY ? cst : st, ZB_CARRY ? 1 : N, ZB_CARRY ? 0 : i, ZB_S_FEET_FZ_HIST, ZB_S_UNDES_FMAX_HIST, cfg.decimation, cfg.sim_dt,
                        cfg.contact_force_threshold, fz_sum, fm_max, air_cur, air_last, contact_t, con_last_unused);
 
   // post-step feet COM velocities (feet_slide)
@@ -2029,7 +2064,7 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_step_kernel(const z
       OUT(ZB_S_FEET_CONTACT_CUR + f) = live(contact_t[f]);
 
     }
-    sens_store<ZB_HIST>(q, st, N, i, ZB_S_FEET_FZ_HIST, ZB_S_UNDES_FMAX_HIST, cfg.decimation, reset,
+    sens_store<ZB_HIST>(q, ZB_CARRY ? cst : st, ZB_CARRY ? 1 : N, ZB_CARRY ? 0 : i, ZB_S_FEET_FZ_HIST, ZB_S_UNDES_FMAX_HIST, cfg.decimation, reset,
                         [&](int row, float v) { OUT(row) = v; });
     OUT(ZB_S_HEADING_SUM) = live(hs);
     OUT(ZB_S_Y_ERR_SUM) = live(ys);
@@ -2068,6 +2103,7 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_step_kernel(const z
   sp.mark(8);
   sp.flush();
 #undef ST
+#undef CST
 }
 
 // reset env_ids (or all when ids == nullptr); logs the reset envs' episode sums into acc
