@@ -1102,7 +1102,7 @@ __device__ __forceinline__ const float* carry_prefetch(const Q& q, const float* 
 // (c0r = Y_r . Y_0), lam = {ln, l1, l2}. The three row dots are reduced across the team; the
 // tangent velocities see the normal update through the cross terms. Arranged for a short
 // dependency chain: the impulse-independent parts are formed while the normal row resolves, and
-// the disk projection is min(1, lim / |l|) (rsq; NaN-free for |l| = 0 via minNum). Returns the
+// the disk projection is min(1, lim / max(|l|, 1e-15)) (rsq; finite for |l| = 0). Returns the
 // new impulses; wd (the lane's coordinate) updated.
 __device__ __forceinline__ float4 pgs_update(const float4 g, const float4 a0, const float4 a1, const float4 lam,
                                              float mu, float& wd) {
@@ -1115,7 +1115,7 @@ __device__ __forceinline__ float4 pgs_update(const float4 g, const float4 a0, co
   float l1 = fmaf(-a1.x, dl, u1);
   float l2 = fmaf(-a1.y, dl, u2);
   const float lim = mu * ln;
-  const float sc = fminf(1.f, lim * __builtin_amdgcn_rsqf(fmaf(l1, l1, l2 * l2)));
+  const float sc = fminf(1.f, lim * __builtin_amdgcn_rsqf(fmaxf(fmaf(l1, l1, l2 * l2), 1e-30f)));
   l1 *= sc;
   l2 *= sc;
   const float d1 = l1 - lam.y, d2 = l2 - lam.z;
