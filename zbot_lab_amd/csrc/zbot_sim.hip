@@ -380,11 +380,13 @@ static_assert(WGT <= WAVE, "one wave per workgroup");
 
 template <int CTRL>
 __device__ __forceinline__ float dppf(float x) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
+  // bound_ctrl: an invalid source lane reads 0, the same as keeping old = 0, but the compiler
+  // need not materialise old (folds into v_add_f32_dpp / drops the v_mov 0)
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, true));
 }
 template <int CTRL>
 __device__ __forceinline__ int dppi(int x) {
-  return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xF, 0xF, false);
+  return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xF, 0xF, true);
 }
 template <int CTRL>
 __device__ __forceinline__ int dppz(int x) {  // out-of-row source lanes read 0 (row shifts)
@@ -408,6 +410,9 @@ __device__ __forceinline__ void suffix_sum(float (&x)[NF]) {
   for (int a = 0; a < NF; ++a) x[a] += dppzf<DPP_SHL + 4>(x[a]);
 }
 __device__ __forceinline__ float tsum(float x) {
+  // keep x's producer (usually a product) out of the first add: contracted into an fma it would
+  // need a separate v_mov_dpp; as a plain add the DPP folds into v_add_f32_dpp
+  asm("" : "+v"(x));
   x += dppf<DPP_XOR1>(x);
   x += dppf<DPP_XOR2>(x);
   x += dppf<DPP_HALF_MIRROR>(x);
