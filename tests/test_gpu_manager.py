@@ -80,6 +80,24 @@ def test_friction_and_one_step_parity(gpu):
     assert ok.mean() >= 0.97, ok.mean()
 
 
+def test_reset_observation_in_step(gpu):
+    """Envs that terminate inside a step are reset by the step kernel; their observation is the
+    post-reset one: base (Isaac Lab root = base link, link 5 of this asset) quat = the reset yaw
+    pose, zero velocities, zero last action. Regression: the default-pose table once took the
+    base quat of link 6 (the walking asset's base), 60 deg off on every reset env."""
+    n = 512
+    g, o, torch = _pair(n, seed=5, feet_close_min=0.125)  # above the default stance: all terminate
+    a = np.zeros((n, 6), np.float32)
+    og, _, tg_, trg = g.step(torch.from_numpy(a).cuda())
+    oo, _, to_, tro = o.step(a)
+    tg_, trg = tg_.cpu().numpy(), trg.cpu().numpy()
+    np.testing.assert_array_equal(tg_, to_)
+    assert tg_.all()
+    og = og.cpu().numpy()
+    np.testing.assert_allclose(og, oo, atol=2e-5)
+    assert np.abs(og[:, 19:25]).max() == 0.0
+
+
 def test_curriculum_fixup_parity(gpu):
     """lin_vel_cmd_levels every 5 steps with a zero threshold: ranges, logs and the commands that the
     reset envs of a firing call redraw from the widened ranges agree with the oracle."""

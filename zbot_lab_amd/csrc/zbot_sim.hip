@@ -371,6 +371,9 @@ constexpr int TL = 16;           // lanes per env
 #ifndef ZB_EPW
 #define ZB_EPW 4
 #endif
+#ifndef ZB_TEAM_CHOL
+#define ZB_TEAM_CHOL 1  // cholesky_team (1) or the redundant per-lane cholesky_inplace (0)
+#endif
 #ifndef ZB_WAVES_PER_SIMD
 #define ZB_WAVES_PER_SIMD 1
 #endif
@@ -1139,6 +1142,40 @@ __device__ __forceinline__ void crba_column(float L[NT], const float Fk[6], cons
   for (int jj = 0; jj <= K; ++jj) L[tri(6 + K, 6 + jj)] = tb<K>(Mk[jj]) + (jj == K ? arm : 0.f);
 }
 
+#if ZB_TEAM_CHOL
+// Team-parallel Cholesky of the 12x12 mass matrix. Lane s owns row own_row(s) of M (joint rows
+// 6 + s in lanes 0-5, where the CRBA leaves column s; root rows s - 6 in lanes 6-11) in R[].
+// Column k: every lane forms its row's t = M[r][k] - sum_{m<k} L[r][m] L[k][m] (row k of L from
+// its packed copy), the owner of row k broadcasts its t (the pivot), every lane takes
+// iv = rsq(pivot) and scales, and column k (rows >= k) is broadcast from the row owners into every
+// lane's packed L. ~200 instructions instead of the ~380 of the redundant factorisation; every
+// lane ends with the same L / inv as cholesky_inplace (lanes 12-15 own no row).
+constexpr int own_lane(int r) { return r < 6 ? r + 6 : r - 6; }
+template <int K, int Rw>
+__device__ __forceinline__ void team_chol_bcast(float v, float L[NT]) {  // column K, rows Rw.. of L
+  L[tri(Rw, K)] = tb<own_lane(Rw)>(v);
+  if constexpr (Rw + 1 < NV) team_chol_bcast<K, Rw + 1>(v, L);
+}
+template <int K>
+__device__ __forceinline__ void team_chol_col(float R[NV], float L[NT], float inv[NV]) {
+  float t = R[K];
+#pragma unroll
+  for (int m = 0; m < K; ++m) t = fmaf(-R[m], L[tri(K, m)], t);
+  const float pv = fmaxf(tb<own_lane(K)>(t), 1e-12f);
+  const float iv = __builtin_amdgcn_rsqf(pv);
+  inv[K] = iv;
+  R[K] = t * iv;
+  L[tri(K, K)] = pv * iv;
+  if constexpr (K + 1 < NV) team_chol_bcast<K, K + 1>(R[K], L);
+}
+__device__ __forceinline__ void cholesky_team(float R[NV], float L[NT], float inv[NV]) {
+  team_chol_col<0>(R, L, inv); team_chol_col<1>(R, L, inv); team_chol_col<2>(R, L, inv);
+  team_chol_col<3>(R, L, inv); team_chol_col<4>(R, L, inv); team_chol_col<5>(R, L, inv);
+  team_chol_col<6>(R, L, inv); team_chol_col<7>(R, L, inv); team_chol_col<8>(R, L, inv);
+  team_chol_col<9>(R, L, inv); team_chol_col<10>(R, L, inv); team_chol_col<11>(R, L, inv);
+}
+#endif
+
 // ------------------------------------------------------------------------- one substep
 // kLinkFriction: per-contact Coulomb coefficient from the per-link table q.fric (standup DR);
 // otherwise cfg.friction everywhere.
@@ -1177,6 +1214,9 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
   float Cb[NV];
   const float arm = dt * (m->kd + dt * m->kp);
   float L[NT];
+#if ZB_TEAM_CHOL
+  float R[NV];  // this lane's row of M (cholesky_team)
+#endif
   {
   float S[ND][6];  // joint motion subspaces (LDS), live through RNEA + CRBA only
   read_S(q, S);
@@ -1246,6 +1286,28 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
       for (int a = 0; a < 6; ++a) t += S[jj][a] * Fk[a];
       Mk[jj] = t;
     }
+#if ZB_TEAM_CHOL
+    // this lane's row of M (own_lane): joint row 6 + s from its own column (lanes 0-5), root row
+    // s - 6 of the Ic_0 block (lane 0's composite) in lanes 6-11
+    {
+      const float m0t = tb<0>(ic[0]), hx = tb<0>(ic[1]), hy = tb<0>(ic[2]), hz = tb<0>(ic[3]);
+      const float i0 = tb<0>(ic[4]), i1 = tb<0>(ic[5]), i2 = tb<0>(ic[6]);
+      const float i3 = tb<0>(ic[7]), i4 = tb<0>(ic[8]), i5 = tb<0>(ic[9]);
+      const int r = q.s - 6;
+      float B[6];  // lower triangle of root row r (entries past the diagonal unused)
+      B[0] = r == 0 ? i0 : r == 1 ? i3 : r == 2 ? i4 : r == 3 ? 0.f : r == 4 ? -hz : hy;
+      B[1] = r == 1 ? i1 : r == 2 ? i5 : r == 3 ? hz : r == 4 ? 0.f : -hx;
+      B[2] = r == 2 ? i2 : r == 3 ? -hy : r == 4 ? hx : 0.f;
+      B[3] = r == 3 ? m0t : 0.f;
+      B[4] = r == 4 ? m0t : 0.f;
+      B[5] = r == 5 ? m0t : 0.f;
+      const bool jrow = q.s < ND;
+#pragma unroll
+      for (int a = 0; a < 6; ++a) R[a] = jrow ? Fk[a] : B[a];
+#pragma unroll
+      for (int jj = 0; jj < ND; ++jj) R[6 + jj] = jrow ? Mk[jj] + (jj == q.s ? arm : 0.f) : 0.f;
+    }
+#else
     // root block from Ic_0 (lane 0)
     const float m0t = tb<0>(ic[0]), hx = tb<0>(ic[1]), hy = tb<0>(ic[2]), hz = tb<0>(ic[3]);
     L[tri(0, 0)] = tb<0>(ic[4]); L[tri(1, 1)] = tb<0>(ic[5]); L[tri(2, 2)] = tb<0>(ic[6]);
@@ -1261,6 +1323,7 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
     crba_column<3>(L, Fk, Mk, arm);
     crba_column<4>(L, Fk, Mk, arm);
     crba_column<5>(L, Fk, Mk, arm);
+#endif
   }
   }  // S
 
@@ -1269,7 +1332,11 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
   // (rank-1 downdate of the factor), then the free velocity is re-solved.
   sp.mark(3);
   float Li[NV];
+#if ZB_TEAM_CHOL
+  cholesky_team(R, L, Li);
+#else
   cholesky_inplace(L, Li);
+#endif
   float u[NV], b[NV], w[NV];
   u[0] = s.av[0]; u[1] = s.av[1]; u[2] = s.av[2];
   u[3] = s.lv[0]; u[4] = s.lv[1]; u[5] = s.lv[2];
