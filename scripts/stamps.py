@@ -1,6 +1,6 @@
 """Per-phase cycle breakdown of zb_step_kernel (diagnostic build libzbot_stamps.so, GPU box)."""
 import os, sys, ctypes as C
-os.environ["ZBOT_LIB"] = "libzbot_stamps.so"
+os.environ.setdefault("ZBOT_LIB", "libzbot_stamps.so")
 R = os.path.dirname(os.path.dirname(os.path.abspath(__file__))); sys.path.insert(0, R)
 import torch
 from zbot_lab_amd import _native as nat

@@ -1073,7 +1073,9 @@ __device__ __forceinline__ void staged_store(const Q& q, int env0, int N, float*
   const int env = env0 + e;
   if (env < N) {
 #pragma unroll
-    for (int f = f0; f < SD; f += WGT / EPW) st[(size_t)f * N + env] = S[e * STG_LEN + f];
+    for (int f = f0; f < SD; f += WGT / EPW) {
+      st[(size_t)f * N + env] = S[e * STG_LEN + f];
+    }
     if (f0 == 0) rew[env] = S[e * STG_LEN + SD + OD];
     if (f0 == 1) term[env] = S[e * STG_LEN + SD + OD + 1] != 0.f ? 1 : 0;
     if (f0 == 2) trunc[env] = S[e * STG_LEN + SD + OD + 2] != 0.f ? 1 : 0;
