@@ -47,8 +47,7 @@ def build(force: bool = False, verbose: bool = False, stamps: bool = False, defi
         cmd.insert(1, "-DZB_STAMPS")
     for d in defines:
         cmd.insert(1, f"-D{d}")
-    for f in flags:
-        cmd.insert(1, f)
+    cmd[1:1] = list(flags)
     if verbose:
         cmd.insert(1, "-Rpass-analysis=kernel-resource-usage")
     subprocess.run(cmd, check=True)
