@@ -1,13 +1,21 @@
 #!/usr/bin/env bash
-# per-physics-step contact sensor (v2 / v4) + manager env: diagnostics, all GPU tests, benches, profiles
+# Round-1 final evidence: GPU tests, bench lines (all tasks, 65536 envs), rocprof summaries r1i.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python scripts/dev/diag_mgr.py > gpurun_out/diag_mgr.log 2>&1 || { cat gpurun_out/diag_mgr.log; exit 1; }
-cat gpurun_out/diag_mgr.log
-timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > gpurun_out/test_gpu_all.log 2>&1; rc=$?
-tail -15 gpurun_out/test_gpu_all.log
-if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-timeout -k 10 300 python bench.py --steps 300 --warmup 30 --cpu-baseline-seconds 10 > gpurun_out/bench_v2.log 2>&1 || exit $?
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/test_gpu_all.log 2>&1 || { tail -30 gpurun_out/test_gpu_all.log; exit 1; }
+tail -2 gpurun_out/test_gpu_all.log
+timeout -k 10 300 python bench.py > gpurun_out/bench_v2.log 2>&1 || exit $?
 tail -1 gpurun_out/bench_v2.log
-timeout -k 10 300 python bench.py --task manager --steps 300 --warmup 30 --cpu-baseline-seconds 10 > gpurun_out/bench_manager.log 2>&1 || exit $?
-tail -1 gpurun_out/bench_manager.log
+for t in manager v4 standup; do
+  timeout -k 10 300 python bench.py --task $t > gpurun_out/bench_$t.log 2>&1 || exit $?
+  tail -1 gpurun_out/bench_$t.log
+done
+timeout -k 10 300 python bench.py --envs-per-gpu 8192 --steps 400 --warmup 40 --no-cpu-baseline > gpurun_out/bench_v2_8192.log 2>&1 || exit $?
+tail -1 gpurun_out/bench_v2_8192.log
+timeout -k 10 300 python bench.py --envs-per-gpu 65536 --steps 200 --warmup 20 --no-cpu-baseline > gpurun_out/bench_v2_65536.log 2>&1 || exit $?
+tail -1 gpurun_out/bench_v2_65536.log
+TAG=r1i PSTEPS=100 bash scripts/gpu_profile.sh > gpurun_out/prof_v2.log 2>&1 || exit $?
+TAG=r1i_mgr BENCH_ARGS="--task manager" PSTEPS=100 bash scripts/gpu_profile.sh > gpurun_out/prof_mgr.log 2>&1 || exit $?
+TAG=r1i_v4 BENCH_ARGS="--task v4" PSTEPS=100 bash scripts/gpu_profile.sh > gpurun_out/prof_v4.log 2>&1 || exit $?
+TAG=r1i_su BENCH_ARGS="--task standup" PSTEPS=50 bash scripts/gpu_profile.sh > gpurun_out/prof_su.log 2>&1 || exit $?
+echo done

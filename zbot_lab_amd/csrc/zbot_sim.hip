@@ -740,10 +740,13 @@ __device__ __forceinline__ T* opaque_ptr(T* p) {
 }
 
 // ------------------------------------------------------------------------- contacts
-// One self-collision candidate pair: up to 4 sphere-pair contacts, in (sa, sb) order. Emits
-// through `out(x, sep, n, code)`; returns the number found.
-template <class F>
-__device__ __forceinline__ int narrow_pair(const Q& q, int pidx, float margin, F&& out) {
+// One self-collision candidate pair: up to 4 sphere-pair contacts, in (sa, sb) order. Test mode
+// (kEmit false) returns the 4-bit mask of sphere pairs within the margin; emit mode writes exactly
+// the sphere pairs of `sel` (the test pass's mask) through `out(x, sep, n, code)`. The write pass
+// never re-tests: two separately compiled copies of the margin test could round differently at
+// the boundary, leaving a counted candidate slot unwritten.
+template <bool kEmit, class F>
+__device__ __forceinline__ unsigned narrow_pair(const Q& q, int pidx, float margin, unsigned sel, F&& out) {
   const int pcode = q.pair_code(pidx);
   const int la = pcode >> 4, lb = pcode & 15;
   float Ra[9], pa[3], Rb[9], pb[3];
@@ -751,7 +754,7 @@ __device__ __forceinline__ int narrow_pair(const Q& q, int pidx, float margin, F
   read_frame(q, link_body(lb), Rb, pb);
   const float4* LA = q.link(la);
   const float4* LB = q.link(lb);
-  int cnt = 0;
+  unsigned hits = 0;
 #pragma unroll
   for (int sa = 0; sa < 2; ++sa) {
     const float4 spa = LA[7 + sa];
@@ -767,19 +770,22 @@ __device__ __forceinline__ int narrow_pair(const Q& q, int pidx, float margin, F
       const float dv[3] = {xa[0] - xb[0], xa[1] - xb[1], xa[2] - xb[2]};
       const float dist = sqrtf(dot3(dv, dv));
       const float sep = dist - (spa.w + spb.w);
-      if (sep < margin && dist > 1e-9f) {
-        float n[3], x[3];
+      const unsigned bit = 1u << (2 * sa + sb);
+      if (kEmit ? (sel & bit) != 0u : (sep < margin && dist > 1e-9f)) {
+        if (kEmit) {
+          float n[3], x[3];
 #pragma unroll
-        for (int a = 0; a < 3; ++a) {
-          n[a] = dv[a] / dist;
-          x[a] = 0.5f * ((xa[a] - n[a] * spa.w) + (xb[a] + n[a] * spb.w));
+          for (int a = 0; a < 3; ++a) {
+            n[a] = dv[a] / dist;
+            x[a] = 0.5f * ((xa[a] - n[a] * spa.w) + (xb[a] + n[a] * spb.w));
+          }
+          out(x, sep, n, (float)(16 * la + lb + 1));
         }
-        out(x, sep, n, (float)(16 * la + lb + 1));
-        ++cnt;
+        hits |= bit;
       }
     }
   }
-  return cnt;
+  return hits;
 }
 
 // Detection + selection for the team's env; returns the number of contacts (team-uniform) and
@@ -839,6 +845,8 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q&
   // self: broadphase (lane s: pairs [PAIRS_PER_LANE s, +PAIRS_PER_LANE)), team OR of the bits,
   // then the candidate pairs' narrow phase (counting pass)
   unsigned long long cmask = 0ull;
+  unsigned smask = 0u;  // test-pass hits of this lane's chunk (4 bits per pair, chunk <= 4)
+  static_assert((NPAIR + TL - 1) / TL <= 8, "smask holds the chunk");
   int cnt_s = 0, chunk = 0, first = 0;
   if (cfg.enable_self_collision) {
     wave_sync();  // union spheres
@@ -866,7 +874,9 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q&
     for (int j = 0; j < chunk && mask; ++j) {
       const int pidx = __builtin_ctzll(mask);
       mask &= mask - 1ull;
-      cnt_s += narrow_pair(q, pidx, margin, [](const float*, float, const float*, float) {});
+      const unsigned hm = narrow_pair<false>(q, pidx, margin, 0u, [](const float*, float, const float*, float) {});
+      cnt_s += __popc(hm);
+      smask |= hm << (4 * j);
     }
   }
   sp.mark(2);
@@ -908,7 +918,7 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q&
     for (int j = 0; j < chunk && mask; ++j) {
       const int pidx = __builtin_ctzll(mask);
       mask &= mask - 1ull;
-      narrow_pair(q, pidx, margin, [&](const float* x, float sep, const float* nn, float code) {
+      narrow_pair<true>(q, pidx, margin, (smask >> (4 * j)) & 15u, [&](const float* x, float sep, const float* nn, float code) {
         if (pos < end) {
           q.cand(pos, 0) = make_float4(x[0], x[1], x[2], sep);
           q.cand(pos, 1) = make_float4(nn[0], nn[1], nn[2], code);
