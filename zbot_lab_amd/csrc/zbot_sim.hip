@@ -500,15 +500,25 @@ constexpr int NCAND = NL * 4 + NSELF;
 //   LOGR  [EPW][ACC] f32    episode-log row of a resetting env (log_flush)
 //   CARRY [EPW][CARRY_W] f32  the env's MDP state rows, prefetched in the prologue (carry_prefetch)
 constexpr int YG_OFF = 0;
-constexpr int AUX_OFF = YG_OFF + NCM * WGT;
+// contact-row granules: slot stride WGT + YG_PAD float4. The PGS reads slot c as one contiguous
+// run (lane -> granule); the contact-row builder (lane c writes granules d = 0..15 of slot c)
+// would put all lanes of a write on the same banks with a 1-KB stride; the pad staggers them.
+#ifndef ZB_YG_PAD
+#define ZB_YG_PAD 1
+#endif
+constexpr int YGS = WGT + ZB_YG_PAD;
+constexpr int AUX_OFF = YG_OFF + NCM * YGS;
 constexpr int LAM_OFF = AUX_OFF + NCM * 2 * EPW;
 constexpr int FRC_OFF = LAM_OFF + NCM * EPW;
 constexpr int CAND_OFF = FRC_OFF + NCM * EPW;
 constexpr int MAP_OFF = CAND_OFF + EPW * NCAND * 2;
 constexpr int KEEP_OFF = MAP_OFF + (EPW * NCM + 3) / 4;
 constexpr int BODY_OFF = KEEP_OFF + (EPW * NCAND + 3) / 4;
-constexpr int JNT_OFF = BODY_OFF + NB * 4 * EPW;
-constexpr int UB_OFF = JNT_OFF + ND * 3 * EPW;
+// per-body / per-joint strides padded by one granule: lane b of a team publishes body b (joint b),
+// so unpadded strides of 16 (12) granules would put the team's writes on the same banks
+constexpr int BODY_S = 4 * EPW + ZB_YG_PAD, JNT_S = 3 * EPW + ZB_YG_PAD;
+constexpr int JNT_OFF = BODY_OFF + NB * BODY_S;
+constexpr int UB_OFF = JNT_OFF + ND * JNT_S;
 constexpr int LNK_OFF = UB_OFF + NL * EPW;
 constexpr int PRE_OFF = LNK_OFF + LNK4;  // [EPW] Pre records (prologue -> MDP)
 constexpr int PRE4 = 8;                   // float4 per Pre record (30 floats)
@@ -532,17 +542,17 @@ static_assert(sizeof(Pre) <= 16 * 8, "Pre fits PRE4 granules");
 struct Q {
   float4* b;
   int lane, e, s;
-  __device__ __forceinline__ float4& yg(int c) const { return b[YG_OFF + c * WGT + lane]; }
-  __device__ __forceinline__ float4& yg_at(int c, int d) const { return b[YG_OFF + c * WGT + TL * e + d]; }
+  __device__ __forceinline__ float4& yg(int c) const { return b[YG_OFF + c * YGS + lane]; }
+  __device__ __forceinline__ float4& yg_at(int c, int d) const { return b[YG_OFF + c * YGS + TL * e + d]; }
   __device__ __forceinline__ float4& aux(int c, int h) const { return b[AUX_OFF + (c * 2 + h) * EPW + e]; }
   __device__ __forceinline__ float4& lam(int c) const { return b[LAM_OFF + c * EPW + e]; }
   __device__ __forceinline__ float4& frc(int c) const { return b[FRC_OFF + c * EPW + e]; }
   __device__ __forceinline__ float4& cand(int p, int h) const { return b[CAND_OFF + (e * NCAND + p) * 2 + h]; }
   __device__ __forceinline__ int& map(int c) const { return reinterpret_cast<int*>(b + MAP_OFF)[e * NCM + c]; }
   __device__ __forceinline__ float& keep(int p) const { return reinterpret_cast<float*>(b + KEEP_OFF)[e * NCAND + p]; }
-  __device__ __forceinline__ float4& body(int bb, int r) const { return b[BODY_OFF + (bb * 4 + r) * EPW + e]; }
+  __device__ __forceinline__ float4& body(int bb, int r) const { return b[BODY_OFF + bb * BODY_S + r * EPW + e]; }
   __device__ __forceinline__ float4& frame(int bb, int r) const { return body(bb, r); }
-  __device__ __forceinline__ float4& jnt(int j, int r) const { return b[JNT_OFF + (j * 3 + r) * EPW + e]; }
+  __device__ __forceinline__ float4& jnt(int j, int r) const { return b[JNT_OFF + j * JNT_S + r * EPW + e]; }
   __device__ __forceinline__ const float4* jtab(int j) const { return b + LNK_OFF + JT_OFF + j * 5; }
   __device__ __forceinline__ const float4* btab(int bb) const { return b + LNK_OFF + BT_OFF + bb * 3; }
   __device__ __forceinline__ float4& ub(int l) const { return b[UB_OFF + l * EPW + e]; }
@@ -1070,7 +1080,7 @@ __device__ __forceinline__ void sens_store(const Q& q, float* __restrict__ st, i
 #define ZB_CARRY 1
 #endif
 constexpr int STG_LEN = 88 + 25 + 3;  // >= max state dim + max obs dim + {reward, term, trunc}
-static_assert(EPW * STG_LEN <= NCM * WGT * 4, "staging fits the contact-row area");
+static_assert(EPW * STG_LEN <= NCM * YGS * 4, "staging fits the contact-row area");
 __device__ __forceinline__ float& Q::stg(int k) const { return reinterpret_cast<float*>(b + YG_OFF)[e * STG_LEN + k]; }
 template <int SD, int OD>
 __device__ __forceinline__ void staged_store(const Q& q, int env0, int N, float* __restrict__ st,
