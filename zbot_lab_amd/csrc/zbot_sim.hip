@@ -507,10 +507,12 @@ constexpr int YG_OFF = 0;
 #define ZB_YG_PAD 1
 #endif
 constexpr int YGS = WGT + ZB_YG_PAD;
+// per-slot records written by lane c (slot c) and read team-uniformly: slot strides padded too
+constexpr int AUX_S = 2 * EPW + ZB_YG_PAD, LAM_S = EPW + ZB_YG_PAD;
 constexpr int AUX_OFF = YG_OFF + NCM * YGS;
-constexpr int LAM_OFF = AUX_OFF + NCM * 2 * EPW;
-constexpr int FRC_OFF = LAM_OFF + NCM * EPW;
-constexpr int CAND_OFF = FRC_OFF + NCM * EPW;
+constexpr int LAM_OFF = AUX_OFF + NCM * AUX_S;
+constexpr int FRC_OFF = LAM_OFF + NCM * LAM_S;
+constexpr int CAND_OFF = FRC_OFF + NCM * LAM_S;
 constexpr int MAP_OFF = CAND_OFF + EPW * NCAND * 2;
 constexpr int KEEP_OFF = MAP_OFF + (EPW * NCM + 3) / 4;
 constexpr int BODY_OFF = KEEP_OFF + (EPW * NCAND + 3) / 4;
@@ -544,9 +546,9 @@ struct Q {
   int lane, e, s;
   __device__ __forceinline__ float4& yg(int c) const { return b[YG_OFF + c * YGS + lane]; }
   __device__ __forceinline__ float4& yg_at(int c, int d) const { return b[YG_OFF + c * YGS + TL * e + d]; }
-  __device__ __forceinline__ float4& aux(int c, int h) const { return b[AUX_OFF + (c * 2 + h) * EPW + e]; }
-  __device__ __forceinline__ float4& lam(int c) const { return b[LAM_OFF + c * EPW + e]; }
-  __device__ __forceinline__ float4& frc(int c) const { return b[FRC_OFF + c * EPW + e]; }
+  __device__ __forceinline__ float4& aux(int c, int h) const { return b[AUX_OFF + c * AUX_S + h * EPW + e]; }
+  __device__ __forceinline__ float4& lam(int c) const { return b[LAM_OFF + c * LAM_S + e]; }
+  __device__ __forceinline__ float4& frc(int c) const { return b[FRC_OFF + c * LAM_S + e]; }
   __device__ __forceinline__ float4& cand(int p, int h) const { return b[CAND_OFF + (e * NCAND + p) * 2 + h]; }
   __device__ __forceinline__ int& map(int c) const { return reinterpret_cast<int*>(b + MAP_OFF)[e * NCM + c]; }
   __device__ __forceinline__ float& keep(int p) const { return reinterpret_cast<float*>(b + KEEP_OFF)[e * NCAND + p]; }
