@@ -1357,6 +1357,11 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
   sp.mark(3);
   float Li[NV];
 #if ZB_TEAM_CHOL
+  // this lane's M row entries of the joint columns, kept for a re-factorisation of the trailing
+  // block if a drive saturates (the contact-row granules are dead until the rows are rebuilt)
+  float4* stash = q.b + YG_OFF + 2 * q.lane;
+  stash[0] = make_float4(R[6], R[7], R[8], R[9]);
+  stash[1] = make_float4(R[10], R[11], 0.f, 0.f);
   cholesky_team(R, L, Li);
 #else
   cholesky_inplace(L, Li);
@@ -1393,6 +1398,27 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
       }
     }
     if (sat) {
+#if ZB_TEAM_CHOL
+      // M changes only on the saturated joints' diagonals (joint coordinates 6..11, the last
+      // ones), so L's leading columns are unchanged: re-factor the trailing 6x6 block from the
+      // stashed rows (= the oracle's full re-factorisation), then re-solve the trailing
+      // coordinates of w (w[0..5] are unchanged too)
+      const float4 s0 = stash[0], s1 = stash[1];
+      const float rt[ND] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y};
+#pragma unroll
+      for (int jj = 0; jj < ND; ++jj) R[6 + jj] = rt[jj] - ((((sat >> jj) & 1u) != 0u && q.s == jj) ? arm : 0.f);
+      team_chol_col<6>(R, L, Li); team_chol_col<7>(R, L, Li); team_chol_col<8>(R, L, Li);
+      team_chol_col<9>(R, L, Li); team_chol_col<10>(R, L, Li); team_chol_col<11>(R, L, Li);
+      float z[NV];
+      fwd_sub(L, Li, b, z);  // only z[0..5] (unchanged) and z[6..11] feed w[6..11] below
+#pragma unroll
+      for (int i = 6; i < NV; ++i) {
+        float t = z[i];
+#pragma unroll
+        for (int k = i; k < NV; ++k) t += L[tri(k, i)] * u[k];
+        w[i] = t;
+      }
+#else
       if (sat & 1u) chol_downdate<6>(L, Li, arm);
       if (sat & 2u) chol_downdate<7>(L, Li, arm);
       if (sat & 4u) chol_downdate<8>(L, Li, arm);
@@ -1404,6 +1430,7 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
       fwd_sub(L, Li, b, z);
 #pragma unroll
       for (int a = 0; a < NV; ++a) w[a] += z[a];
+#endif
     }
   }
 
