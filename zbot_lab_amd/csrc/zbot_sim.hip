@@ -3635,10 +3635,29 @@ __global__ void zb_finalize_kernel(int N, float* __restrict__ st, float* __restr
                                    const uint8_t* __restrict__ term, const uint8_t* __restrict__ trunc) {
   const uint64_t ctr = cnt->calls;
   const uint64_t steps = cnt->steps + (is_step ? 1 : 0);
-  __shared__ float acc_sum[ACC];  // the accumulator slots folded (acc_slot)
+  // fold the accumulator slots (acc_slot): 8 groups of 8 slots x ACC_STRIDE entries, one
+  // thread per (group, entry), which also clears what it read; then a shared sum of the groups
+  constexpr int FG = 8, FS = ACC_SLOTS / FG;
+  static_assert(FG * ACC_STRIDE <= 256 && ACC_SLOTS % FG == 0, "finalize fold layout");
+  __shared__ float acc_part[FG][ACC_STRIDE];
+  __shared__ float acc_sum[ACC];
+  if (threadIdx.x < FG * ACC_STRIDE) {
+    const int g = threadIdx.x / ACC_STRIDE, t = threadIdx.x % ACC_STRIDE;
+    float v[FS];
+#pragma unroll
+    for (int k = 0; k < FS; ++k) v[k] = acc[(g * FS + k) * ACC_STRIDE + t];
+#pragma unroll
+    for (int k = 0; k < FS; ++k) acc[(g * FS + k) * ACC_STRIDE + t] = 0.f;
+    float sum = 0.f;
+#pragma unroll
+    for (int k = 0; k < FS; ++k) sum += v[k];
+    acc_part[g][t] = sum;
+  }
+  __syncthreads();
   if (threadIdx.x < ACC) {
     float v = 0.f;
-    for (int k = 0; k < ACC_SLOTS; ++k) v += acc[k * ACC_STRIDE + threadIdx.x];
+#pragma unroll
+    for (int g = 0; g < FG; ++g) v += acc_part[g][threadIdx.x];
     acc_sum[threadIdx.x] = v;
   }
   __syncthreads();
@@ -3718,7 +3737,6 @@ __global__ void zb_finalize_kernel(int N, float* __restrict__ st, float* __restr
     }
   }
   __syncthreads();
-  for (int k = threadIdx.x; k < ACC_SLOTS * ACC_STRIDE; k += blockDim.x) acc[k] = 0.f;
   if (threadIdx.x == 0) cnt->calls = ctr + 1;
   // lin_vel_cmd_levels widened the ranges in this step: the reference's curriculum runs before the
   // command manager resamples the reset envs, so their commands (and the metrics / observations
