@@ -371,6 +371,9 @@ constexpr int TL = 16;           // lanes per env
 #ifndef ZB_EPW
 #define ZB_EPW 4
 #endif
+#ifndef ZB_PGS_UNROLL
+#define ZB_PGS_UNROLL 1  // PGS slots unrolled (1) or the flattened ping-pong loop (0)
+#endif
 #ifndef ZB_TEAM_CHOL
 #define ZB_TEAM_CHOL 1  // cholesky_team (1) or the redundant per-lane cholesky_inplace (0)
 #endif
@@ -1506,6 +1509,30 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
 #pragma unroll
     for (int d = 0; d < NV; ++d) wd = q.s == d ? w[d] : wd;
     const bool lead = q.s == 0;
+#if ZB_PGS_UNROLL
+    // sweeps outer, the NCM slots unrolled inner: constant LDS offsets (no per-update index /
+    // address arithmetic), slot c >= the wave's largest contact count skipped uniformly, slots
+    // past this env's count masked; the same update order as the flattened loop below
+    const int ncw = max(max(__builtin_amdgcn_readlane(nc, 0), __builtin_amdgcn_readlane(nc, TL)),
+                        max(__builtin_amdgcn_readlane(nc, 2 * TL), __builtin_amdgcn_readlane(nc, 3 * TL)));
+    for (int it = 0; it < cfg.solver_iterations; ++it) {
+      // slot c + 1's granules and impulse are read (unconditionally: the LDS slots exist) while
+      // slot c updates
+      float4 G = q.yg(0), X = q.aux(0, 0), Z = q.aux(0, 1), La = q.lam(0);
+#pragma unroll
+      for (int c = 0; c < NCM; ++c) {
+        const int cn = c + 1 < NCM ? c + 1 : c;
+        const float4 Gn = q.yg(cn), Xn = q.aux(cn, 0), Zn = q.aux(cn, 1), Ln = q.lam(cn);
+        if (c < ncw) {
+          if (c < nc) {
+            const float4 nA = pgs_update(G, X, Z, La, kLinkFriction ? Z.z : mu, wd);
+            if (lead) q.lam(c) = nA;
+          }
+        }
+        G = Gn; X = Xn; Z = Zn; La = Ln;
+      }
+    }
+#else
     const int K = cfg.solver_iterations * nc;
     int cA = 0;
     float4 GA = q.yg(0), XA = q.aux(0, 0), ZA = q.aux(0, 1), LA = q.lam(0);
@@ -1526,6 +1553,7 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
         cA = cA2;
       }
     }
+#endif
     w[0] = tb<0>(wd); w[1] = tb<1>(wd); w[2] = tb<2>(wd); w[3] = tb<3>(wd);
     w[4] = tb<4>(wd); w[5] = tb<5>(wd); w[6] = tb<6>(wd); w[7] = tb<7>(wd);
     w[8] = tb<8>(wd); w[9] = tb<9>(wd); w[10] = tb<10>(wd); w[11] = tb<11>(wd);
