@@ -2747,6 +2747,13 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_v4_step_kernel(
   for (int a = 0; a < 4; ++a) p.quat[a] = ST(ZB_S_ROOT_QUAT + a);
 #pragma unroll
   for (int j = 0; j < ND; ++j) { p.jq[j] = ST(ZB_S_JOINT_POS + j); p.jqd[j] = ST(ZB_S_JOINT_VEL + j); }
+#if ZB_CARRY
+  const float* cst = carry_prefetch<ZB_V4_STATE_DIM>(q, st, N, i);
+#define CST(f) cst[f]
+#else
+  const float* cst = st;
+#define CST(f) ST(f)
+#endif
 
   // _pre_physics_step (v4.py:776-804, mode 1)
   const bool writer = q.s == 0;
@@ -2795,32 +2802,32 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_v4_step_kernel(
   bool in_contact[2];
 #pragma unroll
   for (int f = 0; f < 2; ++f) {
-    air_cur[f] = ST(ZB_V4_FEET_AIR_CUR + f);
-    con_cur[f] = ST(ZB_V4_FEET_CONTACT_CUR + f);
-    air_last[f] = ST(ZB_V4_FEET_AIR_LAST + f);
-    con_last[f] = ST(ZB_V4_FEET_CONTACT_LAST + f);
+    air_cur[f] = CST(ZB_V4_FEET_AIR_CUR + f);
+    con_cur[f] = CST(ZB_V4_FEET_CONTACT_CUR + f);
+    air_last[f] = CST(ZB_V4_FEET_AIR_LAST + f);
+    con_last[f] = CST(ZB_V4_FEET_CONTACT_LAST + f);
   }
-  sens_replay<ZB_V4_HIST>(q, st, N, i, ZB_V4_FEET_FZ_HIST, ZB_V4_UNDES_FMAX_HIST, cfg.decimation, cfg.sim_dt,
+  sens_replay<ZB_V4_HIST>(q, ZB_CARRY ? cst : st, ZB_CARRY ? 1 : N, ZB_CARRY ? 0 : i, ZB_V4_FEET_FZ_HIST, ZB_V4_UNDES_FMAX_HIST, cfg.decimation, cfg.sim_dt,
                           cfg.contact_force_threshold, fz_sum, fm_max, air_cur, air_last, con_cur, con_last);
 #pragma unroll
   for (int f = 0; f < 2; ++f) {
     in_contact[f] = con_cur[f] > 0.f;
     feetF[f] = fz_sum[f] / (float)ZB_V4_HIST;  // mean over the history (v4.py:846-849)
   }
-  const float ep_len = ST(ZB_V4_EP_LEN) + 1.f;
-  float cmd[2] = {ST(ZB_V4_COMMANDS), ST(ZB_V4_COMMANDS + 1)};
-  float tgt = ST(ZB_V4_TARGET_YAW);
-  float ileft = ST(ZB_V4_INTERVAL_LEFT);
-  float f_last[2] = {ST(ZB_V4_FEET_F_LAST), ST(ZB_V4_FEET_F_LAST + 1)};
-  float step_len[2] = {ST(ZB_V4_FEET_STEP_LEN), ST(ZB_V4_FEET_STEP_LEN + 1)};
+  const float ep_len = CST(ZB_V4_EP_LEN) + 1.f;
+  float cmd[2] = {CST(ZB_V4_COMMANDS), CST(ZB_V4_COMMANDS + 1)};
+  float tgt = CST(ZB_V4_TARGET_YAW);
+  float ileft = CST(ZB_V4_INTERVAL_LEFT);
+  float f_last[2] = {CST(ZB_V4_FEET_F_LAST), CST(ZB_V4_FEET_F_LAST + 1)};
+  float step_len[2] = {CST(ZB_V4_FEET_STEP_LEN), CST(ZB_V4_FEET_STEP_LEN + 1)};
   float down[2][3];
 #pragma unroll
   for (int f = 0; f < 2; ++f)
 #pragma unroll
-    for (int a = 0; a < 3; ++a) down[f][a] = ST(ZB_V4_FEET_DOWN_POS + 3 * f + a);
+    for (int a = 0; a < 3; ++a) down[f][a] = CST(ZB_V4_FEET_DOWN_POS + 3 * f + a);
   float sums0[ZB_V4_NUM_REWARD_TERMS];
 #pragma unroll
-  for (int t = 0; t < ZB_V4_NUM_REWARD_TERMS; ++t) sums0[t] = ST(ZB_V4_EP_SUMS + t);
+  for (int t = 0; t < ZB_V4_NUM_REWARD_TERMS; ++t) sums0[t] = CST(ZB_V4_EP_SUMS + t);
   const int stage = cnt->stage;
 
   // _compute_intermediate_values (v4.py:809-849) on the post-step state
@@ -3021,7 +3028,7 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_v4_step_kernel(
       OUT(ZB_V4_FEET_CONTACT_LAST + f) = live(con_last[f]);
 
     }
-    sens_store<ZB_V4_HIST>(q, st, N, i, ZB_V4_FEET_FZ_HIST, ZB_V4_UNDES_FMAX_HIST, cfg.decimation, reset,
+    sens_store<ZB_V4_HIST>(q, ZB_CARRY ? cst : st, ZB_CARRY ? 1 : N, ZB_CARRY ? 0 : i, ZB_V4_FEET_FZ_HIST, ZB_V4_UNDES_FMAX_HIST, cfg.decimation, reset,
                            [&](int row, float v) { OUT(row) = v; });
     OUT(ZB_V4_EP_LEN) = live(ep_len);
 #pragma unroll
@@ -3059,6 +3066,7 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_v4_step_kernel(
   sp.mark(8);
   sp.flush();
 #undef ST
+#undef CST
 }
 
 // explicit resets / construction (init = 1 also draws the interval-event timers, as Isaac Lab's
@@ -3228,6 +3236,12 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_m_step_kernel(
   for (int a = 0; a < 4; ++a) p.quat[a] = ST(ZB_S_ROOT_QUAT + a);
 #pragma unroll
   for (int j = 0; j < ND; ++j) { p.jq[j] = ST(ZB_S_JOINT_POS + j); p.jqd[j] = ST(ZB_S_JOINT_VEL + j); }
+#if ZB_CARRY
+  const float* cst = carry_prefetch<ZB_M_STATE_DIM>(q, st, N, i);
+#define CST(f) cst[f]
+#else
+#define CST(f) ST(f)
+#endif
   if (q.s < NL) q.fric(q.s) = ST(ZB_M_LINK_MU + q.s);
 
   // ActionManager.process_action: RelativeJointPositionAction (scale 0.04 pi, zero offset, clip
@@ -3297,17 +3311,17 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_m_step_kernel(
   const PreM pr = pv;
   st = opaque_ptr(st);
 
-  const float ep_len = ST(ZB_M_EP_LEN) + 1.f;
-  float cmd[3] = {ST(ZB_M_COMMANDS), ST(ZB_M_COMMANDS + 1), ST(ZB_M_COMMANDS + 2)};
-  float tleft = ST(ZB_M_CMD_TIME_LEFT), standing = ST(ZB_M_CMD_STANDING);
-  float met[2] = {ST(ZB_M_METRICS), ST(ZB_M_METRICS + 1)};
-  float f_last[2] = {ST(ZB_M_FEET_F_LAST), ST(ZB_M_FEET_F_LAST + 1)};
-  float step_len[2] = {ST(ZB_M_FEET_STEP_LEN), ST(ZB_M_FEET_STEP_LEN + 1)};
+  const float ep_len = CST(ZB_M_EP_LEN) + 1.f;
+  float cmd[3] = {CST(ZB_M_COMMANDS), CST(ZB_M_COMMANDS + 1), CST(ZB_M_COMMANDS + 2)};
+  float tleft = CST(ZB_M_CMD_TIME_LEFT), standing = CST(ZB_M_CMD_STANDING);
+  float met[2] = {CST(ZB_M_METRICS), CST(ZB_M_METRICS + 1)};
+  float f_last[2] = {CST(ZB_M_FEET_F_LAST), CST(ZB_M_FEET_F_LAST + 1)};
+  float step_len[2] = {CST(ZB_M_FEET_STEP_LEN), CST(ZB_M_FEET_STEP_LEN + 1)};
   float down[2][3];
 #pragma unroll
   for (int f = 0; f < 2; ++f)
 #pragma unroll
-    for (int a = 0; a < 3; ++a) down[f][a] = ST(ZB_M_FEET_DOWN_POS + 3 * f + a);
+    for (int a = 0; a < 3; ++a) down[f][a] = CST(ZB_M_FEET_DOWN_POS + 3 * f + a);
 
   // post-step articulation data: root (= base link) pose, link-origin / COM velocity, angular
   // velocity; feet link poses and COM velocities
@@ -3407,7 +3421,7 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_m_step_kernel(
   for (int t = 0; t < ZB_M_NUM_REWARD_TERMS; ++t) {
     const float v = r[t] * cfg.stage_scales[0][t] * step_dt;
     reward += v;
-    sums[t] = ST(ZB_M_EP_SUMS + t) + v;
+    sums[t] = CST(ZB_M_EP_SUMS + t) + v;
   }
   const bool reset = terminated || time_out;
   const uint64_t hs = env_hash(seed, cnt->calls, i);
@@ -3538,6 +3552,7 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_m_step_kernel(
   sp.mark(8);
   sp.flush();
 #undef ST
+#undef CST
 }
 
 // command of a reset env redrawn after lin_vel_cmd_levels widened the ranges (zb_finalize_kernel):
