@@ -380,6 +380,12 @@ constexpr int TL = 16;           // lanes per env
 #ifndef ZB_WAVES_PER_SIMD
 #define ZB_WAVES_PER_SIMD 1
 #endif
+// The manager kernel needs the explicit bound: left at 1 it takes 256 VGPRs + 4 AGPRs (one wave
+// per SIMD); at 2 it fits 256 registers with 16 B/lane of scratch and runs 39 % faster at 8192 envs.
+// The other step kernels fit 256 VGPRs without spilling either way (LDS allows two waves).
+#ifndef ZB_M_WAVES_PER_SIMD
+#define ZB_M_WAVES_PER_SIMD 2
+#endif
 constexpr int EPW = ZB_EPW;      // envs per workgroup (one wave; EPW < 4 leaves lanes idle)
 constexpr int WGT = TL * EPW;    // threads per workgroup
 static_assert(WGT <= WAVE, "one wave per workgroup");
@@ -485,56 +491,74 @@ constexpr int LNK4 = BT_OFF + NB * 3;
 constexpr int NSELF = 18;
 constexpr int NCAND = NL * 4 + NSELF;
 
-// LDS layout of one workgroup (EPW envs), float4 units:
-//   YG    [NCM][WGT]        lane (e, d) of slot c: {Y0[d], Y1[d], Y2[d], 0} (zero for d >= 12)
-//   AUX   [NCM][2][EPW]     {invm0, invm1, invm2, vmin invm0}, {c01 invm1, c02 invm2, mu, 0}
-//   LAM   [NCM][EPW]        contact impulses {ln, l1, l2, 0}
-//   FRC   [NCM][EPW]        last substep: contact force {f, code}
-//   CAND  [EPW][NCAND][2]   candidates {x, sep}, {n, code = 16 la + lb + 1}
-//   MAP   [EPW][NCM] int    overflow only: solver slot -> candidate position
-//   KEEP  [EPW][NCAND] f32  overflow only: kept flags
+// LDS layout of one workgroup (EPW envs), float4 units. Phase-disjoint buffers share storage so
+// that a workgroup needs <= 20 KB: with 253 VGPRs that lets two waves share a SIMD (8 per CU)
+// once a launch has more than one wave per SIMD (N > 4096 envs).
+//   region U (per substep: detection -> contact rows -> PGS; then the epilogue)
+//     CAND  [EPW][NCAND][2]  candidates {x, sep}, {n, code = 16 la + lb + 1}     detection .. row read
+//     MAP   [EPW][NCM] int   overflow only: solver slot -> candidate position     detection .. row read
+//     KEEP  [EPW][NCAND] u8  overflow only: kept flags                            detection
+//     YG    [NCM][EPW*NV+1]  granule (e, d) of slot c: {Y0[d], Y1[d], Y2[d], 0};  row write .. PGS
+//                            the trailing granule of a slot is zero (lanes d >= NV read it)
+//     STG   [EPW][STG_LEN] f32, LOGR [EPW][ACC] f32                              epilogue only
+//   region V
+//     UB    [NL][EPW]        world union spheres                                  detection only
+//     stash [WGT][2]         M rows of the joint columns (saturated drives)       Cholesky .. re-solve
+//     AUX   [NCM][2][EPW]    {invm0, invm1, invm2, vmin invm0}, {c01 invm1, c02 invm2, mu, 0}
+//     LAM   [NCM][EPW]       contact impulses {ln, l1, l2, 0}                     row write .. sensor
+//     FRC   [NCM][EPW]       contact normal + code (row builder), then force {f, code} (sensor)
 //   BODY  [NB][4][EPW]      body poses {R row 0, p.x}, {R row 1, p.y}, {R row 2, p.z}, {quat}
 //   JNT   [ND][3][EPW]      joints {a, o.x}, {o x a, o.y}, {o.z, -}
-//   UB    [NL][EPW]         world union spheres
-//   LNK   [LNK4]            link table copy
+//   LNK   [LNK4 - NL*LINK4] pair codes, default pose, joint / body tables (the per-link collision
+//                           table is read from global memory: L1-resident, 3 KB)
 //   PRE   [EPW][PRE4]       prologue results parked across the physics
 //   FRIC  [EPW][NL] f32     per-link friction coefficients (standup)
 //   SENS  [EPW][MAXSUB][2]  per-substep contact-sensor record {fz0, fz1, |F0|, |F1|}, {undesired max |F|}
-//   LOGR  [EPW][ACC] f32    episode-log row of a resetting env (log_flush)
 //   CARRY [EPW][CARRY_W] f32  the env's MDP state rows, prefetched in the prologue (carry_prefetch)
-constexpr int YG_OFF = 0;
-// contact-row granules: slot stride WGT + YG_PAD float4. The PGS reads slot c as one contiguous
-// run (lane -> granule); the contact-row builder (lane c writes granules d = 0..15 of slot c)
-// would put all lanes of a write on the same banks with a 1-KB stride; the pad staggers them.
 #ifndef ZB_YG_PAD
 #define ZB_YG_PAD 1
 #endif
-constexpr int YGS = WGT + ZB_YG_PAD;
-// per-slot records written by lane c (slot c) and read team-uniformly: slot strides padded too
-constexpr int AUX_S = 2 * EPW + ZB_YG_PAD, LAM_S = EPW + ZB_YG_PAD;
-constexpr int AUX_OFF = YG_OFF + NCM * YGS;
-constexpr int LAM_OFF = AUX_OFF + NCM * AUX_S;
-constexpr int FRC_OFF = LAM_OFF + NCM * LAM_S;
-constexpr int CAND_OFF = FRC_OFF + NCM * LAM_S;
+constexpr int CAND_OFF = 0;
 constexpr int MAP_OFF = CAND_OFF + EPW * NCAND * 2;
 constexpr int KEEP_OFF = MAP_OFF + (EPW * NCM + 3) / 4;
-constexpr int BODY_OFF = KEEP_OFF + (EPW * NCAND + 3) / 4;
+constexpr int CAND_END = KEEP_OFF + (EPW * NCAND + 15) / 16;
+constexpr int YG_OFF = 0;
+// contact-row slot stride: EPW * NV granules + the zero granule. The PGS reads slot c as one
+// contiguous run (lane (e, d) -> granule e NV + d); the stride is odd, so the contact-row
+// builder's writes (lane c writes granules d = 0..NV-1 of slot c) do not land on one bank group.
+constexpr int YGS = EPW * NV + 1;
+constexpr int YG_END = YG_OFF + NCM * YGS;
+constexpr int U_END = CAND_END > YG_END ? CAND_END : YG_END;
+// per-slot records written by lane c (slot c) and read team-uniformly: slot strides padded
+constexpr int AUX_S = 2 * EPW + ZB_YG_PAD, LAM_S = EPW + ZB_YG_PAD;
+constexpr int V_OFF = U_END;
+constexpr int UB_OFF = V_OFF;       // detection only
+constexpr int STASH_OFF = V_OFF;    // Cholesky .. saturated re-solve (after detection, before rows)
+constexpr int AUX_OFF = V_OFF;
+constexpr int LAM_OFF = AUX_OFF + NCM * AUX_S;
+constexpr int FRC_OFF = LAM_OFF + NCM * LAM_S;
+constexpr int V_END = FRC_OFF + NCM * LAM_S;
+static_assert(NL * EPW <= NCM * AUX_S + NCM * LAM_S, "UB fits below FRC");
+static_assert(2 * WGT <= NCM * AUX_S + NCM * LAM_S, "stash fits below FRC");
+constexpr int BODY_OFF = V_END;
 // per-body / per-joint strides padded by one granule: lane b of a team publishes body b (joint b),
 // so unpadded strides of 16 (12) granules would put the team's writes on the same banks
 constexpr int BODY_S = 4 * EPW + ZB_YG_PAD, JNT_S = 3 * EPW + ZB_YG_PAD;
 constexpr int JNT_OFF = BODY_OFF + NB * BODY_S;
-constexpr int UB_OFF = JNT_OFF + ND * JNT_S;
-constexpr int LNK_OFF = UB_OFF + NL * EPW;
+constexpr int LNK_G = NL * LINK4;      // link-table granules read from global memory
+constexpr int LNK_OFF = JNT_OFF + ND * JNT_S - LNK_G;  // lds[LNK_OFF + t] = links[t] for t >= LNK_G
 constexpr int PRE_OFF = LNK_OFF + LNK4;  // [EPW] Pre records (prologue -> MDP)
 constexpr int PRE4 = 8;                   // float4 per Pre record (30 floats)
 constexpr int FRIC_OFF = PRE_OFF + EPW * PRE4;  // [EPW][NL] f32 per-link friction (standup)
 constexpr int MAXSUB = 8;                 // decimation limit (zb_create checks)
 constexpr int SENS_OFF = FRIC_OFF + (EPW * NL + 3) / 4;
-constexpr int LOGR_OFF = SENS_OFF + EPW * MAXSUB * 2;
 constexpr int LOGR_W = ZB_MAX_REWARD_TERMS + 8;  // = ACC (episode-log entries, defined with the step kernels)
 constexpr int CARRY0 = ZB_S_P_DELTA, CARRY_W = 64;  // state rows [CARRY0, CARRY0 + CARRY_W)
-constexpr int CARRY_OFF = LOGR_OFF + EPW * LOGR_W / 4;
+constexpr int CARRY_OFF = SENS_OFF + EPW * MAXSUB * 2;
 constexpr int LDS4 = CARRY_OFF + EPW * CARRY_W / 4;
+constexpr int STG_LEN = 88 + 25 + 3;  // >= max state dim + max obs dim + {reward, term, trunc}
+constexpr int LOGR_OFF = (EPW * STG_LEN + 3) / 4;  // region U, after STG
+static_assert(LOGR_OFF + EPW * LOGR_W / 4 <= U_END, "STG + LOGR fit region U");
 
 // prologue results the MDP reads after the physics (parked in LDS across the substeps)
 struct Pre {
@@ -547,21 +571,25 @@ static_assert(sizeof(Pre) <= 16 * 8, "Pre fits PRE4 granules");
 struct Q {
   float4* b;
   int lane, e, s;
-  __device__ __forceinline__ float4& yg(int c) const { return b[YG_OFF + c * YGS + lane]; }
-  __device__ __forceinline__ float4& yg_at(int c, int d) const { return b[YG_OFF + c * YGS + TL * e + d]; }
+  const float4* gl;   // per-link collision table (global memory)
+  // this lane's contact-row granule in a slot (the zero granule for s >= NV)
+  __device__ __forceinline__ int ygl() const { return s < NV ? NV * e + s : EPW * NV; }
+  __device__ __forceinline__ float4& yg(const float4* y, int c) const { return const_cast<float4*>(y)[c * YGS]; }
+  __device__ __forceinline__ float4& yg_at(int c, int d) const { return b[YG_OFF + c * YGS + NV * e + d]; }
+  __device__ __forceinline__ float4& yg_zero(int c) const { return b[YG_OFF + c * YGS + EPW * NV]; }
   __device__ __forceinline__ float4& aux(int c, int h) const { return b[AUX_OFF + c * AUX_S + h * EPW + e]; }
   __device__ __forceinline__ float4& lam(int c) const { return b[LAM_OFF + c * LAM_S + e]; }
   __device__ __forceinline__ float4& frc(int c) const { return b[FRC_OFF + c * LAM_S + e]; }
   __device__ __forceinline__ float4& cand(int p, int h) const { return b[CAND_OFF + (e * NCAND + p) * 2 + h]; }
   __device__ __forceinline__ int& map(int c) const { return reinterpret_cast<int*>(b + MAP_OFF)[e * NCM + c]; }
-  __device__ __forceinline__ float& keep(int p) const { return reinterpret_cast<float*>(b + KEEP_OFF)[e * NCAND + p]; }
+  __device__ __forceinline__ unsigned char& keep(int p) const { return reinterpret_cast<unsigned char*>(b + KEEP_OFF)[e * NCAND + p]; }
   __device__ __forceinline__ float4& body(int bb, int r) const { return b[BODY_OFF + bb * BODY_S + r * EPW + e]; }
   __device__ __forceinline__ float4& frame(int bb, int r) const { return body(bb, r); }
   __device__ __forceinline__ float4& jnt(int j, int r) const { return b[JNT_OFF + j * JNT_S + r * EPW + e]; }
   __device__ __forceinline__ const float4* jtab(int j) const { return b + LNK_OFF + JT_OFF + j * 5; }
   __device__ __forceinline__ const float4* btab(int bb) const { return b + LNK_OFF + BT_OFF + bb * 3; }
   __device__ __forceinline__ float4& ub(int l) const { return b[UB_OFF + l * EPW + e]; }
-  __device__ __forceinline__ const float4* link(int l) const { return b + LNK_OFF + l * LINK4; }
+  __device__ __forceinline__ const float4* link(int l) const { return gl + l * LINK4; }
   __device__ __forceinline__ int pair_code(int p) const { return reinterpret_cast<const int*>(b + LNK_OFF + NL * LINK4)[p]; }
   __device__ __forceinline__ const float4* dflt() const { return b + LNK_OFF + DFLT_OFF; }
   __device__ __forceinline__ Pre& pre() const { return *reinterpret_cast<Pre*>(b + PRE_OFF + e * PRE4); }
@@ -571,6 +599,11 @@ struct Q {
   __device__ __forceinline__ float* logr(int ee) const { return reinterpret_cast<float*>(b + LOGR_OFF) + ee * LOGR_W; }
   __device__ __forceinline__ float* carry() const { return reinterpret_cast<float*>(b + CARRY_OFF) + e * CARRY_W; }
 };
+
+__device__ __forceinline__ Q make_q(float4* lds, int lane, const float4* links) {
+  const int e = lane / TL, s = lane % TL;
+  return Q{lds, lane, e, s, links};
+}
 
 __device__ __forceinline__ void read_frame(const Q& q, int body, float R[9], float p[3]) {
   const float4 a = q.frame(body, 0), b = q.frame(body, 1), c = q.frame(body, 2);
@@ -954,13 +987,13 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q&
           const float sj = q.cand(j, 0).w;
           r += (sj < sp_ || (sj == sp_ && j < p)) ? 1 : 0;
         }
-        q.keep(p) = r < NCM ? 1.f : 0.f;
+        q.keep(p) = r < NCM ? 1 : 0;
       }
     wave_sync();
     if (over && q.s < NCM) {
       int c = 0, pos = -1;
       for (int p = 0; p < n; ++p)
-        if (q.keep(p) != 0.f) {
+        if (q.keep(p) != 0) {
           if (c == q.s) pos = p;
           ++c;
         }
@@ -1084,8 +1117,6 @@ __device__ __forceinline__ void sens_store(const Q& q, float* __restrict__ st, i
 #ifndef ZB_CARRY
 #define ZB_CARRY 1
 #endif
-constexpr int STG_LEN = 88 + 25 + 3;  // >= max state dim + max obs dim + {reward, term, trunc}
-static_assert(EPW * STG_LEN <= NCM * YGS * 4, "staging fits the contact-row area");
 __device__ __forceinline__ float& Q::stg(int k) const { return reinterpret_cast<float*>(b + YG_OFF)[e * STG_LEN + k]; }
 template <int SD, int OD>
 __device__ __forceinline__ void staged_store(const Q& q, int env0, int N, float* __restrict__ st,
@@ -1362,7 +1393,7 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
 #if ZB_TEAM_CHOL
   // this lane's M row entries of the joint columns, kept for a re-factorisation of the trailing
   // block if a drive saturates (the contact-row granules are dead until the rows are rebuilt)
-  float4* stash = q.b + YG_OFF + 2 * q.lane;
+  float4* stash = q.b + STASH_OFF + 2 * q.lane;
   stash[0] = make_float4(R[6], R[7], R[8], R[9]);
   stash[1] = make_float4(R[10], R[11], 0.f, 0.f);
   cholesky_team(R, L, Li);
@@ -1441,12 +1472,17 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
   // contact rows (lane s builds slot s): Y = L^-1 J^T (whitened), effective masses, the
   // normal/tangent cross terms and the bias velocity. J of direction d at point x on body b:
   // [x x d ; d ; d.(a_j x (x - o_j)) for joints j < b]
+  // The candidates share storage with the rows (region U): every lane reads its candidate, then
+  // the wave writes. The normal + code go to FRC for the contact sensor.
   if (q.s < nc) {
     const int c = q.s;
     const int pos = over ? q.map(c) : c;
     float S[ND][6], org[ND][3];
     read_joints(q, S, org);
     const float4 g0 = q.cand(pos, 0), gn = q.cand(pos, 1);
+    wave_sync();  // (all active lanes execute this together: the wave's reads precede its writes)
+    q.frc(c) = gn;
+    q.yg_zero(c) = make_float4(0.f, 0.f, 0.f, 0.f);
     const float x[3] = {g0.x, g0.y, g0.z};
     const float n[3] = {gn.x, gn.y, gn.z};
     const float sep = g0.w;
@@ -1485,8 +1521,6 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
     }
 #pragma unroll
     for (int d = 0; d < NV; ++d) q.yg_at(c, d) = make_float4(Y[0][d], Y[1][d], Y[2][d], 0.f);
-#pragma unroll
-    for (int d = NV; d < TL; ++d) q.yg_at(c, d) = make_float4(0.f, 0.f, 0.f, 0.f);
     float vmin;
     if (sep >= 0.f) vmin = -sep / dt;
     else vmin = fminf(cfg.baumgarte * (-sep) / dt, m->max_depenetration_velocity);
@@ -1505,6 +1539,7 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
   // computes. With one contact the prefetched impulse is the one being updated (forwarded).
   {
     const float mu = cfg.friction;
+    const float4* yl = q.b + YG_OFF + q.ygl();
     float wd = 0.f;
 #pragma unroll
     for (int d = 0; d < NV; ++d) wd = q.s == d ? w[d] : wd;
@@ -1518,11 +1553,11 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
     for (int it = 0; it < cfg.solver_iterations; ++it) {
       // slot c + 1's granules and impulse are read (unconditionally: the LDS slots exist) while
       // slot c updates
-      float4 G = q.yg(0), X = q.aux(0, 0), Z = q.aux(0, 1), La = q.lam(0);
+      float4 G = q.yg(yl, 0), X = q.aux(0, 0), Z = q.aux(0, 1), La = q.lam(0);
 #pragma unroll
       for (int c = 0; c < NCM; ++c) {
         const int cn = c + 1 < NCM ? c + 1 : c;
-        const float4 Gn = q.yg(cn), Xn = q.aux(cn, 0), Zn = q.aux(cn, 1), Ln = q.lam(cn);
+        const float4 Gn = q.yg(yl, cn), Xn = q.aux(cn, 0), Zn = q.aux(cn, 1), Ln = q.lam(cn);
         if (c < ncw) {
           if (c < nc) {
             const float4 nA = pgs_update(G, X, Z, La, kLinkFriction ? Z.z : mu, wd);
@@ -1535,17 +1570,17 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
 #else
     const int K = cfg.solver_iterations * nc;
     int cA = 0;
-    float4 GA = q.yg(0), XA = q.aux(0, 0), ZA = q.aux(0, 1), LA = q.lam(0);
+    float4 GA = q.yg(yl, 0), XA = q.aux(0, 0), ZA = q.aux(0, 1), LA = q.lam(0);
     for (int k = 0; k < K; k += 2) {
       const int cB = cA + 1 == nc ? 0 : cA + 1;
-      const float4 GB = q.yg(cB), XB = q.aux(cB, 0), ZB = q.aux(cB, 1);
+      const float4 GB = q.yg(yl, cB), XB = q.aux(cB, 0), ZB = q.aux(cB, 1);
       float4 LB = q.lam(cB);
       const float4 nA = pgs_update(GA, XA, ZA, LA, kLinkFriction ? ZA.z : mu, wd);
       if (lead) q.lam(cA) = nA;
       if (cB == cA) LB = nA;
       if (k + 1 < K) {
         const int cA2 = cB + 1 == nc ? 0 : cB + 1;
-        GA = q.yg(cA2); XA = q.aux(cA2, 0); ZA = q.aux(cA2, 1);
+        GA = q.yg(yl, cA2); XA = q.aux(cA2, 0); ZA = q.aux(cA2, 1);
         LA = q.lam(cA2);
         const float4 nB = pgs_update(GB, XB, ZB, LB, kLinkFriction ? ZB.z : mu, wd);
         if (lead) q.lam(cB) = nB;
@@ -1567,8 +1602,7 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
     // ContactSensor inputs: net force on the feet, max |net force| over undesired links.
     // Lane s forms the force of slot s, then sums the env's contacts onto link s.
     if (q.s < nc) {
-      const int pos = over ? q.map(q.s) : q.s;
-      const float4 gn = q.cand(pos, 1), lam = q.lam(q.s);
+      const float4 gn = q.frc(q.s), lam = q.lam(q.s);
       const float n[3] = {gn.x, gn.y, gn.z};
       float t1[3], t2[3];
       tangents(n, t1, t2);
@@ -1979,8 +2013,8 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_step_kernel(const z
   // a team past N recomputes env N-1 (identical values, identical stores); it never logs
   const int i = env < N ? env : N - 1;
   const bool lead = env < N && lane % TL == 0;
-  const Q q{lds, lane, lane / TL, lane % TL};
-  for (int t = lane; t < LNK4; t += WGT) lds[LNK_OFF + t] = links[t];
+  const Q q = make_q(lds, lane, links);
+  for (int t = LNK_G + lane; t < LNK4; t += WGT) lds[LNK_OFF + t] = links[t];
   // the env's state row: lane s loads fields s, s+16, ... (one coalesced load per field group)
   Stamps sp;
   sp.begin();
@@ -2332,8 +2366,8 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_substeps_kernel(con
   const int lane = threadIdx.x;
   const int env = xcd_block(blockIdx.x, gridDim.x) * EPW + lane / TL;
   const int i = env < N ? env : N - 1;
-  const Q q{lds, lane, lane / TL, lane % TL};
-  for (int t = lane; t < LNK4; t += WGT) lds[LNK_OFF + t] = links[t];
+  const Q q = make_q(lds, lane, links);
+  for (int t = LNK_G + lane; t < LNK4; t += WGT) lds[LNK_OFF + t] = links[t];
   const int mu_row = cfg.task == ZB_TASK_MANAGER_V0 ? ZB_M_LINK_MU : ZB_SU_LINK_MU;
   if (kLinkFriction && q.s < NL) q.fric(q.s) = st[(size_t)(mu_row + q.s) * N + i];
   Phys p;
@@ -2445,8 +2479,8 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_su_step_kernel(
   const int env = xcd_block(blockIdx.x, gridDim.x) * EPW + lane / TL;
   const int i = env < N ? env : N - 1;
   const bool lead = env < N && lane % TL == 0;
-  const Q q{lds, lane, lane / TL, lane % TL};
-  for (int t = lane; t < LNK4; t += WGT) lds[LNK_OFF + t] = links[t];
+  const Q q = make_q(lds, lane, links);
+  for (int t = LNK_G + lane; t < LNK4; t += WGT) lds[LNK_OFF + t] = links[t];
   Stamps sp;
   sp.begin();
 #define ST(f) st[(size_t)(f) * N + i]
@@ -2735,8 +2769,8 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_v4_step_kernel(
   const int env = xcd_block(blockIdx.x, gridDim.x) * EPW + lane / TL;
   const int i = env < N ? env : N - 1;
   const bool lead = env < N && lane % TL == 0;
-  const Q q{lds, lane, lane / TL, lane % TL};
-  for (int t = lane; t < LNK4; t += WGT) lds[LNK_OFF + t] = links[t];
+  const Q q = make_q(lds, lane, links);
+  for (int t = LNK_G + lane; t < LNK4; t += WGT) lds[LNK_OFF + t] = links[t];
   Stamps sp;
   sp.begin();
 #define ST(f) st[(size_t)(f) * N + i]
@@ -3214,7 +3248,7 @@ struct PreM {
 };
 static_assert(sizeof(PreM) <= 16 * PRE4, "PreM fits PRE4 granules");
 
-__global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_m_step_kernel(
+__global__ __launch_bounds__(WGT, ZB_M_WAVES_PER_SIMD) void zb_m_step_kernel(
     const zb_model* __restrict__ mg, const float4* __restrict__ links, zb_task_cfg cfg, int N, float* __restrict__ st,
     const float* __restrict__ act, float* __restrict__ obs, float* __restrict__ rew, uint8_t* __restrict__ term,
     uint8_t* __restrict__ trunc, float* __restrict__ acc, const Counters* __restrict__ cnt, uint64_t seed) {
@@ -3224,8 +3258,8 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_m_step_kernel(
   const int env = xcd_block(blockIdx.x, gridDim.x) * EPW + lane / TL;
   const int i = env < N ? env : N - 1;
   const bool lead = env < N && lane % TL == 0;
-  const Q q{lds, lane, lane / TL, lane % TL};
-  for (int t = lane; t < LNK4; t += WGT) lds[LNK_OFF + t] = links[t];
+  const Q q = make_q(lds, lane, links);
+  for (int t = LNK_G + lane; t < LNK4; t += WGT) lds[LNK_OFF + t] = links[t];
   Stamps sp;
   sp.begin();
 #define ST(f) st[(size_t)(f) * N + i]
