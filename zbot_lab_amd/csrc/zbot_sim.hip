@@ -1128,10 +1128,12 @@ __device__ __forceinline__ void staged_store(const Q& q, int env0, int N, float*
   const int e = q.lane % EPW, f0 = q.lane / EPW;
   const int env = env0 + e;
   if (env < N) {
+#ifndef ZB_DIAG_NO_STATE_STORE  // diagnostic only (scripts/gpu_r1o.sh): measures the state stores' cost
 #pragma unroll
     for (int f = f0; f < SD; f += WGT / EPW) {
       st[(size_t)f * N + env] = S[e * STG_LEN + f];
     }
+#endif
     if (f0 == 0) rew[env] = S[e * STG_LEN + SD + OD];
     if (f0 == 1) term[env] = S[e * STG_LEN + SD + OD + 1] != 0.f ? 1 : 0;
     if (f0 == 2) trunc[env] = S[e * STG_LEN + SD + OD + 2] != 0.f ? 1 : 0;
