@@ -47,6 +47,12 @@ class PPORunnerCfgV2:
     experiment_name: str = "zbot_6b_flat_direct_v2"
     empirical_normalization: bool = False
     clip_actions: float | None = None
+    # RslRlOnPolicyRunnerCfg load / logging fields (cli_args.py:76-85 writes them)
+    run_name: str = ""
+    resume: bool = False
+    load_run: str = ".*"
+    load_checkpoint: str = "model_.*.pt"
+    logger: str = "tensorboard"
     policy: RslRlPpoActorCriticCfg = field(default_factory=RslRlPpoActorCriticCfg)
     algorithm: RslRlPpoAlgorithmCfg = field(default_factory=RslRlPpoAlgorithmCfg)
 

@@ -292,6 +292,15 @@ class PPO:
             sums += torch.stack([value_loss.detach(), surrogate_loss.detach(), entropy_b.mean().detach()])
         self.storage.clear()
 
+    def restore_learning_rate(self) -> None:
+        """After ``optimizer.load_state_dict``: the checkpoint's rate becomes ``lr_t`` (the adaptive
+        rule's state) and every param group reads ``lr_t`` again. ``load_state_dict`` replaces a
+        tensor ``lr`` with a new tensor, which the adaptive rule would no longer update."""
+        lr = self.optimizer.param_groups[0]["lr"]
+        self.lr_t.copy_(lr.detach().reshape(()) if torch.is_tensor(lr) else torch.tensor(float(lr)))
+        for g in self.optimizer.param_groups:
+            g["lr"] = self.lr_t if torch.is_tensor(g["lr"]) else float(self.lr_t)
+
     @property
     def learning_rate(self) -> float:
         return float(self.lr_t)

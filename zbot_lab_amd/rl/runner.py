@@ -85,7 +85,11 @@ class OnPolicyRunner:
         self.multi_gpu_cfg = {"global_rank": self.gpu_global_rank, "world_size": self.gpu_world_size}
 
     # ------------------------------------------------------------------ training
-    def learn(self, num_learning_iterations: int, init_at_random_ep_len: bool = False) -> list[dict]:
+    def learn(self, num_learning_iterations: int, init_at_random_ep_len: bool = False,
+              callback=None) -> list[dict]:
+        """``callback(record)`` (optional) runs after every iteration with its log record, so a caller
+        can print progress from one ``learn(max_iterations)`` call (checkpoints follow
+        ``save_interval`` plus one at the end, as rsl_rl)."""
         env = self.env
         if init_at_random_ep_len:
             env.episode_length_buf = torch.randint_like(env.episode_length_buf, high=int(env.max_episode_length))
@@ -134,6 +138,8 @@ class OnPolicyRunner:
                 for k, v in zip(self._log_keys, (self._log_acc / self.num_steps_per_env).tolist()):
                     rec[k] = v
             self.log.append(rec)
+            if callback is not None:
+                callback(rec)
             if self.gpu_global_rank == 0 and self.log_dir and (it % self.save_interval == 0):
                 self.save(os.path.join(self.log_dir, f"model_{it}.pt"))
         self.current_learning_iteration = start_iter + num_learning_iterations
@@ -210,6 +216,7 @@ class OnPolicyRunner:
         self.alg.policy.load_state_dict(d["model_state_dict"])
         if load_optimizer:
             self.alg.optimizer.load_state_dict(d["optimizer_state_dict"])
+            self.alg.restore_learning_rate()
         self.current_learning_iteration = d["iter"]
         return d.get("infos")
 
