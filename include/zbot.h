@@ -228,6 +228,9 @@ typedef struct zb_model {
   float api_root_in_root[7];    /* pos 3, quat wxyz 4 */
   int32_t api_joint_index[ZB_NUM_DOF];
   float api_joint_sign[ZB_NUM_DOF];
+  /* bit ci: circle ci of the link coincides with a circle of a lower link of the same composite
+   * (the mated faces across a fixed joint); ground detection skips it (one contact set per face) */
+  int32_t link_circle_dup[ZB_NUM_LINKS];
 } zb_model;
 
 /* Task / simulation constants: ZbotDirectEnvCfgV2 (v2.py:26-206) or Zbot6SUpEnvCfg
@@ -289,6 +292,10 @@ typedef struct zb_task_cfg {
   float cmd_resample_s;        /* resampling_time_range (10, 10) */
   float cmd_rel_standing;      /* rel_standing_envs 0.02 */
   float feet_close_min;        /* feet_close termination: feet distance < 0.12 m */
+  /* feet_down_pos_last on reset (v2.py:436, v4.py:996, mdp/rewards.py:42): 0 = the pre-reset
+   * (terminal) feet positions, as the reference's call order reads them (body_link_pos_w before
+   * DirectRLEnv.step's sim.forward()); 1 = the post-reset feet positions */
+  int32_t reset_feet_refresh;
 } zb_task_cfg;
 
 typedef struct zb_sim* zb_handle;

@@ -44,6 +44,7 @@ def _load(double: bool = False):
     lib.zbo_set_state.argtypes = [P, _f]
     lib.zbo_physics_substeps.argtypes = [P, _f, C.c_int, C.c_void_p, C.c_void_p]
     lib.zbo_link_poses.argtypes = [P, _f, _f]
+    lib.zbo_contact_diag.argtypes = [P, _f]
     lib.zbo_link_com_vel.argtypes = [P, _f]
     lib.zbo_energy_momentum.argtypes = [P, _f]
     lib.zbo_pre_physics.argtypes = [C.c_int, C.POINTER(zm.ZbTaskCfg), _f, _f, _f, _f, _f]
@@ -161,6 +162,12 @@ class OracleSim:
         q = np.zeros((self.n, zm.NUM_LINKS, 4), np.float32)
         self.lib.zbo_link_poses(self.h, p, q)
         return p, q
+
+    def contact_diag(self):
+        """[n, 5]: candidates, ground, self, kept, min |sep - margin| of the current state."""
+        d = np.zeros((self.n, 5), np.float32)
+        self.lib.zbo_contact_diag(self.h, d)
+        return d
 
     def link_com_vel(self):
         v = np.zeros((self.n, zm.NUM_LINKS, 3), np.float32)

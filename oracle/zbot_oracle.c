@@ -98,6 +98,7 @@ typedef struct {
   int link_body[NL];
   real link_pos[NL][3], link_rot[NL][4], link_com[NL][3];
   real circle[NL][2][9], sphere[NL][2][4], bound[NL][4];
+  int circle_dup[NL];                 /* bit ci: duplicate of a lower link's mated face (skipped) */
   int npairs, pairs[ZB_MAX_SELF_PAIRS][2];
   real root_pos0[3], root_quat0[4], jq0[ND];
   real kp, kd, effort, vlim, max_depen;
@@ -120,6 +121,7 @@ static void load_mdl(const zb_model* m, mdl_t* o) {
   }
   for (int l = 0; l < NL; ++l) {
     o->link_body[l] = m->link_body[l];
+    o->circle_dup[l] = m->link_circle_dup[l];
     for (int a = 0; a < 3; ++a) { o->link_pos[l][a] = m->link_pos[l][a]; o->link_com[l][a] = m->link_com[l][a]; }
     for (int a = 0; a < 4; ++a) { o->link_rot[l][a] = m->link_rot[l][a]; o->bound[l][a] = m->link_bound[l][a]; }
     for (int c = 0; c < 2; ++c) {
@@ -357,6 +359,7 @@ static void detect(const mdl_t* m, const zb_task_cfg* cfg, const kin_t* k, real 
     if (Pz + k->p[b][2] + bc[2] - m->bound[l][3] > margin) continue;
     int taken = 0;
     for (int ci = 0; ci < 2; ++ci) {
+      if ((m->circle_dup[l] >> ci) & 1) continue; /* mated face: the lower link's candidates stand */
       const real* cd = m->circle[l][ci];
       real C[3], E1[3], E2[3];
       m3_v(R, cd, C);
@@ -927,22 +930,40 @@ static void phys_default(const mdl_t* m, phys_t* s) {
   for (int j = 0; j < ND; ++j) { s->jq[j] = m->jq0[j]; s->jqd[j] = 0; }
 }
 
+/* feet link origins (world = env-local) of a physical state */
+static void feet_world(const mdl_t* m, const phys_t* ph, real out[2][3]) {
+  kin_t k;
+  fk(m, ph, &k);
+  for (int f = 0; f < 2; ++f) {
+    real p[3], q[4];
+    link_pose(m, &k, m->foot_links[f], p, q);
+    for (int a = 0; a < 3; ++a) out[f][a] = p[a] + ph->root_pos[a];
+  }
+}
+
+/* feet_down_pos_last on reset (v2.py:436, v4.py:996, mdp/rewards.py:42): the reference reads
+ * body_link_pos_w inside _reset_idx, after write_*_to_sim but before DirectRLEnv.step's
+ * sim.forward(), so PhysX still reports the pre-reset link transforms: the latch takes the
+ * pre-reset (terminal) feet positions `pre`. cfg->reset_feet_refresh = 1 takes the post-reset
+ * feet instead (Isaac Lab behaviour, unpinned by any reference artefact). */
+static void latch_feet(const mdl_t* m, const zb_task_cfg* cfg, const real pre[2][3], const phys_t* post,
+                       real out[2][3]) {
+  if (cfg->reset_feet_refresh) {
+    feet_world(m, post, out);
+  } else {
+    for (int f = 0; f < 2; ++f)
+      for (int a = 0; a < 3; ++a) out[f][a] = pre[f][a];
+  }
+}
+
 /* _reset_idx for one env (v2.py:413-459); the episode-log accumulation is done by the caller */
-static void reset_env(const mdl_t* m, env_t* e) {
+static void reset_env(const mdl_t* m, const zb_task_cfg* cfg, env_t* e) {
+  real pre[2][3];
+  feet_world(m, &e->ph, pre);
   phys_default(m, &e->ph);
   mdp_t* md = &e->md;
   for (int j = 0; j < ND; ++j) { md->p_delta[j] = 0; md->actions[j] = 0; }
-  /* feet_down_pos_last <- post-reset feet positions (Isaac Lab refreshes link
-   * kinematics on read after write_*_to_sim) */
-  {
-    kin_t k;
-    fk(m, &e->ph, &k);
-    for (int f = 0; f < 2; ++f) {
-      real p[3], q[4];
-      link_pose(m, &k, m->foot_links[f], p, q);
-      for (int a = 0; a < 3; ++a) md->feet_down_pos[f][a] = p[a] + e->ph.root_pos[a];
-    }
-  }
+  latch_feet(m, cfg, pre, &e->ph, md->feet_down_pos);
   md->heading_sum = 0;
   md->yerr_sum = 0;
   /* ContactSensor.reset: history and timers zeroed */
@@ -1370,16 +1391,14 @@ static void v4_reset_env(const zbo_sim* s, uint64_t ctr, int i, env_t* e, int in
   const mdl_t* m = &s->m;
   const uint64_t h = env_hash(s->seed, ctr, i);
   mdp_t* md = &e->md;
+  real pre[2][3];
+  feet_world(m, &e->ph, pre);
   md->current_yaw = reset_pose(m, &s->c, h, &e->ph);
   v4_resample(s, h, 5, md->current_yaw, md->commands, &md->target_yaw);
   if (init) md->interval_left = draw(h, 8) * (s->c.cmd_interval_s[1] - s->c.cmd_interval_s[0]) + s->c.cmd_interval_s[0];
   for (int j = 0; j < ND; ++j) { md->p_delta[j] = 0; md->actions[j] = 0; }
-  kin_t k;
-  fk(m, &e->ph, &k);
+  latch_feet(m, &s->c, pre, &e->ph, md->feet_down_pos);
   for (int f = 0; f < 2; ++f) {
-    real p[3], q[4];
-    link_pose(m, &k, m->foot_links[f], p, q);
-    for (int a = 0; a < 3; ++a) md->feet_down_pos[f][a] = p[a] + e->ph.root_pos[a];
     md->feet_f_last[f] = s->c.feet_f_last_init;
     md->feet_step_len[f] = 0;
     md->feet_air_cur[f] = md->feet_air_last[f] = md->feet_contact_cur[f] = md->feet_contact_last[f] = 0;
@@ -1664,17 +1683,15 @@ static void m_reset_env(const zbo_sim* s, uint64_t ctr, int i, env_t* e) {
   const mdl_t* m = &s->m;
   const uint64_t h = env_hash(s->seed, ctr, i);
   mdp_t* md = &e->md;
+  real pre[2][3];
+  feet_world(m, &e->ph, pre);
   (void)reset_pose(m, &s->c, h, &e->ph);
   m_resample(s, h, M_DRAW_RESET_CMD, md->commands, &md->cmd_standing);
   md->interval_left = s->c.cmd_resample_s;
   md->metrics[0] = md->metrics[1] = 0;
   for (int j = 0; j < ND; ++j) md->actions[j] = 0;
-  kin_t k;
-  fk(m, &e->ph, &k);
+  latch_feet(m, &s->c, pre, &e->ph, md->feet_down_pos);
   for (int f = 0; f < 2; ++f) {
-    real p[3], q[4];
-    link_pose(m, &k, m->foot_links[f], p, q);
-    for (int a = 0; a < 3; ++a) md->feet_down_pos[f][a] = p[a] + e->ph.root_pos[a];
     md->feet_f_last[f] = 0;
     md->feet_step_len[f] = 0;
     md->feet_air_cur[f] = md->feet_air_last[f] = 0;
@@ -1983,6 +2000,7 @@ zbo_sim* zbo_create(const zb_model* model, const zb_task_cfg* cfg, int num_envs,
   s->env = (env_t*)calloc((size_t)num_envs, sizeof(env_t));
   for (int i = 0; i < num_envs; ++i) {
     memset(&s->env[i], 0, sizeof(env_t));
+    phys_default(&s->m, &s->env[i].ph); /* the spawn pose: what the construction-time reset's latch reads */
     if (cfg->task == ZB_TASK_STANDUP_V0) {
       for (int l = 0; l < NL; ++l) s->env[i].md.mu[l] = cfg->friction;
       su_reset_env(&s->m, cfg, seed, 0, i, &s->env[i]); /* construction draws at RNG position 0 */
@@ -1992,7 +2010,7 @@ zbo_sim* zbo_create(const zb_model* model, const zb_task_cfg* cfg, int num_envs,
       for (int l = 0; l < NL; ++l) s->env[i].md.mu[l] = cfg->friction;
       m_reset_env(s, 0, i, &s->env[i]);
     } else {
-      reset_env(&s->m, &s->env[i]);
+      reset_env(&s->m, cfg, &s->env[i]);
     }
   }
   if (cfg->task != ZB_TASK_WALKING_V2) s->call_counter = 1;
@@ -2035,7 +2053,7 @@ int zbo_reset(zbo_sim* s, const int32_t* env_ids, int n) {
       m_reset_env(s, ctr, e, en);
     } else if (s->c.task == ZB_TASK_WALKING_V2) {
       for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) acc[t] += en->md.ep_sums[t];
-      reset_env(&s->m, en);
+      reset_env(&s->m, &s->c, en);
     } else {
       real dur = (real)en->md.ep_len * step_dt;
       if (dur < step_dt) dur = step_dt;
@@ -2115,7 +2133,7 @@ static real step_env(const mdl_t* m, const zb_task_cfg* cfg, env_t* e, const flo
   real rew = mdp_eval(cfg, m->jq0, &pre, &ps, md, act, prev, terms, died, tout);
   if (*died || *tout) {
     for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) acc[t] += md->ep_sums[t];
-    reset_env(m, e);
+    reset_env(m, cfg, e);
   }
   write_obs(m, e, obs);
   return rew;
@@ -2288,6 +2306,74 @@ int zbo_physics_substeps(zbo_sim* s, const float* targets, int nsub, float* net_
         for (int a = 0; a < 3; ++a) net_force[((size_t)e * NL + l) * 3 + a] = (float)so.net_force[l][a];
     if (applied_torque)
       for (int j = 0; j < ND; ++j) applied_torque[(size_t)e * ND + j] = (float)so.applied_torque[j];
+  }
+  return 0;
+}
+
+/* contact diagnostics of the current state (parity debugging): per env [candidates before the
+ * 12-slot selection, ground candidates, self candidates (after the NSELF_MAX cap), kept, min
+ * |sep - margin| over every tested ground rim point and sphere pair (distance to the activation
+ * threshold)] */
+int zbo_contact_diag(zbo_sim* s, float* out) {
+  for (int e = 0; e < s->n; ++e) {
+    kin_t k;
+    fk(&s->m, &s->env[e].ph, &k);
+    clist_t L;
+    L.n = 0;
+    const real margin = s->c.contact_margin;
+    /* detect() without the selection, plus the threshold distance */
+    real mind = 1e30;
+    int ng = 0, ns = 0;
+    const real Pz = s->env[e].ph.root_pos[2];
+    for (int l = 0; l < NL; ++l) {
+      int b = s->m.link_body[l];
+      int taken = 0;
+      for (int ci = 0; ci < 2; ++ci) {
+        if ((s->m.circle_dup[l] >> ci) & 1) continue;
+        const real* cd = s->m.circle[l][ci];
+        real C[3], E1[3], E2[3];
+        m3_v(k.R[b], cd, C);
+        m3_v(k.R[b], cd + 3, E1);
+        m3_v(k.R[b], cd + 6, E2);
+        for (int a = 0; a < 3; ++a) C[a] += k.p[b][a];
+        real al = -E1[2] + (real)RIM_EPS, be = -E2[2];
+        real nrm = sqrtr(al * al + be * be);
+        real cs = 1, sn = 0;
+        if (nrm > (real)1e-12) { cs = al / nrm; sn = be / nrm; }
+        const real rc[4][2] = {{cs, sn}, {-sn, cs}, {-cs, -sn}, {sn, -cs}};
+        for (int r = 0; r < 4; ++r) {
+          real z = C[2] + rc[r][0] * E1[2] + rc[r][1] * E2[2];
+          real sep = Pz + z;
+          real d = (real)fabs((double)(sep - margin));
+          if (d < mind) mind = d;
+          if (sep < margin && taken < NCAND_PER_LINK) { ++taken; ++ng; }
+        }
+      }
+    }
+    if (s->c.enable_self_collision) {
+      for (int p = 0; p < s->m.npairs; ++p) {
+        int la = s->m.pairs[p][0], lb = s->m.pairs[p][1];
+        int ba = s->m.link_body[la], bb = s->m.link_body[lb];
+        for (int sa = 0; sa < 2; ++sa)
+          for (int sb = 0; sb < 2; ++sb) {
+            real xa[3], xb[3];
+            m3_v(k.R[ba], s->m.sphere[la][sa], xa);
+            m3_v(k.R[bb], s->m.sphere[lb][sb], xb);
+            for (int a = 0; a < 3; ++a) { xa[a] += k.p[ba][a]; xb[a] += k.p[bb][a]; }
+            real dv[3] = {xa[0] - xb[0], xa[1] - xb[1], xa[2] - xb[2]};
+            real sep = sqrtr(v3_dot(dv, dv)) - (s->m.sphere[la][sa][3] + s->m.sphere[lb][sb][3]);
+            real d = (real)fabs((double)(sep - margin));
+            if (d < mind) mind = d;
+            if (sep < margin && ns < NSELF_MAX) ++ns;
+          }
+      }
+    }
+    detect(&s->m, &s->c, &k, Pz, &L);
+    out[5 * e + 0] = (float)(ng + ns);
+    out[5 * e + 1] = (float)ng;
+    out[5 * e + 2] = (float)ns;
+    out[5 * e + 3] = (float)L.n;
+    out[5 * e + 4] = (float)mind;
   }
   return 0;
 }

@@ -1,0 +1,230 @@
+"""Full-state parity machinery (tests/test_gpu_fullstate.py): every persistent state row of all four
+tasks randomised to valid values, every row + obs + reward + flags compared after a step, and every
+env outside tolerance explained by the oracle's own discontinuity there.
+
+Why an "explained outlier" rule instead of a 99 % pass: contact activation at the speculative
+margin, the 1 N / 10 N sensor thresholds and the |tau| = effort drive clamp are discontinuities of
+the step map. Two fp32 implementations with different operation order land on different sides of
+one of them whenever the state sits within rounding distance of it. Such an env is detectable
+without knowing which discontinuity it is: perturbing the oracle's own input by ~1e-6 (the scale of
+the GPU/oracle rounding difference) moves its output by more than the tolerance. An env outside
+tolerance where the oracle is stable under that perturbation is a real mismatch and fails the test.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from zbot_lab_amd import model as zm
+
+S, V4, SU, M = zm.S, zm.V4, zm.SU, zm.M
+
+TASKS = ("v2", "v4", "standup", "manager")
+
+
+def task_cfg(task: str) -> zm.TaskCfg:
+    return {"v2": zm.TaskCfg, "v4": zm.TaskCfg.walking_v4, "standup": zm.TaskCfg.standup,
+            "manager": zm.TaskCfg.manager_flat}[task]()
+
+
+def _rows(d: dict, name: str, k: int) -> list:
+    return list(range(d[name], d[name] + k))
+
+
+def row_groups(task: str) -> dict:
+    """State rows by tolerance class: phys_pos / phys_vel (physics), exact (pure functions of the
+    inputs and counters), force (contact-force derived), kin (kinematics-derived latches), sums
+    (episode sums, per-term tolerance), static (read-only: per-link friction)."""
+    pos = list(range(0, 7)) + list(range(13, 19))
+    vel = list(range(7, 13)) + list(range(19, 25))
+    if task == "v2":
+        return dict(phys_pos=pos, phys_vel=vel,
+                    exact=_rows(S, "P_DELTA", 6) + _rows(S, "ACTIONS", 6) + [S["EP_LEN"]] + _rows(S, "FEET_AIR_CUR", 2)
+                    + _rows(S, "FEET_AIR_LAST", 2) + _rows(S, "FEET_CONTACT_CUR", 2),
+                    force=_rows(S, "FEET_F_LAST", 2) + _rows(S, "FEET_FZ_HIST", 10) + _rows(S, "UNDES_FMAX_HIST", 5),
+                    kin=_rows(S, "FEET_DOWN_POS", 6) + _rows(S, "FEET_STEP_LEN", 2) + [S["HEADING_SUM"], S["Y_ERR_SUM"]],
+                    sums=_rows(S, "EP_SUMS", 13), static=[])
+    if task == "v4":
+        return dict(phys_pos=pos, phys_vel=vel,
+                    exact=_rows(V4, "P_DELTA", 6) + _rows(V4, "ACTIONS", 6) + [V4["EP_LEN"], V4["INTERVAL_LEFT"]]
+                    + _rows(V4, "COMMANDS", 2) + [V4["TARGET_YAW"]] + _rows(V4, "FEET_AIR_CUR", 2)
+                    + _rows(V4, "FEET_CONTACT_CUR", 2) + _rows(V4, "FEET_AIR_LAST", 2) + _rows(V4, "FEET_CONTACT_LAST", 2),
+                    force=_rows(V4, "FEET_F_LAST", 2) + _rows(V4, "FEET_FZ_HIST", 6) + _rows(V4, "UNDES_FMAX_HIST", 3),
+                    kin=_rows(V4, "FEET_DOWN_POS", 6) + _rows(V4, "FEET_STEP_LEN", 2) + [V4["CURRENT_YAW"]],
+                    sums=_rows(V4, "EP_SUMS", 15), static=[])
+    if task == "standup":
+        return dict(phys_pos=pos, phys_vel=vel,
+                    exact=_rows(SU, "P_DELTA", 6) + _rows(SU, "ACTIONS", 6) + [SU["EP_LEN"]],
+                    force=[], kin=[SU["CENTER_Z_LAST"]], sums=_rows(SU, "EP_SUMS", 4), static=_rows(SU, "LINK_MU", 12))
+    return dict(phys_pos=pos, phys_vel=vel,
+                exact=_rows(M, "ACTIONS", 6) + _rows(M, "COMMANDS", 3) + [M["CMD_TIME_LEFT"], M["CMD_STANDING"],
+                                                                            M["EP_LEN"]]
+                + _rows(M, "FEET_AIR_CUR", 2) + _rows(M, "FEET_AIR_LAST", 2),
+                force=_rows(M, "FEET_F_LAST", 2) + _rows(M, "FEET_FZ_HIST", 6) + _rows(M, "FEET_FN_HIST", 6),
+                kin=_rows(M, "FEET_DOWN_POS", 6) + _rows(M, "FEET_STEP_LEN", 2) + _rows(M, "METRICS", 2),
+                sums=_rows(M, "EP_SUMS", 11), static=_rows(M, "LINK_MU", 12))
+
+
+# episode-sum terms evaluated from state that is identical on both sides before the step (v2's
+# one-step-lag kinematics, the action rate): tight tolerance; every other term reads post-step
+# physics and gets the physics tolerance on its per-step increment
+TIGHT_TERMS = {
+    "v2": {"base_vel_forward", "feet_downward", "feet_forward", "base_heading_x", "base_heading_x_sum",
+           "base_pos_y_err", "base_pos_y_err_sum", "action_rate"},
+    "v4": {"action_rate"}, "standup": set(), "manager": {"action_rate_l2"},
+}
+
+# (atol, rtol) per class
+TOL = dict(phys_pos=(1e-3, 1e-3), phys_vel=(5e-3, 5e-3), exact=(2e-5, 2e-6), force=(0.05, 0.02),
+           kin=(2e-5, 2e-5), static=(0.0, 0.0), obs=(5e-3, 5e-3))
+
+
+def _quat(rng, n, tilt):
+    ax = rng.normal(size=(n, 3))
+    ax /= np.linalg.norm(ax, axis=1, keepdims=True)
+    h = 0.5 * rng.uniform(0, tilt, n)
+    return np.concatenate([np.cos(h)[:, None], ax * np.sin(h)[:, None]], axis=1)
+
+
+def _qmul(a, b):
+    w1, x1, y1, z1 = a.T
+    w2, x2, y2, z2 = b.T
+    return np.stack([w1 * w2 - x1 * x2 - y1 * y2 - z1 * z2, w1 * x2 + x1 * w2 + y1 * z2 - z1 * y2,
+                     w1 * y2 - x1 * z2 + y1 * w2 + z1 * x2, w1 * z2 + x1 * y2 - y1 * x2 + z1 * w2], axis=1)
+
+
+def random_states(task: str, o, n: int, seed: int, standing: bool = False) -> np.ndarray:
+    """Valid random values in every state row. ``o`` is a fresh OracleSim of the task (its reset
+    state is the base and its FK places the feet latches). ``standing``: small joint noise, zero
+    velocities, MDP rows random as usual."""
+    rng = np.random.default_rng(seed)
+    st = o.get_state().copy()
+    f32 = np.float32
+    jq_s, jqd_s, tilt, vel = (0.05, 0.0, 0.0, 0.0) if standing else (0.15, 0.5, 0.05, 0.1)
+    st[13:19] += rng.normal(0, jq_s, (6, n)).astype(f32)
+    st[19:25] = rng.normal(0, jqd_s, (6, n)).astype(f32)
+    if tilt:
+        st[3:7] = _qmul(_quat(rng, n, tilt), st[3:7].T).T.astype(f32)
+        st[2] += rng.uniform(0, 0.01, n).astype(f32)
+    st[7:13] = rng.normal(0, vel, (6, n)).astype(f32)
+    o.set_state(st)
+    feet = o.link_poses()[0][:, [0, 11]]                     # [n, 2, 3] env-local feet positions
+    D = {"v2": S, "v4": V4, "standup": SU, "manager": M}[task]
+    u = lambda lo, hi, k=None: rng.uniform(lo, hi, (k, n) if k else n).astype(f32)  # noqa: E731
+    ml = {"v2": 999, "v4": 999, "standup": 299, "manager": 999}[task]
+    ep = rng.integers(0, ml - 1, n)
+    ep[rng.random(n) < 0.05] = ml - 2                        # time-outs this step
+    if task == "standup":
+        ep[rng.random(n) < 0.1] = 49                         # center_z_last refresh (ep_len % 50 == 49)
+    st[D["EP_LEN"]] = ep.astype(f32)
+    nt = {"v2": 13, "v4": 15, "standup": 4, "manager": 11}[task]
+    st[D["EP_SUMS"]:D["EP_SUMS"] + nt] = rng.normal(0, 2.0, (nt, n)).astype(f32)
+    if "P_DELTA" in D:
+        st[D["P_DELTA"]:D["P_DELTA"] + 6] = 0.0 if standing else rng.normal(0, 0.3, (6, n)).astype(f32)
+    st[D["ACTIONS"]:D["ACTIONS"] + 6] = (np.tanh(rng.normal(0, 1, (6, n))) if task != "manager"
+                                         else rng.normal(0, 1, (6, n))).astype(f32)
+    if task == "standup":
+        bz = o.link_poses()[0][:, 6, 2]
+        st[SU["CENTER_Z_LAST"]] = (bz + rng.uniform(-0.02, 0.08, n)).astype(f32)
+        st[SU["LINK_MU"]:SU["LINK_MU"] + 12] = u(0.6, 1.0, 12)
+        return st
+    # feet latches, step lengths, last forces
+    st[D["FEET_DOWN_POS"]:D["FEET_DOWN_POS"] + 6] = (feet + rng.normal(0, 0.03, (n, 2, 3))).reshape(n, 6).T.astype(f32)
+    st[D["FEET_STEP_LEN"]:D["FEET_STEP_LEN"] + 2] = u(-0.1, 0.1, 2)
+    st[D["FEET_F_LAST"]:D["FEET_F_LAST"] + 2] = u(0.0, 20.0, 2)
+    hist = {"v2": 5, "v4": 3, "manager": 3}[task]
+    fz = u(0.0, 30.0, 2 * hist) * (rng.random((2 * hist, n)) > 0.3)
+    st[D["FEET_FZ_HIST"]:D["FEET_FZ_HIST"] + 2 * hist] = fz
+    air = rng.random((2, n)) < 0.5
+    st[D["FEET_AIR_CUR"]:D["FEET_AIR_CUR"] + 2] = np.where(air, u(0.005, 0.5, 2), 0.0)
+    st[D["FEET_AIR_LAST"]:D["FEET_AIR_LAST"] + 2] = u(0.0, 0.5, 2)
+    if task in ("v2", "v4"):
+        und = np.zeros((hist, n), f32)
+        hit = rng.random(n) < 0.05
+        und[rng.integers(0, hist, n)[hit], np.nonzero(hit)[0]] = u(0.0, 3.0)[hit]
+        st[D["UNDES_FMAX_HIST"]:D["UNDES_FMAX_HIST"] + hist] = und
+        st[D["FEET_CONTACT_CUR"]:D["FEET_CONTACT_CUR"] + 2] = np.where(air, 0.0, u(0.005, 0.5, 2))
+    if task == "v2":
+        st[S["HEADING_SUM"]] = u(-1, 1)
+        st[S["Y_ERR_SUM"]] = u(-1, 1)
+    if task == "v4":
+        sgn = np.where(rng.random(n) < 0.8, 1.0, -1.0)
+        st[V4["COMMANDS"]] = (sgn * u(0.0, 0.3)).astype(f32)
+        st[V4["COMMANDS"] + 1] = u(-0.1, 0.1)
+        st[V4["TARGET_YAW"]] = u(-np.pi, np.pi)
+        st[V4["CURRENT_YAW"]] = u(-np.pi, np.pi)
+        il = u(0.03, 6.0)
+        small = rng.random(n) < 0.2
+        il[small] = u(0.0, 0.015)[small]                      # interval resample this step
+        st[V4["INTERVAL_LEFT"]] = il
+        st[V4["FEET_CONTACT_LAST"]:V4["FEET_CONTACT_LAST"] + 2] = u(0.0, 0.5, 2)
+    if task == "manager":
+        st[M["COMMANDS"]] = u(-0.1, 0.1)
+        st[M["COMMANDS"] + 1] = 0.0
+        st[M["COMMANDS"] + 2] = 0.0
+        tl = u(0.03, 10.0)
+        small = rng.random(n) < 0.2
+        tl[small] = u(0.0, 0.015)[small]                      # command resample this step
+        st[M["CMD_TIME_LEFT"]] = tl
+        st[M["CMD_STANDING"]] = (rng.random(n) < 0.05).astype(f32)
+        st[M["FEET_FN_HIST"]:M["FEET_FN_HIST"] + 6] = np.sqrt(fz ** 2 + u(0.0, 5.0, 6) ** 2)
+        st[M["METRICS"]:M["METRICS"] + 2] = u(0.0, 1.0, 2)
+        st[M["LINK_MU"]:M["LINK_MU"] + 12] = u(0.3, 1.0, 12)
+    return st
+
+
+def tolerance_rows(task: str, before: np.ndarray, after_o: np.ndarray, nsteps: int = 1) -> np.ndarray:
+    """Per-row, per-env tolerance array [state_dim, n] for comparing GPU vs oracle state.
+
+    ``kin`` rows (feet latches, step lengths, integrators, current yaw, centre height, metrics) and
+    the TIGHT_TERMS sums come from the pre-step state only in v2 and only for one step (the
+    one-step lag); otherwise they read post-step physics and get the physics tolerance."""
+    g = row_groups(task)
+    tol = np.zeros_like(after_o, dtype=np.float64)
+    multi = nsteps > 1
+    lagged = task == "v2" and not multi
+    for cls, rows in g.items():
+        if cls == "sums":
+            continue
+        a, r = TOL["phys_pos"] if cls == "kin" and not lagged else TOL[cls]
+        for k in rows:
+            tol[k] = a + r * np.abs(after_o[k])
+    cfg = task_cfg(task)
+    terms, w = cfg.reward_terms, cfg.reward_weights
+    tight = TIGHT_TERMS[task] if not multi else set()
+    if task != "v2":
+        tight = tight & {"action_rate", "action_rate_l2"}
+    for t, k in enumerate(g["sums"]):
+        inc = np.abs(after_o[k].astype(np.float64) - before[k])
+        base = 2e-5 + 4e-6 * np.abs(after_o[k])
+        # post-step terms: 2 % of the summed increment, plus 1 % of the weighted term scale per step
+        # (a term read from physics within its tolerance moves by ~1e-2 of its unit)
+        loose = 0.02 * inc + nsteps * abs(w.get(terms[t], 0.0)) * cfg.step_dt * 1e-2 + 2e-4
+        tol[k] = base if terms[t] in tight else base + loose
+    return tol
+
+
+def compare(task, sg, so, obs_g, obs_o, rew_g, rew_o, fl_g, fl_o, before, nsteps: int = 1):
+    """Per-env worst error/tolerance ratio over every state row, obs, reward; flags mismatch -> inf.
+    Returns (ratio [n], details per env: list of (name, err, tol))."""
+    tol = tolerance_rows(task, before, so, nsteps)
+    err = np.abs(sg.astype(np.float64) - so)
+    # reset envs: both sides reset -> the state is the reset state (compared with the same tolerances)
+    ratio_rows = np.where(tol > 0, err / np.maximum(tol, 1e-30), np.where(err > 0, np.inf, 0.0))
+    a, r = TOL["obs"]
+    ratio_obs = np.abs(obs_g - obs_o) / (a + r * np.abs(obs_o))
+    rtol_rew = 2e-3 + 2e-3 * np.abs(rew_o)
+    ratio_rew = np.abs(rew_g - rew_o) / rtol_rew
+    flags_bad = np.zeros(sg.shape[1], bool)
+    for fg, fo in zip(fl_g, fl_o):
+        flags_bad |= fg != fo
+    ratio = np.maximum(np.maximum(ratio_rows.max(axis=0), ratio_obs.max(axis=1)), ratio_rew)
+    ratio[flags_bad] = np.inf
+    return ratio, ratio_rows, err, tol, flags_bad
+
+
+def perturb_physics(st: np.ndarray, rng, rel: float = 1e-6, abs_: float = 1e-7) -> np.ndarray:
+    out = st.copy()
+    ph = out[:25].astype(np.float64)
+    ph = ph * (1 + rel * rng.standard_normal(ph.shape)) + abs_ * rng.standard_normal(ph.shape)
+    out[:25] = ph.astype(np.float32)
+    return out

@@ -868,7 +868,9 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q&
     int tk = 0;
 #pragma unroll
     for (int ci = 0; ci < 2; ++ci) {
-      mv3f(R, L[1 + 3 * ci], C[ci]);
+      const float4 cc = L[1 + 3 * ci];
+      const bool face = cc.w == 0.f;  // not a duplicate of a lower link's mated face
+      mv3f(R, cc, C[ci]);
       mv3f(R, L[2 + 3 * ci], E1[ci]);
       mv3f(R, L[3 + 3 * ci], E2[ci]);
       C[ci][0] += p[0]; C[ci][1] += p[1]; C[ci][2] += p[2];
@@ -883,7 +885,7 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q&
         const float cr = r == 0 ? c0 : (r == 1 ? -s0 : (r == 2 ? -c0 : s0));
         const float sr = r == 0 ? s0 : (r == 1 ? c0 : (r == 2 ? -s0 : -c0));
         const float z = C[ci][2] + cr * E1[ci][2] + sr * E2[ci][2];
-        if (near && Pz + z < margin && tk < 4) { vmask |= 1u << (4 * ci + r); ++tk; }
+        if (near && face && Pz + z < margin && tk < 4) { vmask |= 1u << (4 * ci + r); ++tk; }
       }
     }
   }
@@ -1913,18 +1915,48 @@ __device__ __forceinline__ void store_state(float* __restrict__ st, int N, int i
 #undef SV
 }
 
+__device__ __forceinline__ void phys_default(MP m, Phys& p) {
+#pragma unroll
+  for (int a = 0; a < 3; ++a) { p.pos[a] = m->default_root_pos[a]; p.lv[a] = 0.f; p.av[a] = 0.f; }
+#pragma unroll
+  for (int a = 0; a < 4; ++a) p.quat[a] = m->default_root_quat[a];
+#pragma unroll
+  for (int j = 0; j < ND; ++j) { p.jq[j] = m->default_joint_pos[j]; p.jqd[j] = 0.f; }
+}
+
+// feet link origins (env-local world) of a physical state (one lane per env)
+__device__ __forceinline__ void feet_world(MP m, const Phys& p, float out[2][3]) {
+  Kin k;
+  fk(m, p, k);
+  float fq[4];
+  link_pose(m, k, m->foot_links[0], out[0], fq);
+  link_pose(m, k, m->foot_links[1], out[1], fq);
+#pragma unroll
+  for (int a = 0; a < 3; ++a) { out[0][a] += p.pos[a]; out[1][a] += p.pos[a]; }
+}
+
 // _reset_idx for one env (v2.py:413-459); feet_step_len and f_last are NOT reset (reference).
-// feet_down_pos_last = the feet positions of the default pose (dflt[0], dflt[1], zb_derive_kernel).
-__device__ __forceinline__ void reset_env(MP m, const float4* dflt, Phys& p, Mdp& d) {
+// feet_down_pos_last = the pre-reset feet positions (v2.py:436), or with `refresh`
+// the feet positions of the default pose (dflt[0], dflt[1], zb_derive_kernel).
+__device__ __forceinline__ void reset_env(MP m, const float4* dflt, Phys& p, Mdp& d, int refresh) {
+  float pre[2][3];
+  if (!refresh) feet_world(m, p, pre);
 #pragma unroll
   for (int a = 0; a < 3; ++a) { p.pos[a] = m->default_root_pos[a]; p.lv[a] = 0.f; p.av[a] = 0.f; }
 #pragma unroll
   for (int a = 0; a < 4; ++a) p.quat[a] = m->default_root_quat[a];
 #pragma unroll
   for (int j = 0; j < ND; ++j) { p.jq[j] = m->default_joint_pos[j]; p.jqd[j] = 0.f; d.p_delta[j] = 0.f; d.actions[j] = 0.f; }
-  const float4 f0 = dflt[0], f1 = dflt[1];
-  d.down_pos[0][0] = f0.x; d.down_pos[0][1] = f0.y; d.down_pos[0][2] = f0.z;
-  d.down_pos[1][0] = f1.x; d.down_pos[1][1] = f1.y; d.down_pos[1][2] = f1.z;
+  if (refresh) {
+    const float4 f0 = dflt[0], f1 = dflt[1];
+    d.down_pos[0][0] = f0.x; d.down_pos[0][1] = f0.y; d.down_pos[0][2] = f0.z;
+    d.down_pos[1][0] = f1.x; d.down_pos[1][1] = f1.y; d.down_pos[1][2] = f1.z;
+  } else {
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+      for (int a = 0; a < 3; ++a) d.down_pos[f][a] = pre[f][a];
+  }
   d.heading_sum = 0.f;
   d.yerr_sum = 0.f;
 #pragma unroll
@@ -2130,8 +2162,8 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_step_kernel(const z
   sens_replay<ZB_HIST>(q, ZB_CARRY ? cst : st, ZB_CARRY ? 1 : N, ZB_CARRY ? 0 : i, ZB_S_FEET_FZ_HIST, ZB_S_UNDES_FMAX_HIST, cfg.decimation, cfg.sim_dt,
                        cfg.contact_force_threshold, fz_sum, fm_max, air_cur, air_last, contact_t, con_last_unused);
 
-  // post-step feet COM velocities (feet_slide)
-  float feet_vel[2][3], obs_q[4];
+  // post-step feet COM velocities (feet_slide); post-step feet positions (the reset latch)
+  float feet_vel[2][3], obs_q[4], post_feet[2][3];
   {
     wave_sync();  // the last substep's readers of the body poses are done
     fk_team_pose(p, q);
@@ -2140,8 +2172,12 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_step_kernel(const z
     read_joints(q, S, org);
     link_com_vel_q(m, q, p, S, 0, feet_vel[0]);
     link_com_vel_q(m, q, p, S, 11, feet_vel[1]);
-    float bp[3];
+    float bp[3], fq[4];
     link_pose_q(m, q, 6, bp, obs_q);  // base quat of the post-step state (observation)
+    link_pose_q(m, q, 0, post_feet[0], fq);
+    link_pose_q(m, q, 11, post_feet[1], fq);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) { post_feet[0][a] += p.pos[a]; post_feet[1][a] += p.pos[a]; }
   }
   sp.mark(11);
 
@@ -2201,7 +2237,9 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_step_kernel(const z
   if (died) reward -= cfg.terminal_penalty;  // v2.py:379-380
 
   // in-kernel auto-reset (v2.py:413-459): the episode log, then the default state; step_len and
-  // f_last are not reset (reference), feet_down_pos_last = the default feet positions
+  // f_last are not reset (reference); feet_down_pos_last = the pre-reset (post-step) feet positions
+  // (v2.py:436 reads them before sim.forward()), or the default feet with
+  // cfg.reset_feet_refresh
   const uint64_t lmask = __ballot(reset && lead);
   if (reset) {
     if (lead) {
@@ -2219,8 +2257,13 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_step_kernel(const z
 #pragma unroll
     for (int j = 0; j < ND; ++j) { p.jq[j] = m->default_joint_pos[j]; p.jqd[j] = 0.f; }
     const float4 d0 = q.dflt()[0], d1 = q.dflt()[1], dq = q.dflt()[2];
-    down[0][0] = d0.x; down[0][1] = d0.y; down[0][2] = d0.z;
-    down[1][0] = d1.x; down[1][1] = d1.y; down[1][2] = d1.z;
+    if (cfg.reset_feet_refresh) {
+      down[0][0] = d0.x; down[0][1] = d0.y; down[0][2] = d0.z;
+      down[1][0] = d1.x; down[1][1] = d1.y; down[1][2] = d1.z;
+    } else {
+#pragma unroll
+      for (int a = 0; a < 3; ++a) { down[0][a] = post_feet[0][a]; down[1][a] = post_feet[1][a]; }
+    }
     obs_q[0] = dq.x; obs_q[1] = dq.y; obs_q[2] = dq.z; obs_q[3] = dq.w;
   }
   log_flush(q, lmask, acc);
@@ -2296,7 +2339,7 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_step_kernel(const z
 // reset env_ids (or all when ids == nullptr); logs the reset envs' episode sums into acc
 __global__ void zb_reset_kernel(const zb_model* __restrict__ mg, const float4* __restrict__ links, int N,
                                 float* __restrict__ st, const int32_t* __restrict__ ids, int n,
-                                float* __restrict__ acc) {
+                                float* __restrict__ acc, int refresh) {
   MP m = to_mp(mg);
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n) return;
@@ -2308,7 +2351,7 @@ __global__ void zb_reset_kernel(const zb_model* __restrict__ mg, const float4* _
 #pragma unroll
   for (int k = 0; k < ZB_NUM_REWARD_TERMS; ++k) atomicAdd(&acc_slot(acc, t)[k], d.sums[k]);
   atomicAdd(&acc_slot(acc, t)[ACC_NRES], 1.f);
-  reset_env(m, links + DFLT_OFF, p, d);
+  reset_env(m, links + DFLT_OFF, p, d, refresh);
   store_state(st, N, i, p, d);
 }
 
@@ -3006,13 +3049,13 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_v4_step_kernel(
     float R[9];
     qmat(p.quat, R);
 #pragma unroll
-    for (int f = 0; f < 2; ++f) {  // feet_down_pos_last = the reset pose's feet
+    for (int f = 0; f < 2; ++f) {  // feet_down_pos_last: pre-reset feet (v4.py:996) or reset pose's
       const float4 fr = q.dflt()[4 + f];
       const float v[3] = {fr.x, fr.y, fr.z};
       float w3[3];
       mv3(R, v, w3);
 #pragma unroll
-      for (int a = 0; a < 3; ++a) down[f][a] = p.pos[a] + w3[a];
+      for (int a = 0; a < 3; ++a) down[f][a] = cfg.reset_feet_refresh ? p.pos[a] + w3[a] : feet[f][a];
       f_last[f] = cfg.feet_f_last_init;
       step_len[f] = 0.f;
     }
@@ -3123,6 +3166,13 @@ __global__ void zb_v4_reset_kernel(const zb_model* __restrict__ mg, const float4
     for (int k = 0; k < ZB_V4_NUM_REWARD_TERMS; ++k) atomicAdd(&acc_slot(acc, t)[k], ST(ZB_V4_EP_SUMS + k) / dur);
     atomicAdd(&acc_slot(acc, t)[ACC_NRES], 1.f);
   }
+  float pre[2][3];  // the pre-reset feet (the spawn pose at construction)
+  if (!cfg.reset_feet_refresh) {
+    Phys p0;
+    if (init) phys_default(m, p0);
+    else load_phys(st, N, i, p0);
+    feet_world(m, p0, pre);
+  }
   Phys p;
   const uint64_t hs = env_hash(seed, cnt->calls, i);
   const float cur_yaw = reset_pose(m, cfg, hs, p);
@@ -3151,7 +3201,7 @@ __global__ void zb_v4_reset_kernel(const zb_model* __restrict__ mg, const float4
     float w3[3];
     mv3(R, v, w3);
 #pragma unroll
-    for (int a = 0; a < 3; ++a) ST(ZB_V4_FEET_DOWN_POS + 3 * f + a) = p.pos[a] + w3[a];
+    for (int a = 0; a < 3; ++a) ST(ZB_V4_FEET_DOWN_POS + 3 * f + a) = cfg.reset_feet_refresh ? p.pos[a] + w3[a] : pre[f][a];
     ST(ZB_V4_FEET_STEP_LEN + f) = 0.f;
     ST(ZB_V4_FEET_F_LAST + f) = cfg.feet_f_last_init;
     ST(ZB_V4_FEET_AIR_CUR + f) = 0.f;
@@ -3488,13 +3538,13 @@ __global__ __launch_bounds__(WGT, ZB_M_WAVES_PER_SIMD) void zb_m_step_kernel(
     float R[9];
     qmat(p.quat, R);
 #pragma unroll
-    for (int f = 0; f < 2; ++f) {
+    for (int f = 0; f < 2; ++f) {  // reset_my_data: pre-reset feet (rewards.py:42) or reset pose's
       const float4 fr = q.dflt()[4 + f];
       const float v[3] = {fr.x, fr.y, fr.z};
       float w3[3];
       mv3(R, v, w3);
 #pragma unroll
-      for (int a = 0; a < 3; ++a) down[f][a] = p.pos[a] + w3[a];
+      for (int a = 0; a < 3; ++a) down[f][a] = cfg.reset_feet_refresh ? p.pos[a] + w3[a] : feet[f][a];
       f_last[f] = 0.f;
       step_len[f] = 0.f;
     }
@@ -3630,6 +3680,13 @@ __global__ void zb_m_reset_kernel(const zb_model* __restrict__ mg, const float4*
     atomicAdd(&acc_slot(acc, t)[ACC_MET0], ST(ZB_M_METRICS));
     atomicAdd(&acc_slot(acc, t)[ACC_MET1], ST(ZB_M_METRICS + 1));
   }
+  float pre[2][3];  // the pre-reset feet (the spawn pose at construction)
+  if (!cfg.reset_feet_refresh) {
+    Phys p0;
+    if (init) phys_default(m, p0);
+    else load_phys(st, N, i, p0);
+    feet_world(m, p0, pre);
+  }
   Phys p;
   const uint64_t hs = env_hash(seed, cnt->calls, i);
   (void)reset_pose(m, cfg, hs, p);
@@ -3656,7 +3713,7 @@ __global__ void zb_m_reset_kernel(const zb_model* __restrict__ mg, const float4*
     float w3[3];
     mv3(R, v, w3);
 #pragma unroll
-    for (int a = 0; a < 3; ++a) ST(ZB_M_FEET_DOWN_POS + 3 * f + a) = p.pos[a] + w3[a];
+    for (int a = 0; a < 3; ++a) ST(ZB_M_FEET_DOWN_POS + 3 * f + a) = cfg.reset_feet_refresh ? p.pos[a] + w3[a] : pre[f][a];
     ST(ZB_M_FEET_STEP_LEN + f) = 0.f;
     ST(ZB_M_FEET_F_LAST + f) = 0.f;
     ST(ZB_M_FEET_AIR_CUR + f) = 0.f;
@@ -3941,7 +3998,8 @@ int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_dev
       for (int ci = 0; ci < 2; ++ci)
         for (int v = 0; v < 3; ++v) {
           const float* c = m->link_circle[l][ci] + 3 * v;
-          t[1 + 3 * ci + v] = make_float4(c[0], c[1], c[2], 0.f);
+          // C.w = 1: a mated face duplicating a lower link's circle (ground detection skips it)
+          t[1 + 3 * ci + v] = make_float4(c[0], c[1], c[2], v == 0 && ((m->link_circle_dup[l] >> ci) & 1) ? 1.f : 0.f);
         }
       const float* s0 = m->link_sphere[l][0];
       const float* s1 = m->link_sphere[l][1];
@@ -4012,8 +4070,9 @@ int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_dev
     const uint64_t one = 1;
     HIPCHK(hipMemcpy(&h->d_cnt->calls, &one, sizeof(one), hipMemcpyHostToDevice), "hipMemcpy counters");
   } else {
+    // construction: the spawn pose is the default pose, so the latch reads the default feet
     zb_reset_kernel<<<(num_envs + 255) / 256, 256>>>(h->d_model, h->d_links, num_envs, h->d_state, nullptr, num_envs,
-                                                      h->d_acc);
+                                                      h->d_acc, 1);
     rc = launch_check("zb_reset_kernel");
   }
   if (rc) return rc;
@@ -4120,7 +4179,8 @@ int zb_reset(zb_handle h, const int32_t* env_ids, int n, void* stream) {
     zb_m_reset_kernel<<<(cnt + 255) / 256, 256, 0, s>>>(h->d_model, h->d_links, h->cfg, h->n, h->d_state, env_ids, cnt,
                                                         h->d_acc, h->d_cnt, h->seed, 0);
   else
-    zb_reset_kernel<<<(cnt + 255) / 256, 256, 0, s>>>(h->d_model, h->d_links, h->n, h->d_state, env_ids, cnt, h->d_acc);
+    zb_reset_kernel<<<(cnt + 255) / 256, 256, 0, s>>>(h->d_model, h->d_links, h->n, h->d_state, env_ids, cnt, h->d_acc,
+                                                      h->cfg.reset_feet_refresh);
   int rc = launch_check("zb_reset_kernel");
   if (rc) return rc;
   return finalize(h, s, env_ids == nullptr || n == h->n, 1, 0);

@@ -125,6 +125,7 @@ class ZbModel(C.Structure):
         ("base_link", C.c_int32), ("foot_links", C.c_int32 * 2), ("undesired_links", C.c_int32 * 10),
         ("api_root_link", C.c_int32), ("api_root_in_root", C.c_float * 7),
         ("api_joint_index", C.c_int32 * NUM_DOF), ("api_joint_sign", C.c_float * NUM_DOF),
+        ("link_circle_dup", C.c_int32 * NUM_LINKS),
     ]
 
 
@@ -148,6 +149,7 @@ class ZbTaskCfg(C.Structure):
         ("action_scale", C.c_float), ("action_clip", C.c_float), ("obs_corruption", C.c_int32),
         ("obs_noise", C.c_float * 3), ("cmd_resample_s", C.c_float), ("cmd_rel_standing", C.c_float),
         ("feet_close_min", C.c_float),
+        ("reset_feet_refresh", C.c_int32),
     ]
 
 
@@ -457,7 +459,34 @@ def pack_model(rm: RobotModel | None = None) -> ZbModel:
     for k in range(NUM_DOF):
         m.api_joint_index[k] = rm.api_joint_index[k]
         m.api_joint_sign[k] = rm.joint_sign[k]
+    for i, bits in enumerate(duplicate_circles(rm)):
+        m.link_circle_dup[i] = bits
     return m
+
+
+def duplicate_circles(rm: RobotModel, tol: float = 1e-5) -> list:
+    """Per link, bit ci set when circle ci coincides with a circle of a lower-indexed link of the same
+    rigid composite (the mated faces of b_i and a_{i+1} across each fixed joint: same centre, plane and
+    radius). Ground detection skips those, so a mated face yields one contact set (owned by the
+    lower link) instead of two near-identical sets whose order in the 12-slot selection would be
+    decided by rounding."""
+    out = [0] * NUM_LINKS
+    body = lambda l: (l + 1) >> 1  # noqa: E731  (the serial-chain topology, include/zbot.h)
+    for l in range(NUM_LINKS):
+        for ci in range(2):
+            A = np.asarray(rm.circles[l, ci], np.float64)
+            nA = np.cross(A[3:6], A[6:9])
+            for k in range(l):
+                if body(k) != body(l):
+                    continue
+                for cj in range(2):
+                    B = np.asarray(rm.circles[k, cj], np.float64)
+                    nB = np.cross(B[3:6], B[6:9])
+                    same_plane = np.linalg.norm(np.cross(nA / np.linalg.norm(nA), nB / np.linalg.norm(nB))) < tol
+                    same_r = abs(np.linalg.norm(A[3:6]) - np.linalg.norm(B[3:6])) < tol
+                    if np.abs(A[:3] - B[:3]).max() < tol and same_plane and same_r:
+                        out[l] |= 1 << ci
+    return out
 
 
 @dataclass
@@ -510,6 +539,9 @@ class TaskCfg:
     cmd_resample_s: float = 10.0
     cmd_rel_standing: float = 0.02
     feet_close_min: float = 0.12
+    # feet_down_pos_last on reset: False = pre-reset feet (the reference's call order, v2.py:436),
+    # True = post-reset feet
+    reset_feet_refresh: bool = False
     range_period_steps: int | None = None   # manager: lin_vel_cmd_levels fires on counter % this == 0
 
     @classmethod
@@ -636,6 +668,7 @@ class TaskCfg:
         c.cmd_resample_s = self.cmd_resample_s
         c.cmd_rel_standing = self.cmd_rel_standing
         c.feet_close_min = self.feet_close_min
+        c.reset_feet_refresh = int(self.reset_feet_refresh)
         c.reset_pose_body_frame = int(self.reset_pose_body_frame)
         c.task = self.task
         for k in range(4):
