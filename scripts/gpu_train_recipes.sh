@@ -1,0 +1,27 @@
+#!/usr/bin/env bash
+# Behavioural anchors: the stand-up task at the reference's scale and the
+# staged v2 recipe (step2 -> step3 -> step4, 2000 iterations each, chained with --resume), then play.
+# Logs under gpurun_out/train/ (copy the summaries into profiles/<round>_train/).
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out/train
+export TMPDIR=/tmp
+LR=gpurun_out/train/logs
+IT=${ITERS:-2000}
+run() {  # name limit args...
+  local n=$1 l=$2; shift 2
+  echo "== $n"
+  timeout -k 10 $l python -u "$@" > gpurun_out/train/$n.log 2>&1; local rc=$?
+  tail -n 1 gpurun_out/train/$n.log
+  if [ $rc -ne 0 ]; then echo "stop ($n rc=$rc)"; tail -20 gpurun_out/train/$n.log; exit $rc; fi
+}
+if [ -z "${SKIP_STANDUP:-}" ]; then
+  run standup_train 1500 scripts/train.py --task zbot-6b-standup-v0 --num_envs 4096 --max_iterations $IT --log_root $LR --log-every 50 --run_name su4096
+  run standup_play 300 scripts/play.py --task zbot-6b-standup-v0 --num_envs 1024 --log_root $LR --num_steps 290 --fresh_episodes
+fi
+if [ -z "${SKIP_V2:-}" ]; then
+  run v2_step2 1500 scripts/train.py --task zbot-6b-walking-v2 --num_envs 4096 --max_iterations $IT --log_root $LR --log-every 50 --reward_cfg step2 --run_name step2
+  run v2_step3 1500 scripts/train.py --task zbot-6b-walking-v2 --num_envs 4096 --max_iterations $IT --log_root $LR --log-every 50 --reward_cfg step3 --run_name step3 --resume --load_run '.*_step2'
+  run v2_step4 1500 scripts/train.py --task zbot-6b-walking-v2 --num_envs 4096 --max_iterations $IT --log_root $LR --log-every 50 --reward_cfg step4 --run_name step4 --resume --load_run '.*_step3'
+  run v2_play 300 scripts/play.py --task zbot-6b-walking-v2 --num_envs 1024 --log_root $LR --num_steps 999 --fresh_episodes
+fi
+echo done

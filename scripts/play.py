@@ -23,6 +23,26 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+def _posture(env, st, max_envs: int = 512) -> dict:
+    """Posture at the end of the rollout from the final states (the robot model's FK on the host):
+    base link height (v2 dies below 0.22 m, v2.py:405; the stand-up task's standing height) and
+    how upright the feet are (foot z axis . world z; foot_1's sole normal is -z, v2.py:341-343)."""
+    import numpy as np
+
+    from zbot_lab_amd import model as zm
+    rm = env.sim.robot
+    n = min(st.shape[1], max_envs)
+    bz, up = [], []
+    for e in range(n):
+        _, links = rm.fk(st[0:3, e], st[3:7, e], st[13:19, e])
+        bz.append(links[rm.base_link].p[2])
+        up.append([zm.qrot(links[li].q, np.array([0.0, 0.0, sg]))[2] for li, sg in ((0, 1.0), (11, -1.0))])
+    bz, up = np.asarray(bz), np.asarray(up)
+    return {"final_base_z_mean": float(bz.mean()), "final_base_z_quantiles_10_50_90": np.quantile(bz, [0.1, 0.5, 0.9]).tolist(),
+            "final_frac_base_z_ge_0.20": float((bz >= 0.20).mean()),
+            "final_feet_up_alignment_mean": up.mean(axis=0).tolist(), "posture_envs": n}
+
+
 def main(argv=None) -> dict:
     ap = argparse.ArgumentParser(description="Play a checkpoint of an RL agent (zbot_lab_amd).")
     ap.add_argument("--task", default="zbot-6b-walking-v2")
@@ -35,6 +55,8 @@ def main(argv=None) -> dict:
     ap.add_argument("--log_root", default=os.path.join("logs", "rsl_rl"))
     ap.add_argument("--num_steps", type=int, default=1000)
     ap.add_argument("--no_export", action="store_true")
+    ap.add_argument("--fresh_episodes", action="store_true",
+                    help="start every env at episode step 0 (the posture summary then describes step --num_steps)")
     args = ap.parse_args(argv)
 
     import zbot_lab_amd
@@ -79,6 +101,8 @@ def main(argv=None) -> dict:
     n = env.num_envs
     dt = env.unwrapped.step_dt
     x_row = zm.S["ROOT_POS"]
+    if args.fresh_episodes:
+        env.unwrapped.episode_length_buf = torch.zeros_like(env.unwrapped.episode_length_buf)
     obs = env.get_observations()
     obs = obs["policy"] if hasattr(obs, "keys") else obs
     x_prev = sim.get_state()[x_row].clone()
@@ -110,13 +134,14 @@ def main(argv=None) -> dict:
             ep_len.masked_fill_(d, 0.0)
             x_prev = x.clone()
     f = fin.tolist()
+    posture = _posture(env.unwrapped, sim.get_state().cpu().numpy())
     out = {"task": args.task, "checkpoint": resume_path, "exported_jit": exported, "num_envs": n,
            "num_steps": args.num_steps, "mean_reward_per_step": float(rew_sum) / (n * args.num_steps),
            "episodes_finished": int(f[0]), "time_outs": int(f[4]),
            "mean_episode_length": f[1] / f[0] if f[0] else None,
            "mean_episode_return": f[2] / f[0] if f[0] else None,
            "mean_forward_distance_per_episode_m": f[3] / f[0] if f[0] else None,
-           "mean_forward_velocity_m_s": float(vel_sum) / max(float(vel_cnt), 1.0)}
+           "mean_forward_velocity_m_s": float(vel_sum) / max(float(vel_cnt), 1.0), **posture}
     print(json.dumps(out), flush=True)
     env.close()
     return out

@@ -49,6 +49,9 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--log_root", default=os.path.join("logs", "rsl_rl"),
                     help="parent of the experiment folders (reference: logs/rsl_rl)")
     ap.add_argument("--log-every", type=int, default=1)
+    ap.add_argument("--reward_cfg", default=None,
+                    help="zbot-6b-walking-v2 reward stage (step2 / step3 / step4 = v2.py:150-206); the reference "
+                         "edits the active reward_cfg in v2.py between its chained 2000-iteration runs")
     return ap
 
 
@@ -84,6 +87,9 @@ def main(argv=None) -> dict:
         env_cfg.scene.num_envs = args.num_envs
     if args.max_iterations is not None:
         agent_cfg.max_iterations = args.max_iterations
+    if args.reward_cfg is not None:
+        from zbot_lab_amd.envs.walking_v2 import REWARD_CFGS
+        env_cfg.reward_cfg = REWARD_CFGS[args.reward_cfg]
 
     rank, local_rank = 0, 0
     if args.distributed:  # train.py:125-132: device per local rank, seed + rank

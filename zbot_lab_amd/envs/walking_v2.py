@@ -52,6 +52,24 @@ class SolverCfg:
     self_collision: bool = True       # enabled_self_collisions=True (zbot_cfg.py:636)
 
 
+def _scales(**kw) -> dict:
+    return {"reward_scales": dict(kw)}
+
+
+# The staged training recipe of v2.py:150-206: the reference trains 2000 iterations per stage and
+# chains the stages with ``--resume`` (README.md:69), editing the active ``reward_cfg`` between
+# runs; ``step4`` is the active one (v2.py:190-206). scripts/train.py --reward_cfg selects a stage.
+REWARD_CFGS = {
+    "step2": _scales(base_vel_forward=1.0, feet_downward=-2.0, feet_forward=-1.0, base_heading_x=-1.0,  # v2.py:150-167
+                     base_heading_x_sum=-3.0, step_length=5.0, airtime_balance=-15.0, action_rate=-0.1,
+                     torques=-0.002, feet_slide=-10.0, base_pos_y_err=-1.0, base_pos_y_err_sum=-2.0),
+    "step3": _scales(base_vel_forward=1.0, feet_downward=-2.0, feet_forward=-1.0, base_heading_x=-1.0,  # v2.py:169-186
+                     base_heading_x_sum=-5.0, step_length=5.0, airtime_balance=-15.0, action_rate=-0.1,
+                     torques=-0.002, feet_slide=-10.0, base_pos_y_err=-2.0, base_pos_y_err_sum=-2.0),
+    "step4": {"reward_scales": dict(zm.REWARD_WEIGHTS)},                                              # v2.py:190-206
+}
+
+
 @dataclass
 class ZbotDirectEnvCfgV2:
     """Mirror of ``ZbotDirectEnvCfgV2`` (v2.py:26-206)."""
@@ -68,6 +86,9 @@ class ZbotDirectEnvCfgV2:
     reward_cfg: dict = field(default_factory=lambda: {"reward_scales": dict(zm.REWARD_WEIGHTS)})
 
     def task_cfg(self) -> zm.TaskCfg:
+        unknown = set(self.reward_cfg["reward_scales"]) - set(zm.REWARD_TERMS)
+        if unknown:  # e.g. step0's feet_force_diff / feet_force_sum (v2.py:78-91, 563-571)
+            raise NotImplementedError(f"reward terms not compiled into zb_step_kernel: {sorted(unknown)}")
         return zm.TaskCfg(
             sim_dt=self.sim.dt, decimation=self.decimation, episode_length_s=self.episode_length_s,
             termination_height=self.termination_height,
@@ -181,7 +202,11 @@ class ZbotDirectEnvV2:
         # them is built once (no per-step tensor work)
         if getattr(self, "_log", None) is None:
             means, counts = self.sim.read_log()
-            self._log = {k: means[i] for i, k in enumerate(self._log_keys)}
+            # _episode_sums holds the active reward_cfg's keys only (v2.py:254-256)
+            rc = getattr(self.cfg, "reward_cfg", None)
+            active = rc["reward_scales"] if isinstance(rc, dict) and "reward_scales" in rc else None
+            self._log = {k: means[i] for i, k in enumerate(self._log_keys)
+                         if active is None or k.split("/", 1)[1] in active}
             self._log[self._termination_keys[0]] = counts[0]
             self._log[self._termination_keys[1]] = counts[1]
         self.extras["log"] = self._log
