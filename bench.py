@@ -18,11 +18,12 @@ bounded sample, with nproc / affinity / cgroup quota / CPU model stated.
 ``--task v4`` measures zbot-6b-walking-v4 (commands / events / curricula; ``zb_v4_step_kernel``, 790 B
 per env-step: 81 state rows read, 85 written, actions, obs 96 B, reward, flags) at 4096 envs.
 ``--task manager`` measures zbot-6b-walking-m-v0 (the manager-based flat env on ZBOT_6S_V2_CFG;
-``zb_m_step_kernel``, 786 B per env-step: 76 state rows read + written, 12 friction coefficients
-read, actions 24 B, obs 100 B, reward, flags) at 4096 envs with the startup friction randomisation.
+``zb_m_step_kernel``, 834 B per env-step: 76 state rows read + written, 24 static / dynamic friction
+coefficients read, actions 24 B, obs 100 B, reward, flags) at 4096 envs with the startup friction randomisation.
 ``--task standup`` measures the stand-up task instead (zbot-6b-standup-v0,
-32768 envs, friction randomisation on; kernel ``zb_su_step_kernel``, 510 B per env-step: 43 fp32
-state rows read + written, 12 friction coefficients read, actions 24 B, obs 88 B, reward, flags).
+32768 envs, friction randomisation on; kernel ``zb_su_step_kernel``, 558 B per env-step: 43 fp32
+state rows read + written, 24 static / dynamic friction coefficients read, actions 24 B, obs 88 B,
+reward, flags).
 """
 from __future__ import annotations
 
@@ -36,9 +37,9 @@ import torch
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 BYTES_PER_ENV_STEP = 794
-SU_BYTES_PER_ENV_STEP = 2 * 43 * 4 + 12 * 4 + 24 + 88 + 4 + 2  # = 510, stand-up task
+SU_BYTES_PER_ENV_STEP = 2 * 43 * 4 + 24 * 4 + 24 + 88 + 4 + 2  # = 558, stand-up task
 V4_BYTES_PER_ENV_STEP = 81 * 4 + 85 * 4 + 24 + 96 + 4 + 2       # = 790, walking v4
-M_BYTES_PER_ENV_STEP = 76 * 4 + 76 * 4 + 12 * 4 + 24 + 100 + 4 + 2  # = 786, manager flat env
+M_BYTES_PER_ENV_STEP = 76 * 4 + 76 * 4 + 24 * 4 + 24 + 100 + 4 + 2  # = 834, manager flat env
 
 
 def parse():

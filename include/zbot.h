@@ -113,8 +113,9 @@ enum zb_standup_state_field {
   ZB_SU_CENTER_Z_LAST = 37, /* 1  standup.py:511,639-641 */
   ZB_SU_EP_LEN = 38,        /* 1  episode_length_buf (integer-valued float) */
   ZB_SU_EP_SUMS = 39,       /* 4  _episode_sums in reward-term order */
-  ZB_SU_LINK_MU = 43,       /* 12 per-link friction coefficient (read-only for zb_step) */
-  ZB_SU_STATE_DIM = 55
+  ZB_SU_LINK_MU = 43,       /* 12 per-link static friction coefficient (read-only for zb_step) */
+  ZB_SU_LINK_MU_D = 55,     /* 12 per-link dynamic friction coefficient (read-only for zb_step) */
+  ZB_SU_STATE_DIM = 67
 };
 
 /* v4 state, SoA [ZB_V4_STATE_DIM][num_envs] float32; rows 0..24 as in zb_state_field. */
@@ -158,8 +159,9 @@ enum zb_manager_state_field {
   ZB_M_METRICS = 62,          /* 2  command metrics error_vel_xy, error_vel_yaw */
   ZB_M_EP_LEN = 64,           /* 1 */
   ZB_M_EP_SUMS = 65,          /* 11 reward manager episode sums */
-  ZB_M_LINK_MU = 76,          /* 12 per-link friction (physics_material startup event) */
-  ZB_M_STATE_DIM = 88
+  ZB_M_LINK_MU = 76,          /* 12 per-link static friction (physics_material startup event) */
+  ZB_M_LINK_MU_D = 88,        /* 12 per-link dynamic friction */
+  ZB_M_STATE_DIM = 100
 };
 
 /* Manager reward term order = RewardsCfg field order of Zbot6BFlatEnvCfg (zbotlab_env_cfg.py,
@@ -246,7 +248,7 @@ typedef struct zb_task_cfg {
   float terminal_penalty;      /* 20 (v2.py:380); standup 2 (standup.py:630) */
   float joint_speed_limit;     /* 1.0 (v2.py:243) */
   float gravity;               /* 9.81 */
-  float friction;              /* 1.0 static = dynamic, multiply combine (v2.py:49-56,62-68) */
+  float friction;              /* static friction 1.0, multiply combine (v2.py:49-56,62-68) */
   float contact_force_threshold; /* 1.0 N ContactSensorCfg.force_threshold default */
   float contact_margin;        /* speculative contact distance (m) */
   float baumgarte;             /* penetration correction per step (fraction) */
@@ -296,6 +298,9 @@ typedef struct zb_task_cfg {
    * (terminal) feet positions, as the reference's call order reads them (body_link_pos_w before
    * DirectRLEnv.step's sim.forward()); 1 = the post-reset feet positions */
   int32_t reset_feet_refresh;
+  /* dynamic (sliding) friction of the uniform-material tasks: 1.0 (v2.py:49-56,62-68); a contact
+   * whose friction impulse would exceed mu_static * normal slides with mu_dynamic * normal */
+  float friction_dynamic;
 } zb_task_cfg;
 
 typedef struct zb_sim* zb_handle;
@@ -341,11 +346,14 @@ int zb_set_state(zb_handle h, const float* src, void* stream);
 int zb_physics_substeps(zb_handle h, const float* targets, int nsub, float* net_force,
                         float* applied_torque, void* stream);
 
-/* Standup: per-link friction coefficients, device float[N][12] (link order of ZB_NUM_LINKS),
- * e.g. the static friction sampled by randomize_rigid_body_material. Ground contacts use
- * mu[link] * cfg.friction (the terrain's coefficient, multiply combine), self contacts
- * mu[a] * mu[b]. A new handle starts at cfg.friction for every link. */
+/* Standup / manager: per-link friction coefficients, device float[N][12] (link order of
+ * ZB_NUM_LINKS), e.g. the static / dynamic friction sampled by randomize_rigid_body_material
+ * (standup.py:124-136). Ground contacts use mu[link] * cfg.friction (the terrain's coefficient,
+ * multiply combine), self contacts mu[a] * mu[b], for the static and the dynamic coefficient
+ * alike. A new handle starts at cfg.friction / cfg.friction_dynamic for every link.
+ * zb_set_link_friction sets both coefficients to `mu`; zb_set_link_friction_sd sets them apart. */
 int zb_set_link_friction(zb_handle h, const float* mu, void* stream);
+int zb_set_link_friction_sd(zb_handle h, const float* mu_static, const float* mu_dynamic, void* stream);
 
 /* Curriculum stage and common_step_counter (zb_step calls). Host pointers; synchronises. */
 int zb_read_curriculum(zb_handle h, int32_t* stage, int64_t* common_step_counter);

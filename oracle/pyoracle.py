@@ -52,7 +52,7 @@ def _load(double: bool = False):
     lib.zbo_mdp_eval.argtypes = [C.c_int, C.POINTER(zm.ZbTaskCfg), _f, _f, _f, _f, _f, _f, _i, _f, _f, _f,
                                  _f, _f, _f, _f, _u8, _u8]
     lib.zbo_state_dim.argtypes = [P]
-    lib.zbo_set_link_friction.argtypes = [P, _f]
+    lib.zbo_set_link_friction.argtypes = [P, _f, C.c_void_p]
     lib.zbo_read_curriculum.argtypes = [P, C.POINTER(C.c_int32), C.POINTER(C.c_int64)]
     lib.zbo_su_mdp_eval.argtypes = [C.c_int, C.POINTER(zm.ZbTaskCfg), C.c_int, _f, _f, _i, _f, _f, _f, _f, _u8, _u8]
     lib.zbo_su_reset_pose.argtypes = [C.POINTER(zm.ZbModel), C.POINTER(zm.ZbTaskCfg), C.c_uint64, C.c_uint64, C.c_int,
@@ -133,8 +133,9 @@ class OracleSim:
         self.lib.zbo_read_log(self.h, m, c)
         return (m if full else m[:self.num_terms]), c
 
-    def set_link_friction(self, mu):
-        if self.lib.zbo_set_link_friction(self.h, f32(mu)) != 0:
+    def set_link_friction(self, mu, mu_dynamic=None):
+        md = None if mu_dynamic is None else f32(mu_dynamic)
+        if self.lib.zbo_set_link_friction(self.h, f32(mu), None if md is None else md.ctypes.data_as(C.c_void_p)) != 0:
             raise ValueError("per-link friction is a standup / manager task state")
 
     def read_curriculum(self):

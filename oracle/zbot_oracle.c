@@ -152,7 +152,7 @@ typedef struct {
 typedef struct {
   real p_delta[ND], actions[ND];
   real center_z_last;                 /* standup only (standup.py:511) */
-  real mu[NL];                        /* standup only: per-link friction (DR) */
+  real mu[NL], mu_d[NL];              /* standup / manager: per-link static / dynamic friction (DR) */
   real commands[3], target_yaw, interval_left, current_yaw; /* v4 (2 commands) / manager (3; interval_left =
                                                              command time_left) */
   real cmd_standing, metrics[2];      /* manager only */
@@ -505,10 +505,11 @@ typedef struct {
   real applied_torque[ND]; /* Isaac Lab ImplicitActuator estimate at substep start */
 } substep_out_t;
 
-/* mu_link: per-link friction (standup DR; contact coefficient = product, the ground's being
- * cfg->friction), or NULL for cfg->friction on every contact */
+/* mu_link / mu_link_d: per-link static / dynamic friction (standup / manager DR; contact
+ * coefficient = product, the ground's being cfg->friction / cfg->friction_dynamic), or NULL for
+ * the cfg coefficients on every contact */
 static void substep(const mdl_t* m, const zb_task_cfg* cfg, phys_t* s, const real target[ND],
-                    const real* mu_link, substep_out_t* out) {
+                    const real* mu_link, const real* mu_link_d, substep_out_t* out) {
   const real dt = cfg->sim_dt;
   kin_t k;
   fk(m, s, &k);
@@ -627,7 +628,7 @@ static void substep(const mdl_t* m, const zb_task_cfg* cfg, phys_t* s, const rea
   detect(m, cfg, &k, s->root_pos[2], &CL);
   int nc = CL.n;
   real Y[NC_MAX][3][NV];
-  real invm[NC_MAX][3], vmin[NC_MAX], lam[NC_MAX][3], c01[NC_MAX], c02[NC_MAX], muc[NC_MAX];
+  real invm[NC_MAX][3], vmin[NC_MAX], lam[NC_MAX][3], c01[NC_MAX], c02[NC_MAX], muc[NC_MAX], mud[NC_MAX];
   real dirs[NC_MAX][3][3];
   for (int c = 0; c < nc; ++c) {
     const contact_t* ct = &CL.c[c];
@@ -635,6 +636,8 @@ static void substep(const mdl_t* m, const zb_task_cfg* cfg, phys_t* s, const rea
     tangents(ct->n, dirs[c][1], dirs[c][2]);
     /* friction combine mode "multiply" (link x ground, link x link) */
     muc[c] = mu_link ? mu_link[ct->la] * (ct->lb >= 0 ? mu_link[ct->lb] : (real)cfg->friction) : (real)cfg->friction;
+    mud[c] = mu_link_d ? mu_link_d[ct->la] * (ct->lb >= 0 ? mu_link_d[ct->lb] : (real)cfg->friction_dynamic)
+                       : (real)cfg->friction_dynamic;
     for (int r = 0; r < 3; ++r) {
       real J[NV], Jb[NV];
       jac_row(&k, m->link_body[ct->la], ct->x, dirs[c][r], J);
@@ -671,10 +674,12 @@ static void substep(const mdl_t* m, const zb_task_cfg* cfg, phys_t* s, const rea
       real vt1 = v1 + c01[c] * dl, vt2 = v2 + c02[c] * dl;
       real l1 = lam[c][1] - vt1 * invm[c][1];
       real l2 = lam[c][2] - vt2 * invm[c][2];
+      /* static / dynamic Coulomb disk: beyond mu_s ln the contact slides with mu_d ln
+       * (PhysX's static -> dynamic switch; mu_d = mu_s is the plain disk projection) */
       real lim = mu * ln;
       real mag2 = l1 * l1 + l2 * l2;
       if (mag2 > lim * lim) {
-        real sc = lim / sqrtr(mag2);
+        real sc = mud[c] * ln / sqrtr(mag2);
         l1 *= sc; l2 *= sc;
       }
       real d1 = l1 - lam[c][1], d2 = l2 - lam[c][2];
@@ -1154,7 +1159,7 @@ static real su_step_env(const mdl_t* m, const zb_task_cfg* cfg, int stage, uint6
     target[j] = md->p_delta[j] + m->jq0[j];
   }
   substep_out_t so;
-  for (int k = 0; k < cfg->decimation; ++k) substep(m, cfg, &e->ph, target, md->mu, &so);
+  for (int k = 0; k < cfg->decimation; ++k) substep(m, cfg, &e->ph, target, md->mu, md->mu_d, &so);
   md->ep_len += 1;
   for (int j = 0; j < ND; ++j) md->actions[j] = act[j];
   su_links_t L;
@@ -1183,7 +1188,7 @@ static void su_pack_env(const env_t* e, float* st, int n, int i) {
   PUT(ZB_SU_CENTER_Z_LAST, e->md.center_z_last);
   PUT(ZB_SU_EP_LEN, e->md.ep_len);
   for (int t = 0; t < ZB_SU_NUM_REWARD_TERMS; ++t) PUT(ZB_SU_EP_SUMS + t, e->md.ep_sums[t]);
-  for (int l = 0; l < NL; ++l) PUT(ZB_SU_LINK_MU + l, e->md.mu[l]);
+  for (int l = 0; l < NL; ++l) { PUT(ZB_SU_LINK_MU + l, e->md.mu[l]); PUT(ZB_SU_LINK_MU_D + l, e->md.mu_d[l]); }
 #undef PUT
 }
 static void su_unpack_env(env_t* e, const float* st, int n, int i) {
@@ -1197,7 +1202,7 @@ static void su_unpack_env(env_t* e, const float* st, int n, int i) {
   e->md.center_z_last = GET(ZB_SU_CENTER_Z_LAST);
   e->md.ep_len = (int32_t)lrint((double)st[(size_t)ZB_SU_EP_LEN * n + i]);
   for (int t = 0; t < ZB_SU_NUM_REWARD_TERMS; ++t) e->md.ep_sums[t] = GET(ZB_SU_EP_SUMS + t);
-  for (int l = 0; l < NL; ++l) e->md.mu[l] = GET(ZB_SU_LINK_MU + l);
+  for (int l = 0; l < NL; ++l) { e->md.mu[l] = GET(ZB_SU_LINK_MU + l); e->md.mu_d[l] = GET(ZB_SU_LINK_MU_D + l); }
 #undef GET
 }
 
@@ -1443,7 +1448,7 @@ static real v4_step_env(const zbo_sim* s, int stage, uint64_t ctr, int i, env_t*
   for (int k = 0; k < cfg->decimation; ++k) {
     if (k == cfg->decimation - 1)
       for (int j = 0; j < ND; ++j) jqd_prev[j] = e->ph.jqd[j];
-    substep(m, cfg, &e->ph, target, NULL, &so);
+    substep(m, cfg, &e->ph, target, NULL, NULL, &so);
     v4_sensor_update(m, cfg, md, so.net_force);
   }
   md->ep_len += 1;
@@ -1760,7 +1765,7 @@ static real m_step_env(const zbo_sim* s, uint64_t ctr, int i, env_t* e, const fl
     for (int j = 0; j < ND; ++j) target[j] = e->ph.jq[j] + delta[j]; /* apply_actions: q + delta */
     if (k == cfg->decimation - 1)
       for (int j = 0; j < ND; ++j) jqd_prev[j] = e->ph.jqd[j];
-    substep(m, cfg, &e->ph, target, md->mu, &so);
+    substep(m, cfg, &e->ph, target, md->mu, md->mu_d, &so);
     /* ContactSensor.update (every physics step): history shift, air time with elapsed sim_dt */
     for (int f = 0; f < 2; ++f) {
       const real* F = so.net_force[m->foot_links[f]];
@@ -1869,7 +1874,7 @@ static void m_pack_env(const env_t* e, float* st, int n, int i) {
   }
   PUT(ZB_M_EP_LEN, e->md.ep_len);
   for (int t = 0; t < ZB_M_NUM_REWARD_TERMS; ++t) PUT(ZB_M_EP_SUMS + t, e->md.ep_sums[t]);
-  for (int l = 0; l < NL; ++l) PUT(ZB_M_LINK_MU + l, e->md.mu[l]);
+  for (int l = 0; l < NL; ++l) { PUT(ZB_M_LINK_MU + l, e->md.mu[l]); PUT(ZB_M_LINK_MU_D + l, e->md.mu_d[l]); }
 #undef PUT
 }
 
@@ -1893,7 +1898,7 @@ static void m_unpack_env(env_t* e, const float* st, int n, int i) {
   }
   e->md.ep_len = (int32_t)lrint((double)st[(size_t)ZB_M_EP_LEN * n + i]);
   for (int t = 0; t < ZB_M_NUM_REWARD_TERMS; ++t) e->md.ep_sums[t] = GET(ZB_M_EP_SUMS + t);
-  for (int l = 0; l < NL; ++l) e->md.mu[l] = GET(ZB_M_LINK_MU + l);
+  for (int l = 0; l < NL; ++l) { e->md.mu[l] = GET(ZB_M_LINK_MU + l); e->md.mu_d[l] = GET(ZB_M_LINK_MU_D + l); }
 #undef GET
 }
 
@@ -2002,12 +2007,12 @@ zbo_sim* zbo_create(const zb_model* model, const zb_task_cfg* cfg, int num_envs,
     memset(&s->env[i], 0, sizeof(env_t));
     phys_default(&s->m, &s->env[i].ph); /* the spawn pose: what the construction-time reset's latch reads */
     if (cfg->task == ZB_TASK_STANDUP_V0) {
-      for (int l = 0; l < NL; ++l) s->env[i].md.mu[l] = cfg->friction;
+      for (int l = 0; l < NL; ++l) { s->env[i].md.mu[l] = cfg->friction; s->env[i].md.mu_d[l] = cfg->friction_dynamic; }
       su_reset_env(&s->m, cfg, seed, 0, i, &s->env[i]); /* construction draws at RNG position 0 */
     } else if (cfg->task == ZB_TASK_WALKING_V4) {
       v4_reset_env(s, 0, i, &s->env[i], 1);
     } else if (cfg->task == ZB_TASK_MANAGER_V0) {
-      for (int l = 0; l < NL; ++l) s->env[i].md.mu[l] = cfg->friction;
+      for (int l = 0; l < NL; ++l) { s->env[i].md.mu[l] = cfg->friction; s->env[i].md.mu_d[l] = cfg->friction_dynamic; }
       m_reset_env(s, 0, i, &s->env[i]);
     } else {
       reset_env(&s->m, cfg, &s->env[i]);
@@ -2099,7 +2104,7 @@ static real step_env(const mdl_t* m, const zb_task_cfg* cfg, env_t* e, const flo
   /* physics */
   substep_out_t so;
   for (int k = 0; k < cfg->decimation; ++k) {
-    substep(m, cfg, &e->ph, target, NULL, &so);
+    substep(m, cfg, &e->ph, target, NULL, NULL, &so);
     sensor_update(m, cfg, md, so.net_force);
   }
   md->ep_len += 1;
@@ -2278,12 +2283,19 @@ int zbo_state_dim(zbo_sim* s) {
          : s->c.task == ZB_TASK_MANAGER_V0 ? ZB_M_STATE_DIM : ZB_STATE_DIM;
 }
 
-/* standup / manager: per-link friction [n][12] */
-int zbo_set_link_friction(zbo_sim* s, const float* mu) {
+/* standup / manager: per-link static / dynamic friction [n][12] (mu_d NULL: = mu) */
+int zbo_set_link_friction(zbo_sim* s, const float* mu, const float* mu_d) {
   if (s->c.task != ZB_TASK_STANDUP_V0 && s->c.task != ZB_TASK_MANAGER_V0) return -1;
   for (int e = 0; e < s->n; ++e)
-    for (int l = 0; l < NL; ++l) s->env[e].md.mu[l] = mu[(size_t)e * NL + l];
+    for (int l = 0; l < NL; ++l) {
+      s->env[e].md.mu[l] = mu[(size_t)e * NL + l];
+      s->env[e].md.mu_d[l] = (mu_d ? mu_d : mu)[(size_t)e * NL + l];
+    }
   return 0;
+}
+
+int zbo_set_link_friction_sd(zbo_sim* s, const float* mu_static, const float* mu_dynamic) {
+  return zbo_set_link_friction(s, mu_static, mu_dynamic);
 }
 
 int zbo_read_curriculum(zbo_sim* s, int32_t* stage, int64_t* steps) {
@@ -2299,8 +2311,10 @@ int zbo_physics_substeps(zbo_sim* s, const float* targets, int nsub, float* net_
     for (int j = 0; j < ND; ++j) tg[j] = targets[(size_t)e * ND + j];
     substep_out_t so;
     memset(&so, 0, sizeof(so));
-    const real* mu = s->c.task == ZB_TASK_STANDUP_V0 || s->c.task == ZB_TASK_MANAGER_V0 ? s->env[e].md.mu : NULL;
-    for (int k = 0; k < nsub; ++k) substep(&s->m, &s->c, &s->env[e].ph, tg, mu, &so);
+    const int dr = s->c.task == ZB_TASK_STANDUP_V0 || s->c.task == ZB_TASK_MANAGER_V0;
+    const real* mu = dr ? s->env[e].md.mu : NULL;
+    const real* mud = dr ? s->env[e].md.mu_d : NULL;
+    for (int k = 0; k < nsub; ++k) substep(&s->m, &s->c, &s->env[e].ph, tg, mu, mud, &so);
     if (net_force)
       for (int l = 0; l < NL; ++l)
         for (int a = 0; a < 3; ++a) net_force[((size_t)e * NL + l) * 3 + a] = (float)so.net_force[l][a];

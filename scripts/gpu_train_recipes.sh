@@ -5,7 +5,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out/train
 export TMPDIR=/tmp
-LR=gpurun_out/train/logs
+LR=/tmp/zb_train_logs   # checkpoints stay on the box; the per-iteration logs are copied back below
 IT=${ITERS:-2000}
 run() {  # name limit args...
   local n=$1 l=$2; shift 2
@@ -24,4 +24,5 @@ if [ -z "${SKIP_V2:-}" ]; then
   run v2_step4 1500 scripts/train.py --task zbot-6b-walking-v2 --num_envs 4096 --max_iterations $IT --log_root $LR --log-every 50 --reward_cfg step4 --run_name step4 --resume --load_run '.*_step3'
   run v2_play 300 scripts/play.py --task zbot-6b-walking-v2 --num_envs 1024 --log_root $LR --num_steps 999 --fresh_episodes
 fi
+for f in $(find $LR -name train_log.jsonl); do cp $f gpurun_out/train/$(basename $(dirname $f)).jsonl; done
 echo done

@@ -54,14 +54,15 @@ def row_groups(task: str) -> dict:
     if task == "standup":
         return dict(phys_pos=pos, phys_vel=vel,
                     exact=_rows(SU, "P_DELTA", 6) + _rows(SU, "ACTIONS", 6) + [SU["EP_LEN"]],
-                    force=[], kin=[SU["CENTER_Z_LAST"]], sums=_rows(SU, "EP_SUMS", 4), static=_rows(SU, "LINK_MU", 12))
+                    force=[], kin=[SU["CENTER_Z_LAST"]], sums=_rows(SU, "EP_SUMS", 4),
+                    static=_rows(SU, "LINK_MU", 12) + _rows(SU, "LINK_MU_D", 12))
     return dict(phys_pos=pos, phys_vel=vel,
                 exact=_rows(M, "ACTIONS", 6) + _rows(M, "COMMANDS", 3) + [M["CMD_TIME_LEFT"], M["CMD_STANDING"],
                                                                             M["EP_LEN"]]
                 + _rows(M, "FEET_AIR_CUR", 2) + _rows(M, "FEET_AIR_LAST", 2),
                 force=_rows(M, "FEET_F_LAST", 2) + _rows(M, "FEET_FZ_HIST", 6) + _rows(M, "FEET_FN_HIST", 6),
                 kin=_rows(M, "FEET_DOWN_POS", 6) + _rows(M, "FEET_STEP_LEN", 2) + _rows(M, "METRICS", 2),
-                sums=_rows(M, "EP_SUMS", 11), static=_rows(M, "LINK_MU", 12))
+                sums=_rows(M, "EP_SUMS", 11), static=_rows(M, "LINK_MU", 12) + _rows(M, "LINK_MU_D", 12))
 
 
 # episode-sum terms evaluated from state that is identical on both sides before the step (v2's
@@ -126,6 +127,7 @@ def random_states(task: str, o, n: int, seed: int, standing: bool = False) -> np
         bz = o.link_poses()[0][:, 6, 2]
         st[SU["CENTER_Z_LAST"]] = (bz + rng.uniform(-0.02, 0.08, n)).astype(f32)
         st[SU["LINK_MU"]:SU["LINK_MU"] + 12] = u(0.6, 1.0, 12)
+        st[SU["LINK_MU_D"]:SU["LINK_MU_D"] + 12] = u(0.6, 1.0, 12)   # independent draws (standup.py:131-132)
         return st
     # feet latches, step lengths, last forces
     st[D["FEET_DOWN_POS"]:D["FEET_DOWN_POS"] + 6] = (feet + rng.normal(0, 0.03, (n, 2, 3))).reshape(n, 6).T.astype(f32)
@@ -169,6 +171,7 @@ def random_states(task: str, o, n: int, seed: int, standing: bool = False) -> np
         st[M["FEET_FN_HIST"]:M["FEET_FN_HIST"] + 6] = np.sqrt(fz ** 2 + u(0.0, 5.0, 6) ** 2)
         st[M["METRICS"]:M["METRICS"] + 2] = u(0.0, 1.0, 2)
         st[M["LINK_MU"]:M["LINK_MU"] + 12] = u(0.3, 1.0, 12)
+        st[M["LINK_MU_D"]:M["LINK_MU_D"] + 12] = u(0.3, 1.0, 12)
     return st
 
 

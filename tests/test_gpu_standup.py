@@ -62,15 +62,17 @@ def test_friction_substep_parity(gpu):
     n = 512
     g, o, torch = _pair(n, seed=3)
     mu = _friction(n, 1)
-    g.set_link_friction(torch.from_numpy(mu).cuda())
-    o.set_link_friction(mu)
+    mud = _friction(n, 2)   # dynamic drawn independently (standup.py:131-132)
+    g.set_link_friction(torch.from_numpy(mu).cuda(), torch.from_numpy(mud).cuda())
+    o.set_link_friction(mu, mud)
     st = o.get_state()
     rng = np.random.default_rng(2)
     st[zm.S["JOINT_VEL"]:zm.S["JOINT_VEL"] + 6] = rng.normal(0, 1.0, (6, n)).astype(np.float32)
     st[zm.S["ROOT_LINVEL"]:zm.S["ROOT_LINVEL"] + 2] = rng.normal(0, 0.3, (2, n)).astype(np.float32)
     g.set_state(torch.from_numpy(st).cuda())
     o.set_state(st)
-    np.testing.assert_array_equal(g.get_state().cpu().numpy()[SU["LINK_MU"]:], mu.T)
+    np.testing.assert_array_equal(g.get_state().cpu().numpy()[SU["LINK_MU"]:SU["LINK_MU"] + 12], mu.T)
+    np.testing.assert_array_equal(g.get_state().cpu().numpy()[SU["LINK_MU_D"]:SU["LINK_MU_D"] + 12], mud.T)
     tg = rng.normal(0, 0.5, (n, 6)).astype(np.float32)
     g.physics_substeps(torch.from_numpy(tg).cuda(), 1)
     o.physics_substeps(tg, 1)

@@ -51,10 +51,11 @@ def lib():
     L.zb_read_stamps.restype = C.c_int
     L.zb_state_dim.argtypes = [P]
     L.zb_set_link_friction.argtypes = [P, P, P]
+    L.zb_set_link_friction_sd.argtypes = [P, P, P, P]
     L.zb_read_curriculum.argtypes = [P, C.POINTER(C.c_int32), C.POINTER(C.c_int64)]
     for name in ("zb_create", "zb_num_envs", "zb_reset", "zb_step", "zb_observe", "zb_read_log", "zb_set_log_buffers",
                  "zb_get_state", "zb_set_state", "zb_physics_substeps", "zb_profile_begin", "zb_profile_end",
-                 "zb_state_dim", "zb_set_link_friction", "zb_read_curriculum"):
+                 "zb_state_dim", "zb_set_link_friction", "zb_set_link_friction_sd", "zb_read_curriculum"):
         getattr(L, name).restype = C.c_int
     _lib = L
     return L
@@ -62,7 +63,8 @@ def lib():
 
 EXPORTED = ["zb_create", "zb_destroy", "zb_last_error", "zb_num_envs", "zb_reset", "zb_step", "zb_observe",
             "zb_read_log", "zb_set_log_buffers", "zb_get_state", "zb_set_state", "zb_physics_substeps", "zb_profile_begin",
-            "zb_profile_end", "zb_read_stamps", "zb_state_dim", "zb_set_link_friction", "zb_read_curriculum"]
+            "zb_profile_end", "zb_read_stamps", "zb_state_dim", "zb_set_link_friction", "zb_set_link_friction_sd",
+            "zb_read_curriculum"]
 
 
 def check(rc: int, what: str) -> None:

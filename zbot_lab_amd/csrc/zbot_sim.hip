@@ -504,7 +504,7 @@ constexpr int NCAND = NL * 4 + NSELF;
 //   region V
 //     UB    [NL][EPW]        world union spheres                                  detection only
 //     stash [WGT][2]         M rows of the joint columns (saturated drives)       Cholesky .. re-solve
-//     AUX   [NCM][2][EPW]    {invm0, invm1, invm2, vmin invm0}, {c01 invm1, c02 invm2, mu, 0}
+//     AUX   [NCM][2][EPW]    {invm0, invm1, invm2, vmin invm0}, {c01 invm1, c02 invm2, mu_s, mu_d}
 //     LAM   [NCM][EPW]       contact impulses {ln, l1, l2, 0}                     row write .. sensor
 //     FRC   [NCM][EPW]       contact normal + code (row builder), then force {f, code} (sensor)
 //   BODY  [NB][4][EPW]      body poses {R row 0, p.x}, {R row 1, p.y}, {R row 2, p.z}, {quat}
@@ -512,7 +512,7 @@ constexpr int NCAND = NL * 4 + NSELF;
 //   LNK   [LNK4 - NL*LINK4] pair codes, default pose, joint / body tables (the per-link collision
 //                           table is read from global memory: L1-resident, 3 KB)
 //   PRE   [EPW][PRE4]       prologue results parked across the physics
-//   FRIC  [EPW][NL] f32     per-link friction coefficients (standup)
+//   FRIC  [EPW][2][NL] f32  per-link static / dynamic friction coefficients (standup, manager)
 //   SENS  [EPW][MAXSUB][2]  per-substep contact-sensor record {fz0, fz1, |F0|, |F1|}, {undesired max |F|}
 //   CARRY [EPW][CARRY_W] f32  the env's MDP state rows, prefetched in the prologue (carry_prefetch)
 #ifndef ZB_YG_PAD
@@ -549,9 +549,9 @@ constexpr int LNK_G = NL * LINK4;      // link-table granules read from global m
 constexpr int LNK_OFF = JNT_OFF + ND * JNT_S - LNK_G;  // lds[LNK_OFF + t] = links[t] for t >= LNK_G
 constexpr int PRE_OFF = LNK_OFF + LNK4;  // [EPW] Pre records (prologue -> MDP)
 constexpr int PRE4 = 8;                   // float4 per Pre record (30 floats)
-constexpr int FRIC_OFF = PRE_OFF + EPW * PRE4;  // [EPW][NL] f32 per-link friction (standup)
+constexpr int FRIC_OFF = PRE_OFF + EPW * PRE4;  // [EPW][2][NL] f32 per-link static, dynamic friction
 constexpr int MAXSUB = 8;                 // decimation limit (zb_create checks)
-constexpr int SENS_OFF = FRIC_OFF + (EPW * NL + 3) / 4;
+constexpr int SENS_OFF = FRIC_OFF + (EPW * 2 * NL + 3) / 4;
 constexpr int LOGR_W = ZB_MAX_REWARD_TERMS + 8;  // = ACC (episode-log entries, defined with the step kernels)
 constexpr int CARRY0 = ZB_S_P_DELTA, CARRY_W = 64;  // state rows [CARRY0, CARRY0 + CARRY_W)
 constexpr int CARRY_OFF = SENS_OFF + EPW * MAXSUB * 2;
@@ -593,7 +593,8 @@ struct Q {
   __device__ __forceinline__ int pair_code(int p) const { return reinterpret_cast<const int*>(b + LNK_OFF + NL * LINK4)[p]; }
   __device__ __forceinline__ const float4* dflt() const { return b + LNK_OFF + DFLT_OFF; }
   __device__ __forceinline__ Pre& pre() const { return *reinterpret_cast<Pre*>(b + PRE_OFF + e * PRE4); }
-  __device__ __forceinline__ float& fric(int l) const { return reinterpret_cast<float*>(b + FRIC_OFF)[e * NL + l]; }
+  __device__ __forceinline__ float& fric(int l) const { return reinterpret_cast<float*>(b + FRIC_OFF)[e * 2 * NL + l]; }
+  __device__ __forceinline__ float& fricd(int l) const { return reinterpret_cast<float*>(b + FRIC_OFF)[e * 2 * NL + NL + l]; }
   __device__ __forceinline__ float4& sens(int k, int h) const { return b[SENS_OFF + (e * MAXSUB + k) * 2 + h]; }
   __device__ __forceinline__ float& stg(int k) const;  // epilogue staging row of this env (staged_store)
   __device__ __forceinline__ float* logr(int ee) const { return reinterpret_cast<float*>(b + LOGR_OFF) + ee * LOGR_W; }
@@ -1169,13 +1170,13 @@ __device__ __forceinline__ const float* carry_prefetch(const Q& q, const float* 
 
 // One Gauss-Seidel contact update (normal + Coulomb disk). g = {Y0[d], Y1[d], Y2[d], -} of this
 // lane's coordinate d, a0 = {invm0, invm1, invm2, vmin invm0}, a1 = {c01 invm1, c02 invm2, -, -}
-// (c0r = Y_r . Y_0), lam = {ln, l1, l2}. The three row dots are reduced across the team; the
+// (c0r = Y_r . Y_0), lam = {ln, l1, l2}; mu / mu_d the static / dynamic coefficients. The three row dots are reduced across the team; the
 // tangent velocities see the normal update through the cross terms. Arranged for a short
 // dependency chain: the impulse-independent parts are formed while the normal row resolves, and
 // the disk projection is min(1, lim / max(|l|, 1e-15)) (rsq; finite for |l| = 0). Returns the
 // new impulses; wd (the lane's coordinate) updated.
 __device__ __forceinline__ float4 pgs_update(const float4 g, const float4 a0, const float4 a1, const float4 lam,
-                                             float mu, float& wd) {
+                                             float mu, float mu_d, float& wd) {
   const float p0 = tsum(g.x * wd);
   const float p1 = tsum(g.y * wd);
   const float p2 = tsum(g.z * wd);
@@ -1184,8 +1185,10 @@ __device__ __forceinline__ float4 pgs_update(const float4 g, const float4 a0, co
   const float u1 = fmaf(-p1, a0.y, lam.y), u2 = fmaf(-p2, a0.z, lam.z);
   float l1 = fmaf(-a1.x, dl, u1);
   float l2 = fmaf(-a1.y, dl, u2);
-  const float lim = mu * ln;
-  const float sc = fminf(1.f, lim * __builtin_amdgcn_rsqf(fmaxf(fmaf(l1, l1, l2 * l2), 1e-30f)));
+  // static / dynamic Coulomb disk: inside mu ln the impulse sticks; outside it slides at mu_d ln
+  // (mu_d = mu: the plain projection min(1, mu ln / |l|))
+  const float ri = __builtin_amdgcn_rsqf(fmaxf(fmaf(l1, l1, l2 * l2), 1e-30f));
+  const float sc = mu * ln * ri < 1.f ? mu_d * ln * ri : 1.f;
   l1 *= sc;
   l2 *= sc;
   const float d1 = l1 - lam.y, d2 = l2 - lam.z;
@@ -1531,7 +1534,8 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
     q.aux(c, 0) = make_float4(invm[0], invm[1], invm[2], vmin * invm[0]);
     // friction combine mode "multiply": ground (terrain coefficient) x link, link x link
     const float mu_c = kLinkFriction ? q.fric(code >> 4) * (lb >= 0 ? q.fric(lb) : cfg.friction) : 0.f;
-    q.aux(c, 1) = make_float4(dot12(Y[1], Y[0]) * invm[1], dot12(Y[2], Y[0]) * invm[2], mu_c, 0.f);
+    const float mu_cd = kLinkFriction ? q.fricd(code >> 4) * (lb >= 0 ? q.fricd(lb) : cfg.friction_dynamic) : 0.f;
+    q.aux(c, 1) = make_float4(dot12(Y[1], Y[0]) * invm[1], dot12(Y[2], Y[0]) * invm[2], mu_c, mu_cd);
     q.lam(c) = make_float4(0.f, 0.f, 0.f, 0.f);
   }
   wave_sync();
@@ -1542,7 +1546,7 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
   // ping-pong register sets: the granules and impulse of update k+1 are read while update k
   // computes. With one contact the prefetched impulse is the one being updated (forwarded).
   {
-    const float mu = cfg.friction;
+    const float mu = cfg.friction, mu_d = cfg.friction_dynamic;
     const float4* yl = q.b + YG_OFF + q.ygl();
     float wd = 0.f;
 #pragma unroll
@@ -1564,7 +1568,7 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
         const float4 Gn = q.yg(yl, cn), Xn = q.aux(cn, 0), Zn = q.aux(cn, 1), Ln = q.lam(cn);
         if (c < ncw) {
           if (c < nc) {
-            const float4 nA = pgs_update(G, X, Z, La, kLinkFriction ? Z.z : mu, wd);
+            const float4 nA = pgs_update(G, X, Z, La, kLinkFriction ? Z.z : mu, kLinkFriction ? Z.w : mu_d, wd);
             if (lead) q.lam(c) = nA;
           }
         }
@@ -1579,14 +1583,14 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
       const int cB = cA + 1 == nc ? 0 : cA + 1;
       const float4 GB = q.yg(yl, cB), XB = q.aux(cB, 0), ZB = q.aux(cB, 1);
       float4 LB = q.lam(cB);
-      const float4 nA = pgs_update(GA, XA, ZA, LA, kLinkFriction ? ZA.z : mu, wd);
+      const float4 nA = pgs_update(GA, XA, ZA, LA, kLinkFriction ? ZA.z : mu, kLinkFriction ? ZA.w : mu_d, wd);
       if (lead) q.lam(cA) = nA;
       if (cB == cA) LB = nA;
       if (k + 1 < K) {
         const int cA2 = cB + 1 == nc ? 0 : cB + 1;
         GA = q.yg(yl, cA2); XA = q.aux(cA2, 0); ZA = q.aux(cA2, 1);
         LA = q.lam(cA2);
-        const float4 nB = pgs_update(GB, XB, ZB, LB, kLinkFriction ? ZB.z : mu, wd);
+        const float4 nB = pgs_update(GB, XB, ZB, LB, kLinkFriction ? ZB.z : mu, kLinkFriction ? ZB.w : mu_d, wd);
         if (lead) q.lam(cB) = nB;
         if (cA2 == cB) LA = nB;
         cA = cA2;
@@ -2414,7 +2418,11 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_substeps_kernel(con
   const Q q = make_q(lds, lane, links);
   for (int t = LNK_G + lane; t < LNK4; t += WGT) lds[LNK_OFF + t] = links[t];
   const int mu_row = cfg.task == ZB_TASK_MANAGER_V0 ? ZB_M_LINK_MU : ZB_SU_LINK_MU;
-  if (kLinkFriction && q.s < NL) q.fric(q.s) = st[(size_t)(mu_row + q.s) * N + i];
+  const int mud_row = cfg.task == ZB_TASK_MANAGER_V0 ? ZB_M_LINK_MU_D : ZB_SU_LINK_MU_D;
+  if (kLinkFriction && q.s < NL) {
+    q.fric(q.s) = st[(size_t)(mu_row + q.s) * N + i];
+    q.fricd(q.s) = st[(size_t)(mud_row + q.s) * N + i];
+  }
   Phys p;
   load_phys(st, N, i, p);
   float tg[ND], tau[ND], F[1][3];
@@ -2536,7 +2544,10 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_su_step_kernel(
   for (int a = 0; a < 4; ++a) p.quat[a] = ST(ZB_S_ROOT_QUAT + a);
 #pragma unroll
   for (int j = 0; j < ND; ++j) { p.jq[j] = ST(ZB_S_JOINT_POS + j); p.jqd[j] = ST(ZB_S_JOINT_VEL + j); }
-  if (q.s < NL) q.fric(q.s) = ST(ZB_SU_LINK_MU + q.s);  // lane l: link l (visible after the first barrier)
+  if (q.s < NL) {  // lane l: link l (visible after the first barrier)
+    q.fric(q.s) = ST(ZB_SU_LINK_MU + q.s);
+    q.fricd(q.s) = ST(ZB_SU_LINK_MU_D + q.s);
+  }
 
   // _pre_physics_step (standup.py:538-551, mode 1)
   const bool writer = q.s == 0;
@@ -3323,12 +3334,15 @@ __global__ __launch_bounds__(WGT, ZB_M_WAVES_PER_SIMD) void zb_m_step_kernel(
 #pragma unroll
   for (int j = 0; j < ND; ++j) { p.jq[j] = ST(ZB_S_JOINT_POS + j); p.jqd[j] = ST(ZB_S_JOINT_VEL + j); }
 #if ZB_CARRY
-  const float* cst = carry_prefetch<ZB_M_STATE_DIM>(q, st, N, i);
+  const float* cst = carry_prefetch<ZB_M_LINK_MU>(q, st, N, i);  // the friction rows load into FRIC
 #define CST(f) cst[f]
 #else
 #define CST(f) ST(f)
 #endif
-  if (q.s < NL) q.fric(q.s) = ST(ZB_M_LINK_MU + q.s);
+  if (q.s < NL) {
+    q.fric(q.s) = ST(ZB_M_LINK_MU + q.s);
+    q.fricd(q.s) = ST(ZB_M_LINK_MU_D + q.s);
+  }
 
   // ActionManager.process_action: RelativeJointPositionAction (scale 0.04 pi, zero offset, clip
   // +-0.04 pi) in the Isaac Lab joint order, mapped onto the chain's joints
@@ -3726,7 +3740,7 @@ __global__ void zb_m_reset_kernel(const zb_model* __restrict__ mg, const float4*
   for (int k = 0; k < ZB_M_NUM_REWARD_TERMS; ++k) ST(ZB_M_EP_SUMS + k) = 0.f;
   if (init) {
 #pragma unroll
-    for (int l = 0; l < NL; ++l) ST(ZB_M_LINK_MU + l) = cfg.friction;
+    for (int l = 0; l < NL; ++l) { ST(ZB_M_LINK_MU + l) = cfg.friction; ST(ZB_M_LINK_MU_D + l) = cfg.friction_dynamic; }
   }
 #undef ST
 }
@@ -4045,6 +4059,10 @@ int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_dev
     zb_su_friction_kernel<<<(num_envs * NL + 255) / 256, 256>>>(num_envs, h->d_state, nullptr, c->friction, ZB_SU_LINK_MU);
     rc = launch_check("zb_su_friction_kernel");
     if (rc) return rc;
+    zb_su_friction_kernel<<<(num_envs * NL + 255) / 256, 256>>>(num_envs, h->d_state, nullptr, c->friction_dynamic,
+                                                                ZB_SU_LINK_MU_D);
+    rc = launch_check("zb_su_friction_kernel");
+    if (rc) return rc;
     // the construction-time reset draws its poses at RNG position 0; later calls start at 1
     zb_su_reset_kernel<<<(num_envs + 255) / 256, 256>>>(h->d_model, h->cfg, num_envs, h->d_state, nullptr, num_envs,
                                                        h->d_acc, h->d_cnt, h->seed);
@@ -4230,13 +4248,22 @@ int zb_observe(zb_handle h, float* obs, void* stream) {
 
 int zb_state_dim(zb_handle h) { return h ? h->state_dim : -1; }
 
-int zb_set_link_friction(zb_handle h, const float* mu, void* stream) {
-  if (!h || !mu) return set_err(-1, "zb_set_link_friction", hipSuccess);
+int zb_set_link_friction_sd(zb_handle h, const float* mu_static, const float* mu_dynamic, void* stream) {
+  if (!h || !mu_static || !mu_dynamic) return set_err(-1, "zb_set_link_friction_sd", hipSuccess);
   if (h->task != ZB_TASK_STANDUP_V0 && h->task != ZB_TASK_MANAGER_V0)
     return set_err(-1, "zb_set_link_friction: per-link friction is a standup / manager task state", hipSuccess);
+  const bool mgr = h->task == ZB_TASK_MANAGER_V0;
   zb_su_friction_kernel<<<(h->n * NL + 255) / 256, 256, 0, (hipStream_t)stream>>>(
-      h->n, h->d_state, mu, 0.f, h->task == ZB_TASK_MANAGER_V0 ? ZB_M_LINK_MU : ZB_SU_LINK_MU);
+      h->n, h->d_state, mu_static, 0.f, mgr ? ZB_M_LINK_MU : ZB_SU_LINK_MU);
+  int rc = launch_check("zb_su_friction_kernel");
+  if (rc) return rc;
+  zb_su_friction_kernel<<<(h->n * NL + 255) / 256, 256, 0, (hipStream_t)stream>>>(
+      h->n, h->d_state, mu_dynamic, 0.f, mgr ? ZB_M_LINK_MU_D : ZB_SU_LINK_MU_D);
   return launch_check("zb_su_friction_kernel");
+}
+
+int zb_set_link_friction(zb_handle h, const float* mu, void* stream) {
+  return zb_set_link_friction_sd(h, mu, mu, stream);
 }
 
 int zb_read_curriculum(zb_handle h, int32_t* stage, int64_t* common_step_counter) {

@@ -267,6 +267,7 @@ class Zbot6BFlatEnvCfg:
             termination_height=float(self.terminations.base_height.params["minimum_height"]),
             feet_close_min=float(self.terminations.feet_close.params["minimum_distance"]),
             gravity=-self.sim.gravity[2], friction=self.sim.static_friction,
+            friction_dynamic=self.sim.dynamic_friction,
             contact_margin=self.solver.contact_margin, baumgarte=self.solver.baumgarte,
             solver_iterations=self.solver.iterations, enable_self_collision=self.solver.self_collision,
             reset_pose_range=tuple(tuple(pr.get(k, (0.0, 0.0))) for k in ("x", "y", "roll", "yaw")),
@@ -330,7 +331,7 @@ class ZbotManagerBasedRLEnv(ZbotDirectEnvV2):
     def _startup(self) -> None:
         """Startup events: init_my_data (the feet buffers live in the state rows) and
         randomize_rigid_body_material over every body shape (64 buckets of static / dynamic
-        friction ~ U[0.3, 1.0]; the static coefficient is the solver's Coulomb bound)."""
+        friction ~ U[0.3, 1.0]; static and dynamic coefficients go to the solver)."""
         ev = self.cfg.events.physics_material
         if ev is None:
             return
@@ -341,7 +342,7 @@ class ZbotManagerBasedRLEnv(ZbotDirectEnvV2):
         self.material_buckets = torch.rand(nb, 3, generator=g) * (ranges[:, 1] - ranges[:, 0]) + ranges[:, 0]
         bucket_ids = torch.randint(0, nb, (self.num_envs, zm.NUM_LINKS), generator=g)
         self.link_materials = self.material_buckets[bucket_ids]
-        self.sim.set_link_friction(self.link_materials[..., 0])
+        self.sim.set_link_friction(self.link_materials[..., 0], self.link_materials[..., 1])
 
     def _update_log(self) -> None:
         """extras["log"] in ManagerBasedRLEnv._reset_idx order: Episode_Reward/<term> (reward

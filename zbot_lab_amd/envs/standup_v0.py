@@ -8,7 +8,7 @@ runs in the fused stand-up kernel of ``libzbot.so``:
 
 * startup event ``physics_material`` (randomize_rigid_body_material, 124-136): 64 material buckets
   (static, dynamic friction ~ U[0.6, 1.0], restitution 0) drawn once, one bucket per link shape per
-  env; the per-link static friction goes to the kernel (``zb_set_link_friction``), which combines
+  env; the per-link static and dynamic friction go to the kernel (``zb_set_link_friction_sd``), which combines
   it with the terrain's 1.0 (ground contacts) or the other link's (self contacts) by multiplying;
 * reset event ``reset_base`` (reset_root_state_uniform, 33-97, 159-175): x, y ~ U(-0.5, 0.5),
   roll ~ U(-pi/4, pi/4), yaw ~ U(-3.14, 3.14) applied in the kernel at every reset;
@@ -69,6 +69,7 @@ class Zbot6SUpEnvCfg:
             sim_dt=self.sim.dt, decimation=self.decimation, episode_length_s=self.episode_length_s,
             termination_height=self.termination_height, reward_weights=dict(self.reward_cfg["reward_scales"]),
             gravity=-self.sim.gravity[2], friction=self.sim.static_friction,
+            friction_dynamic=self.sim.dynamic_friction,
             contact_margin=self.solver.contact_margin, baumgarte=self.solver.baumgarte,
             solver_iterations=self.solver.iterations, enable_self_collision=self.solver.self_collision,
             reset_pose_range=tuple(tuple(pr.get(k, (0.0, 0.0))) for k in ("x", "y", "roll", "yaw")),
@@ -87,7 +88,7 @@ class Zbot6SUpEnv(ZbotDirectEnvV2):
 
     def _startup(self) -> None:
         """randomize_rigid_body_material (mode "startup"): buckets drawn once on the CPU, then a
-        random bucket per (env, link shape); the static coefficient is the solver's Coulomb bound."""
+        random bucket per (env, link shape); static and dynamic coefficients go to the solver."""
         p = self.cfg.events.physics_material.params
         g = torch.Generator().manual_seed(self.cfg.seed if self.cfg.seed is not None else 0)
         ranges = torch.tensor([p["static_friction_range"], p["dynamic_friction_range"], p["restitution_range"]])
@@ -95,7 +96,7 @@ class Zbot6SUpEnv(ZbotDirectEnvV2):
         self.material_buckets = torch.rand(nb, 3, generator=g) * (ranges[:, 1] - ranges[:, 0]) + ranges[:, 0]
         bucket_ids = torch.randint(0, nb, (self.num_envs, zm.NUM_LINKS), generator=g)
         self.link_materials = self.material_buckets[bucket_ids]  # [N, 12, (static, dynamic, restitution)]
-        self.sim.set_link_friction(self.link_materials[..., 0])
+        self.sim.set_link_friction(self.link_materials[..., 0], self.link_materials[..., 1])
 
     @property
     def curriculum_stage(self) -> int:

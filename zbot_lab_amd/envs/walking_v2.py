@@ -93,7 +93,7 @@ class ZbotDirectEnvCfgV2:
             sim_dt=self.sim.dt, decimation=self.decimation, episode_length_s=self.episode_length_s,
             termination_height=self.termination_height,
             reward_weights=dict(self.reward_cfg["reward_scales"]), gravity=-self.sim.gravity[2],
-            friction=self.sim.static_friction, contact_margin=self.solver.contact_margin,
+            friction=self.sim.static_friction, friction_dynamic=self.sim.dynamic_friction, contact_margin=self.solver.contact_margin,
             baumgarte=self.solver.baumgarte, solver_iterations=self.solver.iterations,
             enable_self_collision=self.solver.self_collision,
         )

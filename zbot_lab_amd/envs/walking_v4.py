@@ -72,7 +72,7 @@ class Zbot6SEnvV4Cfg:
         kw = dict(
             sim_dt=self.sim.dt, decimation=self.decimation, episode_length_s=self.episode_length_s,
             termination_height=self.termination_height, reward_weights=dict(self.reward_cfg["reward_scales"]),
-            gravity=-self.sim.gravity[2], friction=self.sim.static_friction,
+            gravity=-self.sim.gravity[2], friction=self.sim.static_friction, friction_dynamic=self.sim.dynamic_friction,
             contact_margin=self.solver.contact_margin, baumgarte=self.solver.baumgarte,
             solver_iterations=self.solver.iterations, enable_self_collision=self.solver.self_collision,
             reset_pose_range=tuple(tuple(pr.get(k, (0.0, 0.0))) for k in ("x", "y", "roll", "yaw")),

@@ -41,12 +41,12 @@ REWARD_WEIGHTS = {  # v2.py:190-206 ("train reward 2000 step4")
 # zbot-6b-standup-v0 (include/zbot.h enum zb_standup_state_field / zb_standup_reward_term)
 TASK_WALKING_V2, TASK_STANDUP_V0, TASK_WALKING_V4, TASK_MANAGER_V0 = 0, 1, 2, 3
 MAX_REWARD_TERMS, MAX_STAGES, LOG_LEN, LOG_COUNTS = 16, 4, 20, 4
-SU_OBS_DIM, SU_NUM_TERMS, SU_STATE_DIM = 22, 4, 55
+SU_OBS_DIM, SU_NUM_TERMS, SU_STATE_DIM = 22, 4, 67
 SU_REWARD_TERMS = ["upward_2", "shape_symmetry", "feet_downward", "feet_downward_4"]  # standup.py:418-427
 SU_REWARD_WEIGHTS = {"upward_2": 10.0, "shape_symmetry": -1.0, "feet_downward": -1.0, "feet_downward_4": 0.0}
 SU_CURRICULUM_WEIGHTS = {"upward_2": 10.0, "shape_symmetry": -2.0, "feet_downward": -1.0,
                          "feet_downward_4": 2.0}  # my_curriculum stage 1 (standup.py:103-107)
-SU = dict(P_DELTA=25, ACTIONS=31, CENTER_Z_LAST=37, EP_LEN=38, EP_SUMS=39, LINK_MU=43)
+SU = dict(P_DELTA=25, ACTIONS=31, CENTER_Z_LAST=37, EP_LEN=38, EP_SUMS=39, LINK_MU=43, LINK_MU_D=55)
 # ZBOT_6S_CFG_2 init_state (zbot_cfg.py:744-753): lying on its side, joints straight
 SU_ROOT_POS = (0.0, 0.0, 0.05)
 SU_ROOT_ROT = (0.707, 0.0, -0.707, 0.0)
@@ -76,7 +76,7 @@ V4 = dict(P_DELTA=25, ACTIONS=31, COMMANDS=37, TARGET_YAW=39, INTERVAL_LEFT=40, 
 
 # zbot-6b-walking-m-v0, the manager-based flat env (include/zbot.h enum zb_manager_state_field /
 # zb_manager_reward_term); RewardsCfg order after flat_env_cfg.py's overrides (mgr.py:262-357)
-M_OBS_DIM, M_NUM_TERMS, M_STATE_DIM = 25, 11, 88
+M_OBS_DIM, M_NUM_TERMS, M_STATE_DIM = 25, 11, 100
 M_REWARD_TERMS = [
     "track_lin_vel_xy_exp", "track_ang_vel_z_exp", "termination_penalty", "dof_torques_l2", "dof_acc_l2",
     "action_rate_l2", "foot_step_length", "foot_downward", "foot_forward", "feet_slide", "air_time_variance",
@@ -89,7 +89,7 @@ M_REWARD_WEIGHTS = {
 M_TERMINATION_TERMS = ["time_out", "base_height", "feet_close"]  # mgr.py:379-398 minus base_contact (flat)
 M = dict(ACTIONS=25, COMMANDS=31, CMD_TIME_LEFT=34, CMD_STANDING=35, FEET_DOWN_POS=36, FEET_STEP_LEN=42,
          FEET_F_LAST=44, FEET_FZ_HIST=46, FEET_FN_HIST=52, FEET_AIR_CUR=58, FEET_AIR_LAST=60, METRICS=62,
-         EP_LEN=64, EP_SUMS=65, LINK_MU=76)
+         EP_LEN=64, EP_SUMS=65, LINK_MU=76, LINK_MU_D=88)
 
 # state field offsets (include/zbot.h enum zb_state_field)
 S = dict(ROOT_POS=0, ROOT_QUAT=3, ROOT_LINVEL=7, ROOT_ANGVEL=10, JOINT_POS=13, JOINT_VEL=19,
@@ -150,6 +150,7 @@ class ZbTaskCfg(C.Structure):
         ("obs_noise", C.c_float * 3), ("cmd_resample_s", C.c_float), ("cmd_rel_standing", C.c_float),
         ("feet_close_min", C.c_float),
         ("reset_feet_refresh", C.c_int32),
+        ("friction_dynamic", C.c_float),
     ]
 
 
@@ -501,6 +502,7 @@ class TaskCfg:
     joint_speed_limit: float = 1.0
     gravity: float = 9.81
     friction: float = 1.0
+    friction_dynamic: float = 1.0
     contact_force_threshold: float = 1.0
     contact_margin: float = 0.004
     baumgarte: float = 0.2
@@ -669,6 +671,7 @@ class TaskCfg:
         c.cmd_rel_standing = self.cmd_rel_standing
         c.feet_close_min = self.feet_close_min
         c.reset_feet_refresh = int(self.reset_feet_refresh)
+        c.friction_dynamic = self.friction_dynamic
         c.reset_pose_body_frame = int(self.reset_pose_body_frame)
         c.task = self.task
         for k in range(4):

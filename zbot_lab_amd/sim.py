@@ -109,12 +109,16 @@ class ZbotSim:
         """The whole float[ZB_LOG_LEN] log buffer (term means, then the curriculum entries)."""
         return self._log_means
 
-    def set_link_friction(self, mu: torch.Tensor) -> None:
-        """Standup / manager: per-link friction coefficients [N, 12] (randomize_rigid_body_material)."""
+    def set_link_friction(self, mu: torch.Tensor, mu_dynamic: torch.Tensor | None = None) -> None:
+        """Standup / manager: per-link static (and dynamic; default = static) friction [N, 12]
+        (randomize_rigid_body_material)."""
         m = mu.to(device=self.device, dtype=torch.float32).contiguous()
-        if m.shape != (self.num_envs, zm.NUM_LINKS):
-            raise ValueError(f"friction must be [{self.num_envs}, {zm.NUM_LINKS}]")
-        nat.check(self.lib.zb_set_link_friction(self._h, nat.ptr(m), _stream(self.device)), "zb_set_link_friction")
+        md = m if mu_dynamic is None else mu_dynamic.to(device=self.device, dtype=torch.float32).contiguous()
+        for t in (m, md):
+            if t.shape != (self.num_envs, zm.NUM_LINKS):
+                raise ValueError(f"friction must be [{self.num_envs}, {zm.NUM_LINKS}]")
+        nat.check(self.lib.zb_set_link_friction_sd(self._h, nat.ptr(m), nat.ptr(md), _stream(self.device)),
+                  "zb_set_link_friction_sd")
         torch.cuda.current_stream(self.device).synchronize()  # `m` may be a temporary
 
     def read_curriculum(self):
