@@ -629,6 +629,7 @@ static void substep(const mdl_t* m, const zb_task_cfg* cfg, phys_t* s, const rea
   int nc = CL.n;
   real Y[NC_MAX][3][NV];
   real invm[NC_MAX][3], vmin[NC_MAX], lam[NC_MAX][3], c01[NC_MAX], c02[NC_MAX], muc[NC_MAX], mud[NC_MAX];
+  int broken[NC_MAX];
   real dirs[NC_MAX][3][3];
   for (int c = 0; c < nc; ++c) {
     const contact_t* ct = &CL.c[c];
@@ -652,6 +653,7 @@ static void substep(const mdl_t* m, const zb_task_cfg* cfg, phys_t* s, const rea
       lam[c][r] = 0;
     }
     c01[c] = 0; c02[c] = 0;
+    broken[c] = 0;
     for (int a = 0; a < NV; ++a) { c01[c] += Y[c][1][a] * Y[c][0][a]; c02[c] += Y[c][2][a] * Y[c][0][a]; }
     real sep = ct->sep;
     if (sep >= 0) vmin[c] = -sep / dt;
@@ -674,13 +676,17 @@ static void substep(const mdl_t* m, const zb_task_cfg* cfg, phys_t* s, const rea
       real vt1 = v1 + c01[c] * dl, vt2 = v2 + c02[c] * dl;
       real l1 = lam[c][1] - vt1 * invm[c][1];
       real l2 = lam[c][2] - vt2 * invm[c][2];
-      /* static / dynamic Coulomb disk: beyond mu_s ln the contact slides with mu_d ln
-       * (PhysX's static -> dynamic switch; mu_d = mu_s is the plain disk projection) */
-      real lim = mu * ln;
+      /* static / dynamic Coulomb disk (PhysX patch friction): sticks while |l| <= mu_s ln; once
+       * the static cone is exceeded the contact is broken for the rest of this substep's sweeps
+       * and slides with |l| = mu_d ln (mu_d = mu_s: the plain disk projection) */
       real mag2 = l1 * l1 + l2 * l2;
-      if (mag2 > lim * lim) {
-        real sc = mud[c] * ln / sqrtr(mag2);
-        l1 *= sc; l2 *= sc;
+      if (!broken[c] && mag2 > (mu * ln) * (mu * ln)) broken[c] = 1;
+      if (broken[c]) {
+        real lim = mud[c] * ln;
+        if (mag2 > lim * lim) {
+          real sc = lim / sqrtr(mag2);
+          l1 *= sc; l2 *= sc;
+        }
       }
       real d1 = l1 - lam[c][1], d2 = l2 - lam[c][2];
       lam[c][0] = ln; lam[c][1] = l1; lam[c][2] = l2;

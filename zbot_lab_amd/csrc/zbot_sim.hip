@@ -1170,7 +1170,7 @@ __device__ __forceinline__ const float* carry_prefetch(const Q& q, const float* 
 
 // One Gauss-Seidel contact update (normal + Coulomb disk). g = {Y0[d], Y1[d], Y2[d], -} of this
 // lane's coordinate d, a0 = {invm0, invm1, invm2, vmin invm0}, a1 = {c01 invm1, c02 invm2, -, -}
-// (c0r = Y_r . Y_0), lam = {ln, l1, l2}; mu / mu_d the static / dynamic coefficients. The three row dots are reduced across the team; the
+// (c0r = Y_r . Y_0), lam = {ln, l1, l2, broken}; mu / mu_d the static / dynamic coefficients. The three row dots are reduced across the team; the
 // tangent velocities see the normal update through the cross terms. Arranged for a short
 // dependency chain: the impulse-independent parts are formed while the normal row resolves, and
 // the disk projection is min(1, lim / max(|l|, 1e-15)) (rsq; finite for |l| = 0). Returns the
@@ -1185,17 +1185,20 @@ __device__ __forceinline__ float4 pgs_update(const float4 g, const float4 a0, co
   const float u1 = fmaf(-p1, a0.y, lam.y), u2 = fmaf(-p2, a0.z, lam.z);
   float l1 = fmaf(-a1.x, dl, u1);
   float l2 = fmaf(-a1.y, dl, u2);
-  // static / dynamic Coulomb disk: inside mu ln the impulse sticks; outside it slides at mu_d ln
-  // (mu_d = mu: the plain projection min(1, mu ln / |l|))
+  // static / dynamic Coulomb disk (PhysX's patch friction): the contact sticks while |l| <= mu ln;
+  // once the static cone is exceeded it is "broken" (lam.w = 1) for the rest of the substep's
+  // sweeps and slides with |l| = mu_d ln (mu_d = mu: the plain projection min(1, mu ln / |l|))
   const float ri = __builtin_amdgcn_rsqf(fmaxf(fmaf(l1, l1, l2 * l2), 1e-30f));
-  const float sc = mu * ln * ri < 1.f ? mu_d * ln * ri : 1.f;
+  const bool brk = lam.w != 0.f || (mu * ln * ri < 1.f);
+  const float lim = brk ? mu_d * ln * ri : 1.f;
+  const float sc = fminf(lim, 1.f);
   l1 *= sc;
   l2 *= sc;
   const float d1 = l1 - lam.y, d2 = l2 - lam.z;
   wd = fmaf(g.x, dl, wd);
   wd = fmaf(g.y, d1, wd);
   wd = fmaf(g.z, d2, wd);
-  return make_float4(ln, l1, l2, 0.f);
+  return make_float4(ln, l1, l2, brk ? 1.f : 0.f);
 }
 
 // mass-matrix column of joint K (computed in lane K) into every lane's packed lower triangle
