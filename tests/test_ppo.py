@@ -212,7 +212,66 @@ def test_gpu_training_runs_with_graphs(gpu, tmp_path):
     env = RslRlVecEnvWrapper(zbot_lab_amd.make("zbot-6b-walking-v2", cfg=env_cfg))
     runner = OnPolicyRunner(env, agent.to_dict(), log_dir=str(tmp_path), device="cuda:0")
     log = runner.learn(40, init_at_random_ep_len=True)
-    assert runner._graph is not None
+    assert runner._graph is not None and runner._update_graph is not None
     assert all(np.isfinite(r["loss/value_function"]) for r in log)
     assert log[-1]["mean_episode_length"] > log[3]["mean_episode_length"]
+    env.close()
+
+
+@pytest.mark.gpu
+def test_gpu_update_graph_matches_eager(gpu):
+    """The HIP-graph PPO update (captured after the first, eager update) computes the same update
+    as the eager code: from one snapshot (rollout storage, parameters, Adam state, learning rate,
+    batch permutation) the graph replay and an eager ``update_steps`` must agree within fp32
+    tolerance, over several iterations of real rollouts."""
+    import torch
+
+    import zbot_lab_amd
+    from zbot_lab_amd.rl import RslRlVecEnvWrapper
+
+    env_cfg = zbot_lab_amd.tasks.load_cfg("zbot-6b-walking-v2")
+    env_cfg.scene.num_envs = 512
+    env = RslRlVecEnvWrapper(zbot_lab_amd.make("zbot-6b-walking-v2", cfg=env_cfg))
+    torch.manual_seed(0)
+    r = OnPolicyRunner(env, PPORunnerCfgV2().to_dict(), log_dir=None, device="cuda:0", use_graph=False,
+                       graph_update=True)
+    r.learn(1)  # eager update, then the capture
+    assert r._update_graph is not None
+    alg = r.alg
+    params = list(alg.policy.parameters())
+
+    def snapshot():
+        st = [{k: v.clone() for k, v in alg.optimizer.state[p].items()} for p in params]
+        return [p.detach().clone() for p in params], st, alg.lr_t.clone()
+
+    def restore(snap):  # in place: the graph holds these tensors' addresses
+        ps, st, lr = snap
+        with torch.no_grad():
+            for p, v, s_ in zip(params, ps, st):
+                p.copy_(v)
+                for k, t in s_.items():
+                    alg.optimizer.state[p][k].copy_(t)
+            alg.lr_t.copy_(lr)
+
+    obs = env.get_observations()["policy"] if isinstance(env.get_observations(), dict) else env.get_observations()
+    for it in range(4):
+        with torch.no_grad():
+            obs = r._rollout(obs)
+            alg.compute_returns(obs)
+        alg.draw_minibatch_indices()
+        snap = snapshot()
+        r._update_graph.replay()
+        torch.cuda.synchronize()
+        p_graph = torch.cat([p.detach().flatten() for p in params]).clone()
+        lr_graph, sums_graph = float(alg.lr_t), alg.update_sums.clone()
+        restore(snap)
+        alg.update_steps()
+        torch.cuda.synchronize()
+        p_eager = torch.cat([p.detach().flatten() for p in params])
+        assert torch.isfinite(p_graph).all()
+        moved = (p_eager - torch.cat([v.flatten() for v in snap[0]])).abs().max()
+        assert moved > 0  # the update did something
+        assert (p_graph - p_eager).abs().max() <= 1e-6 + 1e-3 * moved, (it, float((p_graph - p_eager).abs().max()))
+        assert abs(lr_graph - float(alg.lr_t)) <= 1e-7
+        torch.testing.assert_close(sums_graph, alg.update_sums, rtol=1e-4, atol=1e-6)
     env.close()

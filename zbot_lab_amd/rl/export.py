@@ -61,12 +61,26 @@ def dump_yaml(filename: str, data) -> None:
         yaml.safe_dump(_plain(data), f, default_flow_style=False, sort_keys=False)
 
 
+def _plain_linears(m: nn.Module) -> nn.Module:
+    """Copy of ``m`` with every ``nn.Linear`` subclass (the PPO's split-K training layer) replaced by
+    a plain ``nn.Linear`` holding the same weights, so TorchScript sees the standard module."""
+    m = copy.deepcopy(m)
+    for name, child in list(m.named_children()):
+        if isinstance(child, nn.Linear) and type(child) is not nn.Linear:
+            lin = nn.Linear(child.in_features, child.out_features, bias=child.bias is not None)
+            lin.load_state_dict(child.state_dict())
+            setattr(m, name, lin)
+        else:
+            setattr(m, name, _plain_linears(child))
+    return m
+
+
 class _TorchPolicyExporter(nn.Module):
     """actor(normalizer(obs)) as a self-contained TorchScript module (rsl_rl's deterministic policy)."""
 
     def __init__(self, policy, normalizer=None):
         super().__init__()
-        self.actor = copy.deepcopy(policy.actor).cpu()
+        self.actor = _plain_linears(policy.actor).cpu()
         self.normalizer = copy.deepcopy(normalizer).cpu() if normalizer is not None else nn.Identity()
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:

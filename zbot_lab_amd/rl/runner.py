@@ -12,11 +12,14 @@ minibatch (``PPO.reduce_parameters``).
 Speed: the rollout keeps obs/actions on the GPU, the env step is one fused kernel, and episode
 statistics are accumulated on the device (one host sync per iteration for the log line). On a GPU
 the whole 24-step rollout (policy sampling, the env kernels through the C ABI, storage writes,
-statistics) is captured once as a HIP graph and replayed every iteration; the first iteration runs
-eagerly and serves as the capture warm-up.
+statistics) is captured once as a HIP graph and replayed every iteration, and so is the PPO update
+(20 minibatches of forward, backward, gradient all-reduce, clipping and fused Adam; the batch
+permutation is drawn eagerly into a fixed buffer before each replay); the first iteration runs
+both eagerly and serves as the capture warm-up.
 """
 from __future__ import annotations
 
+import contextlib
 import os
 import statistics
 import time
@@ -28,13 +31,30 @@ import torch.distributed as dist
 from .ppo import PPO, ActorCritic
 
 
+@contextlib.contextmanager
+def _blas_workspace_fence(device):
+    """Drop the BLAS library's cached per-stream workspaces before and after a graph capture. The
+    GEMMs of a captured graph keep the workspace address they ran with; a workspace cached from
+    eager work (or from another capture) is later reused or freed by code outside the graph, and
+    the replay then computes with -- and writes into -- memory that belongs to someone else (seen
+    here as a captured PPO update that matched the eager one only until the next capture / eager
+    GEMM). Cleared around the capture, the graph allocates its own workspace in its private pool."""
+    torch.cuda.synchronize(device)
+    torch._C._cuda_clearCublasWorkspaces()
+    try:
+        yield
+    finally:
+        torch.cuda.synchronize(device)
+        torch._C._cuda_clearCublasWorkspaces()
+
+
 def _policy_obs(obs):
     return obs["policy"] if isinstance(obs, dict) or hasattr(obs, "keys") else obs
 
 
 class OnPolicyRunner:
     def __init__(self, env, train_cfg: dict, log_dir: str | None = None, device: str = "cpu",
-                 use_graph: bool | None = None):
+                 use_graph: bool | None = None, graph_update: bool | None = None):
         self.cfg = train_cfg
         self.alg_cfg = dict(train_cfg["algorithm"])
         self.policy_cfg = dict(train_cfg["policy"])
@@ -64,13 +84,16 @@ class OnPolicyRunner:
         self.cur_len = torch.zeros(self.env.num_envs, device=self.device)
         self.ep_stats = torch.zeros(3, device=self.device)  # reward sum, length sum, count
         self._log_keys, self._log_acc = None, None
-        self.use_graph = (torch.device(device).type == "cuda") if use_graph is None else use_graph
+        from .. import GRAPHS_SAFE
+        self.use_graph = (torch.device(device).type == "cuda" and GRAPHS_SAFE) if use_graph is None else use_graph
         self._graph = None
         self._g_obs = None
         self._update_graph = None
-        # capturing the update (autograd + fused Adam) segfaults in torch 2.10 / ROCm 7 here
-        # (AccumulateGrad stream mismatch); kept opt-in until that is resolved
-        self.graph_update = False
+        # the 20 minibatch updates are captured as a second graph after the first (eager) update;
+        # PPO.update_steps releases its autograd graph so the capture sees fresh AccumulateGrad
+        # nodes on the capture stream (a live one from the eager update pinned the default stream
+        # and broke the capture)
+        self.graph_update = self.use_graph if graph_update is None else graph_update
 
     def _configure_multi_gpu(self) -> None:
         world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -113,11 +136,13 @@ class OnPolicyRunner:
                 collect_time = time.perf_counter() - t0
                 t1 = time.perf_counter()
                 self.alg.compute_returns(obs)
+            self.alg.draw_minibatch_indices()
             if self._update_graph is not None:
                 self._update_graph.replay()
+                self.alg.storage.clear()  # host-side step counter (the replay runs no Python)
             else:
                 self.alg.update_steps()
-                if self.graph_update and self._graph is not None:
+                if self.graph_update:
                     self._capture_update()
             losses = self.alg.update_stats()
             learn_time = time.perf_counter() - t1
@@ -187,9 +212,8 @@ class OnPolicyRunner:
         self._g_obs = obs.clone()
         storage_step = self.alg.storage.step
         self.alg.storage.step = 0
-        torch.cuda.synchronize(self.device)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with _blas_workspace_fence(self.device), torch.cuda.graph(g):
             last = self._rollout(self._g_obs)
             self._g_obs.copy_(last)
         self.alg.storage.step = storage_step
@@ -198,9 +222,8 @@ class OnPolicyRunner:
     def _capture_update(self) -> None:
         """Record the 20 minibatch updates (forward, backward, gradient all-reduce, clip, fused Adam
         with a device learning rate) as a graph; the eager first update was the warm-up."""
-        torch.cuda.synchronize(self.device)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with _blas_workspace_fence(self.device), torch.cuda.graph(g):
             self.alg.update_steps()
         self._update_graph = g
 
