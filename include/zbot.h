@@ -221,6 +221,9 @@ typedef struct zb_model {
   float default_joint_pos[ZB_NUM_DOF];
   /* ImplicitActuatorCfg (zbot_cfg.py:658-668) + rigid props (zbot_cfg.py:626-634) */
   float kp, kd, effort_limit, velocity_limit, max_depenetration_velocity;
+  /* RigidBodyPropertiesCfg.max_angular_velocity (zbot_cfg.py:632: 1000 deg/s, Isaac Lab's unit),
+   * in rad/s: PhysX clamps the articulation root link's angular velocity to it */
+  float max_angular_velocity;
   /* indices used by the MDP */
   int32_t base_link, foot_links[2], undesired_links[10];
   /* Isaac Lab's view when its articulation root is not chain link 0 (zbot_6s_v09.usd: the base):

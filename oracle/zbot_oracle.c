@@ -101,7 +101,7 @@ typedef struct {
   int circle_dup[NL];                 /* bit ci: duplicate of a lower link's mated face (skipped) */
   int npairs, pairs[ZB_MAX_SELF_PAIRS][2];
   real root_pos0[3], root_quat0[4], jq0[ND];
-  real kp, kd, effort, vlim, max_depen;
+  real kp, kd, effort, vlim, max_depen, wmax;
   int base_link, foot_links[2], undesired[10];
   real api_t[3], api_q[4];            /* Isaac Lab root in the chain root's frame (v09: the base) */
   int api_index[ND];                  /* chain joint j -> Isaac Lab joint order */
@@ -135,6 +135,7 @@ static void load_mdl(const zb_model* m, mdl_t* o) {
   for (int a = 0; a < 4; ++a) o->root_quat0[a] = m->default_root_quat[a];
   o->kp = m->kp; o->kd = m->kd; o->effort = m->effort_limit; o->vlim = m->velocity_limit;
   o->max_depen = m->max_depenetration_velocity;
+  o->wmax = m->max_angular_velocity;
   o->base_link = m->base_link;
   o->foot_links[0] = m->foot_links[0]; o->foot_links[1] = m->foot_links[1];
   for (int k = 0; k < 10; ++k) o->undesired[k] = m->undesired_links[k];
@@ -709,6 +710,14 @@ static void substep(const mdl_t* m, const zb_task_cfg* cfg, phys_t* s, const rea
 
   /* joint speed limit (PhysX max joint velocity = actuator velocity_limit) */
   for (int j = 0; j < ND; ++j) un[6 + j] = clampr(un[6 + j], -m->vlim, m->vlim);
+  /* root link angular speed limit (RigidBodyPropertiesCfg.max_angular_velocity, zbot_cfg.py:632) */
+  {
+    real w2 = un[0] * un[0] + un[1] * un[1] + un[2] * un[2];
+    if (w2 > m->wmax * m->wmax) {
+      real sc = m->wmax / sqrtr(w2);
+      un[0] *= sc; un[1] *= sc; un[2] *= sc;
+    }
+  }
 
   /* semi-implicit Euler. u holds the root twist at the fixed point P; the root origin's
    * classical acceleration adds omega x v_P (spatial -> classical). */

@@ -1640,6 +1640,12 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
 
 #pragma unroll
   for (int j = 0; j < ND; ++j) un[6 + j] = clampf(un[6 + j], -m->velocity_limit, m->velocity_limit);
+  {  // root link angular speed limit (rigid props max_angular_velocity; PhysX scales the vector)
+    const float w2 = un[0] * un[0] + un[1] * un[1] + un[2] * un[2];
+    const float wmax = m->max_angular_velocity;
+    const float sc = w2 > wmax * wmax ? wmax * __builtin_amdgcn_rsqf(w2) : 1.f;
+    un[0] *= sc; un[1] *= sc; un[2] *= sc;
+  }
 
   // semi-implicit Euler (root twist at P -> classical root-origin velocity adds omega x v dt)
   float wv[3];

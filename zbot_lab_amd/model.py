@@ -122,6 +122,7 @@ class ZbModel(C.Structure):
         ("default_joint_pos", C.c_float * NUM_DOF),
         ("kp", C.c_float), ("kd", C.c_float), ("effort_limit", C.c_float),
         ("velocity_limit", C.c_float), ("max_depenetration_velocity", C.c_float),
+        ("max_angular_velocity", C.c_float),
         ("base_link", C.c_int32), ("foot_links", C.c_int32 * 2), ("undesired_links", C.c_int32 * 10),
         ("api_root_link", C.c_int32), ("api_root_in_root", C.c_float * 7),
         ("api_joint_index", C.c_int32 * NUM_DOF), ("api_joint_sign", C.c_float * NUM_DOF),
@@ -446,6 +447,9 @@ def pack_model(rm: RobotModel | None = None) -> ZbModel:
     m.kp, m.kd = c["stiffness"], c["damping"]
     m.effort_limit, m.velocity_limit = c["effort_limit"], c["velocity_limit"]
     m.max_depenetration_velocity = c["max_depenetration_velocity"]
+    # RigidBodyPropertiesCfg(max_angular_velocity=1000.0) in every ZBOT cfg (zbot_cfg.py:632, 683, 732,
+    # 775); Isaac Lab's unit is deg/s, the simulator's rad/s
+    m.max_angular_velocity = math.radians(c.get("max_angular_velocity_deg", 1000.0))
     m.base_link = rm.base_link
     feet = [i for i, n in enumerate(rm.link_names) if n.startswith("foot")]  # "foot.*"
     m.foot_links[0], m.foot_links[1] = feet
