@@ -54,6 +54,8 @@ def main(argv=None) -> dict:
     ap.add_argument("--checkpoint", default=None, help="checkpoint file (else resolved under the log root)")
     ap.add_argument("--log_root", default=os.path.join("logs", "rsl_rl"))
     ap.add_argument("--num_steps", type=int, default=1000)
+    ap.add_argument("--env", action="append", default=[], metavar="PATH=VALUE",
+                    help="env cfg override by dotted path (as scripts/train.py --env)")
     ap.add_argument("--no_export", action="store_true")
     ap.add_argument("--fresh_episodes", action="store_true",
                     help="start every env at episode step 0 (the posture summary then describes step --num_steps)")
@@ -67,6 +69,7 @@ def main(argv=None) -> dict:
     agent_cfg = zbot_lab_amd.tasks.load_cfg(args.task, "rsl_rl_cfg_entry_point")
     if args.num_envs is not None:
         env_cfg.scene.num_envs = args.num_envs
+    zbot_lab_amd.tasks.apply_env_overrides(env_cfg, args.env)
     if args.seed is not None:
         agent_cfg.seed = args.seed
     if args.experiment_name is not None:

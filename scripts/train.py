@@ -52,6 +52,8 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--reward_cfg", default=None,
                     help="zbot-6b-walking-v2 reward stage (step2 / step3 / step4 = v2.py:150-206); the reference "
                          "edits the active reward_cfg in v2.py between its chained 2000-iteration runs")
+    ap.add_argument("--env", action="append", default=[], metavar="PATH=VALUE",
+                    help="env cfg override by dotted path, e.g. solver.iterations=8 (simulator ablations)")
     return ap
 
 
@@ -90,6 +92,7 @@ def main(argv=None) -> dict:
     if args.reward_cfg is not None:
         from zbot_lab_amd.envs.walking_v2 import REWARD_CFGS
         env_cfg.reward_cfg = REWARD_CFGS[args.reward_cfg]
+    zbot_lab_amd.tasks.apply_env_overrides(env_cfg, args.env)
 
     rank, local_rank = 0, 0
     if args.distributed:  # train.py:125-132: device per local rank, seed + rank

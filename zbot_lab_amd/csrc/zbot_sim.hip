@@ -271,50 +271,6 @@ __device__ __forceinline__ void body_si(MP m, const Kin& k, int b, SI& o) {
 constexpr int tri(int r, int c) { return r * (r + 1) / 2 + c; }  // r >= c
 constexpr int NT = NV * (NV + 1) / 2;
 
-// in place: A (lower triangle) -> L with L L^T = A; inv[j] = 1 / L_jj
-__device__ __forceinline__ void cholesky_inplace(float A[NT], float inv[NV]) {
-#pragma unroll
-  for (int j = 0; j < NV; ++j) {
-    float s = A[tri(j, j)];
-#pragma unroll
-    for (int k = 0; k < j; ++k) s -= A[tri(j, k)] * A[tri(j, k)];
-    const float d = sqrtf(fmaxf(s, 1e-12f));
-    A[tri(j, j)] = d;
-    const float iv = 1.f / d;
-    inv[j] = iv;
-#pragma unroll
-    for (int i = j + 1; i < NV; ++i) {
-      float t = A[tri(i, j)];
-#pragma unroll
-      for (int k = 0; k < j; ++k) t -= A[tri(i, k)] * A[tri(j, k)];
-      A[tri(i, j)] = t * iv;
-    }
-  }
-}
-// rank-1 downdate L L^T - a e_J e_J^T (removes the drive armature of a saturated joint);
-// mathematically identical to re-factoring, as the oracle does.
-template <int J>
-__device__ __forceinline__ void chol_downdate(float L[NT], float inv[NV], float a) {
-  float x[NV];
-#pragma unroll
-  for (int i = J; i < NV; ++i) x[i] = 0.f;
-  x[J] = sqrtf(a);
-#pragma unroll
-  for (int k = J; k < NV; ++k) {
-    const float lkk = L[tri(k, k)];
-    const float r = sqrtf(fmaxf(lkk * lkk - x[k] * x[k], 1e-12f));
-    const float c = r * inv[k], sn = x[k] * inv[k];
-    L[tri(k, k)] = r;
-    inv[k] = 1.f / r;
-    const float ic = 1.f / c;
-#pragma unroll
-    for (int i = k + 1; i < NV; ++i) {
-      const float lik = (L[tri(i, k)] - sn * x[i]) * ic;
-      x[i] = c * x[i] - sn * lik;
-      L[tri(i, k)] = lik;
-    }
-  }
-}
 __device__ __forceinline__ void fwd_sub(const float L[NT], const float inv[NV], const float b[NV], float y[NV]) {
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
@@ -331,15 +287,6 @@ __device__ __forceinline__ void bwd_sub(const float L[NT], const float inv[NV], 
 #pragma unroll
     for (int k = i + 1; k < NV; ++k) t -= L[tri(k, i)] * x[k];
     x[i] = t * inv[i];
-  }
-}
-__device__ __forceinline__ void lt_mul(const float L[NT], const float u[NV], float w[NV]) {
-#pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    float t = 0.f;
-#pragma unroll
-    for (int k = i; k < NV; ++k) t += L[tri(k, i)] * u[k];
-    w[i] = t;
   }
 }
 // 12-term dot with a 4-way split accumulation (shorter dependency chain than a serial sum)
@@ -370,12 +317,6 @@ __device__ __forceinline__ MP opaque(MP m) {
 constexpr int TL = 16;           // lanes per env
 #ifndef ZB_EPW
 #define ZB_EPW 4
-#endif
-#ifndef ZB_PGS_UNROLL
-#define ZB_PGS_UNROLL 1  // PGS slots unrolled (1) or the flattened ping-pong loop (0)
-#endif
-#ifndef ZB_TEAM_CHOL
-#define ZB_TEAM_CHOL 1  // cholesky_team (1) or the redundant per-lane cholesky_inplace (0)
 #endif
 #ifndef ZB_WAVES_PER_SIMD
 #define ZB_WAVES_PER_SIMD 1
@@ -1210,14 +1151,13 @@ __device__ __forceinline__ void crba_column(float L[NT], const float Fk[6], cons
   for (int jj = 0; jj <= K; ++jj) L[tri(6 + K, 6 + jj)] = tb<K>(Mk[jj]) + (jj == K ? arm : 0.f);
 }
 
-#if ZB_TEAM_CHOL
 // Team-parallel Cholesky of the 12x12 mass matrix. Lane s owns row own_row(s) of M (joint rows
 // 6 + s in lanes 0-5, where the CRBA leaves column s; root rows s - 6 in lanes 6-11) in R[].
 // Column k: every lane forms its row's t = M[r][k] - sum_{m<k} L[r][m] L[k][m] (row k of L from
 // its packed copy), the owner of row k broadcasts its t (the pivot), every lane takes
 // iv = rsq(pivot) and scales, and column k (rows >= k) is broadcast from the row owners into every
 // lane's packed L. ~200 instructions instead of the ~380 of the redundant factorisation; every
-// lane ends with the same L / inv as cholesky_inplace (lanes 12-15 own no row).
+// lane ends with the full L / inv (lanes 12-15 own no row).
 constexpr int own_lane(int r) { return r < 6 ? r + 6 : r - 6; }
 template <int K, int Rw>
 __device__ __forceinline__ void team_chol_bcast(float v, float L[NT]) {  // column K, rows Rw.. of L
@@ -1242,7 +1182,27 @@ __device__ __forceinline__ void cholesky_team(float R[NV], float L[NT], float in
   team_chol_col<6>(R, L, inv); team_chol_col<7>(R, L, inv); team_chol_col<8>(R, L, inv);
   team_chol_col<9>(R, L, inv); team_chol_col<10>(R, L, inv); team_chol_col<11>(R, L, inv);
 }
-#endif
+// x[s] in lanes s < N (a lane-dependent index into a team-uniform array), 0 in the others
+template <int N>
+__device__ __forceinline__ float pick_lane(const float (&x)[N], int s) {
+  float v = 0.f;
+#pragma unroll
+  for (int j = 0; j < N; ++j) v = s == j ? x[j] : v;
+  return v;
+}
+// Team forward substitution z = L^-1 y, columns K..KE-1. Lane s owns row r = own_row(s) with its
+// L row in R (cholesky_team) and t = y_r - sum_{k<K} L[r][k] z_k; z_K = t_owner / L_KK is
+// broadcast from the owner of row K, every lane removes its row's z_K term, and the owner keeps
+// z_K in wd. Lanes past their own row carry a meaningless t.
+template <int K, int KE>
+__device__ __forceinline__ void team_fwd(const float R[NV], const float inv[NV], float& t, float z[NV], float& wd,
+                                         int s) {
+  const float zk = tb<own_lane(K)>(t) * inv[K];
+  z[K] = zk;
+  wd = s == own_lane(K) ? zk : wd;
+  t = fmaf(-R[K], zk, t);
+  if constexpr (K + 1 < KE) team_fwd<K + 1, KE>(R, inv, t, z, wd, s);
+}
 
 // ------------------------------------------------------------------------- one substep
 // kLinkFriction: per-contact Coulomb coefficient from the per-link table q.fric (standup DR);
@@ -1276,15 +1236,17 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
   nc = detect(cfg, s.pos[2], q, over, sp);
   m = opaque(m0);
 
-  // RNEA bias forces (qddot = 0, gravity as base acceleration), one body per lane: lane b runs
-  // the velocity / acceleration chain up to its body (joints j >= b contribute zero), forms f_b,
-  // and the team suffix sum F_b = sum_{b' >= b} f_b' (DPP row shifts) gives the joint forces.
-  float Cb[NV];
+  // RNEA bias forces (qddot = 0, gravity as base acceleration) and, in the same team suffix sum,
+  // the generalised momentum: lane b runs the velocity / acceleration chain up to its body
+  // (joints j >= b contribute zero) and forms g_b = I_b V_b - dt f_b; the suffix sum
+  // G_b = sum_{b' >= b} g_b' (DPP row shifts) gives the implicit velocity update's right-hand side
+  // M u - dt C row by row: root rows G_0 (lane 0's sum), joint row j S_j . G_{j+1} (lane j). Each
+  // lane keeps the entry of the row it owns in the team Cholesky (own_row), so the free velocity
+  // needs one team forward substitution instead of L^T u plus a redundant L^-1 b.
   const float arm = dt * (m->kd + dt * m->kp);
   float L[NT];
-#if ZB_TEAM_CHOL
-  float R[NV];  // this lane's row of M (cholesky_team)
-#endif
+  float R[NV];   // this lane's row of M (cholesky_team)
+  float yown;    // this lane's row of M u - dt C
   {
   float S[ND][6];  // joint motion subspaces (LDS), live through RNEA + CRBA only
   read_S(q, S);
@@ -1307,7 +1269,7 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
         A[3 + a] += (t2[a] + t3[a]) * qd;
       }
     }
-    float f[6];
+    float g[6];
     {
       float IA[6], IV[6], t1[3], t2[3], t3[3];
       si_mul(Ib, A, IA);
@@ -1317,21 +1279,20 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
       cross3(V, IV + 3, t3);
 #pragma unroll
       for (int a = 0; a < 3; ++a) {
-        f[a] = IA[a] + t1[a] + t2[a];
-        f[3 + a] = IA[3 + a] + t3[a];
+        g[a] = fmaf(-dt, IA[a] + t1[a] + t2[a], IV[a]);
+        g[3 + a] = fmaf(-dt, IA[3 + a] + t3[a], IV[3 + a]);
       }
     }
-    suffix_sum<6>(f);
-    float Fn[6];
+    suffix_sum<6>(g);
+    float yj = 0.f, yr = 0.f;
+    const int r = q.s - 6;  // root row of lanes 6-11
 #pragma unroll
-    for (int a = 0; a < 6; ++a) Fn[a] = dppzf<DPP_SHL + 1>(f[a]);  // F_{j+1} in lane j
-    float cj = 0.f;
-#pragma unroll
-    for (int a = 0; a < 6; ++a) cj += Sown[a] * Fn[a];
-#pragma unroll
-    for (int a = 0; a < 6; ++a) Cb[a] = tb<0>(f[a]);
-    Cb[6] = tb<0>(cj); Cb[7] = tb<1>(cj); Cb[8] = tb<2>(cj);
-    Cb[9] = tb<3>(cj); Cb[10] = tb<4>(cj); Cb[11] = tb<5>(cj);
+    for (int a = 0; a < 6; ++a) {
+      yj = fmaf(Sown[a], dppzf<DPP_SHL + 1>(g[a]), yj);  // G_{j+1} in lane j
+      const float g0 = tb<0>(g[a]);
+      yr = r == a ? g0 : yr;
+    }
+    yown = q.s < ND ? yj : yr;  // lanes 12-15: 0
   }
 
   // CRBA: composite inertias by a team suffix sum; lane k forms F_k = Ic_{k+1} S_k and its
@@ -1354,7 +1315,6 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
       for (int a = 0; a < 6; ++a) t += S[jj][a] * Fk[a];
       Mk[jj] = t;
     }
-#if ZB_TEAM_CHOL
     // this lane's row of M (own_lane): joint row 6 + s from its own column (lanes 0-5), root row
     // s - 6 of the Ic_0 block (lane 0's composite) in lanes 6-11
     {
@@ -1375,106 +1335,68 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
 #pragma unroll
       for (int jj = 0; jj < ND; ++jj) R[6 + jj] = jrow ? Mk[jj] + (jj == q.s ? arm : 0.f) : 0.f;
     }
-#else
-    // root block from Ic_0 (lane 0)
-    const float m0t = tb<0>(ic[0]), hx = tb<0>(ic[1]), hy = tb<0>(ic[2]), hz = tb<0>(ic[3]);
-    L[tri(0, 0)] = tb<0>(ic[4]); L[tri(1, 1)] = tb<0>(ic[5]); L[tri(2, 2)] = tb<0>(ic[6]);
-    L[tri(1, 0)] = tb<0>(ic[7]); L[tri(2, 0)] = tb<0>(ic[8]); L[tri(2, 1)] = tb<0>(ic[9]);
-    L[tri(3, 0)] = 0.f; L[tri(3, 1)] = hz;  L[tri(3, 2)] = -hy;
-    L[tri(4, 0)] = -hz; L[tri(4, 1)] = 0.f; L[tri(4, 2)] = hx;
-    L[tri(5, 0)] = hy;  L[tri(5, 1)] = -hx; L[tri(5, 2)] = 0.f;
-    L[tri(3, 3)] = m0t; L[tri(4, 4)] = m0t; L[tri(5, 5)] = m0t;
-    L[tri(4, 3)] = 0.f; L[tri(5, 3)] = 0.f; L[tri(5, 4)] = 0.f;
-    crba_column<0>(L, Fk, Mk, arm);
-    crba_column<1>(L, Fk, Mk, arm);
-    crba_column<2>(L, Fk, Mk, arm);
-    crba_column<3>(L, Fk, Mk, arm);
-    crba_column<4>(L, Fk, Mk, arm);
-    crba_column<5>(L, Fk, Mk, arm);
-#endif
   }
   }  // S
 
-  // implicit PD drives. Pass 1: all implicit (armature on the diagonal). A joint whose implicit
-  // torque exceeds the effort limit gets an explicit +-limit torque and loses its armature
-  // (rank-1 downdate of the factor), then the free velocity is re-solved.
+  // implicit PD drives. Pass 1: all implicit (armature arm = dt kd + dt^2 kp on the joint
+  // diagonal; the drive adds arm qd + dt (kp (q* - q) - (kd + dt kp) qd) to the joint rows of the
+  // right-hand side). A joint whose implicit torque exceeds the effort limit gets an explicit
+  // +-limit torque and loses its armature, then the trailing rows are re-solved.
   sp.mark(3);
   float Li[NV];
-#if ZB_TEAM_CHOL
   // this lane's M row entries of the joint columns, kept for a re-factorisation of the trailing
   // block if a drive saturates (the contact-row granules are dead until the rows are rebuilt)
   float4* stash = q.b + STASH_OFF + 2 * q.lane;
   stash[0] = make_float4(R[6], R[7], R[8], R[9]);
   stash[1] = make_float4(R[10], R[11], 0.f, 0.f);
   cholesky_team(R, L, Li);
-#else
-  cholesky_inplace(L, Li);
-#endif
-  float u[NV], b[NV], w[NV];
-  u[0] = s.av[0]; u[1] = s.av[1]; u[2] = s.av[2];
-  u[3] = s.lv[0]; u[4] = s.lv[1]; u[5] = s.lv[2];
-#pragma unroll
-  for (int a = 0; a < 6; ++a) b[a] = -dt * Cb[a];
-  float rhs[ND];
+  float rhs[ND], padd[ND];
 #pragma unroll
   for (int j = 0; j < ND; ++j) {
-    u[6 + j] = s.jqd[j];
     rhs[j] = m->kp * (target[j] - s.jq[j]) - (m->kd + dt * m->kp) * s.jqd[j];
-    b[6 + j] = dt * (rhs[j] - Cb[6 + j]);
+    padd[j] = fmaf(arm, s.jqd[j], dt * rhs[j]);
   }
+  // whitened free velocity w = L^-1 ((M + A) u + dt (tau - C)) by team forward substitution;
+  // lane s keeps coordinate own_row(s) as its Gauss-Seidel coordinate wd
+  float t = yown + pick_lane<ND>(padd, q.s);
+  float z[NV], wd = 0.f;
+  team_fwd<0, 6>(R, Li, t, z, wd, q.s);
+  const float t5 = t;  // joint rows after the root columns (a saturated drive restarts here)
+  team_fwd<6, NV>(R, Li, t, z, wd, q.s);
   {
-    float z[NV];
-    lt_mul(L, u, w);
-    fwd_sub(L, Li, b, z);
-#pragma unroll
-    for (int a = 0; a < NV; ++a) w[a] += z[a];
-  }
-  {
+    // joint part of the free velocity (L^-T w restricted to the trailing block) for the
+    // saturation test
     float uf[NV];
-    bwd_sub(L, Li, w, uf);
+#pragma unroll
+    for (int i = NV - 1; i >= 6; --i) {
+      float tt = z[i];
+#pragma unroll
+      for (int k = i + 1; k < NV; ++k) tt -= L[tri(k, i)] * uf[k];
+      uf[i] = tt * Li[i];
+    }
     unsigned sat = 0;
+    float dsat[ND];
 #pragma unroll
     for (int j = 0; j < ND; ++j) {
       const float tau = rhs[j] - (arm / dt) * (uf[6 + j] - s.jqd[j]);
-      if (tau > m->effort_limit || tau < -m->effort_limit) {
-        sat |= 1u << j;
-        b[6 + j] = dt * ((tau > 0.f ? m->effort_limit : -m->effort_limit) - Cb[6 + j]);
-      }
+      const bool sj = tau > m->effort_limit || tau < -m->effort_limit;
+      sat |= sj ? 1u << j : 0u;
+      // joint row j without the drive: - arm qd - dt rhs, with the explicit +-limit torque
+      dsat[j] = sj ? dt * ((tau > 0.f ? m->effort_limit : -m->effort_limit) - rhs[j]) - arm * s.jqd[j] : 0.f;
     }
     if (sat) {
-#if ZB_TEAM_CHOL
       // M changes only on the saturated joints' diagonals (joint coordinates 6..11, the last
-      // ones), so L's leading columns are unchanged: re-factor the trailing 6x6 block from the
-      // stashed rows (= the oracle's full re-factorisation), then re-solve the trailing
-      // coordinates of w (w[0..5] are unchanged too)
+      // ones), so L's leading columns and z[0..5] are unchanged: re-factor the trailing 6x6 block
+      // from the stashed rows (= the oracle's full re-factorisation) and redo the trailing steps
+      // of the forward substitution from the joint rows' state after the root columns
       const float4 s0 = stash[0], s1 = stash[1];
       const float rt[ND] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y};
 #pragma unroll
       for (int jj = 0; jj < ND; ++jj) R[6 + jj] = rt[jj] - ((((sat >> jj) & 1u) != 0u && q.s == jj) ? arm : 0.f);
       team_chol_col<6>(R, L, Li); team_chol_col<7>(R, L, Li); team_chol_col<8>(R, L, Li);
       team_chol_col<9>(R, L, Li); team_chol_col<10>(R, L, Li); team_chol_col<11>(R, L, Li);
-      float z[NV];
-      fwd_sub(L, Li, b, z);  // only z[0..5] (unchanged) and z[6..11] feed w[6..11] below
-#pragma unroll
-      for (int i = 6; i < NV; ++i) {
-        float t = z[i];
-#pragma unroll
-        for (int k = i; k < NV; ++k) t += L[tri(k, i)] * u[k];
-        w[i] = t;
-      }
-#else
-      if (sat & 1u) chol_downdate<6>(L, Li, arm);
-      if (sat & 2u) chol_downdate<7>(L, Li, arm);
-      if (sat & 4u) chol_downdate<8>(L, Li, arm);
-      if (sat & 8u) chol_downdate<9>(L, Li, arm);
-      if (sat & 16u) chol_downdate<10>(L, Li, arm);
-      if (sat & 32u) chol_downdate<11>(L, Li, arm);
-      float z[NV];
-      lt_mul(L, u, w);
-      fwd_sub(L, Li, b, z);
-#pragma unroll
-      for (int a = 0; a < NV; ++a) w[a] += z[a];
-#endif
+      t = t5 + pick_lane<ND>(dsat, q.s);
+      team_fwd<6, NV>(R, Li, t, z, wd, q.s);
     }
   }
 
@@ -1530,7 +1452,7 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
       invm[r] = 1.f / (dot12(Y[r], Y[r]) + 1e-9f);
     }
 #pragma unroll
-    for (int d = 0; d < NV; ++d) q.yg_at(c, d) = make_float4(Y[0][d], Y[1][d], Y[2][d], 0.f);
+    for (int d = 0; d < NV; ++d) q.yg_at(c, own_lane(d)) = make_float4(Y[0][d], Y[1][d], Y[2][d], 0.f);
     float vmin;
     if (sep >= 0.f) vmin = -sep / dt;
     else vmin = fminf(cfg.baumgarte * (-sep) / dt, m->max_depenetration_velocity);
@@ -1542,67 +1464,51 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
     q.lam(c) = make_float4(0.f, 0.f, 0.f, 0.f);
   }
   wave_sync();
+  if (q.s >= nc && q.s < NCM) {
+    // an unused slot is an exact no-op update (zero rows, effective masses and bias: the impulse
+    // stays 0 and w is unchanged), so the sweep needs no per-env mask. (Region U: written only
+    // after every active lane has read its candidate above.)
+    const int c = q.s;
+#pragma unroll
+    for (int d = 0; d < NV; ++d) q.yg_at(c, d) = make_float4(0.f, 0.f, 0.f, 0.f);
+    q.yg_zero(c) = make_float4(0.f, 0.f, 0.f, 0.f);
+    q.aux(c, 0) = make_float4(0.f, 0.f, 0.f, 0.f);
+    q.aux(c, 1) = make_float4(0.f, 0.f, 0.f, 0.f);
+    q.lam(c) = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  wave_sync();
 
   sp.mark(5);
-  // projected Gauss-Seidel on the whitened velocity (Coulomb disk friction); lane s owns w[s].
-  // The sweep is flattened to K = iterations x nc contact updates and unrolled by two with
-  // ping-pong register sets: the granules and impulse of update k+1 are read while update k
-  // computes. With one contact the prefetched impulse is the one being updated (forwarded).
+  // projected Gauss-Seidel on the whitened velocity (Coulomb disk friction); lane s owns
+  // coordinate own_row(s) of w (its granule of every contact row holds that coordinate).
+  float w[NV];
+  // Sweeps outer, the NCM slots unrolled inner: constant LDS offsets, slot c + 1's granules read
+  // while slot c updates, slots c >= the wave's largest contact count skipped uniformly, the
+  // slots between an env's own count and that maximum are no-op updates (zeroed above). The
+  // impulses are team-uniform (every lane computes the same update); the team lead stores them.
   {
     const float mu = cfg.friction, mu_d = cfg.friction_dynamic;
     const float4* yl = q.b + YG_OFF + q.ygl();
-    float wd = 0.f;
-#pragma unroll
-    for (int d = 0; d < NV; ++d) wd = q.s == d ? w[d] : wd;
-    const bool lead = q.s == 0;
-#if ZB_PGS_UNROLL
-    // sweeps outer, the NCM slots unrolled inner: constant LDS offsets (no per-update index /
-    // address arithmetic), slot c >= the wave's largest contact count skipped uniformly, slots
-    // past this env's count masked; the same update order as the flattened loop below
     const int ncw = max(max(__builtin_amdgcn_readlane(nc, 0), __builtin_amdgcn_readlane(nc, TL)),
                         max(__builtin_amdgcn_readlane(nc, 2 * TL), __builtin_amdgcn_readlane(nc, 3 * TL)));
+    const bool lead = q.s == 0;
     for (int it = 0; it < cfg.solver_iterations; ++it) {
-      // slot c + 1's granules and impulse are read (unconditionally: the LDS slots exist) while
-      // slot c updates
       float4 G = q.yg(yl, 0), X = q.aux(0, 0), Z = q.aux(0, 1), La = q.lam(0);
 #pragma unroll
       for (int c = 0; c < NCM; ++c) {
         const int cn = c + 1 < NCM ? c + 1 : c;
         const float4 Gn = q.yg(yl, cn), Xn = q.aux(cn, 0), Zn = q.aux(cn, 1), Ln = q.lam(cn);
         if (c < ncw) {
-          if (c < nc) {
-            const float4 nA = pgs_update(G, X, Z, La, kLinkFriction ? Z.z : mu, kLinkFriction ? Z.w : mu_d, wd);
-            if (lead) q.lam(c) = nA;
-          }
+          const float4 nA = pgs_update(G, X, Z, La, kLinkFriction ? Z.z : mu, kLinkFriction ? Z.w : mu_d, wd);
+          if (lead) q.lam(c) = nA;
         }
         G = Gn; X = Xn; Z = Zn; La = Ln;
       }
     }
-#else
-    const int K = cfg.solver_iterations * nc;
-    int cA = 0;
-    float4 GA = q.yg(yl, 0), XA = q.aux(0, 0), ZA = q.aux(0, 1), LA = q.lam(0);
-    for (int k = 0; k < K; k += 2) {
-      const int cB = cA + 1 == nc ? 0 : cA + 1;
-      const float4 GB = q.yg(yl, cB), XB = q.aux(cB, 0), ZB = q.aux(cB, 1);
-      float4 LB = q.lam(cB);
-      const float4 nA = pgs_update(GA, XA, ZA, LA, kLinkFriction ? ZA.z : mu, kLinkFriction ? ZA.w : mu_d, wd);
-      if (lead) q.lam(cA) = nA;
-      if (cB == cA) LB = nA;
-      if (k + 1 < K) {
-        const int cA2 = cB + 1 == nc ? 0 : cB + 1;
-        GA = q.yg(yl, cA2); XA = q.aux(cA2, 0); ZA = q.aux(cA2, 1);
-        LA = q.lam(cA2);
-        const float4 nB = pgs_update(GB, XB, ZB, LB, kLinkFriction ? ZB.z : mu, kLinkFriction ? ZB.w : mu_d, wd);
-        if (lead) q.lam(cB) = nB;
-        if (cA2 == cB) LA = nB;
-        cA = cA2;
-      }
-    }
-#endif
-    w[0] = tb<0>(wd); w[1] = tb<1>(wd); w[2] = tb<2>(wd); w[3] = tb<3>(wd);
-    w[4] = tb<4>(wd); w[5] = tb<5>(wd); w[6] = tb<6>(wd); w[7] = tb<7>(wd);
-    w[8] = tb<8>(wd); w[9] = tb<9>(wd); w[10] = tb<10>(wd); w[11] = tb<11>(wd);
+    w[0] = tb<own_lane(0)>(wd); w[1] = tb<own_lane(1)>(wd); w[2] = tb<own_lane(2)>(wd);
+    w[3] = tb<own_lane(3)>(wd); w[4] = tb<own_lane(4)>(wd); w[5] = tb<own_lane(5)>(wd);
+    w[6] = tb<own_lane(6)>(wd); w[7] = tb<own_lane(7)>(wd); w[8] = tb<own_lane(8)>(wd);
+    w[9] = tb<own_lane(9)>(wd); w[10] = tb<own_lane(10)>(wd); w[11] = tb<own_lane(11)>(wd);
   }
   wave_sync();  // last impulses visible to every lane
   sp.mark(6);

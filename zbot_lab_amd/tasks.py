@@ -97,3 +97,24 @@ register(
         "rsl_rl_cfg_entry_point": "zbot_lab_amd.rl.cfg:Zbot6BFlatPPORunnerCfg",
     },
 )
+
+
+def apply_env_overrides(env_cfg, overrides):
+    """``--env a.b=v``: set attribute path a.b of the env cfg; v parsed as a Python literal
+    (bool / int / float / tuple) when it is one. Unknown paths raise, so a typo cannot silently
+    train the unmodified cfg."""
+    import ast
+    for item in overrides:
+        path, _, raw = item.partition("=")
+        try:
+            val = ast.literal_eval(raw)
+        except (ValueError, SyntaxError):
+            val = raw
+        *parents, leaf = path.split(".")
+        obj = env_cfg
+        for a in parents:
+            obj = getattr(obj, a)
+        if not hasattr(obj, leaf):
+            raise AttributeError(f"--env {item}: {type(obj).__name__} has no field {leaf!r}")
+        setattr(obj, leaf, val)
+    return env_cfg
