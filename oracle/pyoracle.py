@@ -45,6 +45,9 @@ def _load(double: bool = False):
     lib.zbo_physics_substeps.argtypes = [P, _f, C.c_int, C.c_void_p, C.c_void_p]
     lib.zbo_link_poses.argtypes = [P, _f, _f]
     lib.zbo_contact_diag.argtypes = [P, _f]
+    lib.zbo_hull_pair.argtypes = [_f, _f, C.c_float, _f]
+    lib.zbo_set_gjk_tol.argtypes = [C.c_double]
+    lib.zbo_self_min_sep.argtypes = [P, _f]
     lib.zbo_link_com_vel.argtypes = [P, _f]
     lib.zbo_energy_momentum.argtypes = [P, _f]
     lib.zbo_pre_physics.argtypes = [C.c_int, C.POINTER(zm.ZbTaskCfg), _f, _f, _f, _f, _f]
@@ -168,6 +171,13 @@ class OracleSim:
         """[n, 5]: candidates, ground, self, kept, min |sep - margin| of the current state."""
         d = np.zeros((self.n, 5), np.float32)
         self.lib.zbo_contact_diag(self.h, d)
+        return d
+
+    def self_min_sep(self):
+        """[n]: the smallest self-collision separation of the current state (-2 CORE_M: overlapping
+        cores, deeper than the shape model)."""
+        d = np.zeros(self.n, np.float32)
+        self.lib.zbo_self_min_sep(self.h, d)
         return d
 
     def link_com_vel(self):

@@ -25,7 +25,7 @@
  *   (gravity as base acceleration) -> CRBA mass matrix -> implicit PD drives (armature
  *   dt*kd + dt^2*kp on the joint diagonal; a joint whose implicit torque exceeds the effort
  *   limit is re-solved with an explicit +-limit torque and no armature) -> Cholesky M = L L^T ->
- *   contacts (circle-pair support points vs plane, sphere pairs for self collision) -> projected
+ *   contacts (circle-pair support points vs plane, GJK on rounded disk hulls for self collision) -> projected
  *   Gauss-Seidel on the whitened velocity w = L^T u with rows Y = L^-1 J^T (Coulomb disk
  *   friction) -> u = L^-T w -> joint speed clamp -> semi-implicit Euler, joint wrap.
  */
@@ -48,6 +48,14 @@ typedef ZBO_REAL real;
 #define NC_MAX ZB_MAX_CONTACTS /* contact slots per env per substep (= the HIP kernel) */
 #define NCAND_PER_LINK 4
 #define RIM_EPS 1e-3 /* m; = 2% of the 5 cm module radius */
+/* Self collision: each link's shape (the convex hull of its two circles) is written as a core
+ * hull Minkowski-summed with a ball of radius CORE_M, PhysX-PCM style: the core is the hull of the
+ * two circles moved CORE_M into the shape along their plane normals with radius r - CORE_M. The
+ * caps (disk faces) are exact, the rims are rounded with radius CORE_M. Pair distance = GJK
+ * distance of the cores - 2 CORE_M (exact up to the rim rounding, for penetrations < 2 CORE_M). */
+#define CORE_M 0.004
+#define GJK_MAX_IT 16
+#define GJK_TOL 1e-5 /* m: stop when the upper (|v|) and lower (v.w / |v|) distance bounds are this close */
 #define TWO_PI 6.283185307179586
 #define PI_R 3.14159265358979323846
 
@@ -98,6 +106,7 @@ typedef struct {
   int link_body[NL];
   real link_pos[NL][3], link_rot[NL][4], link_com[NL][3];
   real circle[NL][2][9], sphere[NL][2][4], bound[NL][4];
+  real core[NL][2][9];                /* core circles of the self-collision shape (body frame) */
   int circle_dup[NL];                 /* bit ci: duplicate of a lower link's mated face (skipped) */
   int npairs, pairs[ZB_MAX_SELF_PAIRS][2];
   real root_pos0[3], root_quat0[4], jq0[ND];
@@ -129,6 +138,22 @@ static void load_mdl(const zb_model* m, mdl_t* o) {
       for (int a = 0; a < 4; ++a) o->sphere[l][c][a] = m->link_sphere[l][c][a];
     }
   }
+  for (int l = 0; l < NL; ++l)
+    for (int c = 0; c < 2; ++c) {
+      const real* C = o->circle[l][c];
+      const real* O = o->circle[l][1 - c];
+      real n[3];
+      v3_cross(C + 3, C + 6, n);
+      real nn = sqrtr(v3_dot(n, n));
+      real r = sqrtr(v3_dot(C + 3, C + 3));
+      real to[3] = {O[0] - C[0], O[1] - C[1], O[2] - C[2]};
+      real sg = v3_dot(n, to) < 0 ? (real)-1 : (real)1; /* into the shape */
+      for (int a = 0; a < 3; ++a) {
+        o->core[l][c][a] = C[a] + sg * (real)CORE_M * n[a] / nn;
+        o->core[l][c][3 + a] = C[3 + a] * (r - (real)CORE_M) / r;
+        o->core[l][c][6 + a] = C[6 + a] * (r - (real)CORE_M) / r;
+      }
+    }
   o->npairs = m->num_self_pairs;
   for (int p = 0; p < o->npairs; ++p) { o->pairs[p][0] = m->self_pairs[p][0]; o->pairs[p][1] = m->self_pairs[p][1]; }
   for (int a = 0; a < 3; ++a) o->root_pos0[a] = m->default_root_pos[a];
@@ -320,7 +345,7 @@ typedef struct {
 } contact_t;
 
 /* Candidate list (canonical order): ground candidates link by link (<= NCAND_PER_LINK each),
- * then self-collision candidates in (pair, sphere a, sphere b) order, at most NSELF_MAX of them.
+ * then self-collision candidates in link-pair order (one per pair: hull_pair), at most NSELF_MAX.
  * When more than NC_MAX candidates exist the NC_MAX smallest by (sep, canonical index) are kept;
  * the kept contacts are solved in canonical order. Same rule as the kernel's quad selection. */
 #define NSELF_MAX 18
@@ -342,12 +367,196 @@ static void select_contacts(clist_t* L) {
   L->n = k;
 }
 
+/* ------------------------------------------------------------------ self collision (GJK)
+ * World-frame core circles of link l: centre, two semi-axes (radius baked in). */
+typedef struct { real c[2][9]; } hull_t;
+static double g_gjk_tol = GJK_TOL;
+
+static void world_hull(const mdl_t* m, const kin_t* k, int l, hull_t* h) {
+  int b = m->link_body[l];
+  for (int ci = 0; ci < 2; ++ci) {
+    m3_v(k->R[b], m->core[l][ci], h->c[ci]);
+    m3_v(k->R[b], m->core[l][ci] + 3, h->c[ci] + 3);
+    m3_v(k->R[b], m->core[l][ci] + 6, h->c[ci] + 6);
+    for (int a = 0; a < 3; ++a) h->c[ci][a] += k->p[b][a];
+  }
+}
+
+/* support point of the hull of two circles in direction d (a circle's support is its rim point
+ * along d's in-plane part; the centre when d is normal to the disk) */
+static void hull_support(const hull_t* h, const real d[3], real out[3]) {
+  real best = -1e30;
+  for (int ci = 0; ci < 2; ++ci) {
+    const real* c = h->c[ci];
+    real a = v3_dot(d, c + 3), b = v3_dot(d, c + 6);
+    real nr = sqrtr(a * a + b * b);
+    real p[3];
+    for (int q = 0; q < 3; ++q) p[q] = c[q] + (nr > (real)1e-15 ? (a * c[3 + q] + b * c[6 + q]) / nr : 0);
+    real v = v3_dot(d, p);
+    if (v > best) { best = v; out[0] = p[0]; out[1] = p[1]; out[2] = p[2]; }
+  }
+}
+
+/* One GJK simplex step. The simplex is the newest Minkowski point a (W[0], support point PA[0])
+ * plus the retained points W[1..n]. Candidates are the subsets that contain a, in the order {a},
+ * {a,S1}, {a,S2}, {a,S1,S2}, {a,S3}, {a,S1,S3}, {a,S2,S3}: the affine projection of the origin with
+ * all barycentric weights positive, the shortest kept (a later candidate must be strictly shorter).
+ * With three retained points the tetrahedron decides whether the origin is inside (overlap; a flat
+ * tetrahedron - relative volume < 1e-6 - does not count). The simplex is reduced to the winner
+ * (a first, then the used points in index order) and v, lam set. Returns 1 on overlap. */
+static int simplex_step(real W[4][3], real PA[4][3], int* n, real lam[4], real v[3]) {
+  static const int sub[7][3] = {{0, -1, -1}, {0, 1, -1}, {0, 2, -1}, {0, 1, 2}, {0, 3, -1}, {0, 1, 3}, {0, 2, 3}};
+  real best = v3_dot(W[0], W[0]);
+  int bi = 0;
+  real bl[3] = {1, 0, 0};
+  for (int c = 0; c < 3; ++c) v[c] = W[0][c];
+  for (int k = 1; k < 7; ++k) {
+    int m = sub[k][2] < 0 ? 2 : 3;
+    if (sub[k][m - 1] > *n) continue;
+    real p[3], l[3];
+    if (m == 2) {
+      real e[3];
+      for (int c = 0; c < 3; ++c) e[c] = W[sub[k][1]][c] - W[0][c];
+      real ee = v3_dot(e, e);
+      if (!(ee > (real)1e-20)) continue;
+      real t = -v3_dot(W[0], e) / ee;
+      if (!(t > 0 && t < 1)) continue;
+      for (int c = 0; c < 3; ++c) p[c] = W[0][c] + t * e[c];
+      l[0] = 1 - t; l[1] = t; l[2] = 0;
+    } else {
+      real e1[3], e2[3];
+      for (int c = 0; c < 3; ++c) { e1[c] = W[sub[k][1]][c] - W[0][c]; e2[c] = W[sub[k][2]][c] - W[0][c]; }
+      real g00 = v3_dot(e1, e1), g01 = v3_dot(e1, e2), g11 = v3_dot(e2, e2);
+      real r0 = -v3_dot(W[0], e1), r1 = -v3_dot(W[0], e2);
+      real det = g00 * g11 - g01 * g01;
+      if (!(det > (real)1e-24 * g00 * g11)) continue;
+      real ts = (r0 * g11 - r1 * g01) / det, tt = (g00 * r1 - g01 * r0) / det;
+      if (!(ts > 0 && tt > 0 && ts + tt < 1)) continue;
+      for (int c = 0; c < 3; ++c) p[c] = W[0][c] + ts * e1[c] + tt * e2[c];
+      l[0] = 1 - ts - tt; l[1] = ts; l[2] = tt;
+    }
+    real d2 = v3_dot(p, p);
+    if (d2 < best) {
+      best = d2; bi = k;
+      for (int c = 0; c < 3; ++c) { v[c] = p[c]; bl[c] = l[c]; }
+    }
+  }
+  if (*n == 3) { /* inside the tetrahedron? barycentric coordinates of the origin (Cramer) */
+    real e[3][3], x12[3];
+    for (int j = 0; j < 3; ++j)
+      for (int c = 0; c < 3; ++c) e[j][c] = W[j + 1][c] - W[0][c];
+    v3_cross(e[1], e[2], x12);
+    real det = v3_dot(e[0], x12);
+    real sc = sqrtr(v3_dot(e[0], e[0]) * v3_dot(e[1], e[1]) * v3_dot(e[2], e[2]));
+    if (fabs((double)det) > 1e-6 * (double)sc) {
+      real m0[3] = {-W[0][0], -W[0][1], -W[0][2]}, x20[3], x01[3];
+      v3_cross(e[2], e[0], x20);
+      v3_cross(e[0], e[1], x01);
+      real b0 = v3_dot(m0, x12) / det, b1 = v3_dot(m0, x20) / det, b2 = v3_dot(m0, x01) / det;
+      if (b0 > (real)1e-5 && b1 > (real)1e-5 && b2 > (real)1e-5 && b0 + b1 + b2 < 1 - (real)1e-5) return 1;
+    }
+  }
+  int m = bi == 0 ? 1 : (sub[bi][2] < 0 ? 2 : 3);
+  real NW[4][3], NP[4][3];
+  for (int j = 0; j < m; ++j)
+    for (int c = 0; c < 3; ++c) { NW[j][c] = W[sub[bi][j]][c]; NP[j][c] = PA[sub[bi][j]][c]; }
+  for (int j = 0; j < m; ++j)
+    for (int c = 0; c < 3; ++c) { W[j][c] = NW[j][c]; PA[j][c] = NP[j][c]; }
+  for (int j = 0; j < 4; ++j) lam[j] = j < m ? bl[j] : 0;
+  *n = m - 1;
+  return 0;
+}
+
+/* Self-collision contact of one link pair: GJK distance between the two core hulls from the
+ * initial direction (centre of A's core circles - centre of B's), stopping when
+ * (|v|^2 - v.w) / |v| <= 1 um (the distance bounds |v| and v.w / |v| agree; tighter is below fp32 resolution for nearly touching cores), after GJK_MAX_IT iterations, or early (no contact) once the lower
+ * bound v.w / |v| exceeds early_margin + 2 CORE_M (early_margin = margin for detection). Contact: normal (pa - pb) / d from B to A,
+ * separation d - 2 CORE_M, point (pa + pb) / 2. Cores that overlap (d < 1e-6): normal along the
+ * centre difference, separation -2 CORE_M, point = the mean of the centres. Returns 1 on a
+ * contact within the margin. */
+static int hull_pair(const hull_t* A, const hull_t* B, real margin, real early_margin, contact_t* out) {
+  real ca[3], cb[3], v[3];
+  for (int a = 0; a < 3; ++a) {
+    ca[a] = (real)0.5 * (A->c[0][a] + A->c[1][a]);
+    cb[a] = (real)0.5 * (B->c[0][a] + B->c[1][a]);
+    v[a] = ca[a] - cb[a];
+  }
+  if (v3_dot(v, v) < (real)1e-18) { v[0] = 1; v[1] = 0; v[2] = 0; }
+  real W[4][3], PA[4][3], lam[4] = {1, 0, 0, 0};
+  int n = 0, overlap = 0; /* n = retained points besides the newest W[0] */
+  {
+    real nd[3] = {-v[0], -v[1], -v[2]}, pa[3], pb[3];
+    hull_support(A, nd, pa);
+    hull_support(B, v, pb);
+    for (int a = 0; a < 3; ++a) { PA[0][a] = pa[a]; W[0][a] = pa[a] - pb[a]; v[a] = W[0][a]; }
+  }
+  for (int it = 0; it < GJK_MAX_IT; ++it) {
+    real vv = v3_dot(v, v);
+    if (vv < (real)1e-12) { overlap = 1; break; }
+    real nd[3] = {-v[0], -v[1], -v[2]}, pa[3], pb[3], w[3];
+    hull_support(A, nd, pa);
+    hull_support(B, v, pb);
+    for (int a = 0; a < 3; ++a) w[a] = pa[a] - pb[a];
+    real vw = v3_dot(v, w);
+    if (vw > 0 && vw * vw > vv * (early_margin + 2 * (real)CORE_M) * (early_margin + 2 * (real)CORE_M)) return 0;
+    if (vv - vw <= (real)g_gjk_tol * sqrtr(vv)) break; /* distance bounds within the tolerance */
+    /* the previous newest point is retained last (W[n+1]) and w becomes W[0] */
+    for (int a = 0; a < 3; ++a) {
+      W[n + 1][a] = W[0][a]; PA[n + 1][a] = PA[0][a];
+      W[0][a] = w[a]; PA[0][a] = pa[a];
+    }
+    ++n;
+    if (simplex_step(W, PA, &n, lam, v)) { overlap = 1; break; }
+  }
+  real d = sqrtr(v3_dot(v, v));
+  if (overlap || d < (real)1e-6) {
+    real dv[3] = {ca[0] - cb[0], ca[1] - cb[1], ca[2] - cb[2]};
+    real dn = sqrtr(v3_dot(dv, dv));
+    if (dn < (real)1e-12) { dv[0] = 0; dv[1] = 0; dv[2] = 1; dn = 1; }
+    out->sep = -2 * (real)CORE_M;
+    for (int a = 0; a < 3; ++a) { out->n[a] = dv[a] / dn; out->x[a] = (real)0.5 * (ca[a] + cb[a]); }
+    return out->sep < margin;
+  }
+  real pa[3] = {0, 0, 0};
+  for (int i = 0; i <= n; ++i)
+    for (int a = 0; a < 3; ++a) pa[a] += lam[i] * PA[i][a];
+  out->sep = d - 2 * (real)CORE_M;
+  for (int a = 0; a < 3; ++a) {
+    out->n[a] = v[a] / d;
+    out->x[a] = pa[a] - (real)0.5 * v[a]; /* (pa + pb) / 2 with pb = pa - v */
+  }
+  return out->sep < margin;
+}
+
+/* GJK stopping tolerance (test hook: the parity tests re-run the oracle at other tolerances to tell
+ * an env whose result depends on where GJK stops - an algorithmic discontinuity like the contact
+ * margin - from a real mismatch) */
+int zbo_set_gjk_tol(double tol) {
+  g_gjk_tol = tol > 0 ? tol : GJK_TOL;
+  return 0;
+}
+
+/* test entry point: hull_pair on two world-frame core hulls given as [2][9] floats (centre, two
+ * semi-axes per circle); out = {contact, sep, n[3], x[3]} (tests/test_oracle_selfcollision.py) */
+int zbo_hull_pair(const float* a, const float* b, float margin, float* out) {
+  hull_t A, B;
+  for (int ci = 0; ci < 2; ++ci)
+    for (int q = 0; q < 9; ++q) { A.c[ci][q] = a[9 * ci + q]; B.c[ci][q] = b[9 * ci + q]; }
+  contact_t c;
+  memset(&c, 0, sizeof(c));
+  int hit = hull_pair(&A, &B, (real)margin, (real)margin, &c);
+  out[0] = (float)hit;
+  out[1] = (float)c.sep;
+  for (int q = 0; q < 3; ++q) { out[2 + q] = (float)c.n[q]; out[5 + q] = (float)c.x[q]; }
+  return 0;
+}
+
 /* Ground: each link's shape is the convex hull of two circles (C, E1, E2 in body frame). The
  * lowest rim point of each circle plus its three 90-degree rotations along the rim are the
  * candidates (4 per circle: a flat disk resting on the plane yields a 4-point manifold);
- * per link the first NCAND_PER_LINK below the speculative margin are kept. Self: every sphere
- * pair of every non-adjacent link pair (the kernel's broadphase is conservative, so testing all
- * pairs here finds the same candidates). */
+ * per link the first NCAND_PER_LINK below the speculative margin are kept. Self: the GJK contact
+ * of every non-adjacent link pair (hull_pair; the kernel's broadphase is conservative, so testing
+ * all pairs here finds the same candidates). */
 static void detect(const mdl_t* m, const zb_task_cfg* cfg, const kin_t* k, real Pz, clist_t* L) {
   L->n = 0;
   const real margin = cfg->contact_margin;
@@ -398,31 +607,14 @@ static void detect(const mdl_t* m, const zb_task_cfg* cfg, const kin_t* k, real 
     int nself = 0;
     for (int p = 0; p < m->npairs && nself < NSELF_MAX; ++p) {
       int la = m->pairs[p][0], lb = m->pairs[p][1];
-      int ba = m->link_body[la], bb = m->link_body[lb];
-      for (int sa = 0; sa < 2; ++sa) {
-        real xa[3];
-        m3_v(k->R[ba], m->sphere[la][sa], xa);
-        for (int a = 0; a < 3; ++a) xa[a] += k->p[ba][a];
-        real ra = m->sphere[la][sa][3];
-        for (int sb = 0; sb < 2; ++sb) {
-          real xb[3];
-          m3_v(k->R[bb], m->sphere[lb][sb], xb);
-          for (int a = 0; a < 3; ++a) xb[a] += k->p[bb][a];
-          real rb = m->sphere[lb][sb][3];
-          real dv[3] = {xa[0] - xb[0], xa[1] - xb[1], xa[2] - xb[2]};
-          real dist = sqrtr(v3_dot(dv, dv));
-          real sep = dist - (ra + rb);
-          if (sep < margin && dist > (real)1e-9 && nself < NSELF_MAX) {
-            contact_t c;
-            c.la = la; c.lb = lb; c.sep = sep;
-            for (int a = 0; a < 3; ++a) {
-              c.n[a] = dv[a] / dist;
-              c.x[a] = (real)0.5 * ((xa[a] - c.n[a] * ra) + (xb[a] + c.n[a] * rb));
-            }
-            L->c[L->n++] = c;
-            ++nself;
-          }
-        }
+      hull_t A, B;
+      world_hull(m, k, la, &A);
+      world_hull(m, k, lb, &B);
+      contact_t c;
+      if (hull_pair(&A, &B, margin, margin, &c)) {
+        c.la = la; c.lb = lb;
+        L->c[L->n++] = c;
+        ++nself;
       }
     }
   }
@@ -2341,7 +2533,7 @@ int zbo_physics_substeps(zbo_sim* s, const float* targets, int nsub, float* net_
 
 /* contact diagnostics of the current state (parity debugging): per env [candidates before the
  * 12-slot selection, ground candidates, self candidates (after the NSELF_MAX cap), kept, min
- * |sep - margin| over every tested ground rim point and sphere pair (distance to the activation
+ * |sep - margin| over every tested ground rim point and link pair (distance to the activation
  * threshold)] */
 int zbo_contact_diag(zbo_sim* s, float* out) {
   for (int e = 0; e < s->n; ++e) {
@@ -2381,20 +2573,14 @@ int zbo_contact_diag(zbo_sim* s, float* out) {
     }
     if (s->c.enable_self_collision) {
       for (int p = 0; p < s->m.npairs; ++p) {
-        int la = s->m.pairs[p][0], lb = s->m.pairs[p][1];
-        int ba = s->m.link_body[la], bb = s->m.link_body[lb];
-        for (int sa = 0; sa < 2; ++sa)
-          for (int sb = 0; sb < 2; ++sb) {
-            real xa[3], xb[3];
-            m3_v(k.R[ba], s->m.sphere[la][sa], xa);
-            m3_v(k.R[bb], s->m.sphere[lb][sb], xb);
-            for (int a = 0; a < 3; ++a) { xa[a] += k.p[ba][a]; xb[a] += k.p[bb][a]; }
-            real dv[3] = {xa[0] - xb[0], xa[1] - xb[1], xa[2] - xb[2]};
-            real sep = sqrtr(v3_dot(dv, dv)) - (s->m.sphere[la][sa][3] + s->m.sphere[lb][sb][3]);
-            real d = (real)fabs((double)(sep - margin));
-            if (d < mind) mind = d;
-            if (sep < margin && ns < NSELF_MAX) ++ns;
-          }
+        hull_t A, B;
+        world_hull(&s->m, &k, s->m.pairs[p][0], &A);
+        world_hull(&s->m, &k, s->m.pairs[p][1], &B);
+        contact_t c;
+        hull_pair(&A, &B, margin, (real)1e30, &c); /* no early exit: the separation of every pair */
+        real d = (real)fabs((double)(c.sep - margin));
+        if (d < mind) mind = d;
+        if (c.sep < margin && ns < NSELF_MAX) ++ns;
       }
     }
     detect(&s->m, &s->c, &k, Pz, &L);
@@ -2403,6 +2589,27 @@ int zbo_contact_diag(zbo_sim* s, float* out) {
     out[5 * e + 2] = (float)ns;
     out[5 * e + 3] = (float)L.n;
     out[5 * e + 4] = (float)mind;
+  }
+  return 0;
+}
+
+/* per env: the smallest self-collision separation over all link pairs (GJK on the rounded cores,
+ * no early exit; -2 CORE_M = cores overlapping, beyond the exact range). Parity tests use it to
+ * set aside random test states whose links interpenetrate deeper than the shape model covers. */
+int zbo_self_min_sep(zbo_sim* s, float* out) {
+  for (int e = 0; e < s->n; ++e) {
+    kin_t k;
+    fk(&s->m, &s->env[e].ph, &k);
+    real mn = (real)1e30;
+    for (int p = 0; p < s->m.npairs; ++p) {
+      hull_t A, B;
+      world_hull(&s->m, &k, s->m.pairs[p][0], &A);
+      world_hull(&s->m, &k, s->m.pairs[p][1], &B);
+      contact_t c;
+      hull_pair(&A, &B, (real)1e30, (real)1e30, &c);
+      if (c.sep < mn) mn = c.sep;
+    }
+    out[e] = (float)mn;
   }
   return 0;
 }

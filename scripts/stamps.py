@@ -21,6 +21,9 @@ torch.cuda.synchronize()
 nat.lib().zb_read_stamps(buf)
 waves = (env.num_envs + 3) // 4  # one wave per 4 envs (16 lanes per env)
 tot = sum(buf[k] for k in range(len(names)))
+calls, its, wmax = buf[13], buf[14], buf[15]
+print(f"self collision: {calls / waves / steps / 4:.1f} GJK calls per wave per substep, {its / max(calls, 1):.2f} "
+      f"iterations per call; slowest wave of one launch {wmax:.0f} cycles (mean {tot / waves / steps:.0f})")
 print(f"cycles per wave per step: {tot / waves / steps:.0f}")
 for k in range(len(names)):
     print(f"  {names[k]:32s} {buf[k] / waves / steps:10.0f}  {100 * buf[k] / tot:5.1f} %")

@@ -175,12 +175,15 @@ def random_states(task: str, o, n: int, seed: int, standing: bool = False) -> np
     return st
 
 
-def tolerance_rows(task: str, before: np.ndarray, after_o: np.ndarray, nsteps: int = 1) -> np.ndarray:
+def tolerance_rows(task: str, before: np.ndarray, after_o: np.ndarray, nsteps: int = 1,
+                   reset: np.ndarray | None = None) -> np.ndarray:
     """Per-row, per-env tolerance array [state_dim, n] for comparing GPU vs oracle state.
 
     ``kin`` rows (feet latches, step lengths, integrators, current yaw, centre height, metrics) and
     the TIGHT_TERMS sums come from the pre-step state only in v2 and only for one step (the
-    one-step lag); otherwise they read post-step physics and get the physics tolerance."""
+    one-step lag); otherwise they read post-step physics and get the physics tolerance. So do
+    v2's feet-down latches of the envs that reset in the step (``reset``): the stale latch holds
+    the terminal, post-physics feet positions."""
     g = row_groups(task)
     tol = np.zeros_like(after_o, dtype=np.float64)
     multi = nsteps > 1
@@ -191,6 +194,10 @@ def tolerance_rows(task: str, before: np.ndarray, after_o: np.ndarray, nsteps: i
         a, r = TOL["phys_pos"] if cls == "kin" and not lagged else TOL[cls]
         for k in rows:
             tol[k] = a + r * np.abs(after_o[k])
+    if lagged and reset is not None and reset.any():
+        a, r = TOL["phys_pos"]
+        for k in _rows(S, "FEET_DOWN_POS", 6):
+            tol[k] = np.where(reset, np.maximum(tol[k], a + r * np.abs(after_o[k])), tol[k])
     cfg = task_cfg(task)
     terms, w = cfg.reward_terms, cfg.reward_weights
     tight = TIGHT_TERMS[task] if not multi else set()
@@ -209,7 +216,7 @@ def tolerance_rows(task: str, before: np.ndarray, after_o: np.ndarray, nsteps: i
 def compare(task, sg, so, obs_g, obs_o, rew_g, rew_o, fl_g, fl_o, before, nsteps: int = 1):
     """Per-env worst error/tolerance ratio over every state row, obs, reward; flags mismatch -> inf.
     Returns (ratio [n], details per env: list of (name, err, tol))."""
-    tol = tolerance_rows(task, before, so, nsteps)
+    tol = tolerance_rows(task, before, so, nsteps, reset=np.asarray(fl_o[0]) | np.asarray(fl_o[1]))
     err = np.abs(sg.astype(np.float64) - so)
     # reset envs: both sides reset -> the state is the reset state (compared with the same tolerances)
     ratio_rows = np.where(tol > 0, err / np.maximum(tol, 1e-30), np.where(err > 0, np.inf, 0.0))

@@ -41,7 +41,13 @@ def test_planted_errors_are_unexplained(oracle_lib, task):
     out, sg = _device_f64(task, n, seed, st, [a])
     g = row_groups(task)
     sg = sg.copy()
-    envs = [3, 40, 77, 150]
+    # plant into envs where the oracle is stable (no contact discontinuity nearby) and that do not
+    # reset in the step, so every planted error must be reported as unexplained
+    so, outs = T._run_oracle(task, n, seed, st, [a])
+    ob_o, rw_o, te_o, tr_o = outs[-1]
+    sens = T._sensitivity(task, n, seed, st, [a], so, ob_o, rw_o, (te_o, tr_o), st, 1)
+    calm = [int(e) for e in np.nonzero((sens < 0.3) & ~(te_o | tr_o))[0]]
+    envs = [calm[k] for k in (1, 10, 20, 30)]
     sg[g["sums"][0], envs[0]] += 2e-2            # a per-term episode sum off by a weight-sized error
     sg[g["exact"][0], envs[1]] += 1e-3           # p_delta / raw action carry
     if g["kin"]:

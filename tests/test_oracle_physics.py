@@ -49,7 +49,9 @@ def test_momentum_first_order_without_gravity_and_contact():
     drift = []
     for dt in (0.005, 0.0025):
         n = 8
-        s = _sim(n, zm.TaskCfg(gravity=0.0, sim_dt=dt), double=True)
+        # self collision off: the strong drive transients fold links into each other, and contact
+        # is what the title excludes (impulses are internal, but not first order in dt)
+        s = _sim(n, zm.TaskCfg(gravity=0.0, sim_dt=dt, enable_self_collision=False), double=True)
         st = _airborne(n, seed=3, jqd_sigma=2.0, vel=0.5)
         s.set_state(st)
         em0 = s.energy_momentum()

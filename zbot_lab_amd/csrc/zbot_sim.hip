@@ -37,6 +37,12 @@ constexpr int WAVE = 64;
 constexpr float PI_F = 3.14159265358979323846f;
 constexpr float TWO_PI_F = 6.28318530717958647692f;
 constexpr float RIM_EPS = 1e-3f;  // m; 2% of the module radius (see detect)
+// Self collision on the link shape written as a core hull + a ball of radius kCoreM (PhysX PCM
+// style): the core is the hull of the two circles moved kCoreM into the shape along their normals
+// with radius r - kCoreM; caps exact, rims rounded (= oracle CORE_M)
+constexpr float kCoreM = 0.004f;
+constexpr int kGjkMaxIt = 16;
+constexpr float kGjkTol = 1e-5f;  // m: GJK stops when its distance bounds are this close
 
 // The ZBOT-6 chain topology is compiled in (zb_create checks the model against it):
 // link l belongs to composite body (l+1)/2; joint j connects body j -> j+1.
@@ -57,6 +63,7 @@ __device__ __forceinline__ MP to_mp(const zb_model* m) { return (MP)(uintptr_t)m
 // Built only with -DZB_STAMPS (python -m zbot_lab_amd.build --stamps): s_memtime deltas per phase,
 // summed per wave (lane 0) into g_stamps. Never part of the measured product build.
 constexpr int NSTAMP = 16;
+constexpr int kStampCount0 = 13;  // slots 13, 14 count events (GJK calls, iterations); 15 = max wave cycles
 #ifdef ZB_STAMPS
 __device__ unsigned long long g_stamps[NSTAMP];
 struct Stamps {
@@ -70,15 +77,25 @@ struct Stamps {
     acc[k] += n - t;
     t = n;
   }
+  // per-lane event counts (slots >= kStampCount0), summed over every lane at flush
+  __device__ void count(int k, unsigned v) { acc[k] += v; }
   __device__ void flush() {
     if ((threadIdx.x & 63) == 0)
-      for (int k = 0; k < NSTAMP; ++k) atomicAdd(&g_stamps[k], acc[k]);
+      for (int k = 0; k < kStampCount0; ++k) atomicAdd(&g_stamps[k], acc[k]);
+    for (int k = kStampCount0; k < NSTAMP - 1; ++k)
+      if (acc[k]) atomicAdd(&g_stamps[k], acc[k]);
+    if ((threadIdx.x & 63) == 0) {  // slot NSTAMP - 1: the slowest wave's cycles over the launches
+      unsigned long long tot = 0;
+      for (int k = 0; k < kStampCount0; ++k) tot += acc[k];
+      atomicMax(&g_stamps[NSTAMP - 1], tot);
+    }
   }
 };
 #else
 struct Stamps {
   __device__ void begin() {}
   __device__ void mark(int) {}
+  __device__ void count(int, unsigned) {}
   __device__ void flush() {}
 };
 #endif
@@ -319,7 +336,7 @@ constexpr int TL = 16;           // lanes per env
 #define ZB_EPW 4
 #endif
 #ifndef ZB_WAVES_PER_SIMD
-#define ZB_WAVES_PER_SIMD 1
+#define ZB_WAVES_PER_SIMD 2
 #endif
 // The manager kernel needs the explicit bound: left at 1 it takes 256 VGPRs + 4 AGPRs (one wave
 // per SIMD); at 2 it fits 256 registers with 16 B/lane of scratch and runs 39 % faster at 8192 envs.
@@ -413,8 +430,9 @@ __device__ __forceinline__ int xcd_block(int b, int nb) {
 }
 
 // Device-side per-link collision table (built by zb_create), float4-aligned for per-lane loads:
-// [0] bounding sphere, [1+3ci..3+3ci] circle ci: C, E1, E2 (body frame), [7], [8] inscribed spheres,
-// [9] union sphere of the two (midpoint, max r + half their distance + 1 um) for the broadphase.
+// [0] bounding sphere, [1+3ci..3+3ci] circle ci: C, E1, E2 (body frame), [7 + ci] core circle ci
+// {centre, semi-axis scale (r - kCoreM) / r}, [9] bounding sphere of the two circles (midpoint of
+// the centres, max |C - mid| + r + 1 um) for the self-collision broadphase.
 // After the NL links: the self-pair list as ints (16 la + lb), then the default-pose constants.
 constexpr int LINK4 = 10;
 constexpr int NPAIR = (NL - 1) * (NL - 2) / 2;  // non-adjacent link pairs (55), checked by zb_create
@@ -730,62 +748,265 @@ __device__ __forceinline__ T* opaque_ptr(T* p) {
 }
 
 // ------------------------------------------------------------------------- contacts
-// One self-collision candidate pair: up to 4 sphere-pair contacts, in (sa, sb) order. Test mode
-// (kEmit false) returns the 4-bit mask of sphere pairs within the margin; emit mode writes exactly
-// the sphere pairs of `sel` (the test pass's mask) through `out(x, sep, n, code)`. The write pass
-// never re-tests: two separately compiled copies of the margin test could round differently at
-// the boundary, leaving a counted candidate slot unwritten.
-template <bool kEmit, class F>
-__device__ __forceinline__ unsigned narrow_pair(const Q& q, int pidx, float margin, unsigned sel, F&& out) {
-  const int pcode = q.pair_code(pidx);
-  const int la = pcode >> 4, lb = pcode & 15;
-  float Ra[9], pa[3], Rb[9], pb[3];
-  read_frame(q, link_body(la), Ra, pa);
-  read_frame(q, link_body(lb), Rb, pb);
-  const float4* LA = q.link(la);
-  const float4* LB = q.link(lb);
-  unsigned hits = 0;
+// Self collision: GJK distance between the core hulls of a link pair (world frame, relative to P).
+struct Hull {
+  float c[2][3], e1[2][3], e2[2][3];  // core circles: centre, semi-axes (radius baked in)
+};
+__device__ __forceinline__ void world_hull(const Q& q, int l, Hull& h) {
+  float R[9], p[3];
+  read_frame(q, link_body(l), R, p);
+  const float4* L = q.link(l);
 #pragma unroll
-  for (int sa = 0; sa < 2; ++sa) {
-    const float4 spa = LA[7 + sa];
-    float xa[3];
-    mv3f(Ra, spa, xa);
-    xa[0] += pa[0]; xa[1] += pa[1]; xa[2] += pa[2];
+  for (int ci = 0; ci < 2; ++ci) {
+    const float4 cc = L[7 + ci];
+    float4 e1 = L[2 + 3 * ci], e2 = L[3 + 3 * ci];
+    e1.x *= cc.w; e1.y *= cc.w; e1.z *= cc.w;
+    e2.x *= cc.w; e2.y *= cc.w; e2.z *= cc.w;
+    mv3f(R, cc, h.c[ci]);
+    h.c[ci][0] += p[0]; h.c[ci][1] += p[1]; h.c[ci][2] += p[2];
+    mv3f(R, e1, h.e1[ci]);
+    mv3f(R, e2, h.e2[ci]);
+  }
+}
+// support point of the hull of the two circles along d (a circle's rim point along d's in-plane
+// part; its centre when d is normal to the disk)
+__device__ __forceinline__ void hull_sup(const Hull& h, const float d[3], float o[3]) {
+  float best = 0.f;
 #pragma unroll
-    for (int sb = 0; sb < 2; ++sb) {
-      const float4 spb = LB[7 + sb];
-      float xb[3];
-      mv3f(Rb, spb, xb);
-      xb[0] += pb[0]; xb[1] += pb[1]; xb[2] += pb[2];
-      const float dv[3] = {xa[0] - xb[0], xa[1] - xb[1], xa[2] - xb[2]};
-      const float dist = sqrtf(dot3(dv, dv));
-      const float sep = dist - (spa.w + spb.w);
-      const unsigned bit = 1u << (2 * sa + sb);
-      if (kEmit ? (sel & bit) != 0u : (sep < margin && dist > 1e-9f)) {
-        if (kEmit) {
-          float n[3], x[3];
+  for (int ci = 0; ci < 2; ++ci) {
+    const float a = dot3(d, h.e1[ci]), b = dot3(d, h.e2[ci]);
+    const float ri = __builtin_amdgcn_rsqf(fmaxf(fmaf(a, a, b * b), 1e-30f));
+    float pt[3];
 #pragma unroll
-          for (int a = 0; a < 3; ++a) {
-            n[a] = dv[a] / dist;
-            x[a] = 0.5f * ((xa[a] - n[a] * spa.w) + (xb[a] + n[a] * spb.w));
-          }
-          out(x, sep, n, (float)(16 * la + lb + 1));
-        }
-        hits |= bit;
+    for (int k = 0; k < 3; ++k) pt[k] = h.c[ci][k] + (a * h.e1[ci][k] + b * h.e2[ci][k]) * ri;
+    const float v = dot3(d, pt);
+    const bool take = ci == 0 || v > best;
+    best = take ? v : best;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) o[k] = take ? pt[k] : o[k];
+  }
+}
+struct SelfContact { float x[3], sep, n[3]; };
+// GJK sub-simplex candidates (newest point a, retained points S): the affine projection of the
+// origin onto {a, S_I} / {a, S_I, S_J} with positive barycentric weights, kept if strictly shorter
+template <int I>
+__device__ __forceinline__ void gjk_seg(const float a[3], const float S[3][3], float& best, float bv[3], float bl[3],
+                                        unsigned& bm) {
+  float e[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) e[k] = S[I][k] - a[k];
+  const float ee = dot3(e, e);
+  const float t = -dot3(a, e) / fmaxf(ee, 1e-30f);
+  float p[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) p[k] = a[k] + t * e[k];
+  const float d2 = dot3(p, p);
+  const bool ok = ee > 1e-20f && t > 0.f && t < 1.f && d2 < best;
+  best = ok ? d2 : best;
+  bm = ok ? (1u << I) : bm;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    bv[k] = ok ? p[k] : bv[k];
+    bl[k] = ok ? (k == I ? t : 0.f) : bl[k];
+  }
+}
+template <int I, int J>
+__device__ __forceinline__ void gjk_tri(const float a[3], const float S[3][3], float& best, float bv[3], float bl[3],
+                                        unsigned& bm) {
+  float e1[3], e2[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) { e1[k] = S[I][k] - a[k]; e2[k] = S[J][k] - a[k]; }
+  const float g00 = dot3(e1, e1), g01 = dot3(e1, e2), g11 = dot3(e2, e2);
+  const float r0 = -dot3(a, e1), r1 = -dot3(a, e2);
+  const float det = g00 * g11 - g01 * g01;
+  const float id = 1.f / (fabsf(det) > 1e-30f ? det : 1e-30f);
+  const float ts = (r0 * g11 - r1 * g01) * id, tt = (g00 * r1 - g01 * r0) * id;
+  float p[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) p[k] = a[k] + ts * e1[k] + tt * e2[k];
+  const float d2 = dot3(p, p);
+  const bool ok = det > 1e-24f * g00 * g11 && ts > 0.f && tt > 0.f && ts + tt < 1.f && d2 < best;
+  best = ok ? d2 : best;
+  bm = ok ? ((1u << I) | (1u << J)) : bm;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    bv[k] = ok ? p[k] : bv[k];
+    bl[k] = ok ? (k == I ? ts : (k == J ? tt : 0.f)) : bl[k];
+  }
+}
+
+// Cheap separation test before GJK: from the same v0, up to K steps of the two-point update
+// (v <- the point of segment [v, w] closest to the origin) with GJK's lower bound v.w / |v|; true
+// once the bound exceeds lim = margin + 2 kCoreM (the cores are farther apart than any contact),
+// false when undecided. A rigorous bound, so it never drops a contact that gjk_pair would find.
+__device__ __forceinline__ bool hulls_separated(const Hull& A, const Hull& B, float lim, int K) {
+  float v[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) v[k] = 0.5f * (A.c[0][k] + A.c[1][k]) - 0.5f * (B.c[0][k] + B.c[1][k]);
+  if (dot3(v, v) < 1e-18f) { v[0] = 1.f; v[1] = 0.f; v[2] = 0.f; }
+  bool first = true;
+  for (int it = 0; it <= K; ++it) {
+    const float vv = dot3(v, v);
+    if (!first && vv < 1e-12f) return false;
+    float pa[3], pb[3], w[3];
+    const float nd[3] = {-v[0], -v[1], -v[2]};
+    hull_sup(A, nd, pa);
+    hull_sup(B, v, pb);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) w[k] = pa[k] - pb[k];
+    if (!first) {
+      const float vw = dot3(v, w);
+      if (vw > 0.f && vw * vw > vv * lim * lim) return true;
+    }
+    float e[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) e[k] = w[k] - v[k];
+    const float t = first ? 1.f : fminf(fmaxf(-dot3(v, e) / fmaxf(dot3(e, e), 1e-30f), 0.f), 1.f);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) v[k] += t * e[k];
+    first = false;
+  }
+  return false;
+}
+// GJK (distance) on the core hulls A, B from v0 = centre(A) - centre(B). Simplex = the newest
+// Minkowski point a plus up to three retained points S0..S2 (with their A-side support points);
+// each iteration takes the shortest of the valid affine projections of the subsets containing a,
+// in the order {a}, {a,S0}, {a,S1}, {a,S0,S1}, {a,S2}, {a,S0,S2}, {a,S1,S2} (segments, triangles
+// with positive barycentrics; the tetrahedron only as the inside test).
+// Stops when (|v|^2 - v.w) / |v| <= 1 um (the distance bounds |v| and v.w / |v| agree; tighter is below fp32 resolution for nearly touching cores), after kGjkMaxIt iterations, or as soon as the lower
+// bound v.w / |v| exceeds early_margin + 2 kCoreM (no contact; early_margin = margin in the
+// counting pass, huge when a counted contact is re-computed). Contact: n = (pa - pb) / d
+// (B -> A), sep = d - 2 kCoreM, x = (pa + pb) / 2; overlapping cores: n along the centre
+// difference, sep = -2 kCoreM, x = the mean centre. Same statement as the oracle's hull_pair.
+__device__ __forceinline__ bool gjk_pair(const Hull& A, const Hull& B, float margin, float early_margin,
+                                         SelfContact& out, int& iters) {
+  float v[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) v[k] = 0.5f * (A.c[0][k] + A.c[1][k]) - 0.5f * (B.c[0][k] + B.c[1][k]);
+  if (dot3(v, v) < 1e-18f) { v[0] = 1.f; v[1] = 0.f; v[2] = 0.f; }
+  const float lim = early_margin + 2.f * kCoreM;
+  float S[3][3] = {}, SP[3][3] = {}, lam[4] = {1.f, 0.f, 0.f, 0.f};
+  float ap[3] = {}, aw[3] = {};  // newest point (A support, Minkowski point)
+  int n = -1;          // retained points (-1: the first point not yet taken)
+  bool overlap = false;
+  for (int it = 0; it <= kGjkMaxIt; ++it) {
+    iters = it;
+    const float vv = dot3(v, v);
+    if (n >= 0 && vv < 1e-12f) { overlap = true; break; }
+    float pa[3], pb[3], w[3];
+    const float nd[3] = {-v[0], -v[1], -v[2]};
+    hull_sup(A, nd, pa);
+    hull_sup(B, v, pb);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) w[k] = pa[k] - pb[k];
+    if (n < 0) {  // first point
+#pragma unroll
+      for (int k = 0; k < 3; ++k) { aw[k] = w[k]; ap[k] = pa[k]; v[k] = w[k]; }
+      n = 0;
+      continue;
+    }
+    const float vw = dot3(v, w);
+    if (vw > 0.f && vw * vw > vv * lim * lim) return false;
+    if (vv - vw <= kGjkTol * sqrtf(vv)) break;  // distance bounds within kGjkTol
+    // retire the current newest point into the retained set (slot n), take w as the newest
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      S[2][k] = n == 2 ? aw[k] : S[2][k]; SP[2][k] = n == 2 ? ap[k] : SP[2][k];
+      S[1][k] = n == 1 ? aw[k] : S[1][k]; SP[1][k] = n == 1 ? ap[k] : SP[1][k];
+      S[0][k] = n == 0 ? aw[k] : S[0][k]; SP[0][k] = n == 0 ? ap[k] : SP[0][k];
+      aw[k] = w[k]; ap[k] = pa[k];
+    }
+    ++n;
+    // candidates: {a}, then per retained point i the segment {a, Si} and the triangles {a, Sj, Si}
+    // (j < i), then the inside-tetrahedron test; only the retained points that exist are visited
+    float best = dot3(aw, aw), bv[3] = {aw[0], aw[1], aw[2]}, bl[3] = {0.f, 0.f, 0.f};
+    unsigned bm = 0;  // retained points used (bit i: S_i)
+    gjk_seg<0>(aw, S, best, bv, bl, bm);
+    if (n >= 2) {
+      gjk_seg<1>(aw, S, best, bv, bl, bm);
+      gjk_tri<0, 1>(aw, S, best, bv, bl, bm);
+    }
+    if (n >= 3) {
+      gjk_seg<2>(aw, S, best, bv, bl, bm);
+      gjk_tri<0, 2>(aw, S, best, bv, bl, bm);
+      gjk_tri<1, 2>(aw, S, best, bv, bl, bm);
+    }
+    if (n == 3) {  // origin inside the tetrahedron (a, S0, S1, S2)?
+      float e0[3], e1[3], e2[3], x12[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) { e0[k] = S[0][k] - aw[k]; e1[k] = S[1][k] - aw[k]; e2[k] = S[2][k] - aw[k]; }
+      cross3(e1, e2, x12);
+      const float det = dot3(e0, x12);
+      // a flat tetrahedron (relative volume below 1e-6) or an origin within 1e-5 of a face is no
+      // evidence of an overlap
+      if (fabsf(det) > 1e-6f * sqrtf(dot3(e0, e0) * dot3(e1, e1) * dot3(e2, e2))) {
+        const float id = 1.f / det;
+        float m0[3], x20[3], x01[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) m0[k] = -aw[k];
+        cross3(e2, e0, x20);
+        cross3(e0, e1, x01);
+        const float b0 = dot3(m0, x12) * id, b1 = dot3(m0, x20) * id, b2 = dot3(m0, x01) * id;
+        if (b0 > 1e-5f && b1 > 1e-5f && b2 > 1e-5f && b0 + b1 + b2 < 1.f - 1e-5f) { overlap = true; break; }
       }
     }
+    // new simplex: the newest point + the used retained points (in index order)
+    const int nu = __popc(bm);
+    float T1[3], T1p[3], T2[3], T2p[3];
+    const bool u0 = bm & 1u, u1 = (bm >> 1) & 1u;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      T1[k] = u0 ? S[0][k] : (u1 ? S[1][k] : S[2][k]);
+      T1p[k] = u0 ? SP[0][k] : (u1 ? SP[1][k] : SP[2][k]);
+      T2[k] = (u0 && u1) ? S[1][k] : S[2][k];
+      T2p[k] = (u0 && u1) ? SP[1][k] : SP[2][k];
+    }
+    const float l1 = u0 ? bl[0] : (u1 ? bl[1] : bl[2]);
+    const float l2 = (u0 && u1) ? bl[1] : bl[2];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      S[0][k] = T1[k]; SP[0][k] = T1p[k];
+      S[1][k] = T2[k]; SP[1][k] = T2p[k];
+      v[k] = bv[k];
+    }
+    lam[1] = nu >= 1 ? l1 : 0.f;
+    lam[2] = nu >= 2 ? l2 : 0.f;
+    lam[0] = 1.f - lam[1] - lam[2];
+    n = nu;
   }
-  return hits;
+  // one exit (a struct written on two paths ends up in scratch memory)
+  const float d = sqrtf(dot3(v, v));
+  const bool deep = overlap || d < 1e-6f;
+  float ca[3], cb[3], dv[3];  // core centres (recomputed: not kept live across the iterations)
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    ca[k] = 0.5f * (A.c[0][k] + A.c[1][k]);
+    cb[k] = 0.5f * (B.c[0][k] + B.c[1][k]);
+    dv[k] = ca[k] - cb[k];
+  }
+  const float dn2 = dot3(dv, dv);
+  const bool nodir = dn2 < 1e-24f;
+  const float idn = __builtin_amdgcn_rsqf(fmaxf(dn2, 1e-30f)), id = 1.f / fmaxf(d, 1e-30f);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    // closest point on A's core: the same weights over the A-side support points
+    const float pa = lam[0] * ap[k] + (n >= 1 ? lam[1] * SP[0][k] : 0.f) + (n >= 2 ? lam[2] * SP[1][k] : 0.f);
+    const float nd = nodir ? (k == 2 ? 1.f : 0.f) : dv[k] * idn;
+    out.n[k] = deep ? nd : v[k] * id;
+    out.x[k] = deep ? 0.5f * (ca[k] + cb[k]) : pa - 0.5f * v[k];
+  }
+  out.sep = deep ? -2.f * kCoreM : d - 2.f * kCoreM;
+  return out.sep < margin;
 }
 
 // Detection + selection for the team's env; returns the number of contacts (team-uniform) and
 // `over` (more than NCM candidates: slots go through MAP). Ground: lane s tests link s (the lowest
 // rim point of each circle + 90-degree rotations, the first 4 within the margin). Self: a
-// sphere-union broadphase (centre = midpoint of a link's two spheres, radius r + half their
-// distance: conservative, so it changes which pairs are tested, never which contacts are found),
-// pairs split over the team; candidate pairs are split in rank order into contiguous chunks, one
-// per lane, so candidates stay in canonical order lane by lane. Counting pass, team scan, then
-// each lane writes its candidates at their canonical positions.
+// bounding-sphere broadphase (conservative, so it changes which pairs are tested, never which
+// contacts are found), pairs split over the team; candidate pairs are split in rank order into
+// contiguous chunks, one per lane, so candidates stay in canonical order lane by lane; each
+// candidate pair runs GJK on the core hulls (gjk_pair, one contact per pair). Counting pass, team
+// scan, then each lane writes its candidates at their canonical positions.
 __device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q& q, bool& over, Stamps& sp) {
   const float margin = cfg.contact_margin;
 
@@ -832,14 +1053,37 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q&
     }
   }
   const int cnt_g = __popc(vmask);
+  // ground candidates go first in canonical order: their positions follow from the ground counts
+  // alone, so they are written now (the circle frames are dead before the self-collision pass)
+  const int g_incl = tscan(cnt_g);
+  const int g_tot = tbi<TL - 1>(g_incl);
+  if (cnt_g) {
+    int pos = g_incl - cnt_g;
+    const float code = (float)(16 * l);
+#pragma unroll
+    for (int ci = 0; ci < 2; ++ci)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (vmask & (1u << (4 * ci + r))) {
+          const float c0 = cr0[ci], s0 = sr0[ci];
+          const float cr = r == 0 ? c0 : (r == 1 ? -s0 : (r == 2 ? -c0 : s0));
+          const float sr = r == 0 ? s0 : (r == 1 ? c0 : (r == 2 ? -s0 : -c0));
+          float x[3];
+#pragma unroll
+          for (int a = 0; a < 3; ++a) x[a] = C[ci][a] + cr * E1[ci][a] + sr * E2[ci][a];
+          q.cand(pos, 0) = make_float4(x[0], x[1], x[2], Pz + x[2]);
+          q.cand(pos, 1) = make_float4(0.f, 0.f, 1.f, code);
+          ++pos;
+        }
+  }
   sp.mark(1);
 
   // self: broadphase (lane s: pairs [PAIRS_PER_LANE s, +PAIRS_PER_LANE)), team OR of the bits,
-  // then the candidate pairs' narrow phase (counting pass)
-  unsigned long long cmask = 0ull;
-  unsigned smask = 0u;  // test-pass hits of this lane's chunk (4 bits per pair, chunk <= 4)
-  static_assert((NPAIR + TL - 1) / TL <= 8, "smask holds the chunk");
-  int cnt_s = 0, chunk = 0, first = 0;
+  // then GJK on the candidate pairs of this lane's chunk. Pass 0 counts (early exit on separated
+  // pairs) and keeps the first two hits; after the team scan, pass 1 writes the hits at their
+  // canonical positions, re-running GJK only for a lane's third and later hits (a folded robot
+  // with more than 32 broadphase pairs). One GJK call site for both passes.
+  int s_tot = 0;
   if (cfg.enable_self_collision) {
     wave_sync();  // union spheres
     unsigned long long mask = 0ull;
@@ -859,66 +1103,67 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q&
       mask = (unsigned long long)(unsigned)lo | ((unsigned long long)(unsigned)hi << 32);
     }
     const int K = __popcll(mask);
-    chunk = (K + TL - 1) / TL;
-    first = q.s * chunk;
-    for (int i = first; i > 0 && mask; --i) mask &= mask - 1ull;
-    cmask = mask;  // this lane's chunk starts at the lowest remaining bit
+    const int chunk = (K + TL - 1) / TL;
+    for (int i = q.s * chunk; i > 0 && mask; --i) mask &= mask - 1ull;
+    const unsigned long long cmask = mask;  // this lane's chunk starts at the lowest remaining bit
+    static_assert((NPAIR + TL - 1) / TL <= 32, "smask holds the chunk");
+    unsigned smask = 0u;  // pass-0 hits of this lane's chunk (bit j: pair j of the chunk)
+    SelfContact hit0 = {}, hit1 = {};  // the first two hits are kept for the write pass
+    int cnt_s = 0, hit0_j = -1, hit1_j = -1, pos = 0, end = 0;
+    // cheap separation test on every pair of the chunk; only undecided pairs run GJK
+    unsigned undecided = 0u;
+    mask = cmask;
     for (int j = 0; j < chunk && mask; ++j) {
       const int pidx = __builtin_ctzll(mask);
       mask &= mask - 1ull;
-      const unsigned hm = narrow_pair<false>(q, pidx, margin, 0u, [](const float*, float, const float*, float) {});
-      cnt_s += __popc(hm);
-      smask |= hm << (4 * j);
+      const int pcode = q.pair_code(pidx);
+      Hull A, B;
+      world_hull(q, pcode >> 4, A);
+      world_hull(q, pcode & 15, B);
+      if (!hulls_separated(A, B, margin + 2.f * kCoreM, 3)) undecided |= 1u << j;
+    }
+#pragma unroll 1
+    for (int pass = 0; pass < 2; ++pass) {
+      mask = cmask;
+      for (int j = 0; j < chunk && mask; ++j) {
+        const int pidx = __builtin_ctzll(mask);
+        mask &= mask - 1ull;
+        const bool need = pass == 0 ? ((undecided >> j) & 1u) != 0u : (((smask >> j) & 1u) != 0u && pos < end);
+        if (!need) continue;
+        const int pcode = q.pair_code(pidx);
+        SelfContact sc = j == hit0_j ? hit0 : hit1;
+        if (pass == 0 || (j != hit0_j && j != hit1_j)) {
+          Hull A, B;
+          world_hull(q, pcode >> 4, A);
+          world_hull(q, pcode & 15, B);
+          int its = 0;
+          const bool h = gjk_pair(A, B, pass == 0 ? margin : 1e30f, pass == 0 ? margin : 1e30f, sc, its);
+          sp.count(kStampCount0, 1);
+          sp.count(kStampCount0 + 1, its);
+          if (pass == 0 && h) {
+            if (cnt_s == 0) { hit0 = sc; hit0_j = j; }
+            if (cnt_s == 1) { hit1 = sc; hit1_j = j; }
+            ++cnt_s;
+            smask |= 1u << j;
+          }
+        }
+        if (pass == 1) {
+          q.cand(pos, 0) = make_float4(sc.x[0], sc.x[1], sc.x[2], sc.sep);
+          q.cand(pos, 1) = make_float4(sc.n[0], sc.n[1], sc.n[2], (float)(pcode + 1));
+          ++pos;
+        }
+      }
+      if (pass == 0) {  // canonical positions: after the ground candidates, first NSELF only
+        const int s_incl = tscan(cnt_s);
+        s_tot = tbi<TL - 1>(s_incl);
+        pos = g_tot + s_incl - cnt_s;
+        end = g_tot + NSELF;
+      }
     }
   }
   sp.mark(2);
-
-  // canonical positions (team scans of the packed counts)
-  const int packed = cnt_g | (cnt_s << 8);
-  const int incl = tscan(packed);
-  const int tot = tbi<TL - 1>(incl);
-  const int excl = incl - packed;
-  const int g_tot = tot & 255, s_tot = tot >> 8;
-  const int g_before = excl & 255, s_before = excl >> 8;
   const int n = g_tot + min(s_tot, NSELF);
   over = n > NCM;
-
-  // write pass: ground candidates of link s, then this lane's self candidates (first NSELF)
-  if (cnt_g) {
-    int pos = g_before;
-    const float code = (float)(16 * l);
-#pragma unroll
-    for (int ci = 0; ci < 2; ++ci)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (vmask & (1u << (4 * ci + r))) {
-          const float c0 = cr0[ci], s0 = sr0[ci];
-          const float cr = r == 0 ? c0 : (r == 1 ? -s0 : (r == 2 ? -c0 : s0));
-          const float sr = r == 0 ? s0 : (r == 1 ? c0 : (r == 2 ? -s0 : -c0));
-          float x[3];
-#pragma unroll
-          for (int a = 0; a < 3; ++a) x[a] = C[ci][a] + cr * E1[ci][a] + sr * E2[ci][a];
-          q.cand(pos, 0) = make_float4(x[0], x[1], x[2], Pz + x[2]);
-          q.cand(pos, 1) = make_float4(0.f, 0.f, 1.f, code);
-          ++pos;
-        }
-  }
-  if (cnt_s && s_before < NSELF) {
-    int pos = g_tot + s_before;
-    const int end = g_tot + NSELF;
-    unsigned long long mask = cmask;
-    for (int j = 0; j < chunk && mask; ++j) {
-      const int pidx = __builtin_ctzll(mask);
-      mask &= mask - 1ull;
-      narrow_pair<true>(q, pidx, margin, (smask >> (4 * j)) & 15u, [&](const float* x, float sep, const float* nn, float code) {
-        if (pos < end) {
-          q.cand(pos, 0) = make_float4(x[0], x[1], x[2], sep);
-          q.cand(pos, 1) = make_float4(nn[0], nn[1], nn[2], code);
-        }
-        ++pos;
-      });
-    }
-  }
 
   // overflow (rare): rank every candidate by (sep, canonical index); MAP = kept positions in order
   if (__ballot(over) != 0ull) {
@@ -3930,14 +4175,27 @@ int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_dev
           // C.w = 1: a mated face duplicating a lower link's circle (ground detection skips it)
           t[1 + 3 * ci + v] = make_float4(c[0], c[1], c[2], v == 0 && ((m->link_circle_dup[l] >> ci) & 1) ? 1.f : 0.f);
         }
-      const float* s0 = m->link_sphere[l][0];
-      const float* s1 = m->link_sphere[l][1];
-      t[7] = make_float4(s0[0], s0[1], s0[2], s0[3]);
-      t[8] = make_float4(s1[0], s1[1], s1[2], s1[3]);
-      const double hd = 0.5 * sqrt((double)(s0[0] - s1[0]) * (s0[0] - s1[0]) + (double)(s0[1] - s1[1]) * (s0[1] - s1[1]) +
-                                   (double)(s0[2] - s1[2]) * (s0[2] - s1[2]));
-      t[9] = make_float4(0.5f * (s0[0] + s1[0]), 0.5f * (s0[1] + s1[1]), 0.5f * (s0[2] + s1[2]),
-                         (float)(fmax((double)s0[3], (double)s1[3]) + hd + 1e-6));
+      // self-collision core circles (kCoreM into the shape along each circle's normal, radius
+      // r - kCoreM; the same rule as the oracle's load_mdl): {centre, semi-axis scale}
+      double mid[3], rad = 0.0;
+      for (int a = 0; a < 3; ++a) mid[a] = 0.5 * ((double)m->link_circle[l][0][a] + m->link_circle[l][1][a]);
+      for (int ci = 0; ci < 2; ++ci) {
+        const float* c = m->link_circle[l][ci];
+        const float* o = m->link_circle[l][1 - ci];
+        double n[3] = {(double)c[4] * c[8] - (double)c[5] * c[7], (double)c[5] * c[6] - (double)c[3] * c[8],
+                       (double)c[3] * c[7] - (double)c[4] * c[6]};
+        const double nn = sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+        const double r = sqrt((double)c[3] * c[3] + (double)c[4] * c[4] + (double)c[5] * c[5]);
+        const double to = n[0] * (o[0] - c[0]) + n[1] * (o[1] - c[1]) + n[2] * (o[2] - c[2]);
+        const double sg = to < 0.0 ? -1.0 : 1.0;
+        t[7 + ci] = make_float4((float)(c[0] + sg * kCoreM * n[0] / nn), (float)(c[1] + sg * kCoreM * n[1] / nn),
+                                (float)(c[2] + sg * kCoreM * n[2] / nn), (float)((r - kCoreM) / r));
+        const double dc = sqrt((c[0] - mid[0]) * (c[0] - mid[0]) + (c[1] - mid[1]) * (c[1] - mid[1]) +
+                               (c[2] - mid[2]) * (c[2] - mid[2]));
+        rad = fmax(rad, dc + r);
+      }
+      // bounding sphere of the whole shape (self-collision broadphase)
+      t[9] = make_float4((float)mid[0], (float)mid[1], (float)mid[2], (float)(rad + 1e-6));
     }
     for (int j = 0; j < ND; ++j) {
       float4* t = tab + JT_OFF + j * 5;
