@@ -468,20 +468,56 @@ static int simplex_step(real W[4][3], real PA[4][3], int* n, real lam[4], real v
 }
 
 /* Self-collision contact of one link pair: GJK distance between the two core hulls from the
- * initial direction (centre of A's core circles - centre of B's), stopping when
+ * initial direction best_axis (the largest separating gap of five axes), stopping when
  * (|v|^2 - v.w) / |v| <= 1 um (the distance bounds |v| and v.w / |v| agree; tighter is below fp32 resolution for nearly touching cores), after GJK_MAX_IT iterations, or early (no contact) once the lower
  * bound v.w / |v| exceeds early_margin + 2 CORE_M (early_margin = margin for detection). Contact: normal (pa - pb) / d from B to A,
  * separation d - 2 CORE_M, point (pa + pb) / 2. Cores that overlap (d < 1e-6): normal along the
  * centre difference, separation -2 CORE_M, point = the mean of the centres. Returns 1 on a
  * contact within the margin. */
+/* extent of a hull along unit u: each circle spans c.u +- |(u.E1, u.E2)| */
+static void hull_extent(const hull_t* h, const real u[3], real* lo, real* hi) {
+  for (int ci = 0; ci < 2; ++ci) {
+    const real* c = h->c[ci];
+    real a = v3_dot(u, c + 3), b = v3_dot(u, c + 6);
+    real r = sqrtr(a * a + b * b), m = v3_dot(u, c);
+    if (ci == 0 || m - r < *lo) *lo = m - r;
+    if (ci == 0 || m + r > *hi) *hi = m + r;
+  }
+}
+
+/* GJK's starting direction: of the centre difference and the four circle normals, the axis with
+ * the largest separating gap, oriented from B to A */
+static void best_axis(const hull_t* A, const hull_t* B, real u_out[3]) {
+  real best = -1e30;
+  for (int ax = 0; ax < 5; ++ax) {
+    real u[3];
+    if (ax == 0) {
+      for (int a = 0; a < 3; ++a) u[a] = (real)0.5 * (A->c[0][a] + A->c[1][a]) - (real)0.5 * (B->c[0][a] + B->c[1][a]);
+    } else {
+      const hull_t* H = ax <= 2 ? A : B;
+      v3_cross(H->c[(ax - 1) & 1] + 3, H->c[(ax - 1) & 1] + 6, u);
+    }
+    real nu = sqrtr(v3_dot(u, u));
+    if (nu < (real)1e-15) nu = (real)1e-15;
+    for (int a = 0; a < 3; ++a) u[a] /= nu;
+    real alo, ahi, blo, bhi;
+    hull_extent(A, u, &alo, &ahi);
+    hull_extent(B, u, &blo, &bhi);
+    real gp = alo - bhi, gm = blo - ahi, g = gp > gm ? gp : gm;
+    if (ax == 0 || g > best) {
+      best = g;
+      for (int a = 0; a < 3; ++a) u_out[a] = gp >= gm ? u[a] : -u[a];
+    }
+  }
+}
+
 static int hull_pair(const hull_t* A, const hull_t* B, real margin, real early_margin, contact_t* out) {
   real ca[3], cb[3], v[3];
   for (int a = 0; a < 3; ++a) {
     ca[a] = (real)0.5 * (A->c[0][a] + A->c[1][a]);
     cb[a] = (real)0.5 * (B->c[0][a] + B->c[1][a]);
-    v[a] = ca[a] - cb[a];
   }
-  if (v3_dot(v, v) < (real)1e-18) { v[0] = 1; v[1] = 0; v[2] = 0; }
+  best_axis(A, B, v);
   real W[4][3], PA[4][3], lam[4] = {1, 0, 0, 0};
   int n = 0, overlap = 0; /* n = retained points besides the newest W[0] */
   {

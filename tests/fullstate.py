@@ -7,8 +7,10 @@ margin, the 1 N / 10 N sensor thresholds and the |tau| = effort drive clamp are 
 the step map. Two fp32 implementations with different operation order land on different sides of
 one of them whenever the state sits within rounding distance of it. Such an env is detectable
 without knowing which discontinuity it is: perturbing the oracle's own input by ~1e-6 (the scale of
-the GPU/oracle rounding difference) moves its output by more than the tolerance. An env outside
-tolerance where the oracle is stable under that perturbation is a real mismatch and fails the test.
+the GPU/oracle rounding difference) moves its output by more than the tolerance, or by at least half
+of the GPU's deviation (an env at the tolerance edge). The exact self-collision shape adds one more
+discontinuity, where GJK stops; the sensitivity runs also vary its stopping tolerance. An env outside
+tolerance where the oracle is stable under both is a real mismatch and fails the test.
 """
 from __future__ import annotations
 
