@@ -411,6 +411,21 @@ __device__ __forceinline__ float tb(float x) { return dppf<DPP_BCAST + K>(x); } 
 template <int K>
 __device__ __forceinline__ int tbi(int x) { return dppi<DPP_BCAST + K>(x); }
 
+// position of the r-th (0-based) set bit of m (r < popcount(m)): binary search on popcounts
+__device__ __forceinline__ int nth_set_bit(unsigned long long m, int r) {
+  int pos = 0;
+#pragma unroll
+  for (int w = 32; w >= 1; w >>= 1) {
+    const unsigned long long low = m & ((1ull << w) - 1ull);
+    const int c = __popcll(low);
+    const bool up = r >= c;
+    r -= up ? c : 0;
+    pos += up ? w : 0;
+    m = up ? m >> w : low;
+  }
+  return pos;
+}
+
 // Workgroups of the step / substep kernels are exactly one wave: LDS operations of a wave execute
 // in order, so cross-lane LDS hand-offs need only a compiler-level fence (no s_barrier, and no
 // wait on outstanding global loads/stores, which __syncthreads would add).
@@ -1085,10 +1100,10 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q&
   sp.mark(1);
 
   // self: broadphase (lane s: pairs [PAIRS_PER_LANE s, +PAIRS_PER_LANE)), team OR of the bits,
-  // then GJK on the candidate pairs of this lane's chunk. Pass 0 counts (early exit on separated
-  // pairs) and keeps the first two hits; after the team scan, pass 1 writes the hits at their
-  // canonical positions, re-running GJK only for a lane's third and later hits (a folded robot
-  // with more than 32 broadphase pairs). One GJK call site for both passes.
+  // then the separating-axis test and GJK on the undecided pairs, dealt round-robin by rank over
+  // the team. Pass 0 finds the contacts (and keeps each lane's first); the team OR of the contact
+  // bits by rank gives every contact its canonical position (popcount of the lower ranks); pass 1
+  // writes them, re-running GJK only for a lane's second and later contacts. One GJK call site.
   int s_tot = 0;
   if (cfg.enable_self_collision) {
     wave_sync();  // union spheres
@@ -1109,43 +1124,42 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q&
       mask = (unsigned long long)(unsigned)lo | ((unsigned long long)(unsigned)hi << 32);
     }
     const int K = __popcll(mask);
-    const int chunk = (K + TL - 1) / TL;
+    const int rounds = (K + TL - 1) / TL;
 #ifdef ZB_STAMP_DETECT
     sp.mark(10);  // diagnostic split of the self-collision phase: broadphase
 #endif
-    for (int i = q.s * chunk; i > 0 && mask; --i) mask &= mask - 1ull;
-    const unsigned long long cmask = mask;  // this lane's chunk starts at the lowest remaining bit
-    static_assert((NPAIR + TL - 1) / TL <= 32, "smask holds the chunk");
-    unsigned smask = 0u;  // pass-0 hits of this lane's chunk (bit j: pair j of the chunk)
-    SelfContact hit0 = {}, hit1 = {};  // the first two hits are kept for the write pass
-    int cnt_s = 0, hit0_j = -1, hit1_j = -1, pos = 0, end = 0;
-    // cheap separation test on every pair of the chunk; only undecided pairs run GJK
-    unsigned undecided = 0u;
-    mask = cmask;
-    for (int j = 0; j < chunk && mask; ++j) {
-      const int pidx = __builtin_ctzll(mask);
-      mask &= mask - 1ull;
-      const int pcode = q.pair_code(pidx);
+    // pair of rank r (r-th broadphase pair in index order) goes to lane r % TL: neighbouring pairs
+    // of a folded robot, which tend to be in contact together, land on different lanes
+    const unsigned long long bmask = mask;
+    unsigned undecided = 0u;  // bit k: this lane's pair of round k needs GJK
+    for (int k = 0; k < rounds; ++k) {
+      const int r = q.s + TL * k;
+      if (r >= K) break;
+      const int pcode = q.pair_code(nth_set_bit(bmask, r));
       Hull A, B;
       world_hull(q, pcode >> 4, A);
       world_hull(q, pcode & 15, B);
       float u[3];
-      if (!hulls_separated(A, B, margin + 2.f * kCoreM, u)) undecided |= 1u << j;
+      if (!hulls_separated(A, B, margin + 2.f * kCoreM, u)) undecided |= 1u << k;
     }
 #ifdef ZB_STAMP_DETECT
-    sp.mark(11);  // chunk skip + separating-axis tests
+    sp.mark(11);  // separating-axis tests
 #endif
+    SelfContact hit0 = {};  // this lane's first hit is kept for the write pass
+    int hit0_k = -1;
+    unsigned own = 0u;                // bit k: this lane's pair of round k is a contact
+    unsigned long long allhits = 0ull;  // team: bit r = the pair of rank r is a contact
 #pragma unroll 1
     for (int pass = 0; pass < 2; ++pass) {
-      mask = cmask;
-      for (int j = 0; j < chunk && mask; ++j) {
-        const int pidx = __builtin_ctzll(mask);
-        mask &= mask - 1ull;
-        const bool need = pass == 0 ? ((undecided >> j) & 1u) != 0u : (((smask >> j) & 1u) != 0u && pos < end);
+      for (int k = 0; k < rounds; ++k) {
+        const int r = q.s + TL * k;
+        if (r >= K) break;
+        const int pos = g_tot + __popcll(allhits & ((1ull << r) - 1ull));
+        const bool need = pass == 0 ? ((undecided >> k) & 1u) != 0u : (((own >> k) & 1u) != 0u && pos < g_tot + NSELF);
         if (!need) continue;
-        const int pcode = q.pair_code(pidx);
-        SelfContact sc = j == hit0_j ? hit0 : hit1;
-        if (pass == 0 || (j != hit0_j && j != hit1_j)) {
+        const int pcode = q.pair_code(nth_set_bit(bmask, r));
+        SelfContact sc = hit0;
+        if (pass == 0 || k != hit0_k) {
           Hull A, B;
           world_hull(q, pcode >> 4, A);
           world_hull(q, pcode & 15, B);
@@ -1156,23 +1170,22 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q&
           sp.count(kStampCount0, 1);
           sp.count(kStampCount0 + 1, its);
           if (pass == 0 && h) {
-            if (cnt_s == 0) { hit0 = sc; hit0_j = j; }
-            if (cnt_s == 1) { hit1 = sc; hit1_j = j; }
-            ++cnt_s;
-            smask |= 1u << j;
+            if (own == 0u) { hit0 = sc; hit0_k = k; }
+            own |= 1u << k;
           }
         }
         if (pass == 1) {
           q.cand(pos, 0) = make_float4(sc.x[0], sc.x[1], sc.x[2], sc.sep);
           q.cand(pos, 1) = make_float4(sc.n[0], sc.n[1], sc.n[2], (float)(pcode + 1));
-          ++pos;
         }
       }
-      if (pass == 0) {  // canonical positions: after the ground candidates, first NSELF only
-        const int s_incl = tscan(cnt_s);
-        s_tot = tbi<TL - 1>(s_incl);
-        pos = g_tot + s_incl - cnt_s;
-        end = g_tot + NSELF;
+      if (pass == 0) {  // the team's contacts by rank: canonical positions follow the ground ones
+        unsigned long long mine = 0ull;
+        for (int k = 0; k < rounds; ++k)
+          if ((own >> k) & 1u) mine |= 1ull << (q.s + TL * k);
+        const int lo = tor((int)(unsigned)mine), hi = tor((int)(unsigned)(mine >> 32));
+        allhits = (unsigned long long)(unsigned)lo | ((unsigned long long)(unsigned)hi << 32);
+        s_tot = __popcll(allhits);
       }
     }
   }
