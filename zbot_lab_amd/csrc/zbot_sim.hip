@@ -184,6 +184,26 @@ struct Phys {
   float pos[3], quat[4], lv[3], av[3], jq[ND], jqd[ND];
 };
 
+// Non-finite guard: true when any physics state value is inf / NaN (an exponent test on the bits:
+// -ffast-math folds isfinite away). The step kernels end such an env's episode as `died` with a
+// finite reward and reset it, instead of letting NaN persist in its state (a safety net outside
+// the reference's semantics: finite states never take it).
+__device__ __forceinline__ bool phys_bad(const Phys& p) {
+  unsigned bad = 0u;
+  auto chk = [&bad](float x) {
+    // through an empty asm: under -ffast-math the compiler may assume x finite and fold the test
+    unsigned u = __float_as_uint(x);
+    asm volatile("" : "+v"(u));
+    bad |= ((u >> 23) & 0xffu) == 0xffu ? 1u : 0u;
+  };
+#pragma unroll
+  for (int a = 0; a < 3; ++a) { chk(p.pos[a]); chk(p.lv[a]); chk(p.av[a]); }
+#pragma unroll
+  for (int a = 0; a < 4; ++a) chk(p.quat[a]);
+#pragma unroll
+  for (int j = 0; j < ND; ++j) { chk(p.jq[j]); chk(p.jqd[j]); }
+  return bad != 0u;
+}
 struct Kin {
   float q[NB][4], R[NB][9], p[NB][3];  // p relative to P = root origin
   float ax[ND][3], org[ND][3];
@@ -2381,6 +2401,8 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_step_kernel(const z
   bool died = fm_max > 1.0f;
   died |= pre_base_z < cfg.termination_height;
   died |= fabsf(pre_base_y) > 0.5f;  // base_pos_y_err vs env origin (local frame: 0)
+  const bool blowup = phys_bad(p);     // non-finite guard (phys_bad)
+  died |= blowup;
 
   // _get_rewards (v2.py:371-382) in dict order
   float r[ZB_NUM_REWARD_TERMS];
@@ -2427,6 +2449,13 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_step_kernel(const z
     sums[t] = sums0[t] + v;
   }
   if (died) reward -= cfg.terminal_penalty;  // v2.py:379-380
+  if (blowup) {  // finite reward, the episode sums without this step, no carried non-finite latch
+    reward = -cfg.terminal_penalty;
+#pragma unroll
+    for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) sums[t] = sums0[t];
+#pragma unroll
+    for (int f = 0; f < 2; ++f) { step_len[f] = 0.f; feetF[f] = 0.f; }
+  }
 
   // in-kernel auto-reset (v2.py:413-459): the episode log, then the default state; step_len and
   // f_last are not reset (reference); feet_down_pos_last = the pre-reset (post-step) feet positions
@@ -2449,7 +2478,7 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_step_kernel(const z
 #pragma unroll
     for (int j = 0; j < ND; ++j) { p.jq[j] = m->default_joint_pos[j]; p.jqd[j] = 0.f; }
     const float4 d0 = q.dflt()[0], d1 = q.dflt()[1], dq = q.dflt()[2];
-    if (cfg.reset_feet_refresh) {
+    if (cfg.reset_feet_refresh || blowup) {
       down[0][0] = d0.x; down[0][1] = d0.y; down[0][2] = d0.z;
       down[1][0] = d1.x; down[1][1] = d1.y; down[1][2] = d1.z;
     } else {
@@ -2799,7 +2828,8 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_su_step_kernel(
 
   // _get_dones (standup.py:634-643)
   const bool time_out = ep_len >= (float)(cfg.max_episode_length - 1);
-  const bool died = (czl0 - z6) > cfg.center_z_drop;
+  const bool blowup = phys_bad(p);  // non-finite guard (phys_bad)
+  const bool died = (czl0 - z6) > cfg.center_z_drop || blowup;
   const float czl = ((int)ep_len % cfg.center_z_period == cfg.center_z_period - 1) ? z6 : czl0;
 
   // _get_rewards (standup.py:620-632): reward_func() * scale * step_dt per term, dict order
@@ -2833,6 +2863,11 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_su_step_kernel(
     sums[t] = sums0[t] + v;
   }
   if (died) reward -= cfg.terminal_penalty;  // 629-630
+  if (blowup) {
+    reward = -cfg.terminal_penalty;
+#pragma unroll
+    for (int t = 0; t < ZB_SU_NUM_REWARD_TERMS; ++t) sums[t] = sums0[t];
+  }
   const bool reset = died || time_out;
 
   // _reset_idx (645-703): episode log (sums per second of the env's own episode), new random
