@@ -7,6 +7,8 @@ export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $O/test_gpu.log 2>&1
 rc=$?; tail -1 $O/test_gpu.log
 if [ $rc -ne 0 ]; then grep -E "FAILED" $O/test_gpu.log | head -20; exit $rc; fi
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { tail -5 $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
 bash scripts/gpu_perf.sh $TAG || exit 1
 for args in "--envs-per-gpu 8192" "--envs-per-gpu 65536" "--task standup" "--task v4" "--task manager"; do
   timeout -k 10 300 python bench.py --no-cpu-baseline $args > $O/bench_extra.log 2>&1 || { tail -5 $O/bench_extra.log; exit 1; }
