@@ -371,6 +371,8 @@ int zb_profile_end(zb_handle h, float* total_ms, int* count);
  * zb_step_kernel over all waves since the previous call (phases: DESIGN.md §7). Returns <0 in
  * the product build. */
 int zb_read_stamps(uint64_t* out16);
+/* diagnostic build only: the phase cycles of the slowest wave (same order as zb_read_stamps) */
+int zb_read_stamps_slowest(uint64_t* out16);
 
 #ifdef __cplusplus
 }

@@ -27,3 +27,7 @@ print(f"self collision: {calls / waves / steps / 4:.1f} GJK calls per wave per s
 print(f"cycles per wave per step: {tot / waves / steps:.0f}")
 for k in range(len(names)):
     print(f"  {names[k]:32s} {buf[k] / waves / steps:10.0f}  {100 * buf[k] / tot:5.1f} %")
+slow = (C.c_uint64 * 16)(); nat.lib().zb_read_stamps_slowest(slow)
+print("slowest wave of one launch, by phase:")
+for k in range(len(names)):
+    print(f"  {names[k]:32s} {slow[k]:10.0f}")

@@ -66,6 +66,7 @@ constexpr int NSTAMP = 16;
 constexpr int kStampCount0 = 13;  // slots 13, 14 count events (GJK calls, iterations); 15 = max wave cycles
 #ifdef ZB_STAMPS
 __device__ unsigned long long g_stamps[NSTAMP];
+__device__ unsigned long long g_stamp_slowest[NSTAMP];  // phase cycles of the slowest wave seen
 struct Stamps {
   unsigned long long t, acc[NSTAMP];
   __device__ void begin() {
@@ -87,7 +88,9 @@ struct Stamps {
     if ((threadIdx.x & 63) == 0) {  // slot NSTAMP - 1: the slowest wave's cycles over the launches
       unsigned long long tot = 0;
       for (int k = 0; k < kStampCount0; ++k) tot += acc[k];
-      atomicMax(&g_stamps[NSTAMP - 1], tot);
+      const unsigned long long old = atomicMax(&g_stamps[NSTAMP - 1], tot);
+      if (tot > old)  // its phase breakdown (racy between near-equal waves: a diagnostic)
+        for (int k = 0; k < kStampCount0; ++k) g_stamp_slowest[k] = acc[k];
     }
   }
 };
@@ -805,6 +808,21 @@ __device__ __forceinline__ void world_hull(const Q& q, int l, Hull& h) {
 }
 // support point of the hull of the two circles along d (a circle's rim point along d's in-plane
 // part; its centre when d is normal to the disk)
+// h = the Hull held by the lane at byte address addr (= 4 x lane index), via ds_bpermute; every
+// lane of the wave must execute it
+__device__ __forceinline__ float bperm(int addr, float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(addr, __builtin_bit_cast(int, v)));
+}
+__device__ __forceinline__ void gather_hull(const Hull& own, int addr, Hull& h) {
+#pragma unroll
+  for (int ci = 0; ci < 2; ++ci)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      h.c[ci][k] = bperm(addr, own.c[ci][k]);
+      h.e1[ci][k] = bperm(addr, own.e1[ci][k]);
+      h.e2[ci][k] = bperm(addr, own.e2[ci][k]);
+    }
+}
 __device__ __forceinline__ void hull_sup(const Hull& h, const float d[3], float o[3]) {
   float best = 0.f;
 #pragma unroll
@@ -1152,30 +1170,54 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q&
     // of a folded robot, which tend to be in contact together, land on different lanes
     const unsigned long long bmask = mask;
     unsigned undecided = 0u;  // bit k: this lane's pair of round k needs GJK
-    for (int k = 0; k < rounds; ++k) {
-      const int r = q.s + TL * k;
-      if (r >= K) break;
-      const int pcode = q.pair_code(nth_set_bit(bmask, r));
-      Hull A, B;
-      world_hull(q, pcode >> 4, A);
-      world_hull(q, pcode & 15, B);
-      float u[3];
-      if (!hulls_separated(A, B, margin + 2.f * kCoreM, u)) undecided |= 1u << k;
+    {
+      // lane l builds link l's world hull once; the pair tests gather both hulls from the link
+      // lanes with ds_bpermute (no per-pair frame reads, link-table loads or rotations). The
+      // loop runs the wave's largest round count so every lane takes part in each permute.
+      Hull own;
+      world_hull(q, q.s < NL ? q.s : NL - 1, own);
+      const int rounds_w = max(max(__builtin_amdgcn_readlane(rounds, 0), __builtin_amdgcn_readlane(rounds, TL)),
+                               max(__builtin_amdgcn_readlane(rounds, 2 * TL), __builtin_amdgcn_readlane(rounds, 3 * TL)));
+      const int base = q.lane & ~(TL - 1);
+      for (int k = 0; k < rounds_w; ++k) {
+        const int r = q.s + TL * k;
+        const bool valid = r < K;
+        const int pcode = valid ? q.pair_code(nth_set_bit(bmask, r)) : 0x01;
+        Hull A, B;
+        gather_hull(own, 4 * (base + (pcode >> 4)), A);
+        gather_hull(own, 4 * (base + (pcode & 15)), B);
+        float u[3];
+        if (valid && !hulls_separated(A, B, margin + 2.f * kCoreM, u)) undecided |= 1u << k;
+      }
     }
 #ifdef ZB_STAMP_DETECT
     sp.mark(11);  // separating-axis tests
 #endif
-    SelfContact hit0 = {};  // this lane's first hit is kept for the write pass
+    // the undecided pairs of the whole team, dealt again round-robin (GJK work spread evenly: a
+    // lane runs ceil(U / 16) GJKs, usually one, where the lane of a folded robot's neighbouring
+    // pairs could queue several)
+    unsigned long long und = 0ull;  // team: bit r = the pair of rank r needs GJK
+    {
+      unsigned long long mine = 0ull;
+      for (int k = 0; k < rounds; ++k)
+        if ((undecided >> k) & 1u) mine |= 1ull << (q.s + TL * k);
+      const int lo = tor((int)(unsigned)mine), hi = tor((int)(unsigned)(mine >> 32));
+      und = (unsigned long long)(unsigned)lo | ((unsigned long long)(unsigned)hi << 32);
+    }
+    const int U = __popcll(und);
+    const int urounds = (U + TL - 1) / TL;
+    SelfContact hit0 = {};  // this lane's first contact is kept for the write pass
     int hit0_k = -1;
-    unsigned own = 0u;                // bit k: this lane's pair of round k is a contact
+    unsigned own = 0u;                // bit k: this lane's GJK pair of round k is a contact
     unsigned long long allhits = 0ull;  // team: bit r = the pair of rank r is a contact
 #pragma unroll 1
     for (int pass = 0; pass < 2; ++pass) {
-      for (int k = 0; k < rounds; ++k) {
-        const int r = q.s + TL * k;
-        if (r >= K) break;
+      for (int k = 0; k < urounds; ++k) {
+        const int u = q.s + TL * k;
+        if (u >= U) break;
+        const int r = nth_set_bit(und, u);
         const int pos = g_tot + __popcll(allhits & ((1ull << r) - 1ull));
-        const bool need = pass == 0 ? ((undecided >> k) & 1u) != 0u : (((own >> k) & 1u) != 0u && pos < g_tot + NSELF);
+        const bool need = pass == 0 || (((own >> k) & 1u) != 0u && pos < g_tot + NSELF);
         if (!need) continue;
         const int pcode = q.pair_code(nth_set_bit(bmask, r));
         SelfContact sc = hit0;
@@ -1201,8 +1243,10 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q&
       }
       if (pass == 0) {  // the team's contacts by rank: canonical positions follow the ground ones
         unsigned long long mine = 0ull;
-        for (int k = 0; k < rounds; ++k)
-          if ((own >> k) & 1u) mine |= 1ull << (q.s + TL * k);
+        for (int k = 0; k < urounds; ++k) {
+          const int u = q.s + TL * k;
+          if (u < U && ((own >> k) & 1u)) mine |= 1ull << nth_set_bit(und, u);
+        }
         const int lo = tor((int)(unsigned)mine), hi = tor((int)(unsigned)(mine >> 32));
         allhits = (unsigned long long)(unsigned)lo | ((unsigned long long)(unsigned)hi << 32);
         s_tot = __popcll(allhits);
@@ -4366,6 +4410,19 @@ int zb_profile_end(zb_handle h, float* total_ms, int* count) {
   *count = h->prof_n;
   prof_free(h);
   return 0;
+}
+
+// Diagnostic build only (-DZB_STAMPS): the phase cycles of the slowest wave since the last reset.
+int zb_read_stamps_slowest(uint64_t* out16) {
+#ifdef ZB_STAMPS
+  unsigned long long tmp[NSTAMP];
+  HIPCHK(hipMemcpyFromSymbol(tmp, HIP_SYMBOL(g_stamp_slowest), sizeof(tmp)), "hipMemcpyFromSymbol");
+  for (int k = 0; k < 16; ++k) out16[k] = k < NSTAMP ? tmp[k] : 0;
+  return 0;
+#else
+  (void)out16;
+  return set_err(-1, "zb_read_stamps_slowest: library built without -DZB_STAMPS", hipSuccess);
+#endif
 }
 
 // Diagnostic build only (-DZB_STAMPS): per-phase cycle sums over all waves since the last call.
