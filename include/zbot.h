@@ -211,7 +211,8 @@ typedef struct zb_model {
   float link_com[ZB_NUM_LINKS][3];        /* authored link COM, body frame */
   /* collision shape = convex hull of two circles: centre C, semi-axes E1, E2 (body frame) */
   float link_circle[ZB_NUM_LINKS][2][9];
-  float link_sphere[ZB_NUM_LINKS][2][4];  /* self-collision spheres: centre (body frame), radius */
+  float link_sphere[ZB_NUM_LINKS][2][4];  /* round-1 inscribed spheres (unused since self collision
+                                          * runs GJK on the link hull; kept for the ABI layout) */
   float link_bound[ZB_NUM_LINKS][4];      /* bounding sphere of the shape: centre (body), radius */
   int32_t num_self_pairs;
   int32_t self_pairs[ZB_MAX_SELF_PAIRS][2];

@@ -105,7 +105,7 @@ typedef struct {
   real jp_pos[ND][3], jp_rot[ND][4], jc_pos[ND][3], jc_rot[ND][4];
   int link_body[NL];
   real link_pos[NL][3], link_rot[NL][4], link_com[NL][3];
-  real circle[NL][2][9], sphere[NL][2][4], bound[NL][4];
+  real circle[NL][2][9], bound[NL][4];
   real core[NL][2][9];                /* core circles of the self-collision shape (body frame) */
   int circle_dup[NL];                 /* bit ci: duplicate of a lower link's mated face (skipped) */
   int npairs, pairs[ZB_MAX_SELF_PAIRS][2];
@@ -135,7 +135,6 @@ static void load_mdl(const zb_model* m, mdl_t* o) {
     for (int a = 0; a < 4; ++a) { o->link_rot[l][a] = m->link_rot[l][a]; o->bound[l][a] = m->link_bound[l][a]; }
     for (int c = 0; c < 2; ++c) {
       for (int a = 0; a < 9; ++a) o->circle[l][c][a] = m->link_circle[l][c][a];
-      for (int a = 0; a < 4; ++a) o->sphere[l][c][a] = m->link_sphere[l][c][a];
     }
   }
   for (int l = 0; l < NL; ++l)

@@ -4,7 +4,7 @@ The robot is ``ZBOT_6S_CFG`` (reference ``source/zbot/zbot/assets/zbot_cfg.py:62
 ``zbot_6s_new.usd``; the decoded asset lives in ``assets/zbot6s_model.json`` (written by
 ``tools/extract_model.py``). Here the 12 links / 6 revolute + 5 fixed joints are merged into the 7
 rigid composites the simulator integrates (fixed joints have no DoF), and every per-link quantity
-(link frame, authored COM, collision circles, self-collision spheres) is expressed in its
+(link frame, authored COM, collision circles, round-1 self-collision spheres) is expressed in its
 composite's frame. PhysX uses the authored mass properties verbatim, so do we.
 """
 from __future__ import annotations
