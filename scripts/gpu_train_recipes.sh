@@ -20,9 +20,9 @@ if [ -z "${SKIP_STANDUP:-}" ]; then
   run standup_play 300 scripts/play.py --task zbot-6b-standup-v0 --num_envs 1024 --log_root $LR --num_steps 290 --fresh_episodes $X
 fi
 if [ -z "${SKIP_V2:-}" ]; then
-  run v2_step2 1500 scripts/train.py --task zbot-6b-walking-v2 --num_envs 4096 --max_iterations $IT --log_root $LR --log-every 50 --reward_cfg step2 --run_name step2 $X
-  run v2_step3 1500 scripts/train.py --task zbot-6b-walking-v2 --num_envs 4096 --max_iterations $IT --log_root $LR --log-every 50 --reward_cfg step3 --run_name step3 --resume --load_run '.*_step2' $X
-  run v2_step4 1500 scripts/train.py --task zbot-6b-walking-v2 --num_envs 4096 --max_iterations $IT --log_root $LR --log-every 50 --reward_cfg step4 --run_name step4 --resume --load_run '.*_step3' $X
+  run v2_step2 1500 scripts/train.py --task zbot-6b-walking-v2 --num_envs ${NUM_ENVS:-4096} --max_iterations $IT --log_root $LR --log-every 50 --reward_cfg step2 --run_name step2 $X
+  run v2_step3 1500 scripts/train.py --task zbot-6b-walking-v2 --num_envs ${NUM_ENVS:-4096} --max_iterations $IT --log_root $LR --log-every 50 --reward_cfg step3 --run_name step3 --resume --load_run '.*_step2' $X
+  run v2_step4 1500 scripts/train.py --task zbot-6b-walking-v2 --num_envs ${NUM_ENVS:-4096} --max_iterations $IT --log_root $LR --log-every 50 --reward_cfg step4 --run_name step4 --resume --load_run '.*_step3' $X
   run v2_play 300 scripts/play.py --task zbot-6b-walking-v2 --num_envs 1024 --log_root $LR --num_steps 999 --fresh_episodes $X
 fi
 for f in $(find $LR -name train_log.jsonl); do cp $f gpurun_out/train/$(basename $(dirname $f)).jsonl; done
