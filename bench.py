@@ -176,8 +176,48 @@ def cpu_baseline(num_envs: int, seconds: float, task: str = "walking") -> dict:
                       f"{best} threads), random actions, {dt:.1f} s"}
 
 
+def launch_plan(gpus: int, environ, argv: list[str], port: int | None = None) -> list[str] | None:
+    """How ``bench.py --gpus N`` runs (reference multi-GPU entry: ``train.py:125-132``, one process
+    per GPU). Returns None when this process is the worker (N = 1 without a launcher, or a rank
+    started by torch.distributed.run whose WORLD_SIZE equals N), or the child command line that a
+    plain ``python bench.py --gpus N`` (N > 1, no WORLD_SIZE) spawns: torch.distributed.run with N
+    local ranks on 127.0.0.1. Raises ValueError when --gpus and WORLD_SIZE disagree (a SCALE run
+    must never time fewer GPUs than it reports)."""
+    if gpus < 1:
+        raise ValueError(f"--gpus must be >= 1, got {gpus}")
+    ws = environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != gpus:
+            raise ValueError(f"--gpus {gpus} but WORLD_SIZE={ws}: launch one rank per GPU")
+        return None
+    if gpus == 1:
+        return None
+    if port is None:
+        import socket
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+def run_launcher(cmd: list[str]) -> int:
+    """Parent of an N-GPU run: it never touches the GPU and never execs (the box forbids replacing
+    a process); the ranks' output passes through (rank 0 prints the JSON line) and the parent exits
+    with the launcher's code."""
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     args = parse()
+    cmd = launch_plan(args.gpus, os.environ, sys.argv[1:])
+    if cmd is not None:
+        sys.exit(run_launcher(cmd))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -230,9 +270,16 @@ def main():
     kern_ms, kern_n = env.sim.profile_end()
 
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    per_rank = torch.tensor([n * args.steps / elapsed], dtype=torch.float64, device=dev)
+    rccl_world = 1
     if dist is not None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        gathered = [torch.zeros_like(per_rank) for _ in range(world)]
+        dist.all_gather(gathered, per_rank)
+        per_rank = torch.cat(gathered)
+        rccl_world = dist.get_world_size()
     elapsed = float(t.item())
+    per_rank_rates = [float(v) for v in per_rank.tolist()]
     total_steps = n * world * args.steps
     value = total_steps / elapsed
 
@@ -265,7 +312,8 @@ def main():
             "data": "synthetic: default-pose starts, full reset, randn(N,6) actions seeded 42+rank",
             "config": {"workload": workload,
                        "envs_per_gpu": n, "total_envs": n * world, "decimation": 4, "sim_dt": 0.005,
-                       "parallelism": f"env-sharded x{world} (replicas, no collective)"},
+                       "parallelism": f"env-sharded x{world} (replicas, no collective)",
+                       "rccl_world_size": rccl_world, "per_rank_env_steps_per_s": per_rank_rates},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": kname, "kernel_ms": kern_s * 1e3,

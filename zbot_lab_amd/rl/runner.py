@@ -93,7 +93,11 @@ class OnPolicyRunner:
         # PPO.update_steps releases its autograd graph so the capture sees fresh AccumulateGrad
         # nodes on the capture stream (a live one from the eager update pinned the default stream
         # and broke the capture)
-        self.graph_update = self.use_graph if graph_update is None else graph_update
+        # Multi-GPU: the update's gradient all-reduce (RCCL) would be captured into the graph; no
+        # multi-GPU run has shown a captured all-reduce to match the eager update yet, so the update
+        # stays eager there unless a caller asks for the graph explicitly (the rollout graph has no
+        # collective and is unaffected)
+        self.graph_update = (self.use_graph and not self.is_distributed) if graph_update is None else graph_update
 
     def _configure_multi_gpu(self) -> None:
         world = int(os.environ.get("WORLD_SIZE", "1"))
