@@ -370,6 +370,11 @@ static void select_contacts(clist_t* L) {
  * World-frame core circles of link l: centre, two semi-axes (radius baked in). */
 typedef struct { real c[2][9]; } hull_t;
 static double g_gjk_tol = GJK_TOL;
+static _Thread_local int g_gjk_last_it; /* probe: support iterations of this thread's last hull_pair */
+static int g_gjk_warm = 1;               /* warm start within a step (test hook: 0 = always cold) */
+static int g_gjk_probe = 0;              /* probe: histogram of the GJK calls the kernel would make */
+static long long g_gjk_hist[GJK_MAX_IT + 2];
+static long long g_gjk_uhist[64];        /* probe: undecided pairs per env-substep */
 
 static void world_hull(const mdl_t* m, const kin_t* k, int l, hull_t* h) {
   int b = m->link_body[l];
@@ -510,13 +515,15 @@ static void best_axis(const hull_t* A, const hull_t* B, real u_out[3]) {
   }
 }
 
-static int hull_pair(const hull_t* A, const hull_t* B, real margin, real early_margin, contact_t* out) {
+static int hull_pair(const hull_t* A, const hull_t* B, real margin, real early_margin, const real* v0,
+                     contact_t* out) {
   real ca[3], cb[3], v[3];
   for (int a = 0; a < 3; ++a) {
     ca[a] = (real)0.5 * (A->c[0][a] + A->c[1][a]);
     cb[a] = (real)0.5 * (B->c[0][a] + B->c[1][a]);
   }
-  best_axis(A, B, v);
+  if (v0) { v[0] = v0[0]; v[1] = v0[1]; v[2] = v0[2]; }
+  else best_axis(A, B, v);
   real W[4][3], PA[4][3], lam[4] = {1, 0, 0, 0};
   int n = 0, overlap = 0; /* n = retained points besides the newest W[0] */
   {
@@ -525,7 +532,9 @@ static int hull_pair(const hull_t* A, const hull_t* B, real margin, real early_m
     hull_support(B, v, pb);
     for (int a = 0; a < 3; ++a) { PA[0][a] = pa[a]; W[0][a] = pa[a] - pb[a]; v[a] = W[0][a]; }
   }
+  g_gjk_last_it = 0;
   for (int it = 0; it < GJK_MAX_IT; ++it) {
+    g_gjk_last_it = it + 1;
     real vv = v3_dot(v, v);
     if (vv < (real)1e-12) { overlap = 1; break; }
     real nd[3] = {-v[0], -v[1], -v[2]}, pa[3], pb[3], w[3];
@@ -571,6 +580,68 @@ int zbo_set_gjk_tol(double tol) {
   return 0;
 }
 
+/* largest separating-axis gap of best_axis's five axes (the kernel's hulls_separated test) */
+static real sat_gap(const hull_t* A, const hull_t* B) {
+  real best = -1e30;
+  for (int ax = 0; ax < 5; ++ax) {
+    real u[3];
+    if (ax == 0) {
+      for (int a = 0; a < 3; ++a) u[a] = (real)0.5 * (A->c[0][a] + A->c[1][a]) - (real)0.5 * (B->c[0][a] + B->c[1][a]);
+    } else {
+      const hull_t* H = ax <= 2 ? A : B;
+      v3_cross(H->c[(ax - 1) & 1] + 3, H->c[(ax - 1) & 1] + 6, u);
+    }
+    real nu = sqrtr(v3_dot(u, u));
+    if (nu < (real)1e-15) nu = (real)1e-15;
+    for (int a = 0; a < 3; ++a) u[a] /= nu;
+    real alo, ahi, blo, bhi;
+    hull_extent(A, u, &alo, &ahi);
+    hull_extent(B, u, &blo, &bhi);
+    real gp = alo - bhi, gm = blo - ahi, g = gp > gm ? gp : gm;
+    if (g > best) best = g;
+  }
+  return best;
+}
+
+/* GJK probe (test / tooling hook): the link pairs of every env that the kernel's separating-axis
+ * test leaves to GJK (largest gap <= margin + 2 CORE_M), written as {env, pair, A[2][9], B[2][9]}
+ * (38 floats each, at most max); returns the number of such pairs. */
+int zbo_undecided_pairs(zbo_sim* s, float* out, int max) {
+  int cnt = 0;
+  const real lim = s->c.contact_margin + 2 * (real)CORE_M;
+  for (int e = 0; e < s->n; ++e) {
+    kin_t k;
+    fk(&s->m, &s->env[e].ph, &k);
+    for (int p = 0; p < s->m.npairs; ++p) {
+      hull_t A, B;
+      world_hull(&s->m, &k, s->m.pairs[p][0], &A);
+      world_hull(&s->m, &k, s->m.pairs[p][1], &B);
+      if (sat_gap(&A, &B) > lim) continue;
+      if (cnt < max) {
+        float* o = out + 38 * cnt;
+        o[0] = (float)e; o[1] = (float)p;
+        for (int ci = 0; ci < 2; ++ci)
+          for (int q = 0; q < 9; ++q) { o[2 + 9 * ci + q] = (float)A.c[ci][q]; o[20 + 9 * ci + q] = (float)B.c[ci][q]; }
+      }
+      ++cnt;
+    }
+  }
+  return cnt;
+}
+
+/* GJK probe / warm-start switches (tooling hooks): warm = 0 runs every GJK cold from the best
+ * separating axis; probe = 1 histograms the support iterations of the GJK calls the kernel would
+ * make (pairs the separating-axis test leaves undecided). hist: GJK_MAX_IT + 2 counters. */
+int zbo_gjk_hooks(int warm, int probe, long long* hist) {
+  if (warm >= 0) g_gjk_warm = warm;
+  if (probe >= 0) g_gjk_probe = probe;
+  if (hist) {
+    for (int i = 0; i < GJK_MAX_IT + 2; ++i) { hist[i] = g_gjk_hist[i]; g_gjk_hist[i] = 0; }
+    for (int i = 0; i < 64; ++i) { hist[GJK_MAX_IT + 2 + i] = g_gjk_uhist[i]; g_gjk_uhist[i] = 0; }
+  }
+  return 0;
+}
+
 /* test entry point: hull_pair on two world-frame core hulls given as [2][9] floats (centre, two
  * semi-axes per circle); out = {contact, sep, n[3], x[3]} (tests/test_oracle_selfcollision.py) */
 int zbo_hull_pair(const float* a, const float* b, float margin, float* out) {
@@ -579,11 +650,11 @@ int zbo_hull_pair(const float* a, const float* b, float margin, float* out) {
     for (int q = 0; q < 9; ++q) { A.c[ci][q] = a[9 * ci + q]; B.c[ci][q] = b[9 * ci + q]; }
   contact_t c;
   memset(&c, 0, sizeof(c));
-  int hit = hull_pair(&A, &B, (real)margin, (real)margin, &c);
+  int hit = hull_pair(&A, &B, (real)margin, (real)margin, NULL, &c);
   out[0] = (float)hit;
   out[1] = (float)c.sep;
   for (int q = 0; q < 3; ++q) { out[2 + q] = (float)c.n[q]; out[5 + q] = (float)c.x[q]; }
-  return 0;
+  return g_gjk_last_it; /* support iterations (GJK probe) */
 }
 
 /* Ground: each link's shape is the convex hull of two circles (C, E1, E2 in body frame). The
@@ -592,7 +663,8 @@ int zbo_hull_pair(const float* a, const float* b, float margin, float* out) {
  * per link the first NCAND_PER_LINK below the speculative margin are kept. Self: the GJK contact
  * of every non-adjacent link pair (hull_pair; the kernel's broadphase is conservative, so testing
  * all pairs here finds the same candidates). */
-static void detect(const mdl_t* m, const zb_task_cfg* cfg, const kin_t* k, real Pz, clist_t* L) {
+static void detect(const mdl_t* m, const zb_task_cfg* cfg, const kin_t* k, real Pz, const clist_t* warm,
+                   clist_t* L) {
   L->n = 0;
   const real margin = cfg->contact_margin;
   for (int l = 0; l < NL; ++l) {
@@ -639,19 +711,29 @@ static void detect(const mdl_t* m, const zb_task_cfg* cfg, const kin_t* k, real 
     }
   }
   if (cfg->enable_self_collision) {
-    int nself = 0;
+    int nself = 0, nund = 0;
     for (int p = 0; p < m->npairs && nself < NSELF_MAX; ++p) {
       int la = m->pairs[p][0], lb = m->pairs[p][1];
       hull_t A, B;
       world_hull(m, k, la, &A);
       world_hull(m, k, lb, &B);
+      /* warm start: the pair's contact normal of the previous substep of this step, if kept */
+      const real* v0 = NULL;
+      if (warm)
+        for (int j = 0; j < warm->n; ++j)
+          if (warm->c[j].la == la && warm->c[j].lb == lb) { v0 = warm->c[j].n; break; }
+      if (g_gjk_probe && sat_gap(&A, &B) > margin + 2 * (real)CORE_M) continue; /* kernel: no GJK */
+      ++nund;
       contact_t c;
-      if (hull_pair(&A, &B, margin, margin, &c)) {
+      const int hit = hull_pair(&A, &B, margin, margin, g_gjk_warm ? v0 : NULL, &c);
+      if (g_gjk_probe) __atomic_fetch_add(&g_gjk_hist[g_gjk_last_it], 1, __ATOMIC_RELAXED);
+      if (hit) {
         c.la = la; c.lb = lb;
         L->c[L->n++] = c;
         ++nself;
       }
     }
+    if (g_gjk_probe) __atomic_fetch_add(&g_gjk_uhist[nund < 63 ? nund : 63], 1, __ATOMIC_RELAXED);
   }
   select_contacts(L);
 }
@@ -737,7 +819,7 @@ typedef struct {
  * coefficient = product, the ground's being cfg->friction / cfg->friction_dynamic), or NULL for
  * the cfg coefficients on every contact */
 static void substep(const mdl_t* m, const zb_task_cfg* cfg, phys_t* s, const real target[ND],
-                    const real* mu_link, const real* mu_link_d, substep_out_t* out) {
+                    const real* mu_link, const real* mu_link_d, clist_t* warm, substep_out_t* out) {
   const real dt = cfg->sim_dt;
   kin_t k;
   fk(m, s, &k);
@@ -853,8 +935,9 @@ static void substep(const mdl_t* m, const zb_task_cfg* cfg, phys_t* s, const rea
 
   /* contacts */
   clist_t CL;
-  detect(m, cfg, &k, s->root_pos[2], &CL);
+  detect(m, cfg, &k, s->root_pos[2], warm, &CL);
   int nc = CL.n;
+  if (warm) *warm = CL; /* the next substep of this step warm-starts GJK from these normals */
   real Y[NC_MAX][3][NV];
   real invm[NC_MAX][3], vmin[NC_MAX], lam[NC_MAX][3], c01[NC_MAX], c02[NC_MAX], muc[NC_MAX], mud[NC_MAX];
   int broken[NC_MAX];
@@ -1401,7 +1484,9 @@ static real su_step_env(const mdl_t* m, const zb_task_cfg* cfg, int stage, uint6
     target[j] = md->p_delta[j] + m->jq0[j];
   }
   substep_out_t so;
-  for (int k = 0; k < cfg->decimation; ++k) substep(m, cfg, &e->ph, target, md->mu, md->mu_d, &so);
+  clist_t wl;
+  wl.n = 0;
+  for (int k = 0; k < cfg->decimation; ++k) substep(m, cfg, &e->ph, target, md->mu, md->mu_d, &wl, &so);
   md->ep_len += 1;
   for (int j = 0; j < ND; ++j) md->actions[j] = act[j];
   su_links_t L;
@@ -1687,10 +1772,12 @@ static real v4_step_env(const zbo_sim* s, int stage, uint64_t ctr, int i, env_t*
   }
   substep_out_t so;
   real jqd_prev[ND];
+  clist_t wl;
+  wl.n = 0;
   for (int k = 0; k < cfg->decimation; ++k) {
     if (k == cfg->decimation - 1)
       for (int j = 0; j < ND; ++j) jqd_prev[j] = e->ph.jqd[j];
-    substep(m, cfg, &e->ph, target, NULL, NULL, &so);
+    substep(m, cfg, &e->ph, target, NULL, NULL, &wl, &so);
     v4_sensor_update(m, cfg, md, so.net_force);
   }
   md->ep_len += 1;
@@ -2002,12 +2089,14 @@ static real m_step_env(const zbo_sim* s, uint64_t ctr, int i, env_t* e, const fl
                                        (real)cfg->action_clip);
   substep_out_t so;
   real jqd_prev[ND];
+  clist_t wl;
+  wl.n = 0;
   for (int k = 0; k < cfg->decimation; ++k) {
     real target[ND];
     for (int j = 0; j < ND; ++j) target[j] = e->ph.jq[j] + delta[j]; /* apply_actions: q + delta */
     if (k == cfg->decimation - 1)
       for (int j = 0; j < ND; ++j) jqd_prev[j] = e->ph.jqd[j];
-    substep(m, cfg, &e->ph, target, md->mu, md->mu_d, &so);
+    substep(m, cfg, &e->ph, target, md->mu, md->mu_d, &wl, &so);
     /* ContactSensor.update (every physics step): history shift, air time with elapsed sim_dt */
     for (int f = 0; f < 2; ++f) {
       const real* F = so.net_force[m->foot_links[f]];
@@ -2345,8 +2434,10 @@ static real step_env(const mdl_t* m, const zb_task_cfg* cfg, env_t* e, const flo
   cache_from_phys(m, &e->ph, &pre);
   /* physics */
   substep_out_t so;
+  clist_t wl;
+  wl.n = 0;
   for (int k = 0; k < cfg->decimation; ++k) {
-    substep(m, cfg, &e->ph, target, NULL, NULL, &so);
+    substep(m, cfg, &e->ph, target, NULL, NULL, &wl, &so);
     sensor_update(m, cfg, md, so.net_force);
   }
   md->ep_len += 1;
@@ -2556,7 +2647,9 @@ int zbo_physics_substeps(zbo_sim* s, const float* targets, int nsub, float* net_
     const int dr = s->c.task == ZB_TASK_STANDUP_V0 || s->c.task == ZB_TASK_MANAGER_V0;
     const real* mu = dr ? s->env[e].md.mu : NULL;
     const real* mud = dr ? s->env[e].md.mu_d : NULL;
-    for (int k = 0; k < nsub; ++k) substep(&s->m, &s->c, &s->env[e].ph, tg, mu, mud, &so);
+    clist_t wl;
+    wl.n = 0;
+    for (int k = 0; k < nsub; ++k) substep(&s->m, &s->c, &s->env[e].ph, tg, mu, mud, &wl, &so);
     if (net_force)
       for (int l = 0; l < NL; ++l)
         for (int a = 0; a < 3; ++a) net_force[((size_t)e * NL + l) * 3 + a] = (float)so.net_force[l][a];
@@ -2612,13 +2705,13 @@ int zbo_contact_diag(zbo_sim* s, float* out) {
         world_hull(&s->m, &k, s->m.pairs[p][0], &A);
         world_hull(&s->m, &k, s->m.pairs[p][1], &B);
         contact_t c;
-        hull_pair(&A, &B, margin, (real)1e30, &c); /* no early exit: the separation of every pair */
+        hull_pair(&A, &B, margin, (real)1e30, NULL, &c); /* no early exit: the separation of every pair */
         real d = (real)fabs((double)(c.sep - margin));
         if (d < mind) mind = d;
         if (c.sep < margin && ns < NSELF_MAX) ++ns;
       }
     }
-    detect(&s->m, &s->c, &k, Pz, &L);
+    detect(&s->m, &s->c, &k, Pz, NULL, &L);
     out[5 * e + 0] = (float)(ng + ns);
     out[5 * e + 1] = (float)ng;
     out[5 * e + 2] = (float)ns;
@@ -2641,7 +2734,7 @@ int zbo_self_min_sep(zbo_sim* s, float* out) {
       world_hull(&s->m, &k, s->m.pairs[p][0], &A);
       world_hull(&s->m, &k, s->m.pairs[p][1], &B);
       contact_t c;
-      hull_pair(&A, &B, (real)1e30, (real)1e30, &c);
+      hull_pair(&A, &B, (real)1e30, (real)1e30, NULL, &c);
       if (c.sep < mn) mn = c.sep;
     }
     out[e] = (float)mn;
