@@ -375,6 +375,13 @@ int zb_read_stamps(uint64_t* out16);
 /* diagnostic build only: the phase cycles of the slowest wave (same order as zb_read_stamps) */
 int zb_read_stamps_slowest(uint64_t* out16);
 
+/* Test entry: the self-collision GJK (the step kernels' gjk_quad) on n link pairs given as
+ * world-frame core hulls, device pointers. pairs [n][2][2][9] (per hull two circles: centre, E1,
+ * E2 with the radius baked in), v0 [n][3] start directions or NULL (the hull centre difference),
+ * out [n][9] = {contact, separation, normal[3], point[3], iterations}. Checked against the
+ * oracle's hull_pair (tests/test_gpu_selfcollision.py). */
+int zb_gjk_pairs(const float* pairs, const float* v0, int n, float margin, float* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -471,13 +471,6 @@ static int simplex_step(real W[4][3], real PA[4][3], int* n, real lam[4], real v
   return 0;
 }
 
-/* Self-collision contact of one link pair: GJK distance between the two core hulls from the
- * initial direction best_axis (the largest separating gap of five axes), stopping when
- * (|v|^2 - v.w) / |v| <= 1 um (the distance bounds |v| and v.w / |v| agree; tighter is below fp32 resolution for nearly touching cores), after GJK_MAX_IT iterations, or early (no contact) once the lower
- * bound v.w / |v| exceeds early_margin + 2 CORE_M (early_margin = margin for detection). Contact: normal (pa - pb) / d from B to A,
- * separation d - 2 CORE_M, point (pa + pb) / 2. Cores that overlap (d < 1e-6): normal along the
- * centre difference, separation -2 CORE_M, point = the mean of the centres. Returns 1 on a
- * contact within the margin. */
 /* extent of a hull along unit u: each circle spans c.u +- |(u.E1, u.E2)| */
 static void hull_extent(const hull_t* h, const real u[3], real* lo, real* hi) {
   for (int ci = 0; ci < 2; ++ci) {
@@ -489,32 +482,16 @@ static void hull_extent(const hull_t* h, const real u[3], real* lo, real* hi) {
   }
 }
 
-/* GJK's starting direction: of the centre difference and the four circle normals, the axis with
- * the largest separating gap, oriented from B to A */
-static void best_axis(const hull_t* A, const hull_t* B, real u_out[3]) {
-  real best = -1e30;
-  for (int ax = 0; ax < 5; ++ax) {
-    real u[3];
-    if (ax == 0) {
-      for (int a = 0; a < 3; ++a) u[a] = (real)0.5 * (A->c[0][a] + A->c[1][a]) - (real)0.5 * (B->c[0][a] + B->c[1][a]);
-    } else {
-      const hull_t* H = ax <= 2 ? A : B;
-      v3_cross(H->c[(ax - 1) & 1] + 3, H->c[(ax - 1) & 1] + 6, u);
-    }
-    real nu = sqrtr(v3_dot(u, u));
-    if (nu < (real)1e-15) nu = (real)1e-15;
-    for (int a = 0; a < 3; ++a) u[a] /= nu;
-    real alo, ahi, blo, bhi;
-    hull_extent(A, u, &alo, &ahi);
-    hull_extent(B, u, &blo, &bhi);
-    real gp = alo - bhi, gm = blo - ahi, g = gp > gm ? gp : gm;
-    if (ax == 0 || g > best) {
-      best = g;
-      for (int a = 0; a < 3; ++a) u_out[a] = gp >= gm ? u[a] : -u[a];
-    }
-  }
-}
-
+/* Self-collision contact of one link pair: GJK distance between the two core hulls from the
+ * initial direction v0 (B -> A; the kernel passes the pair's contact normal of the previous
+ * substep of the same step: warm start) or, with v0 = NULL, the hull centre difference. Stops when
+ * (|v|^2 - v.w) / |v| <= GJK_TOL (the distance bounds |v| and v.w / |v| agree), after GJK_MAX_IT
+ * iterations, or early (no contact) once the lower bound v.w / |v| exceeds early_margin +
+ * 2 CORE_M (early_margin = margin for detection). Contact: normal (pa - pb) / d from B to A,
+ * separation d - 2 CORE_M, point (pa + pb) / 2. Cores that overlap (d < 1e-6): normal along the
+ * centre difference, separation -2 CORE_M, point = the mean of the centres. Returns 1 on a
+ * contact within the margin. (The kernel runs the same statement on the 4 lanes of a quad:
+ * gjk_quad in zbot_sim.hip.) */
 static int hull_pair(const hull_t* A, const hull_t* B, real margin, real early_margin, const real* v0,
                      contact_t* out) {
   real ca[3], cb[3], v[3];
@@ -523,7 +500,7 @@ static int hull_pair(const hull_t* A, const hull_t* B, real margin, real early_m
     cb[a] = (real)0.5 * (B->c[0][a] + B->c[1][a]);
   }
   if (v0) { v[0] = v0[0]; v[1] = v0[1]; v[2] = v0[2]; }
-  else best_axis(A, B, v);
+  else { v[0] = ca[0] - cb[0]; v[1] = ca[1] - cb[1]; v[2] = ca[2] - cb[2]; }
   real W[4][3], PA[4][3], lam[4] = {1, 0, 0, 0};
   int n = 0, overlap = 0; /* n = retained points besides the newest W[0] */
   {
@@ -580,7 +557,8 @@ int zbo_set_gjk_tol(double tol) {
   return 0;
 }
 
-/* largest separating-axis gap of best_axis's five axes (the kernel's hulls_separated test) */
+/* largest separating-axis gap over the centre difference and the four circle normals (the kernel's
+ * hulls_separated test) */
 static real sat_gap(const hull_t* A, const hull_t* B) {
   real best = -1e30;
   for (int ax = 0; ax < 5; ++ax) {
@@ -633,7 +611,7 @@ int zbo_undecided_pairs(zbo_sim* s, float* out, int max) {
  * separating axis; probe = 1 histograms the support iterations of the GJK calls the kernel would
  * make (pairs the separating-axis test leaves undecided). hist: GJK_MAX_IT + 2 counters. */
 int zbo_gjk_hooks(int warm, int probe, long long* hist) {
-  if (warm >= 0) g_gjk_warm = warm;
+  if (warm >= 0) g_gjk_warm = warm & 1;
   if (probe >= 0) g_gjk_probe = probe;
   if (hist) {
     for (int i = 0; i < GJK_MAX_IT + 2; ++i) { hist[i] = g_gjk_hist[i]; g_gjk_hist[i] = 0; }
@@ -642,19 +620,35 @@ int zbo_gjk_hooks(int warm, int probe, long long* hist) {
   return 0;
 }
 
-/* test entry point: hull_pair on two world-frame core hulls given as [2][9] floats (centre, two
- * semi-axes per circle); out = {contact, sep, n[3], x[3]} (tests/test_oracle_selfcollision.py) */
-int zbo_hull_pair(const float* a, const float* b, float margin, float* out) {
+/* test entry points: hull_pair on two world-frame core hulls given as [2][9] floats (centre, two
+ * semi-axes per circle) from the start direction v0 (NULL: the hull centre difference);
+ * out = {contact, sep, n[3], x[3]}; returns the support iterations (tests/test_oracle_selfcollision.py,
+ * tests/test_gpu_selfcollision.py, tools/gjk/probe.py) */
+int zbo_hull_pair_from(const float* a, const float* b, float margin, const float* v0, float* out) {
   hull_t A, B;
   for (int ci = 0; ci < 2; ++ci)
     for (int q = 0; q < 9; ++q) { A.c[ci][q] = a[9 * ci + q]; B.c[ci][q] = b[9 * ci + q]; }
   contact_t c;
   memset(&c, 0, sizeof(c));
-  int hit = hull_pair(&A, &B, (real)margin, (real)margin, NULL, &c);
+  real w0[3];
+  if (v0) { w0[0] = v0[0]; w0[1] = v0[1]; w0[2] = v0[2]; }
+  int hit = hull_pair(&A, &B, (real)margin, (real)margin, v0 ? w0 : NULL, &c);
   out[0] = (float)hit;
   out[1] = (float)c.sep;
   for (int q = 0; q < 3; ++q) { out[2 + q] = (float)c.n[q]; out[5 + q] = (float)c.x[q]; }
   return g_gjk_last_it; /* support iterations (GJK probe) */
+}
+int zbo_hull_pair(const float* a, const float* b, float margin, float* out) {
+  return zbo_hull_pair_from(a, b, margin, NULL, out);
+}
+/* mirror of the library's test entry zb_gjk_pairs (host pointers): pairs [n][2][2][9], v0 [n][3] or
+ * NULL, out [n][9] = {contact, sep, n[3], x[3], iterations} */
+int zbo_gjk_pairs(const float* pairs, const float* v0, int n, float margin, float* out, void* stream) {
+  (void)stream;
+  for (int k = 0; k < n; ++k)
+    out[9 * k + 8] = (float)zbo_hull_pair_from(pairs + 36 * k, pairs + 36 * k + 18, margin, v0 ? v0 + 3 * k : NULL,
+                                               out + 9 * k);
+  return 0;
 }
 
 /* Ground: each link's shape is the convex hull of two circles (C, E1, E2 in body frame). The

@@ -38,7 +38,7 @@ def main():
     task = sys.argv[1] if len(sys.argv) > 1 else "zbot-6b-walking-v2"
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 512
     steps = int(sys.argv[3]) if len(sys.argv) > 3 else 200
-    for warm in (0, 1):
+    for warm in [int(w) for w in os.environ.get("MODES", "0,1").split(",")]:
         hh = run(task, n, steps, warm)
         h, u = hh[:NH], hh[NH:]
         tot = h.sum()

@@ -890,10 +890,9 @@ __device__ __forceinline__ void gjk_tri(const float a[3], const float S[3][3], f
 
 // Cheap separation test before GJK: separating-axis gaps along the centre difference and the four
 // circle normals (each circle's extent along u is c.u +- |(u.E1, u.E2)|, exact). True when one
-// gap exceeds lim = margin + 2 kCoreM: the cores are farther apart than any contact. best_u = the
-// axis of the largest gap, oriented B -> A (GJK's starting direction). A rigorous
-// bound, so it never drops a contact that gjk_pair would find; on random-action rollouts it
-// decides ~99 % of the broadphase pairs without iterating.
+// gap exceeds lim = margin + 2 kCoreM: the cores are farther apart than any contact. A rigorous
+// bound, so it never drops a contact that GJK would find; on random-action rollouts it decides
+// ~99 % of the broadphase pairs without iterating.
 __device__ __forceinline__ void hull_extent(const Hull& h, const float u[3], float& lo, float& hi) {
 #pragma unroll
   for (int ci = 0; ci < 2; ++ci) {
@@ -903,7 +902,7 @@ __device__ __forceinline__ void hull_extent(const Hull& h, const float u[3], flo
     hi = ci == 0 ? m + r : fmaxf(hi, m + r);
   }
 }
-__device__ __forceinline__ bool hulls_separated(const Hull& A, const Hull& B, float lim, float best_u[3]) {
+__device__ __forceinline__ bool hulls_separated(const Hull& A, const Hull& B, float lim) {
   float best = -1e30f;
 #pragma unroll
   for (int ax = 0; ax < 5; ++ax) {
@@ -921,27 +920,94 @@ __device__ __forceinline__ bool hulls_separated(const Hull& A, const Hull& B, fl
     hull_extent(A, u, alo, ahi);
     hull_extent(B, u, blo, bhi);
     // gap along u with A on the + side (u), or along -u
-    const float gp = alo - bhi, gm = blo - ahi;
-    const float g = fmaxf(gp, gm);
-    const bool take = ax == 0 || g > best;
-    best = take ? g : best;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) best_u[k] = take ? (gp >= gm ? u[k] : -u[k]) : best_u[k];
+    best = fmaxf(best, fmaxf(alo - bhi, blo - ahi));
   }
   return best > lim;
 }
-// GJK (distance) on the core hulls A, B from v0 = the separating-axis test's best axis (B -> A). Simplex = the newest
-// Minkowski point a plus up to three retained points S0..S2 (with their A-side support points);
-// each iteration takes the shortest of the valid affine projections of the subsets containing a,
-// in the order {a}, {a,S0}, {a,S1}, {a,S0,S1}, {a,S2}, {a,S0,S2}, {a,S1,S2} (segments, triangles
-// with positive barycentrics; the tetrahedron only as the inside test).
-// Stops when (|v|^2 - v.w) / |v| <= 1 um (the distance bounds |v| and v.w / |v| agree; tighter is below fp32 resolution for nearly touching cores), after kGjkMaxIt iterations, or as soon as the lower
-// bound v.w / |v| exceeds early_margin + 2 kCoreM (no contact; early_margin = margin in the
-// counting pass, huge when a counted contact is re-computed). Contact: n = (pa - pb) / d
-// (B -> A), sep = d - 2 kCoreM, x = (pa + pb) / 2; overlapping cores: n along the centre
-// difference, sep = -2 kCoreM, x = the mean centre. Same statement as the oracle's hull_pair.
-__device__ __forceinline__ bool gjk_pair(const Hull& A, const Hull& B, const float v0[3], float margin,
-                                         float early_margin, SelfContact& out, int& iters) {
+// GJK (distance) on the core hulls A, B of a link pair, run by the 4 lanes of a DPP quad: lane j
+// holds circle (j & 1) of hull (j >> 1 ? B : A); the simplex is replicated bit-identically in the
+// 4 lanes. Simplex = the newest Minkowski point a plus up to three retained points S0..S2 (with
+// their A-side support points); each iteration takes the shortest of the valid affine projections
+// of the subsets containing a, first in the order {a}, {a,S0}, {a,S1}, {a,S0,S1}, {a,S2},
+// {a,S0,S2}, {a,S1,S2} (segments, triangles with positive barycentrics; the tetrahedron only as
+// the inside test). Per iteration lane j evaluates its circle's support point (the pair of lanes
+// of one hull keeps the larger, circle 0 on ties) and two of the candidates (j = 0: {a}, {a,S0};
+// 1: {a,S1}, {a,S0,S1}; 2: {a,S2}, {a,S0,S2}; 3: {a,S1,S2}); two DPP butterfly steps pick the
+// first shortest in that order. ~2x fewer instructions per iteration than one lane per pair, and
+// the 4 quads of a team run up to 4 pairs at once (the usual count of undecided pairs).
+// Starts from v0 (B -> A): the pair's contact normal of the previous substep of this step (warm
+// start) or the hull centre difference. Stops when (|v|^2 - v.w) / |v| <= kGjkTol (the distance
+// bounds |v| and v.w / |v| agree), after kGjkMaxIt iterations, or as soon as the lower bound
+// v.w / |v| exceeds early_margin + 2 kCoreM (no contact; early_margin = margin in the counting
+// pass, huge when a counted contact is re-computed). Contact: n = (pa - pb) / d (B -> A),
+// sep = d - 2 kCoreM, x = (pa + pb) / 2; overlapping cores: n along the centre difference,
+// sep = -2 kCoreM, x = the mean centre. Same statement as the oracle's hull_pair.
+constexpr int DPP_QB0 = 0x00, DPP_QB2 = 0xAA;  // quad_perm broadcast of quad lane 0 / 2
+struct QCircle { float c[3], e1[3], e2[3]; };  // world core circle: centre, semi-axes (radius baked in)
+__device__ __forceinline__ void quad_circle(const Q& q, int l, int ci, QCircle& h) {
+  float R[9], p[3];
+  read_frame(q, link_body(l), R, p);
+  const float4* L = q.link(l);
+  const float4 cc = L[7 + ci];
+  float4 e1 = L[2 + 3 * ci], e2 = L[3 + 3 * ci];
+  e1.x *= cc.w; e1.y *= cc.w; e1.z *= cc.w;
+  e2.x *= cc.w; e2.y *= cc.w; e2.z *= cc.w;
+  mv3f(R, cc, h.c);
+  h.c[0] += p[0]; h.c[1] += p[1]; h.c[2] += p[2];
+  mv3f(R, e1, h.e1);
+  mv3f(R, e2, h.e2);
+}
+// hull centres (mean of the two circle centres) of A and B in every lane of the quad
+__device__ __forceinline__ void quad_centres(const QCircle& h, float ca[3], float cb[3]) {
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const float m = 0.5f * (h.c[k] + dppf<DPP_XOR1>(h.c[k]));
+    ca[k] = dppf<DPP_QB0>(m);
+    cb[k] = dppf<DPP_QB2>(m);
+  }
+}
+// support points pa of A along -v and pb of B along v, in every lane of the quad
+__device__ __forceinline__ void quad_support(const QCircle& h, const float v[3], int j, float pa[3], float pb[3]) {
+  const float sg = (j & 2) ? 1.f : -1.f;
+  const float d[3] = {sg * v[0], sg * v[1], sg * v[2]};
+  const float a = dot3(d, h.e1), b = dot3(d, h.e2);
+  const float ri = __builtin_amdgcn_rsqf(fmaxf(fmaf(a, a, b * b), 1e-30f));
+  float pt[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) pt[k] = h.c[k] + (a * h.e1[k] + b * h.e2[k]) * ri;
+  const float val = dot3(d, pt), pv = dppf<DPP_XOR1>(val);
+  const bool mine = (j & 1) ? (val > pv) : !(pv > val);  // circle 0 unless circle 1 is strictly larger
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    // (the DPP read as a statement of its own: inside `?:` it would be evaluated only for the
+    // lanes with !mine, and bound_ctrl then reads 0 from the masked-off source lanes)
+    const float o = dppf<DPP_XOR1>(pt[k]);
+    const float sp = mine ? pt[k] : o;
+    pa[k] = dppf<DPP_QB0>(sp);
+    pb[k] = dppf<DPP_QB2>(sp);
+  }
+}
+// one butterfly step of the candidate selection: take the partner's candidate if it is shorter, or
+// as short and earlier in the canonical order (partner_first: the partner's lane is the lower one)
+template <int CTRL>
+__device__ __forceinline__ void quad_pick(bool partner_first, float& best, float bv[3], float& l1, float& l2,
+                                          unsigned& bm) {
+  const float ob = dppf<CTRL>(best);
+  const bool take = partner_first ? !(ob > best) : (ob < best);
+  best = take ? ob : best;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const float o = dppf<CTRL>(bv[k]);
+    bv[k] = take ? o : bv[k];
+  }
+  const float o1 = dppf<CTRL>(l1), o2 = dppf<CTRL>(l2);
+  const unsigned om = (unsigned)dppi<CTRL>((int)bm);
+  l1 = take ? o1 : l1;
+  l2 = take ? o2 : l2;
+  bm = take ? om : bm;
+}
+__device__ __forceinline__ bool gjk_quad(const QCircle& h, int j, const float v0[3], float margin, float early_margin,
+                                         SelfContact& out, int& iters) {
   float v[3] = {v0[0], v0[1], v0[2]};
   const float lim = early_margin + 2.f * kCoreM;
   float S[3][3] = {}, SP[3][3] = {}, lam[4] = {1.f, 0.f, 0.f, 0.f};
@@ -953,9 +1019,7 @@ __device__ __forceinline__ bool gjk_pair(const Hull& A, const Hull& B, const flo
     const float vv = dot3(v, v);
     if (n >= 0 && vv < 1e-12f) { overlap = true; break; }
     float pa[3], pb[3], w[3];
-    const float nd[3] = {-v[0], -v[1], -v[2]};
-    hull_sup(A, nd, pa);
-    hull_sup(B, v, pb);
+    quad_support(h, v, j, pa, pb);
 #pragma unroll
     for (int k = 0; k < 3; ++k) w[k] = pa[k] - pb[k];
     if (n < 0) {  // first point
@@ -976,20 +1040,54 @@ __device__ __forceinline__ bool gjk_pair(const Hull& A, const Hull& B, const flo
       aw[k] = w[k]; ap[k] = pa[k];
     }
     ++n;
-    // candidates: {a}, then per retained point i the segment {a, Si} and the triangles {a, Sj, Si}
-    // (j < i), then the inside-tetrahedron test; only the retained points that exist are visited
-    float best = dot3(aw, aw), bv[3] = {aw[0], aw[1], aw[2]}, bl[3] = {0.f, 0.f, 0.f};
-    unsigned bm = 0;  // retained points used (bit i: S_i)
-    gjk_seg<0>(aw, S, best, bv, bl, bm);
-    if (n >= 2) {
-      gjk_seg<1>(aw, S, best, bv, bl, bm);
-      gjk_tri<0, 1>(aw, S, best, bv, bl, bm);
+    // this lane's candidates: the segment {a, S_j} (j < 3) and the triangle {a, S_I, S_J}
+    // (j = 1: I, J = 0, 1; j = 2: 0, 2; j = 3: 1, 2); lane 0 starts from {a}
+    float best = j == 0 ? dot3(aw, aw) : 3.0e38f, bv[3] = {aw[0], aw[1], aw[2]}, l1 = 0.f, l2 = 0.f;
+    unsigned bm = 0u;  // retained points used (bit i: S_i)
+    {
+      float e[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) e[k] = (j == 0 ? S[0][k] : (j == 1 ? S[1][k] : S[2][k])) - aw[k];
+      const float ee = dot3(e, e);
+      const float t = -dot3(aw, e) / fmaxf(ee, 1e-30f);
+      float p[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) p[k] = aw[k] + t * e[k];
+      const float d2 = dot3(p, p);
+      const bool ok = j < n && ee > 1e-20f && t > 0.f && t < 1.f && d2 < best;
+      best = ok ? d2 : best;
+      bm = ok ? (1u << j) : bm;
+      l1 = ok ? t : l1;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) bv[k] = ok ? p[k] : bv[k];
     }
-    if (n >= 3) {
-      gjk_seg<2>(aw, S, best, bv, bl, bm);
-      gjk_tri<0, 2>(aw, S, best, bv, bl, bm);
-      gjk_tri<1, 2>(aw, S, best, bv, bl, bm);
+    {
+      float e1[3], e2[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        e1[k] = (j == 3 ? S[1][k] : S[0][k]) - aw[k];
+        e2[k] = (j == 1 ? S[1][k] : S[2][k]) - aw[k];
+      }
+      const float g00 = dot3(e1, e1), g01 = dot3(e1, e2), g11 = dot3(e2, e2);
+      const float r0 = -dot3(aw, e1), r1 = -dot3(aw, e2);
+      const float det = g00 * g11 - g01 * g01;
+      const float id = 1.f / (fabsf(det) > 1e-30f ? det : 1e-30f);
+      const float ts = (r0 * g11 - r1 * g01) * id, tt = (g00 * r1 - g01 * r0) * id;
+      float p[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) p[k] = aw[k] + ts * e1[k] + tt * e2[k];
+      const float d2 = dot3(p, p);
+      const bool valid = j == 1 ? n >= 2 : (j >= 2 && n >= 3);
+      const bool ok = valid && det > 1e-24f * g00 * g11 && ts > 0.f && tt > 0.f && ts + tt < 1.f && d2 < best;
+      best = ok ? d2 : best;
+      bm = ok ? (j == 1 ? 3u : (j == 2 ? 5u : 6u)) : bm;
+      l1 = ok ? ts : l1;
+      l2 = ok ? tt : l2;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) bv[k] = ok ? p[k] : bv[k];
     }
+    quad_pick<DPP_XOR1>((j & 1) != 0, best, bv, l1, l2, bm);
+    quad_pick<DPP_XOR2>((j & 2) != 0, best, bv, l1, l2, bm);
     if (n == 3) {  // origin inside the tetrahedron (a, S0, S1, S2)?
       float e0[3], e1[3], e2[3], x12[3];
 #pragma unroll
@@ -1020,8 +1118,6 @@ __device__ __forceinline__ bool gjk_pair(const Hull& A, const Hull& B, const flo
       T2[k] = (u0 && u1) ? S[1][k] : S[2][k];
       T2p[k] = (u0 && u1) ? SP[1][k] : SP[2][k];
     }
-    const float l1 = u0 ? bl[0] : (u1 ? bl[1] : bl[2]);
-    const float l2 = (u0 && u1) ? bl[1] : bl[2];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       S[0][k] = T1[k]; SP[0][k] = T1p[k];
@@ -1036,13 +1132,10 @@ __device__ __forceinline__ bool gjk_pair(const Hull& A, const Hull& B, const flo
   // one exit (a struct written on two paths ends up in scratch memory)
   const float d = sqrtf(dot3(v, v));
   const bool deep = overlap || d < 1e-6f;
-  float ca[3], cb[3], dv[3];  // core centres (recomputed: not kept live across the iterations)
+  float ca[3], cb[3], dv[3];  // hull centres (recomputed: not kept live across the iterations)
+  quad_centres(h, ca, cb);
 #pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    ca[k] = 0.5f * (A.c[0][k] + A.c[1][k]);
-    cb[k] = 0.5f * (B.c[0][k] + B.c[1][k]);
-    dv[k] = ca[k] - cb[k];
-  }
+  for (int k = 0; k < 3; ++k) dv[k] = ca[k] - cb[k];
   const float dn2 = dot3(dv, dv);
   const bool nodir = dn2 < 1e-24f;
   const float idn = __builtin_amdgcn_rsqf(fmaxf(dn2, 1e-30f)), id = 1.f / fmaxf(d, 1e-30f);
@@ -1066,7 +1159,7 @@ __device__ __forceinline__ bool gjk_pair(const Hull& A, const Hull& B, const flo
 // contiguous chunks, one per lane, so candidates stay in canonical order lane by lane; each
 // candidate pair runs GJK on the core hulls (gjk_pair, one contact per pair). Counting pass, team
 // scan, then each lane writes its candidates at their canonical positions.
-__device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q& q, bool& over, Stamps& sp) {
+__device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q& q, bool warm, bool& over, Stamps& sp) {
   const float margin = cfg.contact_margin;
 
   // ground, counting pass: lane s = link s; keep the world circle frames for the write pass
@@ -1186,16 +1279,14 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q&
         Hull A, B;
         gather_hull(own, 4 * (base + (pcode >> 4)), A);
         gather_hull(own, 4 * (base + (pcode & 15)), B);
-        float u[3];
-        if (valid && !hulls_separated(A, B, margin + 2.f * kCoreM, u)) undecided |= 1u << k;
+        if (valid && !hulls_separated(A, B, margin + 2.f * kCoreM)) undecided |= 1u << k;
       }
     }
 #ifdef ZB_STAMP_DETECT
     sp.mark(11);  // separating-axis tests
 #endif
-    // the undecided pairs of the whole team, dealt again round-robin (GJK work spread evenly: a
-    // lane runs ceil(U / 16) GJKs, usually one, where the lane of a folded robot's neighbouring
-    // pairs could queue several)
+    // the undecided pairs of the whole team by rank; pair u runs GJK on quad u % 4 of the team in
+    // round u / 4 (up to 4 pairs at once: random-action rollouts have at most 4 per env)
     unsigned long long und = 0ull;  // team: bit r = the pair of rank r needs GJK
     {
       unsigned long long mine = 0ull;
@@ -1205,15 +1296,16 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q&
       und = (unsigned long long)(unsigned)lo | ((unsigned long long)(unsigned)hi << 32);
     }
     const int U = __popcll(und);
-    const int urounds = (U + TL - 1) / TL;
-    SelfContact hit0 = {};  // this lane's first contact is kept for the write pass
+    const int qd = q.s >> 2, qj = q.s & 3;  // quad of the team, lane in the quad
+    const int urounds = (U + 3) >> 2;
+    SelfContact hit0 = {};  // this quad's first contact is kept for the write pass
     int hit0_k = -1;
-    unsigned own = 0u;                // bit k: this lane's GJK pair of round k is a contact
+    unsigned own = 0u;                // bit k: this quad's pair of round k is a contact
     unsigned long long allhits = 0ull;  // team: bit r = the pair of rank r is a contact
 #pragma unroll 1
     for (int pass = 0; pass < 2; ++pass) {
       for (int k = 0; k < urounds; ++k) {
-        const int u = q.s + TL * k;
+        const int u = qd + 4 * k;
         if (u >= U) break;
         const int r = nth_set_bit(und, u);
         const int pos = g_tot + __popcll(allhits & ((1ull << r) - 1ull));
@@ -1222,21 +1314,36 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q&
         const int pcode = q.pair_code(nth_set_bit(bmask, r));
         SelfContact sc = hit0;
         if (pass == 0 || k != hit0_k) {
-          Hull A, B;
-          world_hull(q, pcode >> 4, A);
-          world_hull(q, pcode & 15, B);
-          int its = 0;
+          QCircle hc;
+          quad_circle(q, (qj & 2) ? (pcode & 15) : (pcode >> 4), qj & 1, hc);
+          // start: the pair's contact normal of the previous substep of this step (kept contacts
+          // hold {n, code} in FRC; unused slots code -1), else the hull centre difference
           float v0[3];
-          hulls_separated(A, B, margin + 2.f * kCoreM, v0);  // the best axis starts GJK
-          const bool h = gjk_pair(A, B, v0, pass == 0 ? margin : 1e30f, pass == 0 ? margin : 1e30f, sc, its);
-          sp.count(kStampCount0, 1);
-          sp.count(kStampCount0 + 1, its);
+          {
+            float ca[3], cb[3];
+            quad_centres(hc, ca, cb);
+            v0[0] = ca[0] - cb[0]; v0[1] = ca[1] - cb[1]; v0[2] = ca[2] - cb[2];
+          }
+          if (warm) {
+#pragma unroll
+            for (int c = 0; c < NCM; ++c) {
+              const float4 f = q.frc(c);
+              const bool m = f.w == (float)(pcode + 1);
+              v0[0] = m ? f.x : v0[0]; v0[1] = m ? f.y : v0[1]; v0[2] = m ? f.z : v0[2];
+            }
+          }
+          int its = 0;
+          const bool h = gjk_quad(hc, qj, v0, pass == 0 ? margin : 1e30f, pass == 0 ? margin : 1e30f, sc, its);
+          if (qj == 0) {
+            sp.count(kStampCount0, 1);
+            sp.count(kStampCount0 + 1, its);
+          }
           if (pass == 0 && h) {
             if (own == 0u) { hit0 = sc; hit0_k = k; }
             own |= 1u << k;
           }
         }
-        if (pass == 1) {
+        if (pass == 1 && qj == 0) {
           q.cand(pos, 0) = make_float4(sc.x[0], sc.x[1], sc.x[2], sc.sep);
           q.cand(pos, 1) = make_float4(sc.n[0], sc.n[1], sc.n[2], (float)(pcode + 1));
         }
@@ -1244,7 +1351,7 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q&
       if (pass == 0) {  // the team's contacts by rank: canonical positions follow the ground ones
         unsigned long long mine = 0ull;
         for (int k = 0; k < urounds; ++k) {
-          const int u = q.s + TL * k;
+          const int u = qd + 4 * k;
           if (u < U && ((own >> k) & 1u)) mine |= 1ull << nth_set_bit(und, u);
         }
         const int lo = tor((int)(unsigned)mine), hi = tor((int)(unsigned)(mine >> 32));
@@ -1546,7 +1653,7 @@ __device__ __forceinline__ void team_fwd(const float R[NV], const float inv[NV],
 // otherwise cfg.friction everywhere.
 template <bool kDebugForces, bool kLinkFriction>
 __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
-                                        const float target[ND], const Q& q, bool last, SensorOut& so,
+                                        const float target[ND], const Q& q, bool last, bool warm, SensorOut& so,
                                         float (*dbgF)[3], float* dbgTau, Stamps& sp) {
   const float dt = cfg.sim_dt;
   MP m = opaque(m0);
@@ -1570,7 +1677,7 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
   fk_team<true>(s, q, Ib, Sown);
   wave_sync();
   sp.mark(9);
-  nc = detect(cfg, s.pos[2], q, over, sp);
+  nc = detect(cfg, s.pos[2], q, warm, over, sp);
   m = opaque(m0);
 
   // RNEA bias forces (qddot = 0, gravity as base acceleration) and, in the same team suffix sum,
@@ -1812,6 +1919,7 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
     q.aux(c, 0) = make_float4(0.f, 0.f, 0.f, 0.f);
     q.aux(c, 1) = make_float4(0.f, 0.f, 0.f, 0.f);
     q.lam(c) = make_float4(0.f, 0.f, 0.f, 0.f);
+    q.frc(c) = make_float4(0.f, 0.f, 0.f, -1.f);  // no contact: the next substep's GJK starts cold
   }
   wave_sync();
 
@@ -1854,7 +1962,8 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
 
   if (last) {
     // ContactSensor inputs: net force on the feet, max |net force| over undesired links.
-    // Lane s forms the force of slot s, then sums the env's contacts onto link s.
+    // Lane s forms the force of slot s (into AUX, dead after the PGS: FRC keeps the normals for the
+    // next substep's GJK warm start), then sums the env's contacts onto link s.
     if (q.s < nc) {
       const float4 gn = q.frc(q.s), lam = q.lam(q.s);
       const float n[3] = {gn.x, gn.y, gn.z};
@@ -1863,12 +1972,12 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
       float f[3];
 #pragma unroll
       for (int a = 0; a < 3; ++a) f[a] = (lam.x * n[a] + lam.y * t1[a] + lam.z * t2[a]) / dt;
-      q.frc(q.s) = make_float4(f[0], f[1], f[2], gn.w);
+      q.aux(q.s, 0) = make_float4(f[0], f[1], f[2], gn.w);
     }
     wave_sync();
     float Fl[3] = {0.f, 0.f, 0.f};
     for (int c = 0; c < nc; ++c) {
-      const float4 f = q.frc(c);
+      const float4 f = q.aux(c, 0);
       const int code = (int)f.w;
       const int la = code >> 4, lb = (code & 15) - 1;
       const float sa = (q.s == la ? 1.f : 0.f) - (q.s == lb ? 1.f : 0.f);
@@ -2376,7 +2485,7 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_step_kernel(const z
   sp.mark(0);
   for (int k = 0; k < cfg.decimation; ++k) {
     // (a compile-time `true` here lets the scheduler reshape the loop into a 36 B/lane spill)
-    substep<false, false>(m, cfg, p, target, q, opaque_true(), so, nullptr, nullptr, sp);
+    substep<false, false>(m, cfg, p, target, q, opaque_true(), k > 0, so, nullptr, nullptr, sp);
     sens_record(q, k, so);
     sp.mark(7);
   }
@@ -2601,6 +2710,38 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_step_kernel(const z
 #undef CST
 }
 
+// Test entry (zb_gjk_pairs): the self-collision GJK of n link pairs given as world-frame core
+// hulls, one pair per quad (tests/test_gpu_selfcollision.py against the oracle's hull_pair).
+// pairs: [n][2 hulls][2 circles][9] (centre, E1, E2; radius baked in); v0: [n][3] start
+// directions or NULL (hull centre difference); out: [n][9] {contact, sep, n[3], x[3], iterations}.
+__global__ void zb_gjk_kernel(const float* __restrict__ pairs, const float* __restrict__ v0s, int n, float margin,
+                              float* __restrict__ out) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int pr = min(t >> 2, n - 1), j = t & 3;  // quads past n recompute pair n - 1 (no store)
+  const float* c = pairs + (size_t)pr * 36 + 9 * j;
+  QCircle h;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) { h.c[k] = c[k]; h.e1[k] = c[3 + k]; h.e2[k] = c[6 + k]; }
+  float v0[3];
+  {
+    float ca[3], cb[3];
+    quad_centres(h, ca, cb);
+    v0[0] = ca[0] - cb[0]; v0[1] = ca[1] - cb[1]; v0[2] = ca[2] - cb[2];
+  }
+  if (v0s)
+    for (int k = 0; k < 3; ++k) v0[k] = v0s[(size_t)pr * 3 + k];
+  SelfContact sc = {};
+  int its = 0;
+  const bool hit = gjk_quad(h, j, v0, margin, margin, sc, its);
+  if (j == 0 && (t >> 2) < n) {
+    float* o = out + (size_t)pr * 9;
+    o[0] = hit ? 1.f : 0.f;
+    o[1] = sc.sep;
+    for (int k = 0; k < 3; ++k) { o[2 + k] = sc.n[k]; o[5 + k] = sc.x[k]; }
+    o[8] = (float)its;
+  }
+}
+
 // reset env_ids (or all when ids == nullptr); logs the reset envs' episode sums into acc
 __global__ void zb_reset_kernel(const zb_model* __restrict__ mg, const float4* __restrict__ links, int N,
                                 float* __restrict__ st, const int32_t* __restrict__ ids, int n,
@@ -2691,7 +2832,7 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_substeps_kernel(con
   for (int j = 0; j < ND; ++j) { tg[j] = targets[(size_t)i * ND + j]; tau[j] = 0.f; }
   SensorOut so;
   Stamps sp;
-  for (int k = 0; k < nsub; ++k) substep<true, kLinkFriction>(m, cfg, p, tg, q, k == nsub - 1, so, F, tau, sp);
+  for (int k = 0; k < nsub; ++k) substep<true, kLinkFriction>(m, cfg, p, tg, q, k == nsub - 1, k > 0, so, F, tau, sp);
   if (net_force && q.s < NL)
 #pragma unroll
     for (int a = 0; a < 3; ++a) net_force[((size_t)i * NL + q.s) * 3 + a] = F[0][a];
@@ -2828,7 +2969,7 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_su_step_kernel(
   SensorOut so;
   sp.mark(0);
   for (int k = 0; k < cfg.decimation; ++k) {
-    substep<false, true>(m, cfg, p, target, q, false, so, nullptr, nullptr, sp);
+    substep<false, true>(m, cfg, p, target, q, false, k > 0, so, nullptr, nullptr, sp);
     sp.mark(7);
   }
   m = opaque(m);
@@ -3143,7 +3284,7 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_v4_step_kernel(
 #pragma unroll
       for (int j = 0; j < ND; ++j) pv.jqd_prev[j] = p.jqd[j];
     }
-    substep<false, false>(m, cfg, p, target, q, true, so, nullptr, nullptr, sp);
+    substep<false, false>(m, cfg, p, target, q, true, k > 0, so, nullptr, nullptr, sp);
     sens_record(q, k, so);
     sp.mark(7);
   }
@@ -3661,7 +3802,7 @@ __global__ __launch_bounds__(WGT, ZB_M_WAVES_PER_SIMD) void zb_m_step_kernel(
 #pragma unroll
       for (int j = 0; j < ND; ++j) pv.jqd_prev[j] = p.jqd[j];
     }
-    substep<false, true>(m, cfg, p, target, q, true, so, nullptr, nullptr, sp);
+    substep<false, true>(m, cfg, p, target, q, true, k > 0, so, nullptr, nullptr, sp);
 #pragma unroll
     for (int f = 0; f < 2; ++f) {
       const float fn = sqrtf(dot3(so.feet_f[f], so.feet_f[f]));
@@ -4614,6 +4755,13 @@ int zb_physics_substeps(zb_handle h, const float* targets, int nsub, float* net_
     zb_substeps_kernel<false><<<blocks, WGT, 0, (hipStream_t)stream>>>(h->d_model, h->d_links, h->cfg, h->n, h->d_state,
                                                                         targets, nsub, net_force, applied_torque);
   return launch_check("zb_substeps_kernel");
+}
+
+int zb_gjk_pairs(const float* pairs, const float* v0, int n, float margin, float* out, void* stream) {
+  if (!pairs || !out || n < 1) return set_err(-1, "zb_gjk_pairs", hipSuccess);
+  const int threads = 4 * n;
+  zb_gjk_kernel<<<(threads + 63) / 64, 64, 0, (hipStream_t)stream>>>(pairs, v0, n, margin, out);
+  return launch_check("zb_gjk_kernel");
 }
 
 }  // extern "C"
