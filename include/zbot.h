@@ -305,6 +305,13 @@ typedef struct zb_task_cfg {
   /* dynamic (sliding) friction of the uniform-material tasks: 1.0 (v2.py:49-56,62-68); a contact
    * whose friction impulse would exceed mu_static * normal slides with mu_dynamic * normal */
   float friction_dynamic;
+  /* contact solve per substep: 0 = solver_iterations projected Gauss-Seidel sweeps on one
+   * linearisation (bias from the substep's initial separation); 1 = TGS-style (PhysX TGS,
+   * zbot_cfg.py:637-638 solver_position_iteration_count 4 / velocity 0): solver_iterations
+   * sub-iterations of h = sim_dt / solver_iterations, each one sweep whose contact biases are
+   * re-linearised from the separation advanced by the normal velocities of the previous ones, the
+   * pose integrated with the mean of the sub-iteration velocities */
+  int32_t solver_mode;
 } zb_task_cfg;
 
 typedef struct zb_sim* zb_handle;
@@ -374,6 +381,10 @@ int zb_profile_end(zb_handle h, float* total_ms, int* count);
 int zb_read_stamps(uint64_t* out16);
 /* diagnostic build only: the phase cycles of the slowest wave (same order as zb_read_stamps) */
 int zb_read_stamps_slowest(uint64_t* out16);
+/* diagnostic build only: per-launch wave histograms since the previous call: [0, 64) the wave's
+ * largest count of GJK pairs of one env in one substep, [64, 128) the wave's largest per-lane sum
+ * of GJK iterations over the step (bins of 4) */
+int zb_read_stamp_hist(uint64_t* out128);
 
 /* Test entry: the self-collision GJK (the step kernels' gjk_quad) on n link pairs given as
  * world-frame core hulls, device pointers. pairs [n][2][2][9] (per hull two circles: centre, E1,

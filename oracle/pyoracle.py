@@ -49,6 +49,7 @@ def _load(double: bool = False):
     lib.zbo_hull_pair_from.argtypes = [_f, _f, C.c_float, C.c_void_p, _f]
     lib.zbo_gjk_pairs.argtypes = [_f, C.c_void_p, C.c_int, C.c_float, _f, C.c_void_p]
     lib.zbo_set_gjk_tol.argtypes = [C.c_double]
+    lib.zbo_set_sensor_force_scale.argtypes = [C.c_double]
     lib.zbo_self_min_sep.argtypes = [P, _f]
     lib.zbo_link_com_vel.argtypes = [P, _f]
     lib.zbo_energy_momentum.argtypes = [P, _f]

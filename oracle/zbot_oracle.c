@@ -371,6 +371,7 @@ static void select_contacts(clist_t* L) {
 typedef struct { real c[2][9]; } hull_t;
 static double g_gjk_tol = GJK_TOL;
 static _Thread_local int g_gjk_last_it; /* probe: support iterations of this thread's last hull_pair */
+static double g_sensor_force_scale = 1.0; /* test hook: scales the contact forces the sensors see */
 static int g_gjk_warm = 1;               /* warm start within a step (test hook: 0 = always cold) */
 static int g_gjk_probe = 0;              /* probe: histogram of the GJK calls the kernel would make */
 static long long g_gjk_hist[GJK_MAX_IT + 2];
@@ -402,7 +403,7 @@ static void hull_support(const hull_t* h, const real d[3], real out[3]) {
 }
 
 /* One GJK simplex step. The simplex is the newest Minkowski point a (W[0], support point PA[0])
- * plus the retained points W[1..n]. Candidates are the subsets that contain a, in the order {a},
+ * plus the retained points W[1..n] (the previous step's simplex: its newest point first). Candidates are the subsets that contain a, in the order {a},
  * {a,S1}, {a,S2}, {a,S1,S2}, {a,S3}, {a,S1,S3}, {a,S2,S3}: the affine projection of the origin with
  * all barycentric weights positive, the shortest kept (a later candidate must be strictly shorter).
  * With three retained points the tetrahedron decides whether the origin is inside (overlap; a flat
@@ -521,11 +522,10 @@ static int hull_pair(const hull_t* A, const hull_t* B, real margin, real early_m
     real vw = v3_dot(v, w);
     if (vw > 0 && vw * vw > vv * (early_margin + 2 * (real)CORE_M) * (early_margin + 2 * (real)CORE_M)) return 0;
     if (vv - vw <= (real)g_gjk_tol * sqrtr(vv)) break; /* distance bounds within the tolerance */
-    /* the previous newest point is retained last (W[n+1]) and w becomes W[0] */
-    for (int a = 0; a < 3; ++a) {
-      W[n + 1][a] = W[0][a]; PA[n + 1][a] = PA[0][a];
-      W[0][a] = w[a]; PA[0][a] = pa[a];
-    }
+    /* the simplex (the previous newest point first) is retained as W[1..n+1], w becomes W[0] */
+    for (int i = n; i >= 0; --i)
+      for (int a = 0; a < 3; ++a) { W[i + 1][a] = W[i][a]; PA[i + 1][a] = PA[i][a]; }
+    for (int a = 0; a < 3; ++a) { W[0][a] = w[a]; PA[0][a] = pa[a]; }
     ++n;
     if (simplex_step(W, PA, &n, lam, v)) { overlap = 1; break; }
   }
@@ -552,6 +552,15 @@ static int hull_pair(const hull_t* A, const hull_t* B, real margin, real early_m
 /* GJK stopping tolerance (test hook: the parity tests re-run the oracle at other tolerances to tell
  * an env whose result depends on where GJK stops - an algorithmic discontinuity like the contact
  * margin - from a real mismatch) */
+/* contact forces as the sensors see them scaled by s (test hook, 1 = off): the parity tests re-run
+ * the oracle with the forces moved by their comparison tolerance, so that an env whose outcome
+ * flips at a sensor force threshold (touchdown 10 N, is_contact 1 N, ...) within that tolerance
+ * is told from a real mismatch; the physics is unaffected */
+int zbo_set_sensor_force_scale(double s) {
+  g_sensor_force_scale = s > 0 ? s : 1.0;
+  return 0;
+}
+
 int zbo_set_gjk_tol(double tol) {
   g_gjk_tol = tol > 0 ? tol : GJK_TOL;
   return 0;
@@ -809,6 +818,24 @@ typedef struct {
   real applied_torque[ND]; /* Isaac Lab ImplicitActuator estimate at substep start */
 } substep_out_t;
 
+/* contact bias velocity: a speculative contact (sep >= 0) may close its gap within the step h it
+ * is solved for (PGS: the substep dt; TGS: the sub-iteration dt / iterations); a penetration is
+ * pushed out at baumgarte * depth per substep, capped at max_depenetration_velocity
+ * (zbot_cfg.py:633) */
+static real contact_bias(const zb_task_cfg* cfg, const mdl_t* m, real sep, real h, real dt) {
+  if (sep >= 0) return -sep / h;
+  real push = cfg->baumgarte * (-sep) / dt;
+  return push < m->max_depen ? push : m->max_depen;
+}
+static void clamp_speeds(const mdl_t* m, real u[NV]) {
+  for (int j = 0; j < ND; ++j) u[6 + j] = clampr(u[6 + j], -m->vlim, m->vlim);
+  real w2 = u[0] * u[0] + u[1] * u[1] + u[2] * u[2];
+  if (w2 > m->wmax * m->wmax) {
+    real sc = m->wmax / sqrtr(w2);
+    u[0] *= sc; u[1] *= sc; u[2] *= sc;
+  }
+}
+
 /* mu_link / mu_link_d: per-link static / dynamic friction (standup / manager DR; contact
  * coefficient = product, the ground's being cfg->friction / cfg->friction_dynamic), or NULL for
  * the cfg coefficients on every contact */
@@ -934,6 +961,13 @@ static void substep(const mdl_t* m, const zb_task_cfg* cfg, phys_t* s, const rea
   if (warm) *warm = CL; /* the next substep of this step warm-starts GJK from these normals */
   real Y[NC_MAX][3][NV];
   real invm[NC_MAX][3], vmin[NC_MAX], lam[NC_MAX][3], c01[NC_MAX], c02[NC_MAX], muc[NC_MAX], mud[NC_MAX];
+  /* TGS-style solve (cfg->solver_mode 1): solver_iterations sub-iterations of h = dt / iterations;
+   * sepc = each contact's separation advanced by h times its normal velocity after every
+   * sub-iteration (the bias re-linearised), wsum = the sum of the sub-iterations' w */
+  const int tgs = cfg->solver_mode == 1;
+  const real h = dt / (real)cfg->solver_iterations;
+  real sepc[NC_MAX], wsum[NV];
+  for (int a = 0; a < NV; ++a) wsum[a] = 0;
   int broken[NC_MAX];
   real dirs[NC_MAX][3][3];
   for (int c = 0; c < nc; ++c) {
@@ -941,9 +975,10 @@ static void substep(const mdl_t* m, const zb_task_cfg* cfg, phys_t* s, const rea
     for (int a = 0; a < 3; ++a) dirs[c][0][a] = ct->n[a];
     tangents(ct->n, dirs[c][1], dirs[c][2]);
     /* friction combine mode "multiply" (link x ground, link x link) */
-    muc[c] = mu_link ? mu_link[ct->la] * (ct->lb >= 0 ? mu_link[ct->lb] : (real)cfg->friction) : (real)cfg->friction;
     mud[c] = mu_link_d ? mu_link_d[ct->la] * (ct->lb >= 0 ? mu_link_d[ct->lb] : (real)cfg->friction_dynamic)
                        : (real)cfg->friction_dynamic;
+    muc[c] = mu_link ? mu_link[ct->la] * (ct->lb >= 0 ? mu_link[ct->lb] : (real)cfg->friction) : (real)cfg->friction;
+    if (muc[c] < mud[c]) muc[c] = mud[c]; /* static raised to dynamic (PhysX material combine) */
     for (int r = 0; r < 3; ++r) {
       real J[NV], Jb[NV];
       jac_row(&k, m->link_body[ct->la], ct->x, dirs[c][r], J);
@@ -960,17 +995,20 @@ static void substep(const mdl_t* m, const zb_task_cfg* cfg, phys_t* s, const rea
     c01[c] = 0; c02[c] = 0;
     broken[c] = 0;
     for (int a = 0; a < NV; ++a) { c01[c] += Y[c][1][a] * Y[c][0][a]; c02[c] += Y[c][2][a] * Y[c][0][a]; }
-    real sep = ct->sep;
-    if (sep >= 0) vmin[c] = -sep / dt;
-    else {
-      real push = cfg->baumgarte * (-sep) / dt;
-      vmin[c] = push < m->max_depen ? push : m->max_depen;
-    }
+    sepc[c] = ct->sep;
+    vmin[c] = contact_bias(cfg, m, sepc[c], tgs ? h : dt, dt);
   }
   /* Gauss-Seidel over contacts; the three row dots of a contact use the same w, the normal
    * update enters the tangent velocities through the cross terms c01 = Y1.Y0, c02 = Y2.Y0
    * (algebraically the sequential normal-then-friction update). */
   for (int it = 0; it < cfg->solver_iterations; ++it) {
+    if (tgs && it > 0)
+      for (int c = 0; c < nc; ++c) {
+        real vn = 0;
+        for (int a = 0; a < NV; ++a) vn += Y[c][0][a] * w[a];
+        sepc[c] += h * vn;
+        vmin[c] = contact_bias(cfg, m, sepc[c], h, dt);
+      }
     for (int c = 0; c < nc; ++c) {
       const real mu = muc[c];
       real vn = 0, v1 = 0, v2 = 0;
@@ -981,13 +1019,15 @@ static void substep(const mdl_t* m, const zb_task_cfg* cfg, phys_t* s, const rea
       real vt1 = v1 + c01[c] * dl, vt2 = v2 + c02[c] * dl;
       real l1 = lam[c][1] - vt1 * invm[c][1];
       real l2 = lam[c][2] - vt2 * invm[c][2];
-      /* static / dynamic Coulomb disk (PhysX patch friction): sticks while |l| <= mu_s ln; once
-       * the static cone is exceeded the contact is broken for the rest of this substep's sweeps
-       * and slides with |l| = mu_d ln (mu_d = mu_s: the plain disk projection) */
+      /* static / dynamic Coulomb disk (PhysX patch friction): sticks while |l| <= mu_s ln; once a
+       * loaded contact (ln > 0) exceeds the static cone it is broken for the rest of this
+       * substep's sweeps and slides with |l| = mu_d ln (mu_d = mu_s: the plain disk projection);
+       * an unloaded contact's friction is projected to 0 without breaking it */
       real mag2 = l1 * l1 + l2 * l2;
-      if (!broken[c] && mag2 > (mu * ln) * (mu * ln)) broken[c] = 1;
-      if (broken[c]) {
-        real lim = mud[c] * ln;
+      const int over = mag2 > (mu * ln) * (mu * ln);
+      if (!broken[c] && over && ln > 0) broken[c] = 1;
+      if (broken[c] || over) {
+        real lim = (broken[c] ? mud[c] : mu) * ln;
         if (mag2 > lim * lim) {
           real sc = lim / sqrtr(mag2);
           l1 *= sc; l2 *= sc;
@@ -997,9 +1037,14 @@ static void substep(const mdl_t* m, const zb_task_cfg* cfg, phys_t* s, const rea
       lam[c][0] = ln; lam[c][1] = l1; lam[c][2] = l2;
       for (int a = 0; a < NV; ++a) w[a] += Y[c][0][a] * dl + Y[c][1][a] * d1 + Y[c][2][a] * d2;
     }
+    for (int a = 0; a < NV; ++a) wsum[a] += w[a];
   }
-  real un[NV];
+  real un[NV], ua[NV]; /* the new velocity; the pose integrates ua (TGS: the sub-iterations' mean) */
   bwd_sub(L, w, un);
+  if (tgs) {
+    for (int a = 0; a < NV; ++a) wsum[a] /= (real)cfg->solver_iterations;
+    bwd_sub(L, wsum, ua);
+  }
 
   /* net contact force per link */
   for (int l = 0; l < NL; ++l) out->net_force[l][0] = out->net_force[l][1] = out->net_force[l][2] = 0;
@@ -1007,21 +1052,17 @@ static void substep(const mdl_t* m, const zb_task_cfg* cfg, phys_t* s, const rea
     const contact_t* ct = &CL.c[c];
     for (int a = 0; a < 3; ++a) {
       real F = (lam[c][0] * dirs[c][0][a] + lam[c][1] * dirs[c][1][a] + lam[c][2] * dirs[c][2][a]) / dt;
+      F *= (real)g_sensor_force_scale;
       out->net_force[ct->la][a] += F;
       if (ct->lb >= 0) out->net_force[ct->lb][a] -= F;
     }
   }
 
-  /* joint speed limit (PhysX max joint velocity = actuator velocity_limit) */
-  for (int j = 0; j < ND; ++j) un[6 + j] = clampr(un[6 + j], -m->vlim, m->vlim);
-  /* root link angular speed limit (RigidBodyPropertiesCfg.max_angular_velocity, zbot_cfg.py:632) */
-  {
-    real w2 = un[0] * un[0] + un[1] * un[1] + un[2] * un[2];
-    if (w2 > m->wmax * m->wmax) {
-      real sc = m->wmax / sqrtr(w2);
-      un[0] *= sc; un[1] *= sc; un[2] *= sc;
-    }
-  }
+  /* joint speed limit (PhysX max joint velocity = actuator velocity_limit) and root link angular
+   * speed limit (RigidBodyPropertiesCfg.max_angular_velocity, zbot_cfg.py:632), on both */
+  clamp_speeds(m, un);
+  if (tgs) clamp_speeds(m, ua);
+  else memcpy(ua, un, sizeof(un));
 
   /* semi-implicit Euler. u holds the root twist at the fixed point P; the root origin's
    * classical acceleration adds omega x v_P (spatial -> classical). */
@@ -1030,10 +1071,10 @@ static void substep(const mdl_t* m, const zb_task_cfg* cfg, phys_t* s, const rea
   for (int a = 0; a < 3; ++a) {
     s->root_angvel[a] = un[a];
     s->root_linvel[a] = un[3 + a] + dt * wv[a];
-    s->root_pos[a] += dt * s->root_linvel[a];
+    s->root_pos[a] += dt * (tgs ? ua[3 + a] + dt * wv[a] : s->root_linvel[a]);
   }
   {
-    real* om = s->root_angvel;
+    const real* om = ua;
     real th = sqrtr(om[0] * om[0] + om[1] * om[1] + om[2] * om[2]) * dt;
     real dq[4];
     if (th > (real)1e-12) {
@@ -1050,7 +1091,7 @@ static void substep(const mdl_t* m, const zb_task_cfg* cfg, phys_t* s, const rea
   }
   for (int j = 0; j < ND; ++j) {
     s->jqd[j] = un[6 + j];
-    real q = s->jq[j] + dt * s->jqd[j];
+    real q = s->jq[j] + dt * ua[6 + j];
     /* PhysX reports unlimited revolute joints wrapped to [-2pi, 2pi] (test_articulation.py:19-20) */
     if (q > (real)TWO_PI) q -= (real)(2 * TWO_PI);
     else if (q < -(real)TWO_PI) q += (real)(2 * TWO_PI);

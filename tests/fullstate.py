@@ -23,9 +23,29 @@ S, V4, SU, M = zm.S, zm.V4, zm.SU, zm.M
 TASKS = ("v2", "v4", "standup", "manager")
 
 
+SOLVER_MODE = 0  # zb_task_cfg.solver_mode of the configs below (tests switch it with solver_mode())
+
+
 def task_cfg(task: str) -> zm.TaskCfg:
-    return {"v2": zm.TaskCfg, "v4": zm.TaskCfg.walking_v4, "standup": zm.TaskCfg.standup,
-            "manager": zm.TaskCfg.manager_flat}[task]()
+    cfg = {"v2": zm.TaskCfg, "v4": zm.TaskCfg.walking_v4, "standup": zm.TaskCfg.standup,
+           "manager": zm.TaskCfg.manager_flat}[task]()
+    cfg.solver_mode = SOLVER_MODE
+    return cfg
+
+
+class solver_mode:
+    """Context manager: the task configs built inside use this contact solve mode."""
+
+    def __init__(self, mode: int):
+        self.mode = mode
+
+    def __enter__(self):
+        global SOLVER_MODE
+        self.prev, SOLVER_MODE = SOLVER_MODE, self.mode
+
+    def __exit__(self, *exc):
+        global SOLVER_MODE
+        SOLVER_MODE = self.prev
 
 
 def _rows(d: dict, name: str, k: int) -> list:

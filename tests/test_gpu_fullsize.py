@@ -1,16 +1,17 @@
 """BASELINE.json's full sizes (4096 envs = configs[1], 8192 = one GPU's shard of configs[2]'s 65 536,
 and 65 536 on one GPU) through the C ABI, checked by properties that do not depend on N:
 
-* sampled parity: one step of N envs on the GPU vs the CPU oracle run on a spread sample of the same
-  env columns (envs are independent, so a sample is an exact sub-problem) — covers the grid /
-  XCD-aware workgroup renumbering and the last partial workgroup at the real launch sizes;
+* full-state parity: one step of N envs from random full states on the GPU vs the CPU oracle run on
+  a spread sample of the same env columns (envs are independent, so a sample is an exact
+  sub-problem), every state row / obs / reward / flag under the explained-outlier rule of
+  tests/test_gpu_fullstate.py — covers the grid / XCD-aware workgroup renumbering and the last
+  partial workgroup at the real launch sizes (4096, 8192, 65 536);
 * permutation equivariance: permuting the env columns of the state and the action rows permutes every
   output bit-for-bit (no cross-env leakage between the 16-lane teams of a wave or between workgroups);
 * shard equivalence: the two halves of an N-env state stepped in two handles of N/2 give the same
   bits as one handle of N (what the env-sharded multi-GPU bench relies on);
 * determinism + sanity over a 100-step random-action rollout from a full reset: two handles with the
   same seed agree bit-for-bit, everything stays finite, episode lengths stay in [0, 999].
-Tolerances for the oracle comparison are the one-step bar of tests/test_gpu_parity.py.
 """
 from __future__ import annotations
 
@@ -44,30 +45,32 @@ def _sample(n, k=1024, seed=0):
     return np.array(sorted(ids), dtype=np.int64)
 
 
-@pytest.mark.parametrize("n", [4096, 65536])
-def test_full_size_sampled_parity(gpu, n):
-    from oracle.pyoracle import OracleSim
-    st = perturbed_states(n, seed=51, jq_sigma=0.15, jqd_sigma=0.5)
-    rng = np.random.default_rng(9)
-    a = rng.normal(size=(n, 6)).astype(np.float32)
-    g = _sim(n)
+@pytest.mark.parametrize("n", [4096, 8192, 65536])
+def test_full_state_headline_sizes(gpu, n):
+    """Walking v2 at BASELINE's sizes (4096 = configs[1], 8192 = one GPU's shard of configs[2],
+    65 536 on one GPU): one step of all n envs from random full states (every persistent row: sensor
+    histories, timers, feet latches, step lengths, integrators, episode sums), then every state row,
+    obs, reward and both flags of a spread sample of 1024 env columns against the oracle run on
+    those columns (envs are independent, so the sample is an exact sub-problem), under the
+    full-state rule of tests/test_gpu_fullstate.py: every env inside tolerance or explained."""
     import torch
+    import test_gpu_fullstate as F
+    from fullstate import random_states, task_cfg
+    from oracle.pyoracle import OracleSim
+    task, seed = "v2", 29
+    st = random_states(task, OracleSim(n, task_cfg(task), seed=seed), n, seed=300 + n)
+    a = np.random.default_rng(n).normal(size=(n, 6)).astype(np.float32)
+    g = _sim(n, seed=seed)
     g.set_state(torch.from_numpy(st).cuda())
-    obs_g, rew_g, te_g, tr_g = _step(g, a)
-    ids = _sample(n)
-    o = OracleSim(len(ids), zm.TaskCfg(), seed=0)
-    o.set_state(np.ascontiguousarray(st[:, ids]))
-    obs_o, rew_o, te_o, tr_o = o.step(np.ascontiguousarray(a[ids]))
-    assert (tr_g[ids] == tr_o).all()
-    assert (te_g[ids] == te_o).mean() >= 0.99
-    same = te_g[ids] == te_o
-    ok_obs = (np.abs(obs_g[ids] - obs_o) <= 5e-3 + 5e-3 * np.abs(obs_o)).all(axis=1)
-    assert ok_obs[same].mean() >= 0.99, ok_obs[same].mean()
-    ok_rew = np.abs(rew_g[ids] - rew_o) <= 2e-3 + 2e-3 * np.abs(rew_o)
-    assert ok_rew[same].mean() >= 0.99, ok_rew[same].mean()
+    obs, rew, te, tr = _step(g, a)
     sg = g.get_state().cpu().numpy()
-    np.testing.assert_array_equal(sg[S["EP_LEN"], ids][same], o.get_state()[S["EP_LEN"]][same])
     g.close()
+    ids = _sample(n)
+    sub = lambda x: np.ascontiguousarray(x[:, ids])  # noqa: E731
+    g_out = (np.ascontiguousarray(obs[ids]), rew[ids].copy(), te[ids].copy(), tr[ids].copy())
+    nbad = F._check(task, f"one step of {n} envs, sampled columns", len(ids), seed, sub(st),
+                    [np.ascontiguousarray(a[ids])], g_out, sub(sg), torch)
+    assert nbad <= 0.02 * len(ids)
 
 
 def test_permutation_equivariance_65536(gpu):

@@ -15,7 +15,7 @@ from __future__ import annotations
 import numpy as np
 import pytest
 
-from fullstate import TASKS, compare, perturb_physics, random_states, row_groups, task_cfg
+from fullstate import TASKS, compare, perturb_physics, random_states, row_groups, solver_mode, task_cfg
 
 pytestmark = pytest.mark.gpu
 K_SENS = 8
@@ -48,24 +48,39 @@ def _run_oracle(task, n, seed, st, actions, rng=None):
 
 
 def _sensitivity(task, n, seed, st, actions, so, obs_o, rew_o, fl_o, before, nsteps):
-    """Max over K perturbed oracle runs of each env's error ratio vs the unperturbed oracle, and over
+    """Max over K perturbed oracle runs of each env's error ratio vs the unperturbed oracle; over
     runs with GJK's stopping tolerance scaled by 1/4, 1/2, 2 and 4 (where GJK stops is a discontinuity of
     the self-contact normal, as the margin is of contact activation; the fp32 kernel and oracle can
-    stop one iteration apart)."""
+    stop one iteration apart); and over runs whose sensors see the contact forces scaled by 1 -+ 7 %
+    (the force comparison tolerance, 0.05 N + 2 %, at the 1 N is_contact threshold): an env whose
+    air / contact timers, touchdown latch, undesired-contact death or force-flagged reward terms flip
+    there sits at a sensor threshold the two sides' forces straddle within tolerance. Those runs
+    count the non-force rows only (the scaled forces themselves differ by design)."""
     from oracle.pyoracle import lib
     rng = np.random.default_rng(1234)
     sens = np.zeros(n)
-    runs = [(rng, None)] * K_SENS + [(None, t) for t in (0.25e-5, 0.5e-5, 2e-5, 4e-5)]
-    for r_, tol in runs:
+    runs = [(rng, None, None)] * K_SENS + [(None, t, None) for t in (0.25e-5, 0.5e-5, 2e-5, 4e-5)]
+    runs += [(None, None, s) for s in (0.93, 1.07)]
+    force_rows = row_groups(task)["force"]
+    for r_, tol, fs in runs:
         if tol is not None:
             lib().zbo_set_gjk_tol(tol)
+        if fs is not None:
+            lib().zbo_set_sensor_force_scale(fs)
         try:
             sk, outs = _run_oracle(task, n, seed, st, actions, r_)
         finally:
             if tol is not None:
                 lib().zbo_set_gjk_tol(0.0)
+            if fs is not None:
+                lib().zbo_set_sensor_force_scale(1.0)
         ob, rw, te, tr = outs[-1]
-        r, *_ = compare(task, sk, so, ob, obs_o, rw, rew_o, (te, tr), fl_o, before, nsteps)
+        r, rows, *_ = compare(task, sk, so, ob, obs_o, rw, rew_o, (te, tr), fl_o, before, nsteps)
+        if fs is not None:
+            rows = rows.copy()
+            rows[force_rows] = 0.0
+            r = np.maximum(rows.max(axis=0), np.abs(rw - rew_o) / (2e-3 + 2e-3 * np.abs(rew_o)))
+            r[(te != fl_o[0]) | (tr != fl_o[1])] = np.inf
         sens = np.maximum(sens, r)
     return sens
 
@@ -144,3 +159,60 @@ def test_full_state_zero_action_standing(gpu, task):
     sg = g.get_state().cpu().numpy()
     nbad = _check(task, f"{steps} zero-action steps from standing", n, seed, st, [a] * steps, g_out, sg, torch)
     assert nbad <= 0.05 * n
+
+
+def test_full_state_deep_overlap(gpu):
+    """One step from states whose links interpenetrate deeper than 2 CORE_M (the rounded cores
+    intersect): both sides take the centre-difference fallback normal at separation -2 CORE_M, so
+    away from the switch (the core distance crossing 1e-6, GJK's overlap tests) every row agrees
+    under the same explained-outlier rule; no state is set aside."""
+    from oracle.pyoracle import OracleSim
+    task, seed, pool = "v2", 31, 8192
+    o = OracleSim(pool, task_cfg(task), seed=seed)
+    st = random_states(task, o, pool, seed=404)
+    rng = np.random.default_rng(405)
+    st[13:19] += rng.normal(0, 0.6, (6, pool)).astype(np.float32)  # fold links into each other
+    o.set_state(st)
+    deep = np.nonzero(o.self_min_sep() <= -2 * 0.004 + 1e-6)[0]
+    assert len(deep) >= 512, len(deep)
+    ids = deep[:512]
+    n = len(ids)
+    st = np.ascontiguousarray(st[:, ids])
+    g, _, cfg, torch = _sims(task, n, seed)
+    g.set_state(torch.from_numpy(st).cuda())
+    a = np.random.default_rng(406).normal(size=(n, 6)).astype(np.float32)
+    obs, rew, te, tr = g.step(torch.from_numpy(a).cuda())
+    g_out = (obs.cpu().numpy(), rew.cpu().numpy(), te.cpu().numpy().copy(), tr.cpu().numpy().copy())
+    sg = g.get_state().cpu().numpy()
+    nbad = _check(task, "one step from deep self-overlap", n, seed, st, [a], g_out, sg, torch)
+    assert nbad <= 0.05 * n
+
+
+@pytest.mark.parametrize("task", ["v2", "standup"])
+def test_full_state_tgs(gpu, task):
+    """The TGS-style contact solve (zb_task_cfg.solver_mode 1: per-sub-iteration re-linearised
+    biases, pose from the mean sub-iteration velocity): one step from random full states and 20
+    zero-action steps from standing, every row under the same explained-outlier rule."""
+    with solver_mode(1):
+        n, seed = 2048, 19
+        g, o, cfg, torch = _sims(task, n, seed)
+        assert cfg.solver_mode == 1
+        st = random_states(task, o, n, seed=111)
+        g.set_state(torch.from_numpy(st).cuda())
+        a = np.random.default_rng(8).normal(size=(n, 6)).astype(np.float32)
+        obs, rew, te, tr = g.step(torch.from_numpy(a).cuda())
+        g_out = (obs.cpu().numpy(), rew.cpu().numpy(), te.cpu().numpy().copy(), tr.cpu().numpy().copy())
+        nbad = _check(task, "TGS: one step from random full states", n, seed, st, [a], g_out,
+                      g.get_state().cpu().numpy(), torch)
+        assert nbad <= 0.02 * n
+        n, seed, steps = 1024, 6, 20
+        g, o, cfg, torch = _sims(task, n, seed)
+        st = random_states(task, o, n, seed=212, standing=True)
+        g.set_state(torch.from_numpy(st).cuda())
+        at = torch.zeros(n, 6, device="cuda:0")
+        for _ in range(steps):
+            obs, rew, te, tr = g.step(at)
+        g_out = (obs.cpu().numpy(), rew.cpu().numpy(), te.cpu().numpy().copy(), tr.cpu().numpy().copy())
+        nbad = _check(task, f"TGS: {steps} zero-action steps from standing", n, seed, st,
+                      [np.zeros((n, 6), np.float32)] * steps, g_out, g.get_state().cpu().numpy(), torch)
+        assert nbad <= 0.05 * n

@@ -2,7 +2,7 @@
 uses -ffast-math, which folds isfinite away, so the kernels test the exponent bits of the physics
 state after the substeps. An env whose state went inf / NaN ends its episode as `died` with a
 finite reward and is reset; no other env is touched (compared bit for bit with a run that never
-had the bad envs).
+had the bad envs). All four step kernels (walking v2, stand-up, v4, manager).
 """
 from __future__ import annotations
 
@@ -13,7 +13,16 @@ from zbot_lab_amd import model as zm
 
 pytestmark = pytest.mark.gpu
 
-TASKS = {"walking": lambda: zm.TaskCfg(), "standup": lambda: zm.TaskCfg.standup()}
+TASKS = {"walking": lambda: zm.TaskCfg(), "standup": lambda: zm.TaskCfg.standup(),
+         "v4": lambda: zm.TaskCfg.walking_v4(), "manager": lambda: zm.TaskCfg.manager_flat()}
+
+
+def _penalty(task, cfg):
+    """The reward of a poisoned env: -terminal_penalty, or for the manager task its is_terminated
+    term alone (weight x step_dt)."""
+    if task == "manager":
+        return cfg.pack().stage_scales[0][zm.M_REWARD_TERMS.index("termination_penalty")] * cfg.sim_dt * cfg.decimation
+    return -cfg.terminal_penalty
 
 
 @pytest.mark.parametrize("task", sorted(TASKS))
@@ -37,7 +46,7 @@ def test_non_finite_state_is_reset(gpu, task):
     sb = bad.get_state().cpu().numpy()
     assert np.isfinite(ob).all() and np.isfinite(rb).all() and np.isfinite(sb).all()
     assert tb[poisoned].all(), "poisoned envs must terminate"
-    assert (rb[poisoned] == -cfg.terminal_penalty).all()
+    np.testing.assert_allclose(rb[poisoned], _penalty(task, cfg), rtol=1e-6)
     keep = np.setdiff1d(np.arange(n), poisoned)
     np.testing.assert_array_equal(ob[keep], oc[keep])
     np.testing.assert_array_equal(rb[keep], rc[keep])

@@ -77,13 +77,14 @@ def test_one_substep_parity(gpu, airborne):
     so = o.get_state()
     np.testing.assert_allclose(tau_g.cpu().numpy(), tau_o, rtol=1e-5, atol=1e-4)
     # random joint offsets interpenetrate links: states whose links overlap deeper than 2 CORE_M
-    # (the rounded cores intersect: the shape model's fallback normal) are set aside here and
-    # covered by the explained-outlier machinery of test_gpu_fullstate.py
+    # (the rounded cores intersect: the shape model's centre-difference fallback normal, 88 of the
+    # 512 states of this seed) get the bounded check at the end and the full-state check of
+    # test_gpu_fullstate.py::test_full_state_deep_overlap
     from oracle.pyoracle import OracleSim
     probe = OracleSim(n)
     probe.set_state(st)
     shallow = probe.self_min_sep() > -2 * 0.004 + 1e-4
-    assert shallow.mean() > 0.75, shallow.mean()
+    assert 0.80 <= shallow.mean() <= 0.86, shallow.mean()  # the state generator's observed mix
     vel = slice(S["ROOT_LINVEL"], S["JOINT_VEL"] + 6)
     dv = np.abs(sg[vel] - so[vel]) - (2e-3 + 1e-3 * np.abs(so[vel]))
     ok = (dv <= 0).all(axis=0)[shallow]
@@ -96,6 +97,14 @@ def test_one_substep_parity(gpu, airborne):
     fg = nf_g.cpu().numpy()
     okf = (np.abs(fg - nf_o) <= 0.05 + 0.02 * np.abs(nf_o)).all(axis=(1, 2))[shallow]
     assert okf.mean() >= 0.98, f"contact-force parity in {okf.mean():.4f} of envs"
+    # overlapping cores (both sides apply the same fallback: normal along the centre difference,
+    # separation -2 CORE_M): finite, the same links in contact, velocities within 5 cm/s + 5 %
+    deep = ~shallow
+    assert np.isfinite(sg[:, deep]).all()
+    sup = ((np.abs(fg) > 1e-3).any(axis=2) == (np.abs(nf_o) > 1e-3).any(axis=2)).all(axis=1)[deep]
+    assert sup.mean() >= 0.95, f"contact support agrees in {sup.mean():.3f} of the deep-overlap envs"
+    okd = (np.abs(sg[vel] - so[vel]) <= 5e-2 + 5e-2 * np.abs(so[vel])).all(axis=0)[deep]
+    assert okd.mean() >= 0.95, f"deep-overlap velocity agreement in {okd.mean():.3f} of envs"
 
 
 def test_four_substeps_parity(gpu):

@@ -67,12 +67,19 @@ constexpr int kStampCount0 = 13;  // slots 13, 14 count events (GJK calls, itera
 #ifdef ZB_STAMPS
 __device__ unsigned long long g_stamps[NSTAMP];
 __device__ unsigned long long g_stamp_slowest[NSTAMP];  // phase cycles of the slowest wave seen
+// per-launch wave histograms: [0, 64) the wave's largest number of GJK pairs of one env in one
+// substep; [64, 128) the wave's largest per-lane sum of GJK iterations over the step, in bins of 4
+__device__ unsigned long long g_stamp_hist[128];
 struct Stamps {
   unsigned long long t, acc[NSTAMP];
+  unsigned umax, itsum;
   __device__ void begin() {
     t = __builtin_amdgcn_s_memtime();
     for (int k = 0; k < NSTAMP; ++k) acc[k] = 0;
+    umax = 0; itsum = 0;
   }
+  __device__ void note_pairs(unsigned u) { umax = u > umax ? u : umax; }
+  __device__ void note_its(unsigned its) { itsum += its; }
   __device__ void mark(int k) {
     const unsigned long long n = __builtin_amdgcn_s_memtime();
     acc[k] += n - t;
@@ -85,6 +92,16 @@ struct Stamps {
       for (int k = 0; k < kStampCount0; ++k) atomicAdd(&g_stamps[k], acc[k]);
     for (int k = kStampCount0; k < NSTAMP - 1; ++k)
       if (acc[k]) atomicAdd(&g_stamps[k], acc[k]);
+    unsigned um = umax, im = itsum;
+    for (int o = 32; o > 0; o >>= 1) {
+      const unsigned a = __shfl_xor(um, o), b = __shfl_xor(im, o);
+      um = a > um ? a : um;
+      im = b > im ? b : im;
+    }
+    if ((threadIdx.x & 63) == 0) {
+      atomicAdd(&g_stamp_hist[um < 63 ? um : 63], 1ull);
+      atomicAdd(&g_stamp_hist[64 + (im / 4 < 63 ? im / 4 : 63)], 1ull);
+    }
     if ((threadIdx.x & 63) == 0) {  // slot NSTAMP - 1: the slowest wave's cycles over the launches
       unsigned long long tot = 0;
       for (int k = 0; k < kStampCount0; ++k) tot += acc[k];
@@ -99,6 +116,8 @@ struct Stamps {
   __device__ void begin() {}
   __device__ void mark(int) {}
   __device__ void count(int, unsigned) {}
+  __device__ void note_pairs(unsigned) {}
+  __device__ void note_its(unsigned) {}
   __device__ void flush() {}
 };
 #endif
@@ -499,7 +518,7 @@ constexpr int NCAND = NL * 4 + NSELF;
 //                            the trailing granule of a slot is zero (lanes d >= NV read it)
 //     STG   [EPW][STG_LEN] f32, LOGR [EPW][ACC] f32                              epilogue only
 //   region V
-//     UB    [NL][EPW]        world union spheres                                  detection only
+//     CAP   [NL][2][EPW]     world core capsules {circle centre, core radius}     detection only
 //     stash [WGT][2]         M rows of the joint columns (saturated drives)       Cholesky .. re-solve
 //     AUX   [NCM][2][EPW]    {invm0, invm1, invm2, vmin invm0}, {c01 invm1, c02 invm2, mu_s, mu_d}
 //     LAM   [NCM][EPW]       contact impulses {ln, l1, l2, 0}                     row write .. sensor
@@ -535,7 +554,7 @@ constexpr int AUX_OFF = V_OFF;
 constexpr int LAM_OFF = AUX_OFF + NCM * AUX_S;
 constexpr int FRC_OFF = LAM_OFF + NCM * LAM_S;
 constexpr int V_END = FRC_OFF + NCM * LAM_S;
-static_assert(NL * EPW <= NCM * AUX_S + NCM * LAM_S, "UB fits below FRC");
+static_assert(2 * NL * EPW <= NCM * AUX_S + NCM * LAM_S, "CAP fits below FRC");
 static_assert(2 * WGT <= NCM * AUX_S + NCM * LAM_S, "stash fits below FRC");
 constexpr int BODY_OFF = V_END;
 // per-body / per-joint strides padded by one granule: lane b of a team publishes body b (joint b),
@@ -585,7 +604,7 @@ struct Q {
   __device__ __forceinline__ float4& jnt(int j, int r) const { return b[JNT_OFF + j * JNT_S + r * EPW + e]; }
   __device__ __forceinline__ const float4* jtab(int j) const { return b + LNK_OFF + JT_OFF + j * 5; }
   __device__ __forceinline__ const float4* btab(int bb) const { return b + LNK_OFF + BT_OFF + bb * 3; }
-  __device__ __forceinline__ float4& ub(int l) const { return b[UB_OFF + l * EPW + e]; }
+  __device__ __forceinline__ float4& cap(int l, int k) const { return b[UB_OFF + (2 * l + k) * EPW + e]; }
   __device__ __forceinline__ const float4* link(int l) const { return gl + l * LINK4; }
   __device__ __forceinline__ int pair_code(int p) const { return reinterpret_cast<const int*>(b + LNK_OFF + NL * LINK4)[p]; }
   __device__ __forceinline__ const float4* dflt() const { return b + LNK_OFF + DFLT_OFF; }
@@ -893,6 +912,25 @@ __device__ __forceinline__ void gjk_tri(const float a[3], const float S[3][3], f
 // gap exceeds lim = margin + 2 kCoreM: the cores are farther apart than any contact. A rigorous
 // bound, so it never drops a contact that GJK would find; on random-action rollouts it decides
 // ~99 % of the broadphase pairs without iterating.
+// squared distance between the segments p0p1 and q0q1 (xyz of the float4s; closest points by the
+// clamped parameters of the two lines, segments of nonzero length)
+__device__ __forceinline__ float seg_seg_d2(const float4 p0, const float4 p1, const float4 q0, const float4 q1) {
+  const float d1[3] = {p1.x - p0.x, p1.y - p0.y, p1.z - p0.z};
+  const float d2[3] = {q1.x - q0.x, q1.y - q0.y, q1.z - q0.z};
+  const float r[3] = {p0.x - q0.x, p0.y - q0.y, p0.z - q0.z};
+  const float a = fmaxf(dot3(d1, d1), 1e-12f), e = fmaxf(dot3(d2, d2), 1e-12f);
+  const float b = dot3(d1, d2), c = dot3(d1, r), f = dot3(d2, r);
+  const float den = a * e - b * b;
+  float sc = den > 1e-12f * a * e ? clampf((b * f - c * e) / den, 0.f, 1.f) : 0.f;
+  float tc = (b * sc + f) / e;
+  const float s0 = clampf(-c / a, 0.f, 1.f), s1 = clampf((b - c) / a, 0.f, 1.f);
+  sc = tc < 0.f ? s0 : (tc > 1.f ? s1 : sc);
+  tc = clampf(tc, 0.f, 1.f);
+  float dd[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) dd[k] = r[k] + d1[k] * sc - d2[k] * tc;
+  return dot3(dd, dd);
+}
 __device__ __forceinline__ void hull_extent(const Hull& h, const float u[3], float& lo, float& hi) {
 #pragma unroll
   for (int ci = 0; ci < 2; ++ci) {
@@ -926,11 +964,12 @@ __device__ __forceinline__ bool hulls_separated(const Hull& A, const Hull& B, fl
 }
 // GJK (distance) on the core hulls A, B of a link pair, run by the 4 lanes of a DPP quad: lane j
 // holds circle (j & 1) of hull (j >> 1 ? B : A); the simplex is replicated bit-identically in the
-// 4 lanes. Simplex = the newest Minkowski point a plus up to three retained points S0..S2 (with
-// their A-side support points); each iteration takes the shortest of the valid affine projections
-// of the subsets containing a, first in the order {a}, {a,S0}, {a,S1}, {a,S0,S1}, {a,S2},
-// {a,S0,S2}, {a,S1,S2} (segments, triangles with positive barycentrics; the tetrahedron only as
-// the inside test). Per iteration lane j evaluates its circle's support point (the pair of lanes
+// 4 lanes. Simplex = up to three points S0..S2 (with their A-side support points; S0 = the
+// newest of the previous iteration); each iteration adds the support point a and takes the
+// shortest of the valid affine projections of the subsets containing a, first in the order {a},
+// {a,S0}, {a,S1}, {a,S0,S1}, {a,S2}, {a,S0,S2}, {a,S1,S2} (segments, triangles with positive
+// barycentrics; the tetrahedron only as the inside test); the new simplex is a, then the used
+// points in index order. Per iteration lane j evaluates its circle's support point (the pair of lanes
 // of one hull keeps the larger, circle 0 on ties) and two of the candidates (j = 0: {a}, {a,S0};
 // 1: {a,S1}, {a,S0,S1}; 2: {a,S2}, {a,S0,S2}; 3: {a,S1,S2}); two DPP butterfly steps pick the
 // first shortest in that order. ~2x fewer instructions per iteration than one lane per pair, and
@@ -1010,40 +1049,35 @@ __device__ __forceinline__ bool gjk_quad(const QCircle& h, int j, const float v0
                                          SelfContact& out, int& iters) {
   float v[3] = {v0[0], v0[1], v0[2]};
   const float lim = early_margin + 2.f * kCoreM;
-  float S[3][3] = {}, SP[3][3] = {}, lam[4] = {1.f, 0.f, 0.f, 0.f};
-  float ap[3] = {}, aw[3] = {};  // newest point (A support, Minkowski point)
-  int n = -1;          // retained points (-1: the first point not yet taken)
+  // simplex S0..S2 (n points; S0 = the newest of the previous iteration) with their A-side
+  // support points SP and the weights lam of v = sum lam_i S_i
+  float S[3][3] = {}, SP[3][3] = {}, lam[3] = {1.f, 0.f, 0.f};
+  int n = 0;
   bool overlap = false;
   for (int it = 0; it <= kGjkMaxIt; ++it) {
     iters = it;
     const float vv = dot3(v, v);
-    if (n >= 0 && vv < 1e-12f) { overlap = true; break; }
-    float pa[3], pb[3], w[3];
-    quad_support(h, v, j, pa, pb);
+    if (n > 0 && vv < 1e-12f) { overlap = true; break; }
+    float pa[3], aw[3];
+    {
+      float pb[3];
+      quad_support(h, v, j, pa, pb);
 #pragma unroll
-    for (int k = 0; k < 3; ++k) w[k] = pa[k] - pb[k];
-    if (n < 0) {  // first point
+      for (int k = 0; k < 3; ++k) aw[k] = pa[k] - pb[k];
+    }
+    if (n == 0) {  // first point
 #pragma unroll
-      for (int k = 0; k < 3; ++k) { aw[k] = w[k]; ap[k] = pa[k]; v[k] = w[k]; }
-      n = 0;
+      for (int k = 0; k < 3; ++k) { S[0][k] = aw[k]; SP[0][k] = pa[k]; v[k] = aw[k]; }
+      n = 1;
       continue;
     }
-    const float vw = dot3(v, w);
+    const float vw = dot3(v, aw);
     if (vw > 0.f && vw * vw > vv * lim * lim) return false;
     if (vv - vw <= kGjkTol * sqrtf(vv)) break;  // distance bounds within kGjkTol
-    // retire the current newest point into the retained set (slot n), take w as the newest
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      S[2][k] = n == 2 ? aw[k] : S[2][k]; SP[2][k] = n == 2 ? ap[k] : SP[2][k];
-      S[1][k] = n == 1 ? aw[k] : S[1][k]; SP[1][k] = n == 1 ? ap[k] : SP[1][k];
-      S[0][k] = n == 0 ? aw[k] : S[0][k]; SP[0][k] = n == 0 ? ap[k] : SP[0][k];
-      aw[k] = w[k]; ap[k] = pa[k];
-    }
-    ++n;
-    // this lane's candidates: the segment {a, S_j} (j < 3) and the triangle {a, S_I, S_J}
-    // (j = 1: I, J = 0, 1; j = 2: 0, 2; j = 3: 1, 2); lane 0 starts from {a}
+    // this lane's candidates with the new point a = aw: the segment {a, S_j} (j < 3) and the
+    // triangle {a, S_I, S_J} (j = 1: I, J = 0, 1; j = 2: 0, 2; j = 3: 1, 2); lane 0 starts from {a}
     float best = j == 0 ? dot3(aw, aw) : 3.0e38f, bv[3] = {aw[0], aw[1], aw[2]}, l1 = 0.f, l2 = 0.f;
-    unsigned bm = 0u;  // retained points used (bit i: S_i)
+    unsigned bm = 0u;  // simplex points used (bit i: S_i)
     {
       float e[3];
 #pragma unroll
@@ -1107,27 +1141,22 @@ __device__ __forceinline__ bool gjk_quad(const QCircle& h, int j, const float v0
         if (b0 > 1e-5f && b1 > 1e-5f && b2 > 1e-5f && b0 + b1 + b2 < 1.f - 1e-5f) { overlap = true; break; }
       }
     }
-    // new simplex: the newest point + the used retained points (in index order)
+    // new simplex: a first, then the used points in index order
     const int nu = __popc(bm);
-    float T1[3], T1p[3], T2[3], T2p[3];
     const bool u0 = bm & 1u, u1 = (bm >> 1) & 1u;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      T1[k] = u0 ? S[0][k] : (u1 ? S[1][k] : S[2][k]);
-      T1p[k] = u0 ? SP[0][k] : (u1 ? SP[1][k] : SP[2][k]);
-      T2[k] = (u0 && u1) ? S[1][k] : S[2][k];
-      T2p[k] = (u0 && u1) ? SP[1][k] : SP[2][k];
-    }
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      S[0][k] = T1[k]; SP[0][k] = T1p[k];
-      S[1][k] = T2[k]; SP[1][k] = T2p[k];
+      const float t1 = u0 ? S[0][k] : (u1 ? S[1][k] : S[2][k]), t1p = u0 ? SP[0][k] : (u1 ? SP[1][k] : SP[2][k]);
+      const float t2 = (u0 && u1) ? S[1][k] : S[2][k], t2p = (u0 && u1) ? SP[1][k] : SP[2][k];
+      S[2][k] = t2; SP[2][k] = t2p;
+      S[1][k] = t1; SP[1][k] = t1p;
+      S[0][k] = aw[k]; SP[0][k] = pa[k];
       v[k] = bv[k];
     }
     lam[1] = nu >= 1 ? l1 : 0.f;
     lam[2] = nu >= 2 ? l2 : 0.f;
     lam[0] = 1.f - lam[1] - lam[2];
-    n = nu;
+    n = nu + 1;
   }
   // one exit (a struct written on two paths ends up in scratch memory)
   const float d = sqrtf(dot3(v, v));
@@ -1142,7 +1171,7 @@ __device__ __forceinline__ bool gjk_quad(const QCircle& h, int j, const float v0
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     // closest point on A's core: the same weights over the A-side support points
-    const float pa = lam[0] * ap[k] + (n >= 1 ? lam[1] * SP[0][k] : 0.f) + (n >= 2 ? lam[2] * SP[1][k] : 0.f);
+    const float pa = lam[0] * SP[0][k] + (n >= 2 ? lam[1] * SP[1][k] : 0.f) + (n >= 3 ? lam[2] * SP[2][k] : 0.f);
     const float nd = nodir ? (k == 2 ? 1.f : 0.f) : dv[k] * idn;
     out.n[k] = deep ? nd : v[k] * id;
     out.x[k] = deep ? 0.5f * (ca[k] + cb[k]) : pa - 0.5f * v[k];
@@ -1170,12 +1199,6 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q&
     float R[9], p[3];
     read_frame(q, link_body(l), R, p);
     const float4* L = q.link(l);
-    {
-      const float4 us = L[9];
-      float c[3];
-      mv3f(R, us, c);
-      if (q.s < NL) q.ub(l) = make_float4(c[0] + p[0], c[1] + p[1], c[2] + p[2], us.w);
-    }
     const float4 bd = L[0];
     float bc[3];
     mv3f(R, bd, bc);
@@ -1237,17 +1260,30 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q&
   // writes them, re-running GJK only for a lane's second and later contacts. One GJK call site.
   int s_tot = 0;
   if (cfg.enable_self_collision) {
-    wave_sync();  // union spheres
+    // lane l builds link l's world core hull once; its two circle centres + core radius are the
+    // link's capsule (broadphase), the pair tests below gather the hulls with ds_bpermute
+    Hull lh;
+    world_hull(q, q.s < NL ? q.s : NL - 1, lh);
+    if (q.s < NL) {
+      const float rc = q.link(q.s)[2].w;
+      q.cap(q.s, 0) = make_float4(lh.c[0][0], lh.c[0][1], lh.c[0][2], rc);
+      q.cap(q.s, 1) = make_float4(lh.c[1][0], lh.c[1][1], lh.c[1][2], rc);
+    }
+    wave_sync();  // capsules
+    // broadphase: capsule (segment of the core circle centres, radius = the larger core radius)
+    // distance within margin + 2 kCoreM; conservative, so it changes which pairs are tested, never
+    // which contacts are found (~13 of the 55 pairs pass on random-action rollouts: one round of
+    // separating-axis tests instead of two with bounding spheres)
     unsigned long long mask = 0ull;
 #pragma unroll
     for (int j = 0; j < PAIRS_PER_LANE; ++j) {
       const int pidx = PAIRS_PER_LANE * q.s + j;
       if (pidx < NPAIR) {
         const int code = q.pair_code(pidx);
-        const float4 A = q.ub(code >> 4), B = q.ub(code & 15);
-        const float d0 = A.x - B.x, d1 = A.y - B.y, d2 = A.z - B.z;
-        const float rr = A.w + B.w + margin;
-        if (d0 * d0 + d1 * d1 + d2 * d2 <= rr * rr) mask |= 1ull << pidx;
+        const float4 A0 = q.cap(code >> 4, 0), A1 = q.cap(code >> 4, 1);
+        const float4 B0 = q.cap(code & 15, 0), B1 = q.cap(code & 15, 1);
+        const float rr = A0.w + B0.w + margin + 2.f * kCoreM + 1e-5f;
+        if (seg_seg_d2(A0, A1, B0, B1) <= rr * rr) mask |= 1ull << pidx;
       }
     }
     {
@@ -1264,11 +1300,9 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q&
     const unsigned long long bmask = mask;
     unsigned undecided = 0u;  // bit k: this lane's pair of round k needs GJK
     {
-      // lane l builds link l's world hull once; the pair tests gather both hulls from the link
-      // lanes with ds_bpermute (no per-pair frame reads, link-table loads or rotations). The
-      // loop runs the wave's largest round count so every lane takes part in each permute.
-      Hull own;
-      world_hull(q, q.s < NL ? q.s : NL - 1, own);
+      // the pair tests gather both hulls from the link lanes with ds_bpermute (no per-pair frame
+      // reads, link-table loads or rotations). The loop runs the wave's largest round count so
+      // every lane takes part in each permute.
       const int rounds_w = max(max(__builtin_amdgcn_readlane(rounds, 0), __builtin_amdgcn_readlane(rounds, TL)),
                                max(__builtin_amdgcn_readlane(rounds, 2 * TL), __builtin_amdgcn_readlane(rounds, 3 * TL)));
       const int base = q.lane & ~(TL - 1);
@@ -1277,8 +1311,8 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q&
         const bool valid = r < K;
         const int pcode = valid ? q.pair_code(nth_set_bit(bmask, r)) : 0x01;
         Hull A, B;
-        gather_hull(own, 4 * (base + (pcode >> 4)), A);
-        gather_hull(own, 4 * (base + (pcode & 15)), B);
+        gather_hull(lh, 4 * (base + (pcode >> 4)), A);
+        gather_hull(lh, 4 * (base + (pcode & 15)), B);
         if (valid && !hulls_separated(A, B, margin + 2.f * kCoreM)) undecided |= 1u << k;
       }
     }
@@ -1296,6 +1330,7 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q&
       und = (unsigned long long)(unsigned)lo | ((unsigned long long)(unsigned)hi << 32);
     }
     const int U = __popcll(und);
+    sp.note_pairs(U);
     const int qd = q.s >> 2, qj = q.s & 3;  // quad of the team, lane in the quad
     const int urounds = (U + 3) >> 2;
     SelfContact hit0 = {};  // this quad's first contact is kept for the write pass
@@ -1338,6 +1373,7 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q&
             sp.count(kStampCount0, 1);
             sp.count(kStampCount0 + 1, its);
           }
+          sp.note_its(its);
           if (pass == 0 && h) {
             if (own == 0u) { hit0 = sc; hit0_k = k; }
             own |= 1u << k;
@@ -1571,11 +1607,13 @@ __device__ __forceinline__ float4 pgs_update(const float4 g, const float4 a0, co
   float l1 = fmaf(-a1.x, dl, u1);
   float l2 = fmaf(-a1.y, dl, u2);
   // static / dynamic Coulomb disk (PhysX's patch friction): the contact sticks while |l| <= mu ln;
-  // once the static cone is exceeded it is "broken" (lam.w = 1) for the rest of the substep's
-  // sweeps and slides with |l| = mu_d ln (mu_d = mu: the plain projection min(1, mu ln / |l|))
+  // once a loaded contact (ln > 0) exceeds the static cone it is "broken" (lam.w = 1) for the rest
+  // of the substep's sweeps and slides with |l| = mu_d ln (mu_d = mu: the plain projection
+  // min(1, mu ln / |l|)); an unloaded contact's friction is 0 without breaking it
   const float ri = __builtin_amdgcn_rsqf(fmaxf(fmaf(l1, l1, l2 * l2), 1e-30f));
-  const bool brk = lam.w != 0.f || (mu * ln * ri < 1.f);
-  const float lim = brk ? mu_d * ln * ri : 1.f;
+  const bool over = mu * ln * ri < 1.f;
+  const bool brk = lam.w != 0.f || (over && ln > 0.f);
+  const float lim = brk ? mu_d * ln * ri : (over ? mu * ln * ri : 1.f);
   const float sc = fminf(lim, 1.f);
   l1 *= sc;
   l2 *= sc;
@@ -1648,10 +1686,28 @@ __device__ __forceinline__ void team_fwd(const float R[NV], const float inv[NV],
   if constexpr (K + 1 < KE) team_fwd<K + 1, KE>(R, inv, t, z, wd, s);
 }
 
+// contact bias velocity: a speculative contact (sep >= 0) may close its gap within the step h it
+// is solved for (PGS: the substep dt; TGS: the sub-iteration dt / iterations); a penetration is
+// pushed out at baumgarte * depth per substep, capped at max_depenetration_velocity
+// (zbot_cfg.py:633). Same as the oracle's contact_bias.
+__device__ __forceinline__ float contact_bias(const zb_task_cfg& cfg, MP m, float sep, float h, float dt) {
+  return sep >= 0.f ? -sep / h : fminf(cfg.baumgarte * (-sep) / dt, m->max_depenetration_velocity);
+}
+// joint speed clamp (actuator velocity_limit) and root link angular speed limit (rigid props
+// max_angular_velocity; PhysX scales the vector)
+__device__ __forceinline__ void clamp_speeds(MP m, float u[NV]) {
+#pragma unroll
+  for (int j = 0; j < ND; ++j) u[6 + j] = clampf(u[6 + j], -m->velocity_limit, m->velocity_limit);
+  const float w2 = u[0] * u[0] + u[1] * u[1] + u[2] * u[2];
+  const float wmax = m->max_angular_velocity;
+  const float sc = w2 > wmax * wmax ? wmax * __builtin_amdgcn_rsqf(w2) : 1.f;
+  u[0] *= sc; u[1] *= sc; u[2] *= sc;
+}
+
 // ------------------------------------------------------------------------- one substep
 // kLinkFriction: per-contact Coulomb coefficient from the per-link table q.fric (standup DR);
 // otherwise cfg.friction everywhere.
-template <bool kDebugForces, bool kLinkFriction>
+template <bool kDebugForces, bool kLinkFriction, bool kTgs>
 __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
                                         const float target[ND], const Q& q, bool last, bool warm, SensorOut& so,
                                         float (*dbgF)[3], float* dbgTau, Stamps& sp) {
@@ -1850,6 +1906,12 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
   // [x x d ; d ; d.(a_j x (x - o_j)) for joints j < b]
   // The candidates share storage with the rows (region U): every lane reads its candidate, then
   // the wave writes. The normal + code go to FRC for the contact sensor.
+  // TGS-style solve (cfg.solver_mode 1): solver_iterations sub-iterations of h = dt / iterations,
+  // each one sweep whose biases come from the contact's separation advanced by h times its normal
+  // velocity after the previous sub-iteration; lane c keeps slot c's separation in sep_own
+  constexpr bool tgs = kTgs;
+  const float hsub = dt / (float)cfg.solver_iterations;
+  float sep_own = 0.f;
   if (q.s < nc) {
     const int c = q.s;
     const int pos = over ? q.map(c) : c;
@@ -1897,13 +1959,14 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
     }
 #pragma unroll
     for (int d = 0; d < NV; ++d) q.yg_at(c, own_lane(d)) = make_float4(Y[0][d], Y[1][d], Y[2][d], 0.f);
-    float vmin;
-    if (sep >= 0.f) vmin = -sep / dt;
-    else vmin = fminf(cfg.baumgarte * (-sep) / dt, m->max_depenetration_velocity);
+    sep_own = sep;
+    const float vmin = contact_bias(cfg, m, sep, tgs ? hsub : dt, dt);
     q.aux(c, 0) = make_float4(invm[0], invm[1], invm[2], vmin * invm[0]);
     // friction combine mode "multiply": ground (terrain coefficient) x link, link x link
-    const float mu_c = kLinkFriction ? q.fric(code >> 4) * (lb >= 0 ? q.fric(lb) : cfg.friction) : 0.f;
+    // (the static coefficient is raised to the dynamic one where the independent DR draws put it
+    // below, as PhysX's material combine does)
     const float mu_cd = kLinkFriction ? q.fricd(code >> 4) * (lb >= 0 ? q.fricd(lb) : cfg.friction_dynamic) : 0.f;
+    const float mu_c = kLinkFriction ? fmaxf(q.fric(code >> 4) * (lb >= 0 ? q.fric(lb) : cfg.friction), mu_cd) : 0.f;
     q.aux(c, 1) = make_float4(dot12(Y[1], Y[0]) * invm[1], dot12(Y[2], Y[0]) * invm[2], mu_c, mu_cd);
     q.lam(c) = make_float4(0.f, 0.f, 0.f, 0.f);
   }
@@ -1927,17 +1990,32 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
   // projected Gauss-Seidel on the whitened velocity (Coulomb disk friction); lane s owns
   // coordinate own_row(s) of w (its granule of every contact row holds that coordinate).
   float w[NV];
+  float wsum_own;  // TGS: this lane's coordinate of the sub-iterations' mean w
   // Sweeps outer, the NCM slots unrolled inner: constant LDS offsets, slot c + 1's granules read
   // while slot c updates, slots c >= the wave's largest contact count skipped uniformly, the
   // slots between an env's own count and that maximum are no-op updates (zeroed above). The
   // impulses are team-uniform (every lane computes the same update); the team lead stores them.
   {
-    const float mu = cfg.friction, mu_d = cfg.friction_dynamic;
+    const float mu_d = cfg.friction_dynamic, mu = fmaxf(cfg.friction, mu_d);
     const float4* yl = q.b + YG_OFF + q.ygl();
     const int ncw = max(max(__builtin_amdgcn_readlane(nc, 0), __builtin_amdgcn_readlane(nc, TL)),
                         max(__builtin_amdgcn_readlane(nc, 2 * TL), __builtin_amdgcn_readlane(nc, 3 * TL)));
     const bool lead = q.s == 0;
+    float wsum = 0.f;  // TGS: the sum of the sub-iterations' w (this lane's coordinate)
     for (int it = 0; it < cfg.solver_iterations; ++it) {
+      if (tgs && it > 0) {  // re-linearise the biases
+#pragma unroll
+        for (int c = 0; c < NCM; ++c)
+          if (c < ncw) {
+            const float vn = tsum(q.yg(yl, c).x * wd);
+            sep_own = q.s == c ? fmaf(hsub, vn, sep_own) : sep_own;
+          }
+        if (q.s < nc) {
+          const float4 a0 = q.aux(q.s, 0);
+          q.aux(q.s, 0) = make_float4(a0.x, a0.y, a0.z, contact_bias(cfg, m, sep_own, hsub, dt) * a0.x);
+        }
+        wave_sync();
+      }
       float4 G = q.yg(yl, 0), X = q.aux(0, 0), Z = q.aux(0, 1), La = q.lam(0);
 #pragma unroll
       for (int c = 0; c < NCM; ++c) {
@@ -1949,11 +2027,13 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
         }
         G = Gn; X = Xn; Z = Zn; La = Ln;
       }
+      wsum += wd;
     }
     w[0] = tb<own_lane(0)>(wd); w[1] = tb<own_lane(1)>(wd); w[2] = tb<own_lane(2)>(wd);
     w[3] = tb<own_lane(3)>(wd); w[4] = tb<own_lane(4)>(wd); w[5] = tb<own_lane(5)>(wd);
     w[6] = tb<own_lane(6)>(wd); w[7] = tb<own_lane(7)>(wd); w[8] = tb<own_lane(8)>(wd);
     w[9] = tb<own_lane(9)>(wd); w[10] = tb<own_lane(10)>(wd); w[11] = tb<own_lane(11)>(wd);
+    wsum_own = wsum * (1.f / (float)cfg.solver_iterations);
   }
   wave_sync();  // last impulses visible to every lane
   sp.mark(6);
@@ -1990,34 +2070,39 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
     if (kDebugForces) { dbgF[0][0] = Fl[0]; dbgF[0][1] = Fl[1]; dbgF[0][2] = Fl[2]; }
   }
 
-#pragma unroll
-  for (int j = 0; j < ND; ++j) un[6 + j] = clampf(un[6 + j], -m->velocity_limit, m->velocity_limit);
-  {  // root link angular speed limit (rigid props max_angular_velocity; PhysX scales the vector)
-    const float w2 = un[0] * un[0] + un[1] * un[1] + un[2] * un[2];
-    const float wmax = m->max_angular_velocity;
-    const float sc = w2 > wmax * wmax ? wmax * __builtin_amdgcn_rsqf(w2) : 1.f;
-    un[0] *= sc; un[1] *= sc; un[2] *= sc;
-  }
-
-  // semi-implicit Euler (root twist at P -> classical root-origin velocity adds omega x v dt)
+  clamp_speeds(m, un);
+  // semi-implicit Euler (root twist at P -> classical root-origin velocity adds omega x v dt): the
+  // new velocity, then the pose integrated with the pose velocity (PGS: the new velocity; TGS:
+  // the mean of the sub-iterations' velocities, u = L^-T of the mean w)
   float wv[3];
   cross3(s.av, s.lv, wv);
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
     s.av[a] = un[a];
     s.lv[a] = un[3 + a] + dt * wv[a];
-    s.pos[a] += dt * s.lv[a];
   }
+#pragma unroll
+  for (int j = 0; j < ND; ++j) s.jqd[j] = un[6 + j];
+  if (tgs) {
+    w[0] = tb<own_lane(0)>(wsum_own); w[1] = tb<own_lane(1)>(wsum_own); w[2] = tb<own_lane(2)>(wsum_own);
+    w[3] = tb<own_lane(3)>(wsum_own); w[4] = tb<own_lane(4)>(wsum_own); w[5] = tb<own_lane(5)>(wsum_own);
+    w[6] = tb<own_lane(6)>(wsum_own); w[7] = tb<own_lane(7)>(wsum_own); w[8] = tb<own_lane(8)>(wsum_own);
+    w[9] = tb<own_lane(9)>(wsum_own); w[10] = tb<own_lane(10)>(wsum_own); w[11] = tb<own_lane(11)>(wsum_own);
+    bwd_sub(L, Li, w, un);
+    clamp_speeds(m, un);
+  }
+#pragma unroll
+  for (int a = 0; a < 3; ++a) s.pos[a] += dt * (un[3 + a] + dt * wv[a]);
   {
-    const float th = sqrtf(s.av[0] * s.av[0] + s.av[1] * s.av[1] + s.av[2] * s.av[2]) * dt;
+    const float th = sqrtf(un[0] * un[0] + un[1] * un[1] + un[2] * un[2]) * dt;
     float dq[4];
     if (th > 1e-12f) {
       float sn, cs;
       sincos_r(0.5f * th, &sn, &cs);
       const float sc = sn / th * dt;
-      dq[0] = cs; dq[1] = s.av[0] * sc; dq[2] = s.av[1] * sc; dq[3] = s.av[2] * sc;
+      dq[0] = cs; dq[1] = un[0] * sc; dq[2] = un[1] * sc; dq[3] = un[2] * sc;
     } else {
-      dq[0] = 1.f; dq[1] = 0.5f * dt * s.av[0]; dq[2] = 0.5f * dt * s.av[1]; dq[3] = 0.5f * dt * s.av[2];
+      dq[0] = 1.f; dq[1] = 0.5f * dt * un[0]; dq[2] = 0.5f * dt * un[1]; dq[3] = 0.5f * dt * un[2];
     }
     float qn[4];
     qmul(dq, s.quat, qn);
@@ -2026,8 +2111,7 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
   }
 #pragma unroll
   for (int j = 0; j < ND; ++j) {
-    s.jqd[j] = un[6 + j];
-    float qv = s.jq[j] + dt * s.jqd[j];
+    float qv = s.jq[j] + dt * un[6 + j];
     if (qv > TWO_PI_F) qv -= 2.f * TWO_PI_F;
     else if (qv < -TWO_PI_F) qv += 2.f * TWO_PI_F;
     s.jq[j] = qv;
@@ -2399,6 +2483,7 @@ __device__ __forceinline__ void load_phys(const float* __restrict__ st, int N, i
 // One policy step per lane. Live state across the 4 substeps is kept to the physics state, the
 // joint targets and the ~15 floats of the lagged observation cache the rewards need; the MDP
 // state is loaded from HBM only after the physics.
+template <bool kTgs>
 __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_step_kernel(const zb_model* __restrict__ mg,
                                                           const float4* __restrict__ links, zb_task_cfg cfg, int N,
                                                           float* __restrict__ st, const float* __restrict__ act,
@@ -2485,7 +2570,7 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_step_kernel(const z
   sp.mark(0);
   for (int k = 0; k < cfg.decimation; ++k) {
     // (a compile-time `true` here lets the scheduler reshape the loop into a 36 B/lane spill)
-    substep<false, false>(m, cfg, p, target, q, opaque_true(), k > 0, so, nullptr, nullptr, sp);
+    substep<false, false, kTgs>(m, cfg, p, target, q, opaque_true(), k > 0, so, nullptr, nullptr, sp);
     sens_record(q, k, so);
     sp.mark(7);
   }
@@ -2806,7 +2891,7 @@ __global__ void zb_observe_kernel(const zb_model* __restrict__ mg, int N, const 
   write_obs(m, p, d, obs, i);
 }
 
-template <bool kLinkFriction>
+template <bool kLinkFriction, bool kTgs>
 __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_substeps_kernel(const zb_model* __restrict__ mg,
                                                               const float4* __restrict__ links, zb_task_cfg cfg, int N,
                                                               float* __restrict__ st, const float* __restrict__ targets,
@@ -2832,7 +2917,7 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_substeps_kernel(con
   for (int j = 0; j < ND; ++j) { tg[j] = targets[(size_t)i * ND + j]; tau[j] = 0.f; }
   SensorOut so;
   Stamps sp;
-  for (int k = 0; k < nsub; ++k) substep<true, kLinkFriction>(m, cfg, p, tg, q, k == nsub - 1, k > 0, so, F, tau, sp);
+  for (int k = 0; k < nsub; ++k) substep<true, kLinkFriction, kTgs>(m, cfg, p, tg, q, k == nsub - 1, k > 0, so, F, tau, sp);
   if (net_force && q.s < NL)
 #pragma unroll
     for (int a = 0; a < 3; ++a) net_force[((size_t)i * NL + q.s) * 3 + a] = F[0][a];
@@ -2924,6 +3009,7 @@ __device__ __forceinline__ void su_reset_pose(MP m, const zb_task_cfg& cfg, uint
 }
 
 // One stand-up policy step per team (same mapping as zb_step_kernel; no contact sensor).
+template <bool kTgs>
 __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_su_step_kernel(
     const zb_model* __restrict__ mg, const float4* __restrict__ links, zb_task_cfg cfg, int N, float* __restrict__ st,
     const float* __restrict__ act, float* __restrict__ obs, float* __restrict__ rew, uint8_t* __restrict__ term,
@@ -2969,7 +3055,7 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_su_step_kernel(
   SensorOut so;
   sp.mark(0);
   for (int k = 0; k < cfg.decimation; ++k) {
-    substep<false, true>(m, cfg, p, target, q, false, k > 0, so, nullptr, nullptr, sp);
+    substep<false, true, kTgs>(m, cfg, p, target, q, false, k > 0, so, nullptr, nullptr, sp);
     sp.mark(7);
   }
   m = opaque(m);
@@ -3223,6 +3309,7 @@ struct PreV4 {
 };
 static_assert(sizeof(PreV4) <= 16 * PRE4, "PreV4 fits PRE4 granules");
 
+template <bool kTgs>
 __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_v4_step_kernel(
     const zb_model* __restrict__ mg, const float4* __restrict__ links, zb_task_cfg cfg, int N, float* __restrict__ st,
     const float* __restrict__ act, float* __restrict__ obs, float* __restrict__ rew, uint8_t* __restrict__ term,
@@ -3284,7 +3371,7 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_v4_step_kernel(
 #pragma unroll
       for (int j = 0; j < ND; ++j) pv.jqd_prev[j] = p.jqd[j];
     }
-    substep<false, false>(m, cfg, p, target, q, true, k > 0, so, nullptr, nullptr, sp);
+    substep<false, false, kTgs>(m, cfg, p, target, q, true, k > 0, so, nullptr, nullptr, sp);
     sens_record(q, k, so);
     sp.mark(7);
   }
@@ -3361,6 +3448,8 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_v4_step_kernel(
     died = fm > cfg.undesired_force_threshold || base_z < cfg.termination_height;
   }
   const bool time_out = ep_len >= (float)(cfg.max_episode_length - 1);
+  const bool blowup = phys_bad(p);  // non-finite guard (phys_bad), as in the walking kernel
+  died |= blowup;
   float cur_yaw = atan2f(fwd[1], fwd[0]);
   float he;
   {
@@ -3444,6 +3533,11 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_v4_step_kernel(
     sums[t] = sums0[t] + v;
   }
   if (died) reward -= cfg.terminal_penalty;  // v4.py:892-893
+  if (blowup) {  // finite reward, the episode sums without this step
+    reward = -cfg.terminal_penalty;
+#pragma unroll
+    for (int t = 0; t < ZB_V4_NUM_REWARD_TERMS; ++t) sums[t] = sums0[t];
+  }
   const bool reset = died || time_out;
   const uint64_t hs = env_hash(seed, cnt->calls, i);
   float obs_q[4] = {bq[0], bq[1], bq[2], bq[3]};
@@ -3474,7 +3568,7 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_v4_step_kernel(
       float w3[3];
       mv3(R, v, w3);
 #pragma unroll
-      for (int a = 0; a < 3; ++a) down[f][a] = cfg.reset_feet_refresh ? p.pos[a] + w3[a] : feet[f][a];
+      for (int a = 0; a < 3; ++a) down[f][a] = (cfg.reset_feet_refresh || blowup) ? p.pos[a] + w3[a] : feet[f][a];
       f_last[f] = cfg.feet_f_last_init;
       step_len[f] = 0.f;
     }
@@ -3719,6 +3813,7 @@ struct PreM {
 };
 static_assert(sizeof(PreM) <= 16 * PRE4, "PreM fits PRE4 granules");
 
+template <bool kTgs>
 __global__ __launch_bounds__(WGT, ZB_M_WAVES_PER_SIMD) void zb_m_step_kernel(
     const zb_model* __restrict__ mg, const float4* __restrict__ links, zb_task_cfg cfg, int N, float* __restrict__ st,
     const float* __restrict__ act, float* __restrict__ obs, float* __restrict__ rew, uint8_t* __restrict__ term,
@@ -3802,7 +3897,7 @@ __global__ __launch_bounds__(WGT, ZB_M_WAVES_PER_SIMD) void zb_m_step_kernel(
 #pragma unroll
       for (int j = 0; j < ND; ++j) pv.jqd_prev[j] = p.jqd[j];
     }
-    substep<false, true>(m, cfg, p, target, q, true, k > 0, so, nullptr, nullptr, sp);
+    substep<false, true, kTgs>(m, cfg, p, target, q, true, k > 0, so, nullptr, nullptr, sp);
 #pragma unroll
     for (int f = 0; f < 2; ++f) {
       const float fn = sqrtf(dot3(so.feet_f[f], so.feet_f[f]));
@@ -3861,7 +3956,8 @@ __global__ __launch_bounds__(WGT, ZB_M_WAVES_PER_SIMD) void zb_m_step_kernel(
   const bool low = bp[2] < cfg.termination_height;
   const float fd[3] = {feet[0][0] - feet[1][0], feet[0][1] - feet[1][1], feet[0][2] - feet[1][2]};
   const bool close = sqrtf(dot3(fd, fd)) < cfg.feet_close_min;
-  const bool terminated = low || close;
+  const bool blowup = phys_bad(p);  // non-finite guard (phys_bad), as in the walking kernel
+  const bool terminated = low || close || blowup;
 
   // RewardManager.compute: term * weight * step_dt in cfg order (mgr.py:262-357, flat overrides)
   float r[ZB_M_NUM_REWARD_TERMS];
@@ -3931,6 +4027,11 @@ __global__ __launch_bounds__(WGT, ZB_M_WAVES_PER_SIMD) void zb_m_step_kernel(
     reward += v;
     sums[t] = CST(ZB_M_EP_SUMS + t) + v;
   }
+  if (blowup) {  // finite reward (the is_terminated term alone), the episode sums without this step
+    reward = cfg.stage_scales[0][ZB_M_R_TERMINATION] * step_dt;
+#pragma unroll
+    for (int t = 0; t < ZB_M_NUM_REWARD_TERMS; ++t) sums[t] = CST(ZB_M_EP_SUMS + t);
+  }
   const bool reset = terminated || time_out;
   const uint64_t hs = env_hash(seed, cnt->calls, i);
   float a_obs[ND];
@@ -3966,7 +4067,7 @@ __global__ __launch_bounds__(WGT, ZB_M_WAVES_PER_SIMD) void zb_m_step_kernel(
       float w3[3];
       mv3(R, v, w3);
 #pragma unroll
-      for (int a = 0; a < 3; ++a) down[f][a] = cfg.reset_feet_refresh ? p.pos[a] + w3[a] : feet[f][a];
+      for (int a = 0; a < 3; ++a) down[f][a] = (cfg.reset_feet_refresh || blowup) ? p.pos[a] + w3[a] : feet[f][a];
       f_last[f] = 0.f;
       step_len[f] = 0.f;
     }
@@ -4378,8 +4479,10 @@ int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_dev
       }
     if (np != m->num_self_pairs) return set_err(-1, "zb_create: self-collision pair count", hipSuccess);
   }
-  if (c->decimation < 1 || c->decimation > MAXSUB || c->solver_iterations < 0)
-    return set_err(-1, "zb_create: cfg (decimation 1..8, solver_iterations >= 0)", hipSuccess);
+  if (c->decimation < 1 || c->decimation > MAXSUB || c->solver_iterations < 0 || c->solver_mode < 0 ||
+      c->solver_mode > 1 || (c->solver_mode == 1 && c->solver_iterations < 1))
+    return set_err(-1, "zb_create: cfg (decimation 1..8, solver_iterations >= 0, solver_mode 0 / 1 with iterations >= 1)",
+                   hipSuccess);
   if (c->task != ZB_TASK_WALKING_V2 && c->task != ZB_TASK_STANDUP_V0 && c->task != ZB_TASK_WALKING_V4 &&
       c->task != ZB_TASK_MANAGER_V0)
     return set_err(-1, "zb_create: unknown task", hipSuccess);
@@ -4442,8 +4545,18 @@ int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_dev
                                (c[2] - mid[2]) * (c[2] - mid[2]));
         rad = fmax(rad, dc + r);
       }
-      // bounding sphere of the whole shape (self-collision broadphase)
+      // bounding sphere of the whole shape
       t[9] = make_float4((float)mid[0], (float)mid[1], (float)mid[2], (float)(rad + 1e-6));
+      // self-collision broadphase: the core hull lies in the capsule of its two core circle centres
+      // with the larger core radius (+ 1 um)
+      {
+        double rc = 0.0;
+        for (int ci = 0; ci < 2; ++ci) {
+          const float* c = m->link_circle[l][ci];
+          rc = fmax(rc, sqrt((double)c[3] * c[3] + (double)c[4] * c[4] + (double)c[5] * c[5]) - kCoreM);
+        }
+        t[2].w = (float)(rc + 1e-6);
+      }
     }
     for (int j = 0; j < ND; ++j) {
       float4* t = tab + JT_OFF + j * 5;
@@ -4567,6 +4680,19 @@ int zb_read_stamps_slowest(uint64_t* out16) {
 }
 
 // Diagnostic build only (-DZB_STAMPS): per-phase cycle sums over all waves since the last call.
+int zb_read_stamp_hist(uint64_t* out128) {
+#ifdef ZB_STAMPS
+  unsigned long long tmp[128];
+  HIPCHK(hipMemcpyFromSymbol(tmp, HIP_SYMBOL(g_stamp_hist), sizeof(tmp)), "hipMemcpyFromSymbol");
+  for (int k = 0; k < 128; ++k) out128[k] = tmp[k];
+  unsigned long long z[128] = {0};
+  HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_hist), z, sizeof(z)), "hipMemcpyToSymbol");
+  return 0;
+#else
+  (void)out128;
+  return set_err(-1, "zb_read_stamp_hist: library built without -DZB_STAMPS", hipSuccess);
+#endif
+}
 int zb_read_stamps(uint64_t* out16) {
 #ifdef ZB_STAMPS
   unsigned long long tmp[NSTAMP];
@@ -4645,18 +4771,21 @@ int zb_step(zb_handle h, const float* actions, float* obs, float* reward, uint8_
   const int blocks = (h->n + EPW - 1) / EPW;
   const bool prof = h->prof_n < h->prof_max;
   if (prof) HIPCHK(hipEventRecord(h->prof_ev[2 * h->prof_n], s), "hipEventRecord");
+  const bool tgs = h->cfg.solver_mode == 1;
+#define ZB_LAUNCH(K, ...) (tgs ? K<true><<<blocks, WGT, 0, s>>>(__VA_ARGS__) : K<false><<<blocks, WGT, 0, s>>>(__VA_ARGS__))
   if (h->task == ZB_TASK_STANDUP_V0)
-    zb_su_step_kernel<<<blocks, WGT, 0, s>>>(h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward,
-                                             terminated, truncated, h->d_acc, h->d_cnt, h->seed);
+    ZB_LAUNCH(zb_su_step_kernel, h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward, terminated,
+              truncated, h->d_acc, h->d_cnt, h->seed);
   else if (h->task == ZB_TASK_WALKING_V4)
-    zb_v4_step_kernel<<<blocks, WGT, 0, s>>>(h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward,
-                                             terminated, truncated, h->d_acc, h->d_cnt, h->seed);
+    ZB_LAUNCH(zb_v4_step_kernel, h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward, terminated,
+              truncated, h->d_acc, h->d_cnt, h->seed);
   else if (h->task == ZB_TASK_MANAGER_V0)
-    zb_m_step_kernel<<<blocks, WGT, 0, s>>>(h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward,
-                                            terminated, truncated, h->d_acc, h->d_cnt, h->seed);
+    ZB_LAUNCH(zb_m_step_kernel, h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward, terminated,
+              truncated, h->d_acc, h->d_cnt, h->seed);
   else
-    zb_step_kernel<<<blocks, WGT, 0, s>>>(h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward,
-                                          terminated, truncated, h->d_acc);
+    ZB_LAUNCH(zb_step_kernel, h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward, terminated,
+              truncated, h->d_acc);
+#undef ZB_LAUNCH
   int rc = launch_check("zb_step_kernel");
   if (prof) {
     HIPCHK(hipEventRecord(h->prof_ev[2 * h->prof_n + 1], s), "hipEventRecord");
@@ -4748,12 +4877,17 @@ int zb_physics_substeps(zb_handle h, const float* targets, int nsub, float* net_
                         void* stream) {
   if (!h || !targets || nsub < 1) return set_err(-1, "zb_physics_substeps", hipSuccess);
   const int blocks = (h->n + EPW - 1) / EPW;
-  if (h->task == ZB_TASK_STANDUP_V0 || h->task == ZB_TASK_MANAGER_V0)
-    zb_substeps_kernel<true><<<blocks, WGT, 0, (hipStream_t)stream>>>(h->d_model, h->d_links, h->cfg, h->n, h->d_state,
-                                                                       targets, nsub, net_force, applied_torque);
-  else
-    zb_substeps_kernel<false><<<blocks, WGT, 0, (hipStream_t)stream>>>(h->d_model, h->d_links, h->cfg, h->n, h->d_state,
-                                                                        targets, nsub, net_force, applied_torque);
+  const bool dr = h->task == ZB_TASK_STANDUP_V0 || h->task == ZB_TASK_MANAGER_V0, tgs = h->cfg.solver_mode == 1;
+#define ZB_SUB(F, T) zb_substeps_kernel<F, T><<<blocks, WGT, 0, (hipStream_t)stream>>>(h->d_model, h->d_links, h->cfg, \
+                                                 h->n, h->d_state, targets, nsub, net_force, applied_torque)
+  if (dr) {
+    if (tgs) ZB_SUB(true, true);
+    else ZB_SUB(true, false);
+  } else {
+    if (tgs) ZB_SUB(false, true);
+    else ZB_SUB(false, false);
+  }
+#undef ZB_SUB
   return launch_check("zb_substeps_kernel");
 }
 
