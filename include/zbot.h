@@ -55,7 +55,9 @@ extern "C" {
 #define ZB_NUM_REWARD_TERMS 13
 #define ZB_HIST 5             /* contact sensor history_length (v2.py:32) */
 #define ZB_MAX_SELF_PAIRS 64
-#define ZB_MAX_CONTACTS 12    /* contact slots per env per substep (deepest kept) */
+#ifndef ZB_MAX_CONTACTS
+#define ZB_MAX_CONTACTS 12    /* contact slots per env per substep (deepest kept); -D for the cap A/B build */
+#endif
 
 #define ZB_TASK_WALKING_V2 0  /* zbot-6b-walking-v2 (v2.py) */
 #define ZB_TASK_STANDUP_V0 1  /* zbot-6b-standup-v0 (standup.py) */
@@ -383,8 +385,10 @@ int zb_read_stamps(uint64_t* out16);
 int zb_read_stamps_slowest(uint64_t* out16);
 /* diagnostic build only: per-launch wave histograms since the previous call: [0, 64) the wave's
  * largest count of GJK pairs of one env in one substep, [64, 128) the wave's largest per-lane sum
- * of GJK iterations over the step (bins of 4) */
-int zb_read_stamp_hist(uint64_t* out128);
+ * of GJK iterations over the step (bins of 4); [128, 136) contact-cap counters over env-substeps:
+ * env-substeps, more than ZB_MAX_CONTACTS candidates, more than 18 self contacts, self contacts on
+ * overlapping cores, env-substeps with one, self contacts, ground candidates */
+int zb_read_stamp_hist(uint64_t* out136);
 
 /* Test entry: the self-collision GJK (the step kernels' gjk_quad) on n link pairs given as
  * world-frame core hulls, device pointers. pairs [n][2][2][9] (per hull two circles: centre, E1,

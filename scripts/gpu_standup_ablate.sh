@@ -4,6 +4,8 @@
 # and one-factor simulator ablations; each run is followed by a 290-step play from fresh episodes
 # whose posture summary (end-of-episode base z, feet z-axis alignment) is the outcome.
 # Usage: RUNS="base_s1:--seed=1 pgs8:--env=solver.iterations=8" gpurun -- bash scripts/gpu_standup_ablate.sh
+# A run's args may hold lib=<file> (a variant build, e.g. lib=libzbot_nc24.so: ZBOT_LIB for its train
+# and play) and --env=solver.mode=1 (the TGS-style contact solve).
 # C5 batch: NUM_ENVS=32768 ITERS=1000 RUNS="c5_hull:" (profiles/r2e_train/c5_play/)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; O=gpurun_out/standup_ablate; mkdir -p $O
@@ -11,7 +13,10 @@ export TMPDIR=/tmp
 LR=/tmp/zb_su_logs; IT=${ITERS:-2000}
 for spec in ${RUNS:-base:}; do
   name=${spec%%:*}; extra=$(echo "${spec#*:}" | tr ',' ' ')
-  echo "== $name $extra"
+  lib=$(echo "$extra" | tr ' ' '\n' | grep '^lib=' | cut -d= -f2 || true)
+  extra=$(echo "$extra" | tr ' ' '\n' | grep -v '^lib=' | tr '\n' ' ' || true)
+  export ZBOT_LIB=${lib:-libzbot.so}
+  echo "== $name $extra lib=$ZBOT_LIB"
   timeout -k 10 600 python -u scripts/train.py --task zbot-6b-standup-v0 --num_envs ${NUM_ENVS:-4096} --max_iterations $IT \
     --log_root $LR --log-every 250 --run_name $name $extra > $O/$name.train.log 2>&1 || { echo "train $name rc=$?"; tail -5 $O/$name.train.log; exit 1; }
   tail -n 1 $O/$name.train.log

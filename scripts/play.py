@@ -18,9 +18,10 @@ import json
 import os
 import sys
 
-import torch
-
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import zbot_lab_amd  # noqa: E402,F401  (before torch: sets HIP's graph capture mode, zbot_lab_amd/__init__.py)
+import torch  # noqa: E402
+
 
 
 def _posture(env, st, max_envs: int = 512) -> dict:

@@ -27,9 +27,10 @@ import sys
 import time
 from datetime import datetime
 
-import torch
-
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import zbot_lab_amd  # noqa: E402,F401  (before torch: sets HIP's graph capture mode, zbot_lab_amd/__init__.py)
+import torch  # noqa: E402
+
 
 
 def build_parser() -> argparse.ArgumentParser:

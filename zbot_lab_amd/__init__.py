@@ -6,18 +6,34 @@ Hot path: one fused HIP kernel per policy step (``csrc/zbot_sim.hip`` -> ``libzb
 import os as _os
 import sys as _sys
 
-# HIP graphs: ROCm's "packet capture" graph mode (the CLR default) leaves a replayed graph with
-# kernel arguments that later eager launches of the same kernels overwrite -- a captured PPO update
-# or rollout then silently computes with another launch's arguments (tests/test_ppo.py
-# ::test_gpu_update_graph_matches_eager). The runtime reads the switch once, when HIP
-# initialises, so it is set here, before anything touches the GPU. GRAPHS_SAFE records whether that
-# worked (False when the GPU was initialised before this import without the switch); the PPO runner
-# then runs eagerly.
-_torch = _sys.modules.get("torch")
-_late = _torch is not None and getattr(_torch, "cuda", None) is not None and _torch.cuda.is_initialized()
-if not _late:
-    _os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
-GRAPHS_SAFE = _os.environ.get("DEBUG_CLR_GRAPH_PACKET_CAPTURE") == "0"
+# HIP graphs: ROCm's "packet capture" graph mode (the CLR default) makes the captured PPO update
+# replay with wrong results from its second replay on (tests/test_ppo.py
+# ::test_gpu_update_graph_matches_eager fails with DEBUG_CLR_GRAPH_PACKET_CAPTURE=1; minimal HIP and
+# torch graphs of single kernels, fused Adam included, replay correctly in both modes:
+# tools/graph_repro/). The runtime reads the switch once, when HIP initialises --
+# which any HIP call does, torch.cuda.is_available() / device_count() included, even while
+# torch.cuda.is_initialized() is still False. GRAPHS_SAFE is therefore True only when the switch
+# is certain to have been read as "0": it was in the process environment at launch
+# (/proc/self/environ: scripts/train.py and play.py re-launch nothing, they set it before
+# importing torch), or torch was not imported yet when this package set it. Otherwise the PPO
+# runner runs eagerly.
+def _launch_env(name: str):
+    try:
+        with open("/proc/self/environ", "rb") as f:
+            for kv in f.read().split(b"\0"):
+                k, _, v = kv.partition(b"=")
+                if k.decode(errors="replace") == name:
+                    return v.decode(errors="replace")
+    except OSError:
+        pass
+    return None
+
+
+_KNOB = "DEBUG_CLR_GRAPH_PACKET_CAPTURE"
+_torch_first = "torch" in _sys.modules
+if not _torch_first:
+    _os.environ.setdefault(_KNOB, "0")
+GRAPHS_SAFE = _os.environ.get(_KNOB) == "0" and (not _torch_first or _launch_env(_KNOB) == "0")
 
 from . import model  # noqa: F401
 from .tasks import make, register, registered  # noqa: F401

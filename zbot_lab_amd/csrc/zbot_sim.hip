@@ -33,6 +33,7 @@ constexpr int ND = ZB_NUM_DOF;
 constexpr int NL = ZB_NUM_LINKS;
 constexpr int NV = 6 + ND;
 constexpr int NCM = ZB_MAX_CONTACTS;
+constexpr int NSELF = 18;  // self-collision candidates per env (canonical pair order), see the candidate list
 constexpr int WAVE = 64;
 constexpr float PI_F = 3.14159265358979323846f;
 constexpr float TWO_PI_F = 6.28318530717958647692f;
@@ -68,8 +69,13 @@ constexpr int kStampCount0 = 13;  // slots 13, 14 count events (GJK calls, itera
 __device__ unsigned long long g_stamps[NSTAMP];
 __device__ unsigned long long g_stamp_slowest[NSTAMP];  // phase cycles of the slowest wave seen
 // per-launch wave histograms: [0, 64) the wave's largest number of GJK pairs of one env in one
-// substep; [64, 128) the wave's largest per-lane sum of GJK iterations over the step, in bins of 4
-__device__ unsigned long long g_stamp_hist[128];
+// substep; [64, 128) the wave's largest per-lane sum of GJK iterations over the step, in bins of 4;
+// contact-cap counters over env-substeps: [128] env-substeps, [129] more than NCM candidates (the
+// cap selects), [130] more than NSELF self contacts, [131] self contacts on overlapping cores (the
+// centre-difference fallback), [132] env-substeps with such a contact, [133] self contacts,
+// [134] ground candidates
+constexpr int kCapCounters = 128;
+__device__ unsigned long long g_stamp_hist[kCapCounters + 8];
 struct Stamps {
   unsigned long long t, acc[NSTAMP];
   unsigned umax, itsum;
@@ -79,6 +85,18 @@ struct Stamps {
     umax = 0; itsum = 0;
   }
   __device__ void note_pairs(unsigned u) { umax = u > umax ? u : umax; }
+  // contact-cap counters of one env-substep (called by the team lead)
+  __device__ void note_caps(int n_ground, int n_self, int n_deep) {
+    atomicAdd(&g_stamp_hist[kCapCounters], 1ull);
+    if (n_ground + min(n_self, NSELF) > NCM) atomicAdd(&g_stamp_hist[kCapCounters + 1], 1ull);
+    if (n_self > NSELF) atomicAdd(&g_stamp_hist[kCapCounters + 2], 1ull);
+    if (n_deep) {
+      atomicAdd(&g_stamp_hist[kCapCounters + 3], (unsigned long long)n_deep);
+      atomicAdd(&g_stamp_hist[kCapCounters + 4], 1ull);
+    }
+    if (n_self) atomicAdd(&g_stamp_hist[kCapCounters + 5], (unsigned long long)n_self);
+    if (n_ground) atomicAdd(&g_stamp_hist[kCapCounters + 6], (unsigned long long)n_ground);
+  }
   __device__ void note_its(unsigned its) { itsum += its; }
   __device__ void mark(int k) {
     const unsigned long long n = __builtin_amdgcn_s_memtime();
@@ -118,6 +136,7 @@ struct Stamps {
   __device__ void count(int, unsigned) {}
   __device__ void note_pairs(unsigned) {}
   __device__ void note_its(unsigned) {}
+  __device__ void note_caps(int, int, int) {}
   __device__ void flush() {}
 };
 #endif
@@ -504,7 +523,6 @@ constexpr int LNK4 = BT_OFF + NB * 3;
 // Candidate list in canonical order: ground (link by link, <= 4 each), then self candidates in
 // (pair, sphere a, sphere b) order, at most NSELF. More than NCM candidates: the NCM smallest by
 // (sep, canonical index) are kept; kept contacts are solved in canonical order (= oracle detect).
-constexpr int NSELF = 18;
 constexpr int NCAND = NL * 4 + NSELF;
 
 // LDS layout of one workgroup (EPW envs), float4 units. Phase-disjoint buffers share storage so
@@ -1333,6 +1351,9 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q&
     sp.note_pairs(U);
     const int qd = q.s >> 2, qj = q.s & 3;  // quad of the team, lane in the quad
     const int urounds = (U + 3) >> 2;
+#ifdef ZB_STAMPS
+    int deep_quad = 0;  // diagnostic: this quad's contacts on overlapping cores
+#endif
     SelfContact hit0 = {};  // this quad's first contact is kept for the write pass
     int hit0_k = -1;
     unsigned own = 0u;                // bit k: this quad's pair of round k is a contact
@@ -1377,6 +1398,9 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q&
           if (pass == 0 && h) {
             if (own == 0u) { hit0 = sc; hit0_k = k; }
             own |= 1u << k;
+#ifdef ZB_STAMPS
+            if (qj == 0 && sc.sep <= -2.f * kCoreM + 1e-7f) ++deep_quad;
+#endif
           }
         }
         if (pass == 1 && qj == 0) {
@@ -1395,7 +1419,16 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q&
         s_tot = __popcll(allhits);
       }
     }
+#ifdef ZB_STAMPS
+    {
+      const int deep = (int)tsum((float)deep_quad);
+      if (q.s == 0) sp.note_caps(g_tot, s_tot, deep);
+    }
+#endif
   }
+#ifdef ZB_STAMPS
+  else if (q.s == 0) sp.note_caps(g_tot, 0, 0);
+#endif
   sp.mark(2);
   const int n = g_tot + min(s_tot, NSELF);
   over = n > NCM;
@@ -4680,12 +4713,13 @@ int zb_read_stamps_slowest(uint64_t* out16) {
 }
 
 // Diagnostic build only (-DZB_STAMPS): per-phase cycle sums over all waves since the last call.
-int zb_read_stamp_hist(uint64_t* out128) {
+int zb_read_stamp_hist(uint64_t* out136) {
+  uint64_t* out128 = out136;
 #ifdef ZB_STAMPS
-  unsigned long long tmp[128];
+  unsigned long long tmp[kCapCounters + 8];
   HIPCHK(hipMemcpyFromSymbol(tmp, HIP_SYMBOL(g_stamp_hist), sizeof(tmp)), "hipMemcpyFromSymbol");
-  for (int k = 0; k < 128; ++k) out128[k] = tmp[k];
-  unsigned long long z[128] = {0};
+  for (int k = 0; k < kCapCounters + 8; ++k) out128[k] = tmp[k];
+  unsigned long long z[kCapCounters + 8] = {0};
   HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_hist), z, sizeof(z)), "hipMemcpyToSymbol");
   return 0;
 #else
