@@ -489,9 +489,9 @@ static void hull_extent(const hull_t* h, const real u[3], real* lo, real* hi) {
  * (|v|^2 - v.w) / |v| <= GJK_TOL (the distance bounds |v| and v.w / |v| agree), after GJK_MAX_IT
  * iterations, or early (no contact) once the lower bound v.w / |v| exceeds early_margin +
  * 2 CORE_M (early_margin = margin for detection). Contact: normal (pa - pb) / d from B to A,
- * separation d - 2 CORE_M, point (pa + pb) / 2. Cores that overlap (d < 1e-6): normal along the
- * centre difference, separation -2 CORE_M, point = the mean of the centres. Returns 1 on a
- * contact within the margin. (The kernel runs the same statement on the 4 lanes of a quad:
+ * separation d - 2 CORE_M, point (pa + pb) / 2. Cores that overlap (d < 1e-6): the
+ * separating-axis penetration estimate (below). Returns 1 on a contact within the margin. (The
+ * kernel runs the same statement on the 4 lanes of a quad:
  * gjk_quad in zbot_sim.hip.) */
 static int hull_pair(const hull_t* A, const hull_t* B, real margin, real early_margin, const real* v0,
                      contact_t* out) {
@@ -531,11 +531,35 @@ static int hull_pair(const hull_t* A, const hull_t* B, real margin, real early_m
   }
   real d = sqrtr(v3_dot(v, v));
   if (overlap || d < (real)1e-6) {
-    real dv[3] = {ca[0] - cb[0], ca[1] - cb[1], ca[2] - cb[2]};
-    real dn = sqrtr(v3_dot(dv, dv));
-    if (dn < (real)1e-12) { dv[0] = 0; dv[1] = 0; dv[2] = 1; dn = 1; }
-    out->sep = -2 * (real)CORE_M;
-    for (int a = 0; a < 3; ++a) { out->n[a] = dv[a] / dn; out->x[a] = (real)0.5 * (ca[a] + cb[a]); }
+    /* overlapping cores: the separating-axis estimate of the penetration over the centre
+     * difference and the four circle normals -- the axis of the largest (least negative) gap,
+     * oriented B -> A, is the normal, the gap the core separation (>= -true depth); the point is
+     * the mean of the hull centres (the cores' deepest points along a circle normal are a whole
+     * rim, so rounding would pick one) */
+    real best = -1e30, nb[3] = {0, 0, 1};
+    for (int ax = 0; ax < 5; ++ax) {
+      real u[3];
+      if (ax == 0) {
+        for (int a = 0; a < 3; ++a) u[a] = ca[a] - cb[a];
+      } else {
+        const hull_t* H = ax <= 2 ? A : B;
+        v3_cross(H->c[(ax - 1) & 1] + 3, H->c[(ax - 1) & 1] + 6, u);
+      }
+      real nu = sqrtr(v3_dot(u, u));
+      if (nu < (real)1e-12) continue; /* coincident centres: no centre-difference axis */
+      for (int a = 0; a < 3; ++a) u[a] /= nu;
+      real alo, ahi, blo, bhi;
+      hull_extent(A, u, &alo, &ahi);
+      hull_extent(B, u, &blo, &bhi);
+      real gp = alo - bhi, gm = blo - ahi;
+      real g = gp >= gm ? gp : gm;
+      if (g > best) {
+        best = g;
+        for (int a = 0; a < 3; ++a) nb[a] = gp >= gm ? u[a] : -u[a];
+      }
+    }
+    out->sep = (best < 0 ? best : 0) - 2 * (real)CORE_M;
+    for (int a = 0; a < 3; ++a) { out->n[a] = nb[a]; out->x[a] = (real)0.5 * (ca[a] + cb[a]); }
     return out->sep < margin;
   }
   real pa[3] = {0, 0, 0};

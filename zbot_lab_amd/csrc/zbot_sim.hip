@@ -997,8 +997,8 @@ __device__ __forceinline__ bool hulls_separated(const Hull& A, const Hull& B, fl
 // bounds |v| and v.w / |v| agree), after kGjkMaxIt iterations, or as soon as the lower bound
 // v.w / |v| exceeds early_margin + 2 kCoreM (no contact; early_margin = margin in the counting
 // pass, huge when a counted contact is re-computed). Contact: n = (pa - pb) / d (B -> A),
-// sep = d - 2 kCoreM, x = (pa + pb) / 2; overlapping cores: n along the centre difference,
-// sep = -2 kCoreM, x = the mean centre. Same statement as the oracle's hull_pair.
+// sep = d - 2 kCoreM, x = (pa + pb) / 2; overlapping cores: quad_deep. Same statement as the
+// oracle's hull_pair.
 constexpr int DPP_QB0 = 0x00, DPP_QB2 = 0xAA;  // quad_perm broadcast of quad lane 0 / 2
 struct QCircle { float c[3], e1[3], e2[3]; };  // world core circle: centre, semi-axes (radius baked in)
 __device__ __forceinline__ void quad_circle(const Q& q, int l, int ci, QCircle& h) {
@@ -1062,6 +1062,41 @@ __device__ __forceinline__ void quad_pick(bool partner_first, float& best, float
   l1 = take ? o1 : l1;
   l2 = take ? o2 : l2;
   bm = take ? om : bm;
+}
+// Overlapping cores (GJK found the origin inside, or a distance below 1 um): the separating-axis
+// estimate of the penetration over the hull centre difference and the four circle normals (A c0,
+// A c1, B c0, B c1) -- the axis of the largest (least negative) gap, oriented B -> A, is the
+// normal and the gap the core separation (clamped to <= 0; >= -the true depth); the point is the
+// mean of the hull centres (the deepest points along a circle normal are a whole rim: rounding
+// would pick one). Same statement as the oracle's hull_pair.
+__device__ __forceinline__ void quad_deep(const QCircle& h, int j, float n[3], float& sep, float x[3]) {
+  float ca[3], cb[3], cn[3];
+  quad_centres(h, ca, cb);
+  cross3(h.e1, h.e2, cn);  // this lane's circle normal
+  float best = -1e30f, nb[3] = {0.f, 0.f, 1.f};
+#pragma unroll
+  for (int ax = 0; ax < 5; ++ax) {
+    float u[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+      u[k] = ax == 0 ? ca[k] - cb[k]
+                     : (ax == 1 ? dppf<DPP_QB0>(cn[k]) : (ax == 2 ? dppf<0x55>(cn[k]) : (ax == 3 ? dppf<DPP_QB2>(cn[k]) : dppf<0xFF>(cn[k]))));
+    const float uu = dot3(u, u);
+    const float iu = __builtin_amdgcn_rsqf(fmaxf(uu, 1e-30f));
+    u[0] *= iu; u[1] *= iu; u[2] *= iu;
+    const float a = dot3(u, h.e1), b = dot3(u, h.e2);
+    const float r = sqrtf(fmaf(a, a, b * b)), m = dot3(u, h.c);
+    const float lo = fminf(m - r, dppf<DPP_XOR1>(m - r)), hi = fmaxf(m + r, dppf<DPP_XOR1>(m + r));
+    const float alo = dppf<DPP_QB0>(lo), ahi = dppf<DPP_QB0>(hi), blo = dppf<DPP_QB2>(lo), bhi = dppf<DPP_QB2>(hi);
+    const float gp = alo - bhi, gm = blo - ahi, g = gp >= gm ? gp : gm;
+    const bool take = uu > 1e-24f && g > best;
+    best = take ? g : best;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) nb[k] = take ? (gp >= gm ? u[k] : -u[k]) : nb[k];
+  }
+  sep = fminf(best, 0.f) - 2.f * kCoreM;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) { n[k] = nb[k]; x[k] = 0.5f * (ca[k] + cb[k]); }
 }
 __device__ __forceinline__ bool gjk_quad(const QCircle& h, int j, const float v0[3], float margin, float early_margin,
                                          SelfContact& out, int& iters) {
@@ -1179,22 +1214,19 @@ __device__ __forceinline__ bool gjk_quad(const QCircle& h, int j, const float v0
   // one exit (a struct written on two paths ends up in scratch memory)
   const float d = sqrtf(dot3(v, v));
   const bool deep = overlap || d < 1e-6f;
-  float ca[3], cb[3], dv[3];  // hull centres (recomputed: not kept live across the iterations)
-  quad_centres(h, ca, cb);
-#pragma unroll
-  for (int k = 0; k < 3; ++k) dv[k] = ca[k] - cb[k];
-  const float dn2 = dot3(dv, dv);
-  const bool nodir = dn2 < 1e-24f;
-  const float idn = __builtin_amdgcn_rsqf(fmaxf(dn2, 1e-30f)), id = 1.f / fmaxf(d, 1e-30f);
+  const float id = 1.f / fmaxf(d, 1e-30f);
+  float on[3], ox[3], osep = d - 2.f * kCoreM;
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     // closest point on A's core: the same weights over the A-side support points
     const float pa = lam[0] * SP[0][k] + (n >= 2 ? lam[1] * SP[1][k] : 0.f) + (n >= 3 ? lam[2] * SP[2][k] : 0.f);
-    const float nd = nodir ? (k == 2 ? 1.f : 0.f) : dv[k] * idn;
-    out.n[k] = deep ? nd : v[k] * id;
-    out.x[k] = deep ? 0.5f * (ca[k] + cb[k]) : pa - 0.5f * v[k];
+    on[k] = v[k] * id;
+    ox[k] = pa - 0.5f * v[k];
   }
-  out.sep = deep ? -2.f * kCoreM : d - 2.f * kCoreM;
+  if (deep) quad_deep(h, j, on, osep, ox);  // (quad-uniform)
+#pragma unroll
+  for (int k = 0; k < 3; ++k) { out.n[k] = on[k]; out.x[k] = ox[k]; }
+  out.sep = osep;
   return out.sep < margin;
 }
 
