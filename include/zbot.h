@@ -56,7 +56,7 @@ extern "C" {
 #define ZB_HIST 5             /* contact sensor history_length (v2.py:32) */
 #define ZB_MAX_SELF_PAIRS 64
 #ifndef ZB_MAX_CONTACTS
-#define ZB_MAX_CONTACTS 12    /* contact slots per env per substep (deepest kept); -D for the cap A/B build */
+#define ZB_MAX_CONTACTS 12    /* contact slots per env per substep (deepest kept); -D for the cap A/B build (<= 16) */
 #endif
 
 #define ZB_TASK_WALKING_V2 0  /* zbot-6b-walking-v2 (v2.py) */

@@ -55,7 +55,8 @@ typedef ZBO_REAL real;
  * distance of the cores - 2 CORE_M (exact up to the rim rounding, for penetrations < 2 CORE_M). */
 #define CORE_M 0.004
 #define GJK_MAX_IT 16
-#define GJK_TOL 1e-5 /* m: stop when the upper (|v|) and lower (v.w / |v|) distance bounds are this close */
+#define GJK_TOL 1e-5 /* m: stop when the upper (|v|) and best lower (dir.w / |dir|) distance bounds are this close */
+#define GJK_TILT 0.01 /* warm start: tilt of the first three support directions (rad) */
 #define TWO_PI 6.283185307179586
 #define PI_R 3.14159265358979323846
 
@@ -502,26 +503,49 @@ static int hull_pair(const hull_t* A, const hull_t* B, real margin, real early_m
   }
   if (v0) { v[0] = v0[0]; v[1] = v0[1]; v[2] = v0[2]; }
   else { v[0] = ca[0] - cb[0]; v[1] = ca[1] - cb[1]; v[2] = ca[2] - cb[2]; }
+  /* warm start: the first three support directions are v0 tilted by GJK_TILT toward three
+   * directions 120 degrees apart, so the simplex spans a flat face at once (a support along a
+   * face normal is an arbitrary rim point) */
+  real td[3][3];
+  if (v0) {
+    const real iv = 1 / sqrtr(v3_dot(v, v)), u[3] = {v[0] * iv, v[1] * iv, v[2] * iv};
+    const real ax[3] = {fabs((double)u[0]) < 0.57 ? 1 : 0, fabs((double)u[0]) >= 0.57 && fabs((double)u[1]) < 0.57 ? 1 : 0,
+                        fabs((double)u[0]) >= 0.57 && fabs((double)u[1]) >= 0.57 ? 1 : 0};
+    real t1[3], t2[3];
+    v3_cross(u, ax, t1);
+    const real it1 = 1 / sqrtr(v3_dot(t1, t1));
+    for (int a = 0; a < 3; ++a) t1[a] *= it1;
+    v3_cross(u, t1, t2);
+    static const float tc[3] = {1.f, -0.5f, -0.5f}, ts[3] = {0.f, 0.8660254f, -0.8660254f};
+    for (int k = 0; k < 3; ++k)
+      for (int a = 0; a < 3; ++a) td[k][a] = u[a] + (real)GJK_TILT * ((real)tc[k] * t1[a] + (real)ts[k] * t2[a]);
+  }
   real W[4][3], PA[4][3], lam[4] = {1, 0, 0, 0};
   int n = 0, overlap = 0; /* n = retained points besides the newest W[0] */
   {
-    real nd[3] = {-v[0], -v[1], -v[2]}, pa[3], pb[3];
+    const real* d0 = v0 ? td[0] : v;
+    real nd[3] = {-d0[0], -d0[1], -d0[2]}, pa[3], pb[3];
     hull_support(A, nd, pa);
-    hull_support(B, v, pb);
+    hull_support(B, d0, pb);
     for (int a = 0; a < 3; ++a) { PA[0][a] = pa[a]; W[0][a] = pa[a] - pb[a]; v[a] = W[0][a]; }
   }
   g_gjk_last_it = 0;
+  const real lim = early_margin + 2 * (real)CORE_M;
   for (int it = 0; it < GJK_MAX_IT; ++it) {
     g_gjk_last_it = it + 1;
     real vv = v3_dot(v, v);
     if (vv < (real)1e-12) { overlap = 1; break; }
-    real nd[3] = {-v[0], -v[1], -v[2]}, pa[3], pb[3], w[3];
+    const real* dir = v0 && it < 2 ? td[it + 1] : v;
+    real nd[3] = {-dir[0], -dir[1], -dir[2]}, pa[3], pb[3], w[3];
     hull_support(A, nd, pa);
-    hull_support(B, v, pb);
+    hull_support(B, dir, pb);
     for (int a = 0; a < 3; ++a) w[a] = pa[a] - pb[a];
-    real vw = v3_dot(v, w);
-    if (vw > 0 && vw * vw > vv * (early_margin + 2 * (real)CORE_M) * (early_margin + 2 * (real)CORE_M)) return 0;
-    if (vv - vw <= (real)g_gjk_tol * sqrtr(vv)) break; /* distance bounds within the tolerance */
+    /* any direction bounds the distance from below by its support gap dir.w / |dir|: no contact
+     * once that exceeds the margin; converged when the gap along v itself is within the
+     * tolerance of |v| (so the normal v / |v| is converged too) */
+    const real L = v3_dot(dir, w) / sqrtr(v3_dot(dir, dir));
+    if (L > lim) return 0;
+    if (dir == v && sqrtr(vv) - L <= (real)g_gjk_tol) break;
     /* the simplex (the previous newest point first) is retained as W[1..n+1], w becomes W[0] */
     for (int i = n; i >= 0; --i)
       for (int a = 0; a < 3; ++a) { W[i + 1][a] = W[i][a]; PA[i + 1][a] = PA[i][a]; }

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Contact-cap hit rates: how often an env-substep has more
 than ZB_MAX_CONTACTS candidates (the cap selects the deepest), more than 18 self contacts, and self
-contacts on overlapping cores (the centre-difference fallback), per task and situation:
+contacts on overlapping cores (the separating-axis penetration estimate), per task and situation:
 
 * stand-up from its lying start (ZBOT_6S_CFG_2, zbot_cfg.py:741-744; random actions),
 * walking v2 random actions,
@@ -9,7 +9,7 @@ contacts on overlapping cores (the centre-difference fallback), per task and sit
   policy).
 
 Needs the diagnostic build (python -m zbot_lab_amd.build --stamps; counters of zb_read_stamp_hist).
-ZBOT_LIB selects another build for an A/B (e.g. one with -DZB_MAX_CONTACTS=24, with its
+ZBOT_LIB selects another build for an A/B (e.g. one with -DZB_MAX_CONTACTS=16, with its
 termination rate and stand-up outcome). Prints one JSON line per situation.
 Usage (GPU box): ZBOT_LIB=libzbot_stamps.so python scripts/contact_caps.py [N] [ITERS]
 """

@@ -15,7 +15,7 @@ g = torch.Generator(device="cuda"); g.manual_seed(42)
 for k in range(30): env.step(torch.randn(env.num_envs, 6, device="cuda", generator=g))
 torch.cuda.synchronize()
 buf = (C.c_uint64 * 16)(); nat.lib().zb_read_stamps(buf)
-nat.lib().zb_read_stamp_hist((C.c_uint64 * 128)())  # reset the histograms after the warm-up
+nat.lib().zb_read_stamp_hist((C.c_uint64 * 136)())  # reset the histograms after the warm-up
 steps = 100
 for k in range(steps): env.step(torch.randn(env.num_envs, 6, device="cuda", generator=g))
 torch.cuda.synchronize()
@@ -29,7 +29,7 @@ print(f"cycles per wave per step: {tot / waves / steps:.0f}")
 for k in range(len(names)):
     print(f"  {names[k]:32s} {buf[k] / waves / steps:10.0f}  {100 * buf[k] / tot:5.1f} %")
 slow = (C.c_uint64 * 16)(); nat.lib().zb_read_stamps_slowest(slow)
-hist = (C.c_uint64 * 128)(); nat.lib().zb_read_stamp_hist(hist)
+hist = (C.c_uint64 * 136)(); nat.lib().zb_read_stamp_hist(hist)
 print("waves by the largest GJK pair count of one env in one substep:",
       {k: hist[k] for k in range(64) if hist[k]})
 print("waves by the largest per-lane GJK iteration sum over the step (bin of 4):",

@@ -170,9 +170,10 @@ def test_full_state_zero_action_standing(gpu, task):
 
 def test_full_state_deep_overlap(gpu):
     """One step from states whose links interpenetrate deeper than 2 CORE_M (the rounded cores
-    intersect): both sides take the centre-difference fallback normal at separation -2 CORE_M, so
-    away from the switch (the core distance crossing 1e-6, GJK's overlap tests) every row agrees
-    under the same explained-outlier rule; no state is set aside."""
+    intersect): both sides take the separating-axis penetration estimate (normal and depth over the
+    centre difference and the four circle normals, point at the mean hull centre), so away from the
+    switch (the core distance crossing 1e-6, GJK's overlap tests) and the axis choice every row
+    agrees under the same explained-outlier rule; no state is set aside."""
     from oracle.pyoracle import OracleSim
     task, seed, pool = "v2", 31, 8192
     o = OracleSim(pool, task_cfg(task), seed=seed)

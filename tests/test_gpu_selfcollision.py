@@ -2,13 +2,17 @@
 hull_pair (oracle/zbot_oracle.c), through the C ABI's test entry zb_gjk_pairs.
 
 The robot's own link shapes at random relative poses around contact (separated, touching,
-penetrating less than 2 CORE_M, and overlapping cores: the centre-difference fallback), cold
+penetrating less than 2 CORE_M, and overlapping cores: the separating-axis estimate), cold
 (hull centre difference) and warm (a given start direction, as the step kernels pass the pair's
 contact normal of the previous substep). Contact flags must agree away from the margin; where
 both report a contact the separation agrees to 2e-5 m (GJK_TOL 1e-5 plus fp32 rounding), the normal
-to 2e-3 and the point to 1e-4 m. Slowly converging pairs (>= 8 iterations: nearly flat closest
+to 2e-3 and the point to 1e-4 m. A pair may miss the normal / point bound (nearly flat closest
 features, where fp32 rounding changes GJK's path and the normal is poorly determined although the
-distance is not) may miss the normal / point bound: at most 2 % of the contacts.
+distance is not; at most 2 % of the contacts) only if the GPU's answer is itself a converged one
+-- the separating gap of the two cores along the GPU's normal (float64, exact circle supports) is
+within 2e-5 m of its distance and its point lies midway between the core surfaces along that
+normal -- or the oracle's own answer spreads by half the GPU's deviation under 1e-6 relative
+perturbations of the hulls and the start direction.
 """
 from __future__ import annotations
 
@@ -16,7 +20,7 @@ import numpy as np
 import pytest
 
 from oracle import pyoracle
-from tests.test_oracle_selfcollision import CORE_M, _quat, _rot, core_circles, world
+from tests.test_oracle_selfcollision import CORE_M, _quat, _rot, core_circles, rim_points, sat_gap, world
 from zbot_lab_amd import model as zm
 
 pytestmark = pytest.mark.gpu
@@ -58,15 +62,52 @@ def _gpu(pairs, v0=None):
     return out.cpu().numpy()
 
 
-def _compare(g, o):
+def _spread(pairs, v0, k, o):
+    """largest change of the oracle's normal and point of pair k under 1e-6 relative perturbations
+    of its hulls and start direction"""
+    rng = np.random.default_rng(k)
+    dn = dx = 0.0
+    for _ in range(6):
+        p = pairs[k:k + 1] * (1 + 1e-6 * rng.standard_normal(pairs[k:k + 1].shape)).astype(np.float32)
+        v = None if v0 is None else v0[k:k + 1] * (1 + 1e-6 * rng.standard_normal((1, 3))).astype(np.float32)
+        r = _oracle(p.astype(np.float32), v)[0]
+        if r[0] == 1:
+            dn = max(dn, np.abs(r[2:5] - o[k, 2:5]).max())
+            dx = max(dx, np.abs(r[5:8] - o[k, 5:8]).max())
+    return dn, dx
+
+
+def _converged(pair, r):
+    """the GPU's contact of one pair is a converged GJK answer: the gap along its normal is within
+    2e-5 m of its distance, and its point is midway between the core surfaces along the normal"""
+    ha, hb = pair[0].astype(np.float64), pair[1].astype(np.float64)
+    n = r[2:5].astype(np.float64)
+    n /= np.linalg.norm(n)
+    d = float(r[1]) + 2 * CORE_M
+    if abs(sat_gap(ha, hb, n) - d) > 2e-5:
+        return False
+    xa, xb = r[5:8] + n * d / 2, r[5:8] - n * d / 2
+    return (abs(min(rim_points(ha, 4096) @ n) - xa @ n) < 5e-5 and abs(max(rim_points(hb, 4096) @ n) - xb @ n) < 5e-5)
+
+
+def _compare(g, o, pairs, v0=None):
     edge = np.abs(o[:, 1] - MARGIN) < 1e-4  # contact decided at the margin: either answer is right
     flag_ok = (g[:, 0] == o[:, 0]) | edge
     assert flag_ok.all(), np.where(~flag_ok)[0][:20]
     both = (g[:, 0] == 1) & (o[:, 0] == 1)
     deep = both & (o[:, 1] <= -2 * CORE_M + 1e-6)
     assert (np.abs(g[both, 1] - o[both, 1]) < 2e-5).all(), np.abs(g[both, 1] - o[both, 1]).max()
-    off = both & ((np.abs(g[:, 2:5] - o[:, 2:5]).max(axis=1) >= 2e-3) | (np.abs(g[:, 5:8] - o[:, 5:8]).max(axis=1) >= 1e-4))
-    assert (o[off, 8] >= 8).all(), np.where(off & (o[:, 8] < 8))[0][:20]
+    en = np.abs(g[:, 2:5] - o[:, 2:5]).max(axis=1)
+    ex = np.abs(g[:, 5:8] - o[:, 5:8]).max(axis=1)
+    off = both & ((en >= 2e-3) | (ex >= 1e-4))
+    unexplained = []
+    for k in np.nonzero(off)[0]:
+        if not deep[k] and _converged(pairs[k], g[k]):
+            continue
+        dn, dx = _spread(pairs, v0, k, o)
+        if not ((en[k] < 2e-3 or dn >= 0.5 * en[k]) and (ex[k] < 1e-4 or dx >= 0.5 * ex[k])):
+            unexplained.append((int(k), float(en[k]), dn, float(ex[k]), dx))
+    assert not unexplained, unexplained[:10]
     assert off.sum() <= 0.02 * both.sum(), (off.sum(), both.sum())
     return both.sum(), deep.sum()
 
@@ -75,7 +116,7 @@ def test_gjk_quad_matches_oracle_cold():
     pairs = _pairs(4000, seed=11)
     o = _oracle(pairs)
     g = _gpu(pairs)
-    nb, nd = _compare(g, o)
+    nb, nd = _compare(g, o, pairs)
     assert nb - nd > 200 and nd > 20, (nb, nd)  # exact contacts and overlapping cores both exercised
     # iteration counts agree except where a stopping test sits at its threshold
     assert (g[:, 8] == o[:, 8]).mean() > 0.95
@@ -90,4 +131,4 @@ def test_gjk_quad_matches_oracle_warm():
     v0[o0[:, 0] == 0] = rng.normal(size=((o0[:, 0] == 0).sum(), 3))
     o = _oracle(pairs, v0)
     g = _gpu(pairs, v0)
-    _compare(g, o)
+    _compare(g, o, pairs, v0)

@@ -2,8 +2,8 @@
 
 Rolls out random actions on the oracle with the GJK probe on (zbo_gjk_hooks): histogram of the
 support iterations of the GJK calls the kernel makes (pairs its separating-axis test leaves
-undecided), cold (every GJK from the best separating axis) vs warm (from the pair's contact normal
-of the previous substep of the step). Usage: python tools/gjk/probe.py [task] [envs] [steps]
+undecided), cold (every GJK from the hull centre difference) vs warm (from the pair's contact normal
+of the previous substep of the step). Usage: [GJK_TOL=1e-4] python tools/gjk/probe.py [task] [envs] [steps]
 """
 import ctypes as C
 import os
@@ -24,6 +24,8 @@ def run(task, n, steps, warm):
     sim = po.OracleSim(n, cfg=cfg.task_cfg(), seed=1)
     lib = sim.lib
     lib.zbo_gjk_hooks.argtypes = [C.c_int, C.c_int, C.c_void_p]
+    lib.zbo_set_gjk_tol.argtypes = [C.c_double]
+    lib.zbo_set_gjk_tol(float(os.environ.get("GJK_TOL", "0")))
     hist = np.zeros(NH + 64, np.int64)
     lib.zbo_gjk_hooks(warm, 1, hist.ctypes.data)  # clear
     sim.reset()

@@ -44,6 +44,7 @@ constexpr float RIM_EPS = 1e-3f;  // m; 2% of the module radius (see detect)
 constexpr float kCoreM = 0.004f;
 constexpr int kGjkMaxIt = 16;
 constexpr float kGjkTol = 1e-5f;  // m: GJK stops when its distance bounds are this close
+constexpr float kGjkTilt = 0.01f;  // warm start: tilt of the first three support directions (rad)
 
 // The ZBOT-6 chain topology is compiled in (zb_create checks the model against it):
 // link l belongs to composite body (l+1)/2; joint j connects body j -> j+1.
@@ -408,6 +409,8 @@ constexpr int TL = 16;           // lanes per env
 constexpr int EPW = ZB_EPW;      // envs per workgroup (one wave; EPW < 4 leaves lanes idle)
 constexpr int WGT = TL * EPW;    // threads per workgroup
 static_assert(WGT <= WAVE, "one wave per workgroup");
+// lane c of a team builds / zeroes / maps / forces contact slot c: one slot per lane
+static_assert(NCM <= TL, "ZB_MAX_CONTACTS <= 16 (one contact slot per lane of the env's team)");
 
 template <int CTRL>
 __device__ __forceinline__ float dppf(float x) {
@@ -860,71 +863,7 @@ __device__ __forceinline__ void gather_hull(const Hull& own, int addr, Hull& h) 
       h.e2[ci][k] = bperm(addr, own.e2[ci][k]);
     }
 }
-__device__ __forceinline__ void hull_sup(const Hull& h, const float d[3], float o[3]) {
-  float best = 0.f;
-#pragma unroll
-  for (int ci = 0; ci < 2; ++ci) {
-    const float a = dot3(d, h.e1[ci]), b = dot3(d, h.e2[ci]);
-    const float ri = __builtin_amdgcn_rsqf(fmaxf(fmaf(a, a, b * b), 1e-30f));
-    float pt[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) pt[k] = h.c[ci][k] + (a * h.e1[ci][k] + b * h.e2[ci][k]) * ri;
-    const float v = dot3(d, pt);
-    const bool take = ci == 0 || v > best;
-    best = take ? v : best;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) o[k] = take ? pt[k] : o[k];
-  }
-}
 struct SelfContact { float x[3], sep, n[3]; };
-// GJK sub-simplex candidates (newest point a, retained points S): the affine projection of the
-// origin onto {a, S_I} / {a, S_I, S_J} with positive barycentric weights, kept if strictly shorter
-template <int I>
-__device__ __forceinline__ void gjk_seg(const float a[3], const float S[3][3], float& best, float bv[3], float bl[3],
-                                        unsigned& bm) {
-  float e[3];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) e[k] = S[I][k] - a[k];
-  const float ee = dot3(e, e);
-  const float t = -dot3(a, e) / fmaxf(ee, 1e-30f);
-  float p[3];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) p[k] = a[k] + t * e[k];
-  const float d2 = dot3(p, p);
-  const bool ok = ee > 1e-20f && t > 0.f && t < 1.f && d2 < best;
-  best = ok ? d2 : best;
-  bm = ok ? (1u << I) : bm;
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    bv[k] = ok ? p[k] : bv[k];
-    bl[k] = ok ? (k == I ? t : 0.f) : bl[k];
-  }
-}
-template <int I, int J>
-__device__ __forceinline__ void gjk_tri(const float a[3], const float S[3][3], float& best, float bv[3], float bl[3],
-                                        unsigned& bm) {
-  float e1[3], e2[3];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) { e1[k] = S[I][k] - a[k]; e2[k] = S[J][k] - a[k]; }
-  const float g00 = dot3(e1, e1), g01 = dot3(e1, e2), g11 = dot3(e2, e2);
-  const float r0 = -dot3(a, e1), r1 = -dot3(a, e2);
-  const float det = g00 * g11 - g01 * g01;
-  const float id = 1.f / (fabsf(det) > 1e-30f ? det : 1e-30f);
-  const float ts = (r0 * g11 - r1 * g01) * id, tt = (g00 * r1 - g01 * r0) * id;
-  float p[3];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) p[k] = a[k] + ts * e1[k] + tt * e2[k];
-  const float d2 = dot3(p, p);
-  const bool ok = det > 1e-24f * g00 * g11 && ts > 0.f && tt > 0.f && ts + tt < 1.f && d2 < best;
-  best = ok ? d2 : best;
-  bm = ok ? ((1u << I) | (1u << J)) : bm;
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    bv[k] = ok ? p[k] : bv[k];
-    bl[k] = ok ? (k == I ? ts : (k == J ? tt : 0.f)) : bl[k];
-  }
-}
-
 // Cheap separation test before GJK: separating-axis gaps along the centre difference and the four
 // circle normals (each circle's extent along u is c.u +- |(u.E1, u.E2)|, exact). True when one
 // gap exceeds lim = margin + 2 kCoreM: the cores are farther apart than any contact. A rigorous
@@ -993,7 +932,8 @@ __device__ __forceinline__ bool hulls_separated(const Hull& A, const Hull& B, fl
 // first shortest in that order. ~2x fewer instructions per iteration than one lane per pair, and
 // the 4 quads of a team run up to 4 pairs at once (the usual count of undecided pairs).
 // Starts from v0 (B -> A): the pair's contact normal of the previous substep of this step (warm
-// start) or the hull centre difference. Stops when (|v|^2 - v.w) / |v| <= kGjkTol (the distance
+// start, the first three supports along tilted directions: gjk_tilted) or the hull centre
+// difference. Stops when (|v|^2 - v.w) / |v| <= kGjkTol (the distance
 // bounds |v| and v.w / |v| agree), after kGjkMaxIt iterations, or as soon as the lower bound
 // v.w / |v| exceeds early_margin + 2 kCoreM (no contact; early_margin = margin in the counting
 // pass, huge when a counted contact is re-computed). Contact: n = (pa - pb) / d (B -> A),
@@ -1098,8 +1038,25 @@ __device__ __forceinline__ void quad_deep(const QCircle& h, int j, float n[3], f
 #pragma unroll
   for (int k = 0; k < 3; ++k) { n[k] = nb[k]; x[k] = 0.5f * (ca[k] + cb[k]); }
 }
-__device__ __forceinline__ bool gjk_quad(const QCircle& h, int j, const float v0[3], float margin, float early_margin,
-                                         SelfContact& out, int& iters) {
+// Warm start (tilt): the first three support directions are v0 tilted by kGjkTilt toward three
+// directions 120 degrees apart, so the simplex spans a flat face at once (a support along a face
+// normal is an arbitrary rim point); a stop test only along v itself.
+__device__ __forceinline__ void gjk_tilted(const float v0[3], int k, float d[3]) {
+  const float iv = __builtin_amdgcn_rsqf(dot3(v0, v0));
+  const float u[3] = {v0[0] * iv, v0[1] * iv, v0[2] * iv};
+  const bool x = fabsf(u[0]) < 0.57f, y = !x && fabsf(u[1]) < 0.57f, z = !x && !y;
+  const float ax[3] = {x ? 1.f : 0.f, y ? 1.f : 0.f, z ? 1.f : 0.f};
+  float t1[3], t2[3];
+  cross3(u, ax, t1);
+  const float it1 = __builtin_amdgcn_rsqf(dot3(t1, t1));
+  t1[0] *= it1; t1[1] *= it1; t1[2] *= it1;
+  cross3(u, t1, t2);
+  const float tc = k == 0 ? 1.f : -0.5f, ts = k == 0 ? 0.f : (k == 1 ? 0.8660254f : -0.8660254f);
+#pragma unroll
+  for (int a = 0; a < 3; ++a) d[a] = u[a] + kGjkTilt * (tc * t1[a] + ts * t2[a]);
+}
+__device__ __forceinline__ bool gjk_quad(const QCircle& h, int j, const float v0[3], bool tilt, float margin,
+                                         float early_margin, SelfContact& out, int& iters) {
   float v[3] = {v0[0], v0[1], v0[2]};
   const float lim = early_margin + 2.f * kCoreM;
   // simplex S0..S2 (n points; S0 = the newest of the previous iteration) with their A-side
@@ -1111,10 +1068,13 @@ __device__ __forceinline__ bool gjk_quad(const QCircle& h, int j, const float v0
     iters = it;
     const float vv = dot3(v, v);
     if (n > 0 && vv < 1e-12f) { overlap = true; break; }
+    float dir[3] = {v[0], v[1], v[2]};
+    const bool tilted = tilt && it < 3;  // (it is wave-uniform)
+    if (it < 3 && tilt) gjk_tilted(v0, it, dir);
     float pa[3], aw[3];
     {
       float pb[3];
-      quad_support(h, v, j, pa, pb);
+      quad_support(h, dir, j, pa, pb);
 #pragma unroll
       for (int k = 0; k < 3; ++k) aw[k] = pa[k] - pb[k];
     }
@@ -1124,9 +1084,11 @@ __device__ __forceinline__ bool gjk_quad(const QCircle& h, int j, const float v0
       n = 1;
       continue;
     }
-    const float vw = dot3(v, aw);
-    if (vw > 0.f && vw * vw > vv * lim * lim) return false;
-    if (vv - vw <= kGjkTol * sqrtf(vv)) break;  // distance bounds within kGjkTol
+    // any direction bounds the distance from below by its support gap dir.w / |dir|: no contact
+    // once that exceeds the margin; converged when the gap along v itself is within kGjkTol of |v|
+    const float lo = dot3(dir, aw) * __builtin_amdgcn_rsqf(dot3(dir, dir));
+    if (lo > lim) return false;
+    if (!tilted && sqrtf(vv) - lo <= kGjkTol) break;  // distance bounds within kGjkTol
     // this lane's candidates with the new point a = aw: the segment {a, S_j} (j < 3) and the
     // triangle {a, S_I, S_J} (j = 1: I, J = 0, 1; j = 2: 0, 2; j = 3: 1, 2); lane 0 starts from {a}
     float best = j == 0 ? dot3(aw, aw) : 3.0e38f, bv[3] = {aw[0], aw[1], aw[2]}, l1 = 0.f, l2 = 0.f;
@@ -1412,16 +1374,18 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q&
             quad_centres(hc, ca, cb);
             v0[0] = ca[0] - cb[0]; v0[1] = ca[1] - cb[1]; v0[2] = ca[2] - cb[2];
           }
+          bool hot = false;  // warm start from a kept contact of the previous substep
           if (warm) {
 #pragma unroll
             for (int c = 0; c < NCM; ++c) {
               const float4 f = q.frc(c);
               const bool m = f.w == (float)(pcode + 1);
               v0[0] = m ? f.x : v0[0]; v0[1] = m ? f.y : v0[1]; v0[2] = m ? f.z : v0[2];
+              hot = hot || m;
             }
           }
           int its = 0;
-          const bool h = gjk_quad(hc, qj, v0, pass == 0 ? margin : 1e30f, pass == 0 ? margin : 1e30f, sc, its);
+          const bool h = gjk_quad(hc, qj, v0, hot, pass == 0 ? margin : 1e30f, pass == 0 ? margin : 1e30f, sc, its);
           if (qj == 0) {
             sp.count(kStampCount0, 1);
             sp.count(kStampCount0 + 1, its);
@@ -2882,7 +2846,7 @@ __global__ void zb_gjk_kernel(const float* __restrict__ pairs, const float* __re
     for (int k = 0; k < 3; ++k) v0[k] = v0s[(size_t)pr * 3 + k];
   SelfContact sc = {};
   int its = 0;
-  const bool hit = gjk_quad(h, j, v0, margin, margin, sc, its);
+  const bool hit = gjk_quad(h, j, v0, v0s != nullptr, margin, margin, sc, its);
   if (j == 0 && (t >> 2) < n) {
     float* o = out + (size_t)pr * 9;
     o[0] = hit ? 1.f : 0.f;
