@@ -59,6 +59,9 @@ extern "C" {
 #define ZB_MAX_CONTACTS 12    /* contact slots per env per substep (deepest kept); -D for the cap A/B build (<= 16) */
 #endif
 
+#define ZB_WARM_SLOTS 4       /* persistent self-contact cache: kept self contacts carried to the next step */
+#define ZB_WARM_ROWS (4 * ZB_WARM_SLOTS) /* {n.x, n.y, n.z, code} per slot (code -1: none), rows x N */
+
 #define ZB_TASK_WALKING_V2 0  /* zbot-6b-walking-v2 (v2.py) */
 #define ZB_TASK_STANDUP_V0 1  /* zbot-6b-standup-v0 (standup.py) */
 #define ZB_TASK_WALKING_V4 2  /* zbot-6b-walking-v4 (v4.py): v2 + commands, events, curricula */
@@ -348,10 +351,19 @@ int zb_read_log(zb_handle h, float* term_means, int32_t* counts, void* stream);
  * unregisters. */
 int zb_set_log_buffers(zb_handle h, float* term_means, int32_t* counts);
 
-/* Persistent state, device float[zb_state_dim(h)][N] (ZB_STATE_DIM / ZB_SU_STATE_DIM). */
+/* Persistent state, device float[zb_state_dim(h)][N] (ZB_STATE_DIM / ZB_SU_STATE_DIM).
+ * zb_set_state also invalidates the contact cache below. */
 int zb_state_dim(zb_handle h);
 int zb_get_state(zb_handle h, float* dst, void* stream);
 int zb_set_state(zb_handle h, const float* src, void* stream);
+
+/* Walking v2: the solver's persistent self-contact cache, device float[ZB_WARM_ROWS][N] ({normal,
+ * code} of the first ZB_WARM_SLOTS kept self contacts of the last substep; code -1: none), the GJK
+ * warm start of the next step's first substep. Simulator-internal like PhysX's contact cache (no
+ * reference analogue: Isaac Lab never reads it); zb_set_state and resets invalidate it. Parity
+ * tests copy it to the oracle for lock-step comparisons. Other tasks: error. */
+int zb_get_contact_cache(zb_handle h, float* dst, void* stream);
+int zb_set_contact_cache(zb_handle h, const float* src, void* stream);
 
 /* Parity/debug: run `nsub` physics substeps with joint targets float[N][6] (no MDP);
  * if net_force != NULL it receives the last substep's net contact force, float[N][12][3],

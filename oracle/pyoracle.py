@@ -42,6 +42,8 @@ def _load(double: bool = False):
     lib.zbo_read_log.argtypes = [P, _f, _i]
     lib.zbo_get_state.argtypes = [P, _f]
     lib.zbo_set_state.argtypes = [P, _f]
+    lib.zbo_get_contact_cache.argtypes = [P, _f]
+    lib.zbo_set_contact_cache.argtypes = [P, _f]
     lib.zbo_physics_substeps.argtypes = [P, _f, C.c_int, C.c_void_p, C.c_void_p]
     lib.zbo_link_poses.argtypes = [P, _f, _f]
     lib.zbo_contact_diag.argtypes = [P, _f]
@@ -156,6 +158,14 @@ class OracleSim:
 
     def set_state(self, st):
         self.lib.zbo_set_state(self.h, f32(st))
+
+    def get_contact_cache(self):
+        wc = np.zeros((16, self.n), np.float32)
+        self.lib.zbo_get_contact_cache(self.h, wc)
+        return wc
+
+    def set_contact_cache(self, wc):
+        self.lib.zbo_set_contact_cache(self.h, f32(wc))
 
     def physics_substeps(self, targets, nsub):
         nf = np.zeros((self.n, zm.NUM_LINKS, 3), np.float32)

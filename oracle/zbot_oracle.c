@@ -191,7 +191,14 @@ typedef struct {
   real ep_sums[ZB_MAX_REWARD_TERMS];
 } mdp_t;
 
-typedef struct { phys_t ph; mdp_t md; } env_t;
+/* persistent self-contact cache (walking v2): {n, code} of the first ZB_WARM_SLOTS
+ * kept self contacts of the previous step's last substep, the GJK warm start of the next step's
+ * first substep (code = (la << 4) + lb + 1; -1: none). Not part of the state rows: set_state and
+ * resets invalidate it; zbo_{get,set}_contact_cache copy it (ZB_WARM_ROWS x N, the kernel's rows). */
+typedef struct { phys_t ph; mdp_t md; float wc[ZB_WARM_ROWS]; } env_t;
+static void wc_invalidate(float* wc) {
+  for (int r = 0; r < ZB_WARM_ROWS; ++r) wc[r] = (r & 3) == 3 ? -1.f : 0.f;
+}
 
 struct zbo_sim {
   mdl_t m;
@@ -1385,6 +1392,7 @@ static void reset_env(const mdl_t* m, const zb_task_cfg* cfg, env_t* e) {
   md->ep_len = 0;
   for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) md->ep_sums[t] = 0;
   /* NOT reset (reference quirk): feet_step_len, feet_f_last */
+  wc_invalidate(e->wc); /* the pose jumped: no warm start */
 }
 
 static void write_obs(const mdl_t* m, const env_t* e, float* obs) {
@@ -2419,6 +2427,7 @@ zbo_sim* zbo_create(const zb_model* model, const zb_task_cfg* cfg, int num_envs,
   s->env = (env_t*)calloc((size_t)num_envs, sizeof(env_t));
   for (int i = 0; i < num_envs; ++i) {
     memset(&s->env[i], 0, sizeof(env_t));
+    wc_invalidate(s->env[i].wc);
     phys_default(&s->m, &s->env[i].ph); /* the spawn pose: what the construction-time reset's latch reads */
     if (cfg->task == ZB_TASK_STANDUP_V0) {
       for (int l = 0; l < NL; ++l) { s->env[i].md.mu[l] = cfg->friction; s->env[i].md.mu_d[l] = cfg->friction_dynamic; }
@@ -2519,9 +2528,26 @@ static real step_env(const mdl_t* m, const zb_task_cfg* cfg, env_t* e, const flo
   substep_out_t so;
   clist_t wl;
   wl.n = 0;
+  for (int r = 0; r < ZB_WARM_SLOTS; ++r) { /* the first substep's warm start: the cache */
+    const int code = (int)e->wc[4 * r + 3];
+    if (code < 1) continue;
+    contact_t* c = &wl.c[wl.n++];
+    c->la = code >> 4; c->lb = (code & 15) - 1;
+    for (int a = 0; a < 3; ++a) c->n[a] = e->wc[4 * r + a];
+  }
   for (int k = 0; k < cfg->decimation; ++k) {
     substep(m, cfg, &e->ph, target, NULL, NULL, &wl, &so);
     sensor_update(m, cfg, md, so.net_force);
+  }
+  { /* the last substep's kept self contacts, in slot order, into the cache */
+    int r = 0;
+    wc_invalidate(e->wc);
+    for (int j = 0; j < wl.n && r < ZB_WARM_SLOTS; ++j) {
+      if (wl.c[j].lb < 0) continue;
+      for (int a = 0; a < 3; ++a) e->wc[4 * r + a] = (float)wl.c[j].n[a];
+      e->wc[4 * r + 3] = (float)((wl.c[j].la << 4) + wl.c[j].lb + 1);
+      ++r;
+    }
   }
   md->ep_len += 1;
   /* post-step reads */
@@ -2686,7 +2712,19 @@ int zbo_get_state(zbo_sim* s, float* dst) {
     else pack_env(&s->env[e], dst, s->n, e);
   return 0;
 }
+/* the persistent self-contact cache (walking v2): ZB_WARM_ROWS x N floats, the kernel's layout */
+int zbo_get_contact_cache(zbo_sim* s, float* dst) {
+  for (int e = 0; e < s->n; ++e)
+    for (int r = 0; r < ZB_WARM_ROWS; ++r) dst[(size_t)r * s->n + e] = s->env[e].wc[r];
+  return 0;
+}
+int zbo_set_contact_cache(zbo_sim* s, const float* src) {
+  for (int e = 0; e < s->n; ++e)
+    for (int r = 0; r < ZB_WARM_ROWS; ++r) s->env[e].wc[r] = src[(size_t)r * s->n + e];
+  return 0;
+}
 int zbo_set_state(zbo_sim* s, const float* src) {
+  for (int e = 0; e < s->n; ++e) wc_invalidate(s->env[e].wc); /* a new state: no warm start */
   for (int e = 0; e < s->n; ++e)
     if (s->c.task == ZB_TASK_STANDUP_V0) su_unpack_env(&s->env[e], src, s->n, e);
     else if (s->c.task == ZB_TASK_WALKING_V4) v4_unpack_env(&s->env[e], src, s->n, e);

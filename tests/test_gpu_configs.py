@@ -46,12 +46,14 @@ def test_c1_four_envs_1000_steps(gpu):
     unexplained, outside, resets = [], 0, 0
     for k in range(1000):
         a = rng.standard_normal((4, 6)).astype(np.float32)
+        wc = g.get_contact_cache().cpu().numpy()  # the solver's self-contact cache (lock-step: copied)
         obs, rew, te, tr = g.step(torch.from_numpy(a).cuda())
         obs, rew, te, tr = obs.cpu().numpy(), rew.cpu().numpy(), te.cpu().numpy().copy(), tr.cpu().numpy().copy()
         st1 = g.get_state().cpu().numpy()
         log_g = g.read_log()
         c1_step_invariants(k, st, st1, obs, rew, te, tr, log_g[1].cpu().numpy())
         o.set_state(st)
+        o.set_contact_cache(wc)
         ob_o, rw_o, te_o, tr_o = o.step(a)
         ratio, ratio_rows, err, tol, flags_bad = compare("v2", st1, o.get_state(), obs, ob_o, rew, rw_o, (te, tr),
                                                          (te_o, tr_o), st, 1)

@@ -29,7 +29,7 @@ def _sims(task, n, seed):
     return ZbotSim(n, cfg, device="cuda:0", seed=seed), OracleSim(n, cfg, seed=seed), cfg, torch
 
 
-def _run_oracle(task, n, seed, st, actions, rng=None, scale=1.0):
+def _run_oracle(task, n, seed, st, actions, rng=None, scale=1.0, wc=None):
     """The oracle from state ``st``; with ``rng`` the physics rows are perturbed at ~1e-6 (x scale)
     before every step (rounding-level noise injected along the whole trajectory, as the GPU's own
     rounding differences are)."""
@@ -39,15 +39,19 @@ def _run_oracle(task, n, seed, st, actions, rng=None, scale=1.0):
     # the oracle's by more than 1e-6 per step once it passes through 80 substeps of contact solves
     rel, ab = (1e-6 * scale, 1e-7 * scale) if len(actions) == 1 else (1e-5, 1e-6)
     o.set_state(st if rng is None else perturb_physics(st, rng, rel, ab))
+    if wc is not None:  # walking v2: the solver's self-contact cache the GPU started from
+        o.set_contact_cache(wc)
     out = []
     for k, a in enumerate(actions):
-        if rng is not None and k > 0:
+        if rng is not None and k > 0:  # (the solver's contact cache survives the perturbation)
+            wc = o.get_contact_cache()
             o.set_state(perturb_physics(o.get_state(), rng, rel, ab))
+            o.set_contact_cache(wc)
         out.append(o.step(a))
     return o.get_state(), out
 
 
-def _sensitivity(task, n, seed, st, actions, so, obs_o, rew_o, fl_o, before, nsteps):
+def _sensitivity(task, n, seed, st, actions, so, obs_o, rew_o, fl_o, before, nsteps, wc=None):
     """Max over K perturbed oracle runs (physics rows x (1 +- 1e-6); one-step runs also at 1e-5 and
     1e-4) of each env's error ratio vs the unperturbed oracle; over
     runs with GJK's stopping tolerance scaled by 1/4, 1/2, 2 and 4 (where GJK stops is a discontinuity of
@@ -75,7 +79,7 @@ def _sensitivity(task, n, seed, st, actions, so, obs_o, rew_o, fl_o, before, nst
         if fs is not None:
             lib().zbo_set_sensor_force_scale(fs)
         try:
-            sk, outs = _run_oracle(task, n, seed, st, actions, r_, scale)
+            sk, outs = _run_oracle(task, n, seed, st, actions, r_, scale, wc)
         finally:
             if tol is not None:
                 lib().zbo_set_gjk_tol(0.0)
@@ -118,8 +122,8 @@ def _row_names(task):
     return names
 
 
-def _check(task, label, n, seed, st, actions, g_out, sg, torch):
-    so, outs = _run_oracle(task, n, seed, st, actions)
+def _check(task, label, n, seed, st, actions, g_out, sg, torch, wc=None):
+    so, outs = _run_oracle(task, n, seed, st, actions, wc=wc)
     ob_o, rw_o, te_o, tr_o = outs[-1]
     ob_g, rw_g, te_g, tr_g = g_out
     nsteps = len(actions)
@@ -128,7 +132,7 @@ def _check(task, label, n, seed, st, actions, g_out, sg, torch):
     bad = np.nonzero(ratio > 1)[0]
     sens = np.zeros(n)
     if len(bad):
-        sens = _sensitivity(task, n, seed, st, actions, so, ob_o, rw_o, (te_o, tr_o), st, nsteps)
+        sens = _sensitivity(task, n, seed, st, actions, so, ob_o, rw_o, (te_o, tr_o), st, nsteps, wc)
     _report(task, label, ratio, ratio_rows, err, tol, flags_bad, sens, _row_names(task))
     # explained: the oracle's own rounding-level perturbations push the env past the tolerance, or
     # move it by at least half of the GPU's deviation (an env sitting at the tolerance edge)
@@ -224,3 +228,43 @@ def test_full_state_tgs(gpu, task):
         nbad = _check(task, f"TGS: {steps} zero-action steps from standing", n, seed, st,
                       [np.zeros((n, 6), np.float32)] * steps, g_out, g.get_state().cpu().numpy(), torch)
         assert nbad <= 0.05 * n
+
+
+def test_full_state_contact_cache(gpu):
+    """Walking v2's persistent self-contact cache (the first substep's GJK warm start, DESIGN.md
+    §3.2): from states of a random-action rollout (self contacts present) and the oracle's cache of
+    those states, set into the GPU handle, one step on both sides; every state row under the
+    full-state rule (the oracle run from the same cache), and the cache after the step: pair codes
+    identical in >= 99 % of the (slot, env) entries, normals within 2e-3 where the codes agree."""
+    from oracle.pyoracle import OracleSim
+    task, seed, n = "v2", 23, 2048
+    o = OracleSim(n, task_cfg(task), seed=seed)
+    o.reset()
+    rng = np.random.default_rng(77)
+    for _ in range(30):
+        o.step(rng.normal(size=(n, 6)).astype(np.float32) * 2)
+    st, wc = o.get_state(), o.get_contact_cache()
+    hot = (wc[3::4] >= 1).any(axis=0)
+    assert hot.sum() >= 50, hot.sum()
+    g, _, cfg, torch = _sims(task, n, seed)
+    g.set_state(torch.from_numpy(st).cuda())
+    g.set_contact_cache(torch.from_numpy(wc).cuda())
+    np.testing.assert_array_equal(g.get_contact_cache().cpu().numpy(), wc)
+    a = rng.normal(size=(n, 6)).astype(np.float32)
+    obs, rew, te, tr = g.step(torch.from_numpy(a).cuda())
+    g_out = (obs.cpu().numpy(), rew.cpu().numpy(), te.cpu().numpy().copy(), tr.cpu().numpy().copy())
+    sg, wg = g.get_state().cpu().numpy(), g.get_contact_cache().cpu().numpy()
+    _check(task, "one step from a rollout state with its contact cache", n, seed, st, [a], g_out, sg, torch, wc=wc)
+    o2 = OracleSim(n, task_cfg(task), seed=seed)
+    o2.set_state(st)
+    o2.set_contact_cache(wc)
+    o2.step(a)
+    wo = o2.get_contact_cache()
+    same = wg[3::4] == wo[3::4]
+    assert same.mean() >= 0.99, same.mean()
+    both = same & (wo[3::4] >= 1)
+    assert both.sum() >= 50, both.sum()
+    dn = np.abs(np.stack([wg[k::4] for k in range(3)]) - np.stack([wo[k::4] for k in range(3)])).max(axis=0)
+    assert (dn[both] <= 2e-3).mean() >= 0.98, np.sort(dn[both])[-10:]
+    # the in-kernel auto-reset invalidates a resetting env's entries
+    assert (wg[3::4][:, g_out[2] | g_out[3]] == -1).all()

@@ -1,0 +1,87 @@
+"""The solver's persistent self-contact cache (walking v2; DESIGN.md §3.2, include/zbot.h
+zb_get_contact_cache): {normal, pair code} of the first ZB_WARM_SLOTS kept self contacts of a
+step's last substep, the GJK warm start of the next step's first substep. Oracle side (CPU); the
+kernel's copy is compared with it in tests/test_gpu_selfcollision.py.
+
+* after random-action steps the cache holds valid pair codes (non-adjacent links, la < lb) with
+  unit normals, filled from slot 0, one entry per pair;
+* set_state and reset invalidate it, get / set round-trip it;
+* it only changes where GJK starts: one step from the same state with the cache and without agrees
+  to the GJK tolerance's effect on the contact normal (velocities within 2e-2 m/s in 99 % of envs).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from oracle import pyoracle
+from zbot_lab_amd import model as zm
+
+SLOTS = 4
+
+
+def _rollout(n=256, steps=40, seed=1):
+    sim = pyoracle.OracleSim(n, seed=seed)
+    sim.reset()
+    rng = np.random.default_rng(seed)
+    for _ in range(steps):
+        sim.step(rng.normal(size=(n, 6)).astype(np.float32) * 2)
+    return sim, rng
+
+
+def _codes(wc):
+    return wc[3::4].round().astype(np.int64)  # [SLOTS, N]
+
+
+def test_cache_holds_the_last_substeps_self_contacts():
+    sim, _ = _rollout()
+    wc = sim.get_contact_cache()
+    assert wc.shape == (4 * SLOTS, sim.n)
+    codes = _codes(wc)
+    valid = codes >= 1
+    assert valid.any(), "random-action rollouts produce self contacts"
+    la, lb = codes[valid] >> 4, (codes[valid] & 15) - 1
+    assert ((lb >= la + 2) & (lb < zm.NUM_LINKS)).all()  # non-adjacent pairs, canonical order
+    n = np.stack([wc[0::4], wc[1::4], wc[2::4]])  # [3, SLOTS, N]
+    np.testing.assert_allclose(np.linalg.norm(n[:, valid], axis=0), 1.0, atol=1e-4)
+    # slots fill from 0: no valid slot after an empty one; codes of one env distinct
+    for e in range(sim.n):
+        v = valid[:, e]
+        assert (v[:-1] | ~v[1:]).all(), codes[:, e]
+        c = codes[v, e]
+        assert len(set(c.tolist())) == len(c)
+    assert (codes[~valid] == -1).all()
+
+
+def test_cache_invalidated_by_set_state_and_reset():
+    sim, _ = _rollout()
+    wc = sim.get_contact_cache()
+    assert (_codes(wc) >= 1).any()
+    st = sim.get_state()
+    sim.set_state(st)
+    assert (_codes(sim.get_contact_cache()) == -1).all()
+    sim.set_contact_cache(wc)
+    np.testing.assert_array_equal(sim.get_contact_cache(), wc)
+    hot = np.nonzero((_codes(wc) >= 1).any(axis=0))[0]
+    sim.reset(hot[:1].astype(np.int32))
+    after = _codes(sim.get_contact_cache())
+    assert (after[:, hot[0]] == -1).all()
+    others = np.setdiff1d(np.arange(sim.n), hot[:1])
+    np.testing.assert_array_equal(after[:, others], _codes(wc)[:, others])
+
+
+def test_cache_only_moves_the_gjk_start():
+    sim, rng = _rollout(n=512, steps=30, seed=3)
+    st, wc = sim.get_state(), sim.get_contact_cache()
+    a = rng.normal(size=(sim.n, 6)).astype(np.float32) * 2
+    sim.set_state(st)
+    sim.set_contact_cache(wc)
+    sim.step(a)
+    warm = sim.get_state()
+    sim.set_state(st)  # cold: no cache
+    sim.step(a)
+    cold = sim.get_state()
+    vel = np.r_[7:13, 19:25]  # root twist + joint velocities (include/zbot.h ZB_S_ROOT_LINVEL.. / JOINT_VEL)
+    d = np.abs(warm[vel] - cold[vel]).max(axis=0)
+    assert (d <= 2e-2).mean() >= 0.99, np.sort(d)[-10:]
+    hot = (_codes(wc) >= 1).any(axis=0)
+    assert hot.sum() > 10

@@ -44,6 +44,8 @@ def lib():
     L.zb_set_log_buffers.argtypes = [P, P, P]
     L.zb_get_state.argtypes = [P, P, P]
     L.zb_set_state.argtypes = [P, P, P]
+    L.zb_get_contact_cache.argtypes = [P, P, P]
+    L.zb_set_contact_cache.argtypes = [P, P, P]
     L.zb_physics_substeps.argtypes = [P, P, C.c_int, P, P, P]
     L.zb_profile_begin.argtypes = [P, C.c_int]
     L.zb_profile_end.argtypes = [P, C.POINTER(C.c_float), C.POINTER(C.c_int)]
@@ -59,7 +61,8 @@ def lib():
     L.zb_read_curriculum.argtypes = [P, C.POINTER(C.c_int32), C.POINTER(C.c_int64)]
     L.zb_gjk_pairs.argtypes = [P, P, C.c_int, C.c_float, P, P]
     for name in ("zb_create", "zb_num_envs", "zb_reset", "zb_step", "zb_observe", "zb_read_log", "zb_set_log_buffers",
-                 "zb_get_state", "zb_set_state", "zb_physics_substeps", "zb_profile_begin", "zb_profile_end",
+                 "zb_get_state", "zb_set_state", "zb_get_contact_cache", "zb_set_contact_cache", "zb_physics_substeps",
+                 "zb_profile_begin", "zb_profile_end",
                  "zb_state_dim", "zb_set_link_friction", "zb_set_link_friction_sd", "zb_read_curriculum", "zb_gjk_pairs"):
         getattr(L, name).restype = C.c_int
     _lib = L
@@ -67,7 +70,8 @@ def lib():
 
 
 EXPORTED = ["zb_create", "zb_destroy", "zb_last_error", "zb_num_envs", "zb_reset", "zb_step", "zb_observe",
-            "zb_read_log", "zb_set_log_buffers", "zb_get_state", "zb_set_state", "zb_physics_substeps", "zb_profile_begin",
+            "zb_read_log", "zb_set_log_buffers", "zb_get_state", "zb_set_state", "zb_get_contact_cache",
+            "zb_set_contact_cache", "zb_physics_substeps", "zb_profile_begin",
             "zb_profile_end", "zb_read_stamps", "zb_read_stamps_slowest", "zb_read_stamp_hist", "zb_state_dim", "zb_set_link_friction", "zb_set_link_friction_sd",
             "zb_read_curriculum", "zb_gjk_pairs"]
 

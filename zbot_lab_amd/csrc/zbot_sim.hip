@@ -654,6 +654,38 @@ __device__ __forceinline__ void mv3f(const float R[9], const float4 v, float o[3
   mv3(R, a, o);
 }
 
+// ------------------------------------------------------------------------- contact cache
+// Persistent self-contact cache (walking v2): rows 4r .. 4r+3 of env i hold
+// {n, code} of the env's r-th kept self contact of the previous step's last substep (code -1:
+// none), so the first substep's GJK is warm-started like the later ones. Lane s of the team owns
+// row s. Invalidated by set_state, resets and the in-kernel auto-reset.
+static_assert(ZB_WARM_ROWS == TL, "one cache row per lane of the team");
+__device__ __forceinline__ float wc_invalid(int s) { return (s & 3) == 3 ? -1.f : 0.f; }
+// the cache into FRC slots 0 .. ZB_WARM_SLOTS-1 (the GJK warm-start lookup), the other slots empty
+__device__ __forceinline__ void wc_load(const Q& q, const float* __restrict__ wc, int N, int i) {
+  const float v = wc[(size_t)q.s * N + i];
+  if (q.s < NCM) q.frc(q.s) = make_float4(0.f, 0.f, 0.f, -1.f);
+  wave_sync();
+  reinterpret_cast<float*>(&q.frc(q.s >> 2))[q.s & 3] = v;
+}
+// this lane's cache row after the last substep: FRC holds its kept contacts {n, code} by slot
+__device__ __forceinline__ float wc_extract(const Q& q) {
+  const float4 f = q.frc(q.s < NCM ? q.s : 0);
+  const bool self = q.s < NCM && f.w >= 1.f && (((int)f.w) & 15) != 0;  // ground codes: 16 l
+  const unsigned M = (unsigned)(__ballot(self) >> (TL * q.e)) & 0xffffu;
+  const int r = q.s >> 2;
+  float v = wc_invalid(q.s);
+  if (r < __popc(M)) v = reinterpret_cast<const float*>(&q.frc(nth_set_bit(M, r)))[q.s & 3];
+  return v;
+}
+__global__ void zb_wc_fill_kernel(int N, float* __restrict__ wc, const int32_t* __restrict__ ids, int n) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n * ZB_WARM_ROWS) return;
+  const int k = t / ZB_WARM_ROWS, r = t % ZB_WARM_ROWS;
+  const int e = ids ? ids[k] : k;
+  if (e >= 0 && e < N) wc[(size_t)r * N + e] = wc_invalid(r);
+}
+
 // ------------------------------------------------------------------------- team kinematics
 // FK as a parallel prefix over the team: lane 0 holds the root (q0, 0), lane b >= 1 the local
 // transform of joint b-1, M = (jpr * qz(q) * jcr, jpp + rot(jpr * qz(q), jcp)); three DPP row
@@ -2518,7 +2550,7 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_step_kernel(const z
                                                           float* __restrict__ st, const float* __restrict__ act,
                                                           float* __restrict__ obs, float* __restrict__ rew,
                                                           uint8_t* __restrict__ term, uint8_t* __restrict__ trunc,
-                                                          float* __restrict__ acc) {
+                                                          float* __restrict__ acc, float* __restrict__ wc) {
   MP m = to_mp(mg);
   __shared__ float4 lds[LDS4];
   const int lane = threadIdx.x;
@@ -2596,15 +2628,17 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_step_kernel(const z
   // 4 physics substeps, each followed by the contact sensor's update (record parked in LDS); the
   // last one's applied torques feed the torques term
   SensorOut so;
+  wc_load(q, wc, N, i);  // the first substep's GJK warm start (later substeps: the previous one's)
   sp.mark(0);
   for (int k = 0; k < cfg.decimation; ++k) {
     // (a compile-time `true` here lets the scheduler reshape the loop into a 36 B/lane spill)
-    substep<false, false, kTgs>(m, cfg, p, target, q, opaque_true(), k > 0, so, nullptr, nullptr, sp);
+    substep<false, false, kTgs>(m, cfg, p, target, q, opaque_true(), true, so, nullptr, nullptr, sp);
     sens_record(q, k, so);
     sp.mark(7);
   }
   m = opaque(m);
   wave_sync();
+  const float wc_row = wc_extract(q);
   const Pre pr = q.pre();
   const float(&a_now)[ND] = pr.a_now;
   const float(&pdel)[ND] = pr.pdel;
@@ -2755,6 +2789,7 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_step_kernel(const z
     obs_q[0] = dq.x; obs_q[1] = dq.y; obs_q[2] = dq.z; obs_q[3] = dq.w;
   }
   log_flush(q, lmask, acc);
+  wc[(size_t)q.s * N + i] = reset ? wc_invalid(q.s) : wc_row;
   sp.mark(12);
 #if ZB_STAGED_STORES
 #define OUT(f) q.stg(f)
@@ -4454,6 +4489,7 @@ struct zb_sim {
   zb_model* d_model;
   float4* d_links;  // per-link collision table [NL][LINK4] (detect)
   float* d_state;
+  float* d_wc = nullptr;  // persistent self-contact cache (walking v2): ZB_WARM_ROWS x n
   float* d_acc;
   float* d_log_means;
   int32_t* d_log_counts;
@@ -4658,6 +4694,12 @@ int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_dev
   }
   if (rc) return rc;
   HIPCHK(hipMemset(h->d_acc, 0, sizeof(float) * ACC_SLOTS * ACC_STRIDE), "hipMemset acc");
+  if (h->task == ZB_TASK_WALKING_V2) {
+    HIPCHK(hipMalloc(&h->d_wc, sizeof(float) * ZB_WARM_ROWS * (size_t)num_envs), "hipMalloc contact cache");
+    zb_wc_fill_kernel<<<(num_envs * ZB_WARM_ROWS + 255) / 256, 256>>>(num_envs, h->d_wc, nullptr, num_envs);
+    rc = launch_check("zb_wc_fill_kernel");
+    if (rc) return rc;
+  }
   HIPCHK(hipDeviceSynchronize(), "zb_create sync");
   *out = h;
   return 0;
@@ -4744,6 +4786,7 @@ void zb_destroy(zb_handle h) {
   (void)hipFree(h->d_model);
   (void)hipFree(h->d_links);
   (void)hipFree(h->d_state);
+  (void)hipFree(h->d_wc);
   (void)hipFree(h->d_acc);
   (void)hipFree(h->d_cnt);
   (void)hipFree(h->d_log_means);
@@ -4791,6 +4834,11 @@ int zb_reset(zb_handle h, const int32_t* env_ids, int n, void* stream) {
                                                       h->cfg.reset_feet_refresh);
   int rc = launch_check("zb_reset_kernel");
   if (rc) return rc;
+  if (h->d_wc) {
+    zb_wc_fill_kernel<<<(cnt * ZB_WARM_ROWS + 255) / 256, 256, 0, s>>>(h->n, h->d_wc, env_ids, cnt);
+    rc = launch_check("zb_wc_fill_kernel");
+    if (rc) return rc;
+  }
   return finalize(h, s, env_ids == nullptr || n == h->n, 1, 0);
 }
 
@@ -4814,7 +4862,7 @@ int zb_step(zb_handle h, const float* actions, float* obs, float* reward, uint8_
               truncated, h->d_acc, h->d_cnt, h->seed);
   else
     ZB_LAUNCH(zb_step_kernel, h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward, terminated,
-              truncated, h->d_acc);
+              truncated, h->d_acc, h->d_wc);
 #undef ZB_LAUNCH
   int rc = launch_check("zb_step_kernel");
   if (prof) {
@@ -4900,6 +4948,26 @@ int zb_set_state(zb_handle h, const float* src, void* stream) {
   HIPCHK(hipMemcpyAsync(h->d_state, src, sizeof(float) * (size_t)h->state_dim * h->n, hipMemcpyDeviceToDevice,
                         (hipStream_t)stream),
          "hipMemcpyAsync state");
+  if (h->d_wc) {  // a new state: no warm start from the old one's contacts
+    zb_wc_fill_kernel<<<(h->n * ZB_WARM_ROWS + 255) / 256, 256, 0, (hipStream_t)stream>>>(h->n, h->d_wc, nullptr, h->n);
+    return launch_check("zb_wc_fill_kernel");
+  }
+  return 0;
+}
+
+int zb_get_contact_cache(zb_handle h, float* dst, void* stream) {
+  if (!h || !dst || !h->d_wc) return set_err(-1, "zb_get_contact_cache (walking v2 handles)", hipSuccess);
+  HIPCHK(hipMemcpyAsync(dst, h->d_wc, sizeof(float) * ZB_WARM_ROWS * (size_t)h->n, hipMemcpyDeviceToDevice,
+                        (hipStream_t)stream),
+         "hipMemcpyAsync contact cache");
+  return 0;
+}
+
+int zb_set_contact_cache(zb_handle h, const float* src, void* stream) {
+  if (!h || !src || !h->d_wc) return set_err(-1, "zb_set_contact_cache (walking v2 handles)", hipSuccess);
+  HIPCHK(hipMemcpyAsync(h->d_wc, src, sizeof(float) * ZB_WARM_ROWS * (size_t)h->n, hipMemcpyDeviceToDevice,
+                        (hipStream_t)stream),
+         "hipMemcpyAsync contact cache");
   return 0;
 }
 

@@ -139,6 +139,19 @@ class ZbotSim:
         nat.check(self.lib.zb_set_state(self._h, nat.ptr(s), _stream(self.device)), "zb_set_state")
         torch.cuda.current_stream(self.device).synchronize()  # `s` may be a temporary
 
+    def get_contact_cache(self) -> torch.Tensor:
+        """walking v2: the solver's persistent self-contact cache [ZB_WARM_ROWS, N] (include/zbot.h)"""
+        wc = torch.empty(16, self.num_envs, dtype=torch.float32, device=self.device)
+        nat.check(self.lib.zb_get_contact_cache(self._h, nat.ptr(wc), _stream(self.device)), "zb_get_contact_cache")
+        return wc
+
+    def set_contact_cache(self, wc: torch.Tensor) -> None:
+        w = wc.to(device=self.device, dtype=torch.float32).contiguous()
+        if w.shape != (16, self.num_envs):
+            raise ValueError(f"contact cache must be [16, {self.num_envs}]")
+        nat.check(self.lib.zb_set_contact_cache(self._h, nat.ptr(w), _stream(self.device)), "zb_set_contact_cache")
+        torch.cuda.current_stream(self.device).synchronize()
+
     def profile_begin(self, max_launches: int) -> None:
         nat.check(self.lib.zb_profile_begin(self._h, int(max_launches)), "zb_profile_begin")
 
