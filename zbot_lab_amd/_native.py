@@ -55,6 +55,8 @@ def lib():
     L.zb_read_stamps_slowest.restype = C.c_int
     L.zb_read_stamp_hist.argtypes = [P]
     L.zb_read_stamp_hist.restype = C.c_int
+    L.zb_read_wave_times.argtypes = [P, C.c_int]
+    L.zb_read_wave_times.restype = C.c_int
     L.zb_state_dim.argtypes = [P]
     L.zb_set_link_friction.argtypes = [P, P, P]
     L.zb_set_link_friction_sd.argtypes = [P, P, P, P]
@@ -72,7 +74,7 @@ def lib():
 EXPORTED = ["zb_create", "zb_destroy", "zb_last_error", "zb_num_envs", "zb_reset", "zb_step", "zb_observe",
             "zb_read_log", "zb_set_log_buffers", "zb_get_state", "zb_set_state", "zb_get_contact_cache",
             "zb_set_contact_cache", "zb_physics_substeps", "zb_profile_begin",
-            "zb_profile_end", "zb_read_stamps", "zb_read_stamps_slowest", "zb_read_stamp_hist", "zb_state_dim", "zb_set_link_friction", "zb_set_link_friction_sd",
+            "zb_profile_end", "zb_read_stamps", "zb_read_stamps_slowest", "zb_read_stamp_hist", "zb_read_wave_times", "zb_state_dim", "zb_set_link_friction", "zb_set_link_friction_sd",
             "zb_read_curriculum", "zb_gjk_pairs"]
 
 

@@ -77,10 +77,15 @@ __device__ unsigned long long g_stamp_slowest[NSTAMP];  // phase cycles of the s
 // [134] ground candidates
 constexpr int kCapCounters = 128;
 __device__ unsigned long long g_stamp_hist[kCapCounters + 8];
+// per-workgroup record of the latest launch (zb_read_wave_times): start / end on the constant-rate
+// clock (s_memrealtime, 100 MHz, comparable across CUs) and the wave's phase cycles
+constexpr int kWaveRec = 2 + kStampCount0, kMaxWaveRecs = 1 << 16;
+__device__ unsigned long long g_wave_rec[kMaxWaveRecs][kWaveRec];
 struct Stamps {
-  unsigned long long t, acc[NSTAMP];
+  unsigned long long t, rt0, acc[NSTAMP];
   unsigned umax, itsum;
   __device__ void begin() {
+    rt0 = __builtin_amdgcn_s_memrealtime();
     t = __builtin_amdgcn_s_memtime();
     for (int k = 0; k < NSTAMP; ++k) acc[k] = 0;
     umax = 0; itsum = 0;
@@ -88,6 +93,9 @@ struct Stamps {
   __device__ void note_pairs(unsigned u) { umax = u > umax ? u : umax; }
   // contact-cap counters of one env-substep (called by the team lead)
   __device__ void note_caps(int n_ground, int n_self, int n_deep) {
+#ifdef ZB_STAMPS_NO_CAPS  // (timing runs: the counters' global atomics would skew the phases)
+    return;
+#endif
     atomicAdd(&g_stamp_hist[kCapCounters], 1ull);
     if (n_ground + min(n_self, NSELF) > NCM) atomicAdd(&g_stamp_hist[kCapCounters + 1], 1ull);
     if (n_self > NSELF) atomicAdd(&g_stamp_hist[kCapCounters + 2], 1ull);
@@ -120,6 +128,11 @@ struct Stamps {
     if ((threadIdx.x & 63) == 0) {
       atomicAdd(&g_stamp_hist[um < 63 ? um : 63], 1ull);
       atomicAdd(&g_stamp_hist[64 + (im / 4 < 63 ? im / 4 : 63)], 1ull);
+    }
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < kMaxWaveRecs) {
+      g_wave_rec[blockIdx.x][0] = rt0;
+      g_wave_rec[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
+      for (int k = 0; k < kStampCount0; ++k) g_wave_rec[blockIdx.x][2 + k] = acc[k];
     }
     if ((threadIdx.x & 63) == 0) {  // slot NSTAMP - 1: the slowest wave's cycles over the launches
       unsigned long long tot = 0;
@@ -582,7 +595,11 @@ constexpr int BODY_OFF = V_END;
 // so unpadded strides of 16 (12) granules would put the team's writes on the same banks
 constexpr int BODY_S = 4 * EPW + ZB_YG_PAD, JNT_S = 3 * EPW + ZB_YG_PAD;
 constexpr int JNT_OFF = BODY_OFF + NB * BODY_S;
+#ifdef ZB_LINKS_LDS  // experiment: the per-link collision table in LDS too (+1.9 KB per workgroup)
+constexpr int LNK_G = 0;
+#else
 constexpr int LNK_G = NL * LINK4;      // link-table granules read from global memory
+#endif
 constexpr int LNK_OFF = JNT_OFF + ND * JNT_S - LNK_G;  // lds[LNK_OFF + t] = links[t] for t >= LNK_G
 constexpr int PRE_OFF = LNK_OFF + LNK4;  // [EPW] Pre records (prologue -> MDP)
 constexpr int PRE4 = 8;                   // float4 per Pre record (30 floats)
@@ -626,7 +643,11 @@ struct Q {
   __device__ __forceinline__ const float4* jtab(int j) const { return b + LNK_OFF + JT_OFF + j * 5; }
   __device__ __forceinline__ const float4* btab(int bb) const { return b + LNK_OFF + BT_OFF + bb * 3; }
   __device__ __forceinline__ float4& cap(int l, int k) const { return b[UB_OFF + (2 * l + k) * EPW + e]; }
+#ifdef ZB_LINKS_LDS
+  __device__ __forceinline__ const float4* link(int l) const { return b + LNK_OFF + l * LINK4; }
+#else
   __device__ __forceinline__ const float4* link(int l) const { return gl + l * LINK4; }
+#endif
   __device__ __forceinline__ int pair_code(int p) const { return reinterpret_cast<const int*>(b + LNK_OFF + NL * LINK4)[p]; }
   __device__ __forceinline__ const float4* dflt() const { return b + LNK_OFF + DFLT_OFF; }
   __device__ __forceinline__ Pre& pre() const { return *reinterpret_cast<Pre*>(b + PRE_OFF + e * PRE4); }
@@ -4763,6 +4784,19 @@ int zb_read_stamp_hist(uint64_t* out136) {
 #else
   (void)out128;
   return set_err(-1, "zb_read_stamp_hist: library built without -DZB_STAMPS", hipSuccess);
+#endif
+}
+// Diagnostic build only (-DZB_STAMPS): per workgroup of the latest step launch {start, end}
+// (s_memrealtime ticks, 100 MHz) and its 13 phase cycle counts; n workgroups.
+int zb_read_wave_times(uint64_t* out, int n) {
+#ifdef ZB_STAMPS
+  if (!out || n < 0 || n > kMaxWaveRecs) return set_err(-1, "zb_read_wave_times", hipSuccess);
+  HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_rec), sizeof(unsigned long long) * kWaveRec * (size_t)n),
+         "hipMemcpyFromSymbol");
+  return 0;
+#else
+  (void)out; (void)n;
+  return set_err(-1, "zb_read_wave_times: library built without -DZB_STAMPS", hipSuccess);
 #endif
 }
 int zb_read_stamps(uint64_t* out16) {
