@@ -401,8 +401,8 @@ int zb_read_stamps_slowest(uint64_t* out16);
  * env-substeps, more than ZB_MAX_CONTACTS candidates, more than 18 self contacts, self contacts on
  * overlapping cores, env-substeps with one, self contacts, ground candidates */
 int zb_read_stamp_hist(uint64_t* out136);
-/* Diagnostic build only: per workgroup of the latest step launch, 15 values {start, end
- * (s_memrealtime, 100 MHz), 13 phase cycle counts}; out [n][15]. */
+/* Diagnostic build only: per workgroup of the latest step launch, 23 values {start, end
+ * (s_memrealtime, 100 MHz), 13 phase cycle counts, 8 substep end times (walking v2)}; out [n][23]. */
 int zb_read_wave_times(uint64_t* out, int n);
 
 /* Test entry: the self-collision GJK (the step kernels' gjk_quad) on n link pairs given as

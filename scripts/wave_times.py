@@ -42,21 +42,36 @@ def main():
     for _ in range(30):
         env.step(torch.randn(n, 6, device="cuda", generator=g))
     torch.cuda.synchronize()
+    # SAVE_STATE=f.npy keeps the post-warm-up state; LOAD_STATE=f.npy replays every timed launch
+    # from it (identical physics work per launch, whatever the library does with its stores)
+    if os.environ.get("SAVE_STATE"):
+        np.save(os.environ["SAVE_STATE"], env.sim.get_state().cpu().numpy())
+    st0 = None
+    if os.environ.get("LOAD_STATE"):
+        st0 = torch.from_numpy(np.load(os.environ["LOAD_STATE"])).cuda()
     K = int(os.environ.get("K", "20"))
-    rec = np.zeros((waves, 15), np.uint64)
-    spread, span, durs, slow_ph, med_ph = [], [], [], [], []
+    rec = np.zeros((waves, 23), np.uint64)
+    spread, span, durs, slow_ph, med_ph, timeline = [], [], [], [], [], []
     for _ in range(K):
+        if st0 is not None:
+            env.sim.set_state(st0)
         env.step(torch.randn(n, 6, device="cuda", generator=g))
         torch.cuda.synchronize()
         nat.check(nat.lib().zb_read_wave_times(rec.ctypes.data_as(C.c_void_p), waves), "zb_read_wave_times")
         t0, t1 = rec[:, 0].astype(np.int64), rec[:, 1].astype(np.int64)
-        ph = rec[:, 2:].astype(np.float64)
+        ph = rec[:, 2:15].astype(np.float64)
+        sub = rec[:, 15:19].astype(np.int64)
         d = (t1 - t0) * TICK_NS / 1e3  # us
         spread.append((t0.max() - t0.min()) * TICK_NS / 1e3)
         span.append((t1.max() - t0.min()) * TICK_NS / 1e3)
         durs.append(d)
         order = np.argsort(d)
         k = max(1, waves // 100)
+        if not timeline:  # the absolute timeline of the 5 slowest and 3 median waves of the first launch
+            base = t0.min()
+            for w in list(order[-5:]) + list(order[waves // 2 - 1: waves // 2 + 2]):
+                marks = [t0[w]] + list(sub[w]) + [t1[w]]
+                timeline.append(f"  wg {w:5d} xcd {w % 8}: " + " ".join(f"{(x - base) * TICK_NS / 1e3:7.1f}" for x in marks))
         slow_ph.append(ph[order[-k:]].mean(axis=0))
         med_ph.append(ph[order[waves // 2 - k // 2: waves // 2 + k // 2 + 1]].mean(axis=0))
     durs = np.concatenate(durs)
@@ -72,6 +87,8 @@ def main():
     for i, nm in enumerate(NAMES):
         print(f"  {nm:32s} {mp[i]:12.0f} {sp[i]:12.0f} {sp[i] - mp[i]:10.0f}")
     print(f"  {'total':32s} {mp.sum():12.0f} {sp.sum():12.0f} {sp.sum() - mp.sum():10.0f}")
+    print("timeline (us from the launch's first wave start): start, end of substeps 1-4, end")
+    print("\n".join(timeline))
 
 
 if __name__ == "__main__":

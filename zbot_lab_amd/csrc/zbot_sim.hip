@@ -66,6 +66,7 @@ __device__ __forceinline__ MP to_mp(const zb_model* m) { return (MP)(uintptr_t)m
 // summed per wave (lane 0) into g_stamps. Never part of the measured product build.
 constexpr int NSTAMP = 16;
 constexpr int kStampCount0 = 13;  // slots 13, 14 count events (GJK calls, iterations); 15 = max wave cycles
+constexpr int kStampSub = 8;      // substep end times per wave record (>= MAXSUB)
 #ifdef ZB_STAMPS
 __device__ unsigned long long g_stamps[NSTAMP];
 __device__ unsigned long long g_stamp_slowest[NSTAMP];  // phase cycles of the slowest wave seen
@@ -79,13 +80,14 @@ constexpr int kCapCounters = 128;
 __device__ unsigned long long g_stamp_hist[kCapCounters + 8];
 // per-workgroup record of the latest launch (zb_read_wave_times): start / end on the constant-rate
 // clock (s_memrealtime, 100 MHz, comparable across CUs) and the wave's phase cycles
-constexpr int kWaveRec = 2 + kStampCount0, kMaxWaveRecs = 1 << 16;
+constexpr int kWaveRec = 2 + kStampCount0 + kStampSub, kMaxWaveRecs = 1 << 16;
 __device__ unsigned long long g_wave_rec[kMaxWaveRecs][kWaveRec];
 struct Stamps {
-  unsigned long long t, rt0, acc[NSTAMP];
+  unsigned long long t, rt0, rsub[kStampSub], acc[NSTAMP];
   unsigned umax, itsum;
   __device__ void begin() {
     rt0 = __builtin_amdgcn_s_memrealtime();
+    for (int k = 0; k < kStampSub; ++k) rsub[k] = 0;
     t = __builtin_amdgcn_s_memtime();
     for (int k = 0; k < NSTAMP; ++k) acc[k] = 0;
     umax = 0; itsum = 0;
@@ -107,6 +109,7 @@ struct Stamps {
     if (n_ground) atomicAdd(&g_stamp_hist[kCapCounters + 6], (unsigned long long)n_ground);
   }
   __device__ void note_its(unsigned its) { itsum += its; }
+  __device__ void substep_end(int k) { rsub[k] = __builtin_amdgcn_s_memrealtime(); }
   __device__ void mark(int k) {
     const unsigned long long n = __builtin_amdgcn_s_memtime();
     acc[k] += n - t;
@@ -115,6 +118,15 @@ struct Stamps {
   // per-lane event counts (slots >= kStampCount0), summed over every lane at flush
   __device__ void count(int k, unsigned v) { acc[k] += v; }
   __device__ void flush() {
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < kMaxWaveRecs) {
+      g_wave_rec[blockIdx.x][0] = rt0;
+      g_wave_rec[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
+      for (int k = 0; k < kStampCount0; ++k) g_wave_rec[blockIdx.x][2 + k] = acc[k];
+      for (int k = 0; k < kStampSub; ++k) g_wave_rec[blockIdx.x][2 + kStampCount0 + k] = rsub[k];
+    }
+#ifdef ZB_STAMPS_WAVE_ONLY  // timing runs: no contended global atomics while other waves still run
+    return;
+#endif
     if ((threadIdx.x & 63) == 0)
       for (int k = 0; k < kStampCount0; ++k) atomicAdd(&g_stamps[k], acc[k]);
     for (int k = kStampCount0; k < NSTAMP - 1; ++k)
@@ -128,11 +140,6 @@ struct Stamps {
     if ((threadIdx.x & 63) == 0) {
       atomicAdd(&g_stamp_hist[um < 63 ? um : 63], 1ull);
       atomicAdd(&g_stamp_hist[64 + (im / 4 < 63 ? im / 4 : 63)], 1ull);
-    }
-    if ((threadIdx.x & 63) == 0 && blockIdx.x < kMaxWaveRecs) {
-      g_wave_rec[blockIdx.x][0] = rt0;
-      g_wave_rec[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
-      for (int k = 0; k < kStampCount0; ++k) g_wave_rec[blockIdx.x][2 + k] = acc[k];
     }
     if ((threadIdx.x & 63) == 0) {  // slot NSTAMP - 1: the slowest wave's cycles over the launches
       unsigned long long tot = 0;
@@ -150,6 +157,7 @@ struct Stamps {
   __device__ void count(int, unsigned) {}
   __device__ void note_pairs(unsigned) {}
   __device__ void note_its(unsigned) {}
+  __device__ void substep_end(int) {}
   __device__ void note_caps(int, int, int) {}
   __device__ void flush() {}
 };
@@ -2656,6 +2664,7 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_step_kernel(const z
     substep<false, false, kTgs>(m, cfg, p, target, q, opaque_true(), true, so, nullptr, nullptr, sp);
     sens_record(q, k, so);
     sp.mark(7);
+    sp.substep_end(k);
   }
   m = opaque(m);
   wave_sync();
