@@ -603,11 +603,7 @@ constexpr int BODY_OFF = V_END;
 // so unpadded strides of 16 (12) granules would put the team's writes on the same banks
 constexpr int BODY_S = 4 * EPW + ZB_YG_PAD, JNT_S = 3 * EPW + ZB_YG_PAD;
 constexpr int JNT_OFF = BODY_OFF + NB * BODY_S;
-#ifdef ZB_LINKS_LDS  // experiment: the per-link collision table in LDS too (+1.9 KB per workgroup)
-constexpr int LNK_G = 0;
-#else
 constexpr int LNK_G = NL * LINK4;      // link-table granules read from global memory
-#endif
 constexpr int LNK_OFF = JNT_OFF + ND * JNT_S - LNK_G;  // lds[LNK_OFF + t] = links[t] for t >= LNK_G
 constexpr int PRE_OFF = LNK_OFF + LNK4;  // [EPW] Pre records (prologue -> MDP)
 constexpr int PRE4 = 8;                   // float4 per Pre record (30 floats)
@@ -651,11 +647,7 @@ struct Q {
   __device__ __forceinline__ const float4* jtab(int j) const { return b + LNK_OFF + JT_OFF + j * 5; }
   __device__ __forceinline__ const float4* btab(int bb) const { return b + LNK_OFF + BT_OFF + bb * 3; }
   __device__ __forceinline__ float4& cap(int l, int k) const { return b[UB_OFF + (2 * l + k) * EPW + e]; }
-#ifdef ZB_LINKS_LDS
-  __device__ __forceinline__ const float4* link(int l) const { return b + LNK_OFF + l * LINK4; }
-#else
   __device__ __forceinline__ const float4* link(int l) const { return gl + l * LINK4; }
-#endif
   __device__ __forceinline__ int pair_code(int p) const { return reinterpret_cast<const int*>(b + LNK_OFF + NL * LINK4)[p]; }
   __device__ __forceinline__ const float4* dflt() const { return b + LNK_OFF + DFLT_OFF; }
   __device__ __forceinline__ Pre& pre() const { return *reinterpret_cast<Pre*>(b + PRE_OFF + e * PRE4); }
