@@ -37,9 +37,10 @@ import torch
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 BYTES_PER_ENV_STEP = 794 + 2 * 16 * 4  # = 922: SURVEY.md §8d's 794 + the contact cache
-SU_BYTES_PER_ENV_STEP = 2 * 43 * 4 + 24 * 4 + 24 + 88 + 4 + 2  # = 558, stand-up task
-V4_BYTES_PER_ENV_STEP = 81 * 4 + 85 * 4 + 24 + 96 + 4 + 2       # = 790, walking v4
-M_BYTES_PER_ENV_STEP = 76 * 4 + 76 * 4 + 24 * 4 + 24 + 100 + 4 + 2  # = 834, manager flat env
+WC_BYTES = 2 * 16 * 4  # the contact cache read + written
+SU_BYTES_PER_ENV_STEP = 2 * 43 * 4 + 24 * 4 + 24 + 88 + 4 + 2 + WC_BYTES  # = 686, stand-up task
+V4_BYTES_PER_ENV_STEP = 81 * 4 + 85 * 4 + 24 + 96 + 4 + 2 + WC_BYTES       # = 918, walking v4
+M_BYTES_PER_ENV_STEP = 76 * 4 + 76 * 4 + 24 * 4 + 24 + 100 + 4 + 2 + WC_BYTES  # = 962, manager flat env
 
 
 def parse():

@@ -357,11 +357,11 @@ int zb_state_dim(zb_handle h);
 int zb_get_state(zb_handle h, float* dst, void* stream);
 int zb_set_state(zb_handle h, const float* src, void* stream);
 
-/* Walking v2: the solver's persistent self-contact cache, device float[ZB_WARM_ROWS][N] ({normal,
+/* The solver's persistent self-contact cache (every task), device float[ZB_WARM_ROWS][N] ({normal,
  * code} of the first ZB_WARM_SLOTS kept self contacts of the last substep; code -1: none), the GJK
  * warm start of the next step's first substep. Simulator-internal like PhysX's contact cache (no
  * reference analogue: Isaac Lab never reads it); zb_set_state and resets invalidate it. Parity
- * tests copy it to the oracle for lock-step comparisons. Other tasks: error. */
+ * tests copy it to the oracle for lock-step comparisons. */
 int zb_get_contact_cache(zb_handle h, float* dst, void* stream);
 int zb_set_contact_cache(zb_handle h, const float* src, void* stream);
 

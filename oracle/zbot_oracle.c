@@ -191,7 +191,7 @@ typedef struct {
   real ep_sums[ZB_MAX_REWARD_TERMS];
 } mdp_t;
 
-/* persistent self-contact cache (walking v2): {n, code} of the first ZB_WARM_SLOTS
+/* persistent self-contact cache (every task): {n, code} of the first ZB_WARM_SLOTS
  * kept self contacts of the previous step's last substep, the GJK warm start of the next step's
  * first substep (code = (la << 4) + lb + 1; -1: none). Not part of the state rows: set_state and
  * resets invalidate it; zbo_{get,set}_contact_cache copy it (ZB_WARM_ROWS x N, the kernel's rows). */
@@ -372,6 +372,31 @@ static void select_contacts(clist_t* L) {
   for (int i = 0; i < L->n; ++i)
     if (keep[i]) L->c[k++] = L->c[i];
   L->n = k;
+}
+
+/* the persistent self-contact cache (env_t.wc) as the first substep's warm-start list, and the
+ * last substep's kept self contacts, in slot order, back into it (the kernel's wc_load /
+ * wc_extract) */
+static void wc_warm_list(const float* wc, clist_t* wl) {
+  wl->n = 0;
+  for (int r = 0; r < ZB_WARM_SLOTS; ++r) {
+    const int code = (int)wc[4 * r + 3];
+    if (code < 1) continue;
+    contact_t* c = &wl->c[wl->n++];
+    c->la = code >> 4; c->lb = (code & 15) - 1;
+    for (int a = 0; a < 3; ++a) c->n[a] = wc[4 * r + a];
+  }
+}
+static void wc_invalidate(float* wc);
+static void wc_store(const clist_t* wl, float* wc) {
+  int r = 0;
+  wc_invalidate(wc);
+  for (int j = 0; j < wl->n && r < ZB_WARM_SLOTS; ++j) {
+    if (wl->c[j].lb < 0) continue;
+    for (int a = 0; a < 3; ++a) wc[4 * r + a] = (float)wl->c[j].n[a];
+    wc[4 * r + 3] = (float)((wl->c[j].la << 4) + wl->c[j].lb + 1);
+    ++r;
+  }
 }
 
 /* ------------------------------------------------------------------ self collision (GJK)
@@ -1471,6 +1496,7 @@ static void pose_from_samples(const mdl_t* m, const real r[4], int body_frame, p
 /* _reset_idx (standup.py:645-703) minus the log: pose event, joints default, p_delta / actions
  * zero, center_z_last 0.05, ep_len 0, episode sums zero; the friction (startup event) stays */
 static void su_reset_env(const mdl_t* m, const zb_task_cfg* cfg, uint64_t seed, uint64_t ctr, int i, env_t* e) {
+  wc_invalidate(e->wc); /* the pose jumps: no warm start */
   su_reset_pose(m, cfg, seed, ctr, i, &e->ph);
   mdp_t* md = &e->md;
   for (int j = 0; j < ND; ++j) { md->p_delta[j] = 0; md->actions[j] = 0; }
@@ -1576,8 +1602,9 @@ static real su_step_env(const mdl_t* m, const zb_task_cfg* cfg, int stage, uint6
   }
   substep_out_t so;
   clist_t wl;
-  wl.n = 0;
+  wc_warm_list(e->wc, &wl);
   for (int k = 0; k < cfg->decimation; ++k) substep(m, cfg, &e->ph, target, md->mu, md->mu_d, &wl, &so);
+  wc_store(&wl, e->wc);
   md->ep_len += 1;
   for (int j = 0; j < ND; ++j) md->actions[j] = act[j];
   su_links_t L;
@@ -1811,6 +1838,7 @@ static void v4_sensor_update(const mdl_t* m, const zb_task_cfg* cfg, mdp_t* md, 
 /* _reset_idx (920-1001) minus the log: reset events (pose; commands), defaults. init: the
  * construction-time interval timer draw. */
 static void v4_reset_env(const zbo_sim* s, uint64_t ctr, int i, env_t* e, int init) {
+  wc_invalidate(e->wc); /* the pose jumps: no warm start */
   const mdl_t* m = &s->m;
   const uint64_t h = env_hash(s->seed, ctr, i);
   mdp_t* md = &e->md;
@@ -1864,13 +1892,14 @@ static real v4_step_env(const zbo_sim* s, int stage, uint64_t ctr, int i, env_t*
   substep_out_t so;
   real jqd_prev[ND];
   clist_t wl;
-  wl.n = 0;
+  wc_warm_list(e->wc, &wl);
   for (int k = 0; k < cfg->decimation; ++k) {
     if (k == cfg->decimation - 1)
       for (int j = 0; j < ND; ++j) jqd_prev[j] = e->ph.jqd[j];
     substep(m, cfg, &e->ph, target, NULL, NULL, &wl, &so);
     v4_sensor_update(m, cfg, md, so.net_force);
   }
+  wc_store(&wl, e->wc);
   md->ep_len += 1;
   v4_post_t P;
   {
@@ -2105,6 +2134,7 @@ static real m_mdp_eval(const zb_task_cfg* cfg, const m_post_t* P, mdp_t* md, con
  * reset_my_data = feet data at the post-reset feet) and the managers' resets (actions,
  * episode sums, command resample + metrics, contact sensor). init: the construction-time reset. */
 static void m_reset_env(const zbo_sim* s, uint64_t ctr, int i, env_t* e) {
+  wc_invalidate(e->wc); /* the pose jumps: no warm start */
   const mdl_t* m = &s->m;
   const uint64_t h = env_hash(s->seed, ctr, i);
   mdp_t* md = &e->md;
@@ -2181,7 +2211,7 @@ static real m_step_env(const zbo_sim* s, uint64_t ctr, int i, env_t* e, const fl
   substep_out_t so;
   real jqd_prev[ND];
   clist_t wl;
-  wl.n = 0;
+  wc_warm_list(e->wc, &wl);
   for (int k = 0; k < cfg->decimation; ++k) {
     real target[ND];
     for (int j = 0; j < ND; ++j) target[j] = e->ph.jq[j] + delta[j]; /* apply_actions: q + delta */
@@ -2203,6 +2233,7 @@ static real m_step_env(const zbo_sim* s, uint64_t ctr, int i, env_t* e, const fl
       md->feet_air_cur[f] = c ? 0 : md->feet_air_cur[f] + (real)cfg->sim_dt;
     }
   }
+  wc_store(&wl, e->wc);
   md->ep_len += 1;
   m_post_t P;
   real vcom[3];
@@ -2527,28 +2558,12 @@ static real step_env(const mdl_t* m, const zb_task_cfg* cfg, env_t* e, const flo
   /* physics */
   substep_out_t so;
   clist_t wl;
-  wl.n = 0;
-  for (int r = 0; r < ZB_WARM_SLOTS; ++r) { /* the first substep's warm start: the cache */
-    const int code = (int)e->wc[4 * r + 3];
-    if (code < 1) continue;
-    contact_t* c = &wl.c[wl.n++];
-    c->la = code >> 4; c->lb = (code & 15) - 1;
-    for (int a = 0; a < 3; ++a) c->n[a] = e->wc[4 * r + a];
-  }
+  wc_warm_list(e->wc, &wl); /* the first substep's warm start: the cache */
   for (int k = 0; k < cfg->decimation; ++k) {
     substep(m, cfg, &e->ph, target, NULL, NULL, &wl, &so);
     sensor_update(m, cfg, md, so.net_force);
   }
-  { /* the last substep's kept self contacts, in slot order, into the cache */
-    int r = 0;
-    wc_invalidate(e->wc);
-    for (int j = 0; j < wl.n && r < ZB_WARM_SLOTS; ++j) {
-      if (wl.c[j].lb < 0) continue;
-      for (int a = 0; a < 3; ++a) e->wc[4 * r + a] = (float)wl.c[j].n[a];
-      e->wc[4 * r + 3] = (float)((wl.c[j].la << 4) + wl.c[j].lb + 1);
-      ++r;
-    }
-  }
+  wc_store(&wl, e->wc);
   md->ep_len += 1;
   /* post-step reads */
   post_t ps;
@@ -2712,7 +2727,7 @@ int zbo_get_state(zbo_sim* s, float* dst) {
     else pack_env(&s->env[e], dst, s->n, e);
   return 0;
 }
-/* the persistent self-contact cache (walking v2): ZB_WARM_ROWS x N floats, the kernel's layout */
+/* the persistent self-contact cache: ZB_WARM_ROWS x N floats, the kernel's layout */
 int zbo_get_contact_cache(zbo_sim* s, float* dst) {
   for (int e = 0; e < s->n; ++e)
     for (int r = 0; r < ZB_WARM_ROWS; ++r) dst[(size_t)r * s->n + e] = s->env[e].wc[r];

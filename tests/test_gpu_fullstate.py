@@ -230,19 +230,21 @@ def test_full_state_tgs(gpu, task):
         assert nbad <= 0.05 * n
 
 
-def test_full_state_contact_cache(gpu):
-    """Walking v2's persistent self-contact cache (the first substep's GJK warm start, DESIGN.md
-    §3.2): from states of a random-action rollout (self contacts present) and the oracle's cache of
-    those states, set into the GPU handle, one step on both sides; every state row under the
+@pytest.mark.parametrize("task", TASKS)
+def test_full_state_contact_cache(gpu, task):
+    """The persistent self-contact cache (the first substep's GJK warm start):
+    from folded states one oracle step after random joint angles (self contacts present) and the
+    oracle's cache of those states, set into the GPU handle, one step on both sides; every state row under the
     full-state rule (the oracle run from the same cache), and the cache after the step: pair codes
     identical in >= 99 % of the (slot, env) entries, normals within 2e-3 where the codes agree."""
     from oracle.pyoracle import OracleSim
-    task, seed, n = "v2", 23, 2048
+    seed, n = 23, 2048
     o = OracleSim(n, task_cfg(task), seed=seed)
-    o.reset()
     rng = np.random.default_rng(77)
-    for _ in range(30):
-        o.step(rng.normal(size=(n, 6)).astype(np.float32) * 2)
+    st = random_states(task, o, n, seed=78)
+    st[13:19] += rng.normal(0, 1.5, (6, n)).astype(np.float32)  # folded: links in contact
+    o.set_state(st)
+    o.step(rng.normal(size=(n, 6)).astype(np.float32))  # one step leaves its self contacts in the cache
     st, wc = o.get_state(), o.get_contact_cache()
     hot = (wc[3::4] >= 1).any(axis=0)
     assert hot.sum() >= 50, hot.sum()

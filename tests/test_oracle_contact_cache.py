@@ -85,3 +85,24 @@ def test_cache_only_moves_the_gjk_start():
     assert (d <= 2e-2).mean() >= 0.99, np.sort(d)[-10:]
     hot = (_codes(wc) >= 1).any(axis=0)
     assert hot.sum() > 10
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.parametrize("task", ["standup", "v4", "manager"])
+def test_cache_in_every_task(task):
+    """The other tasks keep the same cache (their steps warm-start the first substep too)."""
+    from fullstate import random_states, task_cfg
+    sim = pyoracle.OracleSim(256, task_cfg(task), seed=2)
+    st = random_states(task, sim, 256, seed=9)
+    st[13:19] += np.random.default_rng(9).normal(0, 1.5, (6, 256)).astype(np.float32)  # fold: links touch
+    sim.set_state(st)
+    rng = np.random.default_rng(2)
+    sim.step(rng.normal(size=(256, 6)).astype(np.float32))
+    codes = _codes(sim.get_contact_cache())
+    assert (codes >= 1).any(), task
+    la, lb = codes[codes >= 1] >> 4, (codes[codes >= 1] & 15) - 1
+    assert ((lb >= la + 2) & (lb < zm.NUM_LINKS)).all()
+    sim.set_state(sim.get_state())
+    assert (_codes(sim.get_contact_cache()) == -1).all()

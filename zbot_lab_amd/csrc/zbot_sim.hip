@@ -676,7 +676,7 @@ __device__ __forceinline__ void mv3f(const float R[9], const float4 v, float o[3
 }
 
 // ------------------------------------------------------------------------- contact cache
-// Persistent self-contact cache (walking v2): rows 4r .. 4r+3 of env i hold
+// Persistent self-contact cache (every task's step kernel): rows 4r .. 4r+3 of env i hold
 // {n, code} of the env's r-th kept self contact of the previous step's last substep (code -1:
 // none), so the first substep's GJK is warm-started like the later ones. Lane s of the team owns
 // row s. Invalidated by set_state, resets and the in-kernel auto-reset.
@@ -3099,7 +3099,8 @@ template <bool kTgs>
 __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_su_step_kernel(
     const zb_model* __restrict__ mg, const float4* __restrict__ links, zb_task_cfg cfg, int N, float* __restrict__ st,
     const float* __restrict__ act, float* __restrict__ obs, float* __restrict__ rew, uint8_t* __restrict__ term,
-    uint8_t* __restrict__ trunc, float* __restrict__ acc, const Counters* __restrict__ cnt, uint64_t seed) {
+    uint8_t* __restrict__ trunc, float* __restrict__ acc, const Counters* __restrict__ cnt, uint64_t seed,
+    float* __restrict__ wc) {
   MP m = to_mp(mg);
   __shared__ float4 lds[LDS4];
   const int lane = threadIdx.x;
@@ -3139,13 +3140,15 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_su_step_kernel(
   }
 
   SensorOut so;
+  wc_load(q, wc, N, i);  // the first substep's GJK warm start
   sp.mark(0);
   for (int k = 0; k < cfg.decimation; ++k) {
-    substep<false, true, kTgs>(m, cfg, p, target, q, false, k > 0, so, nullptr, nullptr, sp);
+    substep<false, true, kTgs>(m, cfg, p, target, q, false, true, so, nullptr, nullptr, sp);
     sp.mark(7);
   }
   m = opaque(m);
   wave_sync();
+  const float wc_row = wc_extract(q);
   const Pre pr = q.pre();
   st = opaque_ptr(st);
   const float czl0 = ST(ZB_SU_CENTER_Z_LAST);
@@ -3246,6 +3249,7 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_su_step_kernel(
     qmul(p.quat, qrel, obs_q);
   }
   log_flush(q, lmask, acc);
+  wc[(size_t)q.s * N + i] = reset ? wc_invalid(q.s) : wc_row;
   sp.mark(12);
 #if ZB_STAGED_STORES
 #define OUT(f) q.stg(f)
@@ -3399,7 +3403,8 @@ template <bool kTgs>
 __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_v4_step_kernel(
     const zb_model* __restrict__ mg, const float4* __restrict__ links, zb_task_cfg cfg, int N, float* __restrict__ st,
     const float* __restrict__ act, float* __restrict__ obs, float* __restrict__ rew, uint8_t* __restrict__ term,
-    uint8_t* __restrict__ trunc, float* __restrict__ acc, const Counters* __restrict__ cnt, uint64_t seed) {
+    uint8_t* __restrict__ trunc, float* __restrict__ acc, const Counters* __restrict__ cnt, uint64_t seed,
+    float* __restrict__ wc) {
   MP m = to_mp(mg);
   __shared__ float4 lds[LDS4];
   const int lane = threadIdx.x;
@@ -3450,6 +3455,7 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_v4_step_kernel(
   // applied torques feed the torques term, the joint velocities before it give Isaac Lab's
   // finite-difference joint_acc (ArticulationData.update every substep)
   SensorOut so;
+  wc_load(q, wc, N, i);  // the first substep's GJK warm start
   sp.mark(0);
   for (int k = 0; k < cfg.decimation; ++k) {
     const bool last = k == cfg.decimation - 1;
@@ -3457,12 +3463,13 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_v4_step_kernel(
 #pragma unroll
       for (int j = 0; j < ND; ++j) pv.jqd_prev[j] = p.jqd[j];
     }
-    substep<false, false, kTgs>(m, cfg, p, target, q, true, k > 0, so, nullptr, nullptr, sp);
+    substep<false, false, kTgs>(m, cfg, p, target, q, true, true, so, nullptr, nullptr, sp);
     sens_record(q, k, so);
     sp.mark(7);
   }
   m = opaque(m);
   wave_sync();
+  const float wc_row = wc_extract(q);
   const PreV4 pr = pv;
   st = opaque_ptr(st);
 
@@ -3672,6 +3679,7 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_v4_step_kernel(
     he_obs = atan2f(sn, cs);
   }
   log_flush(q, lmask, acc);
+  wc[(size_t)q.s * N + i] = reset ? wc_invalid(q.s) : wc_row;
   sp.mark(12);
 #if ZB_STAGED_STORES
 #define OUT(f) q.stg(f)
@@ -3903,7 +3911,8 @@ template <bool kTgs>
 __global__ __launch_bounds__(WGT, ZB_M_WAVES_PER_SIMD) void zb_m_step_kernel(
     const zb_model* __restrict__ mg, const float4* __restrict__ links, zb_task_cfg cfg, int N, float* __restrict__ st,
     const float* __restrict__ act, float* __restrict__ obs, float* __restrict__ rew, uint8_t* __restrict__ term,
-    uint8_t* __restrict__ trunc, float* __restrict__ acc, const Counters* __restrict__ cnt, uint64_t seed) {
+    uint8_t* __restrict__ trunc, float* __restrict__ acc, const Counters* __restrict__ cnt, uint64_t seed,
+    float* __restrict__ wc) {
   MP m = to_mp(mg);
   __shared__ float4 lds[LDS4];
   const int lane = threadIdx.x;
@@ -3974,6 +3983,7 @@ __global__ __launch_bounds__(WGT, ZB_M_WAVES_PER_SIMD) void zb_m_step_kernel(
       fz_h[h][f] = hist_in ? ST(ZB_M_FEET_FZ_HIST + 2 * h + f) : 0.f;
       fn_h[h][f] = hist_in ? ST(ZB_M_FEET_FN_HIST + 2 * h + f) : 0.f;
     }
+  wc_load(q, wc, N, i);  // the first substep's GJK warm start
   sp.mark(0);
   for (int k = 0; k < cfg.decimation; ++k) {
     float target[ND];
@@ -3983,7 +3993,7 @@ __global__ __launch_bounds__(WGT, ZB_M_WAVES_PER_SIMD) void zb_m_step_kernel(
 #pragma unroll
       for (int j = 0; j < ND; ++j) pv.jqd_prev[j] = p.jqd[j];
     }
-    substep<false, true, kTgs>(m, cfg, p, target, q, true, k > 0, so, nullptr, nullptr, sp);
+    substep<false, true, kTgs>(m, cfg, p, target, q, true, true, so, nullptr, nullptr, sp);
 #pragma unroll
     for (int f = 0; f < 2; ++f) {
       const float fn = sqrtf(dot3(so.feet_f[f], so.feet_f[f]));
@@ -3997,6 +4007,7 @@ __global__ __launch_bounds__(WGT, ZB_M_WAVES_PER_SIMD) void zb_m_step_kernel(
   }
   m = opaque(m);
   wave_sync();
+  const float wc_row = wc_extract(q);
   const PreM pr = pv;
   st = opaque_ptr(st);
 
@@ -4189,6 +4200,7 @@ __global__ __launch_bounds__(WGT, ZB_M_WAVES_PER_SIMD) void zb_m_step_kernel(
     if (standing > 0.5f) cmd[0] = cmd[1] = cmd[2] = 0.f;
   }
   log_flush(q, lmask, acc);
+  wc[(size_t)q.s * N + i] = reset ? wc_invalid(q.s) : wc_row;
   sp.mark(12);
 #if ZB_STAGED_STORES
 #define OUT(f) q.stg(f)
@@ -4511,7 +4523,7 @@ struct zb_sim {
   zb_model* d_model;
   float4* d_links;  // per-link collision table [NL][LINK4] (detect)
   float* d_state;
-  float* d_wc = nullptr;  // persistent self-contact cache (walking v2): ZB_WARM_ROWS x n
+  float* d_wc = nullptr;  // persistent self-contact cache: ZB_WARM_ROWS x n
   float* d_acc;
   float* d_log_means;
   int32_t* d_log_counts;
@@ -4716,7 +4728,7 @@ int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_dev
   }
   if (rc) return rc;
   HIPCHK(hipMemset(h->d_acc, 0, sizeof(float) * ACC_SLOTS * ACC_STRIDE), "hipMemset acc");
-  if (h->task == ZB_TASK_WALKING_V2) {
+  {
     HIPCHK(hipMalloc(&h->d_wc, sizeof(float) * ZB_WARM_ROWS * (size_t)num_envs), "hipMalloc contact cache");
     zb_wc_fill_kernel<<<(num_envs * ZB_WARM_ROWS + 255) / 256, 256>>>(num_envs, h->d_wc, nullptr, num_envs);
     rc = launch_check("zb_wc_fill_kernel");
@@ -4888,13 +4900,13 @@ int zb_step(zb_handle h, const float* actions, float* obs, float* reward, uint8_
 #define ZB_LAUNCH(K, ...) (tgs ? K<true><<<blocks, WGT, 0, s>>>(__VA_ARGS__) : K<false><<<blocks, WGT, 0, s>>>(__VA_ARGS__))
   if (h->task == ZB_TASK_STANDUP_V0)
     ZB_LAUNCH(zb_su_step_kernel, h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward, terminated,
-              truncated, h->d_acc, h->d_cnt, h->seed);
+              truncated, h->d_acc, h->d_cnt, h->seed, h->d_wc);
   else if (h->task == ZB_TASK_WALKING_V4)
     ZB_LAUNCH(zb_v4_step_kernel, h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward, terminated,
-              truncated, h->d_acc, h->d_cnt, h->seed);
+              truncated, h->d_acc, h->d_cnt, h->seed, h->d_wc);
   else if (h->task == ZB_TASK_MANAGER_V0)
     ZB_LAUNCH(zb_m_step_kernel, h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward, terminated,
-              truncated, h->d_acc, h->d_cnt, h->seed);
+              truncated, h->d_acc, h->d_cnt, h->seed, h->d_wc);
   else
     ZB_LAUNCH(zb_step_kernel, h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward, terminated,
               truncated, h->d_acc, h->d_wc);
@@ -4991,7 +5003,7 @@ int zb_set_state(zb_handle h, const float* src, void* stream) {
 }
 
 int zb_get_contact_cache(zb_handle h, float* dst, void* stream) {
-  if (!h || !dst || !h->d_wc) return set_err(-1, "zb_get_contact_cache (walking v2 handles)", hipSuccess);
+  if (!h || !dst || !h->d_wc) return set_err(-1, "zb_get_contact_cache", hipSuccess);
   HIPCHK(hipMemcpyAsync(dst, h->d_wc, sizeof(float) * ZB_WARM_ROWS * (size_t)h->n, hipMemcpyDeviceToDevice,
                         (hipStream_t)stream),
          "hipMemcpyAsync contact cache");
@@ -4999,7 +5011,7 @@ int zb_get_contact_cache(zb_handle h, float* dst, void* stream) {
 }
 
 int zb_set_contact_cache(zb_handle h, const float* src, void* stream) {
-  if (!h || !src || !h->d_wc) return set_err(-1, "zb_set_contact_cache (walking v2 handles)", hipSuccess);
+  if (!h || !src || !h->d_wc) return set_err(-1, "zb_set_contact_cache", hipSuccess);
   HIPCHK(hipMemcpyAsync(h->d_wc, src, sizeof(float) * ZB_WARM_ROWS * (size_t)h->n, hipMemcpyDeviceToDevice,
                         (hipStream_t)stream),
          "hipMemcpyAsync contact cache");

@@ -140,7 +140,7 @@ class ZbotSim:
         torch.cuda.current_stream(self.device).synchronize()  # `s` may be a temporary
 
     def get_contact_cache(self) -> torch.Tensor:
-        """walking v2: the solver's persistent self-contact cache [ZB_WARM_ROWS, N] (include/zbot.h)"""
+        """the solver's persistent self-contact cache [ZB_WARM_ROWS, N] (include/zbot.h)"""
         wc = torch.empty(16, self.num_envs, dtype=torch.float32, device=self.device)
         nat.check(self.lib.zb_get_contact_cache(self._h, nat.ptr(wc), _stream(self.device)), "zb_get_contact_cache")
         return wc
