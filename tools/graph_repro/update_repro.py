@@ -23,6 +23,10 @@ def mlp(seed):
                                torch.nn.Linear(128, 6)).cuda()
 
 
+def nothing():
+    pass
+
+
 def make_case(opt_kind, clip, between):
     net = mlp(0)
     x = torch.randn(4096, 23, device="cuda")
@@ -42,7 +46,7 @@ def make_case(opt_kind, clip, between):
             torch.nn.utils.clip_grad_norm_(params, 1.0)
         if opt is not None:
             opt.step()
-        else:
+        elif opt_kind == "sgd":
             with torch.no_grad():
                 for p in params:
                     p.add_(p.grad, alpha=-1e-3)
@@ -60,7 +64,10 @@ def make_case(opt_kind, clip, between):
                 for k, t in d.items():
                     opt.state[p][k].copy_(t)
 
-    flat = lambda: torch.cat([p.detach().flatten() for p in params]).clone()  # noqa: E731
+    if opt_kind == "none":  # compare the (clipped) gradients instead of the parameters
+        flat = lambda: torch.cat([p.grad.detach().flatten() for p in params]).clone()  # noqa: E731
+    else:
+        flat = lambda: torch.cat([p.detach().flatten() for p in params]).clone()  # noqa: E731
     return update, snap, restore, flat, x, between
 
 
@@ -123,6 +130,10 @@ def main():
     mode = os.environ.get("DEBUG_CLR_GRAPH_PACKET_CAPTURE")
     cases = [("sgd, torch between", "sgd", False, eager_torch), ("adam, torch between", "adam", False, eager_torch),
              ("adam+clip, torch between", "adam", True, eager_torch),
+             ("adam+clip, nothing between", "adam", True, nothing),
+             ("sgd+clip, torch between", "sgd", True, eager_torch),
+             ("clip only (gradients), torch between", "none", True, eager_torch),
+             ("clip only (gradients), nothing between", "none", True, nothing),
              ("sgd, zbot step between", "sgd", False, eager_zbot), ("adam+clip, zbot step between", "adam", True, eager_zbot)]
     res = {}
     for name, o, c, b in cases:
