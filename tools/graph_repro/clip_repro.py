@@ -1,5 +1,18 @@
-"""The packet-capture symptom narrowed to clip_grad_norm_ (tools/graph_repro/update_repro.py: the
-captured clip alone replays wrong from the second replay on, no eager work needed in between).
+"""The packet-capture symptom narrowed. Result (clip_repro_pc1.out / _pc0.out): with
+DEBUG_CLR_GRAPH_PACKET_CAPTURE=1, a captured GEMM of 1024x512 with K = 8192 followed by a reduction
+over its output (torch.sum or torch.linalg.vector_norm) replays wrong from the second replay on
+(relative errors 1e-4 .. 1e2), with no eager work between replays; the same GEMM followed by an
+elementwise op, smaller GEMMs followed by the same reductions, the reductions alone, foreach norms,
+clip_grad_norm_ on static tensors and a small backward + clip all replay correctly, and every case
+is correct with the variable at 0. The plain-HIP producer -> memset -> consumer graph replays
+correctly in both modes (memset_repro.hip). In the PPO update the weight-gradient GEMMs of a
+4096-sample minibatch feed clip_grad_norm_'s norm: update_repro.py ("clip only") fails the same way.
+So the symptom is inside the ROCm runtime / library stack (a captured library GEMM and a dependent
+reduction under packet capture), not a stale kernel argument of this code: zbot_lab_amd keeps
+packet capture off (its kernels are not involved: update_repro.py fails with no zbot launch).
+
+Each case captures one computation over static input tensors, refills the inputs with new values
+before every replay and compares the replay with the eager computation.
 Each case captures one piece of clip_grad_norm_ over static input tensors shaped like the PPO
 MLP's gradients, refills the inputs with new values before every replay and compares the replay
 with the eager computation. Run per capture mode (fresh processes):
@@ -87,7 +100,25 @@ def cases(g):
     def gemm_small_k():
         return torch.mm(big_b[:256].t(), big_a[:256]).flatten()
 
-    return [("GEMM 256x23, K=4096 (weight gradient)", gemm_tall_k), ("GEMM 128x256, K=4096", gemm_tall_k_256x128),
+    big_d = torch.randn(8192, 1024, device="cuda")
+    big_e = torch.randn(8192, 512, device="cuda")
+    EXTRA.extend([big_d, big_e])
+
+    def gemm_then_norm():  # a dependent reduction right after the weight-gradient GEMM
+        return torch.linalg.vector_norm(torch.mm(big_b.t(), big_a)).reshape(1)
+
+    def big_gemm_then_norm():  # a slower GEMM (1024x512, K = 8192), then its norm
+        return torch.linalg.vector_norm(torch.mm(big_d.t(), big_e)).reshape(1)
+
+    def big_gemm_then_sum():
+        return torch.mm(big_d.t(), big_e).sum().reshape(1)
+
+    def big_gemm_then_scale():  # elementwise consumer
+        return (torch.mm(big_d.t(), big_e) * 0.5).flatten()
+
+    return [("GEMM 256x23 K=4096 -> vector_norm", gemm_then_norm), ("GEMM 1024x512 K=8192 -> vector_norm", big_gemm_then_norm),
+            ("GEMM 1024x512 K=8192 -> sum", big_gemm_then_sum), ("GEMM 1024x512 K=8192 -> x0.5", big_gemm_then_scale),
+            ("GEMM 256x23, K=4096 (weight gradient)", gemm_tall_k), ("GEMM 128x256, K=4096", gemm_tall_k_256x128),
             ("GEMM 256x23, K=256", gemm_small_k),
             ("clip_grad_norm_ on static grads", clip_grad_norm_static), ("clip by hand, in place", inplace_clip),
             ("backward + _foreach_norm", backward_norm), ("backward + clip_grad_norm_", backward_clip),

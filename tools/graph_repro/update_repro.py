@@ -17,20 +17,23 @@ os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "1")
 import torch  # noqa: E402
 
 
-def mlp(seed):
+def mlp(seed, hidden=(256, 128)):
     torch.manual_seed(seed)
-    return torch.nn.Sequential(torch.nn.Linear(23, 256), torch.nn.ELU(), torch.nn.Linear(256, 128), torch.nn.ELU(),
-                               torch.nn.Linear(128, 6)).cuda()
+    layers, d = [], 23
+    for h in hidden:
+        layers += [torch.nn.Linear(d, h), torch.nn.ELU()]
+        d = h
+    return torch.nn.Sequential(*layers, torch.nn.Linear(d, 6)).cuda()
 
 
 def nothing():
     pass
 
 
-def make_case(opt_kind, clip, between):
-    net = mlp(0)
-    x = torch.randn(4096, 23, device="cuda")
-    y = torch.randn(4096, 6, device="cuda")
+def make_case(opt_kind, clip, between, batch=4096, hidden=(256, 128)):
+    net = mlp(0, hidden)
+    x = torch.randn(batch, 23, device="cuda")
+    y = torch.randn(batch, 6, device="cuda")
     lr = torch.tensor(1e-3, device="cuda")
     opt = torch.optim.Adam(net.parameters(), lr=lr, fused=True, capturable=True) if opt_kind == "adam" else None
     params = list(net.parameters())
@@ -64,7 +67,7 @@ def make_case(opt_kind, clip, between):
                 for k, t in d.items():
                     opt.state[p][k].copy_(t)
 
-    if opt_kind == "none":  # compare the (clipped) gradients instead of the parameters
+    if opt_kind in ("none", "grads"):  # compare the (clipped) gradients instead of the parameters
         flat = lambda: torch.cat([p.grad.detach().flatten() for p in params]).clone()  # noqa: E731
     else:
         flat = lambda: torch.cat([p.detach().flatten() for p in params]).clone()  # noqa: E731
@@ -95,8 +98,8 @@ def eager_zbot():
         _env.step(torch.randn(512, 6, device="cuda"))
 
 
-def run(name, opt_kind, clip, between):
-    update, snap, restore, flat, x, between_fn = make_case(opt_kind, clip, between)
+def run(name, opt_kind, clip, between, batch=4096, hidden=(256, 128)):
+    update, snap, restore, flat, x, between_fn = make_case(opt_kind, clip, between, batch, hidden)
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
@@ -135,9 +138,16 @@ def main():
              ("clip only (gradients), torch between", "none", True, eager_torch),
              ("clip only (gradients), nothing between", "none", True, nothing),
              ("sgd, zbot step between", "sgd", False, eager_zbot), ("adam+clip, zbot step between", "adam", True, eager_zbot)]
+    cases += [("backward only (gradients), nothing between", "grads", False, nothing),
+              ("backward only, batch 256", "grads", False, nothing, 256),
+              ("backward only, hidden 64", "grads", False, nothing, 4096, (64,)),
+              ("backward only, hidden 256x128, batch 1024", "grads", False, nothing, 1024),
+              ("clip only, batch 256", "none", True, nothing, 256)]
+    if os.environ.get("ONLY_NEW"):
+        cases = cases[-5:]
     res = {}
-    for name, o, c, b in cases:
-        res[name] = run(name, o, c, b)
+    for name, o, c, b, *extra in cases:
+        res[name] = run(name, o, c, b, *extra)
     print(f"DEBUG_CLR_GRAPH_PACKET_CAPTURE={mode}: " + "; ".join(f"{k}: {'correct' if v else 'WRONG'}" for k, v in res.items()))
     return 0
 

@@ -8,9 +8,10 @@ import sys as _sys
 
 # HIP graphs: ROCm's "packet capture" graph mode (the CLR default) makes the captured PPO update
 # replay with wrong results from its second replay on (tests/test_ppo.py
-# ::test_gpu_update_graph_matches_eager fails with DEBUG_CLR_GRAPH_PACKET_CAPTURE=1; minimal HIP and
-# torch graphs of single kernels, fused Adam included, replay correctly in both modes:
-# tools/graph_repro/). The runtime reads the switch once, when HIP initialises --
+# ::test_gpu_update_graph_matches_eager fails with DEBUG_CLR_GRAPH_PACKET_CAPTURE=1). Narrowed in
+# tools/graph_repro/clip_repro.py: a captured large GEMM (1024x512, K = 8192) followed by a
+# reduction over its output replays wrong under packet capture -- no kernel of this package is
+# involved. The runtime reads the switch once, when HIP initialises --
 # which any HIP call does, torch.cuda.is_available() / device_count() included, even while
 # torch.cuda.is_initialized() is still False. GRAPHS_SAFE is therefore True only when the switch
 # is certain to have been read as "0": it was in the process environment at launch
