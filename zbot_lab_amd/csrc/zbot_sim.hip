@@ -1026,8 +1026,7 @@ __device__ __forceinline__ void quad_support(const QCircle& h, const float v[3],
 #pragma unroll
   for (int k = 0; k < 3; ++k) pt[k] = h.c[k] + (a * h.e1[k] + b * h.e2[k]) * ri;
   const float val = dot3(d, pt), pv = dppf<DPP_XOR1>(val);
-  // circle 0 unless circle 1 is strictly larger (values are finite: >= is !<)
-  const bool mine = val > pv || ((j & 1) == 0 && val == pv);
+  const bool mine = (j & 1) ? (val > pv) : !(pv > val);  // circle 0 unless circle 1 is strictly larger
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     // (the DPP read as a statement of its own: inside `?:` it would be evaluated only for the
@@ -1044,7 +1043,7 @@ template <int CTRL>
 __device__ __forceinline__ void quad_pick(bool partner_first, float& best, float bv[3], float& l1, float& l2,
                                           unsigned& bm) {
   const float ob = dppf<CTRL>(best);
-  const bool take = ob < best || (partner_first && ob == best);  // (finite values)
+  const bool take = partner_first ? !(ob > best) : (ob < best);
   best = take ? ob : best;
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
