@@ -222,11 +222,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # ZB_BENCH_SHARE_GPU=1: rehearsal of the N-rank path on a one-GPU box (every rank on cuda:0, gloo
+    # for the barrier / timing reduction; RCCL cannot put two ranks on one device). Never set by the
+    # SCALE runs, whose ranks each own a GPU.
+    share = world > 1 and os.environ.get("ZB_BENCH_SHARE_GPU") == "1"
+    if share:
+        local_rank = 0
     dist = None
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if share:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
 
@@ -270,8 +279,9 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms, kern_n = env.sim.profile_end()
 
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    per_rank = torch.tensor([n * args.steps / elapsed], dtype=torch.float64, device=dev)
+    rdev = "cpu" if share else dev  # (gloo reduces host tensors)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=rdev)
+    per_rank = torch.tensor([n * args.steps / elapsed], dtype=torch.float64, device=rdev)
     rccl_world = 1
     if dist is not None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -314,7 +324,8 @@ def main():
             "config": {"workload": workload,
                        "envs_per_gpu": n, "total_envs": n * world, "decimation": 4, "sim_dt": 0.005,
                        "parallelism": f"env-sharded x{world} (replicas, no collective)",
-                       "rccl_world_size": rccl_world, "per_rank_env_steps_per_s": per_rank_rates},
+                       "rccl_world_size": rccl_world, "per_rank_env_steps_per_s": per_rank_rates,
+                       **({"rehearsal": "all ranks on cuda:0, gloo collectives"} if share else {})},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": kname, "kernel_ms": kern_s * 1e3,
