@@ -73,6 +73,33 @@ def test_full_state_headline_sizes(gpu, n):
     assert nbad <= 0.02 * len(ids)
 
 
+@pytest.mark.parametrize("task", ["v2", "v4", "manager"])
+def test_full_state_4096_every_solver(gpu, task):
+    """configs[1]'s size for the other walking tasks and for the TGS-style solve: one step of 4096
+    envs from random full states against the oracle run on ALL 4096 columns under the full-state
+    rule (PGS for v4 / manager, TGS-style for v2). Not a column sample: v4's and the manager's
+    command resampling draws from a counter-based generator keyed on the env index, so a column
+    subset is not the same sub-problem there."""
+    import torch
+    import test_gpu_fullstate as F
+    from fullstate import random_states, solver_mode, task_cfg
+    from oracle.pyoracle import OracleSim
+    from zbot_lab_amd.sim import ZbotSim
+    n, seed = 4096, 37
+    with solver_mode(1 if task == "v2" else 0):
+        cfg = task_cfg(task)
+        st = random_states(task, OracleSim(n, cfg, seed=seed), n, seed=500)
+        a = np.random.default_rng(n + 1).normal(size=(n, 6)).astype(np.float32)
+        g = ZbotSim(n, cfg, device="cuda:0", seed=seed)
+        g.set_state(torch.from_numpy(st).cuda())
+        g_out = _step(g, a)
+        sg = g.get_state().cpu().numpy()
+        g.close()
+        nbad = F._check(task, f"one step of {n} envs ({'TGS' if task == 'v2' else 'PGS'})", n, seed, st, [a], g_out,
+                        sg, torch)
+    assert nbad <= 0.02 * n
+
+
 def test_permutation_equivariance_65536(gpu):
     import torch
     n = 65536
