@@ -1624,7 +1624,9 @@ __device__ __forceinline__ void sens_store(const Q& q, float* __restrict__ st, i
 #define ZB_CARRY 1
 #endif
 __device__ __forceinline__ float& Q::stg(int k) const { return reinterpret_cast<float*>(b + YG_OFF)[e * STG_LEN + k]; }
-template <int SD, int OD>
+// WT >= 0: state row WT is stored with agent scope (the walking kernel's episode length, which a
+// fused finalize may overwrite with the full-reset draw from another XCD, finalize_body)
+template <int SD, int OD, int WT = -1>
 __device__ __forceinline__ void staged_store(const Q& q, int env0, int N, float* __restrict__ st,
                                              float* __restrict__ obs, float* __restrict__ rew,
                                              uint8_t* __restrict__ term, uint8_t* __restrict__ trunc) {
@@ -1637,7 +1639,9 @@ __device__ __forceinline__ void staged_store(const Q& q, int env0, int N, float*
 #ifndef ZB_DIAG_NO_STATE_STORE  // diagnostic only (scripts/gpu_r1o.sh): measures the state stores' cost
 #pragma unroll
     for (int f = f0; f < SD; f += WGT / EPW) {
-      st[(size_t)f * N + env] = S[e * STG_LEN + f];
+      const float v = S[e * STG_LEN + f];
+      if (WT >= 0 && f == WT) __hip_atomic_store(&st[(size_t)f * N + env], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else st[(size_t)f * N + env] = v;
     }
 #endif
     if (f0 == 0) rew[env] = S[e * STG_LEN + SD + OD];
@@ -2551,6 +2555,27 @@ __device__ __forceinline__ void log_flush(const Q& q, uint64_t mask, float* acc)
 }
 
 // ------------------------------------------------------------------------- kernels
+// Step-end finalisation arguments (zb_finalize_kernel, or fused into the walking step kernel: its
+// last workgroup runs the same body, FinArgs::done counting the finished workgroups).
+constexpr int FIN_FG = 8;  // finalize fold: accumulator slot groups
+struct FinArgs {
+  float* log_means;
+  int32_t* log_counts;
+  float* user_means;
+  int32_t* user_counts;
+  float episode_s;
+  uint64_t seed;
+  Counters* cnt;
+  int ep_len_row;
+  unsigned* done;  // nullptr: not fused
+};
+template <bool kFused>
+__device__ __forceinline__ void finalize_body(int N, float* __restrict__ st, float* __restrict__ acc,
+                                              const FinArgs& fa, int force_full, int reset_counts, int is_step,
+                                              const zb_task_cfg& cfg, float* __restrict__ obs,
+                                              const uint8_t* __restrict__ term, const uint8_t* __restrict__ trunc,
+                                              float* sh);
+
 __device__ __forceinline__ void load_phys(const float* __restrict__ st, int N, int i, Phys& p) {
 #define LD(f) st[(size_t)(f) * N + i]
 #pragma unroll
@@ -2571,9 +2596,11 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_step_kernel(const z
                                                           float* __restrict__ st, const float* __restrict__ act,
                                                           float* __restrict__ obs, float* __restrict__ rew,
                                                           uint8_t* __restrict__ term, uint8_t* __restrict__ trunc,
-                                                          float* __restrict__ acc, float* __restrict__ wc) {
+                                                          float* __restrict__ acc, float* __restrict__ wc,
+                                                          FinArgs fa) {
   MP m = to_mp(mg);
   __shared__ float4 lds[LDS4];
+  static_assert(LDS4 * 4 >= FIN_FG * ACC_STRIDE + ACC, "fused finalize scratch");
   const int lane = threadIdx.x;
   const int env = xcd_block(blockIdx.x, gridDim.x) * EPW + lane / TL;
   // a team past N recomputes env N-1 (identical values, identical stores); it never logs
@@ -2872,11 +2899,24 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_step_kernel(const z
 #endif
   }
 #if ZB_STAGED_STORES
-  staged_store<ZB_STATE_DIM, ZB_OBS_DIM>(q, xcd_block(blockIdx.x, gridDim.x) * EPW, N, st, obs, rew, term, trunc);
+  staged_store<ZB_STATE_DIM, ZB_OBS_DIM, ZB_S_EP_LEN>(q, xcd_block(blockIdx.x, gridDim.x) * EPW, N, st, obs, rew, term,
+                                                     trunc);
 #endif
 #undef OUT
   sp.mark(8);
   sp.flush();
+  // Fused finalize (FinArgs::done set): one agent-scope add per workgroup after its stores and log
+  // atomics have completed; the workgroup whose add comes last runs zb_finalize_kernel's body. The
+  // log accumulator is only touched by atomics and the episode-length row by agent-scope stores,
+  // so no release fence (an L2 write-back per workgroup) is needed.
+  if (fa.done) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned prev = 0u;
+    if (lane == 0) prev = __hip_atomic_fetch_add(fa.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    prev = __builtin_amdgcn_readfirstlane(prev);
+    if (prev == gridDim.x - 1)
+      finalize_body<true>(N, st, acc, fa, 0, 0, 1, cfg, nullptr, term, trunc, reinterpret_cast<float*>(lds));
+  }
 #undef ST
 #undef CST
 }
@@ -4384,38 +4424,52 @@ __global__ void zb_m_observe_kernel(const zb_model* __restrict__ mg, zb_task_cfg
 // next step (the reference applies the reset-event ones to the commands it resamples in the same
 // call). The manager's lin_vel_cmd_levels is exact: the reset envs' commands are
 // redrawn here when it fires.
-__global__ void zb_finalize_kernel(int N, float* __restrict__ st, float* __restrict__ acc,
-                                   float* __restrict__ log_means, int32_t* __restrict__ log_counts,
-                                   float* __restrict__ user_means, int32_t* __restrict__ user_counts, float episode_s,
-                                   uint64_t seed, Counters* __restrict__ cnt, int force_full, int reset_counts,
-                                   int is_step, int ep_len_row, zb_task_cfg cfg, float* __restrict__ obs,
-                                   const uint8_t* __restrict__ term, const uint8_t* __restrict__ trunc) {
+template <bool kFused>
+__device__ __forceinline__ void finalize_body(int N, float* __restrict__ st, float* __restrict__ acc,
+                                              const FinArgs& fa, int force_full, int reset_counts, int is_step,
+                                              const zb_task_cfg& cfg, float* __restrict__ obs,
+                                              const uint8_t* __restrict__ term, const uint8_t* __restrict__ trunc,
+                                              float* sh) {
+  float* const log_means = fa.log_means;
+  int32_t* const log_counts = fa.log_counts;
+  float* const user_means = fa.user_means;
+  int32_t* const user_counts = fa.user_counts;
+  const float episode_s = fa.episode_s;
+  const uint64_t seed = fa.seed;
+  Counters* const cnt = fa.cnt;
+  const int ep_len_row = fa.ep_len_row;
   const uint64_t ctr = cnt->calls;
   const uint64_t steps = cnt->steps + (is_step ? 1 : 0);
   // fold the accumulator slots (acc_slot): 8 groups of 8 slots x ACC_STRIDE entries, one
-  // thread per (group, entry), which also clears what it read; then a shared sum of the groups
-  constexpr int FG = 8, FS = ACC_SLOTS / FG;
-  static_assert(FG * ACC_STRIDE <= 256 && ACC_SLOTS % FG == 0, "finalize fold layout");
-  __shared__ float acc_part[FG][ACC_STRIDE];
-  __shared__ float acc_sum[ACC];
-  if (threadIdx.x < FG * ACC_STRIDE) {
-    const int g = threadIdx.x / ACC_STRIDE, t = threadIdx.x % ACC_STRIDE;
+  // thread per (group, entry), which also clears what it read; then a shared sum of the groups.
+  // Fused (the step kernel's last workgroup): the slots were filled by agent-scope atomics of the
+  // other workgroups, so they are read and cleared by atomic exchanges (coherent across XCDs).
+  constexpr int FG = FIN_FG, FS = ACC_SLOTS / FG;
+  float* const acc_part = sh;                     // [FG][ACC_STRIDE]
+  float* const acc_sum = sh + FG * ACC_STRIDE;    // [ACC]
+  for (int x = threadIdx.x; x < FG * ACC_STRIDE; x += blockDim.x) {
+    const int g = x / ACC_STRIDE, t = x % ACC_STRIDE;
     float v[FS];
+    if (kFused) {
 #pragma unroll
-    for (int k = 0; k < FS; ++k) v[k] = acc[(g * FS + k) * ACC_STRIDE + t];
+      for (int k = 0; k < FS; ++k) v[k] = atomicExch(&acc[(g * FS + k) * ACC_STRIDE + t], 0.f);
+    } else {
 #pragma unroll
-    for (int k = 0; k < FS; ++k) acc[(g * FS + k) * ACC_STRIDE + t] = 0.f;
+      for (int k = 0; k < FS; ++k) v[k] = acc[(g * FS + k) * ACC_STRIDE + t];
+#pragma unroll
+      for (int k = 0; k < FS; ++k) acc[(g * FS + k) * ACC_STRIDE + t] = 0.f;
+    }
     float sum = 0.f;
 #pragma unroll
     for (int k = 0; k < FS; ++k) sum += v[k];
-    acc_part[g][t] = sum;
+    acc_part[g * ACC_STRIDE + t] = sum;
   }
   __syncthreads();
-  if (threadIdx.x < ACC) {
+  for (int x = threadIdx.x; x < ACC; x += blockDim.x) {
     float v = 0.f;
 #pragma unroll
-    for (int g = 0; g < FG; ++g) v += acc_part[g][threadIdx.x];
-    acc_sum[threadIdx.x] = v;
+    for (int g = 0; g < FG; ++g) v += acc_part[g * ACC_STRIDE + x];
+    acc_sum[x] = v;
   }
   __syncthreads();
   const float nres = acc_sum[ACC_NRES];
@@ -4505,13 +4559,33 @@ __global__ void zb_finalize_kernel(int N, float* __restrict__ st, float* __restr
   if (full && cfg.task != ZB_TASK_MANAGER_V0)  // ManagerBasedRLEnv has no full-reset draw
     for (int i = threadIdx.x; i < N; i += blockDim.x) {
       const uint64_t h = hash64(seed ^ hash64(ctr * 0x100000001B3ull + (uint64_t)i));
-      st[(size_t)ep_len_row * N + i] = (float)(int)(h % (uint64_t)cfg.max_episode_length);
+      const float d = (float)(int)(h % (uint64_t)cfg.max_episode_length);
+      // (fused: an agent-scope store, like the step's own store of this row, so that no XCD's L2
+      // holds a dirty copy of it that could be written back over the draw)
+      if (kFused) __hip_atomic_store(&st[(size_t)ep_len_row * N + i], d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else st[(size_t)ep_len_row * N + i] = d;
     }
+  if (kFused && threadIdx.x == 0) __hip_atomic_store(fa.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+
+__global__ void zb_finalize_kernel(int N, float* __restrict__ st, float* __restrict__ acc,
+                                   float* __restrict__ log_means, int32_t* __restrict__ log_counts,
+                                   float* __restrict__ user_means, int32_t* __restrict__ user_counts, float episode_s,
+                                   uint64_t seed, Counters* __restrict__ cnt, int force_full, int reset_counts,
+                                   int is_step, int ep_len_row, zb_task_cfg cfg, float* __restrict__ obs,
+                                   const uint8_t* __restrict__ term, const uint8_t* __restrict__ trunc) {
+  __shared__ float sh[FIN_FG * ACC_STRIDE + ACC];
+  const FinArgs fa = {log_means, log_counts, user_means, user_counts, episode_s, seed, cnt, ep_len_row, nullptr};
+  finalize_body<false>(N, st, acc, fa, force_full, reset_counts, is_step, cfg, obs, term, trunc, sh);
+}
+
 
 }  // namespace
 
 // =========================================================================== C ABI
+#ifndef ZB_FUSED_FINALIZE_DEFAULT
+#define ZB_FUSED_FINALIZE_DEFAULT 0
+#endif
 struct zb_sim {
   int device;
   int n;
@@ -4532,6 +4606,10 @@ struct zb_sim {
   // optional per-launch timing of zb_step_kernel (hipEvents on the launch stream)
   int prof_max = 0, prof_n = 0;
   hipEvent_t* prof_ev = nullptr;
+  // walking v2: the step-end finalisation runs in the step kernel's last workgroup (FinArgs::done;
+  // ZB_FUSED_FINALIZE=0/1 at create overrides ZB_FUSED_FINALIZE_DEFAULT)
+  unsigned* d_done = nullptr;
+  bool fused = false;
 };
 
 static thread_local char g_err[512] = "";
@@ -4602,6 +4680,14 @@ int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_dev
   HIPCHK(hipMalloc(&h->d_state, sizeof(float) * (size_t)h->state_dim * num_envs), "hipMalloc state");
   HIPCHK(hipMalloc(&h->d_acc, sizeof(float) * ACC_SLOTS * ACC_STRIDE), "hipMalloc acc");
   HIPCHK(hipMalloc(&h->d_cnt, sizeof(Counters)), "hipMalloc counters");
+  {
+    const char* fz = getenv("ZB_FUSED_FINALIZE");
+    if (c->task == ZB_TASK_WALKING_V2 && ZB_STAGED_STORES && (fz ? fz[0] != '0' : ZB_FUSED_FINALIZE_DEFAULT)) {
+      HIPCHK(hipMalloc(&h->d_done, sizeof(unsigned)), "hipMalloc done counter");
+      HIPCHK(hipMemset(h->d_done, 0, sizeof(unsigned)), "hipMemset done counter");
+      h->fused = true;
+    }
+  }
   {
     Counters c0;
     memset(&c0, 0, sizeof(c0));
@@ -4836,6 +4922,7 @@ void zb_destroy(zb_handle h) {
   (void)hipFree(h->d_wc);
   (void)hipFree(h->d_acc);
   (void)hipFree(h->d_cnt);
+  if (h->d_done) (void)hipFree(h->d_done);
   (void)hipFree(h->d_log_means);
   (void)hipFree(h->d_log_counts);
   delete h;
@@ -4907,9 +4994,12 @@ int zb_step(zb_handle h, const float* actions, float* obs, float* reward, uint8_
   else if (h->task == ZB_TASK_MANAGER_V0)
     ZB_LAUNCH(zb_m_step_kernel, h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward, terminated,
               truncated, h->d_acc, h->d_cnt, h->seed, h->d_wc);
-  else
+  else {
+    const FinArgs fa = {h->d_log_means, h->d_log_counts, h->u_log_means, h->u_log_counts, log_episode_s(h),
+                        h->seed, h->d_cnt, ZB_S_EP_LEN, h->fused ? h->d_done : nullptr};
     ZB_LAUNCH(zb_step_kernel, h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward, terminated,
-              truncated, h->d_acc, h->d_wc);
+              truncated, h->d_acc, h->d_wc, fa);
+  }
 #undef ZB_LAUNCH
   int rc = launch_check("zb_step_kernel");
   if (prof) {
@@ -4917,6 +5007,7 @@ int zb_step(zb_handle h, const float* actions, float* obs, float* reward, uint8_
     ++h->prof_n;
   }
   if (rc) return rc;
+  if (h->task == ZB_TASK_WALKING_V2 && h->fused) return 0;  // finalised by the step kernel
   return finalize(h, s, 0, 0, 1, obs, terminated, truncated);
 }
 
