@@ -52,6 +52,8 @@ def _load(double: bool = False):
     lib.zbo_gjk_pairs.argtypes = [_f, C.c_void_p, C.c_int, C.c_float, _f, C.c_void_p]
     lib.zbo_set_gjk_tol.argtypes = [C.c_double]
     lib.zbo_set_sensor_force_scale.argtypes = [C.c_double]
+    lib.zbo_set_plant.argtypes = [C.c_int]
+    lib.zbo_contact_activity.argtypes = [P, _i, C.c_int]
     lib.zbo_self_min_sep.argtypes = [P, _f]
     lib.zbo_link_com_vel.argtypes = [P, _f]
     lib.zbo_energy_momentum.argtypes = [P, _f]
@@ -186,6 +188,13 @@ class OracleSim:
         self.lib.zbo_contact_diag(self.h, d)
         return d
 
+    def contact_activity(self, clear: bool = True):
+        """[n, 2]: loaded ground / self contacts (lambda_n > 0 after the solve) summed over the
+        substeps of the steps since the last clear (test hook)."""
+        out = np.zeros((self.n, 2), np.int32)
+        self.lib.zbo_contact_activity(self.h, out, int(clear))
+        return out
+
     def self_min_sep(self):
         """[n]: the smallest self-collision separation of the current state (-2 CORE_M: overlapping
         cores, deeper than the shape model)."""
@@ -202,6 +211,21 @@ class OracleSim:
         o = np.zeros((self.n, 7), np.float32)
         self.lib.zbo_energy_momentum(self.h, o)
         return o
+
+
+class planted_bug:
+    """Context manager: the oracle library (f32 or f64) runs with a planted contact bug
+    (zbo_set_plant: 1 ground mu x 1.1 on one contact, 2 one self normal flipped, 3 no push-out cap)."""
+
+    def __init__(self, mode: int, double: bool = True):
+        self.mode, self.double = mode, double
+
+    def __enter__(self):
+        lib(self.double).zbo_set_plant(self.mode)
+        return self
+
+    def __exit__(self, *exc):
+        lib(self.double).zbo_set_plant(0)
 
 
 def su_mdp_eval(cfg: zm.TaskCfg, stage: int, link_state, p_delta, ep_len, center_z_last, ep_sums):

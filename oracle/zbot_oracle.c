@@ -216,6 +216,7 @@ struct zbo_sim {
   int changed;                  /* manager: lin_vel_cmd_levels widened the ranges in this call */
   double met_acc[2];            /* manager: summed command metrics of this call's reset envs */
   int nclose;                   /* manager: feet_close terminations of this call */
+  int32_t* act;                 /* [n][2] loaded ground / self contacts summed over substeps (test hook) */
 };
 typedef struct zbo_sim zbo_sim;
 
@@ -405,6 +406,14 @@ typedef struct { real c[2][9]; } hull_t;
 static double g_gjk_tol = GJK_TOL;
 static _Thread_local int g_gjk_last_it; /* probe: support iterations of this thread's last hull_pair */
 static double g_sensor_force_scale = 1.0; /* test hook: scales the contact forces the sensors see */
+/* planted contact bug (test hook, 0 = off; tests/test_fullstate_machinery.py proves that the
+ * full-state parity rule flags a device carrying one): 1 = the first ground contact of every
+ * substep with mu x 1.1, 2 = the first self contact's normal flipped, 3 = the penetration push-out
+ * without the max_depenetration_velocity cap */
+static int g_plant = 0;
+/* per-env contact activity (test hook): the env's [loaded ground, loaded self] counters, set by the
+ * step loops around each env's step */
+static _Thread_local int32_t* t_act = NULL;
 static int g_gjk_warm = 1;               /* warm start within a step (test hook: 0 = always cold) */
 static int g_gjk_probe = 0;              /* probe: histogram of the GJK calls the kernel would make */
 static long long g_gjk_hist[GJK_MAX_IT + 2];
@@ -638,6 +647,11 @@ static int hull_pair(const hull_t* A, const hull_t* B, real margin, real early_m
  * is told from a real mismatch; the physics is unaffected */
 int zbo_set_sensor_force_scale(double s) {
   g_sensor_force_scale = s > 0 ? s : 1.0;
+  return 0;
+}
+
+int zbo_set_plant(int mode) {
+  g_plant = mode;
   return 0;
 }
 
@@ -905,6 +919,7 @@ typedef struct {
 static real contact_bias(const zb_task_cfg* cfg, const mdl_t* m, real sep, real h, real dt) {
   if (sep >= 0) return -sep / h;
   real push = cfg->baumgarte * (-sep) / dt;
+  if (g_plant == 3) return push; /* planted bug: no cap */
   return push < m->max_depen ? push : m->max_depen;
 }
 static void clamp_speeds(const mdl_t* m, real u[NV]) {
@@ -1050,8 +1065,13 @@ static void substep(const mdl_t* m, const zb_task_cfg* cfg, phys_t* s, const rea
   for (int a = 0; a < NV; ++a) wsum[a] = 0;
   int broken[NC_MAX];
   real dirs[NC_MAX][3][3];
+  int planted = 0;
   for (int c = 0; c < nc; ++c) {
-    const contact_t* ct = &CL.c[c];
+    contact_t* ct = &CL.c[c];
+    if (g_plant == 2 && !planted && ct->lb >= 0) {
+      for (int a = 0; a < 3; ++a) ct->n[a] = -ct->n[a];
+      planted = 1;
+    }
     for (int a = 0; a < 3; ++a) dirs[c][0][a] = ct->n[a];
     tangents(ct->n, dirs[c][1], dirs[c][2]);
     /* friction combine mode "multiply" (link x ground, link x link) */
@@ -1059,6 +1079,7 @@ static void substep(const mdl_t* m, const zb_task_cfg* cfg, phys_t* s, const rea
                        : (real)cfg->friction_dynamic;
     muc[c] = mu_link ? mu_link[ct->la] * (ct->lb >= 0 ? mu_link[ct->lb] : (real)cfg->friction) : (real)cfg->friction;
     if (muc[c] < mud[c]) muc[c] = mud[c]; /* static raised to dynamic (PhysX material combine) */
+    if (g_plant == 1 && !planted && ct->lb < 0) { muc[c] *= (real)1.1; mud[c] *= (real)1.1; planted = 1; }
     for (int r = 0; r < 3; ++r) {
       real J[NV], Jb[NV];
       jac_row(&k, m->link_body[ct->la], ct->x, dirs[c][r], J);
@@ -1119,6 +1140,9 @@ static void substep(const mdl_t* m, const zb_task_cfg* cfg, phys_t* s, const rea
     }
     for (int a = 0; a < NV; ++a) wsum[a] += w[a];
   }
+  if (t_act)
+    for (int c = 0; c < nc; ++c)
+      if (lam[c][0] > 0) ++t_act[CL.c[c].lb >= 0];
   real un[NV], ua[NV]; /* the new velocity; the pose integrates ua (TGS: the sub-iterations' mean) */
   bwd_sub(L, w, un);
   if (tgs) {
@@ -2456,6 +2480,7 @@ zbo_sim* zbo_create(const zb_model* model, const zb_task_cfg* cfg, int num_envs,
   s->yaw[0] = cfg->cmd_yaw_range[0]; s->yaw[1] = cfg->cmd_yaw_range[1];
   s->prob_pos = cfg->stage_prob_pos[0];
   s->env = (env_t*)calloc((size_t)num_envs, sizeof(env_t));
+  s->act = (int32_t*)calloc((size_t)num_envs * 2, sizeof(int32_t));
   for (int i = 0; i < num_envs; ++i) {
     memset(&s->env[i], 0, sizeof(env_t));
     wc_invalidate(s->env[i].wc);
@@ -2479,6 +2504,7 @@ zbo_sim* zbo_create(const zb_model* model, const zb_task_cfg* cfg, int num_envs,
 void zbo_destroy(zbo_sim* s) {
   if (!s) return;
   free(s->env);
+  free(s->act);
   free(s);
 }
 
@@ -2628,10 +2654,12 @@ int zbo_step(zbo_sim* s, const float* actions, float* obs, float* reward, uint8_
       const float* a = actions + (size_t)e * ZB_ACT_DIM;
       float* o = obs + (size_t)e * od;
       real r;
+      t_act = s->act + 2 * (size_t)e;
       if (task == ZB_TASK_STANDUP_V0) r = su_step_env(&s->m, &s->c, stage, s->seed, ctr, e, &s->env[e], a, o, &died, &tout, acc_l);
       else if (task == ZB_TASK_WALKING_V4) r = v4_step_env(s, stage, ctr, e, &s->env[e], a, o, &died, &tout, acc_l);
       else if (task == ZB_TASK_MANAGER_V0) r = m_step_env(s, ctr, e, &s->env[e], a, o, &died, &close, &tout, acc_l, met_l);
       else r = step_env(&s->m, &s->c, &s->env[e], a, o, &died, &tout, acc_l);
+      t_act = NULL;
       reward[e] = (float)r;
       /* manager: terminated = base_height | feet_close; the log counts each term */
       terminated[e] = (uint8_t)(died || close);
@@ -2654,6 +2682,14 @@ int zbo_step(zbo_sim* s, const float* actions, float* obs, float* reward, uint8_
   if (task == ZB_TASK_MANAGER_V0 && s->changed)
     for (int e = 0; e < s->n; ++e)
       if (terminated[e] || truncated[e]) m_fixup_env(s, ctr, e, &s->env[e], obs + (size_t)e * od);
+  return 0;
+}
+
+/* test hook: per env [loaded ground contacts, loaded self contacts] (lambda_n > 0 after the
+ * solve) summed over the substeps of the zbo_step calls since the last clear */
+int zbo_contact_activity(zbo_sim* s, int32_t* out, int clear) {
+  memcpy(out, s->act, (size_t)s->n * 2 * sizeof(int32_t));
+  if (clear) memset(s->act, 0, (size_t)s->n * 2 * sizeof(int32_t));
   return 0;
 }
 

@@ -1,7 +1,9 @@
 """CPU check of the full-state parity machinery (tests/fullstate.py) that test_gpu_fullstate.py runs
 against the HIP kernels: with the f64 oracle standing in for the device, every env agrees or is an
-explained discontinuity; and a planted error of the size a wrong weight / latch / integrator would
-cause is reported as unexplained."""
+explained discontinuity; a planted error of the size a wrong weight / latch / integrator would
+cause is reported as unexplained; and a device carrying a planted contact-path bug (one ground
+contact's friction x 1.1, one self contact's normal flipped, the push-out cap removed) is caught in
+the contact-active envs where the bug acts, however sensitive those envs are."""
 from __future__ import annotations
 
 import re
@@ -45,7 +47,8 @@ def test_planted_errors_are_unexplained(oracle_lib, task):
     # reset in the step, so every planted error must be reported as unexplained
     so, outs = T._run_oracle(task, n, seed, st, [a])
     ob_o, rw_o, te_o, tr_o = outs[-1]
-    sens = T._sensitivity(task, n, seed, st, [a], so, ob_o, rw_o, (te_o, tr_o), st, 1)
+    fam = T._sensitivity(task, n, seed, st, [a], so, ob_o, rw_o, (te_o, tr_o), st, 1)
+    sens = np.max(np.stack(list(fam.values())), axis=0)
     calm = [int(e) for e in np.nonzero((sens < 0.3) & ~(te_o | tr_o))[0]]
     envs = [calm[k] for k in (1, 10, 20, 30)]
     sg[g["sums"][0], envs[0]] += 2e-2            # a per-term episode sum off by a weight-sized error
@@ -58,3 +61,43 @@ def test_planted_errors_are_unexplained(oracle_lib, task):
     listed = {int(v) for v in re.findall(r"\d+", str(ei.value).split(":")[-1].split("\n")[0])}
     for e in envs if g["kin"] else envs[:2] + envs[3:]:
         assert e in listed, (e, listed)
+
+
+def _plant_states(task, kind, n, seed):
+    """States where the planted bug acts: random full states (ground contacts, sliding feet) for the
+    friction bug; folded states (links in contact) for the flipped self normal; random states sunk
+    2-5 cm into the ground (push-out 0.2 x depth / dt = 0.8-2 m/s, above the 1 m/s cap) for the
+    push-out cap."""
+    from oracle.pyoracle import OracleSim
+    o = OracleSim(n, task_cfg(task), seed=seed)
+    st = random_states(task, o, n, seed=seed + 1)
+    rng = np.random.default_rng(seed + 2)
+    if kind == 2:  # (the lying stand-up start loads fewer of its folds' pairs: wider folds)
+        st[13:19] += rng.normal(0, 3.0 if task == "standup" else 1.5, (6, n)).astype(np.float32)
+    if kind == 3:
+        st[2] -= rng.uniform(0.02, 0.05, n).astype(np.float32)
+    return st
+
+
+@pytest.mark.parametrize("task", TASKS)
+@pytest.mark.parametrize("kind", [1, 2, 3], ids=["ground_mu_x1.1", "self_normal_flipped", "no_pushout_cap"])
+def test_planted_contact_bugs_are_caught(oracle_lib, task, kind):
+    """The device is the f64 oracle with a planted contact-path bug (oracle zbo_set_plant); the
+    checker is the unmodified f32 oracle with its perturbation envelope. The full-state rule must
+    fail with unexplained envs, and every unexplained env must be one where the bug can act (a
+    loaded contact of the planted kind in the device or the checker run: a flipped normal can
+    unload a contact the checker loads): the rule flags contact-path bugs in
+    contact-active, sensitive envs, not only calm ones."""
+    from oracle.pyoracle import planted_bug
+    n, seed = 256, 41
+    st = _plant_states(task, kind, n, seed)
+    a = np.random.default_rng(seed + 3).normal(size=(n, 6)).astype(np.float32)
+    with planted_bug(kind, double=True):
+        sg, outs, act = T._run_oracle(task, n, seed, st, [a], double=True, activity=True)
+    act = act + T._run_oracle(task, n, seed, st, [a], activity=True)[2]   # either side's contacts
+    where = act[:, 1] > 0 if kind == 2 else act[:, 0] > 0
+    assert where.sum() >= 20, where.sum()
+    with pytest.raises(AssertionError, match="oracle is stable") as ei:
+        T._check(task, f"planted contact bug {kind}", n, seed, st, [a], outs[-1], sg, None)
+    listed = {int(v) for v in re.findall(r"\d+", str(ei.value).split(": [")[-1])}
+    assert listed and all(where[e] for e in listed), (sorted(listed), np.nonzero(where)[0][:20])

@@ -73,20 +73,21 @@ def test_full_state_headline_sizes(gpu, n):
     assert nbad <= 0.02 * len(ids)
 
 
-@pytest.mark.parametrize("task", ["v2", "v4", "manager"])
-def test_full_state_4096_every_solver(gpu, task):
-    """configs[1]'s size for the other walking tasks and for the TGS-style solve: one step of 4096
-    envs from random full states against the oracle run on ALL 4096 columns under the full-state
-    rule (PGS for v4 / manager, TGS-style for v2). Not a column sample: v4's and the manager's
-    command resampling draws from a counter-based generator keyed on the env index, so a column
-    subset is not the same sub-problem there."""
+@pytest.mark.parametrize("task,mode", [("v2", 0), ("v2", 1), ("v4", 0), ("manager", 0)],
+                         ids=["v2-pgs", "v2-tgs", "v4-pgs", "manager-pgs"])
+def test_full_state_4096_every_solver(gpu, task, mode):
+    """configs[1]'s size, every column: one step of 4096 envs from random full states against the
+    oracle run on ALL 4096 columns under the full-state rule, for the benchmarked walking v2 PGS
+    solve, v2's TGS-style solve, v4 and the manager. (v4's and the manager's command resampling
+    draws from a counter-based generator keyed on the env index, so a column subset would not be
+    the same sub-problem there.)"""
     import torch
     import test_gpu_fullstate as F
     from fullstate import random_states, solver_mode, task_cfg
     from oracle.pyoracle import OracleSim
     from zbot_lab_amd.sim import ZbotSim
     n, seed = 4096, 37
-    with solver_mode(1 if task == "v2" else 0):
+    with solver_mode(mode):
         cfg = task_cfg(task)
         st = random_states(task, OracleSim(n, cfg, seed=seed), n, seed=500)
         a = np.random.default_rng(n + 1).normal(size=(n, 6)).astype(np.float32)
@@ -95,7 +96,7 @@ def test_full_state_4096_every_solver(gpu, task):
         g_out = _step(g, a)
         sg = g.get_state().cpu().numpy()
         g.close()
-        nbad = F._check(task, f"one step of {n} envs ({'TGS' if task == 'v2' else 'PGS'})", n, seed, st, [a], g_out,
+        nbad = F._check(task, f"one step of {n} envs ({'TGS' if mode else 'PGS'}, every column)", n, seed, st, [a], g_out,
                         sg, torch)
     assert nbad <= 0.02 * n
 
