@@ -15,15 +15,20 @@ self-contact cache read + written (128 B), actions 24 B, obs 92 B, reward 4 B, t
 OpenMP over envs) on all of this host's cores available to the process and on one thread, on a
 bounded sample, with nproc / affinity / cgroup quota / CPU model stated.
 
-``--task v4`` measures zbot-6b-walking-v4 (commands / events / curricula; ``zb_v4_step_kernel``, 790 B
-per env-step: 81 state rows read, 85 written, actions, obs 96 B, reward, flags) at 4096 envs.
-``--task manager`` measures zbot-6b-walking-m-v0 (the manager-based flat env on ZBOT_6S_V2_CFG;
-``zb_m_step_kernel``, 834 B per env-step: 76 state rows read + written, 24 static / dynamic friction
-coefficients read, actions 24 B, obs 100 B, reward, flags) at 4096 envs with the startup friction randomisation.
-``--task standup`` measures the stand-up task instead (zbot-6b-standup-v0,
-32768 envs, friction randomisation on; kernel ``zb_su_step_kernel``, 558 B per env-step: 43 fp32
-state rows read + written, 24 static / dynamic friction coefficients read, actions 24 B, obs 88 B,
-reward, flags).
+``--task v4`` measures zbot-6b-walking-v4 (commands / events / curricula; ``zb_v4_step_kernel``, 918 B
+per env-step: 81 state rows read, 85 written, actions, obs 96 B, reward, flags, the contact cache) at
+4096 envs. ``--task manager`` measures zbot-6b-walking-m-v0 (the manager-based flat env on
+ZBOT_6S_V2_CFG; ``zb_m_step_kernel``, 962 B per env-step: 76 state rows read + written, 24 static /
+dynamic friction coefficients read, actions 24 B, obs 100 B, reward, flags, the contact cache) at 4096
+envs with the startup friction randomisation. ``--task standup`` measures the stand-up task instead
+(zbot-6b-standup-v0, 32768 envs, friction randomisation on; kernel
+``zb_su_step_kernel``, 686 B per env-step: 43 fp32 state rows read + written, 24 static / dynamic
+friction coefficients read, actions 24 B, obs 88 B, reward, flags, the contact cache).
+
+``--rehearsal`` (with N ranks under torch.distributed.run on a one-GPU box): every rank on cuda:0,
+gloo for the barrier and the timing reduction (RCCL cannot place two ranks on one device). The line
+then reports ``n_gpus`` 1 and the rank count under ``config.rehearsal_ranks``: it is a one-GPU
+measurement of the N-rank plumbing, never a multi-GPU result.
 """
 from __future__ import annotations
 
@@ -56,6 +61,8 @@ def parse():
     # ablation knobs (the reported line uses the defaults)
     p.add_argument("--solver-iterations", type=int, default=None)
     p.add_argument("--no-self-collision", action="store_true")
+    p.add_argument("--rehearsal", action="store_true",
+                   help="N ranks share cuda:0 over gloo (one-GPU box rehearsal; reports n_gpus 1)")
     return p.parse_args()
 
 
@@ -214,30 +221,48 @@ def run_launcher(cmd: list[str]) -> int:
     return subprocess.run(cmd, env=env).returncode
 
 
+def rank_plan(environ, rehearsal: bool = False) -> dict:
+    """Process-group and device plan of one bench rank (reference: train.py:125-132, one process per
+    GPU): rank / world from the launcher's env; with world > 1 the backend is "nccl" (= RCCL over
+    xGMI on ROCm) bound to device cuda:LOCAL_RANK, or, in a --rehearsal, "gloo" with every rank on
+    cuda:0 and host-side reductions. ``n_gpus`` is what the JSON line reports."""
+    world = int(environ.get("WORLD_SIZE", "1"))
+    rank = int(environ.get("RANK", "0"))
+    local_rank = int(environ.get("LOCAL_RANK", "0"))
+    share = world > 1 and rehearsal
+    if share:
+        local_rank = 0
+    backend = None if world == 1 else ("gloo" if share else "nccl")
+    return {"world": world, "rank": rank, "local_rank": local_rank, "share": share, "backend": backend,
+            "device": f"cuda:{local_rank}", "reduce_device": "cpu" if share else f"cuda:{local_rank}",
+            "n_gpus": 1 if share else world}
+
+
+def init_group(plan: dict, dist_mod=None):
+    """Initialise the process group of ``plan`` (None for one rank). RCCL gets the rank's device so
+    its communicator binds to that GPU at init."""
+    if plan["backend"] is None:
+        return None
+    if dist_mod is None:
+        import torch.distributed as dist_mod
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if plan["backend"] == "nccl":
+        dist_mod.init_process_group("nccl", device_id=torch.device(plan["device"]))
+    else:
+        dist_mod.init_process_group(plan["backend"])
+    return dist_mod
+
+
 def main():
     args = parse()
     cmd = launch_plan(args.gpus, os.environ, sys.argv[1:])
     if cmd is not None:
         sys.exit(run_launcher(cmd))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    # ZB_BENCH_SHARE_GPU=1: rehearsal of the N-rank path on a one-GPU box (every rank on cuda:0, gloo
-    # for the barrier / timing reduction; RCCL cannot put two ranks on one device). Never set by the
-    # SCALE runs, whose ranks each own a GPU.
-    share = world > 1 and os.environ.get("ZB_BENCH_SHARE_GPU") == "1"
-    if share:
-        local_rank = 0
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if share:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    plan = rank_plan(os.environ, args.rehearsal)
+    world, rank, local_rank, share = plan["world"], plan["rank"], plan["local_rank"], plan["share"]
+    dist = init_group(plan)
     torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    dev = torch.device(plan["device"])
 
     from zbot_lab_amd.envs import (Zbot6BFlatEnvCfg, Zbot6SEnvV4, Zbot6SEnvV4Cfg, Zbot6SUpEnv, Zbot6SUpEnvCfg,
                                    ZbotDirectEnvCfgV2, ZbotDirectEnvV2, ZbotManagerBasedRLEnv)
@@ -279,16 +304,16 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms, kern_n = env.sim.profile_end()
 
-    rdev = "cpu" if share else dev  # (gloo reduces host tensors)
+    rdev = plan["reduce_device"]  # (gloo reduces host tensors)
     t = torch.tensor([elapsed], dtype=torch.float64, device=rdev)
     per_rank = torch.tensor([n * args.steps / elapsed], dtype=torch.float64, device=rdev)
-    rccl_world = 1
+    coll_world = 1
     if dist is not None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         gathered = [torch.zeros_like(per_rank) for _ in range(world)]
         dist.all_gather(gathered, per_rank)
         per_rank = torch.cat(gathered)
-        rccl_world = dist.get_world_size()
+        coll_world = dist.get_world_size()
     elapsed = float(t.item())
     per_rank_rates = [float(v) for v in per_rank.tolist()]
     total_steps = n * world * args.steps
@@ -312,7 +337,7 @@ def main():
             "metric": "env-steps/sec at 4096/65536 envs, 1->8 GPUs; % HBM roofline",
             "value": value,
             "unit": "env-steps/s",
-            "n_gpus": world,
+            "n_gpus": plan["n_gpus"],
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
@@ -324,8 +349,10 @@ def main():
             "config": {"workload": workload,
                        "envs_per_gpu": n, "total_envs": n * world, "decimation": 4, "sim_dt": 0.005,
                        "parallelism": f"env-sharded x{world} (replicas, no collective)",
-                       "rccl_world_size": rccl_world, "per_rank_env_steps_per_s": per_rank_rates,
-                       **({"rehearsal": "all ranks on cuda:0, gloo collectives"} if share else {})},
+                       "collective": {"backend": plan["backend"], "world_size": coll_world},
+                       "per_rank_env_steps_per_s": per_rank_rates,
+                       **({"rehearsal_ranks": world, "rehearsal": "all ranks on cuda:0, gloo collectives"}
+                          if share else {})},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": kname, "kernel_ms": kern_s * 1e3,

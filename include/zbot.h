@@ -367,7 +367,8 @@ int zb_set_contact_cache(zb_handle h, const float* src, void* stream);
 
 /* Parity/debug: run `nsub` physics substeps with joint targets float[N][6] (no MDP);
  * if net_force != NULL it receives the last substep's net contact force, float[N][12][3],
- * and applied_torque (if != NULL) Isaac Lab's clipped PD estimate float[N][6]. */
+ * and applied_torque (if != NULL) Isaac Lab's clipped PD estimate float[N][6]. The persistent
+ * self-contact cache is invalidated (the next zb_step's first substep starts GJK cold). */
 int zb_physics_substeps(zb_handle h, const float* targets, int nsub, float* net_force,
                         float* applied_torque, void* stream);
 

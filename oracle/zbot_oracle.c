@@ -2827,6 +2827,7 @@ int zbo_physics_substeps(zbo_sim* s, const float* targets, int nsub, float* net_
         for (int a = 0; a < 3; ++a) net_force[((size_t)e * NL + l) * 3 + a] = (float)so.net_force[l][a];
     if (applied_torque)
       for (int j = 0; j < ND; ++j) applied_torque[(size_t)e * ND + j] = (float)so.applied_torque[j];
+    wc_invalidate(s->env[e].wc); /* the physics moved: the cache describes another state */
   }
   return 0;
 }

@@ -91,3 +91,47 @@ def test_runner_update_graph_follows_rollout_graph_single_rank(monkeypatch):
     from zbot_lab_amd.rl import OnPolicyRunner, PPORunnerCfgV2
     r = OnPolicyRunner(ToyVecEnv(n=8), PPORunnerCfgV2().to_dict(), log_dir=None, device="cpu", use_graph=True)
     assert r.graph_update is True
+
+
+def test_rank_plan_single_rank():
+    p = bench.rank_plan({})
+    assert p["backend"] is None and p["n_gpus"] == 1 and p["device"] == "cuda:0"
+    assert bench.init_group(p, dist_mod=object()) is None  # no process group for one rank
+
+
+@pytest.mark.parametrize("rank", [0, 3, 7])
+def test_rank_plan_scale_run_binds_rccl_to_the_local_gpu(rank):
+    """The driver's SCALE command (torch.distributed.run, 8 ranks): backend "nccl" (RCCL), each rank's
+    communicator bound at init to cuda:LOCAL_RANK, device-side reductions, n_gpus = WORLD_SIZE."""
+    env = {"WORLD_SIZE": "8", "RANK": str(rank), "LOCAL_RANK": str(rank)}
+    p = bench.rank_plan(env)
+    assert p["backend"] == "nccl" and p["n_gpus"] == 8 and not p["share"]
+    assert p["device"] == f"cuda:{rank}" and p["reduce_device"] == f"cuda:{rank}"
+
+    calls = []
+
+    class FakeDist:
+        def init_process_group(self, backend, **kw):
+            calls.append((backend, kw))
+
+    bench.init_group(p, dist_mod=FakeDist())
+    (backend, kw), = calls
+    assert backend == "nccl" and str(kw["device_id"]) == f"cuda:{rank}"
+
+
+def test_rank_plan_rehearsal_reports_one_gpu():
+    """--rehearsal: every rank on cuda:0 over gloo; the line reports n_gpus 1 (never a multi-GPU
+    result), and only the explicit flag turns it on (an environment variable does not)."""
+    env = {"WORLD_SIZE": "2", "RANK": "1", "LOCAL_RANK": "1", "ZB_BENCH_SHARE_GPU": "1"}
+    assert bench.rank_plan(env)["backend"] == "nccl"        # no flag: a real 2-GPU rank
+    p = bench.rank_plan(env, rehearsal=True)
+    assert p["backend"] == "gloo" and p["device"] == "cuda:0" and p["reduce_device"] == "cpu"
+    assert p["n_gpus"] == 1 and p["share"]
+    calls = []
+
+    class FakeDist:
+        def init_process_group(self, backend, **kw):
+            calls.append((backend, kw))
+
+    bench.init_group(p, dist_mod=FakeDist())
+    assert calls == [("gloo", {})]

@@ -6,14 +6,16 @@
 //   (v2.py:371-382, terms 461-561) -> _reset_idx (v2.py:413-459) -> _get_observations
 //   (v2.py:312-369)      [v2.py = source/zbot/zbot/tasks/zbot6b_direct/zbot_direct_6dof_bipedal_env_v2.py]
 //
-// Mapping: one env per lane, 64-lane workgroups (one wave). Persistent state is
-// SoA [field][env] in HBM, so every field load/store is one coalesced 256-B wave access; it is
-// read once and written once per step. Model constants are wave-uniform (scalar loads). The
-// 12-DoF dynamics (FK, RNEA, CRBA, 12x12 Cholesky, triangular solves) live in VGPRs, fully
-// unrolled over the fixed ZBOT-6 topology. The variable-length contact system (up to
-// ZB_MAX_CONTACTS rows x 3 directions x 12 whitened coordinates) is staged in LDS, lane-strided
-// ([slot][field][lane]) so every ds_read/ds_write is bank-conflict free. No MFMA: the largest
-// dense contraction is 12x12 per env.
+// Mapping: one env per 16-lane team (one DPP row), 4 envs per 64-lane wave =
+// workgroup, N/4 workgroups renumbered XCD-major. Persistent state is SoA [field][env] in HBM,
+// read once and written once per step; lane s of a team loads / stores rows s + 16k, so one
+// instruction moves 16 rows x 4 envs. Model constants are wave-uniform (scalar loads). Within a
+// team: FK as a DPP prefix over the chain, RNEA / CRBA one body per lane, the 12x12 Cholesky with
+// one row per lane, ground contact one link per lane, self collision as a capsule broadphase +
+// separating-axis test dealt over the lanes and GJK on DPP quads, PGS with lane s owning one
+// whitened coordinate (row dots reduced by DPP). The contact rows (up to ZB_MAX_CONTACTS slots x 3
+// directions x 12 coordinates) and the per-substep sensor records are staged in LDS. No MFMA: the
+// largest dense contraction is 12x12 per env.
 //
 // The algorithm is the one restated on the CPU in oracle/zbot_oracle.c (the parity oracle);
 // the two are written independently and compared by tests/test_gpu_parity.py.
@@ -2905,17 +2907,19 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_step_kernel(const z
 #undef OUT
   sp.mark(8);
   sp.flush();
-  // Fused finalize (FinArgs::done set): one agent-scope add per workgroup after its stores and log
-  // atomics have completed; the workgroup whose add comes last runs zb_finalize_kernel's body. The
-  // log accumulator is only touched by atomics and the episode-length row by agent-scope stores,
-  // so no release fence (an L2 write-back per workgroup) is needed.
+  // Fused finalize (FinArgs::done set, opt-in): one agent-scope release add per workgroup after
+  // its stores and log atomics; the workgroup whose add comes last takes an agent-scope acquire
+  // fence and runs zb_finalize_kernel's body. Release / acquire make the hand-over correct under the
+  // HIP memory model (the release writes back this XCD's L2: the path costs more than the separate
+  // finalize launch it replaces, DESIGN.md §7, and stays off by default).
   if (fa.done) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     unsigned prev = 0u;
-    if (lane == 0) prev = __hip_atomic_fetch_add(fa.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0) prev = __hip_atomic_fetch_add(fa.done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     prev = __builtin_amdgcn_readfirstlane(prev);
-    if (prev == gridDim.x - 1)
+    if (prev == gridDim.x - 1) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       finalize_body<true>(N, st, acc, fa, 0, 0, 1, cfg, nullptr, term, trunc, reinterpret_cast<float*>(lds));
+    }
   }
 #undef ST
 #undef CST
@@ -4682,7 +4686,9 @@ int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_dev
   HIPCHK(hipMalloc(&h->d_cnt, sizeof(Counters)), "hipMalloc counters");
   {
     const char* fz = getenv("ZB_FUSED_FINALIZE");
-    if (c->task == ZB_TASK_WALKING_V2 && ZB_STAGED_STORES && (fz ? fz[0] != '0' : ZB_FUSED_FINALIZE_DEFAULT)) {
+    // only an explicit "1" / "0" overrides the default (an empty value or "false" does not enable it)
+    const int fz_on = fz && fz[0] == '1' && fz[1] == 0, fz_off = fz && fz[0] == '0' && fz[1] == 0;
+    if (c->task == ZB_TASK_WALKING_V2 && ZB_STAGED_STORES && (fz_on || (!fz_off && ZB_FUSED_FINALIZE_DEFAULT))) {
       HIPCHK(hipMalloc(&h->d_done, sizeof(unsigned)), "hipMalloc done counter");
       HIPCHK(hipMemset(h->d_done, 0, sizeof(unsigned)), "hipMemset done counter");
       h->fused = true;
@@ -5124,7 +5130,11 @@ int zb_physics_substeps(zb_handle h, const float* targets, int nsub, float* net_
     else ZB_SUB(false, false);
   }
 #undef ZB_SUB
-  return launch_check("zb_substeps_kernel");
+  const int rc = launch_check("zb_substeps_kernel");
+  if (rc || !h->d_wc) return rc;
+  // the physics moved: the self-contact cache describes another state (cold start next step)
+  zb_wc_fill_kernel<<<(h->n * ZB_WARM_ROWS + 255) / 256, 256, 0, (hipStream_t)stream>>>(h->n, h->d_wc, nullptr, h->n);
+  return launch_check("zb_wc_fill_kernel");
 }
 
 int zb_gjk_pairs(const float* pairs, const float* v0, int n, float margin, float* out, void* stream) {

@@ -175,9 +175,13 @@ class ZbotDirectEnvV2:
 
     @episode_length_buf.setter
     def episode_length_buf(self, value: torch.Tensor) -> None:
+        """Writes only the counter row: the solver's self-contact cache (simulator-internal, not a
+        state row) survives, so rsl_rl's init_at_random_ep_len does not cold-start GJK."""
         st = self.sim.get_state()
+        wc = self.sim.get_contact_cache()
         st[self._ep_len_row] = value.to(device=self.device, dtype=torch.float32)
         self.sim.set_state(st)
+        self.sim.set_contact_cache(wc)
 
     def seed(self, seed: int = -1) -> int:
         return seed
