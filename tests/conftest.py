@@ -6,6 +6,10 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
+# before any test module imports torch: the package sets HIP's graph-capture mode ahead of HIP's
+# initialisation (zbot_lab_amd/__init__.py), so the runner's HIP graphs are on whatever the order
+# in which pytest collects the test files
+import zbot_lab_amd  # noqa: E402,F401
 
 
 def pytest_configure(config):

@@ -1,0 +1,124 @@
+"""The PPO minibatch update on libzbot_ppo.so (fp32 MFMA kernels, zbot_lab_amd/rl/fused.py) against
+the torch autograd statement of the same update (zbot_lab_amd/rl/ppo.py, rsl_rl semantics,
+reference agents/rsl_rl_ppo_cfg.py:65-91): the gradients of one minibatch (every weight, bias and
+the std) and its loss / KL statistics, and a whole update (20 minibatches with the adaptive learning
+rate, clipping and Adam) from the same snapshot. Tolerances are fp32 summation-order ones."""
+from __future__ import annotations
+
+import copy
+import os
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _alg(hidden, obs_dim=23, act=6, envs=512, steps=24, seed=0):
+    import torch
+    from zbot_lab_amd.rl.ppo import PPO, ActorCritic
+    torch.manual_seed(seed)
+    pol = ActorCritic(obs_dim, obs_dim, act, actor_hidden_dims=hidden, critic_hidden_dims=hidden)
+    alg = PPO(pol, device="cuda:0")
+    alg.init_storage(envs, steps, obs_dim, obs_dim, act)
+    st = alg.storage
+    g = torch.Generator(device="cuda:0").manual_seed(seed + 1)
+    for t in (st.observations, st.critic_observations, st.actions, st.rewards, st.values, st.mu):
+        t.copy_(torch.randn(t.shape, device="cuda:0", generator=g))
+    st.critic_observations.copy_(st.observations + 0.1 * st.critic_observations)
+    st.sigma.copy_(0.5 + torch.rand(st.sigma.shape, device="cuda:0", generator=g))
+    st.dones.copy_((torch.rand(st.dones.shape, device="cuda:0", generator=g) < 0.05).float())
+    with torch.no_grad():  # old log-probs near the current policy's, so ratios straddle the clip range
+        pol.update_distribution(st.observations.flatten(0, 1))
+        lp = pol.get_actions_log_prob(st.actions.flatten(0, 1)).view(steps, envs, 1)
+        st.actions_log_prob.copy_(lp + 0.3 * torch.randn(lp.shape, device="cuda:0", generator=g))
+        st.values.copy_(pol.evaluate(st.critic_observations.flatten(0, 1)).view(steps, envs, 1)
+                        + 0.3 * torch.randn(st.values.shape, device="cuda:0", generator=g))
+    st.step = steps
+    alg.compute_returns(st.critic_observations[-1])
+    st.step = steps
+    alg.draw_minibatch_indices()
+    return alg
+
+
+def _torch_minibatch(alg, i):
+    """update_steps' loss for minibatch i of the first epoch, backward into .grad (autograd)."""
+    import torch
+    gen = alg.storage.mini_batch_generator(alg.num_mini_batches, 1, alg.mb_indices)
+    for k, mbt in enumerate(gen):
+        if k == i:
+            break
+    obs_b, cobs_b, act_b, tv_b, adv_b, ret_b, old_lp_b, old_mu_b, old_sigma_b = mbt
+    pol = alg.policy
+    pol.update_distribution(obs_b)
+    lp_b = pol.get_actions_log_prob(act_b)
+    value_b = pol.evaluate(cobs_b)
+    mu_b, sigma_b, entropy_b = pol.action_mean, pol.action_std, pol.entropy
+    with torch.no_grad():
+        kl = torch.sum(torch.log(sigma_b / old_sigma_b + 1e-5)
+                       + (old_sigma_b.square() + (old_mu_b - mu_b).square()) / (2.0 * sigma_b.square()) - 0.5, dim=-1)
+    ratio = torch.exp(lp_b - torch.squeeze(old_lp_b))
+    s1 = -torch.squeeze(adv_b) * ratio
+    s2 = -torch.squeeze(adv_b) * torch.clamp(ratio, 1.0 - alg.clip_param, 1.0 + alg.clip_param)
+    surr = torch.max(s1, s2).mean()
+    vc = tv_b + (value_b - tv_b).clamp(-alg.clip_param, alg.clip_param)
+    vl = torch.max((value_b - ret_b).pow(2), (vc - ret_b).pow(2)).mean()
+    loss = surr + alg.value_loss_coef * vl - alg.entropy_coef * entropy_b.mean()
+    alg.optimizer.zero_grad(set_to_none=False)
+    loss.backward()
+    return torch.stack([kl.mean(), vl.detach(), surr.detach(), entropy_b.mean().detach()])
+
+
+@pytest.mark.parametrize("hidden", [[128, 128, 128], [256, 256, 128]], ids=["v2-nets", "standup-nets"])
+def test_fused_minibatch_gradients_match_autograd(gpu, hidden):
+    import torch
+    from zbot_lab_amd.rl import fused
+    alg = _alg(hidden)
+    mb = alg.storage.num_envs * alg.storage.num_transitions_per_env // alg.num_mini_batches
+    assert fused.supported(alg.policy, mb)
+    for i in (0, 3):
+        ref_stats = _torch_minibatch(alg, i)
+        ref = [p.grad.detach().clone() for p in alg.policy.parameters()]
+        f = fused.FusedUpdate(alg, mb)
+        f.pack()
+        stats = f.minibatch(alg.storage, alg.mb_indices, i * mb).clone()
+        torch.cuda.synchronize()
+        got = [p.grad.detach().clone() for p in alg.policy.parameters()]
+        names = [n for n, _ in alg.policy.named_parameters()]
+        for n, r, g in zip(names, ref, got):
+            scale = r.abs().max().item()
+            err = (g - r).abs().max().item()
+            assert err <= 1e-5 * scale + 1e-9, (i, n, err, scale)
+        torch.testing.assert_close(stats, ref_stats, rtol=1e-5, atol=1e-7)
+
+
+def test_fused_update_matches_torch_update(gpu, monkeypatch):
+    """A whole update (5 epochs x 4 minibatches: rate rule, clipping, Adam) from one snapshot, the
+    fused path against the torch path: parameters, learning rate and the logged loss sums."""
+    import torch
+    alg_f = _alg([128, 128, 128], seed=3)
+    alg_t = copy.deepcopy(alg_f)
+    monkeypatch.setenv("ZBOT_PPO_FUSED", "0")
+    alg_t.optimizer = torch.optim.Adam(alg_t.policy.parameters(), lr=alg_t.lr_t, fused=True, capturable=True)
+    p0 = torch.cat([p.detach().flatten() for p in alg_t.policy.parameters()]).clone()
+    alg_t.update_steps()
+    monkeypatch.setenv("ZBOT_PPO_FUSED", "1")
+    alg_f.update_steps()
+    assert alg_f._fused is not None and alg_t._fused is None
+    torch.cuda.synchronize()
+    pf = torch.cat([p.detach().flatten() for p in alg_f.policy.parameters()])
+    pt = torch.cat([p.detach().flatten() for p in alg_t.policy.parameters()])
+    moved = (pt - p0).abs()
+    d = (pf - pt).abs()
+    print(f"\nfused vs torch update: max |dp| {d.max().item():.3g} (99.9% {d.quantile(0.999).item():.3g}), "
+          f"max move {moved.max().item():.3g}, lr {float(alg_f.lr_t):.4g} / {float(alg_t.lr_t):.4g}")
+    assert moved.max() > 0
+    # Adam normalises each coordinate by its own gradient history: a gradient that summation order
+    # moves by 1e-6 moves the step of a near-zero coordinate by up to its whole size, so the bound is
+    # on the bulk and on the worst coordinate separately
+    assert d.quantile(0.999) <= 1e-3 * moved.max()
+    assert d.max() <= 0.05 * moved.max()
+    assert abs(float(alg_f.lr_t) - float(alg_t.lr_t)) <= 1e-7 + 1e-5 * float(alg_t.lr_t)
+    torch.testing.assert_close(alg_f.update_sums, alg_t.update_sums, rtol=1e-4, atol=1e-6)
+    opt_f, opt_t = alg_f.optimizer, alg_t.optimizer
+    for pf_, pt_ in zip(alg_f.policy.parameters(), alg_t.policy.parameters()):
+        assert float(opt_f.state[pf_]["step"]) == float(opt_t.state[pt_]["step"]) == 20.0

@@ -88,3 +88,39 @@ def test_product_path_fails_loudly_without_gpu():
         ZbotSim(4, device="cuda:0")
     with pytest.raises(_native.ZbotError):
         ZbotSim(4, device="cpu")
+
+
+def test_ppo_library_exports_and_struct_layouts():
+    """libzbot_ppo.so (include/zbot_ppo.h) exports every declared entry point, its ctypes structs have
+    the C sizes, and the host-side shape check answers without a GPU."""
+    import tempfile
+    from zbot_lab_amd import build
+    from zbot_lab_amd.rl import fused
+    path = build.build_ppo()
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True, check=True).stdout
+    text = open(os.path.join(ROOT, "include", "zbot_ppo.h")).read()
+    declared = set(re.findall(r"^\s*(?:int|int64_t|const char\*)\s+(zbp_\w+)\s*\(", text, re.M))
+    assert declared == set(fused.EXPORTED)
+    assert declared <= set(re.findall(r"\bT (zbp_\w+)", out))
+    assert b"gfx950" in open(path, "rb").read()
+    src = ('#include <stdio.h>\n#include "zbot_ppo.h"\nint main(){printf("%zu %zu %zu %zu\\n", sizeof(zbp_net), '
+           'sizeof(zbp_batch), sizeof(zbp_loss_cfg), sizeof(zbp_params));}\n')
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "p.c")
+        open(c, "w").write(src)
+        exe = os.path.join(d, "p")
+        subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), c, "-o", exe], check=True)
+        sizes = list(map(int, subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split()))
+    assert sizes == [C.sizeof(fused.Net), C.sizeof(fused.Batch), C.sizeof(fused.LossCfg), C.sizeof(fused.Params)]
+    L = fused.lib()
+    n = fused.Net()
+    n.n_layers = 4
+    for i, dd in enumerate([23, 128, 128, 128, 6]):
+        n.dim[i] = dd
+    for i in range(4):
+        n.w[i] = n.b[i] = 16  # non-null; not dereferenced by the shape check
+    m = fused.Net.from_buffer_copy(n)
+    m.dim[4] = 1
+    assert L.zbp_workspace_floats(C.byref(n), C.byref(m), 24576) > 0
+    n.dim[2] = 100  # hidden dims must be multiples of 32
+    assert L.zbp_workspace_floats(C.byref(n), C.byref(m), 24576) < 0

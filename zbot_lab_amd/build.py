@@ -55,9 +55,28 @@ def build(force: bool = False, verbose: bool = False, stamps: bool = False, defi
     return out
 
 
+PPO_SRC = os.path.join(HERE, "csrc", "ppo_mlp.hip")
+PPO_OUT = os.path.join(HERE, "libzbot_ppo.so")
+
+
+def build_ppo(force: bool = False) -> str:
+    """libzbot_ppo.so: the fused PPO minibatch update (fp32 MFMA, include/zbot_ppo.h). Plain -O3:
+    no fast-math (expf / logf / division as torch computes them)."""
+    deps = [PPO_SRC, os.path.join(ROOT, "include", "zbot_ppo.h"), os.path.abspath(__file__)]
+    if not force and os.path.exists(PPO_OUT) and all(os.path.getmtime(PPO_OUT) >= os.path.getmtime(d) for d in deps):
+        return PPO_OUT
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-I", os.path.join(ROOT, "include"),
+           "-o", PPO_OUT + ".tmp", PPO_SRC]
+    subprocess.run(cmd, check=True)
+    os.replace(PPO_OUT + ".tmp", PPO_OUT)
+    return PPO_OUT
+
+
 if __name__ == "__main__":
     defs = tuple(a[2:] for a in sys.argv[1:] if a.startswith("-D"))
     outs = [a[6:] for a in sys.argv[1:] if a.startswith("--out=")]
     flags = tuple(a[8:] for a in sys.argv[1:] if a.startswith("--flags="))
     print(build(force="--force" in sys.argv, verbose="-v" in sys.argv, stamps="--stamps" in sys.argv,
                 defines=defs, out=outs[0] if outs else None, flags=flags))
+    if not defs and not outs and not flags and "--stamps" not in sys.argv:
+        print(build_ppo(force="--force" in sys.argv))

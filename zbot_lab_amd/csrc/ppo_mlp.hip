@@ -1,0 +1,717 @@
+// ppo_mlp.hip — the PPO minibatch update of rsl_rl's ActorCritic as fp32 MFMA kernels for gfx950
+// (libzbot_ppo.so, C ABI include/zbot_ppo.h). Restates zbot_lab_amd/rl/ppo.py:PPO.update_steps
+// (rsl_rl PPO, reference agents/rsl_rl_ppo_cfg.py:65-91, ppo_learning_notes.md:521-548) per
+// minibatch in four launches instead of ~150 torch kernels:
+//
+//   k_pack    padded / transposed weight images in the workspace (Wp [P1][P0], Wt [P0][P1])
+//   k_rows    one workgroup per 32 minibatch rows: gather the rows through the permutation, actor
+//             forward (Linear + ELU, v_mfma_f32_32x32x2_f32 with the activations in LDS), the
+//             Gaussian log-prob / KL / clipped surrogate and its gradient, actor backward dX; then
+//             the critic forward, clipped value loss and backward. Every layer's input X_l and
+//             pre-activation gradient dZ_l go to HBM for the weight gradients.
+//   k_wgrad   dW_l = dZ_l^T X_l and db_l = sum dZ_l, one wave per 32x32 weight tile and row split
+//             (split-K over the minibatch rows), partial tiles to the workspace
+//   k_reduce  partial tiles -> every parameter's .grad, the std gradient, the minibatch stats
+//
+// and, on one GPU, k_optim (adaptive learning rate, global-norm clipping, Adam) + the re-pack.
+// Exact fp32 throughout (the MFMA is a k-ordered fmaf chain); results differ from torch's only by
+// summation order. MI355X mapping: the weights (<= 450 KB per net) stay L2-resident and stream as
+// the MFMA B operand; activations of a row tile live in LDS (row stride P + 4 floats: conflict-free
+// ds_read_b128); every workgroup holds one row tile and four waves split a layer's output columns.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "zbot_ppo.h"
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+constexpr int TR = 32;            // rows per tile (the MFMA's M)
+constexpr int MAXL = ZBP_MAX_LAYERS;
+constexpr int PART = 32 * 32 + 32;  // one weight-gradient partial tile + its bias column
+constexpr int NSTAT = 16;           // per-row-tile partial sums (surrogate, value, kl, std grads)
+
+thread_local char g_err[256] = "";
+int fail(int code, const char* what) {
+  snprintf(g_err, sizeof(g_err), "%s", what);
+  return code;
+}
+int hip_fail(hipError_t e, const char* what) {
+  snprintf(g_err, sizeof(g_err), "%s: %s", what, hipGetErrorString(e));
+  return -2;
+}
+
+inline int pad32(int d) { return (d + 31) & ~31; }
+
+// one net in the workspace: dims and float offsets of its images and row buffers
+struct NetW {
+  int L, d[MAXL + 1], p[MAXL + 1];
+  int64_t wp[MAXL], wt[MAXL], bp[MAXL];  // padded weights [p(l+1)][p(l)], transposed [p(l)][p(l+1)], bias [p(l+1)]
+  int64_t x[MAXL], dz[MAXL];             // row buffers: X_l [B][p(l)], dZ_l [B][p(l+1)]
+};
+struct Layout {
+  NetW n[2];
+  int64_t stats;  // [tiles][NSTAT] per-row-tile partial sums
+  int64_t part;   // [splits][wtiles][PART] weight-gradient partials
+  int wtiles, tile0[2 * MAXL + 1];  // weight tiles of (net, layer) in order, prefix counts
+  int splits;
+  int64_t scratch;  // [64] per-block gradient sums of squares (zbp_optimizer_step)
+  int64_t total;
+};
+
+Layout make_layout(const zbp_net* a, const zbp_net* c, int B) {
+  Layout lo{};
+  int64_t off = 0;
+  auto take = [&](int64_t n) { int64_t o = off; off += (n + 63) & ~int64_t(63); return o; };
+  const zbp_net* nets[2] = {a, c};
+  int t = 0;
+  for (int k = 0; k < 2; ++k) {
+    NetW& w = lo.n[k];
+    w.L = nets[k]->n_layers;
+    for (int l = 0; l <= w.L; ++l) { w.d[l] = nets[k]->dim[l]; w.p[l] = pad32(w.d[l]); }
+    for (int l = 0; l < w.L; ++l) {
+      w.wp[l] = take((int64_t)w.p[l + 1] * w.p[l]);
+      w.wt[l] = take((int64_t)w.p[l] * w.p[l + 1]);
+      w.bp[l] = take(w.p[l + 1]);
+      w.x[l] = take((int64_t)B * w.p[l]);
+      w.dz[l] = take((int64_t)B * w.p[l + 1]);
+      lo.tile0[k * MAXL + l] = t;
+      t += (w.p[l + 1] / 32) * (w.p[l] / 32);
+    }
+    for (int l = w.L; l < MAXL; ++l) lo.tile0[k * MAXL + l] = t;
+  }
+  lo.tile0[2 * MAXL] = t;
+  lo.wtiles = t;
+  lo.stats = take((int64_t)(B / TR) * NSTAT);
+  // row splits of the weight gradients: ~4 waves per SIMD over the chip, each split >= 256 rows
+  int s = 1;
+  // (rows per split a multiple of 16: k_wgrad's 8-step unrolled loop over row pairs)
+  while (s < 64 && (int64_t)t * s * 2 <= 4096 && B / (s * 2) >= 256 && B % (16 * s * 2) == 0) s *= 2;
+  lo.splits = s;
+  lo.part = take((int64_t)s * t * PART);
+  lo.scratch = take(64);
+  lo.total = off;
+  return lo;
+}
+
+const char* check_net(const zbp_net* n) {
+  if (!n || n->n_layers < 1 || n->n_layers > MAXL) return "n_layers must be 1..4";
+  if (n->dim[0] < 1 || n->dim[0] > 32) return "input dim must be 1..32";
+  for (int l = 1; l < n->n_layers; ++l)
+    if (n->dim[l] < 32 || n->dim[l] > 256 || n->dim[l] % 32) return "hidden dims must be multiples of 32 up to 256";
+  if (n->dim[n->n_layers] < 1 || n->dim[n->n_layers] > 32) return "output dim must be 1..32";
+  for (int l = 0; l < n->n_layers; ++l)
+    if (!n->w[l] || !n->b[l]) return "null weight / bias";
+  return nullptr;
+}
+
+__device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// C[32 rows][32 cols] = sum_k A[r][k] B[k][c] over k < kp (kp a multiple of 32): A row-major in LDS
+// (row stride sa floats), B given as the 32 rows m[(c0 + c) * ldm + k] of a row-major global matrix
+// (the reduction index contiguous). Lane (c = lane & 31, h = lane >> 5) feeds A[c][.] / B[.][c] on
+// the reduction indices [h kp / 2, (h + 1) kp / 2) (the MFMA's k = 0 / 1 halves).
+__device__ __forceinline__ f32x16 tile_mma(const float* __restrict__ a, int sa, const float* __restrict__ m, int ldm,
+                                           int kp, int c0) {
+  const int lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5, half = kp >> 1;
+  const float* ar = a + c * sa + h * half;
+  const float* br = m + (int64_t)(c0 + c) * ldm + h * half;
+  f32x16 acc = {};
+  float4 bn = *reinterpret_cast<const float4*>(br);
+  for (int s = 0; s < half; s += 4) {
+    const float4 bv = bn;
+    if (s + 4 < half) bn = *reinterpret_cast<const float4*>(br + s + 4);
+    const float4 av = *reinterpret_cast<const float4*>(ar + s);
+    acc = mfma(av.x, bv.x, acc);
+    acc = mfma(av.y, bv.y, acc);
+    acc = mfma(av.z, bv.z, acc);
+    acc = mfma(av.w, bv.w, acc);
+  }
+  return acc;
+}
+// row / column of accumulator register r of a 32x32 MFMA tile in this lane
+__device__ __forceinline__ int acc_row(int r) { return (r & 3) + 8 * (r >> 2) + 4 * ((threadIdx.x & 63) >> 5); }
+__device__ __forceinline__ int acc_col() { return threadIdx.x & 31; }
+
+// ------------------------------------------------------------------------------- k_pack
+struct PackArgs {
+  NetW n[2];
+  const float* w[2][MAXL];
+  const float* b[2][MAXL];
+  float* ws;
+};
+__global__ void k_pack(PackArgs A) {
+  const int net = blockIdx.y, l = blockIdx.z;
+  const NetW& w = A.n[net];
+  if (l >= w.L) return;
+  const int P0 = w.p[l], P1 = w.p[l + 1], D0 = w.d[l], D1 = w.d[l + 1];
+  float* wp = A.ws + w.wp[l];
+  float* wt = A.ws + w.wt[l];
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < P0 * P1; e += gridDim.x * blockDim.x) {
+    const int n = e / P0, k = e % P0;
+    const float v = (n < D1 && k < D0) ? A.w[net][l][n * D0 + k] : 0.f;
+    wp[e] = v;
+    wt[k * P1 + n] = v;
+  }
+  if (blockIdx.x == 0)
+    for (int n = threadIdx.x; n < P1; n += blockDim.x) A.ws[w.bp[l] + n] = n < D1 ? A.b[net][l][n] : 0.f;
+}
+
+// ------------------------------------------------------------------------------- k_rows
+struct RowArgs {
+  NetW n[2];
+  zbp_batch bt;
+  zbp_loss_cfg lc;
+  const float* std_param;
+  float* ws;
+  int64_t stats;
+  int lds_x[MAXL], lds_dz[2], lds_out, lds_red;  // LDS float offsets
+};
+
+// forward through one net for the row tile; the output layer's pre-activations land in `out`
+// ([32][33]: row stride 33)
+__device__ void net_forward(const RowArgs& A, const NetW& w, float* lds, int row0) {
+  const int wave = threadIdx.x >> 6;
+  for (int l = 0; l < w.L; ++l) {
+    const int P0 = w.p[l], P1 = w.p[l + 1];
+    const bool last = l == w.L - 1;
+    float* xs = lds + A.lds_x[l];
+    const float* wp = A.ws + w.wp[l];
+    const float* bp = A.ws + w.bp[l];
+    for (int t = wave; t < P1 / 32; t += 4) {
+      const f32x16 acc = tile_mma(xs, P0 + 4, wp, P0, P0, 32 * t);
+      const int n = 32 * t + acc_col();
+      const float bias = bp[n];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int i = acc_row(r);
+        float v = acc[r] + bias;
+        if (last) {
+          lds[A.lds_out + i * 33 + n] = v;
+        } else {
+          v = v > 0.f ? v : expf(v) - 1.f;  // ELU(alpha = 1), as ATen's elu kernel
+          lds[A.lds_x[l + 1] + i * (P1 + 4) + n] = v;
+          A.ws[w.x[l + 1] + (int64_t)(row0 + i) * P1 + n] = v;
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// backward through one net from dZ of the output layer (in lds_dz[0], row stride 36)
+__device__ void net_backward(const RowArgs& A, const NetW& w, float* lds, int row0) {
+  const int wave = threadIdx.x >> 6;
+  int cur = 0;
+  for (int l = w.L - 1; l >= 1; --l) {
+    const int P0 = w.p[l], P1 = w.p[l + 1];
+    const float* dz = lds + A.lds_dz[cur];
+    float* dzn = lds + A.lds_dz[cur ^ 1];
+    const float* xs = lds + A.lds_x[l];
+    const float* wt = A.ws + w.wt[l];
+    for (int t = wave; t < P0 / 32; t += 4) {
+      const f32x16 acc = tile_mma(dz, P1 + 4, wt, P1, P1, 32 * t);
+      const int k = 32 * t + acc_col();
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int i = acc_row(r);
+        const float x = xs[i * (P0 + 4) + k];
+        const float g = acc[r] * (x > 0.f ? 1.f : x + 1.f);  // ELU'(z) = exp(z) = x + 1 for z <= 0
+        dzn[i * (P0 + 4) + k] = g;
+        A.ws[w.dz[l - 1] + (int64_t)(row0 + i) * P0 + k] = g;
+      }
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+}
+
+// gather the tile's input rows (obs or critic obs) into X_0 (LDS + HBM), zero-padded
+__device__ void gather_input(const RowArgs& A, const NetW& w, const float* src, int dim, float* lds, int row0) {
+  const int P0 = w.p[0];
+  for (int e = threadIdx.x; e < TR * P0; e += blockDim.x) {
+    const int i = e / P0, k = e % P0;
+    const int64_t row = A.bt.idx[A.bt.idx_offset + row0 + i];
+    const float v = k < dim ? src[row * dim + k] : 0.f;
+    lds[A.lds_x[0] + i * (P0 + 4) + k] = v;
+    A.ws[w.x[0] + (int64_t)(row0 + i) * P0 + k] = v;
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+__global__ __launch_bounds__(256) void k_rows(RowArgs A) {
+  extern __shared__ float lds[];
+  const int row0 = blockIdx.x * TR;
+  const int tid = threadIdx.x;
+  const zbp_batch& bt = A.bt;
+  const int NA = bt.num_actions;
+  const float invB = 1.f / (float)bt.batch;
+  float* red = lds + A.lds_red;  // [NSTAT] per-tile sums
+  if (tid < NSTAT) red[tid] = 0.f;
+
+  // ---- actor: forward, Gaussian log-prob, clipped surrogate, KL; dL/dmu into dZ of the output
+  const NetW& wa = A.n[0];
+  gather_input(A, wa, bt.obs, bt.obs_dim, lds, row0);
+  net_forward(A, wa, lds, row0);
+  {
+    float* dz = lds + A.lds_dz[0];
+    const int Pout = wa.p[wa.L];
+    for (int e = tid; e < TR * Pout; e += blockDim.x) dz[(e / Pout) * (Pout + 4) + e % Pout] = 0.f;
+    __syncthreads();
+    float surr = 0.f, kl = 0.f, sg[NSTAT - 3];
+#pragma unroll
+    for (int a = 0; a < NSTAT - 3; ++a) sg[a] = 0.f;
+    if (tid < TR) {
+      const int i = tid;
+      const int64_t row = bt.idx[bt.idx_offset + row0 + i];
+      const float kLog2Pi = 0.91893853320467274178f;  // log(sqrt(2 pi))
+      float lp = 0.f;
+      for (int a = 0; a < NA; ++a) {
+        const float mu = lds[A.lds_out + i * 33 + a], s = A.std_param[a];
+        const float x = bt.actions[row * NA + a], diff = x - mu;
+        lp += -(diff * diff) / (2.f * (s * s)) - logf(s) - kLog2Pi;
+        const float os = bt.sigma[row * NA + a], om = bt.mu[row * NA + a];
+        kl += logf(s / os + 1e-5f) + (os * os + (om - mu) * (om - mu)) / (2.f * (s * s)) - 0.5f;
+      }
+      const float adv = bt.advantages[row], clip = A.lc.clip_param;
+      const float ratio = expf(lp - bt.log_prob[row]);
+      const float rc = fminf(fmaxf(ratio, 1.f - clip), 1.f + clip);
+      const float s1 = -adv * ratio, s2 = -adv * rc;
+      surr = fmaxf(s1, s2);
+      // d max(s1, s2) / d ratio (torch.max splits a tie evenly; clamp passes the gradient inside
+      // [1 - clip, 1 + clip], bounds included)
+      const float in = (ratio >= 1.f - clip && ratio <= 1.f + clip) ? 1.f : 0.f;
+      const float w1 = s1 > s2 ? 1.f : (s1 < s2 ? 0.f : 0.5f);
+      const float g = (w1 * -adv + (1.f - w1) * -adv * in) * ratio * invB;  // dL / dlog_prob
+#pragma unroll
+      for (int a = 0; a < NSTAT - 3; ++a) {
+        if (a >= NA) break;
+        const float mu = lds[A.lds_out + i * 33 + a], s = A.std_param[a];
+        const float diff = bt.actions[row * NA + a] - mu;
+        dz[i * (Pout + 4) + a] = g * diff / (s * s);
+        A.ws[wa.dz[wa.L - 1] + (int64_t)(row0 + i) * Pout + a] = g * diff / (s * s);
+        sg[a] = g * (diff * diff / (s * s * s) - 1.f / s);
+      }
+    }
+    // the padding columns of the output dZ row buffer
+    for (int e = tid; e < TR * Pout; e += blockDim.x)
+      if (e % Pout >= NA) A.ws[wa.dz[wa.L - 1] + (int64_t)(row0 + e / Pout) * Pout + e % Pout] = 0.f;
+    if (tid < 64) {
+      surr = wave_sum(surr);
+      kl = wave_sum(kl);
+#pragma unroll
+      for (int a = 0; a < NSTAT - 3; ++a) sg[a] = wave_sum(sg[a]);
+      if (tid == 0) {
+        red[0] = surr;
+        red[2] = kl;
+#pragma unroll
+        for (int a = 0; a < NSTAT - 3; ++a) red[3 + a] = sg[a];
+      }
+    }
+    __syncthreads();
+  }
+  net_backward(A, wa, lds, row0);
+
+  // ---- critic: forward, clipped value loss, backward
+  const NetW& wc = A.n[1];
+  gather_input(A, wc, bt.critic_obs, bt.critic_obs_dim, lds, row0);
+  net_forward(A, wc, lds, row0);
+  {
+    float* dz = lds + A.lds_dz[0];
+    const int Pout = wc.p[wc.L];
+    for (int e = tid; e < TR * Pout; e += blockDim.x) {
+      dz[(e / Pout) * (Pout + 4) + e % Pout] = 0.f;
+      if (e % Pout) A.ws[wc.dz[wc.L - 1] + (int64_t)(row0 + e / Pout) * Pout + e % Pout] = 0.f;
+    }
+    __syncthreads();
+    float vl = 0.f;
+    if (tid < TR) {
+      const int i = tid;
+      const int64_t row = bt.idx[bt.idx_offset + row0 + i];
+      const float v = lds[A.lds_out + i * 33], tv = bt.values[row], ret = bt.returns[row], clip = A.lc.clip_param;
+      float dv;
+      if (A.lc.use_clipped_value_loss) {
+        const float vd = v - tv;
+        const float vc = tv + fminf(fmaxf(vd, -clip), clip);
+        const float ea = (v - ret) * (v - ret), ec = (vc - ret) * (vc - ret);
+        vl = fmaxf(ea, ec);
+        const float wa_ = ea > ec ? 1.f : (ea < ec ? 0.f : 0.5f);
+        const float in = (vd >= -clip && vd <= clip) ? 1.f : 0.f;
+        dv = wa_ * 2.f * (v - ret) + (1.f - wa_) * 2.f * (vc - ret) * in;
+      } else {
+        vl = (ret - v) * (ret - v);
+        dv = 2.f * (v - ret);
+      }
+      dv *= A.lc.value_loss_coef * invB;
+      dz[i * (Pout + 4)] = dv;
+      A.ws[wc.dz[wc.L - 1] + (int64_t)(row0 + i) * Pout] = dv;
+    }
+    if (tid < 64) {
+      vl = wave_sum(vl);
+      if (tid == 0) red[1] = vl;
+    }
+    __syncthreads();
+  }
+  net_backward(A, wc, lds, row0);
+  if (tid < NSTAT) A.ws[A.stats + (int64_t)blockIdx.x * NSTAT + tid] = red[tid];
+}
+
+// ------------------------------------------------------------------------------- k_wgrad
+struct WgradArgs {
+  NetW n[2];
+  int tile0[2 * MAXL + 1];
+  int wtiles, splits, batch;
+  float* ws;
+  int64_t part;
+};
+// one wave: the 32x32 tile (n0, k0) of dW_l = dZ_l^T X_l over the rows of one split, and db_l
+// (the k0 = 0 tiles). A[n][r] = dZ[r][n0 + n], B[r][k] = X[r][k0 + k]; lane half h takes rows
+// r0 + 2 s + h.
+__global__ __launch_bounds__(256) void k_wgrad(WgradArgs A) {
+  const int item = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (item >= A.wtiles * A.splits) return;
+  const int tile = item % A.wtiles, split = item / A.wtiles;
+  int nl = 0;
+  while (nl + 1 < 2 * MAXL && A.tile0[nl + 1] <= tile) ++nl;
+  const NetW& w = A.n[nl / MAXL];
+  const int l = nl % MAXL;
+  const int P0 = w.p[l], P1 = w.p[l + 1];
+  const int t = tile - A.tile0[nl], kt = P0 / 32;
+  const int n0 = 32 * (t / kt), k0 = 32 * (t % kt);
+  const int rows = A.batch / A.splits, r0 = split * rows;
+  const int lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
+  const float* dz = A.ws + w.dz[l] + (int64_t)(r0 + h) * P1 + n0 + c;
+  const float* x = A.ws + w.x[l] + (int64_t)(r0 + h) * P0 + k0 + c;
+  f32x16 acc = {};
+  float bsum = 0.f;
+  for (int s = 0; s < rows / 2; s += 8) {
+    float av[8], bv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      av[u] = dz[(int64_t)(2 * (s + u)) * P1];
+      bv[u] = x[(int64_t)(2 * (s + u)) * P0];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      acc = mfma(av[u], bv[u], acc);
+      bsum += av[u];
+    }
+  }
+  float* out = A.ws + A.part + ((int64_t)split * A.wtiles + tile) * PART;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) out[acc_row(r) * 32 + acc_col()] = acc[r];  // [n][k]
+  bsum += __shfl_xor(bsum, 32);
+  if (k0 == 0 && h == 0) out[1024 + c] = bsum;
+}
+
+// ------------------------------------------------------------------------------- k_reduce
+struct ReduceArgs {
+  NetW n[2];
+  int tile0[2 * MAXL + 1];
+  int wtiles, splits, row_tiles, batch, num_actions;
+  float* gw[2][MAXL];
+  float* gb[2][MAXL];
+  const float* std_param;
+  float* std_grad;
+  float* stats;
+  float entropy_coef;
+  const float* ws;
+  int64_t part, rstats;
+  int64_t total;  // parameter elements (weights + biases) of both nets
+};
+__global__ __launch_bounds__(256) void k_reduce(ReduceArgs A) {
+  const int64_t e0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (blockIdx.x == gridDim.x - 1) {
+    // the scalars: per-row-tile sums -> stats, the std gradient (+ the entropy bonus term)
+    __shared__ float acc[NSTAT];
+    if (threadIdx.x < NSTAT) {
+      float s = 0.f;
+      for (int t = 0; t < A.row_tiles; ++t) s += A.ws[A.rstats + (int64_t)t * NSTAT + threadIdx.x];
+      acc[threadIdx.x] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const float invB = 1.f / (float)A.batch;
+      float ent = 0.f;
+      for (int a = 0; a < A.num_actions; ++a) ent += 0.5f + 0.91893853320467274178f + logf(A.std_param[a]);
+      A.stats[0] = acc[2] * invB;  // kl mean
+      A.stats[1] = acc[1] * invB;  // value loss
+      A.stats[2] = acc[0] * invB;  // surrogate loss
+      A.stats[3] = ent;            // entropy (every row's)
+      for (int a = 0; a < A.num_actions; ++a) A.std_grad[a] = acc[3 + a] - A.entropy_coef / A.std_param[a];
+    }
+    return;
+  }
+  for (int64_t e = e0; e < A.total; e += (int64_t)(gridDim.x - 1) * blockDim.x) {
+    // locate (net, layer, weight or bias, n, k)
+    int64_t r = e;
+    int net = 0, l = 0;
+    bool bias = false;
+    int n = 0, k = 0;
+    for (net = 0; net < 2; ++net) {
+      const NetW& w = A.n[net];
+      bool found = false;
+      for (l = 0; l < w.L; ++l) {
+        const int64_t nw = (int64_t)w.d[l + 1] * w.d[l];
+        if (r < nw) { n = (int)(r / w.d[l]); k = (int)(r % w.d[l]); found = true; break; }
+        r -= nw;
+        if (r < w.d[l + 1]) { n = (int)r; bias = true; found = true; break; }
+        r -= w.d[l + 1];
+      }
+      if (found) break;
+    }
+    const NetW& w = A.n[net];
+    const int kt = w.p[l] / 32;
+    const int tile = A.tile0[net * MAXL + l] + (n / 32) * kt + (bias ? 0 : k / 32);
+    const int idx = bias ? 1024 + n % 32 : (n % 32) * 32 + k % 32;
+    float s = 0.f;
+    for (int sp = 0; sp < A.splits; ++sp) s += A.ws[A.part + ((int64_t)sp * A.wtiles + tile) * PART + idx];
+    if (bias) A.gb[net][l][n] = s;
+    else A.gw[net][l][(int64_t)n * w.d[l] + k] = s;
+  }
+}
+
+// ------------------------------------------------------------------------------- k_optim
+struct OptimArgs {
+  zbp_params P;
+  float* lr;
+  const float* stats;
+  float* acc;
+  float desired_kl, max_norm, b1, b2, eps;
+  float* norm2;  // workspace scratch: [64] per-block sums of squares (k_norm), summed in order by k_adam
+};
+__global__ __launch_bounds__(256) void k_norm(OptimArgs A) {
+  // global gradient norm^2 over every tensor (one block per tensor slice, atomics into norm2)
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int t = 0; t < A.P.n_params; ++t)
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < A.P.numel[t]; e += (int64_t)gridDim.x * blockDim.x) {
+      const float g = A.P.grad[t][e];
+      s += g * g;
+    }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) A.norm2[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);  // fixed order
+}
+__global__ __launch_bounds__(256) void k_adam(OptimArgs A) {
+  // learning rate rule (rsl_rl adaptive schedule, on the minibatch KL), clip coefficient, Adam
+  const float kl = A.stats[0];
+  float lr = *A.lr;
+  if (A.desired_kl > 0.f) {
+    if (kl > A.desired_kl * 2.f) lr = fmaxf(lr / 1.5f, 1e-5f);
+    else if (kl > 0.f && kl < A.desired_kl / 2.f) lr = fminf(lr * 1.5f, 1e-2f);
+  }
+  float n2 = 0.f;
+  for (int b = 0; b < 64; ++b) n2 += A.norm2[b];
+  const float total = sqrtf(n2);
+  const float coef = fminf(A.max_norm / (total + 1e-6f), 1.f);
+  const float step = A.P.step[0][0] + 1.f;
+  const float bc1 = 1.f - powf(A.b1, step), bc2s = sqrtf(1.f - powf(A.b2, step));
+  const float step_size = lr / bc1;
+  for (int t = 0; t < A.P.n_params; ++t)
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < A.P.numel[t]; e += (int64_t)gridDim.x * blockDim.x) {
+      const float g = A.P.grad[t][e] * coef;
+      A.P.grad[t][e] = g;
+      const float m = A.b1 * A.P.exp_avg[t][e] + (1.f - A.b1) * g;
+      const float v = A.b2 * A.P.exp_avg_sq[t][e] + (1.f - A.b2) * g * g;
+      A.P.exp_avg[t][e] = m;
+      A.P.exp_avg_sq[t][e] = v;
+      A.P.param[t][e] -= step_size * m / (sqrtf(v) / bc2s + A.eps);
+    }
+  // (every block reads the old lr / step: k_optim_tail writes the new ones after this launch)
+}
+__global__ void k_optim_tail(OptimArgs A) {
+  if (threadIdx.x != 0) return;
+  const float kl = A.stats[0];
+  float lr = *A.lr;
+  if (A.desired_kl > 0.f) {
+    if (kl > A.desired_kl * 2.f) lr = fmaxf(lr / 1.5f, 1e-5f);
+    else if (kl > 0.f && kl < A.desired_kl / 2.f) lr = fminf(lr * 1.5f, 1e-2f);
+  }
+  *A.lr = lr;
+  const float step = A.P.step[0][0] + 1.f;
+  for (int t = 0; t < A.P.n_params; ++t) A.P.step[t][0] = step;
+  A.acc[0] += A.stats[1];
+  A.acc[1] += A.stats[2];
+  A.acc[2] += A.stats[3];
+}
+
+int launch_check(const char* what) {
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : hip_fail(e, what);
+}
+
+PackArgs pack_args(const Layout& lo, const zbp_net* a, const zbp_net* c, float* ws) {
+  PackArgs P{};
+  P.n[0] = lo.n[0];
+  P.n[1] = lo.n[1];
+  const zbp_net* nets[2] = {a, c};
+  for (int k = 0; k < 2; ++k)
+    for (int l = 0; l < nets[k]->n_layers; ++l) { P.w[k][l] = nets[k]->w[l]; P.b[k][l] = nets[k]->b[l]; }
+  P.ws = ws;
+  return P;
+}
+int do_pack(const Layout& lo, const zbp_net* a, const zbp_net* c, float* ws, hipStream_t s) {
+  const int L = lo.n[0].L > lo.n[1].L ? lo.n[0].L : lo.n[1].L;
+  k_pack<<<dim3(64, 2, L), 256, 0, s>>>(pack_args(lo, a, c, ws));
+  return launch_check("k_pack");
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* zbp_last_error(void) { return g_err; }
+
+int64_t zbp_workspace_floats(const zbp_net* actor, const zbp_net* critic, int32_t batch) {
+  if (check_net(actor) || check_net(critic) || batch < TR || batch % TR) return -1;
+  return make_layout(actor, critic, batch).total;
+}
+
+int zbp_pack(const zbp_net* actor, const zbp_net* critic, float* ws, int32_t batch, void* stream) {
+  if (const char* e = check_net(actor)) return fail(-1, e);
+  if (const char* e = check_net(critic)) return fail(-1, e);
+  if (!ws || batch < TR || batch % TR) return fail(-1, "zbp_pack: workspace / batch");
+  return do_pack(make_layout(actor, critic, batch), actor, critic, ws, (hipStream_t)stream);
+}
+
+int zbp_minibatch(const zbp_net* actor, const zbp_net* critic, const float* std_param, float* std_grad,
+                  const zbp_batch* batch, const zbp_loss_cfg* loss, float* ws, float* stats, void* stream) {
+  if (const char* e = check_net(actor)) return fail(-1, e);
+  if (const char* e = check_net(critic)) return fail(-1, e);
+  if (!batch || !loss || !ws || !stats || !std_param || !std_grad) return fail(-1, "zbp_minibatch: null argument");
+  const int B = batch->batch;
+  if (B < TR || B % TR) return fail(-1, "zbp_minibatch: batch must be a positive multiple of 32");
+  if (batch->num_actions != actor->dim[actor->n_layers] || batch->num_actions > NSTAT - 3)
+    return fail(-1, "zbp_minibatch: num_actions must match the actor output (<= 13)");
+  if (batch->obs_dim != actor->dim[0] || batch->critic_obs_dim != critic->dim[0] || critic->dim[critic->n_layers] != 1)
+    return fail(-1, "zbp_minibatch: observation dims / critic output");
+  for (int k = 0; k < 2; ++k) {
+    const zbp_net* n = k ? critic : actor;
+    for (int l = 0; l < n->n_layers; ++l)
+      if (!n->gw[l] || !n->gb[l]) return fail(-1, "zbp_minibatch: null .grad buffer");
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const Layout lo = make_layout(actor, critic, B);
+
+  RowArgs R{};
+  R.n[0] = lo.n[0];
+  R.n[1] = lo.n[1];
+  R.bt = *batch;
+  R.lc = *loss;
+  R.std_param = std_param;
+  R.ws = ws;
+  R.stats = lo.stats;
+  int off = 0, pmax = 0;
+  for (int l = 0; l < MAXL; ++l) {
+    const int p = lo.n[0].p[l] > lo.n[1].p[l] ? lo.n[0].p[l] : lo.n[1].p[l];
+    R.lds_x[l] = off;
+    off += TR * (p + 4);
+  }
+  for (int k = 0; k < 2; ++k)
+    for (int l = 0; l <= MAXL; ++l) pmax = lo.n[k].p[l] > pmax ? lo.n[k].p[l] : pmax;
+  R.lds_dz[0] = off;
+  off += TR * (pmax + 4);
+  R.lds_dz[1] = off;
+  off += TR * (pmax + 4);
+  R.lds_out = off;
+  off += TR * 33;
+  R.lds_red = off;
+  off += NSTAT;
+  const size_t lds = sizeof(float) * off;
+  if (lds > 160 * 1024) return fail(-1, "zbp_minibatch: nets too wide for the LDS row tile");
+  static bool lds_set = false;  // (a host-side attribute: set once, outside any stream capture's ops)
+  if (!lds_set) {
+    const hipError_t e = hipFuncSetAttribute((const void*)k_rows, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return hip_fail(e, "hipFuncSetAttribute k_rows");
+    lds_set = true;
+  }
+  k_rows<<<B / TR, 256, lds, s>>>(R);
+  if (int rc = launch_check("k_rows")) return rc;
+
+  WgradArgs W{};
+  W.n[0] = lo.n[0];
+  W.n[1] = lo.n[1];
+  for (int i = 0; i <= 2 * MAXL; ++i) W.tile0[i] = lo.tile0[i];
+  W.wtiles = lo.wtiles;
+  W.splits = lo.splits;
+  W.batch = B;
+  W.ws = ws;
+  W.part = lo.part;
+  const int items = lo.wtiles * lo.splits;
+  k_wgrad<<<(items + 3) / 4, 256, 0, s>>>(W);
+  if (int rc = launch_check("k_wgrad")) return rc;
+
+  ReduceArgs D{};
+  D.n[0] = lo.n[0];
+  D.n[1] = lo.n[1];
+  for (int i = 0; i <= 2 * MAXL; ++i) D.tile0[i] = lo.tile0[i];
+  D.wtiles = lo.wtiles;
+  D.splits = lo.splits;
+  D.row_tiles = B / TR;
+  D.batch = B;
+  D.num_actions = batch->num_actions;
+  int64_t total = 0;
+  for (int k = 0; k < 2; ++k) {
+    const zbp_net* n = k ? critic : actor;
+    for (int l = 0; l < n->n_layers; ++l) {
+      D.gw[k][l] = n->gw[l];
+      D.gb[k][l] = n->gb[l];
+      total += (int64_t)n->dim[l + 1] * n->dim[l] + n->dim[l + 1];
+    }
+  }
+  D.total = total;
+  D.std_param = std_param;
+  D.std_grad = std_grad;
+  D.stats = stats;
+  D.entropy_coef = loss->entropy_coef;
+  D.ws = ws;
+  D.part = lo.part;
+  D.rstats = lo.stats;
+  const int blocks = (int)((total + 255) / 256 < 512 ? (total + 255) / 256 : 512) + 1;
+  k_reduce<<<blocks, 256, 0, s>>>(D);
+  return launch_check("k_reduce");
+}
+
+int zbp_optimizer_step(const zbp_params* params, float* lr, const float* stats, float* acc, float desired_kl,
+                       float max_grad_norm, float beta1, float beta2, float eps, const zbp_net* actor,
+                       const zbp_net* critic, float* ws, int32_t batch, void* stream) {
+  if (!params || params->n_params < 1 || params->n_params > ZBP_MAX_PARAMS || !lr || !stats || !acc || !ws)
+    return fail(-1, "zbp_optimizer_step: bad argument");
+  if (const char* e = check_net(actor)) return fail(-1, e);
+  if (const char* e = check_net(critic)) return fail(-1, e);
+  hipStream_t s = (hipStream_t)stream;
+  const Layout lo = make_layout(actor, critic, batch);
+  OptimArgs O{};
+  O.P = *params;
+  O.lr = lr;
+  O.stats = stats;
+  O.acc = acc;
+  O.desired_kl = desired_kl;
+  O.max_norm = max_grad_norm;
+  O.b1 = beta1;
+  O.b2 = beta2;
+  O.eps = eps;
+  O.norm2 = ws + lo.scratch;
+  k_norm<<<64, 256, 0, s>>>(O);
+  if (int rc = launch_check("k_norm")) return rc;
+  k_adam<<<64, 256, 0, s>>>(O);
+  if (int rc = launch_check("k_adam")) return rc;
+  k_optim_tail<<<1, 64, 0, s>>>(O);
+  if (int rc = launch_check("k_optim_tail")) return rc;
+  return do_pack(lo, actor, critic, ws, s);
+}
+
+}  // extern "C"

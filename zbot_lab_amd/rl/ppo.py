@@ -11,12 +11,18 @@ this is a compatible restatement: same module names and tensor semantics, same c
 * ``PPO.update``: ``num_learning_epochs`` x ``num_mini_batches`` shuffled minibatches; adaptive LR
   from the Gaussian KL (desired_kl, x/÷1.5, bounded [1e-5, 1e-2]); clipped surrogate + clipped
   value loss - entropy bonus; global-norm gradient clipping; Adam.
+* On a GPU the minibatches run on ``libzbot_ppo.so`` (``zbot_lab_amd/rl/fused.py``, hand-written fp32
+  MFMA kernels: forward, loss, backward in four launches per minibatch; on one GPU the adaptive
+  learning rate, clipping and Adam fused too) whenever the nets fit its limits; the torch autograd path
+  below is the same statement and serves CPU tensors (``ZBOT_PPO_FUSED=0`` selects it on a GPU).
 * Multi-GPU: one process per GPU; per minibatch ONE all-reduce averages the
   flattened gradient with the minibatch's KL mean appended (one bucket, 292 KB for v2) before the
   learning-rate rule and clipping — RCCL over xGMI when the process group is ``nccl`` (torch's
   name for RCCL on ROCm), gloo on CPU. Every rank applies the rule to the same averaged KL.
 """
 from __future__ import annotations
+
+import os
 
 import torch
 import torch.distributed as dist
@@ -222,6 +228,7 @@ class PPO:
         self.gpu_world_size = multi_gpu_cfg["world_size"] if multi_gpu_cfg else 1
         self._tr: dict = {}
         self.generator: torch.Generator | None = None
+        self._fused = None  # rl/fused.FusedUpdate, built at the first GPU update
 
     def init_storage(self, num_envs: int, num_transitions_per_env: int, obs_dim: int, critic_obs_dim: int,
                      action_dim: int) -> None:
@@ -311,12 +318,30 @@ class PPO:
         m = (self.update_sums / n).tolist()
         return {"value_function": m[0], "surrogate": m[1], "entropy": m[2]}
 
+    def fused_update(self):
+        """The libzbot_ppo driver for this policy and minibatch size, or None (CPU tensors, nets
+        outside the kernels' limits, or ZBOT_PPO_FUSED=0)."""
+        if self._fused is None and os.environ.get("ZBOT_PPO_FUSED", "1") != "0" and self.storage is not None:
+            from . import fused
+            mb = self.storage.num_envs * self.storage.num_transitions_per_env // self.num_mini_batches
+            if fused.supported(self.policy, mb):
+                self._fused = fused.FusedUpdate(self, mb)
+        return self._fused
+
+    def invalidate_fused(self) -> None:
+        """Parameters / optimizer state replaced (checkpoint load): rebuild the fused driver."""
+        self._fused = None
+
     def update_steps(self) -> None:
         """All minibatch updates with no host synchronisation (graph-capturable on a GPU), over the
         permutation in ``mb_indices`` (``draw_minibatch_indices`` first)."""
         sums = self.update_sums
         sums.zero_()
         adaptive = self.desired_kl is not None and self.schedule == "adaptive"
+        f = self.fused_update()
+        if f is not None:
+            self._update_steps_fused(f, sums, adaptive)
+            return
         for (obs_b, cobs_b, act_b, target_values_b, adv_b, returns_b, old_lp_b, old_mu_b,
              old_sigma_b) in self.storage.mini_batch_generator(self.num_mini_batches, self.num_learning_epochs,
                                                                self.mb_indices):
@@ -361,6 +386,27 @@ class PPO:
         # which remember the stream they were created on, and a later HIP-graph capture of this
         # update would then synchronise with that (default) stream and break the capture
         self.policy.distribution = None
+        self.storage.clear()
+
+    def _update_steps_fused(self, f, sums: torch.Tensor, adaptive: bool) -> None:
+        """update_steps on libzbot_ppo: the same minibatches (rsl_rl's generator order), each one
+        zbp_minibatch (forward, loss, backward into every .grad); then either the fused optimizer
+        (one GPU) or torch's all-reduce / rate rule / clipping / Adam and a re-pack (multi-GPU)."""
+        f.pack()
+        mb = f.batch
+        for _ in range(self.num_learning_epochs):
+            for i in range(self.num_mini_batches):
+                stats = f.minibatch(self.storage, self.mb_indices, i * mb)
+                if self.is_multi_gpu:
+                    kl_mean = self.reduce_parameters(stats[0].clone() if adaptive else None)
+                    if adaptive:
+                        self._adapt_learning_rate(kl_mean)
+                    nn.utils.clip_grad_norm_(self.policy.parameters(), self.max_grad_norm)
+                    self.optimizer.step()
+                    sums += stats[1:4]
+                    f.pack()
+                else:
+                    f.optimizer_step(sums)
         self.storage.clear()
 
     def restore_learning_rate(self) -> None:

@@ -244,6 +244,7 @@ class OnPolicyRunner:
         if load_optimizer:
             self.alg.optimizer.load_state_dict(d["optimizer_state_dict"])
             self.alg.restore_learning_rate()
+            self.alg.invalidate_fused()  # the fused update re-reads the new optimizer state
         self.current_learning_iteration = d["iter"]
         return d.get("infos")
 
