@@ -102,6 +102,13 @@ int zbp_optimizer_step(const zbp_params* params, float* lr, const float* stats, 
                        float max_grad_norm, float beta1, float beta2, float eps, const zbp_net* actor,
                        const zbp_net* critic, float* ws, int32_t batch, void* stream);
 
+/* GAE (RolloutStorage.compute_returns): rewards / dones / values [steps][envs] (time-out bootstrap
+ * already in the rewards), last_values [envs] -> returns, advantages = returns - values, then (if
+ * normalize) advantages normalised by their mean and unbiased std (+1e-8). scratch: >= 258 floats. */
+int zbp_gae(const float* rewards, const float* dones, const float* values, const float* last_values, float* returns,
+            float* advantages, int32_t steps, int32_t envs, float gamma, float lam, int32_t normalize, float* scratch,
+            void* stream);
+
 const char* zbp_last_error(void);
 
 #ifdef __cplusplus

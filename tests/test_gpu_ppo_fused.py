@@ -122,3 +122,23 @@ def test_fused_update_matches_torch_update(gpu, monkeypatch):
     opt_f, opt_t = alg_f.optimizer, alg_t.optimizer
     for pf_, pt_ in zip(alg_f.policy.parameters(), alg_t.policy.parameters()):
         assert float(opt_f.state[pf_]["step"]) == float(opt_t.state[pt_]["step"]) == 20.0
+
+
+def test_fused_gae_matches_torch(gpu, monkeypatch):
+    """RolloutStorage.compute_returns on zbp_gae (three launches) against the torch recursion:
+    returns, advantages and their normalisation."""
+    import torch
+    alg = _alg([128, 128, 128], envs=4096, seed=5)
+    st = alg.storage
+    last = torch.randn(st.num_envs, 1, device="cuda:0")
+    monkeypatch.setenv("ZBOT_PPO_FUSED", "0")
+    st.compute_returns(last, 0.99, 0.95, True)
+    ret_t, adv_t = st.returns.clone(), st.advantages.clone()
+    monkeypatch.setenv("ZBOT_PPO_FUSED", "1")
+    st.returns.zero_()
+    st.advantages.zero_()
+    st.compute_returns(last, 0.99, 0.95, True)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(st.returns, ret_t, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(st.advantages, adv_t, rtol=1e-4, atol=1e-5)
+    assert abs(float(st.advantages.mean())) < 1e-5 and abs(float(st.advantages.std()) - 1.0) < 1e-4

@@ -87,10 +87,10 @@ Layout make_layout(const zbp_net* a, const zbp_net* c, int B) {
   lo.tile0[2 * MAXL] = t;
   lo.wtiles = t;
   lo.stats = take((int64_t)(B / TR) * NSTAT);
-  // row splits of the weight gradients: ~4 waves per SIMD over the chip, each split >= 256 rows
+  // row splits of the weight gradients (one workgroup of 4 waves per tile and split): ~2 workgroups
+  // per CU, each wave >= 128 rows, a multiple of 16 (k_wgrad's loop over pairs of row octets)
   int s = 1;
-  // (rows per split a multiple of 16: k_wgrad's 8-step unrolled loop over row pairs)
-  while (s < 64 && (int64_t)t * s * 2 <= 4096 && B / (s * 2) >= 256 && B % (16 * s * 2) == 0) s *= 2;
+  while (s < 64 && (int64_t)t * s * 2 <= 1024 && B / (s * 2 * 4) >= 128 && B % (16 * 4 * s * 2) == 0) s *= 2;
   lo.splits = s;
   lo.part = take((int64_t)s * t * PART);
   lo.scratch = take(64);
@@ -115,27 +115,34 @@ __device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
 
 // C[32 rows][32 cols] = sum_k A[r][k] B[k][c] over k < kp (kp a multiple of 32): A row-major in LDS
 // (row stride sa floats), B given as the 32 rows m[(c0 + c) * ldm + k] of a row-major global matrix
-// (the reduction index contiguous). Lane (c = lane & 31, h = lane >> 5) feeds A[c][.] / B[.][c] on
-// the reduction indices [h kp / 2, (h + 1) kp / 2) (the MFMA's k = 0 / 1 halves).
+// (the reduction index contiguous, L2-resident). Lane (c = lane & 31, h = lane >> 5) feeds
+// A[c][.] / B[.][c] on the reduction indices [h kp / 2, (h + 1) kp / 2) (the MFMA's k = 0 / 1
+// halves). The B stream runs 16 MFMAs (four float4) ahead of its use: one wave per SIMD has no
+// other wave to cover an L2 round trip.
 __device__ __forceinline__ f32x16 tile_mma(const float* __restrict__ a, int sa, const float* __restrict__ m, int ldm,
                                            int kp, int c0) {
   const int lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5, half = kp >> 1;
   const float* ar = a + c * sa + h * half;
-  const float* br = m + (int64_t)(c0 + c) * ldm + h * half;
+  const float4* br = reinterpret_cast<const float4*>(m + (int64_t)(c0 + c) * ldm + h * half);
+  const int nq = half >> 2;  // float4 steps (>= 4)
   f32x16 acc = {};
-  float4 bn = *reinterpret_cast<const float4*>(br);
-  for (int s = 0; s < half; s += 4) {
-    const float4 bv = bn;
-    if (s + 4 < half) bn = *reinterpret_cast<const float4*>(br + s + 4);
-    const float4 av = *reinterpret_cast<const float4*>(ar + s);
-    acc = mfma(av.x, bv.x, acc);
-    acc = mfma(av.y, bv.y, acc);
-    acc = mfma(av.z, bv.z, acc);
-    acc = mfma(av.w, bv.w, acc);
+  float4 b0 = br[0], b1 = br[1], b2 = br[2], b3 = br[3];
+  for (int q = 0; q < nq; q += 4) {
+    const float4 a0 = *reinterpret_cast<const float4*>(ar + 4 * q);
+    const float4 a1 = *reinterpret_cast<const float4*>(ar + 4 * q + 4);
+    const float4 a2 = *reinterpret_cast<const float4*>(ar + 4 * q + 8);
+    const float4 a3 = *reinterpret_cast<const float4*>(ar + 4 * q + 12);
+    const float4 u0 = b0, u1 = b1, u2 = b2, u3 = b3;
+    if (q + 4 < nq) { b0 = br[q + 4]; b1 = br[q + 5]; b2 = br[q + 6]; b3 = br[q + 7]; }
+    acc = mfma(a0.x, u0.x, acc); acc = mfma(a0.y, u0.y, acc); acc = mfma(a0.z, u0.z, acc); acc = mfma(a0.w, u0.w, acc);
+    acc = mfma(a1.x, u1.x, acc); acc = mfma(a1.y, u1.y, acc); acc = mfma(a1.z, u1.z, acc); acc = mfma(a1.w, u1.w, acc);
+    acc = mfma(a2.x, u2.x, acc); acc = mfma(a2.y, u2.y, acc); acc = mfma(a2.z, u2.z, acc); acc = mfma(a2.w, u2.w, acc);
+    acc = mfma(a3.x, u3.x, acc); acc = mfma(a3.y, u3.y, acc); acc = mfma(a3.z, u3.z, acc); acc = mfma(a3.w, u3.w, acc);
   }
   return acc;
 }
-// row / column of accumulator register r of a 32x32 MFMA tile in this lane
+// row / column of accumulator register r of a 32x32 MFMA tile in this lane: registers 4q .. 4q + 3
+// hold rows 8q + 4h .. 8q + 4h + 3 of column lane & 31
 __device__ __forceinline__ int acc_row(int r) { return (r & 3) + 8 * (r >> 2) + 4 * ((threadIdx.x & 63) >> 5); }
 __device__ __forceinline__ int acc_col() { return threadIdx.x & 31; }
 
@@ -164,6 +171,10 @@ __global__ void k_pack(PackArgs A) {
 }
 
 // ------------------------------------------------------------------------------- k_rows
+// Row buffers in HBM are feature-major (X_l [p(l)][B], dZ_l [p(l+1)][B]): a row tile writes whole
+// 128-byte lines (32 rows of one feature) as float4 quads of rows, and k_wgrad streams float4 quads
+// of rows per lane. In LDS the tile's activations are row-major [32][P + 4]; the backward pass
+// writes dZ_{l-1} over X_l in place (each element read once by the thread that overwrites it).
 struct RowArgs {
   NetW n[2];
   zbp_batch bt;
@@ -171,17 +182,18 @@ struct RowArgs {
   const float* std_param;
   float* ws;
   int64_t stats;
-  int lds_x[MAXL], lds_dz[2], lds_out, lds_red;  // LDS float offsets
+  int B;
+  int lds_x[MAXL], lds_dz, lds_out, lds_red;  // LDS float offsets
 };
 
 // forward through one net for the row tile; the output layer's pre-activations land in `out`
-// ([32][33]: row stride 33)
+// ([32][33])
 __device__ void net_forward(const RowArgs& A, const NetW& w, float* lds, int row0) {
-  const int wave = threadIdx.x >> 6;
+  const int wave = threadIdx.x >> 6, h = (threadIdx.x & 63) >> 5;
   for (int l = 0; l < w.L; ++l) {
     const int P0 = w.p[l], P1 = w.p[l + 1];
     const bool last = l == w.L - 1;
-    float* xs = lds + A.lds_x[l];
+    const float* xs = lds + A.lds_x[l];
     const float* wp = A.ws + w.wp[l];
     const float* bp = A.ws + w.bp[l];
     for (int t = wave; t < P1 / 32; t += 4) {
@@ -189,46 +201,54 @@ __device__ void net_forward(const RowArgs& A, const NetW& w, float* lds, int row
       const int n = 32 * t + acc_col();
       const float bias = bp[n];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int i = acc_row(r);
-        float v = acc[r] + bias;
-        if (last) {
-          lds[A.lds_out + i * 33 + n] = v;
-        } else {
-          v = v > 0.f ? v : expf(v) - 1.f;  // ELU(alpha = 1), as ATen's elu kernel
-          lds[A.lds_x[l + 1] + i * (P1 + 4) + n] = v;
-          A.ws[w.x[l + 1] + (int64_t)(row0 + i) * P1 + n] = v;
+      for (int q = 0; q < 4; ++q) {
+        float v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int i = 8 * q + 4 * h + u;
+          v[u] = acc[4 * q + u] + bias;
+          if (last) {
+            lds[A.lds_out + i * 33 + n] = v[u];
+          } else {
+            v[u] = v[u] > 0.f ? v[u] : expf(v[u]) - 1.f;  // ELU(alpha = 1), as ATen's elu kernel
+            lds[A.lds_x[l + 1] + i * (P1 + 4) + n] = v[u];
+          }
         }
+        if (!last)
+          *reinterpret_cast<float4*>(A.ws + w.x[l + 1] + (int64_t)n * A.B + row0 + 8 * q + 4 * h) =
+              make_float4(v[0], v[1], v[2], v[3]);
       }
     }
     __syncthreads();
   }
 }
 
-// backward through one net from dZ of the output layer (in lds_dz[0], row stride 36)
+// backward through one net from dZ of the output layer (lds_dz, [32][p(L) + 4])
 __device__ void net_backward(const RowArgs& A, const NetW& w, float* lds, int row0) {
-  const int wave = threadIdx.x >> 6;
-  int cur = 0;
+  const int wave = threadIdx.x >> 6, h = (threadIdx.x & 63) >> 5;
   for (int l = w.L - 1; l >= 1; --l) {
     const int P0 = w.p[l], P1 = w.p[l + 1];
-    const float* dz = lds + A.lds_dz[cur];
-    float* dzn = lds + A.lds_dz[cur ^ 1];
-    const float* xs = lds + A.lds_x[l];
+    const float* dz = lds + (l == w.L - 1 ? A.lds_dz : A.lds_x[l + 1]);
+    float* xs = lds + A.lds_x[l];  // X_l, overwritten by dZ_{l-1}
     const float* wt = A.ws + w.wt[l];
     for (int t = wave; t < P0 / 32; t += 4) {
       const f32x16 acc = tile_mma(dz, P1 + 4, wt, P1, P1, 32 * t);
       const int k = 32 * t + acc_col();
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int i = acc_row(r);
-        const float x = xs[i * (P0 + 4) + k];
-        const float g = acc[r] * (x > 0.f ? 1.f : x + 1.f);  // ELU'(z) = exp(z) = x + 1 for z <= 0
-        dzn[i * (P0 + 4) + k] = g;
-        A.ws[w.dz[l - 1] + (int64_t)(row0 + i) * P0 + k] = g;
+      for (int q = 0; q < 4; ++q) {
+        float g[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int i = 8 * q + 4 * h + u;
+          const float x = xs[i * (P0 + 4) + k];
+          g[u] = acc[4 * q + u] * (x > 0.f ? 1.f : x + 1.f);  // ELU'(z) = exp(z) = x + 1 for z <= 0
+          xs[i * (P0 + 4) + k] = g[u];
+        }
+        *reinterpret_cast<float4*>(A.ws + w.dz[l - 1] + (int64_t)k * A.B + row0 + 8 * q + 4 * h) =
+            make_float4(g[0], g[1], g[2], g[3]);
       }
     }
     __syncthreads();
-    cur ^= 1;
   }
 }
 
@@ -236,11 +256,11 @@ __device__ void net_backward(const RowArgs& A, const NetW& w, float* lds, int ro
 __device__ void gather_input(const RowArgs& A, const NetW& w, const float* src, int dim, float* lds, int row0) {
   const int P0 = w.p[0];
   for (int e = threadIdx.x; e < TR * P0; e += blockDim.x) {
-    const int i = e / P0, k = e % P0;
+    const int k = e / TR, i = e % TR;
     const int64_t row = A.bt.idx[A.bt.idx_offset + row0 + i];
     const float v = k < dim ? src[row * dim + k] : 0.f;
     lds[A.lds_x[0] + i * (P0 + 4) + k] = v;
-    A.ws[w.x[0] + (int64_t)(row0 + i) * P0 + k] = v;
+    A.ws[w.x[0] + (int64_t)k * A.B + row0 + i] = v;
   }
   __syncthreads();
 }
@@ -265,10 +285,8 @@ __global__ __launch_bounds__(256) void k_rows(RowArgs A) {
   gather_input(A, wa, bt.obs, bt.obs_dim, lds, row0);
   net_forward(A, wa, lds, row0);
   {
-    float* dz = lds + A.lds_dz[0];
+    float* dz = lds + A.lds_dz;
     const int Pout = wa.p[wa.L];
-    for (int e = tid; e < TR * Pout; e += blockDim.x) dz[(e / Pout) * (Pout + 4) + e % Pout] = 0.f;
-    __syncthreads();
     float surr = 0.f, kl = 0.f, sg[NSTAT - 3];
 #pragma unroll
     for (int a = 0; a < NSTAT - 3; ++a) sg[a] = 0.f;
@@ -294,19 +312,20 @@ __global__ __launch_bounds__(256) void k_rows(RowArgs A) {
       const float in = (ratio >= 1.f - clip && ratio <= 1.f + clip) ? 1.f : 0.f;
       const float w1 = s1 > s2 ? 1.f : (s1 < s2 ? 0.f : 0.5f);
       const float g = (w1 * -adv + (1.f - w1) * -adv * in) * ratio * invB;  // dL / dlog_prob
+      for (int a = 0; a < Pout; ++a) {
+        float d = 0.f;
+        if (a < NA) {
+          const float mu = lds[A.lds_out + i * 33 + a], s = A.std_param[a];
+          const float diff = bt.actions[row * NA + a] - mu;
+          d = g * diff / (s * s);
 #pragma unroll
-      for (int a = 0; a < NSTAT - 3; ++a) {
-        if (a >= NA) break;
-        const float mu = lds[A.lds_out + i * 33 + a], s = A.std_param[a];
-        const float diff = bt.actions[row * NA + a] - mu;
-        dz[i * (Pout + 4) + a] = g * diff / (s * s);
-        A.ws[wa.dz[wa.L - 1] + (int64_t)(row0 + i) * Pout + a] = g * diff / (s * s);
-        sg[a] = g * (diff * diff / (s * s * s) - 1.f / s);
+          for (int b = 0; b < NSTAT - 3; ++b)
+            if (b == a) sg[b] = g * (diff * diff / (s * s * s) - 1.f / s);
+        }
+        dz[i * (Pout + 4) + a] = d;
+        A.ws[wa.dz[wa.L - 1] + (int64_t)a * A.B + row0 + i] = d;
       }
     }
-    // the padding columns of the output dZ row buffer
-    for (int e = tid; e < TR * Pout; e += blockDim.x)
-      if (e % Pout >= NA) A.ws[wa.dz[wa.L - 1] + (int64_t)(row0 + e / Pout) * Pout + e % Pout] = 0.f;
     if (tid < 64) {
       surr = wave_sum(surr);
       kl = wave_sum(kl);
@@ -328,13 +347,8 @@ __global__ __launch_bounds__(256) void k_rows(RowArgs A) {
   gather_input(A, wc, bt.critic_obs, bt.critic_obs_dim, lds, row0);
   net_forward(A, wc, lds, row0);
   {
-    float* dz = lds + A.lds_dz[0];
+    float* dz = lds + A.lds_dz;
     const int Pout = wc.p[wc.L];
-    for (int e = tid; e < TR * Pout; e += blockDim.x) {
-      dz[(e / Pout) * (Pout + 4) + e % Pout] = 0.f;
-      if (e % Pout) A.ws[wc.dz[wc.L - 1] + (int64_t)(row0 + e / Pout) * Pout + e % Pout] = 0.f;
-    }
-    __syncthreads();
     float vl = 0.f;
     if (tid < TR) {
       const int i = tid;
@@ -354,8 +368,10 @@ __global__ __launch_bounds__(256) void k_rows(RowArgs A) {
         dv = 2.f * (v - ret);
       }
       dv *= A.lc.value_loss_coef * invB;
-      dz[i * (Pout + 4)] = dv;
-      A.ws[wc.dz[wc.L - 1] + (int64_t)(row0 + i) * Pout] = dv;
+      for (int a = 0; a < Pout; ++a) {
+        dz[i * (Pout + 4) + a] = a == 0 ? dv : 0.f;
+        A.ws[wc.dz[wc.L - 1] + (int64_t)a * A.B + row0 + i] = a == 0 ? dv : 0.f;
+      }
     }
     if (tid < 64) {
       vl = wave_sum(vl);
@@ -375,44 +391,43 @@ struct WgradArgs {
   float* ws;
   int64_t part;
 };
-// one wave: the 32x32 tile (n0, k0) of dW_l = dZ_l^T X_l over the rows of one split, and db_l
-// (the k0 = 0 tiles). A[n][r] = dZ[r][n0 + n], B[r][k] = X[r][k0 + k]; lane half h takes rows
-// r0 + 2 s + h.
+// One workgroup = one 32x32 tile (n0, k0) of dW_l = dZ_l^T X_l (+ db_l for k0 = 0) over the rows of
+// one split; its four waves take a quarter of the rows each and are summed in LDS. A[n][r] =
+// dZ_l[n0 + n][r], B[r][k] = X_l[k0 + k][r] (feature-major, float4 quads of rows: lane half h takes
+// rows 8 j + 4 h .. 8 j + 4 h + 3, one MFMA each).
 __global__ __launch_bounds__(256) void k_wgrad(WgradArgs A) {
-  const int item = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (item >= A.wtiles * A.splits) return;
-  const int tile = item % A.wtiles, split = item / A.wtiles;
+  __shared__ float red[4][PART];
+  const int tile = blockIdx.x % A.wtiles, split = blockIdx.x / A.wtiles;
   int nl = 0;
   while (nl + 1 < 2 * MAXL && A.tile0[nl + 1] <= tile) ++nl;
   const NetW& w = A.n[nl / MAXL];
   const int l = nl % MAXL;
-  const int P0 = w.p[l], P1 = w.p[l + 1];
+  const int P0 = w.p[l];
   const int t = tile - A.tile0[nl], kt = P0 / 32;
   const int n0 = 32 * (t / kt), k0 = 32 * (t % kt);
-  const int rows = A.batch / A.splits, r0 = split * rows;
-  const int lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
-  const float* dz = A.ws + w.dz[l] + (int64_t)(r0 + h) * P1 + n0 + c;
-  const float* x = A.ws + w.x[l] + (int64_t)(r0 + h) * P0 + k0 + c;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
+  const int rows = A.batch / (A.splits * 4), r0 = (split * 4 + wave) * rows;
+  const float4* dz = reinterpret_cast<const float4*>(A.ws + w.dz[l] + (int64_t)(n0 + c) * A.batch + r0 + 4 * h);
+  const float4* x = reinterpret_cast<const float4*>(A.ws + w.x[l] + (int64_t)(k0 + c) * A.batch + r0 + 4 * h);
+  const int nj = rows / 8;  // float4 steps (row octets)
   f32x16 acc = {};
   float bsum = 0.f;
-  for (int s = 0; s < rows / 2; s += 8) {
-    float av[8], bv[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      av[u] = dz[(int64_t)(2 * (s + u)) * P1];
-      bv[u] = x[(int64_t)(2 * (s + u)) * P0];
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      acc = mfma(av[u], bv[u], acc);
-      bsum += av[u];
-    }
+  float4 a0 = dz[0], a1 = dz[2], b0 = x[0], b1 = x[2];
+  for (int j = 0; j < nj; j += 2) {
+    const float4 u0 = a0, u1 = a1, v0 = b0, v1 = b1;
+    if (j + 2 < nj) { a0 = dz[2 * j + 4]; a1 = dz[2 * j + 6]; b0 = x[2 * j + 4]; b1 = x[2 * j + 6]; }
+    acc = mfma(u0.x, v0.x, acc); acc = mfma(u0.y, v0.y, acc); acc = mfma(u0.z, v0.z, acc); acc = mfma(u0.w, v0.w, acc);
+    acc = mfma(u1.x, v1.x, acc); acc = mfma(u1.y, v1.y, acc); acc = mfma(u1.z, v1.z, acc); acc = mfma(u1.w, v1.w, acc);
+    bsum += ((u0.x + u0.y) + (u0.z + u0.w)) + ((u1.x + u1.y) + (u1.z + u1.w));
   }
-  float* out = A.ws + A.part + ((int64_t)split * A.wtiles + tile) * PART;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) out[acc_row(r) * 32 + acc_col()] = acc[r];  // [n][k]
+  for (int r = 0; r < 16; ++r) red[wave][acc_row(r) * 32 + acc_col()] = acc[r];  // [n][k]
   bsum += __shfl_xor(bsum, 32);
-  if (k0 == 0 && h == 0) out[1024 + c] = bsum;
+  if (h == 0) red[wave][1024 + c] = bsum;
+  __syncthreads();
+  float* out = A.ws + A.part + ((int64_t)split * A.wtiles + tile) * PART;
+  for (int e = threadIdx.x; e < PART; e += blockDim.x)
+    out[e] = (red[0][e] + red[1][e]) + (red[2][e] + red[3][e]);
 }
 
 // ------------------------------------------------------------------------------- k_reduce
@@ -428,57 +443,54 @@ struct ReduceArgs {
   float entropy_coef;
   const float* ws;
   int64_t part, rstats;
-  int64_t total;  // parameter elements (weights + biases) of both nets
 };
+// one workgroup per weight tile: the split partials summed in order into .grad (weights of the tile,
+// and the bias for k0 = 0); the last workgroup: the scalars
 __global__ __launch_bounds__(256) void k_reduce(ReduceArgs A) {
-  const int64_t e0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (blockIdx.x == gridDim.x - 1) {
-    // the scalars: per-row-tile sums -> stats, the std gradient (+ the entropy bonus term)
-    __shared__ float acc[NSTAT];
-    if (threadIdx.x < NSTAT) {
-      float s = 0.f;
-      for (int t = 0; t < A.row_tiles; ++t) s += A.ws[A.rstats + (int64_t)t * NSTAT + threadIdx.x];
-      acc[threadIdx.x] = s;
-    }
+  if (blockIdx.x == (unsigned)A.wtiles) {
+    // per-row-tile sums -> stats, the std gradient (+ the entropy bonus term)
+    __shared__ float acc[NSTAT][17];
+    const int k = threadIdx.x & 15, part = threadIdx.x >> 4;  // 16 lanes per statistic
+    float s = 0.f;
+    for (int t = part; t < A.row_tiles; t += 16) s += A.ws[A.rstats + (int64_t)t * NSTAT + k];
+    acc[k][part] = s;
     __syncthreads();
     if (threadIdx.x == 0) {
+      float tot[NSTAT];
+      for (int q = 0; q < NSTAT; ++q) {
+        float v = 0.f;
+        for (int p = 0; p < 16; ++p) v += acc[q][p];
+        tot[q] = v;
+      }
       const float invB = 1.f / (float)A.batch;
       float ent = 0.f;
       for (int a = 0; a < A.num_actions; ++a) ent += 0.5f + 0.91893853320467274178f + logf(A.std_param[a]);
-      A.stats[0] = acc[2] * invB;  // kl mean
-      A.stats[1] = acc[1] * invB;  // value loss
-      A.stats[2] = acc[0] * invB;  // surrogate loss
+      A.stats[0] = tot[2] * invB;  // kl mean
+      A.stats[1] = tot[1] * invB;  // value loss
+      A.stats[2] = tot[0] * invB;  // surrogate loss
       A.stats[3] = ent;            // entropy (every row's)
-      for (int a = 0; a < A.num_actions; ++a) A.std_grad[a] = acc[3 + a] - A.entropy_coef / A.std_param[a];
+      for (int a = 0; a < A.num_actions; ++a) A.std_grad[a] = tot[3 + a] - A.entropy_coef / A.std_param[a];
     }
     return;
   }
-  for (int64_t e = e0; e < A.total; e += (int64_t)(gridDim.x - 1) * blockDim.x) {
-    // locate (net, layer, weight or bias, n, k)
-    int64_t r = e;
-    int net = 0, l = 0;
-    bool bias = false;
-    int n = 0, k = 0;
-    for (net = 0; net < 2; ++net) {
-      const NetW& w = A.n[net];
-      bool found = false;
-      for (l = 0; l < w.L; ++l) {
-        const int64_t nw = (int64_t)w.d[l + 1] * w.d[l];
-        if (r < nw) { n = (int)(r / w.d[l]); k = (int)(r % w.d[l]); found = true; break; }
-        r -= nw;
-        if (r < w.d[l + 1]) { n = (int)r; bias = true; found = true; break; }
-        r -= w.d[l + 1];
-      }
-      if (found) break;
-    }
-    const NetW& w = A.n[net];
-    const int kt = w.p[l] / 32;
-    const int tile = A.tile0[net * MAXL + l] + (n / 32) * kt + (bias ? 0 : k / 32);
-    const int idx = bias ? 1024 + n % 32 : (n % 32) * 32 + k % 32;
+  const int tile = blockIdx.x;
+  int nl = 0;
+  while (nl + 1 < 2 * MAXL && A.tile0[nl + 1] <= tile) ++nl;
+  const int net = nl / MAXL, l = nl % MAXL;
+  const NetW& w = A.n[net];
+  const int t = tile - A.tile0[nl], kt = w.p[l] / 32;
+  const int n0 = 32 * (t / kt), k0 = 32 * (t % kt);
+  const int D0 = w.d[l], D1 = w.d[l + 1];
+  for (int e = threadIdx.x; e < PART; e += blockDim.x) {
     float s = 0.f;
-    for (int sp = 0; sp < A.splits; ++sp) s += A.ws[A.part + ((int64_t)sp * A.wtiles + tile) * PART + idx];
-    if (bias) A.gb[net][l][n] = s;
-    else A.gw[net][l][(int64_t)n * w.d[l] + k] = s;
+    for (int sp = 0; sp < A.splits; ++sp) s += A.ws[A.part + ((int64_t)sp * A.wtiles + tile) * PART + e];
+    if (e < 1024) {
+      const int n = n0 + e / 32, k = k0 + e % 32;
+      if (n < D1 && k < D0) A.gw[net][l][(int64_t)n * D0 + k] = s;
+    } else if (k0 == 0) {
+      const int n = n0 + e - 1024;
+      if (n < D1) A.gb[net][l][n] = s;
+    }
   }
 }
 
@@ -492,7 +504,7 @@ struct OptimArgs {
   float* norm2;  // workspace scratch: [64] per-block sums of squares (k_norm), summed in order by k_adam
 };
 __global__ __launch_bounds__(256) void k_norm(OptimArgs A) {
-  // global gradient norm^2 over every tensor (one block per tensor slice, atomics into norm2)
+  // global gradient norm^2: per-block partial sums in a fixed order (deterministic)
   __shared__ float red[4];
   float s = 0.f;
   for (int t = 0; t < A.P.n_params; ++t)
@@ -546,6 +558,70 @@ __global__ void k_optim_tail(OptimArgs A) {
   A.acc[0] += A.stats[1];
   A.acc[1] += A.stats[2];
   A.acc[2] += A.stats[3];
+}
+
+// ------------------------------------------------------------------------------- GAE
+// RolloutStorage.compute_returns (zbot_lab_amd/rl/ppo.py; rsl_rl GAE with time-out bootstrapping
+// already folded into the rewards): one thread per env runs the backward recursion over T steps;
+// advantages = returns - values, then normalised by the mean and the unbiased std over all T x N.
+// Partial sums per block in a fixed order (deterministic).
+constexpr int GAE_BLOCKS = 256;
+__global__ __launch_bounds__(256) void k_gae(const float* __restrict__ rew, const float* __restrict__ done,
+                                             const float* __restrict__ val, const float* __restrict__ last,
+                                             float* __restrict__ ret, float* __restrict__ adv, int T, int N, float gamma,
+                                             float lam, float* __restrict__ part) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int n = blockIdx.x * blockDim.x + threadIdx.x; n < N; n += gridDim.x * blockDim.x) {
+    float a = 0.f, next = last[n];
+    for (int k = T - 1; k >= 0; --k) {
+      const int64_t e = (int64_t)k * N + n;
+      const float v = val[e], nt = 1.f - done[e];
+      const float delta = rew[e] + nt * gamma * next - v;
+      a = delta + nt * gamma * lam * a;
+      const float r = a + v;
+      ret[e] = r;
+      const float d = r - v;
+      adv[e] = d;
+      s += d;
+      next = v;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+// one block: the mean, then the unbiased variance around it -> part[GAE_BLOCKS .. +2] = {mean, 1/(std + 1e-8)}
+__global__ __launch_bounds__(1024) void k_adv_stats(const float* __restrict__ adv, int64_t M, float* __restrict__ part) {
+  __shared__ float red[16];
+  __shared__ float mean_s;
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int b = 0; b < GAE_BLOCKS; ++b) t += part[b];
+    mean_s = t / (float)M;
+  }
+  __syncthreads();
+  const float mean = mean_s;
+  float q = 0.f;
+  for (int64_t e = threadIdx.x; e < M; e += blockDim.x) {
+    const float d = adv[e] - mean;
+    q += d * d;
+  }
+  for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = q;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += red[w];
+    part[GAE_BLOCKS] = mean;
+    part[GAE_BLOCKS + 1] = 1.f / (sqrtf(t / (float)(M - 1)) + 1e-8f);
+  }
+}
+__global__ __launch_bounds__(256) void k_adv_norm(float* __restrict__ adv, int64_t M, const float* __restrict__ part) {
+  const float mean = part[GAE_BLOCKS], inv = part[GAE_BLOCKS + 1];
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < M; e += (int64_t)gridDim.x * blockDim.x)
+    adv[e] = (adv[e] - mean) * inv;
 }
 
 int launch_check(const char* what) {
@@ -614,18 +690,15 @@ int zbp_minibatch(const zbp_net* actor, const zbp_net* critic, const float* std_
   R.std_param = std_param;
   R.ws = ws;
   R.stats = lo.stats;
-  int off = 0, pmax = 0;
+  R.B = B;
+  int off = 0;
   for (int l = 0; l < MAXL; ++l) {
     const int p = lo.n[0].p[l] > lo.n[1].p[l] ? lo.n[0].p[l] : lo.n[1].p[l];
     R.lds_x[l] = off;
     off += TR * (p + 4);
   }
-  for (int k = 0; k < 2; ++k)
-    for (int l = 0; l <= MAXL; ++l) pmax = lo.n[k].p[l] > pmax ? lo.n[k].p[l] : pmax;
-  R.lds_dz[0] = off;
-  off += TR * (pmax + 4);
-  R.lds_dz[1] = off;
-  off += TR * (pmax + 4);
+  R.lds_dz = off;  // the output layer's dZ ([32][p(L) + 4], p(L) = 32)
+  off += TR * (32 + 4);
   R.lds_out = off;
   off += TR * 33;
   R.lds_red = off;
@@ -650,8 +723,7 @@ int zbp_minibatch(const zbp_net* actor, const zbp_net* critic, const float* std_
   W.batch = B;
   W.ws = ws;
   W.part = lo.part;
-  const int items = lo.wtiles * lo.splits;
-  k_wgrad<<<(items + 3) / 4, 256, 0, s>>>(W);
+  k_wgrad<<<lo.wtiles * lo.splits, 256, 0, s>>>(W);
   if (int rc = launch_check("k_wgrad")) return rc;
 
   ReduceArgs D{};
@@ -663,16 +735,13 @@ int zbp_minibatch(const zbp_net* actor, const zbp_net* critic, const float* std_
   D.row_tiles = B / TR;
   D.batch = B;
   D.num_actions = batch->num_actions;
-  int64_t total = 0;
   for (int k = 0; k < 2; ++k) {
     const zbp_net* n = k ? critic : actor;
     for (int l = 0; l < n->n_layers; ++l) {
       D.gw[k][l] = n->gw[l];
       D.gb[k][l] = n->gb[l];
-      total += (int64_t)n->dim[l + 1] * n->dim[l] + n->dim[l + 1];
     }
   }
-  D.total = total;
   D.std_param = std_param;
   D.std_grad = std_grad;
   D.stats = stats;
@@ -680,8 +749,7 @@ int zbp_minibatch(const zbp_net* actor, const zbp_net* critic, const float* std_
   D.ws = ws;
   D.part = lo.part;
   D.rstats = lo.stats;
-  const int blocks = (int)((total + 255) / 256 < 512 ? (total + 255) / 256 : 512) + 1;
-  k_reduce<<<blocks, 256, 0, s>>>(D);
+  k_reduce<<<lo.wtiles + 1, 256, 0, s>>>(D);
   return launch_check("k_reduce");
 }
 
@@ -707,11 +775,28 @@ int zbp_optimizer_step(const zbp_params* params, float* lr, const float* stats, 
   O.norm2 = ws + lo.scratch;
   k_norm<<<64, 256, 0, s>>>(O);
   if (int rc = launch_check("k_norm")) return rc;
-  k_adam<<<64, 256, 0, s>>>(O);
+  k_adam<<<256, 256, 0, s>>>(O);
   if (int rc = launch_check("k_adam")) return rc;
   k_optim_tail<<<1, 64, 0, s>>>(O);
   if (int rc = launch_check("k_optim_tail")) return rc;
   return do_pack(lo, actor, critic, ws, s);
+}
+
+int zbp_gae(const float* rewards, const float* dones, const float* values, const float* last_values, float* returns,
+            float* advantages, int32_t steps, int32_t envs, float gamma, float lam, int32_t normalize, float* scratch,
+            void* stream) {
+  if (!rewards || !dones || !values || !last_values || !returns || !advantages || !scratch || steps < 1 || envs < 1)
+    return fail(-1, "zbp_gae: bad argument");
+  hipStream_t s = (hipStream_t)stream;
+  k_gae<<<GAE_BLOCKS, 256, 0, s>>>(rewards, dones, values, last_values, returns, advantages, steps, envs, gamma, lam,
+                                   scratch);
+  if (int rc = launch_check("k_gae")) return rc;
+  if (!normalize) return 0;
+  const int64_t M = (int64_t)steps * envs;
+  k_adv_stats<<<1, 1024, 0, s>>>(advantages, M, scratch);
+  if (int rc = launch_check("k_adv_stats")) return rc;
+  k_adv_norm<<<256, 256, 0, s>>>(advantages, M, scratch);
+  return launch_check("k_adv_norm");
 }
 
 }  // extern "C"

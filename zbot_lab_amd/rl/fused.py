@@ -49,7 +49,7 @@ class Params(C.Structure):
                 ("step", C.c_void_p * MAXP)]
 
 
-EXPORTED = ["zbp_workspace_floats", "zbp_pack", "zbp_minibatch", "zbp_optimizer_step", "zbp_last_error"]
+EXPORTED = ["zbp_workspace_floats", "zbp_pack", "zbp_minibatch", "zbp_optimizer_step", "zbp_gae", "zbp_last_error"]
 _lib = None
 
 
@@ -69,7 +69,8 @@ def lib():
     L.zbp_minibatch.argtypes = [C.POINTER(Net), C.POINTER(Net), P, P, C.POINTER(Batch), C.POINTER(LossCfg), P, P, P]
     L.zbp_optimizer_step.argtypes = [C.POINTER(Params), P, P, P, C.c_float, C.c_float, C.c_float, C.c_float,
                                      C.c_float, C.POINTER(Net), C.POINTER(Net), P, C.c_int32, P]
-    for n in ("zbp_pack", "zbp_minibatch", "zbp_optimizer_step"):
+    L.zbp_gae.argtypes = [P, P, P, P, P, P, C.c_int32, C.c_int32, C.c_float, C.c_float, C.c_int32, P, P]
+    for n in ("zbp_pack", "zbp_minibatch", "zbp_optimizer_step", "zbp_gae"):
         getattr(L, n).restype = C.c_int
     _lib = L
     return L
@@ -87,6 +88,19 @@ def _p(t: torch.Tensor | None):
     if not t.is_contiguous():
         raise ZbotError("tensor passed to libzbot_ppo must be contiguous")
     return C.c_void_p(t.data_ptr())
+
+
+def gae(storage, last_values: torch.Tensor, gamma: float, lam: float, normalize: bool) -> None:
+    """RolloutStorage.compute_returns in three launches (zbp_gae): returns, advantages and their
+    normalisation, in place in the storage."""
+    sc = getattr(storage, "_gae_scratch", None)
+    if sc is None:
+        sc = storage._gae_scratch = torch.zeros(512, device=storage.values.device)
+    lv = last_values.reshape(-1).contiguous()
+    _check(lib().zbp_gae(_p(storage.rewards), _p(storage.dones), _p(storage.values), _p(lv), _p(storage.returns),
+                         _p(storage.advantages), storage.num_transitions_per_env, storage.num_envs, float(gamma),
+                         float(lam), int(normalize), _p(sc), C.c_void_p(torch.cuda.current_stream(sc.device).cuda_stream)),
+           "zbp_gae")
 
 
 def mlp_layers(seq: nn.Sequential):
