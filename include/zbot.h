@@ -317,6 +317,11 @@ typedef struct zb_task_cfg {
    * re-linearised from the separation advanced by the normal velocities of the previous ones, the
    * pose integrated with the mean of the sub-iteration velocities */
   int32_t solver_mode;
+  /* self-contact manifold (PhysX PCM keeps up to 4 points per convex pair; zbot_cfg.py:636
+   * enabled_self_collisions): 1 = a pair whose two nearest features are disk faces (cap on cap)
+   * contributes up to 4 points (rim points of either face inside the other), every
+   * other pair its one GJK point; 0 = one point per pair */
+  int32_t self_manifold;
 } zb_task_cfg;
 
 typedef struct zb_sim* zb_handle;

@@ -49,8 +49,10 @@ def _load(double: bool = False):
     lib.zbo_contact_diag.argtypes = [P, _f]
     lib.zbo_hull_pair.argtypes = [_f, _f, C.c_float, _f]
     lib.zbo_hull_pair_from.argtypes = [_f, _f, C.c_float, C.c_void_p, _f]
+    lib.zbo_pair_manifold.argtypes = [_f, _f, C.c_float, _f]
     lib.zbo_gjk_pairs.argtypes = [_f, C.c_void_p, C.c_int, C.c_float, _f, C.c_void_p]
     lib.zbo_set_gjk_tol.argtypes = [C.c_double]
+    lib.zbo_set_face_cos.argtypes = [C.c_double]
     lib.zbo_set_sensor_force_scale.argtypes = [C.c_double]
     lib.zbo_set_plant.argtypes = [C.c_int]
     lib.zbo_contact_activity.argtypes = [P, _i, C.c_int]

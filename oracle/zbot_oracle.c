@@ -394,6 +394,9 @@ static void wc_store(const clist_t* wl, float* wc) {
   wc_invalidate(wc);
   for (int j = 0; j < wl->n && r < ZB_WARM_SLOTS; ++j) {
     if (wl->c[j].lb < 0) continue;
+    int dup = 0; /* a manifold's points share the pair's normal: one entry per pair */
+    for (int i = 0; i < j; ++i) dup |= wl->c[i].la == wl->c[j].la && wl->c[i].lb == wl->c[j].lb;
+    if (dup) continue;
     for (int a = 0; a < 3; ++a) wc[4 * r + a] = (float)wl->c[j].n[a];
     wc[4 * r + 3] = (float)((wl->c[j].la << 4) + wl->c[j].lb + 1);
     ++r;
@@ -638,6 +641,107 @@ static int hull_pair(const hull_t* A, const hull_t* B, real margin, real early_m
   return out->sep < margin;
 }
 
+/* Self-contact manifold (cfg->self_manifold; PhysX PCM keeps up to 4 points per convex pair): when
+ * the nearest features of the two core hulls along the pair normal n (B -> A) are both disk faces --
+ * a core circle whose plane normal is within FACE_COS of the direction (A: -n, B: +n) and that
+ * supports its hull along it -- the pair contributes the corners of the faces' overlap: rim points
+ * of B's core face (angles from the in-plane direction toward A's face centre: all four quarter
+ * points if B's disk lies inside A's, else the tip and the two rim crossings of a lens) carried
+ * along +n to A's face plane, kept if the foot lies inside A's core disk and the core gap minus
+ * 2 CORE_M is within the margin; then A's rim the same way toward B (along -n). The first 4 kept
+ * in that order are the manifold {x = midpoint, n, sep} (a lens: B's tip, its two crossings, A's
+ * tip); none kept (or the faces not both present): the GJK contact alone. (The kernel runs the same statement on the 4 lanes of
+ * the pair's quad: face_manifold in zbot_sim.hip.) */
+#define FACE_COS 0.9659258262890683 /* cos 15 deg */
+#define FACE_INSET_C 0.9995500337489875 /* cos / sin of 0.03 rad: the lens crossings moved inside */
+#define FACE_INSET_S 0.029995500202495664
+static double g_face_cos = FACE_COS; /* test hook (zbo_set_face_cos): the parity tests move the threshold */
+static int hull_face(const hull_t* H, const real d[3], real u[3]) {
+  real sv[2], uu[2][3], al[2];
+  for (int ci = 0; ci < 2; ++ci) {
+    const real* c = H->c[ci];
+    v3_cross(c + 3, c + 6, uu[ci]);
+    const real iu = 1 / sqrtr(v3_dot(uu[ci], uu[ci]));
+    for (int a = 0; a < 3; ++a) uu[ci][a] *= iu;
+    al[ci] = v3_dot(uu[ci], d);
+    const real r = sqrtr(v3_dot(c + 3, c + 3));
+    const real s2 = 1 - al[ci] * al[ci];
+    sv[ci] = v3_dot(c, d) + r * sqrtr(s2 > 0 ? s2 : 0);
+  }
+  const int f = sv[1] > sv[0] ? 1 : 0; /* the supporting circle (circle 0 on a tie) */
+  if (fabs((double)al[f]) < g_face_cos) return -1;
+  const real sg = al[f] < 0 ? (real)-1 : (real)1; /* oriented along d */
+  for (int a = 0; a < 3; ++a) u[a] = sg * uu[f][a];
+  return f;
+}
+static int face_manifold(const hull_t* A, const hull_t* B, const contact_t* c0, real margin, contact_t out[4]) {
+  const real nA[3] = {-c0->n[0], -c0->n[1], -c0->n[2]};
+  real ua[3], ub[3];
+  const int fa = hull_face(A, nA, ua), fb = hull_face(B, c0->n, ub);
+  if (fa < 0 || fb < 0) return 0;
+  int k = 0;
+  for (int side = 0; side < 2 && k < 4; ++side) {
+    /* side 0: B's rim onto A's face along +n; side 1: A's rim onto B's face along -n */
+    const real* cs = side == 0 ? B->c[fb] : A->c[fa];
+    const real* us = side == 0 ? ub : ua;
+    const real* ct = side == 0 ? A->c[fa] : B->c[fb];
+    const real* ut = side == 0 ? ua : ub;
+    const real sg = side == 0 ? (real)1 : (real)-1;
+    const real rs = sqrtr(v3_dot(cs + 3, cs + 3)), rt = sqrtr(v3_dot(ct + 3, ct + 3));
+    /* rim angles: measured from d0, the in-plane direction toward the other face's centre at
+     * in-plane distance d. This rim inside the other disk: 0 / 90 / 180 / 270 deg; the other disk
+     * inside this one: none; a lens: the tip (0) and the two rim crossings (+-alpha) moved
+     * FACE_INSET rad toward the tip; apart: the tip only. Samples as (cos, sin) pairs. */
+    real d0[3], d1[3];
+    for (int a = 0; a < 3; ++a) d0[a] = ct[a] - cs[a];
+    const real du = v3_dot(d0, us);
+    for (int a = 0; a < 3; ++a) d0[a] -= du * us[a];
+    const real d = sqrtr(v3_dot(d0, d0));
+    if (d < (real)1e-9) { /* concentric faces: a fixed in-plane axis */
+      const real ax[3] = {fabs((double)us[0]) < 0.9 ? 1 : 0, fabs((double)us[0]) < 0.9 ? 0 : 1, 0};
+      const real au = v3_dot(ax, us);
+      for (int a = 0; a < 3; ++a) d0[a] = ax[a] - au * us[a];
+      const real id0 = 1 / sqrtr(v3_dot(d0, d0));
+      for (int a = 0; a < 3; ++a) d0[a] *= id0;
+    } else {
+      for (int a = 0; a < 3; ++a) d0[a] /= d;
+    }
+    v3_cross(us, d0, d1);
+    real cs_[4], sn_[4];
+    int na = 0;
+    if (d + rs <= rt) {
+      cs_[0] = 1; sn_[0] = 0; cs_[1] = 0; sn_[1] = 1; cs_[2] = -1; sn_[2] = 0; cs_[3] = 0; sn_[3] = -1; na = 4;
+    } else if (d + rt > rs) {
+      cs_[0] = 1; sn_[0] = 0; na = 1;
+      if (d < rs + rt) {
+        const real ca = clampr((d * d + rs * rs - rt * rt) / (2 * d * rs), -1, 1);
+        const real sa = sqrtr(1 - ca * ca);
+        const real ci = (real)FACE_INSET_C, si = (real)FACE_INSET_S; /* rotate by -FACE_INSET */
+        cs_[1] = ca * ci + sa * si; sn_[1] = sa * ci - ca * si;
+        cs_[2] = cs_[1]; sn_[2] = -sn_[1];
+        na = 3;
+      }
+    }
+    const real den = sg * v3_dot(c0->n, ut);
+    if (fabs((double)den) < 1e-6) continue;
+    for (int r = 0; r < na && k < 4; ++r) {
+      const real cr = cs_[r], sr = sn_[r];
+      real p[3], q[3], w[3];
+      for (int a = 0; a < 3; ++a) p[a] = cs[a] + rs * (cr * d0[a] + sr * d1[a]);
+      for (int a = 0; a < 3; ++a) w[a] = ct[a] - p[a];
+      const real t = v3_dot(w, ut) / den; /* p + t sg n lies on the target face plane */
+      for (int a = 0; a < 3; ++a) q[a] = p[a] + t * sg * c0->n[a] - ct[a];
+      if (v3_dot(q, q) > rt * rt) continue;
+      const real sep = t - 2 * (real)CORE_M;
+      if (!(sep < margin)) continue;
+      contact_t* o = &out[k++];
+      o->la = c0->la; o->lb = c0->lb; o->sep = sep;
+      for (int a = 0; a < 3; ++a) { o->n[a] = c0->n[a]; o->x[a] = p[a] + (real)0.5 * t * sg * c0->n[a]; }
+    }
+  }
+  return k;
+}
+
 /* GJK stopping tolerance (test hook: the parity tests re-run the oracle at other tolerances to tell
  * an env whose result depends on where GJK stops - an algorithmic discontinuity like the contact
  * margin - from a real mismatch) */
@@ -652,6 +756,13 @@ int zbo_set_sensor_force_scale(double s) {
 
 int zbo_set_plant(int mode) {
   g_plant = mode;
+  return 0;
+}
+
+/* the face-alignment threshold of the self-contact manifold (test hook; 0 = the default): where a
+ * pair switches between one point and a face manifold is a discontinuity like the contact margin */
+int zbo_set_face_cos(double c) {
+  g_face_cos = c > 0 ? c : FACE_COS;
   return 0;
 }
 
@@ -741,6 +852,23 @@ int zbo_hull_pair_from(const float* a, const float* b, float margin, const float
   for (int q = 0; q < 3; ++q) { out[2 + q] = (float)c.n[q]; out[5 + q] = (float)c.x[q]; }
   return g_gjk_last_it; /* support iterations (GJK probe) */
 }
+/* test entry: hull_pair + face_manifold on two world-frame core hulls; out [4][7] = {sep, n[3], x[3]}
+ * per point; returns the number of points (0: no contact, 1: the GJK contact alone) */
+int zbo_pair_manifold(const float* a, const float* b, float margin, float* out) {
+  hull_t A, B;
+  for (int ci = 0; ci < 2; ++ci)
+    for (int q = 0; q < 9; ++q) { A.c[ci][q] = a[9 * ci + q]; B.c[ci][q] = b[9 * ci + q]; }
+  contact_t c, mf[4];
+  memset(&c, 0, sizeof(c));
+  if (!hull_pair(&A, &B, (real)margin, (real)margin, NULL, &c)) return 0;
+  int k = c.sep > -2 * (real)CORE_M + (real)1e-7 ? face_manifold(&A, &B, &c, (real)margin, mf) : 0;
+  if (k == 0) { mf[0] = c; k = 1; }
+  for (int j = 0; j < k; ++j) {
+    out[7 * j] = (float)mf[j].sep;
+    for (int q = 0; q < 3; ++q) { out[7 * j + 1 + q] = (float)mf[j].n[q]; out[7 * j + 4 + q] = (float)mf[j].x[q]; }
+  }
+  return k;
+}
 int zbo_hull_pair(const float* a, const float* b, float margin, float* out) {
   return zbo_hull_pair_from(a, b, margin, NULL, out);
 }
@@ -826,8 +954,17 @@ static void detect(const mdl_t* m, const zb_task_cfg* cfg, const kin_t* k, real 
       if (g_gjk_probe) __atomic_fetch_add(&g_gjk_hist[g_gjk_last_it], 1, __ATOMIC_RELAXED);
       if (hit) {
         c.la = la; c.lb = lb;
-        L->c[L->n++] = c;
-        ++nself;
+        contact_t mf[4];
+        const int k = cfg->self_manifold && c.sep > -2 * (real)CORE_M + (real)1e-7 ? face_manifold(&A, &B, &c, margin, mf)
+                                                                                 : 0;
+        if (k == 0) {
+          L->c[L->n++] = c;
+          ++nself;
+        }
+        for (int j = 0; j < k && nself < NSELF_MAX; ++j) {
+          L->c[L->n++] = mf[j];
+          ++nself;
+        }
       }
     }
     if (g_gjk_probe) __atomic_fetch_add(&g_gjk_uhist[nund < 63 ? nund : 63], 1, __ATOMIC_RELAXED);

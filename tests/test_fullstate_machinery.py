@@ -27,7 +27,7 @@ def _device_f64(task, n, seed, st, actions):
 @pytest.mark.parametrize("task", TASKS)
 def test_f64_oracle_passes_full_state_check(oracle_lib, task):
     from oracle.pyoracle import OracleSim
-    n, seed = 256, 17
+    n, seed = 512, 17  # (the 2 % outlier bound over 512 envs: a one-env fluctuation is not a failure)
     st = random_states(task, OracleSim(n, task_cfg(task), seed=seed), n, seed=101)
     a = np.random.default_rng(7).normal(size=(n, 6)).astype(np.float32)
     out, sg = _device_f64(task, n, seed, st, [a])

@@ -60,7 +60,7 @@ def _run_oracle(task, n, seed, st, actions, rng=None, scale=1.0, wc=None, double
 
 
 # the perturbed-oracle runs, by family (the explained-outlier envelope, tests/fullstate.py)
-SENS_FAMILIES = ("1e-6", "1e-5", "1e-4", "gjk_tol", "sensor_force")
+SENS_FAMILIES = ("1e-6", "1e-5", "1e-4", "gjk_tol", "face_cos", "sensor_force")
 
 
 def _sensitivity(task, n, seed, st, actions, so, obs_o, rew_o, fl_o, before, nsteps, wc=None):
@@ -75,6 +75,9 @@ def _sensitivity(task, n, seed, st, actions, so, obs_o, rew_o, fl_o, before, nst
     * "gjk_tol": GJK's stopping tolerance scaled by 1/4, 1/2, 2 and 4 (where GJK stops is a
       discontinuity of the self-contact normal, as the margin is of contact activation; the fp32
       kernel and oracle can stop one iteration apart).
+    * "face_cos": the self-contact manifold's face-alignment threshold (15 degrees) moved by -+ 0.5
+      degree: where a pair switches between one point and a face manifold is a discontinuity of the
+      contact set (oracle zbo_set_face_cos).
     * "sensor_force": the sensors see the contact forces scaled by 1 -+ 7 % (the force comparison
       tolerance, 0.05 N + 2 %, at the 1 N is_contact threshold): an env whose air / contact timers,
       touchdown latch, undesired-contact death or force-flagged reward terms flip there sits at a
@@ -85,15 +88,18 @@ def _sensitivity(task, n, seed, st, actions, so, obs_o, rew_o, fl_o, before, nst
     fam = {f: np.zeros(n) for f in SENS_FAMILIES}
     scales = [(1.0, "1e-6")] * (K_SENS // 2) + [(10.0, "1e-5")] * (K_SENS // 4) \
         + [(100.0, "1e-4")] * (K_SENS - K_SENS // 2 - K_SENS // 4)
-    runs = [(rng, None, None, sc, f) for sc, f in scales]
-    runs += [(None, t, None, 1.0, "gjk_tol") for t in (0.25e-5, 0.5e-5, 2e-5, 4e-5)]
-    runs += [(None, None, s, 1.0, "sensor_force") for s in (0.93, 1.07)]
+    runs = [(rng, None, None, sc, f, None) for sc, f in scales]
+    runs += [(None, t, None, 1.0, "gjk_tol", None) for t in (0.25e-5, 0.5e-5, 2e-5, 4e-5)]
+    runs += [(None, None, None, 1.0, "face_cos", c) for c in (np.cos(np.radians(14.5)), np.cos(np.radians(15.5)))]
+    runs += [(None, None, s, 1.0, "sensor_force", None) for s in (0.93, 1.07)]
     force_rows = row_groups(task)["force"]
-    for r_, tol, fs, scale, f in runs:
+    for r_, tol, fs, scale, f, fc in runs:
         if tol is not None:
             lib().zbo_set_gjk_tol(tol)
         if fs is not None:
             lib().zbo_set_sensor_force_scale(fs)
+        if fc is not None:
+            lib().zbo_set_face_cos(float(fc))
         try:
             sk, outs = _run_oracle(task, n, seed, st, actions, r_, scale, wc)
         finally:
@@ -101,6 +107,8 @@ def _sensitivity(task, n, seed, st, actions, so, obs_o, rew_o, fl_o, before, nst
                 lib().zbo_set_gjk_tol(0.0)
             if fs is not None:
                 lib().zbo_set_sensor_force_scale(1.0)
+            if fc is not None:
+                lib().zbo_set_face_cos(0.0)
         ob, rw, te, tr = outs[-1]
         r, rows, *_ = compare(task, sk, so, ob, obs_o, rw, rew_o, (te, tr), fl_o, before, nsteps)
         if fs is not None:

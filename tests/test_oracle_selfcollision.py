@@ -197,3 +197,120 @@ def test_overlapping_cores_penetration_estimate(link_cores):
         res.append(d_sat / d_ref)
     r = np.asarray(res)
     assert np.median(r) < 1.2 and (r < 1.5).mean() > 0.75, r
+
+
+def pair_manifold(ha, hb, margin):
+    out = np.zeros((4, 7), np.float32)
+    k = pyoracle.lib().zbo_pair_manifold(np.ascontiguousarray(ha, np.float32).ravel(),
+                                          np.ascontiguousarray(hb, np.float32).ravel(), margin, out.ravel())
+    return out[:k]
+
+
+def _flat_link(r0, r1=None):
+    """Two parallel circles 5.3 cm apart (a flat stack), radii r0 (face at z = 0) and r1 (top)."""
+    r1 = r0 if r1 is None else r1
+    circ = np.zeros((2, 9))
+    circ[0, 3:6] = [r0, 0, 0]; circ[0, 6:9] = [0, r0, 0]
+    circ[1, :3] = [0, 0, 0.053]; circ[1, 3:6] = [r1, 0, 0]; circ[1, 6:9] = [0, r1, 0]
+    return core_circles(circ)
+
+
+def _check_manifold_geometry(ha, hb, pts, margin):
+    """Every manifold point: normal = the pair normal, x the midpoint of a core-rim point of one face
+    and its foot on the other face's plane along n, the foot inside that face's core disk, sep the
+    core gap along n minus 2 CORE_M, within the margin."""
+    for p in pts:
+        sep, n, x = p[0], p[1:4], p[4:7]
+        assert abs(np.linalg.norm(n) - 1) < 1e-5 and sep < margin
+        xa, xb = x + n * (sep / 2 + CORE_M), x - n * (sep / 2 + CORE_M)  # the two core points
+        # one of them on a face plane of its hull, the other on a core rim (brute force over circles)
+        def on_plane(h, y):
+            return min(abs(np.cross(h[c, 3:6], h[c, 6:9]) @ (y - h[c, :3])) / np.linalg.norm(np.cross(h[c, 3:6], h[c, 6:9]))
+                       for c in range(2))
+
+        def on_rim(h, y):
+            return min(abs(np.linalg.norm(y - h[c, :3]) - np.linalg.norm(h[c, 3:6])) + on_plane(h[c:c + 1].repeat(2, 0), y)
+                       for c in range(2))
+        assert on_plane(ha, xa) < 2e-5 and on_plane(hb, xb) < 2e-5
+        assert min(on_rim(ha, xa), on_rim(hb, xb)) < 5e-5
+
+
+def test_face_manifold_parallel_caps():
+    """Cap on cap (cfg self_manifold): a smaller disk face below a larger one gives the 4 rim points
+    of the smaller face, each at the plane gap; offset equal disks give the two tips of the lens
+    (one rim point of each face); the GJK contact alone when the faces do not face each other."""
+    big, small = _flat_link(0.05), _flat_link(0.04)
+    for gap in (0.003, 0.0005, -0.002):
+        ha = world(big, np.eye(3), np.array([0, 0, 0.053 + gap]))
+        hb = world(small, np.eye(3), np.array([0.004, -0.003, 0.0]))
+        pts = pair_manifold(ha, hb, 0.004)
+        assert len(pts) == 4, (gap, pts)
+        assert np.allclose(pts[:, 0], gap, atol=2e-6), pts[:, 0]
+        assert np.allclose(pts[:, 1:4], [0, 0, 1], atol=1e-5)
+        _check_manifold_geometry(ha, hb, pts, 0.004)
+    ha = world(big, np.eye(3), np.array([0, 0, 0.053 + 0.001]))
+    hb = world(big, np.eye(3), np.array([0.03, 0.0, 0.0]))
+    pts = pair_manifold(ha, hb, 0.004)
+    assert len(pts) == 4, pts
+    # the lens corners: B's rim point toward A's centre (x = 0.03 - r_core), B's two rim crossings
+    # (0.03 rad inside the lens), A's rim point toward B's centre (x = r_core)
+    rc = 0.05 - CORE_M
+    np.testing.assert_allclose(pts[[0, 3], 4], [0.03 - rc, rc], atol=1e-6)
+    assert abs(pts[1, 4] - 0.015) < 2e-3 and abs(pts[2, 4] - 0.015) < 2e-3 and pts[1, 5] * pts[2, 5] < 0
+    _check_manifold_geometry(ha, hb, pts, 0.004)
+    _check_manifold_geometry(ha, hb, pts, 0.004)
+    # side by side (rim on rim): one point, the GJK contact
+    R = _rot(np.array([np.cos(np.pi / 4), np.sin(np.pi / 4), 0, 0]))
+    ha = world(big, R, np.array([0, 0.0, 0.11]))
+    hb = world(big, R, np.zeros(3))
+    pts = pair_manifold(ha, hb, 0.004)
+    if len(pts):
+        assert len(pts) == 1
+        np.testing.assert_allclose(pts[0, :4], hull_pair(ha, hb, 0.004)[1:5], atol=1e-6)
+
+
+def test_face_manifold_tilted_caps_keep_points_within_margin(link_cores):
+    """Tilted faces (up to 12 degrees): the rim points whose gap exceeds the margin drop out, the
+    rest satisfy the geometry; robot link shapes at random face-to-face poses."""
+    rng = np.random.default_rng(11)
+    counts = []
+    for _ in range(60):
+        tilt = rng.uniform(0, np.radians(12))
+        ax = rng.normal(size=3)
+        ax[2] = 0
+        ax /= np.linalg.norm(ax)
+        q = np.concatenate([[np.cos(tilt / 2)], np.sin(tilt / 2) * ax])
+        ha = world(_flat_link(0.05), _rot(q), np.array([rng.uniform(-0.02, 0.02), rng.uniform(-0.02, 0.02),
+                                                        0.053 + rng.uniform(-0.003, 0.004)]))
+        hb = world(_flat_link(0.05), np.eye(3), np.zeros(3))
+        pts = pair_manifold(ha, hb, 0.004)
+        if len(pts) == 0:
+            continue
+        counts.append(len(pts))
+        if len(pts) > 1:
+            _check_manifold_geometry(ha, hb, pts, 0.004)
+            d_ref = brute_distance(ha, hb)
+            assert pts[:, 0].min() >= d_ref - 2 * CORE_M - 1e-5  # no point deeper than the true distance
+    assert len(counts) > 30 and max(counts) == 4 and min(counts) >= 1
+
+
+def test_manifold_in_folded_rollouts():
+    """Folded stand-up robots produce multi-point self contacts with the manifold on, none with it
+    off; the rollouts stay finite either way."""
+    tot = {}
+    for mf in (0, 1):
+        cfg = zm.TaskCfg.standup()
+        cfg.self_manifold = mf
+        sim = pyoracle.OracleSim(256, cfg, seed=3)
+        sim.reset()
+        st = sim.get_state()
+        st[13:19] += np.random.default_rng(4).normal(0, 1.5, (6, 256)).astype(np.float32)
+        sim.set_state(st)
+        rng = np.random.default_rng(0)
+        n = 0
+        for _ in range(20):
+            obs, rew, te, tr = sim.step(rng.normal(size=(256, 6)).astype(np.float32))
+            assert np.isfinite(obs).all() and np.isfinite(rew).all()
+            n += int(sim.contact_diag()[:, 2].sum())
+        tot[mf] = n
+    assert tot[1] > tot[0] > 0, tot

@@ -686,7 +686,7 @@ static_assert(ZB_WARM_ROWS == TL, "one cache row per lane of the team");
 __device__ __forceinline__ float wc_invalid(int s) { return (s & 3) == 3 ? -1.f : 0.f; }
 // the cache into FRC slots 0 .. ZB_WARM_SLOTS-1 (the GJK warm-start lookup), the other slots empty
 __device__ __forceinline__ void wc_load(const Q& q, const float* __restrict__ wc, int N, int i) {
-  const float v = wc[(size_t)q.s * N + i];
+  const float v = wc[(unsigned)(q.s * N + i)];  // (32-bit index: N * ZB_WARM_ROWS < 2^32)
   if (q.s < NCM) q.frc(q.s) = make_float4(0.f, 0.f, 0.f, -1.f);
   wave_sync();
   reinterpret_cast<float*>(&q.frc(q.s >> 2))[q.s & 3] = v;
@@ -694,7 +694,11 @@ __device__ __forceinline__ void wc_load(const Q& q, const float* __restrict__ wc
 // this lane's cache row after the last substep: FRC holds its kept contacts {n, code} by slot
 __device__ __forceinline__ float wc_extract(const Q& q) {
   const float4 f = q.frc(q.s < NCM ? q.s : 0);
-  const bool self = q.s < NCM && f.w >= 1.f && (((int)f.w) & 15) != 0;  // ground codes: 16 l
+  bool self = q.s < NCM && f.w >= 1.f && (((int)f.w) & 15) != 0;  // ground codes: 16 l
+  // one entry per pair: a face manifold's points share the pair's normal (= oracle wc_store)
+#pragma unroll
+  for (int c = 0; c < NCM - 1; ++c)
+    if (c < q.s && q.frc(c).w == f.w) self = false;
   const unsigned M = (unsigned)(__ballot(self) >> (TL * q.e)) & 0xffffu;
   const int r = q.s >> 2;
   float v = wc_invalid(q.s);
@@ -1247,6 +1251,125 @@ __device__ __forceinline__ bool gjk_quad(const QCircle& h, int j, const float v0
   return out.sep < margin;
 }
 
+// Self-contact manifold on the pair's quad (cfg.self_manifold; the oracle's face_manifold, PhysX
+// PCM keeps up to 4 points per convex pair): each lane tests its core circle as the face of its
+// hull along the pair normal (A: -n, B: +n; the hull's supporting circle with its plane normal
+// within 15 degrees); with a face on both sides, lane j evaluates sample j of B's rim carried along
+// +n onto A's face plane (side 0) and sample j of A's rim carried along -n onto B's (side 1) -- the
+// samples: all four quarter points when the source disk lies inside the target, else the tip toward
+// the target centre and the two lens crossings moved 0.03 rad toward it -- kept when the foot lies
+// inside the target core disk and the core gap - 2 kCoreM is within the margin. The first 4 kept in
+// (side, sample) order form the manifold. Returns its size (0: no face manifold: the GJK contact
+// alone); with `write`, this lane's kept samples go to candidate positions pos + their manifold
+// rank (below `end`). Quad-uniform control flow (DPP within the quad).
+constexpr float kFaceCos = 0.9659258262890683f;  // cos 15 deg (= oracle FACE_COS)
+constexpr float kFaceInsetC = 0.9995500337489875f, kFaceInsetS = 0.029995500202495664f;  // cos / sin 0.03
+__device__ __forceinline__ int quad_manifold(const QCircle& h, int j, const SelfContact& sc, float margin, bool write,
+                                             const Q& qq, int pos, int end, float code) {
+  const float sgd = (j & 2) ? 1.f : -1.f;
+  const float dd[3] = {sgd * sc.n[0], sgd * sc.n[1], sgd * sc.n[2]};
+  float u[3];
+  cross3(h.e1, h.e2, u);
+  const float iu = __builtin_amdgcn_rsqf(fmaxf(dot3(u, u), 1e-30f));
+  u[0] *= iu; u[1] *= iu; u[2] *= iu;
+  const float al = dot3(u, dd);
+  const float r = sqrtf(dot3(h.e1, h.e1));
+  const float sv = dot3(h.c, dd) + r * sqrtf(fmaxf(1.f - al * al, 0.f));
+  const float psv = dppf<DPP_XOR1>(sv);
+  const bool sup = (j & 1) ? (sv > psv) : !(psv > sv);
+  int fm = (sup && fabsf(al) >= kFaceCos) ? (1 << j) : 0;
+  fm |= dppi<DPP_XOR1>(fm);
+  fm |= dppi<DPP_XOR2>(fm);
+  if (!(fm & 3) || !(fm & 12)) return 0;
+  const float so = al < 0.f ? -1.f : 1.f;
+  const float uo[3] = {so * u[0], so * u[1], so * u[2]};
+  const bool a1 = !(fm & 1), b3 = !(fm & 4);  // A's face on quad lane 1 (else 0), B's on 3 (else 2)
+  float ca[3], ua[3], cb[3], ub[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const float c0 = dppf<0x00>(h.c[k]), c1 = dppf<0x55>(h.c[k]), c2 = dppf<0xAA>(h.c[k]), c3 = dppf<0xFF>(h.c[k]);
+    const float u0 = dppf<0x00>(uo[k]), u1 = dppf<0x55>(uo[k]), u2 = dppf<0xAA>(uo[k]), u3 = dppf<0xFF>(uo[k]);
+    ca[k] = a1 ? c1 : c0; ua[k] = a1 ? u1 : u0;
+    cb[k] = b3 ? c3 : c2; ub[k] = b3 ? u3 : u2;
+  }
+  const float r0 = dppf<0x00>(r), r1 = dppf<0x55>(r), r2 = dppf<0xAA>(r), r3 = dppf<0xFF>(r);
+  const float ra = a1 ? r1 : r0, rb = b3 ? r3 : r2;
+  bool v[2];
+  float4 px[2];  // this lane's two samples {x, sep}
+#pragma unroll
+  for (int side = 0; side < 2; ++side) {
+    const float* cs = side ? ca : cb;
+    const float* us = side ? ua : ub;
+    const float* ct = side ? cb : ca;
+    const float* ut = side ? ub : ua;
+    const float rs = side ? ra : rb, rt = side ? rb : ra, sg = side ? -1.f : 1.f;
+    float d0[3] = {ct[0] - cs[0], ct[1] - cs[1], ct[2] - cs[2]};
+    const float du = dot3(d0, us);
+    d0[0] -= du * us[0]; d0[1] -= du * us[1]; d0[2] -= du * us[2];
+    const float dl = sqrtf(dot3(d0, d0));
+    if (dl < 1e-9f) {  // concentric faces: a fixed in-plane axis
+      const float ax[3] = {fabsf(us[0]) < 0.9f ? 1.f : 0.f, fabsf(us[0]) < 0.9f ? 0.f : 1.f, 0.f};
+      const float au = dot3(ax, us);
+      d0[0] = ax[0] - au * us[0]; d0[1] = ax[1] - au * us[1]; d0[2] = ax[2] - au * us[2];
+      const float id0 = __builtin_amdgcn_rsqf(dot3(d0, d0));
+      d0[0] *= id0; d0[1] *= id0; d0[2] *= id0;
+    } else {
+      const float id0 = 1.f / dl;
+      d0[0] *= id0; d0[1] *= id0; d0[2] *= id0;
+    }
+    float d1[3];
+    cross3(us, d0, d1);
+    // this lane's sample j: (cr, sr) and whether the side has one
+    float cr = 1.f, sr = 0.f;
+    bool has;
+    if (dl + rs <= rt) {
+      has = true;
+      cr = j == 0 ? 1.f : (j == 2 ? -1.f : 0.f);
+      sr = j == 1 ? 1.f : (j == 3 ? -1.f : 0.f);
+    } else if (dl + rt > rs) {
+      const bool lens = dl < rs + rt;
+      has = j == 0 || (lens && j < 3);
+      if (j == 1 || j == 2) {
+        const float c_ = clampf((dl * dl + rs * rs - rt * rt) / (2.f * dl * rs), -1.f, 1.f);
+        const float s_ = sqrtf(fmaxf(1.f - c_ * c_, 0.f));
+        cr = c_ * kFaceInsetC + s_ * kFaceInsetS;
+        sr = (s_ * kFaceInsetC - c_ * kFaceInsetS) * (j == 1 ? 1.f : -1.f);
+      }
+    } else {
+      has = false;
+    }
+    const float den = sg * dot3(sc.n, ut);
+    float p[3], w[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) p[k] = cs[k] + rs * (cr * d0[k] + sr * d1[k]);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) w[k] = ct[k] - p[k];
+    const float t = dot3(w, ut) / (fabsf(den) < 1e-6f ? 1.f : den);
+    float qv[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) qv[k] = p[k] + t * sg * sc.n[k] - ct[k];
+    const float sep = t - 2.f * kCoreM;
+    v[side] = has && !(fabsf(den) < 1e-6f) && !(dot3(qv, qv) > rt * rt) && sep < margin;
+    px[side] = make_float4(p[0] + 0.5f * t * sg * sc.n[0], p[1] + 0.5f * t * sg * sc.n[1], p[2] + 0.5f * t * sg * sc.n[2],
+                           sep);
+  }
+  int vm = (v[0] ? 1 << j : 0) | (v[1] ? 16 << j : 0);
+  vm |= dppi<DPP_XOR1>(vm);
+  vm |= dppi<DPP_XOR2>(vm);
+  if (write) {
+#pragma unroll
+    for (int side = 0; side < 2; ++side) {
+      const int k = pos + __popc(vm & ((1 << (4 * side + j)) - 1));
+      if (v[side] && k < pos + 4 && k < end) {
+        qq.cand(k, 0) = px[side];
+        qq.cand(k, 1) = make_float4(sc.n[0], sc.n[1], sc.n[2], code);
+      }
+    }
+  }
+  const int cnt = __popc(vm);
+  return cnt < 4 ? cnt : 4;
+}
+
 // Detection + selection for the team's env; returns the number of contacts (team-uniform) and
 // `over` (more than NCM candidates: slots go through MAP). Ground: lane s tests link s (the lowest
 // rim point of each circle + 90-degree rotations, the first 4 within the margin). Self: a
@@ -1405,22 +1528,27 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q&
 #endif
     SelfContact hit0 = {};  // this quad's first contact is kept for the write pass
     int hit0_k = -1;
-    unsigned own = 0u;                // bit k: this quad's pair of round k is a contact
-    unsigned long long allhits = 0ull;  // team: bit r = the pair of rank r is a contact
+    // bit k: this quad's pair of round k is a contact (own) of points - 1 = lo + 2 hi (own_lo / own_hi)
+    unsigned own = 0u, own_lo = 0u, own_hi = 0u;
+    // team, bit r: the pair of rank r is a contact (allhits), its points - 1 = exl + 2 exh: a pair's
+    // first candidate position is g_tot + the points of the lower ranks
+    unsigned long long allhits = 0ull, exl = 0ull, exh = 0ull;
+    const bool mfon = cfg.self_manifold != 0;
 #pragma unroll 1
     for (int pass = 0; pass < 2; ++pass) {
       for (int k = 0; k < urounds; ++k) {
         const int u = qd + 4 * k;
         if (u >= U) break;
         const int r = nth_set_bit(und, u);
-        const int pos = g_tot + __popcll(allhits & ((1ull << r) - 1ull));
+        const unsigned long long lowr = (1ull << r) - 1ull;
+        const int pos = g_tot + __popcll(allhits & lowr) + __popcll(exl & lowr) + 2 * __popcll(exh & lowr);
         const bool need = pass == 0 || (((own >> k) & 1u) != 0u && pos < g_tot + NSELF);
         if (!need) continue;
         const int pcode = q.pair_code(nth_set_bit(bmask, r));
         SelfContact sc = hit0;
+        QCircle hc;
+        quad_circle(q, (qj & 2) ? (pcode & 15) : (pcode >> 4), qj & 1, hc);
         if (pass == 0 || k != hit0_k) {
-          QCircle hc;
-          quad_circle(q, (qj & 2) ? (pcode & 15) : (pcode >> 4), qj & 1, hc);
           // start: the pair's contact normal of the previous substep of this step (kept contacts
           // hold {n, code} in FRC; unused slots code -1), else the hull centre difference
           float v0[3];
@@ -1453,21 +1581,40 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q&
             if (qj == 0 && sc.sep <= -2.f * kCoreM + 1e-7f) ++deep_quad;
 #endif
           }
+          if (pass == 0 && !h) continue;
         }
-        if (pass == 1 && qj == 0) {
+        // the face manifold of a contact (cores apart: the overlap estimate stays one point); the
+        // write pass stores its points
+        const int mc = (mfon && sc.sep > -2.f * kCoreM + 1e-7f)
+                           ? quad_manifold(hc, qj, sc, margin, pass == 1, q, pos, g_tot + NSELF, (float)(pcode + 1))
+                           : 0;
+        if (pass == 0) {
+          own_lo |= (mc == 2 || mc == 4) ? 1u << k : 0u;
+          own_hi |= mc >= 3 ? 1u << k : 0u;
+        } else if (mc == 0 && qj == 0) {
           q.cand(pos, 0) = make_float4(sc.x[0], sc.x[1], sc.x[2], sc.sep);
           q.cand(pos, 1) = make_float4(sc.n[0], sc.n[1], sc.n[2], (float)(pcode + 1));
         }
       }
       if (pass == 0) {  // the team's contacts by rank: canonical positions follow the ground ones
-        unsigned long long mine = 0ull;
+        unsigned long long m1 = 0ull, ml = 0ull, mh = 0ull;
         for (int k = 0; k < urounds; ++k) {
           const int u = qd + 4 * k;
-          if (u < U && ((own >> k) & 1u)) mine |= 1ull << nth_set_bit(und, u);
+          if (u < U && ((own >> k) & 1u)) {
+            const unsigned long long bit = 1ull << nth_set_bit(und, u);
+            m1 |= bit;
+            ml |= ((own_lo >> k) & 1u) ? bit : 0ull;
+            mh |= ((own_hi >> k) & 1u) ? bit : 0ull;
+          }
         }
-        const int lo = tor((int)(unsigned)mine), hi = tor((int)(unsigned)(mine >> 32));
-        allhits = (unsigned long long)(unsigned)lo | ((unsigned long long)(unsigned)hi << 32);
-        s_tot = __popcll(allhits);
+        auto team_or = [](unsigned long long m) {
+          const int lo = tor((int)(unsigned)m), hi = tor((int)(unsigned)(m >> 32));
+          return (unsigned long long)(unsigned)lo | ((unsigned long long)(unsigned)hi << 32);
+        };
+        allhits = team_or(m1);
+        exl = team_or(ml);
+        exh = team_or(mh);
+        s_tot = __popcll(allhits) + __popcll(exl) + 2 * __popcll(exh);
       }
     }
 #ifdef ZB_STAMPS
@@ -2840,7 +2987,12 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_step_kernel(const z
     obs_q[0] = dq.x; obs_q[1] = dq.y; obs_q[2] = dq.z; obs_q[3] = dq.w;
   }
   log_flush(q, lmask, acc);
-  wc[(size_t)q.s * N + i] = reset ? wc_invalid(q.s) : wc_row;
+  {
+    // (an opaque 32-bit index: the load's address is not kept across the physics in a 64-bit register)
+    unsigned wi = (unsigned)(q.s * N + i);
+    asm volatile("" : "+v"(wi));
+    wc[wi] = reset ? wc_invalid(q.s) : wc_row;
+  }
   sp.mark(12);
 #if ZB_STAGED_STORES
 #define OUT(f) q.stg(f)
@@ -3293,7 +3445,12 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_su_step_kernel(
     qmul(p.quat, qrel, obs_q);
   }
   log_flush(q, lmask, acc);
-  wc[(size_t)q.s * N + i] = reset ? wc_invalid(q.s) : wc_row;
+  {
+    // (an opaque 32-bit index: the load's address is not kept across the physics in a 64-bit register)
+    unsigned wi = (unsigned)(q.s * N + i);
+    asm volatile("" : "+v"(wi));
+    wc[wi] = reset ? wc_invalid(q.s) : wc_row;
+  }
   sp.mark(12);
 #if ZB_STAGED_STORES
 #define OUT(f) q.stg(f)
@@ -3723,7 +3880,12 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_v4_step_kernel(
     he_obs = atan2f(sn, cs);
   }
   log_flush(q, lmask, acc);
-  wc[(size_t)q.s * N + i] = reset ? wc_invalid(q.s) : wc_row;
+  {
+    // (an opaque 32-bit index: the load's address is not kept across the physics in a 64-bit register)
+    unsigned wi = (unsigned)(q.s * N + i);
+    asm volatile("" : "+v"(wi));
+    wc[wi] = reset ? wc_invalid(q.s) : wc_row;
+  }
   sp.mark(12);
 #if ZB_STAGED_STORES
 #define OUT(f) q.stg(f)
@@ -4244,7 +4406,12 @@ __global__ __launch_bounds__(WGT, ZB_M_WAVES_PER_SIMD) void zb_m_step_kernel(
     if (standing > 0.5f) cmd[0] = cmd[1] = cmd[2] = 0.f;
   }
   log_flush(q, lmask, acc);
-  wc[(size_t)q.s * N + i] = reset ? wc_invalid(q.s) : wc_row;
+  {
+    // (an opaque 32-bit index: the load's address is not kept across the physics in a 64-bit register)
+    unsigned wi = (unsigned)(q.s * N + i);
+    asm volatile("" : "+v"(wi));
+    wc[wi] = reset ? wc_invalid(q.s) : wc_row;
+  }
   sp.mark(12);
 #if ZB_STAGED_STORES
 #define OUT(f) q.stg(f)

@@ -270,7 +270,7 @@ class Zbot6BFlatEnvCfg:
             friction_dynamic=self.sim.dynamic_friction,
             contact_margin=self.solver.contact_margin, baumgarte=self.solver.baumgarte,
             solver_iterations=self.solver.iterations, enable_self_collision=self.solver.self_collision,
-            solver_mode=self.solver.mode,
+            solver_mode=self.solver.mode, self_manifold=self.solver.self_manifold,
             reset_pose_range=tuple(tuple(pr.get(k, (0.0, 0.0))) for k in ("x", "y", "roll", "yaw")),
             cmd_vel_range=tuple(cmd.ranges.lin_vel_x), cmd_yaw_range=tuple(cmd.ranges.lin_vel_y),
             range_limit_vel=tuple(cmd.limit_ranges.lin_vel_x), range_limit_yaw=tuple(cmd.limit_ranges.lin_vel_y),

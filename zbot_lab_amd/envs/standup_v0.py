@@ -72,7 +72,7 @@ class Zbot6SUpEnvCfg:
             friction_dynamic=self.sim.dynamic_friction,
             contact_margin=self.solver.contact_margin, baumgarte=self.solver.baumgarte,
             solver_iterations=self.solver.iterations, enable_self_collision=self.solver.self_collision,
-            solver_mode=self.solver.mode,
+            solver_mode=self.solver.mode, self_manifold=self.solver.self_manifold,
             reset_pose_range=tuple(tuple(pr.get(k, (0.0, 0.0))) for k in ("x", "y", "roll", "yaw")),
             curriculum=self.events.my_curric is not None, curriculum_weights=dict(self.curriculum_weights),
         )

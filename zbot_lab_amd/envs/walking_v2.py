@@ -51,6 +51,7 @@ class SolverCfg:
     baumgarte: float = 0.2
     self_collision: bool = True       # enabled_self_collisions=True (zbot_cfg.py:636)
     mode: int = 0                     # 0: PGS sweeps; 1: TGS-style sub-iterations (zb_task_cfg.solver_mode)
+    self_manifold: int = 1            # 1: cap-on-cap self contacts with up to 4 points (zb_task_cfg.self_manifold)
 
 
 def _scales(**kw) -> dict:
@@ -96,7 +97,7 @@ class ZbotDirectEnvCfgV2:
             reward_weights=dict(self.reward_cfg["reward_scales"]), gravity=-self.sim.gravity[2],
             friction=self.sim.static_friction, friction_dynamic=self.sim.dynamic_friction, contact_margin=self.solver.contact_margin,
             baumgarte=self.solver.baumgarte, solver_iterations=self.solver.iterations,
-            enable_self_collision=self.solver.self_collision, solver_mode=self.solver.mode,
+            enable_self_collision=self.solver.self_collision, solver_mode=self.solver.mode, self_manifold=self.solver.self_manifold,
         )
 
 

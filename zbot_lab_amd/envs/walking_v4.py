@@ -75,7 +75,7 @@ class Zbot6SEnvV4Cfg:
             gravity=-self.sim.gravity[2], friction=self.sim.static_friction, friction_dynamic=self.sim.dynamic_friction,
             contact_margin=self.solver.contact_margin, baumgarte=self.solver.baumgarte,
             solver_iterations=self.solver.iterations, enable_self_collision=self.solver.self_collision,
-            solver_mode=self.solver.mode,
+            solver_mode=self.solver.mode, self_manifold=self.solver.self_manifold,
             reset_pose_range=tuple(tuple(pr.get(k, (0.0, 0.0))) for k in ("x", "y", "roll", "yaw")),
             cmd_vel_range=tuple(cp["velocity_range"]), cmd_yaw_range=tuple(cp["yaw_range"]),
             cmd_dual_sign=bool(cp["dual_sign"]), cmd_offset=float(cp["offset"]), cmd_prob_pos=float(cp["prob_pos"]),

@@ -152,7 +152,7 @@ class ZbTaskCfg(C.Structure):
         ("feet_close_min", C.c_float),
         ("reset_feet_refresh", C.c_int32),
         ("friction_dynamic", C.c_float),
-        ("solver_mode", C.c_int32),
+        ("solver_mode", C.c_int32), ("self_manifold", C.c_int32),
     ]
 
 
@@ -513,6 +513,7 @@ class TaskCfg:
     baumgarte: float = 0.2
     solver_iterations: int = 4   # = solver_position_iteration_count (zbot_cfg.py:637)
     solver_mode: int = 0         # 0: PGS sweeps on one linearisation; 1: TGS-style (zb_task_cfg.solver_mode)
+    self_manifold: int = 1       # cap-on-cap self contacts with up to 4 points (zb_task_cfg.self_manifold)
     enable_self_collision: bool = True
     task: int = TASK_WALKING_V2
     # stand-up / v4 reset pose (reset_root_state_uniform): x, y, roll, yaw ranges
@@ -679,6 +680,7 @@ class TaskCfg:
         c.reset_feet_refresh = int(self.reset_feet_refresh)
         c.friction_dynamic = self.friction_dynamic
         c.solver_mode = int(self.solver_mode)
+        c.self_manifold = int(self.self_manifold)
         c.reset_pose_body_frame = int(self.reset_pose_body_frame)
         c.task = self.task
         for k in range(4):
