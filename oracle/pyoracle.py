@@ -185,8 +185,9 @@ class OracleSim:
         return p, q
 
     def contact_diag(self):
-        """[n, 5]: candidates, ground, self, kept, min |sep - margin| of the current state."""
-        d = np.zeros((self.n, 5), np.float32)
+        """[n, 6]: candidates, ground, self pairs in contact, kept, min |sep - margin|, kept self points
+        (a face manifold counts each point) of the current state."""
+        d = np.zeros((self.n, 6), np.float32)
         self.lib.zbo_contact_diag(self.h, d)
         return d
 

@@ -3022,11 +3022,14 @@ int zbo_contact_diag(zbo_sim* s, float* out) {
       }
     }
     detect(&s->m, &s->c, &k, Pz, NULL, &L);
-    out[5 * e + 0] = (float)(ng + ns);
-    out[5 * e + 1] = (float)ng;
-    out[5 * e + 2] = (float)ns;
-    out[5 * e + 3] = (float)L.n;
-    out[5 * e + 4] = (float)mind;
+    int kself = 0; /* kept self-contact points (face manifolds count every point) */
+    for (int j = 0; j < L.n; ++j) kself += L.c[j].lb >= 0;
+    out[6 * e + 0] = (float)(ng + ns);
+    out[6 * e + 1] = (float)ng;
+    out[6 * e + 2] = (float)ns;
+    out[6 * e + 3] = (float)L.n;
+    out[6 * e + 4] = (float)mind;
+    out[6 * e + 5] = (float)kself;
   }
   return 0;
 }

@@ -350,3 +350,35 @@ def test_full_state_contact_cache(gpu, task):
     assert (dn[both] <= 2e-3).mean() >= 0.95 and (dn[both] <= 5e-2).mean() >= 0.99, np.sort(dn[both])[-10:]
     # the in-kernel auto-reset invalidates a resetting env's entries
     assert (wg[3::4][:, g_out[2] | g_out[3]] == -1).all()
+
+
+@pytest.mark.parametrize("task", ["v2", "standup"])
+def test_full_state_face_manifold(gpu, task):
+    """The self-contact face manifold (zb_task_cfg.self_manifold, DESIGN.md §3.2: cap on cap, up to 4
+    points per pair): folded states in which at least one link pair is a face-to-face contact (the
+    oracle's candidate list has more self points than with one point per pair), one step on both
+    sides under the full-state rule."""
+    from oracle.pyoracle import OracleSim
+    # (face-to-face pairs are rare among random folds: ~0.1 % of uniformly random joint angles)
+    seed, pool = 43, 65536
+    cfg1, cfg0 = task_cfg(task), task_cfg(task)
+    cfg0.self_manifold = 0
+    o1, o0 = OracleSim(pool, cfg1, seed=seed), OracleSim(pool, cfg0, seed=seed)
+    st = random_states(task, o1, pool, seed=606)
+    st[13:19] = np.random.default_rng(607).uniform(-np.pi, np.pi, (6, pool)).astype(np.float32)
+    o1.set_state(st)
+    o0.set_state(st)
+    extra = o1.contact_diag()[:, 5] - o0.contact_diag()[:, 5]
+    ids = np.nonzero(extra > 0)[0][:512]
+    assert len(ids) >= 40, len(ids)
+    n = len(ids)
+    st = np.ascontiguousarray(st[:, ids])
+    g, _, cfg, torch = _sims(task, n, seed)
+    assert cfg.self_manifold == 1
+    g.set_state(torch.from_numpy(st).cuda())
+    a = np.random.default_rng(608).normal(size=(n, 6)).astype(np.float32)
+    obs, rew, te, tr = g.step(torch.from_numpy(a).cuda())
+    g_out = (obs.cpu().numpy(), rew.cpu().numpy(), te.cpu().numpy().copy(), tr.cpu().numpy().copy())
+    nbad = _check(task, "one step from folded states with face manifolds", n, seed, st, [a], g_out,
+                  g.get_state().cpu().numpy(), torch)
+    assert nbad <= 0.05 * n
