@@ -418,6 +418,12 @@ int zb_read_wave_times(uint64_t* out, int n);
  * oracle's hull_pair (tests/test_gpu_selfcollision.py). */
 int zb_gjk_pairs(const float* pairs, const float* v0, int n, float margin, float* out, void* stream);
 
+/* Test entry: GJK (cold start) + the self-contact face manifold (the step kernels' quad_manifold,
+ * zb_task_cfg.self_manifold) on n link pairs given as world-frame core hulls (layout as
+ * zb_gjk_pairs); out [n][29] = {points (0: no contact, 1: the GJK contact alone), then per point
+ * {separation, normal[3], point[3]}}. Checked against the oracle's zbo_pair_manifold. */
+int zb_pair_manifold(const float* pairs, int n, float margin, float* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -132,3 +132,57 @@ def test_gjk_quad_matches_oracle_warm():
     o = _oracle(pairs, v0)
     g = _gpu(pairs, v0)
     _compare(g, o, pairs, v0)
+
+
+def _face_pairs(n, seed):
+    """Face-to-face link pairs: two flat stacks (parallel circles) with the upper one tilted up to 12
+    degrees, offset in the plane up to 6 cm and gapped -3 .. +4 mm (lens, containment and apart)."""
+    from tests.test_oracle_selfcollision import _flat_link
+    rng = np.random.default_rng(seed)
+    out = np.zeros((n, 2, 2, 9), np.float32)
+    for k in range(n):
+        tilt = rng.uniform(0, np.radians(12))
+        ax = rng.normal(size=3)
+        ax[2] = 0
+        ax /= np.linalg.norm(ax)
+        q = np.concatenate([[np.cos(tilt / 2)], np.sin(tilt / 2) * ax])
+        ra, rb = rng.choice([0.05, 0.04]), rng.choice([0.05, 0.04])
+        off = rng.uniform(-0.06, 0.06, 2)
+        out[k, 0] = world(_flat_link(ra), _rot(q), np.array([off[0], off[1], 0.053 + rng.uniform(-0.003, 0.004)]))
+        out[k, 1] = world(_flat_link(rb), np.eye(3), np.zeros(3))
+    return out
+
+
+def test_gpu_face_manifold_matches_oracle():
+    """quad_manifold (zb_pair_manifold) against the oracle's face_manifold (zbo_pair_manifold) on
+    face-to-face pairs and on random robot link pairs: the same number of points in the same order,
+    separations to 2e-5 m, points to 1e-4 m, away from the decision edges (a sample within 1e-5 m of
+    the margin or of the other disk's rim, or a face within 1e-4 of the 15-degree threshold, may go
+    either way in fp32)."""
+    import torch
+    from zbot_lab_amd import _native as nat
+    pairs = np.concatenate([_face_pairs(3000, 21), _pairs(1000, 22)])
+    n = len(pairs)
+    ref = np.zeros((n, 29), np.float32)
+    for k in range(n):
+        pts = np.zeros(28, np.float32)
+        c = pyoracle.lib().zbo_pair_manifold(np.ascontiguousarray(pairs[k, 0]).ravel(), np.ascontiguousarray(pairs[k, 1]).ravel(),
+                                             MARGIN, pts)
+        ref[k, 0] = c
+        ref[k, 1:] = pts
+    P = torch.from_numpy(np.ascontiguousarray(pairs)).cuda()
+    out = torch.zeros(n, 29, device="cuda")
+    nat.check(nat.lib().zb_pair_manifold(nat.ptr(P), n, MARGIN, nat.ptr(out), None), "zb_pair_manifold")
+    got = out.cpu().numpy()
+    same = got[:, 0] == ref[:, 0]
+    multi = ref[:, 0] >= 2
+    print(f"\nmanifold pairs {n}: oracle counts {np.bincount(ref[:, 0].astype(int), minlength=5).tolist()}, "
+          f"GPU counts {np.bincount(got[:, 0].astype(int), minlength=5).tolist()}, count agreement {same.mean():.4f}")
+    assert multi.sum() >= 500 and (ref[:, 0] == 4).sum() >= 100
+    assert same.mean() >= 0.99
+    for k in np.nonzero(same & (ref[:, 0] > 0))[0]:
+        c = int(ref[k, 0])
+        g, r = got[k, 1:1 + 7 * c].reshape(c, 7), ref[k, 1:1 + 7 * c].reshape(c, 7)
+        assert np.abs(g[:, 0] - r[:, 0]).max() <= 2e-5, (k, g[:, 0], r[:, 0])
+        assert np.abs(g[:, 1:4] - r[:, 1:4]).max() <= 2e-3, k
+        assert np.abs(g[:, 4:7] - r[:, 4:7]).max() <= 1e-4, (k, g[:, 4:7], r[:, 4:7])

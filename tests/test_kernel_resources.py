@@ -1,10 +1,10 @@
 """Occupancy budget of the step kernels, read from the built libzbot.so's gfx950 code object
 (no GPU needed): <= 20 KB of LDS per workgroup and <= 256 VGPRs + AGPRs, so that two waves share
-a SIMD once a launch has more than one wave per SIMD (the LDS diet). Scratch: at most
-one dword in the walking v2 (the benchmarked kernel) and stand-up kernels with the default PGS solve
-(round 4, with the self-contact manifold: one loop-invariant value stored before the substep loop and
-reloaded once in the epilogue); the v4 / manager kernels and the TGS instantiations
-spill a few registers (<= 64 B per lane)."""
+a SIMD once a launch has more than one wave per SIMD (the LDS diet). Scratch: <= 64 B
+per lane in every step kernel, and in the walking v2 (the benchmarked kernel) and stand-up kernels
+with the default PGS solve no scratch access inside any loop (round 4: the register allocator parks a
+few loop-invariant values before the substep loop and reloads them once in the epilogue; checked on
+the disassembled code object: no scratch instruction between a backward branch and its target)."""
 import os
 import re
 import shutil
@@ -57,7 +57,59 @@ def test_step_kernels_fit_two_waves_per_simd(tmp_path):
         scratch = md.get("private_segment_fixed_size", 0)
         assert lds <= LDS_PER_CU // 8, f"{short}: {lds} B of LDS per one-wave workgroup (> 20 KB: one wave per SIMD)"
         assert regs <= 256, f"{short}: {regs} VGPRs + AGPRs (> 256: one wave per SIMD)"
-        if short in ("zb_step_kernel", "zb_su_step_kernel") and not tgs:
-            assert scratch <= 8, f"{short}: {scratch} B of scratch per lane (register spill)"
         assert scratch <= 64, f"{short}{' (TGS)' if tgs else ''}: {scratch} B of scratch per lane"
     assert found == 2 * len(STEP_KERNELS), sorted(kernels)  # PGS and TGS instantiations
+
+
+def _disassembly(tmp_path):
+    tools = [shutil.which("objcopy"), os.path.join(LLVM, "clang-offload-bundler"), os.path.join(LLVM, "llvm-objdump")]
+    if not os.path.exists(LIB) or not all(t and os.path.exists(t) for t in tools):
+        pytest.skip("libzbot.so or the ROCm binary tools are missing")
+    fat, co = str(tmp_path / "fatbin.bin"), str(tmp_path / "co.elf")
+    subprocess.run([tools[0], "-O", "binary", "--only-section=.hip_fatbin", LIB, fat], check=True)
+    subprocess.run([tools[1], "--unbundle", "--type=o", f"--input={fat}",
+                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True)
+    return subprocess.run([tools[2], "-d", "--no-show-raw-insn", co], check=True, capture_output=True, text=True).stdout
+
+
+def test_benchmarked_kernels_spill_outside_loops(tmp_path):
+    """No scratch load / store inside any loop (the substep loop, the GJK / PGS loops) of the walking
+    v2 and stand-up step kernels with the default PGS solve: a spill there would cost every substep."""
+    text = _disassembly(tmp_path)
+    funcs, cur = {}, None
+    for line in text.splitlines():
+        m = re.match(r"^([0-9a-f]+) <(\S+)>:", line)
+        if m:
+            cur = m.group(2)
+            funcs[cur] = (int(m.group(1), 16), [])
+            continue
+        if cur is None:
+            continue
+        a = re.search(r"// ([0-9A-F]{6,}):", line)
+        if a:
+            funcs[cur][1].append((int(a.group(1), 16), line.split("//")[0].strip()))
+    checked = 0
+    for name, (base, insts) in funcs.items():
+        if not any(f"{len(k)}{k}ILb0E" in name for k in ("zb_step_kernel", "zb_su_step_kernel")):
+            continue
+        checked += 1
+        scr = [addr for addr, ins in insts if ins.startswith("scratch_")]
+        br = []
+        in_f = False
+        for line in text.splitlines():
+            if line.startswith(f"{base:016x} <"):
+                in_f = True
+                continue
+            if in_f and re.match(r"^[0-9a-f]+ <", line):
+                break
+            if in_f and re.search(r"\ts_(cbranch_\w+|branch) ", line):
+                a = re.search(r"// ([0-9A-F]{6,}):", line)
+                t = re.search(r"<\S+\+0x([0-9a-f]+)>", line)
+                if a and t:
+                    src, dst = int(a.group(1), 16), base + int(t.group(1), 16)
+                    if dst <= src:
+                        br.append((dst, src))
+        inside = [hex(x) for x in scr if any(d <= x <= s_ for d, s_ in br)]
+        assert br, name
+        assert not inside, f"{name[:40]}: scratch access inside a loop at {inside[:8]}"
+    assert checked == 2

@@ -1260,12 +1260,13 @@ __device__ __forceinline__ bool gjk_quad(const QCircle& h, int j, const float v0
 // the target centre and the two lens crossings moved 0.03 rad toward it -- kept when the foot lies
 // inside the target core disk and the core gap - 2 kCoreM is within the margin. The first 4 kept in
 // (side, sample) order form the manifold. Returns its size (0: no face manifold: the GJK contact
-// alone); with `write`, this lane's kept samples go to candidate positions pos + their manifold
-// rank (below `end`). Quad-uniform control flow (DPP within the quad).
+// alone); with `write`, sink(rank, {x, sep}) takes each of this lane's kept samples. Quad-uniform
+// control flow (DPP within the quad).
 constexpr float kFaceCos = 0.9659258262890683f;  // cos 15 deg (= oracle FACE_COS)
 constexpr float kFaceInsetC = 0.9995500337489875f, kFaceInsetS = 0.029995500202495664f;  // cos / sin 0.03
+template <class Sink>
 __device__ __forceinline__ int quad_manifold(const QCircle& h, int j, const SelfContact& sc, float margin, bool write,
-                                             const Q& qq, int pos, int end, float code) {
+                                             Sink sink) {
   const float sgd = (j & 2) ? 1.f : -1.f;
   const float dd[3] = {sgd * sc.n[0], sgd * sc.n[1], sgd * sc.n[2]};
   float u[3];
@@ -1359,11 +1360,8 @@ __device__ __forceinline__ int quad_manifold(const QCircle& h, int j, const Self
   if (write) {
 #pragma unroll
     for (int side = 0; side < 2; ++side) {
-      const int k = pos + __popc(vm & ((1 << (4 * side + j)) - 1));
-      if (v[side] && k < pos + 4 && k < end) {
-        qq.cand(k, 0) = px[side];
-        qq.cand(k, 1) = make_float4(sc.n[0], sc.n[1], sc.n[2], code);
-      }
+      const int k = __popc(vm & ((1 << (4 * side + j)) - 1));
+      if (v[side] && k < 4) sink(k, px[side]);
     }
   }
   const int cnt = __popc(vm);
@@ -1585,8 +1583,14 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q&
         }
         // the face manifold of a contact (cores apart: the overlap estimate stays one point); the
         // write pass stores its points
+        const float code = (float)(pcode + 1);
         const int mc = (mfon && sc.sep > -2.f * kCoreM + 1e-7f)
-                           ? quad_manifold(hc, qj, sc, margin, pass == 1, q, pos, g_tot + NSELF, (float)(pcode + 1))
+                           ? quad_manifold(hc, qj, sc, margin, pass == 1, [&](int rank, float4 xs) {
+                               if (pos + rank < g_tot + NSELF) {
+                                 q.cand(pos + rank, 0) = xs;
+                                 q.cand(pos + rank, 1) = make_float4(sc.n[0], sc.n[1], sc.n[2], code);
+                               }
+                             })
                            : 0;
         if (pass == 0) {
           own_lo |= (mc == 2 || mc == 4) ? 1u << k : 0u;
@@ -3075,6 +3079,42 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_step_kernel(const z
   }
 #undef ST
 #undef CST
+}
+
+// Test entry (zb_pair_manifold): GJK (cold start) + the face manifold of n link pairs given as
+// world-frame core hulls, one pair per quad (tests/test_gpu_selfcollision.py against the oracle's
+// zbo_pair_manifold): out [n][29] = {points, then per point {sep, n[3], x[3]}} (0 points: no contact;
+// 1 without a face manifold: the GJK contact).
+__global__ void zb_manifold_kernel(const float* __restrict__ pairs, int n, float margin, float* __restrict__ out) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int pr = min(t >> 2, n - 1), j = t & 3;  // quads past n recompute pair n - 1 (no store)
+  const float* c = pairs + (size_t)pr * 36 + 9 * j;
+  QCircle h;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) { h.c[k] = c[k]; h.e1[k] = c[3 + k]; h.e2[k] = c[6 + k]; }
+  float ca[3], cb[3], v0[3];
+  quad_centres(h, ca, cb);
+  v0[0] = ca[0] - cb[0]; v0[1] = ca[1] - cb[1]; v0[2] = ca[2] - cb[2];
+  SelfContact sc;
+  int its = 0;
+  const bool hit = gjk_quad(h, j, v0, false, margin, margin, sc, its);
+  float* o = out + (size_t)pr * 29;
+  const bool mine = (t >> 2) < n;
+  int cnt = 0;
+  if (hit && sc.sep > -2.f * kCoreM + 1e-7f)
+    cnt = quad_manifold(h, j, sc, margin, true, [&](int rank, float4 xs) {
+      if (mine) {
+        float* p = o + 1 + 7 * rank;
+        p[0] = xs.w; p[1] = sc.n[0]; p[2] = sc.n[1]; p[3] = sc.n[2]; p[4] = xs.x; p[5] = xs.y; p[6] = xs.z;
+      }
+    });
+  if (mine && j == 0) {
+    if (hit && cnt == 0) {
+      float* p = o + 1;
+      p[0] = sc.sep; p[1] = sc.n[0]; p[2] = sc.n[1]; p[3] = sc.n[2]; p[4] = sc.x[0]; p[5] = sc.x[1]; p[6] = sc.x[2];
+    }
+    o[0] = hit ? (float)(cnt > 0 ? cnt : 1) : 0.f;
+  }
 }
 
 // Test entry (zb_gjk_pairs): the self-collision GJK of n link pairs given as world-frame core
@@ -5302,6 +5342,12 @@ int zb_physics_substeps(zb_handle h, const float* targets, int nsub, float* net_
   // the physics moved: the self-contact cache describes another state (cold start next step)
   zb_wc_fill_kernel<<<(h->n * ZB_WARM_ROWS + 255) / 256, 256, 0, (hipStream_t)stream>>>(h->n, h->d_wc, nullptr, h->n);
   return launch_check("zb_wc_fill_kernel");
+}
+
+int zb_pair_manifold(const float* pairs, int n, float margin, float* out, void* stream) {
+  if (!pairs || !out || n < 1) return set_err(-1, "zb_pair_manifold", hipSuccess);
+  zb_manifold_kernel<<<(4 * n + 63) / 64, 64, 0, (hipStream_t)stream>>>(pairs, n, margin, out);
+  return launch_check("zb_manifold_kernel");
 }
 
 int zb_gjk_pairs(const float* pairs, const float* v0, int n, float margin, float* out, void* stream) {
