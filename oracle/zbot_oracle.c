@@ -650,7 +650,8 @@ static int hull_pair(const hull_t* A, const hull_t* B, real margin, real early_m
  * along +n to A's face plane, kept if the foot lies inside A's core disk and the core gap minus
  * 2 CORE_M is within the margin; then A's rim the same way toward B (along -n). The first 4 kept
  * in that order are the manifold {x = midpoint, n, sep} (a lens: B's tip, its two crossings, A's
- * tip); none kept (or the faces not both present): the GJK contact alone. (The kernel runs the same statement on the 4 lanes of
+ * tip), all along A's face normal (n = -A's outward face normal); none kept (or the faces not both
+ * present): the GJK contact alone. (The kernel runs the same statement on the 4 lanes of
  * the pair's quad: face_manifold in zbot_sim.hip.) */
 #define FACE_COS 0.9659258262890683 /* cos 15 deg */
 #define FACE_INSET_C 0.9995500337489875 /* cos / sin of 0.03 rad: the lens crossings moved inside */
@@ -679,6 +680,9 @@ static int face_manifold(const hull_t* A, const hull_t* B, const contact_t* c0, 
   real ua[3], ub[3];
   const int fa = hull_face(A, nA, ua), fb = hull_face(B, c0->n, ub);
   if (fa < 0 || fb < 0) return 0;
+  /* the manifold's normal: A's face normal (B -> A), exact for the face pair where GJK's normal of
+   * two nearly parallel faces is poorly determined (PhysX clips against a reference face too) */
+  const real nr[3] = {-ua[0], -ua[1], -ua[2]};
   int k = 0;
   for (int side = 0; side < 2 && k < 4; ++side) {
     /* side 0: B's rim onto A's face along +n; side 1: A's rim onto B's face along -n */
@@ -722,7 +726,7 @@ static int face_manifold(const hull_t* A, const hull_t* B, const contact_t* c0, 
         na = 3;
       }
     }
-    const real den = sg * v3_dot(c0->n, ut);
+    const real den = sg * v3_dot(nr, ut);
     if (fabs((double)den) < 1e-6) continue;
     for (int r = 0; r < na && k < 4; ++r) {
       const real cr = cs_[r], sr = sn_[r];
@@ -730,13 +734,13 @@ static int face_manifold(const hull_t* A, const hull_t* B, const contact_t* c0, 
       for (int a = 0; a < 3; ++a) p[a] = cs[a] + rs * (cr * d0[a] + sr * d1[a]);
       for (int a = 0; a < 3; ++a) w[a] = ct[a] - p[a];
       const real t = v3_dot(w, ut) / den; /* p + t sg n lies on the target face plane */
-      for (int a = 0; a < 3; ++a) q[a] = p[a] + t * sg * c0->n[a] - ct[a];
+      for (int a = 0; a < 3; ++a) q[a] = p[a] + t * sg * nr[a] - ct[a];
       if (v3_dot(q, q) > rt * rt) continue;
       const real sep = t - 2 * (real)CORE_M;
       if (!(sep < margin)) continue;
       contact_t* o = &out[k++];
       o->la = c0->la; o->lb = c0->lb; o->sep = sep;
-      for (int a = 0; a < 3; ++a) { o->n[a] = c0->n[a]; o->x[a] = p[a] + (real)0.5 * t * sg * c0->n[a]; }
+      for (int a = 0; a < 3; ++a) { o->n[a] = nr[a]; o->x[a] = p[a] + (real)0.5 * t * sg * nr[a]; }
     }
   }
   return k;

@@ -1295,6 +1295,7 @@ __device__ __forceinline__ int quad_manifold(const QCircle& h, int j, const Self
   }
   const float r0 = dppf<0x00>(r), r1 = dppf<0x55>(r), r2 = dppf<0xAA>(r), r3 = dppf<0xFF>(r);
   const float ra = a1 ? r1 : r0, rb = b3 ? r3 : r2;
+  const float nr[3] = {-ua[0], -ua[1], -ua[2]};  // the manifold's normal: A's face normal (B -> A)
   bool v[2];
   float4 px[2];  // this lane's two samples {x, sep}
 #pragma unroll
@@ -1339,7 +1340,7 @@ __device__ __forceinline__ int quad_manifold(const QCircle& h, int j, const Self
     } else {
       has = false;
     }
-    const float den = sg * dot3(sc.n, ut);
+    const float den = sg * dot3(nr, ut);
     float p[3], w[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) p[k] = cs[k] + rs * (cr * d0[k] + sr * d1[k]);
@@ -1348,11 +1349,10 @@ __device__ __forceinline__ int quad_manifold(const QCircle& h, int j, const Self
     const float t = dot3(w, ut) / (fabsf(den) < 1e-6f ? 1.f : den);
     float qv[3];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) qv[k] = p[k] + t * sg * sc.n[k] - ct[k];
+    for (int k = 0; k < 3; ++k) qv[k] = p[k] + t * sg * nr[k] - ct[k];
     const float sep = t - 2.f * kCoreM;
     v[side] = has && !(fabsf(den) < 1e-6f) && !(dot3(qv, qv) > rt * rt) && sep < margin;
-    px[side] = make_float4(p[0] + 0.5f * t * sg * sc.n[0], p[1] + 0.5f * t * sg * sc.n[1], p[2] + 0.5f * t * sg * sc.n[2],
-                           sep);
+    px[side] = make_float4(p[0] + 0.5f * t * sg * nr[0], p[1] + 0.5f * t * sg * nr[1], p[2] + 0.5f * t * sg * nr[2], sep);
   }
   int vm = (v[0] ? 1 << j : 0) | (v[1] ? 16 << j : 0);
   vm |= dppi<DPP_XOR1>(vm);
@@ -1361,7 +1361,7 @@ __device__ __forceinline__ int quad_manifold(const QCircle& h, int j, const Self
 #pragma unroll
     for (int side = 0; side < 2; ++side) {
       const int k = __popc(vm & ((1 << (4 * side + j)) - 1));
-      if (v[side] && k < 4) sink(k, px[side]);
+      if (v[side] && k < 4) sink(k, px[side], nr);
     }
   }
   const int cnt = __popc(vm);
@@ -1585,10 +1585,10 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q&
         // write pass stores its points
         const float code = (float)(pcode + 1);
         const int mc = (mfon && sc.sep > -2.f * kCoreM + 1e-7f)
-                           ? quad_manifold(hc, qj, sc, margin, pass == 1, [&](int rank, float4 xs) {
+                           ? quad_manifold(hc, qj, sc, margin, pass == 1, [&](int rank, float4 xs, const float* nn) {
                                if (pos + rank < g_tot + NSELF) {
                                  q.cand(pos + rank, 0) = xs;
-                                 q.cand(pos + rank, 1) = make_float4(sc.n[0], sc.n[1], sc.n[2], code);
+                                 q.cand(pos + rank, 1) = make_float4(nn[0], nn[1], nn[2], code);
                                }
                              })
                            : 0;
@@ -3102,10 +3102,10 @@ __global__ void zb_manifold_kernel(const float* __restrict__ pairs, int n, float
   const bool mine = (t >> 2) < n;
   int cnt = 0;
   if (hit && sc.sep > -2.f * kCoreM + 1e-7f)
-    cnt = quad_manifold(h, j, sc, margin, true, [&](int rank, float4 xs) {
+    cnt = quad_manifold(h, j, sc, margin, true, [&](int rank, float4 xs, const float* nn) {
       if (mine) {
         float* p = o + 1 + 7 * rank;
-        p[0] = xs.w; p[1] = sc.n[0]; p[2] = sc.n[1]; p[3] = sc.n[2]; p[4] = xs.x; p[5] = xs.y; p[6] = xs.z;
+        p[0] = xs.w; p[1] = nn[0]; p[2] = nn[1]; p[3] = nn[2]; p[4] = xs.x; p[5] = xs.y; p[6] = xs.z;
       }
     });
   if (mine && j == 0) {
