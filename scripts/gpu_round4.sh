@@ -3,9 +3,11 @@
 # rocprofv3 trace / PMC (gpu_perf.sh), the other bench configs, then the PPO training profile.
 # Usage: gpurun --timeout 1200 -- bash scripts/gpu_round4.sh <tag>
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; TAG=${1:-r4}; O=gpurun_out/$TAG; mkdir -p $O; export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests -m gpu -v -s --timeout 300 --timeout-method thread > $O/test_gpu.log 2>&1
-rc=$?; grep -E "^(FAILED|ERROR)|passed|failed" $O/test_gpu.log | tail -6
-[ $rc -eq 0 ] || exit $rc
+if [ -z "${NO_SUITE:-}" ]; then
+  timeout -k 10 600 python -u -m pytest tests -m gpu -v -s --timeout 300 --timeout-method thread > $O/test_gpu.log 2>&1
+  rc=$?; grep -E "^(FAILED|ERROR)|passed|failed" $O/test_gpu.log | tail -6
+  [ $rc -eq 0 ] || exit $rc
+fi
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { tail -5 $O/smoke.log; exit 1; }
 tail -1 $O/smoke.log
 bash scripts/gpu_perf.sh $TAG || exit 1

@@ -61,6 +61,51 @@ def test_step_kernels_fit_two_waves_per_simd(tmp_path):
     assert found == 2 * len(STEP_KERNELS), sorted(kernels)  # PGS and TGS instantiations
 
 
+def _descriptor_vgpr_granules(tmp_path):
+    """GRANULATED_WORKITEM_VGPR_COUNT (COMPUTE_PGM_RSRC1 bits 0-5, kernel descriptor offset 48) of every
+    step kernel's .kd symbol."""
+    tools = [shutil.which("objcopy"), os.path.join(LLVM, "clang-offload-bundler"), os.path.join(LLVM, "llvm-readelf")]
+    if not os.path.exists(LIB) or not all(t and os.path.exists(t) for t in tools):
+        pytest.skip("libzbot.so or the ROCm binary tools are missing")
+    fat, co = str(tmp_path / "fatbin.bin"), str(tmp_path / "co.elf")
+    subprocess.run([tools[0], "-O", "binary", "--only-section=.hip_fatbin", LIB, fat], check=True)
+    subprocess.run([tools[1], "--unbundle", "--type=o", f"--input={fat}",
+                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True)
+    out = subprocess.run([tools[2], "-s", "-S", co], check=True, capture_output=True, text=True).stdout
+    secs = {}
+    for line in out.splitlines():
+        m = re.match(r"\s*\[\s*\d+\]\s+(\S+)\s+\S+\s+([0-9a-f]+)\s+([0-9a-f]+)", line)
+        if m:
+            secs[m.group(1)] = (int(m.group(2), 16), int(m.group(3), 16))
+    data = open(co, "rb").read()
+    addr, off = secs[".rodata"]
+    gran = {}
+    for line in out.splitlines():
+        p = line.split()
+        if len(p) >= 8 and p[-1].endswith(".kd"):
+            o = int(p[1], 16) - addr + off
+            gran[p[-1][:-3]] = int.from_bytes(data[o + 48:o + 52], "little") & 63
+    return gran
+
+
+def test_vgpr_allocation_reconciles_rocprof(tmp_path):
+    """rocprofv3's VGPR_Count column reads 128 for the step kernels (profiles/r4e/pmc_*.csv) while the
+    code object's metadata says 253-256 VGPRs: rocprof multiplies the descriptor's granule count by 4,
+    the pre-gfx90a granule, but gfx950 allocates VGPRs in granules of 8. Both numbers come from the
+    same field: (granules) x 8 is the real allocation, and it covers metadata vgpr_count + agpr_count."""
+    md, gran = _kernel_metadata(tmp_path), _descriptor_vgpr_granules(tmp_path)
+    found = 0
+    for name, m in md.items():
+        if not any(f"{len(k)}{k}" in name for k in STEP_KERNELS):
+            continue
+        found += 1
+        g = gran[name] + 1
+        regs = m["vgpr_count"] + m.get("agpr_count", 0)
+        print(f"{name[18:40]}: metadata {regs} regs, descriptor {g} granules -> {8 * g} allocated (rocprof shows {4 * g})")
+        assert 8 * g >= regs > 8 * (g - 1), (name, regs, g)
+    assert found == 2 * len(STEP_KERNELS)
+
+
 def _disassembly(tmp_path):
     tools = [shutil.which("objcopy"), os.path.join(LLVM, "clang-offload-bundler"), os.path.join(LLVM, "llvm-objdump")]
     if not os.path.exists(LIB) or not all(t and os.path.exists(t) for t in tools):
