@@ -10,6 +10,6 @@ run --solver-iterations 0
 run --no-self-collision
 run --solver-iterations 0 --no-self-collision
 run --solver-iterations 8
-run --envs-per-gpu 1024
+run --envs-per-gpu 2048
 run --envs-per-gpu 16384
 run --envs-per-gpu 65536

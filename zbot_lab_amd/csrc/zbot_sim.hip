@@ -1776,6 +1776,11 @@ __device__ __forceinline__ void sens_store(const Q& q, float* __restrict__ st, i
 #ifndef ZB_CARRY
 #define ZB_CARRY 1
 #endif
+// state and observation stores write-through (sc1 vector stores): the bytes leave the XCD L2 as
+// the waves finish instead of in the end-of-kernel write-back (profiles/r4_wt: -0.7 us per step)
+#ifndef ZB_WT_STORES
+#define ZB_WT_STORES 1
+#endif
 __device__ __forceinline__ float& Q::stg(int k) const { return reinterpret_cast<float*>(b + YG_OFF)[e * STG_LEN + k]; }
 // WT >= 0: state row WT is stored with agent scope (the walking kernel's episode length, which a
 // fused finalize may overwrite with the full-reset draw from another XCD, finalize_body)
@@ -1793,7 +1798,8 @@ __device__ __forceinline__ void staged_store(const Q& q, int env0, int N, float*
 #pragma unroll
     for (int f = f0; f < SD; f += WGT / EPW) {
       const float v = S[e * STG_LEN + f];
-      if (WT >= 0 && f == WT) __hip_atomic_store(&st[(size_t)f * N + env], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (ZB_WT_STORES || (WT >= 0 && f == WT))
+        __hip_atomic_store(&st[(size_t)f * N + env], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       else st[(size_t)f * N + env] = v;
     }
 #endif
@@ -1804,7 +1810,11 @@ __device__ __forceinline__ void staged_store(const Q& q, int env0, int N, float*
   const int nv = min(EPW, N - env0);
 #pragma unroll
   for (int t = q.lane; t < EPW * OD; t += WGT)
-    if (t < nv * OD) obs[(size_t)env0 * OD + t] = S[(t / OD) * STG_LEN + SD + t % OD];
+    if (t < nv * OD) {
+      const float v = S[(t / OD) * STG_LEN + SD + t % OD];
+      if (ZB_WT_STORES) __hip_atomic_store(&obs[(size_t)env0 * OD + t], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else obs[(size_t)env0 * OD + t] = v;
+    }
 }
 
 // MDP carry prefetch: the env's MDP state rows (everything after the 25 physics rows) are loaded
