@@ -619,6 +619,13 @@ constexpr int LDS4 = CARRY_OFF + EPW * CARRY_W / 4;
 constexpr int STG_LEN = 88 + 25 + 3;  // >= max state dim + max obs dim + {reward, term, trunc}
 constexpr int LOGR_OFF = (EPW * STG_LEN + 3) / 4;  // region U, after STG
 static_assert(LOGR_OFF + EPW * LOGR_W / 4 <= U_END, "STG + LOGR fit region U");
+// split step kernel (zb_step_split_kernel: a physics wave and a collision wave per workgroup of EPW
+// envs): the hand-off record per env {contacts, overflow, root height, -} and the physics wave's
+// Cholesky stash in its own region (the collision wave builds the world capsules in region V
+// meanwhile)
+constexpr int SPL_OFF = LDS4;
+constexpr int STASH_S_OFF = SPL_OFF + EPW;
+constexpr int LDS4S = STASH_S_OFF + 2 * WGT;
 
 // prologue results the MDP reads after the physics (parked in LDS across the substeps)
 struct Pre {
@@ -649,6 +656,7 @@ struct Q {
   __device__ __forceinline__ const float4* jtab(int j) const { return b + LNK_OFF + JT_OFF + j * 5; }
   __device__ __forceinline__ const float4* btab(int bb) const { return b + LNK_OFF + BT_OFF + bb * 3; }
   __device__ __forceinline__ float4& cap(int l, int k) const { return b[UB_OFF + (2 * l + k) * EPW + e]; }
+  __device__ __forceinline__ float4& spl() const { return b[SPL_OFF + e]; }
   __device__ __forceinline__ const float4* link(int l) const { return gl + l * LINK4; }
   __device__ __forceinline__ int pair_code(int p) const { return reinterpret_cast<const int*>(b + LNK_OFF + NL * LINK4)[p]; }
   __device__ __forceinline__ const float4* dflt() const { return b + LNK_OFF + DFLT_OFF; }
@@ -1956,7 +1964,9 @@ __device__ __forceinline__ void clamp_speeds(MP m, float u[NV]) {
 // ------------------------------------------------------------------------- one substep
 // kLinkFriction: per-contact Coulomb coefficient from the per-link table q.fric (standup DR);
 // otherwise cfg.friction everywhere.
-template <bool kDebugForces, bool kLinkFriction, bool kTgs>
+// kSplit (zb_step_split_kernel): detection runs on the workgroup's collision wave between the two
+// workgroup barriers below, concurrently with this wave's RNEA / CRBA / Cholesky / drives.
+template <bool kDebugForces, bool kLinkFriction, bool kTgs, bool kSplit = false>
 __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
                                         const float target[ND], const Q& q, bool last, bool warm, SensorOut& so,
                                         float (*dbgF)[3], float* dbgTau, Stamps& sp) {
@@ -1980,9 +1990,16 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
   bool over;
   wave_sync();  // the previous substep's LDS readers are done
   fk_team<true>(s, q, Ib, Sown);
-  wave_sync();
-  sp.mark(9);
-  nc = detect(cfg, s.pos[2], q, warm, over, sp);
+  if (kSplit) {
+    if (q.s == 0) q.spl().z = s.pos[2];
+    __syncthreads();  // poses, root heights and the warm-start normals to the collision wave
+    nc = 0;
+    over = false;
+  } else {
+    wave_sync();
+    sp.mark(9);
+    nc = detect(cfg, s.pos[2], q, warm, over, sp);
+  }
   m = opaque(m0);
 
   // RNEA bias forces (qddot = 0, gravity as base acceleration) and, in the same team suffix sum,
@@ -2095,7 +2112,7 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
   float Li[NV];
   // this lane's M row entries of the joint columns, kept for a re-factorisation of the trailing
   // block if a drive saturates (the contact-row granules are dead until the rows are rebuilt)
-  float4* stash = q.b + STASH_OFF + 2 * q.lane;
+  float4* stash = q.b + (kSplit ? STASH_S_OFF : STASH_OFF) + 2 * q.lane;
   stash[0] = make_float4(R[6], R[7], R[8], R[9]);
   stash[1] = make_float4(R[10], R[11], 0.f, 0.f);
   cholesky_team(R, L, Li);
@@ -2150,6 +2167,12 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
   }
 
   sp.mark(4);
+  if (kSplit) {
+    __syncthreads();  // the collision wave's candidates
+    const float4 r = q.spl();
+    nc = __float_as_int(r.x);
+    over = r.y != 0.f;
+  }
   // contact rows (lane s builds slot s): Y = L^-1 J^T (whitened), effective masses, the
   // normal/tangent cross terms and the bias velocity. J of direction d at point x on body b:
   // [x x d ; d ; d.(a_j x (x - o_j)) for joints j < b]
@@ -2731,6 +2754,7 @@ struct FinArgs {
   Counters* cnt;
   int ep_len_row;
   unsigned* done;  // nullptr: not fused
+  int split_role;  // zb_step_split_kernel: which wave runs the physics (0 / 1: wave 0 / 1; 2: by SIMD slot)
 };
 template <bool kFused>
 __device__ __forceinline__ void finalize_body(int N, float* __restrict__ st, float* __restrict__ acc,
@@ -2753,18 +2777,15 @@ __device__ __forceinline__ void load_phys(const float* __restrict__ st, int N, i
 // One policy step per lane. Live state across the 4 substeps is kept to the physics state, the
 // joint targets and the ~15 floats of the lagged observation cache the rewards need; the MDP
 // state is loaded from HBM only after the physics.
-template <bool kTgs>
-__global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_step_kernel(const zb_model* __restrict__ mg,
-                                                          const float4* __restrict__ links, zb_task_cfg cfg, int N,
-                                                          float* __restrict__ st, const float* __restrict__ act,
-                                                          float* __restrict__ obs, float* __restrict__ rew,
-                                                          uint8_t* __restrict__ term, uint8_t* __restrict__ trunc,
-                                                          float* __restrict__ acc, float* __restrict__ wc,
-                                                          FinArgs fa) {
+template <bool kTgs, bool kSplit>
+__device__ __forceinline__ void step_body(const zb_model* __restrict__ mg, const float4* __restrict__ links,
+                                          zb_task_cfg cfg, int N, float* __restrict__ st,
+                                          const float* __restrict__ act, float* __restrict__ obs,
+                                          float* __restrict__ rew, uint8_t* __restrict__ term,
+                                          uint8_t* __restrict__ trunc, float* __restrict__ acc,
+                                          float* __restrict__ wc, FinArgs fa, float4* lds) {
   MP m = to_mp(mg);
-  __shared__ float4 lds[LDS4];
-  static_assert(LDS4 * 4 >= FIN_FG * ACC_STRIDE + ACC, "fused finalize scratch");
-  const int lane = threadIdx.x;
+  const int lane = kSplit ? (int)threadIdx.x & (WGT - 1) : (int)threadIdx.x;  // (split: either wave)
   const int env = xcd_block(blockIdx.x, gridDim.x) * EPW + lane / TL;
   // a team past N recomputes env N-1 (identical values, identical stores); it never logs
   const int i = env < N ? env : N - 1;
@@ -2843,7 +2864,7 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_step_kernel(const z
   sp.mark(0);
   for (int k = 0; k < cfg.decimation; ++k) {
     // (a compile-time `true` here lets the scheduler reshape the loop into a 36 B/lane spill)
-    substep<false, false, kTgs>(m, cfg, p, target, q, opaque_true(), true, so, nullptr, nullptr, sp);
+    substep<false, false, kTgs, kSplit>(m, cfg, p, target, q, opaque_true(), true, so, nullptr, nullptr, sp);
     sens_record(q, k, so);
     sp.mark(7);
     sp.substep_end(k);
@@ -3078,7 +3099,7 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_step_kernel(const z
   // fence and runs zb_finalize_kernel's body. Release / acquire make the hand-over correct under the
   // HIP memory model (the release writes back this XCD's L2: the path costs more than the separate
   // finalize launch it replaces, DESIGN.md §7, and stays off by default).
-  if (fa.done) {
+  if (!kSplit && fa.done) {
     unsigned prev = 0u;
     if (lane == 0) prev = __hip_atomic_fetch_add(fa.done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     prev = __builtin_amdgcn_readfirstlane(prev);
@@ -3089,6 +3110,77 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_step_kernel(const z
   }
 #undef ST
 #undef CST
+}
+
+// kOcc (every step kernel): 2 = up to 256 registers (two waves per SIMD once a launch has more
+// waves than SIMDs); 1 = 512 registers (256 VGPRs + 256 AGPRs claimed), so one wave per SIMD: at
+// N <= 4096 envs (<= 1024 waves) the dispatcher then gives every wave its own SIMD, whereas with
+// two-wave occupancy it doubles up 6-11 % of the SIMDs and leaves as many idle
+// (tools/probe/wave_placement.hip), and the doubled-up waves set the launch's tail.
+template <bool kTgs, int kOcc>
+__global__ __launch_bounds__(WGT, kOcc) void zb_step_kernel(const zb_model* __restrict__ mg,
+                                                          const float4* __restrict__ links, zb_task_cfg cfg, int N,
+                                                          float* __restrict__ st, const float* __restrict__ act,
+                                                          float* __restrict__ obs, float* __restrict__ rew,
+                                                          uint8_t* __restrict__ term, uint8_t* __restrict__ trunc,
+                                                          float* __restrict__ acc, float* __restrict__ wc,
+                                                          FinArgs fa) {
+  __shared__ float4 lds[LDS4];
+  static_assert(LDS4 * 4 >= FIN_FG * ACC_STRIDE + ACC, "fused finalize scratch");
+  if (kOcc == 1) asm volatile("" ::: "a255");
+  step_body<kTgs, false>(mg, links, cfg, N, st, act, obs, rew, term, trunc, acc, wc, fa, lds);
+}
+
+// The collision wave of zb_step_split_kernel: each substep, between the physics wave's two
+// barriers, the ground and self-collision detection of the workgroup's EPW envs (detect, from
+// the poses the physics wave's FK left in LDS) into the candidate list, then the env's contact
+// count and overflow flag into its hand-off record. Same barrier count as the physics wave
+// (2 per substep, cfg.decimation substeps), then it exits.
+__device__ __forceinline__ void collide_wave(const zb_task_cfg& cfg, float4* lds, const float4* __restrict__ links) {
+  const Q q = make_q(lds, (int)threadIdx.x & (WGT - 1), links);
+  Stamps sp;  // (diagnostic build: this wave's stamps are not recorded)
+  for (int k = 0; k < cfg.decimation; ++k) {
+    __syncthreads();
+    bool over = false;
+    const int nc = detect(cfg, q.spl().z, q, true, over, sp);
+    if (q.s == 0) {
+      q.spl().x = __int_as_float(nc);
+      q.spl().y = over ? 1.f : 0.f;
+    }
+    __syncthreads();
+  }
+}
+
+// Walking v2 step with detection on a second wave (ZB_SPLIT, N <= 4096: a launch of one wave per
+// SIMD leaves each SIMD room for a second wave): workgroup = EPW envs x {physics wave, collision
+// wave}; per substep the env's critical path is FK -> max(detection, RNEA + CRBA + Cholesky +
+// drives) -> contact rows -> PGS -> integration instead of their sum. Bit-identical to
+// zb_step_kernel (same instructions per role, same LDS contents at each hand-off).
+template <bool kTgs>
+__global__ __launch_bounds__(2 * WGT, ZB_WAVES_PER_SIMD) void zb_step_split_kernel(
+    const zb_model* __restrict__ mg, const float4* __restrict__ links, zb_task_cfg cfg, int N, float* __restrict__ st,
+    const float* __restrict__ act, float* __restrict__ obs, float* __restrict__ rew, uint8_t* __restrict__ term,
+    uint8_t* __restrict__ trunc, float* __restrict__ acc, float* __restrict__ wc, FinArgs fa) {
+  __shared__ float4 lds[LDS4S];
+  // (scalar, wave-uniform role tests: the compiler must not treat the branch as divergent and run
+  // one role's barriers in the other wave with an empty exec mask)
+  const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x) / WGT;
+  int phys_wave = fa.split_role == 1 ? 1 : 0;
+  if (fa.split_role == 2) {
+    // wave 0 asks for the physics when its (SIMD, wave slot) parity is even, so that the two
+    // waves a SIMD holds (this workgroup's and another's) tend to take different roles
+    if (w == 0 && threadIdx.x == 0) {
+      const unsigned hw = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));  // HW_REG_HW_ID
+      lds[SPL_OFF].w = (float)(((hw & 15u) + ((hw >> 4) & 3u)) & 1u);
+    }
+    __syncthreads();
+    phys_wave = __builtin_amdgcn_readfirstlane((int)lds[SPL_OFF].w);
+  }
+  if (w != phys_wave) {
+    collide_wave(cfg, lds, links);
+    return;
+  }
+  step_body<kTgs, true>(mg, links, cfg, N, st, act, obs, rew, term, trunc, acc, wc, fa, lds);
 }
 
 // Test entry (zb_pair_manifold): GJK (cold start) + the face manifold of n link pairs given as
@@ -3341,14 +3433,15 @@ __device__ __forceinline__ void su_reset_pose(MP m, const zb_task_cfg& cfg, uint
 }
 
 // One stand-up policy step per team (same mapping as zb_step_kernel; no contact sensor).
-template <bool kTgs>
-__global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_su_step_kernel(
+template <bool kTgs, int kOcc>
+__global__ __launch_bounds__(WGT, kOcc) void zb_su_step_kernel(
     const zb_model* __restrict__ mg, const float4* __restrict__ links, zb_task_cfg cfg, int N, float* __restrict__ st,
     const float* __restrict__ act, float* __restrict__ obs, float* __restrict__ rew, uint8_t* __restrict__ term,
     uint8_t* __restrict__ trunc, float* __restrict__ acc, const Counters* __restrict__ cnt, uint64_t seed,
     float* __restrict__ wc) {
   MP m = to_mp(mg);
   __shared__ float4 lds[LDS4];
+  if (kOcc == 1) asm volatile("" ::: "a255");  // (zb_step_kernel: kOcc)
   const int lane = threadIdx.x;
   const int env = xcd_block(blockIdx.x, gridDim.x) * EPW + lane / TL;
   const int i = env < N ? env : N - 1;
@@ -3650,14 +3743,15 @@ struct PreV4 {
 };
 static_assert(sizeof(PreV4) <= 16 * PRE4, "PreV4 fits PRE4 granules");
 
-template <bool kTgs>
-__global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_v4_step_kernel(
+template <bool kTgs, int kOcc>
+__global__ __launch_bounds__(WGT, kOcc) void zb_v4_step_kernel(
     const zb_model* __restrict__ mg, const float4* __restrict__ links, zb_task_cfg cfg, int N, float* __restrict__ st,
     const float* __restrict__ act, float* __restrict__ obs, float* __restrict__ rew, uint8_t* __restrict__ term,
     uint8_t* __restrict__ trunc, float* __restrict__ acc, const Counters* __restrict__ cnt, uint64_t seed,
     float* __restrict__ wc) {
   MP m = to_mp(mg);
   __shared__ float4 lds[LDS4];
+  if (kOcc == 1) asm volatile("" ::: "a255");  // (zb_step_kernel: kOcc)
   const int lane = threadIdx.x;
   const int env = xcd_block(blockIdx.x, gridDim.x) * EPW + lane / TL;
   const int i = env < N ? env : N - 1;
@@ -4163,14 +4257,15 @@ struct PreM {
 };
 static_assert(sizeof(PreM) <= 16 * PRE4, "PreM fits PRE4 granules");
 
-template <bool kTgs>
-__global__ __launch_bounds__(WGT, ZB_M_WAVES_PER_SIMD) void zb_m_step_kernel(
+template <bool kTgs, int kOcc>
+__global__ __launch_bounds__(WGT, kOcc) void zb_m_step_kernel(
     const zb_model* __restrict__ mg, const float4* __restrict__ links, zb_task_cfg cfg, int N, float* __restrict__ st,
     const float* __restrict__ act, float* __restrict__ obs, float* __restrict__ rew, uint8_t* __restrict__ term,
     uint8_t* __restrict__ trunc, float* __restrict__ acc, const Counters* __restrict__ cnt, uint64_t seed,
     float* __restrict__ wc) {
   MP m = to_mp(mg);
   __shared__ float4 lds[LDS4];
+  if (kOcc == 1) asm volatile("" ::: "a255");  // (zb_step_kernel: kOcc)
   const int lane = threadIdx.x;
   const int env = xcd_block(blockIdx.x, gridDim.x) * EPW + lane / TL;
   const int i = env < N ? env : N - 1;
@@ -4804,6 +4899,15 @@ __global__ void zb_finalize_kernel(int N, float* __restrict__ st, float* __restr
 }  // namespace
 
 // =========================================================================== C ABI
+#ifndef ZB_SPLIT_DEFAULT
+#define ZB_SPLIT_DEFAULT 0
+#endif
+#ifndef ZB_OCC1_DEFAULT
+#define ZB_OCC1_DEFAULT 0
+#endif
+#ifndef ZB_SPLIT_ROLE_DEFAULT
+#define ZB_SPLIT_ROLE_DEFAULT 0
+#endif
 #ifndef ZB_FUSED_FINALIZE_DEFAULT
 #define ZB_FUSED_FINALIZE_DEFAULT 0
 #endif
@@ -4831,6 +4935,9 @@ struct zb_sim {
   // ZB_FUSED_FINALIZE=0/1 at create overrides ZB_FUSED_FINALIZE_DEFAULT)
   unsigned* d_done = nullptr;
   bool fused = false;
+  bool split = false;  // walking v2: zb_step_split_kernel (ZB_SPLIT)
+  bool occ1 = false;   // step kernels with one wave per SIMD (kOcc = 1; ZB_OCC1)
+  int split_role = 0;  // ZB_SPLIT_ROLE
 };
 
 static thread_local char g_err[512] = "";
@@ -4910,6 +5017,17 @@ int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_dev
       HIPCHK(hipMemset(h->d_done, 0, sizeof(unsigned)), "hipMemset done counter");
       h->fused = true;
     }
+  }
+  {
+    const char* sv = getenv("ZB_SPLIT");
+    const int sv_on = sv && sv[0] == '1' && sv[1] == 0, sv_off = sv && sv[0] == '0' && sv[1] == 0;
+    h->split = c->task == ZB_TASK_WALKING_V2 && !h->fused && (sv_on || (!sv_off && ZB_SPLIT_DEFAULT && num_envs <= 4096));
+    // one wave per SIMD at <= 4096 envs (<= one wave per SIMD anyway): ZB_OCC1=0/1 overrides
+    const char* oc = getenv("ZB_OCC1");
+    const int oc_on = oc && oc[0] == '1' && oc[1] == 0, oc_off = oc && oc[0] == '0' && oc[1] == 0;
+    h->occ1 = oc_on || (!oc_off && ZB_OCC1_DEFAULT && num_envs <= 4096);
+    const char* sr = getenv("ZB_SPLIT_ROLE");
+    h->split_role = sr && (sr[0] == '1' || sr[0] == '2') && sr[1] == 0 ? sr[0] - '0' : ZB_SPLIT_ROLE_DEFAULT;
   }
   {
     Counters c0;
@@ -5207,7 +5325,10 @@ int zb_step(zb_handle h, const float* actions, float* obs, float* reward, uint8_
   const bool prof = h->prof_n < h->prof_max;
   if (prof) HIPCHK(hipEventRecord(h->prof_ev[2 * h->prof_n], s), "hipEventRecord");
   const bool tgs = h->cfg.solver_mode == 1;
-#define ZB_LAUNCH(K, ...) (tgs ? K<true><<<blocks, WGT, 0, s>>>(__VA_ARGS__) : K<false><<<blocks, WGT, 0, s>>>(__VA_ARGS__))
+  const bool one = h->occ1;
+#define ZB_LAUNCH(K, ...)                                                                          \
+  (tgs ? (one ? K<true, 1><<<blocks, WGT, 0, s>>>(__VA_ARGS__) : K<true, 2><<<blocks, WGT, 0, s>>>(__VA_ARGS__)) \
+       : (one ? K<false, 1><<<blocks, WGT, 0, s>>>(__VA_ARGS__) : K<false, 2><<<blocks, WGT, 0, s>>>(__VA_ARGS__)))
   if (h->task == ZB_TASK_STANDUP_V0)
     ZB_LAUNCH(zb_su_step_kernel, h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward, terminated,
               truncated, h->d_acc, h->d_cnt, h->seed, h->d_wc);
@@ -5219,9 +5340,18 @@ int zb_step(zb_handle h, const float* actions, float* obs, float* reward, uint8_
               truncated, h->d_acc, h->d_cnt, h->seed, h->d_wc);
   else {
     const FinArgs fa = {h->d_log_means, h->d_log_counts, h->u_log_means, h->u_log_counts, log_episode_s(h),
-                        h->seed, h->d_cnt, ZB_S_EP_LEN, h->fused ? h->d_done : nullptr};
-    ZB_LAUNCH(zb_step_kernel, h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward, terminated,
-              truncated, h->d_acc, h->d_wc, fa);
+                        h->seed, h->d_cnt, ZB_S_EP_LEN, h->fused ? h->d_done : nullptr, h->split_role};
+    if (h->split) {
+      if (tgs)
+        zb_step_split_kernel<true><<<blocks, 2 * WGT, 0, s>>>(h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions,
+                                                             obs, reward, terminated, truncated, h->d_acc, h->d_wc, fa);
+      else
+        zb_step_split_kernel<false><<<blocks, 2 * WGT, 0, s>>>(h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions,
+                                                              obs, reward, terminated, truncated, h->d_acc, h->d_wc, fa);
+    } else {
+      ZB_LAUNCH(zb_step_kernel, h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward, terminated,
+                truncated, h->d_acc, h->d_wc, fa);
+    }
   }
 #undef ZB_LAUNCH
   int rc = launch_check("zb_step_kernel");
