@@ -44,7 +44,10 @@ constexpr float RIM_EPS = 1e-3f;  // m; 2% of the module radius (see detect)
 // style): the core is the hull of the two circles moved kCoreM into the shape along their normals
 // with radius r - kCoreM; caps exact, rims rounded (= oracle CORE_M)
 constexpr float kCoreM = 0.004f;
-constexpr int kGjkMaxIt = 16;
+#ifndef ZB_GJK_MAXIT
+#define ZB_GJK_MAXIT 16
+#endif
+constexpr int kGjkMaxIt = ZB_GJK_MAXIT;
 constexpr float kGjkTol = 1e-5f;  // m: GJK stops when its distance bounds are this close
 constexpr float kGjkTilt = 0.01f;  // warm start: tilt of the first three support directions (rad)
 
@@ -4903,7 +4906,7 @@ __global__ void zb_finalize_kernel(int N, float* __restrict__ st, float* __restr
 #define ZB_SPLIT_DEFAULT 0
 #endif
 #ifndef ZB_OCC1_DEFAULT
-#define ZB_OCC1_DEFAULT 0
+#define ZB_OCC1_DEFAULT 1
 #endif
 #ifndef ZB_SPLIT_ROLE_DEFAULT
 #define ZB_SPLIT_ROLE_DEFAULT 0

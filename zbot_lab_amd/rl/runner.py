@@ -59,6 +59,7 @@ class OnPolicyRunner:
         self.alg_cfg = dict(train_cfg["algorithm"])
         self.policy_cfg = dict(train_cfg["policy"])
         self.device = device
+        self._dev_is_cuda = torch.device(device).type == "cuda"
         self.env = env
         self._configure_multi_gpu()
         obs = _policy_obs(self.env.get_observations())
@@ -137,6 +138,8 @@ class OnPolicyRunner:
                     if self.use_graph:
                         self._capture(obs)
                         obs = self._g_obs
+                if self._dev_is_cuda:  # the rollout's GPU time counts as collection, not learning
+                    torch.cuda.synchronize(self.device)
                 collect_time = time.perf_counter() - t0
                 t1 = time.perf_counter()
                 self.alg.compute_returns(obs)
