@@ -315,7 +315,10 @@ typedef struct zb_task_cfg {
    * zbot_cfg.py:637-638 solver_position_iteration_count 4 / velocity 0): solver_iterations
    * sub-iterations of h = sim_dt / solver_iterations, each one sweep whose contact biases are
    * re-linearised from the separation advanced by the normal velocities of the previous ones, the
-   * pose integrated with the mean of the sub-iteration velocities */
+   * pose integrated with the mean of the sub-iteration velocities; 2 = mode 1 plus
+   * the per-position-iteration refresh of the ground contacts: before each sub-iteration after the
+   * first, every ground contact's point (its rim candidate re-supported), separation and Jacobian
+   * rows are re-evaluated at the pose the sub-iterations so far reached (walking v2 and stand-up) */
   int32_t solver_mode;
   /* self-contact manifold (PhysX PCM keeps up to 4 points per convex pair; zbot_cfg.py:636
    * enabled_self_collisions): 1 = a pair whose two nearest features are disk faces (cap on cap)

@@ -350,6 +350,7 @@ typedef struct {
   real x[3];           /* contact point, rel P */
   real n[3];           /* normal: impulse on la along +n */
   real sep;            /* separation (negative = penetration) */
+  int rim;             /* ground: 4 circle + rim rotation of the candidate (ground_rim_point) */
 } contact_t;
 
 /* Candidate list (canonical order): ground candidates link by link (<= NCAND_PER_LINK each),
@@ -892,41 +893,49 @@ int zbo_gjk_pairs(const float* pairs, const float* v0, int n, float margin, floa
  * per link the first NCAND_PER_LINK below the speculative margin are kept. Self: the GJK contact
  * of every non-adjacent link pair (hull_pair; the kernel's broadphase is conservative, so testing
  * all pairs here finds the same candidates). */
+/* ground candidate r (0: the lowest rim point, 1-3: its 90-degree rotations along the rim) of
+ * circle ci of link l at the pose k: the rim angle of the lowest point is biased by RIM_EPS toward
+ * E1 so that a (nearly) flat disk gets a fixed, body-attached 4-point manifold instead of a
+ * rounding-noise direction. Position relative to k's origin. */
+static void ground_rim_point(const mdl_t* m, const kin_t* k, int l, int ci, int r, real x[3]) {
+  const int b = m->link_body[l];
+  const real* R = k->R[b];
+  const real* cd = m->circle[l][ci];
+  real C[3], E1[3], E2[3];
+  m3_v(R, cd, C);
+  m3_v(R, cd + 3, E1);
+  m3_v(R, cd + 6, E2);
+  for (int a = 0; a < 3; ++a) C[a] += k->p[b][a];
+  real al = -E1[2] + (real)RIM_EPS, be = -E2[2];
+  real nrm = sqrtr(al * al + be * be);
+  real cs = 1, sn = 0;
+  if (nrm > (real)1e-12) { cs = al / nrm; sn = be / nrm; }
+  real cr, sr;
+  if (r == 0) { cr = cs; sr = sn; }
+  else if (r == 1) { cr = -sn; sr = cs; }
+  else if (r == 2) { cr = -cs; sr = -sn; }
+  else { cr = sn; sr = -cs; }
+  for (int a = 0; a < 3; ++a) x[a] = C[a] + cr * E1[a] + sr * E2[a];
+}
+
 static void detect(const mdl_t* m, const zb_task_cfg* cfg, const kin_t* k, real Pz, const clist_t* warm,
                    clist_t* L) {
   L->n = 0;
   const real margin = cfg->contact_margin;
   for (int l = 0; l < NL; ++l) {
-    int b = m->link_body[l];
-    const real* R = k->R[b];
+    const real* R = k->R[m->link_body[l]];
     /* cull: bounding sphere entirely above the margin */
     real bc[3];
     m3_v(R, m->bound[l], bc);
-    if (Pz + k->p[b][2] + bc[2] - m->bound[l][3] > margin) continue;
+    if (Pz + k->p[m->link_body[l]][2] + bc[2] - m->bound[l][3] > margin) continue;
     int taken = 0;
     for (int ci = 0; ci < 2; ++ci) {
       if ((m->circle_dup[l] >> ci) & 1) continue; /* mated face: the lower link's candidates stand */
-      const real* cd = m->circle[l][ci];
-      real C[3], E1[3], E2[3];
-      m3_v(R, cd, C);
-      m3_v(R, cd + 3, E1);
-      m3_v(R, cd + 6, E2);
-      for (int a = 0; a < 3; ++a) C[a] += k->p[b][a];
-      /* rim angle of the lowest point, biased by RIM_EPS toward E1 so that a (nearly) flat disk
-       * gets a fixed, body-attached 4-point manifold instead of a rounding-noise direction */
-      real al = -E1[2] + (real)RIM_EPS, be = -E2[2];
-      real nrm = sqrtr(al * al + be * be);
-      real cs = 1, sn = 0;
-      if (nrm > (real)1e-12) { cs = al / nrm; sn = be / nrm; }
       for (int r = 0; r < 4; ++r) {
-        real cr, sr;
-        if (r == 0) { cr = cs; sr = sn; }
-        else if (r == 1) { cr = -sn; sr = cs; }
-        else if (r == 2) { cr = -cs; sr = -sn; }
-        else { cr = sn; sr = -cs; }
         contact_t c;
-        for (int a = 0; a < 3; ++a) c.x[a] = C[a] + cr * E1[a] + sr * E2[a];
+        ground_rim_point(m, k, l, ci, r, c.x);
         c.sep = Pz + c.x[2];
+        c.rim = 4 * ci + r;
         /* the first NCAND_PER_LINK valid candidates in the fixed order (circle 0: lowest, +90,
          * +180, +270 degrees; then circle 1): a fixed order (not a depth sort) keeps the
          * Gauss-Seidel row order independent of rounding when rim points sit at one depth */
@@ -957,7 +966,7 @@ static void detect(const mdl_t* m, const zb_task_cfg* cfg, const kin_t* k, real 
       const int hit = hull_pair(&A, &B, margin, margin, g_gjk_warm ? v0 : NULL, &c);
       if (g_gjk_probe) __atomic_fetch_add(&g_gjk_hist[g_gjk_last_it], 1, __ATOMIC_RELAXED);
       if (hit) {
-        c.la = la; c.lb = lb;
+        c.la = la; c.lb = lb; c.rim = -1;
         contact_t mf[4];
         const int k = cfg->self_manifold && c.sep > -2 * (real)CORE_M + (real)1e-7 ? face_manifold(&A, &B, &c, margin, mf)
                                                                                  : 0;
@@ -1069,6 +1078,36 @@ static void clamp_speeds(const mdl_t* m, real u[NV]) {
   if (w2 > m->wmax * m->wmax) {
     real sc = m->wmax / sqrtr(w2);
     u[0] *= sc; u[1] *= sc; u[2] *= sc;
+  }
+}
+
+/* the pose integration of a substep over time T with the pose velocity ua (root twist at P) and
+ * wv = omega x v_P at the substep start: root origin += T (v + T wv), root orientation by the exact
+ * exponential map, joints += T qdot wrapped as PhysX reports them */
+static void advance_pose(phys_t* s, const real ua[NV], const real wv[3], real T) {
+  for (int a = 0; a < 3; ++a) s->root_pos[a] += T * (ua[3 + a] + T * wv[a]);
+  {
+    const real* om = ua;
+    real th = sqrtr(om[0] * om[0] + om[1] * om[1] + om[2] * om[2]) * T;
+    real dq[4];
+    if (th > (real)1e-12) {
+      real sc = (real)sin((double)(0.5 * th)) / th * T;
+      dq[0] = (real)cos((double)(0.5 * th));
+      dq[1] = om[0] * sc; dq[2] = om[1] * sc; dq[3] = om[2] * sc;
+    } else {
+      dq[0] = 1; dq[1] = (real)0.5 * T * om[0]; dq[2] = (real)0.5 * T * om[1]; dq[3] = (real)0.5 * T * om[2];
+    }
+    real qn[4];
+    q_mul(dq, s->root_quat, qn);
+    q_normalize(qn);
+    for (int a = 0; a < 4; ++a) s->root_quat[a] = qn[a];
+  }
+  for (int j = 0; j < ND; ++j) {
+    real q = s->jq[j] + T * ua[6 + j];
+    /* PhysX reports unlimited revolute joints wrapped to [-2pi, 2pi] (test_articulation.py:19-20) */
+    if (q > (real)TWO_PI) q -= (real)(2 * TWO_PI);
+    else if (q < -(real)TWO_PI) q += (real)(2 * TWO_PI);
+    s->jq[j] = q;
   }
 }
 
@@ -1199,8 +1238,16 @@ static void substep(const mdl_t* m, const zb_task_cfg* cfg, phys_t* s, const rea
   real invm[NC_MAX][3], vmin[NC_MAX], lam[NC_MAX][3], c01[NC_MAX], c02[NC_MAX], muc[NC_MAX], mud[NC_MAX];
   /* TGS-style solve (cfg->solver_mode 1): solver_iterations sub-iterations of h = dt / iterations;
    * sepc = each contact's separation advanced by h times its normal velocity after every
-   * sub-iteration (the bias re-linearised), wsum = the sum of the sub-iterations' w */
-  const int tgs = cfg->solver_mode == 1;
+   * sub-iteration (the bias re-linearised), wsum = the sum of the sub-iterations' w.
+   * solver_mode 2 adds the per-position-iteration refresh of the ground contacts (PhysX TGS,
+   * zbot_cfg.py:637-638): before sub-iteration it > 0 the pose is advanced by it * h with the mean
+   * velocity of the sub-iterations so far (the same integration as the substep's end), and every
+   * ground contact's point (its rim candidate re-supported at that pose), separation and Jacobian
+   * rows are re-evaluated there; the mass matrix and its factor stay the substep's, the rows
+   * keep mapping the root twist at the substep's P. Self contacts keep mode 1's linear advance. */
+  const int tgs = cfg->solver_mode >= 1, refresh = cfg->solver_mode == 2;
+  real wv[3]; /* omega x v_P at the substep start (the classical correction of the root origin) */
+  v3_cross(s->root_angvel, s->root_linvel, wv);
   const real h = dt / (real)cfg->solver_iterations;
   real sepc[NC_MAX], wsum[NV];
   for (int a = 0; a < NV; ++a) wsum[a] = 0;
@@ -1251,6 +1298,40 @@ static void substep(const mdl_t* m, const zb_task_cfg* cfg, phys_t* s, const rea
         sepc[c] += h * vn;
         vmin[c] = contact_bias(cfg, m, sepc[c], h, dt);
       }
+    if (refresh && it > 0) {
+      real wm[NV], um[NV];
+      for (int a = 0; a < NV; ++a) wm[a] = wsum[a] / (real)it;
+      bwd_sub(L, wm, um);
+      clamp_speeds(m, um);
+      phys_t s2 = *s;
+      advance_pose(&s2, um, wv, (real)it * h);
+      kin_t k2;
+      fk(m, &s2, &k2);
+      real dP[3]; /* k2 relative to the substep's P: the rows keep the substep's root reference */
+      for (int a = 0; a < 3; ++a) dP[a] = s2.root_pos[a] - s->root_pos[a];
+      for (int b = 0; b < NB; ++b)
+        for (int a = 0; a < 3; ++a) k2.p[b][a] += dP[a];
+      for (int j = 0; j < ND; ++j)
+        for (int a = 0; a < 3; ++a) k2.org[j][a] += dP[a];
+      for (int c = 0; c < nc; ++c) {
+        const contact_t* ct = &CL.c[c];
+        if (ct->lb >= 0) continue;
+        real x[3];
+        ground_rim_point(m, &k2, ct->la, ct->rim >> 2, ct->rim & 3, x);
+        sepc[c] = s->root_pos[2] + x[2];
+        for (int r = 0; r < 3; ++r) {
+          real J[NV];
+          jac_row(&k2, m->link_body[ct->la], x, dirs[c][r], J);
+          fwd_sub(L, J, Y[c][r]);
+          real yy = 0;
+          for (int a = 0; a < NV; ++a) yy += Y[c][r][a] * Y[c][r][a];
+          invm[c][r] = (real)1 / (yy + (real)1e-9);
+        }
+        c01[c] = 0; c02[c] = 0;
+        for (int a = 0; a < NV; ++a) { c01[c] += Y[c][1][a] * Y[c][0][a]; c02[c] += Y[c][2][a] * Y[c][0][a]; }
+        vmin[c] = contact_bias(cfg, m, sepc[c], h, dt);
+      }
+    }
     for (int c = 0; c < nc; ++c) {
       const real mu = muc[c];
       real vn = 0, v1 = 0, v2 = 0;
@@ -1311,37 +1392,12 @@ static void substep(const mdl_t* m, const zb_task_cfg* cfg, phys_t* s, const rea
 
   /* semi-implicit Euler. u holds the root twist at the fixed point P; the root origin's
    * classical acceleration adds omega x v_P (spatial -> classical). */
-  real wv[3];
-  v3_cross(s->root_angvel, s->root_linvel, wv);
+  advance_pose(s, ua, wv, dt);
   for (int a = 0; a < 3; ++a) {
     s->root_angvel[a] = un[a];
     s->root_linvel[a] = un[3 + a] + dt * wv[a];
-    s->root_pos[a] += dt * (tgs ? ua[3 + a] + dt * wv[a] : s->root_linvel[a]);
   }
-  {
-    const real* om = ua;
-    real th = sqrtr(om[0] * om[0] + om[1] * om[1] + om[2] * om[2]) * dt;
-    real dq[4];
-    if (th > (real)1e-12) {
-      real sc = (real)sin((double)(0.5 * th)) / th * dt;
-      dq[0] = (real)cos((double)(0.5 * th));
-      dq[1] = om[0] * sc; dq[2] = om[1] * sc; dq[3] = om[2] * sc;
-    } else {
-      dq[0] = 1; dq[1] = (real)0.5 * dt * om[0]; dq[2] = (real)0.5 * dt * om[1]; dq[3] = (real)0.5 * dt * om[2];
-    }
-    real qn[4];
-    q_mul(dq, s->root_quat, qn);
-    q_normalize(qn);
-    for (int a = 0; a < 4; ++a) s->root_quat[a] = qn[a];
-  }
-  for (int j = 0; j < ND; ++j) {
-    s->jqd[j] = un[6 + j];
-    real q = s->jq[j] + dt * ua[6 + j];
-    /* PhysX reports unlimited revolute joints wrapped to [-2pi, 2pi] (test_articulation.py:19-20) */
-    if (q > (real)TWO_PI) q -= (real)(2 * TWO_PI);
-    else if (q < -(real)TWO_PI) q += (real)(2 * TWO_PI);
-    s->jq[j] = q;
-  }
+  for (int j = 0; j < ND; ++j) s->jqd[j] = un[6 + j];
 }
 
 /* ------------------------------------------------------------------------- MDP pieces */

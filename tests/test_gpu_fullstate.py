@@ -304,21 +304,24 @@ def test_full_state_deep_overlap(gpu):
     assert nbad <= 0.05 * n
 
 
+@pytest.mark.parametrize("mode", [1, 2], ids=["tgs", "tgs-refresh"])
 @pytest.mark.parametrize("task", ["v2", "standup"])
-def test_full_state_tgs(gpu, task):
+def test_full_state_tgs(gpu, task, mode):
     """The TGS-style contact solve (zb_task_cfg.solver_mode 1: per-sub-iteration re-linearised
-    biases, pose from the mean sub-iteration velocity): one step from random full states and 20
-    zero-action steps from standing, every row under the same explained-outlier rule."""
-    with solver_mode(1):
+    biases, pose from the mean sub-iteration velocity; mode 2 also re-evaluates every ground
+    contact's point, separation and Jacobian rows at each sub-iteration's pose): one step from random
+    full states and 20 zero-action steps from standing, every row under the same explained-outlier
+    rule."""
+    with solver_mode(mode):
         n, seed = 2048, 19
         g, o, cfg, torch = _sims(task, n, seed)
-        assert cfg.solver_mode == 1
+        assert cfg.solver_mode == mode
         st = random_states(task, o, n, seed=111)
         g.set_state(torch.from_numpy(st).cuda())
         a = np.random.default_rng(8).normal(size=(n, 6)).astype(np.float32)
         obs, rew, te, tr = g.step(torch.from_numpy(a).cuda())
         g_out = (obs.cpu().numpy(), rew.cpu().numpy(), te.cpu().numpy().copy(), tr.cpu().numpy().copy())
-        nbad = _check(task, "TGS: one step from random full states", n, seed, st, [a], g_out,
+        nbad = _check(task, f"TGS mode {mode}: one step from random full states", n, seed, st, [a], g_out,
                       g.get_state().cpu().numpy(), torch)
         assert nbad <= 0.02 * n
         n, seed, steps = 1024, 6, 20
@@ -329,7 +332,7 @@ def test_full_state_tgs(gpu, task):
         for _ in range(steps):
             obs, rew, te, tr = g.step(at)
         g_out = (obs.cpu().numpy(), rew.cpu().numpy(), te.cpu().numpy().copy(), tr.cpu().numpy().copy())
-        nbad = _check(task, f"TGS: {steps} zero-action steps from standing", n, seed, st,
+        nbad = _check(task, f"TGS mode {mode}: {steps} zero-action steps from standing", n, seed, st,
                       [np.zeros((n, 6), np.float32)] * steps, g_out, g.get_state().cpu().numpy(), torch)
         # (20 TGS steps of standing contact: 4.8-5.1 % of envs end outside tolerance, every one
         # explained; the f64-baseline aggregate in _check bounds the fraction, this is a sanity cap)

@@ -53,6 +53,7 @@ def test_step_kernels_fit_two_waves_per_simd(tmp_path):
         found += 1
         tgs = "ILb1E" in name  # template argument kTgs
         occ1 = "ELi1E" in name  # template argument kOcc = 1: one wave per SIMD (<= 4096 envs)
+        refresh = "ELb1EE" in name  # template argument kRefresh: the opt-in TGS refresh (solver_mode 2)
         lds = md["group_segment_fixed_size"]
         regs = md["vgpr_count"]  # (gfx950 metadata: the unified total, AGPRs included)
         scratch = md.get("private_segment_fixed_size", 0)
@@ -61,8 +62,12 @@ def test_step_kernels_fit_two_waves_per_simd(tmp_path):
             assert regs > 256 and regs <= 512 and scratch == 0, (short, regs, scratch)
             continue
         assert regs <= 256, f"{short}: {regs} VGPRs + AGPRs (> 256: one wave per SIMD)"
+        if refresh:  # opt-in, not benchmarked: the refresh's FK + row rebuild inside the sweeps spills
+            assert scratch <= 256, f"{short} (TGS refresh): {scratch} B of scratch per lane"
+            continue
         assert scratch <= 64, f"{short}{' (TGS)' if tgs else ''}: {scratch} B of scratch per lane"
-    assert found == 4 * len(STEP_KERNELS), sorted(kernels)  # PGS / TGS x occupancy 1 / 2
+    # PGS / TGS x occupancy 1 / 2, plus the TGS refresh (occupancy 2) of walking v2 and stand-up
+    assert found == 4 * len(STEP_KERNELS) + 2, sorted(kernels)
 
 
 def _descriptor_vgpr_granules(tmp_path):
@@ -107,7 +112,7 @@ def test_vgpr_allocation_reconciles_rocprof(tmp_path):
         regs = m["vgpr_count"]  # (unified total)
         print(f"{name[18:40]}: metadata {regs} regs, descriptor {g} granules -> {8 * g} allocated (rocprof shows {4 * g})")
         assert 8 * g >= regs > 8 * (g - 1), (name, regs, g)
-    assert found == 4 * len(STEP_KERNELS)
+    assert found == 4 * len(STEP_KERNELS) + 2
 
 
 def _disassembly(tmp_path):

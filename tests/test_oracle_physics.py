@@ -188,3 +188,57 @@ def test_static_friction_raised_to_dynamic():
     for _ in range(40):
         s.step(a_rng.normal(size=(n, 6)).astype(np.float32))
     assert not np.array_equal(s.get_state()[:25], runs[1][:25])
+
+
+def _tgs_cfg(mode, **kw):
+    return zm.TaskCfg(solver_mode=mode, **kw)
+
+
+def test_tgs_refresh_standing_is_stable():
+    """solver_mode 2 (TGS with the per-position-iteration refresh of the ground contacts,
+    zbot_cfg.py:637-638): 5 s of zero actions from the default pose stay upright with both feet
+    carrying the weight, as with the other solves."""
+    n = 8
+    s = _sim(n, _tgs_cfg(2))
+    s.reset()
+    st = s.get_state()
+    st[S["EP_LEN"]] = 0
+    s.set_state(st)
+    for _ in range(250):
+        _, r, term, trunc = s.step(np.zeros((n, 6), np.float32))
+        assert not term.any()
+    p, _ = s.link_poses()
+    np.testing.assert_allclose(p[:, 6, 2], 0.2545, atol=2e-3)
+    out = s.get_state()
+    assert np.abs(out[S["JOINT_VEL"]:S["JOINT_VEL"] + 6]).max() < 0.1
+    fz = out[S["FEET_FZ_HIST"]:S["FEET_FZ_HIST"] + 2]
+    np.testing.assert_allclose(fz.sum(axis=0), 3.005 * 9.81, rtol=0.05)
+
+
+def test_tgs_refresh_touches_ground_contacts_only():
+    """The refresh re-evaluates ground contacts only: airborne envs (self contacts allowed) step
+    bit-identically under modes 1 and 2, and so does every env with a single sub-iteration (no
+    refresh point); envs resting on the ground differ, by less than the solve's own convergence
+    scale."""
+    n = 32
+    st = _airborne(n, seed=11, jqd_sigma=3.0, vel=0.5)
+    tg = st[S["JOINT_POS"]:S["JOINT_POS"] + 6].T.copy() + 0.3
+    outs = []
+    for mode in (1, 2):
+        s = _sim(n, _tgs_cfg(mode))
+        s.set_state(st)
+        s.physics_substeps(tg, 4)
+        outs.append(s.get_state())
+    np.testing.assert_array_equal(outs[0], outs[1])
+    ground = perturbed_states(n, seed=12)
+    outs = []
+    for mode, iters in ((1, 1), (2, 1), (1, 4), (2, 4)):
+        s = _sim(n, _tgs_cfg(mode, solver_iterations=iters))
+        s.set_state(ground)
+        s.physics_substeps(ground[S["JOINT_POS"]:S["JOINT_POS"] + 6].T.copy(), 4)
+        outs.append(s.get_state())
+    np.testing.assert_array_equal(outs[0], outs[1])
+    d = np.abs(outs[3] - outs[2])
+    assert d.max() > 0  # the refresh acts on ground contacts
+    v = S["JOINT_VEL"]
+    assert d[v:v + 6].max() < 0.5, d[v:v + 6].max()

@@ -1964,12 +1964,138 @@ __device__ __forceinline__ void clamp_speeds(MP m, float u[NV]) {
   u[0] *= sc; u[1] *= sc; u[2] *= sc;
 }
 
+// ground rim candidate r (0: the lowest rim point, 1-3: its 90-degree rotations) of circle ci of
+// link l at the pose in LDS, relative to that pose's root origin: detect's formula (oracle
+// ground_rim_point). Used by the TGS refresh (kRefresh).
+__device__ __forceinline__ void ground_rim_point(const Q& q, int l, int ci, int r, float x[3]) {
+  float R[9], p[3];
+  read_frame(q, link_body(l), R, p);
+  const float4* L = q.link(l);
+  float C[3], E1[3], E2[3];
+  mv3f(R, L[1 + 3 * ci], C);
+  mv3f(R, L[2 + 3 * ci], E1);
+  mv3f(R, L[3 + 3 * ci], E2);
+  C[0] += p[0]; C[1] += p[1]; C[2] += p[2];
+  const float al = -E1[2] + RIM_EPS, be = -E2[2];
+  const float nrm = sqrtf(al * al + be * be);
+  float c0 = 1.f, s0 = 0.f;
+  if (nrm > 1e-12f) { c0 = al / nrm; s0 = be / nrm; }
+  const float cr = r == 0 ? c0 : (r == 1 ? -s0 : (r == 2 ? -c0 : s0));
+  const float sr = r == 0 ? s0 : (r == 1 ? c0 : (r == 2 ? -s0 : -c0));
+#pragma unroll
+  for (int a = 0; a < 3; ++a) x[a] = C[a] + cr * E1[a] + sr * E2[a];
+}
+
+// the pose integration of a substep over time T with the pose velocity ua (root twist at P) and
+// wv = omega x v_P at the substep start (oracle advance_pose): root origin += T (v + T wv), the
+// orientation by the exact exponential map, joints += T qdot wrapped as PhysX reports them
+__device__ __forceinline__ void advance_pose(Phys& s, const float ua[NV], const float wv[3], float T) {
+#pragma unroll
+  for (int a = 0; a < 3; ++a) s.pos[a] += T * (ua[3 + a] + T * wv[a]);
+  {
+    const float th = sqrtf(ua[0] * ua[0] + ua[1] * ua[1] + ua[2] * ua[2]) * T;
+    float dq[4];
+    if (th > 1e-12f) {
+      float sn, cs;
+      sincos_r(0.5f * th, &sn, &cs);
+      const float sc = sn / th * T;
+      dq[0] = cs; dq[1] = ua[0] * sc; dq[2] = ua[1] * sc; dq[3] = ua[2] * sc;
+    } else {
+      dq[0] = 1.f; dq[1] = 0.5f * T * ua[0]; dq[2] = 0.5f * T * ua[1]; dq[3] = 0.5f * T * ua[2];
+    }
+    float qn[4];
+    qmul(dq, s.quat, qn);
+    qnormalize(qn);
+    s.quat[0] = qn[0]; s.quat[1] = qn[1]; s.quat[2] = qn[2]; s.quat[3] = qn[3];
+  }
+#pragma unroll
+  for (int j = 0; j < ND; ++j) {
+    float qv = s.jq[j] + T * ua[6 + j];
+    if (qv > TWO_PI_F) qv -= 2.f * TWO_PI_F;
+    else if (qv < -TWO_PI_F) qv += 2.f * TWO_PI_F;
+    s.jq[j] = qv;
+  }
+}
+
+// TGS per-position-iteration refresh of the ground contacts (solver_mode 2; oracle substep,
+// `refresh`): the pose after T = it h with the mean velocity of the sub-iterations so far
+// (wm = this lane's coordinate of the mean w; the same integration as the substep's end), FK
+// there, and lane c re-evaluates its ground contact: the rim candidate re-supported at that pose,
+// the separation, the three Jacobian rows (the root columns still at the substep's P, the mass
+// matrix factor the substep's), the effective masses, cross terms and bias. Self contacts keep the
+// linear advance. The LDS pose records hold the refreshed pose afterwards (nothing later in the
+// substep reads them; the next substep's FK rewrites them).
+__device__ __forceinline__ void refresh_ground(const zb_task_cfg& cfg, MP m, const Phys& s, const Q& q, const float L[NT],
+                                            const float Li[NV], float wm, float T, float hsub, float dt, int nc,
+                                            int rim_own, int gl_own, float& sep_own) {
+  float w[NV], um[NV];
+  w[0] = tb<own_lane(0)>(wm); w[1] = tb<own_lane(1)>(wm); w[2] = tb<own_lane(2)>(wm);
+  w[3] = tb<own_lane(3)>(wm); w[4] = tb<own_lane(4)>(wm); w[5] = tb<own_lane(5)>(wm);
+  w[6] = tb<own_lane(6)>(wm); w[7] = tb<own_lane(7)>(wm); w[8] = tb<own_lane(8)>(wm);
+  w[9] = tb<own_lane(9)>(wm); w[10] = tb<own_lane(10)>(wm); w[11] = tb<own_lane(11)>(wm);
+  bwd_sub(L, Li, w, um);
+  clamp_speeds(m, um);
+  float wv[3];
+  cross3(s.av, s.lv, wv);
+  Phys p2 = s;
+  advance_pose(p2, um, wv, T);
+  wave_sync();
+  fk_team_pose(p2, q);
+  wave_sync();
+  if (q.s < nc && rim_own >= 0) {
+    const int c = q.s;
+    float x[3];
+    ground_rim_point(q, gl_own, rim_own >> 2, rim_own & 3, x);
+    const float sep = p2.pos[2] + x[2];
+    const float xr[3] = {x[0] + (p2.pos[0] - s.pos[0]), x[1] + (p2.pos[1] - s.pos[1]), x[2] + (p2.pos[2] - s.pos[2])};
+    float S[ND][6], org[ND][3];
+    read_joints(q, S, org);
+    const int ba = link_body(gl_own);
+    float cj[ND][3];
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+      const float xo[3] = {x[0] - org[j][0], x[1] - org[j][1], x[2] - org[j][2]};
+      float c3[3];
+      cross3(S[j], xo, c3);
+      const float sg = j < ba ? 1.f : 0.f;
+      cj[j][0] = sg * c3[0]; cj[j][1] = sg * c3[1]; cj[j][2] = sg * c3[2];
+    }
+    const float n[3] = {0.f, 0.f, 1.f};
+    float t1[3], t2[3];
+    tangents(n, t1, t2);
+    float invm[3], Y[3][NV];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      float d[3];
+#pragma unroll
+      for (int a = 0; a < 3; ++a) d[a] = r == 0 ? n[a] : (r == 1 ? t1[a] : t2[a]);
+      float J[NV], xd[3];
+      cross3(xr, d, xd);
+      J[0] = xd[0]; J[1] = xd[1]; J[2] = xd[2];
+      J[3] = d[0]; J[4] = d[1]; J[5] = d[2];
+#pragma unroll
+      for (int j = 0; j < ND; ++j) J[6 + j] = dot3(cj[j], d);
+      fwd_sub(L, Li, J, Y[r]);
+      invm[r] = 1.f / (dot12(Y[r], Y[r]) + 1e-9f);
+    }
+#pragma unroll
+    for (int d = 0; d < NV; ++d) q.yg_at(c, own_lane(d)) = make_float4(Y[0][d], Y[1][d], Y[2][d], 0.f);
+    sep_own = sep;
+    const float4 a1 = q.aux(c, 1);
+    q.aux(c, 0) = make_float4(invm[0], invm[1], invm[2], contact_bias(cfg, m, sep, hsub, dt) * invm[0]);
+    q.aux(c, 1) = make_float4(dot12(Y[1], Y[0]) * invm[1], dot12(Y[2], Y[0]) * invm[2], a1.z, a1.w);
+  }
+  wave_sync();
+}
+
 // ------------------------------------------------------------------------- one substep
 // kLinkFriction: per-contact Coulomb coefficient from the per-link table q.fric (standup DR);
 // otherwise cfg.friction everywhere.
 // kSplit (zb_step_split_kernel): detection runs on the workgroup's collision wave between the two
 // workgroup barriers below, concurrently with this wave's RNEA / CRBA / Cholesky / drives.
-template <bool kDebugForces, bool kLinkFriction, bool kTgs, bool kSplit = false>
+// kRefresh (zb_task_cfg.solver_mode 2, with kTgs): before every sub-iteration after the first the
+// ground contacts are re-evaluated at the pose the sub-iterations so far reached (see the sweeps).
+template <bool kDebugForces, bool kLinkFriction, bool kTgs, bool kSplit = false, bool kRefresh = false>
 __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
                                         const float target[ND], const Q& q, bool last, bool warm, SensorOut& so,
                                         float (*dbgF)[3], float* dbgTau, Stamps& sp) {
@@ -2187,6 +2313,7 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
   constexpr bool tgs = kTgs;
   const float hsub = dt / (float)cfg.solver_iterations;
   float sep_own = 0.f;
+  int rim_own = -1, gl_own = 0;  // kRefresh: slot q.s's ground link and rim candidate (4 ci + r)
   if (q.s < nc) {
     const int c = q.s;
     const int pos = over ? q.map(c) : c;
@@ -2203,6 +2330,18 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
     const int ba = link_body(code >> 4);
     const int lb = (code & 15) - 1;
     const int bb = lb >= 0 ? link_body(lb) : -1;
+    if (kRefresh && lb < 0) {
+      // which rim candidate detect made this point from: the nearest of the link's 8 at this pose
+      gl_own = code >> 4;
+      float best = 3.4e38f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float xc[3];
+        ground_rim_point(q, gl_own, k >> 2, k & 3, xc);
+        const float d2 = (xc[0] - x[0]) * (xc[0] - x[0]) + (xc[1] - x[1]) * (xc[1] - x[1]) + (xc[2] - x[2]) * (xc[2] - x[2]);
+        if (d2 < best) { best = d2; rim_own = k; }
+      }
+    }
     // per-joint lever vectors a_j x (x - o_j), signed by which side of the contact the joint is on
     float cj[ND][3];
 #pragma unroll
@@ -2290,6 +2429,8 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
           q.aux(q.s, 0) = make_float4(a0.x, a0.y, a0.z, contact_bias(cfg, m, sep_own, hsub, dt) * a0.x);
         }
         wave_sync();
+        if (kRefresh) refresh_ground(cfg, m, s, q, L, Li, wsum / (float)it, (float)it * hsub, hsub, dt, nc, rim_own,
+                                     gl_own, sep_own);
       }
       float4 G = q.yg(yl, 0), X = q.aux(0, 0), Z = q.aux(0, 1), La = q.lam(0);
 #pragma unroll
@@ -2780,7 +2921,7 @@ __device__ __forceinline__ void load_phys(const float* __restrict__ st, int N, i
 // One policy step per lane. Live state across the 4 substeps is kept to the physics state, the
 // joint targets and the ~15 floats of the lagged observation cache the rewards need; the MDP
 // state is loaded from HBM only after the physics.
-template <bool kTgs, bool kSplit>
+template <bool kTgs, bool kSplit, bool kRefresh = false>
 __device__ __forceinline__ void step_body(const zb_model* __restrict__ mg, const float4* __restrict__ links,
                                           zb_task_cfg cfg, int N, float* __restrict__ st,
                                           const float* __restrict__ act, float* __restrict__ obs,
@@ -2867,7 +3008,7 @@ __device__ __forceinline__ void step_body(const zb_model* __restrict__ mg, const
   sp.mark(0);
   for (int k = 0; k < cfg.decimation; ++k) {
     // (a compile-time `true` here lets the scheduler reshape the loop into a 36 B/lane spill)
-    substep<false, false, kTgs, kSplit>(m, cfg, p, target, q, opaque_true(), true, so, nullptr, nullptr, sp);
+    substep<false, false, kTgs, kSplit, kRefresh>(m, cfg, p, target, q, opaque_true(), true, so, nullptr, nullptr, sp);
     sens_record(q, k, so);
     sp.mark(7);
     sp.substep_end(k);
@@ -3120,7 +3261,7 @@ __device__ __forceinline__ void step_body(const zb_model* __restrict__ mg, const
 // N <= 4096 envs (<= 1024 waves) the dispatcher then gives every wave its own SIMD, whereas with
 // two-wave occupancy it doubles up 6-11 % of the SIMDs and leaves as many idle
 // (tools/probe/wave_placement.hip), and the doubled-up waves set the launch's tail.
-template <bool kTgs, int kOcc>
+template <bool kTgs, int kOcc, bool kRefresh = false>
 __global__ __launch_bounds__(WGT, kOcc) void zb_step_kernel(const zb_model* __restrict__ mg,
                                                           const float4* __restrict__ links, zb_task_cfg cfg, int N,
                                                           float* __restrict__ st, const float* __restrict__ act,
@@ -3131,7 +3272,7 @@ __global__ __launch_bounds__(WGT, kOcc) void zb_step_kernel(const zb_model* __re
   __shared__ float4 lds[LDS4];
   static_assert(LDS4 * 4 >= FIN_FG * ACC_STRIDE + ACC, "fused finalize scratch");
   if (kOcc == 1) asm volatile("" ::: "a255");
-  step_body<kTgs, false>(mg, links, cfg, N, st, act, obs, rew, term, trunc, acc, wc, fa, lds);
+  step_body<kTgs, false, kRefresh>(mg, links, cfg, N, st, act, obs, rew, term, trunc, acc, wc, fa, lds);
 }
 
 // The collision wave of zb_step_split_kernel: each substep, between the physics wave's two
@@ -3318,7 +3459,7 @@ __global__ void zb_observe_kernel(const zb_model* __restrict__ mg, int N, const 
   write_obs(m, p, d, obs, i);
 }
 
-template <bool kLinkFriction, bool kTgs>
+template <bool kLinkFriction, bool kTgs, bool kRefresh = false>
 __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_substeps_kernel(const zb_model* __restrict__ mg,
                                                               const float4* __restrict__ links, zb_task_cfg cfg, int N,
                                                               float* __restrict__ st, const float* __restrict__ targets,
@@ -3344,7 +3485,8 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_substeps_kernel(con
   for (int j = 0; j < ND; ++j) { tg[j] = targets[(size_t)i * ND + j]; tau[j] = 0.f; }
   SensorOut so;
   Stamps sp;
-  for (int k = 0; k < nsub; ++k) substep<true, kLinkFriction, kTgs>(m, cfg, p, tg, q, k == nsub - 1, k > 0, so, F, tau, sp);
+  for (int k = 0; k < nsub; ++k)
+    substep<true, kLinkFriction, kTgs, false, kRefresh>(m, cfg, p, tg, q, k == nsub - 1, k > 0, so, F, tau, sp);
   if (net_force && q.s < NL)
 #pragma unroll
     for (int a = 0; a < 3; ++a) net_force[((size_t)i * NL + q.s) * 3 + a] = F[0][a];
@@ -3436,7 +3578,7 @@ __device__ __forceinline__ void su_reset_pose(MP m, const zb_task_cfg& cfg, uint
 }
 
 // One stand-up policy step per team (same mapping as zb_step_kernel; no contact sensor).
-template <bool kTgs, int kOcc>
+template <bool kTgs, int kOcc, bool kRefresh = false>
 __global__ __launch_bounds__(WGT, kOcc) void zb_su_step_kernel(
     const zb_model* __restrict__ mg, const float4* __restrict__ links, zb_task_cfg cfg, int N, float* __restrict__ st,
     const float* __restrict__ act, float* __restrict__ obs, float* __restrict__ rew, uint8_t* __restrict__ term,
@@ -3485,7 +3627,7 @@ __global__ __launch_bounds__(WGT, kOcc) void zb_su_step_kernel(
   wc_load(q, wc, N, i);  // the first substep's GJK warm start
   sp.mark(0);
   for (int k = 0; k < cfg.decimation; ++k) {
-    substep<false, true, kTgs>(m, cfg, p, target, q, false, true, so, nullptr, nullptr, sp);
+    substep<false, true, kTgs, false, kRefresh>(m, cfg, p, target, q, false, true, so, nullptr, nullptr, sp);
     sp.mark(7);
   }
   m = opaque(m);
@@ -4988,8 +5130,10 @@ int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_dev
     if (np != m->num_self_pairs) return set_err(-1, "zb_create: self-collision pair count", hipSuccess);
   }
   if (c->decimation < 1 || c->decimation > MAXSUB || c->solver_iterations < 0 || c->solver_mode < 0 ||
-      c->solver_mode > 1 || (c->solver_mode == 1 && c->solver_iterations < 1))
-    return set_err(-1, "zb_create: cfg (decimation 1..8, solver_iterations >= 0, solver_mode 0 / 1 with iterations >= 1)",
+      c->solver_mode > 2 || (c->solver_mode >= 1 && c->solver_iterations < 1) ||
+      (c->solver_mode == 2 && c->task != ZB_TASK_WALKING_V2 && c->task != ZB_TASK_STANDUP_V0))
+    return set_err(-1, "zb_create: cfg (decimation 1..8, solver_iterations >= 0, solver_mode 0 / 1 / 2 with iterations "
+                       ">= 1; mode 2 for walking v2 and stand-up)",
                    hipSuccess);
   if (c->task != ZB_TASK_WALKING_V2 && c->task != ZB_TASK_STANDUP_V0 && c->task != ZB_TASK_WALKING_V4 &&
       c->task != ZB_TASK_MANAGER_V0)
@@ -5024,7 +5168,7 @@ int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_dev
   {
     const char* sv = getenv("ZB_SPLIT");
     const int sv_on = sv && sv[0] == '1' && sv[1] == 0, sv_off = sv && sv[0] == '0' && sv[1] == 0;
-    h->split = c->task == ZB_TASK_WALKING_V2 && !h->fused && (sv_on || (!sv_off && ZB_SPLIT_DEFAULT && num_envs <= 4096));
+    h->split = c->task == ZB_TASK_WALKING_V2 && !h->fused && c->solver_mode != 2 && (sv_on || (!sv_off && ZB_SPLIT_DEFAULT && num_envs <= 4096));
     // one wave per SIMD at <= 4096 envs (<= one wave per SIMD anyway): ZB_OCC1=0/1 overrides
     const char* oc = getenv("ZB_OCC1");
     const int oc_on = oc && oc[0] == '1' && oc[1] == 0, oc_off = oc && oc[0] == '0' && oc[1] == 0;
@@ -5327,13 +5471,16 @@ int zb_step(zb_handle h, const float* actions, float* obs, float* reward, uint8_
   const int blocks = (h->n + EPW - 1) / EPW;
   const bool prof = h->prof_n < h->prof_max;
   if (prof) HIPCHK(hipEventRecord(h->prof_ev[2 * h->prof_n], s), "hipEventRecord");
-  const bool tgs = h->cfg.solver_mode == 1;
+  const bool tgs = h->cfg.solver_mode >= 1, refresh = h->cfg.solver_mode == 2;
   const bool one = h->occ1;
 #define ZB_LAUNCH(K, ...)                                                                          \
   (tgs ? (one ? K<true, 1><<<blocks, WGT, 0, s>>>(__VA_ARGS__) : K<true, 2><<<blocks, WGT, 0, s>>>(__VA_ARGS__)) \
        : (one ? K<false, 1><<<blocks, WGT, 0, s>>>(__VA_ARGS__) : K<false, 2><<<blocks, WGT, 0, s>>>(__VA_ARGS__)))
+  // solver_mode 2 (the TGS refresh): walking v2 and stand-up only (zb_create), two-wave occupancy
+#define ZB_LAUNCH_R(K, ...)                                                                        \
+  (refresh ? K<true, 2, true><<<blocks, WGT, 0, s>>>(__VA_ARGS__) : ZB_LAUNCH(K, __VA_ARGS__))
   if (h->task == ZB_TASK_STANDUP_V0)
-    ZB_LAUNCH(zb_su_step_kernel, h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward, terminated,
+    ZB_LAUNCH_R(zb_su_step_kernel, h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward, terminated,
               truncated, h->d_acc, h->d_cnt, h->seed, h->d_wc);
   else if (h->task == ZB_TASK_WALKING_V4)
     ZB_LAUNCH(zb_v4_step_kernel, h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward, terminated,
@@ -5352,10 +5499,11 @@ int zb_step(zb_handle h, const float* actions, float* obs, float* reward, uint8_
         zb_step_split_kernel<false><<<blocks, 2 * WGT, 0, s>>>(h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions,
                                                               obs, reward, terminated, truncated, h->d_acc, h->d_wc, fa);
     } else {
-      ZB_LAUNCH(zb_step_kernel, h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward, terminated,
+      ZB_LAUNCH_R(zb_step_kernel, h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward, terminated,
                 truncated, h->d_acc, h->d_wc, fa);
     }
   }
+#undef ZB_LAUNCH_R
 #undef ZB_LAUNCH
   int rc = launch_check("zb_step_kernel");
   if (prof) {
@@ -5469,15 +5617,18 @@ int zb_physics_substeps(zb_handle h, const float* targets, int nsub, float* net_
                         void* stream) {
   if (!h || !targets || nsub < 1) return set_err(-1, "zb_physics_substeps", hipSuccess);
   const int blocks = (h->n + EPW - 1) / EPW;
-  const bool dr = h->task == ZB_TASK_STANDUP_V0 || h->task == ZB_TASK_MANAGER_V0, tgs = h->cfg.solver_mode == 1;
-#define ZB_SUB(F, T) zb_substeps_kernel<F, T><<<blocks, WGT, 0, (hipStream_t)stream>>>(h->d_model, h->d_links, h->cfg, \
-                                                 h->n, h->d_state, targets, nsub, net_force, applied_torque)
+  const bool dr = h->task == ZB_TASK_STANDUP_V0 || h->task == ZB_TASK_MANAGER_V0, tgs = h->cfg.solver_mode >= 1;
+  const bool refresh = h->cfg.solver_mode == 2;
+#define ZB_SUB(F, T, R) zb_substeps_kernel<F, T, R><<<blocks, WGT, 0, (hipStream_t)stream>>>(h->d_model, h->d_links, \
+                                                 h->cfg, h->n, h->d_state, targets, nsub, net_force, applied_torque)
   if (dr) {
-    if (tgs) ZB_SUB(true, true);
-    else ZB_SUB(true, false);
+    if (refresh) ZB_SUB(true, true, true);
+    else if (tgs) ZB_SUB(true, true, false);
+    else ZB_SUB(true, false, false);
   } else {
-    if (tgs) ZB_SUB(false, true);
-    else ZB_SUB(false, false);
+    if (refresh) ZB_SUB(false, true, true);
+    else if (tgs) ZB_SUB(false, true, false);
+    else ZB_SUB(false, false, false);
   }
 #undef ZB_SUB
   const int rc = launch_check("zb_substeps_kernel");
