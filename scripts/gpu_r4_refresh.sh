@@ -7,3 +7,5 @@ timeout -k 10 420 python -u -m pytest tests/test_gpu_fullstate.py tests/test_gpu
 rc=$?; grep -E "^(FAILED|ERROR)|passed|failed|unexplained" $O/test_refresh.log | tail -12
 case $rc in 0|1) ;; *) exit $rc ;; esac
 bash scripts/gpu_round4.sh $TAG
+timeout -k 10 300 env ZBOT_LIB=libzbot_stamps_t.so python scripts/wave_times.py > $O/wave_times.log 2>&1 || { tail -5 $O/wave_times.log; exit 1; }
+grep -v amdgpu.ids $O/wave_times.log | head -30

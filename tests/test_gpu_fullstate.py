@@ -120,12 +120,12 @@ def _sensitivity(task, n, seed, st, actions, so, obs_o, rew_o, fl_o, before, nst
     return fam
 
 
-def _refine(task, n, seed, st, actions, so, obs_o, rew_o, fl_o, before, nsteps, wc=None, k=32):
+def _refine(task, n, seed, st, actions, so, obs_o, rew_o, fl_o, before, nsteps, wc=None, k=32, rseed=4321):
     """A second, larger draw of the rounding-scale families (k runs: 3/4 at 1e-6, 1/4 at 1e-5, a new
     random stream) for a check that still has unexplained envs after the first K_SENS draws: the
     envelope is a maximum over random perturbations, and a discrete event (a contact switching on,
     a sensor threshold) is reached by some perturbation directions only."""
-    rng = np.random.default_rng(4321)
+    rng = np.random.default_rng(rseed)
     fam = {"1e-6": np.zeros(n), "1e-5": np.zeros(n)}
     for j in range(k):
         scale, f = (1.0, "1e-6") if j < 3 * k // 4 else (10.0, "1e-5")
@@ -185,6 +185,9 @@ def _row_names(task):
 # implementations of one algorithm, each against the f64 one):
 # frac <= AGG_FRAC_K x baseline + AGG_FRAC_ABS and median <= AGG_MED_K x baseline + AGG_MED_ABS.
 AGG_FRAC_K, AGG_FRAC_ABS = 2.0, 0.005
+# at most this many envs still unexplained after the 32-run refinement get a deep draw of
+# REFINE_DEEP_RUNS rounding-scale runs (a quarter of that for multi-step checks); more fail at once
+REFINE_DEEP_MAX, REFINE_DEEP_RUNS = 4, 1024
 AGG_MED_K, AGG_MED_ABS = 4.0, 0.02
 
 
@@ -236,6 +239,20 @@ def _check(task, label, n, seed, st, actions, g_out, sg, torch, wc=None, stats=N
         print(f"  refined envelope (32 more rounding-scale runs) for {len(unexplained)} unexplained envs: "
               + ", ".join(f"env {e} ratio {ratio[e]:.3g} envelope {sens[e]:.3g}" for e in unexplained[:8])
               + f"; still unexplained {len(still)}")
+        if 0 < len(still) <= REFINE_DEEP_MAX:
+            # a rare discrete event: the oracle's own output can jump by tens of newtons at the
+            # rounding scale in ~0.1-1 % of draws (env 6192 of the 65 536-env check), which
+            # 8 + 32 draws miss; draw it properly for the few envs still left
+            k = REFINE_DEEP_RUNS if nsteps == 1 else REFINE_DEEP_RUNS // 4
+            fam3 = _refine(task, n, seed, st, actions, so, ob_o, rw_o, (te_o, tr_o), st, nsteps, wc, k=k, rseed=8642)
+            for f, v in fam3.items():
+                fam[f] = np.maximum(fam[f], v)
+            sens = np.max(np.stack([fam[f] for f in SENS_FAMILIES]), axis=0)
+            deep = [e for e in still if not _explained(ratio[e], sens[e])]
+            print(f"  deep envelope ({k} more rounding-scale runs) for {len(still)} envs: "
+                  + ", ".join(f"env {e} ratio {ratio[e]:.3g} envelope {sens[e]:.3g}" for e in still)
+                  + f"; still unexplained {len(deep)}")
+            still = deep
         unexplained = still
     assert not unexplained, f"{task}: {len(unexplained)} envs outside tolerance where the oracle is stable: {unexplained[:20]}"
     assert frac <= AGG_FRAC_K * frac_o + AGG_FRAC_ABS, \
