@@ -109,6 +109,38 @@ int zbp_gae(const float* rewards, const float* dones, const float* values, const
             float* advantages, int32_t steps, int32_t envs, float gamma, float lam, int32_t normalize, float* scratch,
             void* stream);
 
+/* One rollout step of PPO.act (rsl_rl ActorCritic.act / evaluate / get_actions_log_prob and the
+ * transition fields of RolloutStorage.add; zbot_lab_amd/rl/ppo.py) for `rows` envs in one launch:
+ * actions = mu + std * noise (noise: the caller's standard-normal draw, [rows][num_actions]), its
+ * Gaussian log-probability summed over the actions, the critic's value; writes actions [rows][na]
+ * (the env's input) and the storage slot of this step: observations, critic observations, actions,
+ * values, log-probabilities, mu, sigma. Reads the workspace's weight images (zbp_pack must follow
+ * every parameter change; zbp_optimizer_step re-packs itself). Replaces the ~30 torch kernels of a
+ * policy step (runner._rollout). */
+typedef struct {
+  const float* obs;         /* [rows][obs_dim] */
+  const float* critic_obs;  /* [rows][critic_obs_dim] */
+  const float* noise;       /* [rows][num_actions] */
+  float* actions;           /* [rows][num_actions] out */
+  float* st_obs;            /* storage slot [rows][obs_dim] out */
+  float* st_critic_obs;     /* [rows][critic_obs_dim] out */
+  float* st_actions;        /* [rows][num_actions] out */
+  float* st_values;         /* [rows] out */
+  float* st_log_prob;       /* [rows] out */
+  float* st_mu;             /* [rows][num_actions] out */
+  float* st_sigma;          /* [rows][num_actions] out */
+  int32_t rows, obs_dim, critic_obs_dim, num_actions;
+} zbp_act_io;
+int zbp_act(const zbp_net* actor, const zbp_net* critic, const float* std_param, const zbp_act_io* io, float* ws,
+            int32_t batch, void* stream);
+/* PPO.process_env_step + the runner's episode statistics for one step (runner._rollout): storage
+ * reward = reward (+ gamma * value where time_outs, rsl_rl's bootstrap; time_outs may be NULL),
+ * storage done = done; cur_rew += reward, cur_len += 1, and over the envs with done > 0
+ * ep_stats[0..2] += {sum cur_rew, sum cur_len, count} before their cur_rew / cur_len reset to 0.
+ * rewards / values / cur_* [n] fp32, dones [n] int64, time_outs [n] uint8 (bool). One launch. */
+int zbp_env_post(const float* rewards, const int64_t* dones, const uint8_t* time_outs, const float* values, float gamma,
+                 float* st_rewards, float* st_dones, float* cur_rew, float* cur_len, float* ep_stats, int32_t n,
+                 void* stream);
 const char* zbp_last_error(void);
 
 #ifdef __cplusplus

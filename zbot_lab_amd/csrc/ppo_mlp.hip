@@ -187,15 +187,17 @@ struct RowArgs {
 };
 
 // forward through one net for the row tile; the output layer's pre-activations land in `out`
-// ([32][33])
-__device__ void net_forward(const RowArgs& A, const NetW& w, float* lds, int row0) {
+// ([32][33]). kStore: every hidden layer's input X_l also goes to the HBM row buffers (feature-major,
+// B rows) for the weight gradients; the rollout's forward (k_act) keeps them in LDS only.
+template <bool kStore>
+__device__ void net_forward_t(const NetW& w, float* ws, int B, const int* lds_x, int lds_out, float* lds, int row0) {
   const int wave = threadIdx.x >> 6, h = (threadIdx.x & 63) >> 5;
   for (int l = 0; l < w.L; ++l) {
     const int P0 = w.p[l], P1 = w.p[l + 1];
     const bool last = l == w.L - 1;
-    const float* xs = lds + A.lds_x[l];
-    const float* wp = A.ws + w.wp[l];
-    const float* bp = A.ws + w.bp[l];
+    const float* xs = lds + lds_x[l];
+    const float* wp = ws + w.wp[l];
+    const float* bp = ws + w.bp[l];
     for (int t = wave; t < P1 / 32; t += 4) {
       const f32x16 acc = tile_mma(xs, P0 + 4, wp, P0, P0, 32 * t);
       const int n = 32 * t + acc_col();
@@ -208,19 +210,22 @@ __device__ void net_forward(const RowArgs& A, const NetW& w, float* lds, int row
           const int i = 8 * q + 4 * h + u;
           v[u] = acc[4 * q + u] + bias;
           if (last) {
-            lds[A.lds_out + i * 33 + n] = v[u];
+            lds[lds_out + i * 33 + n] = v[u];
           } else {
             v[u] = v[u] > 0.f ? v[u] : expf(v[u]) - 1.f;  // ELU(alpha = 1), as ATen's elu kernel
-            lds[A.lds_x[l + 1] + i * (P1 + 4) + n] = v[u];
+            lds[lds_x[l + 1] + i * (P1 + 4) + n] = v[u];
           }
         }
-        if (!last)
-          *reinterpret_cast<float4*>(A.ws + w.x[l + 1] + (int64_t)n * A.B + row0 + 8 * q + 4 * h) =
+        if (kStore && !last)
+          *reinterpret_cast<float4*>(ws + w.x[l + 1] + (int64_t)n * B + row0 + 8 * q + 4 * h) =
               make_float4(v[0], v[1], v[2], v[3]);
       }
     }
     __syncthreads();
   }
+}
+__device__ void net_forward(const RowArgs& A, const NetW& w, float* lds, int row0) {
+  net_forward_t<true>(w, A.ws, A.B, A.lds_x, A.lds_out, lds, row0);
 }
 
 // backward through one net from dZ of the output layer (lds_dz, [32][p(L) + 4])
@@ -560,6 +565,102 @@ __global__ void k_optim_tail(OptimArgs A) {
   A.acc[2] += A.stats[3];
 }
 
+// ------------------------------------------------------------------------------- rollout
+// PPO.act (zbot_lab_amd/rl/ppo.py; rsl_rl ActorCritic.act + evaluate + get_actions_log_prob and
+// RolloutStorage.add's transition fields) for one policy step of every env: one workgroup per 32
+// rows gathers the observations (and writes them into the storage slot), runs the actor forward,
+// draws a = mu + std * noise (noise = the caller's torch.randn_like), the Gaussian log-probability
+// sum_a (-(a - mu)^2 / (2 std^2) - log std - log sqrt(2 pi)) and the critic's value; every
+// transition field lands in the storage slot of this step, the actions also in `actions` (the
+// env's input). The forward reads the workspace's weight images (zbp_pack).
+struct ActArgs {
+  NetW n[2];
+  float* ws;
+  const float* std_param;
+  const float* obs;
+  const float* cobs;
+  const float* noise;
+  int obs_dim, cobs_dim, na, rows;
+  float *actions, *s_obs, *s_cobs, *s_act, *s_val, *s_lp, *s_mu, *s_sig;
+  int lds_x[MAXL], lds_out;
+};
+__device__ void act_gather(const NetW& w, const float* src, int dim, float* st, int rows, float* lds, int lds_x0,
+                           int row0) {
+  const int P0 = w.p[0];
+  for (int e = threadIdx.x; e < TR * P0; e += blockDim.x) {
+    const int i = e / P0, k = e % P0;  // (row-major: the source rows are contiguous)
+    const int row = row0 + i;
+    const float v = (k < dim && row < rows) ? src[(int64_t)row * dim + k] : 0.f;
+    lds[lds_x0 + i * (P0 + 4) + k] = v;
+    if (k < dim && row < rows) st[(int64_t)row * dim + k] = v;
+  }
+  __syncthreads();
+}
+__global__ __launch_bounds__(256) void k_act(ActArgs A) {
+  extern __shared__ float lds[];
+  const int row0 = blockIdx.x * TR, tid = threadIdx.x;
+  act_gather(A.n[0], A.obs, A.obs_dim, A.s_obs, A.rows, lds, A.lds_x[0], row0);
+  net_forward_t<false>(A.n[0], A.ws, 0, A.lds_x, A.lds_out, lds, row0);
+  if (tid < TR && row0 + tid < A.rows) {
+    const int64_t row = row0 + tid;
+    const float kLog2Pi = 0.91893853320467274178f;  // log(sqrt(2 pi))
+    float lp = 0.f;
+    for (int a = 0; a < A.na; ++a) {
+      const float mu = lds[A.lds_out + tid * 33 + a], s = A.std_param[a];
+      const float x = mu + s * A.noise[row * A.na + a], diff = x - mu;
+      lp += -(diff * diff) / (2.f * (s * s)) - logf(s) - kLog2Pi;
+      A.actions[row * A.na + a] = x;
+      A.s_act[row * A.na + a] = x;
+      A.s_mu[row * A.na + a] = mu;
+      A.s_sig[row * A.na + a] = s;
+    }
+    A.s_lp[row] = lp;
+  }
+  __syncthreads();  // (the output tile is reused by the critic)
+  act_gather(A.n[1], A.cobs, A.cobs_dim, A.s_cobs, A.rows, lds, A.lds_x[0], row0);
+  net_forward_t<false>(A.n[1], A.ws, 0, A.lds_x, A.lds_out, lds, row0);
+  if (tid < TR && row0 + tid < A.rows) A.s_val[row0 + tid] = lds[A.lds_out + tid * 33];
+}
+
+// PPO.process_env_step + the runner's episode bookkeeping (zbot_lab_amd/rl/runner.py _rollout) for
+// one step, one workgroup: the storage slot's reward (+ gamma * value on time-outs, rsl_rl's
+// bootstrap) and done; cur_rew += reward, cur_len += 1; over the done envs ep_stats += {sum cur_rew,
+// sum cur_len, count} (a fixed-order block reduction), then their cur_rew / cur_len are cleared.
+__global__ __launch_bounds__(1024) void k_env_post(const float* __restrict__ rew, const int64_t* __restrict__ done,
+                                                   const uint8_t* __restrict__ tout, const float* __restrict__ val,
+                                                   float gamma, float* __restrict__ s_rew, float* __restrict__ s_done,
+                                                   float* __restrict__ cur_rew, float* __restrict__ cur_len,
+                                                   float* __restrict__ ep_stats, int n) {
+  __shared__ float red[3][16];
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+  for (int e = threadIdx.x; e < n; e += blockDim.x) {
+    const float r = rew[e];
+    const bool d = done[e] > 0;
+    s_rew[e] = tout && tout[e] ? r + gamma * val[e] : r;
+    s_done[e] = (float)done[e];
+    const float cr = cur_rew[e] + r, cl = cur_len[e] + 1.f;
+    if (d) { a0 += cr; a1 += cl; a2 += 1.f; }
+    cur_rew[e] = d ? 0.f : cr;
+    cur_len[e] = d ? 0.f : cl;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    a0 += __shfl_xor(a0, o);
+    a1 += __shfl_xor(a1, o);
+    a2 += __shfl_xor(a2, o);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = a0;
+    red[1][threadIdx.x >> 6] = a1;
+    red[2][threadIdx.x >> 6] = a2;
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    float t = 0.f;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += red[threadIdx.x][w];
+    ep_stats[threadIdx.x] += t;
+  }
+}
+
 // ------------------------------------------------------------------------------- GAE
 // RolloutStorage.compute_returns (zbot_lab_amd/rl/ppo.py; rsl_rl GAE with time-out bootstrapping
 // already folded into the rewards): one thread per env runs the backward recursion over T steps;
@@ -780,6 +881,68 @@ int zbp_optimizer_step(const zbp_params* params, float* lr, const float* stats, 
   k_optim_tail<<<1, 64, 0, s>>>(O);
   if (int rc = launch_check("k_optim_tail")) return rc;
   return do_pack(lo, actor, critic, ws, s);
+}
+
+int zbp_act(const zbp_net* actor, const zbp_net* critic, const float* std_param, const zbp_act_io* io, float* ws,
+            int32_t batch, void* stream) {
+  if (const char* e = check_net(actor)) return fail(-1, e);
+  if (const char* e = check_net(critic)) return fail(-1, e);
+  if (!io || !ws || !std_param || !io->obs || !io->critic_obs || !io->noise || !io->actions || !io->st_obs ||
+      !io->st_critic_obs || !io->st_actions || !io->st_values || !io->st_log_prob || !io->st_mu || !io->st_sigma)
+    return fail(-1, "zbp_act: null argument");
+  if (io->rows < 1 || batch < TR || batch % TR) return fail(-1, "zbp_act: rows / batch");
+  if (io->num_actions != actor->dim[actor->n_layers] || io->obs_dim != actor->dim[0] ||
+      io->critic_obs_dim != critic->dim[0] || critic->dim[critic->n_layers] != 1)
+    return fail(-1, "zbp_act: observation / action dims");
+  const Layout lo = make_layout(actor, critic, batch);
+  ActArgs A{};
+  A.n[0] = lo.n[0];
+  A.n[1] = lo.n[1];
+  A.ws = ws;
+  A.std_param = std_param;
+  A.obs = io->obs;
+  A.cobs = io->critic_obs;
+  A.noise = io->noise;
+  A.obs_dim = io->obs_dim;
+  A.cobs_dim = io->critic_obs_dim;
+  A.na = io->num_actions;
+  A.rows = io->rows;
+  A.actions = io->actions;
+  A.s_obs = io->st_obs;
+  A.s_cobs = io->st_critic_obs;
+  A.s_act = io->st_actions;
+  A.s_val = io->st_values;
+  A.s_lp = io->st_log_prob;
+  A.s_mu = io->st_mu;
+  A.s_sig = io->st_sigma;
+  int off = 0;
+  for (int l = 0; l < MAXL; ++l) {
+    const int p = lo.n[0].p[l] > lo.n[1].p[l] ? lo.n[0].p[l] : lo.n[1].p[l];
+    A.lds_x[l] = off;
+    off += TR * (p + 4);
+  }
+  A.lds_out = off;
+  off += TR * 33;
+  const size_t lds = sizeof(float) * off;
+  if (lds > 160 * 1024) return fail(-1, "zbp_act: nets too wide for the LDS row tile");
+  static bool lds_set = false;
+  if (!lds_set) {
+    const hipError_t e = hipFuncSetAttribute((const void*)k_act, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return hip_fail(e, "hipFuncSetAttribute k_act");
+    lds_set = true;
+  }
+  k_act<<<(io->rows + TR - 1) / TR, 256, lds, (hipStream_t)stream>>>(A);
+  return launch_check("k_act");
+}
+
+int zbp_env_post(const float* rewards, const int64_t* dones, const uint8_t* time_outs, const float* values, float gamma,
+                 float* st_rewards, float* st_dones, float* cur_rew, float* cur_len, float* ep_stats, int32_t n,
+                 void* stream) {
+  if (!rewards || !dones || !values || !st_rewards || !st_dones || !cur_rew || !cur_len || !ep_stats || n < 1)
+    return fail(-1, "zbp_env_post: bad argument");
+  k_env_post<<<1, 1024, 0, (hipStream_t)stream>>>(rewards, dones, time_outs, values, gamma, st_rewards, st_dones, cur_rew,
+                                                  cur_len, ep_stats, n);
+  return launch_check("k_env_post");
 }
 
 int zbp_gae(const float* rewards, const float* dones, const float* values, const float* last_values, float* returns,

@@ -43,13 +43,21 @@ class LossCfg(C.Structure):
                 ("use_clipped_value_loss", C.c_int32)]
 
 
+class ActIO(C.Structure):
+    _fields_ = [("obs", C.c_void_p), ("critic_obs", C.c_void_p), ("noise", C.c_void_p), ("actions", C.c_void_p),
+                ("st_obs", C.c_void_p), ("st_critic_obs", C.c_void_p), ("st_actions", C.c_void_p),
+                ("st_values", C.c_void_p), ("st_log_prob", C.c_void_p), ("st_mu", C.c_void_p), ("st_sigma", C.c_void_p),
+                ("rows", C.c_int32), ("obs_dim", C.c_int32), ("critic_obs_dim", C.c_int32), ("num_actions", C.c_int32)]
+
+
 class Params(C.Structure):
     _fields_ = [("n_params", C.c_int32), ("numel", C.c_int64 * MAXP), ("param", C.c_void_p * MAXP),
                 ("grad", C.c_void_p * MAXP), ("exp_avg", C.c_void_p * MAXP), ("exp_avg_sq", C.c_void_p * MAXP),
                 ("step", C.c_void_p * MAXP)]
 
 
-EXPORTED = ["zbp_workspace_floats", "zbp_pack", "zbp_minibatch", "zbp_optimizer_step", "zbp_gae", "zbp_last_error"]
+EXPORTED = ["zbp_workspace_floats", "zbp_pack", "zbp_minibatch", "zbp_optimizer_step", "zbp_gae", "zbp_act",
+            "zbp_env_post", "zbp_last_error"]
 _lib = None
 
 
@@ -70,7 +78,9 @@ def lib():
     L.zbp_optimizer_step.argtypes = [C.POINTER(Params), P, P, P, C.c_float, C.c_float, C.c_float, C.c_float,
                                      C.c_float, C.POINTER(Net), C.POINTER(Net), P, C.c_int32, P]
     L.zbp_gae.argtypes = [P, P, P, P, P, P, C.c_int32, C.c_int32, C.c_float, C.c_float, C.c_int32, P, P]
-    for n in ("zbp_pack", "zbp_minibatch", "zbp_optimizer_step", "zbp_gae"):
+    L.zbp_act.argtypes = [C.POINTER(Net), C.POINTER(Net), P, C.POINTER(ActIO), P, C.c_int32, P]
+    L.zbp_env_post.argtypes = [P, P, P, P, C.c_float, P, P, P, P, P, C.c_int32, P]
+    for n in ("zbp_pack", "zbp_minibatch", "zbp_optimizer_step", "zbp_gae", "zbp_act", "zbp_env_post"):
         getattr(L, n).restype = C.c_int
     _lib = L
     return L
@@ -234,6 +244,51 @@ class FusedUpdate:
                                         float(alg.max_grad_norm), float(b1), float(b2), float(g["eps"]),
                                         C.byref(self.na), C.byref(self.nc), _p(self.ws), self.batch, self._stream()),
                "zbp_optimizer_step")
+
+    # -- rollout (runner._rollout's policy step and post-step bookkeeping, one launch each)
+    def act(self, obs: torch.Tensor, critic_obs: torch.Tensor, storage) -> torch.Tensor:
+        """PPO.act on zbp_act: the actions (a static buffer) and the transition fields written
+        straight into the storage slot ``storage.step``; the noise is torch.randn_like's draw, as in
+        the torch path. The weight images are re-packed at a rollout's first step (parameters may
+        have changed outside zbp_optimizer_step: a torch optimizer, a checkpoint load)."""
+        k = storage.step
+        if k >= storage.num_transitions_per_env:
+            raise OverflowError("rollout buffer overflow")
+        if k == 0:
+            self.pack()
+        n, na = obs.shape[0], storage.actions.shape[-1]
+        if getattr(self, "_act_out", None) is None or self._act_out.shape != (n, na):
+            self._act_out = torch.zeros(n, na, device=obs.device)
+            self._noise = torch.zeros(n, na, device=obs.device)
+        torch.randn(n, na, out=self._noise, device=obs.device)
+        obs, critic_obs = obs.contiguous(), critic_obs.contiguous()
+        io = ActIO()
+        io.obs, io.critic_obs, io.noise, io.actions = obs.data_ptr(), critic_obs.data_ptr(), self._noise.data_ptr(), \
+            self._act_out.data_ptr()
+        io.st_obs, io.st_critic_obs = storage.observations[k].data_ptr(), storage.critic_observations[k].data_ptr()
+        io.st_actions, io.st_values = storage.actions[k].data_ptr(), storage.values[k].data_ptr()
+        io.st_log_prob, io.st_mu = storage.actions_log_prob[k].data_ptr(), storage.mu[k].data_ptr()
+        io.st_sigma = storage.sigma[k].data_ptr()
+        io.rows, io.obs_dim, io.critic_obs_dim, io.num_actions = n, obs.shape[-1], critic_obs.shape[-1], na
+        _check(lib().zbp_act(C.byref(self.na), C.byref(self.nc), _p(self.alg.policy.std), C.byref(io), _p(self.ws),
+                             self.batch, self._stream()), "zbp_act")
+        return self._act_out
+
+    def env_post(self, storage, rewards: torch.Tensor, dones: torch.Tensor, time_outs, gamma: float,
+                 cur_rew: torch.Tensor, cur_len: torch.Tensor, ep_stats: torch.Tensor) -> None:
+        """PPO.process_env_step + the runner's episode statistics (zbp_env_post); advances the slot."""
+        k = storage.step
+        tout = time_outs
+        if tout is not None and tout.dtype not in (torch.bool, torch.uint8):  # (bool: one byte, 0 / 1)
+            tout = tout.to(torch.uint8)
+        if dones.dtype != torch.int64:
+            dones = dones.to(torch.int64)
+        _check(lib().zbp_env_post(_p(rewards.contiguous()), _p(dones.contiguous()),
+                                  None if tout is None else _p(tout.contiguous()), _p(storage.values[k]),
+                                  float(gamma), _p(storage.rewards[k]), _p(storage.dones[k]), _p(cur_rew), _p(cur_len),
+                                  _p(ep_stats), rewards.shape[0], self._stream()), "zbp_env_post")
+        self._tout = tout  # (alive until the stream has consumed it)
+        storage.step += 1
 
     def rebind(self) -> None:
         """After parameters or optimizer state were replaced (checkpoint load)."""

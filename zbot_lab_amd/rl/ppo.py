@@ -332,6 +332,13 @@ class PPO:
                 self._fused = fused.FusedUpdate(self, mb)
         return self._fused
 
+    def fused_rollout(self):
+        """The libzbot_ppo driver for the rollout's policy steps (zbp_act / zbp_env_post), or None
+        (CPU, nets outside the kernels' limits, ZBOT_PPO_FUSED=0 or ZBOT_ROLLOUT_FUSED=0)."""
+        if os.environ.get("ZBOT_ROLLOUT_FUSED", "1") == "0" or self.storage is None or not self.storage.values.is_cuda:
+            return None
+        return self.fused_update()
+
     def invalidate_fused(self) -> None:
         """Parameters / optimizer state replaced (checkpoint load): rebuild the fused driver."""
         self._fused = None

@@ -185,6 +185,22 @@ class OnPolicyRunner:
         self.ep_stats.zero_()
         if self._log_acc is not None:
             self._log_acc.zero_()
+        # on a GPU the policy step and the post-step bookkeeping are one launch each (libzbot_ppo:
+        # zbp_act, zbp_env_post) instead of ~40 torch kernels; same statements as the loop below
+        fr = self.alg.fused_rollout()
+        if fr is not None:
+            st = self.alg.storage
+            for _ in range(self.num_steps_per_env):
+                actions = fr.act(obs, obs, st)
+                obs_d, rewards, dones, extras = env.step(actions.to(env.device))
+                obs = _policy_obs(obs_d).to(self.device)
+                tout = extras.get("time_outs") if isinstance(extras, dict) else None
+                fr.env_post(st, rewards.to(self.device), dones.to(self.device),
+                            None if tout is None else tout.to(self.device), self.alg.gamma, self.cur_rew, self.cur_len,
+                            self.ep_stats)
+                self._accumulate_log(extras)
+            self._extras = extras
+            return obs
         for _ in range(self.num_steps_per_env):
             actions = self.alg.act(obs, obs)
             obs_d, rewards, dones, extras = env.step(actions.to(env.device))
@@ -211,8 +227,30 @@ class OnPolicyRunner:
         if self._log_keys is None:
             self._log_keys = list(log.keys())
             self._log_acc = torch.zeros(len(self._log_keys), device=self.device)
+            self._log_groups = self._log_views(log)
+        if self._log_groups is not None and all(log[k] is self._log_src[i] for i, k in enumerate(self._log_keys)):
+            # the env's log values are fixed 0-d views into a few device buffers: one gather + one
+            # index_add per buffer instead of a copy per key
+            for base, src, dst in self._log_groups:
+                self._log_acc.index_add_(0, dst, base.index_select(0, src).to(torch.float32))
+            return
         vals = [log[k] if torch.is_tensor(log[k]) else torch.tensor(float(log[k])) for k in self._log_keys]
         self._log_acc += torch.stack([v.to(self.device, torch.float32).reshape(()) for v in vals])
+
+    def _log_views(self, log):
+        """[(flat base buffer, source indices, accumulator indices)] when every log value is a 0-d
+        view of a 1-d device buffer (walking v2 / v4 / manager: zb_read_log's buffers), else None."""
+        self._log_src = [log[k] for k in self._log_keys]
+        groups = {}
+        for i, v in enumerate(self._log_src):
+            b = v._base if torch.is_tensor(v) else None
+            if b is None or v.dim() != 0 or b.dim() != 1 or not b.is_contiguous() or b.device != self._log_acc.device:
+                return None
+            e = groups.setdefault(id(b), (b, [], []))
+            e[1].append(v.storage_offset() - b.storage_offset())
+            e[2].append(i)
+        dev = self._log_acc.device
+        return [(b, torch.tensor(src, device=dev), torch.tensor(dst, device=dev)) for b, src, dst in groups.values()]
 
     def _capture(self, obs: torch.Tensor) -> None:
         """Record one rollout (reading obs from a static buffer) as a graph; nothing executes."""
