@@ -1787,10 +1787,13 @@ __device__ __forceinline__ void sens_store(const Q& q, float* __restrict__ st, i
 #ifndef ZB_CARRY
 #define ZB_CARRY 1
 #endif
-// state and observation stores write-through (sc1 vector stores): the bytes leave the XCD L2 as
-// the waves finish instead of in the end-of-kernel write-back (profiles/r4_wt: -0.7 us per step)
+// state and observation stores write-through (sc1 vector stores, -DZB_WT_STORES=1): the bytes leave
+// the XCD L2 as the waves finish instead of in the end-of-kernel write-back (profiles/r4_wt: 0.6 %
+// faster), but each 16-byte row piece of a staged store then goes to HBM as its own partial-line
+// write: WRITE_SIZE 1.7x the bytes written (profiles/r4h) against 1.0x with write-back. Off by
+// default.
 #ifndef ZB_WT_STORES
-#define ZB_WT_STORES 1
+#define ZB_WT_STORES 0
 #endif
 __device__ __forceinline__ float& Q::stg(int k) const { return reinterpret_cast<float*>(b + YG_OFF)[e * STG_LEN + k]; }
 // WT >= 0: state row WT is stored with agent scope (the walking kernel's episode length, which a
