@@ -153,8 +153,7 @@ def test_fused_act_matches_torch_policy(gpu, hidden):
     from zbot_lab_amd.rl import fused
     for envs in (512, 200):
         alg = _alg(hidden, envs=envs)
-        mb = alg.storage.num_envs * alg.storage.num_transitions_per_env // alg.num_mini_batches
-        fu = fused.FusedUpdate(alg, mb)
+        fu = fused.FusedUpdate(alg, 256)  # (the minibatch size shapes only the update's row buffers)
         st = alg.storage
         st.clear()
         obs = torch.randn(envs, 23, device="cuda:0")
@@ -178,7 +177,6 @@ def test_fused_act_matches_torch_policy(gpu, hidden):
         assert (st.actions_log_prob[3].view(-1) - ref_lp).abs().max() <= tol(ref_lp)
         assert (st.values[3] - ref_v).abs().max() <= tol(ref_v)
         assert torch.equal(st.observations[3], obs) and torch.equal(st.critic_observations[3], obs)
-        assert float(st.values[2].abs().max()) != 0.0 or True  # (other slots untouched: not written)
 
 
 def test_fused_env_post_matches_torch(gpu):

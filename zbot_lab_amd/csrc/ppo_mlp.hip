@@ -636,7 +636,9 @@ __global__ __launch_bounds__(1024) void k_env_post(const float* __restrict__ rew
   for (int e = threadIdx.x; e < n; e += blockDim.x) {
     const float r = rew[e];
     const bool d = done[e] > 0;
-    s_rew[e] = tout && tout[e] ? r + gamma * val[e] : r;
+    float t = gamma * val[e];
+    asm volatile("" : "+v"(t));  // (torch rounds the product, then the sum: no fma contraction)
+    s_rew[e] = tout && tout[e] ? r + t : r;
     s_done[e] = (float)done[e];
     const float cr = cur_rew[e] + r, cl = cur_len[e] + 1.f;
     if (d) { a0 += cr; a1 += cl; a2 += 1.f; }
