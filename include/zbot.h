@@ -323,7 +323,9 @@ typedef struct zb_task_cfg {
   /* self-contact manifold (PhysX PCM keeps up to 4 points per convex pair; zbot_cfg.py:636
    * enabled_self_collisions): 1 = a pair whose two nearest features are disk faces (cap on cap)
    * contributes up to 4 points (rim points of either face inside the other), every
-   * other pair its one GJK point; 0 = one point per pair */
+   * other pair its one GJK point; 2 (default) = 1 plus side-by-side pairs whose nearest features are
+   * two rulings within 5 degrees of the contact plane and of each other: the GJK point and the two
+   * ends of the rulings' overlap (up to 3 points); 0 = one point per pair */
   int32_t self_manifold;
 } zb_task_cfg;
 

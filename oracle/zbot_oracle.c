@@ -747,6 +747,84 @@ static int face_manifold(const hull_t* A, const hull_t* B, const contact_t* c0, 
   return k;
 }
 
+/* Rim (ruling) manifold (cfg->self_manifold 2, round 4; PhysX PCM keeps up to 4 points per convex
+ * pair): two links lying side by side touch along a line -- the nearest features are a ruling of each
+ * core hull, the segment between the support points of its two circles along the pair direction (A:
+ * -n, B: +n). When both rulings lie within RIM_DEG of the contact plane and of each other, the pair
+ * contributes up to 3 points: the GJK point, then the two ends of the rulings' overlap along A's
+ * ruling (kept when more than 1 mm from the GJK point along it and within the margin), each with
+ * the normal n made perpendicular to A's ruling (the component of a line contact's GJK normal along
+ * the line is determined only to GJK's tolerance cone); an end's separation is the gap between the
+ * two rulings along that normal at that end, minus 2 CORE_M. Rulings absent or crossing: the GJK
+ * contact alone. (The kernel: the rim branch of quad_manifold, on the pair's quad.) */
+#define RIM_COS 0.9961946980917455 /* cos 5 deg */
+static double g_rim_cos = RIM_COS; /* moved with the face threshold by zbo_set_face_cos (15 deg -> 5 deg scale) */
+static void hull_ruling(const hull_t* H, const real d[3], real p[2][3]) {
+  for (int ci = 0; ci < 2; ++ci) {
+    const real* c = H->c[ci];
+    const real a = v3_dot(d, c + 3), b = v3_dot(d, c + 6);
+    const real nr = sqrtr(a * a + b * b);
+    for (int q = 0; q < 3; ++q) p[ci][q] = c[q] + (nr > (real)1e-15 ? (a * c[3 + q] + b * c[6 + q]) / nr : 0);
+  }
+}
+static int rim_manifold(const hull_t* A, const hull_t* B, const contact_t* c0, real margin, contact_t out[3]) {
+  const real* n = c0->n;
+  const real nA[3] = {-n[0], -n[1], -n[2]};
+  real pa[2][3], pb[2][3];
+  hull_ruling(A, nA, pa);
+  hull_ruling(B, n, pb);
+  real sa[3], sb[3];
+  for (int q = 0; q < 3; ++q) { sa[q] = pa[1][q] - pa[0][q]; sb[q] = pb[1][q] - pb[0][q]; }
+  const real la = sqrtr(v3_dot(sa, sa)), lb = sqrtr(v3_dot(sb, sb));
+  if (la < (real)1e-3 || lb < (real)1e-3) return 0;
+  const real sin_t = (real)sqrt(1.0 - g_rim_cos * g_rim_cos);
+  /* both rulings within RIM_DEG of the contact plane, and of each other */
+  if (fabs((double)v3_dot(sa, n)) > sin_t * la || fabs((double)v3_dot(sb, n)) > sin_t * lb) return 0;
+  if (fabs((double)v3_dot(sa, sb)) < g_rim_cos * la * lb) return 0;
+  real ah[3];
+  for (int q = 0; q < 3; ++q) ah[q] = sa[q] / la;
+  real nr[3];
+  const real na = v3_dot(n, ah);
+  for (int q = 0; q < 3; ++q) nr[q] = n[q] - na * ah[q];
+  const real inr = 1 / sqrtr(v3_dot(nr, nr));
+  for (int q = 0; q < 3; ++q) nr[q] *= inr;
+  /* the overlap of the rulings along A's: t in [0, la] on A, B's ends at tb0, tb1 */
+  real w0[3], w1[3], wg[3];
+  for (int q = 0; q < 3; ++q) { w0[q] = pb[0][q] - pa[0][q]; w1[q] = pb[1][q] - pa[0][q]; wg[q] = c0->x[q] - pa[0][q]; }
+  const real tb0 = v3_dot(w0, ah), tb1 = v3_dot(w1, ah), tg = v3_dot(wg, ah);
+  const real lo = fmax((double)0, (double)(tb0 < tb1 ? tb0 : tb1)), hi = fmin((double)la, (double)(tb0 < tb1 ? tb1 : tb0));
+  int k = 0;
+  out[k] = *c0;
+  for (int q = 0; q < 3; ++q) out[k].n[q] = nr[q];
+  ++k;
+  if (!(hi - lo > (real)1e-3)) return k;
+  const real dtb = tb1 - tb0;
+  for (int e = 0; e < 2; ++e) {
+    const real t = e == 0 ? lo : hi;
+    if (!(fabs((double)(t - tg)) > 1e-3)) continue;
+    const real ua = t / la, ub = (t - tb0) / dtb;
+    real xa[3], xb[3], g[3];
+    for (int q = 0; q < 3; ++q) {
+      xa[q] = pa[0][q] + ua * sa[q];
+      xb[q] = pb[0][q] + ub * sb[q];
+      g[q] = xa[q] - xb[q];
+    }
+    const real sep = v3_dot(g, nr) - 2 * (real)CORE_M;
+    if (!(sep < margin)) continue;
+    contact_t* o = &out[k++];
+    o->la = c0->la; o->lb = c0->lb; o->sep = sep; o->rim = -1;
+    for (int q = 0; q < 3; ++q) { o->n[q] = nr[q]; o->x[q] = (real)0.5 * (xa[q] + xb[q]); }
+  }
+  return k;
+}
+/* the self-contact manifold of cfg->self_manifold (1: faces, 2: faces, else rims; 0: none) */
+static int self_manifold(int mode, const hull_t* A, const hull_t* B, const contact_t* c0, real margin, contact_t out[4]) {
+  if (mode < 1 || !(c0->sep > -2 * (real)CORE_M + (real)1e-7)) return 0;
+  const int k = face_manifold(A, B, c0, margin, out);
+  if (k > 0 || mode < 2) return k;
+  return rim_manifold(A, B, c0, margin, out);
+}
+
 /* GJK stopping tolerance (test hook: the parity tests re-run the oracle at other tolerances to tell
  * an env whose result depends on where GJK stops - an algorithmic discontinuity like the contact
  * margin - from a real mismatch) */
@@ -768,6 +846,7 @@ int zbo_set_plant(int mode) {
  * pair switches between one point and a face manifold is a discontinuity like the contact margin */
 int zbo_set_face_cos(double c) {
   g_face_cos = c > 0 ? c : FACE_COS;
+  g_rim_cos = c > 0 ? cos(acos(c) / 3.0) : RIM_COS; /* the rim threshold moves with it (15 -> 5 deg) */
   return 0;
 }
 
@@ -857,8 +936,14 @@ int zbo_hull_pair_from(const float* a, const float* b, float margin, const float
   for (int q = 0; q < 3; ++q) { out[2 + q] = (float)c.n[q]; out[5 + q] = (float)c.x[q]; }
   return g_gjk_last_it; /* support iterations (GJK probe) */
 }
-/* test entry: hull_pair + face_manifold on two world-frame core hulls; out [4][7] = {sep, n[3], x[3]}
- * per point; returns the number of points (0: no contact, 1: the GJK contact alone) */
+/* test entry: hull_pair + the self-contact manifold (mode zbo_set_pair_manifold_mode, default 2) on
+ * two world-frame core hulls; out [4][7] = {sep, n[3], x[3]} per point; returns the number of points
+ * (0: no contact, 1: the GJK contact alone) */
+static int g_pair_manifold_mode = 2;
+int zbo_set_pair_manifold_mode(int m) {
+  g_pair_manifold_mode = m;
+  return 0;
+}
 int zbo_pair_manifold(const float* a, const float* b, float margin, float* out) {
   hull_t A, B;
   for (int ci = 0; ci < 2; ++ci)
@@ -866,7 +951,7 @@ int zbo_pair_manifold(const float* a, const float* b, float margin, float* out) 
   contact_t c, mf[4];
   memset(&c, 0, sizeof(c));
   if (!hull_pair(&A, &B, (real)margin, (real)margin, NULL, &c)) return 0;
-  int k = c.sep > -2 * (real)CORE_M + (real)1e-7 ? face_manifold(&A, &B, &c, (real)margin, mf) : 0;
+  int k = self_manifold(g_pair_manifold_mode, &A, &B, &c, (real)margin, mf);
   if (k == 0) { mf[0] = c; k = 1; }
   for (int j = 0; j < k; ++j) {
     out[7 * j] = (float)mf[j].sep;
@@ -968,8 +1053,7 @@ static void detect(const mdl_t* m, const zb_task_cfg* cfg, const kin_t* k, real 
       if (hit) {
         c.la = la; c.lb = lb; c.rim = -1;
         contact_t mf[4];
-        const int k = cfg->self_manifold && c.sep > -2 * (real)CORE_M + (real)1e-7 ? face_manifold(&A, &B, &c, margin, mf)
-                                                                                 : 0;
+        const int k = self_manifold(cfg->self_manifold, &A, &B, &c, margin, mf);
         if (k == 0) {
           L->c[L->n++] = c;
           ++nself;

@@ -400,19 +400,21 @@ def test_full_state_contact_cache(gpu, task):
     assert (wg[3::4][:, g_out[2] | g_out[3]] == -1).all()
 
 
+@pytest.mark.parametrize("kind", ["face", "rim"])
 @pytest.mark.parametrize("task", ["v2", "standup"])
-def test_full_state_face_manifold(gpu, task):
-    """The self-contact face manifold (zb_task_cfg.self_manifold, DESIGN.md §3.2: cap on cap, up to 4
-    points per pair): folded states in which at least one link pair is a face-to-face contact (the
-    oracle's candidate list has more self points than with one point per pair), one step on both
-    sides under the full-state rule."""
+def test_full_state_face_manifold(gpu, task, kind):
+    """The self-contact manifold (zb_task_cfg.self_manifold 2): "face": folded
+    states in which at least one link pair is a face-to-face contact (cap on cap, up to 4 points: the
+    oracle's candidate list has more self points than with one point per pair); "rim": folded states
+    in which a side-by-side pair gets its rim manifold (more self points than with the face manifold
+    alone); one step on both sides under the full-state rule."""
     from oracle.pyoracle import OracleSim
     # (face-to-face pairs are rare among random folds: ~0.08 % of uniformly random joint angles, and
     # in nearly all of them other link pairs overlap by several cm -- the median min separation is
     # -6 cm; scaling the angles towards the default pose finds almost no gentle face contacts)
     seed, pool = 43, 131072
     cfg1, cfg0 = task_cfg(task), task_cfg(task)
-    cfg0.self_manifold = 0
+    cfg0.self_manifold = 0 if kind == "face" else 1
     o1, o0 = OracleSim(pool, cfg1, seed=seed), OracleSim(pool, cfg0, seed=seed)
     st = random_states(task, o1, pool, seed=606)
     st[13:19] = np.random.default_rng(607).uniform(-np.pi, np.pi, (6, pool)).astype(np.float32)
@@ -424,12 +426,12 @@ def test_full_state_face_manifold(gpu, task):
     n = len(ids)
     st = np.ascontiguousarray(st[:, ids])
     g, _, cfg, torch = _sims(task, n, seed)
-    assert cfg.self_manifold == 1
+    assert cfg.self_manifold == 2
     g.set_state(torch.from_numpy(st).cuda())
     a = np.random.default_rng(608).normal(size=(n, 6)).astype(np.float32)
     obs, rew, te, tr = g.step(torch.from_numpy(a).cuda())
     g_out = (obs.cpu().numpy(), rew.cpu().numpy(), te.cpu().numpy().copy(), tr.cpu().numpy().copy())
-    nbad = _check(task, "one step from folded states with face manifolds", n, seed, st, [a], g_out,
+    nbad = _check(task, f"one step from folded states with {kind} manifolds", n, seed, st, [a], g_out,
                   g.get_state().cpu().numpy(), torch)
     # these folds are violent (several deep link overlaps pushed apart in one step): a fifth to a
     # third of the envs sit at a discontinuity. Every one must be explained, and the contact-active

@@ -153,6 +153,74 @@ def _face_pairs(n, seed):
     return out
 
 
+def _rot_axis(axis, ang):
+    axis = np.asarray(axis, float) / np.linalg.norm(axis)
+    K = np.array([[0, -axis[2], axis[1]], [axis[2], 0, -axis[0]], [-axis[1], axis[0], 0]])
+    return np.eye(3) + np.sin(ang) * K + (1 - np.cos(ang)) * K @ K
+
+
+def _rim_pairs(n, seed):
+    """Two flat links lying side by side (axes along x, one above the other), A tilted by up to 8
+    degrees about a random axis, shifted along the axis by up to 3 cm, gap -3 .. 4 mm, the whole
+    configuration rotated at random: rulings within and beyond the 5-degree rim threshold."""
+    from tests.test_oracle_selfcollision import _flat_link
+    rng = np.random.default_rng(seed)
+    lie = _rot_axis([0, 1, 0], np.pi / 2)
+    out = np.zeros((n, 2, 2, 9), np.float32)
+    for k in range(n):
+        ra, rb = rng.uniform(0.035, 0.05, 2)
+        tilt = _rot_axis(rng.normal(size=3), np.radians(rng.uniform(0, 8)))
+        G = _rot(_quat(rng))
+        pa = np.array([rng.uniform(-0.03, 0.03), 0.0, ra + rb + rng.uniform(-0.003, 0.004)])
+        ha = world(_flat_link(ra), G @ tilt @ lie, G @ pa)
+        hb = world(_flat_link(rb), G @ lie, np.zeros(3))
+        out[k, 0], out[k, 1] = ha, hb
+    return out
+
+
+def _compare_manifolds(pairs, label, ntol_multi):
+    """zb_pair_manifold vs zbo_pair_manifold: counts and (for agreeing counts) points."""
+    import torch
+    from zbot_lab_amd import _native as nat
+    n = len(pairs)
+    ref = np.zeros((n, 29), np.float32)
+    for k in range(n):
+        pts = np.zeros(28, np.float32)
+        c = pyoracle.lib().zbo_pair_manifold(np.ascontiguousarray(pairs[k, 0]).ravel(), np.ascontiguousarray(pairs[k, 1]).ravel(),
+                                             MARGIN, pts)
+        ref[k, 0] = c
+        ref[k, 1:] = pts
+    P = torch.from_numpy(np.ascontiguousarray(pairs)).cuda()
+    out = torch.zeros(n, 29, device="cuda")
+    nat.check(nat.lib().zb_pair_manifold(nat.ptr(P), n, MARGIN, nat.ptr(out), None), "zb_pair_manifold")
+    got = out.cpu().numpy()
+    same = got[:, 0] == ref[:, 0]
+    print(f"\n{label} pairs {n}: oracle counts {np.bincount(ref[:, 0].astype(int), minlength=5).tolist()}, "
+          f"GPU counts {np.bincount(got[:, 0].astype(int), minlength=5).tolist()}, count agreement {same.mean():.4f}")
+    bad = []
+    for k in np.nonzero(same & (ref[:, 0] > 0))[0]:
+        c = int(ref[k, 0])
+        g, r = got[k, 1:1 + 7 * c].reshape(c, 7), ref[k, 1:1 + 7 * c].reshape(c, 7)
+        ntol = 2e-3 if c == 1 else ntol_multi
+        if not (np.abs(g[:, 0] - r[:, 0]).max() <= 2e-5 and np.abs(g[:, 1:4] - r[:, 1:4]).max() <= ntol
+                and np.abs(g[:, 4:7] - r[:, 4:7]).max() <= 1e-4):
+            bad.append((int(k), c, float(np.abs(g - r).max())))
+    print(f"pairs outside the point bounds: {len(bad)} {bad[:8]}")
+    return ref, got, same, bad
+
+
+def test_gpu_rim_manifold_matches_oracle():
+    """The rim manifold (self_manifold 2: side-by-side rulings, the GJK point + the overlap's ends)
+    of quad_manifold (zb_pair_manifold) against the oracle's rim_manifold on 4000 side-by-side pairs:
+    the same number of points in the same order for >= 99 % (a ruling within fp32 rounding of the
+    5-degree thresholds or an end within rounding of the 1 mm rule may go either way), separations
+    to 2e-5 m, normals to 5e-4, points to 1e-4 m."""
+    ref, got, same, bad = _compare_manifolds(_rim_pairs(4000, 31), "rim manifold", 5e-4)
+    assert (ref[:, 0] >= 2).sum() >= 1000 and (ref[:, 0] == 3).sum() >= 40  # (parallel rulings: GJK ends at one end)
+    assert same.mean() >= 0.99
+    assert len(bad) <= 0.01 * same.sum(), bad[:20]
+
+
 def test_gpu_face_manifold_matches_oracle():
     """quad_manifold (zb_pair_manifold) against the oracle's face_manifold (zbo_pair_manifold) on
     face-to-face pairs and on random robot link pairs: the same number of points in the same order,

@@ -13,6 +13,8 @@ penetrating pairs (separation -overlap while the overlap is below 2 CORE_M).
 from __future__ import annotations
 
 
+import ctypes as C
+
 import numpy as np
 import pytest
 
@@ -314,3 +316,83 @@ def test_manifold_in_folded_rollouts():
             n += int(sim.contact_diag()[:, 5].sum())
         tot[mf] = n
     assert tot[1] > tot[0] > 0, tot
+
+
+def _rot_axis(axis, ang):
+    axis = np.asarray(axis, float) / np.linalg.norm(axis)
+    K = np.array([[0, -axis[2], axis[1]], [axis[2], 0, -axis[0]], [-axis[1], axis[0], 0]])
+    return np.eye(3) + np.sin(ang) * K + (1 - np.cos(ang)) * K @ K
+
+
+def _ruling_line_gap(ha, hb, n, t_pts):
+    """Gap along n between the two hulls' support rulings (the segments between their circles'
+    support points along -n / +n) at the points t_pts (brute force: nearest points on the lines)."""
+    def sup(h, d):
+        p = []
+        for c in range(2):
+            a, b = d @ h[c, 3:6], d @ h[c, 6:9]
+            p.append(h[c, :3] + (a * h[c, 3:6] + b * h[c, 6:9]) / np.hypot(a, b))
+        return np.array(p)
+    pa, pb = sup(ha, -n), sup(hb, n)
+    return pa, pb
+
+
+def test_rim_manifold_side_by_side():
+    """Side by side (cfg self_manifold 2): two links lying with parallel axes touch along a line;
+    the pair gives the GJK point plus the two ends of the rulings' overlap, every point at the line
+    gap (constant along parallel rulings), normals perpendicular to the rulings; with the second link
+    shifted along the axis the overlap shrinks to the common part; rulings crossing at 20 degrees
+    give the GJK point alone; a tilt within 5 degrees keeps the ends at the rulings' gap there."""
+    link = _flat_link(0.05)
+    axis_x = _rot_axis([0, 1, 0], np.pi / 2)  # the link's axis (z) along x: lying on its side
+    for gap in (0.002, 0.0004):
+        ha = world(link, axis_x, np.array([0.0, 0.0, 2 * 0.05 + gap]))
+        hb = world(link, axis_x, np.array([0.0, 0.0, 0.0]))
+        pts = pair_manifold(ha, hb, 0.004)
+        assert len(pts) in (2, 3), (gap, pts)  # (an end within 1 mm of the GJK point is not repeated)
+        np.testing.assert_allclose(pts[:, 0], gap, atol=5e-6)
+        np.testing.assert_allclose(pts[:, 1:4], np.tile([0, 0, 1], (len(pts), 1)), atol=1e-5)
+        # the points span the core rulings (the link lies along x in [0, 0.053], its cores inset by CORE_M)
+        assert abs(pts[:, 4].min() - CORE_M) < 1e-3 + 1e-5 and abs(pts[:, 4].max() - (0.053 - CORE_M)) < 1e-3 + 1e-5
+    ha = world(link, axis_x, np.array([0.02, 0.0, 2 * 0.05 + 0.001]))
+    hb = world(link, axis_x, np.array([0.0, 0.0, 0.0]))
+    pts = pair_manifold(ha, hb, 0.004)
+    assert len(pts) in (2, 3)
+    assert abs(pts[:, 4].min() - (0.02 + CORE_M)) < 1e-3 + 1e-5 and abs(pts[:, 4].max() - (0.053 - CORE_M)) < 1e-3 + 1e-5
+    # crossing rulings: one point
+    ha = world(link, _rot_axis([0, 0, 1], np.radians(20)) @ axis_x, np.array([0.0, 0.0, 0.101]))
+    hb = world(link, axis_x, np.array([0.0, 0.0, 0.0]))
+    pts = pair_manifold(ha, hb, 0.004)
+    assert len(pts) == 1
+    # a small tilt (3 degrees about y): the ends' separations are the gaps of the two core rulings
+    # along the reported normal at those ends (direct evaluation on the support lines)
+    ha = world(link, _rot_axis([0, 1, 0], np.radians(3)) @ axis_x, np.array([0.0, 0.0, 0.1005]))
+    hb = world(link, axis_x, np.array([0.0, 0.0, 0.0]))
+    pts = pair_manifold(ha, hb, 0.004)
+    assert len(pts) >= 2, pts
+    n = pts[0, 1:4].astype(float)
+    pa, pb = _ruling_line_gap(ha, hb, n, None)
+    for p in pts[1:]:
+        x = p[4:7].astype(float)
+        ta = (x - pa[0]) @ (pa[1] - pa[0]) / np.sum((pa[1] - pa[0]) ** 2)
+        tb = (x - pb[0]) @ (pb[1] - pb[0]) / np.sum((pb[1] - pb[0]) ** 2)
+        xa, xb = pa[0] + ta * (pa[1] - pa[0]), pb[0] + tb * (pb[1] - pb[0])
+        assert abs((xa - xb) @ n - 2 * CORE_M - p[0]) < 2e-5, (p, (xa - xb) @ n - 2 * CORE_M)
+    assert pts[:, 0].max() - pts[:, 0].min() > 1e-3  # the tilt shows in the gaps along the line
+    assert abs(n @ (pa[1] - pa[0])) < 1e-6  # perpendicular to A's ruling
+
+
+def test_rim_manifold_mode_switch():
+    """self_manifold 1 keeps the face manifold only: the side-by-side pair is the GJK point alone."""
+    link = _flat_link(0.05)
+    axis_x = _rot_axis([0, 1, 0], np.pi / 2)
+    ha = world(link, axis_x, np.array([0.0, 0.0, 0.101]))
+    hb = world(link, axis_x, np.array([0.0, 0.0, 0.0]))
+    lib = pyoracle.lib()
+    lib.zbo_set_pair_manifold_mode.argtypes = [C.c_int]
+    try:
+        lib.zbo_set_pair_manifold_mode(1)
+        assert len(pair_manifold(ha, hb, 0.004)) == 1
+    finally:
+        lib.zbo_set_pair_manifold_mode(2)
+    assert len(pair_manifold(ha, hb, 0.004)) >= 2

@@ -1275,9 +1275,74 @@ __device__ __forceinline__ bool gjk_quad(const QCircle& h, int j, const float v0
 // control flow (DPP within the quad).
 constexpr float kFaceCos = 0.9659258262890683f;  // cos 15 deg (= oracle FACE_COS)
 constexpr float kFaceInsetC = 0.9995500337489875f, kFaceInsetS = 0.029995500202495664f;  // cos / sin 0.03
+constexpr float kRimCos = 0.9961946980917455f, kRimSin = 0.08715574274765817f;  // cos / sin 5 deg (= oracle RIM_COS)
+
+// Rim (ruling) manifold on the pair's quad (cfg.self_manifold 2, no face pair; the oracle's
+// rim_manifold): lane j's circle support point along its hull's direction (A: -n, B: +n), the four
+// broadcast in the quad; when A's ruling (A c0 -> A c1 supports) and B's lie within 5 degrees of the
+// contact plane and of each other: the GJK point (lane 0 writes it) and the two ends of the rulings'
+// overlap along A's ruling (lanes 1 and 2), more than 1 mm from the GJK point and within the margin,
+// all with the normal made perpendicular to A's ruling. Returns the point count (0: no rim pair).
+template <class Sink>
+__device__ __forceinline__ int quad_rim(const QCircle& h, int j, const SelfContact& sc, float margin, bool write,
+                                        Sink sink) {
+  const float sgd = (j & 2) ? 1.f : -1.f;
+  const float dd[3] = {sgd * sc.n[0], sgd * sc.n[1], sgd * sc.n[2]};
+  const float a = dot3(dd, h.e1), b = dot3(dd, h.e2);
+  const float ri = __builtin_amdgcn_rsqf(fmaxf(fmaf(a, a, b * b), 1e-30f));
+  float p[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) p[k] = h.c[k] + (a * h.e1[k] + b * h.e2[k]) * ri;
+  float a0[3], sa[3], b0[3], sb[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const float p0 = dppf<0x00>(p[k]), p1 = dppf<0x55>(p[k]), p2 = dppf<0xAA>(p[k]), p3 = dppf<0xFF>(p[k]);
+    a0[k] = p0; sa[k] = p1 - p0; b0[k] = p2; sb[k] = p3 - p2;
+  }
+  const float la = sqrtf(dot3(sa, sa)), lb = sqrtf(dot3(sb, sb));
+  if (la < 1e-3f || lb < 1e-3f) return 0;
+  if (fabsf(dot3(sa, sc.n)) > kRimSin * la || fabsf(dot3(sb, sc.n)) > kRimSin * lb) return 0;
+  if (fabsf(dot3(sa, sb)) < kRimCos * la * lb) return 0;
+  const float ila = 1.f / la;
+  const float ah[3] = {sa[0] * ila, sa[1] * ila, sa[2] * ila};
+  const float na = dot3(sc.n, ah);
+  float nr[3] = {sc.n[0] - na * ah[0], sc.n[1] - na * ah[1], sc.n[2] - na * ah[2]};
+  const float inr = __builtin_amdgcn_rsqf(fmaxf(dot3(nr, nr), 1e-30f));
+  nr[0] *= inr; nr[1] *= inr; nr[2] *= inr;
+  const float w0[3] = {b0[0] - a0[0], b0[1] - a0[1], b0[2] - a0[2]};
+  const float wg[3] = {sc.x[0] - a0[0], sc.x[1] - a0[1], sc.x[2] - a0[2]};
+  const float tb0 = dot3(w0, ah), tb1 = tb0 + dot3(sb, ah), tg = dot3(wg, ah);
+  const float lo = fmaxf(0.f, fminf(tb0, tb1)), hi = fminf(la, fmaxf(tb0, tb1));
+  const bool span = hi - lo > 1e-3f;
+  const float dtb = tb1 - tb0;
+  bool ok[2];
+  float4 px[2];
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const float t = e ? hi : lo;
+    const float ua = t * ila, ub = (t - tb0) / (fabsf(dtb) > 1e-12f ? dtb : 1e-12f);
+    float xa[3], xb[3], g[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      xa[k] = a0[k] + ua * sa[k];
+      xb[k] = b0[k] + ub * sb[k];
+      g[k] = xa[k] - xb[k];
+    }
+    const float sep = dot3(g, nr) - 2.f * kCoreM;
+    ok[e] = span && fabsf(t - tg) > 1e-3f && sep < margin;
+    px[e] = make_float4(0.5f * (xa[0] + xb[0]), 0.5f * (xa[1] + xb[1]), 0.5f * (xa[2] + xb[2]), sep);
+  }
+  if (write) {
+    if (j == 0) sink(0, make_float4(sc.x[0], sc.x[1], sc.x[2], sc.sep), nr);
+    if (j == 1 && ok[0]) sink(1, px[0], nr);
+    if (j == 2 && ok[1]) sink(ok[0] ? 2 : 1, px[1], nr);
+  }
+  return 1 + (ok[0] ? 1 : 0) + (ok[1] ? 1 : 0);
+}
+
 template <class Sink>
 __device__ __forceinline__ int quad_manifold(const QCircle& h, int j, const SelfContact& sc, float margin, bool write,
-                                             Sink sink) {
+                                             bool rim, Sink sink) {
   const float sgd = (j & 2) ? 1.f : -1.f;
   const float dd[3] = {sgd * sc.n[0], sgd * sc.n[1], sgd * sc.n[2]};
   float u[3];
@@ -1292,7 +1357,7 @@ __device__ __forceinline__ int quad_manifold(const QCircle& h, int j, const Self
   int fm = (sup && fabsf(al) >= kFaceCos) ? (1 << j) : 0;
   fm |= dppi<DPP_XOR1>(fm);
   fm |= dppi<DPP_XOR2>(fm);
-  if (!(fm & 3) || !(fm & 12)) return 0;
+  if (!(fm & 3) || !(fm & 12)) return rim ? quad_rim(h, j, sc, margin, write, sink) : 0;
   const float so = al < 0.f ? -1.f : 1.f;
   const float uo[3] = {so * u[0], so * u[1], so * u[2]};
   const bool a1 = !(fm & 1), b3 = !(fm & 4);  // A's face on quad lane 1 (else 0), B's on 3 (else 2)
@@ -1542,7 +1607,7 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q&
     // team, bit r: the pair of rank r is a contact (allhits), its points - 1 = exl + 2 exh: a pair's
     // first candidate position is g_tot + the points of the lower ranks
     unsigned long long allhits = 0ull, exl = 0ull, exh = 0ull;
-    const bool mfon = cfg.self_manifold != 0;
+    const bool mfon = cfg.self_manifold != 0, rimon = cfg.self_manifold >= 2;
 #pragma unroll 1
     for (int pass = 0; pass < 2; ++pass) {
       for (int k = 0; k < urounds; ++k) {
@@ -1596,7 +1661,7 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q&
         // write pass stores its points
         const float code = (float)(pcode + 1);
         const int mc = (mfon && sc.sep > -2.f * kCoreM + 1e-7f)
-                           ? quad_manifold(hc, qj, sc, margin, pass == 1, [&](int rank, float4 xs, const float* nn) {
+                           ? quad_manifold(hc, qj, sc, margin, pass == 1, rimon, [&](int rank, float4 xs, const float* nn) {
                                if (pos + rank < g_tot + NSELF) {
                                  q.cand(pos + rank, 0) = xs;
                                  q.cand(pos + rank, 1) = make_float4(nn[0], nn[1], nn[2], code);
@@ -3351,7 +3416,7 @@ __global__ void zb_manifold_kernel(const float* __restrict__ pairs, int n, float
   const bool mine = (t >> 2) < n;
   int cnt = 0;
   if (hit && sc.sep > -2.f * kCoreM + 1e-7f)
-    cnt = quad_manifold(h, j, sc, margin, true, [&](int rank, float4 xs, const float* nn) {
+    cnt = quad_manifold(h, j, sc, margin, true, true, [&](int rank, float4 xs, const float* nn) {
       if (mine) {
         float* p = o + 1 + 7 * rank;
         p[0] = xs.w; p[1] = nn[0]; p[2] = nn[1]; p[3] = nn[2]; p[4] = xs.x; p[5] = xs.y; p[6] = xs.z;

@@ -51,7 +51,7 @@ class SolverCfg:
     baumgarte: float = 0.2
     self_collision: bool = True       # enabled_self_collisions=True (zbot_cfg.py:636)
     mode: int = 0                     # 0: PGS sweeps; 1: TGS-style sub-iterations; 2: TGS + ground-contact refresh (zb_task_cfg.solver_mode)
-    self_manifold: int = 1            # 1: cap-on-cap self contacts with up to 4 points (zb_task_cfg.self_manifold)
+    self_manifold: int = 2            # 2: cap-on-cap (up to 4 points) + side-by-side rims (up to 3); 1: caps only; 0: off (zb_task_cfg.self_manifold)
 
 
 def _scales(**kw) -> dict:
