@@ -412,7 +412,8 @@ def test_full_state_face_manifold(gpu, task, kind):
     # (face-to-face pairs are rare among random folds: ~0.08 % of uniformly random joint angles, and
     # in nearly all of them other link pairs overlap by several cm -- the median min separation is
     # -6 cm; scaling the angles towards the default pose finds almost no gentle face contacts)
-    seed, pool = 43, 131072
+    # (rim points are rarer still: ~2 in 10 000 random folds, so the rim case draws a larger pool)
+    seed, pool = 43, 131072 if kind == "face" else 393216
     cfg1, cfg0 = task_cfg(task), task_cfg(task)
     cfg0.self_manifold = 0 if kind == "face" else 1
     o1, o0 = OracleSim(pool, cfg1, seed=seed), OracleSim(pool, cfg0, seed=seed)
@@ -422,7 +423,7 @@ def test_full_state_face_manifold(gpu, task, kind):
     o0.set_state(st)
     extra = o1.contact_diag()[:, 5] - o0.contact_diag()[:, 5]
     ids = np.nonzero(extra > 0)[0][:512]
-    assert len(ids) >= 64, len(ids)
+    assert len(ids) >= (64 if kind == "face" else 40), len(ids)
     n = len(ids)
     st = np.ascontiguousarray(st[:, ids])
     g, _, cfg, torch = _sims(task, n, seed)
