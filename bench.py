@@ -61,6 +61,7 @@ def parse():
     # ablation knobs (the reported line uses the defaults)
     p.add_argument("--solver-iterations", type=int, default=None)
     p.add_argument("--no-self-collision", action="store_true")
+    p.add_argument("--self-manifold", type=int, default=None, help="zb_task_cfg.self_manifold (0 / 1 / 2)")
     p.add_argument("--rehearsal", action="store_true",
                    help="N ranks share cuda:0 over gloo (one-GPU box rehearsal; reports n_gpus 1)")
     return p.parse_args()
@@ -276,6 +277,8 @@ def main():
     cfg.seed = 42 + rank
     if args.solver_iterations is not None:
         cfg.solver.iterations = args.solver_iterations
+    if args.self_manifold is not None:
+        cfg.solver.self_manifold = args.self_manifold
     if args.no_self_collision:
         cfg.solver.self_collision = False
     env = (Zbot6SUpEnv(cfg) if standup else Zbot6SEnvV4(cfg) if v4 else ZbotManagerBasedRLEnv(cfg) if mgr

@@ -751,11 +751,12 @@ static int face_manifold(const hull_t* A, const hull_t* B, const contact_t* c0, 
  * pair): two links lying side by side touch along a line -- the nearest features are a ruling of each
  * core hull, the segment between the support points of its two circles along the pair direction (A:
  * -n, B: +n). When both rulings lie within RIM_DEG of the contact plane and of each other, the pair
- * contributes up to 3 points: the GJK point, then the two ends of the rulings' overlap along A's
- * ruling (kept when more than 1 mm from the GJK point along it and within the margin), each with
- * the normal n made perpendicular to A's ruling (the component of a line contact's GJK normal along
- * the line is determined only to GJK's tolerance cone); an end's separation is the gap between the
- * two rulings along that normal at that end, minus 2 CORE_M. Rulings absent or crossing: the GJK
+ * contributes up to 3 points: the GJK point (with its GJK normal, which also warm-starts the pair's
+ * GJK in the next substep), then the two ends of the rulings' overlap along A's ruling (kept when
+ * more than 1 mm from the GJK point along it and within the margin), each with the normal n made
+ * perpendicular to A's ruling (the component of a line contact's GJK normal along the line is
+ * determined only to GJK's tolerance cone); an end's separation is the gap between the two rulings
+ * along that normal at that end, minus 2 CORE_M. Rulings absent or crossing: the GJK
  * contact alone. (The kernel: the rim branch of quad_manifold, on the pair's quad.) */
 #define RIM_COS 0.9961946980917455 /* cos 5 deg */
 static double g_rim_cos = RIM_COS; /* moved with the face threshold by zbo_set_face_cos (15 deg -> 5 deg scale) */
@@ -794,9 +795,7 @@ static int rim_manifold(const hull_t* A, const hull_t* B, const contact_t* c0, r
   const real tb0 = v3_dot(w0, ah), tb1 = v3_dot(w1, ah), tg = v3_dot(wg, ah);
   const real lo = fmax((double)0, (double)(tb0 < tb1 ? tb0 : tb1)), hi = fmin((double)la, (double)(tb0 < tb1 ? tb1 : tb0));
   int k = 0;
-  out[k] = *c0;
-  for (int q = 0; q < 3; ++q) out[k].n[q] = nr[q];
-  ++k;
+  out[k++] = *c0; /* (its own GJK normal: the pair's warm start in the next substep, as without a rim) */
   if (!(hi - lo > (real)1e-3)) return k;
   const real dtb = tb1 - tb0;
   for (int e = 0; e < 2; ++e) {

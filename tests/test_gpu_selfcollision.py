@@ -178,7 +178,7 @@ def _rim_pairs(n, seed):
     return out
 
 
-def _compare_manifolds(pairs, label, ntol_multi):
+def _compare_manifolds(pairs, label, ntol_multi, gjk_first=False):
     """zb_pair_manifold vs zbo_pair_manifold: counts and (for agreeing counts) points."""
     import torch
     from zbot_lab_amd import _native as nat
@@ -201,8 +201,11 @@ def _compare_manifolds(pairs, label, ntol_multi):
     for k in np.nonzero(same & (ref[:, 0] > 0))[0]:
         c = int(ref[k, 0])
         g, r = got[k, 1:1 + 7 * c].reshape(c, 7), ref[k, 1:1 + 7 * c].reshape(c, 7)
-        ntol = 2e-3 if c == 1 else ntol_multi
-        if not (np.abs(g[:, 0] - r[:, 0]).max() <= 2e-5 and np.abs(g[:, 1:4] - r[:, 1:4]).max() <= ntol
+        # (rim manifolds: the first point is the GJK point with GJK's own normal)
+        ntol = np.full(c, 2e-3 if c == 1 else ntol_multi)
+        if gjk_first:
+            ntol[0] = 2e-3
+        if not (np.abs(g[:, 0] - r[:, 0]).max() <= 2e-5 and (np.abs(g[:, 1:4] - r[:, 1:4]).max(axis=1) <= ntol).all()
                 and np.abs(g[:, 4:7] - r[:, 4:7]).max() <= 1e-4):
             bad.append((int(k), c, float(np.abs(g - r).max())))
     print(f"pairs outside the point bounds: {len(bad)} {bad[:8]}")
@@ -215,7 +218,7 @@ def test_gpu_rim_manifold_matches_oracle():
     the same number of points in the same order for >= 99 % (a ruling within fp32 rounding of the
     5-degree thresholds or an end within rounding of the 1 mm rule may go either way), separations
     to 2e-5 m, normals to 5e-4, points to 1e-4 m."""
-    ref, got, same, bad = _compare_manifolds(_rim_pairs(4000, 31), "rim manifold", 5e-4)
+    ref, got, same, bad = _compare_manifolds(_rim_pairs(4000, 31), "rim manifold", 5e-4, gjk_first=True)
     assert (ref[:, 0] >= 2).sum() >= 1000 and (ref[:, 0] == 3).sum() >= 40  # (parallel rulings: GJK ends at one end)
     assert same.mean() >= 0.99
     assert len(bad) <= 0.01 * same.sum(), bad[:20]

@@ -351,7 +351,8 @@ def test_rim_manifold_side_by_side():
         pts = pair_manifold(ha, hb, 0.004)
         assert len(pts) in (2, 3), (gap, pts)  # (an end within 1 mm of the GJK point is not repeated)
         np.testing.assert_allclose(pts[:, 0], gap, atol=5e-6)
-        np.testing.assert_allclose(pts[:, 1:4], np.tile([0, 0, 1], (len(pts), 1)), atol=1e-5)
+        np.testing.assert_allclose(pts[1:, 1:4], np.tile([0, 0, 1], (len(pts) - 1, 1)), atol=1e-5)  # the ends
+        np.testing.assert_allclose(pts[0, 1:4], [0, 0, 1], atol=3e-3)  # the GJK point keeps GJK's normal
         # the points span the core rulings (the link lies along x in [0, 0.053], its cores inset by CORE_M)
         assert abs(pts[:, 4].min() - CORE_M) < 1e-3 + 1e-5 and abs(pts[:, 4].max() - (0.053 - CORE_M)) < 1e-3 + 1e-5
     ha = world(link, axis_x, np.array([0.02, 0.0, 2 * 0.05 + 0.001]))
@@ -370,7 +371,7 @@ def test_rim_manifold_side_by_side():
     hb = world(link, axis_x, np.array([0.0, 0.0, 0.0]))
     pts = pair_manifold(ha, hb, 0.004)
     assert len(pts) >= 2, pts
-    n = pts[0, 1:4].astype(float)
+    n = pts[-1, 1:4].astype(float)  # (an end's normal: perpendicular to A's ruling)
     pa, pb = _ruling_line_gap(ha, hb, n, None)
     for p in pts[1:]:
         x = p[4:7].astype(float)

@@ -1280,9 +1280,10 @@ constexpr float kRimCos = 0.9961946980917455f, kRimSin = 0.08715574274765817f;  
 // Rim (ruling) manifold on the pair's quad (cfg.self_manifold 2, no face pair; the oracle's
 // rim_manifold): lane j's circle support point along its hull's direction (A: -n, B: +n), the four
 // broadcast in the quad; when A's ruling (A c0 -> A c1 supports) and B's lie within 5 degrees of the
-// contact plane and of each other: the GJK point (lane 0 writes it) and the two ends of the rulings'
-// overlap along A's ruling (lanes 1 and 2), more than 1 mm from the GJK point and within the margin,
-// all with the normal made perpendicular to A's ruling. Returns the point count (0: no rim pair).
+// contact plane and of each other: the GJK point with its GJK normal (lane 0 writes it; the pair's
+// warm start in the next substep) and the two ends of the rulings' overlap along A's ruling (lanes 1
+// and 2), more than 1 mm from the GJK point and within the margin, with the normal made
+// perpendicular to A's ruling. Returns the point count (0: no rim pair).
 template <class Sink>
 __device__ __forceinline__ int quad_rim(const QCircle& h, int j, const SelfContact& sc, float margin, bool write,
                                         Sink sink) {
@@ -1333,7 +1334,7 @@ __device__ __forceinline__ int quad_rim(const QCircle& h, int j, const SelfConta
     px[e] = make_float4(0.5f * (xa[0] + xb[0]), 0.5f * (xa[1] + xb[1]), 0.5f * (xa[2] + xb[2]), sep);
   }
   if (write) {
-    if (j == 0) sink(0, make_float4(sc.x[0], sc.x[1], sc.x[2], sc.sep), nr);
+    if (j == 0) sink(0, make_float4(sc.x[0], sc.x[1], sc.x[2], sc.sep), sc.n);  // (GJK's normal: the warm start)
     if (j == 1 && ok[0]) sink(1, px[0], nr);
     if (j == 2 && ok[1]) sink(ok[0] ? 2 : 1, px[1], nr);
   }
