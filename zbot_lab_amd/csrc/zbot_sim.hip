@@ -1634,8 +1634,10 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q&
           }
           bool hot = false;  // warm start from a kept contact of the previous substep
           if (warm) {
+            // (downwards: the pair's first kept point wins, the oracle's first match -- a rim
+            // manifold's GJK point, whose GJK normal is the better start than its ends' normal)
 #pragma unroll
-            for (int c = 0; c < NCM; ++c) {
+            for (int c = NCM - 1; c >= 0; --c) {
               const float4 f = q.frc(c);
               const bool m = f.w == (float)(pcode + 1);
               v0[0] = m ? f.x : v0[0]; v0[1] = m ? f.y : v0[1]; v0[2] = m ? f.z : v0[2];
