@@ -275,3 +275,49 @@ def test_gpu_update_graph_matches_eager(gpu):
         assert abs(lr_graph - float(alg.lr_t)) <= 1e-7
         torch.testing.assert_close(sums_graph, alg.update_sums, rtol=1e-4, atol=1e-6)
     env.close()
+
+
+class ViewLogToyEnv(LogToyEnv):
+    """extras["log"] as fixed 0-d views into two device buffers (float means, int32 counts), like
+    the walking tasks' zb_read_log buffers: the runner's one-gather-per-buffer accumulation path."""
+
+    def __init__(self, **kw):
+        super().__init__(**kw)
+        self.means = torch.zeros(4)
+        self.counts = torch.zeros(2, dtype=torch.int32)
+        self._log = {"Episode_Reward/a": self.means[2], "Episode_Reward/b": self.means[0],
+                     "Episode_Termination/c": self.counts[1]}
+
+    def step(self, actions):
+        o, r, d, ex = super().step(actions)
+        self.means.copy_(torch.tensor([1.0, 0.0, 2.0, 0.0]) * self.k)
+        self.counts[1] = self.k % 3
+        ex["log"] = self._log
+        return o, r, d, ex
+
+
+def test_runner_log_views_accumulate_like_copies():
+    """The gather path (_log_views) gives the mean over the rollout's steps of every key, as the
+    per-key copy path does."""
+    from zbot_lab_amd.rl import OnPolicyRunner, PPORunnerCfgV2
+    cfg = PPORunnerCfgV2()
+    cfg.num_steps_per_env = 4
+    runner = OnPolicyRunner(ViewLogToyEnv(n=16), cfg.to_dict(), log_dir=None, device="cpu")
+    log = runner.learn(2)
+    assert runner._log_groups is not None and len(runner._log_groups) == 2
+    assert log[0]["Episode_Reward/a"] == pytest.approx(2 * (1 + 2 + 3 + 4) / 4)
+    assert log[0]["Episode_Reward/b"] == pytest.approx((1 + 2 + 3 + 4) / 4)
+    assert log[1]["Episode_Termination/c"] == pytest.approx((5 % 3 + 6 % 3 + 7 % 3 + 8 % 3) / 4)
+
+
+def test_fused_rollout_is_gpu_only(monkeypatch):
+    """The fused rollout step (zbp_act / zbp_env_post) serves GPU storage only and can be switched
+    off (ZBOT_ROLLOUT_FUSED=0); on the CPU the runner keeps the torch statements."""
+    from zbot_lab_amd.rl.ppo import PPO, ActorCritic
+    pol = ActorCritic(23, 23, 6)
+    alg = PPO(pol, device="cpu")
+    assert alg.fused_rollout() is None  # no storage yet
+    alg.init_storage(64, 24, 23, 23, 6)
+    assert alg.fused_rollout() is None  # CPU tensors
+    monkeypatch.setenv("ZBOT_ROLLOUT_FUSED", "0")
+    assert alg.fused_rollout() is None
