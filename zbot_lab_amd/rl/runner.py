@@ -286,6 +286,8 @@ class OnPolicyRunner:
             self.alg.optimizer.load_state_dict(d["optimizer_state_dict"])
             self.alg.restore_learning_rate()
             self.alg.invalidate_fused()  # the fused update re-reads the new optimizer state
+        # captured graphs hold the old fused driver's workspace: re-capture on the next iteration
+        self._graph, self._update_graph = None, None
         self.current_learning_iteration = d["iter"]
         return d.get("infos")
 
