@@ -904,6 +904,40 @@ int zbo_undecided_pairs(zbo_sim* s, float* out, int max) {
   return cnt;
 }
 
+/* GJK tail probe (tooling, tools/gjk/tail_classes.py): the probe's GJK calls by the configuration
+ * they converge to (0 no contact within the margin, 1 face on face, 2 a ruling lying on a face
+ * within RIM_DEG, 3 side-by-side rulings within RIM_DEG -- the rim manifold's case --, 4 side by side
+ * within FACE_DEG, 5 any other: point-like) x support iterations */
+#define GJK_NCLS 6
+static long long g_gjk_cls[GJK_NCLS][GJK_MAX_IT + 2];
+static int gjk_class(const hull_t* A, const hull_t* B, const contact_t* c, int hit) {
+  if (!hit) return 0;
+  const real nA[3] = {-c->n[0], -c->n[1], -c->n[2]};
+  real ua[3], ub[3];
+  const int fa = hull_face(A, nA, ua), fb = hull_face(B, c->n, ub);
+  if (fa >= 0 && fb >= 0) return 1;
+  real pa[2][3], pb[2][3], sa[3], sb[3];
+  hull_ruling(A, nA, pa);
+  hull_ruling(B, c->n, pb);
+  for (int q = 0; q < 3; ++q) { sa[q] = pa[1][q] - pa[0][q]; sb[q] = pb[1][q] - pb[0][q]; }
+  const real la = sqrtr(v3_dot(sa, sa)), lb = sqrtr(v3_dot(sb, sb));
+  const real s5 = (real)0.08715574274765817, s15 = (real)0.25881904510252074;
+  const int ra5 = la > (real)1e-3 && fabs((double)v3_dot(sa, c->n)) <= s5 * la;
+  const int rb5 = lb > (real)1e-3 && fabs((double)v3_dot(sb, c->n)) <= s5 * lb;
+  if ((fa >= 0 && rb5) || (fb >= 0 && ra5)) return 2;
+  const int ra15 = la > (real)1e-3 && fabs((double)v3_dot(sa, c->n)) <= s15 * la;
+  const int rb15 = lb > (real)1e-3 && fabs((double)v3_dot(sb, c->n)) <= s15 * lb;
+  const real cab = la > 0 && lb > 0 ? fabs((double)v3_dot(sa, sb)) / (la * lb) : 0;
+  if (ra5 && rb5 && cab >= (real)RIM_COS) return 3;
+  if (ra15 && rb15 && cab >= (real)FACE_COS) return 4;
+  return 5;
+}
+int zbo_gjk_classes(long long* out) {
+  for (int k = 0; k < GJK_NCLS; ++k)
+    for (int i = 0; i < GJK_MAX_IT + 2; ++i) { out[k * (GJK_MAX_IT + 2) + i] = g_gjk_cls[k][i]; g_gjk_cls[k][i] = 0; }
+  return GJK_MAX_IT + 2;
+}
+
 /* GJK probe / warm-start switches (tooling hooks): warm = 0 runs every GJK cold from the best
  * separating axis; probe = 1 histograms the support iterations of the GJK calls the kernel would
  * make (pairs the separating-axis test leaves undecided). hist: GJK_MAX_IT + 2 counters. */
@@ -1048,7 +1082,10 @@ static void detect(const mdl_t* m, const zb_task_cfg* cfg, const kin_t* k, real 
       ++nund;
       contact_t c;
       const int hit = hull_pair(&A, &B, margin, margin, g_gjk_warm ? v0 : NULL, &c);
-      if (g_gjk_probe) __atomic_fetch_add(&g_gjk_hist[g_gjk_last_it], 1, __ATOMIC_RELAXED);
+      if (g_gjk_probe) {
+        __atomic_fetch_add(&g_gjk_hist[g_gjk_last_it], 1, __ATOMIC_RELAXED);
+        __atomic_fetch_add(&g_gjk_cls[gjk_class(&A, &B, &c, hit)][g_gjk_last_it], 1, __ATOMIC_RELAXED);
+      }
       if (hit) {
         c.la = la; c.lb = lb; c.rim = -1;
         contact_t mf[4];
