@@ -10,7 +10,7 @@ bracketed by barrier + synchronize; the max time over ranks is used. Prints ONE 
 
 ``roofline``: the dominant kernel is ``zb_step_kernel``; its per-launch time is measured in this
 process with hipEvents on the launch stream (libzbot ``zb_profile_begin/end``). Algorithmic bytes
-per env-step = 922 B: 84 fp32 persistent state read + written, the 16-float
+per env-step = 946 B: 87 fp32 persistent state read + written, the 16-float
 self-contact cache read + written (128 B), actions 24 B, obs 92 B, reward 4 B, two flag bytes. ``cpu_baseline``: the C oracle (same model + algorithm,
 OpenMP over envs) on all of this host's cores available to the process and on one thread, on a
 bounded sample, with nproc / affinity / cgroup quota / CPU model stated.
@@ -41,7 +41,9 @@ import time
 import torch
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-BYTES_PER_ENV_STEP = 794 + 2 * 16 * 4  # = 922: SURVEY.md §8d's 794 + the contact cache
+# = 946: SURVEY.md §8d's 794 + the contact cache + round 5's three rows (step0's feet_force_sum
+# and the episode sums of its two terms, v2.py:78-92, 238)
+BYTES_PER_ENV_STEP = 794 + 2 * 16 * 4 + 2 * 3 * 4
 WC_BYTES = 2 * 16 * 4  # the contact cache read + written
 SU_BYTES_PER_ENV_STEP = 2 * 43 * 4 + 24 * 4 + 24 + 88 + 4 + 2 + WC_BYTES  # = 686, stand-up task
 V4_BYTES_PER_ENV_STEP = 81 * 4 + 85 * 4 + 24 + 96 + 4 + 2 + WC_BYTES       # = 918, walking v4

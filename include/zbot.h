@@ -52,7 +52,7 @@ extern "C" {
 #define ZB_NUM_DOF 6          /* revolute joint1..joint6 */
 #define ZB_ACT_DIM 6
 #define ZB_OBS_DIM 23
-#define ZB_NUM_REWARD_TERMS 13
+#define ZB_NUM_REWARD_TERMS 15  /* step4's 13 (v2.py:190-206) + step0's feet_force_diff / feet_force_sum (v2.py:78-91) */
 #define ZB_HIST 5             /* contact sensor history_length (v2.py:32) */
 #define ZB_MAX_SELF_PAIRS 64
 #ifndef ZB_MAX_CONTACTS
@@ -106,8 +106,9 @@ enum zb_state_field {
   ZB_S_FEET_AIR_LAST = 66,  /* 2  last_air_time[feet] */
   ZB_S_FEET_CONTACT_CUR = 68,/*2  current_contact_time[feet] */
   ZB_S_EP_LEN = 70,         /* 1  episode_length_buf (integer-valued float) */
-  ZB_S_EP_SUMS = 71,        /* 13 _episode_sums in reward-term order */
-  ZB_STATE_DIM = 84
+  ZB_S_EP_SUMS = 71,        /* 15 _episode_sums in reward-term order */
+  ZB_S_FEET_FORCE_SUM = 86, /* 1  v2.py:238 (step0's feet_force_sum integrator, zeroed on reset :437) */
+  ZB_STATE_DIM = 87
 };
 
 /* Stand-up task state, SoA [ZB_SU_STATE_DIM][num_envs] float32. Rows 0..24 (root, joints) are
@@ -190,11 +191,13 @@ enum zb_standup_reward_term {
   ZB_SU_R_UPWARD_2 = 0, ZB_SU_R_SHAPE_SYMMETRY, ZB_SU_R_FEET_DOWNWARD, ZB_SU_R_FEET_DOWNWARD_4
 };
 
-/* Reward term order = dict order of ZbotDirectEnvCfgV2.reward_cfg (v2.py:190-206). */
+/* Reward term order = dict order of ZbotDirectEnvCfgV2.reward_cfg (v2.py:190-206), then step0's two
+ * feet-force terms (v2.py:78-91, 563-571; feet_force_diff before feet_force_sum, as in that dict). */
 enum zb_reward_term {
   ZB_R_BASE_VEL_FORWARD = 0, ZB_R_FEET_DOWNWARD, ZB_R_FEET_FORWARD, ZB_R_BASE_HEADING_X,
   ZB_R_BASE_HEADING_X_SUM, ZB_R_STEP_LENGTH, ZB_R_AIRTIME_BALANCE, ZB_R_ACTION_RATE,
-  ZB_R_TORQUES, ZB_R_FEET_SLIDE, ZB_R_BASE_POS_Y_ERR, ZB_R_BASE_POS_Y_ERR_SUM, ZB_R_AIRTIME_SUM
+  ZB_R_TORQUES, ZB_R_FEET_SLIDE, ZB_R_BASE_POS_Y_ERR, ZB_R_BASE_POS_Y_ERR_SUM, ZB_R_AIRTIME_SUM,
+  ZB_R_FEET_FORCE_DIFF, ZB_R_FEET_FORCE_SUM
 };
 
 /* Robot model: ZBOT_6S_CFG (zbot_cfg.py:621-669) + zbot_6s_new.usd, fixed joints merged.
@@ -327,6 +330,13 @@ typedef struct zb_task_cfg {
    * two rulings within 5 degrees of the contact plane and of each other: the GJK point and the two
    * ends of the rulings' overlap (up to 3 points); 0 = one point per pair */
   int32_t self_manifold;
+  /* walking v2: bit t set = reward term t is in the active reward_cfg (v2.py:246-257 builds
+   * reward_functions from its keys). The reference updates a stateful term's buffers inside its
+   * _reward_<name> only, so they advance only while the term is active: base_heading_x_sum
+   * (v2.py:484-487), base_pos_y_err_sum (497-500), step_length's touchdown latches and
+   * feet_contact_forces_last (509-533), feet_force_sum (567-571). A term can be active with
+   * weight 0. Other tasks ignore it. */
+  uint32_t reward_active;
 } zb_task_cfg;
 
 typedef struct zb_sim* zb_handle;

@@ -184,7 +184,7 @@ typedef struct {
   real cmd_standing, metrics[2];      /* manager only */
   real feet_fn_hist[3][2];            /* manager only: |net force| of the feet, per physics step */
   real feet_down_pos[2][3], feet_step_len[2], feet_f_last[2];
-  real heading_sum, yerr_sum;
+  real heading_sum, yerr_sum, force_sum; /* force_sum: v2 step0's feet_force_sum (v2.py:238) */
   real feet_fz_hist[ZB_HIST][2], undes_fmax_hist[ZB_HIST];
   real feet_air_cur[2], feet_air_last[2], feet_contact_cur[2], feet_contact_last[2];
   int32_t ep_len;
@@ -1623,13 +1623,18 @@ static real mdp_eval(const zb_task_cfg* cfg, const real jq0[ND], const obs_cache
     r[ZB_R_FEET_FORWARD] = s;
   }
   r[ZB_R_BASE_HEADING_X] = (real)fabs((double)pre->heading_err);
-  md->heading_sum = clampr(md->heading_sum + (real)0.01 * pre->heading_err, -1, 1);
+  /* a stateful term's buffers advance only while it is in the active reward_cfg: the reference
+   * updates them inside _reward_<name>, which exists only for the cfg's keys (v2.py:249-252) */
+  const uint32_t on = cfg->reward_active;
+  if ((on >> ZB_R_BASE_HEADING_X_SUM) & 1u)
+    md->heading_sum = clampr(md->heading_sum + (real)0.01 * pre->heading_err, -1, 1);
   r[ZB_R_BASE_HEADING_X_SUM] = (real)fabs((double)md->heading_sum);
   {
     /* step_length v2.py:509-533 */
+    const int step_on = (on >> ZB_R_STEP_LENGTH) & 1u;
     real minlen = 0;
     for (int f = 0; f < 2; ++f) {
-      int down = feetF[f] > (real)10.0 && md->feet_f_last[f] < (real)10.0;
+      int down = step_on && feetF[f] > (real)10.0 && md->feet_f_last[f] < (real)10.0;
       if (down) {
         real d[3] = {pre->feet_pos[f][0] - md->feet_down_pos[f][0], pre->feet_pos[f][1] - md->feet_down_pos[f][1],
                      pre->feet_pos[f][2] - md->feet_down_pos[f][2]};
@@ -1638,8 +1643,10 @@ static real mdp_eval(const zb_task_cfg* cfg, const real jq0[ND], const obs_cache
       }
     }
     minlen = md->feet_step_len[0] < md->feet_step_len[1] ? md->feet_step_len[0] : md->feet_step_len[1];
-    md->feet_f_last[0] = feetF[0];
-    md->feet_f_last[1] = feetF[1];
+    if (step_on) {  /* v2.py:532 */
+      md->feet_f_last[0] = feetF[0];
+      md->feet_f_last[1] = feetF[1];
+    }
     r[ZB_R_STEP_LENGTH] = (real)tanh((double)(15 * minlen));
   }
   r[ZB_R_AIRTIME_BALANCE] = (real)fabs((double)(ps->feet_air_last[0] - ps->feet_air_last[1]));
@@ -1663,9 +1670,15 @@ static real mdp_eval(const zb_task_cfg* cfg, const real jq0[ND], const obs_cache
   }
   r[ZB_R_BASE_POS_Y_ERR] = (real)fabs((double)(pre->feet_pos[0][1] + pre->feet_pos[1][1] - 2 * ps->origin_y)) +
                            (real)fabs((double)(pre->base_pos[1] - ps->origin_y));
-  md->yerr_sum = clampr(md->yerr_sum + (real)0.01 * base_y_err, -1, 1);
+  if ((on >> ZB_R_BASE_POS_Y_ERR_SUM) & 1u) md->yerr_sum = clampr(md->yerr_sum + (real)0.01 * base_y_err, -1, 1);
   r[ZB_R_BASE_POS_Y_ERR_SUM] = (real)fabs((double)md->yerr_sum);
   r[ZB_R_AIRTIME_SUM] = (real)tanh((double)(ps->feet_air_last[0] + ps->feet_air_last[1]));
+  /* step0 (v2.py:563-571, dict order diff before sum): the difference is signed by the integrator
+   * before this step's update; torch.sign(0) = 0 */
+  r[ZB_R_FEET_FORCE_DIFF] = (feetF[1] - feetF[0]) *
+                            (md->force_sum > 0 ? (real)1 : (md->force_sum < 0 ? (real)-1 : (real)0));
+  if ((on >> ZB_R_FEET_FORCE_SUM) & 1u) md->force_sum = md->force_sum + (real)0.001 * (feetF[0] - feetF[1]);
+  r[ZB_R_FEET_FORCE_SUM] = (real)fabs((double)md->force_sum);
 
   real rew = 0;
   for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) {
@@ -1752,6 +1765,7 @@ static void reset_env(const mdl_t* m, const zb_task_cfg* cfg, env_t* e) {
   latch_feet(m, cfg, pre, &e->ph, md->feet_down_pos);
   md->heading_sum = 0;
   md->yerr_sum = 0;
+  md->force_sum = 0; /* v2.py:437 */
   /* ContactSensor.reset: history and timers zeroed */
   for (int h = 0; h < ZB_HIST; ++h) { md->feet_fz_hist[h][0] = md->feet_fz_hist[h][1] = 0; md->undes_fmax_hist[h] = 0; }
   for (int f = 0; f < 2; ++f) { md->feet_air_cur[f] = md->feet_air_last[f] = md->feet_contact_cur[f] = 0; }
@@ -3035,6 +3049,7 @@ static void pack_env(const env_t* e, float* st, int n, int i) {
   }
   PUT(ZB_S_HEADING_SUM, e->md.heading_sum);
   PUT(ZB_S_Y_ERR_SUM, e->md.yerr_sum);
+  PUT(ZB_S_FEET_FORCE_SUM, e->md.force_sum);
   for (int h = 0; h < ZB_HIST; ++h) {
     PUT(ZB_S_FEET_FZ_HIST + 2 * h, e->md.feet_fz_hist[h][0]);
     PUT(ZB_S_FEET_FZ_HIST + 2 * h + 1, e->md.feet_fz_hist[h][1]);
@@ -3062,6 +3077,7 @@ static void unpack_env(env_t* e, const float* st, int n, int i) {
   }
   e->md.heading_sum = GET(ZB_S_HEADING_SUM);
   e->md.yerr_sum = GET(ZB_S_Y_ERR_SUM);
+  e->md.force_sum = GET(ZB_S_FEET_FORCE_SUM);
   for (int h = 0; h < ZB_HIST; ++h) {
     e->md.feet_fz_hist[h][0] = GET(ZB_S_FEET_FZ_HIST + 2 * h);
     e->md.feet_fz_hist[h][1] = GET(ZB_S_FEET_FZ_HIST + 2 * h + 1);
@@ -3288,7 +3304,7 @@ int zbo_obs_cache(int n, const float* base_pos, const float* base_quat, const fl
 
 /* _get_dones + _get_rewards on raw inputs. cache: [n][30] from zbo_obs_cache of the PREVIOUS
  * _get_observations; mdp_state: [n][13] = feet_down_pos 6, feet_step_len 2, feet_f_last 2,
- * heading_sum, yerr_sum, (pad); ep_sums [n][13] in/out. */
+ * heading_sum, yerr_sum, feet_force_sum; ep_sums [n][ZB_NUM_REWARD_TERMS] in/out. */
 int zbo_mdp_eval(int n, const zb_task_cfg* cfg, const float* cache, const float* applied_torque,
                  const float* feet_vel /*[n][2][3]*/, const float* feet_fz_hist /*[n][5][2]*/,
                  const float* undes_fmax_hist /*[n][5]*/, const float* feet_air_last /*[n][2]*/,
@@ -3332,6 +3348,7 @@ int zbo_mdp_eval(int n, const zb_task_cfg* cfg, const float* cache, const float*
     }
     md.heading_sum = st[10];
     md.yerr_sum = st[11];
+    md.force_sum = st[12];
     for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) md.ep_sums[t] = ep_sums[(size_t)e * ZB_NUM_REWARD_TERMS + t];
     real a_[ND], p_[ND], tr[ZB_NUM_REWARD_TERMS];
     for (int j = 0; j < ND; ++j) { a_[j] = act[(size_t)e * ND + j]; p_[j] = prev_act[(size_t)e * ND + j]; }
@@ -3348,6 +3365,7 @@ int zbo_mdp_eval(int n, const zb_task_cfg* cfg, const float* cache, const float*
     }
     st[10] = (float)md.heading_sum;
     st[11] = (float)md.yerr_sum;
+    st[12] = (float)md.force_sum;
     died[e] = (uint8_t)d;
     time_out[e] = (uint8_t)to;
   }

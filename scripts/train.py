@@ -51,7 +51,7 @@ def build_parser() -> argparse.ArgumentParser:
                     help="parent of the experiment folders (reference: logs/rsl_rl)")
     ap.add_argument("--log-every", type=int, default=1)
     ap.add_argument("--reward_cfg", default=None,
-                    help="zbot-6b-walking-v2 reward stage (step2 / step3 / step4 = v2.py:150-206); the reference "
+                    help="zbot-6b-walking-v2 reward stage (step0 / step1 / step1_v1 / step1_v2 / step2 / step3 / step4 = v2.py:77-206); the reference "
                          "edits the active reward_cfg in v2.py between its chained 2000-iteration runs")
     ap.add_argument("--env", action="append", default=[], metavar="PATH=VALUE",
                     help="env cfg override by dotted path, e.g. solver.iterations=8 (simulator ablations)")

@@ -21,6 +21,12 @@ from zbot_lab_amd import model as zm
 S, V4, SU, M = zm.S, zm.V4, zm.SU, zm.M
 
 TASKS = ("v2", "v4", "standup", "manager")
+# "v2:<stage>": walking v2 with a stage of the staged reward recipe (zbot_lab_amd.envs.walking_v2
+# REWARD_CFGS, v2.py:77-206); every other helper treats it as "v2"
+
+
+def base_task(task: str) -> str:
+    return task.split(":", 1)[0]
 
 
 SOLVER_MODE = 0  # zb_task_cfg.solver_mode of the configs below (tests switch it with solver_mode())
@@ -28,7 +34,10 @@ SOLVER_MODE = 0  # zb_task_cfg.solver_mode of the configs below (tests switch it
 
 def task_cfg(task: str) -> zm.TaskCfg:
     cfg = {"v2": zm.TaskCfg, "v4": zm.TaskCfg.walking_v4, "standup": zm.TaskCfg.standup,
-           "manager": zm.TaskCfg.manager_flat}[task]()
+           "manager": zm.TaskCfg.manager_flat}[base_task(task)]()
+    if ":" in task:
+        from zbot_lab_amd.envs.walking_v2 import REWARD_CFGS
+        cfg.reward_weights = dict(REWARD_CFGS[task.split(":", 1)[1]]["reward_scales"])
     cfg.solver_mode = SOLVER_MODE
     return cfg
 
@@ -55,7 +64,9 @@ def _rows(d: dict, name: str, k: int) -> list:
 def row_groups(task: str) -> dict:
     """State rows by tolerance class: phys_pos / phys_vel (physics), exact (pure functions of the
     inputs and counters), force (contact-force derived), kin (kinematics-derived latches), sums
-    (episode sums, per-term tolerance), static (read-only: per-link friction)."""
+    (episode sums, per-term tolerance), static (read-only: per-link friction), fsum (walking v2's
+    feet_force_sum: an integrator of 0.001 x the post-step feet force difference)."""
+    task = base_task(task)
     pos = list(range(0, 7)) + list(range(13, 19))
     vel = list(range(7, 13)) + list(range(19, 25))
     if task == "v2":
@@ -64,7 +75,7 @@ def row_groups(task: str) -> dict:
                     + _rows(S, "FEET_AIR_LAST", 2) + _rows(S, "FEET_CONTACT_CUR", 2),
                     force=_rows(S, "FEET_F_LAST", 2) + _rows(S, "FEET_FZ_HIST", 10) + _rows(S, "UNDES_FMAX_HIST", 5),
                     kin=_rows(S, "FEET_DOWN_POS", 6) + _rows(S, "FEET_STEP_LEN", 2) + [S["HEADING_SUM"], S["Y_ERR_SUM"]],
-                    sums=_rows(S, "EP_SUMS", 13), static=[])
+                    sums=_rows(S, "EP_SUMS", zm.NUM_TERMS), static=[], fsum=[S["FEET_FORCE_SUM"]])
     if task == "v4":
         return dict(phys_pos=pos, phys_vel=vel,
                     exact=_rows(V4, "P_DELTA", 6) + _rows(V4, "ACTIONS", 6) + [V4["EP_LEN"], V4["INTERVAL_LEFT"]]
@@ -96,9 +107,9 @@ TIGHT_TERMS = {
     "v4": {"action_rate"}, "standup": set(), "manager": {"action_rate_l2"},
 }
 
-# (atol, rtol) per class
+# (atol, rtol) per class; fsum's atol is per step (0.001 x both feet's force tolerance at ~20 N)
 TOL = dict(phys_pos=(1e-3, 1e-3), phys_vel=(5e-3, 5e-3), exact=(2e-5, 2e-6), force=(0.05, 0.02),
-           kin=(2e-5, 2e-5), static=(0.0, 0.0), obs=(5e-3, 5e-3))
+           kin=(2e-5, 2e-5), static=(0.0, 0.0), obs=(5e-3, 5e-3), fsum=(2e-4, 1e-3))
 
 
 def _quat(rng, n, tilt):
@@ -119,6 +130,7 @@ def random_states(task: str, o, n: int, seed: int, standing: bool = False) -> np
     """Valid random values in every state row. ``o`` is a fresh OracleSim of the task (its reset
     state is the base and its FK places the feet latches). ``standing``: small joint noise, zero
     velocities, MDP rows random as usual."""
+    task = base_task(task)
     rng = np.random.default_rng(seed)
     st = o.get_state().copy()
     f32 = np.float32
@@ -139,7 +151,7 @@ def random_states(task: str, o, n: int, seed: int, standing: bool = False) -> np
     if task == "standup":
         ep[rng.random(n) < 0.1] = 49                         # center_z_last refresh (ep_len % 50 == 49)
     st[D["EP_LEN"]] = ep.astype(f32)
-    nt = {"v2": 13, "v4": 15, "standup": 4, "manager": 11}[task]
+    nt = {"v2": zm.NUM_TERMS, "v4": 15, "standup": 4, "manager": 11}[task]
     st[D["EP_SUMS"]:D["EP_SUMS"] + nt] = rng.normal(0, 2.0, (nt, n)).astype(f32)
     if "P_DELTA" in D:
         st[D["P_DELTA"]:D["P_DELTA"] + 6] = 0.0 if standing else rng.normal(0, 0.3, (6, n)).astype(f32)
@@ -170,6 +182,7 @@ def random_states(task: str, o, n: int, seed: int, standing: bool = False) -> np
     if task == "v2":
         st[S["HEADING_SUM"]] = u(-1, 1)
         st[S["Y_ERR_SUM"]] = u(-1, 1)
+        st[S["FEET_FORCE_SUM"]] = rng.normal(0, 0.05, n).astype(f32)
     if task == "v4":
         sgn = np.where(rng.random(n) < 0.8, 1.0, -1.0)
         st[V4["COMMANDS"]] = (sgn * u(0.0, 0.3)).astype(f32)
@@ -207,6 +220,7 @@ def tolerance_rows(task: str, before: np.ndarray, after_o: np.ndarray, nsteps: i
     v2's feet-down latches of the envs that reset in the step (``reset``): the stale latch holds
     the terminal, post-physics feet positions."""
     g = row_groups(task)
+    full, task = task, base_task(task)
     tol = np.zeros_like(after_o, dtype=np.float64)
     multi = nsteps > 1
     lagged = task == "v2" and not multi
@@ -214,13 +228,15 @@ def tolerance_rows(task: str, before: np.ndarray, after_o: np.ndarray, nsteps: i
         if cls == "sums":
             continue
         a, r = TOL["phys_pos"] if cls == "kin" and not lagged else TOL[cls]
+        if cls == "fsum":
+            a *= nsteps
         for k in rows:
             tol[k] = a + r * np.abs(after_o[k])
     if lagged and reset is not None and reset.any():
         a, r = TOL["phys_pos"]
         for k in _rows(S, "FEET_DOWN_POS", 6):
             tol[k] = np.where(reset, np.maximum(tol[k], a + r * np.abs(after_o[k])), tol[k])
-    cfg = task_cfg(task)
+    cfg = task_cfg(full)
     terms, w = cfg.reward_terms, cfg.reward_weights
     tight = TIGHT_TERMS[task] if not multi else set()
     if task != "v2":

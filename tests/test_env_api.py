@@ -63,7 +63,7 @@ def test_registry_matches_reference_registration():
     assert cfg.decimation == 4 and cfg.action_space == 6 and cfg.observation_space == 23
     assert cfg.scene.num_envs == 4096 and cfg.scene.env_spacing == 4.0
     assert abs(cfg.sim.dt - 1 / 200) < 1e-12 and cfg.termination_height == 0.22
-    assert list(cfg.reward_cfg["reward_scales"]) == zm.REWARD_TERMS
+    assert list(cfg.reward_cfg["reward_scales"]) == zm.REWARD_TERMS[:13]   # step4 (v2.py:190-206)
     agent = load_cfg("zbot-6b-walking-v2", "rsl_rl_cfg_entry_point")
     assert isinstance(agent, PPORunnerCfgV2)
     d = agent.to_dict()

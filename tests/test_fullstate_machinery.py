@@ -24,7 +24,7 @@ def _device_f64(task, n, seed, st, actions):
     return out, d.get_state()
 
 
-@pytest.mark.parametrize("task", TASKS)
+@pytest.mark.parametrize("task", TASKS + ("v2:step0",))
 def test_f64_oracle_passes_full_state_check(oracle_lib, task):
     from oracle.pyoracle import OracleSim
     n, seed = 512, 17  # (the 2 % outlier bound over 512 envs: a one-env fluctuation is not a failure)

@@ -92,7 +92,7 @@ def _sensitivity(task, n, seed, st, actions, so, obs_o, rew_o, fl_o, before, nst
     runs += [(None, t, None, 1.0, "gjk_tol", None) for t in (0.25e-5, 0.5e-5, 2e-5, 4e-5)]
     runs += [(None, None, None, 1.0, "face_cos", c) for c in (np.cos(np.radians(14.5)), np.cos(np.radians(15.5)))]
     runs += [(None, None, s, 1.0, "sensor_force", None) for s in (0.93, 1.07)]
-    force_rows = row_groups(task)["force"]
+    force_rows = row_groups(task)["force"] + row_groups(task).get("fsum", [])
     for r_, tol, fs, scale, f, fc in runs:
         if tol is not None:
             lib().zbo_set_gjk_tol(tol)
@@ -290,6 +290,38 @@ def test_full_state_zero_action_standing(gpu, task):
     g_out = (obs.cpu().numpy(), rew.cpu().numpy(), te.cpu().numpy().copy(), tr.cpu().numpy().copy())
     sg = g.get_state().cpu().numpy()
     nbad = _check(task, f"{steps} zero-action steps from standing", n, seed, st, [a] * steps, g_out, sg, torch)
+    assert nbad <= 0.05 * n
+
+
+@pytest.mark.parametrize("stage", ["step0", "step1"])
+def test_full_state_v2_stage(gpu, stage):
+    """The first stages of the staged v2 recipe (v2.py:78-110; step0 adds feet_force_diff /
+    feet_force_sum and the feet_force_sum row; each stage advances only its active terms'
+    buffers): one step from random full states and 20 zero-action steps from standing, every row
+    (feet_force_sum included) under the full-state rule."""
+    task = f"v2:{stage}"
+    n, seed = 2048, 29
+    g, o, cfg, torch = _sims(task, n, seed)
+    if stage == "step0":  # the feet-force terms on, step_length (its latches) off
+        assert cfg.pack().reward_active >> 13 == 3 and "step_length" not in cfg.reward_weights
+    st = random_states(task, o, n, seed=121)
+    g.set_state(torch.from_numpy(st).cuda())
+    a = np.random.default_rng(9).normal(size=(n, 6)).astype(np.float32)
+    obs, rew, te, tr = g.step(torch.from_numpy(a).cuda())
+    g_out = (obs.cpu().numpy(), rew.cpu().numpy(), te.cpu().numpy().copy(), tr.cpu().numpy().copy())
+    sg = g.get_state().cpu().numpy()
+    nbad = _check(task, "one step from random full states", n, seed, st, [a], g_out, sg, torch)
+    assert nbad <= 0.02 * n
+    n, seed, steps = 1024, 7, 20
+    g, o, cfg, torch = _sims(task, n, seed)
+    st = random_states(task, o, n, seed=222, standing=True)
+    g.set_state(torch.from_numpy(st).cuda())
+    at = torch.zeros(n, 6, device="cuda:0")
+    for _ in range(steps):
+        obs, rew, te, tr = g.step(at)
+    g_out = (obs.cpu().numpy(), rew.cpu().numpy(), te.cpu().numpy().copy(), tr.cpu().numpy().copy())
+    nbad = _check(task, f"{steps} zero-action steps from standing", n, seed, st, [np.zeros((n, 6), np.float32)] * steps,
+                  g_out, g.get_state().cpu().numpy(), torch)
     assert nbad <= 0.05 * n
 
 

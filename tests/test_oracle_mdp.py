@@ -25,9 +25,11 @@ def gold():
 
 
 def test_golden_metadata(gold):
-    assert list(gold["term_names"]) == zm.REWARD_TERMS
+    # (step4, the reference's active cfg: the first 13 terms; step0's two follow in REWARD_TERMS)
+    assert list(gold["term_names"]) == zm.REWARD_TERMS[:13]
     cfg = zm.TaskCfg().pack()
-    np.testing.assert_allclose(np.array(cfg.reward_scales[:]), gold["scales_x_step_dt"], rtol=1e-6)
+    np.testing.assert_allclose(np.array(cfg.reward_scales[:13]), gold["scales_x_step_dt"], rtol=1e-6)
+    assert list(cfg.reward_scales[13:]) == [0.0, 0.0]
     np.testing.assert_allclose(gold["default_joint_pos"], zm.load_model().default_joint_pos, atol=1e-7)
     # the golden run exercises every branch: deaths, time-outs, touchdowns
     assert 0.1 < gold["died"].mean() < 0.9 and 0.05 < gold["time_out"].mean() < 0.9
@@ -83,14 +85,15 @@ def test_oracle_mdp_matches_reference(gold, oracle_lib):
                          died, tout)
         assert (died.astype(bool) == gold["died"][t]).all(), f"died mismatch at call {t}"
         assert (tout.astype(bool) == gold["time_out"][t]).all(), f"time_out mismatch at call {t}"
-        np.testing.assert_allclose(terms, gold["terms"][t], rtol=1e-5, atol=1e-6, err_msg=f"terms @ {t}")
+        np.testing.assert_allclose(terms[:, :13], gold["terms"][t], rtol=1e-5, atol=1e-6, err_msg=f"terms @ {t}")
+        assert (terms[:, 13:] == 0).all()
         np.testing.assert_allclose(rew, gold["reward"][t], rtol=1e-5, atol=1e-5)
         np.testing.assert_allclose(st[:, 10], gold["heading_sum"][t], rtol=1e-5, atol=1e-7)
         np.testing.assert_allclose(st[:, 11], gold["y_err_sum"][t], rtol=1e-5, atol=1e-7)
         np.testing.assert_allclose(st[:, 6:8], gold["feet_step_length"][t], rtol=1e-5, atol=1e-6)
         np.testing.assert_allclose(st[:, 0:6], gold["feet_down_pos_last"][t].reshape(N, 6), rtol=1e-6, atol=1e-6)
         np.testing.assert_allclose(st[:, 8:10], gold["feet_contact_forces_last"][t], rtol=1e-6, atol=1e-5)
-        np.testing.assert_allclose(sums, gold["episode_sums"][t], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(sums[:, :13], gold["episode_sums"][t], rtol=1e-5, atol=1e-6)
 
         # observation (v2.py:351-365): base quat from the post-step frame, joint pos - default, ...
         post = _cache(lib, gold["frame_body_link_pos_w"][t + 1], gold["frame_body_link_quat_w"][t + 1],
@@ -109,3 +112,95 @@ def test_obs_cache_matches_reference_kinematics(gold, oracle_lib):
     scale = gold["scales_x_step_dt"][zm.REWARD_TERMS.index("base_heading_x")]
     np.testing.assert_allclose(np.abs(c[:, 10]) * scale, gold["terms"][0][:, 3], rtol=1e-5, atol=1e-7)
     np.testing.assert_allclose(c[:, 3:7], gold["obs0"][:, :4], atol=0)
+
+
+STAGES_GOLD = os.path.join(os.path.dirname(__file__), "golden", "mdp_v2_stages.npz")
+
+
+@pytest.fixture(scope="module")
+def stages_gold():
+    return dict(np.load(STAGES_GOLD, allow_pickle=False))
+
+
+def test_stage_cfgs_match_reference(stages_gold):
+    """REWARD_CFGS (zbot_lab_amd/envs/walking_v2.py) equal the reward_cfg blocks of the reference's v2
+    file, read from its text by tools/gen_mdp_stage_goldens.py (v2.py:77-206), in dict order."""
+    from zbot_lab_amd.envs.walking_v2 import REWARD_CFGS
+    for stage in stages_gold["stages"]:
+        names = list(stages_gold[f"{stage}/term_names"])
+        mine = REWARD_CFGS[str(stage)]["reward_scales"]
+        assert list(mine) == names, stage
+        np.testing.assert_array_equal([mine[k] for k in names], stages_gold[f"{stage}/weights"])
+
+
+@pytest.mark.parametrize("stage", ["step0", "step1", "step1_v1", "step1_v2", "step2", "step3", "step4"])
+def test_oracle_mdp_matches_reference_stage(stages_gold, oracle_lib, stage):
+    """Every stage of the staged v2 recipe against the reference's own module: the active terms
+    (scaled), inactive terms exactly 0, the reward, both flags, and the persistent buffers -- which
+    advance only while their term is active (feet_force_sum, base_heading_x_sum, base_pos_y_err_sum,
+    the step-length latches and feet_contact_forces_last; v2.py:484-533, 563-571); step0's
+    feet_force_diff reads feet_force_sum before its update."""
+    import ctypes as C
+    from zbot_lab_amd.envs.walking_v2 import REWARD_CFGS
+    g = stages_gold
+    lib = oracle_lib.lib()
+    cfg = zm.TaskCfg(reward_weights=dict(REWARD_CFGS[stage]["reward_scales"])).pack()
+    names = list(g[f"{stage}/term_names"])
+    idx = [zm.REWARD_TERMS.index(k) for k in names]
+    off = [t for t in range(zm.NUM_TERMS) if t not in idx]
+    np.testing.assert_allclose([cfg.reward_scales[t] for t in idx], g[f"{stage}/scales_x_step_dt"], rtol=1e-6)
+    assert cfg.reward_active == sum(1 << t for t in idx)
+    T, N = g[f"{stage}/reward"].shape
+    jq0 = g["default_joint_pos"].astype(np.float32)
+    p_delta = np.zeros((N, 6), np.float32)
+    origin_y = np.ascontiguousarray(g["env_origins"][:, 1], np.float32)
+    st = np.zeros((N, 13), np.float32)
+    st[:, 0:6] = g["init_feet_down_pos_last"].reshape(N, 6)
+    st[:, 6:8] = g["init_feet_step_length"]
+    st[:, 8:10] = g["init_feet_contact_forces_last"]
+    st[:, 10] = g["init_base_heading_x_sum"]
+    st[:, 11] = g["init_base_pos_y_err_sum"]
+    st[:, 12] = g["init_feet_force_sum"]
+    sums = np.zeros((N, zm.NUM_TERMS), np.float32)
+    ep = g["init_episode_length_buf"].astype(np.int32)
+
+    def cache(t):
+        pos, quat, vel = (g["frame_" + k][t] for k in ("body_link_pos_w", "body_link_quat_w", "body_com_lin_vel_w"))
+        c = np.zeros((N, 30), np.float32)
+        lib.zbo_obs_cache(N, np.ascontiguousarray(pos[:, 1]), np.ascontiguousarray(quat[:, 1]),
+                          np.ascontiguousarray(pos[:, [0, 2]]), np.ascontiguousarray(quat[:, [0, 2]]),
+                          np.ascontiguousarray(vel[:, 1]), c)
+        return c
+
+    for t in range(T):
+        act_out = np.zeros((N, 6), np.float32)
+        targets = np.zeros((N, 6), np.float32)
+        lib.zbo_pre_physics(N, C.byref(cfg), jq0, np.ascontiguousarray(g["actions"][t]), p_delta, act_out, targets)
+        hist = g["frame_net_forces_w_history"][t + 1]
+        fz = np.ascontiguousarray(hist[:, :, [0, 11], 2], np.float32)
+        fmax = np.ascontiguousarray(np.linalg.norm(hist[:, :, UNDESIRED], axis=-1).max(axis=2), np.float32)
+        feet_vel = np.ascontiguousarray(g["frame_body_com_lin_vel_w"][t + 1][:, [0, 2]], np.float32)
+        air = np.ascontiguousarray(g["frame_last_air_time"][t + 1], np.float32)
+        ep = ep + 1
+        rew = np.zeros(N, np.float32)
+        terms = np.zeros((N, zm.NUM_TERMS), np.float32)
+        died = np.zeros(N, np.uint8)
+        tout = np.zeros(N, np.uint8)
+        lib.zbo_mdp_eval(N, C.byref(cfg), cache(t), np.ascontiguousarray(g["frame_applied_torque"][t + 1]), feet_vel,
+                         fz, fmax, air, ep, origin_y, act_out, np.ascontiguousarray(g[f"{stage}/prev_actions"][t]), st,
+                         sums, rew, terms, died, tout)
+        assert (died.astype(bool) == g[f"{stage}/died"][t]).all(), f"died @ {t}"
+        assert (tout.astype(bool) == g[f"{stage}/time_out"][t]).all(), f"time_out @ {t}"
+        np.testing.assert_allclose(terms[:, idx], g[f"{stage}/terms"][t], rtol=1e-5, atol=1e-6, err_msg=f"terms @ {t}")
+        assert (terms[:, off] == 0).all()
+        np.testing.assert_allclose(rew, g[f"{stage}/reward"][t], rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(st[:, 12], g[f"{stage}/feet_force_sum"][t], rtol=1e-5, atol=1e-7)
+        np.testing.assert_allclose(st[:, 10], g[f"{stage}/heading_sum"][t], rtol=1e-5, atol=1e-7)
+        np.testing.assert_allclose(st[:, 11], g[f"{stage}/y_err_sum"][t], rtol=1e-5, atol=1e-7)
+        np.testing.assert_allclose(st[:, 6:8], g[f"{stage}/feet_step_length"][t], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(st[:, 0:6], g[f"{stage}/feet_down_pos_last"][t].reshape(N, 6), rtol=1e-6, atol=1e-6)
+        np.testing.assert_allclose(st[:, 8:10], g[f"{stage}/feet_contact_forces_last"][t], rtol=1e-6, atol=1e-5)
+        np.testing.assert_allclose(sums[:, idx], g[f"{stage}/episode_sums"][t], rtol=1e-5, atol=1e-6)
+    if stage == "step0":  # the sign branch of feet_force_diff saw both signs, and the integrator moved
+        assert (g["step0/feet_force_sum"] > 0).any() and (g["step0/feet_force_sum"] < 0).any()
+        assert not np.allclose(g["step0/feet_force_sum"][-1], g["init_feet_force_sum"])

@@ -2774,7 +2774,7 @@ __device__ __forceinline__ void make_cache_q(MP m, const Q& q, const Phys& s, Ca
 struct Mdp {
   float p_delta[ND], actions[ND];
   float down_pos[2][3], step_len[2], f_last[2];
-  float heading_sum, yerr_sum;
+  float heading_sum, yerr_sum, force_sum;
   float fz_hist[ZB_HIST][2], fmax_hist[ZB_HIST];
   float air_cur[2], air_last[2], contact_cur[2];
   float ep_len;
@@ -2804,6 +2804,7 @@ __device__ __forceinline__ void load_state(const float* __restrict__ st, int N, 
   }
   d.heading_sum = LD(ZB_S_HEADING_SUM);
   d.yerr_sum = LD(ZB_S_Y_ERR_SUM);
+  d.force_sum = LD(ZB_S_FEET_FORCE_SUM);
 #pragma unroll
   for (int h = 0; h < ZB_HIST; ++h) {
     d.fz_hist[h][0] = LD(ZB_S_FEET_FZ_HIST + 2 * h);
@@ -2839,6 +2840,7 @@ __device__ __forceinline__ void store_state(float* __restrict__ st, int N, int i
   }
   SV(ZB_S_HEADING_SUM, d.heading_sum);
   SV(ZB_S_Y_ERR_SUM, d.yerr_sum);
+  SV(ZB_S_FEET_FORCE_SUM, d.force_sum);
 #pragma unroll
   for (int h = 0; h < ZB_HIST; ++h) {
     SV(ZB_S_FEET_FZ_HIST + 2 * h, d.fz_hist[h][0]);
@@ -2895,6 +2897,7 @@ __device__ __forceinline__ void reset_env(MP m, const float4* dflt, Phys& p, Mdp
   }
   d.heading_sum = 0.f;
   d.yerr_sum = 0.f;
+  d.force_sum = 0.f;  // v2.py:437
 #pragma unroll
   for (int h = 0; h < ZB_HIST; ++h) { d.fz_hist[h][0] = d.fz_hist[h][1] = 0.f; d.fmax_hist[h] = 0.f; }
 #pragma unroll
@@ -3113,7 +3116,7 @@ __device__ __forceinline__ void step_body(const zb_model* __restrict__ mg, const
     for (int a = 0; a < 3; ++a) down[f][a] = CST(ZB_S_FEET_DOWN_POS + 3 * f + a);
   }
   const float ep_len = CST(ZB_S_EP_LEN) + 1.f;
-  const float hs0 = CST(ZB_S_HEADING_SUM), ys0 = CST(ZB_S_Y_ERR_SUM);
+  const float hs0 = CST(ZB_S_HEADING_SUM), ys0 = CST(ZB_S_Y_ERR_SUM), fs0 = CST(ZB_S_FEET_FORCE_SUM);
 #pragma unroll
   for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) sums0[t] = CST(ZB_S_EP_SUMS + t);
   sp.mark(10);
@@ -3153,17 +3156,20 @@ __device__ __forceinline__ void step_body(const zb_model* __restrict__ mg, const
   const bool blowup = phys_bad(p);     // non-finite guard (phys_bad)
   died |= blowup;
 
-  // _get_rewards (v2.py:371-382) in dict order
+  // _get_rewards (v2.py:371-382) in dict order. A stateful term's buffers advance only while the
+  // term is in the active reward_cfg (they are updated inside its _reward_<name>; cfg.reward_active)
+  const uint32_t on = cfg.reward_active;
   float r[ZB_NUM_REWARD_TERMS];
   r[ZB_R_BASE_VEL_FORWARD] = r_pre[0];
   r[ZB_R_FEET_DOWNWARD] = r_pre[1];
   r[ZB_R_FEET_FORWARD] = r_pre[2];
   r[ZB_R_BASE_HEADING_X] = r_pre[3];
-  const float hs = clampf(hs0 + 0.01f * pre_heading, -1.f, 1.f);
+  const float hs = (on >> ZB_R_BASE_HEADING_X_SUM) & 1u ? clampf(hs0 + 0.01f * pre_heading, -1.f, 1.f) : hs0;
   r[ZB_R_BASE_HEADING_X_SUM] = fabsf(hs);
+  const bool step_on = (on >> ZB_R_STEP_LENGTH) & 1u;
 #pragma unroll
   for (int f = 0; f < 2; ++f) {
-    if (feetF[f] > 10.f && f_last0[f] < 10.f) {   // touchdown, v2.py:514-517
+    if (step_on && feetF[f] > 10.f && f_last0[f] < 10.f) {   // touchdown, v2.py:514-517
       float dv[3];
 #pragma unroll
       for (int a = 0; a < 3; ++a) {
@@ -3185,9 +3191,14 @@ __device__ __forceinline__ void step_body(const zb_model* __restrict__ mg, const
     r[ZB_R_FEET_SLIDE] = sacc;
   }
   r[ZB_R_BASE_POS_Y_ERR] = r_pre[4];
-  const float ys = clampf(ys0 + 0.01f * pre_base_y, -1.f, 1.f);
+  const float ys = (on >> ZB_R_BASE_POS_Y_ERR_SUM) & 1u ? clampf(ys0 + 0.01f * pre_base_y, -1.f, 1.f) : ys0;
   r[ZB_R_BASE_POS_Y_ERR_SUM] = fabsf(ys);
   r[ZB_R_AIRTIME_SUM] = tanh_r(air_last[0] + air_last[1]);
+  // step0's feet-force terms (v2.py:563-571): the difference is signed by the integrator before
+  // feet_force_sum updates it (dict order); torch.sign(0) = 0
+  r[ZB_R_FEET_FORCE_DIFF] = (feetF[1] - feetF[0]) * (fs0 > 0.f ? 1.f : (fs0 < 0.f ? -1.f : 0.f));
+  const float fs = (on >> ZB_R_FEET_FORCE_SUM) & 1u ? fs0 + 0.001f * (feetF[0] - feetF[1]) : fs0;
+  r[ZB_R_FEET_FORCE_SUM] = fabsf(fs);
 
   float reward = 0.f, sums[ZB_NUM_REWARD_TERMS];
   const bool reset = died || time_out;
@@ -3264,7 +3275,7 @@ __device__ __forceinline__ void step_body(const zb_model* __restrict__ mg, const
 #pragma unroll
       for (int a = 0; a < 3; ++a) OUT(ZB_S_FEET_DOWN_POS + 3 * f + a) = down[f][a];
       OUT(ZB_S_FEET_STEP_LEN + f) = step_len[f];
-      OUT(ZB_S_FEET_F_LAST + f) = feetF[f];
+      OUT(ZB_S_FEET_F_LAST + f) = step_on ? feetF[f] : f_last0[f];  // refreshed by step_length only (v2.py:532)
       OUT(ZB_S_FEET_AIR_CUR + f) = live(air_cur[f]);
       OUT(ZB_S_FEET_AIR_LAST + f) = live(air_last[f]);
       OUT(ZB_S_FEET_CONTACT_CUR + f) = live(contact_t[f]);
@@ -3274,6 +3285,7 @@ __device__ __forceinline__ void step_body(const zb_model* __restrict__ mg, const
                         [&](int row, float v) { OUT(row) = v; });
     OUT(ZB_S_HEADING_SUM) = live(hs);
     OUT(ZB_S_Y_ERR_SUM) = live(ys);
+    OUT(ZB_S_FEET_FORCE_SUM) = live(fs);
     OUT(ZB_S_EP_LEN) = live(ep_len);
 #pragma unroll
     for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) OUT(ZB_S_EP_SUMS + t) = live(sums[t]);

@@ -58,10 +58,23 @@ def _scales(**kw) -> dict:
     return {"reward_scales": dict(kw)}
 
 
-# The staged training recipe of v2.py:150-206: the reference trains 2000 iterations per stage and
+# The staged training recipe of v2.py:78-206: the reference trains 2000 iterations per stage and
 # chains the stages with ``--resume`` (README.md:69), editing the active ``reward_cfg`` between
 # runs; ``step4`` is the active one (v2.py:190-206). scripts/train.py --reward_cfg selects a stage.
+# step0 ("just stepping walk base") adds the feet-force terms (v2.py:563-571); step1 has three
+# variants, v0 marked "use this" (v2.py:94-148).
 REWARD_CFGS = {
+    "step0": _scales(base_vel_forward=1.0, feet_downward=-1.0, feet_forward=-1.0, base_heading_x=-1.0,  # v2.py:78-92
+                     feet_force_diff=0.5, feet_force_sum=-0.1, base_pos_y_err=-1.0),
+    "step1": _scales(base_vel_forward=1.0, feet_downward=-1.0, feet_forward=-1.0, base_heading_x=-1.0,  # v2.py:94-110
+                     base_heading_x_sum=-3.0, step_length=5.0, airtime_balance=-15.0, action_rate=-0.1,
+                     torques=-0.002, feet_slide=-10.0, base_pos_y_err=-1.0),
+    "step1_v1": _scales(base_vel_forward=1.0, feet_downward=-1.5, feet_forward=-0.5, base_heading_x=-1.0,  # v2.py:112-129
+                        base_heading_x_sum=-3.0, step_length=5.0, airtime_balance=-15.0, action_rate=-0.1,
+                        torques=-0.002, feet_slide=-10.0, base_pos_y_err=-1.5, base_pos_y_err_sum=-1.5),
+    "step1_v2": _scales(base_vel_forward=1.0, feet_downward=-2.0, feet_forward=-0.2, base_heading_x=-1.0,  # v2.py:131-148
+                        base_heading_x_sum=-5.0, step_length=5.0, airtime_balance=-15.0, action_rate=-0.1,
+                        torques=-0.002, feet_slide=-10.0, base_pos_y_err=-2.0, base_pos_y_err_sum=-2.0),
     "step2": _scales(base_vel_forward=1.0, feet_downward=-2.0, feet_forward=-1.0, base_heading_x=-1.0,  # v2.py:150-167
                      base_heading_x_sum=-3.0, step_length=5.0, airtime_balance=-15.0, action_rate=-0.1,
                      torques=-0.002, feet_slide=-10.0, base_pos_y_err=-1.0, base_pos_y_err_sum=-2.0),
@@ -89,7 +102,7 @@ class ZbotDirectEnvCfgV2:
 
     def task_cfg(self) -> zm.TaskCfg:
         unknown = set(self.reward_cfg["reward_scales"]) - set(zm.REWARD_TERMS)
-        if unknown:  # e.g. step0's feet_force_diff / feet_force_sum (v2.py:78-91, 563-571)
+        if unknown:  # ZbotDirectEnvV2.__init__ would fail the same way (getattr "_reward_" + name, v2.py:252)
             raise NotImplementedError(f"reward terms not compiled into zb_step_kernel: {sorted(unknown)}")
         return zm.TaskCfg(
             sim_dt=self.sim.dt, decimation=self.decimation, episode_length_s=self.episode_length_s,

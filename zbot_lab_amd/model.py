@@ -20,16 +20,16 @@ import numpy as np
 ASSET = os.path.join(os.path.dirname(__file__), "assets", "zbot6s_model.json")
 
 NUM_LINKS, NUM_BODIES, NUM_DOF = 12, 7, 6
-OBS_DIM, ACT_DIM, NUM_TERMS, HIST = 23, 6, 13, 5
+OBS_DIM, ACT_DIM, NUM_TERMS, HIST = 23, 6, 15, 5
 MAX_SELF_PAIRS = 64
-STATE_DIM = 84
+STATE_DIM = 87
 
 LINK_NAMES = ["foot_0", "b1", "a2", "b2", "a3", "b3", "base", "b4", "a5", "b5", "a6", "foot_1"]
 JOINT_NAMES = ["joint1", "joint2", "joint3", "joint4", "joint5", "joint6"]
-REWARD_TERMS = [  # dict order of ZbotDirectEnvCfgV2.reward_cfg (v2.py:190-206)
+REWARD_TERMS = [  # dict order of ZbotDirectEnvCfgV2.reward_cfg (v2.py:190-206), then step0's feet-force terms
     "base_vel_forward", "feet_downward", "feet_forward", "base_heading_x", "base_heading_x_sum",
     "step_length", "airtime_balance", "action_rate", "torques", "feet_slide", "base_pos_y_err",
-    "base_pos_y_err_sum", "airtime_sum",
+    "base_pos_y_err_sum", "airtime_sum", "feet_force_diff", "feet_force_sum",   # v2.py:78-91, 563-571
 ]
 REWARD_WEIGHTS = {  # v2.py:190-206 ("train reward 2000 step4")
     "base_vel_forward": 1.0, "feet_downward": -2.0, "feet_forward": -1.0, "base_heading_x": -1.0,
@@ -95,7 +95,7 @@ M = dict(ACTIONS=25, COMMANDS=31, CMD_TIME_LEFT=34, CMD_STANDING=35, FEET_DOWN_P
 S = dict(ROOT_POS=0, ROOT_QUAT=3, ROOT_LINVEL=7, ROOT_ANGVEL=10, JOINT_POS=13, JOINT_VEL=19,
          P_DELTA=25, ACTIONS=31, FEET_DOWN_POS=37, FEET_STEP_LEN=43, FEET_F_LAST=45, HEADING_SUM=47,
          Y_ERR_SUM=48, FEET_FZ_HIST=49, UNDES_FMAX_HIST=59, FEET_AIR_CUR=64, FEET_AIR_LAST=66,
-         FEET_CONTACT_CUR=68, EP_LEN=70, EP_SUMS=71)
+         FEET_CONTACT_CUR=68, EP_LEN=70, EP_SUMS=71, FEET_FORCE_SUM=86)
 
 
 # ----------------------------------------------------------------------------- ctypes mirrors
@@ -153,6 +153,7 @@ class ZbTaskCfg(C.Structure):
         ("reset_feet_refresh", C.c_int32),
         ("friction_dynamic", C.c_float),
         ("solver_mode", C.c_int32), ("self_manifold", C.c_int32),
+        ("reward_active", C.c_uint32),
     ]
 
 
@@ -636,9 +637,17 @@ class TaskCfg:
         c.max_episode_length = self.max_episode_length
         c.termination_height = self.termination_height
         if self.task == TASK_WALKING_V2:
+            unknown = set(self.reward_weights) - set(REWARD_TERMS)
+            if unknown:
+                raise NotImplementedError(f"reward terms not compiled into zb_step_kernel: {sorted(unknown)}")
             for k, name in enumerate(REWARD_TERMS):
                 # v2.py:250-252 multiplies every weight by step_dt at env construction
                 c.reward_scales[k] = self.reward_weights.get(name, 0.0) * self.step_dt
+                # the terms of the active reward_cfg (a stateful term's buffers advance only then)
+                if name in self.reward_weights:
+                    c.reward_active |= 1 << k
+        else:
+            c.reward_active = 0xFFFFFFFF
         # standup.py:624 / v4.py:886 multiply by step_dt per term in _get_rewards (the kernel does)
         ws = self.stage_weights()
         if len(ws) > MAX_STAGES:
