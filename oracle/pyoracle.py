@@ -57,6 +57,7 @@ def _load(double: bool = False):
     lib.zbo_set_plant.argtypes = [C.c_int]
     lib.zbo_contact_activity.argtypes = [P, _i, C.c_int]
     lib.zbo_self_min_sep.argtypes = [P, _f]
+    lib.zbo_pair_classes.argtypes = [P, _f]
     lib.zbo_link_com_vel.argtypes = [P, _f]
     lib.zbo_energy_momentum.argtypes = [P, _f]
     lib.zbo_pre_physics.argtypes = [C.c_int, C.POINTER(zm.ZbTaskCfg), _f, _f, _f, _f, _f]
@@ -197,6 +198,14 @@ class OracleSim:
         out = np.zeros((self.n, 2), np.int32)
         self.lib.zbo_contact_activity(self.h, out, int(clear))
         return out
+
+    def pair_classes(self):
+        """[n, 8] self-contact classes per env (oracle zbo_pair_classes): pairs in contact, face-manifold
+        pairs, rim-manifold pairs, overlapping-core pairs, min separation, self points, first face /
+        rim pair index (-1: none)."""
+        d = np.zeros((self.n, 8), np.float32)
+        self.lib.zbo_pair_classes(self.h, d)
+        return d
 
     def self_min_sep(self):
         """[n]: the smallest self-collision separation of the current state (-2 CORE_M: overlapping

@@ -413,7 +413,10 @@ static double g_sensor_force_scale = 1.0; /* test hook: scales the contact force
 /* planted contact bug (test hook, 0 = off; tests/test_fullstate_machinery.py proves that the
  * full-state parity rule flags a device carrying one): 1 = the first ground contact of every
  * substep with mu x 1.1, 2 = the first self contact's normal flipped, 3 = the penetration push-out
- * without the max_depenetration_velocity cap */
+ * without the max_depenetration_velocity cap; rare branches (they act in the few envs that reach
+ * them): 4 = the rim manifold's end points with their normal flipped, 5 = every face-manifold
+ * sample 1 mm farther from the target face (its separation + 1 mm), 6 = the overlapping-core
+ * separating-axis estimate without the centre-difference axis */
 static int g_plant = 0;
 /* per-env contact activity (test hook): the env's [loaded ground, loaded self] counters, set by the
  * step loops around each env's step */
@@ -616,6 +619,7 @@ static int hull_pair(const hull_t* A, const hull_t* B, real margin, real early_m
       }
       real nu = sqrtr(v3_dot(u, u));
       if (nu < (real)1e-12) continue; /* coincident centres: no centre-difference axis */
+      if (g_plant == 6 && ax == 0) continue; /* planted bug */
       for (int a = 0; a < 3; ++a) u[a] /= nu;
       real alo, ahi, blo, bhi;
       hull_extent(A, u, &alo, &ahi);
@@ -734,7 +738,7 @@ static int face_manifold(const hull_t* A, const hull_t* B, const contact_t* c0, 
       real p[3], q[3], w[3];
       for (int a = 0; a < 3; ++a) p[a] = cs[a] + rs * (cr * d0[a] + sr * d1[a]);
       for (int a = 0; a < 3; ++a) w[a] = ct[a] - p[a];
-      const real t = v3_dot(w, ut) / den; /* p + t sg n lies on the target face plane */
+      const real t = v3_dot(w, ut) / den + (g_plant == 5 ? (real)1e-3 : 0); /* p + t sg n lies on the target face plane (planted bug 5: + 1 mm) */
       for (int a = 0; a < 3; ++a) q[a] = p[a] + t * sg * nr[a] - ct[a];
       if (v3_dot(q, q) > rt * rt) continue;
       const real sep = t - 2 * (real)CORE_M;
@@ -812,7 +816,8 @@ static int rim_manifold(const hull_t* A, const hull_t* B, const contact_t* c0, r
     if (!(sep < margin)) continue;
     contact_t* o = &out[k++];
     o->la = c0->la; o->lb = c0->lb; o->sep = sep; o->rim = -1;
-    for (int q = 0; q < 3; ++q) { o->n[q] = nr[q]; o->x[q] = (real)0.5 * (xa[q] + xb[q]); }
+    const real fl = g_plant == 4 ? (real)-1 : (real)1; /* planted bug 4: the end's normal flipped */
+    for (int q = 0; q < 3; ++q) { o->n[q] = fl * nr[q]; o->x[q] = (real)0.5 * (xa[q] + xb[q]); }
   }
   return k;
 }
@@ -3233,6 +3238,44 @@ int zbo_contact_diag(zbo_sim* s, float* out) {
 /* per env: the smallest self-collision separation over all link pairs (GJK on the rounded cores,
  * no early exit; -2 CORE_M = cores overlapping, beyond the exact range). Parity tests use it to
  * set aside random test states whose links interpenetrate deeper than the shape model covers. */
+/* per env, the self-contact classes of its link pairs at the current state (tests: constructed
+ * manifold states, planted rare-branch bugs): out [n][8] = {pairs in contact, face-manifold pairs,
+ * rim-manifold pairs (>= 2 points), overlapping-core pairs (the separating-axis branch), min core
+ * separation - 2 CORE_M over the pairs, self points (cfg->self_manifold), the first face pair's
+ * index (-1: none), the first rim pair's index (-1: none)} */
+int zbo_pair_classes(zbo_sim* s, float* out) {
+  const real margin = s->c.contact_margin;
+#pragma omp parallel for schedule(dynamic, 64)
+  for (int e = 0; e < s->n; ++e) {
+    kin_t k;
+    fk(&s->m, &s->env[e].ph, &k);
+    int nh = 0, nf = 0, nr = 0, nd = 0, np_ = 0, pf = -1, pr = -1;
+    real mn = (real)1e30;
+    for (int p = 0; p < s->m.npairs; ++p) {
+      hull_t A, B;
+      world_hull(&s->m, &k, s->m.pairs[p][0], &A);
+      world_hull(&s->m, &k, s->m.pairs[p][1], &B);
+      contact_t c, mf[4];
+      memset(&c, 0, sizeof(c));
+      const int hit = hull_pair(&A, &B, margin, margin, NULL, &c);
+      if (c.sep < mn && hit) mn = c.sep;
+      if (!hit) continue;
+      ++nh;
+      if (!(c.sep > -2 * (real)CORE_M + (real)1e-7)) ++nd;
+      c.la = s->m.pairs[p][0]; c.lb = s->m.pairs[p][1];
+      const int kf = s->c.self_manifold >= 1 ? self_manifold(1, &A, &B, &c, margin, mf) : 0;
+      const int km = self_manifold(s->c.self_manifold, &A, &B, &c, margin, mf);
+      if (kf > 0) { ++nf; if (pf < 0) pf = p; }
+      else if (km >= 2) { ++nr; if (pr < 0) pr = p; }
+      np_ += km > 0 ? km : 1;
+    }
+    float* o = out + 8 * (size_t)e;
+    o[0] = (float)nh; o[1] = (float)nf; o[2] = (float)nr; o[3] = (float)nd;
+    o[4] = (float)(nh ? mn : 1); o[5] = (float)np_; o[6] = (float)pf; o[7] = (float)pr;
+  }
+  return 0;
+}
+
 int zbo_self_min_sep(zbo_sim* s, float* out) {
   for (int e = 0; e < s->n; ++e) {
     kin_t k;

@@ -276,3 +276,50 @@ def perturb_physics(st: np.ndarray, rng, rel: float = 1e-6, abs_: float = 1e-7) 
     ph = ph * (1 + rel * rng.standard_normal(ph.shape)) + abs_ * rng.standard_normal(ph.shape)
     out[:25] = ph.astype(np.float32)
     return out
+
+
+SEEDS = None
+
+
+def manifold_seeds() -> dict:
+    """Joint angles of gentle folds per self-contact class (tests/golden/manifold_seeds.npz, written
+    by tools/manifold_seeds.py): "face" (one pair cap on cap), "rim" (one pair side by side), "deep"
+    (one pair with overlapping cores); no other pair overlaps."""
+    global SEEDS
+    if SEEDS is None:
+        import os
+        SEEDS = dict(np.load(os.path.join(os.path.dirname(__file__), "golden", "manifold_seeds.npz"), allow_pickle=False))
+    return SEEDS
+
+
+CLASS_COL = {"face": 1, "rim": 2, "deep": 3}   # zbo_pair_classes column that marks the class
+
+
+def constructed_states(task: str, kind: str, n: int, seed: int, jitter: float = 0.003, lift: float = 0.06):
+    """n full states (random MDP rows, tests/fullstate.random_states) whose joint angles are built from
+    the ``kind`` seeds of manifold_seeds() plus N(0, jitter) rad, with the root raised so that every
+    link origin is at least ``lift`` above the ground (self contact only); a draw whose class does not
+    survive the jitter (or that gains an overlapping pair) is drawn again. Returns (states, seed
+    index per env)."""
+    from oracle.pyoracle import OracleSim
+    seeds = manifold_seeds()[kind]
+    rng = np.random.default_rng(seed)
+    o = OracleSim(n, task_cfg(task), seed=seed)
+    st = random_states(task, o, n, seed=seed + 1)
+    which = np.arange(n) % len(seeds)
+    todo = np.arange(n)
+    for _ in range(50):
+        if not len(todo):
+            break
+        st[13:19, todo] = (seeds[which[todo]] + rng.normal(0, jitter, (len(todo), 6))).T.astype(np.float32)
+        o.set_state(st)
+        z = o.link_poses()[0][:, :, 2].min(axis=1)
+        st[2] += np.maximum(lift - z, 0).astype(np.float32)
+        o.set_state(st)
+        pc = o.pair_classes()
+        ok = pc[:, CLASS_COL[kind]] > 0
+        ok &= (pc[:, 3] == 0) if kind != "deep" else (pc[:, 3] == 1)
+        todo = np.nonzero(~ok)[0]
+        which[todo] = rng.integers(0, len(seeds), len(todo))
+    assert not len(todo), f"{len(todo)} {kind} states did not keep their class"
+    return st, which
