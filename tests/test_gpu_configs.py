@@ -155,3 +155,27 @@ def test_c4_ppo_4096_envs(gpu, tmp_path):
     assert log[-1]["mean_episode_length"] > log[1]["mean_episode_length"]
     assert log[-1]["fps"] > 5e5, log[-1]["fps"]      # 98 304 samples per iteration
     env.close()
+
+
+def test_c5_ppo_standup_32768_envs(gpu, tmp_path):
+    """C5's training (zbot-6b-standup-v0 at 32 768 envs, friction DR and random reset poses on,
+    Zbot6SUpEnvPPOCfg's [256, 256, 128] nets, reference rsl_rl_ppo_cfg.py:264-289): 5 iterations on
+    the fused path (zbp_act rollout, zbp_minibatch / zbp_optimizer_step update): finite losses and
+    rewards, the fps floor, and the curriculum counter read from the device (my_curriculum,
+    standup.py:99-111: 24 steps per iteration, stage 0 until 24 000 steps)."""
+    import zbot_lab_amd
+    from zbot_lab_amd.rl import OnPolicyRunner, RslRlVecEnvWrapper
+    from zbot_lab_amd.rl.cfg import Zbot6SUpEnvPPOCfg
+    cfg = zbot_lab_amd.tasks.load_cfg("zbot-6b-standup-v0")
+    cfg.scene.num_envs = 32768
+    env = RslRlVecEnvWrapper(zbot_lab_amd.make("zbot-6b-standup-v0", cfg=cfg))
+    runner = OnPolicyRunner(env, Zbot6SUpEnvPPOCfg().to_dict(), log_dir=str(tmp_path), device="cuda:0")
+    log = runner.learn(5, init_at_random_ep_len=True)
+    assert runner.alg._fused is not None          # the fused update and rollout ran
+    assert all(np.isfinite(r["loss/value_function"]) and np.isfinite(r["loss/surrogate"])
+               and np.isfinite(r["mean_reward"]) for r in log[1:])
+    stage, counter = env.unwrapped.sim.read_curriculum()
+    assert stage == 0 and counter == 5 * 24, (stage, counter)
+    print(f"\nC5 PPO: fps {[round(r['fps']) for r in log]}, learn {[round(r['learn_time'], 4) for r in log]}")
+    assert log[-1]["fps"] > 3e6, log[-1]["fps"]      # 786 432 samples per iteration (round 4: 7.0 M/s)
+    env.close()

@@ -139,8 +139,12 @@ def test_fused_gae_matches_torch(gpu, monkeypatch):
     st.advantages.zero_()
     st.compute_returns(last, 0.99, 0.95, True)
     torch.cuda.synchronize()
-    torch.testing.assert_close(st.returns, ret_t, rtol=1e-5, atol=1e-5)
-    torch.testing.assert_close(st.advantages, adv_t, rtol=1e-4, atol=1e-5)
+    # the recursion rounds every op as torch's kernels do (no fma contraction): returns agree to the
+    # last bit in practice; the normalisation's mean / std reduce in another order than torch's
+    print(f"\nGAE fused vs torch: returns max |d| {(st.returns - ret_t).abs().max().item():.3g}, "
+          f"advantages max |d| {(st.advantages - adv_t).abs().max().item():.3g}")
+    torch.testing.assert_close(st.returns, ret_t, rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(st.advantages, adv_t, rtol=2e-5, atol=2e-6)
     assert abs(float(st.advantages.mean())) < 1e-5 and abs(float(st.advantages.std()) - 1.0) < 1e-4
 
 

@@ -680,8 +680,11 @@ __global__ __launch_bounds__(256) void k_gae(const float* __restrict__ rew, cons
     for (int k = T - 1; k >= 0; --k) {
       const int64_t e = (int64_t)k * N + n;
       const float v = val[e], nt = 1.f - done[e];
-      const float delta = rew[e] + nt * gamma * next - v;
-      a = delta + nt * gamma * lam * a;
+      // torch rounds every product and sum of the recursion (one kernel per op): no fma contraction
+      float p = nt * gamma * next, q = nt * gamma * lam * a;
+      asm volatile("" : "+v"(p), "+v"(q));
+      const float delta = rew[e] + p - v;
+      a = delta + q;
       const float r = a + v;
       ret[e] = r;
       const float d = r - v;
@@ -695,7 +698,7 @@ __global__ __launch_bounds__(256) void k_gae(const float* __restrict__ rew, cons
   __syncthreads();
   if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
-// one block: the mean, then the unbiased variance around it -> part[GAE_BLOCKS .. +2] = {mean, 1/(std + 1e-8)}
+// one block: the mean, then the unbiased variance around it -> part[GAE_BLOCKS .. +2] = {mean, std + 1e-8}
 __global__ __launch_bounds__(1024) void k_adv_stats(const float* __restrict__ adv, int64_t M, float* __restrict__ part) {
   __shared__ float red[16];
   __shared__ float mean_s;
@@ -718,13 +721,13 @@ __global__ __launch_bounds__(1024) void k_adv_stats(const float* __restrict__ ad
     float t = 0.f;
     for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += red[w];
     part[GAE_BLOCKS] = mean;
-    part[GAE_BLOCKS + 1] = 1.f / (sqrtf(t / (float)(M - 1)) + 1e-8f);
+    part[GAE_BLOCKS + 1] = sqrtf(t / (float)(M - 1)) + 1e-8f;
   }
 }
 __global__ __launch_bounds__(256) void k_adv_norm(float* __restrict__ adv, int64_t M, const float* __restrict__ part) {
-  const float mean = part[GAE_BLOCKS], inv = part[GAE_BLOCKS + 1];
+  const float mean = part[GAE_BLOCKS], den = part[GAE_BLOCKS + 1];
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < M; e += (int64_t)gridDim.x * blockDim.x)
-    adv[e] = (adv[e] - mean) * inv;
+    adv[e] = (adv[e] - mean) / den;  // (a division, as torch's (adv - mean) / (std + 1e-8))
 }
 
 int launch_check(const char* what) {

@@ -61,6 +61,23 @@ EXPORTED = ["zbp_workspace_floats", "zbp_pack", "zbp_minibatch", "zbp_optimizer_
 _lib = None
 
 
+_warned = False
+
+
+def available() -> bool:
+    """Whether libzbot_ppo.so is built. When it is not, the PPO update, GAE and rollout run on the
+    torch statement (the reference's rsl_rl path) after a one-time warning; the simulator itself has
+    no such fallback (libzbot.so is required)."""
+    global _warned
+    if os.path.exists(LIB_PATH):
+        return True
+    if not _warned:
+        import warnings
+        warnings.warn(f"{LIB_PATH} not built (python -m zbot_lab_amd.build): PPO runs on the torch path")
+        _warned = True
+    return False
+
+
 def lib():
     """Load libzbot_ppo.so (raises ZbotError when it is not built)."""
     global _lib
@@ -131,7 +148,7 @@ def supported(policy, batch: int) -> bool:
         la, lc = mlp_layers(policy.actor), mlp_layers(policy.critic)
     except TypeError:
         return False
-    if la is None or lc is None or batch % 32 or batch < 32:
+    if la is None or lc is None or batch % 32 or batch < 32 or not available():
         return False
     if not all(p.is_cuda and p.dtype == torch.float32 for p in policy.parameters()):
         return False
@@ -214,6 +231,11 @@ class FusedUpdate:
         g = opt.param_groups[0]
         if g.get("weight_decay", 0) or g.get("amsgrad") or g.get("maximize"):
             raise ZbotError("zbp_optimizer_step implements plain Adam")
+        # one step counter drives every parameter's bias correction in the kernels (they read step[0]
+        # and write it back to all): refuse states whose counters differ (a partially loaded state)
+        steps = {float(opt.state[p]["step"]) if opt.state[p] else 0.0 for p in ps}
+        if len(steps) > 1:
+            raise ZbotError(f"zbp_optimizer_step needs one Adam step count for every parameter, got {sorted(steps)}")
         P = Params()
         P.n_params = len(ps)
         for i, p in enumerate(ps):

@@ -176,8 +176,9 @@ class RolloutStorage:
                         normalize_advantage: bool = True) -> None:
         if self.values.is_cuda and os.environ.get("ZBOT_PPO_FUSED", "1") != "0":
             from . import fused  # the same recursion in three launches (zbp_gae)
-            fused.gae(self, last_values, gamma, lam, normalize_advantage)
-            return
+            if fused.available():
+                fused.gae(self, last_values, gamma, lam, normalize_advantage)
+                return
         adv = torch.zeros_like(last_values)
         for k in reversed(range(self.num_transitions_per_env)):
             next_values = last_values if k == self.num_transitions_per_env - 1 else self.values[k + 1]
