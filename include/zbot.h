@@ -328,7 +328,9 @@ typedef struct zb_task_cfg {
    * contributes up to 4 points (rim points of either face inside the other), every
    * other pair its one GJK point; 2 (default) = 1 plus side-by-side pairs whose nearest features are
    * two rulings within 5 degrees of the contact plane and of each other: the GJK point and the two
-   * ends of the rulings' overlap (up to 3 points); 0 = one point per pair */
+   * ends of the rulings' overlap (up to 3 points); 3 = 2 plus a ruling lying on a face (a face on one
+   * side, a ruling within 5 degrees of the contact plane on the other): the GJK point and the ends of
+   * the ruling's stretch over the face disk (up to 3 points); 0 = one point per pair */
   int32_t self_manifold;
   /* walking v2: bit t set = reward term t is in the active reward_cfg (v2.py:246-257 builds
    * reward_functions from its keys). The reference updates a stateful term's buffers inside its
@@ -438,6 +440,8 @@ int zb_gjk_pairs(const float* pairs, const float* v0, int n, float margin, float
  * zb_gjk_pairs); out [n][29] = {points (0: no contact, 1: the GJK contact alone), then per point
  * {separation, normal[3], point[3]}}. Checked against the oracle's zbo_pair_manifold. */
 int zb_pair_manifold(const float* pairs, int n, float margin, float* out, void* stream);
+/* The same with the manifold mode (zb_task_cfg.self_manifold 1..3; zb_pair_manifold = mode 2). */
+int zb_pair_manifold_mode(const float* pairs, int n, float margin, int mode, float* out, void* stream);
 
 #ifdef __cplusplus
 }

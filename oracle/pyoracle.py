@@ -200,10 +200,10 @@ class OracleSim:
         return out
 
     def pair_classes(self):
-        """[n, 8] self-contact classes per env (oracle zbo_pair_classes): pairs in contact, face-manifold
-        pairs, rim-manifold pairs, overlapping-core pairs, min separation, self points, first face /
-        rim pair index (-1: none)."""
-        d = np.zeros((self.n, 8), np.float32)
+        """[n, 10] self-contact classes per env (oracle zbo_pair_classes): pairs in contact, face-manifold
+        pairs, side-by-side rim-manifold pairs, overlapping-core pairs, min separation, self points,
+        first face / rim pair index (-1: none), ruling-on-face pairs, first ruling-on-face pair index."""
+        d = np.zeros((self.n, 10), np.float32)
         self.lib.zbo_pair_classes(self.h, d)
         return d
 

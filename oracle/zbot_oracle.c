@@ -821,11 +821,76 @@ static int rim_manifold(const hull_t* A, const hull_t* B, const contact_t* c0, r
   }
   return k;
 }
-/* the self-contact manifold of cfg->self_manifold (1: faces, 2: faces, else rims; 0: none) */
+/* Ruling on a face (cfg->self_manifold 3, round 5; PhysX PCM keeps up to 4 points per convex pair):
+ * one hull presents a face along the pair direction (hull_face: a core circle within FACE_COS of it
+ * that supports the hull) and the other a ruling (hull_ruling) within RIM_DEG of the contact plane --
+ * a link lying on another's cap. Up to 3 points: the GJK point (its GJK normal: the pair's warm
+ * start), then the two ends of the ruling's stretch over the face's core disk (the segment clipped
+ * to the disk in the face plane), kept when more than 1 mm from the GJK point along the ruling and
+ * within the margin, each with the face's exact normal (B -> A) and the ruling end's distance to the
+ * face plane minus 2 CORE_M, at the midpoint between the end and its foot on the face. */
+static int rim_face_manifold(const hull_t* A, const hull_t* B, const contact_t* c0, real margin, contact_t out[3]) {
+  const real* n = c0->n;
+  const real nA[3] = {-n[0], -n[1], -n[2]};
+  real ua[3], ub[3], pr[2][3];
+  const int fa = hull_face(A, nA, ua), fb = hull_face(B, n, ub);
+  if ((fa >= 0) == (fb >= 0)) return 0;
+  /* the face (centre cf, outward normal uf toward the other hull, core radius rf) and the ruling */
+  const real* cf = fa >= 0 ? A->c[fa] : B->c[fb];
+  const real* uf = fa >= 0 ? ua : ub;
+  if (fa >= 0) hull_ruling(B, n, pr);
+  else hull_ruling(A, nA, pr);
+  real nr[3];  /* the contact normal B -> A: -A's face normal, or B's */
+  for (int q = 0; q < 3; ++q) nr[q] = fa >= 0 ? -uf[q] : uf[q];
+  real sv[3];
+  for (int q = 0; q < 3; ++q) sv[q] = pr[1][q] - pr[0][q];
+  const real ls = sqrtr(v3_dot(sv, sv));
+  if (ls < (real)1e-3) return 0;
+  const real sin_t = (real)sqrt(1.0 - g_rim_cos * g_rim_cos);
+  if (fabs((double)v3_dot(sv, n)) > sin_t * ls) return 0;
+  /* the stretch of the ruling whose foot lies inside the face's core disk: |P (x(t) - cf)| <= rf */
+  const real rf = sqrtr(v3_dot(cf + 3, cf + 3));
+  real q0[3], qs[3];
+  for (int q = 0; q < 3; ++q) q0[q] = pr[0][q] - cf[q];
+  const real q0u = v3_dot(q0, uf), qsu = v3_dot(sv, uf);
+  for (int q = 0; q < 3; ++q) { q0[q] -= q0u * uf[q]; qs[q] = sv[q] - qsu * uf[q]; }
+  const real a = v3_dot(qs, qs), b = 2 * v3_dot(q0, qs), c = v3_dot(q0, q0) - rf * rf;
+  const real disc = b * b - 4 * a * c;
+  int k = 0;
+  out[k++] = *c0;
+  if (!(a > (real)1e-12) || !(disc > 0)) return k;
+  const real sq = sqrtr(disc);
+  const real lo = fmax(0.0, (double)((-b - sq) / (2 * a))), hi = fmin(1.0, (double)((-b + sq) / (2 * a)));
+  if (!((hi - lo) * ls > (real)1e-3)) return k;
+  real wg[3];
+  for (int q = 0; q < 3; ++q) wg[q] = c0->x[q] - pr[0][q];
+  const real tg = v3_dot(wg, sv) / (ls * ls);
+  for (int e = 0; e < 2; ++e) {
+    const real t = e == 0 ? lo : hi;
+    if (!(fabs((double)(t - tg)) * ls > 1e-3)) continue;
+    real x[3], g;
+    for (int q = 0; q < 3; ++q) x[q] = pr[0][q] + t * sv[q];
+    {
+      real d[3];
+      for (int q = 0; q < 3; ++q) d[q] = x[q] - cf[q];
+      g = v3_dot(d, uf);
+    }
+    const real sep = g - 2 * (real)CORE_M;
+    if (!(sep < margin)) continue;
+    contact_t* o = &out[k++];
+    o->la = c0->la; o->lb = c0->lb; o->sep = sep; o->rim = -1;
+    for (int q = 0; q < 3; ++q) { o->n[q] = nr[q]; o->x[q] = x[q] - (real)0.5 * g * uf[q]; }
+  }
+  return k;
+}
+
+/* the self-contact manifold of cfg->self_manifold (1: faces; 2: faces, else side-by-side rims; 3:
+ * faces, else a ruling on a face, else side-by-side rims; 0: none) */
 static int self_manifold(int mode, const hull_t* A, const hull_t* B, const contact_t* c0, real margin, contact_t out[4]) {
   if (mode < 1 || !(c0->sep > -2 * (real)CORE_M + (real)1e-7)) return 0;
-  const int k = face_manifold(A, B, c0, margin, out);
+  int k = face_manifold(A, B, c0, margin, out);
   if (k > 0 || mode < 2) return k;
+  if (mode >= 3 && (k = rim_face_manifold(A, B, c0, margin, out)) > 0) return k;
   return rim_manifold(A, B, c0, margin, out);
 }
 
@@ -995,6 +1060,14 @@ int zbo_pair_manifold(const float* a, const float* b, float margin, float* out) 
     out[7 * j] = (float)mf[j].sep;
     for (int q = 0; q < 3; ++q) { out[7 * j + 1 + q] = (float)mf[j].n[q]; out[7 * j + 4 + q] = (float)mf[j].x[q]; }
   }
+  return k;
+}
+/* the same with the manifold mode (mirror of the library's zb_pair_manifold_mode) */
+int zbo_pair_manifold_mode(const float* a, const float* b, float margin, int mode, float* out) {
+  const int m0 = g_pair_manifold_mode;
+  g_pair_manifold_mode = mode;
+  const int k = zbo_pair_manifold(a, b, margin, out);
+  g_pair_manifold_mode = m0;
   return k;
 }
 int zbo_hull_pair(const float* a, const float* b, float margin, float* out) {
@@ -3239,17 +3312,18 @@ int zbo_contact_diag(zbo_sim* s, float* out) {
  * no early exit; -2 CORE_M = cores overlapping, beyond the exact range). Parity tests use it to
  * set aside random test states whose links interpenetrate deeper than the shape model covers. */
 /* per env, the self-contact classes of its link pairs at the current state (tests: constructed
- * manifold states, planted rare-branch bugs): out [n][8] = {pairs in contact, face-manifold pairs,
- * rim-manifold pairs (>= 2 points), overlapping-core pairs (the separating-axis branch), min core
- * separation - 2 CORE_M over the pairs, self points (cfg->self_manifold), the first face pair's
- * index (-1: none), the first rim pair's index (-1: none)} */
+ * manifold states, planted rare-branch bugs): out [n][10] = {pairs in contact, face-manifold pairs,
+ * rim-manifold pairs (side by side, >= 2 points), overlapping-core pairs (the separating-axis
+ * branch), min core separation - 2 CORE_M over the pairs, self points (cfg->self_manifold), the
+ * first face pair's index (-1: none), the first rim pair's index (-1: none), ruling-on-face pairs
+ * (>= 2 points), the first ruling-on-face pair's index (-1: none)} */
 int zbo_pair_classes(zbo_sim* s, float* out) {
   const real margin = s->c.contact_margin;
 #pragma omp parallel for schedule(dynamic, 64)
   for (int e = 0; e < s->n; ++e) {
     kin_t k;
     fk(&s->m, &s->env[e].ph, &k);
-    int nh = 0, nf = 0, nr = 0, nd = 0, np_ = 0, pf = -1, pr = -1;
+    int nh = 0, nf = 0, nr = 0, nd = 0, np_ = 0, pf = -1, pr = -1, nrf = 0, prf = -1;
     real mn = (real)1e30;
     for (int p = 0; p < s->m.npairs; ++p) {
       hull_t A, B;
@@ -3264,14 +3338,16 @@ int zbo_pair_classes(zbo_sim* s, float* out) {
       if (!(c.sep > -2 * (real)CORE_M + (real)1e-7)) ++nd;
       c.la = s->m.pairs[p][0]; c.lb = s->m.pairs[p][1];
       const int kf = s->c.self_manifold >= 1 ? self_manifold(1, &A, &B, &c, margin, mf) : 0;
+      const int kr = s->c.self_manifold >= 3 && kf == 0 ? rim_face_manifold(&A, &B, &c, margin, mf) : 0;
       const int km = self_manifold(s->c.self_manifold, &A, &B, &c, margin, mf);
       if (kf > 0) { ++nf; if (pf < 0) pf = p; }
-      else if (km >= 2) { ++nr; if (pr < 0) pr = p; }
+      else if (kr >= 2) { ++nrf; if (prf < 0) prf = p; }
+      else if (kr == 0 && km >= 2) { ++nr; if (pr < 0) pr = p; }
       np_ += km > 0 ? km : 1;
     }
-    float* o = out + 8 * (size_t)e;
+    float* o = out + 10 * (size_t)e;
     o[0] = (float)nh; o[1] = (float)nf; o[2] = (float)nr; o[3] = (float)nd;
-    o[4] = (float)(nh ? mn : 1); o[5] = (float)np_; o[6] = (float)pf; o[7] = (float)pr;
+    o[4] = (float)(nh ? mn : 1); o[5] = (float)np_; o[6] = (float)pf; o[7] = (float)pr; o[8] = (float)nrf; o[9] = (float)prf;
   }
   return 0;
 }

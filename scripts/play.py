@@ -117,13 +117,25 @@ def main(argv=None) -> dict:
     fin = torch.zeros(5, device=sim.device)  # episodes, length sum, return sum, distance sum, time-outs
     vel_sum = torch.zeros((), device=sim.device)
     vel_cnt = torch.zeros((), device=sim.device)
+    # walking v2's contact sensor (state rows FEET_AIR_CUR / FEET_AIR_LAST): the gait's air time --
+    # foot-steps in the air, touchdowns (last_air_time refreshed) and the air time they end
+    gait = sim.state_dim == zm.STATE_DIM and args.task.startswith("zbot-6b-walking-v2")
+    air = torch.zeros(3, device=sim.device)  # airborne foot-steps, touchdowns, air time at touchdown
+    a_last = sim.get_state()[zm.S["FEET_AIR_LAST"]:zm.S["FEET_AIR_LAST"] + 2].clone() if gait else None
     with torch.inference_mode():
         for _ in range(args.num_steps):
             actions = policy(obs)
             obs_d, rew, dones, extras = env.step(actions)
             obs = obs_d["policy"] if hasattr(obs_d, "keys") else obs_d
-            x = sim.get_state()[x_row]
+            stt = sim.get_state()
+            x = stt[x_row]
             d = dones > 0
+            if gait:
+                cur = stt[zm.S["FEET_AIR_CUR"]:zm.S["FEET_AIR_CUR"] + 2]
+                last = stt[zm.S["FEET_AIR_LAST"]:zm.S["FEET_AIR_LAST"] + 2]
+                td = (last != a_last) & (last > 0) & ~d
+                air += torch.stack([(cur > 0).sum().float(), td.sum().float(), torch.where(td, last, 0.0).sum()])
+                a_last = last.clone()
             alive = ~d
             vel_sum += torch.where(alive, (x - x_prev) / dt, 0.0).sum()
             vel_cnt += alive.sum()
@@ -146,6 +158,10 @@ def main(argv=None) -> dict:
            "mean_episode_return": f[2] / f[0] if f[0] else None,
            "mean_forward_distance_per_episode_m": f[3] / f[0] if f[0] else None,
            "mean_forward_velocity_m_s": float(vel_sum) / max(float(vel_cnt), 1.0), **posture}
+    if gait:
+        a = air.tolist()
+        out.update(airborne_foot_fraction=a[0] / (2 * n * args.num_steps), touchdowns_per_env_s=a[1] / (n * args.num_steps * dt),
+                   mean_air_time_at_touchdown_s=a[2] / a[1] if a[1] else None)
     print(json.dumps(out), flush=True)
     env.close()
     return out

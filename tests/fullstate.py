@@ -30,6 +30,7 @@ def base_task(task: str) -> str:
 
 
 SOLVER_MODE = 0  # zb_task_cfg.solver_mode of the configs below (tests switch it with solver_mode())
+SELF_MANIFOLD = None  # zb_task_cfg.self_manifold override (tests switch it with self_manifold())
 
 
 def task_cfg(task: str) -> zm.TaskCfg:
@@ -39,6 +40,8 @@ def task_cfg(task: str) -> zm.TaskCfg:
         from zbot_lab_amd.envs.walking_v2 import REWARD_CFGS
         cfg.reward_weights = dict(REWARD_CFGS[task.split(":", 1)[1]]["reward_scales"])
     cfg.solver_mode = SOLVER_MODE
+    if SELF_MANIFOLD is not None:
+        cfg.self_manifold = SELF_MANIFOLD
     return cfg
 
 
@@ -55,6 +58,21 @@ class solver_mode:
     def __exit__(self, *exc):
         global SOLVER_MODE
         SOLVER_MODE = self.prev
+
+
+class self_manifold:
+    """Context manager: the task configs built inside use this self-contact manifold mode."""
+
+    def __init__(self, mode: int):
+        self.mode = mode
+
+    def __enter__(self):
+        global SELF_MANIFOLD
+        self.prev, SELF_MANIFOLD = SELF_MANIFOLD, self.mode
+
+    def __exit__(self, *exc):
+        global SELF_MANIFOLD
+        SELF_MANIFOLD = self.prev
 
 
 def _rows(d: dict, name: str, k: int) -> list:
@@ -292,7 +310,7 @@ def manifold_seeds() -> dict:
     return SEEDS
 
 
-CLASS_COL = {"face": 1, "rim": 2, "deep": 3}   # zbo_pair_classes column that marks the class
+CLASS_COL = {"face": 1, "rim": 2, "deep": 3, "rimface": 8}   # zbo_pair_classes column that marks the class
 
 
 def constructed_states(task: str, kind: str, n: int, seed: int, jitter: float = 0.003, lift: float = 0.06):
@@ -304,7 +322,9 @@ def constructed_states(task: str, kind: str, n: int, seed: int, jitter: float = 
     from oracle.pyoracle import OracleSim
     seeds = manifold_seeds()[kind]
     rng = np.random.default_rng(seed)
-    o = OracleSim(n, task_cfg(task), seed=seed)
+    cfg = task_cfg(task)
+    cfg.self_manifold = 3  # (classes as self_manifold 3 sees them: a ruling-on-face pair is not a rim pair)
+    o = OracleSim(n, cfg, seed=seed)
     st = random_states(task, o, n, seed=seed + 1)
     which = np.arange(n) % len(seeds)
     todo = np.arange(n)

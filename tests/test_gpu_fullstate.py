@@ -483,24 +483,31 @@ def test_full_state_contact_cache(gpu, task):
     assert (wg[3::4][:, g_out[2] | g_out[3]] == -1).all()
 
 
-@pytest.mark.parametrize("kind", ["face", "rim"])
+@pytest.mark.parametrize("kind", ["face", "rim", "rimface"])
 @pytest.mark.parametrize("task", ["v2", "standup"])
 def test_full_state_face_manifold(gpu, task, kind):
     """The self-contact manifold (zb_task_cfg.self_manifold 2) on 512 constructed
     gentle folds per case (tests/fullstate.constructed_states: the joint angles of a seed fold from
     tests/golden/manifold_seeds.npz plus 3 mrad of jitter, the class checked by the oracle's
     per-pair classes): "face" -- one link pair cap on cap (up to 4 points), "rim" -- one pair side by
-    side (the GJK point + the two ends of the rulings' overlap), no overlapping cores anywhere; one
-    step on both sides under the full-state rule, with the contact-active aggregate against the f64
-    oracle over all 512 envs."""
-    from fullstate import constructed_states
+    side (the GJK point + the two ends of the rulings' overlap), "rimface" -- one link lying on
+    another's cap (self_manifold 3: the GJK point + the ends of the ruling over the cap disk), no
+    overlapping cores anywhere; one step on both sides under the full-state rule, with the
+    contact-active aggregate against the f64 oracle over all 512 envs."""
+    from fullstate import constructed_states, self_manifold
     seed, n = 43, 512
-    st, which = constructed_states(task, kind, n, seed=606)
-    g, o, cfg, torch = _sims(task, n, seed)
-    assert cfg.self_manifold == 2
-    o.set_state(st)
-    pc = o.pair_classes()
-    assert (pc[:, {"face": 1, "rim": 2}[kind]] > 0).all() and (pc[:, 3] == 0).all()
+    mode = 3 if kind == "rimface" else 2
+    with self_manifold(mode):
+        st, which = constructed_states(task, kind, n, seed=606)
+        g, o, cfg, torch = _sims(task, n, seed)
+        assert cfg.self_manifold == mode
+        o.set_state(st)
+        pc = o.pair_classes()
+        assert (pc[:, {"face": 1, "rim": 2, "rimface": 8}[kind]] > 0).all() and (pc[:, 3] == 0).all()
+        _manifold_step(task, kind, n, seed, st, which, pc, g, torch)
+
+
+def _manifold_step(task, kind, n, seed, st, which, pc, g, torch):
     print(f"\n[{task} {kind}] {n} constructed envs from {len(np.unique(which))} seed folds; self points per env "
           f"{pc[:, 5].mean():.2f}")
     g.set_state(torch.from_numpy(st).cuda())

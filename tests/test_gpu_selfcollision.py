@@ -178,21 +178,29 @@ def _rim_pairs(n, seed):
     return out
 
 
-def _compare_manifolds(pairs, label, ntol_multi, gjk_first=False):
-    """zb_pair_manifold vs zbo_pair_manifold: counts and (for agreeing counts) points."""
+def _compare_manifolds(pairs, label, ntol_multi, gjk_first=False, mode=2):
+    """zb_pair_manifold_mode vs zbo_pair_manifold (self_manifold ``mode``): counts and (for agreeing
+    counts) points."""
+    import ctypes as C
     import torch
     from zbot_lab_amd import _native as nat
     n = len(pairs)
     ref = np.zeros((n, 29), np.float32)
-    for k in range(n):
-        pts = np.zeros(28, np.float32)
-        c = pyoracle.lib().zbo_pair_manifold(np.ascontiguousarray(pairs[k, 0]).ravel(), np.ascontiguousarray(pairs[k, 1]).ravel(),
-                                             MARGIN, pts)
-        ref[k, 0] = c
-        ref[k, 1:] = pts
+    lib = pyoracle.lib()
+    lib.zbo_set_pair_manifold_mode.argtypes = [C.c_int]
+    lib.zbo_set_pair_manifold_mode(mode)
+    try:
+        for k in range(n):
+            pts = np.zeros(28, np.float32)
+            c = lib.zbo_pair_manifold(np.ascontiguousarray(pairs[k, 0]).ravel(), np.ascontiguousarray(pairs[k, 1]).ravel(),
+                                      MARGIN, pts)
+            ref[k, 0] = c
+            ref[k, 1:] = pts
+    finally:
+        lib.zbo_set_pair_manifold_mode(2)
     P = torch.from_numpy(np.ascontiguousarray(pairs)).cuda()
     out = torch.zeros(n, 29, device="cuda")
-    nat.check(nat.lib().zb_pair_manifold(nat.ptr(P), n, MARGIN, nat.ptr(out), None), "zb_pair_manifold")
+    nat.check(nat.lib().zb_pair_manifold_mode(nat.ptr(P), n, MARGIN, mode, nat.ptr(out), None), "zb_pair_manifold_mode")
     got = out.cpu().numpy()
     same = got[:, 0] == ref[:, 0]
     print(f"\n{label} pairs {n}: oracle counts {np.bincount(ref[:, 0].astype(int), minlength=5).tolist()}, "
@@ -220,6 +228,39 @@ def test_gpu_rim_manifold_matches_oracle():
     to 2e-5 m, normals to 5e-4, points to 1e-4 m."""
     ref, got, same, bad = _compare_manifolds(_rim_pairs(4000, 31), "rim manifold", 5e-4, gjk_first=True)
     assert (ref[:, 0] >= 2).sum() >= 1000 and (ref[:, 0] == 3).sum() >= 40  # (parallel rulings: GJK ends at one end)
+    assert same.mean() >= 0.99
+    assert len(bad) <= 0.01 * same.sum(), bad[:20]
+
+
+def _rimface_pairs(n, seed):
+    """A link lying on its side over an upright link's cap: the lying link tilted by up to 8 degrees
+    about a random axis, shifted over the cap by up to 4 cm, gap -3 .. 4 mm, the whole configuration
+    rotated at random: rulings within and beyond the 5-degree threshold, stretches inside and across
+    the cap's rim, and the GJK point at either end."""
+    from tests.test_oracle_selfcollision import _flat_link
+    rng = np.random.default_rng(seed)
+    lie = _rot_axis([0, 1, 0], np.pi / 2)
+    out = np.zeros((n, 2, 2, 9), np.float32)
+    for k in range(n):
+        ra, rb = rng.uniform(0.035, 0.05, 2)
+        tilt = _rot_axis(rng.normal(size=3), np.radians(rng.uniform(0, 8)))
+        G = _rot(_quat(rng))
+        pa = np.array([rng.uniform(-0.04, 0.02), rng.uniform(-0.02, 0.02), 0.053 + ra + rng.uniform(-0.003, 0.004)])
+        ha = world(_flat_link(ra), G @ tilt @ lie, G @ pa)
+        hb = world(_flat_link(rb), G, np.zeros(3))
+        out[k, 0], out[k, 1] = (ha, hb) if k % 2 == 0 else (hb, ha)   # the face on B, then on A
+    return out
+
+
+def test_gpu_ruling_on_face_manifold_matches_oracle():
+    """The ruling-on-face manifold (self_manifold 3, round 5: the GJK point + the ends of the lying
+    link's ruling over the cap's disk) of quad_manifold (zb_pair_manifold_mode) against the oracle's
+    rim_face_manifold on 4000 pairs, the face on either hull: the same number of points in the same
+    order for >= 99 %, separations to 2e-5 m, the ends' normals (the cap's exact normal) to 5e-4,
+    points to 1e-4 m."""
+    ref, got, same, bad = _compare_manifolds(_rimface_pairs(4000, 41), "ruling-on-face manifold", 5e-4,
+                                             gjk_first=True, mode=3)
+    assert (ref[:, 0] >= 2).sum() >= 1000 and (ref[:, 0] == 3).sum() >= 100, np.bincount(ref[:, 0].astype(int))
     assert same.mean() >= 0.99
     assert len(bad) <= 0.01 * same.sum(), bad[:20]
 

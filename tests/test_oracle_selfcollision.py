@@ -397,3 +397,46 @@ def test_rim_manifold_mode_switch():
     finally:
         lib.zbo_set_pair_manifold_mode(2)
     assert len(pair_manifold(ha, hb, 0.004)) >= 2
+
+
+def test_ruling_on_face_manifold():
+    """A link lying on another's cap (cfg self_manifold 3, round 5): the GJK point
+    plus the two ends of the lying link's core ruling clipped to the cap's core disk, each with the
+    cap's normal and the end's height above the cap plane minus 2 CORE_M (direct evaluation); a ruling
+    reaching past the cap is cut at the disk's rim; a 3-degree tilt shows in the ends' gaps; a
+    10-degree tilt (outside RIM_DEG) and self_manifold 2 give the GJK point alone."""
+    link = _flat_link(0.05)
+    axis_x = _rot_axis([0, 1, 0], np.pi / 2)  # the link's axis along x: lying on its side
+    rc = 0.05 - CORE_M
+    lib = pyoracle.lib()
+    lib.zbo_set_pair_manifold_mode.argtypes = [C.c_int]
+    try:
+        lib.zbo_set_pair_manifold_mode(3)
+        hb = world(link, np.eye(3), np.zeros(3))                    # upright: its top cap at z = 0.053
+        for px, gap in ((-0.02, 0.002), (-0.02, 0.0004), (0.02, 0.001)):
+            ha = world(link, axis_x, np.array([px, 0.0, 0.053 + 0.05 + gap]))
+            pts = pair_manifold(ha, hb, 0.004)
+            assert len(pts) in (2, 3), (px, gap, pts)
+            np.testing.assert_allclose(pts[:, 0], gap, atol=5e-6)
+            np.testing.assert_allclose(pts[1:, 1:4], np.tile([0, 0, 1], (len(pts) - 1, 1)), atol=1e-6)
+            np.testing.assert_allclose(pts[1:, 6], 0.053 - CORE_M + (gap + 2 * CORE_M) / 2, atol=1e-6)  # midpoints
+            lo, hi = px + CORE_M, min(px + 0.053 - CORE_M, rc)            # the ruling clipped to the cap disk
+            assert abs(pts[:, 4].min() - lo) < 1e-3 + 1e-6 and abs(pts[:, 4].max() - hi) < 1e-3 + 1e-6, pts[:, 4]
+            assert np.all(np.hypot(pts[1:, 4], pts[1:, 5]) <= rc + 1e-6)
+        # 3 degrees about y: the ends' gaps are their heights above the cap's core plane
+        ha = world(link, _rot_axis([0, 1, 0], np.radians(3)) @ axis_x, np.array([-0.02, 0.0, 0.053 + 0.05 + 0.0005]))
+        pts = pair_manifold(ha, hb, 0.004)
+        assert len(pts) >= 2, pts
+        for p in pts[1:]:
+            # the core point on A: the midpoint raised by half the core gap along the cap normal
+            xa = p[4:7] + (p[0] + 2 * CORE_M) / 2 * np.array([0, 0, 1.0])
+            assert abs(xa[2] - (0.053 - CORE_M) - 2 * CORE_M - p[0]) < 2e-6
+        assert pts[:, 0].max() - pts[:, 0].min() > 1e-3  # (the GJK point sits at the low end)
+        # 10 degrees: outside RIM_DEG
+        ha = world(link, _rot_axis([0, 1, 0], np.radians(10)) @ axis_x, np.array([-0.02, 0.0, 0.053 + 0.05 + 0.001]))
+        assert len(pair_manifold(ha, hb, 0.004)) <= 1
+        lib.zbo_set_pair_manifold_mode(2)
+        ha = world(link, axis_x, np.array([-0.02, 0.0, 0.053 + 0.05 + 0.001]))
+        assert len(pair_manifold(ha, hb, 0.004)) == 1
+    finally:
+        lib.zbo_set_pair_manifold_mode(2)

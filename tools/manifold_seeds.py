@@ -9,7 +9,7 @@ one (a face pair almost always comes with deep overlaps elsewhere, so uniform sa
 finds few gentle ones: VERDICT r4). The tests then build their envs from these seeds directly --
 each seed's joint angles plus a small jitter, kept when the class survives -- instead of sampling.
 
-Writes tests/golden/manifold_seeds.npz: {face, rim, deep}: [k, 6] joint angles (float32).
+Writes tests/golden/manifold_seeds.npz: {face, rim, deep, rimface}: [k, 6] joint angles (float32).
 """
 from __future__ import annotations
 
@@ -30,16 +30,19 @@ POOL, ROUNDS, MAX_SEEDS = 500_000, 8, 256
 
 
 def classify(pc: np.ndarray) -> dict:
-    """Gentle classes from zbo_pair_classes rows: no overlapping cores except the deep class's one."""
+    """Gentle classes from zbo_pair_classes rows (self_manifold 3): no overlapping cores except the deep
+    class's one."""
     gentle = pc[:, 3] == 0
     return {"face": gentle & (pc[:, 1] > 0), "rim": gentle & (pc[:, 2] > 0),
-            "deep": (pc[:, 3] == 1) & (pc[:, 0] <= 2)}
+            "deep": (pc[:, 3] == 1) & (pc[:, 0] <= 2), "rimface": gentle & (pc[:, 8] > 0)}
 
 
 def main():
-    o = OracleSim(POOL, task_cfg("v2"), seed=1)
+    cfg = task_cfg("v2")
+    cfg.self_manifold = 3
+    o = OracleSim(POOL, cfg, seed=1)
     base = random_states("v2", o, POOL, seed=5)
-    seeds = {k: [] for k in ("face", "rim", "deep")}
+    seeds = {k: [] for k in ("face", "rim", "deep", "rimface")}
     for r in range(ROUNDS):
         st = base.copy()
         st[13:19] = np.random.default_rng(100 + r).uniform(-np.pi, np.pi, (6, POOL)).astype(np.float32)

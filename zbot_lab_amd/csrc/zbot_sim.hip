@@ -622,13 +622,6 @@ constexpr int LDS4 = CARRY_OFF + EPW * CARRY_W / 4;
 constexpr int STG_LEN = 88 + 25 + 3;  // >= max state dim + max obs dim + {reward, term, trunc}
 constexpr int LOGR_OFF = (EPW * STG_LEN + 3) / 4;  // region U, after STG
 static_assert(LOGR_OFF + EPW * LOGR_W / 4 <= U_END, "STG + LOGR fit region U");
-// split step kernel (zb_step_split_kernel: a physics wave and a collision wave per workgroup of EPW
-// envs): the hand-off record per env {contacts, overflow, root height, -} and the physics wave's
-// Cholesky stash in its own region (the collision wave builds the world capsules in region V
-// meanwhile)
-constexpr int SPL_OFF = LDS4;
-constexpr int STASH_S_OFF = SPL_OFF + EPW;
-constexpr int LDS4S = STASH_S_OFF + 2 * WGT;
 
 // prologue results the MDP reads after the physics (parked in LDS across the substeps)
 struct Pre {
@@ -659,7 +652,6 @@ struct Q {
   __device__ __forceinline__ const float4* jtab(int j) const { return b + LNK_OFF + JT_OFF + j * 5; }
   __device__ __forceinline__ const float4* btab(int bb) const { return b + LNK_OFF + BT_OFF + bb * 3; }
   __device__ __forceinline__ float4& cap(int l, int k) const { return b[UB_OFF + (2 * l + k) * EPW + e]; }
-  __device__ __forceinline__ float4& spl() const { return b[SPL_OFF + e]; }
   __device__ __forceinline__ const float4* link(int l) const { return gl + l * LINK4; }
   __device__ __forceinline__ int pair_code(int p) const { return reinterpret_cast<const int*>(b + LNK_OFF + NL * LINK4)[p]; }
   __device__ __forceinline__ const float4* dflt() const { return b + LNK_OFF + DFLT_OFF; }
@@ -1341,9 +1333,80 @@ __device__ __forceinline__ int quad_rim(const QCircle& h, int j, const SelfConta
   return 1 + (ok[0] ? 1 : 0) + (ok[1] ? 1 : 0);
 }
 
+// Ruling on a face (cfg.self_manifold 3; the oracle's rim_face_manifold): exactly one hull presents a
+// face (fm: the face mask of quad_manifold; uo / r: this lane's circle normal oriented along its
+// hull's direction and its core radius), the other its ruling within 5 degrees of the contact plane
+// (the segment between its two circles' support points): the GJK point (lane 0, GJK's normal) and
+// the two ends of the ruling's stretch over the face's core disk (lanes 1 and 2), more than 1 mm
+// from the GJK point along the ruling and within the margin, with the face's normal (B -> A) and the
+// end's height above the face plane minus 2 kCoreM. Returns the point count (0: not this case).
+template <class Sink>
+__device__ __forceinline__ int quad_rimface(const QCircle& h, int j, const SelfContact& sc, float margin, bool write,
+                                            Sink sink, int fm, const float uo[3], float r) {
+  const float sgd = (j & 2) ? 1.f : -1.f;
+  const float dd[3] = {sgd * sc.n[0], sgd * sc.n[1], sgd * sc.n[2]};
+  const float a = dot3(dd, h.e1), b = dot3(dd, h.e2);
+  const float ri = __builtin_amdgcn_rsqf(fmaxf(fmaf(a, a, b * b), 1e-30f));
+  float p[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) p[k] = h.c[k] + (a * h.e1[k] + b * h.e2[k]) * ri;
+  const bool fa = (fm & 3) != 0;
+  const bool l1 = fa ? (fm & 1) == 0 : (fm & 4) == 0;  // the face on the second circle of its hull
+  float cf[3], uf[3], r0[3], sv[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const float c0 = dppf<0x00>(h.c[k]), c1 = dppf<0x55>(h.c[k]), c2 = dppf<0xAA>(h.c[k]), c3 = dppf<0xFF>(h.c[k]);
+    const float u0 = dppf<0x00>(uo[k]), u1 = dppf<0x55>(uo[k]), u2 = dppf<0xAA>(uo[k]), u3 = dppf<0xFF>(uo[k]);
+    const float p0 = dppf<0x00>(p[k]), p1 = dppf<0x55>(p[k]), p2 = dppf<0xAA>(p[k]), p3 = dppf<0xFF>(p[k]);
+    cf[k] = fa ? (l1 ? c1 : c0) : (l1 ? c3 : c2);
+    uf[k] = fa ? (l1 ? u1 : u0) : (l1 ? u3 : u2);
+    r0[k] = fa ? p2 : p0;                 // the other hull's ruling
+    sv[k] = fa ? p3 - p2 : p1 - p0;
+  }
+  const float rr0 = dppf<0x00>(r), rr1 = dppf<0x55>(r), rr2 = dppf<0xAA>(r), rr3 = dppf<0xFF>(r);
+  const float rf = fa ? (l1 ? rr1 : rr0) : (l1 ? rr3 : rr2);
+  const float ls = sqrtf(dot3(sv, sv));
+  if (ls < 1e-3f || fabsf(dot3(sv, sc.n)) > kRimSin * ls) return 0;
+  const float sg = fa ? -1.f : 1.f;
+  const float nr[3] = {sg * uf[0], sg * uf[1], sg * uf[2]};  // B -> A
+  float q0[3], qs[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) q0[k] = r0[k] - cf[k];
+  const float q0u = dot3(q0, uf), qsu = dot3(sv, uf);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) { q0[k] -= q0u * uf[k]; qs[k] = sv[k] - qsu * uf[k]; }
+  const float qa = dot3(qs, qs), qb = 2.f * dot3(q0, qs), qc = dot3(q0, q0) - rf * rf;
+  const float disc = qb * qb - 4.f * qa * qc;
+  const float sq = sqrtf(fmaxf(disc, 0.f)), i2a = 0.5f / fmaxf(qa, 1e-30f);
+  const float lo = fmaxf(0.f, (-qb - sq) * i2a), hi = fminf(1.f, (-qb + sq) * i2a);
+  const bool span = qa > 1e-12f && disc > 0.f && (hi - lo) * ls > 1e-3f;
+  const float wg[3] = {sc.x[0] - r0[0], sc.x[1] - r0[1], sc.x[2] - r0[2]};
+  const float tg = dot3(wg, sv) / (ls * ls);
+  bool ok[2];
+  float4 px[2];
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const float t = e ? hi : lo;
+    float x[3], d[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { x[k] = r0[k] + t * sv[k]; d[k] = x[k] - cf[k]; }
+    const float g = dot3(d, uf), sep = g - 2.f * kCoreM;
+    ok[e] = span && fabsf(t - tg) * ls > 1e-3f && sep < margin;
+    px[e] = make_float4(x[0] - 0.5f * g * uf[0], x[1] - 0.5f * g * uf[1], x[2] - 0.5f * g * uf[2], sep);
+  }
+  if (write) {
+    if (j == 0) sink(0, make_float4(sc.x[0], sc.x[1], sc.x[2], sc.sep), sc.n);  // (GJK's normal: the warm start)
+    if (j == 1 && ok[0]) sink(1, px[0], nr);
+    if (j == 2 && ok[1]) sink(ok[0] ? 2 : 1, px[1], nr);
+  }
+  return 1 + (ok[0] ? 1 : 0) + (ok[1] ? 1 : 0);
+}
+
+// mode = cfg.self_manifold: 1 faces; 2 faces, else side-by-side rims; 3 faces, else a ruling on a
+// face, else side-by-side rims (the oracle's self_manifold)
 template <class Sink>
 __device__ __forceinline__ int quad_manifold(const QCircle& h, int j, const SelfContact& sc, float margin, bool write,
-                                             bool rim, Sink sink) {
+                                             int mode, Sink sink) {
   const float sgd = (j & 2) ? 1.f : -1.f;
   const float dd[3] = {sgd * sc.n[0], sgd * sc.n[1], sgd * sc.n[2]};
   float u[3];
@@ -1358,9 +1421,15 @@ __device__ __forceinline__ int quad_manifold(const QCircle& h, int j, const Self
   int fm = (sup && fabsf(al) >= kFaceCos) ? (1 << j) : 0;
   fm |= dppi<DPP_XOR1>(fm);
   fm |= dppi<DPP_XOR2>(fm);
-  if (!(fm & 3) || !(fm & 12)) return rim ? quad_rim(h, j, sc, margin, write, sink) : 0;
   const float so = al < 0.f ? -1.f : 1.f;
   const float uo[3] = {so * u[0], so * u[1], so * u[2]};
+  if (!(fm & 3) || !(fm & 12)) {
+    if (mode >= 3 && ((fm & 3) == 0) != ((fm & 12) == 0)) {  // a face on exactly one side
+      const int k = quad_rimface(h, j, sc, margin, write, sink, fm, uo, r);
+      if (k > 0) return k;
+    }
+    return mode >= 2 ? quad_rim(h, j, sc, margin, write, sink) : 0;
+  }
   const bool a1 = !(fm & 1), b3 = !(fm & 4);  // A's face on quad lane 1 (else 0), B's on 3 (else 2)
   float ca[3], ua[3], cb[3], ub[3];
 #pragma unroll
@@ -1608,7 +1677,7 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q&
     // team, bit r: the pair of rank r is a contact (allhits), its points - 1 = exl + 2 exh: a pair's
     // first candidate position is g_tot + the points of the lower ranks
     unsigned long long allhits = 0ull, exl = 0ull, exh = 0ull;
-    const bool mfon = cfg.self_manifold != 0, rimon = cfg.self_manifold >= 2;
+    const bool mfon = cfg.self_manifold != 0;
 #pragma unroll 1
     for (int pass = 0; pass < 2; ++pass) {
       for (int k = 0; k < urounds; ++k) {
@@ -1664,7 +1733,7 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q&
         // write pass stores its points
         const float code = (float)(pcode + 1);
         const int mc = (mfon && sc.sep > -2.f * kCoreM + 1e-7f)
-                           ? quad_manifold(hc, qj, sc, margin, pass == 1, rimon, [&](int rank, float4 xs, const float* nn) {
+                           ? quad_manifold(hc, qj, sc, margin, pass == 1, cfg.self_manifold, [&](int rank, float4 xs, const float* nn) {
                                if (pos + rank < g_tot + NSELF) {
                                  q.cand(pos + rank, 0) = xs;
                                  q.cand(pos + rank, 1) = make_float4(nn[0], nn[1], nn[2], code);
@@ -1855,18 +1924,8 @@ __device__ __forceinline__ void sens_store(const Q& q, float* __restrict__ st, i
 #ifndef ZB_CARRY
 #define ZB_CARRY 1
 #endif
-// state and observation stores write-through (sc1 vector stores, -DZB_WT_STORES=1): the bytes leave
-// the XCD L2 as the waves finish instead of in the end-of-kernel write-back (profiles/r4_wt: 0.6 %
-// faster), but each 16-byte row piece of a staged store then goes to HBM as its own partial-line
-// write: WRITE_SIZE 1.7x the bytes written (profiles/r4h) against 1.0x with write-back. Off by
-// default.
-#ifndef ZB_WT_STORES
-#define ZB_WT_STORES 0
-#endif
 __device__ __forceinline__ float& Q::stg(int k) const { return reinterpret_cast<float*>(b + YG_OFF)[e * STG_LEN + k]; }
-// WT >= 0: state row WT is stored with agent scope (the walking kernel's episode length, which a
-// fused finalize may overwrite with the full-reset draw from another XCD, finalize_body)
-template <int SD, int OD, int WT = -1>
+template <int SD, int OD>
 __device__ __forceinline__ void staged_store(const Q& q, int env0, int N, float* __restrict__ st,
                                              float* __restrict__ obs, float* __restrict__ rew,
                                              uint8_t* __restrict__ term, uint8_t* __restrict__ trunc) {
@@ -1876,15 +1935,8 @@ __device__ __forceinline__ void staged_store(const Q& q, int env0, int N, float*
   const int e = q.lane % EPW, f0 = q.lane / EPW;
   const int env = env0 + e;
   if (env < N) {
-#ifndef ZB_DIAG_NO_STATE_STORE  // diagnostic only (scripts/gpu_r1o.sh): measures the state stores' cost
 #pragma unroll
-    for (int f = f0; f < SD; f += WGT / EPW) {
-      const float v = S[e * STG_LEN + f];
-      if (ZB_WT_STORES || (WT >= 0 && f == WT))
-        __hip_atomic_store(&st[(size_t)f * N + env], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      else st[(size_t)f * N + env] = v;
-    }
-#endif
+    for (int f = f0; f < SD; f += WGT / EPW) st[(size_t)f * N + env] = S[e * STG_LEN + f];
     if (f0 == 0) rew[env] = S[e * STG_LEN + SD + OD];
     if (f0 == 1) term[env] = S[e * STG_LEN + SD + OD + 1] != 0.f ? 1 : 0;
     if (f0 == 2) trunc[env] = S[e * STG_LEN + SD + OD + 2] != 0.f ? 1 : 0;
@@ -1893,9 +1945,7 @@ __device__ __forceinline__ void staged_store(const Q& q, int env0, int N, float*
 #pragma unroll
   for (int t = q.lane; t < EPW * OD; t += WGT)
     if (t < nv * OD) {
-      const float v = S[(t / OD) * STG_LEN + SD + t % OD];
-      if (ZB_WT_STORES) __hip_atomic_store(&obs[(size_t)env0 * OD + t], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      else obs[(size_t)env0 * OD + t] = v;
+      obs[(size_t)env0 * OD + t] = S[(t / OD) * STG_LEN + SD + t % OD];
     }
 }
 
@@ -2162,11 +2212,9 @@ __device__ __forceinline__ void refresh_ground(const zb_task_cfg& cfg, MP m, con
 // ------------------------------------------------------------------------- one substep
 // kLinkFriction: per-contact Coulomb coefficient from the per-link table q.fric (standup DR);
 // otherwise cfg.friction everywhere.
-// kSplit (zb_step_split_kernel): detection runs on the workgroup's collision wave between the two
-// workgroup barriers below, concurrently with this wave's RNEA / CRBA / Cholesky / drives.
 // kRefresh (zb_task_cfg.solver_mode 2, with kTgs): before every sub-iteration after the first the
 // ground contacts are re-evaluated at the pose the sub-iterations so far reached (see the sweeps).
-template <bool kDebugForces, bool kLinkFriction, bool kTgs, bool kSplit = false, bool kRefresh = false>
+template <bool kDebugForces, bool kLinkFriction, bool kTgs, bool kRefresh = false>
 __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
                                         const float target[ND], const Q& q, bool last, bool warm, SensorOut& so,
                                         float (*dbgF)[3], float* dbgTau, Stamps& sp) {
@@ -2190,16 +2238,9 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
   bool over;
   wave_sync();  // the previous substep's LDS readers are done
   fk_team<true>(s, q, Ib, Sown);
-  if (kSplit) {
-    if (q.s == 0) q.spl().z = s.pos[2];
-    __syncthreads();  // poses, root heights and the warm-start normals to the collision wave
-    nc = 0;
-    over = false;
-  } else {
-    wave_sync();
-    sp.mark(9);
-    nc = detect(cfg, s.pos[2], q, warm, over, sp);
-  }
+  wave_sync();
+  sp.mark(9);
+  nc = detect(cfg, s.pos[2], q, warm, over, sp);
   m = opaque(m0);
 
   // RNEA bias forces (qddot = 0, gravity as base acceleration) and, in the same team suffix sum,
@@ -2312,7 +2353,7 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
   float Li[NV];
   // this lane's M row entries of the joint columns, kept for a re-factorisation of the trailing
   // block if a drive saturates (the contact-row granules are dead until the rows are rebuilt)
-  float4* stash = q.b + (kSplit ? STASH_S_OFF : STASH_OFF) + 2 * q.lane;
+  float4* stash = q.b + STASH_OFF + 2 * q.lane;
   stash[0] = make_float4(R[6], R[7], R[8], R[9]);
   stash[1] = make_float4(R[10], R[11], 0.f, 0.f);
   cholesky_team(R, L, Li);
@@ -2367,12 +2408,6 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
   }
 
   sp.mark(4);
-  if (kSplit) {
-    __syncthreads();  // the collision wave's candidates
-    const float4 r = q.spl();
-    nc = __float_as_int(r.x);
-    over = r.y != 0.f;
-  }
   // contact rows (lane s builds slot s): Y = L^-1 J^T (whitened), effective masses, the
   // normal/tangent cross terms and the bias velocity. J of direction d at point x on body b:
   // [x x d ; d ; d.(a_j x (x - o_j)) for joints j < b]
@@ -2959,8 +2994,7 @@ __device__ __forceinline__ void log_flush(const Q& q, uint64_t mask, float* acc)
 }
 
 // ------------------------------------------------------------------------- kernels
-// Step-end finalisation arguments (zb_finalize_kernel, or fused into the walking step kernel: its
-// last workgroup runs the same body, FinArgs::done counting the finished workgroups).
+// Step-end finalisation arguments (zb_finalize_kernel).
 constexpr int FIN_FG = 8;  // finalize fold: accumulator slot groups
 struct FinArgs {
   float* log_means;
@@ -2971,15 +3005,7 @@ struct FinArgs {
   uint64_t seed;
   Counters* cnt;
   int ep_len_row;
-  unsigned* done;  // nullptr: not fused
-  int split_role;  // zb_step_split_kernel: which wave runs the physics (0 / 1: wave 0 / 1; 2: by SIMD slot)
 };
-template <bool kFused>
-__device__ __forceinline__ void finalize_body(int N, float* __restrict__ st, float* __restrict__ acc,
-                                              const FinArgs& fa, int force_full, int reset_counts, int is_step,
-                                              const zb_task_cfg& cfg, float* __restrict__ obs,
-                                              const uint8_t* __restrict__ term, const uint8_t* __restrict__ trunc,
-                                              float* sh);
 
 __device__ __forceinline__ void load_phys(const float* __restrict__ st, int N, int i, Phys& p) {
 #define LD(f) st[(size_t)(f) * N + i]
@@ -2995,15 +3021,15 @@ __device__ __forceinline__ void load_phys(const float* __restrict__ st, int N, i
 // One policy step per lane. Live state across the 4 substeps is kept to the physics state, the
 // joint targets and the ~15 floats of the lagged observation cache the rewards need; the MDP
 // state is loaded from HBM only after the physics.
-template <bool kTgs, bool kSplit, bool kRefresh = false>
+template <bool kTgs, bool kRefresh = false>
 __device__ __forceinline__ void step_body(const zb_model* __restrict__ mg, const float4* __restrict__ links,
                                           zb_task_cfg cfg, int N, float* __restrict__ st,
                                           const float* __restrict__ act, float* __restrict__ obs,
                                           float* __restrict__ rew, uint8_t* __restrict__ term,
                                           uint8_t* __restrict__ trunc, float* __restrict__ acc,
-                                          float* __restrict__ wc, FinArgs fa, float4* lds) {
+                                          float* __restrict__ wc, float4* lds) {
   MP m = to_mp(mg);
-  const int lane = kSplit ? (int)threadIdx.x & (WGT - 1) : (int)threadIdx.x;  // (split: either wave)
+  const int lane = (int)threadIdx.x;
   const int env = xcd_block(blockIdx.x, gridDim.x) * EPW + lane / TL;
   // a team past N recomputes env N-1 (identical values, identical stores); it never logs
   const int i = env < N ? env : N - 1;
@@ -3082,7 +3108,7 @@ __device__ __forceinline__ void step_body(const zb_model* __restrict__ mg, const
   sp.mark(0);
   for (int k = 0; k < cfg.decimation; ++k) {
     // (a compile-time `true` here lets the scheduler reshape the loop into a 36 B/lane spill)
-    substep<false, false, kTgs, kSplit, kRefresh>(m, cfg, p, target, q, opaque_true(), true, so, nullptr, nullptr, sp);
+    substep<false, false, kTgs, kRefresh>(m, cfg, p, target, q, opaque_true(), true, so, nullptr, nullptr, sp);
     sens_record(q, k, so);
     sp.mark(7);
     sp.substep_end(k);
@@ -3315,26 +3341,11 @@ __device__ __forceinline__ void step_body(const zb_model* __restrict__ mg, const
 #endif
   }
 #if ZB_STAGED_STORES
-  staged_store<ZB_STATE_DIM, ZB_OBS_DIM, ZB_S_EP_LEN>(q, xcd_block(blockIdx.x, gridDim.x) * EPW, N, st, obs, rew, term,
-                                                     trunc);
+  staged_store<ZB_STATE_DIM, ZB_OBS_DIM>(q, xcd_block(blockIdx.x, gridDim.x) * EPW, N, st, obs, rew, term, trunc);
 #endif
 #undef OUT
   sp.mark(8);
   sp.flush();
-  // Fused finalize (FinArgs::done set, opt-in): one agent-scope release add per workgroup after
-  // its stores and log atomics; the workgroup whose add comes last takes an agent-scope acquire
-  // fence and runs zb_finalize_kernel's body. Release / acquire make the hand-over correct under the
-  // HIP memory model (the release writes back this XCD's L2: the path costs more than the separate
-  // finalize launch it replaces, DESIGN.md §7, and stays off by default).
-  if (!kSplit && fa.done) {
-    unsigned prev = 0u;
-    if (lane == 0) prev = __hip_atomic_fetch_add(fa.done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    prev = __builtin_amdgcn_readfirstlane(prev);
-    if (prev == gridDim.x - 1) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      finalize_body<true>(N, st, acc, fa, 0, 0, 1, cfg, nullptr, term, trunc, reinterpret_cast<float*>(lds));
-    }
-  }
 #undef ST
 #undef CST
 }
@@ -3350,71 +3361,17 @@ __global__ __launch_bounds__(WGT, kOcc) void zb_step_kernel(const zb_model* __re
                                                           float* __restrict__ st, const float* __restrict__ act,
                                                           float* __restrict__ obs, float* __restrict__ rew,
                                                           uint8_t* __restrict__ term, uint8_t* __restrict__ trunc,
-                                                          float* __restrict__ acc, float* __restrict__ wc,
-                                                          FinArgs fa) {
+                                                          float* __restrict__ acc, float* __restrict__ wc) {
   __shared__ float4 lds[LDS4];
-  static_assert(LDS4 * 4 >= FIN_FG * ACC_STRIDE + ACC, "fused finalize scratch");
   if (kOcc == 1) asm volatile("" ::: "a255");
-  step_body<kTgs, false, kRefresh>(mg, links, cfg, N, st, act, obs, rew, term, trunc, acc, wc, fa, lds);
-}
-
-// The collision wave of zb_step_split_kernel: each substep, between the physics wave's two
-// barriers, the ground and self-collision detection of the workgroup's EPW envs (detect, from
-// the poses the physics wave's FK left in LDS) into the candidate list, then the env's contact
-// count and overflow flag into its hand-off record. Same barrier count as the physics wave
-// (2 per substep, cfg.decimation substeps), then it exits.
-__device__ __forceinline__ void collide_wave(const zb_task_cfg& cfg, float4* lds, const float4* __restrict__ links) {
-  const Q q = make_q(lds, (int)threadIdx.x & (WGT - 1), links);
-  Stamps sp;  // (diagnostic build: this wave's stamps are not recorded)
-  for (int k = 0; k < cfg.decimation; ++k) {
-    __syncthreads();
-    bool over = false;
-    const int nc = detect(cfg, q.spl().z, q, true, over, sp);
-    if (q.s == 0) {
-      q.spl().x = __int_as_float(nc);
-      q.spl().y = over ? 1.f : 0.f;
-    }
-    __syncthreads();
-  }
-}
-
-// Walking v2 step with detection on a second wave (ZB_SPLIT, N <= 4096: a launch of one wave per
-// SIMD leaves each SIMD room for a second wave): workgroup = EPW envs x {physics wave, collision
-// wave}; per substep the env's critical path is FK -> max(detection, RNEA + CRBA + Cholesky +
-// drives) -> contact rows -> PGS -> integration instead of their sum. Bit-identical to
-// zb_step_kernel (same instructions per role, same LDS contents at each hand-off).
-template <bool kTgs>
-__global__ __launch_bounds__(2 * WGT, ZB_WAVES_PER_SIMD) void zb_step_split_kernel(
-    const zb_model* __restrict__ mg, const float4* __restrict__ links, zb_task_cfg cfg, int N, float* __restrict__ st,
-    const float* __restrict__ act, float* __restrict__ obs, float* __restrict__ rew, uint8_t* __restrict__ term,
-    uint8_t* __restrict__ trunc, float* __restrict__ acc, float* __restrict__ wc, FinArgs fa) {
-  __shared__ float4 lds[LDS4S];
-  // (scalar, wave-uniform role tests: the compiler must not treat the branch as divergent and run
-  // one role's barriers in the other wave with an empty exec mask)
-  const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x) / WGT;
-  int phys_wave = fa.split_role == 1 ? 1 : 0;
-  if (fa.split_role == 2) {
-    // wave 0 asks for the physics when its (SIMD, wave slot) parity is even, so that the two
-    // waves a SIMD holds (this workgroup's and another's) tend to take different roles
-    if (w == 0 && threadIdx.x == 0) {
-      const unsigned hw = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));  // HW_REG_HW_ID
-      lds[SPL_OFF].w = (float)(((hw & 15u) + ((hw >> 4) & 3u)) & 1u);
-    }
-    __syncthreads();
-    phys_wave = __builtin_amdgcn_readfirstlane((int)lds[SPL_OFF].w);
-  }
-  if (w != phys_wave) {
-    collide_wave(cfg, lds, links);
-    return;
-  }
-  step_body<kTgs, true>(mg, links, cfg, N, st, act, obs, rew, term, trunc, acc, wc, fa, lds);
+  step_body<kTgs, kRefresh>(mg, links, cfg, N, st, act, obs, rew, term, trunc, acc, wc, lds);
 }
 
 // Test entry (zb_pair_manifold): GJK (cold start) + the face manifold of n link pairs given as
 // world-frame core hulls, one pair per quad (tests/test_gpu_selfcollision.py against the oracle's
 // zbo_pair_manifold): out [n][29] = {points, then per point {sep, n[3], x[3]}} (0 points: no contact;
 // 1 without a face manifold: the GJK contact).
-__global__ void zb_manifold_kernel(const float* __restrict__ pairs, int n, float margin, float* __restrict__ out) {
+__global__ void zb_manifold_kernel(const float* __restrict__ pairs, int n, float margin, int mode, float* __restrict__ out) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   const int pr = min(t >> 2, n - 1), j = t & 3;  // quads past n recompute pair n - 1 (no store)
   const float* c = pairs + (size_t)pr * 36 + 9 * j;
@@ -3431,7 +3388,7 @@ __global__ void zb_manifold_kernel(const float* __restrict__ pairs, int n, float
   const bool mine = (t >> 2) < n;
   int cnt = 0;
   if (hit && sc.sep > -2.f * kCoreM + 1e-7f)
-    cnt = quad_manifold(h, j, sc, margin, true, true, [&](int rank, float4 xs, const float* nn) {
+    cnt = quad_manifold(h, j, sc, margin, true, mode, [&](int rank, float4 xs, const float* nn) {
       if (mine) {
         float* p = o + 1 + 7 * rank;
         p[0] = xs.w; p[1] = nn[0]; p[2] = nn[1]; p[3] = nn[2]; p[4] = xs.x; p[5] = xs.y; p[6] = xs.z;
@@ -3569,7 +3526,7 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_substeps_kernel(con
   SensorOut so;
   Stamps sp;
   for (int k = 0; k < nsub; ++k)
-    substep<true, kLinkFriction, kTgs, false, kRefresh>(m, cfg, p, tg, q, k == nsub - 1, k > 0, so, F, tau, sp);
+    substep<true, kLinkFriction, kTgs, kRefresh>(m, cfg, p, tg, q, k == nsub - 1, k > 0, so, F, tau, sp);
   if (net_force && q.s < NL)
 #pragma unroll
     for (int a = 0; a < 3; ++a) net_force[((size_t)i * NL + q.s) * 3 + a] = F[0][a];
@@ -3710,7 +3667,7 @@ __global__ __launch_bounds__(WGT, kOcc) void zb_su_step_kernel(
   wc_load(q, wc, N, i);  // the first substep's GJK warm start
   sp.mark(0);
   for (int k = 0; k < cfg.decimation; ++k) {
-    substep<false, true, kTgs, false, kRefresh>(m, cfg, p, target, q, false, true, so, nullptr, nullptr, sp);
+    substep<false, true, kTgs, kRefresh>(m, cfg, p, target, q, false, true, so, nullptr, nullptr, sp);
     sp.mark(7);
   }
   m = opaque(m);
@@ -4968,7 +4925,6 @@ __global__ void zb_m_observe_kernel(const zb_model* __restrict__ mg, zb_task_cfg
 // next step (the reference applies the reset-event ones to the commands it resamples in the same
 // call). The manager's lin_vel_cmd_levels is exact: the reset envs' commands are
 // redrawn here when it fires.
-template <bool kFused>
 __device__ __forceinline__ void finalize_body(int N, float* __restrict__ st, float* __restrict__ acc,
                                               const FinArgs& fa, int force_full, int reset_counts, int is_step,
                                               const zb_task_cfg& cfg, float* __restrict__ obs,
@@ -4986,23 +4942,16 @@ __device__ __forceinline__ void finalize_body(int N, float* __restrict__ st, flo
   const uint64_t steps = cnt->steps + (is_step ? 1 : 0);
   // fold the accumulator slots (acc_slot): 8 groups of 8 slots x ACC_STRIDE entries, one
   // thread per (group, entry), which also clears what it read; then a shared sum of the groups.
-  // Fused (the step kernel's last workgroup): the slots were filled by agent-scope atomics of the
-  // other workgroups, so they are read and cleared by atomic exchanges (coherent across XCDs).
   constexpr int FG = FIN_FG, FS = ACC_SLOTS / FG;
   float* const acc_part = sh;                     // [FG][ACC_STRIDE]
   float* const acc_sum = sh + FG * ACC_STRIDE;    // [ACC]
   for (int x = threadIdx.x; x < FG * ACC_STRIDE; x += blockDim.x) {
     const int g = x / ACC_STRIDE, t = x % ACC_STRIDE;
     float v[FS];
-    if (kFused) {
 #pragma unroll
-      for (int k = 0; k < FS; ++k) v[k] = atomicExch(&acc[(g * FS + k) * ACC_STRIDE + t], 0.f);
-    } else {
+    for (int k = 0; k < FS; ++k) v[k] = acc[(g * FS + k) * ACC_STRIDE + t];
 #pragma unroll
-      for (int k = 0; k < FS; ++k) v[k] = acc[(g * FS + k) * ACC_STRIDE + t];
-#pragma unroll
-      for (int k = 0; k < FS; ++k) acc[(g * FS + k) * ACC_STRIDE + t] = 0.f;
-    }
+    for (int k = 0; k < FS; ++k) acc[(g * FS + k) * ACC_STRIDE + t] = 0.f;
     float sum = 0.f;
 #pragma unroll
     for (int k = 0; k < FS; ++k) sum += v[k];
@@ -5103,13 +5052,8 @@ __device__ __forceinline__ void finalize_body(int N, float* __restrict__ st, flo
   if (full && cfg.task != ZB_TASK_MANAGER_V0)  // ManagerBasedRLEnv has no full-reset draw
     for (int i = threadIdx.x; i < N; i += blockDim.x) {
       const uint64_t h = hash64(seed ^ hash64(ctr * 0x100000001B3ull + (uint64_t)i));
-      const float d = (float)(int)(h % (uint64_t)cfg.max_episode_length);
-      // (fused: an agent-scope store, like the step's own store of this row, so that no XCD's L2
-      // holds a dirty copy of it that could be written back over the draw)
-      if (kFused) __hip_atomic_store(&st[(size_t)ep_len_row * N + i], d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      else st[(size_t)ep_len_row * N + i] = d;
+      st[(size_t)ep_len_row * N + i] = (float)(int)(h % (uint64_t)cfg.max_episode_length);
     }
-  if (kFused && threadIdx.x == 0) __hip_atomic_store(fa.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __global__ void zb_finalize_kernel(int N, float* __restrict__ st, float* __restrict__ acc,
@@ -5119,25 +5063,16 @@ __global__ void zb_finalize_kernel(int N, float* __restrict__ st, float* __restr
                                    int is_step, int ep_len_row, zb_task_cfg cfg, float* __restrict__ obs,
                                    const uint8_t* __restrict__ term, const uint8_t* __restrict__ trunc) {
   __shared__ float sh[FIN_FG * ACC_STRIDE + ACC];
-  const FinArgs fa = {log_means, log_counts, user_means, user_counts, episode_s, seed, cnt, ep_len_row, nullptr};
-  finalize_body<false>(N, st, acc, fa, force_full, reset_counts, is_step, cfg, obs, term, trunc, sh);
+  const FinArgs fa = {log_means, log_counts, user_means, user_counts, episode_s, seed, cnt, ep_len_row};
+  finalize_body(N, st, acc, fa, force_full, reset_counts, is_step, cfg, obs, term, trunc, sh);
 }
 
 
 }  // namespace
 
 // =========================================================================== C ABI
-#ifndef ZB_SPLIT_DEFAULT
-#define ZB_SPLIT_DEFAULT 0
-#endif
 #ifndef ZB_OCC1_DEFAULT
 #define ZB_OCC1_DEFAULT 1
-#endif
-#ifndef ZB_SPLIT_ROLE_DEFAULT
-#define ZB_SPLIT_ROLE_DEFAULT 0
-#endif
-#ifndef ZB_FUSED_FINALIZE_DEFAULT
-#define ZB_FUSED_FINALIZE_DEFAULT 0
 #endif
 struct zb_sim {
   int device;
@@ -5159,13 +5094,7 @@ struct zb_sim {
   // optional per-launch timing of zb_step_kernel (hipEvents on the launch stream)
   int prof_max = 0, prof_n = 0;
   hipEvent_t* prof_ev = nullptr;
-  // walking v2: the step-end finalisation runs in the step kernel's last workgroup (FinArgs::done;
-  // ZB_FUSED_FINALIZE=0/1 at create overrides ZB_FUSED_FINALIZE_DEFAULT)
-  unsigned* d_done = nullptr;
-  bool fused = false;
-  bool split = false;  // walking v2: zb_step_split_kernel (ZB_SPLIT)
   bool occ1 = false;   // step kernels with one wave per SIMD (kOcc = 1; ZB_OCC1)
-  int split_role = 0;  // ZB_SPLIT_ROLE
 };
 
 static thread_local char g_err[512] = "";
@@ -5214,9 +5143,10 @@ int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_dev
   }
   if (c->decimation < 1 || c->decimation > MAXSUB || c->solver_iterations < 0 || c->solver_mode < 0 ||
       c->solver_mode > 2 || (c->solver_mode >= 1 && c->solver_iterations < 1) ||
-      (c->solver_mode == 2 && c->task != ZB_TASK_WALKING_V2 && c->task != ZB_TASK_STANDUP_V0))
+      (c->solver_mode == 2 && c->task != ZB_TASK_WALKING_V2 && c->task != ZB_TASK_STANDUP_V0) ||
+      c->self_manifold < 0 || c->self_manifold > 3)
     return set_err(-1, "zb_create: cfg (decimation 1..8, solver_iterations >= 0, solver_mode 0 / 1 / 2 with iterations "
-                       ">= 1; mode 2 for walking v2 and stand-up)",
+                       ">= 1; mode 2 for walking v2 and stand-up; self_manifold 0..3)",
                    hipSuccess);
   if (c->task != ZB_TASK_WALKING_V2 && c->task != ZB_TASK_STANDUP_V0 && c->task != ZB_TASK_WALKING_V4 &&
       c->task != ZB_TASK_MANAGER_V0)
@@ -5239,25 +5169,11 @@ int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_dev
   HIPCHK(hipMalloc(&h->d_acc, sizeof(float) * ACC_SLOTS * ACC_STRIDE), "hipMalloc acc");
   HIPCHK(hipMalloc(&h->d_cnt, sizeof(Counters)), "hipMalloc counters");
   {
-    const char* fz = getenv("ZB_FUSED_FINALIZE");
-    // only an explicit "1" / "0" overrides the default (an empty value or "false" does not enable it)
-    const int fz_on = fz && fz[0] == '1' && fz[1] == 0, fz_off = fz && fz[0] == '0' && fz[1] == 0;
-    if (c->task == ZB_TASK_WALKING_V2 && ZB_STAGED_STORES && (fz_on || (!fz_off && ZB_FUSED_FINALIZE_DEFAULT))) {
-      HIPCHK(hipMalloc(&h->d_done, sizeof(unsigned)), "hipMalloc done counter");
-      HIPCHK(hipMemset(h->d_done, 0, sizeof(unsigned)), "hipMemset done counter");
-      h->fused = true;
-    }
-  }
-  {
-    const char* sv = getenv("ZB_SPLIT");
-    const int sv_on = sv && sv[0] == '1' && sv[1] == 0, sv_off = sv && sv[0] == '0' && sv[1] == 0;
-    h->split = c->task == ZB_TASK_WALKING_V2 && !h->fused && c->solver_mode != 2 && (sv_on || (!sv_off && ZB_SPLIT_DEFAULT && num_envs <= 4096));
-    // one wave per SIMD at <= 4096 envs (<= one wave per SIMD anyway): ZB_OCC1=0/1 overrides
+    // one wave per SIMD at <= 4096 envs (<= one wave per SIMD anyway): ZB_OCC1=0/1 overrides (only
+    // an explicit "1" / "0": an empty value or "false" does not)
     const char* oc = getenv("ZB_OCC1");
     const int oc_on = oc && oc[0] == '1' && oc[1] == 0, oc_off = oc && oc[0] == '0' && oc[1] == 0;
     h->occ1 = oc_on || (!oc_off && ZB_OCC1_DEFAULT && num_envs <= 4096);
-    const char* sr = getenv("ZB_SPLIT_ROLE");
-    h->split_role = sr && (sr[0] == '1' || sr[0] == '2') && sr[1] == 0 ? sr[0] - '0' : ZB_SPLIT_ROLE_DEFAULT;
   }
   {
     Counters c0;
@@ -5493,7 +5409,6 @@ void zb_destroy(zb_handle h) {
   (void)hipFree(h->d_wc);
   (void)hipFree(h->d_acc);
   (void)hipFree(h->d_cnt);
-  if (h->d_done) (void)hipFree(h->d_done);
   (void)hipFree(h->d_log_means);
   (void)hipFree(h->d_log_counts);
   delete h;
@@ -5571,21 +5486,9 @@ int zb_step(zb_handle h, const float* actions, float* obs, float* reward, uint8_
   else if (h->task == ZB_TASK_MANAGER_V0)
     ZB_LAUNCH(zb_m_step_kernel, h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward, terminated,
               truncated, h->d_acc, h->d_cnt, h->seed, h->d_wc);
-  else {
-    const FinArgs fa = {h->d_log_means, h->d_log_counts, h->u_log_means, h->u_log_counts, log_episode_s(h),
-                        h->seed, h->d_cnt, ZB_S_EP_LEN, h->fused ? h->d_done : nullptr, h->split_role};
-    if (h->split) {
-      if (tgs)
-        zb_step_split_kernel<true><<<blocks, 2 * WGT, 0, s>>>(h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions,
-                                                             obs, reward, terminated, truncated, h->d_acc, h->d_wc, fa);
-      else
-        zb_step_split_kernel<false><<<blocks, 2 * WGT, 0, s>>>(h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions,
-                                                              obs, reward, terminated, truncated, h->d_acc, h->d_wc, fa);
-    } else {
-      ZB_LAUNCH_R(zb_step_kernel, h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward, terminated,
-                truncated, h->d_acc, h->d_wc, fa);
-    }
-  }
+  else
+    ZB_LAUNCH_R(zb_step_kernel, h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward, terminated,
+              truncated, h->d_acc, h->d_wc);
 #undef ZB_LAUNCH_R
 #undef ZB_LAUNCH
   int rc = launch_check("zb_step_kernel");
@@ -5594,7 +5497,6 @@ int zb_step(zb_handle h, const float* actions, float* obs, float* reward, uint8_
     ++h->prof_n;
   }
   if (rc) return rc;
-  if (h->task == ZB_TASK_WALKING_V2 && h->fused) return 0;  // finalised by the step kernel
   return finalize(h, s, 0, 0, 1, obs, terminated, truncated);
 }
 
@@ -5721,10 +5623,14 @@ int zb_physics_substeps(zb_handle h, const float* targets, int nsub, float* net_
   return launch_check("zb_wc_fill_kernel");
 }
 
-int zb_pair_manifold(const float* pairs, int n, float margin, float* out, void* stream) {
-  if (!pairs || !out || n < 1) return set_err(-1, "zb_pair_manifold", hipSuccess);
-  zb_manifold_kernel<<<(4 * n + 63) / 64, 64, 0, (hipStream_t)stream>>>(pairs, n, margin, out);
+int zb_pair_manifold_mode(const float* pairs, int n, float margin, int mode, float* out, void* stream) {
+  if (!pairs || !out || n < 1 || mode < 1 || mode > 3) return set_err(-1, "zb_pair_manifold", hipSuccess);
+  zb_manifold_kernel<<<(4 * n + 63) / 64, 64, 0, (hipStream_t)stream>>>(pairs, n, margin, mode, out);
   return launch_check("zb_manifold_kernel");
+}
+
+int zb_pair_manifold(const float* pairs, int n, float margin, float* out, void* stream) {
+  return zb_pair_manifold_mode(pairs, n, margin, 2, out, stream);
 }
 
 int zb_gjk_pairs(const float* pairs, const float* v0, int n, float margin, float* out, void* stream) {
