@@ -1442,8 +1442,11 @@ static void substep(const mdl_t* m, const zb_task_cfg* cfg, phys_t* s, const rea
    * velocity of the sub-iterations so far (the same integration as the substep's end), and every
    * ground contact's point (its rim candidate re-supported at that pose), separation and Jacobian
    * rows are re-evaluated there; the mass matrix and its factor stay the substep's, the rows
-   * keep mapping the root twist at the substep's P. Self contacts keep mode 1's linear advance. */
-  const int tgs = cfg->solver_mode >= 1, refresh = cfg->solver_mode == 2;
+   * keep mapping the root twist at the substep's P. Self contacts keep mode 1's linear advance;
+   * solver_mode 3 refreshes them too: each self contact's two body-fixed anchors (placed so that
+   * n.(pa - pb) is the detected separation) are carried to the advanced pose, the separation is
+   * n.(pa' - pb') along the substep's normal and the rows are re-evaluated at their midpoint. */
+  const int tgs = cfg->solver_mode >= 1, refresh = cfg->solver_mode >= 2, refresh_self = cfg->solver_mode == 3;
   real wv[3]; /* omega x v_P at the substep start (the classical correction of the root origin) */
   v3_cross(s->root_angvel, s->root_linvel, wv);
   const real h = dt / (real)cfg->solver_iterations;
@@ -1451,6 +1454,7 @@ static void substep(const mdl_t* m, const zb_task_cfg* cfg, phys_t* s, const rea
   for (int a = 0; a < NV; ++a) wsum[a] = 0;
   int broken[NC_MAX];
   real dirs[NC_MAX][3][3];
+  real anc[NC_MAX][2][3]; /* solver_mode 3: self contacts' anchors in their bodies' frames */
   int planted = 0;
   for (int c = 0; c < nc; ++c) {
     contact_t* ct = &CL.c[c];
@@ -1484,6 +1488,17 @@ static void substep(const mdl_t* m, const zb_task_cfg* cfg, phys_t* s, const rea
     for (int a = 0; a < NV; ++a) { c01[c] += Y[c][1][a] * Y[c][0][a]; c02[c] += Y[c][2][a] * Y[c][0][a]; }
     sepc[c] = ct->sep;
     vmin[c] = contact_bias(cfg, m, sepc[c], tgs ? h : dt, dt);
+    if (refresh_self && ct->lb >= 0) {
+      /* self contact: body-fixed anchors pa = x + n sep / 2 on A, pb = x - n sep / 2 on B (so
+       * n.(pa - pb) = sep at this pose), kept in the bodies' frames for the refresh */
+      const int bs[2] = {m->link_body[ct->la], m->link_body[ct->lb]};
+      for (int e = 0; e < 2; ++e) {
+        const real* R = k.R[bs[e]];
+        real d[3];
+        for (int a = 0; a < 3; ++a) d[a] = ct->x[a] + (e ? -(real)0.5 : (real)0.5) * ct->sep * ct->n[a] - k.p[bs[e]][a];
+        for (int a = 0; a < 3; ++a) anc[c][e][a] = R[a] * d[0] + R[3 + a] * d[1] + R[6 + a] * d[2];
+      }
+    }
   }
   /* Gauss-Seidel over contacts; the three row dots of a contact use the same w, the normal
    * update enters the tangent velocities through the cross terms c01 = Y1.Y0, c02 = Y2.Y0
@@ -1513,13 +1528,34 @@ static void substep(const mdl_t* m, const zb_task_cfg* cfg, phys_t* s, const rea
         for (int a = 0; a < 3; ++a) k2.org[j][a] += dP[a];
       for (int c = 0; c < nc; ++c) {
         const contact_t* ct = &CL.c[c];
-        if (ct->lb >= 0) continue;
+        if (ct->lb >= 0 && !refresh_self) continue;
         real x[3];
-        ground_rim_point(m, &k2, ct->la, ct->rim >> 2, ct->rim & 3, x);
-        sepc[c] = s->root_pos[2] + x[2];
+        if (ct->lb < 0) {
+          ground_rim_point(m, &k2, ct->la, ct->rim >> 2, ct->rim & 3, x);
+          sepc[c] = s->root_pos[2] + x[2];
+        } else {
+          /* the anchors at the advanced pose: separation n.(pa' - pb') along the substep's normal,
+           * the rows at their midpoint */
+          real pe[2][3];
+          const int bs[2] = {m->link_body[ct->la], m->link_body[ct->lb]};
+          for (int e = 0; e < 2; ++e) {
+            m3_v(k2.R[bs[e]], anc[c][e], pe[e]);
+            for (int a = 0; a < 3; ++a) pe[e][a] += k2.p[bs[e]][a];
+          }
+          sepc[c] = 0;
+          for (int a = 0; a < 3; ++a) {
+            sepc[c] += ct->n[a] * (pe[0][a] - pe[1][a]);
+            x[a] = (real)0.5 * (pe[0][a] + pe[1][a]);
+          }
+        }
         for (int r = 0; r < 3; ++r) {
           real J[NV];
           jac_row(&k2, m->link_body[ct->la], x, dirs[c][r], J);
+          if (ct->lb >= 0) {
+            real Jb[NV];
+            jac_row(&k2, m->link_body[ct->lb], x, dirs[c][r], Jb);
+            for (int a = 0; a < NV; ++a) J[a] -= Jb[a];
+          }
           fwd_sub(L, J, Y[c][r]);
           real yy = 0;
           for (int a = 0; a < NV; ++a) yy += Y[c][r][a] * Y[c][r][a];

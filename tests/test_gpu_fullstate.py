@@ -404,12 +404,13 @@ def test_full_state_deep_overlap(gpu):
     assert nbad <= 0.05 * n
 
 
-@pytest.mark.parametrize("mode", [1, 2], ids=["tgs", "tgs-refresh"])
+@pytest.mark.parametrize("mode", [1, 2, 3], ids=["tgs", "tgs-refresh", "tgs-refresh-self"])
 @pytest.mark.parametrize("task", ["v2", "standup"])
 def test_full_state_tgs(gpu, task, mode):
     """The TGS-style contact solve (zb_task_cfg.solver_mode 1: per-sub-iteration re-linearised
     biases, pose from the mean sub-iteration velocity; mode 2 also re-evaluates every ground
-    contact's point, separation and Jacobian rows at each sub-iteration's pose): one step from random
+    contact's point, separation and Jacobian rows at each sub-iteration's pose, mode 3 every self
+    contact's too): one step from random
     full states and 20 zero-action steps from standing, every row under the same explained-outlier
     rule."""
     with solver_mode(mode):
@@ -517,3 +518,21 @@ def _manifold_step(task, kind, n, seed, st, which, pc, g, torch):
     nbad = _check(task, f"one step from constructed {kind}-manifold folds", n, seed, st, [a], g_out,
                   g.get_state().cpu().numpy(), torch)
     assert nbad <= 0.05 * n
+
+
+@pytest.mark.parametrize("kind", ["face", "rim"])
+@pytest.mark.parametrize("task", ["v2", "standup"])
+def test_full_state_self_refresh(gpu, task, kind):
+    """The TGS refresh of the self contacts (zb_task_cfg.solver_mode 3: each self contact's two
+    body-fixed anchors carried to every sub-iteration's pose, the separation and rows re-evaluated
+    there) on 512 constructed gentle folds per case (cap on cap / side by side, as in
+    test_full_state_face_manifold): one step on both sides under the full-state rule."""
+    from fullstate import constructed_states, self_manifold, solver_mode
+    seed, n = 47, 512
+    with self_manifold(2), solver_mode(3):
+        st, which = constructed_states(task, kind, n, seed=616)
+        g, o, cfg, torch = _sims(task, n, seed)
+        assert cfg.solver_mode == 3 and cfg.self_manifold == 2
+        o.set_state(st)
+        pc = o.pair_classes()
+        _manifold_step(task, f"{kind} (self refresh)", n, seed, st, which, pc, g, torch)

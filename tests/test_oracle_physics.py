@@ -242,3 +242,40 @@ def test_tgs_refresh_touches_ground_contacts_only():
     assert d.max() > 0  # the refresh acts on ground contacts
     v = S["JOINT_VEL"]
     assert d[v:v + 6].max() < 0.5, d[v:v + 6].max()
+
+
+def test_tgs_self_refresh_touches_self_contacts_only():
+    """solver_mode 3 adds the refresh of the self contacts (body-fixed anchors carried to each
+    sub-iteration's pose): on ground-only states it steps bit-identically to mode 2, on constructed
+    self-contact folds (airborne, tests/fullstate.constructed_states) it differs from mode 2; with a
+    single sub-iteration (no refresh point) modes 2 and 3 agree there too."""
+    import sys, os
+    sys.path.insert(0, os.path.dirname(__file__))
+    from fullstate import constructed_states, self_manifold, task_cfg
+    from oracle.pyoracle import OracleSim
+    n = 32
+    ground = perturbed_states(n, seed=12)
+    outs = []
+    for mode in (2, 3):  # (self collision off: the ground contacts alone)
+        s = _sim(n, _tgs_cfg(mode, solver_iterations=4, enable_self_collision=False))
+        s.set_state(ground)
+        s.physics_substeps(ground[S["JOINT_POS"]:S["JOINT_POS"] + 6].T.copy(), 4)
+        outs.append(s.get_state())
+    np.testing.assert_array_equal(outs[0], outs[1])
+    with self_manifold(2):
+        st, _ = constructed_states("v2", "face", 64, seed=3)
+    a = np.random.default_rng(608).normal(size=(64, 6)).astype(np.float32)
+    res = {}
+    for mode, iters in ((2, 1), (3, 1), (2, 4), (3, 4)):
+        cfg = task_cfg("v2")
+        cfg.self_manifold, cfg.solver_mode, cfg.solver_iterations = 2, mode, iters
+        o = OracleSim(64, cfg, seed=1)
+        o.set_state(st)
+        o.contact_activity()
+        o.step(a)
+        res[mode, iters] = (o.get_state(), o.contact_activity()[:, 1] > 0)
+    np.testing.assert_array_equal(res[2, 1][0], res[3, 1][0])
+    diff = (res[3, 4][0] != res[2, 4][0]).any(axis=0)
+    loaded = res[2, 4][1] | res[3, 4][1]
+    assert loaded.sum() >= 10 and (diff & loaded).sum() >= 0.9 * loaded.sum()  # the refresh acts on the loaded ones
+    assert np.isfinite(res[3, 4][0]).all()

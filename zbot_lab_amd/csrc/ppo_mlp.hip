@@ -9,7 +9,8 @@
 //             Gaussian log-prob / KL / clipped surrogate and its gradient, actor backward dX; then
 //             the critic forward, clipped value loss and backward. Every layer's input X_l and
 //             pre-activation gradient dZ_l go to HBM for the weight gradients.
-//   k_wgrad   dW_l = dZ_l^T X_l and db_l = sum dZ_l, one wave per 32x32 weight tile and row split
+//   k_wgrad   dW_l = dZ_l^T X_l and db_l = sum dZ_l, one wave per 32-row output tile (against every
+//             k-tile of the layer) and row split
 //             (split-K over the minibatch rows), partial tiles to the workspace
 //   k_reduce  partial tiles -> every parameter's .grad, the std gradient, the minibatch stats
 //
@@ -17,7 +18,7 @@
 // Exact fp32 throughout (the MFMA is a k-ordered fmaf chain); results differ from torch's only by
 // summation order. MI355X mapping: the weights (<= 450 KB per net) stay L2-resident and stream as
 // the MFMA B operand; activations of a row tile live in LDS (row stride P + 4 floats: conflict-free
-// ds_read_b128); every workgroup holds one row tile and four waves split a layer's output columns.
+// ds_read_b128); every workgroup holds one row tile and its waves split a layer's output columns.
 #include <hip/hip_runtime.h>
 
 #include <math.h>
@@ -34,6 +35,10 @@ constexpr int TR = 32;            // rows per tile (the MFMA's M)
 constexpr int MAXL = ZBP_MAX_LAYERS;
 constexpr int PART = 32 * 32 + 32;  // one weight-gradient partial tile + its bias column
 constexpr int NSTAT = 16;           // per-row-tile partial sums (surrogate, value, kl, std grads)
+// k_rows workgroup: 8 waves on one 32-row tile (a layer's output tiles dealt over them): with the
+// C5 nets' 97 KB of activations one workgroup fits a CU, so two waves share each SIMD and cover each
+// other's LDS / L2 waits
+constexpr int ROW_THREADS = 512;
 
 thread_local char g_err[256] = "";
 int fail(int code, const char* what) {
@@ -58,6 +63,7 @@ struct Layout {
   int64_t stats;  // [tiles][NSTAT] per-row-tile partial sums
   int64_t part;   // [splits][wtiles][PART] weight-gradient partials
   int wtiles, tile0[2 * MAXL + 1];  // weight tiles of (net, layer) in order, prefix counts
+  int ngroups, grp0[2 * MAXL + 1];  // k_wgrad workgroups (<= 4 output tiles each) of (net, layer), prefix counts
   int splits;
   int64_t scratch;  // [64] per-block gradient sums of squares (zbp_optimizer_step)
   int64_t total;
@@ -86,11 +92,20 @@ Layout make_layout(const zbp_net* a, const zbp_net* c, int B) {
   }
   lo.tile0[2 * MAXL] = t;
   lo.wtiles = t;
+  // weight-gradient workgroups: per (net, layer) groups of up to 4 output tiles (one wave each)
+  int g = 0;
+  for (int k = 0; k < 2; ++k)
+    for (int l = 0; l < MAXL; ++l) {
+      lo.grp0[k * MAXL + l] = g;
+      if (l < lo.n[k].L) g += (lo.n[k].p[l + 1] / 32 + 3) / 4;
+    }
+  lo.grp0[2 * MAXL] = g;
+  lo.ngroups = g;
   lo.stats = take((int64_t)(B / TR) * NSTAT);
-  // row splits of the weight gradients (one workgroup of 4 waves per tile and split): ~2 workgroups
-  // per CU, each wave >= 128 rows, a multiple of 16 (k_wgrad's loop over pairs of row octets)
+  // row splits of the weight gradients: ~3 waves per SIMD (k_wgrad), each split >= 256 rows, a
+  // multiple of 16 (k_wgrad's loop over pairs of row octets)
   int s = 1;
-  while (s < 64 && (int64_t)t * s * 2 <= 1024 && B / (s * 2 * 4) >= 128 && B % (16 * 4 * s * 2) == 0) s *= 2;
+  while (s < 256 && (int64_t)g * 4 * s * 2 <= 3 * 1024 && B / (s * 2) >= 256 && B % (16 * s * 2) == 0) s *= 2;
   lo.splits = s;
   lo.part = take((int64_t)s * t * PART);
   lo.scratch = take(64);
@@ -191,14 +206,14 @@ struct RowArgs {
 // B rows) for the weight gradients; the rollout's forward (k_act) keeps them in LDS only.
 template <bool kStore>
 __device__ void net_forward_t(const NetW& w, float* ws, int B, const int* lds_x, int lds_out, float* lds, int row0) {
-  const int wave = threadIdx.x >> 6, h = (threadIdx.x & 63) >> 5;
+  const int wave = threadIdx.x >> 6, h = (threadIdx.x & 63) >> 5, nw = blockDim.x >> 6;
   for (int l = 0; l < w.L; ++l) {
     const int P0 = w.p[l], P1 = w.p[l + 1];
     const bool last = l == w.L - 1;
     const float* xs = lds + lds_x[l];
     const float* wp = ws + w.wp[l];
     const float* bp = ws + w.bp[l];
-    for (int t = wave; t < P1 / 32; t += 4) {
+    for (int t = wave; t < P1 / 32; t += nw) {
       const f32x16 acc = tile_mma(xs, P0 + 4, wp, P0, P0, 32 * t);
       const int n = 32 * t + acc_col();
       const float bias = bp[n];
@@ -230,13 +245,13 @@ __device__ void net_forward(const RowArgs& A, const NetW& w, float* lds, int row
 
 // backward through one net from dZ of the output layer (lds_dz, [32][p(L) + 4])
 __device__ void net_backward(const RowArgs& A, const NetW& w, float* lds, int row0) {
-  const int wave = threadIdx.x >> 6, h = (threadIdx.x & 63) >> 5;
+  const int wave = threadIdx.x >> 6, h = (threadIdx.x & 63) >> 5, nw = blockDim.x >> 6;
   for (int l = w.L - 1; l >= 1; --l) {
     const int P0 = w.p[l], P1 = w.p[l + 1];
     const float* dz = lds + (l == w.L - 1 ? A.lds_dz : A.lds_x[l + 1]);
     float* xs = lds + A.lds_x[l];  // X_l, overwritten by dZ_{l-1}
     const float* wt = A.ws + w.wt[l];
-    for (int t = wave; t < P0 / 32; t += 4) {
+    for (int t = wave; t < P0 / 32; t += nw) {
       const f32x16 acc = tile_mma(dz, P1 + 4, wt, P1, P1, 32 * t);
       const int k = 32 * t + acc_col();
 #pragma unroll
@@ -275,7 +290,7 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
-__global__ __launch_bounds__(256) void k_rows(RowArgs A) {
+__global__ __launch_bounds__(ROW_THREADS) void k_rows(RowArgs A) {
   extern __shared__ float lds[];
   const int row0 = blockIdx.x * TR;
   const int tid = threadIdx.x;
@@ -391,48 +406,69 @@ __global__ __launch_bounds__(256) void k_rows(RowArgs A) {
 // ------------------------------------------------------------------------------- k_wgrad
 struct WgradArgs {
   NetW n[2];
-  int tile0[2 * MAXL + 1];
-  int wtiles, splits, batch;
+  int tile0[2 * MAXL + 1], grp0[2 * MAXL + 1];
+  int wtiles, ngroups, splits, batch;
   float* ws;
   int64_t part;
 };
-// One workgroup = one 32x32 tile (n0, k0) of dW_l = dZ_l^T X_l (+ db_l for k0 = 0) over the rows of
-// one split; its four waves take a quarter of the rows each and are summed in LDS. A[n][r] =
-// dZ_l[n0 + n][r], B[r][k] = X_l[k0 + k][r] (feature-major, float4 quads of rows: lane half h takes
-// rows 8 j + 4 h .. 8 j + 4 h + 3, one MFMA each).
-__global__ __launch_bounds__(256) void k_wgrad(WgradArgs A) {
-  __shared__ float red[4][PART];
-  const int tile = blockIdx.x % A.wtiles, split = blockIdx.x / A.wtiles;
+// dW_l = dZ_l^T X_l and db_l = sum dZ_l over the rows of one split. One workgroup = up to four 32-row
+// output tiles of one layer (n-tiles, one per wave); each wave accumulates its n-tile against every
+// k-tile of the layer (<= 8 accumulators), so the dZ rows of a tile are read once per split and the
+// X rows once per group of four n-tiles (the waves of a workgroup read the same X lines: L1 / L2
+// hits) -- instead of once per 32x32 tile. A[n][r] = dZ_l[n0 + n][r], B[r][k] = X_l[k0 + k][r]
+// (feature-major, float4 quads of rows: lane half h takes rows 8 j + 4 h .. 8 j + 4 h + 3, one MFMA
+// each); the next row octet's quads are loaded while the current one's MFMAs issue. Partial tiles
+// (and the bias column of the k0 = 0 tile) go to the workspace in k_reduce's layout.
+__global__ __launch_bounds__(256, 2) void k_wgrad(WgradArgs A) {
+  const int grp = blockIdx.x % A.ngroups, split = blockIdx.x / A.ngroups;
   int nl = 0;
-  while (nl + 1 < 2 * MAXL && A.tile0[nl + 1] <= tile) ++nl;
+  while (nl + 1 < 2 * MAXL && A.grp0[nl + 1] <= grp) ++nl;
   const NetW& w = A.n[nl / MAXL];
   const int l = nl % MAXL;
-  const int P0 = w.p[l];
-  const int t = tile - A.tile0[nl], kt = P0 / 32;
-  const int n0 = 32 * (t / kt), k0 = 32 * (t % kt);
+  const int Tk = w.p[l] / 32, Tn = w.p[l + 1] / 32;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
-  const int rows = A.batch / (A.splits * 4), r0 = (split * 4 + wave) * rows;
-  const float4* dz = reinterpret_cast<const float4*>(A.ws + w.dz[l] + (int64_t)(n0 + c) * A.batch + r0 + 4 * h);
-  const float4* x = reinterpret_cast<const float4*>(A.ws + w.x[l] + (int64_t)(k0 + c) * A.batch + r0 + 4 * h);
-  const int nj = rows / 8;  // float4 steps (row octets)
-  f32x16 acc = {};
-  float bsum = 0.f;
-  float4 a0 = dz[0], a1 = dz[2], b0 = x[0], b1 = x[2];
-  for (int j = 0; j < nj; j += 2) {
-    const float4 u0 = a0, u1 = a1, v0 = b0, v1 = b1;
-    if (j + 2 < nj) { a0 = dz[2 * j + 4]; a1 = dz[2 * j + 6]; b0 = x[2 * j + 4]; b1 = x[2 * j + 6]; }
-    acc = mfma(u0.x, v0.x, acc); acc = mfma(u0.y, v0.y, acc); acc = mfma(u0.z, v0.z, acc); acc = mfma(u0.w, v0.w, acc);
-    acc = mfma(u1.x, v1.x, acc); acc = mfma(u1.y, v1.y, acc); acc = mfma(u1.z, v1.z, acc); acc = mfma(u1.w, v1.w, acc);
-    bsum += ((u0.x + u0.y) + (u0.z + u0.w)) + ((u1.x + u1.y) + (u1.z + u1.w));
-  }
+  const int nt = 4 * (grp - A.grp0[nl]) + wave;
+  if (nt >= Tn) return;  // (no barrier below)
+  const int rows = A.batch / A.splits, r0 = split * rows;
+  const float4* dz = reinterpret_cast<const float4*>(A.ws + w.dz[l] + (int64_t)(32 * nt + c) * A.batch + r0 + 4 * h);
+  const float* xb = A.ws + w.x[l] + (int64_t)c * A.batch + r0 + 4 * h;
+  const int64_t xk = (int64_t)32 * A.batch;  // k-tile stride of X (floats)
+  f32x16 acc[8];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) red[wave][acc_row(r) * 32 + acc_col()] = acc[r];  // [n][k]
+  for (int k = 0; k < 8; ++k) acc[k] = f32x16{};
+  float bsum = 0.f;
+  const int nj = rows / 8;  // row octets
+  float4 a = dz[0], b[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) b[k] = k < Tk ? *reinterpret_cast<const float4*>(xb + k * xk) : float4{};
+  for (int j = 0; j < nj; ++j) {
+    const float4 u = a;
+    float4 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = b[k];
+    if (j + 1 < nj) {
+      a = dz[2 * j + 2];
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (k < Tk) b[k] = *reinterpret_cast<const float4*>(xb + k * xk + 8 * (j + 1));
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (k < Tk) {
+        acc[k] = mfma(u.x, v[k].x, acc[k]); acc[k] = mfma(u.y, v[k].y, acc[k]);
+        acc[k] = mfma(u.z, v[k].z, acc[k]); acc[k] = mfma(u.w, v[k].w, acc[k]);
+      }
+    bsum += (u.x + u.y) + (u.z + u.w);
+  }
   bsum += __shfl_xor(bsum, 32);
-  if (h == 0) red[wave][1024 + c] = bsum;
-  __syncthreads();
-  float* out = A.ws + A.part + ((int64_t)split * A.wtiles + tile) * PART;
-  for (int e = threadIdx.x; e < PART; e += blockDim.x)
-    out[e] = (red[0][e] + red[1][e]) + (red[2][e] + red[3][e]);
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+    if (k < Tk) {
+      float* out = A.ws + A.part + ((int64_t)split * A.wtiles + A.tile0[nl] + nt * Tk + k) * PART;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) out[acc_row(r) * 32 + acc_col()] = acc[k][r];  // [n][k]
+      if (k == 0 && h == 0) out[1024 + c] = bsum;
+    }
 }
 
 // ------------------------------------------------------------------------------- k_reduce
@@ -817,19 +853,21 @@ int zbp_minibatch(const zbp_net* actor, const zbp_net* critic, const float* std_
     if (e != hipSuccess) return hip_fail(e, "hipFuncSetAttribute k_rows");
     lds_set = true;
   }
-  k_rows<<<B / TR, 256, lds, s>>>(R);
+  k_rows<<<B / TR, ROW_THREADS, lds, s>>>(R);
   if (int rc = launch_check("k_rows")) return rc;
 
   WgradArgs W{};
   W.n[0] = lo.n[0];
   W.n[1] = lo.n[1];
   for (int i = 0; i <= 2 * MAXL; ++i) W.tile0[i] = lo.tile0[i];
+  for (int i = 0; i <= 2 * MAXL; ++i) W.grp0[i] = lo.grp0[i];
   W.wtiles = lo.wtiles;
+  W.ngroups = lo.ngroups;
   W.splits = lo.splits;
   W.batch = B;
   W.ws = ws;
   W.part = lo.part;
-  k_wgrad<<<lo.wtiles * lo.splits, 256, 0, s>>>(W);
+  k_wgrad<<<lo.ngroups * lo.splits, 256, 0, s>>>(W);
   if (int rc = launch_check("k_wgrad")) return rc;
 
   ReduceArgs D{};

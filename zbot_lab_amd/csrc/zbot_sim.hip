@@ -2138,17 +2138,17 @@ __device__ __forceinline__ void advance_pose(Phys& s, const float ua[NV], const 
   }
 }
 
-// TGS per-position-iteration refresh of the ground contacts (solver_mode 2; oracle substep,
+// TGS per-position-iteration refresh of the ground contacts (solver_modes 2, 3; oracle substep,
 // `refresh`): the pose after T = it h with the mean velocity of the sub-iterations so far
 // (wm = this lane's coordinate of the mean w; the same integration as the substep's end), FK
 // there, and lane c re-evaluates its ground contact: the rim candidate re-supported at that pose,
 // the separation, the three Jacobian rows (the root columns still at the substep's P, the mass
 // matrix factor the substep's), the effective masses, cross terms and bias. Self contacts keep the
-// linear advance. The LDS pose records hold the refreshed pose afterwards (nothing later in the
+// linear advance in mode 2 and are refreshed in mode 3 (below). The LDS pose records hold the refreshed pose afterwards (nothing later in the
 // substep reads them; the next substep's FK rewrites them).
-__device__ __forceinline__ void refresh_ground(const zb_task_cfg& cfg, MP m, const Phys& s, const Q& q, const float L[NT],
-                                            const float Li[NV], float wm, float T, float hsub, float dt, int nc,
-                                            int rim_own, int gl_own, float& sep_own) {
+__device__ __forceinline__ void refresh_contacts(const zb_task_cfg& cfg, MP m, const Phys& s, const Q& q, const float L[NT],
+                                              const float Li[NV], float wm, float T, float hsub, float dt, int nc,
+                                              int rim_own, int gl_own, const float anc[6], float& sep_own) {
   float w[NV], um[NV];
   w[0] = tb<own_lane(0)>(wm); w[1] = tb<own_lane(1)>(wm); w[2] = tb<own_lane(2)>(wm);
   w[3] = tb<own_lane(3)>(wm); w[4] = tb<own_lane(4)>(wm); w[5] = tb<own_lane(5)>(wm);
@@ -2163,25 +2163,48 @@ __device__ __forceinline__ void refresh_ground(const zb_task_cfg& cfg, MP m, con
   wave_sync();
   fk_team_pose(p2, q);
   wave_sync();
-  if (q.s < nc && rim_own >= 0) {
+  // self contacts (solver_mode 3): lane c's body-fixed anchors anc (pa on A, pb on B, placed at the
+  // substep's pose so that n.(pa - pb) is the detected separation) carried to the advanced pose; the
+  // separation n.(pa' - pb') along the substep's normal, the rows at the anchors' midpoint
+  const bool self_ref = cfg.solver_mode == 3 && rim_own < 0;
+  if (q.s < nc && (rim_own >= 0 || self_ref)) {
     const int c = q.s;
-    float x[3];
-    ground_rim_point(q, gl_own, rim_own >> 2, rim_own & 3, x);
-    const float sep = p2.pos[2] + x[2];
+    const float4 fr = q.frc(c);  // the substep's normal and code
+    const int code = (int)fr.w;
+    const int lb = (code & 15) - 1;
+    const bool gnd = rim_own >= 0;
+    const int ba = link_body(gnd ? gl_own : code >> 4), bb = gnd ? -1 : link_body(lb);
+    float x[3], sep, n[3];
+    if (gnd) {
+      ground_rim_point(q, gl_own, rim_own >> 2, rim_own & 3, x);
+      sep = p2.pos[2] + x[2];
+      n[0] = 0.f; n[1] = 0.f; n[2] = 1.f;
+    } else {
+      float R[9], pA[3], pB[3], pa[3], pb[3];
+      read_frame(q, ba, R, pA);
+      mv3(R, anc, pa);
+      read_frame(q, bb, R, pB);
+      mv3(R, anc + 3, pb);
+#pragma unroll
+      for (int a = 0; a < 3; ++a) { pa[a] += pA[a]; pb[a] += pB[a]; }
+      n[0] = fr.x; n[1] = fr.y; n[2] = fr.z;
+      sep = n[0] * (pa[0] - pb[0]) + n[1] * (pa[1] - pb[1]) + n[2] * (pa[2] - pb[2]);
+#pragma unroll
+      for (int a = 0; a < 3; ++a) x[a] = 0.5f * (pa[a] + pb[a]);
+    }
+    const float root = gnd ? 1.f : 0.f;  // self contacts: the root terms cancel
     const float xr[3] = {x[0] + (p2.pos[0] - s.pos[0]), x[1] + (p2.pos[1] - s.pos[1]), x[2] + (p2.pos[2] - s.pos[2])};
     float S[ND][6], org[ND][3];
     read_joints(q, S, org);
-    const int ba = link_body(gl_own);
     float cj[ND][3];
 #pragma unroll
     for (int j = 0; j < ND; ++j) {
       const float xo[3] = {x[0] - org[j][0], x[1] - org[j][1], x[2] - org[j][2]};
       float c3[3];
       cross3(S[j], xo, c3);
-      const float sg = j < ba ? 1.f : 0.f;
+      const float sg = (j < ba ? 1.f : 0.f) - (j < bb ? 1.f : 0.f);
       cj[j][0] = sg * c3[0]; cj[j][1] = sg * c3[1]; cj[j][2] = sg * c3[2];
     }
-    const float n[3] = {0.f, 0.f, 1.f};
     float t1[3], t2[3];
     tangents(n, t1, t2);
     float invm[3], Y[3][NV];
@@ -2192,8 +2215,8 @@ __device__ __forceinline__ void refresh_ground(const zb_task_cfg& cfg, MP m, con
       for (int a = 0; a < 3; ++a) d[a] = r == 0 ? n[a] : (r == 1 ? t1[a] : t2[a]);
       float J[NV], xd[3];
       cross3(xr, d, xd);
-      J[0] = xd[0]; J[1] = xd[1]; J[2] = xd[2];
-      J[3] = d[0]; J[4] = d[1]; J[5] = d[2];
+      J[0] = root * xd[0]; J[1] = root * xd[1]; J[2] = root * xd[2];
+      J[3] = root * d[0]; J[4] = root * d[1]; J[5] = root * d[2];
 #pragma unroll
       for (int j = 0; j < ND; ++j) J[6 + j] = dot3(cj[j], d);
       fwd_sub(L, Li, J, Y[r]);
@@ -2212,8 +2235,8 @@ __device__ __forceinline__ void refresh_ground(const zb_task_cfg& cfg, MP m, con
 // ------------------------------------------------------------------------- one substep
 // kLinkFriction: per-contact Coulomb coefficient from the per-link table q.fric (standup DR);
 // otherwise cfg.friction everywhere.
-// kRefresh (zb_task_cfg.solver_mode 2, with kTgs): before every sub-iteration after the first the
-// ground contacts are re-evaluated at the pose the sub-iterations so far reached (see the sweeps).
+// kRefresh (zb_task_cfg.solver_mode 2 / 3, with kTgs): before every sub-iteration after the first the
+// ground contacts (mode 3: and the self contacts) are re-evaluated at the pose the sub-iterations so far reached (see the sweeps).
 template <bool kDebugForces, bool kLinkFriction, bool kTgs, bool kRefresh = false>
 __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
                                         const float target[ND], const Q& q, bool last, bool warm, SensorOut& so,
@@ -2420,6 +2443,7 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
   const float hsub = dt / (float)cfg.solver_iterations;
   float sep_own = 0.f;
   int rim_own = -1, gl_own = 0;  // kRefresh: slot q.s's ground link and rim candidate (4 ci + r)
+  float anc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // kRefresh, solver_mode 3: slot q.s's self-contact anchors
   if (q.s < nc) {
     const int c = q.s;
     const int pos = over ? q.map(c) : c;
@@ -2446,6 +2470,18 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
         ground_rim_point(q, gl_own, k >> 2, k & 3, xc);
         const float d2 = (xc[0] - x[0]) * (xc[0] - x[0]) + (xc[1] - x[1]) * (xc[1] - x[1]) + (xc[2] - x[2]) * (xc[2] - x[2]);
         if (d2 < best) { best = d2; rim_own = k; }
+      }
+    }
+    if (kRefresh && lb >= 0 && cfg.solver_mode == 3) {
+      // the self contact's body-fixed anchors x +- n sep / 2 on A / B (oracle substep, `anc`)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        float R[9], p[3];
+        read_frame(q, e ? bb : ba, R, p);
+        const float hs = e ? -0.5f * sep : 0.5f * sep;
+        const float d[3] = {x[0] + hs * n[0] - p[0], x[1] + hs * n[1] - p[1], x[2] + hs * n[2] - p[2]};
+#pragma unroll
+        for (int a = 0; a < 3; ++a) anc[3 * e + a] = R[a] * d[0] + R[3 + a] * d[1] + R[6 + a] * d[2];
       }
     }
     // per-joint lever vectors a_j x (x - o_j), signed by which side of the contact the joint is on
@@ -2535,8 +2571,8 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
           q.aux(q.s, 0) = make_float4(a0.x, a0.y, a0.z, contact_bias(cfg, m, sep_own, hsub, dt) * a0.x);
         }
         wave_sync();
-        if (kRefresh) refresh_ground(cfg, m, s, q, L, Li, wsum / (float)it, (float)it * hsub, hsub, dt, nc, rim_own,
-                                     gl_own, sep_own);
+        if (kRefresh) refresh_contacts(cfg, m, s, q, L, Li, wsum / (float)it, (float)it * hsub, hsub, dt, nc, rim_own,
+                                       gl_own, anc, sep_own);
       }
       float4 G = q.yg(yl, 0), X = q.aux(0, 0), Z = q.aux(0, 1), La = q.lam(0);
 #pragma unroll
@@ -5142,11 +5178,11 @@ int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_dev
     if (np != m->num_self_pairs) return set_err(-1, "zb_create: self-collision pair count", hipSuccess);
   }
   if (c->decimation < 1 || c->decimation > MAXSUB || c->solver_iterations < 0 || c->solver_mode < 0 ||
-      c->solver_mode > 2 || (c->solver_mode >= 1 && c->solver_iterations < 1) ||
-      (c->solver_mode == 2 && c->task != ZB_TASK_WALKING_V2 && c->task != ZB_TASK_STANDUP_V0) ||
+      c->solver_mode > 3 || (c->solver_mode >= 1 && c->solver_iterations < 1) ||
+      (c->solver_mode >= 2 && c->task != ZB_TASK_WALKING_V2 && c->task != ZB_TASK_STANDUP_V0) ||
       c->self_manifold < 0 || c->self_manifold > 3)
-    return set_err(-1, "zb_create: cfg (decimation 1..8, solver_iterations >= 0, solver_mode 0 / 1 / 2 with iterations "
-                       ">= 1; mode 2 for walking v2 and stand-up; self_manifold 0..3)",
+    return set_err(-1, "zb_create: cfg (decimation 1..8, solver_iterations >= 0, solver_mode 0..3, iterations "
+                       ">= 1 from mode 1; modes 2, 3 for walking v2 and stand-up; self_manifold 0..3)",
                    hipSuccess);
   if (c->task != ZB_TASK_WALKING_V2 && c->task != ZB_TASK_STANDUP_V0 && c->task != ZB_TASK_WALKING_V4 &&
       c->task != ZB_TASK_MANAGER_V0)
@@ -5469,12 +5505,12 @@ int zb_step(zb_handle h, const float* actions, float* obs, float* reward, uint8_
   const int blocks = (h->n + EPW - 1) / EPW;
   const bool prof = h->prof_n < h->prof_max;
   if (prof) HIPCHK(hipEventRecord(h->prof_ev[2 * h->prof_n], s), "hipEventRecord");
-  const bool tgs = h->cfg.solver_mode >= 1, refresh = h->cfg.solver_mode == 2;
+  const bool tgs = h->cfg.solver_mode >= 1, refresh = h->cfg.solver_mode >= 2;
   const bool one = h->occ1;
 #define ZB_LAUNCH(K, ...)                                                                          \
   (tgs ? (one ? K<true, 1><<<blocks, WGT, 0, s>>>(__VA_ARGS__) : K<true, 2><<<blocks, WGT, 0, s>>>(__VA_ARGS__)) \
        : (one ? K<false, 1><<<blocks, WGT, 0, s>>>(__VA_ARGS__) : K<false, 2><<<blocks, WGT, 0, s>>>(__VA_ARGS__)))
-  // solver_mode 2 (the TGS refresh): walking v2 and stand-up only (zb_create), two-wave occupancy
+  // solver_modes 2, 3 (the TGS refresh): walking v2 and stand-up only (zb_create), two-wave occupancy
 #define ZB_LAUNCH_R(K, ...)                                                                        \
   (refresh ? K<true, 2, true><<<blocks, WGT, 0, s>>>(__VA_ARGS__) : ZB_LAUNCH(K, __VA_ARGS__))
   if (h->task == ZB_TASK_STANDUP_V0)
@@ -5603,7 +5639,7 @@ int zb_physics_substeps(zb_handle h, const float* targets, int nsub, float* net_
   if (!h || !targets || nsub < 1) return set_err(-1, "zb_physics_substeps", hipSuccess);
   const int blocks = (h->n + EPW - 1) / EPW;
   const bool dr = h->task == ZB_TASK_STANDUP_V0 || h->task == ZB_TASK_MANAGER_V0, tgs = h->cfg.solver_mode >= 1;
-  const bool refresh = h->cfg.solver_mode == 2;
+  const bool refresh = h->cfg.solver_mode >= 2;
 #define ZB_SUB(F, T, R) zb_substeps_kernel<F, T, R><<<blocks, WGT, 0, (hipStream_t)stream>>>(h->d_model, h->d_links, \
                                                  h->cfg, h->n, h->d_state, targets, nsub, net_force, applied_torque)
   if (dr) {

@@ -50,7 +50,7 @@ class SolverCfg:
     contact_margin: float = 0.004
     baumgarte: float = 0.2
     self_collision: bool = True       # enabled_self_collisions=True (zbot_cfg.py:636)
-    mode: int = 0                     # 0: PGS sweeps; 1: TGS-style sub-iterations; 2: TGS + ground-contact refresh (zb_task_cfg.solver_mode)
+    mode: int = 0                     # 0: PGS sweeps; 1: TGS-style sub-iterations; 2: TGS + ground-contact refresh; 3: + self-contact refresh (zb_task_cfg.solver_mode)
     self_manifold: int = 2            # 2: cap-on-cap (up to 4 points) + side-by-side rims (up to 3); 1: caps only; 0: off (zb_task_cfg.self_manifold)
 
 

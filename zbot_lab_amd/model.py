@@ -513,7 +513,7 @@ class TaskCfg:
     contact_margin: float = 0.004
     baumgarte: float = 0.2
     solver_iterations: int = 4   # = solver_position_iteration_count (zbot_cfg.py:637)
-    solver_mode: int = 0         # 0: PGS sweeps on one linearisation; 1: TGS-style; 2: TGS + per-iteration ground refresh (zb_task_cfg.solver_mode)
+    solver_mode: int = 0         # 0: PGS sweeps on one linearisation; 1: TGS-style; 2: TGS + per-iteration ground refresh; 3: + self-contact refresh (zb_task_cfg.solver_mode)
     self_manifold: int = 2       # 2: cap-on-cap (up to 4 points) + side-by-side rims (up to 3); 1: caps only; 0: one point per pair
     enable_self_collision: bool = True
     task: int = TASK_WALKING_V2
