@@ -68,10 +68,15 @@ def _torch_minibatch(alg, i):
     return torch.stack([kl.mean(), vl.detach(), surr.detach(), entropy_b.mean().detach()])
 
 
+@pytest.mark.parametrize("rows", ["reg", "lds"])
 @pytest.mark.parametrize("hidden", [[128, 128, 128], [256, 256, 128]], ids=["v2-nets", "standup-nets"])
-def test_fused_minibatch_gradients_match_autograd(gpu, hidden):
+def test_fused_minibatch_gradients_match_autograd(gpu, hidden, rows, monkeypatch):
+    """rows: the register-resident row kernel (k_rows_reg, these shapes' default) or the LDS one
+    (ZBP_ROWS=lds, every other shape)."""
     import torch
     from zbot_lab_amd.rl import fused
+    if rows == "lds":
+        monkeypatch.setenv("ZBP_ROWS", "lds")
     alg = _alg(hidden)
     mb = alg.storage.num_envs * alg.storage.num_transitions_per_env // alg.num_mini_batches
     assert fused.supported(alg.policy, mb)
@@ -148,13 +153,17 @@ def test_fused_gae_matches_torch(gpu, monkeypatch):
     assert abs(float(st.advantages.mean())) < 1e-5 and abs(float(st.advantages.std()) - 1.0) < 1e-4
 
 
+@pytest.mark.parametrize("rows", ["reg", "lds"])
 @pytest.mark.parametrize("hidden", [[128, 128, 128], [256, 256, 128]], ids=["v2-nets", "standup-nets"])
-def test_fused_act_matches_torch_policy(gpu, hidden):
+def test_fused_act_matches_torch_policy(gpu, hidden, rows, monkeypatch):
     """zbp_act (the rollout's policy step, runner._rollout) against PPO.act's torch statement with the
     same standard-normal draw: actions, mu, sigma, log-probabilities, values and the observations in
-    the storage slot (fp32 summation-order tolerances); rows not a multiple of 32 included."""
+    the storage slot (fp32 summation-order tolerances); rows not a multiple of 32 included. rows: the
+    register-resident forward (k_act_reg) or the LDS one (ZBP_ROWS=lds)."""
     import torch
     from zbot_lab_amd.rl import fused
+    if rows == "lds":
+        monkeypatch.setenv("ZBP_ROWS", "lds")
     for envs in (512, 200):
         alg = _alg(hidden, envs=envs)
         fu = fused.FusedUpdate(alg, 256)  # (the minibatch size shapes only the update's row buffers)

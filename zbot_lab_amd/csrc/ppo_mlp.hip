@@ -24,6 +24,7 @@
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "zbot_ppo.h"
@@ -56,6 +57,7 @@ inline int pad32(int d) { return (d + 31) & ~31; }
 struct NetW {
   int L, d[MAXL + 1], p[MAXL + 1];
   int64_t wp[MAXL], wt[MAXL], bp[MAXL];  // padded weights [p(l+1)][p(l)], transposed [p(l)][p(l+1)], bias [p(l+1)]
+  int64_t wr[MAXL], wtr[MAXL];           // the same in k_rows_reg's lane order (forward / backward A operands)
   int64_t x[MAXL], dz[MAXL];             // row buffers: X_l [B][p(l)], dZ_l [B][p(l+1)]
 };
 struct Layout {
@@ -83,6 +85,8 @@ Layout make_layout(const zbp_net* a, const zbp_net* c, int B) {
       w.wp[l] = take((int64_t)w.p[l + 1] * w.p[l]);
       w.wt[l] = take((int64_t)w.p[l] * w.p[l + 1]);
       w.bp[l] = take(w.p[l + 1]);
+      w.wr[l] = take((int64_t)w.p[l + 1] * w.p[l]);
+      w.wtr[l] = take((int64_t)w.p[l] * w.p[l + 1]);
       w.x[l] = take((int64_t)B * w.p[l]);
       w.dz[l] = take((int64_t)B * w.p[l + 1]);
       lo.tile0[k * MAXL + l] = t;
@@ -175,11 +179,22 @@ __global__ void k_pack(PackArgs A) {
   const int P0 = w.p[l], P1 = w.p[l + 1], D0 = w.d[l], D1 = w.d[l + 1];
   float* wp = A.ws + w.wp[l];
   float* wt = A.ws + w.wt[l];
+  float* wr = A.ws + w.wr[l];
+  float* wtr = A.ws + w.wtr[l];
+  const int T0 = P0 / 32, T1 = P1 / 32;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < P0 * P1; e += gridDim.x * blockDim.x) {
     const int n = e / P0, k = e % P0;
     const float v = (n < D1 && k < D0) ? A.w[net][l][n * D0 + k] : 0.f;
     wp[e] = v;
     wt[k * P1 + n] = v;
+    // k_rows_reg's A operands: block (output tile, reduction tile), lane (i = output index & 31,
+    // h = reduction index bit 2), 16 floats (reduction index 8 q + 4 h + u -> entry 4 q + u)
+    {
+      const int kk = k & 31, j = 4 * (kk >> 3) + (kk & 3), hh = (kk >> 2) & 1;
+      wr[((int64_t)((n >> 5) * T0 + (k >> 5)) * 64 + (n & 31) + 32 * hh) * 16 + j] = v;
+      const int nn = n & 31, jb = 4 * (nn >> 3) + (nn & 3), hb = (nn >> 2) & 1;
+      wtr[((int64_t)((k >> 5) * T1 + (n >> 5)) * 64 + (k & 31) + 32 * hb) * 16 + jb] = v;
+    }
   }
   if (blockIdx.x == 0)
     for (int n = threadIdx.x; n < P1; n += blockDim.x) A.ws[w.bp[l] + n] = n < D1 ? A.b[net][l][n] : 0.f;
@@ -401,6 +416,261 @@ __global__ __launch_bounds__(ROW_THREADS) void k_rows(RowArgs A) {
   }
   net_backward(A, wc, lds, row0);
   if (tid < NSTAT) A.ws[A.stats + (int64_t)blockIdx.x * NSTAT + tid] = red[tid];
+}
+
+// ------------------------------------------------------------------------------- k_rows_reg
+// k_rows for the shipped net shapes (three hidden layers of 32 T1, 32 T2, 32 T3 units, inputs and
+// outputs <= 32: rsl_rl's [128, 128, 128] and the stand-up / v2 [256, 256, 128]), one WAVE per 32-row
+// tile and the activations in registers: no LDS, no barriers, every wave runs its tile through both
+// nets on its own. A layer is the transposed product Z^T = W X^T on v_mfma_f32_32x32x2_f32 with the
+// weights as the A operand (lane-ordered images wr / wtr, k_pack) and the activations as the B
+// operand straight from the previous layer's accumulators: an accumulator tile holds, in lane
+// (row r = lane & 31, h = lane >> 5), register 4 q + u, feature 8 q + 4 h + u of row r -- exactly the
+// B operand of 16 MFMAs whose reduction index runs over those features in that order. One wave per
+// SIMD (up to 512 VGPRs + AGPRs): a 256-wide layer keeps 8 input + 8 output tiles (256 registers)
+// live. X_l and dZ_l still go to HBM feature-major for k_wgrad; the backward pass reads X_l back for
+// ELU'.
+typedef f32x16 Tile;
+
+__device__ __forceinline__ int rr_feat(int j) { return 8 * (j >> 2) + 4 * ((threadIdx.x & 63) >> 5) + (j & 3); }
+// feature-major row buffers: element (feature 32 o + 8 q + 4 h + u, row row0 + r) of a [P][B] buffer at
+// base = buffer + row0 as base[uniform part (32 o + 8 q + u) B] + lane part (4 h B + r): the uniform part
+// stays scalar (one SGPR pair per access) and the lane part one 32-bit VGPR offset
+__device__ __forceinline__ int rr_lane_off(int B) { return 4 * ((threadIdx.x & 63) >> 5) * B + (threadIdx.x & 31); }
+__device__ __forceinline__ float* rr_at(float* base, int o, int j, int B) {
+  return base + (int64_t)(32 * o + 8 * (j >> 2) + (j & 3)) * B;
+}
+
+// out[o] = sum_i A(o, i) in[i] over the blocks of a lane-ordered image: block (o, i) = 16 floats per
+// lane, the A operands of 16 MFMAs whose B operands are in[i]'s registers. Reduction tiles outer, so
+// consecutive blocks feed different accumulators; block b + 2's operands load while block b issues.
+template <int TI, int TO>
+__device__ __forceinline__ void rr_layer(const float* __restrict__ img, const Tile (&in)[TI], Tile (&out)[TO]) {
+  const float4* wl = reinterpret_cast<const float4*>(img) + 4 * (threadIdx.x & 63);
+  constexpr int NB = TI * TO, D = 2;
+#pragma unroll
+  for (int o = 0; o < TO; ++o) out[o] = Tile{};
+  float4 buf[D + 1][4];
+#pragma unroll
+  for (int b = 0; b < D; ++b)
+    if (b < NB) {
+      const int i = b / TO, o = b % TO;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) buf[b][c] = wl[(o * TI + i) * 256 + c];
+    }
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const int i = b / TO, o = b % TO;
+    if (b + D < NB) {
+      const int i2 = (b + D) / TO, o2 = (b + D) % TO;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) buf[(b + D) % (D + 1)][c] = wl[(o2 * TI + i2) * 256 + c];
+    }
+    const float4* w = buf[b % (D + 1)];
+    Tile a = out[o];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      a = mfma(w[c].x, in[i][4 * c + 0], a);
+      a = mfma(w[c].y, in[i][4 * c + 1], a);
+      a = mfma(w[c].z, in[i][4 * c + 2], a);
+      a = mfma(w[c].w, in[i][4 * c + 3], a);
+    }
+    out[o] = a;
+    __builtin_amdgcn_sched_barrier(0);  // (keeps the scheduler from hoisting every block's loads)
+  }
+}
+
+// forward layer l: + bias, ELU (hidden layers: also X_{l+1} to HBM, feature-major)
+template <int TI, int TO, bool kLast, bool kStore = true>
+__device__ __forceinline__ void rr_forward(const NetW& w, int l, float* __restrict__ ws, int B, int row0,
+                                           const Tile (&in)[TI], Tile (&out)[TO]) {
+  const int h = (threadIdx.x & 63) >> 5, lo = rr_lane_off(B);
+  rr_layer<TI, TO>(ws + w.wr[l], in, out);
+  const float* bp = ws + w.bp[l];
+  float* xb = ws + w.x[l + 1] + row0;
+#pragma unroll
+  for (int o = 0; o < TO; ++o)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 bq = *reinterpret_cast<const float4*>(bp + 32 * o + 8 * q + 4 * h);
+      const float bv[4] = {bq.x, bq.y, bq.z, bq.w};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float v = out[o][4 * q + u] + bv[u];
+        if (!kLast) {
+          v = v > 0.f ? v : expf(v) - 1.f;  // ELU(alpha = 1), as ATen's elu kernel
+          if (kStore) rr_at(xb, o, 4 * q + u, B)[lo] = v;
+        }
+        out[o][4 * q + u] = v;
+      }
+    }
+}
+
+// backward through layer l >= 1: dZ_{l-1} = (W_l^T dZ_l) * ELU'(X_l), to registers and HBM
+template <int TI, int TO>
+__device__ __forceinline__ void rr_backward(const NetW& w, int l, float* __restrict__ ws, int B, int row0,
+                                            const Tile (&dz)[TI], Tile (&out)[TO]) {
+  const int lo = rr_lane_off(B);
+  rr_layer<TI, TO>(ws + w.wtr[l], dz, out);
+  float* xb = ws + w.x[l] + row0;
+  float* db = ws + w.dz[l - 1] + row0;
+#pragma unroll
+  for (int o = 0; o < TO; ++o)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const float x = rr_at(xb, o, j, B)[lo];
+      const float g = out[o][j] * (x > 0.f ? 1.f : x + 1.f);  // ELU'(z) = exp(z) = x + 1 for z <= 0
+      out[o][j] = g;
+      rr_at(db, o, j, B)[lo] = g;
+    }
+}
+
+// the tile's input rows (through the permutation) as the first layer's B operand, zero-padded to 32
+__device__ __forceinline__ void rr_gather(const NetW& w, float* __restrict__ ws, int B, int row0, const float* src, int dim,
+                                          int64_t row, Tile (&x)[1]) {
+  const int lo = rr_lane_off(B);
+  float* xb = ws + w.x[0] + row0;
+  const float* sr = src + row * dim;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int k = rr_feat(j);
+    const float v = k < dim ? sr[k] : 0.f;
+    x[0][j] = v;
+    rr_at(xb, 0, j, B)[lo] = v;
+  }
+}
+
+__device__ __forceinline__ void rr_store_dz(const NetW& w, float* __restrict__ ws, int B, int row0, const Tile& d) {
+  const int lo = rr_lane_off(B);
+  float* db = ws + w.dz[w.L - 1] + row0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) rr_at(db, 0, j, B)[lo] = d[j];
+}
+
+// (the [128, 128, 128] nets fit 256 registers: two waves per SIMD)
+template <int T1, int T2, int T3>
+__global__ __launch_bounds__(256, (T1 > 4 || T2 > 4) ? 1 : 2) void k_rows_reg(RowArgs A) {
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (tile * TR >= A.B) return;  // (no barriers: whole waves leave)
+  const int row0 = tile * TR, B = A.B;
+  const zbp_batch& bt = A.bt;
+  const int NA = bt.num_actions;
+  const float invB = 1.f / (float)bt.batch;
+  const int64_t row = bt.idx[bt.idx_offset + row0 + r];
+  float* ws = A.ws;
+  float* st = ws + A.stats + (int64_t)tile * NSTAT;
+
+  // ---- actor: forward, Gaussian log-prob, clipped surrogate, KL; dL/dmu into dZ of the output
+  const NetW& wa = A.n[0];
+  Tile z[1];
+  {
+    Tile x0[1], x1[T1], x2[T2], x3[T3];
+    rr_gather(wa, ws, B, row0, bt.obs, bt.obs_dim, row, x0);
+    rr_forward<1, T1, false>(wa, 0, ws, B, row0, x0, x1);
+    rr_forward<T1, T2, false>(wa, 1, ws, B, row0, x1, x2);
+    rr_forward<T2, T3, false>(wa, 2, ws, B, row0, x2, x3);
+    rr_forward<T3, 1, true>(wa, 3, ws, B, row0, x3, z);
+  }
+  Tile dz[1];
+  {
+    // lane (r, h) holds actions 8 q + 4 h + u of row r: per-half partial sums, then the halves'
+    const float kLog2Pi = 0.91893853320467274178f;  // log(sqrt(2 pi))
+    float lp = 0.f, kl = 0.f, diff[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int n = rr_feat(j);
+      diff[j] = 0.f;
+      if (n < NA) {
+        const float mu = z[0][j], s = A.std_param[n];
+        const float d = bt.actions[row * NA + n] - mu;
+        diff[j] = d;
+        lp += -(d * d) / (2.f * (s * s)) - logf(s) - kLog2Pi;
+        const float os = bt.sigma[row * NA + n], om = bt.mu[row * NA + n];
+        kl += logf(s / os + 1e-5f) + (os * os + (om - mu) * (om - mu)) / (2.f * (s * s)) - 0.5f;
+      }
+    }
+    lp += __shfl_xor(lp, 32);
+    kl += __shfl_xor(kl, 32);
+    const float adv = bt.advantages[row], clip = A.lc.clip_param;
+    const float ratio = expf(lp - bt.log_prob[row]);
+    const float rc = fminf(fmaxf(ratio, 1.f - clip), 1.f + clip);
+    const float s1 = -adv * ratio, s2 = -adv * rc;
+    const float surr = fmaxf(s1, s2);
+    // d max(s1, s2) / d ratio (torch.max splits a tie evenly; clamp passes the gradient inside
+    // [1 - clip, 1 + clip], bounds included)
+    const float in = (ratio >= 1.f - clip && ratio <= 1.f + clip) ? 1.f : 0.f;
+    const float w1 = s1 > s2 ? 1.f : (s1 < s2 ? 0.f : 0.5f);
+    const float g = (w1 * -adv + (1.f - w1) * -adv * in) * ratio * invB;  // dL / dlog_prob
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int n = rr_feat(j);
+      float d = 0.f, sg = 0.f;
+      if (n < NA) {
+        const float s = A.std_param[n];
+        d = g * diff[j] / (s * s);
+        sg = g * (diff[j] * diff[j] / (s * s * s) - 1.f / s);
+      }
+      dz[0][j] = d;
+      if (j < 8) {  // actions < 16: the std gradient summed over the tile's rows (one half's lanes)
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) sg += __shfl_xor(sg, o);
+        if (r == 0 && n < NA) st[3 + n] = sg;
+      }
+    }
+    rr_store_dz(wa, ws, B, row0, dz[0]);
+    const float su = wave_sum(h == 0 ? surr : 0.f), ks = wave_sum(h == 0 ? kl : 0.f);
+    if (lane == 0) {
+      st[0] = su;
+      st[2] = ks;
+      for (int a = 3 + NA; a < NSTAT; ++a) st[a] = 0.f;
+    }
+  }
+  {
+    Tile d3[T3], d2[T2], d1[T1];
+    rr_backward<1, T3>(wa, 3, ws, B, row0, dz, d3);
+    rr_backward<T3, T2>(wa, 2, ws, B, row0, d3, d2);
+    rr_backward<T2, T1>(wa, 1, ws, B, row0, d2, d1);
+  }
+
+  // ---- critic: forward, clipped value loss, backward
+  const NetW& wc = A.n[1];
+  {
+    Tile x0[1], x1[T1], x2[T2], x3[T3];
+    rr_gather(wc, ws, B, row0, bt.critic_obs, bt.critic_obs_dim, row, x0);
+    rr_forward<1, T1, false>(wc, 0, ws, B, row0, x0, x1);
+    rr_forward<T1, T2, false>(wc, 1, ws, B, row0, x1, x2);
+    rr_forward<T2, T3, false>(wc, 2, ws, B, row0, x2, x3);
+    rr_forward<T3, 1, true>(wc, 3, ws, B, row0, x3, z);
+  }
+  {
+    const float v = __shfl(z[0][0], r), tv = bt.values[row], ret = bt.returns[row], clip = A.lc.clip_param;
+    float vl, dv;
+    if (A.lc.use_clipped_value_loss) {
+      const float vd = v - tv;
+      const float vc = tv + fminf(fmaxf(vd, -clip), clip);
+      const float ea = (v - ret) * (v - ret), ec = (vc - ret) * (vc - ret);
+      vl = fmaxf(ea, ec);
+      const float wa_ = ea > ec ? 1.f : (ea < ec ? 0.f : 0.5f);
+      const float in = (vd >= -clip && vd <= clip) ? 1.f : 0.f;
+      dv = wa_ * 2.f * (v - ret) + (1.f - wa_) * 2.f * (vc - ret) * in;
+    } else {
+      vl = (ret - v) * (ret - v);
+      dv = 2.f * (v - ret);
+    }
+    dv *= A.lc.value_loss_coef * invB;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) dz[0][j] = (h == 0 && j == 0) ? dv : 0.f;
+    rr_store_dz(wc, ws, B, row0, dz[0]);
+    const float vs = wave_sum(h == 0 ? vl : 0.f);
+    if (lane == 0) st[1] = vs;
+  }
+  {
+    Tile d3[T3], d2[T2], d1[T1];
+    rr_backward<1, T3>(wc, 3, ws, B, row0, dz, d3);
+    rr_backward<T3, T2>(wc, 2, ws, B, row0, d3, d2);
+    rr_backward<T2, T1>(wc, 1, ws, B, row0, d2, d1);
+  }
 }
 
 // ------------------------------------------------------------------------------- k_wgrad
@@ -658,6 +928,59 @@ __global__ __launch_bounds__(256) void k_act(ActArgs A) {
   if (tid < TR && row0 + tid < A.rows) A.s_val[row0 + tid] = lds[A.lds_out + tid * 33];
 }
 
+// k_act on the register-resident forward (k_rows_reg's shapes): one wave per 32 rows, no LDS
+template <int T1, int T2, int T3>
+__global__ __launch_bounds__(256, (T1 > 4 || T2 > 4) ? 1 : 2) void k_act_reg(ActArgs A) {
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * TR;
+  if (row0 >= A.rows) return;
+  const int64_t row = row0 + r;
+  const bool ok = row < A.rows;
+  const int na = A.na;
+  Tile z[1];
+#pragma unroll
+  for (int net = 0; net < 2; ++net) {
+    const NetW& w = A.n[net];
+    const int dim = net ? A.cobs_dim : A.obs_dim;
+    const float* src = (net ? A.cobs : A.obs) + row * dim;
+    float* st = (net ? A.s_cobs : A.s_obs) + row * dim;
+    Tile x0[1], x1[T1], x2[T2], x3[T3];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int k = rr_feat(j);
+      const float v = (ok && k < dim) ? src[k] : 0.f;
+      x0[0][j] = v;
+      if (ok && k < dim) st[k] = v;
+    }
+    rr_forward<1, T1, false, false>(w, 0, A.ws, 0, 0, x0, x1);
+    rr_forward<T1, T2, false, false>(w, 1, A.ws, 0, 0, x1, x2);
+    rr_forward<T2, T3, false, false>(w, 2, A.ws, 0, 0, x2, x3);
+    rr_forward<T3, 1, true, false>(w, 3, A.ws, 0, 0, x3, z);
+    if (net == 0) {
+      // lane (r, h) holds actions 8 q + 4 h + u of row r
+      const float kLog2Pi = 0.91893853320467274178f;  // log(sqrt(2 pi))
+      float lp = 0.f;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int n = rr_feat(j);
+        if (ok && n < na) {
+          const float mu = z[0][j], s = A.std_param[n];
+          const float x = mu + s * A.noise[row * na + n], diff = x - mu;
+          lp += -(diff * diff) / (2.f * (s * s)) - logf(s) - kLog2Pi;
+          A.actions[row * na + n] = x;
+          A.s_act[row * na + n] = x;
+          A.s_mu[row * na + n] = mu;
+          A.s_sig[row * na + n] = s;
+        }
+      }
+      lp += __shfl_xor(lp, 32);
+      if (ok && h == 0) A.s_lp[row] = lp;
+    } else if (ok && h == 0) {
+      A.s_val[row] = z[0][0];
+    }
+  }
+}
+
 // PPO.process_env_step + the runner's episode bookkeeping (zbot_lab_amd/rl/runner.py _rollout) for
 // one step, one workgroup: the storage slot's reward (+ gamma * value on time-outs, rsl_rl's
 // bootstrap) and done; cur_rew += reward, cur_len += 1; over the done envs ep_stats += {sum cur_rew,
@@ -766,6 +1089,21 @@ __global__ __launch_bounds__(256) void k_adv_norm(float* __restrict__ adv, int64
     adv[e] = (adv[e] - mean) / den;  // (a division, as torch's (adv - mean) / (std + 1e-8))
 }
 
+// k_rows_reg instantiation for the nets' shape: 1 = hidden [256, 256, 128], 2 = [128, 128, 128] (both
+// nets; inputs / outputs <= 32), 0 = none (k_rows)
+int reg_shape(const Layout& lo) {
+  const char* e = getenv("ZBP_ROWS");  // (read per call: tests switch it)
+  if (e && strcmp(e, "lds") == 0) return 0;
+  const NetW &a = lo.n[0], &c = lo.n[1];
+  if (a.L != 4 || c.L != 4) return 0;
+  for (int l = 0; l <= 4; ++l)
+    if (a.p[l] != c.p[l]) return 0;
+  if (a.p[0] != 32 || a.p[4] != 32) return 0;
+  if (a.p[1] == 256 && a.p[2] == 256 && a.p[3] == 128) return 1;
+  if (a.p[1] == 128 && a.p[2] == 128 && a.p[3] == 128) return 2;
+  return 0;
+}
+
 int launch_check(const char* what) {
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : hip_fail(e, what);
@@ -853,7 +1191,14 @@ int zbp_minibatch(const zbp_net* actor, const zbp_net* critic, const float* std_
     if (e != hipSuccess) return hip_fail(e, "hipFuncSetAttribute k_rows");
     lds_set = true;
   }
-  k_rows<<<B / TR, ROW_THREADS, lds, s>>>(R);
+  // the register-resident row kernel for the shipped shapes (ZBP_ROWS=lds: the LDS one, for A/Bs)
+  const int shape = reg_shape(lo);
+  if (shape == 1)
+    k_rows_reg<8, 8, 4><<<(B / TR + 3) / 4, 256, 0, s>>>(R);
+  else if (shape == 2)
+    k_rows_reg<4, 4, 4><<<(B / TR + 3) / 4, 256, 0, s>>>(R);
+  else
+    k_rows<<<B / TR, ROW_THREADS, lds, s>>>(R);
   if (int rc = launch_check("k_rows")) return rc;
 
   WgradArgs W{};
@@ -974,7 +1319,13 @@ int zbp_act(const zbp_net* actor, const zbp_net* critic, const float* std_param,
     if (e != hipSuccess) return hip_fail(e, "hipFuncSetAttribute k_act");
     lds_set = true;
   }
-  k_act<<<(io->rows + TR - 1) / TR, 256, lds, (hipStream_t)stream>>>(A);
+  const int shape = reg_shape(lo), wgs = ((io->rows + TR - 1) / TR + 3) / 4;
+  if (shape == 1)
+    k_act_reg<8, 8, 4><<<wgs, 256, 0, (hipStream_t)stream>>>(A);
+  else if (shape == 2)
+    k_act_reg<4, 4, 4><<<wgs, 256, 0, (hipStream_t)stream>>>(A);
+  else
+    k_act<<<(io->rows + TR - 1) / TR, 256, lds, (hipStream_t)stream>>>(A);
   return launch_check("k_act");
 }
 
