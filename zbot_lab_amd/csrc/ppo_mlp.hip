@@ -53,6 +53,12 @@ int hip_fail(hipError_t e, const char* what) {
 
 inline int pad32(int d) { return (d + 31) & ~31; }
 
+// Row buffers (X_l, dZ_l) in HBM are octet-blocked feature-major: feature f of minibatch row i of a
+// P-feature buffer at ((i >> 3) P + f) 8 + (i & 7), i.e. for every octet of rows the features' 8-row
+// runs (32 B) back to back. k_wgrad's lanes (one feature each, four rows) then read 1 KB contiguous
+// per instruction (8 full lines) instead of one 16-byte piece from each of 32 lines.
+__host__ __device__ __forceinline__ int64_t rbo(int P, int f, int i) { return ((int64_t)(i >> 3) * P + f) * 8 + (i & 7); }
+
 // one net in the workspace: dims and float offsets of its images and row buffers
 struct NetW {
   int L, d[MAXL + 1], p[MAXL + 1];
@@ -65,7 +71,7 @@ struct Layout {
   int64_t stats;  // [tiles][NSTAT] per-row-tile partial sums
   int64_t part;   // [splits][wtiles][PART] weight-gradient partials
   int wtiles, tile0[2 * MAXL + 1];  // weight tiles of (net, layer) in order, prefix counts
-  int ngroups, grp0[2 * MAXL + 1];  // k_wgrad workgroups (<= 4 output tiles each) of (net, layer), prefix counts
+  int ngroups, grp0[2 * MAXL + 1];  // k_wgrad workgroups (<= 4 x 4 output x reduction tiles) of (net, layer), prefix counts
   int splits;
   int64_t scratch;  // [64] per-block gradient sums of squares (zbp_optimizer_step)
   int64_t total;
@@ -96,20 +102,21 @@ Layout make_layout(const zbp_net* a, const zbp_net* c, int B) {
   }
   lo.tile0[2 * MAXL] = t;
   lo.wtiles = t;
-  // weight-gradient workgroups: per (net, layer) groups of up to 4 output tiles (one wave each)
+  // weight-gradient workgroups: per (net, layer) groups of up to 4 output tiles (one wave each) x up
+  // to 4 reduction tiles
   int g = 0;
   for (int k = 0; k < 2; ++k)
     for (int l = 0; l < MAXL; ++l) {
       lo.grp0[k * MAXL + l] = g;
-      if (l < lo.n[k].L) g += (lo.n[k].p[l + 1] / 32 + 3) / 4;
+      if (l < lo.n[k].L) g += ((lo.n[k].p[l + 1] / 32 + 3) / 4) * ((lo.n[k].p[l] / 32 + 3) / 4);
     }
   lo.grp0[2 * MAXL] = g;
   lo.ngroups = g;
   lo.stats = take((int64_t)(B / TR) * NSTAT);
-  // row splits of the weight gradients: ~3 waves per SIMD (k_wgrad), each split >= 256 rows, a
-  // multiple of 16 (k_wgrad's loop over pairs of row octets)
+  // row splits of the weight gradients: ~4 waves per SIMD (k_wgrad), each split >= 256 rows, a
+  // multiple of 8 (row octets)
   int s = 1;
-  while (s < 256 && (int64_t)g * 4 * s * 2 <= 3 * 1024 && B / (s * 2) >= 256 && B % (16 * s * 2) == 0) s *= 2;
+  while (s < 256 && (int64_t)g * 4 * s * 2 <= 4 * 1024 && B / (s * 2) >= 256 && B % (8 * s * 2) == 0) s *= 2;
   lo.splits = s;
   lo.part = take((int64_t)s * t * PART);
   lo.scratch = take(64);
@@ -247,7 +254,7 @@ __device__ void net_forward_t(const NetW& w, float* ws, int B, const int* lds_x,
           }
         }
         if (kStore && !last)
-          *reinterpret_cast<float4*>(ws + w.x[l + 1] + (int64_t)n * B + row0 + 8 * q + 4 * h) =
+          *reinterpret_cast<float4*>(ws + w.x[l + 1] + rbo(P1, n, row0 + 8 * q + 4 * h)) =
               make_float4(v[0], v[1], v[2], v[3]);
       }
     }
@@ -279,7 +286,7 @@ __device__ void net_backward(const RowArgs& A, const NetW& w, float* lds, int ro
           g[u] = acc[4 * q + u] * (x > 0.f ? 1.f : x + 1.f);  // ELU'(z) = exp(z) = x + 1 for z <= 0
           xs[i * (P0 + 4) + k] = g[u];
         }
-        *reinterpret_cast<float4*>(A.ws + w.dz[l - 1] + (int64_t)k * A.B + row0 + 8 * q + 4 * h) =
+        *reinterpret_cast<float4*>(A.ws + w.dz[l - 1] + rbo(P0, k, row0 + 8 * q + 4 * h)) =
             make_float4(g[0], g[1], g[2], g[3]);
       }
     }
@@ -295,7 +302,7 @@ __device__ void gather_input(const RowArgs& A, const NetW& w, const float* src, 
     const int64_t row = A.bt.idx[A.bt.idx_offset + row0 + i];
     const float v = k < dim ? src[row * dim + k] : 0.f;
     lds[A.lds_x[0] + i * (P0 + 4) + k] = v;
-    A.ws[w.x[0] + (int64_t)k * A.B + row0 + i] = v;
+    A.ws[w.x[0] + rbo(P0, k, row0 + i)] = v;
   }
   __syncthreads();
 }
@@ -358,7 +365,7 @@ __global__ __launch_bounds__(ROW_THREADS) void k_rows(RowArgs A) {
             if (b == a) sg[b] = g * (diff * diff / (s * s * s) - 1.f / s);
         }
         dz[i * (Pout + 4) + a] = d;
-        A.ws[wa.dz[wa.L - 1] + (int64_t)a * A.B + row0 + i] = d;
+        A.ws[wa.dz[wa.L - 1] + rbo(Pout, a, row0 + i)] = d;
       }
     }
     if (tid < 64) {
@@ -405,7 +412,7 @@ __global__ __launch_bounds__(ROW_THREADS) void k_rows(RowArgs A) {
       dv *= A.lc.value_loss_coef * invB;
       for (int a = 0; a < Pout; ++a) {
         dz[i * (Pout + 4) + a] = a == 0 ? dv : 0.f;
-        A.ws[wc.dz[wc.L - 1] + (int64_t)a * A.B + row0 + i] = a == 0 ? dv : 0.f;
+        A.ws[wc.dz[wc.L - 1] + rbo(Pout, a, row0 + i)] = a == 0 ? dv : 0.f;
       }
     }
     if (tid < 64) {
@@ -433,13 +440,16 @@ __global__ __launch_bounds__(ROW_THREADS) void k_rows(RowArgs A) {
 typedef f32x16 Tile;
 
 __device__ __forceinline__ int rr_feat(int j) { return 8 * (j >> 2) + 4 * ((threadIdx.x & 63) >> 5) + (j & 3); }
-// feature-major row buffers: element (feature 32 o + 8 q + 4 h + u, row row0 + r) of a [P][B] buffer at
-// base = buffer + row0 as base[uniform part (32 o + 8 q + u) B] + lane part (4 h B + r): the uniform part
-// stays scalar (one SGPR pair per access) and the lane part one 32-bit VGPR offset
-__device__ __forceinline__ int rr_lane_off(int B) { return 4 * ((threadIdx.x & 63) >> 5) * B + (threadIdx.x & 31); }
-__device__ __forceinline__ float* rr_at(float* base, int o, int j, int B) {
-  return base + (int64_t)(32 * o + 8 * (j >> 2) + (j & 3)) * B;
+// row buffers (rbo): element (feature 32 o + 8 q + 4 h + u, row row0 + r) of a P-feature buffer at
+// base = buffer + rbo(P, 0, row0) as base[uniform part (32 o + 8 q + u) 8] + lane part
+// ((r >> 3) P 8 + 32 h + (r & 7)): the uniform part stays scalar (one SGPR pair per access), the lane
+// part one 32-bit VGPR offset
+__device__ __forceinline__ int rr_lane_off(int P) {
+  const int r = threadIdx.x & 31;
+  return (r >> 3) * P * 8 + 32 * ((threadIdx.x & 63) >> 5) + (r & 7);
 }
+__device__ __forceinline__ float* rr_base(float* buf, int P, int row0) { return buf + (int64_t)(row0 >> 3) * P * 8; }
+__device__ __forceinline__ float* rr_at(float* base, int o, int j) { return base + (32 * o + 8 * (j >> 2) + (j & 3)) * 8; }
 
 // out[o] = sum_i A(o, i) in[i] over the blocks of a lane-ordered image: block (o, i) = 16 floats per
 // lane, the A operands of 16 MFMAs whose B operands are in[i]'s registers. Reduction tiles outer, so
@@ -484,10 +494,10 @@ __device__ __forceinline__ void rr_layer(const float* __restrict__ img, const Ti
 template <int TI, int TO, bool kLast, bool kStore = true>
 __device__ __forceinline__ void rr_forward(const NetW& w, int l, float* __restrict__ ws, int B, int row0,
                                            const Tile (&in)[TI], Tile (&out)[TO]) {
-  const int h = (threadIdx.x & 63) >> 5, lo = rr_lane_off(B);
+  const int h = (threadIdx.x & 63) >> 5, lo = rr_lane_off(32 * TO);
   rr_layer<TI, TO>(ws + w.wr[l], in, out);
   const float* bp = ws + w.bp[l];
-  float* xb = ws + w.x[l + 1] + row0;
+  float* xb = rr_base(ws + w.x[l + 1], 32 * TO, row0);
 #pragma unroll
   for (int o = 0; o < TO; ++o)
 #pragma unroll
@@ -499,7 +509,7 @@ __device__ __forceinline__ void rr_forward(const NetW& w, int l, float* __restri
         float v = out[o][4 * q + u] + bv[u];
         if (!kLast) {
           v = v > 0.f ? v : expf(v) - 1.f;  // ELU(alpha = 1), as ATen's elu kernel
-          if (kStore) rr_at(xb, o, 4 * q + u, B)[lo] = v;
+          if (kStore) rr_at(xb, o, 4 * q + u)[lo] = v;
         }
         out[o][4 * q + u] = v;
       }
@@ -510,41 +520,41 @@ __device__ __forceinline__ void rr_forward(const NetW& w, int l, float* __restri
 template <int TI, int TO>
 __device__ __forceinline__ void rr_backward(const NetW& w, int l, float* __restrict__ ws, int B, int row0,
                                             const Tile (&dz)[TI], Tile (&out)[TO]) {
-  const int lo = rr_lane_off(B);
+  const int lo = rr_lane_off(32 * TO);
   rr_layer<TI, TO>(ws + w.wtr[l], dz, out);
-  float* xb = ws + w.x[l] + row0;
-  float* db = ws + w.dz[l - 1] + row0;
+  float* xb = rr_base(ws + w.x[l], 32 * TO, row0);
+  float* db = rr_base(ws + w.dz[l - 1], 32 * TO, row0);
 #pragma unroll
   for (int o = 0; o < TO; ++o)
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
-      const float x = rr_at(xb, o, j, B)[lo];
+      const float x = rr_at(xb, o, j)[lo];
       const float g = out[o][j] * (x > 0.f ? 1.f : x + 1.f);  // ELU'(z) = exp(z) = x + 1 for z <= 0
       out[o][j] = g;
-      rr_at(db, o, j, B)[lo] = g;
+      rr_at(db, o, j)[lo] = g;
     }
 }
 
 // the tile's input rows (through the permutation) as the first layer's B operand, zero-padded to 32
 __device__ __forceinline__ void rr_gather(const NetW& w, float* __restrict__ ws, int B, int row0, const float* src, int dim,
                                           int64_t row, Tile (&x)[1]) {
-  const int lo = rr_lane_off(B);
-  float* xb = ws + w.x[0] + row0;
+  const int lo = rr_lane_off(32);
+  float* xb = rr_base(ws + w.x[0], 32, row0);
   const float* sr = src + row * dim;
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
     const int k = rr_feat(j);
     const float v = k < dim ? sr[k] : 0.f;
     x[0][j] = v;
-    rr_at(xb, 0, j, B)[lo] = v;
+    rr_at(xb, 0, j)[lo] = v;
   }
 }
 
 __device__ __forceinline__ void rr_store_dz(const NetW& w, float* __restrict__ ws, int B, int row0, const Tile& d) {
-  const int lo = rr_lane_off(B);
-  float* db = ws + w.dz[w.L - 1] + row0;
+  const int lo = rr_lane_off(32);
+  float* db = rr_base(ws + w.dz[w.L - 1], 32, row0);
 #pragma unroll
-  for (int j = 0; j < 16; ++j) rr_at(db, 0, j, B)[lo] = d[j];
+  for (int j = 0; j < 16; ++j) rr_at(db, 0, j)[lo] = d[j];
 }
 
 // (the [128, 128, 128] nets fit 256 registers: two waves per SIMD)
@@ -682,49 +692,51 @@ struct WgradArgs {
   int64_t part;
 };
 // dW_l = dZ_l^T X_l and db_l = sum dZ_l over the rows of one split. One workgroup = up to four 32-row
-// output tiles of one layer (n-tiles, one per wave); each wave accumulates its n-tile against every
-// k-tile of the layer (<= 8 accumulators), so the dZ rows of a tile are read once per split and the
-// X rows once per group of four n-tiles (the waves of a workgroup read the same X lines: L1 / L2
-// hits) -- instead of once per 32x32 tile. A[n][r] = dZ_l[n0 + n][r], B[r][k] = X_l[k0 + k][r]
-// (feature-major, float4 quads of rows: lane half h takes rows 8 j + 4 h .. 8 j + 4 h + 3, one MFMA
-// each); the next row octet's quads are loaded while the current one's MFMAs issue. Partial tiles
-// (and the bias column of the k0 = 0 tile) go to the workspace in k_reduce's layout.
-__global__ __launch_bounds__(256, 2) void k_wgrad(WgradArgs A) {
+// output tiles of one layer (n-tiles, one per wave) against up to four of its k-tiles; each wave
+// accumulates its n-tile against those k-tiles (<= 4 accumulators), so the waves of a workgroup read
+// the same X lines (L1 / L2 hits). A[n][r] = dZ_l[n0 + n][r], B[r][k] = X_l[k0 + k][r] from the
+// octet-blocked row buffers (rbo): lane half h takes rows 8 j + 4 h .. 8 j + 4 h + 3 of one feature,
+// one float4 and four MFMAs per tile; a wave instruction reads 1 KB contiguous. The next row octet's
+// quads load while the current one's MFMAs issue. Partial tiles (and the bias column of the k0 = 0
+// tile) go to the workspace in k_reduce's layout.
+__global__ __launch_bounds__(256, 3) void k_wgrad(WgradArgs A) {
   const int grp = blockIdx.x % A.ngroups, split = blockIdx.x / A.ngroups;
   int nl = 0;
   while (nl + 1 < 2 * MAXL && A.grp0[nl + 1] <= grp) ++nl;
   const NetW& w = A.n[nl / MAXL];
   const int l = nl % MAXL;
-  const int Tk = w.p[l] / 32, Tn = w.p[l + 1] / 32;
+  const int P0 = w.p[l], P1 = w.p[l + 1], Tk = P0 / 32, Tn = P1 / 32, KG = (Tk + 3) / 4;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
-  const int nt = 4 * (grp - A.grp0[nl]) + wave;
+  const int g = grp - A.grp0[nl], nt = 4 * (g / KG) + wave, kt0 = 4 * (g % KG);
   if (nt >= Tn) return;  // (no barrier below)
+  const int nk = min(4, Tk - kt0);
   const int rows = A.batch / A.splits, r0 = split * rows;
-  const float4* dz = reinterpret_cast<const float4*>(A.ws + w.dz[l] + (int64_t)(32 * nt + c) * A.batch + r0 + 4 * h);
-  const float* xb = A.ws + w.x[l] + (int64_t)c * A.batch + r0 + 4 * h;
-  const int64_t xk = (int64_t)32 * A.batch;  // k-tile stride of X (floats)
-  f32x16 acc[8];
+  // octet j of the split: dZ quad at dz + j * P1 * 8, X quads at xb + kk * 256 + j * P0 * 8
+  const float* dz = A.ws + w.dz[l] + rbo(P1, 32 * nt + c, r0 + 4 * h);
+  const float* xb = A.ws + w.x[l] + rbo(P0, 32 * kt0 + c, r0 + 4 * h);
+  const int64_t sd = (int64_t)P1 * 8, sx = (int64_t)P0 * 8;
+  f32x16 acc[4];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) acc[k] = f32x16{};
+  for (int k = 0; k < 4; ++k) acc[k] = f32x16{};
   float bsum = 0.f;
-  const int nj = rows / 8;  // row octets
-  float4 a = dz[0], b[8];
+  const int nj = rows / 8;
+  float4 a = *reinterpret_cast<const float4*>(dz), b[4];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) b[k] = k < Tk ? *reinterpret_cast<const float4*>(xb + k * xk) : float4{};
+  for (int k = 0; k < 4; ++k) b[k] = k < nk ? *reinterpret_cast<const float4*>(xb + k * 256) : float4{};
   for (int j = 0; j < nj; ++j) {
     const float4 u = a;
-    float4 v[8];
+    float4 v[4];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = b[k];
+    for (int k = 0; k < 4; ++k) v[k] = b[k];
     if (j + 1 < nj) {
-      a = dz[2 * j + 2];
+      a = *reinterpret_cast<const float4*>(dz + (j + 1) * sd);
 #pragma unroll
-      for (int k = 0; k < 8; ++k)
-        if (k < Tk) b[k] = *reinterpret_cast<const float4*>(xb + k * xk + 8 * (j + 1));
+      for (int k = 0; k < 4; ++k)
+        if (k < nk) b[k] = *reinterpret_cast<const float4*>(xb + k * 256 + (j + 1) * sx);
     }
 #pragma unroll
-    for (int k = 0; k < 8; ++k)
-      if (k < Tk) {
+    for (int k = 0; k < 4; ++k)
+      if (k < nk) {
         acc[k] = mfma(u.x, v[k].x, acc[k]); acc[k] = mfma(u.y, v[k].y, acc[k]);
         acc[k] = mfma(u.z, v[k].z, acc[k]); acc[k] = mfma(u.w, v[k].w, acc[k]);
       }
@@ -732,12 +744,12 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(WgradArgs A) {
   }
   bsum += __shfl_xor(bsum, 32);
 #pragma unroll
-  for (int k = 0; k < 8; ++k)
-    if (k < Tk) {
-      float* out = A.ws + A.part + ((int64_t)split * A.wtiles + A.tile0[nl] + nt * Tk + k) * PART;
+  for (int k = 0; k < 4; ++k)
+    if (k < nk) {
+      float* out = A.ws + A.part + ((int64_t)split * A.wtiles + A.tile0[nl] + nt * Tk + kt0 + k) * PART;
 #pragma unroll
       for (int r = 0; r < 16; ++r) out[acc_row(r) * 32 + acc_col()] = acc[k][r];  // [n][k]
-      if (k == 0 && h == 0) out[1024 + c] = bsum;
+      if (kt0 + k == 0 && h == 0) out[1024 + c] = bsum;
     }
 }
 
