@@ -113,10 +113,10 @@ Layout make_layout(const zbp_net* a, const zbp_net* c, int B) {
   lo.grp0[2 * MAXL] = g;
   lo.ngroups = g;
   lo.stats = take((int64_t)(B / TR) * NSTAT);
-  // row splits of the weight gradients: ~4 waves per SIMD (k_wgrad), each split >= 256 rows, a
-  // multiple of 8 (row octets)
+  // row splits of the weight gradients: ~8 waves per SIMD (k_wgrad), each split >= 256 rows, a
+  // multiple of 16 (pairs of row octets)
   int s = 1;
-  while (s < 256 && (int64_t)g * 4 * s * 2 <= 4 * 1024 && B / (s * 2) >= 256 && B % (8 * s * 2) == 0) s *= 2;
+  while (s < 256 && (int64_t)g * 4 * s * 2 <= 8 * 1024 && B / (s * 2) >= 256 && B % (16 * s * 2) == 0) s *= 2;
   lo.splits = s;
   lo.part = take((int64_t)s * t * PART);
   lo.scratch = take(64);
@@ -194,13 +194,15 @@ __global__ void k_pack(PackArgs A) {
     const float v = (n < D1 && k < D0) ? A.w[net][l][n * D0 + k] : 0.f;
     wp[e] = v;
     wt[k * P1 + n] = v;
-    // k_rows_reg's A operands: block (output tile, reduction tile), lane (i = output index & 31,
-    // h = reduction index bit 2), 16 floats (reduction index 8 q + 4 h + u -> entry 4 q + u)
+    // k_rows_reg's A operands: blocks in its order (reduction tile outer, output tile inner), in a
+    // block lane (i = output index & 31, h = reduction index bit 2) holds 16 floats (reduction
+    // index 8 q + 4 h + u -> entry j = 4 q + u), stored as [q][lane][u] (a wave's float4 q of
+    // every lane is one contiguous KB: conflict-free ds_read_b128 from the LDS copy)
     {
       const int kk = k & 31, j = 4 * (kk >> 3) + (kk & 3), hh = (kk >> 2) & 1;
-      wr[((int64_t)((n >> 5) * T0 + (k >> 5)) * 64 + (n & 31) + 32 * hh) * 16 + j] = v;
+      wr[(int64_t)((k >> 5) * T1 + (n >> 5)) * 1024 + ((j >> 2) * 64 + (n & 31) + 32 * hh) * 4 + (j & 3)] = v;
       const int nn = n & 31, jb = 4 * (nn >> 3) + (nn & 3), hb = (nn >> 2) & 1;
-      wtr[((int64_t)((k >> 5) * T1 + (n >> 5)) * 64 + (k & 31) + 32 * hb) * 16 + jb] = v;
+      wtr[(int64_t)((n >> 5) * T0 + (k >> 5)) * 1024 + ((jb >> 2) * 64 + (k & 31) + 32 * hb) * 4 + (jb & 3)] = v;
     }
   }
   if (blockIdx.x == 0)
@@ -451,51 +453,76 @@ __device__ __forceinline__ int rr_lane_off(int P) {
 __device__ __forceinline__ float* rr_base(float* buf, int P, int row0) { return buf + (int64_t)(row0 >> 3) * P * 8; }
 __device__ __forceinline__ float* rr_at(float* base, int o, int j) { return base + (32 * o + 8 * (j >> 2) + (j & 3)) * 8; }
 
-// out[o] = sum_i A(o, i) in[i] over the blocks of a lane-ordered image: block (o, i) = 16 floats per
-// lane, the A operands of 16 MFMAs whose B operands are in[i]'s registers. Reduction tiles outer, so
-// consecutive blocks feed different accumulators; block b + 2's operands load while block b issues.
+// out[o] = sum_i A(o, i) in[i] over the blocks of a lane-ordered image: block b = (i, o) (reduction
+// tile outer, so consecutive blocks feed different accumulators) = 16 floats per lane, the A operands
+// of 16 MFMAs whose B operands are in[i]'s registers. The workgroup's four waves (four row tiles)
+// share the weights through LDS: chunks of RR_CB blocks (32 KB) are copied by all 256 threads into
+// one of two LDS buffers while the previous chunk is consumed, one barrier per chunk -- a quarter of
+// the L2 weight traffic of per-wave streaming and LDS instead of L2 latency on the MFMA path.
+constexpr int RR_CB = 8;
+constexpr int RR_LDS_F4 = 2 * RR_CB * 256;  // float4s of the two chunk buffers (64 KB)
 template <int TI, int TO>
-__device__ __forceinline__ void rr_layer(const float* __restrict__ img, const Tile (&in)[TI], Tile (&out)[TO]) {
-  const float4* wl = reinterpret_cast<const float4*>(img) + 4 * (threadIdx.x & 63);
-  constexpr int NB = TI * TO, D = 2;
+__device__ __forceinline__ void rr_layer(const float* __restrict__ img, float4* __restrict__ wl, const Tile (&in)[TI],
+                                         Tile (&out)[TO]) {
+  constexpr int NB = TI * TO, NC = (NB + RR_CB - 1) / RR_CB;
+  const int t = threadIdx.x, lane = t & 63;
+  const float4* g = reinterpret_cast<const float4*>(img);
 #pragma unroll
   for (int o = 0; o < TO; ++o) out[o] = Tile{};
-  float4 buf[D + 1][4];
+  float4 st[RR_CB];  // this thread's share of a chunk in flight: float4 t + 256 m of it
 #pragma unroll
-  for (int b = 0; b < D; ++b)
-    if (b < NB) {
-      const int i = b / TO, o = b % TO;
+  for (int m = 0; m < RR_CB; ++m)
+    if (m < NB) st[m] = g[t + 256 * m];
 #pragma unroll
-      for (int c = 0; c < 4; ++c) buf[b][c] = wl[(o * TI + i) * 256 + c];
+  for (int m = 0; m < RR_CB; ++m)
+    if (m < NB) wl[t + 256 * m] = st[m];
+  __syncthreads();
+  if (NC > 1) {
+#pragma unroll
+    for (int m = 0; m < RR_CB; ++m)
+      if (RR_CB + m < NB) st[m] = g[RR_CB * 256 + t + 256 * m];
+  }
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const float4* cb = wl + (c & 1) * RR_CB * 256 + lane;
+#pragma unroll
+    for (int bb = 0; bb < RR_CB; ++bb) {
+      const int b = c * RR_CB + bb;
+      if (b < NB) {
+        const int i = b / TO, o = b % TO;
+        const float4 w[4] = {cb[bb * 256], cb[bb * 256 + 64], cb[bb * 256 + 128], cb[bb * 256 + 192]};
+        Tile a = out[o];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          a = mfma(w[q].x, in[i][4 * q + 0], a);
+          a = mfma(w[q].y, in[i][4 * q + 1], a);
+          a = mfma(w[q].z, in[i][4 * q + 2], a);
+          a = mfma(w[q].w, in[i][4 * q + 3], a);
+        }
+        out[o] = a;
+      }
     }
+    if (c + 1 < NC) {
+      float4* nb = wl + ((c + 1) & 1) * RR_CB * 256;
 #pragma unroll
-  for (int b = 0; b < NB; ++b) {
-    const int i = b / TO, o = b % TO;
-    if (b + D < NB) {
-      const int i2 = (b + D) / TO, o2 = (b + D) % TO;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) buf[(b + D) % (D + 1)][c] = wl[(o2 * TI + i2) * 256 + c];
+      for (int m = 0; m < RR_CB; ++m)
+        if ((c + 1) * RR_CB + m < NB) nb[t + 256 * m] = st[m];
     }
-    const float4* w = buf[b % (D + 1)];
-    Tile a = out[o];
+    __syncthreads();  // chunk c consumed by every wave, chunk c + 1 in LDS
+    if (c + 2 < NC) {
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      a = mfma(w[c].x, in[i][4 * c + 0], a);
-      a = mfma(w[c].y, in[i][4 * c + 1], a);
-      a = mfma(w[c].z, in[i][4 * c + 2], a);
-      a = mfma(w[c].w, in[i][4 * c + 3], a);
+      for (int m = 0; m < RR_CB; ++m)
+        if ((c + 2) * RR_CB + m < NB) st[m] = g[(c + 2) * RR_CB * 256 + t + 256 * m];
     }
-    out[o] = a;
-    __builtin_amdgcn_sched_barrier(0);  // (keeps the scheduler from hoisting every block's loads)
   }
 }
 
 // forward layer l: + bias, ELU (hidden layers: also X_{l+1} to HBM, feature-major)
 template <int TI, int TO, bool kLast, bool kStore = true>
-__device__ __forceinline__ void rr_forward(const NetW& w, int l, float* __restrict__ ws, int B, int row0,
+__device__ __forceinline__ void rr_forward(const NetW& w, int l, float* __restrict__ ws, float4* __restrict__ wl, int row0,
                                            const Tile (&in)[TI], Tile (&out)[TO]) {
   const int h = (threadIdx.x & 63) >> 5, lo = rr_lane_off(32 * TO);
-  rr_layer<TI, TO>(ws + w.wr[l], in, out);
+  rr_layer<TI, TO>(ws + w.wr[l], wl, in, out);
   const float* bp = ws + w.bp[l];
   float* xb = rr_base(ws + w.x[l + 1], 32 * TO, row0);
 #pragma unroll
@@ -518,10 +545,10 @@ __device__ __forceinline__ void rr_forward(const NetW& w, int l, float* __restri
 
 // backward through layer l >= 1: dZ_{l-1} = (W_l^T dZ_l) * ELU'(X_l), to registers and HBM
 template <int TI, int TO>
-__device__ __forceinline__ void rr_backward(const NetW& w, int l, float* __restrict__ ws, int B, int row0,
+__device__ __forceinline__ void rr_backward(const NetW& w, int l, float* __restrict__ ws, float4* __restrict__ wl, int row0,
                                             const Tile (&dz)[TI], Tile (&out)[TO]) {
   const int lo = rr_lane_off(32 * TO);
-  rr_layer<TI, TO>(ws + w.wtr[l], dz, out);
+  rr_layer<TI, TO>(ws + w.wtr[l], wl, dz, out);
   float* xb = rr_base(ws + w.x[l], 32 * TO, row0);
   float* db = rr_base(ws + w.dz[l - 1], 32 * TO, row0);
 #pragma unroll
@@ -560,9 +587,9 @@ __device__ __forceinline__ void rr_store_dz(const NetW& w, float* __restrict__ w
 // (the [128, 128, 128] nets fit 256 registers: two waves per SIMD)
 template <int T1, int T2, int T3>
 __global__ __launch_bounds__(256, (T1 > 4 || T2 > 4) ? 1 : 2) void k_rows_reg(RowArgs A) {
+  __shared__ float4 wl[RR_LDS_F4];
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
-  const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (tile * TR >= A.B) return;  // (no barriers: whole waves leave)
+  const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);  // (B / 32 a multiple of 4: reg_shape)
   const int row0 = tile * TR, B = A.B;
   const zbp_batch& bt = A.bt;
   const int NA = bt.num_actions;
@@ -577,10 +604,10 @@ __global__ __launch_bounds__(256, (T1 > 4 || T2 > 4) ? 1 : 2) void k_rows_reg(Ro
   {
     Tile x0[1], x1[T1], x2[T2], x3[T3];
     rr_gather(wa, ws, B, row0, bt.obs, bt.obs_dim, row, x0);
-    rr_forward<1, T1, false>(wa, 0, ws, B, row0, x0, x1);
-    rr_forward<T1, T2, false>(wa, 1, ws, B, row0, x1, x2);
-    rr_forward<T2, T3, false>(wa, 2, ws, B, row0, x2, x3);
-    rr_forward<T3, 1, true>(wa, 3, ws, B, row0, x3, z);
+    rr_forward<1, T1, false>(wa, 0, ws, wl, row0, x0, x1);
+    rr_forward<T1, T2, false>(wa, 1, ws, wl, row0, x1, x2);
+    rr_forward<T2, T3, false>(wa, 2, ws, wl, row0, x2, x3);
+    rr_forward<T3, 1, true>(wa, 3, ws, wl, row0, x3, z);
   }
   Tile dz[1];
   {
@@ -638,9 +665,9 @@ __global__ __launch_bounds__(256, (T1 > 4 || T2 > 4) ? 1 : 2) void k_rows_reg(Ro
   }
   {
     Tile d3[T3], d2[T2], d1[T1];
-    rr_backward<1, T3>(wa, 3, ws, B, row0, dz, d3);
-    rr_backward<T3, T2>(wa, 2, ws, B, row0, d3, d2);
-    rr_backward<T2, T1>(wa, 1, ws, B, row0, d2, d1);
+    rr_backward<1, T3>(wa, 3, ws, wl, row0, dz, d3);
+    rr_backward<T3, T2>(wa, 2, ws, wl, row0, d3, d2);
+    rr_backward<T2, T1>(wa, 1, ws, wl, row0, d2, d1);
   }
 
   // ---- critic: forward, clipped value loss, backward
@@ -648,10 +675,10 @@ __global__ __launch_bounds__(256, (T1 > 4 || T2 > 4) ? 1 : 2) void k_rows_reg(Ro
   {
     Tile x0[1], x1[T1], x2[T2], x3[T3];
     rr_gather(wc, ws, B, row0, bt.critic_obs, bt.critic_obs_dim, row, x0);
-    rr_forward<1, T1, false>(wc, 0, ws, B, row0, x0, x1);
-    rr_forward<T1, T2, false>(wc, 1, ws, B, row0, x1, x2);
-    rr_forward<T2, T3, false>(wc, 2, ws, B, row0, x2, x3);
-    rr_forward<T3, 1, true>(wc, 3, ws, B, row0, x3, z);
+    rr_forward<1, T1, false>(wc, 0, ws, wl, row0, x0, x1);
+    rr_forward<T1, T2, false>(wc, 1, ws, wl, row0, x1, x2);
+    rr_forward<T2, T3, false>(wc, 2, ws, wl, row0, x2, x3);
+    rr_forward<T3, 1, true>(wc, 3, ws, wl, row0, x3, z);
   }
   {
     const float v = __shfl(z[0][0], r), tv = bt.values[row], ret = bt.returns[row], clip = A.lc.clip_param;
@@ -677,9 +704,9 @@ __global__ __launch_bounds__(256, (T1 > 4 || T2 > 4) ? 1 : 2) void k_rows_reg(Ro
   }
   {
     Tile d3[T3], d2[T2], d1[T1];
-    rr_backward<1, T3>(wc, 3, ws, B, row0, dz, d3);
-    rr_backward<T3, T2>(wc, 2, ws, B, row0, d3, d2);
-    rr_backward<T2, T1>(wc, 1, ws, B, row0, d2, d1);
+    rr_backward<1, T3>(wc, 3, ws, wl, row0, dz, d3);
+    rr_backward<T3, T2>(wc, 2, ws, wl, row0, d3, d2);
+    rr_backward<T2, T1>(wc, 1, ws, wl, row0, d2, d1);
   }
 }
 
@@ -719,21 +746,14 @@ __global__ __launch_bounds__(256, 3) void k_wgrad(WgradArgs A) {
 #pragma unroll
   for (int k = 0; k < 4; ++k) acc[k] = f32x16{};
   float bsum = 0.f;
-  const int nj = rows / 8;
-  float4 a = *reinterpret_cast<const float4*>(dz), b[4];
+  const int nj = rows / 8;  // (even: make_layout)
+  // two octets in flight while two are consumed
+  auto load = [&](int j, float4& a, float4 (&b)[4]) {
+    a = *reinterpret_cast<const float4*>(dz + j * sd);
 #pragma unroll
-  for (int k = 0; k < 4; ++k) b[k] = k < nk ? *reinterpret_cast<const float4*>(xb + k * 256) : float4{};
-  for (int j = 0; j < nj; ++j) {
-    const float4 u = a;
-    float4 v[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) v[k] = b[k];
-    if (j + 1 < nj) {
-      a = *reinterpret_cast<const float4*>(dz + (j + 1) * sd);
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (k < nk) b[k] = *reinterpret_cast<const float4*>(xb + k * 256 + (j + 1) * sx);
-    }
+    for (int k = 0; k < 4; ++k) b[k] = k < nk ? *reinterpret_cast<const float4*>(xb + k * 256 + j * sx) : float4{};
+  };
+  auto step = [&](const float4 u, const float4 (&v)[4]) {
 #pragma unroll
     for (int k = 0; k < 4; ++k)
       if (k < nk) {
@@ -741,6 +761,21 @@ __global__ __launch_bounds__(256, 3) void k_wgrad(WgradArgs A) {
         acc[k] = mfma(u.z, v[k].z, acc[k]); acc[k] = mfma(u.w, v[k].w, acc[k]);
       }
     bsum += (u.x + u.y) + (u.z + u.w);
+  };
+  float4 a0, a1, b0[4], b1[4];
+  load(0, a0, b0);
+  load(1, a1, b1);
+  for (int j = 0; j < nj; j += 2) {
+    const float4 u0 = a0, u1 = a1;
+    float4 v0[4], v1[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { v0[k] = b0[k]; v1[k] = b1[k]; }
+    if (j + 2 < nj) {
+      load(j + 2, a0, b0);
+      load(j + 3, a1, b1);
+    }
+    step(u0, v0);
+    step(u1, v1);
   }
   bsum += __shfl_xor(bsum, 32);
 #pragma unroll
@@ -943,9 +978,9 @@ __global__ __launch_bounds__(256) void k_act(ActArgs A) {
 // k_act on the register-resident forward (k_rows_reg's shapes): one wave per 32 rows, no LDS
 template <int T1, int T2, int T3>
 __global__ __launch_bounds__(256, (T1 > 4 || T2 > 4) ? 1 : 2) void k_act_reg(ActArgs A) {
+  __shared__ float4 wl[RR_LDS_F4];
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
-  const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * TR;
-  if (row0 >= A.rows) return;
+  const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * TR;  // (waves past the rows run on zeros, store nothing)
   const int64_t row = row0 + r;
   const bool ok = row < A.rows;
   const int na = A.na;
@@ -964,10 +999,10 @@ __global__ __launch_bounds__(256, (T1 > 4 || T2 > 4) ? 1 : 2) void k_act_reg(Act
       x0[0][j] = v;
       if (ok && k < dim) st[k] = v;
     }
-    rr_forward<1, T1, false, false>(w, 0, A.ws, 0, 0, x0, x1);
-    rr_forward<T1, T2, false, false>(w, 1, A.ws, 0, 0, x1, x2);
-    rr_forward<T2, T3, false, false>(w, 2, A.ws, 0, 0, x2, x3);
-    rr_forward<T3, 1, true, false>(w, 3, A.ws, 0, 0, x3, z);
+    rr_forward<1, T1, false, false>(w, 0, A.ws, wl, 0, x0, x1);
+    rr_forward<T1, T2, false, false>(w, 1, A.ws, wl, 0, x1, x2);
+    rr_forward<T2, T3, false, false>(w, 2, A.ws, wl, 0, x2, x3);
+    rr_forward<T3, 1, true, false>(w, 3, A.ws, wl, 0, x3, z);
     if (net == 0) {
       // lane (r, h) holds actions 8 q + 4 h + u of row r
       const float kLog2Pi = 0.91893853320467274178f;  // log(sqrt(2 pi))
@@ -1103,7 +1138,8 @@ __global__ __launch_bounds__(256) void k_adv_norm(float* __restrict__ adv, int64
 
 // k_rows_reg instantiation for the nets' shape: 1 = hidden [256, 256, 128], 2 = [128, 128, 128] (both
 // nets; inputs / outputs <= 32), 0 = none (k_rows)
-int reg_shape(const Layout& lo) {
+int reg_shape(const Layout& lo, int B = 128) {
+  if (B % (4 * TR)) return 0;  // (k_rows_reg: whole workgroups of four row tiles)
   const char* e = getenv("ZBP_ROWS");  // (read per call: tests switch it)
   if (e && strcmp(e, "lds") == 0) return 0;
   const NetW &a = lo.n[0], &c = lo.n[1];
@@ -1204,7 +1240,7 @@ int zbp_minibatch(const zbp_net* actor, const zbp_net* critic, const float* std_
     lds_set = true;
   }
   // the register-resident row kernel for the shipped shapes (ZBP_ROWS=lds: the LDS one, for A/Bs)
-  const int shape = reg_shape(lo);
+  const int shape = reg_shape(lo, B);
   if (shape == 1)
     k_rows_reg<8, 8, 4><<<(B / TR + 3) / 4, 256, 0, s>>>(R);
   else if (shape == 2)
