@@ -188,21 +188,19 @@ __global__ void k_pack(PackArgs A) {
   float* wt = A.ws + w.wt[l];
   float* wr = A.ws + w.wr[l];
   float* wtr = A.ws + w.wtr[l];
-  const int T0 = P0 / 32, T1 = P1 / 32;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < P0 * P1; e += gridDim.x * blockDim.x) {
     const int n = e / P0, k = e % P0;
     const float v = (n < D1 && k < D0) ? A.w[net][l][n * D0 + k] : 0.f;
     wp[e] = v;
     wt[k * P1 + n] = v;
-    // k_rows_reg's A operands: blocks in its order (reduction tile outer, output tile inner), in a
-    // block lane (i = output index & 31, h = reduction index bit 2) holds 16 floats (reduction
-    // index 8 q + 4 h + u -> entry j = 4 q + u), stored as [q][lane][u] (a wave's float4 q of
-    // every lane is one contiguous KB: conflict-free ds_read_b128 from the LDS copy)
+    // k_rows_reg's A operands (v_mfma_f32_16x16x4_f32): 16 x 16 blocks in its order (reduction
+    // tile outer, output tile inner); in a block, lane (output index & 15) + 16 g holds the four
+    // reduction indices 4 g + u as one float4 (a block is one contiguous KB: conflict-free
+    // ds_read_b128 from the LDS copy)
     {
-      const int kk = k & 31, j = 4 * (kk >> 3) + (kk & 3), hh = (kk >> 2) & 1;
-      wr[(int64_t)((k >> 5) * T1 + (n >> 5)) * 1024 + ((j >> 2) * 64 + (n & 31) + 32 * hh) * 4 + (j & 3)] = v;
-      const int nn = n & 31, jb = 4 * (nn >> 3) + (nn & 3), hb = (nn >> 2) & 1;
-      wtr[(int64_t)((n >> 5) * T0 + (k >> 5)) * 1024 + ((jb >> 2) * 64 + (k & 31) + 32 * hb) * 4 + (jb & 3)] = v;
+      const int T1h = P1 / 16, T0h = P0 / 16;
+      wr[(int64_t)((k >> 4) * T1h + (n >> 4)) * 256 + ((n & 15) + 16 * ((k >> 2) & 3)) * 4 + (k & 3)] = v;
+      wtr[(int64_t)((n >> 4) * T0h + (k >> 4)) * 256 + ((k & 15) + 16 * ((n >> 2) & 3)) * 4 + (n & 3)] = v;
     }
   }
   if (blockIdx.x == 0)
@@ -428,169 +426,187 @@ __global__ __launch_bounds__(ROW_THREADS) void k_rows(RowArgs A) {
 }
 
 // ------------------------------------------------------------------------------- k_rows_reg
-// k_rows for the shipped net shapes (three hidden layers of 32 T1, 32 T2, 32 T3 units, inputs and
-// outputs <= 32: rsl_rl's [128, 128, 128] and the stand-up / v2 [256, 256, 128]), one WAVE per 32-row
-// tile and the activations in registers: no LDS, no barriers, every wave runs its tile through both
-// nets on its own. A layer is the transposed product Z^T = W X^T on v_mfma_f32_32x32x2_f32 with the
-// weights as the A operand (lane-ordered images wr / wtr, k_pack) and the activations as the B
-// operand straight from the previous layer's accumulators: an accumulator tile holds, in lane
-// (row r = lane & 31, h = lane >> 5), register 4 q + u, feature 8 q + 4 h + u of row r -- exactly the
-// B operand of 16 MFMAs whose reduction index runs over those features in that order. One wave per
-// SIMD (up to 512 VGPRs + AGPRs): a 256-wide layer keeps 8 input + 8 output tiles (256 registers)
-// live. X_l and dZ_l still go to HBM feature-major for k_wgrad; the backward pass reads X_l back for
-// ELU'.
-typedef f32x16 Tile;
+// k_rows for the shipped net shapes (three hidden layers of 16 T1, 16 T2, 16 T3 units, inputs and
+// outputs <= 32: rsl_rl's [128, 128, 128] and the stand-up / v2 [256, 256, 128]), one WAVE per 16-row
+// tile and the activations in registers. A layer is the transposed product Z^T = W X^T on
+// v_mfma_f32_16x16x4_f32 with the weights as the A operand and the activations as the B operand
+// straight from the previous layer's accumulators: an accumulator tile (4 registers) holds, in lane
+// (row r = lane & 15, g = lane >> 4), register u, feature 4 g + u of row r -- exactly the B operand
+// of 4 MFMAs whose reduction index runs over the tile's 16 features. A 256-wide layer keeps 16 input
+// + 16 output tiles (128 registers) live, so two waves share each SIMD and cover each other's
+// epilogues (bias, ELU, the row-buffer stores) and memory waits. The workgroup's four waves share
+// the weights through LDS (double-buffered 32 KB chunks of 32 blocks, one barrier per chunk). X_l
+// and dZ_l go to HBM octet-blocked (rbo) for k_wgrad; the backward pass reads X_l back for ELU'.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef f32x4 Tile;
 
-__device__ __forceinline__ int rr_feat(int j) { return 8 * (j >> 2) + 4 * ((threadIdx.x & 63) >> 5) + (j & 3); }
-// row buffers (rbo): element (feature 32 o + 8 q + 4 h + u, row row0 + r) of a P-feature buffer at
-// base = buffer + rbo(P, 0, row0) as base[uniform part (32 o + 8 q + u) 8] + lane part
-// ((r >> 3) P 8 + 32 h + (r & 7)): the uniform part stays scalar (one SGPR pair per access), the lane
-// part one 32-bit VGPR offset
+__device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ int rr_g() { return (threadIdx.x & 63) >> 4; }
+// row buffers (rbo): element (feature 16 o + 4 g + u, row row0 + r) of a P-feature buffer at
+// base = buffer + rbo(P, 0, row0) as base[uniform part (16 o + u) 8] + lane part
+// ((r >> 3) P 8 + 32 g + (r & 7)): the uniform part stays scalar, the lane part one VGPR offset
 __device__ __forceinline__ int rr_lane_off(int P) {
-  const int r = threadIdx.x & 31;
-  return (r >> 3) * P * 8 + 32 * ((threadIdx.x & 63) >> 5) + (r & 7);
+  const int r = threadIdx.x & 15;
+  return (r >> 3) * P * 8 + 32 * rr_g() + (r & 7);
 }
 __device__ __forceinline__ float* rr_base(float* buf, int P, int row0) { return buf + (int64_t)(row0 >> 3) * P * 8; }
-__device__ __forceinline__ float* rr_at(float* base, int o, int j) { return base + (32 * o + 8 * (j >> 2) + (j & 3)) * 8; }
+__device__ __forceinline__ float* rr_at(float* base, int o, int u) { return base + (16 * o + u) * 8; }
 
 // out[o] = sum_i A(o, i) in[i] over the blocks of a lane-ordered image: block b = (i, o) (reduction
-// tile outer, so consecutive blocks feed different accumulators) = 16 floats per lane, the A operands
-// of 16 MFMAs whose B operands are in[i]'s registers. The workgroup's four waves (four row tiles)
-// share the weights through LDS: chunks of RR_CB blocks (32 KB) are copied by all 256 threads into
-// one of two LDS buffers while the previous chunk is consumed, one barrier per chunk -- a quarter of
-// the L2 weight traffic of per-wave streaming and LDS instead of L2 latency on the MFMA path.
-constexpr int RR_CB = 8;
-constexpr int RR_LDS_F4 = 2 * RR_CB * 256;  // float4s of the two chunk buffers (64 KB)
+// tile outer: consecutive blocks feed different accumulators) = one float4 per lane, the A operands
+// of 4 MFMAs whose B operands are in[i]'s registers, read from the workgroup's LDS copy of the
+// current chunk while the next chunk is in flight from L2.
+constexpr int RR_CB = 32;                     // blocks per chunk (32 KB)
+constexpr int RR_LDS_F4 = 2 * RR_CB * 64;     // float4s of the two chunk buffers (64 KB)
+constexpr int RR_WG = 256;                    // threads per workgroup (4 waves, 4 row tiles)
 template <int TI, int TO>
 __device__ __forceinline__ void rr_layer(const float* __restrict__ img, float4* __restrict__ wl, const Tile (&in)[TI],
                                          Tile (&out)[TO]) {
-  constexpr int NB = TI * TO, NC = (NB + RR_CB - 1) / RR_CB;
+  constexpr int NB = TI * TO, NC = (NB + RR_CB - 1) / RR_CB, PER = RR_CB * 64 / RR_WG;  // float4s per thread per chunk
   const int t = threadIdx.x, lane = t & 63;
   const float4* g = reinterpret_cast<const float4*>(img);
+  constexpr int NF = NB * 64;  // float4s of the image
 #pragma unroll
   for (int o = 0; o < TO; ++o) out[o] = Tile{};
-  float4 st[RR_CB];  // this thread's share of a chunk in flight: float4 t + 256 m of it
+  float4 st[PER];
 #pragma unroll
-  for (int m = 0; m < RR_CB; ++m)
-    if (m < NB) st[m] = g[t + 256 * m];
+  for (int m = 0; m < PER; ++m)
+    if (m * RR_WG < NF) st[m] = (t + m * RR_WG < NF) ? g[t + m * RR_WG] : float4{};
 #pragma unroll
-  for (int m = 0; m < RR_CB; ++m)
-    if (m < NB) wl[t + 256 * m] = st[m];
+  for (int m = 0; m < PER; ++m)
+    if (m * RR_WG < NF) wl[t + m * RR_WG] = st[m];
   __syncthreads();
   if (NC > 1) {
 #pragma unroll
-    for (int m = 0; m < RR_CB; ++m)
-      if (RR_CB + m < NB) st[m] = g[RR_CB * 256 + t + 256 * m];
+    for (int m = 0; m < PER; ++m) {
+      const int e = RR_CB * 64 + t + m * RR_WG;
+      if (RR_CB * 64 + m * RR_WG < NF) st[m] = e < NF ? g[e] : float4{};
+    }
   }
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
-    const float4* cb = wl + (c & 1) * RR_CB * 256 + lane;
+    const float4* cb = wl + (c & 1) * RR_CB * 64 + lane;
 #pragma unroll
     for (int bb = 0; bb < RR_CB; ++bb) {
       const int b = c * RR_CB + bb;
       if (b < NB) {
         const int i = b / TO, o = b % TO;
-        const float4 w[4] = {cb[bb * 256], cb[bb * 256 + 64], cb[bb * 256 + 128], cb[bb * 256 + 192]};
+        const float4 w = cb[bb * 64];
         Tile a = out[o];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          a = mfma(w[q].x, in[i][4 * q + 0], a);
-          a = mfma(w[q].y, in[i][4 * q + 1], a);
-          a = mfma(w[q].z, in[i][4 * q + 2], a);
-          a = mfma(w[q].w, in[i][4 * q + 3], a);
-        }
+        a = mfma16(w.x, in[i][0], a);
+        a = mfma16(w.y, in[i][1], a);
+        a = mfma16(w.z, in[i][2], a);
+        a = mfma16(w.w, in[i][3], a);
         out[o] = a;
       }
     }
     if (c + 1 < NC) {
-      float4* nb = wl + ((c + 1) & 1) * RR_CB * 256;
+      float4* nb = wl + ((c + 1) & 1) * RR_CB * 64;
 #pragma unroll
-      for (int m = 0; m < RR_CB; ++m)
-        if ((c + 1) * RR_CB + m < NB) nb[t + 256 * m] = st[m];
+      for (int m = 0; m < PER; ++m)
+        if ((c + 1) * RR_CB * 64 + m * RR_WG < NF) nb[t + m * RR_WG] = st[m];
     }
     __syncthreads();  // chunk c consumed by every wave, chunk c + 1 in LDS
     if (c + 2 < NC) {
 #pragma unroll
-      for (int m = 0; m < RR_CB; ++m)
-        if ((c + 2) * RR_CB + m < NB) st[m] = g[(c + 2) * RR_CB * 256 + t + 256 * m];
+      for (int m = 0; m < PER; ++m) {
+        const int e = (c + 2) * RR_CB * 64 + t + m * RR_WG;
+        if ((c + 2) * RR_CB * 64 + m * RR_WG < NF) st[m] = e < NF ? g[e] : float4{};
+      }
     }
   }
 }
 
-// forward layer l: + bias, ELU (hidden layers: also X_{l+1} to HBM, feature-major)
+// forward layer l: + bias, ELU (hidden layers: also X_{l+1} to HBM)
 template <int TI, int TO, bool kLast, bool kStore = true>
 __device__ __forceinline__ void rr_forward(const NetW& w, int l, float* __restrict__ ws, float4* __restrict__ wl, int row0,
                                            const Tile (&in)[TI], Tile (&out)[TO]) {
-  const int h = (threadIdx.x & 63) >> 5, lo = rr_lane_off(32 * TO);
+  const int lo = rr_lane_off(16 * TO);
   rr_layer<TI, TO>(ws + w.wr[l], wl, in, out);
-  const float* bp = ws + w.bp[l];
-  float* xb = rr_base(ws + w.x[l + 1], 32 * TO, row0);
+  const float* bp = ws + w.bp[l] + 4 * rr_g();
+  float* xb = rr_base(ws + w.x[l + 1], 16 * TO, row0);
 #pragma unroll
-  for (int o = 0; o < TO; ++o)
+  for (int o = 0; o < TO; ++o) {
+    const float4 bq = *reinterpret_cast<const float4*>(bp + 16 * o);
+    const float bv[4] = {bq.x, bq.y, bq.z, bq.w};
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float4 bq = *reinterpret_cast<const float4*>(bp + 32 * o + 8 * q + 4 * h);
-      const float bv[4] = {bq.x, bq.y, bq.z, bq.w};
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        float v = out[o][4 * q + u] + bv[u];
-        if (!kLast) {
-          v = v > 0.f ? v : expf(v) - 1.f;  // ELU(alpha = 1), as ATen's elu kernel
-          if (kStore) rr_at(xb, o, 4 * q + u)[lo] = v;
-        }
-        out[o][4 * q + u] = v;
+    for (int u = 0; u < 4; ++u) {
+      float v = out[o][u] + bv[u];
+      if (!kLast) {
+        v = v > 0.f ? v : expf(v) - 1.f;  // ELU(alpha = 1), as ATen's elu kernel
+        if (kStore) rr_at(xb, o, u)[lo] = v;
       }
+      out[o][u] = v;
     }
+  }
 }
 
 // backward through layer l >= 1: dZ_{l-1} = (W_l^T dZ_l) * ELU'(X_l), to registers and HBM
 template <int TI, int TO>
 __device__ __forceinline__ void rr_backward(const NetW& w, int l, float* __restrict__ ws, float4* __restrict__ wl, int row0,
                                             const Tile (&dz)[TI], Tile (&out)[TO]) {
-  const int lo = rr_lane_off(32 * TO);
+  const int lo = rr_lane_off(16 * TO);
   rr_layer<TI, TO>(ws + w.wtr[l], wl, dz, out);
-  float* xb = rr_base(ws + w.x[l], 32 * TO, row0);
-  float* db = rr_base(ws + w.dz[l - 1], 32 * TO, row0);
+  float* xb = rr_base(ws + w.x[l], 16 * TO, row0);
+  float* db = rr_base(ws + w.dz[l - 1], 16 * TO, row0);
 #pragma unroll
   for (int o = 0; o < TO; ++o)
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const float x = rr_at(xb, o, j)[lo];
-      const float g = out[o][j] * (x > 0.f ? 1.f : x + 1.f);  // ELU'(z) = exp(z) = x + 1 for z <= 0
-      out[o][j] = g;
-      rr_at(db, o, j)[lo] = g;
+    for (int u = 0; u < 4; ++u) {
+      const float x = rr_at(xb, o, u)[lo];
+      const float gr = out[o][u] * (x > 0.f ? 1.f : x + 1.f);  // ELU'(z) = exp(z) = x + 1 for z <= 0
+      out[o][u] = gr;
+      rr_at(db, o, u)[lo] = gr;
     }
 }
 
 // the tile's input rows (through the permutation) as the first layer's B operand, zero-padded to 32
-__device__ __forceinline__ void rr_gather(const NetW& w, float* __restrict__ ws, int B, int row0, const float* src, int dim,
-                                          int64_t row, Tile (&x)[1]) {
+__device__ __forceinline__ void rr_gather(const NetW& w, float* __restrict__ ws, int row0, const float* src, int dim,
+                                          int64_t row, Tile (&x)[2]) {
   const int lo = rr_lane_off(32);
   float* xb = rr_base(ws + w.x[0], 32, row0);
   const float* sr = src + row * dim;
 #pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const int k = rr_feat(j);
-    const float v = k < dim ? sr[k] : 0.f;
-    x[0][j] = v;
-    rr_at(xb, 0, j)[lo] = v;
-  }
+  for (int o = 0; o < 2; ++o)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = 16 * o + 4 * rr_g() + u;
+      const float v = k < dim ? sr[k] : 0.f;
+      x[o][u] = v;
+      rr_at(xb, o, u)[lo] = v;
+    }
 }
 
-__device__ __forceinline__ void rr_store_dz(const NetW& w, float* __restrict__ ws, int B, int row0, const Tile& d) {
+__device__ __forceinline__ void rr_store_dz(const NetW& w, float* __restrict__ ws, int row0, const Tile (&d)[2]) {
   const int lo = rr_lane_off(32);
   float* db = rr_base(ws + w.dz[w.L - 1], 32, row0);
 #pragma unroll
-  for (int j = 0; j < 16; ++j) rr_at(db, 0, j)[lo] = d[j];
+  for (int o = 0; o < 2; ++o)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) rr_at(db, o, u)[lo] = d[o][u];
 }
 
-// (the [128, 128, 128] nets fit 256 registers: two waves per SIMD)
+// sum over the 16 rows of a wave (lanes with the same g)
+__device__ __forceinline__ float rr_row_sum(float v) {
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o);
+  return v;
+}
+// sum over the 4 feature groups of a row (lanes r, r + 16, r + 32, r + 48)
+__device__ __forceinline__ float rr_feat_sum(float v) {
+  v += __shfl_xor(v, 16);
+  return v + __shfl_xor(v, 32);
+}
+
+constexpr int RR_TR = 16;  // rows per wave
 template <int T1, int T2, int T3>
-__global__ __launch_bounds__(256, (T1 > 4 || T2 > 4) ? 1 : 2) void k_rows_reg(RowArgs A) {
+__global__ __launch_bounds__(RR_WG, 2) void k_rows_reg(RowArgs A) {
   __shared__ float4 wl[RR_LDS_F4];
-  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
-  const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);  // (B / 32 a multiple of 4: reg_shape)
-  const int row0 = tile * TR, B = A.B;
+  const int lane = threadIdx.x & 63, r = lane & 15, gq = lane >> 4;
+  const int tile = blockIdx.x * (RR_WG / 64) + (threadIdx.x >> 6);  // (B a multiple of 64: reg_shape)
+  const int row0 = tile * RR_TR;
   const zbp_batch& bt = A.bt;
   const int NA = bt.num_actions;
   const float invB = 1.f / (float)bt.batch;
@@ -600,26 +616,26 @@ __global__ __launch_bounds__(256, (T1 > 4 || T2 > 4) ? 1 : 2) void k_rows_reg(Ro
 
   // ---- actor: forward, Gaussian log-prob, clipped surrogate, KL; dL/dmu into dZ of the output
   const NetW& wa = A.n[0];
-  Tile z[1];
+  Tile z[2];
   {
-    Tile x0[1], x1[T1], x2[T2], x3[T3];
-    rr_gather(wa, ws, B, row0, bt.obs, bt.obs_dim, row, x0);
-    rr_forward<1, T1, false>(wa, 0, ws, wl, row0, x0, x1);
+    Tile x0[2], x1[T1], x2[T2], x3[T3];
+    rr_gather(wa, ws, row0, bt.obs, bt.obs_dim, row, x0);
+    rr_forward<2, T1, false>(wa, 0, ws, wl, row0, x0, x1);
     rr_forward<T1, T2, false>(wa, 1, ws, wl, row0, x1, x2);
     rr_forward<T2, T3, false>(wa, 2, ws, wl, row0, x2, x3);
-    rr_forward<T3, 1, true>(wa, 3, ws, wl, row0, x3, z);
+    rr_forward<T3, 2, true>(wa, 3, ws, wl, row0, x3, z);
   }
-  Tile dz[1];
+  Tile dz[2];
   {
-    // lane (r, h) holds actions 8 q + 4 h + u of row r: per-half partial sums, then the halves'
+    // lane (r, g) holds actions 4 g + u (tile 0) and 16 + 4 g + u (tile 1) of row r
     const float kLog2Pi = 0.91893853320467274178f;  // log(sqrt(2 pi))
-    float lp = 0.f, kl = 0.f, diff[16];
+    float lp = 0.f, kl = 0.f, diff[8];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int n = rr_feat(j);
+    for (int j = 0; j < 8; ++j) {
+      const int n = 16 * (j >> 2) + 4 * gq + (j & 3);
       diff[j] = 0.f;
       if (n < NA) {
-        const float mu = z[0][j], s = A.std_param[n];
+        const float mu = z[j >> 2][j & 3], s = A.std_param[n];
         const float d = bt.actions[row * NA + n] - mu;
         diff[j] = d;
         lp += -(d * d) / (2.f * (s * s)) - logf(s) - kLog2Pi;
@@ -627,8 +643,8 @@ __global__ __launch_bounds__(256, (T1 > 4 || T2 > 4) ? 1 : 2) void k_rows_reg(Ro
         kl += logf(s / os + 1e-5f) + (os * os + (om - mu) * (om - mu)) / (2.f * (s * s)) - 0.5f;
       }
     }
-    lp += __shfl_xor(lp, 32);
-    kl += __shfl_xor(kl, 32);
+    lp = rr_feat_sum(lp);
+    kl = rr_feat_sum(kl);
     const float adv = bt.advantages[row], clip = A.lc.clip_param;
     const float ratio = expf(lp - bt.log_prob[row]);
     const float rc = fminf(fmaxf(ratio, 1.f - clip), 1.f + clip);
@@ -640,23 +656,20 @@ __global__ __launch_bounds__(256, (T1 > 4 || T2 > 4) ? 1 : 2) void k_rows_reg(Ro
     const float w1 = s1 > s2 ? 1.f : (s1 < s2 ? 0.f : 0.5f);
     const float g = (w1 * -adv + (1.f - w1) * -adv * in) * ratio * invB;  // dL / dlog_prob
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int n = rr_feat(j);
+    for (int j = 0; j < 8; ++j) {
+      const int n = 16 * (j >> 2) + 4 * gq + (j & 3);
       float d = 0.f, sg = 0.f;
       if (n < NA) {
         const float s = A.std_param[n];
         d = g * diff[j] / (s * s);
         sg = g * (diff[j] * diff[j] / (s * s * s) - 1.f / s);
       }
-      dz[0][j] = d;
-      if (j < 8) {  // actions < 16: the std gradient summed over the tile's rows (one half's lanes)
-#pragma unroll
-        for (int o = 1; o < 32; o <<= 1) sg += __shfl_xor(sg, o);
-        if (r == 0 && n < NA) st[3 + n] = sg;
-      }
+      dz[j >> 2][j & 3] = d;
+      sg = rr_row_sum(sg);  // the std gradient summed over the tile's rows
+      if (r == 0 && n < NA) st[3 + n] = sg;
     }
-    rr_store_dz(wa, ws, B, row0, dz[0]);
-    const float su = wave_sum(h == 0 ? surr : 0.f), ks = wave_sum(h == 0 ? kl : 0.f);
+    rr_store_dz(wa, ws, row0, dz);
+    const float su = wave_sum(gq == 0 ? surr : 0.f), ks = wave_sum(gq == 0 ? kl : 0.f);
     if (lane == 0) {
       st[0] = su;
       st[2] = ks;
@@ -665,7 +678,7 @@ __global__ __launch_bounds__(256, (T1 > 4 || T2 > 4) ? 1 : 2) void k_rows_reg(Ro
   }
   {
     Tile d3[T3], d2[T2], d1[T1];
-    rr_backward<1, T3>(wa, 3, ws, wl, row0, dz, d3);
+    rr_backward<2, T3>(wa, 3, ws, wl, row0, dz, d3);
     rr_backward<T3, T2>(wa, 2, ws, wl, row0, d3, d2);
     rr_backward<T2, T1>(wa, 1, ws, wl, row0, d2, d1);
   }
@@ -673,12 +686,12 @@ __global__ __launch_bounds__(256, (T1 > 4 || T2 > 4) ? 1 : 2) void k_rows_reg(Ro
   // ---- critic: forward, clipped value loss, backward
   const NetW& wc = A.n[1];
   {
-    Tile x0[1], x1[T1], x2[T2], x3[T3];
-    rr_gather(wc, ws, B, row0, bt.critic_obs, bt.critic_obs_dim, row, x0);
-    rr_forward<1, T1, false>(wc, 0, ws, wl, row0, x0, x1);
+    Tile x0[2], x1[T1], x2[T2], x3[T3];
+    rr_gather(wc, ws, row0, bt.critic_obs, bt.critic_obs_dim, row, x0);
+    rr_forward<2, T1, false>(wc, 0, ws, wl, row0, x0, x1);
     rr_forward<T1, T2, false>(wc, 1, ws, wl, row0, x1, x2);
     rr_forward<T2, T3, false>(wc, 2, ws, wl, row0, x2, x3);
-    rr_forward<T3, 1, true>(wc, 3, ws, wl, row0, x3, z);
+    rr_forward<T3, 2, true>(wc, 3, ws, wl, row0, x3, z);
   }
   {
     const float v = __shfl(z[0][0], r), tv = bt.values[row], ret = bt.returns[row], clip = A.lc.clip_param;
@@ -697,14 +710,14 @@ __global__ __launch_bounds__(256, (T1 > 4 || T2 > 4) ? 1 : 2) void k_rows_reg(Ro
     }
     dv *= A.lc.value_loss_coef * invB;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) dz[0][j] = (h == 0 && j == 0) ? dv : 0.f;
-    rr_store_dz(wc, ws, B, row0, dz[0]);
-    const float vs = wave_sum(h == 0 ? vl : 0.f);
+    for (int j = 0; j < 8; ++j) dz[j >> 2][j & 3] = (gq == 0 && j == 0) ? dv : 0.f;
+    rr_store_dz(wc, ws, row0, dz);
+    const float vs = wave_sum(gq == 0 ? vl : 0.f);
     if (lane == 0) st[1] = vs;
   }
   {
     Tile d3[T3], d2[T2], d1[T1];
-    rr_backward<1, T3>(wc, 3, ws, wl, row0, dz, d3);
+    rr_backward<2, T3>(wc, 3, ws, wl, row0, dz, d3);
     rr_backward<T3, T2>(wc, 2, ws, wl, row0, d3, d2);
     rr_backward<T2, T1>(wc, 1, ws, wl, row0, d2, d1);
   }
@@ -975,43 +988,44 @@ __global__ __launch_bounds__(256) void k_act(ActArgs A) {
   if (tid < TR && row0 + tid < A.rows) A.s_val[row0 + tid] = lds[A.lds_out + tid * 33];
 }
 
-// k_act on the register-resident forward (k_rows_reg's shapes): one wave per 32 rows, no LDS
+// k_act on the register-resident forward (k_rows_reg's shapes): one wave per 16 rows, the weights
+// shared through LDS
 template <int T1, int T2, int T3>
-__global__ __launch_bounds__(256, (T1 > 4 || T2 > 4) ? 1 : 2) void k_act_reg(ActArgs A) {
+__global__ __launch_bounds__(RR_WG, 2) void k_act_reg(ActArgs A) {
   __shared__ float4 wl[RR_LDS_F4];
-  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
-  const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * TR;  // (waves past the rows run on zeros, store nothing)
+  const int lane = threadIdx.x & 63, r = lane & 15, gq = lane >> 4;
+  const int row0 = (blockIdx.x * (RR_WG / 64) + (threadIdx.x >> 6)) * RR_TR;  // (waves past the rows run on zeros, store nothing)
   const int64_t row = row0 + r;
   const bool ok = row < A.rows;
   const int na = A.na;
-  Tile z[1];
+  Tile z[2];
 #pragma unroll
   for (int net = 0; net < 2; ++net) {
     const NetW& w = A.n[net];
     const int dim = net ? A.cobs_dim : A.obs_dim;
     const float* src = (net ? A.cobs : A.obs) + row * dim;
     float* st = (net ? A.s_cobs : A.s_obs) + row * dim;
-    Tile x0[1], x1[T1], x2[T2], x3[T3];
+    Tile x0[2], x1[T1], x2[T2], x3[T3];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int k = rr_feat(j);
+    for (int j = 0; j < 8; ++j) {
+      const int k = 16 * (j >> 2) + 4 * gq + (j & 3);
       const float v = (ok && k < dim) ? src[k] : 0.f;
-      x0[0][j] = v;
+      x0[j >> 2][j & 3] = v;
       if (ok && k < dim) st[k] = v;
     }
-    rr_forward<1, T1, false, false>(w, 0, A.ws, wl, 0, x0, x1);
+    rr_forward<2, T1, false, false>(w, 0, A.ws, wl, 0, x0, x1);
     rr_forward<T1, T2, false, false>(w, 1, A.ws, wl, 0, x1, x2);
     rr_forward<T2, T3, false, false>(w, 2, A.ws, wl, 0, x2, x3);
-    rr_forward<T3, 1, true, false>(w, 3, A.ws, wl, 0, x3, z);
+    rr_forward<T3, 2, true, false>(w, 3, A.ws, wl, 0, x3, z);
     if (net == 0) {
-      // lane (r, h) holds actions 8 q + 4 h + u of row r
+      // lane (r, g) holds actions 4 g + u and 16 + 4 g + u of row r
       const float kLog2Pi = 0.91893853320467274178f;  // log(sqrt(2 pi))
       float lp = 0.f;
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const int n = rr_feat(j);
+      for (int j = 0; j < 8; ++j) {
+        const int n = 16 * (j >> 2) + 4 * gq + (j & 3);
         if (ok && n < na) {
-          const float mu = z[0][j], s = A.std_param[n];
+          const float mu = z[j >> 2][j & 3], s = A.std_param[n];
           const float x = mu + s * A.noise[row * na + n], diff = x - mu;
           lp += -(diff * diff) / (2.f * (s * s)) - logf(s) - kLog2Pi;
           A.actions[row * na + n] = x;
@@ -1020,9 +1034,9 @@ __global__ __launch_bounds__(256, (T1 > 4 || T2 > 4) ? 1 : 2) void k_act_reg(Act
           A.s_sig[row * na + n] = s;
         }
       }
-      lp += __shfl_xor(lp, 32);
-      if (ok && h == 0) A.s_lp[row] = lp;
-    } else if (ok && h == 0) {
+      lp = rr_feat_sum(lp);
+      if (ok && gq == 0) A.s_lp[row] = lp;
+    } else if (ok && gq == 0) {
       A.s_val[row] = z[0][0];
     }
   }
@@ -1139,7 +1153,7 @@ __global__ __launch_bounds__(256) void k_adv_norm(float* __restrict__ adv, int64
 // k_rows_reg instantiation for the nets' shape: 1 = hidden [256, 256, 128], 2 = [128, 128, 128] (both
 // nets; inputs / outputs <= 32), 0 = none (k_rows)
 int reg_shape(const Layout& lo, int B = 128) {
-  if (B % (4 * TR)) return 0;  // (k_rows_reg: whole workgroups of four row tiles)
+  if (B % 64) return 0;  // (k_rows_reg: whole workgroups of four 16-row tiles)
   const char* e = getenv("ZBP_ROWS");  // (read per call: tests switch it)
   if (e && strcmp(e, "lds") == 0) return 0;
   const NetW &a = lo.n[0], &c = lo.n[1];
@@ -1242,9 +1256,9 @@ int zbp_minibatch(const zbp_net* actor, const zbp_net* critic, const float* std_
   // the register-resident row kernel for the shipped shapes (ZBP_ROWS=lds: the LDS one, for A/Bs)
   const int shape = reg_shape(lo, B);
   if (shape == 1)
-    k_rows_reg<8, 8, 4><<<(B / TR + 3) / 4, 256, 0, s>>>(R);
+    k_rows_reg<16, 16, 8><<<B / 64, RR_WG, 0, s>>>(R);
   else if (shape == 2)
-    k_rows_reg<4, 4, 4><<<(B / TR + 3) / 4, 256, 0, s>>>(R);
+    k_rows_reg<8, 8, 8><<<B / 64, RR_WG, 0, s>>>(R);
   else
     k_rows<<<B / TR, ROW_THREADS, lds, s>>>(R);
   if (int rc = launch_check("k_rows")) return rc;
@@ -1367,11 +1381,11 @@ int zbp_act(const zbp_net* actor, const zbp_net* critic, const float* std_param,
     if (e != hipSuccess) return hip_fail(e, "hipFuncSetAttribute k_act");
     lds_set = true;
   }
-  const int shape = reg_shape(lo), wgs = ((io->rows + TR - 1) / TR + 3) / 4;
+  const int shape = reg_shape(lo), wgs = (io->rows + 63) / 64;
   if (shape == 1)
-    k_act_reg<8, 8, 4><<<wgs, 256, 0, (hipStream_t)stream>>>(A);
+    k_act_reg<16, 16, 8><<<wgs, RR_WG, 0, (hipStream_t)stream>>>(A);
   else if (shape == 2)
-    k_act_reg<4, 4, 4><<<wgs, 256, 0, (hipStream_t)stream>>>(A);
+    k_act_reg<8, 8, 8><<<wgs, RR_WG, 0, (hipStream_t)stream>>>(A);
   else
     k_act<<<(io->rows + TR - 1) / TR, 256, lds, (hipStream_t)stream>>>(A);
   return launch_check("k_act");
