@@ -112,7 +112,7 @@ Layout make_layout(const zbp_net* a, const zbp_net* c, int B) {
     }
   lo.grp0[2 * MAXL] = g;
   lo.ngroups = g;
-  lo.stats = take((int64_t)(B / TR) * NSTAT);
+  lo.stats = take((int64_t)(B / 16) * NSTAT);  // (per 32-row tile of k_rows, per 16-row wave of k_rows_reg)
   // row splits of the weight gradients: ~4 waves per SIMD (k_wgrad), each split >= 256 rows, a
   // multiple of 16 (pairs of row octets)
   int s = 1;
@@ -1291,7 +1291,7 @@ int zbp_minibatch(const zbp_net* actor, const zbp_net* critic, const float* std_
   for (int i = 0; i <= 2 * MAXL; ++i) D.tile0[i] = lo.tile0[i];
   D.wtiles = lo.wtiles;
   D.splits = lo.splits;
-  D.row_tiles = B / TR;
+  D.row_tiles = shape ? B / RR_TR : B / TR;
   D.batch = B;
   D.num_actions = batch->num_actions;
   for (int k = 0; k < 2; ++k) {
