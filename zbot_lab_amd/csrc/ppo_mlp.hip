@@ -114,9 +114,9 @@ Layout make_layout(const zbp_net* a, const zbp_net* c, int B) {
   lo.ngroups = g;
   lo.stats = take((int64_t)(B / 16) * NSTAT);  // (per 32-row tile of k_rows, per 16-row wave of k_rows_reg)
   // row splits of the weight gradients: ~4 waves per SIMD (k_wgrad), each split >= 256 rows, a
-  // multiple of 16 (pairs of row octets)
+  // multiple of 8 (row octets)
   int s = 1;
-  while (s < 256 && (int64_t)g * 4 * s * 2 <= 4 * 1024 && B / (s * 2) >= 256 && B % (16 * s * 2) == 0) s *= 2;
+  while (s < 256 && (int64_t)g * 4 * s * 2 <= 4 * 1024 && B / (s * 2) >= 256 && B % (8 * s * 2) == 0) s *= 2;
   lo.splits = s;
   lo.part = take((int64_t)s * t * PART);
   lo.scratch = take(64);
@@ -733,60 +733,13 @@ struct WgradArgs {
 };
 // dW_l = dZ_l^T X_l and db_l = sum dZ_l over the rows of one split. One workgroup = up to four 32-row
 // output tiles of one layer (n-tiles, one per wave) against up to four of its k-tiles; each wave
-// accumulates its n-tile against those NK k-tiles (NK accumulators, interleaved so consecutive MFMAs
-// never share one), so the waves of a workgroup read the same X lines (L1 / L2 hits).
-// A[n][r] = dZ_l[n0 + n][r], B[r][k] = X_l[k0 + k][r] from the octet-blocked row buffers (rbo): lane
-// half h takes rows 8 j + 4 h .. 8 j + 4 h + 3 of one feature, one float4 and four MFMAs per tile;
-// a wave instruction reads 1 KB contiguous. Two octets are in flight while two are consumed (the
-// loads past the split's end are clamped to its last octet: no branch in the loop). Partial tiles
-// (and the bias column of the k0 = 0 tile) go to the workspace in k_reduce's layout.
-template <int NK>
-__device__ __forceinline__ void wgrad_body(const WgradArgs& A, const float* dz, const float* xb, int64_t sd, int64_t sx,
-                                           int nj, int nl, int nt, int Tk, int kt0, int split) {
-  const int lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
-  f32x16 acc[NK];
-#pragma unroll
-  for (int k = 0; k < NK; ++k) acc[k] = f32x16{};
-  float bsum = 0.f;
-  float4 a0, a1, b0[NK], b1[NK];
-  auto load = [&](int j, float4& a, float4 (&b)[NK]) {
-    a = *reinterpret_cast<const float4*>(dz + j * sd);
-#pragma unroll
-    for (int k = 0; k < NK; ++k) b[k] = *reinterpret_cast<const float4*>(xb + k * 256 + j * sx);
-  };
-  auto step = [&](const float4 u, const float4 (&v)[NK]) {
-#pragma unroll
-    for (int k = 0; k < NK; ++k) acc[k] = mfma(u.x, v[k].x, acc[k]);
-#pragma unroll
-    for (int k = 0; k < NK; ++k) acc[k] = mfma(u.y, v[k].y, acc[k]);
-#pragma unroll
-    for (int k = 0; k < NK; ++k) acc[k] = mfma(u.z, v[k].z, acc[k]);
-#pragma unroll
-    for (int k = 0; k < NK; ++k) acc[k] = mfma(u.w, v[k].w, acc[k]);
-    bsum += (u.x + u.y) + (u.z + u.w);
-  };
-  load(0, a0, b0);
-  load(1, a1, b1);
-  for (int j = 0; j < nj; j += 2) {
-    const float4 u0 = a0, u1 = a1;
-    float4 v0[NK], v1[NK];
-#pragma unroll
-    for (int k = 0; k < NK; ++k) { v0[k] = b0[k]; v1[k] = b1[k]; }
-    load(min(j + 2, nj - 2), a0, b0);
-    load(min(j + 3, nj - 1), a1, b1);
-    step(u0, v0);
-    step(u1, v1);
-  }
-  bsum += __shfl_xor(bsum, 32);
-#pragma unroll
-  for (int k = 0; k < NK; ++k) {
-    float* out = A.ws + A.part + ((int64_t)split * A.wtiles + A.tile0[nl] + nt * Tk + kt0 + k) * PART;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) out[acc_row(r) * 32 + acc_col()] = acc[k][r];  // [n][k]
-    if (kt0 + k == 0 && h == 0) out[1024 + c] = bsum;
-  }
-}
-__global__ __launch_bounds__(256, 2) void k_wgrad(WgradArgs A) {
+// accumulates its n-tile against those k-tiles (<= 4 accumulators), so the waves of a workgroup read
+// the same X lines (L1 / L2 hits). A[n][r] = dZ_l[n0 + n][r], B[r][k] = X_l[k0 + k][r] from the
+// octet-blocked row buffers (rbo): lane half h takes rows 8 j + 4 h .. 8 j + 4 h + 3 of one feature,
+// one float4 and four MFMAs per tile; a wave instruction reads 1 KB contiguous. The next row octet's
+// quads load while the current one's MFMAs issue. Partial tiles (and the bias column of the k0 = 0
+// tile) go to the workspace in k_reduce's layout.
+__global__ __launch_bounds__(256, 3) void k_wgrad(WgradArgs A) {
   const int grp = blockIdx.x % A.ngroups, split = blockIdx.x / A.ngroups;
   int nl = 0;
   while (nl + 1 < 2 * MAXL && A.grp0[nl + 1] <= grp) ++nl;
@@ -802,11 +755,42 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(WgradArgs A) {
   const float* dz = A.ws + w.dz[l] + rbo(P1, 32 * nt + c, r0 + 4 * h);
   const float* xb = A.ws + w.x[l] + rbo(P0, 32 * kt0 + c, r0 + 4 * h);
   const int64_t sd = (int64_t)P1 * 8, sx = (int64_t)P0 * 8;
-  const int nj = rows / 8;  // (even: make_layout)
-  if (nk == 4) wgrad_body<4>(A, dz, xb, sd, sx, nj, nl, nt, Tk, kt0, split);
-  else if (nk == 3) wgrad_body<3>(A, dz, xb, sd, sx, nj, nl, nt, Tk, kt0, split);
-  else if (nk == 2) wgrad_body<2>(A, dz, xb, sd, sx, nj, nl, nt, Tk, kt0, split);
-  else wgrad_body<1>(A, dz, xb, sd, sx, nj, nl, nt, Tk, kt0, split);
+  f32x16 acc[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) acc[k] = f32x16{};
+  float bsum = 0.f;
+  const int nj = rows / 8;
+  float4 a = *reinterpret_cast<const float4*>(dz), b[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) b[k] = k < nk ? *reinterpret_cast<const float4*>(xb + k * 256) : float4{};
+  for (int j = 0; j < nj; ++j) {
+    const float4 u = a;
+    float4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = b[k];
+    if (j + 1 < nj) {
+      a = *reinterpret_cast<const float4*>(dz + (j + 1) * sd);
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (k < nk) b[k] = *reinterpret_cast<const float4*>(xb + k * 256 + (j + 1) * sx);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (k < nk) {
+        acc[k] = mfma(u.x, v[k].x, acc[k]); acc[k] = mfma(u.y, v[k].y, acc[k]);
+        acc[k] = mfma(u.z, v[k].z, acc[k]); acc[k] = mfma(u.w, v[k].w, acc[k]);
+      }
+    bsum += (u.x + u.y) + (u.z + u.w);
+  }
+  bsum += __shfl_xor(bsum, 32);
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (k < nk) {
+      float* out = A.ws + A.part + ((int64_t)split * A.wtiles + A.tile0[nl] + nt * Tk + kt0 + k) * PART;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) out[acc_row(r) * 32 + acc_col()] = acc[k][r];  // [n][k]
+      if (kt0 + k == 0 && h == 0) out[1024 + c] = bsum;
+    }
 }
 
 // ------------------------------------------------------------------------------- k_reduce
@@ -830,9 +814,14 @@ __global__ __launch_bounds__(256) void k_reduce(ReduceArgs A) {
     // per-row-tile sums -> stats, the std gradient (+ the entropy bonus term)
     __shared__ float acc[NSTAT][17];
     const int k = threadIdx.x & 15, part = threadIdx.x >> 4;  // 16 lanes per statistic
-    float s = 0.f;
-    for (int t = part; t < A.row_tiles; t += 16) s += A.ws[A.rstats + (int64_t)t * NSTAT + k];
-    acc[k][part] = s;
+    // (eight independent partial sums: the loads of a thread stay in flight together)
+    float sv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int t = part;
+    for (; t + 7 * 16 < A.row_tiles; t += 8 * 16)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) sv[u] += A.ws[A.rstats + (int64_t)(t + 16 * u) * NSTAT + k];
+    for (; t < A.row_tiles; t += 16) sv[0] += A.ws[A.rstats + (int64_t)t * NSTAT + k];
+    acc[k][part] = ((sv[0] + sv[1]) + (sv[2] + sv[3])) + ((sv[4] + sv[5]) + (sv[6] + sv[7]));
     __syncthreads();
     if (threadIdx.x == 0) {
       float tot[NSTAT];
