@@ -114,9 +114,9 @@ Layout make_layout(const zbp_net* a, const zbp_net* c, int B) {
   lo.ngroups = g;
   lo.stats = take((int64_t)(B / 16) * NSTAT);  // (per 32-row tile of k_rows, per 16-row wave of k_rows_reg)
   // row splits of the weight gradients: ~4 waves per SIMD (k_wgrad), each split >= 256 rows, a
-  // multiple of 8 (row octets)
+  // multiple of 32 (k_wgrad's LDS chunks)
   int s = 1;
-  while (s < 256 && (int64_t)g * 4 * s * 2 <= 4 * 1024 && B / (s * 2) >= 256 && B % (8 * s * 2) == 0) s *= 2;
+  while (s < 256 && (int64_t)g * 4 * s * 2 <= 4 * 1024 && B / (s * 2) >= 256 && B % (32 * s * 2) == 0) s *= 2;
   lo.splits = s;
   lo.part = take((int64_t)s * t * PART);
   lo.scratch = take(64);
@@ -731,66 +731,118 @@ struct WgradArgs {
   float* ws;
   int64_t part;
 };
-// dW_l = dZ_l^T X_l and db_l = sum dZ_l over the rows of one split. One workgroup = up to four 32-row
-// output tiles of one layer (n-tiles, one per wave) against up to four of its k-tiles; each wave
-// accumulates its n-tile against those k-tiles (<= 4 accumulators), so the waves of a workgroup read
-// the same X lines (L1 / L2 hits). A[n][r] = dZ_l[n0 + n][r], B[r][k] = X_l[k0 + k][r] from the
-// octet-blocked row buffers (rbo): lane half h takes rows 8 j + 4 h .. 8 j + 4 h + 3 of one feature,
-// one float4 and four MFMAs per tile; a wave instruction reads 1 KB contiguous. The next row octet's
-// quads load while the current one's MFMAs issue. Partial tiles (and the bias column of the k0 = 0
-// tile) go to the workspace in k_reduce's layout.
-__global__ __launch_bounds__(256, 3) void k_wgrad(WgradArgs A) {
+// dW_l = dZ_l^T X_l and db_l = sum dZ_l over the rows of one split. One workgroup = one block of up to
+// 128 output rows (n) x 128 reduction columns (k) of one layer; its four waves take 64 x 64 quadrants
+// (2 x 2 tiles of 32 x 32, v_mfma_f32_32x32x2_f32). The split's rows stream through LDS in chunks
+// of 32 rows (four octets): dZ_l[n0 .. n0 + 127] and X_l[k0 .. k0 + 127] of a chunk are 2 x 4 contiguous
+// 4 KB pieces of the octet-blocked row buffers (rbo), copied by all 256 threads into one of two
+// buffers while the previous chunk is consumed (one barrier per chunk); every element is read from
+// HBM / L2 once per block instead of once per wave. A wave reads its operands as float4 quads of
+// rows (conflict-free ds_read_b128: a wave's 64 lanes cover one contiguous KB) and issues 16 MFMAs
+// per octet. Partial tiles (and the bias column of the k0 = 0 tiles) go to the workspace in
+// k_reduce's layout.
+constexpr int WG_CHUNK_F = 2 * 4 * 128 * 8;  // floats of one chunk buffer (dZ + X: 32 KB)
+__global__ __launch_bounds__(256, 2) void k_wgrad(WgradArgs A) {
+  __shared__ float4 lds4[2 * WG_CHUNK_F / 4];
+  float* lds = reinterpret_cast<float*>(lds4);
   const int grp = blockIdx.x % A.ngroups, split = blockIdx.x / A.ngroups;
   int nl = 0;
   while (nl + 1 < 2 * MAXL && A.grp0[nl + 1] <= grp) ++nl;
   const NetW& w = A.n[nl / MAXL];
   const int l = nl % MAXL;
   const int P0 = w.p[l], P1 = w.p[l + 1], Tk = P0 / 32, Tn = P1 / 32, KG = (Tk + 3) / 4;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
-  const int g = grp - A.grp0[nl], nt = 4 * (g / KG) + wave, kt0 = 4 * (g % KG);
-  if (nt >= Tn) return;  // (no barrier below)
-  const int nk = min(4, Tk - kt0);
-  const int rows = A.batch / A.splits, r0 = split * rows;
-  // octet j of the split: dZ quad at dz + j * P1 * 8, X quads at xb + kk * 256 + j * P0 * 8
-  const float* dz = A.ws + w.dz[l] + rbo(P1, 32 * nt + c, r0 + 4 * h);
-  const float* xb = A.ws + w.x[l] + rbo(P0, 32 * kt0 + c, r0 + 4 * h);
-  const int64_t sd = (int64_t)P1 * 8, sx = (int64_t)P0 * 8;
-  f32x16 acc[4];
+  const int t = threadIdx.x, wave = t >> 6, lane = t & 63, c = lane & 31, h = lane >> 5;
+  const int g = grp - A.grp0[nl], nt0 = 4 * (g / KG), kt0 = 4 * (g % KG);
+  const int nb = min(4, Tn - nt0), kb = min(4, Tk - kt0);  // tiles of the block
+  const int rows = A.batch / A.splits, r0 = split * rows, nch = rows / 32;
+  // chunk copy: per octet, dZ features n0 .. n0 + 32 nb - 1 and X features k0 .. k0 + 32 kb - 1 (8 rows each)
+  const int fn = 32 * nb * 8 / 4, fk = 32 * kb * 8 / 4;  // float4s per octet
+  const float4* gz = reinterpret_cast<const float4*>(A.ws + w.dz[l] + rbo(P1, 32 * nt0, r0));
+  const float4* gx = reinterpret_cast<const float4*>(A.ws + w.x[l] + rbo(P0, 32 * kt0, r0));
+  const int64_t oz = (int64_t)P1 * 2, ox = (int64_t)P0 * 2;  // float4 stride of an octet
+  // thread t copies float4s t + 256 m, m < 8, of the chunk's 4 x 256 (dZ) + 4 x 256 (X) slots;
+  // slot (part, octet o, float4 f) -> LDS float4 part 1024 + o 256 + f
+  float4 st[8];
+  auto fetch = [&](int ch) {
 #pragma unroll
-  for (int k = 0; k < 4; ++k) acc[k] = f32x16{};
-  float bsum = 0.f;
-  const int nj = rows / 8;
-  float4 a = *reinterpret_cast<const float4*>(dz), b[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) b[k] = k < nk ? *reinterpret_cast<const float4*>(xb + k * 256) : float4{};
-  for (int j = 0; j < nj; ++j) {
-    const float4 u = a;
-    float4 v[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) v[k] = b[k];
-    if (j + 1 < nj) {
-      a = *reinterpret_cast<const float4*>(dz + (j + 1) * sd);
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (k < nk) b[k] = *reinterpret_cast<const float4*>(xb + k * 256 + (j + 1) * sx);
+    for (int m = 0; m < 8; ++m) {
+      const int e = t + 256 * m, part = e >> 10, o = (e >> 8) & 3, f = e & 255;
+      const int j = 4 * ch + o;  // octet of the split
+      float4 v = float4{};
+      if (part == 0) { if (f < fn) v = gz[j * oz + f]; }
+      else if (f < fk) v = gx[j * ox + f];
+      st[m] = v;
     }
+  };
+  auto stash = [&](int buf) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (k < nk) {
-        acc[k] = mfma(u.x, v[k].x, acc[k]); acc[k] = mfma(u.y, v[k].y, acc[k]);
-        acc[k] = mfma(u.z, v[k].z, acc[k]); acc[k] = mfma(u.w, v[k].w, acc[k]);
+    for (int m = 0; m < 8; ++m) lds4[buf * (WG_CHUNK_F / 4) + t + 256 * m] = st[m];
+  };
+  // this wave's quadrant: n tiles 2 (wave >> 1) + {0, 1}, k tiles 2 (wave & 1) + {0, 1}
+  const int qn = 2 * (wave >> 1), qk = 2 * (wave & 1);
+  const bool on[2][2] = {{qn < nb && qk < kb, qn < nb && qk + 1 < kb}, {qn + 1 < nb && qk < kb, qn + 1 < nb && qk + 1 < kb}};
+  const bool any = on[0][0];
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = f32x16{};
+  float bsum[2] = {0.f, 0.f};
+  const bool bias = kt0 == 0 && (wave & 1) == 0;
+  fetch(0);
+  stash(0);
+  __syncthreads();
+  if (nch > 1) fetch(1);
+  for (int ch = 0; ch < nch; ++ch) {
+    const float* bz = lds + (ch & 1) * WG_CHUNK_F;
+    const float* bx = bz + 4096;
+    if (any) {
+#pragma unroll
+      for (int o = 0; o < 4; ++o) {
+        float4 za[2], xb[2];
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+          za[a] = *reinterpret_cast<const float4*>(bz + o * 1024 + (32 * (qn + a) + c) * 8 + 4 * h);
+          xb[a] = *reinterpret_cast<const float4*>(bx + o * 1024 + (32 * (qk + a) + c) * 8 + 4 * h);
+        }
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int b = 0; b < 2; ++b) acc[a][b] = mfma(za[a].x, xb[b].x, acc[a][b]);
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int b = 0; b < 2; ++b) acc[a][b] = mfma(za[a].y, xb[b].y, acc[a][b]);
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int b = 0; b < 2; ++b) acc[a][b] = mfma(za[a].z, xb[b].z, acc[a][b]);
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int b = 0; b < 2; ++b) acc[a][b] = mfma(za[a].w, xb[b].w, acc[a][b]);
+        if (bias)
+#pragma unroll
+          for (int a = 0; a < 2; ++a) bsum[a] += (za[a].x + za[a].y) + (za[a].z + za[a].w);
       }
-    bsum += (u.x + u.y) + (u.z + u.w);
-  }
-  bsum += __shfl_xor(bsum, 32);
-#pragma unroll
-  for (int k = 0; k < 4; ++k)
-    if (k < nk) {
-      float* out = A.ws + A.part + ((int64_t)split * A.wtiles + A.tile0[nl] + nt * Tk + kt0 + k) * PART;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) out[acc_row(r) * 32 + acc_col()] = acc[k][r];  // [n][k]
-      if (kt0 + k == 0 && h == 0) out[1024 + c] = bsum;
     }
+    if (ch + 1 < nch) stash((ch + 1) & 1);
+    __syncthreads();  // chunk ch consumed by every wave, chunk ch + 1 in LDS
+    if (ch + 2 < nch) fetch(ch + 2);
+  }
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    const float bs = bsum[a] + __shfl_xor(bsum[a], 32);
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+      if (on[a][b]) {
+        const int nt = nt0 + qn + a, kt = kt0 + qk + b;
+        float* out = A.ws + A.part + ((int64_t)split * A.wtiles + A.tile0[nl] + nt * Tk + kt) * PART;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) out[acc_row(r) * 32 + acc_col()] = acc[a][b][r];  // [n][k]
+        if (kt == 0 && h == 0) out[1024 + c] = bs;
+      }
+  }
 }
 
 // ------------------------------------------------------------------------------- k_reduce
