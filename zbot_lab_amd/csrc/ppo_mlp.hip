@@ -761,7 +761,8 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(WgradArgs A) {
   const float4* gx = reinterpret_cast<const float4*>(A.ws + w.x[l] + rbo(P0, 32 * kt0, r0));
   const int64_t oz = (int64_t)P1 * 2, ox = (int64_t)P0 * 2;  // float4 stride of an octet
   // thread t copies float4s t + 256 m, m < 8, of the chunk's 4 x 256 (dZ) + 4 x 256 (X) slots;
-  // slot (part, octet o, float4 f) -> LDS float4 part 1024 + o 256 + f
+  // slot (part, octet o, float4 f = 2 feature + half) -> LDS float4 part 1024 + o 256 + half 128 + feature
+  // (a wave's operand read, lane (c, h) at h 128 + feature c: every 16 lanes read 256 contiguous bytes)
   float4 st[8];
   auto fetch = [&](int ch) {
 #pragma unroll
@@ -776,7 +777,10 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(WgradArgs A) {
   };
   auto stash = [&](int buf) {
 #pragma unroll
-    for (int m = 0; m < 8; ++m) lds4[buf * (WG_CHUNK_F / 4) + t + 256 * m] = st[m];
+    for (int m = 0; m < 8; ++m) {
+      const int e = t + 256 * m;
+      lds4[buf * (WG_CHUNK_F / 4) + (e & ~255) + (e & 1) * 128 + ((e & 255) >> 1)] = st[m];
+    }
   };
   // this wave's quadrant: n tiles 2 (wave >> 1) + {0, 1}, k tiles 2 (wave & 1) + {0, 1}
   const int qn = 2 * (wave >> 1), qk = 2 * (wave & 1);
@@ -802,8 +806,8 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(WgradArgs A) {
         float4 za[2], xb[2];
 #pragma unroll
         for (int a = 0; a < 2; ++a) {
-          za[a] = *reinterpret_cast<const float4*>(bz + o * 1024 + (32 * (qn + a) + c) * 8 + 4 * h);
-          xb[a] = *reinterpret_cast<const float4*>(bx + o * 1024 + (32 * (qk + a) + c) * 8 + 4 * h);
+          za[a] = *reinterpret_cast<const float4*>(bz + o * 1024 + (h * 128 + 32 * (qn + a) + c) * 4);
+          xb[a] = *reinterpret_cast<const float4*>(bx + o * 1024 + (h * 128 + 32 * (qk + a) + c) * 4);
         }
 #pragma unroll
         for (int a = 0; a < 2; ++a)

@@ -48,7 +48,10 @@ constexpr float kCoreM = 0.004f;
 #define ZB_GJK_MAXIT 16
 #endif
 constexpr int kGjkMaxIt = ZB_GJK_MAXIT;
-constexpr float kGjkTol = 1e-5f;  // m: GJK stops when its distance bounds are this close
+#ifndef ZB_GJK_TOL
+#define ZB_GJK_TOL 1e-5f  // (variant builds for the A/B: scripts/gpu_r5_bench_ab.sh)
+#endif
+constexpr float kGjkTol = ZB_GJK_TOL;  // m: GJK stops when its distance bounds are this close
 constexpr float kGjkTilt = 0.01f;  // warm start: tilt of the first three support directions (rad)
 
 // The ZBOT-6 chain topology is compiled in (zb_create checks the model against it):
