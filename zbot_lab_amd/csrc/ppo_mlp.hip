@@ -461,30 +461,34 @@ __device__ __forceinline__ float* rr_at(float* base, int o, int u) { return base
 constexpr int RR_CB = 32;                     // blocks per chunk (32 KB)
 constexpr int RR_LDS_F4 = 2 * RR_CB * 64;     // float4s of the two chunk buffers (64 KB)
 constexpr int RR_WG = 256;                    // threads per workgroup (4 waves, 4 row tiles)
+constexpr int RR_PER = RR_CB * 64 / RR_WG;    // float4s per thread per chunk
+typedef float4 RrStage[RR_PER];               // this thread's share of a chunk in flight
+// chunk `chunk` of an image of NB blocks into the thread's stage registers (zero past the end)
+template <int NB>
+__device__ __forceinline__ void rr_fetch(const float* __restrict__ img, int chunk, RrStage& st) {
+  constexpr int NF = NB * 64;
+  const float4* g = reinterpret_cast<const float4*>(img);
+#pragma unroll
+  for (int m = 0; m < RR_PER; ++m) {
+    const int e = chunk * RR_CB * 64 + threadIdx.x + m * RR_WG;
+    if (chunk * RR_CB * 64 + m * RR_WG < NF) st[m] = e < NF ? g[e] : float4{};
+  }
+}
+// out[o] = sum_i A(o, i) in[i]; st holds the image's chunk 0 on entry (the caller fetched it, ahead of
+// its own epilogue stores: a wait for the weights never waits for those stores to drain)
 template <int TI, int TO>
 __device__ __forceinline__ void rr_layer(const float* __restrict__ img, float4* __restrict__ wl, const Tile (&in)[TI],
-                                         Tile (&out)[TO]) {
-  constexpr int NB = TI * TO, NC = (NB + RR_CB - 1) / RR_CB, PER = RR_CB * 64 / RR_WG;  // float4s per thread per chunk
+                                         Tile (&out)[TO], RrStage& st) {
+  constexpr int NB = TI * TO, NC = (NB + RR_CB - 1) / RR_CB;
+  constexpr int NF = NB * 64;
   const int t = threadIdx.x, lane = t & 63;
-  const float4* g = reinterpret_cast<const float4*>(img);
-  constexpr int NF = NB * 64;  // float4s of the image
 #pragma unroll
   for (int o = 0; o < TO; ++o) out[o] = Tile{};
-  float4 st[PER];
 #pragma unroll
-  for (int m = 0; m < PER; ++m)
-    if (m * RR_WG < NF) st[m] = (t + m * RR_WG < NF) ? g[t + m * RR_WG] : float4{};
-#pragma unroll
-  for (int m = 0; m < PER; ++m)
+  for (int m = 0; m < RR_PER; ++m)
     if (m * RR_WG < NF) wl[t + m * RR_WG] = st[m];
   __syncthreads();
-  if (NC > 1) {
-#pragma unroll
-    for (int m = 0; m < PER; ++m) {
-      const int e = RR_CB * 64 + t + m * RR_WG;
-      if (RR_CB * 64 + m * RR_WG < NF) st[m] = e < NF ? g[e] : float4{};
-    }
-  }
+  if (NC > 1) rr_fetch<NB>(img, 1, st);
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
     const float4* cb = wl + (c & 1) * RR_CB * 64 + lane;
@@ -505,26 +509,22 @@ __device__ __forceinline__ void rr_layer(const float* __restrict__ img, float4* 
     if (c + 1 < NC) {
       float4* nb = wl + ((c + 1) & 1) * RR_CB * 64;
 #pragma unroll
-      for (int m = 0; m < PER; ++m)
+      for (int m = 0; m < RR_PER; ++m)
         if ((c + 1) * RR_CB * 64 + m * RR_WG < NF) nb[t + m * RR_WG] = st[m];
     }
     __syncthreads();  // chunk c consumed by every wave, chunk c + 1 in LDS
-    if (c + 2 < NC) {
-#pragma unroll
-      for (int m = 0; m < PER; ++m) {
-        const int e = (c + 2) * RR_CB * 64 + t + m * RR_WG;
-        if ((c + 2) * RR_CB * 64 + m * RR_WG < NF) st[m] = e < NF ? g[e] : float4{};
-      }
-    }
+    if (c + 2 < NC) rr_fetch<NB>(img, c + 2, st);
   }
 }
 
 // forward layer l: + bias, ELU (hidden layers: also X_{l+1} to HBM)
-template <int TI, int TO, bool kLast, bool kStore = true>
+// (NBN > 0: the next layer's image `next` has NBN blocks; its chunk 0 is fetched before this epilogue)
+template <int TI, int TO, bool kLast, bool kStore, int NBN>
 __device__ __forceinline__ void rr_forward(const NetW& w, int l, float* __restrict__ ws, float4* __restrict__ wl, int row0,
-                                           const Tile (&in)[TI], Tile (&out)[TO]) {
+                                           const Tile (&in)[TI], Tile (&out)[TO], RrStage& st, const float* next) {
   const int lo = rr_lane_off(16 * TO);
-  rr_layer<TI, TO>(ws + w.wr[l], wl, in, out);
+  rr_layer<TI, TO>(ws + w.wr[l], wl, in, out, st);
+  if (NBN > 0) rr_fetch<NBN>(next, 0, st);
   const float* bp = ws + w.bp[l] + 4 * rr_g();
   float* xb = rr_base(ws + w.x[l + 1], 16 * TO, row0);
 #pragma unroll
@@ -544,18 +544,28 @@ __device__ __forceinline__ void rr_forward(const NetW& w, int l, float* __restri
 }
 
 // backward through layer l >= 1: dZ_{l-1} = (W_l^T dZ_l) * ELU'(X_l), to registers and HBM
-template <int TI, int TO>
+template <int TI, int TO, int NBN>
 __device__ __forceinline__ void rr_backward(const NetW& w, int l, float* __restrict__ ws, float4* __restrict__ wl, int row0,
-                                            const Tile (&dz)[TI], Tile (&out)[TO]) {
+                                            const Tile (&dz)[TI], Tile (&out)[TO], RrStage& st, const float* next) {
   const int lo = rr_lane_off(16 * TO);
-  rr_layer<TI, TO>(ws + w.wtr[l], wl, dz, out);
   float* xb = rr_base(ws + w.x[l], 16 * TO, row0);
   float* db = rr_base(ws + w.dz[l - 1], 16 * TO, row0);
+  // X_l for ELU': loaded ahead of the product where the registers allow (its latency then hides
+  // under the MFMAs; the 256 x 256 layer has no room at two waves per SIMD and loads it after)
+  constexpr bool kPre = TI + 2 * TO <= 40;
+  Tile xl[TO];
+  if (kPre)
+#pragma unroll
+    for (int o = 0; o < TO; ++o)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) xl[o][u] = rr_at(xb, o, u)[lo];
+  rr_layer<TI, TO>(ws + w.wtr[l], wl, dz, out, st);
+  if (NBN > 0) rr_fetch<NBN>(next, 0, st);
 #pragma unroll
   for (int o = 0; o < TO; ++o)
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const float x = rr_at(xb, o, u)[lo];
+      const float x = kPre ? xl[o][u] : rr_at(xb, o, u)[lo];
       const float gr = out[o][u] * (x > 0.f ? 1.f : x + 1.f);  // ELU'(z) = exp(z) = x + 1 for z <= 0
       out[o][u] = gr;
       rr_at(db, o, u)[lo] = gr;
@@ -615,15 +625,20 @@ __global__ __launch_bounds__(RR_WG, 2) void k_rows_reg(RowArgs A) {
   float* st = ws + A.stats + (int64_t)tile * NSTAT;
 
   // ---- actor: forward, Gaussian log-prob, clipped surrogate, KL; dL/dmu into dZ of the output
+  // (every layer fetches the next layer's first weight chunk before its epilogue; the last forward
+  // layer fetches the backward's, the actor's last backward layer the critic's first)
   const NetW& wa = A.n[0];
+  const NetW& wc = A.n[1];
+  RrStage wst;
+  rr_fetch<2 * T1>(ws + wa.wr[0], 0, wst);
   Tile z[2];
   {
     Tile x0[2], x1[T1], x2[T2], x3[T3];
     rr_gather(wa, ws, row0, bt.obs, bt.obs_dim, row, x0);
-    rr_forward<2, T1, false>(wa, 0, ws, wl, row0, x0, x1);
-    rr_forward<T1, T2, false>(wa, 1, ws, wl, row0, x1, x2);
-    rr_forward<T2, T3, false>(wa, 2, ws, wl, row0, x2, x3);
-    rr_forward<T3, 2, true>(wa, 3, ws, wl, row0, x3, z);
+    rr_forward<2, T1, false, true, T1 * T2>(wa, 0, ws, wl, row0, x0, x1, wst, ws + wa.wr[1]);
+    rr_forward<T1, T2, false, true, T2 * T3>(wa, 1, ws, wl, row0, x1, x2, wst, ws + wa.wr[2]);
+    rr_forward<T2, T3, false, true, T3 * 2>(wa, 2, ws, wl, row0, x2, x3, wst, ws + wa.wr[3]);
+    rr_forward<T3, 2, true, true, 2 * T3>(wa, 3, ws, wl, row0, x3, z, wst, ws + wa.wtr[3]);
   }
   Tile dz[2];
   {
@@ -678,20 +693,19 @@ __global__ __launch_bounds__(RR_WG, 2) void k_rows_reg(RowArgs A) {
   }
   {
     Tile d3[T3], d2[T2], d1[T1];
-    rr_backward<2, T3>(wa, 3, ws, wl, row0, dz, d3);
-    rr_backward<T3, T2>(wa, 2, ws, wl, row0, d3, d2);
-    rr_backward<T2, T1>(wa, 1, ws, wl, row0, d2, d1);
+    rr_backward<2, T3, T3 * T2>(wa, 3, ws, wl, row0, dz, d3, wst, ws + wa.wtr[2]);
+    rr_backward<T3, T2, T2 * T1>(wa, 2, ws, wl, row0, d3, d2, wst, ws + wa.wtr[1]);
+    rr_backward<T2, T1, 2 * T1>(wa, 1, ws, wl, row0, d2, d1, wst, ws + wc.wr[0]);
   }
 
   // ---- critic: forward, clipped value loss, backward
-  const NetW& wc = A.n[1];
   {
     Tile x0[2], x1[T1], x2[T2], x3[T3];
     rr_gather(wc, ws, row0, bt.critic_obs, bt.critic_obs_dim, row, x0);
-    rr_forward<2, T1, false>(wc, 0, ws, wl, row0, x0, x1);
-    rr_forward<T1, T2, false>(wc, 1, ws, wl, row0, x1, x2);
-    rr_forward<T2, T3, false>(wc, 2, ws, wl, row0, x2, x3);
-    rr_forward<T3, 2, true>(wc, 3, ws, wl, row0, x3, z);
+    rr_forward<2, T1, false, true, T1 * T2>(wc, 0, ws, wl, row0, x0, x1, wst, ws + wc.wr[1]);
+    rr_forward<T1, T2, false, true, T2 * T3>(wc, 1, ws, wl, row0, x1, x2, wst, ws + wc.wr[2]);
+    rr_forward<T2, T3, false, true, T3 * 2>(wc, 2, ws, wl, row0, x2, x3, wst, ws + wc.wr[3]);
+    rr_forward<T3, 2, true, true, 2 * T3>(wc, 3, ws, wl, row0, x3, z, wst, ws + wc.wtr[3]);
   }
   {
     const float v = __shfl(z[0][0], r), tv = bt.values[row], ret = bt.returns[row], clip = A.lc.clip_param;
@@ -717,9 +731,9 @@ __global__ __launch_bounds__(RR_WG, 2) void k_rows_reg(RowArgs A) {
   }
   {
     Tile d3[T3], d2[T2], d1[T1];
-    rr_backward<2, T3>(wc, 3, ws, wl, row0, dz, d3);
-    rr_backward<T3, T2>(wc, 2, ws, wl, row0, d3, d2);
-    rr_backward<T2, T1>(wc, 1, ws, wl, row0, d2, d1);
+    rr_backward<2, T3, T3 * T2>(wc, 3, ws, wl, row0, dz, d3, wst, ws + wc.wtr[2]);
+    rr_backward<T3, T2, T2 * T1>(wc, 2, ws, wl, row0, d3, d2, wst, ws + wc.wtr[1]);
+    rr_backward<T2, T1, 0>(wc, 1, ws, wl, row0, d2, d1, wst, nullptr);
   }
 }
 
@@ -1052,6 +1066,8 @@ __global__ __launch_bounds__(RR_WG, 2) void k_act_reg(ActArgs A) {
   const bool ok = row < A.rows;
   const int na = A.na;
   Tile z[2];
+  RrStage wst;
+  rr_fetch<2 * T1>(A.ws + A.n[0].wr[0], 0, wst);
 #pragma unroll
   for (int net = 0; net < 2; ++net) {
     const NetW& w = A.n[net];
@@ -1066,10 +1082,13 @@ __global__ __launch_bounds__(RR_WG, 2) void k_act_reg(ActArgs A) {
       x0[j >> 2][j & 3] = v;
       if (ok && k < dim) st[k] = v;
     }
-    rr_forward<2, T1, false, false>(w, 0, A.ws, wl, 0, x0, x1);
-    rr_forward<T1, T2, false, false>(w, 1, A.ws, wl, 0, x1, x2);
-    rr_forward<T2, T3, false, false>(w, 2, A.ws, wl, 0, x2, x3);
-    rr_forward<T3, 2, true, false>(w, 3, A.ws, wl, 0, x3, z);
+    rr_forward<2, T1, false, false, T1 * T2>(w, 0, A.ws, wl, 0, x0, x1, wst, A.ws + w.wr[1]);
+    rr_forward<T1, T2, false, false, T2 * T3>(w, 1, A.ws, wl, 0, x1, x2, wst, A.ws + w.wr[2]);
+    rr_forward<T2, T3, false, false, T3 * 2>(w, 2, A.ws, wl, 0, x2, x3, wst, A.ws + w.wr[3]);
+    if (net == 0)
+      rr_forward<T3, 2, true, false, 2 * T1>(w, 3, A.ws, wl, 0, x3, z, wst, A.ws + A.n[1].wr[0]);
+    else
+      rr_forward<T3, 2, true, false, 0>(w, 3, A.ws, wl, 0, x3, z, wst, nullptr);
     if (net == 0) {
       // lane (r, g) holds actions 4 g + u and 16 + 4 g + u of row r
       const float kLog2Pi = 0.91893853320467274178f;  // log(sqrt(2 pi))
