@@ -77,6 +77,20 @@ struct Layout {
   int64_t total;
 };
 
+// k_wgrad workgroups resident at once: two per CU (64 KB of LDS each); the CU count of the current
+// device (256 on MI355X; 256 when no device is visible)
+int wgrad_slots() {
+  static const int cus = [] {
+    int d = 0, n = 0;
+    if (hipGetDevice(&d) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess ||
+        n <= 0)
+      n = 256;
+    (void)hipGetLastError();
+    return n;
+  }();
+  return 2 * cus;
+}
+
 Layout make_layout(const zbp_net* a, const zbp_net* c, int B) {
   Layout lo{};
   int64_t off = 0;
@@ -113,10 +127,12 @@ Layout make_layout(const zbp_net* a, const zbp_net* c, int B) {
   lo.grp0[2 * MAXL] = g;
   lo.ngroups = g;
   lo.stats = take((int64_t)(B / 16) * NSTAT);  // (per 32-row tile of k_rows, per 16-row wave of k_rows_reg)
-  // row splits of the weight gradients: ~4 waves per SIMD (k_wgrad), each split >= 256 rows, a
-  // multiple of 32 (k_wgrad's LDS chunks)
-  int s = 1;
-  while (s < 256 && (int64_t)g * 4 * s * 2 <= 4 * 1024 && B / (s * 2) >= 256 && B % (32 * s * 2) == 0) s *= 2;
+  // row splits of the weight gradients: as many as fill the device's resident k_wgrad workgroups in
+  // ONE round (groups x splits <= slots; a second, partly filled round would leave most CUs idle for
+  // a whole split's time); a split is a contiguous range of 32-row chunks (k_wgrad's LDS chunks)
+  const int C = B / 32;
+  int s = wgrad_slots() / g;
+  s = s < 1 ? 1 : (s > C ? C : (s > 1024 ? 1024 : s));
   lo.splits = s;
   lo.part = take((int64_t)s * t * PART);
   lo.scratch = take(64);
@@ -552,20 +568,19 @@ __device__ __forceinline__ void rr_backward(const NetW& w, int l, float* __restr
   float* db = rr_base(ws + w.dz[l - 1], 16 * TO, row0);
   // X_l for ELU': loaded ahead of the product where the registers allow (its latency then hides
   // under the MFMAs; the 256 x 256 layer has no room at two waves per SIMD and loads it after)
-  constexpr bool kPre = TI + 2 * TO <= 40;
+  constexpr int NPRE = TI + 2 * TO <= 40 ? TO : TO / 2;  // tiles of X_l loaded ahead
   Tile xl[TO];
-  if (kPre)
 #pragma unroll
-    for (int o = 0; o < TO; ++o)
+  for (int o = 0; o < NPRE; ++o)
 #pragma unroll
-      for (int u = 0; u < 4; ++u) xl[o][u] = rr_at(xb, o, u)[lo];
+    for (int u = 0; u < 4; ++u) xl[o][u] = rr_at(xb, o, u)[lo];
   rr_layer<TI, TO>(ws + w.wtr[l], wl, dz, out, st);
   if (NBN > 0) rr_fetch<NBN>(next, 0, st);
 #pragma unroll
   for (int o = 0; o < TO; ++o)
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const float x = kPre ? xl[o][u] : rr_at(xb, o, u)[lo];
+      const float x = o < NPRE ? xl[o][u] : rr_at(xb, o, u)[lo];
       const float gr = out[o][u] * (x > 0.f ? 1.f : x + 1.f);  // ELU'(z) = exp(z) = x + 1 for z <= 0
       out[o][u] = gr;
       rr_at(db, o, u)[lo] = gr;
@@ -768,7 +783,9 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(WgradArgs A) {
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63, c = lane & 31, h = lane >> 5;
   const int g = grp - A.grp0[nl], nt0 = 4 * (g / KG), kt0 = 4 * (g % KG);
   const int nb = min(4, Tn - nt0), kb = min(4, Tk - kt0);  // tiles of the block
-  const int rows = A.batch / A.splits, r0 = split * rows, nch = rows / 32;
+  const int C = A.batch / 32;  // the split's chunks [c0, c1)
+  const int c0 = (int)((int64_t)split * C / A.splits), c1 = (int)((int64_t)(split + 1) * C / A.splits);
+  const int r0 = 32 * c0, nch = c1 - c0;
   // chunk copy: per octet, dZ features n0 .. n0 + 32 nb - 1 and X features k0 .. k0 + 32 kb - 1 (8 rows each)
   const int fn = 32 * nb * 8 / 4, fk = 32 * kb * 8 / 4;  // float4s per octet
   const float4* gz = reinterpret_cast<const float4*>(A.ws + w.dz[l] + rbo(P1, 32 * nt0, r0));
