@@ -96,6 +96,26 @@ def test_fused_minibatch_gradients_match_autograd(gpu, hidden, rows, monkeypatch
         torch.testing.assert_close(stats, ref_stats, rtol=1e-5, atol=1e-7)
 
 
+def test_fused_minibatch_gradients_small_ragged_batch(gpu):
+    """A 96-row minibatch (16 envs x 24 steps / 4): not a multiple of 64, so the LDS row kernel runs
+    (k_rows_reg needs whole 64-row workgroups), and k_wgrad splits its 3 row chunks one per split."""
+    from zbot_lab_amd.rl import fused
+    for hidden in ([256, 256, 128], [128, 128, 128]):
+        alg = _alg(hidden, envs=16)
+        mb = alg.storage.num_envs * alg.storage.num_transitions_per_env // alg.num_mini_batches
+        assert mb == 96 and fused.supported(alg.policy, mb)
+        ref_stats = _torch_minibatch(alg, 1)
+        ref = [p.grad.detach().clone() for p in alg.policy.parameters()]
+        f = fused.FusedUpdate(alg, mb)
+        f.pack()
+        stats = f.minibatch(alg.storage, alg.mb_indices, mb).clone()
+        got = [p.grad.detach().clone() for p in alg.policy.parameters()]
+        for (n, _), r, g in zip(alg.policy.named_parameters(), ref, got):
+            assert (g - r).abs().max().item() <= 1e-5 * r.abs().max().item() + 1e-9, (hidden, n)
+        import torch
+        torch.testing.assert_close(stats, ref_stats, rtol=1e-5, atol=1e-7)
+
+
 def test_fused_update_matches_torch_update(gpu, monkeypatch):
     """A whole update (5 epochs x 4 minibatches: rate rule, clipping, Adam) from one snapshot, the
     fused path against the torch path: parameters, learning rate and the logged loss sums."""
