@@ -898,25 +898,44 @@ struct ReduceArgs {
 // and the bias for k0 = 0); the last workgroup: the scalars
 __global__ __launch_bounds__(256) void k_reduce(ReduceArgs A) {
   if (blockIdx.x == (unsigned)A.wtiles) {
-    // per-row-tile sums -> stats, the std gradient (+ the entropy bonus term)
-    __shared__ float acc[NSTAT][17];
-    const int k = threadIdx.x & 15, part = threadIdx.x >> 4;  // 16 lanes per statistic
-    // (eight independent partial sums: the loads of a thread stay in flight together)
-    float sv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    int t = part;
-    for (; t + 7 * 16 < A.row_tiles; t += 8 * 16)
+    // per-row-tile sums -> stats, the std gradient (+ the entropy bonus term): thread t sums row
+    // tiles t, t + 256, ... (one row = 16 floats = four float4, two rows in flight), then a fixed-order
+    // tree over the block (deterministic)
+    __shared__ float red[256][NSTAT + 1];
+    const int t = threadIdx.x;
+    float sv[NSTAT];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) sv[u] += A.ws[A.rstats + (int64_t)(t + 16 * u) * NSTAT + k];
-    for (; t < A.row_tiles; t += 16) sv[0] += A.ws[A.rstats + (int64_t)t * NSTAT + k];
-    acc[k][part] = ((sv[0] + sv[1]) + (sv[2] + sv[3])) + ((sv[4] + sv[5]) + (sv[6] + sv[7]));
+    for (int q = 0; q < NSTAT; ++q) sv[q] = 0.f;
+    const float4* rs = reinterpret_cast<const float4*>(A.ws + A.rstats);
+    int rt = t;
+    for (; rt + 256 < A.row_tiles; rt += 512) {
+      float4 v[8];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) { v[c] = rs[(int64_t)rt * 4 + c]; v[4 + c] = rs[(int64_t)(rt + 256) * 4 + c]; }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        sv[4 * c] += v[c].x + v[4 + c].x; sv[4 * c + 1] += v[c].y + v[4 + c].y;
+        sv[4 * c + 2] += v[c].z + v[4 + c].z; sv[4 * c + 3] += v[c].w + v[4 + c].w;
+      }
+    }
+    for (; rt < A.row_tiles; rt += 256)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float4 v = rs[(int64_t)rt * 4 + c];
+        sv[4 * c] += v.x; sv[4 * c + 1] += v.y; sv[4 * c + 2] += v.z; sv[4 * c + 3] += v.w;
+      }
+#pragma unroll
+    for (int q = 0; q < NSTAT; ++q) red[t][q] = sv[q];
     __syncthreads();
+    for (int st = 128; st > 0; st >>= 1) {
+      if (t < st)
+#pragma unroll
+        for (int q = 0; q < NSTAT; ++q) red[t][q] += red[t + st][q];
+      __syncthreads();
+    }
     if (threadIdx.x == 0) {
       float tot[NSTAT];
-      for (int q = 0; q < NSTAT; ++q) {
-        float v = 0.f;
-        for (int p = 0; p < 16; ++p) v += acc[q][p];
-        tot[q] = v;
-      }
+      for (int q = 0; q < NSTAT; ++q) tot[q] = red[0][q];
       const float invB = 1.f / (float)A.batch;
       float ent = 0.f;
       for (int a = 0; a < A.num_actions; ++a) ent += 0.5f + 0.91893853320467274178f + logf(A.std_param[a]);
@@ -957,16 +976,26 @@ struct OptimArgs {
   float* acc;
   float desired_kl, max_norm, b1, b2, eps;
   float* norm2;  // workspace scratch: [64] per-block sums of squares (k_norm), summed in order by k_adam
+  int64_t total;  // elements over all the tensors
 };
+// flat element g over the tensors in order -> (tensor t, element e): every thread's elements are
+// independent loads (a loop over the tensors per thread would chain one memory round trip per tensor)
+__device__ __forceinline__ void flat_elem(const zbp_params& P, int64_t g, int& t, int64_t& e) {
+  t = 0;
+  while (t + 1 < P.n_params && g >= P.numel[t]) { g -= P.numel[t]; ++t; }
+  e = g;
+}
 __global__ __launch_bounds__(256) void k_norm(OptimArgs A) {
   // global gradient norm^2: per-block partial sums in a fixed order (deterministic)
   __shared__ float red[4];
   float s = 0.f;
-  for (int t = 0; t < A.P.n_params; ++t)
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < A.P.numel[t]; e += (int64_t)gridDim.x * blockDim.x) {
-      const float g = A.P.grad[t][e];
-      s += g * g;
-    }
+  for (int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; f < A.total; f += (int64_t)gridDim.x * blockDim.x) {
+    int t;
+    int64_t e;
+    flat_elem(A.P, f, t, e);
+    const float g = A.P.grad[t][e];
+    s += g * g;
+  }
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
@@ -987,16 +1016,18 @@ __global__ __launch_bounds__(256) void k_adam(OptimArgs A) {
   const float step = A.P.step[0][0] + 1.f;
   const float bc1 = 1.f - powf(A.b1, step), bc2s = sqrtf(1.f - powf(A.b2, step));
   const float step_size = lr / bc1;
-  for (int t = 0; t < A.P.n_params; ++t)
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < A.P.numel[t]; e += (int64_t)gridDim.x * blockDim.x) {
-      const float g = A.P.grad[t][e] * coef;
-      A.P.grad[t][e] = g;
-      const float m = A.b1 * A.P.exp_avg[t][e] + (1.f - A.b1) * g;
-      const float v = A.b2 * A.P.exp_avg_sq[t][e] + (1.f - A.b2) * g * g;
-      A.P.exp_avg[t][e] = m;
-      A.P.exp_avg_sq[t][e] = v;
-      A.P.param[t][e] -= step_size * m / (sqrtf(v) / bc2s + A.eps);
-    }
+  for (int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; f < A.total; f += (int64_t)gridDim.x * blockDim.x) {
+    int t;
+    int64_t e;
+    flat_elem(A.P, f, t, e);
+    const float g = A.P.grad[t][e] * coef;
+    A.P.grad[t][e] = g;
+    const float m = A.b1 * A.P.exp_avg[t][e] + (1.f - A.b1) * g;
+    const float v = A.b2 * A.P.exp_avg_sq[t][e] + (1.f - A.b2) * g * g;
+    A.P.exp_avg[t][e] = m;
+    A.P.exp_avg_sq[t][e] = v;
+    A.P.param[t][e] -= step_size * m / (sqrtf(v) / bc2s + A.eps);
+  }
   // (every block reads the old lr / step: k_optim_tail writes the new ones after this launch)
 }
 __global__ void k_optim_tail(OptimArgs A) {
@@ -1413,6 +1444,8 @@ int zbp_optimizer_step(const zbp_params* params, float* lr, const float* stats, 
   O.b2 = beta2;
   O.eps = eps;
   O.norm2 = ws + lo.scratch;
+  O.total = 0;
+  for (int t = 0; t < params->n_params; ++t) O.total += params->numel[t];
   k_norm<<<64, 256, 0, s>>>(O);
   if (int rc = launch_check("k_norm")) return rc;
   k_adam<<<256, 256, 0, s>>>(O);
