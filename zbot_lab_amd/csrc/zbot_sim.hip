@@ -20,6 +20,7 @@
 // The algorithm is the one restated on the CPU in oracle/zbot_oracle.c (the parity oracle);
 // the two are written independently and compared by tests/test_gpu_parity.py.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <math.h>
 #include <stdint.h>
@@ -5155,6 +5156,17 @@ static int launch_check(const char* what) {
   return 0;
 }
 
+// a step-kernel launch; with events (zb_profile_begin) the dispatch itself records the kernel's start
+// and end (hipExtLaunchKernelGGL): the in-process time then is the kernel's own, as rocprofv3 reports
+// it, without the latency of separate event packets
+template <typename F, typename... Args>
+void zb_launch(F kernel, int blocks, hipStream_t s, hipEvent_t e0, hipEvent_t e1, Args... args) {
+  if (e0)
+    hipExtLaunchKernelGGL(kernel, dim3(blocks), dim3(WGT), 0, s, e0, e1, 0, args...);
+  else
+    hipLaunchKernelGGL(kernel, dim3(blocks), dim3(WGT), 0, s, args...);
+}
+
 extern "C" {
 
 const char* zb_last_error(void) { return g_err; }
@@ -5507,15 +5519,15 @@ int zb_step(zb_handle h, const float* actions, float* obs, float* reward, uint8_
   hipStream_t s = (hipStream_t)stream;
   const int blocks = (h->n + EPW - 1) / EPW;
   const bool prof = h->prof_n < h->prof_max;
-  if (prof) HIPCHK(hipEventRecord(h->prof_ev[2 * h->prof_n], s), "hipEventRecord");
+  hipEvent_t e0 = prof ? h->prof_ev[2 * h->prof_n] : nullptr, e1 = prof ? h->prof_ev[2 * h->prof_n + 1] : nullptr;
   const bool tgs = h->cfg.solver_mode >= 1, refresh = h->cfg.solver_mode >= 2;
   const bool one = h->occ1;
 #define ZB_LAUNCH(K, ...)                                                                          \
-  (tgs ? (one ? K<true, 1><<<blocks, WGT, 0, s>>>(__VA_ARGS__) : K<true, 2><<<blocks, WGT, 0, s>>>(__VA_ARGS__)) \
-       : (one ? K<false, 1><<<blocks, WGT, 0, s>>>(__VA_ARGS__) : K<false, 2><<<blocks, WGT, 0, s>>>(__VA_ARGS__)))
+  (tgs ? (one ? zb_launch(K<true, 1>, blocks, s, e0, e1, __VA_ARGS__) : zb_launch(K<true, 2>, blocks, s, e0, e1, __VA_ARGS__)) \
+       : (one ? zb_launch(K<false, 1>, blocks, s, e0, e1, __VA_ARGS__) : zb_launch(K<false, 2>, blocks, s, e0, e1, __VA_ARGS__)))
   // solver_modes 2, 3 (the TGS refresh): walking v2 and stand-up only (zb_create), two-wave occupancy
 #define ZB_LAUNCH_R(K, ...)                                                                        \
-  (refresh ? K<true, 2, true><<<blocks, WGT, 0, s>>>(__VA_ARGS__) : ZB_LAUNCH(K, __VA_ARGS__))
+  (refresh ? zb_launch(K<true, 2, true>, blocks, s, e0, e1, __VA_ARGS__) : ZB_LAUNCH(K, __VA_ARGS__))
   if (h->task == ZB_TASK_STANDUP_V0)
     ZB_LAUNCH_R(zb_su_step_kernel, h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward, terminated,
               truncated, h->d_acc, h->d_cnt, h->seed, h->d_wc);
@@ -5531,10 +5543,7 @@ int zb_step(zb_handle h, const float* actions, float* obs, float* reward, uint8_
 #undef ZB_LAUNCH_R
 #undef ZB_LAUNCH
   int rc = launch_check("zb_step_kernel");
-  if (prof) {
-    HIPCHK(hipEventRecord(h->prof_ev[2 * h->prof_n + 1], s), "hipEventRecord");
-    ++h->prof_n;
-  }
+  if (prof) ++h->prof_n;
   if (rc) return rc;
   return finalize(h, s, 0, 0, 1, obs, terminated, truncated);
 }
