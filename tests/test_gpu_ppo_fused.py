@@ -179,12 +179,14 @@ def test_fused_act_matches_torch_policy(gpu, hidden, rows, monkeypatch):
     """zbp_act (the rollout's policy step, runner._rollout) against PPO.act's torch statement with the
     same standard-normal draw: actions, mu, sigma, log-probabilities, values and the observations in
     the storage slot (fp32 summation-order tolerances); rows not a multiple of 32 included. rows: the
-    register-resident forward (k_act_reg) or the LDS one (ZBP_ROWS=lds)."""
+    register-resident forward (k_act_reg, rollouts of >= 16384 rows) or the LDS one (ZBP_ROWS=lds,
+    and every smaller rollout)."""
     import torch
     from zbot_lab_amd.rl import fused
     if rows == "lds":
         monkeypatch.setenv("ZBP_ROWS", "lds")
-    for envs in (512, 200):
+    # (k_act_reg takes rollouts of >= 16384 rows; 16 400 is not a multiple of its 64-row workgroups)
+    for envs in ((16400, 512) if rows == "reg" else (512, 200)):
         alg = _alg(hidden, envs=envs)
         fu = fused.FusedUpdate(alg, 256)  # (the minibatch size shapes only the update's row buffers)
         st = alg.storage
