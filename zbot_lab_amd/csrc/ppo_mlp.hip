@@ -638,6 +638,17 @@ __global__ __launch_bounds__(RR_WG, 2) void k_rows_reg(RowArgs A) {
   const int64_t row = bt.idx[bt.idx_offset + row0 + r];
   float* ws = A.ws;
   float* st = ws + A.stats + (int64_t)tile * NSTAT;
+  // the losses' inputs of this lane's row and actions (4 g + u, u < 4: num_actions <= 13 < 16), loaded
+  // ahead of the forward passes so their latency hides under them
+  const float adv_in = bt.advantages[row], lp_in = bt.log_prob[row], tv_in = bt.values[row], ret_in = bt.returns[row];
+  float act_in[4], mu_in[4], sig_in[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int n = 4 * gq + u;
+    act_in[u] = n < NA ? bt.actions[row * NA + n] : 0.f;
+    mu_in[u] = n < NA ? bt.mu[row * NA + n] : 0.f;
+    sig_in[u] = n < NA ? bt.sigma[row * NA + n] : 1.f;
+  }
 
   // ---- actor: forward, Gaussian log-prob, clipped surrogate, KL; dL/dmu into dZ of the output
   // (every layer fetches the next layer's first weight chunk before its epilogue; the last forward
@@ -666,17 +677,17 @@ __global__ __launch_bounds__(RR_WG, 2) void k_rows_reg(RowArgs A) {
       diff[j] = 0.f;
       if (n < NA) {
         const float mu = z[j >> 2][j & 3], s = A.std_param[n];
-        const float d = bt.actions[row * NA + n] - mu;
+        const float d = act_in[j & 3] - mu;  // (n < NA only in tile 0: j < 4)
         diff[j] = d;
         lp += -(d * d) / (2.f * (s * s)) - logf(s) - kLog2Pi;
-        const float os = bt.sigma[row * NA + n], om = bt.mu[row * NA + n];
+        const float os = sig_in[j & 3], om = mu_in[j & 3];
         kl += logf(s / os + 1e-5f) + (os * os + (om - mu) * (om - mu)) / (2.f * (s * s)) - 0.5f;
       }
     }
     lp = rr_feat_sum(lp);
     kl = rr_feat_sum(kl);
-    const float adv = bt.advantages[row], clip = A.lc.clip_param;
-    const float ratio = expf(lp - bt.log_prob[row]);
+    const float adv = adv_in, clip = A.lc.clip_param;
+    const float ratio = expf(lp - lp_in);
     const float rc = fminf(fmaxf(ratio, 1.f - clip), 1.f + clip);
     const float s1 = -adv * ratio, s2 = -adv * rc;
     const float surr = fmaxf(s1, s2);
@@ -723,7 +734,7 @@ __global__ __launch_bounds__(RR_WG, 2) void k_rows_reg(RowArgs A) {
     rr_forward<T3, 2, true, true, 2 * T3>(wc, 3, ws, wl, row0, x3, z, wst, ws + wc.wtr[3]);
   }
   {
-    const float v = __shfl(z[0][0], r), tv = bt.values[row], ret = bt.returns[row], clip = A.lc.clip_param;
+    const float v = __shfl(z[0][0], r), tv = tv_in, ret = ret_in, clip = A.lc.clip_param;
     float vl, dv;
     if (A.lc.use_clipped_value_loss) {
       const float vd = v - tv;
