@@ -73,12 +73,12 @@ def test_full_state_headline_sizes(gpu, n):
     assert nbad <= 0.02 * len(ids)
 
 
-@pytest.mark.parametrize("task,mode", [("v2", 0), ("v2", 1), ("v2", 2), ("v4", 0), ("manager", 0)],
-                         ids=["v2-pgs", "v2-tgs", "v2-tgs-refresh", "v4-pgs", "manager-pgs"])
+@pytest.mark.parametrize("task,mode", [("v2", 0), ("v2", 1), ("v2", 2), ("v2", 3), ("v4", 0), ("manager", 0)],
+                         ids=["v2-pgs", "v2-tgs", "v2-tgs-refresh", "v2-tgs-refresh-self", "v4-pgs", "manager-pgs"])
 def test_full_state_4096_every_solver(gpu, task, mode):
     """configs[1]'s size, every column: one step of 4096 envs from random full states against the
     oracle run on ALL 4096 columns under the full-state rule, for the benchmarked walking v2 PGS
-    solve, v2's TGS-style solve, v4 and the manager. (v4's and the manager's command resampling
+    solve, v2's TGS-style solves (modes 1-3), v4 and the manager. (v4's and the manager's command resampling
     draws from a counter-based generator keyed on the env index, so a column subset would not be
     the same sub-problem there.)"""
     import torch
@@ -96,7 +96,7 @@ def test_full_state_4096_every_solver(gpu, task, mode):
         g_out = _step(g, a)
         sg = g.get_state().cpu().numpy()
         g.close()
-        nbad = F._check(task, f"one step of {n} envs ({['PGS', 'TGS', 'TGS refresh'][mode]}, every column)", n, seed, st, [a], g_out,
+        nbad = F._check(task, f"one step of {n} envs ({['PGS', 'TGS', 'TGS refresh', 'TGS refresh + self'][mode]}, every column)", n, seed, st, [a], g_out,
                         sg, torch)
     assert nbad <= 0.02 * n
 
