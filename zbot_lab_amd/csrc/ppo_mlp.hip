@@ -1,24 +1,27 @@
 // ppo_mlp.hip — the PPO minibatch update of rsl_rl's ActorCritic as fp32 MFMA kernels for gfx950
 // (libzbot_ppo.so, C ABI include/zbot_ppo.h). Restates zbot_lab_amd/rl/ppo.py:PPO.update_steps
 // (rsl_rl PPO, reference agents/rsl_rl_ppo_cfg.py:65-91, ppo_learning_notes.md:521-548) per
-// minibatch in four launches instead of ~150 torch kernels:
+// minibatch in a handful of launches instead of ~150 torch kernels:
 //
-//   k_pack    padded / transposed weight images in the workspace (Wp [P1][P0], Wt [P0][P1])
-//   k_rows    one workgroup per 32 minibatch rows: gather the rows through the permutation, actor
-//             forward (Linear + ELU, v_mfma_f32_32x32x2_f32 with the activations in LDS), the
-//             Gaussian log-prob / KL / clipped surrogate and its gradient, actor backward dX; then
-//             the critic forward, clipped value loss and backward. Every layer's input X_l and
-//             pre-activation gradient dZ_l go to HBM for the weight gradients.
-//   k_wgrad   dW_l = dZ_l^T X_l and db_l = sum dZ_l, one wave per 32-row output tile (against every
-//             k-tile of the layer) and row split
-//             (split-K over the minibatch rows), partial tiles to the workspace
-//   k_reduce  partial tiles -> every parameter's .grad, the std gradient, the minibatch stats
+//   k_pack       padded / transposed / lane-ordered weight images in the workspace
+//   k_rows_reg   (the shipped net shapes) one wave per 16 minibatch rows, activations in registers:
+//                gather through the permutation, actor forward (Linear + ELU on
+//                v_mfma_f32_16x16x4_f32, the previous layer's accumulators as the B operand, weights
+//                shared by the workgroup's four waves through LDS), Gaussian log-prob / KL / clipped
+//                surrogate and its gradient, actor backward dX; then the critic forward, clipped value
+//                loss and backward. Every layer's input X_l and pre-activation gradient dZ_l go to HBM
+//                (octet-blocked rows) for the weight gradients.
+//   k_rows       the same with the activations in LDS (32-row tiles; any other shape, ZBP_ROWS=lds)
+//   k_wgrad      dW_l = dZ_l^T X_l and db_l = sum dZ_l: an LDS-tiled GEMM over the minibatch rows,
+//                128 x 128 output blocks, split-K over row ranges sized to one round of the device's
+//                resident workgroups; partial tiles to the workspace
+//   k_reduce     partial tiles -> every parameter's .grad, the std gradient, the minibatch stats
 //
-// and, on one GPU, k_optim (adaptive learning rate, global-norm clipping, Adam) + the re-pack.
-// Exact fp32 throughout (the MFMA is a k-ordered fmaf chain); results differ from torch's only by
-// summation order. MI355X mapping: the weights (<= 450 KB per net) stay L2-resident and stream as
-// the MFMA B operand; activations of a row tile live in LDS (row stride P + 4 floats: conflict-free
-// ds_read_b128); every workgroup holds one row tile and its waves split a layer's output columns.
+// and, on one GPU, k_norm / k_adam / k_optim_tail (adaptive learning rate, global-norm clipping,
+// Adam) + the re-pack; the rollout's policy step (k_act_reg / k_act), its bookkeeping (k_env_post) and
+// GAE (k_gae, k_adv_stats, k_adv_norm). Exact fp32 throughout (the MFMA is a k-ordered fmaf chain);
+// results differ from torch's only by summation order. MI355X mapping: the weights (<= 450 KB per
+// net) stay L2-resident; design and measurements in DESIGN.md §7 (round 5).
 #include <hip/hip_runtime.h>
 
 #include <math.h>
