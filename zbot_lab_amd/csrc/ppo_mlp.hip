@@ -477,29 +477,31 @@ __device__ __forceinline__ float* rr_at(float* base, int o, int u) { return base
 // tile outer: consecutive blocks feed different accumulators) = one float4 per lane, the A operands
 // of 4 MFMAs whose B operands are in[i]'s registers, read from the workgroup's LDS copy of the
 // current chunk while the next chunk is in flight from L2.
-constexpr int RR_CB = 32;                     // blocks per chunk (32 KB)
-constexpr int RR_LDS_F4 = 2 * RR_CB * 64;     // float4s of the two chunk buffers (64 KB)
+// CB = blocks per chunk: 32 (32 KB chunks, 64 KB of LDS per workgroup: two workgroups per CU) for
+// the 256-wide nets; 16 for the 128-wide ones, whose waves fit three to a SIMD (168 registers) and
+// whose three workgroups per CU then need 32 KB of LDS each
 constexpr int RR_WG = 256;                    // threads per workgroup (4 waves, 4 row tiles)
-constexpr int RR_PER = RR_CB * 64 / RR_WG;    // float4s per thread per chunk
-typedef float4 RrStage[RR_PER];               // this thread's share of a chunk in flight
+template <int T1> constexpr int rr_cb() { return T1 <= 8 ? 16 : 32; }
+template <int T1> constexpr int rr_occ() { return T1 <= 8 ? 3 : 2; }
+template <int CB> using RrStage = float4[CB * 64 / RR_WG];  // this thread's share of a chunk in flight
 // chunk `chunk` of an image of NB blocks into the thread's stage registers (zero past the end)
-template <int NB>
-__device__ __forceinline__ void rr_fetch(const float* __restrict__ img, int chunk, RrStage& st) {
-  constexpr int NF = NB * 64;
+template <int NB, int CB>
+__device__ __forceinline__ void rr_fetch(const float* __restrict__ img, int chunk, RrStage<CB>& st) {
+  constexpr int NF = NB * 64, PER = CB * 64 / RR_WG;
   const float4* g = reinterpret_cast<const float4*>(img);
 #pragma unroll
-  for (int m = 0; m < RR_PER; ++m) {
-    const int e = chunk * RR_CB * 64 + threadIdx.x + m * RR_WG;
-    if (chunk * RR_CB * 64 + m * RR_WG < NF) st[m] = e < NF ? g[e] : float4{};
+  for (int m = 0; m < PER; ++m) {
+    const int e = chunk * CB * 64 + threadIdx.x + m * RR_WG;
+    if (chunk * CB * 64 + m * RR_WG < NF) st[m] = e < NF ? g[e] : float4{};
   }
 }
 // out[o] = sum_i A(o, i) in[i]; st holds the image's chunk 0 on entry (the caller fetched it, ahead of
 // its own epilogue stores: a wait for the weights never waits for those stores to drain)
-template <int TI, int TO>
+template <int TI, int TO, int CB>
 __device__ __forceinline__ void rr_layer(const float* __restrict__ img, float4* __restrict__ wl, const Tile (&in)[TI],
-                                         Tile (&out)[TO], RrStage& st) {
-  constexpr int NB = TI * TO, NC = (NB + RR_CB - 1) / RR_CB;
-  constexpr int NF = NB * 64;
+                                         Tile (&out)[TO], RrStage<CB>& st) {
+  constexpr int NB = TI * TO, NC = (NB + CB - 1) / CB;
+  constexpr int NF = NB * 64, RR_PER = CB * 64 / RR_WG;
   const int t = threadIdx.x, lane = t & 63;
 #pragma unroll
   for (int o = 0; o < TO; ++o) out[o] = Tile{};
@@ -507,13 +509,13 @@ __device__ __forceinline__ void rr_layer(const float* __restrict__ img, float4* 
   for (int m = 0; m < RR_PER; ++m)
     if (m * RR_WG < NF) wl[t + m * RR_WG] = st[m];
   __syncthreads();
-  if (NC > 1) rr_fetch<NB>(img, 1, st);
+  if (NC > 1) rr_fetch<NB, CB>(img, 1, st);
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
-    const float4* cb = wl + (c & 1) * RR_CB * 64 + lane;
+    const float4* cb = wl + (c & 1) * CB * 64 + lane;
 #pragma unroll
-    for (int bb = 0; bb < RR_CB; ++bb) {
-      const int b = c * RR_CB + bb;
+    for (int bb = 0; bb < CB; ++bb) {
+      const int b = c * CB + bb;
       if (b < NB) {
         const int i = b / TO, o = b % TO;
         const float4 w = cb[bb * 64];
@@ -526,24 +528,24 @@ __device__ __forceinline__ void rr_layer(const float* __restrict__ img, float4* 
       }
     }
     if (c + 1 < NC) {
-      float4* nb = wl + ((c + 1) & 1) * RR_CB * 64;
+      float4* nb = wl + ((c + 1) & 1) * CB * 64;
 #pragma unroll
       for (int m = 0; m < RR_PER; ++m)
-        if ((c + 1) * RR_CB * 64 + m * RR_WG < NF) nb[t + m * RR_WG] = st[m];
+        if ((c + 1) * CB * 64 + m * RR_WG < NF) nb[t + m * RR_WG] = st[m];
     }
     __syncthreads();  // chunk c consumed by every wave, chunk c + 1 in LDS
-    if (c + 2 < NC) rr_fetch<NB>(img, c + 2, st);
+    if (c + 2 < NC) rr_fetch<NB, CB>(img, c + 2, st);
   }
 }
 
 // forward layer l: + bias, ELU (hidden layers: also X_{l+1} to HBM)
 // (NBN > 0: the next layer's image `next` has NBN blocks; its chunk 0 is fetched before this epilogue)
-template <int TI, int TO, bool kLast, bool kStore, int NBN>
+template <int TI, int TO, bool kLast, bool kStore, int NBN, int CB>
 __device__ __forceinline__ void rr_forward(const NetW& w, int l, float* __restrict__ ws, float4* __restrict__ wl, int row0,
-                                           const Tile (&in)[TI], Tile (&out)[TO], RrStage& st, const float* next) {
+                                           const Tile (&in)[TI], Tile (&out)[TO], RrStage<CB>& st, const float* next) {
   const int lo = rr_lane_off(16 * TO);
-  rr_layer<TI, TO>(ws + w.wr[l], wl, in, out, st);
-  if (NBN > 0) rr_fetch<NBN>(next, 0, st);
+  rr_layer<TI, TO, CB>(ws + w.wr[l], wl, in, out, st);
+  if (NBN > 0) rr_fetch<NBN, CB>(next, 0, st);
   const float* bp = ws + w.bp[l] + 4 * rr_g();
   float* xb = rr_base(ws + w.x[l + 1], 16 * TO, row0);
 #pragma unroll
@@ -563,9 +565,9 @@ __device__ __forceinline__ void rr_forward(const NetW& w, int l, float* __restri
 }
 
 // backward through layer l >= 1: dZ_{l-1} = (W_l^T dZ_l) * ELU'(X_l), to registers and HBM
-template <int TI, int TO, int NBN>
+template <int TI, int TO, int NBN, int CB>
 __device__ __forceinline__ void rr_backward(const NetW& w, int l, float* __restrict__ ws, float4* __restrict__ wl, int row0,
-                                            const Tile (&dz)[TI], Tile (&out)[TO], RrStage& st, const float* next) {
+                                            const Tile (&dz)[TI], Tile (&out)[TO], RrStage<CB>& st, const float* next) {
   const int lo = rr_lane_off(16 * TO);
   float* xb = rr_base(ws + w.x[l], 16 * TO, row0);
   float* db = rr_base(ws + w.dz[l - 1], 16 * TO, row0);
@@ -577,8 +579,8 @@ __device__ __forceinline__ void rr_backward(const NetW& w, int l, float* __restr
   for (int o = 0; o < NPRE; ++o)
 #pragma unroll
     for (int u = 0; u < 4; ++u) xl[o][u] = rr_at(xb, o, u)[lo];
-  rr_layer<TI, TO>(ws + w.wtr[l], wl, dz, out, st);
-  if (NBN > 0) rr_fetch<NBN>(next, 0, st);
+  rr_layer<TI, TO, CB>(ws + w.wtr[l], wl, dz, out, st);
+  if (NBN > 0) rr_fetch<NBN, CB>(next, 0, st);
 #pragma unroll
   for (int o = 0; o < TO; ++o)
 #pragma unroll
@@ -630,10 +632,14 @@ __device__ __forceinline__ float rr_feat_sum(float v) {
 
 constexpr int RR_TR = 16;  // rows per wave
 template <int T1, int T2, int T3>
-__global__ __launch_bounds__(RR_WG, 2) void k_rows_reg(RowArgs A) {
-  __shared__ float4 wl[RR_LDS_F4];
+__global__ __launch_bounds__(RR_WG, rr_occ<T1>()) void k_rows_reg(RowArgs A) {
+  constexpr int CB = rr_cb<T1>();
+  __shared__ float4 wl[2 * CB * 64];
   const int lane = threadIdx.x & 63, r = lane & 15, gq = lane >> 4;
-  const int tile = blockIdx.x * (RR_WG / 64) + (threadIdx.x >> 6);  // (B a multiple of 64: reg_shape)
+  // workgroup pairs: even = the actor's pass over four row tiles, odd = the critic's over the same
+  // tiles (the two nets share nothing but the tile's statistics slots, which they write apart)
+  const int net = blockIdx.x & 1;
+  const int tile = (blockIdx.x >> 1) * (RR_WG / 64) + (threadIdx.x >> 6);  // (B a multiple of 64: reg_shape)
   const int row0 = tile * RR_TR;
   const zbp_batch& bt = A.bt;
   const int NA = bt.num_actions;
@@ -643,7 +649,12 @@ __global__ __launch_bounds__(RR_WG, 2) void k_rows_reg(RowArgs A) {
   float* st = ws + A.stats + (int64_t)tile * NSTAT;
   // the losses' inputs of this lane's row and actions (4 g + u, u < 4: num_actions <= 13 < 16), loaded
   // ahead of the forward passes so their latency hides under them
-  const float adv_in = bt.advantages[row], lp_in = bt.log_prob[row], tv_in = bt.values[row], ret_in = bt.returns[row];
+  const NetW& wa = A.n[0];
+  const NetW& wc = A.n[1];
+  RrStage<CB> wst;
+  Tile z[2], dz[2];
+  if (net == 0) {
+  const float adv_in = bt.advantages[row], lp_in = bt.log_prob[row];
   float act_in[4], mu_in[4], sig_in[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
@@ -655,21 +666,16 @@ __global__ __launch_bounds__(RR_WG, 2) void k_rows_reg(RowArgs A) {
 
   // ---- actor: forward, Gaussian log-prob, clipped surrogate, KL; dL/dmu into dZ of the output
   // (every layer fetches the next layer's first weight chunk before its epilogue; the last forward
-  // layer fetches the backward's, the actor's last backward layer the critic's first)
-  const NetW& wa = A.n[0];
-  const NetW& wc = A.n[1];
-  RrStage wst;
-  rr_fetch<2 * T1>(ws + wa.wr[0], 0, wst);
-  Tile z[2];
+  // layer fetches the backward's)
+  rr_fetch<2 * T1, CB>(ws + wa.wr[0], 0, wst);
   {
     Tile x0[2], x1[T1], x2[T2], x3[T3];
     rr_gather(wa, ws, row0, bt.obs, bt.obs_dim, row, x0);
-    rr_forward<2, T1, false, true, T1 * T2>(wa, 0, ws, wl, row0, x0, x1, wst, ws + wa.wr[1]);
-    rr_forward<T1, T2, false, true, T2 * T3>(wa, 1, ws, wl, row0, x1, x2, wst, ws + wa.wr[2]);
-    rr_forward<T2, T3, false, true, T3 * 2>(wa, 2, ws, wl, row0, x2, x3, wst, ws + wa.wr[3]);
-    rr_forward<T3, 2, true, true, 2 * T3>(wa, 3, ws, wl, row0, x3, z, wst, ws + wa.wtr[3]);
+    rr_forward<2, T1, false, true, T1 * T2, CB>(wa, 0, ws, wl, row0, x0, x1, wst, ws + wa.wr[1]);
+    rr_forward<T1, T2, false, true, T2 * T3, CB>(wa, 1, ws, wl, row0, x1, x2, wst, ws + wa.wr[2]);
+    rr_forward<T2, T3, false, true, T3 * 2, CB>(wa, 2, ws, wl, row0, x2, x3, wst, ws + wa.wr[3]);
+    rr_forward<T3, 2, true, true, 2 * T3, CB>(wa, 3, ws, wl, row0, x3, z, wst, ws + wa.wtr[3]);
   }
-  Tile dz[2];
   {
     // lane (r, g) holds actions 4 g + u (tile 0) and 16 + 4 g + u (tile 1) of row r
     const float kLog2Pi = 0.91893853320467274178f;  // log(sqrt(2 pi))
@@ -722,19 +728,21 @@ __global__ __launch_bounds__(RR_WG, 2) void k_rows_reg(RowArgs A) {
   }
   {
     Tile d3[T3], d2[T2], d1[T1];
-    rr_backward<2, T3, T3 * T2>(wa, 3, ws, wl, row0, dz, d3, wst, ws + wa.wtr[2]);
-    rr_backward<T3, T2, T2 * T1>(wa, 2, ws, wl, row0, d3, d2, wst, ws + wa.wtr[1]);
-    rr_backward<T2, T1, 2 * T1>(wa, 1, ws, wl, row0, d2, d1, wst, ws + wc.wr[0]);
+    rr_backward<2, T3, T3 * T2, CB>(wa, 3, ws, wl, row0, dz, d3, wst, ws + wa.wtr[2]);
+    rr_backward<T3, T2, T2 * T1, CB>(wa, 2, ws, wl, row0, d3, d2, wst, ws + wa.wtr[1]);
+    rr_backward<T2, T1, 0, CB>(wa, 1, ws, wl, row0, d2, d1, wst, nullptr);
   }
-
+  } else {
+  const float tv_in = bt.values[row], ret_in = bt.returns[row];
   // ---- critic: forward, clipped value loss, backward
+  rr_fetch<2 * T1, CB>(ws + wc.wr[0], 0, wst);
   {
     Tile x0[2], x1[T1], x2[T2], x3[T3];
     rr_gather(wc, ws, row0, bt.critic_obs, bt.critic_obs_dim, row, x0);
-    rr_forward<2, T1, false, true, T1 * T2>(wc, 0, ws, wl, row0, x0, x1, wst, ws + wc.wr[1]);
-    rr_forward<T1, T2, false, true, T2 * T3>(wc, 1, ws, wl, row0, x1, x2, wst, ws + wc.wr[2]);
-    rr_forward<T2, T3, false, true, T3 * 2>(wc, 2, ws, wl, row0, x2, x3, wst, ws + wc.wr[3]);
-    rr_forward<T3, 2, true, true, 2 * T3>(wc, 3, ws, wl, row0, x3, z, wst, ws + wc.wtr[3]);
+    rr_forward<2, T1, false, true, T1 * T2, CB>(wc, 0, ws, wl, row0, x0, x1, wst, ws + wc.wr[1]);
+    rr_forward<T1, T2, false, true, T2 * T3, CB>(wc, 1, ws, wl, row0, x1, x2, wst, ws + wc.wr[2]);
+    rr_forward<T2, T3, false, true, T3 * 2, CB>(wc, 2, ws, wl, row0, x2, x3, wst, ws + wc.wr[3]);
+    rr_forward<T3, 2, true, true, 2 * T3, CB>(wc, 3, ws, wl, row0, x3, z, wst, ws + wc.wtr[3]);
   }
   {
     const float v = __shfl(z[0][0], r), tv = tv_in, ret = ret_in, clip = A.lc.clip_param;
@@ -760,9 +768,10 @@ __global__ __launch_bounds__(RR_WG, 2) void k_rows_reg(RowArgs A) {
   }
   {
     Tile d3[T3], d2[T2], d1[T1];
-    rr_backward<2, T3, T3 * T2>(wc, 3, ws, wl, row0, dz, d3, wst, ws + wc.wtr[2]);
-    rr_backward<T3, T2, T2 * T1>(wc, 2, ws, wl, row0, d3, d2, wst, ws + wc.wtr[1]);
-    rr_backward<T2, T1, 0>(wc, 1, ws, wl, row0, d2, d1, wst, nullptr);
+    rr_backward<2, T3, T3 * T2, CB>(wc, 3, ws, wl, row0, dz, d3, wst, ws + wc.wtr[2]);
+    rr_backward<T3, T2, T2 * T1, CB>(wc, 2, ws, wl, row0, d3, d2, wst, ws + wc.wtr[1]);
+    rr_backward<T2, T1, 0, CB>(wc, 1, ws, wl, row0, d2, d1, wst, nullptr);
+  }
   }
 }
 
@@ -1127,15 +1136,16 @@ __global__ __launch_bounds__(256) void k_act(ActArgs A) {
 // shared through LDS
 template <int T1, int T2, int T3>
 __global__ __launch_bounds__(RR_WG, 2) void k_act_reg(ActArgs A) {
-  __shared__ float4 wl[RR_LDS_F4];
+  constexpr int CB = 32;
+  __shared__ float4 wl[2 * CB * 64];
   const int lane = threadIdx.x & 63, r = lane & 15, gq = lane >> 4;
   const int row0 = (blockIdx.x * (RR_WG / 64) + (threadIdx.x >> 6)) * RR_TR;  // (waves past the rows run on zeros, store nothing)
   const int64_t row = row0 + r;
   const bool ok = row < A.rows;
   const int na = A.na;
   Tile z[2];
-  RrStage wst;
-  rr_fetch<2 * T1>(A.ws + A.n[0].wr[0], 0, wst);
+  RrStage<CB> wst;
+  rr_fetch<2 * T1, CB>(A.ws + A.n[0].wr[0], 0, wst);
 #pragma unroll
   for (int net = 0; net < 2; ++net) {
     const NetW& w = A.n[net];
@@ -1150,13 +1160,13 @@ __global__ __launch_bounds__(RR_WG, 2) void k_act_reg(ActArgs A) {
       x0[j >> 2][j & 3] = v;
       if (ok && k < dim) st[k] = v;
     }
-    rr_forward<2, T1, false, false, T1 * T2>(w, 0, A.ws, wl, 0, x0, x1, wst, A.ws + w.wr[1]);
-    rr_forward<T1, T2, false, false, T2 * T3>(w, 1, A.ws, wl, 0, x1, x2, wst, A.ws + w.wr[2]);
-    rr_forward<T2, T3, false, false, T3 * 2>(w, 2, A.ws, wl, 0, x2, x3, wst, A.ws + w.wr[3]);
+    rr_forward<2, T1, false, false, T1 * T2, CB>(w, 0, A.ws, wl, 0, x0, x1, wst, A.ws + w.wr[1]);
+    rr_forward<T1, T2, false, false, T2 * T3, CB>(w, 1, A.ws, wl, 0, x1, x2, wst, A.ws + w.wr[2]);
+    rr_forward<T2, T3, false, false, T3 * 2, CB>(w, 2, A.ws, wl, 0, x2, x3, wst, A.ws + w.wr[3]);
     if (net == 0)
-      rr_forward<T3, 2, true, false, 2 * T1>(w, 3, A.ws, wl, 0, x3, z, wst, A.ws + A.n[1].wr[0]);
+      rr_forward<T3, 2, true, false, 2 * T1, CB>(w, 3, A.ws, wl, 0, x3, z, wst, A.ws + A.n[1].wr[0]);
     else
-      rr_forward<T3, 2, true, false, 0>(w, 3, A.ws, wl, 0, x3, z, wst, nullptr);
+      rr_forward<T3, 2, true, false, 0, CB>(w, 3, A.ws, wl, 0, x3, z, wst, nullptr);
     if (net == 0) {
       // lane (r, g) holds actions 4 g + u and 16 + 4 g + u of row r
       const float kLog2Pi = 0.91893853320467274178f;  // log(sqrt(2 pi))
@@ -1396,9 +1406,9 @@ int zbp_minibatch(const zbp_net* actor, const zbp_net* critic, const float* std_
   // the register-resident row kernel for the shipped shapes (ZBP_ROWS=lds: the LDS one, for A/Bs)
   const int shape = reg_shape(lo, B);
   if (shape == 1)
-    k_rows_reg<16, 16, 8><<<B / 64, RR_WG, 0, s>>>(R);
+    k_rows_reg<16, 16, 8><<<2 * (B / 64), RR_WG, 0, s>>>(R);
   else if (shape == 2)
-    k_rows_reg<8, 8, 8><<<B / 64, RR_WG, 0, s>>>(R);
+    k_rows_reg<8, 8, 8><<<2 * (B / 64), RR_WG, 0, s>>>(R);
   else
     k_rows<<<B / TR, ROW_THREADS, lds, s>>>(R);
   if (int rc = launch_check("k_rows")) return rc;

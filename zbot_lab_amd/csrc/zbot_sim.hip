@@ -1407,8 +1407,10 @@ __device__ __forceinline__ int quad_rimface(const QCircle& h, int j, const SelfC
 }
 
 // mode = cfg.self_manifold: 1 faces; 2 faces, else side-by-side rims; 3 faces, else a ruling on a
-// face, else side-by-side rims (the oracle's self_manifold)
-template <class Sink>
+// face, else side-by-side rims (the oracle's self_manifold). kRf: mode 3 compiled in -- only the
+// kernels launched for self_manifold 3 carry it (its code in the default kernel costs 0.9 % of the
+// step through register allocation alone)
+template <bool kRf, class Sink>
 __device__ __forceinline__ int quad_manifold(const QCircle& h, int j, const SelfContact& sc, float margin, bool write,
                                              int mode, Sink sink) {
   const float sgd = (j & 2) ? 1.f : -1.f;
@@ -1428,7 +1430,7 @@ __device__ __forceinline__ int quad_manifold(const QCircle& h, int j, const Self
   const float so = al < 0.f ? -1.f : 1.f;
   const float uo[3] = {so * u[0], so * u[1], so * u[2]};
   if (!(fm & 3) || !(fm & 12)) {
-    if (mode >= 3 && ((fm & 3) == 0) != ((fm & 12) == 0)) {  // a face on exactly one side
+    if (kRf && mode >= 3 && ((fm & 3) == 0) != ((fm & 12) == 0)) {  // a face on exactly one side
       const int k = quad_rimface(h, j, sc, margin, write, sink, fm, uo, r);
       if (k > 0) return k;
     }
@@ -1526,6 +1528,7 @@ __device__ __forceinline__ int quad_manifold(const QCircle& h, int j, const Self
 // contiguous chunks, one per lane, so candidates stay in canonical order lane by lane; each
 // candidate pair runs GJK on the core hulls (gjk_pair, one contact per pair). Counting pass, team
 // scan, then each lane writes its candidates at their canonical positions.
+template <bool kRf>
 __device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q& q, bool warm, bool& over, Stamps& sp) {
   const float margin = cfg.contact_margin;
 
@@ -1737,7 +1740,7 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q&
         // write pass stores its points
         const float code = (float)(pcode + 1);
         const int mc = (mfon && sc.sep > -2.f * kCoreM + 1e-7f)
-                           ? quad_manifold(hc, qj, sc, margin, pass == 1, cfg.self_manifold, [&](int rank, float4 xs, const float* nn) {
+                           ? quad_manifold<kRf>(hc, qj, sc, margin, pass == 1, cfg.self_manifold, [&](int rank, float4 xs, const float* nn) {
                                if (pos + rank < g_tot + NSELF) {
                                  q.cand(pos + rank, 0) = xs;
                                  q.cand(pos + rank, 1) = make_float4(nn[0], nn[1], nn[2], code);
@@ -2241,11 +2244,14 @@ __device__ __forceinline__ void refresh_contacts(const zb_task_cfg& cfg, MP m, c
 // otherwise cfg.friction everywhere.
 // kRefresh (zb_task_cfg.solver_mode 2 / 3, with kTgs): before every sub-iteration after the first the
 // ground contacts (mode 3: and the self contacts) are re-evaluated at the pose the sub-iterations so far reached (see the sweeps).
-template <bool kDebugForces, bool kLinkFriction, bool kTgs, bool kRefresh = false>
+template <bool kDebugForces, bool kLinkFriction, bool kTgs, bool kRefresh = false, bool kRf = false>
 __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
                                         const float target[ND], const Q& q, bool last, bool warm, SensorOut& so,
                                         float (*dbgF)[3], float* dbgTau, Stamps& sp) {
-  const float dt = cfg.sim_dt;
+  // (dt through an empty asm: its own scalar register, not a lane of the cfg words the compiler
+  // loads as one 16-register tuple, which a spill would reload whole at every use)
+  float dt = cfg.sim_dt;
+  asm volatile("" : "+s"(dt));
   MP m = opaque(m0);
 
   if (last) {
@@ -2267,7 +2273,7 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
   fk_team<true>(s, q, Ib, Sown);
   wave_sync();
   sp.mark(9);
-  nc = detect(cfg, s.pos[2], q, warm, over, sp);
+  nc = detect<kRf>(cfg, s.pos[2], q, warm, over, sp);
   m = opaque(m0);
 
   // RNEA bias forces (qddot = 0, gravity as base acceleration) and, in the same team suffix sum,
@@ -3061,7 +3067,7 @@ __device__ __forceinline__ void load_phys(const float* __restrict__ st, int N, i
 // One policy step per lane. Live state across the 4 substeps is kept to the physics state, the
 // joint targets and the ~15 floats of the lagged observation cache the rewards need; the MDP
 // state is loaded from HBM only after the physics.
-template <bool kTgs, bool kRefresh = false>
+template <bool kTgs, bool kRefresh = false, bool kRf = false>
 __device__ __forceinline__ void step_body(const zb_model* __restrict__ mg, const float4* __restrict__ links,
                                           zb_task_cfg cfg, int N, float* __restrict__ st,
                                           const float* __restrict__ act, float* __restrict__ obs,
@@ -3148,7 +3154,7 @@ __device__ __forceinline__ void step_body(const zb_model* __restrict__ mg, const
   sp.mark(0);
   for (int k = 0; k < cfg.decimation; ++k) {
     // (a compile-time `true` here lets the scheduler reshape the loop into a 36 B/lane spill)
-    substep<false, false, kTgs, kRefresh>(m, cfg, p, target, q, opaque_true(), true, so, nullptr, nullptr, sp);
+    substep<false, false, kTgs, kRefresh, kRf>(m, cfg, p, target, q, opaque_true(), true, so, nullptr, nullptr, sp);
     sens_record(q, k, so);
     sp.mark(7);
     sp.substep_end(k);
@@ -3395,7 +3401,8 @@ __device__ __forceinline__ void step_body(const zb_model* __restrict__ mg, const
 // N <= 4096 envs (<= 1024 waves) the dispatcher then gives every wave its own SIMD, whereas with
 // two-wave occupancy it doubles up 6-11 % of the SIMDs and leaves as many idle
 // (tools/probe/wave_placement.hip), and the doubled-up waves set the launch's tail.
-template <bool kTgs, int kOcc, bool kRefresh = false>
+// kRf: the ruling-on-face manifold compiled in (launched for self_manifold 3 only)
+template <bool kTgs, int kOcc, bool kRefresh = false, bool kRf = false>
 __global__ __launch_bounds__(WGT, kOcc) void zb_step_kernel(const zb_model* __restrict__ mg,
                                                           const float4* __restrict__ links, zb_task_cfg cfg, int N,
                                                           float* __restrict__ st, const float* __restrict__ act,
@@ -3404,7 +3411,7 @@ __global__ __launch_bounds__(WGT, kOcc) void zb_step_kernel(const zb_model* __re
                                                           float* __restrict__ acc, float* __restrict__ wc) {
   __shared__ float4 lds[LDS4];
   if (kOcc == 1) asm volatile("" ::: "a255");
-  step_body<kTgs, kRefresh>(mg, links, cfg, N, st, act, obs, rew, term, trunc, acc, wc, lds);
+  step_body<kTgs, kRefresh, kRf>(mg, links, cfg, N, st, act, obs, rew, term, trunc, acc, wc, lds);
 }
 
 // Test entry (zb_pair_manifold): GJK (cold start) + the face manifold of n link pairs given as
@@ -3428,7 +3435,7 @@ __global__ void zb_manifold_kernel(const float* __restrict__ pairs, int n, float
   const bool mine = (t >> 2) < n;
   int cnt = 0;
   if (hit && sc.sep > -2.f * kCoreM + 1e-7f)
-    cnt = quad_manifold(h, j, sc, margin, true, mode, [&](int rank, float4 xs, const float* nn) {
+    cnt = quad_manifold<true>(h, j, sc, margin, true, mode, [&](int rank, float4 xs, const float* nn) {
       if (mine) {
         float* p = o + 1 + 7 * rank;
         p[0] = xs.w; p[1] = nn[0]; p[2] = nn[1]; p[3] = nn[2]; p[4] = xs.x; p[5] = xs.y; p[6] = xs.z;
@@ -3566,7 +3573,7 @@ __global__ __launch_bounds__(WGT, ZB_WAVES_PER_SIMD) void zb_substeps_kernel(con
   SensorOut so;
   Stamps sp;
   for (int k = 0; k < nsub; ++k)
-    substep<true, kLinkFriction, kTgs, kRefresh>(m, cfg, p, tg, q, k == nsub - 1, k > 0, so, F, tau, sp);
+    substep<true, kLinkFriction, kTgs, kRefresh, true>(m, cfg, p, tg, q, k == nsub - 1, k > 0, so, F, tau, sp);
   if (net_force && q.s < NL)
 #pragma unroll
     for (int a = 0; a < 3; ++a) net_force[((size_t)i * NL + q.s) * 3 + a] = F[0][a];
@@ -3658,7 +3665,7 @@ __device__ __forceinline__ void su_reset_pose(MP m, const zb_task_cfg& cfg, uint
 }
 
 // One stand-up policy step per team (same mapping as zb_step_kernel; no contact sensor).
-template <bool kTgs, int kOcc, bool kRefresh = false>
+template <bool kTgs, int kOcc, bool kRefresh = false, bool kRf = false>
 __global__ __launch_bounds__(WGT, kOcc) void zb_su_step_kernel(
     const zb_model* __restrict__ mg, const float4* __restrict__ links, zb_task_cfg cfg, int N, float* __restrict__ st,
     const float* __restrict__ act, float* __restrict__ obs, float* __restrict__ rew, uint8_t* __restrict__ term,
@@ -3707,7 +3714,7 @@ __global__ __launch_bounds__(WGT, kOcc) void zb_su_step_kernel(
   wc_load(q, wc, N, i);  // the first substep's GJK warm start
   sp.mark(0);
   for (int k = 0; k < cfg.decimation; ++k) {
-    substep<false, true, kTgs, kRefresh>(m, cfg, p, target, q, false, true, so, nullptr, nullptr, sp);
+    substep<false, true, kTgs, kRefresh, kRf>(m, cfg, p, target, q, false, true, so, nullptr, nullptr, sp);
     sp.mark(7);
   }
   m = opaque(m);
@@ -5195,9 +5202,11 @@ int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_dev
   if (c->decimation < 1 || c->decimation > MAXSUB || c->solver_iterations < 0 || c->solver_mode < 0 ||
       c->solver_mode > 3 || (c->solver_mode >= 1 && c->solver_iterations < 1) ||
       (c->solver_mode >= 2 && c->task != ZB_TASK_WALKING_V2 && c->task != ZB_TASK_STANDUP_V0) ||
-      c->self_manifold < 0 || c->self_manifold > 3)
+      c->self_manifold < 0 || c->self_manifold > 3 ||
+      (c->self_manifold == 3 && c->task != ZB_TASK_WALKING_V2 && c->task != ZB_TASK_STANDUP_V0))
     return set_err(-1, "zb_create: cfg (decimation 1..8, solver_iterations >= 0, solver_mode 0..3, iterations "
-                       ">= 1 from mode 1; modes 2, 3 for walking v2 and stand-up; self_manifold 0..3)",
+                       ">= 1 from mode 1; modes 2, 3 for walking v2 and stand-up; self_manifold 0..3, 3 for "
+                       "walking v2 and stand-up)",
                    hipSuccess);
   if (c->task != ZB_TASK_WALKING_V2 && c->task != ZB_TASK_STANDUP_V0 && c->task != ZB_TASK_WALKING_V4 &&
       c->task != ZB_TASK_MANAGER_V0)
@@ -5525,9 +5534,14 @@ int zb_step(zb_handle h, const float* actions, float* obs, float* reward, uint8_
 #define ZB_LAUNCH(K, ...)                                                                          \
   (tgs ? (one ? zb_launch(K<true, 1>, blocks, s, e0, e1, __VA_ARGS__) : zb_launch(K<true, 2>, blocks, s, e0, e1, __VA_ARGS__)) \
        : (one ? zb_launch(K<false, 1>, blocks, s, e0, e1, __VA_ARGS__) : zb_launch(K<false, 2>, blocks, s, e0, e1, __VA_ARGS__)))
-  // solver_modes 2, 3 (the TGS refresh): walking v2 and stand-up only (zb_create), two-wave occupancy
+  // solver_modes 2, 3 (the TGS refresh) and self_manifold 3 (the ruling-on-face manifold): walking v2
+  // and stand-up only (zb_create), two-wave occupancy
+  const bool rf = h->cfg.self_manifold == 3;
 #define ZB_LAUNCH_R(K, ...)                                                                        \
-  (refresh ? zb_launch(K<true, 2, true>, blocks, s, e0, e1, __VA_ARGS__) : ZB_LAUNCH(K, __VA_ARGS__))
+  (rf ? (refresh ? zb_launch(K<true, 2, true, true>, blocks, s, e0, e1, __VA_ARGS__)                 \
+                 : (tgs ? zb_launch(K<true, 2, false, true>, blocks, s, e0, e1, __VA_ARGS__)          \
+                        : zb_launch(K<false, 2, false, true>, blocks, s, e0, e1, __VA_ARGS__)))       \
+      : refresh ? zb_launch(K<true, 2, true>, blocks, s, e0, e1, __VA_ARGS__) : ZB_LAUNCH(K, __VA_ARGS__))
   if (h->task == ZB_TASK_STANDUP_V0)
     ZB_LAUNCH_R(zb_su_step_kernel, h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward, terminated,
               truncated, h->d_acc, h->d_cnt, h->seed, h->d_wc);
