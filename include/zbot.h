@@ -330,7 +330,8 @@ typedef struct zb_task_cfg {
    * two rulings within 5 degrees of the contact plane and of each other: the GJK point and the two
    * ends of the rulings' overlap (up to 3 points); 3 = 2 plus a ruling lying on a face (a face on one
    * side, a ruling within 5 degrees of the contact plane on the other): the GJK point and the ends of
-   * the ruling's stretch over the face disk (up to 3 points); 0 = one point per pair */
+   * the ruling's stretch over the face disk (up to 3 points; walking v2 and stand-up, whose kernels
+   * for it are separate builds); 0 = one point per pair */
   int32_t self_manifold;
   /* walking v2: bit t set = reward term t is in the active reward_cfg (v2.py:246-257 builds
    * reward_functions from its keys). The reference updates a stateful term's buffers inside its

@@ -173,20 +173,23 @@ def test_fused_gae_matches_torch(gpu, monkeypatch):
     assert abs(float(st.advantages.mean())) < 1e-5 and abs(float(st.advantages.std()) - 1.0) < 1e-4
 
 
-@pytest.mark.parametrize("rows", ["reg", "lds"])
+@pytest.mark.parametrize("rows", ["reg", "lds", "reg-small"])
 @pytest.mark.parametrize("hidden", [[128, 128, 128], [256, 256, 128]], ids=["v2-nets", "standup-nets"])
 def test_fused_act_matches_torch_policy(gpu, hidden, rows, monkeypatch):
     """zbp_act (the rollout's policy step, runner._rollout) against PPO.act's torch statement with the
     same standard-normal draw: actions, mu, sigma, log-probabilities, values and the observations in
     the storage slot (fp32 summation-order tolerances); rows not a multiple of 32 included. rows: the
-    register-resident forward (k_act_reg, rollouts of >= 16384 rows) or the LDS one (ZBP_ROWS=lds,
-    and every smaller rollout)."""
+    register-resident forward (k_act_reg, rollouts of >= 4096 rows; reg-small: forced at 200 rows) or
+    the LDS one (ZBP_ACT=lds, and every smaller rollout)."""
     import torch
     from zbot_lab_amd.rl import fused
     if rows == "lds":
         monkeypatch.setenv("ZBP_ROWS", "lds")
-    # (k_act_reg takes rollouts of >= 16384 rows; 16 400 is not a multiple of its 64-row workgroups)
-    for envs in ((16400, 512) if rows == "reg" else (512, 200)):
+        monkeypatch.setenv("ZBP_ACT", "lds")
+    if rows == "reg-small":  # (the register-resident forward forced below its row threshold)
+        monkeypatch.setenv("ZBP_ACT", "reg")
+    # (k_act_reg takes rollouts of >= 4096 rows; 16 400 is not a multiple of its 64-row workgroups)
+    for envs in {"reg": (16400, 4096), "lds": (4096, 200), "reg-small": (200,)}[rows]:
         alg = _alg(hidden, envs=envs)
         fu = fused.FusedUpdate(alg, 256)  # (the minibatch size shapes only the update's row buffers)
         st = alg.storage

@@ -1135,19 +1135,23 @@ __global__ __launch_bounds__(256) void k_act(ActArgs A) {
 // k_act on the register-resident forward (k_rows_reg's shapes): one wave per 16 rows, the weights
 // shared through LDS
 template <int T1, int T2, int T3>
+#ifndef ZBP_ACT_REG_MIN
+#define ZBP_ACT_REG_MIN 4096
+#endif
 __global__ __launch_bounds__(RR_WG, 2) void k_act_reg(ActArgs A) {
   constexpr int CB = 32;
   __shared__ float4 wl[2 * CB * 64];
   const int lane = threadIdx.x & 63, r = lane & 15, gq = lane >> 4;
-  const int row0 = (blockIdx.x * (RR_WG / 64) + (threadIdx.x >> 6)) * RR_TR;  // (waves past the rows run on zeros, store nothing)
+  // workgroup pairs: even = the actor over four row tiles, odd = the critic over the same tiles
+  const int net = blockIdx.x & 1;
+  const int row0 = ((blockIdx.x >> 1) * (RR_WG / 64) + (threadIdx.x >> 6)) * RR_TR;  // (waves past the rows run on zeros, store nothing)
   const int64_t row = row0 + r;
   const bool ok = row < A.rows;
   const int na = A.na;
   Tile z[2];
   RrStage<CB> wst;
-  rr_fetch<2 * T1, CB>(A.ws + A.n[0].wr[0], 0, wst);
-#pragma unroll
-  for (int net = 0; net < 2; ++net) {
+  rr_fetch<2 * T1, CB>(A.ws + A.n[net].wr[0], 0, wst);
+  {
     const NetW& w = A.n[net];
     const int dim = net ? A.cobs_dim : A.obs_dim;
     const float* src = (net ? A.cobs : A.obs) + row * dim;
@@ -1163,10 +1167,7 @@ __global__ __launch_bounds__(RR_WG, 2) void k_act_reg(ActArgs A) {
     rr_forward<2, T1, false, false, T1 * T2, CB>(w, 0, A.ws, wl, 0, x0, x1, wst, A.ws + w.wr[1]);
     rr_forward<T1, T2, false, false, T2 * T3, CB>(w, 1, A.ws, wl, 0, x1, x2, wst, A.ws + w.wr[2]);
     rr_forward<T2, T3, false, false, T3 * 2, CB>(w, 2, A.ws, wl, 0, x2, x3, wst, A.ws + w.wr[3]);
-    if (net == 0)
-      rr_forward<T3, 2, true, false, 2 * T1, CB>(w, 3, A.ws, wl, 0, x3, z, wst, A.ws + A.n[1].wr[0]);
-    else
-      rr_forward<T3, 2, true, false, 0, CB>(w, 3, A.ws, wl, 0, x3, z, wst, nullptr);
+    rr_forward<T3, 2, true, false, 0, CB>(w, 3, A.ws, wl, 0, x3, z, wst, nullptr);
     if (net == 0) {
       // lane (r, g) holds actions 4 g + u and 16 + 4 g + u of row r
       const float kLog2Pi = 0.91893853320467274178f;  // log(sqrt(2 pi))
@@ -1533,9 +1534,12 @@ int zbp_act(const zbp_net* actor, const zbp_net* critic, const float* std_param,
     if (e != hipSuccess) return hip_fail(e, "hipFuncSetAttribute k_act");
     lds_set = true;
   }
-  // (the register-resident forward once the rows fill the CUs: below that its 64-row workgroups are
-  // too few and the LDS kernel's 32-row ones win, e.g. 35 vs 42 us at 4096 rows, 242 vs 147 at 32 768)
-  const int shape = io->rows >= 16384 ? reg_shape(lo) : 0, wgs = (io->rows + 63) / 64;
+  // (the register-resident forward, actor and critic in separate workgroups, from ZBP_ACT_REG_MIN rows
+  // (4096): 23.5 us against the LDS kernel's 34.9 at 4096 rows (before the split 42 us: too few
+  // workgroups), 146 against 242 at 32 768 (profiles/r5y); ZBP_ACT=lds / reg for A/Bs)
+  const char* ea = getenv("ZBP_ACT");
+  const int reg_min = ea && !strcmp(ea, "reg") ? 0 : (ea && !strcmp(ea, "lds") ? (1 << 30) : ZBP_ACT_REG_MIN);
+  const int shape = io->rows >= reg_min ? reg_shape(lo) : 0, wgs = 2 * ((io->rows + 63) / 64);
   if (shape == 1)
     k_act_reg<16, 16, 8><<<wgs, RR_WG, 0, (hipStream_t)stream>>>(A);
   else if (shape == 2)
