@@ -91,7 +91,13 @@ int wgrad_slots() {
     (void)hipGetLastError();
     return n;
   }();
-  return 2 * cus;
+  // (ZBP_WGRAD_SLOTS_PER_CU, read once: the split-K A/B; default 2 = the resident k_wgrad workgroups)
+  static const int per_cu = [] {
+    const char* e = getenv("ZBP_WGRAD_SLOTS_PER_CU");
+    const int v = e ? atoi(e) : 2;
+    return v >= 1 && v <= 8 ? v : 2;
+  }();
+  return per_cu * cus;
 }
 
 Layout make_layout(const zbp_net* a, const zbp_net* c, int B) {
