@@ -220,3 +220,19 @@ def test_rollout_statistics(gpu):
     # whole rollout: statistics
     assert abs(rg.mean() - ro.mean()) <= 0.1 * abs(ro.mean()) + 0.01, (rg.mean(), ro.mean())
     assert abs(dg.mean() - do.mean()) <= 0.25 * do.mean() + 0.002, (dg.mean(), do.mean())
+
+
+def test_create_rejects_ruling_on_face_outside_v2_and_standup(gpu):
+    """zb_create refuses self_manifold 3 for v4 and the manager env (include/zbot.h: the ruling-on-face
+    code is compiled only into the walking v2 and stand-up kernels launched for it) instead of running
+    it as mode 2; walking v2 and stand-up accept it."""
+    from zbot_lab_amd._native import ZbotError
+    from zbot_lab_amd.sim import ZbotSim
+    for make in (zm.TaskCfg.walking_v4, zm.TaskCfg.manager_flat):
+        cfg = make()
+        cfg.self_manifold = 3
+        with pytest.raises(ZbotError):
+            ZbotSim(64, cfg, device="cuda:0", seed=0)
+    for cfg in (zm.TaskCfg(), zm.TaskCfg.standup()):
+        cfg.self_manifold = 3
+        ZbotSim(64, cfg, device="cuda:0", seed=0).close()
