@@ -63,7 +63,9 @@ def parse():
     # ablation knobs (the reported line uses the defaults)
     p.add_argument("--solver-iterations", type=int, default=None)
     p.add_argument("--no-self-collision", action="store_true")
-    p.add_argument("--self-manifold", type=int, default=None, help="zb_task_cfg.self_manifold (0 / 1 / 2)")
+    p.add_argument("--self-manifold", type=int, default=None, help="zb_task_cfg.self_manifold (0 / 1 / 2 / 3)")
+    p.add_argument("--solver-mode", type=int, default=None,
+                   help="zb_task_cfg.solver_mode (0 PGS, 1 TGS, 2 TGS + ground refresh, 3 + self refresh)")
     p.add_argument("--rehearsal", action="store_true",
                    help="N ranks share cuda:0 over gloo (one-GPU box rehearsal; reports n_gpus 1)")
     return p.parse_args()
@@ -72,50 +74,62 @@ def parse():
 ENVS_PER_WORKGROUP = 4         # zb_step_kernel: one 64-lane workgroup = 4 envs x 16 lanes
 
 
-def pmc_traffic(num_envs: int, kernel: str = "zb_step_kernel"):
-    """HBM bytes per zb_step_kernel launch from the committed rocprofv3 PMC passes (separate
-    FETCH_SIZE / WRITE_SIZE runs, profiles/<round>/pmc_*_zb_step_kernel.csv) for the same grid
-    (work-items = 64 per workgroup of 4 envs).
-    FETCH_SIZE/WRITE_SIZE are KiB. Calibrated for this kernel's access patterns (team loads and
-    staged stores under the XCD-aware workgroup mapping, tools/calib, profiles/r1i_calib):
-    FETCH_SIZE counts 1/2 of the bytes read (the guide's gfx950 tally), WRITE_SIZE the bytes
-    written, so traffic = 2 x FETCH + WRITE. Returns (bytes, source) or (None, None)."""
-    import csv
-    import glob
+VALU_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: FP32 vector peak (256 CUs x 4 SIMDs x 64 FLOP/clk x 2.4 GHz)
+VALU_LANE_OPS_PEAK_T = 39.3   # one wave64 VALU instruction per SIMD per 4 cycles: 256 x 4 x 16 lanes x 2.4 GHz
+ROOFLINE_PMC = "roofline_pmc.json"
+
+
+def pmc_entry(num_envs: int, kernel: str = "zb_step_kernel"):
+    """The PMC-derived numbers of the dominant kernel for this grid (work-items = 64 per workgroup of 4
+    envs) from the tracked ``roofline_pmc.json`` (written by scripts/prof_summary.py from the rocprofv3
+    passes committed under profiles/<round>/; it travels to the GPU box, profiles/ does not). None when
+    no pass covers this kernel and grid."""
     here = os.path.dirname(os.path.abspath(__file__))
-    for d in sorted(glob.glob(os.path.join(here, "profiles", "r*")), reverse=True):
-        vals = {}
-        for name in ("FETCH_SIZE", "WRITE_SIZE"):
-            for f in glob.glob(os.path.join(d, f"pmc_*_{kernel}.csv")):
-                for row in csv.DictReader(open(f)):
-                    grid = -(-num_envs // ENVS_PER_WORKGROUP) * 64
-                    if row["counter"] == name and int(row["grid"]) == grid:
-                        vals[name] = float(row["mean_per_dispatch"]) * 1024.0
-        if len(vals) == 2:
-            return 2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"], os.path.relpath(d, here)
-    return None, None
+    grid = -(-num_envs // ENVS_PER_WORKGROUP) * 64
+    try:
+        db = json.load(open(os.path.join(here, ROOFLINE_PMC)))
+    except (OSError, ValueError):
+        return None
+    return db.get(f"{kernel}@{grid}")
+
+
+def pmc_traffic(num_envs: int, kernel: str = "zb_step_kernel"):
+    """HBM bytes per launch: 2 x FETCH_SIZE + WRITE_SIZE (separate rocprofv3 passes, KiB). Calibrated for
+    this kernel's access patterns (team loads and staged stores under the XCD-aware workgroup mapping,
+    tools/calib, profiles/r1i_calib): FETCH_SIZE counts 1/2 of the bytes read (the guide's gfx950 tally),
+    WRITE_SIZE the bytes written. Returns (bytes, source) or (None, None)."""
+    e = pmc_entry(num_envs, kernel)
+    if e is None or "traffic_bytes" not in e:
+        return None, None
+    return e["traffic_bytes"], e["source"]
 
 
 def pmc_issue(num_envs: int, kernel: str = "zb_step_kernel"):
-    """VALU issue fraction of the dominant kernel from the committed PMC passes (same grid): the
-    quad-cycles a wave spends issuing VALU instructions (SQ_ACTIVE_INST_VALU) over its resident
-    quad-cycles (SQ_WAVE_CYCLES), plus VALU instructions per wave. With one wave per SIMD (4096
-    envs) this is the SIMD's VALU utilisation — the kernel's real bound."""
-    import csv
-    import glob
-    here = os.path.dirname(os.path.abspath(__file__))
-    grid = -(-num_envs // ENVS_PER_WORKGROUP) * 64
-    for d in sorted(glob.glob(os.path.join(here, "profiles", "r*")), reverse=True):
-        vals = {}
-        for f in glob.glob(os.path.join(d, f"pmc_sq*_{kernel}.csv")):
-            for row in csv.DictReader(open(f)):
-                if int(row["grid"]) == grid:
-                    vals[row["counter"]] = float(row["mean_per_dispatch"])
-        if all(k in vals for k in ("SQ_ACTIVE_INST_VALU", "SQ_WAVE_CYCLES", "SQ_INSTS_VALU", "SQ_WAVES")):
-            return {"bound": "valu-issue", "frac": vals["SQ_ACTIVE_INST_VALU"] / vals["SQ_WAVE_CYCLES"],
-                    "valu_insts_per_wave": vals["SQ_INSTS_VALU"] / vals["SQ_WAVES"],
-                    "waves": vals["SQ_WAVES"], "source": os.path.relpath(d, here)}
-    return None
+    """VALU issue fraction of the dominant kernel (same grid): the quad-cycles a wave spends issuing VALU
+    instructions (SQ_ACTIVE_INST_VALU) over its resident quad-cycles (SQ_WAVE_CYCLES), plus VALU
+    instructions per wave. With one wave per SIMD (4096 envs) this is the SIMD's VALU utilisation -- the
+    kernel's real bound."""
+    e = pmc_entry(num_envs, kernel)
+    if e is None or "issue_frac" not in e:
+        return None
+    return {"bound": "valu-issue", "frac": e["issue_frac"], "wait_any_frac": e.get("wait_any_frac"),
+            "valu_insts_per_wave": e.get("valu_insts_per_wave"), "waves": e.get("waves"), "source": e["source"]}
+
+
+def valu_roofline(num_envs: int, kernel_s: float, kernel: str = "zb_step_kernel"):
+    """The VALU half of the roofline: VALU lane-instructions per launch (SQ_INSTS_VALU x 64 lanes, inactive
+    lanes included) over the kernel time measured in this run. ``achieved`` counts every lane-instruction
+    as an FMA (2 FLOP) -- an upper bound on the FP32 rate -- against the 157.3 TF vector peak (which
+    assumes packed FMAs); ``issue_frac_device`` is the lane-instruction rate against the chip's
+    non-packed issue rate (39.3 T lane-instructions/s)."""
+    e = pmc_entry(num_envs, kernel)
+    if e is None or "valu_insts_per_wave" not in e or not kernel_s:
+        return None
+    lane_ops = e["valu_insts_per_wave"] * e["waves"] * 64.0
+    tflops = 2.0 * lane_ops / kernel_s / 1e12
+    return {"bound": "valu", "achieved": tflops, "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s (upper bound)",
+            "frac": tflops / VALU_PEAK_TFLOPS, "lane_ops_per_env_step": lane_ops / num_envs,
+            "issue_frac_device": lane_ops / kernel_s / 1e12 / VALU_LANE_OPS_PEAK_T, "source": e["source"]}
 
 
 def host_cpu_info() -> dict:
@@ -281,6 +295,8 @@ def main():
         cfg.solver.iterations = args.solver_iterations
     if args.self_manifold is not None:
         cfg.solver.self_manifold = args.self_manifold
+    if args.solver_mode is not None:
+        cfg.solver.mode = args.solver_mode
     if args.no_self_collision:
         cfg.solver.self_collision = False
     env = (Zbot6SUpEnv(cfg) if standup else Zbot6SEnvV4(cfg) if v4 else ZbotManagerBasedRLEnv(cfg) if mgr
@@ -353,6 +369,9 @@ def main():
             "data": "synthetic: default-pose starts, full reset, randn(N,6) actions seeded 42+rank",
             "config": {"workload": workload,
                        "envs_per_gpu": n, "total_envs": n * world, "decimation": 4, "sim_dt": 0.005,
+                       "solver": {"mode": cfg.solver.mode, "iterations": cfg.solver.iterations,
+                                  "self_manifold": cfg.solver.self_manifold,
+                                  "self_collision": cfg.solver.self_collision},
                        "parallelism": f"env-sharded x{world} (replicas, no collective)",
                        "collective": {"backend": plan["backend"], "world_size": coll_world},
                        "per_rank_env_steps_per_s": per_rank_rates,
@@ -361,7 +380,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": kname, "kernel_ms": kern_s * 1e3,
-                         "bytes_per_env_step": bpe, "issue": pmc_issue(n, kname)},
+                         "bytes_per_env_step": bpe, "issue": pmc_issue(n, kname),
+                         "valu": valu_roofline(n, kern_s, kname)},
             "cpu_baseline": None,
         }
         if not args.no_cpu_baseline and world == 1:

@@ -331,14 +331,20 @@ typedef struct zb_task_cfg {
    * ends of the rulings' overlap (up to 3 points); 3 = 2 plus a ruling lying on a face (a face on one
    * side, a ruling within 5 degrees of the contact plane on the other): the GJK point and the ends of
    * the ruling's stretch over the face disk (up to 3 points; walking v2 and stand-up, whose kernels
-   * for it are separate builds); 0 = one point per pair */
+   * for it are separate builds); a ruling-on-face pair that keeps no end point is tested as a
+   * side-by-side pair as in 2 (a pair that qualifies for both takes the ruling-on-face points: 30 of
+   * 56 side-by-side pairs in 200 k random folds, 3 of whose envs end with one point fewer than in
+   * mode 2); 0 = one point per pair */
   int32_t self_manifold;
   /* walking v2: bit t set = reward term t is in the active reward_cfg (v2.py:246-257 builds
    * reward_functions from its keys). The reference updates a stateful term's buffers inside its
    * _reward_<name> only, so they advance only while the term is active: base_heading_x_sum
    * (v2.py:484-487), base_pos_y_err_sum (497-500), step_length's touchdown latches and
    * feet_contact_forces_last (509-533), feet_force_sum (567-571). A term can be active with
-   * weight 0. Other tasks ignore it. */
+   * weight 0. Other tasks ignore it. zb_create rejects a walking-v2 cfg in which a term with a non-zero
+   * reward_scales[t] has bit t clear (set every bit, 0xFFFFFFFF, for "all terms active").
+   * ABI: this trailing field was added in round 5; a caller built against the older struct must be
+   * rebuilt (sizeof(zb_task_cfg) grew by 4 bytes). */
   uint32_t reward_active;
 } zb_task_cfg;
 
@@ -373,6 +379,14 @@ int zb_read_log(zb_handle h, float* term_means, int32_t* counts, void* stream);
  * resets fills in stream order, exactly as zb_read_log would (no per-step copies). NULL, NULL
  * unregisters. */
 int zb_set_log_buffers(zb_handle h, float* term_means, int32_t* counts);
+/* Register a caller-owned device accumulator float[ZB_LOG_LEN + ZB_LOG_COUNTS]: every later zb_step
+ * adds the log's current values to it in stream order (the term means as zb_read_log returns them --
+ * this step's when it had resets, else the last step-with-resets' -- then the counts as floats),
+ * inside the step's finalize launch. It replaces the host runner's per-step sum of extras["log"]
+ * (rsl_rl's OnPolicyRunner appends every step's log and averages it at log time,
+ * rsl_rl/runners/on_policy_runner.py; the reference's train.py:205 runner.learn). Resets do not
+ * add. NULL unregisters. */
+int zb_set_log_accumulator(zb_handle h, float* acc);
 
 /* Persistent state, device float[zb_state_dim(h)][N] (ZB_STATE_DIM / ZB_SU_STATE_DIM).
  * zb_set_state also invalidates the contact cache below. */

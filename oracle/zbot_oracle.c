@@ -885,12 +885,13 @@ static int rim_face_manifold(const hull_t* A, const hull_t* B, const contact_t* 
 }
 
 /* the self-contact manifold of cfg->self_manifold (1: faces; 2: faces, else side-by-side rims; 3:
- * faces, else a ruling on a face, else side-by-side rims; 0: none) */
+ * faces, else a ruling on a face with at least one end point, else side-by-side rims; 0: none) */
 static int self_manifold(int mode, const hull_t* A, const hull_t* B, const contact_t* c0, real margin, contact_t out[4]) {
   if (mode < 1 || !(c0->sep > -2 * (real)CORE_M + (real)1e-7)) return 0;
   int k = face_manifold(A, B, c0, margin, out);
   if (k > 0 || mode < 2) return k;
-  if (mode >= 3 && (k = rim_face_manifold(A, B, c0, margin, out)) > 0) return k;
+  /* (a ruling-on-face pair that keeps only its GJK point may still lie side by side: ADVICE r5) */
+  if (mode >= 3 && (k = rim_face_manifold(A, B, c0, margin, out)) >= 2) return k;
   return rim_manifold(A, B, c0, margin, out);
 }
 
@@ -3344,9 +3345,6 @@ int zbo_contact_diag(zbo_sim* s, float* out) {
   return 0;
 }
 
-/* per env: the smallest self-collision separation over all link pairs (GJK on the rounded cores,
- * no early exit; -2 CORE_M = cores overlapping, beyond the exact range). Parity tests use it to
- * set aside random test states whose links interpenetrate deeper than the shape model covers. */
 /* per env, the self-contact classes of its link pairs at the current state (tests: constructed
  * manifold states, planted rare-branch bugs): out [n][10] = {pairs in contact, face-manifold pairs,
  * rim-manifold pairs (side by side, >= 2 points), overlapping-core pairs (the separating-axis
@@ -3378,7 +3376,7 @@ int zbo_pair_classes(zbo_sim* s, float* out) {
       const int km = self_manifold(s->c.self_manifold, &A, &B, &c, margin, mf);
       if (kf > 0) { ++nf; if (pf < 0) pf = p; }
       else if (kr >= 2) { ++nrf; if (prf < 0) prf = p; }
-      else if (kr == 0 && km >= 2) { ++nr; if (pr < 0) pr = p; }
+      else if (km >= 2) { ++nr; if (pr < 0) pr = p; }
       np_ += km > 0 ? km : 1;
     }
     float* o = out + 10 * (size_t)e;
@@ -3388,6 +3386,9 @@ int zbo_pair_classes(zbo_sim* s, float* out) {
   return 0;
 }
 
+/* per env: the smallest self-collision separation over all link pairs (GJK on the rounded cores,
+ * no early exit; -2 CORE_M = cores overlapping, beyond the exact range). Parity tests use it to
+ * set aside random test states whose links interpenetrate deeper than the shape model covers. */
 int zbo_self_min_sep(zbo_sim* s, float* out) {
   for (int e = 0; e < s->n; ++e) {
     kin_t k;

@@ -1,4 +1,4 @@
-"""Shared test helpers: seeded perturbed simulator states (numpy, SoA [84][N])."""
+"""Shared test helpers: seeded perturbed simulator states (numpy, SoA [87][N] for walking v2, include/zbot.h)."""
 from __future__ import annotations
 
 import numpy as np

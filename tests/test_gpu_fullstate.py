@@ -238,6 +238,18 @@ REFINE_DEEP_MAX, REFINE_DEEP_RUNS = 4, 1024
 AGG_MED_K, AGG_MED_ABS = 4.0, 0.02
 
 
+def _record_stats(task, label, n, **kw):
+    """ZB_PARITY_STATS=<file>: append one JSON line per check (the library under test, the check, its
+    aggregate numbers) -- the build-flag A/B of DESIGN.md §6 reads them (scripts/parity_ab.py)."""
+    import json
+    import os
+    path = os.environ.get("ZB_PARITY_STATS")
+    if path:
+        with open(path, "a") as f:
+            f.write(json.dumps({"lib": os.environ.get("ZBOT_LIB", "libzbot.so"), "task": task, "check": label,
+                                "envs": n, **kw}) + "\n")
+
+
 def _aggregate(ratio, active):
     r = ratio[active]
     return (float((r > 1).mean()) if len(r) else 0.0), (float(np.median(np.minimum(r, 1e6))) if len(r) else 0.0)
@@ -276,6 +288,8 @@ def _check(task, label, n, seed, st, actions, g_out, sg, torch, wc=None, stats=N
           f"{frac_g:.2%} / {med_g:.3g}; f64 vs f32 oracle {frac_x:.2%} / {med_x:.3g})")
     if stats is not None:
         stats.update(frac=frac, med=med, frac_f32=frac_o, med_f32=med_o, active=int(active.sum()), nbad=len(bad))
+    _record_stats(task, label, n, frac=frac, med=med, frac_f32=frac_o, med_f32=med_o, frac_vs_f32=frac_g,
+                  med_vs_f32=med_g, active=int(active.sum()), nbad=len(bad))
     unexplained = [int(e) for e in bad if not _explained(ratio[e], sens[e])]
     ndeep = 0
     if unexplained:

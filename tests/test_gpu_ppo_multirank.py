@@ -97,3 +97,90 @@ def test_two_rank_fused_update_matches_torch_update(gpu):
     # (update_sums are rank-local losses in both paths: rsl_rl logs the local minibatch losses)
     for r in range(2):
         np.testing.assert_allclose(fu[r][6], to[r][6], rtol=1e-4, atol=1e-6)
+
+
+def _seg_worker(rank, world, port, q):
+    """Two updates from one snapshot: the second eager, then again with the minibatch segments captured
+    as HIP graphs on either side of the all-reduce (PPO.capture_update_segments)."""
+    os.environ["ZBOT_PPO_FUSED"] = "1"
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    from zbot_lab_amd.rl.ppo import PPO, ActorCritic
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = "cuda:0"
+        torch.manual_seed(11 + rank)
+        pol = ActorCritic(23, 23, 6, actor_hidden_dims=[128, 128, 128], critic_hidden_dims=[128, 128, 128])
+        alg = PPO(pol, device=dev, multi_gpu_cfg={"global_rank": rank, "world_size": world})
+        alg.broadcast_parameters()
+        envs, steps = 512, 24
+        alg.init_storage(envs, steps, 23, 23, 6)
+        st = alg.storage
+        g = torch.Generator(device=dev).manual_seed(100 + rank)
+        for t in (st.observations, st.critic_observations, st.actions, st.rewards, st.mu):
+            t.copy_(torch.randn(t.shape, device=dev, generator=g))
+        st.sigma.copy_(0.5 + torch.rand(st.sigma.shape, device=dev, generator=g))
+        st.dones.copy_((torch.rand(st.dones.shape, device=dev, generator=g) < 0.05).float())
+        with torch.no_grad():
+            pol.update_distribution(st.observations.flatten(0, 1))
+            st.actions_log_prob.copy_(pol.get_actions_log_prob(st.actions.flatten(0, 1)).view(steps, envs, 1))
+            st.values.copy_(pol.evaluate(st.critic_observations.flatten(0, 1)).view(steps, envs, 1))
+        st.step = steps
+        alg.compute_returns(st.critic_observations[-1])
+
+        def update(seed):
+            alg.generator = torch.Generator(device=dev).manual_seed(seed)
+            alg.draw_minibatch_indices()
+            alg.update_steps()
+            torch.cuda.synchronize()
+
+        update(99)  # the eager first update (the driver, its Adam state and the bucket now exist)
+        assert alg._fused is not None and alg._flat is not None
+        opt = alg.optimizer
+        ps = list(pol.parameters())
+        snap = ([p.detach().clone() for p in ps],
+                [{k: v.clone() for k, v in opt.state[p].items()} for p in ps], alg.lr_t.clone())
+
+        def restore():
+            for p, v in zip(ps, snap[0]):
+                p.data.copy_(v)
+            for p, d in zip(ps, snap[1]):
+                for k, v in d.items():
+                    opt.state[p][k].copy_(v)
+            alg.lr_t.copy_(snap[2])
+
+        update(7)
+        eager = (torch.cat([p.detach().flatten() for p in ps]).cpu().numpy(), float(alg.lr_t),
+                 alg.update_sums.cpu().numpy())
+        restore()
+        ok = alg.capture_update_segments()
+        update(7)
+        graphed = (torch.cat([p.detach().flatten() for p in ps]).cpu().numpy(), float(alg.lr_t),
+                   alg.update_sums.cpu().numpy())
+        q.put((rank, ok, len(alg._seg_pre or []), eager, graphed))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_update_graph_segments_match_eager(gpu):
+    """with world > 1 the update graph is split at the all-reduce (graph -> all-reduce
+    -> graph per minibatch); on two gloo ranks sharing cuda:0 the graphed update is bit-identical to the
+    eager one from the same snapshot, and both ranks stay identical."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29600 + (os.getpid() + 13) % 900
+    ps = [ctx.Process(target=_seg_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = sorted([q.get(timeout=240) for _ in ps], key=lambda t: t[0])
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0, p.exitcode
+    for rank, ok, npre, eager, graphed in out:
+        assert ok and npre == 4
+        np.testing.assert_array_equal(eager[0], graphed[0])
+        assert eager[1] == graphed[1]
+        np.testing.assert_array_equal(eager[2], graphed[2])
+    np.testing.assert_array_equal(out[0][3][0], out[1][3][0])

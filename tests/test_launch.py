@@ -67,7 +67,7 @@ def _runner_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_runner_update_graph_off_by_default_multi_rank():
+def test_runner_update_graph_default_multi_rank():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -80,8 +80,10 @@ def test_runner_update_graph_off_by_default_multi_rank():
         assert p.exitcode == 0
     for rank, is_dist, use_graph, graph_update, forced in out:
         assert is_dist and use_graph          # rollout graph unaffected
-        assert graph_update is False          # update stays eager with world > 1
-        assert forced is True                 # an explicit request is honoured
+        # world > 1: graphs on either side of each minibatch's all-reduce (PPO.capture_update_segments,
+        # after the first eager update; a runner without the fused driver drops back to eager there)
+        assert graph_update is True
+        assert forced is True
 
 
 def test_runner_update_graph_follows_rollout_graph_single_rank(monkeypatch):

@@ -73,7 +73,7 @@ def test_oracle_exports_mirror():
     for s in header_symbols():
         if s in ("zb_last_error", "zb_num_envs", "zb_profile_begin", "zb_profile_end", "zb_create", "zb_destroy",
                  "zb_read_stamps", "zb_read_stamps_slowest", "zb_read_stamp_hist", "zb_read_wave_times",
-                 "zb_set_log_buffers"):
+                 "zb_set_log_buffers", "zb_set_log_accumulator"):
             continue
         assert hasattr(L, "zbo_" + s[3:]), s
 
@@ -125,3 +125,19 @@ def test_ppo_library_exports_and_struct_layouts():
     assert L.zbp_workspace_floats(C.byref(n), C.byref(m), 24576) > 0
     n.dim[2] = 100  # hidden dims must be multiples of 32
     assert L.zbp_workspace_floats(C.byref(n), C.byref(m), 24576) < 0
+
+
+def test_create_rejects_weighted_term_without_active_bit():
+    """a walking-v2 cfg whose weighted term has its reward_active bit clear (e.g. a C caller that
+    zero-initialises the struct) is refused before any HIP call, instead of silently freezing that term's
+    buffers (include/zbot.h reward_active)."""
+    from zbot_lab_amd import _native
+    from zbot_lab_amd import model as zm
+    L = _native.lib()
+    m = zm.load_model()
+    mc = zm.pack_model(m)
+    c = zm.TaskCfg().pack()
+    c.reward_active = 0
+    h = C.c_void_p()
+    rc = L.zb_create(C.byref(mc), C.byref(c), 4, 0, 0, C.byref(h))
+    assert rc < 0 and b"reward_active" in L.zb_last_error()

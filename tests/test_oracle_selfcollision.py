@@ -14,6 +14,7 @@ from __future__ import annotations
 
 
 import ctypes as C
+import os
 
 import numpy as np
 import pytest
@@ -440,3 +441,27 @@ def test_ruling_on_face_manifold():
         assert len(pair_manifold(ha, hb, 0.004)) == 1
     finally:
         lib.zbo_set_pair_manifold_mode(2)
+
+
+def test_ruling_on_face_falls_through_to_side_by_side():
+    """with self_manifold 3 a pair whose ruling-on-face test keeps only its GJK point is still
+    tested as a side-by-side pair, so mode 3 loses no side-by-side pair of mode 2 (each one is a
+    side-by-side or a ruling-on-face pair in mode 3), on random folds (zbo_pair_classes)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from fullstate import random_states, task_cfg
+    from oracle.pyoracle import OracleSim
+    n, res = 60_000, {}
+    for sm in (2, 3):
+        cfg = task_cfg("v2")
+        cfg.self_manifold = sm
+        o = OracleSim(n, cfg, seed=1)
+        st = random_states("v2", o, n, seed=5)
+        st[13:19] = np.random.default_rng(100).uniform(-np.pi, np.pi, (6, n)).astype(np.float32)
+        o.set_state(st)
+        res[sm] = o.pair_classes()
+    a, b = res[2], res[3]
+    rim2 = a[:, 2] > 0
+    assert rim2.sum() >= 5
+    assert np.all((b[rim2, 2] + b[rim2, 8]) >= a[rim2, 2])  # every mode-2 rim pair kept as rim or rim-on-face
+    assert (b[:, 5] < a[:, 5]).sum() <= 1e-4 * n           # points removed only where rim-on-face wins

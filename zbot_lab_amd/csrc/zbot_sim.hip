@@ -1398,7 +1398,9 @@ __device__ __forceinline__ int quad_rimface(const QCircle& h, int j, const SelfC
     ok[e] = span && fabsf(t - tg) * ls > 1e-3f && sep < margin;
     px[e] = make_float4(x[0] - 0.5f * g * uf[0], x[1] - 0.5f * g * uf[1], x[2] - 0.5f * g * uf[2], sep);
   }
-  if (write) {
+  // (quad-uniform: every input above is broadcast over the quad) with the GJK point alone the pair
+  // falls through to the side-by-side test (quad_manifold), so nothing is written for it here
+  if (write && (ok[0] || ok[1])) {
     if (j == 0) sink(0, make_float4(sc.x[0], sc.x[1], sc.x[2], sc.sep), sc.n);  // (GJK's normal: the warm start)
     if (j == 1 && ok[0]) sink(1, px[0], nr);
     if (j == 2 && ok[1]) sink(ok[0] ? 2 : 1, px[1], nr);
@@ -1407,7 +1409,7 @@ __device__ __forceinline__ int quad_rimface(const QCircle& h, int j, const SelfC
 }
 
 // mode = cfg.self_manifold: 1 faces; 2 faces, else side-by-side rims; 3 faces, else a ruling on a
-// face, else side-by-side rims (the oracle's self_manifold). kRf: mode 3 compiled in -- only the
+// face with at least one end point, else side-by-side rims (the oracle's self_manifold). kRf: mode 3 compiled in -- only the
 // kernels launched for self_manifold 3 carry it (its code in the default kernel costs 0.9 % of the
 // step through register allocation alone)
 template <bool kRf, class Sink>
@@ -1432,7 +1434,7 @@ __device__ __forceinline__ int quad_manifold(const QCircle& h, int j, const Self
   if (!(fm & 3) || !(fm & 12)) {
     if (kRf && mode >= 3 && ((fm & 3) == 0) != ((fm & 12) == 0)) {  // a face on exactly one side
       const int k = quad_rimface(h, j, sc, margin, write, sink, fm, uo, r);
-      if (k > 0) return k;
+      if (k >= 2) return k;  // (the GJK point alone: the pair may still lie side by side)
     }
     return mode >= 2 ? quad_rim(h, j, sc, margin, write, sink) : 0;
   }
@@ -3051,6 +3053,7 @@ struct FinArgs {
   uint64_t seed;
   Counters* cnt;
   int ep_len_row;
+  float* user_acc;  // zb_set_log_accumulator: += this step's log values (float[ZB_LOG_LEN + ZB_LOG_COUNTS])
 };
 
 __device__ __forceinline__ void load_phys(const float* __restrict__ st, int N, int i, Phys& p) {
@@ -5089,6 +5092,11 @@ __device__ __forceinline__ void finalize_body(int N, float* __restrict__ st, flo
   }
   __syncthreads();
   if (threadIdx.x == 0) cnt->calls = ctr + 1;
+  // the caller's per-step log accumulator (the PPO runner's mean over a rollout of extras["log"]): every
+  // step adds the current values, those of this step if it had resets, else the last ones (persistent)
+  if (is_step && fa.user_acc && threadIdx.x < ZB_LOG_LEN + ZB_LOG_COUNTS)
+    fa.user_acc[threadIdx.x] += threadIdx.x < ZB_LOG_LEN ? log_means[threadIdx.x]
+                                                         : (float)log_counts[threadIdx.x - ZB_LOG_LEN];
   // lin_vel_cmd_levels widened the ranges in this step: the reference's curriculum runs before the
   // command manager resamples the reset envs, so their commands (and the metrics / observations
   // that read them) are redrawn from the same draws with the new ranges (rare: at most once per
@@ -5108,9 +5116,10 @@ __global__ void zb_finalize_kernel(int N, float* __restrict__ st, float* __restr
                                    float* __restrict__ user_means, int32_t* __restrict__ user_counts, float episode_s,
                                    uint64_t seed, Counters* __restrict__ cnt, int force_full, int reset_counts,
                                    int is_step, int ep_len_row, zb_task_cfg cfg, float* __restrict__ obs,
-                                   const uint8_t* __restrict__ term, const uint8_t* __restrict__ trunc) {
+                                   const uint8_t* __restrict__ term, const uint8_t* __restrict__ trunc,
+                                   float* __restrict__ user_acc) {
   __shared__ float sh[FIN_FG * ACC_STRIDE + ACC];
-  const FinArgs fa = {log_means, log_counts, user_means, user_counts, episode_s, seed, cnt, ep_len_row};
+  const FinArgs fa = {log_means, log_counts, user_means, user_counts, episode_s, seed, cnt, ep_len_row, user_acc};
   finalize_body(N, st, acc, fa, force_full, reset_counts, is_step, cfg, obs, term, trunc, sh);
 }
 
@@ -5138,6 +5147,7 @@ struct zb_sim {
   int32_t* d_log_counts;
   float* u_log_means = nullptr;     // optional caller buffers (zb_set_log_buffers)
   int32_t* u_log_counts = nullptr;
+  float* u_log_acc = nullptr;       // optional caller accumulator (zb_set_log_accumulator)
   // optional per-launch timing of zb_step_kernel (hipEvents on the launch stream)
   int prof_max = 0, prof_n = 0;
   hipEvent_t* prof_ev = nullptr;
@@ -5212,6 +5222,10 @@ int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_dev
       c->task != ZB_TASK_MANAGER_V0)
     return set_err(-1, "zb_create: unknown task", hipSuccess);
   if (c->num_stages < 1 || c->num_stages > ZB_MAX_STAGES) return set_err(-1, "zb_create: num_stages", hipSuccess);
+  if (c->task == ZB_TASK_WALKING_V2)  // a weighted term must be active (a zero-initialised reward_active would
+    for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t)  // freeze its buffers silently; include/zbot.h)
+      if (c->reward_scales[t] != 0.f && !((c->reward_active >> t) & 1u))
+        return set_err(-1, "zb_create: reward term with a non-zero scale but its reward_active bit clear", hipSuccess);
   if (c->task == ZB_TASK_STANDUP_V0 && c->center_z_period < 1) return set_err(-1, "zb_create: center_z_period", hipSuccess);
   HIPCHK(hipSetDevice(hip_device), "hipSetDevice");
   zb_sim* h = new zb_sim();
@@ -5491,7 +5505,7 @@ static int finalize(zb_handle h, hipStream_t s, int full, int reset_counts, int 
                                                      : ZB_S_EP_LEN;
   zb_finalize_kernel<<<1, 256, 0, s>>>(h->n, h->d_state, h->d_acc, h->d_log_means, h->d_log_counts, h->u_log_means,
                                        h->u_log_counts, log_episode_s(h), h->seed, h->d_cnt, full, reset_counts, is_step,
-                                       ep_row, h->cfg, obs, term, trunc);
+                                       ep_row, h->cfg, obs, term, trunc, h->u_log_acc);
   return launch_check("zb_finalize_kernel");
 }
 
@@ -5621,6 +5635,12 @@ int zb_set_log_buffers(zb_handle h, float* term_means, int32_t* counts) {
   if (!h || (!term_means) != (!counts)) return set_err(-1, "zb_set_log_buffers", hipSuccess);
   h->u_log_means = term_means;
   h->u_log_counts = counts;
+  return 0;
+}
+
+int zb_set_log_accumulator(zb_handle h, float* acc) {
+  if (!h) return set_err(-1, "zb_set_log_accumulator", hipSuccess);
+  h->u_log_acc = acc;
   return 0;
 }
 

@@ -234,6 +234,10 @@ class PPO:
         self._tr: dict = {}
         self.generator: torch.Generator | None = None
         self._fused = None  # rl/fused.FusedUpdate, built at the first GPU update
+        # world > 1 on the fused path: each minibatch is [graph: kernels, flatten] -> all-reduce ->
+        # [graph: average, unflatten, rate rule, clip, Adam, re-pack] (capture_update_segments)
+        self._flat = None
+        self._seg_pre, self._seg_post = None, None
 
     def init_storage(self, num_envs: int, num_transitions_per_env: int, obs_dim: int, critic_obs_dim: int,
                      action_dim: int) -> None:
@@ -343,6 +347,7 @@ class PPO:
     def invalidate_fused(self) -> None:
         """Parameters / optimizer state replaced (checkpoint load): rebuild the fused driver."""
         self._fused = None
+        self._flat, self._seg_pre, self._seg_post = None, None, None
 
     def update_steps(self) -> None:
         """All minibatch updates with no host synchronisation (graph-capturable on a GPU), over the
@@ -402,24 +407,79 @@ class PPO:
 
     def _update_steps_fused(self, f, sums: torch.Tensor, adaptive: bool) -> None:
         """update_steps on libzbot_ppo: the same minibatches (rsl_rl's generator order), each one
-        zbp_minibatch (forward, loss, backward into every .grad); then either the fused optimizer
-        (one GPU) or torch's all-reduce / rate rule / clipping / Adam and a re-pack (multi-GPU)."""
+        zbp_minibatch (forward, loss, backward into every .grad), then zbp_optimizer_step (the adaptive
+        rate on the minibatch KL, global-norm clipping, Adam, the re-pack). With world > 1 the gradients
+        and the KL are averaged over the ranks in between: one flat bucket, one all-reduce per minibatch
+        (reference train.py:125-132; rsl_rl's reduce_parameters), the steps on either side of it HIP
+        graphs once ``capture_update_segments`` ran."""
         f.pack()
         mb = f.batch
-        for _ in range(self.num_learning_epochs):
-            for i in range(self.num_mini_batches):
-                stats = f.minibatch(self.storage, self.mb_indices, i * mb)
-                if self.is_multi_gpu:
-                    kl_mean = self.reduce_parameters(stats[0].clone() if adaptive else None)
-                    if adaptive:
-                        self._adapt_learning_rate(kl_mean)
-                    nn.utils.clip_grad_norm_(self.policy.parameters(), self.max_grad_norm)
-                    self.optimizer.step()
-                    sums += stats[1:4]
-                    f.pack()
-                else:
+        if self.is_multi_gpu:
+            if self._flat is None:
+                ps = self._grad_params()
+                self._flat = torch.zeros(sum(p.numel() for p in ps) + 1, device=self.lr_t.device)
+            for _ in range(self.num_learning_epochs):
+                for i in range(self.num_mini_batches):
+                    if self._seg_pre is not None:
+                        self._seg_pre[i].replay()
+                    else:
+                        self._mgpu_pre(f, i * mb)
+                    dist.all_reduce(self._flat, op=dist.ReduceOp.SUM)
+                    if self._seg_post is not None:
+                        self._seg_post.replay()
+                    else:
+                        self._mgpu_post(f, sums)
+        else:
+            for _ in range(self.num_learning_epochs):
+                for i in range(self.num_mini_batches):
+                    f.minibatch(self.storage, self.mb_indices, i * mb)
                     f.optimizer_step(sums)
         self.storage.clear()
+
+    def _grad_params(self) -> list:
+        """The optimizer's parameters in bucket order (every one has a .grad on the fused path)."""
+        return [p for g in self.optimizer.param_groups for p in g["params"]]
+
+    def _mgpu_pre(self, f, offset: int) -> None:
+        """One rank's minibatch: gradients into .grad, then [every .grad, the minibatch KL] into the
+        flat all-reduce bucket."""
+        stats = f.minibatch(self.storage, self.mb_indices, offset)
+        torch.cat([p.grad.reshape(-1) for p in self._grad_params()] + [stats[0:1]], out=self._flat)
+
+    def _mgpu_post(self, f, sums: torch.Tensor) -> None:
+        """The ranks' average back into .grad and the KL slot, then the fused optimizer step."""
+        self._flat.div_(self.gpu_world_size)
+        ps = self._grad_params()
+        off = 0
+        views = []
+        for p in ps:
+            views.append(self._flat[off:off + p.numel()].view_as(p))
+            off += p.numel()
+        torch._foreach_copy_([p.grad for p in ps], views)
+        f.stats[0:1].copy_(self._flat[off:off + 1])
+        f.optimizer_step(sums)
+
+    def capture_update_segments(self) -> bool:
+        """world > 1, fused path, after one eager update (the driver, its Adam state and the bucket
+        exist): capture the minibatch segments on either side of the all-reduce as HIP graphs -- one
+        per minibatch slot before it (its row offset; reused by every epoch) and one after it. The
+        all-reduce stays outside the graphs (a collective is never captured). Returns
+        whether the segments are in use."""
+        f = self._fused
+        if not self.is_multi_gpu or f is None or self._flat is None or not hasattr(f, "_params"):
+            return False
+        mb = f.batch
+        pre = []
+        for i in range(self.num_mini_batches):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._mgpu_pre(f, i * mb)
+            pre.append(g)
+        post = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(post):
+            self._mgpu_post(f, self.update_sums)
+        self._seg_pre, self._seg_post = pre, post
+        return True
 
     def restore_learning_rate(self) -> None:
         """After ``optimizer.load_state_dict``: the checkpoint's rate becomes ``lr_t`` (the adaptive

@@ -85,6 +85,7 @@ class OnPolicyRunner:
         self.cur_len = torch.zeros(self.env.num_envs, device=self.device)
         self.ep_stats = torch.zeros(3, device=self.device)  # reward sum, length sum, count
         self._log_keys, self._log_acc = None, None
+        self._native_acc, self._native_idx = None, None  # the step's finalize launch sums the log (zb_set_log_accumulator)
         from .. import GRAPHS_SAFE
         self.use_graph = (torch.device(device).type == "cuda" and GRAPHS_SAFE) if use_graph is None else use_graph
         self._graph = None
@@ -94,11 +95,10 @@ class OnPolicyRunner:
         # PPO.update_steps releases its autograd graph so the capture sees fresh AccumulateGrad
         # nodes on the capture stream (a live one from the eager update pinned the default stream
         # and broke the capture)
-        # Multi-GPU: the update's gradient all-reduce (RCCL) would be captured into the graph; no
-        # multi-GPU run has shown a captured all-reduce to match the eager update yet, so the update
-        # stays eager there unless a caller asks for the graph explicitly (the rollout graph has no
-        # collective and is unaffected)
-        self.graph_update = (self.use_graph and not self.is_distributed) if graph_update is None else graph_update
+        # Multi-GPU: a collective is never captured. On the fused path each minibatch's kernels before
+        # and after its gradient all-reduce are two graphs and the all-reduce runs between them
+        # (PPO.capture_update_segments); without the fused driver the update stays eager there
+        self.graph_update = self.use_graph if graph_update is None else graph_update
 
     def _configure_multi_gpu(self) -> None:
         world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -149,8 +149,10 @@ class OnPolicyRunner:
                 self.alg.storage.clear()  # host-side step counter (the replay runs no Python)
             else:
                 self.alg.update_steps()
-                if self.graph_update:
+                if self.graph_update and not self.is_distributed:
                     self._capture_update()
+                elif self.graph_update and self.alg._seg_pre is None and not self.alg.capture_update_segments():
+                    self.graph_update = False  # (no fused driver: eager multi-GPU update)
             losses = self.alg.update_stats()
             learn_time = time.perf_counter() - t1
             stats = self.ep_stats.tolist()
@@ -167,7 +169,8 @@ class OnPolicyRunner:
                    "learning_rate": self.alg.learning_rate, "mean_noise_std": self.alg.policy.std.mean().item(),
                    **{f"loss/{k}": v for k, v in losses.items()}}
             if self._log_keys:  # rsl_rl: mean over the rollout's per-step extras["log"] values
-                for k, v in zip(self._log_keys, (self._log_acc / self.num_steps_per_env).tolist()):
+                acc = self._log_acc if self._native_acc is None else self._native_acc.index_select(0, self._native_idx)
+                for k, v in zip(self._log_keys, (acc / self.num_steps_per_env).tolist()):
                     rec[k] = v
             self.log.append(rec)
             if callback is not None:
@@ -185,6 +188,8 @@ class OnPolicyRunner:
         self.ep_stats.zero_()
         if self._log_acc is not None:
             self._log_acc.zero_()
+        if self._native_acc is not None:
+            self._native_acc.zero_()
         # on a GPU the policy step and the post-step bookkeeping are one launch each (libzbot_ppo:
         # zbp_act, zbp_env_post) instead of ~40 torch kernels; same statements as the loop below
         fr = self.alg.fused_rollout()
@@ -228,6 +233,12 @@ class OnPolicyRunner:
             self._log_keys = list(log.keys())
             self._log_acc = torch.zeros(len(self._log_keys), device=self.device)
             self._log_groups = self._log_views(log)
+            if self._native_log_setup():
+                return
+        if self._native_acc is not None:
+            if all(log[k] is self._log_src[i] for i, k in enumerate(self._log_keys)):
+                return  # summed by the env's own finalize launch
+            raise RuntimeError("extras['log'] changed its buffers after the native log accumulator was registered")
         if self._log_groups is not None and all(log[k] is self._log_src[i] for i, k in enumerate(self._log_keys)):
             # the env's log values are fixed 0-d views into a few device buffers: one gather + one
             # index_add per buffer instead of a copy per key
@@ -236,6 +247,32 @@ class OnPolicyRunner:
             return
         vals = [log[k] if torch.is_tensor(log[k]) else torch.tensor(float(log[k])) for k in self._log_keys]
         self._log_acc += torch.stack([v.to(self.device, torch.float32).reshape(()) for v in vals])
+
+    def _native_log_setup(self) -> bool:
+        """When every log value is a view of the simulator's own log buffers (zb_set_log_buffers), register
+        an accumulator that the step's finalize launch adds them to (zb_set_log_accumulator): no torch
+        launch per step for the log. This step, which ran before the registration, is
+        added here once."""
+        sim = getattr(getattr(self.env, "unwrapped", self.env), "sim", None)
+        if (self._log_groups is None or sim is None or not hasattr(sim, "set_log_accumulator")
+                or getattr(sim, "device", None) != self._log_acc.device):
+            return False
+        from .. import model as zm
+        means, counts = sim.log_buffer, sim.log_count_buffer
+        idx = []
+        for v in self._log_src:
+            if v._base is means:
+                idx.append(v.storage_offset() - means.storage_offset())
+            elif v._base is counts:
+                idx.append(zm.LOG_LEN + v.storage_offset() - counts.storage_offset())
+            else:
+                return False
+        self._native_idx = torch.tensor(idx, device=self._log_acc.device)
+        self._native_acc = torch.zeros(zm.LOG_LEN + zm.LOG_COUNTS, device=self._log_acc.device)
+        now = torch.cat([means.to(torch.float32), counts.to(torch.float32)])
+        self._native_acc.copy_(now)  # this step's values (the accumulator starts from zero each rollout)
+        sim.set_log_accumulator(self._native_acc)
+        return True
 
     def _log_views(self, log):
         """[(flat base buffer, source indices, accumulator indices)] when every log value is a 0-d

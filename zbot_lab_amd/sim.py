@@ -109,6 +109,21 @@ class ZbotSim:
         """The whole float[ZB_LOG_LEN] log buffer (term means, then the curriculum entries)."""
         return self._log_means
 
+    @property
+    def log_count_buffer(self) -> torch.Tensor:
+        """The int32[ZB_LOG_COUNTS] termination-count buffer."""
+        return self._log_counts
+
+    def set_log_accumulator(self, acc: torch.Tensor | None) -> None:
+        """Register a device float[ZB_LOG_LEN + ZB_LOG_COUNTS] accumulator that every later step adds the
+        log's current values to inside its finalize launch (zb_set_log_accumulator; the PPO runner's
+        per-rollout sum of extras["log"]); None unregisters. The tensor must stay alive while registered."""
+        if acc is not None and (acc.dtype != torch.float32 or acc.device != self.device or not acc.is_contiguous()
+                                or acc.numel() != zm.LOG_LEN + zm.LOG_COUNTS):
+            raise ValueError(f"accumulator must be a contiguous float32 [{zm.LOG_LEN + zm.LOG_COUNTS}] tensor on {self.device}")
+        self._log_acc_ref = acc
+        nat.check(self.lib.zb_set_log_accumulator(self._h, nat.ptr(acc)), "zb_set_log_accumulator")
+
     def set_link_friction(self, mu: torch.Tensor, mu_dynamic: torch.Tensor | None = None) -> None:
         """Standup / manager: per-link static (and dynamic; default = static) friction [N, 12]
         (randomize_rigid_body_material)."""
