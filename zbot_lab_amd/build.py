@@ -25,7 +25,7 @@ STAMPS_OUT = os.path.join(HERE, "libzbot_stamps.so")
 
 def build(force: bool = False, verbose: bool = False, stamps: bool = False, defines: tuple = (),
           out: str | None = None, flags: tuple = ()) -> str:
-    """defines / out: an experiment variant (e.g. ``-DZB_STAGED_STORES=0`` into ``libzbot_x.so``),
+    """defines / out: an experiment variant (e.g. ``-DZB_GJK_TOL=3e-5f`` into ``libzbot_x.so``),
     selected at run time with ZBOT_LIB=<file name>."""
     out = os.path.join(HERE, out) if out else (STAMPS_OUT if stamps else OUT)
     deps = [SRC, os.path.join(ROOT, "include", "zbot.h"), os.path.abspath(__file__)]

@@ -424,9 +424,6 @@ __device__ __forceinline__ MP opaque(MP m) {
 // (quad_perm, row_half_mirror, row_mirror), which leave all 16 lanes bit-identical sums, so the
 // redundant scalar work stays identical across the team.
 constexpr int TL = 16;           // lanes per env
-#ifndef ZB_EPW
-#define ZB_EPW 4
-#endif
 #ifndef ZB_WAVES_PER_SIMD
 #define ZB_WAVES_PER_SIMD 2
 #endif
@@ -436,7 +433,7 @@ constexpr int TL = 16;           // lanes per env
 #ifndef ZB_M_WAVES_PER_SIMD
 #define ZB_M_WAVES_PER_SIMD 2
 #endif
-constexpr int EPW = ZB_EPW;      // envs per workgroup (one wave; EPW < 4 leaves lanes idle)
+constexpr int EPW = 4;           // envs per workgroup (one wave)
 constexpr int WGT = TL * EPW;    // threads per workgroup
 static_assert(WGT <= WAVE, "one wave per workgroup");
 // lane c of a team builds / zeroes / maps / forces contact slot c: one slot per lane
@@ -1159,17 +1156,23 @@ __device__ __forceinline__ bool gjk_quad(const QCircle& h, int j, const float v0
     // triangle {a, S_I, S_J} (j = 1: I, J = 0, 1; j = 2: 0, 2; j = 3: 1, 2); lane 0 starts from {a}
     float best = j == 0 ? dot3(aw, aw) : 3.0e38f, bv[3] = {aw[0], aw[1], aw[2]}, l1 = 0.f, l2 = 0.f;
     unsigned bm = 0u;  // simplex points used (bit i: S_i)
-    {
-      float e[3];
+    // edge vectors from a: e2 = S_y - a with y = j (lane 3: y = 2) is both the segment's edge and the
+    // triangle's second edge (lanes 1, 2 share every term of the segment with their triangle), e1 =
+    // S_x - a with x = 0 (lane 3: x = 1)
+    float e1[3], e2[3];
 #pragma unroll
-      for (int k = 0; k < 3; ++k) e[k] = (j == 0 ? S[0][k] : (j == 1 ? S[1][k] : S[2][k])) - aw[k];
-      const float ee = dot3(e, e);
-      const float t = -dot3(aw, e) / fmaxf(ee, 1e-30f);
+    for (int k = 0; k < 3; ++k) {
+      e1[k] = (j == 3 ? S[1][k] : S[0][k]) - aw[k];
+      e2[k] = (j == 0 ? S[0][k] : (j == 1 ? S[1][k] : S[2][k])) - aw[k];
+    }
+    const float g11 = dot3(e2, e2), r1 = -dot3(aw, e2);
+    {
+      const float t = r1 / fmaxf(g11, 1e-30f);
       float p[3];
 #pragma unroll
-      for (int k = 0; k < 3; ++k) p[k] = aw[k] + t * e[k];
+      for (int k = 0; k < 3; ++k) p[k] = aw[k] + t * e2[k];
       const float d2 = dot3(p, p);
-      const bool ok = j < n && ee > 1e-20f && t > 0.f && t < 1.f && d2 < best;
+      const bool ok = j < n && g11 > 1e-20f && t > 0.f && t < 1.f && d2 < best;
       best = ok ? d2 : best;
       bm = ok ? (1u << j) : bm;
       l1 = ok ? t : l1;
@@ -1177,14 +1180,8 @@ __device__ __forceinline__ bool gjk_quad(const QCircle& h, int j, const float v0
       for (int k = 0; k < 3; ++k) bv[k] = ok ? p[k] : bv[k];
     }
     {
-      float e1[3], e2[3];
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        e1[k] = (j == 3 ? S[1][k] : S[0][k]) - aw[k];
-        e2[k] = (j == 1 ? S[1][k] : S[2][k]) - aw[k];
-      }
-      const float g00 = dot3(e1, e1), g01 = dot3(e1, e2), g11 = dot3(e2, e2);
-      const float r0 = -dot3(aw, e1), r1 = -dot3(aw, e2);
+      const float g00 = dot3(e1, e1), g01 = dot3(e1, e2);
+      const float r0 = -dot3(aw, e1);
       const float det = g00 * g11 - g01 * g01;
       const float id = 1.f / (fabsf(det) > 1e-30f ? det : 1e-30f);
       const float ts = (r0 * g11 - r1 * g01) * id, tt = (g00 * r1 - g01 * r0) * id;
@@ -1203,7 +1200,11 @@ __device__ __forceinline__ bool gjk_quad(const QCircle& h, int j, const float v0
     }
     quad_pick<DPP_XOR1>((j & 1) != 0, best, bv, l1, l2, bm);
     quad_pick<DPP_XOR2>((j & 2) != 0, best, bv, l1, l2, bm);
-    if (n == 3) {  // origin inside the tetrahedron (a, S0, S1, S2)?
+    // origin inside the tetrahedron (a, S0, S1, S2)? Only possible when the support gap along dir is
+    // not positive: a is the minimiser of dir.x over the Minkowski difference, so lo > 0 puts the
+    // origin outside it (the test's 1e-5 barycentric margins cannot pass there either); the gate skips
+    // the ~60-instruction test in all but overlapping pairs' iterations (quad-uniform: lo is)
+    if (n == 3 && lo <= 0.f) {
       float e0[3], e1[3], e2[3], x12[3];
 #pragma unroll
       for (int k = 0; k < 3; ++k) { e0[k] = S[0][k] - aw[k]; e1[k] = S[1][k] - aw[k]; e2[k] = S[2][k] - aw[k]; }
@@ -1927,12 +1928,6 @@ __device__ __forceinline__ void sens_store(const Q& q, float* __restrict__ st, i
 // the whole wave stores them: one store instruction covers 16 state rows x the EPW consecutive
 // envs of the workgroup, the EPW observation rows go out as one contiguous run. This replaces ~110
 // single-lane-per-env store instructions per wave with ~9 full-wave ones.
-#ifndef ZB_STAGED_STORES
-#define ZB_STAGED_STORES 1
-#endif
-#ifndef ZB_CARRY
-#define ZB_CARRY 1
-#endif
 __device__ __forceinline__ float& Q::stg(int k) const { return reinterpret_cast<float*>(b + YG_OFF)[e * STG_LEN + k]; }
 template <int SD, int OD>
 __device__ __forceinline__ void staged_store(const Q& q, int env0, int N, float* __restrict__ st,
@@ -3096,13 +3091,8 @@ __device__ __forceinline__ void step_body(const zb_model* __restrict__ mg, const
   for (int a = 0; a < 4; ++a) p.quat[a] = ST(ZB_S_ROOT_QUAT + a);
 #pragma unroll
   for (int j = 0; j < ND; ++j) { p.jq[j] = ST(ZB_S_JOINT_POS + j); p.jqd[j] = ST(ZB_S_JOINT_VEL + j); }
-#if ZB_CARRY
   const float* cst = carry_prefetch<ZB_STATE_DIM>(q, st, N, i);
 #define CST(f) cst[f]
-#else
-  const float* cst = st;
-#define CST(f) ST(f)
-#endif
 
   // _pre_physics_step (v2.py:276-287); _actions / p_delta are stored with the rest at the end
   // (one writer lane per env; the team holds identical values)
@@ -3198,7 +3188,7 @@ __device__ __forceinline__ void step_body(const zb_model* __restrict__ mg, const
 
   // ContactSensor (history 5, updated every physics step): histories and timers after the substeps
   float fz_sum[2], fm_max;
-  sens_replay<ZB_HIST>(q, ZB_CARRY ? cst : st, ZB_CARRY ? 1 : N, ZB_CARRY ? 0 : i, ZB_S_FEET_FZ_HIST, ZB_S_UNDES_FMAX_HIST, cfg.decimation, cfg.sim_dt,
+  sens_replay<ZB_HIST>(q, cst, 1, 0, ZB_S_FEET_FZ_HIST, ZB_S_UNDES_FMAX_HIST, cfg.decimation, cfg.sim_dt,
                        cfg.contact_force_threshold, fz_sum, fm_max, air_cur, air_last, contact_t, con_last_unused);
 
   // post-step feet COM velocities (feet_slide); post-step feet positions (the reset latch)
@@ -3330,11 +3320,7 @@ __device__ __forceinline__ void step_body(const zb_model* __restrict__ mg, const
     wc[wi] = reset ? wc_invalid(q.s) : wc_row;
   }
   sp.mark(12);
-#if ZB_STAGED_STORES
 #define OUT(f) q.stg(f)
-#else
-#define OUT(f) ST(f)
-#endif
   if (writer) {
     auto live = [reset](float v) { return reset ? 0.f : v; };  // fields zeroed by _reset_idx
 #pragma unroll
@@ -3356,7 +3342,7 @@ __device__ __forceinline__ void step_body(const zb_model* __restrict__ mg, const
       OUT(ZB_S_FEET_CONTACT_CUR + f) = live(contact_t[f]);
 
     }
-    sens_store<ZB_HIST>(q, ZB_CARRY ? cst : st, ZB_CARRY ? 1 : N, ZB_CARRY ? 0 : i, ZB_S_FEET_FZ_HIST, ZB_S_UNDES_FMAX_HIST, cfg.decimation, reset,
+    sens_store<ZB_HIST>(q, cst, 1, 0, ZB_S_FEET_FZ_HIST, ZB_S_UNDES_FMAX_HIST, cfg.decimation, reset,
                         [&](int row, float v) { OUT(row) = v; });
     OUT(ZB_S_HEADING_SUM) = live(hs);
     OUT(ZB_S_Y_ERR_SUM) = live(ys);
@@ -3366,11 +3352,7 @@ __device__ __forceinline__ void step_body(const zb_model* __restrict__ mg, const
     for (int t = 0; t < ZB_NUM_REWARD_TERMS; ++t) OUT(ZB_S_EP_SUMS + t) = live(sums[t]);
 
     // _get_observations (v2.py:351-365) of the post-step / post-reset state
-#if ZB_STAGED_STORES
     float* o = &q.stg(ZB_STATE_DIM);
-#else
-    float* o = obs + (size_t)i * ZB_OBS_DIM;
-#endif
     o[0] = obs_q[0]; o[1] = obs_q[1]; o[2] = obs_q[2]; o[3] = obs_q[3];
 #pragma unroll
     for (int j = 0; j < ND; ++j) {
@@ -3379,19 +3361,11 @@ __device__ __forceinline__ void step_body(const zb_model* __restrict__ mg, const
       o[16 + j] = live(a_now[j]);
     }
     o[22] = cfg.joint_speed_limit;
-#if ZB_STAGED_STORES
     o[ZB_OBS_DIM] = reward;
     o[ZB_OBS_DIM + 1] = died ? 1.f : 0.f;
     o[ZB_OBS_DIM + 2] = time_out ? 1.f : 0.f;
-#else
-    rew[i] = reward;
-    term[i] = died ? 1 : 0;
-    trunc[i] = time_out ? 1 : 0;
-#endif
   }
-#if ZB_STAGED_STORES
   staged_store<ZB_STATE_DIM, ZB_OBS_DIM>(q, xcd_block(blockIdx.x, gridDim.x) * EPW, N, st, obs, rew, term, trunc);
-#endif
 #undef OUT
   sp.mark(8);
   sp.flush();
@@ -3830,11 +3804,7 @@ __global__ __launch_bounds__(WGT, kOcc) void zb_su_step_kernel(
     wc[wi] = reset ? wc_invalid(q.s) : wc_row;
   }
   sp.mark(12);
-#if ZB_STAGED_STORES
 #define OUT(f) q.stg(f)
-#else
-#define OUT(f) ST(f)
-#endif
   if (writer) {
     auto live = [reset](float v) { return reset ? 0.f : v; };
 #pragma unroll
@@ -3851,11 +3821,7 @@ __global__ __launch_bounds__(WGT, kOcc) void zb_su_step_kernel(
     for (int t = 0; t < ZB_SU_NUM_REWARD_TERMS; ++t) OUT(ZB_SU_EP_SUMS + t) = live(sums[t]);
 
     // _get_observations (593-618): base quat, joint_pos - default, joint_vel, actions
-#if ZB_STAGED_STORES
     float* o = &q.stg(ZB_SU_LINK_MU);
-#else
-    float* o = obs + (size_t)i * ZB_SU_OBS_DIM;
-#endif
     o[0] = obs_q[0]; o[1] = obs_q[1]; o[2] = obs_q[2]; o[3] = obs_q[3];
 #pragma unroll
     for (int j = 0; j < ND; ++j) {
@@ -3863,19 +3829,11 @@ __global__ __launch_bounds__(WGT, kOcc) void zb_su_step_kernel(
       o[10 + j] = p.jqd[j];
       o[16 + j] = live(pr.a_now[j]);
     }
-#if ZB_STAGED_STORES
     q.stg(ZB_SU_LINK_MU + ZB_SU_OBS_DIM) = reward;
     q.stg(ZB_SU_LINK_MU + ZB_SU_OBS_DIM + 1) = died ? 1.f : 0.f;
     q.stg(ZB_SU_LINK_MU + ZB_SU_OBS_DIM + 2) = time_out ? 1.f : 0.f;
-#else
-    rew[i] = reward;
-    term[i] = died ? 1 : 0;
-    trunc[i] = time_out ? 1 : 0;
-#endif
   }
-#if ZB_STAGED_STORES
   staged_store<ZB_SU_LINK_MU, ZB_SU_OBS_DIM>(q, xcd_block(blockIdx.x, gridDim.x) * EPW, N, st, obs, rew, term, trunc);
-#endif
 #undef OUT
   sp.mark(8);
   sp.flush();
@@ -4003,13 +3961,8 @@ __global__ __launch_bounds__(WGT, kOcc) void zb_v4_step_kernel(
   for (int a = 0; a < 4; ++a) p.quat[a] = ST(ZB_S_ROOT_QUAT + a);
 #pragma unroll
   for (int j = 0; j < ND; ++j) { p.jq[j] = ST(ZB_S_JOINT_POS + j); p.jqd[j] = ST(ZB_S_JOINT_VEL + j); }
-#if ZB_CARRY
   const float* cst = carry_prefetch<ZB_V4_STATE_DIM>(q, st, N, i);
 #define CST(f) cst[f]
-#else
-  const float* cst = st;
-#define CST(f) ST(f)
-#endif
 
   // _pre_physics_step (v4.py:776-804, mode 1)
   const bool writer = q.s == 0;
@@ -4065,7 +4018,7 @@ __global__ __launch_bounds__(WGT, kOcc) void zb_v4_step_kernel(
     air_last[f] = CST(ZB_V4_FEET_AIR_LAST + f);
     con_last[f] = CST(ZB_V4_FEET_CONTACT_LAST + f);
   }
-  sens_replay<ZB_V4_HIST>(q, ZB_CARRY ? cst : st, ZB_CARRY ? 1 : N, ZB_CARRY ? 0 : i, ZB_V4_FEET_FZ_HIST, ZB_V4_UNDES_FMAX_HIST, cfg.decimation, cfg.sim_dt,
+  sens_replay<ZB_V4_HIST>(q, cst, 1, 0, ZB_V4_FEET_FZ_HIST, ZB_V4_UNDES_FMAX_HIST, cfg.decimation, cfg.sim_dt,
                           cfg.contact_force_threshold, fz_sum, fm_max, air_cur, air_last, con_cur, con_last);
 #pragma unroll
   for (int f = 0; f < 2; ++f) {
@@ -4266,11 +4219,7 @@ __global__ __launch_bounds__(WGT, kOcc) void zb_v4_step_kernel(
     wc[wi] = reset ? wc_invalid(q.s) : wc_row;
   }
   sp.mark(12);
-#if ZB_STAGED_STORES
 #define OUT(f) q.stg(f)
-#else
-#define OUT(f) ST(f)
-#endif
   if (writer) {
     auto live = [reset](float v) { return reset ? 0.f : v; };
 #pragma unroll
@@ -4299,18 +4248,14 @@ __global__ __launch_bounds__(WGT, kOcc) void zb_v4_step_kernel(
       OUT(ZB_V4_FEET_CONTACT_LAST + f) = live(con_last[f]);
 
     }
-    sens_store<ZB_V4_HIST>(q, ZB_CARRY ? cst : st, ZB_CARRY ? 1 : N, ZB_CARRY ? 0 : i, ZB_V4_FEET_FZ_HIST, ZB_V4_UNDES_FMAX_HIST, cfg.decimation, reset,
+    sens_store<ZB_V4_HIST>(q, cst, 1, 0, ZB_V4_FEET_FZ_HIST, ZB_V4_UNDES_FMAX_HIST, cfg.decimation, reset,
                            [&](int row, float v) { OUT(row) = v; });
     OUT(ZB_V4_EP_LEN) = live(ep_len);
 #pragma unroll
     for (int t = 0; t < ZB_V4_NUM_REWARD_TERMS; ++t) OUT(ZB_V4_EP_SUMS + t) = live(sums[t]);
 
     // _get_observations (v4.py:851-881)
-#if ZB_STAGED_STORES
     float* o = &q.stg(ZB_V4_STATE_DIM);
-#else
-    float* o = obs + (size_t)i * ZB_V4_OBS_DIM;
-#endif
     o[0] = obs_q[0]; o[1] = obs_q[1]; o[2] = obs_q[2]; o[3] = obs_q[3];
 #pragma unroll
     for (int j = 0; j < ND; ++j) {
@@ -4320,19 +4265,11 @@ __global__ __launch_bounds__(WGT, kOcc) void zb_v4_step_kernel(
     }
     o[22] = cmd[0];
     o[23] = he_obs;
-#if ZB_STAGED_STORES
     q.stg(ZB_V4_STATE_DIM + ZB_V4_OBS_DIM) = reward;
     q.stg(ZB_V4_STATE_DIM + ZB_V4_OBS_DIM + 1) = died ? 1.f : 0.f;
     q.stg(ZB_V4_STATE_DIM + ZB_V4_OBS_DIM + 2) = time_out ? 1.f : 0.f;
-#else
-    rew[i] = reward;
-    term[i] = died ? 1 : 0;
-    trunc[i] = time_out ? 1 : 0;
-#endif
   }
-#if ZB_STAGED_STORES
   staged_store<ZB_V4_STATE_DIM, ZB_V4_OBS_DIM>(q, xcd_block(blockIdx.x, gridDim.x) * EPW, N, st, obs, rew, term, trunc);
-#endif
 #undef OUT
   sp.mark(8);
   sp.flush();
@@ -4517,12 +4454,8 @@ __global__ __launch_bounds__(WGT, kOcc) void zb_m_step_kernel(
   for (int a = 0; a < 4; ++a) p.quat[a] = ST(ZB_S_ROOT_QUAT + a);
 #pragma unroll
   for (int j = 0; j < ND; ++j) { p.jq[j] = ST(ZB_S_JOINT_POS + j); p.jqd[j] = ST(ZB_S_JOINT_VEL + j); }
-#if ZB_CARRY
   const float* cst = carry_prefetch<ZB_M_LINK_MU>(q, st, N, i);  // the friction rows load into FRIC
 #define CST(f) cst[f]
-#else
-#define CST(f) ST(f)
-#endif
   if (q.s < NL) {
     q.fric(q.s) = ST(ZB_M_LINK_MU + q.s);
     q.fricd(q.s) = ST(ZB_M_LINK_MU_D + q.s);
@@ -4793,11 +4726,7 @@ __global__ __launch_bounds__(WGT, kOcc) void zb_m_step_kernel(
     wc[wi] = reset ? wc_invalid(q.s) : wc_row;
   }
   sp.mark(12);
-#if ZB_STAGED_STORES
 #define OUT(f) q.stg(f)
-#else
-#define OUT(f) ST(f)
-#endif
   if (writer) {
     auto live = [reset](float v) { return reset ? 0.f : v; };
 #pragma unroll
@@ -4828,24 +4757,12 @@ __global__ __launch_bounds__(WGT, kOcc) void zb_m_step_kernel(
     OUT(ZB_M_EP_LEN) = live(ep_len);
 #pragma unroll
     for (int t = 0; t < ZB_M_NUM_REWARD_TERMS; ++t) OUT(ZB_M_EP_SUMS + t) = live(sums[t]);
-#if ZB_STAGED_STORES
     m_write_obs(m, cfg, hs, bq, cmd, p, a_obs, &q.stg(ZB_M_LINK_MU));
-#else
-    m_write_obs(m, cfg, hs, bq, cmd, p, a_obs, obs + (size_t)i * ZB_M_OBS_DIM);
-#endif
-#if ZB_STAGED_STORES
     q.stg(ZB_M_LINK_MU + ZB_M_OBS_DIM) = reward;
     q.stg(ZB_M_LINK_MU + ZB_M_OBS_DIM + 1) = terminated ? 1.f : 0.f;
     q.stg(ZB_M_LINK_MU + ZB_M_OBS_DIM + 2) = time_out ? 1.f : 0.f;
-#else
-    rew[i] = reward;
-    term[i] = terminated ? 1 : 0;
-    trunc[i] = time_out ? 1 : 0;
-#endif
   }
-#if ZB_STAGED_STORES
   staged_store<ZB_M_LINK_MU, ZB_M_OBS_DIM>(q, xcd_block(blockIdx.x, gridDim.x) * EPW, N, st, obs, rew, term, trunc);
-#endif
 #undef OUT
   sp.mark(8);
   sp.flush();
