@@ -13,6 +13,7 @@
 #   benchab          bench lines once per library in $LIBS, interleaved $ROUNDS times
 #   recipe           the staged v2 recipe test (tests/test_gpu_recipe.py)
 #   tests            pytest -m gpu on $TESTS
+#   nofin            bench lines with and without the finalize launch (ZB_DIAG_NO_FINALIZE, diagnostic)
 #   train_v2 / train_c5   rocprof kernel traces of short training runs
 #   rehearsal        two ranks of bench.py sharing cuda:0 over gloo (plumbing, not scaling)
 set -u
@@ -68,6 +69,11 @@ for s in "$@"; do
       for r in $(seq ${ROUNDS:-2}); do for lib in ${LIBS:-libzbot.so}; do for n in 4096 8192; do
         run benchab_${lib%.so}_${n}_$r 300 env ZBOT_LIB=$lib python bench.py --envs-per-gpu $n --no-cpu-baseline
       done; done; done ;;
+    nofin)  # diagnostic: the step without its finalize launch (wrong episode log; the launch's share)
+      for r in 1 2; do for n in 4096 8192; do
+        run nofin_${n}_$r 300 python bench.py --envs-per-gpu $n --no-cpu-baseline
+        run nofin_diag_${n}_$r 300 env ZB_DIAG_NO_FINALIZE=1 python bench.py --envs-per-gpu $n --no-cpu-baseline
+      done; done ;;
     recipe)
       run recipe 900 $PT tests/test_gpu_recipe.py -m gpu ;;
     tests)

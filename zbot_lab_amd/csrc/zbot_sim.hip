@@ -5065,6 +5065,10 @@ struct zb_sim {
   float* u_log_means = nullptr;     // optional caller buffers (zb_set_log_buffers)
   int32_t* u_log_counts = nullptr;
   float* u_log_acc = nullptr;       // optional caller accumulator (zb_set_log_accumulator)
+  // ZB_DIAG_NO_FINALIZE=1 (diagnostic only, wrong results: no episode log, no full-reset draw, no
+  // step counter): zb_step skips the finalize launch, to measure what that launch and its kernel
+  // boundary cost per step
+  bool diag_no_finalize = false;
   // optional per-launch timing of zb_step_kernel (hipEvents on the launch stream)
   int prof_max = 0, prof_n = 0;
   hipEvent_t* prof_ev = nullptr;
@@ -5165,6 +5169,8 @@ int zb_create(const zb_model* m, const zb_task_cfg* c, int num_envs, int hip_dev
     const char* oc = getenv("ZB_OCC1");
     const int oc_on = oc && oc[0] == '1' && oc[1] == 0, oc_off = oc && oc[0] == '0' && oc[1] == 0;
     h->occ1 = oc_on || (!oc_off && ZB_OCC1_DEFAULT && num_envs <= 4096);
+    const char* nf = getenv("ZB_DIAG_NO_FINALIZE");
+    h->diag_no_finalize = nf && nf[0] == '1' && nf[1] == 0;
   }
   {
     Counters c0;
@@ -5466,13 +5472,19 @@ int zb_step(zb_handle h, const float* actions, float* obs, float* reward, uint8_
   (tgs ? (one ? zb_launch(K<true, 1>, blocks, s, e0, e1, __VA_ARGS__) : zb_launch(K<true, 2>, blocks, s, e0, e1, __VA_ARGS__)) \
        : (one ? zb_launch(K<false, 1>, blocks, s, e0, e1, __VA_ARGS__) : zb_launch(K<false, 2>, blocks, s, e0, e1, __VA_ARGS__)))
   // solver_modes 2, 3 (the TGS refresh) and self_manifold 3 (the ruling-on-face manifold): walking v2
-  // and stand-up only (zb_create), two-wave occupancy
+  // and stand-up only (zb_create); one wave per SIMD at <= 4096 envs as the default kernels (round 6:
+  // the refresh's FK and row rebuild inside the sweeps spill at two-wave occupancy)
   const bool rf = h->cfg.self_manifold == 3;
 #define ZB_LAUNCH_R(K, ...)                                                                        \
-  (rf ? (refresh ? zb_launch(K<true, 2, true, true>, blocks, s, e0, e1, __VA_ARGS__)                 \
-                 : (tgs ? zb_launch(K<true, 2, false, true>, blocks, s, e0, e1, __VA_ARGS__)          \
-                        : zb_launch(K<false, 2, false, true>, blocks, s, e0, e1, __VA_ARGS__)))       \
-      : refresh ? zb_launch(K<true, 2, true>, blocks, s, e0, e1, __VA_ARGS__) : ZB_LAUNCH(K, __VA_ARGS__))
+  (rf ? (refresh ? (one ? zb_launch(K<true, 1, true, true>, blocks, s, e0, e1, __VA_ARGS__)          \
+                        : zb_launch(K<true, 2, true, true>, blocks, s, e0, e1, __VA_ARGS__))         \
+                 : (tgs ? (one ? zb_launch(K<true, 1, false, true>, blocks, s, e0, e1, __VA_ARGS__)  \
+                               : zb_launch(K<true, 2, false, true>, blocks, s, e0, e1, __VA_ARGS__)) \
+                        : (one ? zb_launch(K<false, 1, false, true>, blocks, s, e0, e1, __VA_ARGS__) \
+                               : zb_launch(K<false, 2, false, true>, blocks, s, e0, e1, __VA_ARGS__)))) \
+      : refresh ? (one ? zb_launch(K<true, 1, true>, blocks, s, e0, e1, __VA_ARGS__)                 \
+                       : zb_launch(K<true, 2, true>, blocks, s, e0, e1, __VA_ARGS__))                \
+                : ZB_LAUNCH(K, __VA_ARGS__))
   if (h->task == ZB_TASK_STANDUP_V0)
     ZB_LAUNCH_R(zb_su_step_kernel, h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward, terminated,
               truncated, h->d_acc, h->d_cnt, h->seed, h->d_wc);
@@ -5490,6 +5502,7 @@ int zb_step(zb_handle h, const float* actions, float* obs, float* reward, uint8_
   int rc = launch_check("zb_step_kernel");
   if (prof) ++h->prof_n;
   if (rc) return rc;
+  if (h->diag_no_finalize) return 0;  // (diagnostic, DESIGN.md §7: the finalize launch's share of a step)
   return finalize(h, s, 0, 0, 1, obs, terminated, truncated);
 }
 
