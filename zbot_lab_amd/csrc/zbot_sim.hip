@@ -1702,7 +1702,11 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q&
         SelfContact sc = hit0;
         QCircle hc;
         quad_circle(q, (qj & 2) ? (pcode & 15) : (pcode >> 4), qj & 1, hc);
+#ifdef ZB_DIAG_NO_RERUN  // diagnostic build (wrong contacts): what the write pass's GJK re-runs cost
+        if (pass == 0) {
+#else
         if (pass == 0 || k != hit0_k) {
+#endif
           // start: the pair's contact normal of the previous substep of this step (kept contacts
           // hold {n, code} in FRC; unused slots code -1), else the hull centre difference
           float v0[3];
