@@ -13,6 +13,7 @@
 #   benchab          bench lines once per library in $LIBS, interleaved $ROUNDS times
 #   recipe           the staged v2 recipe test (tests/test_gpu_recipe.py)
 #   tests            pytest -m gpu on $TESTS
+#   budget           tools/error_budget.py (device vs f32 oracle error against f64, per part of a substep)
 #   nofin            bench lines with and without the finalize launch (ZB_DIAG_NO_FINALIZE, diagnostic)
 #   train_v2 / train_c5   rocprof kernel traces of short training runs
 #   rehearsal        two ranks of bench.py sharing cuda:0 over gloo (plumbing, not scaling)
@@ -78,6 +79,8 @@ for s in "$@"; do
       run recipe 900 $PT tests/test_gpu_recipe.py -m gpu ;;
     tests)
       run tests 900 $PT ${TESTS:?TESTS=<pytest paths>} -m gpu ;;
+    budget)
+      run error_budget 300 python tools/error_budget.py 2048 ;;
     train_v2)
       run train_v2 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/train_v2 -o run -- \
         python3 scripts/train.py --task zbot-6b-walking-v2 --num_envs 4096 --max_iterations 30 \

@@ -275,8 +275,8 @@ def _check(task, label, n, seed, st, actions, g_out, sg, torch, wc=None, stats=N
     sd, outs_d = _run_oracle(task, n, seed, st, actions, wc=wc, double=True)
     ob_d, rw_d, te_d, tr_d = outs_d[-1]
     ref_d = (ob_d, rw_d, (te_d, tr_d))
-    ratio_gd = compare(task, sg, sd, ob_g, ob_d, rw_g, rw_d, (te_g, tr_g), ref_d[2], st, nsteps)[0]
-    ratio_od = compare(task, so, sd, ob_o, ob_d, rw_o, rw_d, (te_o, tr_o), ref_d[2], st, nsteps)[0]
+    ratio_gd, rows_gd = compare(task, sg, sd, ob_g, ob_d, rw_g, rw_d, (te_g, tr_g), ref_d[2], st, nsteps)[:2]
+    ratio_od, rows_od = compare(task, so, sd, ob_o, ob_d, rw_o, rw_d, (te_o, tr_o), ref_d[2], st, nsteps)[:2]
     ratio_do = compare(task, sd, so, ob_d, ob_o, rw_d, rw_o, ref_d[2], (te_o, tr_o), st, nsteps)[0]
     active = act.sum(axis=1) > 0
     frac, med = _aggregate(ratio_gd, active)
@@ -286,10 +286,20 @@ def _check(task, label, n, seed, st, actions, g_out, sg, torch, wc=None, stats=N
     print(f"  contact-active envs {int(active.sum())} of {n}, against the f64 oracle: device outliers {frac:.2%} "
           f"median err/tol {med:.3g}; f32 oracle {frac_o:.2%} / {med_o:.3g}  (device vs f32 oracle "
           f"{frac_g:.2%} / {med_g:.3g}; f64 vs f32 oracle {frac_x:.2%} / {med_x:.3g})")
+    # which quantities carry the device's error against f64: per row class, the median over the
+    # contact-active envs of the class's worst err/tol, device and f32 oracle
+    groups = {}
+    for cls, rows in row_groups(task).items():
+        if rows and active.any():
+            g_ = float(np.median(np.minimum(rows_gd[rows][:, active].max(axis=0), 1e6)))
+            o_ = float(np.median(np.minimum(rows_od[rows][:, active].max(axis=0), 1e6)))
+            groups[cls] = (g_, o_)
+    print("  by class, median worst err/tol vs f64 (device / f32 oracle): "
+          + ", ".join(f"{c} {g_:.3g} / {o_:.3g}" for c, (g_, o_) in groups.items()))
     if stats is not None:
         stats.update(frac=frac, med=med, frac_f32=frac_o, med_f32=med_o, active=int(active.sum()), nbad=len(bad))
     _record_stats(task, label, n, frac=frac, med=med, frac_f32=frac_o, med_f32=med_o, frac_vs_f32=frac_g,
-                  med_vs_f32=med_g, active=int(active.sum()), nbad=len(bad))
+                  med_vs_f32=med_g, active=int(active.sum()), nbad=len(bad), groups=groups)
     unexplained = [int(e) for e in bad if not _explained(ratio[e], sens[e])]
     ndeep = 0
     if unexplained:

@@ -502,6 +502,46 @@ __device__ __forceinline__ float tb(float x) { return dppf<DPP_BCAST + K>(x); } 
 template <int K>
 __device__ __forceinline__ int tbi(int x) { return dppi<DPP_BCAST + K>(x); }
 
+// tanh of the env's raw actions (_pre_physics_step's torch.tanh, v2.py:276-287), correctly rounded: lane
+// j < ND evaluates action j in double and the team broadcasts, as the oracle's (real)tanh((double)a).
+// The single-precision polynomial (tanh_r, ~1e-7) doubled the device's median error against exact
+// arithmetic on p_delta / actions; this costs one double tanh per lane per step.
+// tanh in double, rounded to float: expm1(2|x|) by Cody-Waite reduction (n = rint(y / ln 2)) and the
+// Taylor series of e^r - 1 to r^13 (|r| <= ln 2 / 2: < 1e-17 relative), then em1 / (em1 + 2) with
+// one Newton step on the reciprocal (no cancellation for small |x|: em1 = q there)
+__device__ __forceinline__ float tanh_f64(float xf) {
+  const double y = 2.0 * fmin(fabs((double)xf), 20.0);
+  const double n = rint(y * 1.4426950408889634074);
+  const double r = fma(-n, 1.90821492927058770002e-10, fma(-n, 6.93147180369123816490e-01, y));
+  double p = 1.0 / 6227020800.0;
+  p = fma(p, r, 1.0 / 479001600.0);
+  p = fma(p, r, 1.0 / 39916800.0);
+  p = fma(p, r, 1.0 / 3628800.0);
+  p = fma(p, r, 1.0 / 362880.0);
+  p = fma(p, r, 1.0 / 40320.0);
+  p = fma(p, r, 1.0 / 5040.0);
+  p = fma(p, r, 1.0 / 720.0);
+  p = fma(p, r, 1.0 / 120.0);
+  p = fma(p, r, 1.0 / 24.0);
+  p = fma(p, r, 1.0 / 6.0);
+  p = fma(p, r, 0.5);
+  p = fma(p, r, 1.0);
+  const double q = p * r;  // e^r - 1
+  const double em1 = n == 0.0 ? q : ldexp(1.0 + q, (int)n) - 1.0;
+  const double d = em1 + 2.0;
+  double rc = __builtin_amdgcn_rcp(d);
+  rc = fma(rc, fma(-d, rc, 1.0), rc);
+  rc = fma(rc, fma(-d, rc, 1.0), rc);
+  return copysignf((float)(em1 * rc), xf);
+}
+__device__ __forceinline__ void actions_tanh(const float* __restrict__ act, int i, int s, float out[ND]) {
+  // (every lane evaluates one -- lanes past ND repeat action 0 -- so no divergent branch splits the
+  // prologue)
+  const float mine = tanh_f64(act[(size_t)i * ZB_ACT_DIM + (s < ND ? s : 0)]);
+  out[0] = tb<0>(mine); out[1] = tb<1>(mine); out[2] = tb<2>(mine);
+  out[3] = tb<3>(mine); out[4] = tb<4>(mine); out[5] = tb<5>(mine);
+}
+
 // position of the r-th (0-based) set bit of m (r < popcount(m)): binary search on popcounts
 __device__ __forceinline__ int nth_set_bit(unsigned long long m, int r) {
   int pos = 0;
@@ -3107,10 +3147,12 @@ __device__ __forceinline__ void step_body(const zb_model* __restrict__ mg, const
     // what the MDP needs after the physics is parked in LDS (Pre), not held in registers
     Pre pr;
     pr.action_rate = 0.f;
+    float a_tanh[ND];
+    actions_tanh(act, i, q.s, a_tanh);
 #pragma unroll
     for (int j = 0; j < ND; ++j) {
       const float a_prev = ST(ZB_S_ACTIONS + j);
-      pr.a_now[j] = tanh_r(act[(size_t)i * ZB_ACT_DIM + j]);
+      pr.a_now[j] = a_tanh[j];
       pr.pdel[j] = clampf(ST(ZB_S_P_DELTA + j) + PI_F * pr.a_now[j] * cfg.joint_speed_limit * step_dt, -PI_F, PI_F);
       target[j] = pr.pdel[j] + m->default_joint_pos[j];
       pr.action_rate += (pr.a_now[j] - a_prev) * (pr.a_now[j] - a_prev);   // v2.py:502-507
@@ -3682,9 +3724,11 @@ __global__ __launch_bounds__(WGT, kOcc) void zb_su_step_kernel(
   float target[ND];
   {
     Pre pr;
+    float a_tanh[ND];
+    actions_tanh(act, i, q.s, a_tanh);
 #pragma unroll
     for (int j = 0; j < ND; ++j) {
-      pr.a_now[j] = tanh_r(act[(size_t)i * ZB_ACT_DIM + j]);
+      pr.a_now[j] = a_tanh[j];
       pr.pdel[j] = clampf(ST(ZB_SU_P_DELTA + j) + PI_F * pr.a_now[j] * cfg.joint_speed_limit * step_dt, -PI_F, PI_F);
       target[j] = pr.pdel[j] + m->default_joint_pos[j];
     }
@@ -3976,10 +4020,12 @@ __global__ __launch_bounds__(WGT, kOcc) void zb_v4_step_kernel(
   {
     PreV4 pr;
     pr.action_rate = 0.f;
+    float a_tanh[ND];
+    actions_tanh(act, i, q.s, a_tanh);
 #pragma unroll
     for (int j = 0; j < ND; ++j) {
       const float a_prev = ST(ZB_V4_ACTIONS + j);
-      pr.a_now[j] = tanh_r(act[(size_t)i * ZB_ACT_DIM + j]);
+      pr.a_now[j] = a_tanh[j];
       pr.pdel[j] = clampf(ST(ZB_V4_P_DELTA + j) + PI_F * pr.a_now[j] * cfg.joint_speed_limit * step_dt, -PI_F, PI_F);
       target[j] = pr.pdel[j] + m->default_joint_pos[j];
       pr.action_rate += (pr.a_now[j] - a_prev) * (pr.a_now[j] - a_prev);
