@@ -6,7 +6,7 @@
 #   suite            pytest -m gpu (the driver's suite) + smoke()
 #   bench            the default bench line (4096 envs, with the CPU leg)
 #   lines            bench lines: 4096 / 8192 / 65536 envs and the other tasks (no CPU leg)
-#   solver           bench lines at solver modes 0 / 3 x self_manifold 2 / 3 x 4096 / 8192 / 65536 envs
+#   solver           bench lines at solver modes $MODES (0 3) x self_manifold $SMS (2 3) x $SIZES envs
 #   prof             rocprofv3 kernel trace + stats, then separate PMC passes, on bench.py; writes
 #                    roofline_pmc.json (scripts/prof_summary.py)
 #   parityab         the full-state parity checks once per library in $LIBS (ZB_PARITY_STATS JSONL)
@@ -43,7 +43,7 @@ for s in "$@"; do
       for n in 4096 8192 65536; do run bench_$n 300 python bench.py --envs-per-gpu $n --no-cpu-baseline; done
       for t in standup v4 manager; do run bench_$t 300 python bench.py --task $t --no-cpu-baseline; done ;;
     solver)
-      for n in 4096 8192 65536; do for m in 0 3; do for sm in 2 3; do
+      for n in ${SIZES:-4096 8192 65536}; do for m in ${MODES:-0 3}; do for sm in ${SMS:-2 3}; do
         run solver_n${n}_m${m}_sm${sm} 300 python bench.py --envs-per-gpu $n --solver-mode $m --self-manifold $sm \
           --no-cpu-baseline
       done; done; done ;;
@@ -80,7 +80,7 @@ for s in "$@"; do
     tests)
       run tests 900 $PT ${TESTS:?TESTS=<pytest paths>} -m gpu ;;
     budget)
-      run error_budget 300 python tools/error_budget.py 2048 ;;
+      for lib in ${LIBS:-libzbot.so}; do run error_budget_${lib%.so} 300 env ZBOT_LIB=$lib python tools/error_budget.py 2048; done ;;
     train_v2)
       run train_v2 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/train_v2 -o run -- \
         python3 scripts/train.py --task zbot-6b-walking-v2 --num_envs 4096 --max_iterations 30 \

@@ -124,7 +124,10 @@ def test_manager_registration_and_cfg():
     from zbot_lab_amd.envs.manager_flat import DoneTerm, EventTerm, RewTerm
     assert {"zbot-6b-walking-m-v0", "zbot-6b-walking-m-play-v0"} <= set(zbot_lab_amd.tasks.registered())
     cfg = zbot_lab_amd.tasks.load_cfg("zbot-6b-walking-m-v0")
-    assert dataclasses.asdict(cfg.task_cfg()) == dataclasses.asdict(zm.TaskCfg.manager_flat())
+    # (the env's solver default is the product configuration, DESIGN.md §3.6: TGS, mode 1; the raw ABI
+    # mirror TaskCfg keeps the C struct's PGS default)
+    assert dataclasses.asdict(cfg.task_cfg()) == dataclasses.asdict(zm.TaskCfg.manager_flat(solver_mode=1))
+    assert cfg.task_cfg().self_manifold == 2
     cfg.rewards.feet_slide.weight = -3.0
     cfg.commands.base_velocity.ranges.lin_vel_x = (-0.2, 0.2)
     t = cfg.task_cfg()

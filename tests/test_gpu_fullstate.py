@@ -296,8 +296,12 @@ def _check(task, label, n, seed, st, actions, g_out, sg, torch, wc=None, stats=N
             groups[cls] = (g_, o_)
     print("  by class, median worst err/tol vs f64 (device / f32 oracle): "
           + ", ".join(f"{c} {g_:.3g} / {o_:.3g}" for c, (g_, o_) in groups.items()))
+    # the f32 oracle's own outlier count against f64 on the same states: the rounding-noise baseline of
+    # the per-check outlier caps (test_full_state_tgs)
+    nbad_f32 = int((ratio_do > 1).sum())
     if stats is not None:
-        stats.update(frac=frac, med=med, frac_f32=frac_o, med_f32=med_o, active=int(active.sum()), nbad=len(bad))
+        stats.update(frac=frac, med=med, frac_f32=frac_o, med_f32=med_o, active=int(active.sum()), nbad=len(bad),
+                     nbad_f32=nbad_f32)
     _record_stats(task, label, n, frac=frac, med=med, frac_f32=frac_o, med_f32=med_o, frac_vs_f32=frac_g,
                   med_vs_f32=med_g, active=int(active.sum()), nbad=len(bad), groups=groups)
     unexplained = [int(e) for e in bad if not _explained(ratio[e], sens[e])]
@@ -457,12 +461,14 @@ def test_full_state_tgs(gpu, task, mode):
         for _ in range(steps):
             obs, rew, te, tr = g.step(at)
         g_out = (obs.cpu().numpy(), rew.cpu().numpy(), te.cpu().numpy().copy(), tr.cpu().numpy().copy())
+        stats = {}
         nbad = _check(task, f"TGS mode {mode}: {steps} zero-action steps from standing", n, seed, st,
-                      [np.zeros((n, 6), np.float32)] * steps, g_out, g.get_state().cpu().numpy(), torch)
-        # (20 TGS steps of standing contact: 4.8-5.1 % of envs end outside tolerance in mode 1,
-        # 6.7-7.1 % with the refresh (modes 2, 3; r4-r5 runs), every one explained; the f64-baseline
-        # aggregate in _check bounds the fraction, this is a sanity cap)
-        assert nbad <= 0.085 * n
+                      [np.zeros((n, 6), np.float32)] * steps, g_out, g.get_state().cpu().numpy(), torch, stats=stats)
+        # the envs outside tolerance (device against the f32 oracle), bounded by the f32 oracle's own count
+        # against f64 on the same states -- two f32 implementations each differ from exact arithmetic
+        # by their rounding -- as the aggregate rule does (round 5 had a hand-set
+        # 8.5 % cap here): v2 mode 1 46 envs against a bound of 2 x 32 + 5 = 69
+        assert nbad <= 2 * stats["nbad_f32"] + 0.005 * n, (nbad, stats["nbad_f32"])
 
 
 @pytest.mark.parametrize("task", TASKS)

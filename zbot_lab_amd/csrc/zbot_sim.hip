@@ -49,6 +49,9 @@ constexpr float kCoreM = 0.004f;
 #define ZB_GJK_MAXIT 16
 #endif
 constexpr int kGjkMaxIt = ZB_GJK_MAXIT;
+#ifndef ZB_RSQ_NR
+#define ZB_RSQ_NR 0
+#endif
 #ifndef ZB_GJK_TOL
 #define ZB_GJK_TOL 1e-5f  // (variant builds for the A/B: scripts/gpu_r5_bench_ab.sh)
 #endif
@@ -1720,8 +1723,11 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q&
 #ifdef ZB_STAMPS
     int deep_quad = 0;  // diagnostic: this quad's contacts on overlapping cores
 #endif
-    SelfContact hit0 = {};  // this quad's first contact is kept for the write pass
-    int hit0_k = -1;
+    // this quad's first two contacts are kept for the write pass, which re-runs GJK only for a third
+    // (round 6: the re-runs cost 3 % of the step at 4096 envs -- folded robots, whose quads hold two
+    // contact pairs, are the slow waves; ZB_DIAG_NO_RERUN bounds it)
+    SelfContact hit0 = {}, hit1 = {};
+    int hit0_k = -1, hit1_k = -1;
     // bit k: this quad's pair of round k is a contact (own) of points - 1 = lo + 2 hi (own_lo / own_hi)
     unsigned own = 0u, own_lo = 0u, own_hi = 0u;
     // team, bit r: the pair of rank r is a contact (allhits), its points - 1 = exl + 2 exh: a pair's
@@ -1740,12 +1746,17 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q&
         if (!need) continue;
         const int pcode = q.pair_code(nth_set_bit(bmask, r));
         SelfContact sc = hit0;
+        if (pass == 1 && k == hit1_k) {
+          sc.n[0] = hit1.n[0]; sc.n[1] = hit1.n[1]; sc.n[2] = hit1.n[2];
+          sc.x[0] = hit1.x[0]; sc.x[1] = hit1.x[1]; sc.x[2] = hit1.x[2];
+          sc.sep = hit1.sep;
+        }
         QCircle hc;
         quad_circle(q, (qj & 2) ? (pcode & 15) : (pcode >> 4), qj & 1, hc);
 #ifdef ZB_DIAG_NO_RERUN  // diagnostic build (wrong contacts): what the write pass's GJK re-runs cost
         if (pass == 0) {
 #else
-        if (pass == 0 || k != hit0_k) {
+        if (pass == 0 || (k != hit0_k && k != hit1_k)) {
 #endif
           // start: the pair's contact normal of the previous substep of this step (kept contacts
           // hold {n, code} in FRC; unused slots code -1), else the hull centre difference
@@ -1775,7 +1786,13 @@ __device__ __forceinline__ int detect(const zb_task_cfg& cfg, float Pz, const Q&
           }
           sp.note_its(its);
           if (pass == 0 && h) {
-            if (own == 0u) { hit0 = sc; hit0_k = k; }
+            if (own == 0u) {
+              hit0 = sc;
+              hit0_k = k;
+            } else if (hit1_k < 0) {
+              hit1 = sc;
+              hit1_k = k;
+            }
             own |= 1u << k;
 #ifdef ZB_STAMPS
             if (qj == 0 && sc.sep <= -2.f * kCoreM + 1e-7f) ++deep_quad;
@@ -2081,7 +2098,14 @@ __device__ __forceinline__ void team_chol_col(float R[NV], float L[NT], float in
 #pragma unroll
   for (int m = 0; m < K; ++m) t = fmaf(-R[m], L[tri(K, m)], t);
   const float pv = fmaxf(tb<own_lane(K)>(t), 1e-12f);
+#if ZB_RSQ_NR
+  // v_rsq_f32 (1 ulp) refined by one Newton step: every whitened quantity (the free velocity, the
+  // contact rows Y = L^-1 J^T, their effective masses) is scaled by these pivots
+  float iv = __builtin_amdgcn_rsqf(pv);
+  iv = fmaf(0.5f * iv, fmaf(-pv * iv, iv, 1.f), iv);
+#else
   const float iv = __builtin_amdgcn_rsqf(pv);
+#endif
   inv[K] = iv;
   R[K] = t * iv;
   L[tri(K, K)] = pv * iv;

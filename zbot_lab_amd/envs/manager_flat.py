@@ -208,7 +208,8 @@ class Zbot6BFlatEnvCfg:
     decimation: int = 4
     episode_length_s: float = 20.0
     sim: SimulationCfg = field(default_factory=SimulationCfg)
-    solver: SolverCfg = field(default_factory=SolverCfg)
+    # (the ruling-on-face manifold is compiled into the walking v2 / stand-up kernels only)
+    solver: SolverCfg = field(default_factory=lambda: SolverCfg(self_manifold=2))
     seed: int | None = None
 
     # the DirectRLEnv-style fields the shared env base reads

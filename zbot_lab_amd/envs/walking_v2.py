@@ -50,8 +50,17 @@ class SolverCfg:
     contact_margin: float = 0.004
     baumgarte: float = 0.2
     self_collision: bool = True       # enabled_self_collisions=True (zbot_cfg.py:636)
-    mode: int = 0                     # 0: PGS sweeps; 1: TGS-style sub-iterations; 2: TGS + ground-contact refresh; 3: + self-contact refresh (zb_task_cfg.solver_mode)
-    self_manifold: int = 2            # 2: cap-on-cap (up to 4 points) + side-by-side rims (up to 3); 1: caps only; 0: off (zb_task_cfg.self_manifold)
+    # zb_task_cfg.solver_mode. 1 (default, round 6): PhysX TGS with solver_position_iteration_count 4 /
+    # velocity 0 (zbot_cfg.py:637-638) -- 4 sub-iterations of dt / 4 on the step's constraint rows, each
+    # contact's separation advanced by the accumulated relative motion along its normal;
+    # 0: 4 projected Gauss-Seidel sweeps on one linearisation (rounds 1-5 default); 2: 1 + the ground
+    # contacts re-evaluated at every sub-iteration's pose; 3: 2 + the self contacts too
+    mode: int = 1
+    # zb_task_cfg.self_manifold. 3 (default, round 6; walking v2 and stand-up): cap-on-cap (up to 4
+    # points), a link lying on another's cap (up to 3), side-by-side rims (up to 3) -- PhysX PCM keeps up
+    # to 4 points per convex pair (zbot_cfg.py:636); 2: without the ruling-on-face case (v4 / manager
+    # default); 1: caps only; 0: one point per pair
+    self_manifold: int = 3
 
 
 def _scales(**kw) -> dict:

@@ -59,7 +59,8 @@ class Zbot6SEnvV4Cfg:
     contact_history_length: int = 3
     sim: SimulationCfg = field(default_factory=SimulationCfg)
     scene: InteractiveSceneCfg = field(default_factory=InteractiveSceneCfg)
-    solver: SolverCfg = field(default_factory=SolverCfg)
+    # (the ruling-on-face manifold is compiled into the walking v2 / stand-up kernels only)
+    solver: SolverCfg = field(default_factory=lambda: SolverCfg(self_manifold=2))
     events: EventCfgV4 = field(default_factory=EventCfgV4)
     seed: int | None = None
     reward_cfg: dict = field(default_factory=lambda: {"reward_scales": dict(zm.V4_REWARD_WEIGHTS)})
