@@ -2635,13 +2635,16 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
     float wsum = 0.f;  // TGS: the sum of the sub-iterations' w (this lane's coordinate)
     for (int it = 0; it < cfg.solver_iterations; ++it) {
       if (tgs && it > 0) {  // re-linearise the biases
-#pragma unroll
-        for (int c = 0; c < NCM; ++c)
-          if (c < ncw) {
-            const float vn = tsum(q.yg(yl, c).x * wd);
-            sep_own = q.s == c ? fmaf(hsub, vn, sep_own) : sep_own;
-          }
+        // every contact's normal velocity Y0_c . w at once (round 6): w broadcast to the team, lane c
+        // reads its slot's 12 granules -- one short chain instead of a team reduction per contact
+        const float wb[NV] = {tb<own_lane(0)>(wd), tb<own_lane(1)>(wd), tb<own_lane(2)>(wd), tb<own_lane(3)>(wd),
+                              tb<own_lane(4)>(wd), tb<own_lane(5)>(wd), tb<own_lane(6)>(wd), tb<own_lane(7)>(wd),
+                              tb<own_lane(8)>(wd), tb<own_lane(9)>(wd), tb<own_lane(10)>(wd), tb<own_lane(11)>(wd)};
         if (q.s < nc) {
+          float vn = 0.f;
+#pragma unroll
+          for (int d = 0; d < NV; ++d) vn = fmaf(q.yg_at(q.s, own_lane(d)).x, wb[d], vn);
+          sep_own = fmaf(hsub, vn, sep_own);
           const float4 a0 = q.aux(q.s, 0);
           q.aux(q.s, 0) = make_float4(a0.x, a0.y, a0.z, contact_bias(cfg, m, sep_own, hsub, dt) * a0.x);
         }
