@@ -173,7 +173,7 @@ def test_fused_gae_matches_torch(gpu, monkeypatch):
     assert abs(float(st.advantages.mean())) < 1e-5 and abs(float(st.advantages.std()) - 1.0) < 1e-4
 
 
-@pytest.mark.parametrize("rows", ["reg", "lds", "reg-small"])
+@pytest.mark.parametrize("rows", ["reg", "lds", "reg-small", "split", "split-small"])
 @pytest.mark.parametrize("hidden", [[128, 128, 128], [256, 256, 128]], ids=["v2-nets", "standup-nets"])
 def test_fused_act_matches_torch_policy(gpu, hidden, rows, monkeypatch):
     """zbp_act (the rollout's policy step, runner._rollout) against PPO.act's torch statement with the
@@ -188,8 +188,16 @@ def test_fused_act_matches_torch_policy(gpu, hidden, rows, monkeypatch):
         monkeypatch.setenv("ZBP_ACT", "lds")
     if rows == "reg-small":  # (the register-resident forward forced below its row threshold)
         monkeypatch.setenv("ZBP_ACT", "reg")
+    if rows == "reg":  # (k_act_reg itself; the 128-wide nets take k_act_split by default, round 6)
+        monkeypatch.setenv("ZBP_ACT", "reg")
+    if rows.startswith("split"):  # k_act_split: the 128-wide nets' default from 4096 rows; forced below
+        if hidden[0] != 128:
+            pytest.skip("k_act_split serves the 128-wide nets")
+        if rows == "split-small":
+            monkeypatch.setenv("ZBP_ACT", "split")
     # (k_act_reg takes rollouts of >= 4096 rows; 16 400 is not a multiple of its 64-row workgroups)
-    for envs in {"reg": (16400, 4096), "lds": (4096, 200), "reg-small": (200,)}[rows]:
+    for envs in {"reg": (16400, 4096), "lds": (4096, 200), "reg-small": (200,), "split": (16400, 4096),
+                 "split-small": (200, 40)}[rows]:
         alg = _alg(hidden, envs=envs)
         fu = fused.FusedUpdate(alg, 256)  # (the minibatch size shapes only the update's row buffers)
         st = alg.storage

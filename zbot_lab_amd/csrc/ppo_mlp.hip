@@ -1144,6 +1144,9 @@ template <int T1, int T2, int T3>
 #ifndef ZBP_ACT_REG_MIN
 #define ZBP_ACT_REG_MIN 4096
 #endif
+#ifndef ZBP_ACT_SPLIT_MAX
+#define ZBP_ACT_SPLIT_MAX 65536
+#endif
 __global__ __launch_bounds__(RR_WG, 2) void k_act_reg(ActArgs A) {
   constexpr int CB = 32;
   __shared__ float4 wl[2 * CB * 64];
@@ -1196,6 +1199,123 @@ __global__ __launch_bounds__(RR_WG, 2) void k_act_reg(ActArgs A) {
     } else if (ok && gq == 0) {
       A.s_val[row] = z[0][0];
     }
+  }
+}
+
+// k_act for rollouts of the 128-wide nets (rsl_rl's [128, 128, 128], walking v2; round 6): one
+// workgroup of four waves per 16-row tile and net, the waves splitting every layer's output tiles
+// (a quarter each) and exchanging the layer's activations through LDS (double-buffered, one barrier
+// per layer); each wave reads its own output tiles' weight blocks from L2 (no staging). At 4096 rows
+// that is 2048 waves (two per SIMD) with a quarter of k_act_reg's MFMAs each, against k_act_reg's 512
+// waves holding the whole net. Same statement (same per-lane accumulation order within a tile).
+template <int TI, int TO, bool kElu>
+__device__ __forceinline__ void as_layer(const float* __restrict__ img, const float* __restrict__ bias,
+                                         const Tile (&in)[TI], Tile (&out)[TO], Tile* __restrict__ xs, int wv,
+                                         int lane) {
+  constexpr int TQ = TO / 4;
+  const float4* g = reinterpret_cast<const float4*>(img);
+  float4 wb[TI][TQ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int q = 0; q < TQ; ++q) wb[i][q] = g[(i * TO + wv * TQ + q) * 64 + lane];
+  Tile acc[TQ];
+#pragma unroll
+  for (int q = 0; q < TQ; ++q) acc[q] = Tile{};
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int q = 0; q < TQ; ++q) {
+      Tile a = acc[q];
+      a = mfma16(wb[i][q].x, in[i][0], a);
+      a = mfma16(wb[i][q].y, in[i][1], a);
+      a = mfma16(wb[i][q].z, in[i][2], a);
+      a = mfma16(wb[i][q].w, in[i][3], a);
+      acc[q] = a;
+    }
+  const float* bp = bias + 4 * ((lane & 63) >> 4);
+#pragma unroll
+  for (int q = 0; q < TQ; ++q) {
+    const int o = wv * TQ + q;
+    const float4 bq = *reinterpret_cast<const float4*>(bp + 16 * o);
+    const float bv[4] = {bq.x, bq.y, bq.z, bq.w};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      float v = acc[q][u] + bv[u];
+      if (kElu) v = v > 0.f ? v : expf(v) - 1.f;  // ELU(alpha = 1), as ATen's elu kernel
+      acc[q][u] = v;
+    }
+    xs[o * 64 + lane] = acc[q];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int o = 0; o < TO; ++o) out[o] = xs[o * 64 + lane];
+}
+
+template <int T1, int T2, int T3>
+__global__ __launch_bounds__(256, 2) void k_act_split(ActArgs A) {
+  static_assert(T1 % 4 == 0 && T2 % 4 == 0 && T3 % 4 == 0, "output tiles split over four waves");
+  constexpr int TM = T1 > T2 ? (T1 > T3 ? T1 : T3) : (T2 > T3 ? T2 : T3);
+  __shared__ Tile xs[2][TM * 64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, r = lane & 15, gq = lane >> 4;
+  const int net = blockIdx.x & 1;
+  const int64_t row = (int64_t)(blockIdx.x >> 1) * 16 + r;
+  const bool ok = row < A.rows;
+  const int na = A.na;
+  const NetW& w = A.n[net];
+  Tile x0[2], x1[T1], x2[T2], x3[T3];
+  {
+    const int dim = net ? A.cobs_dim : A.obs_dim;
+    const float* src = (net ? A.cobs : A.obs) + row * dim;
+    float* st = (net ? A.s_cobs : A.s_obs) + row * dim;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 16 * (j >> 2) + 4 * gq + (j & 3);
+      const float v = (ok && k < dim) ? src[k] : 0.f;
+      x0[j >> 2][j & 3] = v;
+      if (wv == 0 && ok && k < dim) st[k] = v;
+    }
+  }
+  as_layer<2, T1, true>(A.ws + w.wr[0], A.ws + w.bp[0], x0, x1, xs[0], wv, lane);
+  as_layer<T1, T2, true>(A.ws + w.wr[1], A.ws + w.bp[1], x1, x2, xs[1], wv, lane);
+  as_layer<T2, T3, true>(A.ws + w.wr[2], A.ws + w.bp[2], x2, x3, xs[0], wv, lane);
+  if (wv != 0) return;
+  // the output layer (2 tiles in the image: num_actions <= 13 and the value live in tile 0), wave 0
+  Tile z = Tile{};
+  {
+    const float4* g = reinterpret_cast<const float4*>(A.ws + w.wr[3]);
+#pragma unroll
+    for (int i = 0; i < T3; ++i) {
+      const float4 wq = g[(i * 2 + 0) * 64 + lane];
+      z = mfma16(wq.x, x3[i][0], z);
+      z = mfma16(wq.y, x3[i][1], z);
+      z = mfma16(wq.z, x3[i][2], z);
+      z = mfma16(wq.w, x3[i][3], z);
+    }
+    const float4 bq = *reinterpret_cast<const float4*>(A.ws + w.bp[3] + 4 * gq);
+    z[0] += bq.x; z[1] += bq.y; z[2] += bq.z; z[3] += bq.w;
+  }
+  if (net == 0) {
+    // lane (r, g) holds actions 4 g + u of row r
+    const float kLog2Pi = 0.91893853320467274178f;  // log(sqrt(2 pi))
+    float lp = 0.f;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int n = 4 * gq + u;
+      if (ok && n < na) {
+        const float mu = z[u], s = A.std_param[n];
+        const float x = mu + s * A.noise[row * na + n], diff = x - mu;
+        lp += -(diff * diff) / (2.f * (s * s)) - logf(s) - kLog2Pi;
+        A.actions[row * na + n] = x;
+        A.s_act[row * na + n] = x;
+        A.s_mu[row * na + n] = mu;
+        A.s_sig[row * na + n] = s;
+      }
+    }
+    lp = rr_feat_sum(lp);
+    if (ok && gq == 0) A.s_lp[row] = lp;
+  } else if (ok && gq == 0) {
+    A.s_val[row] = z[0];
   }
 }
 
@@ -1544,9 +1664,15 @@ int zbp_act(const zbp_net* actor, const zbp_net* critic, const float* std_param,
   // (4096): 23.5 us against the LDS kernel's 34.9 at 4096 rows (before the split 42 us: too few
   // workgroups), 146 against 242 at 32 768 (profiles/r5y); ZBP_ACT=lds / reg for A/Bs)
   const char* ea = getenv("ZBP_ACT");
-  const int reg_min = ea && !strcmp(ea, "reg") ? 0 : (ea && !strcmp(ea, "lds") ? (1 << 30) : ZBP_ACT_REG_MIN);
+  const bool f_reg = ea && !strcmp(ea, "reg"), f_lds = ea && !strcmp(ea, "lds"), f_split = ea && !strcmp(ea, "split");
+  const int reg_min = (f_reg || f_split) ? 0 : (f_lds ? (1 << 30) : ZBP_ACT_REG_MIN);
   const int shape = io->rows >= reg_min ? reg_shape(lo) : 0, wgs = 2 * ((io->rows + 63) / 64);
-  if (shape == 1)
+  // the 128-wide nets (shape 2): the split-output forward (k_act_split, round 6) up to
+  // ZBP_ACT_SPLIT_MAX rows; ZBP_ACT=reg / lds / split forces a kernel for A/Bs and tests
+  const bool split = shape == 2 && !f_reg && (f_split || io->rows <= ZBP_ACT_SPLIT_MAX);
+  if (split)
+    k_act_split<8, 8, 8><<<2 * ((io->rows + 15) / 16), 256, 0, (hipStream_t)stream>>>(A);
+  else if (shape == 1)
     k_act_reg<16, 16, 8><<<wgs, RR_WG, 0, (hipStream_t)stream>>>(A);
   else if (shape == 2)
     k_act_reg<8, 8, 8><<<wgs, RR_WG, 0, (hipStream_t)stream>>>(A);
