@@ -387,6 +387,10 @@ int zb_set_log_buffers(zb_handle h, float* term_means, int32_t* counts);
  * rsl_rl/runners/on_policy_runner.py; the reference's train.py:205 runner.learn). Resets do not
  * add. NULL unregisters. */
 int zb_set_log_accumulator(zb_handle h, float* acc);
+/* Register a caller-owned device int64[N]: every later zb_step writes terminated | truncated into it
+ * (rsl_rl's dones, RslRlVecEnvWrapper.step; isaaclab_rl's wrapper computes it with two torch ops per
+ * step) from the step kernel's own flag stores. NULL unregisters. */
+int zb_set_done_buffer(zb_handle h, int64_t* dones);
 
 /* Persistent state, device float[zb_state_dim(h)][N] (ZB_STATE_DIM / ZB_SU_STATE_DIM).
  * zb_set_state also invalidates the contact cache below. */

@@ -143,6 +143,31 @@ def test_native_log_accumulator_matches_per_step_sum(gpu, task):
     env.close()
 
 
+@pytest.mark.parametrize("task", ["zbot-6b-walking-v2", "zbot-6b-standup-v0", "zbot-6b-walking-v4",
+                                  "zbot-6b-walking-m-v0"])
+def test_done_buffer_matches_flags(gpu, task):
+    """zb_set_done_buffer: the wrapper's dones (written by the step kernel's epilogue) equal
+    (terminated | truncated).long() every step, over steps with terminations and time-outs."""
+    import torch
+    import zbot_lab_amd
+    from zbot_lab_amd.rl.vecenv import RslRlVecEnvWrapper
+    cfg = zbot_lab_amd.tasks.load_cfg(task)
+    cfg.scene.num_envs = 1000  # not a multiple of the 4 envs per wave: the ragged last wave
+    env = zbot_lab_amd.make(task, cfg=cfg)
+    w = RslRlVecEnvWrapper(env)
+    assert w._dones is not None
+    env.episode_length_buf = torch.randint_like(env.episode_length_buf, high=int(env.max_episode_length))
+    g = torch.Generator(device=env.device).manual_seed(5)
+    seen = torch.zeros(2, dtype=torch.long, device=env.device)
+    for _ in range(50):
+        _, _, dones, extras = w.step(torch.randn(1000, 6, device=env.device, generator=g) * 2)
+        term, trunc = env.sim.terminated, env.sim.truncated
+        assert dones.dtype == torch.long and torch.equal(dones, (term | trunc).to(torch.long))
+        seen += torch.stack([term.sum(), trunc.sum()]).to(torch.long)
+    assert int(seen.sum()) > 0
+    env.close()
+
+
 def test_runner_uses_native_log_accumulator(gpu, tmp_path):
     """The runner registers the accumulator and its per-iteration log means equal the torch path's."""
     import torch

@@ -1993,7 +1993,8 @@ __device__ __forceinline__ float& Q::stg(int k) const { return reinterpret_cast<
 template <int SD, int OD>
 __device__ __forceinline__ void staged_store(const Q& q, int env0, int N, float* __restrict__ st,
                                              float* __restrict__ obs, float* __restrict__ rew,
-                                             uint8_t* __restrict__ term, uint8_t* __restrict__ trunc) {
+                                             uint8_t* __restrict__ term, uint8_t* __restrict__ trunc,
+                                             int64_t* __restrict__ done) {
   static_assert(SD + OD + 3 <= STG_LEN, "staging row");
   wave_sync();
   const float* S = reinterpret_cast<const float*>(q.b + YG_OFF);
@@ -2005,6 +2006,8 @@ __device__ __forceinline__ void staged_store(const Q& q, int env0, int N, float*
     if (f0 == 0) rew[env] = S[e * STG_LEN + SD + OD];
     if (f0 == 1) term[env] = S[e * STG_LEN + SD + OD + 1] != 0.f ? 1 : 0;
     if (f0 == 2) trunc[env] = S[e * STG_LEN + SD + OD + 2] != 0.f ? 1 : 0;
+    // the caller's done buffer (zb_set_done_buffer): terminated | truncated as int64, rsl_rl's dones
+    if (done && f0 == 3) done[env] = (S[e * STG_LEN + SD + OD + 1] != 0.f || S[e * STG_LEN + SD + OD + 2] != 0.f) ? 1 : 0;
   }
   const int nv = min(EPW, N - env0);
 #pragma unroll
@@ -3141,8 +3144,8 @@ __device__ __forceinline__ void step_body(const zb_model* __restrict__ mg, const
                                           zb_task_cfg cfg, int N, float* __restrict__ st,
                                           const float* __restrict__ act, float* __restrict__ obs,
                                           float* __restrict__ rew, uint8_t* __restrict__ term,
-                                          uint8_t* __restrict__ trunc, float* __restrict__ acc,
-                                          float* __restrict__ wc, float4* lds) {
+                                          uint8_t* __restrict__ trunc, int64_t* __restrict__ done,
+                                          float* __restrict__ acc, float* __restrict__ wc, float4* lds) {
   MP m = to_mp(mg);
   const int lane = (int)threadIdx.x;
   const int env = xcd_block(blockIdx.x, gridDim.x) * EPW + lane / TL;
@@ -3438,7 +3441,7 @@ __device__ __forceinline__ void step_body(const zb_model* __restrict__ mg, const
     o[ZB_OBS_DIM + 1] = died ? 1.f : 0.f;
     o[ZB_OBS_DIM + 2] = time_out ? 1.f : 0.f;
   }
-  staged_store<ZB_STATE_DIM, ZB_OBS_DIM>(q, xcd_block(blockIdx.x, gridDim.x) * EPW, N, st, obs, rew, term, trunc);
+  staged_store<ZB_STATE_DIM, ZB_OBS_DIM>(q, xcd_block(blockIdx.x, gridDim.x) * EPW, N, st, obs, rew, term, trunc, done);
 #undef OUT
   sp.mark(8);
   sp.flush();
@@ -3458,10 +3461,11 @@ __global__ __launch_bounds__(WGT, kOcc) void zb_step_kernel(const zb_model* __re
                                                           float* __restrict__ st, const float* __restrict__ act,
                                                           float* __restrict__ obs, float* __restrict__ rew,
                                                           uint8_t* __restrict__ term, uint8_t* __restrict__ trunc,
-                                                          float* __restrict__ acc, float* __restrict__ wc) {
+                                                          int64_t* __restrict__ done, float* __restrict__ acc,
+                                                          float* __restrict__ wc) {
   __shared__ float4 lds[LDS4];
   if (kOcc == 1) asm volatile("" ::: "a255");
-  step_body<kTgs, kRefresh, kRf>(mg, links, cfg, N, st, act, obs, rew, term, trunc, acc, wc, lds);
+  step_body<kTgs, kRefresh, kRf>(mg, links, cfg, N, st, act, obs, rew, term, trunc, done, acc, wc, lds);
 }
 
 // Test entry (zb_pair_manifold): GJK (cold start) + the face manifold of n link pairs given as
@@ -3719,8 +3723,8 @@ template <bool kTgs, int kOcc, bool kRefresh = false, bool kRf = false>
 __global__ __launch_bounds__(WGT, kOcc) void zb_su_step_kernel(
     const zb_model* __restrict__ mg, const float4* __restrict__ links, zb_task_cfg cfg, int N, float* __restrict__ st,
     const float* __restrict__ act, float* __restrict__ obs, float* __restrict__ rew, uint8_t* __restrict__ term,
-    uint8_t* __restrict__ trunc, float* __restrict__ acc, const Counters* __restrict__ cnt, uint64_t seed,
-    float* __restrict__ wc) {
+    uint8_t* __restrict__ trunc, int64_t* __restrict__ done, float* __restrict__ acc,
+    const Counters* __restrict__ cnt, uint64_t seed, float* __restrict__ wc) {
   MP m = to_mp(mg);
   __shared__ float4 lds[LDS4];
   if (kOcc == 1) asm volatile("" ::: "a255");  // (zb_step_kernel: kOcc)
@@ -3908,7 +3912,7 @@ __global__ __launch_bounds__(WGT, kOcc) void zb_su_step_kernel(
     q.stg(ZB_SU_LINK_MU + ZB_SU_OBS_DIM + 1) = died ? 1.f : 0.f;
     q.stg(ZB_SU_LINK_MU + ZB_SU_OBS_DIM + 2) = time_out ? 1.f : 0.f;
   }
-  staged_store<ZB_SU_LINK_MU, ZB_SU_OBS_DIM>(q, xcd_block(blockIdx.x, gridDim.x) * EPW, N, st, obs, rew, term, trunc);
+  staged_store<ZB_SU_LINK_MU, ZB_SU_OBS_DIM>(q, xcd_block(blockIdx.x, gridDim.x) * EPW, N, st, obs, rew, term, trunc, done);
 #undef OUT
   sp.mark(8);
   sp.flush();
@@ -4015,8 +4019,8 @@ template <bool kTgs, int kOcc>
 __global__ __launch_bounds__(WGT, kOcc) void zb_v4_step_kernel(
     const zb_model* __restrict__ mg, const float4* __restrict__ links, zb_task_cfg cfg, int N, float* __restrict__ st,
     const float* __restrict__ act, float* __restrict__ obs, float* __restrict__ rew, uint8_t* __restrict__ term,
-    uint8_t* __restrict__ trunc, float* __restrict__ acc, const Counters* __restrict__ cnt, uint64_t seed,
-    float* __restrict__ wc) {
+    uint8_t* __restrict__ trunc, int64_t* __restrict__ done, float* __restrict__ acc,
+    const Counters* __restrict__ cnt, uint64_t seed, float* __restrict__ wc) {
   MP m = to_mp(mg);
   __shared__ float4 lds[LDS4];
   if (kOcc == 1) asm volatile("" ::: "a255");  // (zb_step_kernel: kOcc)
@@ -4346,7 +4350,7 @@ __global__ __launch_bounds__(WGT, kOcc) void zb_v4_step_kernel(
     q.stg(ZB_V4_STATE_DIM + ZB_V4_OBS_DIM + 1) = died ? 1.f : 0.f;
     q.stg(ZB_V4_STATE_DIM + ZB_V4_OBS_DIM + 2) = time_out ? 1.f : 0.f;
   }
-  staged_store<ZB_V4_STATE_DIM, ZB_V4_OBS_DIM>(q, xcd_block(blockIdx.x, gridDim.x) * EPW, N, st, obs, rew, term, trunc);
+  staged_store<ZB_V4_STATE_DIM, ZB_V4_OBS_DIM>(q, xcd_block(blockIdx.x, gridDim.x) * EPW, N, st, obs, rew, term, trunc, done);
 #undef OUT
   sp.mark(8);
   sp.flush();
@@ -4510,8 +4514,8 @@ template <bool kTgs, int kOcc>
 __global__ __launch_bounds__(WGT, kOcc) void zb_m_step_kernel(
     const zb_model* __restrict__ mg, const float4* __restrict__ links, zb_task_cfg cfg, int N, float* __restrict__ st,
     const float* __restrict__ act, float* __restrict__ obs, float* __restrict__ rew, uint8_t* __restrict__ term,
-    uint8_t* __restrict__ trunc, float* __restrict__ acc, const Counters* __restrict__ cnt, uint64_t seed,
-    float* __restrict__ wc) {
+    uint8_t* __restrict__ trunc, int64_t* __restrict__ done, float* __restrict__ acc,
+    const Counters* __restrict__ cnt, uint64_t seed, float* __restrict__ wc) {
   MP m = to_mp(mg);
   __shared__ float4 lds[LDS4];
   if (kOcc == 1) asm volatile("" ::: "a255");  // (zb_step_kernel: kOcc)
@@ -4839,7 +4843,7 @@ __global__ __launch_bounds__(WGT, kOcc) void zb_m_step_kernel(
     q.stg(ZB_M_LINK_MU + ZB_M_OBS_DIM + 1) = terminated ? 1.f : 0.f;
     q.stg(ZB_M_LINK_MU + ZB_M_OBS_DIM + 2) = time_out ? 1.f : 0.f;
   }
-  staged_store<ZB_M_LINK_MU, ZB_M_OBS_DIM>(q, xcd_block(blockIdx.x, gridDim.x) * EPW, N, st, obs, rew, term, trunc);
+  staged_store<ZB_M_LINK_MU, ZB_M_OBS_DIM>(q, xcd_block(blockIdx.x, gridDim.x) * EPW, N, st, obs, rew, term, trunc, done);
 #undef OUT
   sp.mark(8);
   sp.flush();
@@ -5142,6 +5146,7 @@ struct zb_sim {
   float* u_log_means = nullptr;     // optional caller buffers (zb_set_log_buffers)
   int32_t* u_log_counts = nullptr;
   float* u_log_acc = nullptr;       // optional caller accumulator (zb_set_log_accumulator)
+  int64_t* u_done = nullptr;        // optional caller done buffer (zb_set_done_buffer)
   // ZB_DIAG_NO_FINALIZE=1 (diagnostic only, wrong results: no episode log, no full-reset draw, no
   // step counter): zb_step skips the finalize launch, to measure what that launch and its kernel
   // boundary cost per step
@@ -5564,16 +5569,16 @@ int zb_step(zb_handle h, const float* actions, float* obs, float* reward, uint8_
                 : ZB_LAUNCH(K, __VA_ARGS__))
   if (h->task == ZB_TASK_STANDUP_V0)
     ZB_LAUNCH_R(zb_su_step_kernel, h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward, terminated,
-              truncated, h->d_acc, h->d_cnt, h->seed, h->d_wc);
+              truncated, h->u_done, h->d_acc, h->d_cnt, h->seed, h->d_wc);
   else if (h->task == ZB_TASK_WALKING_V4)
     ZB_LAUNCH(zb_v4_step_kernel, h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward, terminated,
-              truncated, h->d_acc, h->d_cnt, h->seed, h->d_wc);
+              truncated, h->u_done, h->d_acc, h->d_cnt, h->seed, h->d_wc);
   else if (h->task == ZB_TASK_MANAGER_V0)
     ZB_LAUNCH(zb_m_step_kernel, h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward, terminated,
-              truncated, h->d_acc, h->d_cnt, h->seed, h->d_wc);
+              truncated, h->u_done, h->d_acc, h->d_cnt, h->seed, h->d_wc);
   else
     ZB_LAUNCH_R(zb_step_kernel, h->d_model, h->d_links, h->cfg, h->n, h->d_state, actions, obs, reward, terminated,
-              truncated, h->d_acc, h->d_wc);
+              truncated, h->u_done, h->d_acc, h->d_wc);
 #undef ZB_LAUNCH_R
 #undef ZB_LAUNCH
   int rc = launch_check("zb_step_kernel");
@@ -5642,6 +5647,12 @@ int zb_set_log_buffers(zb_handle h, float* term_means, int32_t* counts) {
   if (!h || (!term_means) != (!counts)) return set_err(-1, "zb_set_log_buffers", hipSuccess);
   h->u_log_means = term_means;
   h->u_log_counts = counts;
+  return 0;
+}
+
+int zb_set_done_buffer(zb_handle h, int64_t* dones) {
+  if (!h) return set_err(-1, "zb_set_done_buffer", hipSuccess);
+  h->u_done = dones;
   return 0;
 }
 

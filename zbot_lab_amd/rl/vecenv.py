@@ -30,6 +30,10 @@ class RslRlVecEnvWrapper:
         self.max_episode_length = env.unwrapped.max_episode_length
         self.num_actions = env.unwrapped.single_action_space.shape[0]
         self.cfg = env.unwrapped.cfg
+        # the native sim writes terminated | truncated as int64 into a registered buffer inside its step
+        # kernel (zb_set_done_buffer), so step() returns that instead of two torch launches per step
+        sim = getattr(env.unwrapped, "sim", None)
+        self._dones = sim.done_buffer() if hasattr(sim, "done_buffer") else None
         self.env.reset()
 
     @property
@@ -58,7 +62,7 @@ class RslRlVecEnvWrapper:
         if self.clip_actions is not None:
             actions = torch.clamp(actions, -self.clip_actions, self.clip_actions)
         obs, rew, terminated, truncated, extras = self.env.step(actions)
-        dones = (terminated | truncated).to(dtype=torch.long)
+        dones = self._dones if self._dones is not None else (terminated | truncated).to(dtype=torch.long)
         extras["time_outs"] = truncated
         return _as_obs(obs, self.num_envs), rew, dones, extras
 

@@ -114,6 +114,15 @@ class ZbotSim:
         """The int32[ZB_LOG_COUNTS] termination-count buffer."""
         return self._log_counts
 
+    def done_buffer(self) -> torch.Tensor:
+        """A persistent int64 [N] tensor that every later step fills with terminated | truncated from the step
+        kernel's own flag stores (zb_set_done_buffer): rsl_rl's dones without the wrapper's two torch
+        launches per step. Registered on first use; the same tensor afterwards."""
+        if getattr(self, "_dones", None) is None:
+            self._dones = torch.zeros(self.num_envs, dtype=torch.long, device=self.device)
+            nat.check(self.lib.zb_set_done_buffer(self._h, nat.ptr(self._dones)), "zb_set_done_buffer")
+        return self._dones
+
     def set_log_accumulator(self, acc: torch.Tensor | None) -> None:
         """Register a device float[ZB_LOG_LEN + ZB_LOG_COUNTS] accumulator that every later step adds the
         log's current values to inside its finalize launch (zb_set_log_accumulator; the PPO runner's
