@@ -15,6 +15,7 @@
 #   tests            pytest -m gpu on $TESTS
 #   budget           tools/error_budget.py (device vs f32 oracle error against f64, per part of a substep)
 #   nofin            bench lines with and without the finalize launch (ZB_DIAG_NO_FINALIZE, diagnostic)
+#   train            60 walking-v2 training iterations, no profiler (the fps column)
 #   train_v2 / train_c5   rocprof kernel traces of short training runs
 #   rehearsal        two ranks of bench.py sharing cuda:0 over gloo (plumbing, not scaling)
 set -u
@@ -81,6 +82,9 @@ for s in "$@"; do
       run tests 900 $PT ${TESTS:?TESTS=<pytest paths>} -m gpu ;;
     budget)
       for lib in ${LIBS:-libzbot.so}; do run error_budget_${lib%.so} 300 env ZBOT_LIB=$lib python tools/error_budget.py 2048; done ;;
+    train)  # plain (no profiler) walking-v2 training throughput, 60 iterations
+      run train 400 python scripts/train.py --task zbot-6b-walking-v2 --num_envs 4096 --max_iterations 60 \
+        --log_root $O/train_logs ;;
     train_v2)
       run train_v2 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/train_v2 -o run -- \
         python3 scripts/train.py --task zbot-6b-walking-v2 --num_envs 4096 --max_iterations 30 \

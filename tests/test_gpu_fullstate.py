@@ -232,6 +232,12 @@ def _row_names(task):
 # implementations of one algorithm, each against the f64 one):
 # frac <= AGG_FRAC_K x baseline + AGG_FRAC_ABS and median <= AGG_MED_K x baseline + AGG_MED_ABS.
 AGG_FRAC_K, AGG_FRAC_ABS = 2.0, 0.005
+# multi-step checks (20 steps of standing contact): the contact solve's per-substep rounding excess
+# over the f32 oracle (1.35-1.67x, tools/error_budget.py) compounds, and the outlier fraction then
+# moves with code generation alone: PGS v2 1.76-2.73 %, v4 1.66-2.25 % over six builds of one source
+# (f32 oracle 1.07 / 0.68 %). 3x keeps >= 11 % headroom on every build measured;
+# the one-step checks, where the device's factor is 0.7-1.3x, stay at 2x.
+AGG_FRAC_K_MULTI = 3.0
 # at most this many envs still unexplained after the 32-run refinement get a deep draw of
 # REFINE_DEEP_RUNS rounding-scale runs (a quarter of that for multi-step checks); more fail at once
 REFINE_DEEP_MAX, REFINE_DEEP_RUNS = 4, 1024
@@ -334,7 +340,8 @@ def _check(task, label, n, seed, st, actions, g_out, sg, torch, wc=None, stats=N
     if stats is not None:
         stats["deep_draw"] = ndeep
     assert not unexplained, f"{task}: {len(unexplained)} envs outside tolerance where the oracle is stable: {unexplained[:20]}"
-    assert frac <= AGG_FRAC_K * frac_o + AGG_FRAC_ABS, \
+    k_frac = AGG_FRAC_K if nsteps == 1 else AGG_FRAC_K_MULTI
+    assert frac <= k_frac * frac_o + AGG_FRAC_ABS, \
         f"{task}: contact-active outlier fraction {frac:.3%} vs the f32 oracle's {frac_o:.3%} (both against f64)"
     assert med <= AGG_MED_K * med_o + AGG_MED_ABS, \
         f"{task}: contact-active median err/tol {med:.3g} vs the f32 oracle's {med_o:.3g} (both against f64)"
