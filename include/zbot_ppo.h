@@ -87,7 +87,11 @@ int zbp_minibatch(const zbp_net* actor, const zbp_net* critic, const float* std_
  * over the params listed in `params` (the torch optimizer's param order): n_params tensors with
  * numel / param / grad / exp_avg / exp_avg_sq pointers. lr and step are device scalars (torch's
  * capturable Adam keeps `step` as a float tensor; one shared step counter is read from step[0] and
- * every tensor's own counter written). Then re-packs the workspace (zbp_pack). acc[3] += stats[1..3]. */
+ * every tensor's own counter written). Then re-packs the workspace (zbp_pack). acc[3] += stats[1..3].
+ * norm_from_minibatch != 0: the gradient norm comes from the per-tile sums of squares the last
+ * zbp_minibatch on this workspace left (one launch fewer); only valid when the .grad buffers and
+ * std_grad are still exactly what that call wrote (one GPU, no all-reduce or hook in between);
+ * 0: recomputed from params->grad. */
 #define ZBP_MAX_PARAMS 24
 typedef struct {
   int32_t n_params;
@@ -100,7 +104,8 @@ typedef struct {
 } zbp_params;
 int zbp_optimizer_step(const zbp_params* params, float* lr, const float* stats, float* acc, float desired_kl,
                        float max_grad_norm, float beta1, float beta2, float eps, const zbp_net* actor,
-                       const zbp_net* critic, float* ws, int32_t batch, void* stream);
+                       const zbp_net* critic, float* ws, int32_t batch, int32_t norm_from_minibatch,
+                       void* stream);
 
 /* GAE (RolloutStorage.compute_returns): rewards / dones / values [steps][envs] (time-out bootstrap
  * already in the rewards), last_values [envs] -> returns, advantages = returns - values, then (if

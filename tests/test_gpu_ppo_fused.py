@@ -149,6 +149,36 @@ def test_fused_update_matches_torch_update(gpu, monkeypatch):
         assert float(opt_f.state[pf_]["step"]) == float(opt_t.state[pt_]["step"]) == 20.0
 
 
+@pytest.mark.parametrize("hidden", [[128, 128, 128], [256, 256, 128]], ids=["v2-nets", "standup-nets"])
+def test_optimizer_norm_from_minibatch(gpu, hidden, monkeypatch):
+    """zbp_optimizer_step's gradient norm from k_reduce's per-tile sums of squares (the one-GPU path)
+    against k_norm's recomputation from .grad, with clipping active: the same parameters, rate and
+    step up to the two norms' summation order."""
+    import torch
+    monkeypatch.setenv("ZBOT_PPO_FUSED", "1")
+    a0 = _alg(hidden, seed=7)
+    a1 = copy.deepcopy(a0)
+    res = []
+    for alg, nfm in ((a0, True), (a1, False)):
+        alg.max_grad_norm = 0.05  # well below the gradients' norm: the clip coefficient scales every step
+        f = alg.fused_update()
+        assert f is not None
+        f.pack()
+        sums = torch.zeros_like(alg.update_sums)
+        for i in range(3):
+            f.minibatch(alg.storage, alg.mb_indices, i * f.batch)
+            f.optimizer_step(sums, grads_from_minibatch=nfm)
+        assert f._norm_ok
+        torch.cuda.synchronize()
+        res.append((torch.cat([p.detach().flatten() for p in alg.policy.parameters()]), float(alg.lr_t),
+                    [float(alg.optimizer.state[p]["step"]) for p in alg.policy.parameters()], sums.clone()))
+    (p0, lr0, st0, s0), (p1, lr1, st1, s1) = res
+    assert st0 == st1 and set(st0) == {3.0}
+    assert lr0 == lr1
+    torch.testing.assert_close(p0, p1, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(s0, s1, rtol=1e-5, atol=1e-7)
+
+
 def test_fused_gae_matches_torch(gpu, monkeypatch):
     """RolloutStorage.compute_returns on zbp_gae (three launches) against the torch recursion:
     returns, advantages and their normalisation."""

@@ -17,8 +17,8 @@
 //                resident workgroups; partial tiles to the workspace
 //   k_reduce     partial tiles -> every parameter's .grad, the std gradient, the minibatch stats
 //
-// and, on one GPU, k_norm / k_adam / k_optim_tail (adaptive learning rate, global-norm clipping,
-// Adam) + the re-pack; the rollout's policy step (k_act_reg / k_act), its bookkeeping (k_env_post) and
+// and, on one GPU, k_adam (adaptive learning rate, global-norm clipping from k_reduce's per-tile sums
+// of squares, or k_norm's, Adam) + the re-pack (k_pack, which also writes the new rate and step); the rollout's policy step (k_act_reg / k_act), its bookkeeping (k_env_post) and
 // GAE (k_gae, k_adv_stats, k_adv_norm). Exact fp32 throughout (the MFMA is a k-ordered fmaf chain);
 // results differ from torch's only by summation order. MI355X mapping: the weights (<= 450 KB per
 // net) stay L2-resident; design and measurements in DESIGN.md §7 (round 5).
@@ -76,7 +76,7 @@ struct Layout {
   int wtiles, tile0[2 * MAXL + 1];  // weight tiles of (net, layer) in order, prefix counts
   int ngroups, grp0[2 * MAXL + 1];  // k_wgrad workgroups (<= 4 x 4 output x reduction tiles) of (net, layer), prefix counts
   int splits;
-  int64_t scratch;  // [64] per-block gradient sums of squares (zbp_optimizer_step)
+  int64_t scratch;  // [max(64, wtiles + 1)] gradient sums of squares: k_norm's per block, or k_reduce's per weight tile
   int64_t total;
 };
 
@@ -144,7 +144,7 @@ Layout make_layout(const zbp_net* a, const zbp_net* c, int B) {
   s = s < 1 ? 1 : (s > C ? C : (s > 1024 ? 1024 : s));
   lo.splits = s;
   lo.part = take((int64_t)s * t * PART);
-  lo.scratch = take(64);
+  lo.scratch = take(t + 1 > 64 ? t + 1 : 64);
   lo.total = off;
   return lo;
 }
@@ -203,8 +203,32 @@ struct PackArgs {
   const float* w[2][MAXL];
   const float* b[2][MAXL];
   float* ws;
+  // zbp_optimizer_step's tail (tail != 0; one thread): the new learning rate and step counter, which
+  // every k_adam workgroup read as the old ones (so written after that launch), and the loss sums
+  int tail, n_params;
+  float* lr;
+  const float* stats;
+  float* acc;
+  float desired_kl;
+  float* step[ZBP_MAX_PARAMS];
 };
+__device__ __forceinline__ float adaptive_lr(float lr, float kl, float desired_kl) {
+  // rsl_rl's adaptive schedule on the minibatch KL
+  if (desired_kl > 0.f) {
+    if (kl > desired_kl * 2.f) lr = fmaxf(lr / 1.5f, 1e-5f);
+    else if (kl > 0.f && kl < desired_kl / 2.f) lr = fminf(lr * 1.5f, 1e-2f);
+  }
+  return lr;
+}
 __global__ void k_pack(PackArgs A) {
+  if (A.tail && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x == 0) {
+    *A.lr = adaptive_lr(*A.lr, A.stats[0], A.desired_kl);
+    const float step = A.step[0][0] + 1.f;
+    for (int t = 0; t < A.n_params; ++t) A.step[t][0] = step;
+    A.acc[0] += A.stats[1];
+    A.acc[1] += A.stats[2];
+    A.acc[2] += A.stats[3];
+  }
   const int net = blockIdx.y, l = blockIdx.z;
   const NetW& w = A.n[net];
   if (l >= w.L) return;
@@ -922,9 +946,11 @@ struct ReduceArgs {
   float entropy_coef;
   const float* ws;
   int64_t part, rstats;
+  float* norm2;  // [wtiles + 1]: each tile's sum of squared gradients (the last: the std's), for zbp_optimizer_step
 };
 // one workgroup per weight tile: the split partials summed in order into .grad (weights of the tile,
-// and the bias for k0 = 0); the last workgroup: the scalars
+// and the bias for k0 = 0) and the tile's sum of their squares (fixed order); the last workgroup: the
+// scalars
 __global__ __launch_bounds__(256) void k_reduce(ReduceArgs A) {
   if (blockIdx.x == (unsigned)A.wtiles) {
     // per-row-tile sums -> stats, the std gradient (+ the entropy bonus term): thread t sums row
@@ -972,7 +998,13 @@ __global__ __launch_bounds__(256) void k_reduce(ReduceArgs A) {
       A.stats[1] = tot[1] * invB;  // value loss
       A.stats[2] = tot[0] * invB;  // surrogate loss
       A.stats[3] = ent;            // entropy (every row's)
-      for (int a = 0; a < A.num_actions; ++a) A.std_grad[a] = tot[3 + a] - A.entropy_coef / A.std_param[a];
+      float ss = 0.f;
+      for (int a = 0; a < A.num_actions; ++a) {
+        const float g = tot[3 + a] - A.entropy_coef / A.std_param[a];
+        A.std_grad[a] = g;
+        ss += g * g;
+      }
+      A.norm2[A.wtiles] = ss;
     }
     return;
   }
@@ -984,6 +1016,7 @@ __global__ __launch_bounds__(256) void k_reduce(ReduceArgs A) {
   const int t = tile - A.tile0[nl], kt = w.p[l] / 32;
   const int n0 = 32 * (t / kt), k0 = 32 * (t % kt);
   const int D0 = w.d[l], D1 = w.d[l + 1];
+  float ss = 0.f;
   for (int e = threadIdx.x; e < PART; e += blockDim.x) {
     // (eight partial sums: eight split partials in flight per thread; a fixed order)
     float sv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -995,12 +1028,17 @@ __global__ __launch_bounds__(256) void k_reduce(ReduceArgs A) {
     const float s = ((sv[0] + sv[1]) + (sv[2] + sv[3])) + ((sv[4] + sv[5]) + (sv[6] + sv[7]));
     if (e < 1024) {
       const int n = n0 + e / 32, k = k0 + e % 32;
-      if (n < D1 && k < D0) A.gw[net][l][(int64_t)n * D0 + k] = s;
+      if (n < D1 && k < D0) { A.gw[net][l][(int64_t)n * D0 + k] = s; ss += s * s; }
     } else if (k0 == 0) {
       const int n = n0 + e - 1024;
-      if (n < D1) A.gb[net][l][n] = s;
+      if (n < D1) { A.gb[net][l][n] = s; ss += s * s; }
     }
   }
+  __shared__ float red[4];
+  ss = wave_sum(ss);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+  __syncthreads();
+  if (threadIdx.x == 0) A.norm2[tile] = (red[0] + red[1]) + (red[2] + red[3]);  // fixed order
 }
 
 // ------------------------------------------------------------------------------- k_optim
@@ -1010,7 +1048,8 @@ struct OptimArgs {
   const float* stats;
   float* acc;
   float desired_kl, max_norm, b1, b2, eps;
-  float* norm2;  // workspace scratch: [64] per-block sums of squares (k_norm), summed in order by k_adam
+  float* norm2;  // workspace scratch: nparts sums of squares (k_norm's per block or k_reduce's per tile), summed in order by k_adam
+  int nparts;
   int64_t total;  // elements over all the tensors
 };
 // flat element g over the tensors in order -> (tensor t, element e): every thread's elements are
@@ -1038,14 +1077,9 @@ __global__ __launch_bounds__(256) void k_norm(OptimArgs A) {
 }
 __global__ __launch_bounds__(256) void k_adam(OptimArgs A) {
   // learning rate rule (rsl_rl adaptive schedule, on the minibatch KL), clip coefficient, Adam
-  const float kl = A.stats[0];
-  float lr = *A.lr;
-  if (A.desired_kl > 0.f) {
-    if (kl > A.desired_kl * 2.f) lr = fmaxf(lr / 1.5f, 1e-5f);
-    else if (kl > 0.f && kl < A.desired_kl / 2.f) lr = fminf(lr * 1.5f, 1e-2f);
-  }
+  const float lr = adaptive_lr(*A.lr, A.stats[0], A.desired_kl);
   float n2 = 0.f;
-  for (int b = 0; b < 64; ++b) n2 += A.norm2[b];
+  for (int b = 0; b < A.nparts; ++b) n2 += A.norm2[b];
   const float total = sqrtf(n2);
   const float coef = fminf(A.max_norm / (total + 1e-6f), 1.f);
   const float step = A.P.step[0][0] + 1.f;
@@ -1063,22 +1097,7 @@ __global__ __launch_bounds__(256) void k_adam(OptimArgs A) {
     A.P.exp_avg_sq[t][e] = v;
     A.P.param[t][e] -= step_size * m / (sqrtf(v) / bc2s + A.eps);
   }
-  // (every block reads the old lr / step: k_optim_tail writes the new ones after this launch)
-}
-__global__ void k_optim_tail(OptimArgs A) {
-  if (threadIdx.x != 0) return;
-  const float kl = A.stats[0];
-  float lr = *A.lr;
-  if (A.desired_kl > 0.f) {
-    if (kl > A.desired_kl * 2.f) lr = fmaxf(lr / 1.5f, 1e-5f);
-    else if (kl > 0.f && kl < A.desired_kl / 2.f) lr = fminf(lr * 1.5f, 1e-2f);
-  }
-  *A.lr = lr;
-  const float step = A.P.step[0][0] + 1.f;
-  for (int t = 0; t < A.P.n_params; ++t) A.P.step[t][0] = step;
-  A.acc[0] += A.stats[1];
-  A.acc[1] += A.stats[2];
-  A.acc[2] += A.stats[3];
+  // (every block reads the old lr / step: the k_pack launch after this one writes the new ones)
 }
 
 // ------------------------------------------------------------------------------- rollout
@@ -1458,9 +1477,20 @@ PackArgs pack_args(const Layout& lo, const zbp_net* a, const zbp_net* c, float* 
   P.ws = ws;
   return P;
 }
-int do_pack(const Layout& lo, const zbp_net* a, const zbp_net* c, float* ws, hipStream_t s) {
+int do_pack(const Layout& lo, const zbp_net* a, const zbp_net* c, float* ws, hipStream_t s,
+            const PackArgs* tail = nullptr) {
   const int L = lo.n[0].L > lo.n[1].L ? lo.n[0].L : lo.n[1].L;
-  k_pack<<<dim3(64, 2, L), 256, 0, s>>>(pack_args(lo, a, c, ws));
+  PackArgs P = pack_args(lo, a, c, ws);
+  if (tail) {
+    P.tail = 1;
+    P.n_params = tail->n_params;
+    P.lr = tail->lr;
+    P.stats = tail->stats;
+    P.acc = tail->acc;
+    P.desired_kl = tail->desired_kl;
+    for (int t = 0; t < tail->n_params; ++t) P.step[t] = tail->step[t];
+  }
+  k_pack<<<dim3(64, 2, L), 256, 0, s>>>(P);
   return launch_check("k_pack");
 }
 
@@ -1577,13 +1607,14 @@ int zbp_minibatch(const zbp_net* actor, const zbp_net* critic, const float* std_
   D.ws = ws;
   D.part = lo.part;
   D.rstats = lo.stats;
+  D.norm2 = ws + lo.scratch;
   k_reduce<<<lo.wtiles + 1, 256, 0, s>>>(D);
   return launch_check("k_reduce");
 }
 
 int zbp_optimizer_step(const zbp_params* params, float* lr, const float* stats, float* acc, float desired_kl,
                        float max_grad_norm, float beta1, float beta2, float eps, const zbp_net* actor,
-                       const zbp_net* critic, float* ws, int32_t batch, void* stream) {
+                       const zbp_net* critic, float* ws, int32_t batch, int32_t norm_from_minibatch, void* stream) {
   if (!params || params->n_params < 1 || params->n_params > ZBP_MAX_PARAMS || !lr || !stats || !acc || !ws)
     return fail(-1, "zbp_optimizer_step: bad argument");
   if (const char* e = check_net(actor)) return fail(-1, e);
@@ -1603,13 +1634,23 @@ int zbp_optimizer_step(const zbp_params* params, float* lr, const float* stats, 
   O.norm2 = ws + lo.scratch;
   O.total = 0;
   for (int t = 0; t < params->n_params; ++t) O.total += params->numel[t];
-  k_norm<<<64, 256, 0, s>>>(O);
-  if (int rc = launch_check("k_norm")) return rc;
+  if (norm_from_minibatch) {
+    O.nparts = lo.wtiles + 1;  // k_reduce's per-tile sums of the gradients it wrote
+  } else {
+    O.nparts = 64;
+    k_norm<<<64, 256, 0, s>>>(O);
+    if (int rc = launch_check("k_norm")) return rc;
+  }
   k_adam<<<256, 256, 0, s>>>(O);
   if (int rc = launch_check("k_adam")) return rc;
-  k_optim_tail<<<1, 64, 0, s>>>(O);
-  if (int rc = launch_check("k_optim_tail")) return rc;
-  return do_pack(lo, actor, critic, ws, s);
+  PackArgs T{};
+  T.n_params = params->n_params;
+  T.lr = lr;
+  T.stats = stats;
+  T.acc = acc;
+  T.desired_kl = desired_kl;
+  for (int t = 0; t < params->n_params; ++t) T.step[t] = params->step[t];
+  return do_pack(lo, actor, critic, ws, s, &T);
 }
 
 int zbp_act(const zbp_net* actor, const zbp_net* critic, const float* std_param, const zbp_act_io* io, float* ws,

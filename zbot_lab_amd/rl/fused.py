@@ -93,7 +93,7 @@ def lib():
     L.zbp_pack.argtypes = [C.POINTER(Net), C.POINTER(Net), P, C.c_int32, P]
     L.zbp_minibatch.argtypes = [C.POINTER(Net), C.POINTER(Net), P, P, C.POINTER(Batch), C.POINTER(LossCfg), P, P, P]
     L.zbp_optimizer_step.argtypes = [C.POINTER(Params), P, P, P, C.c_float, C.c_float, C.c_float, C.c_float,
-                                     C.c_float, C.POINTER(Net), C.POINTER(Net), P, C.c_int32, P]
+                                     C.c_float, C.POINTER(Net), C.POINTER(Net), P, C.c_int32, C.c_int32, P]
     L.zbp_gae.argtypes = [P, P, P, P, P, P, C.c_int32, C.c_int32, C.c_float, C.c_float, C.c_int32, P, P]
     L.zbp_act.argtypes = [C.POINTER(Net), C.POINTER(Net), P, C.POINTER(ActIO), P, C.c_int32, P]
     L.zbp_env_post.argtypes = [P, P, P, P, C.c_float, P, P, P, P, P, C.c_int32, P]
@@ -253,18 +253,30 @@ class FusedUpdate:
         self._steps = [opt.state[p]["step"] for p in ps]  # (keep the tensors alive)
         return P
 
-    def optimizer_step(self, acc: torch.Tensor) -> None:
+    def _grads_all_from_minibatch(self) -> bool:
+        """The optimizer's parameters are exactly what zbp_minibatch writes gradients for (both nets'
+        weights and biases, the std): then the norm can come from its per-tile sums."""
+        ps = [p for g in self.alg.optimizer.param_groups for p in g["params"]]
+        want = sum(n.dim[l] * n.dim[l + 1] + n.dim[l + 1] for n in (self.na, self.nc) for l in range(n.n_layers))
+        return sum(p.numel() for p in ps) == want + int(self.na.dim[self.na.n_layers])
+
+    def optimizer_step(self, acc: torch.Tensor, grads_from_minibatch: bool = False) -> None:
         """Adaptive learning rate (on the minibatch KL), global-norm clipping and Adam on one GPU,
-        then the re-pack; acc[0:3] += value loss, surrogate, entropy."""
+        then the re-pack; acc[0:3] += value loss, surrogate, entropy. grads_from_minibatch: the .grad
+        buffers are untouched since the last minibatch() (one GPU), so the gradient norm is taken from
+        that call's per-tile sums of squares instead of a launch of its own."""
         alg = self.alg
         g = alg.optimizer.param_groups[0]
         b1, b2 = g["betas"]
         dk = alg.desired_kl if (alg.desired_kl is not None and alg.schedule == "adaptive") else 0.0
         if not hasattr(self, "_params"):
             self._params = self._adam_state()
+            self._norm_ok = self._grads_all_from_minibatch()
+        nfm = 1 if (grads_from_minibatch and self._norm_ok) else 0
         _check(lib().zbp_optimizer_step(C.byref(self._params), _p(alg.lr_t), _p(self.stats), _p(acc), float(dk),
                                         float(alg.max_grad_norm), float(b1), float(b2), float(g["eps"]),
-                                        C.byref(self.na), C.byref(self.nc), _p(self.ws), self.batch, self._stream()),
+                                        C.byref(self.na), C.byref(self.nc), _p(self.ws), self.batch, nfm,
+                                        self._stream()),
                "zbp_optimizer_step")
 
     # -- rollout (runner._rollout's policy step and post-step bookkeeping, one launch each)

@@ -433,7 +433,7 @@ class PPO:
             for _ in range(self.num_learning_epochs):
                 for i in range(self.num_mini_batches):
                     f.minibatch(self.storage, self.mb_indices, i * mb)
-                    f.optimizer_step(sums)
+                    f.optimizer_step(sums, grads_from_minibatch=True)
         self.storage.clear()
 
     def _grad_params(self) -> list:
