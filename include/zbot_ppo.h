@@ -116,7 +116,10 @@ int zbp_gae(const float* rewards, const float* dones, const float* values, const
 
 /* One rollout step of PPO.act (rsl_rl ActorCritic.act / evaluate / get_actions_log_prob and the
  * transition fields of RolloutStorage.add; zbot_lab_amd/rl/ppo.py) for `rows` envs in one launch:
- * actions = mu + std * noise (noise: the caller's standard-normal draw, [rows][num_actions]), its
+ * actions = mu + std * noise (noise: the caller's standard-normal draw, [rows][num_actions], or NULL:
+ * drawn in the kernel, a counter-based standard normal keyed by noise_seed, the workspace's draw
+ * counter -- which every zbp_pack / zbp_optimizer_step advances --, noise_step, the row and the
+ * action), its
  * Gaussian log-probability summed over the actions, the critic's value; writes actions [rows][na]
  * (the env's input) and the storage slot of this step: observations, critic observations, actions,
  * values, log-probabilities, mu, sigma. Reads the workspace's weight images (zbp_pack must follow
@@ -125,7 +128,7 @@ int zbp_gae(const float* rewards, const float* dones, const float* values, const
 typedef struct {
   const float* obs;         /* [rows][obs_dim] */
   const float* critic_obs;  /* [rows][critic_obs_dim] */
-  const float* noise;       /* [rows][num_actions] */
+  const float* noise;       /* [rows][num_actions], or NULL (in-kernel draw) */
   float* actions;           /* [rows][num_actions] out */
   float* st_obs;            /* storage slot [rows][obs_dim] out */
   float* st_critic_obs;     /* [rows][critic_obs_dim] out */
@@ -135,6 +138,8 @@ typedef struct {
   float* st_mu;             /* [rows][num_actions] out */
   float* st_sigma;          /* [rows][num_actions] out */
   int32_t rows, obs_dim, critic_obs_dim, num_actions;
+  int32_t noise_step;       /* (noise == NULL) the rollout step: distinct draws per step of a rollout */
+  int32_t noise_seed;       /* (noise == NULL) the caller's stream, e.g. one per rank */
 } zbp_act_io;
 int zbp_act(const zbp_net* actor, const zbp_net* critic, const float* std_param, const zbp_act_io* io, float* ws,
             int32_t batch, void* stream);

@@ -255,6 +255,47 @@ def test_fused_act_matches_torch_policy(gpu, hidden, rows, monkeypatch):
         assert torch.equal(st.observations[3], obs) and torch.equal(st.critic_observations[3], obs)
 
 
+def test_fused_act_kernel_noise(gpu):
+    """zbp_act with the in-kernel draw (io->noise NULL, the runner's default): the noise implied by the
+    actions, (a - mu) / sigma, is standard normal (moments, tails, no correlation across actions),
+    differs between rollout steps and after a re-pack, and repeats for the same counter and step; the
+    log-probability and the storage slot are those of the actions drawn."""
+    import torch
+    from zbot_lab_amd.rl import fused
+    envs = 16384
+    alg = _alg([128, 128, 128], envs=envs)
+    fu = fused.FusedUpdate(alg, 256)
+    st = alg.storage
+    st.clear()
+    obs = torch.randn(envs, 23, device="cuda:0")
+    fu.pack()
+    draws = {}
+    for key, k, repack in (("a", 3, False), ("b", 4, False), ("c", 3, True)):
+        if repack:
+            fu.pack()
+        st.step = k
+        a = fu.act(obs, obs, st, kernel_noise=True).clone()
+        draws[key] = ((a - st.mu[k]) / st.sigma[k], a, k)
+    torch.cuda.synchronize()
+    z = draws["a"][0]
+    n = z.numel()
+    assert abs(float(z.mean())) < 5.0 / n ** 0.5
+    assert abs(float(z.std()) - 1.0) < 0.02
+    assert abs(float((z.abs() > 1.96).float().mean()) - 0.05) < 0.005
+    c = torch.corrcoef(z.T)
+    assert float((c - torch.eye(c.shape[0], device=c.device)).abs().max()) < 0.05
+    for other in ("b", "c"):
+        r = torch.corrcoef(torch.stack([z.flatten(), draws[other][0].flatten()]))[0, 1]
+        assert abs(float(r)) < 0.05, other
+    # the log-probability stored is the drawn actions' under (mu, sigma)
+    pol = alg.policy
+    with torch.no_grad():
+        pol.update_distribution(obs)
+        ref_lp = pol.get_actions_log_prob(draws["c"][1])
+    assert (st.actions_log_prob[3].view(-1) - ref_lp).abs().max() <= 1e-4 * max(1.0, float(ref_lp.abs().max()))
+    assert torch.equal(st.actions[3], draws["c"][1])
+
+
 def test_fused_env_post_matches_torch(gpu):
     """zbp_env_post against PPO.process_env_step + the runner's episode bookkeeping: storage reward
     with the time-out bootstrap and done exactly, cur_rew / cur_len exactly, ep_stats to fp32

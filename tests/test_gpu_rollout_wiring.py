@@ -43,6 +43,7 @@ def test_fused_rollout_matches_torch_rollout(gpu, tmp_path, monkeypatch):
     obs0 = (obs0["policy"] if isinstance(obs0, dict) else obs0).clone()
     cur0 = (torch.randn(4096, device="cuda:0"), torch.randint(0, 50, (4096,), device="cuda:0").float())
     rec = {}
+    monkeypatch.setenv("ZBOT_KERNEL_NOISE", "0")  # (torch's draw on both paths: same noise, same rollout)
     for mode in ("1", "0"):
         monkeypatch.setenv("ZBOT_ROLLOUT_FUSED", mode)
         sim.set_state(s0)

@@ -72,11 +72,15 @@ struct NetW {
 struct Layout {
   NetW n[2];
   int64_t stats;  // [tiles][NSTAT] per-row-tile partial sums
-  int64_t part;   // [splits][wtiles][PART] weight-gradient partials
+  int64_t part;   // [splits (the largest)][wtiles][PART] weight-gradient partials
   int wtiles, tile0[2 * MAXL + 1];  // weight tiles of (net, layer) in order, prefix counts
   int ngroups, grp0[2 * MAXL + 1];  // k_wgrad workgroups (<= 4 x 4 output x reduction tiles) of (net, layer), prefix counts
-  int splits;
+  int splits;                       // the largest row split count
+  int sp_nl[2 * MAXL];              // row splits of (net, layer) (one count for all, see make_layout)
+  int ord[2 * MAXL];                // k_wgrad launch order of the (net, layer)s
+  int blk0[2 * MAXL + 1];           // k_wgrad launch: first workgroup of the (net, layer) at order position i
   int64_t scratch;  // [max(64, wtiles + 1)] gradient sums of squares: k_norm's per block, or k_reduce's per weight tile
+  int64_t rng;      // [1] uint32: the draw counter of the in-kernel action noise, advanced by every k_pack
   int64_t total;
 };
 
@@ -138,13 +142,32 @@ Layout make_layout(const zbp_net* a, const zbp_net* c, int B) {
   lo.stats = take((int64_t)(B / 16) * NSTAT);  // (per 32-row tile of k_rows, per 16-row wave of k_rows_reg)
   // row splits of the weight gradients: as many as fill the device's resident k_wgrad workgroups in
   // ONE round (groups x splits <= slots; a second, partly filled round would leave most CUs idle for
-  // a whole split's time); a split is a contiguous range of 32-row chunks (k_wgrad's LDS chunks)
+  // a whole split's time); a split is a contiguous range of 32-row chunks (k_wgrad's LDS chunks). The
+  // same count for every layer: a chunk costs about the same in every group (its copy and barrier
+  // latency, not the MFMAs, set the pace: splits weighted by the groups' MFMA work made the launch
+  // 66 -> 87 us)
   const int C = B / 32;
   int s = wgrad_slots() / g;
   s = s < 1 ? 1 : (s > C ? C : (s > 1024 ? 1024 : s));
+  // launch order: the layers whose blocks keep all four waves' MFMAs busy (2 x 2 tiles per wave)
+  // first, then the input / output layers (half the MFMAs per wave): with the launch filling every CU's
+  // first slot before its second, a CU then pairs a busy block with a light one instead of two busy ones
+  int b = 0, pos = 0;
+  for (int pass = 0; pass < 2; ++pass)
+    for (int nl = 0; nl < 2 * MAXL; ++nl) {
+      const int k = nl / MAXL, l = nl % MAXL;
+      const bool busy = l < lo.n[k].L && lo.n[k].p[l + 1] >= 64 && lo.n[k].p[l] >= 64;
+      if ((pass == 0) != busy) continue;
+      lo.ord[pos] = nl;
+      lo.blk0[pos++] = b;
+      lo.sp_nl[nl] = s;
+      b += (lo.grp0[nl + 1] - lo.grp0[nl]) * s;
+    }
+  lo.blk0[2 * MAXL] = b;
   lo.splits = s;
   lo.part = take((int64_t)s * t * PART);
   lo.scratch = take(t + 1 > 64 ? t + 1 : 64);
+  lo.rng = take(1);
   lo.total = off;
   return lo;
 }
@@ -211,6 +234,7 @@ struct PackArgs {
   float* acc;
   float desired_kl;
   float* step[ZBP_MAX_PARAMS];
+  uint32_t* rng;  // the workspace's noise draw counter: +1 per launch (one thread)
 };
 __device__ __forceinline__ float adaptive_lr(float lr, float kl, float desired_kl) {
   // rsl_rl's adaptive schedule on the minibatch KL
@@ -221,6 +245,7 @@ __device__ __forceinline__ float adaptive_lr(float lr, float kl, float desired_k
   return lr;
 }
 __global__ void k_pack(PackArgs A) {
+  if (blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x == 0) *A.rng += 1u;
   if (A.tail && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x == 0) {
     *A.lr = adaptive_lr(*A.lr, A.stats[0], A.desired_kl);
     const float step = A.step[0][0] + 1.f;
@@ -808,7 +833,7 @@ __global__ __launch_bounds__(RR_WG, rr_occ<T1>()) void k_rows_reg(RowArgs A) {
 // ------------------------------------------------------------------------------- k_wgrad
 struct WgradArgs {
   NetW n[2];
-  int tile0[2 * MAXL + 1], grp0[2 * MAXL + 1];
+  int tile0[2 * MAXL + 1], grp0[2 * MAXL + 1], blk0[2 * MAXL + 1], sp_nl[2 * MAXL], ord[2 * MAXL];
   int wtiles, ngroups, splits, batch;
   float* ws;
   int64_t part;
@@ -827,9 +852,12 @@ constexpr int WG_CHUNK_F = 2 * 4 * 128 * 8;  // floats of one chunk buffer (dZ +
 __global__ __launch_bounds__(256, 2) void k_wgrad(WgradArgs A) {
   __shared__ float4 lds4[2 * WG_CHUNK_F / 4];
   float* lds = reinterpret_cast<float*>(lds4);
-  const int grp = blockIdx.x % A.ngroups, split = blockIdx.x / A.ngroups;
-  int nl = 0;
-  while (nl + 1 < 2 * MAXL && A.grp0[nl + 1] <= grp) ++nl;
+  // workgroup -> (net, layer) by the launch prefix, then (group, split) inside it, groups interleaved
+  int pos = 0;
+  while (pos + 1 < 2 * MAXL && A.blk0[pos + 1] <= (int)blockIdx.x) ++pos;
+  const int nl = A.ord[pos];
+  const int ng = A.grp0[nl + 1] - A.grp0[nl], local = (int)blockIdx.x - A.blk0[pos];
+  const int grp = A.grp0[nl] + local % ng, split = local / ng, nsplit = A.sp_nl[nl];
   const NetW& w = A.n[nl / MAXL];
   const int l = nl % MAXL;
   const int P0 = w.p[l], P1 = w.p[l + 1], Tk = P0 / 32, Tn = P1 / 32, KG = (Tk + 3) / 4;
@@ -837,7 +865,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(WgradArgs A) {
   const int g = grp - A.grp0[nl], nt0 = 4 * (g / KG), kt0 = 4 * (g % KG);
   const int nb = min(4, Tn - nt0), kb = min(4, Tk - kt0);  // tiles of the block
   const int C = A.batch / 32;  // the split's chunks [c0, c1)
-  const int c0 = (int)((int64_t)split * C / A.splits), c1 = (int)((int64_t)(split + 1) * C / A.splits);
+  const int c0 = (int)((int64_t)split * C / nsplit), c1 = (int)((int64_t)(split + 1) * C / nsplit);
   const int r0 = 32 * c0, nch = c1 - c0;
   // chunk copy: per octet, dZ features n0 .. n0 + 32 nb - 1 and X features k0 .. k0 + 32 kb - 1 (8 rows each)
   const int fn = 32 * nb * 8 / 4, fk = 32 * kb * 8 / 4;  // float4s per octet
@@ -938,6 +966,7 @@ struct ReduceArgs {
   NetW n[2];
   int tile0[2 * MAXL + 1];
   int wtiles, splits, row_tiles, batch, num_actions;
+  int sp_nl[2 * MAXL];
   float* gw[2][MAXL];
   float* gb[2][MAXL];
   const float* std_param;
@@ -950,19 +979,21 @@ struct ReduceArgs {
 };
 // one workgroup per weight tile: the split partials summed in order into .grad (weights of the tile,
 // and the bias for k0 = 0) and the tile's sum of their squares (fixed order); the last workgroup: the
-// scalars
-__global__ __launch_bounds__(256) void k_reduce(ReduceArgs A) {
+// scalars. 1024 threads: a thread sums one partial element over the splits with 16 loads in flight
+// (with 256 threads and 8 in flight the launch waited on ~30 dependent rounds of partial loads)
+constexpr int RED_THREADS = 1024;
+__global__ __launch_bounds__(RED_THREADS) void k_reduce(ReduceArgs A) {
   if (blockIdx.x == (unsigned)A.wtiles) {
-    // per-row-tile sums -> stats, the std gradient (+ the entropy bonus term): thread t sums row
+    // per-row-tile sums -> stats, the std gradient (+ the entropy bonus term): thread t < 256 sums row
     // tiles t, t + 256, ... (one row = 16 floats = four float4, two rows in flight), then a fixed-order
-    // tree over the block (deterministic)
+    // tree over those 256 (deterministic); the other threads only take part in the barriers
     __shared__ float red[256][NSTAT + 1];
     const int t = threadIdx.x;
     float sv[NSTAT];
 #pragma unroll
     for (int q = 0; q < NSTAT; ++q) sv[q] = 0.f;
     const float4* rs = reinterpret_cast<const float4*>(A.ws + A.rstats);
-    int rt = t;
+    int rt = t < 256 ? t : A.row_tiles;
     for (; rt + 256 < A.row_tiles; rt += 512) {
       float4 v[8];
 #pragma unroll
@@ -979,8 +1010,9 @@ __global__ __launch_bounds__(256) void k_reduce(ReduceArgs A) {
         const float4 v = rs[(int64_t)rt * 4 + c];
         sv[4 * c] += v.x; sv[4 * c + 1] += v.y; sv[4 * c + 2] += v.z; sv[4 * c + 3] += v.w;
       }
+    if (t < 256)
 #pragma unroll
-    for (int q = 0; q < NSTAT; ++q) red[t][q] = sv[q];
+      for (int q = 0; q < NSTAT; ++q) red[t][q] = sv[q];
     __syncthreads();
     for (int st = 128; st > 0; st >>= 1) {
       if (t < st)
@@ -1018,14 +1050,22 @@ __global__ __launch_bounds__(256) void k_reduce(ReduceArgs A) {
   const int D0 = w.d[l], D1 = w.d[l + 1];
   float ss = 0.f;
   for (int e = threadIdx.x; e < PART; e += blockDim.x) {
-    // (eight partial sums: eight split partials in flight per thread; a fixed order)
-    float sv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    int sp = 0;
-    for (; sp + 8 <= A.splits; sp += 8)
+    // (sixteen partial sums: sixteen split partials in flight per thread; a fixed order)
+    float sv[16];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) sv[u] += A.ws[A.part + ((int64_t)(sp + u) * A.wtiles + tile) * PART + e];
-    for (; sp < A.splits; ++sp) sv[0] += A.ws[A.part + ((int64_t)sp * A.wtiles + tile) * PART + e];
-    const float s = ((sv[0] + sv[1]) + (sv[2] + sv[3])) + ((sv[4] + sv[5]) + (sv[6] + sv[7]));
+    for (int u = 0; u < 16; ++u) sv[u] = 0.f;
+    int sp = 0;
+    const float* src = A.ws + A.part + (int64_t)tile * PART + e;
+    const int64_t stride = (int64_t)A.wtiles * PART;
+    const int nsp = A.sp_nl[nl];  // (this tile's layer's splits)
+    for (; sp + 16 <= nsp; sp += 16)
+#pragma unroll
+      for (int u = 0; u < 16; ++u) sv[u] += src[(int64_t)(sp + u) * stride];
+    for (; sp < nsp; ++sp) sv[0] += src[(int64_t)sp * stride];
+    float s8[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s8[u] = sv[u] + sv[u + 8];
+    const float s = ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
     if (e < 1024) {
       const int n = n0 + e / 32, k = k0 + e % 32;
       if (n < D1 && k < D0) { A.gw[net][l][(int64_t)n * D0 + k] = s; ss += s * s; }
@@ -1034,11 +1074,15 @@ __global__ __launch_bounds__(256) void k_reduce(ReduceArgs A) {
       if (n < D1) { A.gb[net][l][n] = s; ss += s * s; }
     }
   }
-  __shared__ float red[4];
+  __shared__ float red[RED_THREADS / 64];
   ss = wave_sum(ss);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
   __syncthreads();
-  if (threadIdx.x == 0) A.norm2[tile] = (red[0] + red[1]) + (red[2] + red[3]);  // fixed order
+  if (threadIdx.x == 0) {
+    float v = 0.f;
+    for (int k = 0; k < RED_THREADS / 64; ++k) v += red[k];  // fixed order
+    A.norm2[tile] = v;
+  }
 }
 
 // ------------------------------------------------------------------------------- k_optim
@@ -1078,9 +1122,17 @@ __global__ __launch_bounds__(256) void k_norm(OptimArgs A) {
 __global__ __launch_bounds__(256) void k_adam(OptimArgs A) {
   // learning rate rule (rsl_rl adaptive schedule, on the minibatch KL), clip coefficient, Adam
   const float lr = adaptive_lr(*A.lr, A.stats[0], A.desired_kl);
-  float n2 = 0.f;
-  for (int b = 0; b < A.nparts; ++b) n2 += A.norm2[b];
-  const float total = sqrtf(n2);
+  // the global norm^2 from the partial sums: the first wave loads them lane-parallel and sums with a
+  // butterfly (the same fixed order in every block), then shares it through LDS
+  __shared__ float n2s;
+  if (threadIdx.x < 64) {
+    float v = 0.f;
+    for (int b = threadIdx.x; b < A.nparts; b += 64) v += A.norm2[b];
+    v = wave_sum(v);
+    if (threadIdx.x == 0) n2s = v;
+  }
+  __syncthreads();
+  const float total = sqrtf(n2s);
   const float coef = fminf(A.max_norm / (total + 1e-6f), 1.f);
   const float step = A.P.step[0][0] + 1.f;
   const float bc1 = 1.f - powf(A.b1, step), bc2s = sqrtf(1.f - powf(A.b2, step));
@@ -1114,11 +1166,34 @@ struct ActArgs {
   const float* std_param;
   const float* obs;
   const float* cobs;
-  const float* noise;
+  const float* noise;   // the caller's draw, or nullptr: noise_at draws it
+  const uint32_t* rng;  // (noise == nullptr) the workspace's draw counter
+  int noise_step;
+  uint32_t noise_seed;
   int obs_dim, cobs_dim, na, rows;
   float *actions, *s_obs, *s_cobs, *s_act, *s_val, *s_lp, *s_mu, *s_sig;
   int lds_x[MAXL], lds_out;
 };
+// The in-kernel action noise (zbp_act with io->noise == NULL): a standard normal per (row, action)
+// from a counter-based draw -- splitmix64 of (the caller's seed, e.g. per rank; the workspace's draw
+// counter, which every k_pack advances, so every rollout and every update; the rollout step; row;
+// action), Box-Muller on its
+// 24-bit halves. The same distribution as torch.randn, another stream; no launch of its own.
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+__device__ __forceinline__ float noise_at(const ActArgs& A, int row, int n) {
+  if (A.noise) return A.noise[row * A.na + n];
+  const uint64_t key = ((uint64_t)A.noise_seed << 32) ^ ((uint64_t)*A.rng << 12) ^ (uint64_t)(uint32_t)A.noise_step;
+  const uint64_t h = mix64(mix64(key) ^ (uint64_t)((int64_t)row * A.na + n));
+  const float u1 = ((float)(uint32_t)(h >> 40) + 1.f) * 5.9604644775390625e-8f;  // (0, 1]
+  const float u2 = (float)(uint32_t)((h >> 16) & 0xFFFFFFu) * 5.9604644775390625e-8f;  // [0, 1)
+  return sqrtf(-2.f * logf(u1)) * cosf(6.28318530717958647692f * u2);
+}
+
 __device__ void act_gather(const NetW& w, const float* src, int dim, float* st, int rows, float* lds, int lds_x0,
                            int row0) {
   const int P0 = w.p[0];
@@ -1142,7 +1217,7 @@ __global__ __launch_bounds__(256) void k_act(ActArgs A) {
     float lp = 0.f;
     for (int a = 0; a < A.na; ++a) {
       const float mu = lds[A.lds_out + tid * 33 + a], s = A.std_param[a];
-      const float x = mu + s * A.noise[row * A.na + a], diff = x - mu;
+      const float x = mu + s * noise_at(A, row, a), diff = x - mu;
       lp += -(diff * diff) / (2.f * (s * s)) - logf(s) - kLog2Pi;
       A.actions[row * A.na + a] = x;
       A.s_act[row * A.na + a] = x;
@@ -1205,7 +1280,7 @@ __global__ __launch_bounds__(RR_WG, 2) void k_act_reg(ActArgs A) {
         const int n = 16 * (j >> 2) + 4 * gq + (j & 3);
         if (ok && n < na) {
           const float mu = z[j >> 2][j & 3], s = A.std_param[n];
-          const float x = mu + s * A.noise[row * na + n], diff = x - mu;
+          const float x = mu + s * noise_at(A, row, n), diff = x - mu;
           lp += -(diff * diff) / (2.f * (s * s)) - logf(s) - kLog2Pi;
           A.actions[row * na + n] = x;
           A.s_act[row * na + n] = x;
@@ -1323,7 +1398,7 @@ __global__ __launch_bounds__(256, 2) void k_act_split(ActArgs A) {
       const int n = 4 * gq + u;
       if (ok && n < na) {
         const float mu = z[u], s = A.std_param[n];
-        const float x = mu + s * A.noise[row * na + n], diff = x - mu;
+        const float x = mu + s * noise_at(A, row, n), diff = x - mu;
         lp += -(diff * diff) / (2.f * (s * s)) - logf(s) - kLog2Pi;
         A.actions[row * na + n] = x;
         A.s_act[row * na + n] = x;
@@ -1475,6 +1550,7 @@ PackArgs pack_args(const Layout& lo, const zbp_net* a, const zbp_net* c, float* 
   for (int k = 0; k < 2; ++k)
     for (int l = 0; l < nets[k]->n_layers; ++l) { P.w[k][l] = nets[k]->w[l]; P.b[k][l] = nets[k]->b[l]; }
   P.ws = ws;
+  P.rng = reinterpret_cast<uint32_t*>(ws + lo.rng);
   return P;
 }
 int do_pack(const Layout& lo, const zbp_net* a, const zbp_net* c, float* ws, hipStream_t s,
@@ -1575,13 +1651,16 @@ int zbp_minibatch(const zbp_net* actor, const zbp_net* critic, const float* std_
   W.n[1] = lo.n[1];
   for (int i = 0; i <= 2 * MAXL; ++i) W.tile0[i] = lo.tile0[i];
   for (int i = 0; i <= 2 * MAXL; ++i) W.grp0[i] = lo.grp0[i];
+  for (int i = 0; i <= 2 * MAXL; ++i) W.blk0[i] = lo.blk0[i];
+  for (int i = 0; i < 2 * MAXL; ++i) W.sp_nl[i] = lo.sp_nl[i];
+  for (int i = 0; i < 2 * MAXL; ++i) W.ord[i] = lo.ord[i];
   W.wtiles = lo.wtiles;
   W.ngroups = lo.ngroups;
   W.splits = lo.splits;
   W.batch = B;
   W.ws = ws;
   W.part = lo.part;
-  k_wgrad<<<lo.ngroups * lo.splits, 256, 0, s>>>(W);
+  k_wgrad<<<lo.blk0[2 * MAXL], 256, 0, s>>>(W);
   if (int rc = launch_check("k_wgrad")) return rc;
 
   ReduceArgs D{};
@@ -1590,6 +1669,7 @@ int zbp_minibatch(const zbp_net* actor, const zbp_net* critic, const float* std_
   for (int i = 0; i <= 2 * MAXL; ++i) D.tile0[i] = lo.tile0[i];
   D.wtiles = lo.wtiles;
   D.splits = lo.splits;
+  for (int i = 0; i < 2 * MAXL; ++i) D.sp_nl[i] = lo.sp_nl[i];
   D.row_tiles = shape ? B / RR_TR : B / TR;
   D.batch = B;
   D.num_actions = batch->num_actions;
@@ -1608,7 +1688,7 @@ int zbp_minibatch(const zbp_net* actor, const zbp_net* critic, const float* std_
   D.part = lo.part;
   D.rstats = lo.stats;
   D.norm2 = ws + lo.scratch;
-  k_reduce<<<lo.wtiles + 1, 256, 0, s>>>(D);
+  k_reduce<<<lo.wtiles + 1, RED_THREADS, 0, s>>>(D);
   return launch_check("k_reduce");
 }
 
@@ -1657,7 +1737,7 @@ int zbp_act(const zbp_net* actor, const zbp_net* critic, const float* std_param,
             int32_t batch, void* stream) {
   if (const char* e = check_net(actor)) return fail(-1, e);
   if (const char* e = check_net(critic)) return fail(-1, e);
-  if (!io || !ws || !std_param || !io->obs || !io->critic_obs || !io->noise || !io->actions || !io->st_obs ||
+  if (!io || !ws || !std_param || !io->obs || !io->critic_obs || !io->actions || !io->st_obs ||
       !io->st_critic_obs || !io->st_actions || !io->st_values || !io->st_log_prob || !io->st_mu || !io->st_sigma)
     return fail(-1, "zbp_act: null argument");
   if (io->rows < 1 || batch < TR || batch % TR) return fail(-1, "zbp_act: rows / batch");
@@ -1673,6 +1753,9 @@ int zbp_act(const zbp_net* actor, const zbp_net* critic, const float* std_param,
   A.obs = io->obs;
   A.cobs = io->critic_obs;
   A.noise = io->noise;
+  A.rng = reinterpret_cast<const uint32_t*>(ws + lo.rng);
+  A.noise_step = io->noise_step;
+  A.noise_seed = (uint32_t)io->noise_seed;
   A.obs_dim = io->obs_dim;
   A.cobs_dim = io->critic_obs_dim;
   A.na = io->num_actions;

@@ -47,7 +47,8 @@ class ActIO(C.Structure):
     _fields_ = [("obs", C.c_void_p), ("critic_obs", C.c_void_p), ("noise", C.c_void_p), ("actions", C.c_void_p),
                 ("st_obs", C.c_void_p), ("st_critic_obs", C.c_void_p), ("st_actions", C.c_void_p),
                 ("st_values", C.c_void_p), ("st_log_prob", C.c_void_p), ("st_mu", C.c_void_p), ("st_sigma", C.c_void_p),
-                ("rows", C.c_int32), ("obs_dim", C.c_int32), ("critic_obs_dim", C.c_int32), ("num_actions", C.c_int32)]
+                ("rows", C.c_int32), ("obs_dim", C.c_int32), ("critic_obs_dim", C.c_int32), ("num_actions", C.c_int32),
+                ("noise_step", C.c_int32), ("noise_seed", C.c_int32)]
 
 
 class Params(C.Structure):
@@ -280,11 +281,13 @@ class FusedUpdate:
                "zbp_optimizer_step")
 
     # -- rollout (runner._rollout's policy step and post-step bookkeeping, one launch each)
-    def act(self, obs: torch.Tensor, critic_obs: torch.Tensor, storage) -> torch.Tensor:
+    def act(self, obs: torch.Tensor, critic_obs: torch.Tensor, storage, kernel_noise: bool = False) -> torch.Tensor:
         """PPO.act on zbp_act: the actions (a static buffer) and the transition fields written
         straight into the storage slot ``storage.step``; the noise is torch.randn_like's draw, as in
-        the torch path. The weight images are re-packed at a rollout's first step (parameters may
-        have changed outside zbp_optimizer_step: a torch optimizer, a checkpoint load)."""
+        the torch path, or with ``kernel_noise`` the kernel's own counter-based standard normal (no
+        torch launch; another stream of the same distribution). The weight images are re-packed at a
+        rollout's first step (parameters may have changed outside zbp_optimizer_step: a torch
+        optimizer, a checkpoint load)."""
         k = storage.step
         if k >= storage.num_transitions_per_env:
             raise OverflowError("rollout buffer overflow")
@@ -294,11 +297,16 @@ class FusedUpdate:
         if getattr(self, "_act_out", None) is None or self._act_out.shape != (n, na):
             self._act_out = torch.zeros(n, na, device=obs.device)
             self._noise = torch.zeros(n, na, device=obs.device)
-        torch.randn(n, na, out=self._noise, device=obs.device)
+        if not kernel_noise:
+            torch.randn(n, na, out=self._noise, device=obs.device)
         obs, critic_obs = obs.contiguous(), critic_obs.contiguous()
         io = ActIO()
-        io.obs, io.critic_obs, io.noise, io.actions = obs.data_ptr(), critic_obs.data_ptr(), self._noise.data_ptr(), \
-            self._act_out.data_ptr()
+        io.obs, io.critic_obs, io.actions = obs.data_ptr(), critic_obs.data_ptr(), self._act_out.data_ptr()
+        io.noise = None if kernel_noise else self._noise.data_ptr()
+        io.noise_step = k
+        if getattr(self, "_noise_seed", None) is None:  # from torch's generator: per-rank seeds carry over
+            self._noise_seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
+        io.noise_seed = self._noise_seed
         io.st_obs, io.st_critic_obs = storage.observations[k].data_ptr(), storage.critic_observations[k].data_ptr()
         io.st_actions, io.st_values = storage.actions[k].data_ptr(), storage.values[k].data_ptr()
         io.st_log_prob, io.st_mu = storage.actions_log_prob[k].data_ptr(), storage.mu[k].data_ptr()

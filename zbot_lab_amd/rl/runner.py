@@ -195,8 +195,10 @@ class OnPolicyRunner:
         fr = self.alg.fused_rollout()
         if fr is not None:
             st = self.alg.storage
+            # the action noise drawn inside zbp_act (ZBOT_KERNEL_NOISE=0: torch.randn, as the torch path)
+            kn = os.environ.get("ZBOT_KERNEL_NOISE", "1") != "0"
             for _ in range(self.num_steps_per_env):
-                actions = fr.act(obs, obs, st)
+                actions = fr.act(obs, obs, st, kernel_noise=kn)
                 obs_d, rewards, dones, extras = env.step(actions.to(env.device))
                 obs = _policy_obs(obs_d).to(self.device)
                 tout = extras.get("time_outs") if isinstance(extras, dict) else None
