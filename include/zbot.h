@@ -429,6 +429,9 @@ int zb_read_curriculum(zb_handle h, int32_t* stage, int64_t* common_step_counter
  * the launch stream right around the kernel (bench.py's roofline figure). zb_profile_end waits
  * for the last event and returns the summed kernel time. */
 int zb_profile_begin(zb_handle h, int max_launches);
+/* Time only every stride-th zb_step launch from now on (default 1): the event-recording dispatch
+ * adds ~5.7 us to the step it brackets (bench.py samples every 8th timed step). */
+int zb_profile_stride(zb_handle h, int stride);
 int zb_profile_end(zb_handle h, float* total_ms, int* count);
 
 /* Diagnostic builds only (compiled with -DZB_STAMPS): per-phase s_memtime cycle sums of

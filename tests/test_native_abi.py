@@ -71,7 +71,7 @@ def test_oracle_exports_mirror():
     from oracle import pyoracle
     L = pyoracle.lib()
     for s in header_symbols():
-        if s in ("zb_last_error", "zb_num_envs", "zb_profile_begin", "zb_profile_end", "zb_create", "zb_destroy",
+        if s in ("zb_last_error", "zb_num_envs", "zb_profile_begin", "zb_profile_end", "zb_profile_stride", "zb_create", "zb_destroy",
                  "zb_read_stamps", "zb_read_stamps_slowest", "zb_read_stamp_hist", "zb_read_wave_times",
                  "zb_set_log_buffers", "zb_set_log_accumulator", "zb_set_done_buffer"):
             continue

@@ -50,6 +50,7 @@ def lib():
     L.zb_set_contact_cache.argtypes = [P, P, P]
     L.zb_physics_substeps.argtypes = [P, P, C.c_int, P, P, P]
     L.zb_profile_begin.argtypes = [P, C.c_int]
+    L.zb_profile_stride.argtypes = [P, C.c_int]
     L.zb_profile_end.argtypes = [P, C.POINTER(C.c_float), C.POINTER(C.c_int)]
     L.zb_read_stamps.argtypes = [P]
     L.zb_read_stamps.restype = C.c_int
@@ -68,7 +69,7 @@ def lib():
     L.zb_pair_manifold_mode.argtypes = [P, C.c_int, C.c_float, C.c_int, P, P]
     for name in ("zb_create", "zb_num_envs", "zb_reset", "zb_step", "zb_observe", "zb_read_log", "zb_set_log_buffers", "zb_set_log_accumulator", "zb_set_done_buffer",
                  "zb_get_state", "zb_set_state", "zb_get_contact_cache", "zb_set_contact_cache", "zb_physics_substeps",
-                 "zb_profile_begin", "zb_profile_end",
+                 "zb_profile_begin", "zb_profile_end", "zb_profile_stride",
                  "zb_state_dim", "zb_set_link_friction", "zb_set_link_friction_sd", "zb_read_curriculum", "zb_gjk_pairs", "zb_pair_manifold", "zb_pair_manifold_mode"):
         getattr(L, name).restype = C.c_int
     _lib = L
@@ -77,7 +78,7 @@ def lib():
 
 EXPORTED = ["zb_create", "zb_destroy", "zb_last_error", "zb_num_envs", "zb_reset", "zb_step", "zb_observe",
             "zb_read_log", "zb_set_log_buffers", "zb_set_log_accumulator", "zb_set_done_buffer", "zb_get_state", "zb_set_state", "zb_get_contact_cache",
-            "zb_set_contact_cache", "zb_physics_substeps", "zb_profile_begin",
+            "zb_set_contact_cache", "zb_physics_substeps", "zb_profile_begin", "zb_profile_stride",
             "zb_profile_end", "zb_read_stamps", "zb_read_stamps_slowest", "zb_read_stamp_hist", "zb_read_wave_times", "zb_state_dim", "zb_set_link_friction", "zb_set_link_friction_sd",
             "zb_read_curriculum", "zb_gjk_pairs", "zb_pair_manifold", "zb_pair_manifold_mode"]
 

@@ -176,7 +176,10 @@ class ZbotSim:
         nat.check(self.lib.zb_set_contact_cache(self._h, nat.ptr(w), _stream(self.device)), "zb_set_contact_cache")
         torch.cuda.current_stream(self.device).synchronize()
 
-    def profile_begin(self, max_launches: int) -> None:
+    def profile_begin(self, max_launches: int, stride: int = 1) -> None:
+        """Time the next zb_step_kernel launches with HIP events: every ``stride``-th one, at most
+        ``max_launches`` of them (the event dispatch adds ~5.7 us to a step it brackets)."""
+        nat.check(self.lib.zb_profile_stride(self._h, int(stride)), "zb_profile_stride")
         nat.check(self.lib.zb_profile_begin(self._h, int(max_launches)), "zb_profile_begin")
 
     def profile_end(self):
