@@ -2060,10 +2060,11 @@ __device__ __forceinline__ float4 pgs_update(const float4 g, const float4 a0, co
   // of the substep's sweeps and slides with |l| = mu_d ln (mu_d = mu: the plain projection
   // min(1, mu ln / |l|)); an unloaded contact's friction is 0 without breaking it
   const float ri = __builtin_amdgcn_rsqf(fmaxf(fmaf(l1, l1, l2 * l2), 1e-30f));
-  const bool over = mu * ln * ri < 1.f;
-  const bool brk = lam.w != 0.f || (over && ln > 0.f);
-  const float lim = brk ? mu_d * ln * ri : (over ? mu * ln * ri : 1.f);
-  const float sc = fminf(lim, 1.f);
+  const float ts = mu * ln * ri, td = mu_d * ln * ri;  // the static / dynamic cone over |l|
+  const bool over = ts < 1.f;
+  const bool brk = (lam.w != 0.f) | (over & (ln > 0.f));  // (bitwise: no short-circuit branch)
+  // (one select, no branch: unbroken, min(ts, 1) is ts inside the static cone and 1 outside it)
+  const float sc = fminf(brk ? td : ts, 1.f);
   l1 *= sc;
   l2 *= sc;
   const float d1 = l1 - lam.y, d2 = l2 - lam.z;
