@@ -1,8 +1,8 @@
 """HIP kernel (libzbot.so, through the C ABI) vs the CPU oracle on identical seeded states.
 
 Bar: fp32 on both sides, different operation order / FMA contraction / libm, so
-  * one substep from identical states: joint/root velocities within 2e-3 abs + 1e-3 rel,
-    positions within 1e-5 (they move by dt * velocity);
+  * one substep from identical states: joint/root velocities within 2e-3 abs + 1e-3 rel of the f32
+    oracle or of the f64 oracle, positions within 1e-5 (they move by dt * velocity);
   * one policy step (4 substeps + MDP): observations / rewards within the tolerances below for
     >= 99 % of envs, done flags identical for >= 99 % (contact activation at the speculative
     margin is a discontinuity: a 1-ulp difference can flip one contact); integer / counter state
@@ -86,9 +86,21 @@ def test_one_substep_parity(gpu, airborne):
     shallow = probe.self_min_sep() > -2 * 0.004 + 1e-4
     assert 0.80 <= shallow.mean() <= 0.86, shallow.mean()  # the state generator's observed mix
     vel = slice(S["ROOT_LINVEL"], S["JOINT_VEL"] + 6)
+    # within tolerance of the f32 oracle, or of the f64 oracle where the f32 one is itself off: a
+    # contact-switching state moves the f32 oracle's own result by up to 4e-2 against exact
+    # arithmetic (round 6: of the envs outside tolerance of the f32 oracle, most are within 6e-4 of
+    # the f64 oracle -- the f32 oracle is the outlier there)
+    o64 = OracleSim(n, double=True)
+    o64.set_state(st)
+    o64.physics_substeps(tg, 1)
+    s64 = o64.get_state()
     dv = np.abs(sg[vel] - so[vel]) - (2e-3 + 1e-3 * np.abs(so[vel]))
-    ok = (dv <= 0).all(axis=0)[shallow]
-    assert ok.mean() >= 0.99, f"velocity parity in {ok.mean():.4f} of envs; worst {dv[:, shallow].max():.3e}"
+    dv64 = np.abs(sg[vel] - s64[vel]) - (2e-3 + 1e-3 * np.abs(s64[vel]))
+    ok32 = (dv <= 0).all(axis=0)[shallow]
+    ok = ok32 | (dv64 <= 0).all(axis=0)[shallow]
+    print(f"\nvelocity parity: {int((~ok32).sum())} of {ok32.size} envs outside tolerance of the f32 oracle, "
+          f"{int((~ok).sum())} of them also of the f64 oracle")
+    assert ok.mean() >= 0.99, f"velocity parity in {ok.mean():.4f} of envs; worst {np.minimum(dv, dv64)[:, shallow].max():.3e}"
     pos = np.r_[S["ROOT_POS"]:S["ROOT_POS"] + 7, S["JOINT_POS"]:S["JOINT_POS"] + 6]
     dp = np.abs(sg[pos] - so[pos])
     okp = (dp <= 2e-5 + 1e-5 * np.abs(so[pos])).all(axis=0)[shallow]

@@ -744,8 +744,7 @@ __device__ __forceinline__ float wc_extract(const Q& q) {
   bool self = q.s < NCM && f.w >= 1.f && (((int)f.w) & 15) != 0;  // ground codes: 16 l
   // one entry per pair: a face manifold's points share the pair's normal (= oracle wc_store)
 #pragma unroll
-  for (int c = 0; c < NCM - 1; ++c)
-    if (c < q.s && q.frc(c).w == f.w) self = false;
+  for (int c = 0; c < NCM - 1; ++c) self = self & !((c < q.s) & (q.frc(c).w == f.w));  // (bitwise: no branches)
   const unsigned M = (unsigned)(__ballot(self) >> (TL * q.e)) & 0xffffu;
   const int r = q.s >> 2;
   float v = wc_invalid(q.s);
@@ -786,15 +785,16 @@ __device__ __forceinline__ void fk_scan_step(float qv[4], float tv[3], int lane_
   for (int a = 0; a < 4; ++a) qs[a] = dppf<DPP_SHR + D>(qv[a]);
 #pragma unroll
   for (int a = 0; a < 3; ++a) ts[a] = dppf<DPP_SHR + D>(tv[a]);
-  if (lane_b >= D) {
-    float qn[4], rt[3];
-    qmul(qs, qv, qn);
-    qrot(qs, tv, rt);
+  // every lane composes, the lanes below D keep theirs (selects: a divergent branch here cost more
+  // in exec-mask instructions than the selects)
+  float qn[4], rt[3];
+  qmul(qs, qv, qn);
+  qrot(qs, tv, rt);
+  const bool on = lane_b >= D;
 #pragma unroll
-    for (int a = 0; a < 4; ++a) qv[a] = qn[a];
+  for (int a = 0; a < 4; ++a) qv[a] = on ? qn[a] : qv[a];
 #pragma unroll
-    for (int a = 0; a < 3; ++a) tv[a] = ts[a] + rt[a];
-  }
+  for (int a = 0; a < 3; ++a) tv[a] = on ? ts[a] + rt[a] : tv[a];
 }
 
 template <bool kInertia>
@@ -1215,7 +1215,7 @@ __device__ __forceinline__ bool gjk_quad(const QCircle& h, int j, const float v0
 #pragma unroll
       for (int k = 0; k < 3; ++k) p[k] = aw[k] + t * e2[k];
       const float d2 = dot3(p, p);
-      const bool ok = j < n && g11 > 1e-20f && t > 0.f && t < 1.f && d2 < best;
+      const bool ok = (j < n) & (g11 > 1e-20f) & (t > 0.f) & (t < 1.f) & (d2 < best);  // (bitwise: no branches)
       best = ok ? d2 : best;
       bm = ok ? (1u << j) : bm;
       l1 = ok ? t : l1;
@@ -1232,8 +1232,8 @@ __device__ __forceinline__ bool gjk_quad(const QCircle& h, int j, const float v0
 #pragma unroll
       for (int k = 0; k < 3; ++k) p[k] = aw[k] + ts * e1[k] + tt * e2[k];
       const float d2 = dot3(p, p);
-      const bool valid = j == 1 ? n >= 2 : (j >= 2 && n >= 3);
-      const bool ok = valid && det > 1e-24f * g00 * g11 && ts > 0.f && tt > 0.f && ts + tt < 1.f && d2 < best;
+      const bool valid = j == 1 ? n >= 2 : ((j >= 2) & (n >= 3));
+      const bool ok = valid & (det > 1e-24f * g00 * g11) & (ts > 0.f) & (tt > 0.f) & (ts + tt < 1.f) & (d2 < best);
       best = ok ? d2 : best;
       bm = ok ? (j == 1 ? 3u : (j == 2 ? 5u : 6u)) : bm;
       l1 = ok ? ts : l1;
@@ -1263,7 +1263,7 @@ __device__ __forceinline__ bool gjk_quad(const QCircle& h, int j, const float v0
         cross3(e2, e0, x20);
         cross3(e0, e1, x01);
         const float b0 = dot3(m0, x12) * id, b1 = dot3(m0, x20) * id, b2 = dot3(m0, x01) * id;
-        if (b0 > 1e-5f && b1 > 1e-5f && b2 > 1e-5f && b0 + b1 + b2 < 1.f - 1e-5f) { overlap = true; break; }
+        if ((b0 > 1e-5f) & (b1 > 1e-5f) & (b2 > 1e-5f) & (b0 + b1 + b2 < 1.f - 1e-5f)) { overlap = true; break; }
       }
     }
     // new simplex: a first, then the used points in index order
@@ -2148,7 +2148,9 @@ __device__ __forceinline__ void team_fwd(const float R[NV], const float inv[NV],
 // pushed out at baumgarte * depth per substep, capped at max_depenetration_velocity
 // (zbot_cfg.py:633). Same as the oracle's contact_bias.
 __device__ __forceinline__ float contact_bias(const zb_task_cfg& cfg, MP m, float sep, float h, float dt) {
-  return sep >= 0.f ? -sep / h : fminf(cfg.baumgarte * (-sep) / dt, m->max_depenetration_velocity);
+  // (both sides evaluated and selected: no divergent branch in the TGS sub-iterations)
+  const float spec = -sep / h, push = fminf(cfg.baumgarte * (-sep) / dt, m->max_depenetration_velocity);
+  return sep >= 0.f ? spec : push;
 }
 // joint speed clamp (actuator velocity_limit) and root link angular speed limit (rigid props
 // max_angular_velocity; PhysX scales the vector)
@@ -2431,10 +2433,24 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
       const float i0 = tb<0>(ic[4]), i1 = tb<0>(ic[5]), i2 = tb<0>(ic[6]);
       const float i3 = tb<0>(ic[7]), i4 = tb<0>(ic[8]), i5 = tb<0>(ic[9]);
       const int r = q.s - 6;
-      float B[6];  // lower triangle of root row r (entries past the diagonal unused)
-      B[0] = r == 0 ? i0 : r == 1 ? i3 : r == 2 ? i4 : r == 3 ? 0.f : r == 4 ? -hz : hy;
-      B[1] = r == 1 ? i1 : r == 2 ? i5 : r == 3 ? hz : r == 4 ? 0.f : -hx;
-      B[2] = r == 2 ? i2 : r == 3 ? -hy : r == 4 ? hx : 0.f;
+      // lower triangle of root row r (entries past the diagonal unused). One select per statement:
+      // written as nested ?: chains, clang emitted branches that SimplifyCFG folded into a
+      // compare-and-branch tree on r with out-of-line blocks (~100 scalar instructions per substep)
+      float B[6];
+      B[0] = hy;
+      B[0] = r == 4 ? -hz : B[0];
+      B[0] = r == 3 ? 0.f : B[0];
+      B[0] = r == 2 ? i4 : B[0];
+      B[0] = r == 1 ? i3 : B[0];
+      B[0] = r == 0 ? i0 : B[0];
+      B[1] = -hx;
+      B[1] = r == 4 ? 0.f : B[1];
+      B[1] = r == 3 ? hz : B[1];
+      B[1] = r == 2 ? i5 : B[1];
+      B[1] = r == 1 ? i1 : B[1];
+      B[2] = r == 4 ? hx : 0.f;
+      B[2] = r == 3 ? -hy : B[2];
+      B[2] = r == 2 ? i2 : B[2];
       B[3] = r == 3 ? m0t : 0.f;
       B[4] = r == 4 ? m0t : 0.f;
       B[5] = r == 5 ? m0t : 0.f;
@@ -2629,13 +2645,12 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
   // Sweeps outer, the NCM slots unrolled inner: constant LDS offsets, slot c + 1's granules read
   // while slot c updates, slots c >= the wave's largest contact count skipped uniformly, the
   // slots between an env's own count and that maximum are no-op updates (zeroed above). The
-  // impulses are team-uniform (every lane computes the same update); the team lead stores them.
+  // impulses are team-uniform (every lane computes the same update, and every lane stores it).
   {
     const float mu_d = cfg.friction_dynamic, mu = fmaxf(cfg.friction, mu_d);
     const float4* yl = q.b + YG_OFF + q.ygl();
     const int ncw = max(max(__builtin_amdgcn_readlane(nc, 0), __builtin_amdgcn_readlane(nc, TL)),
                         max(__builtin_amdgcn_readlane(nc, 2 * TL), __builtin_amdgcn_readlane(nc, 3 * TL)));
-    const bool lead = q.s == 0;
     float wsum = 0.f;  // TGS: the sum of the sub-iterations' w (this lane's coordinate)
     for (int it = 0; it < cfg.solver_iterations; ++it) {
       if (tgs && it > 0) {  // re-linearise the biases
@@ -2663,7 +2678,10 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
         const float4 Gn = q.yg(yl, cn), Xn = q.aux(cn, 0), Zn = q.aux(cn, 1), Ln = q.lam(cn);
         if (c < ncw) {
           const float4 nA = pgs_update(G, X, Z, La, kLinkFriction ? Z.z : mu, kLinkFriction ? Z.w : mu_d, wd);
-          if (lead) q.lam(c) = nA;
+          // every lane of the team stores the same impulse to the same address (team-uniform:
+          // identical bits in all 16 lanes; an LDS write to one address is not a bank conflict), so
+          // the store needs no exec-mask switch around it
+          q.lam(c) = nA;
         }
         G = Gn; X = Xn; Z = Zn; La = Ln;
       }
@@ -2751,10 +2769,12 @@ __device__ __forceinline__ void substep(MP m0, const zb_task_cfg& cfg, Phys& s,
   }
 #pragma unroll
   for (int j = 0; j < ND; ++j) {
-    float qv = s.jq[j] + dt * un[6 + j];
-    if (qv > TWO_PI_F) qv -= 2.f * TWO_PI_F;
-    else if (qv < -TWO_PI_F) qv += 2.f * TWO_PI_F;
-    s.jq[j] = qv;
+    const float qv = s.jq[j] + dt * un[6 + j];
+    // (the wrap as selects: written as if / else if it compiled to two divergent branches per joint)
+    const float qd = qv - 2.f * TWO_PI_F, qu = qv + 2.f * TWO_PI_F;
+    float qw = qv < -TWO_PI_F ? qu : qv;
+    qw = qv > TWO_PI_F ? qd : qw;
+    s.jq[j] = qw;
   }
 }
 
